@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MNIST CNN training images/sec for the whole node (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W [--impl fused|torch|ddp]
+
+For N>1 the driver launches one rank per GPU with ``torch.distributed.run``; ranks read
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment. Model: the reference's 2-conv CNN
+(horovod/tensorflow_mnist.py:38-73, 3,274,634 params, random init), per-GPU batch 100
+(:160-161), TF1 Adam (:130) with LR × size (:123), gradients averaged across ranks every step
+(:133). Data: synthetic 28×28 images resident on the device (no network for MNIST).
+
+Implementations:
+  fused  — mihvd's hand-written CDNA4 HIP kernels: bf16 MFMA forward/backward with fp32 master
+           weights, gradients written straight into the fusion buffer, RCCL allreduce on it,
+           fused TF1-Adam; the whole step (incl. the allreduce) replayed as one HIP graph.
+  torch  — stock PyTorch-ROCm ops (fp32) + mihvd DistributedOptimizer (bucketed RCCL allreduce).
+  ddp    — stock PyTorch-ROCm ops (fp32) + torch DDP + torch Adam: the measured comparator
+           (the reference publishes no images/sec).
+
+Timing: W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize on both
+sides; the max elapsed over ranks is used. Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec (whole node) MNIST CNN at 1/2/4/8 MI355X; scaling efficiency"
+PER_GPU_BATCH = 100
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--impl", choices=["fused", "torch", "ddp"], default=os.environ.get("MIHVD_BENCH_IMPL", "fused"))
+    ap.add_argument("--batch-size", type=int, default=PER_GPU_BATCH)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--graph-steps", type=int, default=0, help="fused: steps captured per HIP graph (0=auto)")
+    ap.add_argument("--pool-batches", type=int, default=60, help="synthetic batches resident on device")
+    ap.add_argument("--compression", choices=["none", "bf16"], default="none")
+    return ap.parse_args()
+
+
+def synthetic_pool(n_batches, batch, device, seed=0):
+    from mihvd.utils.data import synthetic_mnist
+
+    (x, y), _ = synthetic_mnist(n_train=n_batches * batch, n_test=10, seed=seed)
+    xt = torch.from_numpy(x.reshape(-1, 784)).to(device=device, dtype=torch.float32).div_(255.0)
+    yt = torch.from_numpy(y.astype("int64")).to(device)
+    return xt, yt
+
+
+def make_torch_step(args, hvd, device, ddp=False):
+    from mihvd.models.mnist import MNISTConvNet, softmax_cross_entropy
+    from mihvd.optim import TFAdam
+
+    model = MNISTConvNet(impl="torch", seed=42).to(device)
+    lr = args.lr * hvd.size()
+    if ddp:
+        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index] if device.type == "cuda" else None)
+        opt = torch.optim.Adam(model.parameters(), lr=lr)
+    else:
+        net = model
+        hvd.broadcast_parameters(model.state_dict(), 0)
+        comp = hvd.Compression.bf16 if args.compression == "bf16" else hvd.Compression.none
+        opt = hvd.DistributedOptimizer(TFAdam(model.parameters(), lr=lr), named_parameters=model.named_parameters(),
+                                       compression=comp)
+    X, Y = synthetic_pool(args.pool_batches, args.batch_size, device, seed=hvd.rank())
+    state = {"i": 0}
+
+    def step():
+        i = state["i"] % args.pool_batches
+        state["i"] += 1
+        xb = X[i * args.batch_size:(i + 1) * args.batch_size]
+        yb = Y[i * args.batch_size:(i + 1) * args.batch_size]
+        opt.zero_grad(set_to_none=False) if not ddp else opt.zero_grad()
+        loss = softmax_cross_entropy(net(xb), yb)
+        loss.backward()
+        opt.step()
+        return loss
+
+    return step, "fp32", lambda: None
+
+
+def make_fused_step(args, hvd, device):
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    tr = FusedMNISTTrainer(batch_size=args.batch_size, lr=args.lr * hvd.size(), seed=42, device=device,
+                           compression=args.compression)
+    tr.broadcast(0)
+    X, Y = synthetic_pool(args.pool_batches, args.batch_size, device, seed=hvd.rank())
+    tr.set_device_dataset(X, Y)
+    k = args.graph_steps or 10
+    tr.build_graph(steps_per_replay=k)
+
+    def step():
+        tr.run_graph()
+
+    return step, "bf16", tr
+
+
+def main():
+    args = parse()
+    import mihvd.torch as hvd
+
+    hvd.init()
+    device = hvd.device()
+    n = hvd.size()
+    if args.impl == "fused":
+        step, dtype, tr = make_fused_step(args, hvd, device)
+        per_call = tr.steps_per_replay
+    else:
+        step, dtype, _ = make_torch_step(args, hvd, device, ddp=args.impl == "ddp")
+        per_call = 1
+    calls_warm = max(1, -(-args.warmup // per_call))
+    calls = max(1, -(-args.steps // per_call))
+    steps_timed = calls * per_call
+    for _ in range(calls_warm):
+        step()
+    sync = (lambda: torch.cuda.synchronize()) if device.type == "cuda" else (lambda: None)
+    sync()
+    hvd.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        step()
+    sync()
+    hvd.barrier()
+    sync()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=device)
+    if n > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    ms = el / steps_timed * 1000.0
+    ips = steps_timed * args.batch_size * n / el
+    loss_val = None
+    if args.impl == "fused":
+        loss_val = float(tr.last_loss())
+    if hvd.rank() == 0:
+        rec = {
+            "metric": METRIC, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": steps_timed,
+            "warmup": calls_warm * per_call, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": dtype, "data": "synthetic 28x28 uint8-derived images, device-resident; random-init weights",
+            "config": {"model": "tensorflow_mnist 2-conv CNN (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.5-fc10, 3,274,634 params)",
+                       "global_batch": args.batch_size * n, "per_gpu_batch": args.batch_size, "seq_len": None,
+                       "image_shape": [28, 28, 1], "parallelism": f"dp{n}", "impl": args.impl,
+                       "optimizer": "Adam (TF1 rule), lr=%g x size" % args.lr,
+                       "allreduce": "RCCL allreduce of the fp32 gradient fusion buffer every step" +
+                                    (" (bf16 wire)" if args.compression == "bf16" else ""),
+                       "steps_per_graph": per_call, "final_loss": loss_val},
+        }
+        print(json.dumps(rec), flush=True)
+    hvd.shutdown()
+
+
+if __name__ == "__main__":
+    main()

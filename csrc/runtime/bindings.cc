@@ -1,0 +1,108 @@
+// pybind11 bindings for the mihvd host runtime (module mihvd._native._mihvd_runtime).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "runtime.h"
+
+namespace py = pybind11;
+using namespace mihvd;
+
+PYBIND11_MODULE(_mihvd_runtime, m) {
+  m.doc() = "mihvd native host runtime: bucket planner, controller, timeline, stall inspector";
+
+  py::class_<TensorSpec>(m, "TensorSpec")
+      .def(py::init<>())
+      .def(py::init([](int64_t numel, int elem_size, int dtype, int device) {
+             TensorSpec s;
+             s.numel = numel;
+             s.elem_size = elem_size;
+             s.dtype = dtype;
+             s.device = device;
+             return s;
+           }),
+           py::arg("numel"), py::arg("elem_size"), py::arg("dtype") = 0, py::arg("device") = 0)
+      .def_readwrite("numel", &TensorSpec::numel)
+      .def_readwrite("elem_size", &TensorSpec::elem_size)
+      .def_readwrite("dtype", &TensorSpec::dtype)
+      .def_readwrite("device", &TensorSpec::device);
+
+  py::class_<BucketPlan>(m, "BucketPlan")
+      .def_readonly("members", &BucketPlan::members)
+      .def_readonly("offsets", &BucketPlan::offsets)
+      .def_readonly("numel", &BucketPlan::numel)
+      .def_readonly("dtype", &BucketPlan::dtype)
+      .def_readonly("device", &BucketPlan::device)
+      .def_readonly("tensor_bucket", &BucketPlan::tensor_bucket)
+      .def_readonly("tensor_offset", &BucketPlan::tensor_offset)
+      .def("__len__", [](const BucketPlan& p) { return p.members.size(); });
+
+  m.def("plan_buckets", &plan_buckets, py::arg("specs"), py::arg("order"),
+        py::arg("threshold_bytes"), py::arg("align_bytes") = 256);
+
+  py::class_<Controller>(m, "Controller")
+      .def(py::init<std::vector<int>, int, int>(), py::arg("tensor_bucket"),
+           py::arg("num_buckets"), py::arg("passes_per_step") = 1)
+      .def("mark_ready", &Controller::mark_ready)
+      .def("flush", &Controller::flush)
+      .def("reset", &Controller::reset)
+      .def("pending_in_bucket", &Controller::pending_in_bucket)
+      .def_property_readonly("launched", &Controller::launched)
+      .def_property_readonly("num_buckets", &Controller::num_buckets)
+      .def_property_readonly("passes_per_step", &Controller::passes_per_step);
+
+  m.def("fnv1a64", [](const std::string& s) { return fnv1a64(s); });
+  m.def("tensor_signature", &tensor_signature);
+
+  py::class_<Timeline>(m, "Timeline")
+      .def(py::init<const std::string&, int>(), py::arg("path"), py::arg("rank") = 0)
+      .def("begin", &Timeline::begin, py::arg("name"), py::arg("cat") = "op", py::arg("tid") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("end", &Timeline::end, py::arg("name"), py::arg("cat") = "op", py::arg("tid") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("complete", &Timeline::complete, py::arg("name"), py::arg("cat"), py::arg("tid"),
+           py::arg("ts_us"), py::arg("dur_us"))
+      .def("instant", &Timeline::instant, py::arg("name"), py::arg("cat") = "op",
+           py::arg("tid") = 0)
+      .def("counter", &Timeline::counter)
+      .def("now_us", &Timeline::now_us)
+      .def("flush", &Timeline::flush, py::call_guard<py::gil_scoped_release>())
+      .def("close", &Timeline::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("events_written", &Timeline::events_written)
+      .def_property_readonly("path", &Timeline::path);
+
+  py::class_<StallReport>(m, "StallReport")
+      .def_readonly("name", &StallReport::name)
+      .def_readonly("age_s", &StallReport::age_s);
+
+  py::class_<StallInspector>(m, "StallInspector")
+      .def(py::init<double, double, double, int>(), py::arg("warn_s") = 60.0,
+           py::arg("shutdown_s") = 0.0, py::arg("poll_s") = 1.0, py::arg("rank") = 0)
+      .def("submit", &StallInspector::submit)
+      .def("complete", &StallInspector::complete)
+      .def("outstanding", &StallInspector::outstanding, py::arg("older_than_s") = 0.0)
+      .def("num_outstanding", &StallInspector::num_outstanding)
+      .def("start", &StallInspector::start)
+      .def("stop", &StallInspector::stop, py::call_guard<py::gil_scoped_release>())
+      .def("set_hard_abort", &StallInspector::set_hard_abort)
+      .def_property_readonly("stalled", &StallInspector::stalled)
+      .def_property_readonly("warnings_emitted", &StallInspector::warnings_emitted);
+
+  py::class_<FaultAction>(m, "FaultAction")
+      .def_readonly("kind", &FaultAction::kind)
+      .def_readonly("rank", &FaultAction::rank)
+      .def_readonly("step", &FaultAction::step)
+      .def_readonly("args", &FaultAction::args);
+
+  py::class_<FaultPlan>(m, "FaultPlan")
+      .def(py::init<const std::string&>())
+      .def("due", &FaultPlan::due)
+      .def_property_readonly("actions", &FaultPlan::actions);
+
+  py::class_<StepStats>(m, "StepStats")
+      .def(py::init<size_t>(), py::arg("window") = 100)
+      .def("add", &StepStats::add)
+      .def("mean", &StepStats::mean)
+      .def("percentile", &StepStats::percentile)
+      .def("reset", &StepStats::reset)
+      .def_property_readonly("count", &StepStats::count);
+}

@@ -1,0 +1,323 @@
+"""Process-world management: ``init / shutdown / rank / size / local_rank / local_size``.
+
+Capability parity with the Horovod calls made by the reference:
+``hvd.init()`` (horovod/tensorflow_mnist.py:90, tensorflow_mnist_gpu.py:93), ``hvd.rank()``
+(:109,159), ``hvd.size()`` (:123,146), ``hvd.local_rank()`` (:155), ``hvd.local_size()`` and
+``hvd.nccl_built()`` (:127).
+
+MI355X design: one process per GPU. The data plane is ``torch.distributed`` with the ``nccl``
+backend, which on ROCm *is* RCCL over xGMI; CPU-only runs (tests, BASELINE config 1) use
+``gloo``. ``init()`` pins ``cuda:<local_rank>`` (the ``visible_device_list=str(local_rank)`` of
+tensorflow_mnist.py:155), builds the local/cross sub-groups used by hierarchical reductions,
+starts the native stall inspector and timeline, and registers ``shutdown`` at exit.
+"""
+from __future__ import annotations
+
+import atexit
+import datetime
+import enum
+import logging
+import os
+import threading
+
+import torch
+import torch.distributed as dist
+
+from .config import Config
+from .utils import env as _env
+
+log = logging.getLogger("mihvd")
+
+
+class ReduceOp(enum.IntEnum):
+    Average = 0
+    Sum = 1
+    Adasum = 2
+    Min = 3
+    Max = 4
+    Product = 5
+
+
+Average = ReduceOp.Average
+Sum = ReduceOp.Sum
+Adasum = ReduceOp.Adasum
+Min = ReduceOp.Min
+Max = ReduceOp.Max
+Product = ReduceOp.Product
+
+
+class _Context:
+    def __init__(self):
+        self.initialized = False
+        self.topology: _env.Topology | None = None
+        self.config: Config | None = None
+        self.backend: str | None = None
+        self.device: torch.device = torch.device("cpu")
+        self.world_group = None
+        self.local_group = None
+        self.cross_group = None
+        self.owns_pg = False
+        self.timeline = None
+        self.stall = None
+        self.fault_plan = None
+        self.lock = threading.RLock()
+
+
+_ctx = _Context()
+
+
+class NotInitializedError(RuntimeError):
+    pass
+
+
+def _require():
+    if not _ctx.initialized:
+        raise NotInitializedError("mihvd has not been initialized; call mihvd.init() first")
+    return _ctx
+
+
+def _choose_backend(cfg: Config) -> str:
+    if cfg.backend in ("nccl", "rccl"):
+        return "nccl"
+    if cfg.backend == "gloo":
+        return "gloo"
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def init(comm=None, process_sets=None, config: Config | None = None):
+    """Initialise the process world. Idempotent (repeated calls are no-ops)."""
+    with _ctx.lock:
+        if _ctx.initialized:
+            return
+        cfg = config or Config.from_env()
+        topo = _env.discover()
+        backend = _choose_backend(cfg)
+        logging.basicConfig(level=getattr(logging, cfg.log_level, logging.INFO),
+                            format="[%(asctime)s] [rank " + str(topo.rank) + "] %(message)s")
+        if backend == "nccl":
+            ndev = torch.cuda.device_count()
+            if ndev == 0:
+                raise RuntimeError("backend nccl (RCCL) requested but no GPU is visible")
+            device = torch.device("cuda", topo.local_rank % ndev)
+            torch.cuda.set_device(device)
+        else:
+            device = torch.device("cpu")
+        timeout = datetime.timedelta(seconds=cfg.timeout_s)
+        if dist.is_initialized():
+            _ctx.owns_pg = False
+            if dist.get_world_size() != topo.size and topo.source != "single":
+                raise RuntimeError("existing process group does not match the launcher environment")
+            topo = _env.Topology(dist.get_rank(), dist.get_world_size(),
+                                 topo.local_rank if topo.source != "single" else dist.get_rank(),
+                                 topo.local_size if topo.source != "single" else dist.get_world_size(),
+                                 topo.cross_rank, topo.cross_size, topo.master_addr, topo.master_port, "existing")
+            backend = dist.get_backend()
+        elif topo.size == 1 and topo.master_port is None:
+            # Single process without a launcher: an in-memory store, no sockets needed.
+            dist.init_process_group(backend, store=dist.HashStore(), rank=0, world_size=1, timeout=timeout,
+                                    **({"device_id": device} if backend == "nccl" else {}))
+            _ctx.owns_pg = True
+        else:
+            port = topo.master_port or 29500
+            url = f"tcp://{topo.master_addr}:{port}"
+            kwargs = {"device_id": device} if backend == "nccl" else {}
+            dist.init_process_group(backend, init_method=url, rank=topo.rank, world_size=topo.size,
+                                    timeout=timeout, **kwargs)
+            _ctx.owns_pg = True
+        _ctx.topology = topo
+        _ctx.config = cfg
+        _ctx.backend = backend
+        _ctx.device = device
+        _ctx.world_group = dist.group.WORLD
+        _build_subgroups(topo)
+        _start_observability(cfg, topo)
+        _ctx.initialized = True
+        atexit.register(shutdown)
+        if topo.rank == 0:
+            log.debug("mihvd initialised: %s backend=%s device=%s config=%s", topo, backend, device, cfg)
+
+
+def _build_subgroups(topo: _env.Topology):
+    """Local (same host) and cross (same local rank) groups for hierarchical reductions.
+
+    ``new_group`` is collective over the world, so every rank creates every group in the same order.
+    """
+    if topo.size == 1:
+        _ctx.local_group = dist.group.WORLD
+        _ctx.cross_group = dist.group.WORLD
+        return
+    ls = topo.local_size
+    if topo.size % ls != 0:
+        _ctx.local_group = None
+        _ctx.cross_group = None
+        return
+    nodes = topo.size // ls
+    local_group = cross_group = None
+    if nodes == 1:
+        local_group = dist.group.WORLD
+    else:
+        for n in range(nodes):
+            g = dist.new_group(list(range(n * ls, (n + 1) * ls)))
+            if n == topo.rank // ls:
+                local_group = g
+    if ls == 1:
+        cross_group = dist.group.WORLD
+    else:
+        for lr in range(ls):
+            g = dist.new_group(list(range(lr, topo.size, ls)))
+            if lr == topo.rank % ls:
+                cross_group = g
+    _ctx.local_group = local_group
+    _ctx.cross_group = cross_group
+
+
+def _start_observability(cfg: Config, topo: _env.Topology):
+    from ._native import runtime
+
+    rt = runtime()
+    if cfg.timeline:
+        path = cfg.timeline.replace("{rank}", str(topo.rank))
+        if "{rank}" not in cfg.timeline and topo.size > 1:
+            root, ext = os.path.splitext(path)
+            path = f"{root}.rank{topo.rank}{ext or '.json'}"
+        _ctx.timeline = rt.Timeline(path, topo.rank)
+    if not cfg.stall_check_disable and cfg.stall_check_s > 0:
+        _ctx.stall = rt.StallInspector(cfg.stall_check_s, cfg.stall_shutdown_s, min(1.0, cfg.stall_check_s / 4), topo.rank)
+        _ctx.stall.start()
+    if cfg.fault:
+        _ctx.fault_plan = rt.FaultPlan(cfg.fault)
+
+
+def shutdown():
+    """Tear down the world (``hvd.shutdown``). Safe to call more than once."""
+    with _ctx.lock:
+        if not _ctx.initialized:
+            return
+        try:
+            from .parallel import collectives
+
+            collectives._drain_all()
+        except Exception:  # pragma: no cover
+            pass
+        if _ctx.stall is not None:
+            _ctx.stall.stop()
+            _ctx.stall = None
+        if _ctx.timeline is not None:
+            _ctx.timeline.close()
+            _ctx.timeline = None
+        if _ctx.owns_pg and dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:  # pragma: no cover
+                pass
+        _ctx.initialized = False
+        _ctx.world_group = _ctx.local_group = _ctx.cross_group = None
+
+
+def is_initialized() -> bool:
+    return _ctx.initialized
+
+
+def rank() -> int:
+    return _require().topology.rank
+
+
+def size() -> int:
+    return _require().topology.size
+
+
+def local_rank() -> int:
+    return _require().topology.local_rank
+
+
+def local_size() -> int:
+    return _require().topology.local_size
+
+
+def cross_rank() -> int:
+    return _require().topology.cross_rank
+
+
+def cross_size() -> int:
+    return _require().topology.cross_size
+
+
+def is_homogeneous() -> bool:
+    t = _require().topology
+    return t.size % t.local_size == 0
+
+
+def device() -> torch.device:
+    return _require().device
+
+
+def backend() -> str:
+    return _require().backend
+
+
+def config() -> Config:
+    return _require().config
+
+
+def rccl_built() -> bool:
+    """True when the collective data plane is RCCL (torch ``nccl`` backend on ROCm).
+
+    Before ``init()`` this reports whether RCCL *can* be used on this machine.
+    """
+    if _ctx.initialized:
+        return _ctx.backend == "nccl"
+    return dist.is_nccl_available() and torch.cuda.is_available()
+
+
+def nccl_built() -> bool:
+    """Horovod-compatible alias of :func:`rccl_built` (used by the reference's Adasum LR rule,
+    horovod/tensorflow_mnist.py:127)."""
+    return rccl_built()
+
+
+def gloo_built() -> bool:
+    return dist.is_gloo_available()
+
+
+def mpi_built() -> bool:
+    return False
+
+
+def mpi_enabled() -> bool:
+    return False
+
+
+def gloo_enabled() -> bool:
+    return _ctx.initialized and _ctx.backend == "gloo"
+
+
+def mpi_threads_supported() -> bool:
+    return False
+
+
+def rocm_built() -> bool:
+    return torch.version.hip is not None
+
+
+def cuda_built() -> bool:
+    return False
+
+
+def timeline():
+    return _ctx.timeline
+
+
+def start_timeline(path: str, mark_cycles: bool = False):
+    from ._native import runtime
+
+    c = _require()
+    if c.timeline is not None:
+        c.timeline.close()
+    c.timeline = runtime().Timeline(path, c.topology.rank)
+
+
+def stop_timeline():
+    c = _require()
+    if c.timeline is not None:
+        c.timeline.close()
+        c.timeline = None

@@ -1,0 +1,339 @@
+"""Keras-shaped training API: ``import mihvd.keras as hvd`` (horovod.tensorflow.keras parity).
+
+The reference's GPU entrypoint (horovod/tensorflow_mnist_gpu.py) compiles a Keras model with a
+Horovod-wrapped Adam and trains it with ``model.fit`` and two Horovod callbacks (:147-163):
+
+* ``callbacks.BroadcastGlobalVariablesCallback(0)`` — broadcast model + optimizer variables at
+  the end of the first batch (optimizer slots exist only after one step);
+* ``callbacks.MetricAverageCallback()`` — allreduce-average the epoch metrics;
+* rank 0 only: ``TensorBoard(log_dir='./logs')`` and ``ModelCheckpoint('./checkpoints/
+  mnist-{epoch}.h5', save_best_only=True)``; at the end ``evaluate`` and ``save('./final_model')``.
+
+``Model`` below provides ``compile / fit / evaluate / save`` over any torch module, with the
+mixed-precision policy of the reference (:26-28) mapped to the MI355X-native ``bfloat16``
+autocast (``'mixed_bfloat16'``, default) or ``'mixed_float16'`` with dynamic loss scaling.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+from .basics import *  # noqa: F401,F403
+from . import basics as _b
+from .parallel import collectives as C
+from .parallel.compression import Compression  # noqa: F401
+from .parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters  # noqa: F401
+from .utils.logging import MetricsWriter
+
+
+# ------------------------------------------------------------------------------------------ #
+# Callbacks
+# ------------------------------------------------------------------------------------------ #
+class Callback:
+    model: "Model" = None
+
+    def set_model(self, model):
+        self.model = model
+
+    def on_train_begin(self, logs=None):
+        pass
+
+    def on_train_end(self, logs=None):
+        pass
+
+    def on_epoch_begin(self, epoch, logs=None):
+        pass
+
+    def on_epoch_end(self, epoch, logs=None):
+        pass
+
+    def on_batch_begin(self, batch, logs=None):
+        pass
+
+    def on_batch_end(self, batch, logs=None):
+        pass
+
+
+class BroadcastGlobalVariablesCallback(Callback):
+    def __init__(self, root_rank: int = 0, device: str = ""):
+        self.root_rank = root_rank
+        self.broadcast_done = False
+
+    def on_batch_end(self, batch, logs=None):
+        if self.broadcast_done:
+            return
+        broadcast_parameters(self.model.module.state_dict(), self.root_rank)
+        broadcast_optimizer_state(self.model.optimizer, self.root_rank)
+        self.broadcast_done = True
+
+
+class MetricAverageCallback(Callback):
+    """Average every numeric entry of ``logs`` across ranks with one fused allreduce."""
+
+    def __init__(self, device: str = ""):
+        pass
+
+    def on_epoch_end(self, epoch, logs=None):
+        if logs is None or not _b.is_initialized() or _b.size() == 1:
+            return
+        keys = sorted(k for k, v in logs.items() if isinstance(v, (int, float, np.floating)))
+        if not keys:
+            return
+        t = torch.tensor([float(logs[k]) for k in keys], dtype=torch.float64, device=_b.device())
+        t = C.allreduce(t, op=_b.Average, name="metrics")
+        for k, v in zip(keys, t.tolist()):
+            logs[k] = v
+
+
+class LearningRateWarmupCallback(Callback):
+    """Linear LR warmup from ``initial_lr / size`` to ``initial_lr`` over ``warmup_epochs``."""
+
+    def __init__(self, initial_lr, warmup_epochs=5, momentum_correction=True, steps_per_epoch=None, verbose=0):
+        self.initial_lr = initial_lr
+        self.warmup_epochs = warmup_epochs
+        self.steps_per_epoch = steps_per_epoch
+        self._epoch = 0
+
+    def on_epoch_begin(self, epoch, logs=None):
+        self._epoch = epoch
+
+    def on_batch_begin(self, batch, logs=None):
+        if self._epoch >= self.warmup_epochs:
+            return
+        spe = self.steps_per_epoch or self.model._steps_per_epoch or 1
+        progress = (self._epoch + batch / spe) / self.warmup_epochs
+        size = _b.size() if _b.is_initialized() else 1
+        lr = self.initial_lr / size * (1 + progress * (size - 1))
+        for g in self.model.optimizer.param_groups:
+            g["lr"] = lr
+
+
+class ModelCheckpoint(Callback):
+    def __init__(self, filepath, monitor="val_loss", save_best_only=False, mode="min", verbose=0):
+        self.filepath = filepath
+        self.monitor = monitor
+        self.save_best_only = save_best_only
+        self.mode = mode
+        self.best = math.inf if mode == "min" else -math.inf
+        self.saved: list[str] = []
+
+    def on_epoch_end(self, epoch, logs=None):
+        logs = logs or {}
+        path = self.filepath.format(epoch=epoch + 1, **{k: v for k, v in logs.items()})
+        cur = logs.get(self.monitor)
+        if self.save_best_only:
+            if cur is None:
+                return
+            better = cur < self.best if self.mode == "min" else cur > self.best
+            if not better:
+                return
+            self.best = cur
+        self.model.save(path)
+        self.saved.append(path)
+
+
+class TensorBoard(Callback):
+    """Scalar logging to ``<log_dir>/metrics.jsonl`` (TensorBoard itself is not installed)."""
+
+    def __init__(self, log_dir="./logs", **kw):
+        self.log_dir = log_dir
+        self.writer = None
+
+    def on_train_begin(self, logs=None):
+        self.writer = MetricsWriter(self.log_dir)
+
+    def on_epoch_end(self, epoch, logs=None):
+        if self.writer:
+            self.writer.scalars({k: v for k, v in (logs or {}).items() if isinstance(v, (int, float))}, epoch)
+
+    def on_train_end(self, logs=None):
+        if self.writer:
+            self.writer.close()
+
+
+class _CallbacksNS:
+    BroadcastGlobalVariablesCallback = BroadcastGlobalVariablesCallback
+    MetricAverageCallback = MetricAverageCallback
+    LearningRateWarmupCallback = LearningRateWarmupCallback
+    ModelCheckpoint = ModelCheckpoint
+    TensorBoard = TensorBoard
+    Callback = Callback
+
+
+callbacks = _CallbacksNS()
+
+
+# ------------------------------------------------------------------------------------------ #
+# Model
+# ------------------------------------------------------------------------------------------ #
+class _LossScaler:
+    """Dynamic loss scaling for the fp16 policy (Keras LossScaleOptimizer semantics)."""
+
+    def __init__(self, init_scale=2.0 ** 15, growth_interval=2000):
+        self.scale = init_scale
+        self.growth_interval = growth_interval
+        self.good_steps = 0
+
+    def unscale_and_check(self, params) -> bool:
+        finite = True
+        for p in params:
+            if p.grad is not None:
+                p.grad.div_(self.scale)
+                if not torch.isfinite(p.grad).all():
+                    finite = False
+        if finite:
+            self.good_steps += 1
+            if self.good_steps >= self.growth_interval:
+                self.scale *= 2
+                self.good_steps = 0
+        else:
+            self.scale = max(1.0, self.scale / 2)
+            self.good_steps = 0
+        return finite
+
+
+class Model:
+    def __init__(self, module: torch.nn.Module, policy: str = "float32"):
+        self.module = module
+        self.policy = policy
+        self.optimizer = None
+        self.loss_fn = None
+        self.metrics = []
+        self.history = {}
+        self._steps_per_epoch = None
+        self._scaler = _LossScaler() if policy == "mixed_float16" else None
+
+    def compile(self, optimizer, loss, metrics=()):
+        self.optimizer = optimizer
+        self.loss_fn = loss
+        self.metrics = list(metrics)
+
+    def _device(self):
+        return next(self.module.parameters()).device
+
+    def _autocast(self):
+        dev = self._device().type
+        if self.policy == "mixed_bfloat16":
+            return torch.autocast(dev, dtype=torch.bfloat16)
+        if self.policy == "mixed_float16":
+            return torch.autocast(dev, dtype=torch.float16)
+        return torch.autocast(dev, enabled=False)
+
+    def _batch(self, x, y, idx):
+        dev = self._device()
+        xb = torch.as_tensor(x[idx], device=dev).float()
+        yb = torch.as_tensor(y[idx], device=dev).long()
+        return xb, yb
+
+    def train_on_batch(self, xb, yb):
+        self.module.train()
+        self.optimizer.zero_grad()
+        with self._autocast():
+            logits = self.module(xb)
+        loss = self.loss_fn(logits.float(), yb)
+        if self._scaler is not None:
+            (loss * self._scaler.scale).backward()
+            self.optimizer.synchronize()
+            ok = self._scaler.unscale_and_check([p for g in self.optimizer.param_groups for p in g["params"]])
+            if ok:
+                with self.optimizer.skip_synchronize():
+                    self.optimizer.step()
+            else:
+                self.optimizer._synchronized = False
+        else:
+            loss.backward()
+            self.optimizer.step()
+        acc = (logits.argmax(1) == yb).float().mean()
+        return loss.detach(), acc.detach()
+
+    @torch.no_grad()
+    def evaluate(self, x, y, batch_size=100, steps=None, verbose=0):
+        self.module.eval()
+        n = len(x)
+        steps = steps or max(1, n // batch_size)
+        tot_loss = torch.zeros((), device=self._device())
+        tot_acc = torch.zeros((), device=self._device())
+        for s in range(steps):
+            idx = np.arange(s * batch_size, min(n, (s + 1) * batch_size))
+            xb, yb = self._batch(x, y, idx)
+            with self._autocast():
+                logits = self.module(xb)
+            tot_loss += self.loss_fn(logits.float(), yb)
+            tot_acc += (logits.argmax(1) == yb).float().mean()
+        return [float(tot_loss) / steps, float(tot_acc) / steps]
+
+    def fit(self, x, y, batch_size=100, epochs=1, steps_per_epoch=None, validation_data=None, validation_steps=None,
+            callbacks=(), verbose=1, shuffle=True, seed=None):
+        cbs = list(callbacks)
+        for cb in cbs:
+            cb.set_model(self)
+        n = len(x)
+        steps_per_epoch = steps_per_epoch or max(1, n // batch_size)
+        self._steps_per_epoch = steps_per_epoch
+        rng = np.random.default_rng(seed)
+        for cb in cbs:
+            cb.on_train_begin()
+        perm = rng.permutation(n) if shuffle else np.arange(n)
+        pos = 0
+        for epoch in range(epochs):
+            for cb in cbs:
+                cb.on_epoch_begin(epoch)
+            t0 = time.time()
+            sum_loss = torch.zeros((), device=self._device())
+            sum_acc = torch.zeros((), device=self._device())
+            for step in range(steps_per_epoch):
+                if pos + batch_size > n:
+                    perm = rng.permutation(n) if shuffle else np.arange(n)
+                    pos = 0
+                idx = perm[pos:pos + batch_size]
+                pos += batch_size
+                for cb in cbs:
+                    cb.on_batch_begin(step)
+                xb, yb = self._batch(x, y, idx)
+                loss, acc = self.train_on_batch(xb, yb)
+                sum_loss += loss
+                sum_acc += acc
+                for cb in cbs:
+                    cb.on_batch_end(step, {})
+            logs = {"loss": float(sum_loss) / steps_per_epoch, "accuracy": float(sum_acc) / steps_per_epoch}
+            if validation_data is not None:
+                vl, va = self.evaluate(validation_data[0], validation_data[1], batch_size, validation_steps)
+                logs["val_loss"], logs["val_accuracy"] = vl, va
+            for cb in cbs:
+                cb.on_epoch_end(epoch, logs)
+            for k, v in logs.items():
+                self.history.setdefault(k, []).append(v)
+            if verbose:
+                dt = time.time() - t0
+                print(f"Epoch {epoch + 1}/{epochs} - {dt:.1f}s - " +
+                      " - ".join(f"{k}: {v:.4f}" for k, v in logs.items()), file=sys.stdout, flush=True)
+        for cb in cbs:
+            cb.on_train_end()
+        return self
+
+    def save(self, path: str):
+        """Save weights + optimizer state. A path without an extension is treated as a
+        directory (the SavedModel shape of ``model.save('./final_model')``)."""
+        state = {"model": {k: v.detach().cpu() for k, v in self.module.state_dict().items()}}
+        if os.path.splitext(path)[1] == "":
+            os.makedirs(path, exist_ok=True)
+            target = os.path.join(path, "model.pt")
+        else:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+            target = path
+        tmp = target + ".tmp"
+        torch.save(state, tmp)
+        os.replace(tmp, target)
+        return target
+
+    @staticmethod
+    def load_weights(module, path: str):
+        target = os.path.join(path, "model.pt") if os.path.isdir(path) else path
+        sd = torch.load(target, map_location="cpu", weights_only=True)["model"]
+        module.load_state_dict(sd)
+        return module

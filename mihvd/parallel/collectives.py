@@ -1,0 +1,381 @@
+"""Tensor collectives with Horovod semantics (``hvd.allreduce / allgather / broadcast / alltoall /
+reducescatter``, their ``_async`` forms, ``synchronize`` and ``poll``).
+
+Each call is one RCCL collective on the process group (``nccl`` backend = RCCL over xGMI on
+MI355X; ``gloo`` on CPU). Async calls return an integer handle; the native stall inspector tracks
+every outstanding handle and the native timeline records a span per collective.
+"""
+from __future__ import annotations
+
+import itertools
+import threading
+from typing import Any, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .. import basics
+from ..basics import ReduceOp
+from .compression import Compression
+
+_handles: dict[int, "_Handle"] = {}
+_hlock = threading.Lock()
+_next = itertools.count(1)
+
+
+class _Handle:
+    __slots__ = ("work", "output", "post", "stall_id", "name", "done", "t0")
+
+    def __init__(self, work, output, post, name):
+        self.work = work
+        self.output = output
+        self.post = post
+        self.name = name
+        self.done = False
+        ctx = basics._ctx
+        self.stall_id = ctx.stall.submit(name) if ctx.stall is not None else None
+        self.t0 = ctx.timeline.now_us() if ctx.timeline is not None else None
+
+
+def _register(work, output, post, name) -> int:
+    h = next(_next)
+    with _hlock:
+        _handles[h] = _Handle(work, output, post, name)
+    return h
+
+
+def _finish(h: "_Handle"):
+    if h.done:
+        return h.output
+    works = h.work if isinstance(h.work, (list, tuple)) else [h.work]
+    for w in works:
+        if w is not None:
+            w.wait()
+    if h.post is not None:
+        h.output = h.post(h.output)
+    h.done = True
+    ctx = basics._ctx
+    if h.stall_id is not None and ctx.stall is not None:
+        ctx.stall.complete(h.stall_id)
+    if h.t0 is not None and ctx.timeline is not None:
+        kind = h.name.split(".", 1)[0].upper()
+        ctx.timeline.complete(h.name, kind, 1, h.t0, ctx.timeline.now_us() - h.t0)
+    return h.output
+
+
+def synchronize(handle: int):
+    """Wait for an async collective and return its output tensor."""
+    with _hlock:
+        h = _handles.pop(handle, None)
+    if h is None:
+        raise ValueError(f"unknown or already synchronized handle {handle}")
+    return _finish(h)
+
+
+def poll(handle: int) -> bool:
+    with _hlock:
+        h = _handles.get(handle)
+    if h is None:
+        raise ValueError(f"unknown handle {handle}")
+    works = h.work if isinstance(h.work, (list, tuple)) else [h.work]
+    return all(w is None or w.is_completed() for w in works)
+
+
+def _drain_all():
+    with _hlock:
+        hs = list(_handles.items())
+        _handles.clear()
+    for _, h in hs:
+        try:
+            _finish(h)
+        except Exception:
+            pass
+
+
+def _torch_op(op: ReduceOp):
+    return {
+        ReduceOp.Sum: dist.ReduceOp.SUM,
+        ReduceOp.Average: dist.ReduceOp.SUM,
+        ReduceOp.Min: dist.ReduceOp.MIN,
+        ReduceOp.Max: dist.ReduceOp.MAX,
+        ReduceOp.Product: dist.ReduceOp.PRODUCT,
+    }[op]
+
+
+def _resolve_op(average, op):
+    if op is not None and average is not None:
+        raise ValueError("pass either op= or the deprecated average=, not both")
+    if op is None:
+        op = ReduceOp.Average if (average is None or average) else ReduceOp.Sum
+    return ReduceOp(op)
+
+
+def _group(process_set=None):
+    return None if process_set is None else process_set
+
+
+def _group_size(group) -> int:
+    return dist.get_world_size(group) if group is not None else basics.size()
+
+
+# ------------------------------------------------------------------------------------------ #
+# allreduce
+# ------------------------------------------------------------------------------------------ #
+def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postscale_factor, group,
+                    segments=None, async_op=True):
+    ctx = basics._require()
+    op = ReduceOp(op)
+    n = _group_size(group)
+    if op == ReduceOp.Adasum:
+        from .adasum import adasum_allreduce_
+
+        if out is not tensor:
+            out.copy_(tensor)
+        if prescale_factor != 1.0:
+            out.mul_(prescale_factor)
+        adasum_dispatch_(out, segments)
+        if postscale_factor != 1.0:
+            out.mul_(postscale_factor)
+        return _register(None, out, None, f"allreduce.{name}")
+    wire, cctx = compression.compress(tensor)
+    if wire is tensor and out is not tensor:
+        out.copy_(tensor)
+        wire = out
+    if prescale_factor != 1.0:
+        wire.mul_(prescale_factor)
+    work = dist.all_reduce(wire, op=_torch_op(op), group=group, async_op=True) if n > 1 else None
+    scale = postscale_factor / n if op == ReduceOp.Average else postscale_factor
+
+    def post(_o, wire=wire, cctx=cctx, out=out, scale=scale):
+        res = compression.decompress(wire, cctx)
+        if res is not out:
+            out.copy_(res)
+        if scale != 1.0:
+            out.mul_(scale)
+        return out
+
+    return _register(work, out, post, f"allreduce.{name}")
+
+
+def adasum_dispatch_(flat: torch.Tensor, segments=None):
+    """Adasum with Horovod-GPU semantics: hierarchical (average within node, Adasum across nodes)
+    on the RCCL data plane, flat Adasum on gloo or when MIHVD_ADASUM_FLAT=1."""
+    from .adasum import adasum_allreduce_
+
+    ctx = basics._require()
+    topo = ctx.topology
+    hierarchical = (ctx.backend == "nccl" and not ctx.config.adasum_flat and topo.local_size > 1
+                    and ctx.local_group is not None)
+    if not hierarchical:
+        return adasum_allreduce_(flat, segments)
+    dist.all_reduce(flat, group=ctx.local_group)
+    flat.div_(topo.local_size)
+    if topo.cross_size > 1:
+        ranks = list(range(topo.local_rank, topo.size, topo.local_size))
+        adasum_allreduce_(flat, segments, ranks=ranks, group=ctx.cross_group)
+    return flat
+
+
+def allreduce_async(tensor, average=None, name=None, op=None, prescale_factor=1.0, postscale_factor=1.0,
+                    compression=Compression.none, process_set=None) -> int:
+    op = _resolve_op(average, op)
+    out = torch.empty_like(tensor)
+    return _allreduce_impl(tensor, out, name or "tensor", op, compression, prescale_factor, postscale_factor,
+                           _group(process_set))
+
+
+def allreduce_async_(tensor, average=None, name=None, op=None, prescale_factor=1.0, postscale_factor=1.0,
+                     compression=Compression.none, process_set=None) -> int:
+    op = _resolve_op(average, op)
+    return _allreduce_impl(tensor, tensor, name or "tensor", op, compression, prescale_factor, postscale_factor,
+                           _group(process_set))
+
+
+def allreduce(tensor, average=None, name=None, compression=Compression.none, op=None, prescale_factor=1.0,
+              postscale_factor=1.0, process_set=None):
+    return synchronize(allreduce_async(tensor, average, name, op, prescale_factor, postscale_factor, compression,
+                                       process_set))
+
+
+def allreduce_(tensor, average=None, name=None, op=None, prescale_factor=1.0, postscale_factor=1.0,
+               process_set=None):
+    return synchronize(allreduce_async_(tensor, average, name, op, prescale_factor, postscale_factor,
+                                        process_set=process_set))
+
+
+def grouped_allreduce(tensors: Sequence[torch.Tensor], average=None, name=None, compression=Compression.none,
+                      op=None, prescale_factor=1.0, postscale_factor=1.0, process_set=None):
+    """Fused allreduce of many tensors: one flat buffer per dtype, one collective each."""
+    op = _resolve_op(average, op)
+    outs: list[Any] = [None] * len(tensors)
+    by_dtype: dict[torch.dtype, list[int]] = {}
+    for i, t in enumerate(tensors):
+        by_dtype.setdefault(t.dtype, []).append(i)
+    for dt, idxs in by_dtype.items():
+        flat = torch.cat([tensors[i].reshape(-1) for i in idxs])
+        segs, off = [], 0
+        for i in idxs:
+            segs.append((off, off + tensors[i].numel()))
+            off += tensors[i].numel()
+        h = _allreduce_impl(flat, flat, name or "grouped", op, compression, prescale_factor, postscale_factor,
+                            _group(process_set), segments=segs)
+        flat = synchronize(h)
+        for i, (s, e) in zip(idxs, segs):
+            outs[i] = flat[s:e].view_as(tensors[i])
+    return outs
+
+
+# ------------------------------------------------------------------------------------------ #
+# broadcast / allgather / alltoall / reducescatter
+# ------------------------------------------------------------------------------------------ #
+def broadcast_async_(tensor, root_rank, name=None, process_set=None) -> int:
+    basics._require()
+    group = _group(process_set)
+    work = dist.broadcast(tensor, src=root_rank, group=group, async_op=True) if _group_size(group) > 1 else None
+    return _register(work, tensor, None, f"broadcast.{name or 'tensor'}")
+
+
+def broadcast_async(tensor, root_rank, name=None, process_set=None) -> int:
+    out = tensor.clone()
+    return broadcast_async_(out, root_rank, name, process_set)
+
+
+def broadcast(tensor, root_rank, name=None, process_set=None):
+    return synchronize(broadcast_async(tensor, root_rank, name, process_set))
+
+
+def broadcast_(tensor, root_rank, name=None, process_set=None):
+    return synchronize(broadcast_async_(tensor, root_rank, name, process_set))
+
+
+def allgather_async(tensor, name=None, process_set=None) -> int:
+    """Concatenate every rank's tensor along dim 0 (first dimensions may differ)."""
+    basics._require()
+    group = _group(process_set)
+    n = _group_size(group)
+    if n == 1:
+        return _register(None, tensor.clone(), None, f"allgather.{name or 'tensor'}")
+    t = tensor.contiguous()
+    if t.dim() == 0:
+        t = t.view(1)
+    dim0 = torch.tensor([t.shape[0]], dtype=torch.long, device=t.device)
+    sizes = [torch.empty_like(dim0) for _ in range(n)]
+    dist.all_gather(sizes, dim0, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    if mx != t.shape[0]:
+        pad = torch.zeros((mx - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        t = torch.cat([t, pad])
+    bufs = [torch.empty_like(t) for _ in range(n)]
+    work = dist.all_gather(bufs, t, group=group, async_op=True)
+
+    def post(_o, bufs=bufs, sizes=sizes):
+        return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+
+    return _register(work, None, post, f"allgather.{name or 'tensor'}")
+
+
+def allgather(tensor, name=None, process_set=None):
+    return synchronize(allgather_async(tensor, name, process_set))
+
+
+def alltoall(tensor, splits=None, name=None, process_set=None):
+    """Scatter slices of dim 0 to every rank and gather what they send back (``hvd.alltoall``).
+    Returns ``(output, received_splits)``."""
+    basics._require()
+    group = _group(process_set)
+    n = _group_size(group)
+    if splits is None:
+        if tensor.shape[0] % n:
+            raise ValueError("alltoall: first dimension must divide the world size when splits is None")
+        splits = [tensor.shape[0] // n] * n
+    splits = [int(s) for s in (splits.tolist() if torch.is_tensor(splits) else splits)]
+    if n == 1:
+        return tensor.clone(), torch.tensor(splits)
+    send_counts = torch.tensor(splits, dtype=torch.long, device=tensor.device)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    rsplits = [int(x) for x in recv_counts.tolist()]
+    out = torch.empty((sum(rsplits),) + tuple(tensor.shape[1:]), dtype=tensor.dtype, device=tensor.device)
+    if basics.backend() == "gloo":
+        # gloo has no uneven all_to_all_single for every dtype: emulate with point-to-point.
+        ins = list(torch.split(tensor.contiguous(), splits))
+        outs = list(torch.split(out, rsplits))
+        ops = []
+        me = dist.get_rank(group) if group is not None else basics.rank()
+        for p in range(n):
+            if p == me:
+                outs[p].copy_(ins[p])
+                continue
+            if ins[p].numel():
+                ops.append(dist.P2POp(dist.isend, ins[p].contiguous(), p, group))
+            if outs[p].numel():
+                ops.append(dist.P2POp(dist.irecv, outs[p], p, group))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+    else:
+        dist.all_to_all_single(out, tensor.contiguous(), rsplits, splits, group=group)
+    return out, torch.tensor(rsplits)
+
+
+def reducescatter(tensor, op=ReduceOp.Average, name=None, process_set=None):
+    """Reduce across ranks, then return this rank's dim-0 slice (``hvd.reducescatter``)."""
+    basics._require()
+    group = _group(process_set)
+    n = _group_size(group)
+    if n == 1:
+        return tensor.clone()
+    op = ReduceOp(op)
+    t = tensor.contiguous()
+    dim0 = t.shape[0]
+    base, rem = divmod(dim0, n)
+    counts = [base + (1 if i < rem else 0) for i in range(n)]
+    me = dist.get_rank(group) if group is not None else basics.rank()
+    if rem == 0 and basics.backend() == "nccl":
+        out = torch.empty((counts[me],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, t, op=_torch_op(op), group=group)
+    else:
+        full = t.clone()
+        dist.all_reduce(full, op=_torch_op(op), group=group)
+        start = sum(counts[:me])
+        out = full[start:start + counts[me]].clone()
+    if op == ReduceOp.Average:
+        out.div_(n)
+    return out
+
+
+def barrier(process_set=None):
+    basics._require()
+    if basics.size() > 1:
+        if basics.backend() == "nccl":
+            dist.barrier(device_ids=[basics.device().index])
+        else:
+            dist.barrier()
+
+
+def join(device=-1) -> int:
+    """Horovod ``join``: block until every rank arrives; returns the last rank to join."""
+    basics._require()
+    t = torch.tensor([basics.rank()], dtype=torch.long, device=basics.device())
+    if basics.size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
+
+
+def broadcast_object(obj, root_rank=0, name=None, process_set=None):
+    basics._require()
+    if basics.size() == 1:
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=root_rank, group=_group(process_set),
+                               device=basics.device() if basics.backend() == "nccl" else None)
+    return lst[0]
+
+
+def allgather_object(obj, name=None, process_set=None):
+    basics._require()
+    if basics.size() == 1:
+        return [obj]
+    out = [None] * basics.size()
+    dist.all_gather_object(out, obj, group=_group(process_set))
+    return out

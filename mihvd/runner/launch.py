@@ -1,0 +1,341 @@
+"""``mihvdrun`` — an mpirun/horovodrun-compatible launcher.
+
+The reference's MPIJob launcher runs (horovod/tensorflow-mnist.yaml:17-38)::
+
+    mpirun -np 2 --allow-run-as-root -bind-to none -map-by slot -x LD_LIBRARY_PATH -x PATH \
+           -mca pml ob1 -mca btl ^openib python /examples/tensorflow_mnist.py
+
+``mihvdrun`` accepts exactly that argv (plus horovodrun's ``-np N -H host:slots``). MPI transport
+flags (``-mca``, ``-bind-to``) are accepted and ignored — the data plane is RCCL over xGMI, the
+bootstrap is torch's TCP store at ``MASTER_ADDR:MASTER_PORT``. Ranks are laid out by
+``-map-by slot`` (fill each host) or ``-map-by node`` (round robin); local ranks on a host get
+consecutive GPUs. Remote hosts are reached over ssh, as mpirun does inside an MPIJob (hostfile from
+``--hostfile`` or ``$OMPI_MCA_orte_default_hostfile``, which the MPI Operator mounts).
+
+Each rank receives ``RANK WORLD_SIZE LOCAL_RANK LOCAL_WORLD_SIZE GROUP_RANK MASTER_ADDR
+MASTER_PORT`` and the Open MPI equivalents ``OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK,LOCAL_SIZE}``.
+If any rank exits non-zero the others are terminated and that exit code is returned (mpirun
+semantics: one dead rank aborts the job).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shlex
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+from dataclasses import dataclass, field
+
+_IGNORED_WITH_ARG = {"-bind-to", "--bind-to", "-map-by", "--map-by", "-rank-by", "--rank-by", "--output-filename",
+                     "-output-filename", "--prefix", "-prefix", "-wdir", "--wdir", "-wd"}
+_IGNORED_FLAGS = {"--allow-run-as-root", "-allow-run-as-root", "--oversubscribe", "-oversubscribe",
+                  "--report-bindings", "-report-bindings", "--display-map", "-display-map", "-q", "--quiet",
+                  "--gloo", "--mpi", "--nccl", "--rccl", "--use-hwthread-cpus", "-use-hwthread-cpus",
+                  "--bind-to-core", "-bind-to-core", "--enable-recovery", "-v"}
+
+
+@dataclass
+class LaunchSpec:
+    np: int = 1
+    hosts: list[tuple[str, int]] = field(default_factory=list)
+    map_by: str = "slot"
+    env_forward: dict[str, str | None] = field(default_factory=dict)
+    mca: list[tuple[str, str]] = field(default_factory=list)
+    ignored: list[str] = field(default_factory=list)
+    tag_output: bool = False
+    master_addr: str | None = None
+    master_port: int | None = None
+    ssh_port: int | None = None
+    extra_env: dict[str, str] = field(default_factory=dict)
+    start_timeout: float = 120.0
+    verbose: bool = False
+    command: list[str] = field(default_factory=list)
+
+
+def parse_hosts(spec: str) -> list[tuple[str, int]]:
+    out = []
+    for item in spec.split(","):
+        item = item.strip()
+        if not item:
+            continue
+        if ":" in item:
+            h, s = item.rsplit(":", 1)
+            out.append((h, int(s)))
+        else:
+            out.append((item, 1))
+    return out
+
+
+def parse_hostfile(path: str) -> list[tuple[str, int]]:
+    out = []
+    with open(path) as f:
+        for line in f:
+            line = line.split("#", 1)[0].strip()
+            if not line:
+                continue
+            parts = line.split()
+            host, slots = parts[0], 1
+            if ":" in host:
+                host, s = host.rsplit(":", 1)
+                slots = int(s)
+            for p in parts[1:]:
+                if p.startswith("slots="):
+                    slots = int(p.split("=", 1)[1])
+            out.append((host, slots))
+    return out
+
+
+def parse_args(argv: list[str]) -> LaunchSpec:
+    """Hand-rolled parser: mpirun mixes single-dash long options with GNU style."""
+    spec = LaunchSpec()
+    i = 0
+    n = len(argv)
+    hostfile = None
+    np_given = False
+
+    def need(k):
+        if i + 1 >= n:
+            raise SystemExit(f"mihvdrun: option {k} needs an argument")
+        return argv[i + 1]
+
+    while i < n:
+        a = argv[i]
+        if a == "--":
+            spec.command = argv[i + 1:]
+            break
+        if a in ("-np", "--np", "-n", "-c"):
+            spec.np = int(need(a)); np_given = True; i += 2; continue
+        if a.startswith("-np="):
+            spec.np = int(a.split("=", 1)[1]); np_given = True; i += 1; continue
+        if a in ("-H", "--host", "-host", "--hosts"):
+            spec.hosts = parse_hosts(need(a)); i += 2; continue
+        if a in ("--hostfile", "-hostfile", "--machinefile", "-machinefile", "-hf"):
+            hostfile = need(a); i += 2; continue
+        if a in ("-map-by", "--map-by"):
+            spec.map_by = need(a).split(":", 1)[0].lower(); spec.ignored.append(f"{a} {argv[i + 1]}"); i += 2; continue
+        if a in ("-x",):
+            kv = need(a)
+            if "=" in kv:
+                k, v = kv.split("=", 1)
+                spec.env_forward[k] = v
+            else:
+                spec.env_forward[kv] = None
+            i += 2; continue
+        if a in ("-mca", "--mca", "-gmca", "--gmca"):
+            if i + 2 >= n:
+                raise SystemExit(f"mihvdrun: {a} needs two arguments")
+            spec.mca.append((argv[i + 1], argv[i + 2])); i += 3; continue
+        if a in ("--tag-output", "-tag-output"):
+            spec.tag_output = True; i += 1; continue
+        if a in ("--master-addr", "--master_addr"):
+            spec.master_addr = need(a); i += 2; continue
+        if a in ("--master-port", "--master_port"):
+            spec.master_port = int(need(a)); i += 2; continue
+        if a in ("-p", "--ssh-port"):
+            spec.ssh_port = int(need(a)); i += 2; continue
+        if a in ("--start-timeout",):
+            spec.start_timeout = float(need(a)); i += 2; continue
+        if a in ("--verbose",):
+            spec.verbose = True; i += 1; continue
+        if a in ("--timeline-filename",):
+            spec.extra_env["MIHVD_TIMELINE"] = need(a); i += 2; continue
+        if a in ("--fusion-threshold-mb",):
+            spec.extra_env["MIHVD_FUSION_THRESHOLD"] = str(int(float(need(a)) * 1024 * 1024)); i += 2; continue
+        if a in ("--cycle-time-ms",):
+            spec.extra_env["MIHVD_CYCLE_TIME"] = need(a); i += 2; continue
+        if a in ("--stall-check-warning-time-seconds",):
+            spec.extra_env["MIHVD_STALL_CHECK_TIME_SECONDS"] = need(a); i += 2; continue
+        if a in ("--stall-check-shutdown-time-seconds",):
+            spec.extra_env["MIHVD_STALL_SHUTDOWN_TIME_SECONDS"] = need(a); i += 2; continue
+        if a in ("--no-stall-check",):
+            spec.extra_env["MIHVD_STALL_CHECK_DISABLE"] = "1"; i += 1; continue
+        if a in ("--hierarchical-allreduce",):
+            spec.extra_env["MIHVD_HIERARCHICAL_ALLREDUCE"] = "1"; i += 1; continue
+        if a in _IGNORED_WITH_ARG:
+            spec.ignored.append(f"{a} {need(a)}"); i += 2; continue
+        if a in _IGNORED_FLAGS:
+            spec.ignored.append(a); i += 1; continue
+        if a.startswith("-"):
+            raise SystemExit(f"mihvdrun: unknown option {a}")
+        spec.command = argv[i:]
+        break
+    if not spec.command:
+        raise SystemExit("mihvdrun: no command given")
+    if hostfile is None and not spec.hosts and os.environ.get("OMPI_MCA_orte_default_hostfile"):
+        hostfile = os.environ["OMPI_MCA_orte_default_hostfile"]
+    if hostfile:
+        spec.hosts = parse_hostfile(hostfile)
+    if not spec.hosts:
+        spec.hosts = [("localhost", spec.np)]
+    if not np_given:
+        spec.np = sum(s for _, s in spec.hosts)
+    return spec
+
+
+def assign_ranks(hosts: list[tuple[str, int]], np_: int, map_by: str = "slot"):
+    """Returns [(rank, host, local_rank, local_size, node_index)]."""
+    total = sum(s for _, s in hosts)
+    if np_ > total:
+        raise SystemExit(f"mihvdrun: -np {np_} exceeds the {total} slots available on {hosts}")
+    per_host: list[list[int]] = [[] for _ in hosts]
+    if map_by == "node":
+        r = 0
+        while r < np_:
+            for h, (_, slots) in enumerate(hosts):
+                if r < np_ and len(per_host[h]) < slots:
+                    per_host[h].append(r)
+                    r += 1
+    else:
+        r = 0
+        for h, (_, slots) in enumerate(hosts):
+            take = min(slots, np_ - r)
+            per_host[h].extend(range(r, r + take))
+            r += take
+    out = []
+    node = 0
+    for h, ranks in enumerate(per_host):
+        if not ranks:
+            continue
+        for lr, rank in enumerate(ranks):
+            out.append((rank, hosts[h][0], lr, len(ranks), node))
+        node += 1
+    return sorted(out)
+
+
+def _is_local(host: str) -> bool:
+    if host in ("localhost", "127.0.0.1", "::1"):
+        return True
+    try:
+        return host in (socket.gethostname(), socket.getfqdn())
+    except Exception:
+        return False
+
+
+def _free_port(addr="127.0.0.1") -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((addr if addr != "localhost" else "127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def build_rank_env(spec: LaunchSpec, rank, local_rank, local_size, node, master_addr, master_port, base_env=None):
+    base = dict(os.environ if base_env is None else base_env)
+    env = {}
+    for k, v in spec.env_forward.items():
+        if v is not None:
+            env[k] = v
+        elif k in base:
+            env[k] = base[k]
+    env.update(spec.extra_env)
+    env.update({
+        "RANK": str(rank), "WORLD_SIZE": str(spec.np), "LOCAL_RANK": str(local_rank),
+        "LOCAL_WORLD_SIZE": str(local_size), "GROUP_RANK": str(node), "MASTER_ADDR": master_addr,
+        "MASTER_PORT": str(master_port), "OMPI_COMM_WORLD_RANK": str(rank), "OMPI_COMM_WORLD_SIZE": str(spec.np),
+        "OMPI_COMM_WORLD_LOCAL_RANK": str(local_rank), "OMPI_COMM_WORLD_LOCAL_SIZE": str(local_size),
+        "MIHVD_LAUNCHED": "1",
+    })
+    return env
+
+
+class _Proc:
+    def __init__(self, rank, popen):
+        self.rank = rank
+        self.popen = popen
+
+
+def _pump(stream, out, prefix):
+    for line in iter(stream.readline, b""):
+        if prefix:
+            out.buffer.write(prefix.encode() + line)
+        else:
+            out.buffer.write(line)
+        out.flush()
+    stream.close()
+
+
+def launch(spec: LaunchSpec) -> int:
+    layout = assign_ranks(spec.hosts, spec.np, spec.map_by)
+    first_host = layout[0][1]
+    all_local = all(_is_local(h) for _, h, *_ in layout)
+    master_addr = spec.master_addr or ("127.0.0.1" if all_local else first_host)
+    master_port = spec.master_port or (_free_port() if all_local else 29500)
+    if spec.verbose:
+        for m in spec.ignored:
+            print(f"mihvdrun: ignoring MPI option {m}", file=sys.stderr)
+        for k, v in spec.mca:
+            print(f"mihvdrun: ignoring MCA parameter {k}={v} (data plane is RCCL)", file=sys.stderr)
+    procs: list[_Proc] = []
+    threads = []
+    for rank, host, lr, ls, node in layout:
+        renv = build_rank_env(spec, rank, lr, ls, node, master_addr, master_port)
+        if _is_local(host):
+            env = dict(os.environ)
+            env.update(renv)
+            cmd = spec.command
+        else:
+            exports = " ".join(f"{k}={shlex.quote(v)}" for k, v in renv.items())
+            remote = f"cd {shlex.quote(os.getcwd())} && env {exports} " + " ".join(shlex.quote(c) for c in spec.command)
+            cmd = ["ssh", "-o", "StrictHostKeyChecking=no"] + (["-p", str(spec.ssh_port)] if spec.ssh_port else []) + [host, remote]
+            env = dict(os.environ)
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
+        procs.append(_Proc(rank, p))
+        pre_o = f"[1,{rank}]<stdout>:" if spec.tag_output else ""
+        pre_e = f"[1,{rank}]<stderr>:" if spec.tag_output else ""
+        for s, o, pre in ((p.stdout, sys.stdout, pre_o), (p.stderr, sys.stderr, pre_e)):
+            t = threading.Thread(target=_pump, args=(s, o, pre), daemon=True)
+            t.start()
+            threads.append(t)
+
+    def terminate_all(sig=signal.SIGTERM):
+        for pr in procs:
+            if pr.popen.poll() is None:
+                try:
+                    os.killpg(pr.popen.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_signal(signum, frame):
+        terminate_all(signal.SIGTERM)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGINT, signal.SIGTERM)}
+    exit_code = 0
+    try:
+        remaining = set(range(len(procs)))
+        while remaining:
+            for i in list(remaining):
+                rc = procs[i].popen.poll()
+                if rc is None:
+                    continue
+                remaining.discard(i)
+                if rc != 0 and exit_code == 0:
+                    exit_code = rc if rc > 0 else 128 - rc
+                    print(f"mihvdrun: rank {procs[i].rank} exited with code {rc}; terminating the job",
+                          file=sys.stderr, flush=True)
+                    terminate_all(signal.SIGTERM)
+                    deadline = time.time() + 10
+                    while time.time() < deadline and any(p.popen.poll() is None for p in procs):
+                        time.sleep(0.05)
+                    terminate_all(signal.SIGKILL)
+            time.sleep(0.02)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+        for t in threads:
+            t.join(timeout=5)
+    return exit_code
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    if argv and argv[0] in ("-h", "--help"):
+        print(__doc__)
+        return 0
+    spec = parse_args(argv)
+    return launch(spec)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

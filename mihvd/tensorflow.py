@@ -1,0 +1,305 @@
+"""TF1-shaped training API: ``import mihvd.tensorflow as hvd``.
+
+The reference's launched entrypoint (horovod/tensorflow_mnist.py) drives training with
+``tf.train.MonitoredTrainingSession`` and three hooks (:138-150, :165-171). This module gives the
+same control flow on PyTorch-ROCm:
+
+* ``BroadcastGlobalVariablesHook(root_rank)`` — after the session is created *and* restored,
+  broadcasts every global variable (weights, optimizer slots, global_step) from ``root_rank``.
+* ``StopAtStepHook(last_step=...)``, ``LoggingTensorHook(tensors, every_n_iter)``,
+  ``StepCounterHook`` (``global_step/sec``), ``CheckpointSaverHook`` (rank-0 ``./checkpoints``).
+* ``MonitoredTrainingSession(checkpoint_dir, hooks, state=...)`` — restore latest checkpoint →
+  hooks' ``after_create_session`` → ``run()`` loop with ``before_run``/``after_run`` → final save.
+
+A *train state* object owns the variables (see ``TorchTrainState`` and
+``mihvd.models.fused_mnist.FusedMNISTTrainer``): ``variables()`` maps TF names to tensors,
+``load_variables()`` restores them, ``broadcast(root)`` syncs them, ``global_step`` counts steps.
+"""
+from __future__ import annotations
+
+import logging
+import time
+
+import torch
+
+from .basics import *  # noqa: F401,F403  (init, rank, size, Average, Adasum, ...)
+from . import basics as _b
+from .parallel.collectives import (allgather, allreduce, broadcast, broadcast_object,  # noqa: F401
+                                   broadcast_)
+from .parallel.compression import Compression  # noqa: F401
+from .parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters  # noqa: F401
+from .utils import checkpoint as ckpt
+from .utils.logging import log_kv
+
+log = logging.getLogger("mihvd")
+
+
+# ------------------------------------------------------------------------------------------ #
+# Train state
+# ------------------------------------------------------------------------------------------ #
+class TorchTrainState:
+    """Variables of a TF-named torch model (``ordered_parameters()``) plus a torch Adam."""
+
+    def __init__(self, model, optimizer=None):
+        self.model = model
+        self.optimizer = optimizer
+        self.global_step = 0
+
+    def named_variables(self):
+        if hasattr(self.model, "ordered_parameters"):
+            return list(self.model.ordered_parameters())
+        return [(n.replace(".", "/"), p) for n, p in self.model.named_parameters()]
+
+    def variables(self):
+        return ckpt.adam_to_tf_vars(self.named_variables(), self.optimizer, self.global_step)
+
+    def load_variables(self, variables):
+        self.global_step = ckpt.tf_vars_to_adam(variables, self.named_variables(), self.optimizer)
+
+    def broadcast(self, root_rank=0):
+        broadcast_parameters(self.model.state_dict(), root_rank)
+        if self.optimizer is not None:
+            broadcast_optimizer_state(self.optimizer, root_rank)
+        self.global_step = int(broadcast_object(self.global_step, root_rank))
+
+
+# ------------------------------------------------------------------------------------------ #
+# Hooks
+# ------------------------------------------------------------------------------------------ #
+class SessionRunArgs:
+    def __init__(self, fetches=None):
+        self.fetches = fetches
+
+
+class SessionRunValues:
+    def __init__(self, results):
+        self.results = results
+
+
+class SessionRunContext:
+    def __init__(self, session):
+        self.session = session
+        self._stop = False
+
+    def request_stop(self):
+        self._stop = True
+        self.session._stop_requested = True
+
+    @property
+    def stop_requested(self):
+        return self._stop
+
+
+class SessionRunHook:
+    def begin(self):
+        pass
+
+    def after_create_session(self, session, coord=None):
+        pass
+
+    def before_run(self, run_context):
+        return None
+
+    def after_run(self, run_context, run_values):
+        pass
+
+    def end(self, session):
+        pass
+
+
+class BroadcastGlobalVariablesHook(SessionRunHook):
+    """Broadcast all global variables from ``root_rank`` after session creation/restore
+    (reference: horovod/tensorflow_mnist.py:139-143)."""
+
+    def __init__(self, root_rank: int = 0, device: str = ""):
+        self.root_rank = root_rank
+        self.broadcasted = False
+
+    def after_create_session(self, session, coord=None):
+        session.state.broadcast(self.root_rank)
+        self.broadcasted = True
+
+
+class StopAtStepHook(SessionRunHook):
+    def __init__(self, num_steps: int | None = None, last_step: int | None = None):
+        if (num_steps is None) == (last_step is None):
+            raise ValueError("exactly one of num_steps and last_step must be specified")
+        self._num_steps = num_steps
+        self._last_step = last_step
+
+    def after_create_session(self, session, coord=None):
+        if self._last_step is None:
+            self._last_step = session.state.global_step + self._num_steps
+        if session.state.global_step >= self._last_step:
+            session._stop_requested = True
+
+    def after_run(self, run_context, run_values):
+        if run_context.session.state.global_step >= self._last_step:
+            run_context.request_stop()
+
+    @property
+    def last_step(self):
+        return self._last_step
+
+
+class LoggingTensorHook(SessionRunHook):
+    """Print named values every ``every_n_iter`` runs, on every rank (tensorflow_mnist.py:148-149).
+
+    ``tensors`` maps display names to result keys (``'global_step'`` is the session's step)."""
+
+    def __init__(self, tensors, every_n_iter: int = 10, formatter=None):
+        if isinstance(tensors, (list, tuple)):
+            tensors = {t: t for t in tensors}
+        self.tensors = {k: (v if isinstance(v, str) else k) for k, v in tensors.items()}
+        self.every_n = every_n_iter
+        self.formatter = formatter
+        self._iter = 0
+        self._t = None
+        self.lines: list[str] = []
+
+    def after_run(self, run_context, run_values):
+        if self._iter % self.every_n == 0:
+            vals = {}
+            res = run_values.results or {}
+            for name, key in self.tensors.items():
+                if key in ("global_step", "step") and key not in res:
+                    v = run_context.session.state.global_step
+                else:
+                    v = res.get(key)
+                if torch.is_tensor(v):
+                    v = v.item() if v.numel() == 1 else v.tolist()
+                vals[name] = v
+            now = time.time()
+            el = None if self._t is None else now - self._t
+            self._t = now
+            if self.formatter:
+                line = self.formatter(vals)
+                print(line, flush=True)
+            else:
+                line = log_kv("", **vals, **({"sec": round(el, 3)} if el is not None else {}))
+            self.lines.append(line)
+        self._iter += 1
+
+
+class StepCounterHook(SessionRunHook):
+    """``global_step/sec`` (+ images/sec when ``batch_size`` is given) every N steps."""
+
+    def __init__(self, every_n_steps: int = 100, batch_size: int | None = None, world_size: int | None = None):
+        self.every_n = every_n_steps
+        self.batch_size = batch_size
+        self.world_size = world_size
+        self._t0 = None
+        self._s0 = None
+        self.last_rate = None
+
+    def after_create_session(self, session, coord=None):
+        self._t0 = time.perf_counter()
+        self._s0 = session.state.global_step
+
+    def after_run(self, run_context, run_values):
+        s = run_context.session.state.global_step
+        if s - self._s0 >= self.every_n:
+            session = run_context.session
+            session.state_sync()
+            now = time.perf_counter()
+            rate = (s - self._s0) / (now - self._t0)
+            self.last_rate = rate
+            kv = {"global_step/sec": round(rate, 2)}
+            if self.batch_size:
+                ws = self.world_size or (_b.size() if _b.is_initialized() else 1)
+                kv["img_per_sec"] = round(rate * self.batch_size * ws, 1)
+            log_kv("", **kv)
+            self._t0, self._s0 = now, s
+
+
+class CheckpointSaverHook(SessionRunHook):
+    def __init__(self, checkpoint_dir, save_secs=600, save_steps=None, max_to_keep=5):
+        self.mgr = ckpt.CheckpointManager(checkpoint_dir, save_secs, save_steps, max_to_keep)
+        self.saved: list[str] = []
+
+    def after_create_session(self, session, coord=None):
+        self.mgr._last_step = session.state.global_step
+
+    def after_run(self, run_context, run_values):
+        step = run_context.session.state.global_step
+        if self.mgr.should_save(step):
+            run_context.session.state_sync()
+            self.saved.append(self.mgr.save(run_context.session.state.variables(), step))
+
+    def end(self, session):
+        step = session.state.global_step
+        if self.mgr._last_step != step:
+            session.state_sync()
+            self.saved.append(self.mgr.save(session.state.variables(), step))
+
+
+# ------------------------------------------------------------------------------------------ #
+# Session
+# ------------------------------------------------------------------------------------------ #
+class MonitoredTrainingSession:
+    """Context manager mirroring ``tf.train.MonitoredTrainingSession`` semantics.
+
+    ``run(train_op, feed_dict)`` calls ``train_op(**feed_dict)`` (or ``train_op(*feed_dict)``),
+    increments ``global_step`` and returns the step's results dict."""
+
+    def __init__(self, checkpoint_dir=None, hooks=(), config=None, state=None, save_checkpoint_secs=600,
+                 save_checkpoint_steps=None, log_step_count_steps=None, max_to_keep=5, chief_only_hooks=()):
+        if state is None:
+            raise ValueError("MonitoredTrainingSession needs a train state (model variables)")
+        self.state = state
+        self.checkpoint_dir = checkpoint_dir
+        self.hooks = list(hooks)
+        if checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps):
+            self.hooks.append(CheckpointSaverHook(checkpoint_dir, save_checkpoint_secs, save_checkpoint_steps, max_to_keep))
+        if log_step_count_steps:
+            self.hooks.append(StepCounterHook(log_step_count_steps))
+        self.hooks.extend(chief_only_hooks)
+        self._stop_requested = False
+        self.restored_from = None
+
+    def state_sync(self):
+        if hasattr(self.state, "sync"):
+            self.state.sync()
+
+    def __enter__(self):
+        for h in self.hooks:
+            h.begin()
+        if self.checkpoint_dir:
+            prefix = ckpt.latest_checkpoint(self.checkpoint_dir)
+            if prefix is not None:
+                self.state.load_variables(ckpt.Saver.restore(prefix))
+                self.restored_from = prefix
+                log.info("restored %s (global_step=%d)", prefix, self.state.global_step)
+        for h in self.hooks:
+            h.after_create_session(self, None)
+        return self
+
+    def should_stop(self) -> bool:
+        return self._stop_requested
+
+    def run(self, train_op, feed_dict=None):
+        ctx = SessionRunContext(self)
+        for h in self.hooks:
+            h.before_run(ctx)
+        if feed_dict is None:
+            res = train_op()
+        elif isinstance(feed_dict, dict):
+            res = train_op(**feed_dict)
+        else:
+            res = train_op(*feed_dict)
+        self.state.global_step += 1
+        if res is not None and not isinstance(res, dict):
+            res = {"result": res}
+        vals = SessionRunValues(res)
+        for h in self.hooks:
+            h.after_run(ctx, vals)
+        return res
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is None:
+            for h in self.hooks:
+                h.end(self)
+        return False
+
+    def close(self):
+        self.__exit__(None, None, None)

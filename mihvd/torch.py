@@ -1,0 +1,15 @@
+"""Horovod-PyTorch-compatible API surface: ``import mihvd.torch as hvd``.
+
+Everything the reference's entrypoints call through ``horovod.tensorflow`` /
+``horovod.tensorflow.keras`` is available here for PyTorch-ROCm models.
+"""
+from .basics import (Adasum, Average, Max, Min, Product, ReduceOp, Sum, backend, config, cross_rank, cross_size,
+                     cuda_built, device, gloo_built, gloo_enabled, init, is_homogeneous, is_initialized, local_rank,
+                     local_size, mpi_built, mpi_enabled, mpi_threads_supported, nccl_built, rank, rccl_built,
+                     rocm_built, shutdown, size, start_timeline, stop_timeline)
+from .parallel.collectives import (allgather, allgather_async, allgather_object, allreduce, allreduce_,
+                                   allreduce_async, allreduce_async_, alltoall, barrier, broadcast, broadcast_,
+                                   broadcast_async, broadcast_async_, broadcast_object, grouped_allreduce, join, poll,
+                                   reducescatter, synchronize)
+from .parallel.compression import Compression
+from .parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters

@@ -1,0 +1,102 @@
+"""Multi-process CPU tests: ranks are separate processes launched by ``mihvdrun`` (gloo backend),
+rendezvousing over 127.0.0.1 — the "multi-node without a cluster" strategy of SURVEY.md §4."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "workers", "dist_worker.py")
+
+pytestmark = pytest.mark.slow
+
+
+def run_scenario(tmp_path, scenario, np_=2, env=None, timeout=120, expect_ok=True):
+    e = dict(os.environ)
+    e.update({"MIHVD_BACKEND": "gloo", "PYTHONPATH": ROOT, "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", str(np_), "--allow-run-as-root", "-bind-to", "none",
+           "-map-by", "slot", "-x", "PATH", "-mca", "pml", "ob1", "-mca", "btl", "^openib",
+           sys.executable, WORKER, scenario, str(tmp_path)]
+    p = subprocess.run(cmd, env=e, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    if expect_ok:
+        assert p.returncode == 0, p.stdout + p.stderr
+    outs = []
+    for r in range(np_):
+        f = tmp_path / f"{scenario}.{r}.json"
+        outs.append(json.loads(f.read_text()) if f.exists() else None)
+    return p, outs
+
+
+def test_collectives_two_ranks(tmp_path):
+    _, (a, b) = run_scenario(tmp_path, "collectives")
+    base = [float(i) for i in range(6)]
+    assert a["sum"] == [2 * x + 1 for x in base] == b["sum"]
+    assert a["avg"] == [x + 0.5 for x in base]
+    assert a["min"] == base and a["max"] == [x + 1 for x in base]
+    assert a["bf16"] == a["sum"]
+    assert a["fp16"] == a["avg"]
+    assert a["allgather"] == [[0.0, 0.0], [1.0, 1.0], [1.0, 1.0]] == b["allgather"]
+    assert a["broadcast"] == [1.0] * 3 and b["broadcast_"] == [0.0] * 3
+    # alltoall: rank r receives slice r from every rank
+    assert a["alltoall"] == [0.0, 1.0, 100.0, 101.0] and b["alltoall"] == [2.0, 3.0, 102.0, 103.0]
+    assert a["reducescatter"] == [[3.0] * 3] * 2
+    assert a["object"] == {"rank": 0, "msg": "hi"} == b["object"]
+    assert a["allgather_object"] == [0, 10]
+    assert a["grouped"] == [[1.0] * 3, [[3.0, 3.0], [3.0, 3.0]]]
+    assert a["async"] == [1.0] * 4
+    assert a["join"] == 1
+
+
+def test_dp_equivalence(tmp_path):
+    _, outs = run_scenario(tmp_path, "dp_equivalence")
+    for o in outs:
+        assert o["maxdiff_0"] < 1e-5 and o["maxdiff_67108864"] < 1e-5
+        assert o["nbuckets_0"] > 1 and o["nbuckets_67108864"] == 1
+
+
+def test_dp_equivalence_four_ranks(tmp_path):
+    _, outs = run_scenario(tmp_path, "dp_equivalence", np_=4)
+    assert all(o["maxdiff_0"] < 1e-5 for o in outs)
+
+
+def test_backward_passes_per_step(tmp_path):
+    _, outs = run_scenario(tmp_path, "bpps")
+    assert all(o["diff"] < 1e-4 for o in outs)
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4])
+def test_adasum(tmp_path, np_):
+    _, outs = run_scenario(tmp_path, "adasum", np_=np_)
+    for o in outs:
+        assert o["diff"] < 1e-9
+        assert o["param_spread"] < 1e-6
+
+
+def test_broadcast_optimizer_state(tmp_path):
+    _, (a, b) = run_scenario(tmp_path, "optimizer_state")
+    assert a == b and a["nstate"] > 0 and a["lr"] == pytest.approx(1e-3)
+
+
+def test_metric_average(tmp_path):
+    _, (a, b) = run_scenario(tmp_path, "metric_average")
+    assert a["loss"] == b["loss"] == 0.5 and a["accuracy"] == 1.0 and a["name"] == "x"
+
+
+def test_stall_inspector_aborts_job(tmp_path):
+    env = {"MIHVD_STALL_CHECK_TIME_SECONDS": "1", "MIHVD_STALL_SHUTDOWN_TIME_SECONDS": "3"}
+    p, outs = run_scenario(tmp_path, "stall", env=env, expect_ok=False, timeout=120)
+    assert p.returncode != 0
+    assert "stall inspector" in p.stderr
+    assert outs[0] is None
+
+
+def test_fault_kill_tears_down_job(tmp_path):
+    p, outs = run_scenario(tmp_path, "fault", env={"MIHVD_FAULT": "kill:rank=1:step=3:code=7"}, expect_ok=False)
+    assert p.returncode == 7
+    assert "rank 1 exited with code 7" in p.stderr
+    assert outs == [None, None]

@@ -1,0 +1,182 @@
+"""Multi-process scenarios, launched by tests through ``mihvdrun -np N`` (gloo on CPU).
+
+Usage: python dist_worker.py <scenario> <outdir>. Each rank writes <outdir>/<scenario>.<rank>.json.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mihvd.torch as hvd  # noqa: E402
+
+
+def out(outdir, name, payload):
+    with open(os.path.join(outdir, f"{name}.{hvd.rank()}.json"), "w") as f:
+        json.dump(payload, f)
+
+
+def sc_collectives(outdir):
+    r, n = hvd.rank(), hvd.size()
+    res = {}
+    t = torch.arange(6, dtype=torch.float32) + r
+    res["sum"] = hvd.allreduce(t, op=hvd.Sum).tolist()
+    res["avg"] = hvd.allreduce(t).tolist()
+    res["min"] = hvd.allreduce(t, op=hvd.Min).tolist()
+    res["max"] = hvd.allreduce(t, op=hvd.Max).tolist()
+    res["bf16"] = hvd.allreduce(t, op=hvd.Sum, compression=hvd.Compression.bf16).tolist()
+    res["fp16"] = hvd.allreduce(t, compression=hvd.Compression.fp16).tolist()
+    x = torch.full((r + 1, 2), float(r))
+    res["allgather"] = hvd.allgather(x).tolist()
+    b = torch.full((3,), float(r))
+    res["broadcast"] = hvd.broadcast(b, root_rank=n - 1).tolist()
+    hvd.broadcast_(b, root_rank=0)
+    res["broadcast_"] = b.tolist()
+    a2a_in = torch.arange(n * 2, dtype=torch.float32) + 100 * r
+    o, splits = hvd.alltoall(a2a_in)
+    res["alltoall"] = o.tolist()
+    res["reducescatter"] = hvd.reducescatter(torch.ones(n * 2, 3) * (r + 1), op=hvd.Sum).tolist()
+    res["object"] = hvd.broadcast_object({"rank": r, "msg": "hi"}, root_rank=0)
+    res["allgather_object"] = hvd.allgather_object(r * 10)
+    g = hvd.grouped_allreduce([torch.ones(3) * r, torch.ones(2, 2) * (r + 1)], op=hvd.Sum)
+    res["grouped"] = [x.tolist() for x in g]
+    h = hvd.allreduce_async(torch.ones(4) * r, op=hvd.Sum, name="async")
+    while not hvd.poll(h):
+        time.sleep(0.001)
+    res["async"] = hvd.synchronize(h).tolist()
+    res["join"] = hvd.join()
+    out(outdir, "collectives", res)
+
+
+def _model(seed):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Tanh(), torch.nn.Linear(16, 4))
+
+
+def sc_dp_equivalence(outdir):
+    """N ranks × B samples == 1 process × N·B samples (Average)."""
+    r, n = hvd.rank(), hvd.size()
+    gen = torch.Generator().manual_seed(7)
+    X = torch.randn(n * 5, 8, generator=gen)
+    Y = torch.randn(n * 5, 4, generator=gen)
+    res = {}
+    for thresh in (0, 64 * 1024 * 1024):
+        m = _model(seed=100 + r)  # different init on purpose: broadcast must fix it
+        hvd.broadcast_parameters(m.state_dict(), root_rank=0)
+        opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), named_parameters=m.named_parameters(),
+                                       fusion_threshold=thresh if thresh else 64)
+        ref = _model(seed=100)
+        ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
+        for step in range(3):
+            opt.zero_grad()
+            xs, ys = X[r * 5:(r + 1) * 5], Y[r * 5:(r + 1) * 5]
+            torch.nn.functional.mse_loss(m(xs), ys).backward()
+            opt.step()
+            ropt.zero_grad()
+            # mean of per-rank means == global mean (equal shard sizes)
+            torch.nn.functional.mse_loss(ref(X), Y).backward()
+            ropt.step()
+        diff = max((a - b).abs().max().item() for a, b in zip(m.parameters(), ref.parameters()))
+        res[f"maxdiff_{thresh}"] = diff
+        res[f"nbuckets_{thresh}"] = len(opt.buckets)
+    out(outdir, "dp_equivalence", res)
+
+
+def sc_bpps(outdir):
+    """backward_passes_per_step=2 accumulates locally, then one allreduce."""
+    r, n = hvd.rank(), hvd.size()
+    m = _model(seed=5)
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.0), named_parameters=m.named_parameters(),
+                                   backward_passes_per_step=2, op=hvd.Sum)
+    opt.zero_grad()
+    for k in range(2):
+        m(torch.ones(2, 8) * (r + 1 + k)).sum().backward()
+    opt.step()
+    g = m[2].bias.grad.clone()
+    m2 = _model(seed=5)
+    for rr in range(n):
+        for k in range(2):
+            m2(torch.ones(2, 8) * (rr + 1 + k)).sum().backward()
+    out(outdir, "bpps", {"diff": (g - m2[2].bias.grad).abs().max().item()})
+
+
+def sc_adasum(outdir):
+    from mihvd.parallel.adasum import adasum_reference
+
+    r, n = hvd.rank(), hvd.size()
+    vecs = [torch.tensor([1.0 + i, -2.0 * i, 0.5, 3.0 - i, 1.0, 2.0], dtype=torch.float64) for i in range(n)]
+    segs = [(0, 3), (3, 6)]
+    got = hvd.grouped_allreduce([vecs[r][:3].clone(), vecs[r][3:].clone()], op=hvd.Adasum)
+    ref = adasum_reference(vecs, segs)
+    d = max((torch.cat([got[0], got[1]]) - ref).abs().max().item(), 0)
+    # Optimizer path with Adasum
+    m = _model(seed=1)
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.01), op=hvd.Adasum)
+    opt.zero_grad()
+    m(torch.randn(3, 8) * (r + 1)).sum().backward()
+    opt.step()
+    ps = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    allp = hvd.allgather(ps.view(1, -1))
+    out(outdir, "adasum", {"diff": d, "param_spread": (allp - allp[0]).abs().max().item()})
+
+
+def sc_optimizer_state(outdir):
+    r = hvd.rank()
+    m = _model(seed=r)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3 * (r + 1))
+    if r == 0:  # only the root has optimizer state
+        m(torch.ones(1, 8)).sum().backward()
+        opt.step()
+    hvd.broadcast_parameters(m.state_dict(), 0)
+    hvd.broadcast_optimizer_state(opt, 0)
+    st = opt.state_dict()
+    sig = {
+        "lr": st["param_groups"][0]["lr"],
+        "nstate": len(st["state"]),
+        "m0": float(st["state"][0]["exp_avg"].sum()) if st["state"] else None,
+        "w": float(sum(p.sum() for p in m.parameters())),
+    }
+    out(outdir, "optimizer_state", sig)
+
+
+def sc_metric_average(outdir):
+    import mihvd.keras as khvd
+
+    cb = khvd.callbacks.MetricAverageCallback()
+    logs = {"loss": float(hvd.rank()), "accuracy": 0.5 + hvd.rank(), "name": "x"}
+    cb.on_epoch_end(0, logs)
+    out(outdir, "metric_average", logs)
+
+
+def sc_stall(outdir):
+    # rank 0 issues a collective rank 1 never joins -> stall inspector warns then aborts (134).
+    if hvd.rank() == 0:
+        hvd.allreduce(torch.ones(1), name="lonely")
+    else:
+        time.sleep(30)
+    out(outdir, "stall", {"unexpected": True})
+
+
+def sc_fault(outdir):
+    from mihvd.utils import faults
+
+    for step in range(10):
+        faults.maybe_inject(step)
+        hvd.allreduce(torch.ones(1), name=f"s{step}")
+    out(outdir, "fault", {"completed": True})
+
+
+def main():
+    scenario, outdir = sys.argv[1], sys.argv[2]
+    hvd.init()
+    globals()["sc_" + scenario](outdir)
+    hvd.shutdown()
+
+
+if __name__ == "__main__":
+    main()
