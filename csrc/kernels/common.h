@@ -1,0 +1,82 @@
+// Shared CDNA4 (gfx950) device helpers for the mihvd MNIST hot path.
+//
+// * wave64 everywhere; MFMA is v_mfma_f32_16x16x32_bf16 (bf16 in, fp32 accumulate).
+//   Fragment maps (cdna_hip_programming.md §3): lane l holds
+//     A[m = l&15][k = 8*(l>>4) + j], B[k = 8*(l>>4) + j][n = l&15]   (j = 0..7)
+//     C[row = 4*(l>>4) + i][col = l&15]                              (i = 0..3)
+// * Operand images in LDS come in two shapes:
+//     K-contiguous [row][k]  -> one ds_read_b128 per fragment          (frag_kcontig)
+//     K-strided    [k][col]  -> two ds_read_b64_tr_b16 per fragment    (frag_tr)
+//   so every global tensor is staged in its natural layout and never transposed in HBM.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mihvd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define LDS_PTR(T) __attribute__((address_space(3))) T*
+
+__device__ __forceinline__ u16 f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (inputs are finite)
+  return (u16)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Fragment from a K-contiguous LDS image: rows are M (or N) indices, k contiguous.
+// `p` points at this lane's 8 elements (row r, k0 + 8*(lane>>4)); must be 16-byte aligned.
+__device__ __forceinline__ bf16x8 frag_ld128(const u16* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+// Fragment from a K-strided LDS image ([k][col], col contiguous) via two transposed reads.
+// rowp0 = address of row (8*(lane>>4) + q) of this k-block, rowp1 = that of row +4, where
+// q = (lane&15)>>2, each already offset by the column 4*(lane&3) of the 16-column block.
+__device__ __forceinline__ bf16x8 frag_tr(const u16* rowp0, const u16* rowp1) {
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(short4_t))(rowp0));
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(short4_t))(rowp1));
+  typedef short short8_t __attribute__((ext_vector_type(8)));
+  short8_t s = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, s);
+}
+
+// Counter-based dropout RNG (stateless: mask(seed, step, index) is recomputable anywhere).
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+  h ^= h >> 16; h *= 0x7FEB352Du;
+  h ^= h >> 15; h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+// keep with probability 1-rate; rate is quantised to 1/2^24.
+__device__ __forceinline__ bool dropout_keep(uint32_t seed, uint32_t step, uint32_t idx, uint32_t thresh24) {
+  return (hash3(seed, step, idx) >> 8) >= thresh24;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Step-state words kept on the device so a whole training step replays from a HIP graph:
+//   state[0] = forward step index (read by data/dropout kernels, bumped by the optimizer)
+//   state[1] = optimizer step t   (bumped by the head kernel, read by the optimizer)
+enum { ST_FWD = 0, ST_OPT = 1, ST_WORDS = 4 };
+
+}  // namespace mihvd

@@ -1,0 +1,116 @@
+// Fused optimizer over the flat fp32 parameter buffer (K12/K13 of SURVEY.md §2.5).
+//
+// One pass reads (p, m, v, g) and writes (p, m, v) plus the bf16 shadow of p that the MFMA
+// forward/backward kernels consume, so no separate cast kernel runs per step. The gradient scale
+// (1/size for Average, fused here instead of a separate division) and the TF1 Adam rule
+// (horovod/tensorflow_mnist.py:130):
+//     lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t);  p -= lr_t * m / (sqrt(v) + eps)
+// With a device step-state tensor the step t is read on the device (graph-replayable) and the
+// forward step counter is advanced by block 0.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+
+#include "common.h"
+
+namespace mihvd {
+
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, u16* __restrict__ shadow,
+                                                   int64_t n4, int64_t* __restrict__ state, int64_t host_t, float lr,
+                                                   float b1, float b2, float eps, float gscale, int rule) {
+  const float t = (float)(state ? state[ST_OPT] : host_t);
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  // rule 0: TF1 (eps outside the bias-corrected sqrt); rule 1: torch.optim.Adam
+  const float lr_t = rule == 0 ? lr * sqrtf(bc2) / bc1 : lr / bc1;
+  const float eps_t = rule == 0 ? eps : eps * sqrtf(bc2);
+  const float inv_sqrt_bc2 = rule == 0 ? 1.f : 1.f / sqrtf(bc2);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pa = &pp.x;
+    const float* ga = &gg.x;
+    float* ma = &mm.x;
+    float* va = &vv.x;
+    u16 sh[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = ga[k] * gscale;
+      ma[k] = fmaf(b1, ma[k], (1.f - b1) * gk);
+      va[k] = fmaf(b2, va[k], (1.f - b2) * gk * gk);
+      pa[k] -= lr_t * ma[k] / (sqrtf(va[k]) * inv_sqrt_bc2 + eps_t);
+      sh[k] = f2bf(pa[k]);
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (shadow)
+      reinterpret_cast<uint2*>(shadow)[i] = make_uint2((uint32_t)sh[0] | ((uint32_t)sh[1] << 16),
+                                                       (uint32_t)sh[2] | ((uint32_t)sh[3] << 16));
+  }
+  if (state && blockIdx.x == 0 && threadIdx.x == 0) state[ST_FWD] += 1;
+}
+
+__global__ void __launch_bounds__(256) scale_cast_kernel(const float* __restrict__ src, u16* __restrict__ dst, int64_t n4,
+                                                         float scale) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 s = reinterpret_cast<const float4*>(src)[i];
+    reinterpret_cast<uint2*>(dst)[i] = make_uint2((uint32_t)f2bf(s.x * scale) | ((uint32_t)f2bf(s.y * scale) << 16),
+                                                  (uint32_t)f2bf(s.z * scale) | ((uint32_t)f2bf(s.w * scale) << 16));
+  }
+}
+
+__global__ void __launch_bounds__(256) bf16_to_f32_kernel(const u16* __restrict__ src, float* __restrict__ dst, int64_t n4,
+                                                          float scale) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const uint2 s = reinterpret_cast<const uint2*>(src)[i];
+    reinterpret_cast<float4*>(dst)[i] = make_float4(bf2f((u16)(s.x & 0xffff)) * scale, bf2f((u16)(s.x >> 16)) * scale,
+                                                    bf2f((u16)(s.y & 0xffff)) * scale, bf2f((u16)(s.y >> 16)) * scale);
+  }
+}
+
+static int grid_for(int64_t n4) {
+  int64_t g = (n4 + 255) / 256;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 2048));
+}
+
+void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
+               const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
+               double grad_scale, int64_t rule) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(p.dtype() == at::kFloat && g.dtype() == at::kFloat && m.dtype() == at::kFloat && v.dtype() == at::kFloat,
+              "adam_step: fp32 buffers expected");
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam_step: size mismatch");
+  TORCH_CHECK(n % 4 == 0, "adam_step: flat buffer length must be a multiple of 4");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adam_step: contiguous");
+  u16* sp = nullptr;
+  if (shadow.has_value() && shadow->defined()) {
+    TORCH_CHECK(shadow->dtype() == at::kBFloat16 && shadow->numel() == n, "adam_step: shadow must be bf16 like p");
+    sp = (u16*)shadow->data_ptr();
+  }
+  int64_t* st = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  TORCH_CHECK(st != nullptr || host_step >= 1, "adam_step: step must be >= 1");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  adam_kernel<<<grid_for(n / 4), 256, 0, stream>>>(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                                                   v.data_ptr<float>(), sp, n / 4, st, host_step, (float)lr, (float)b1,
+                                                   (float)b2, (float)eps, (float)grad_scale, (int)rule);
+}
+
+void scale_cast_bf16(const at::Tensor& src, at::Tensor& dst, double scale) {
+  TORCH_CHECK(src.dtype() == at::kFloat && dst.dtype() == at::kBFloat16 && src.numel() == dst.numel() && src.numel() % 4 == 0,
+              "scale_cast_bf16");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  scale_cast_kernel<<<grid_for(src.numel() / 4), 256, 0, stream>>>(src.data_ptr<float>(), (u16*)dst.data_ptr(),
+                                                                   src.numel() / 4, (float)scale);
+}
+
+void bf16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale) {
+  TORCH_CHECK(src.dtype() == at::kBFloat16 && dst.dtype() == at::kFloat && src.numel() == dst.numel() && src.numel() % 4 == 0,
+              "bf16_to_f32");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  bf16_to_f32_kernel<<<grid_for(src.numel() / 4), 256, 0, stream>>>((const u16*)src.data_ptr(), dst.data_ptr<float>(),
+                                                                     src.numel() / 4, (float)scale);
+}
+
+}  // namespace mihvd

@@ -1,0 +1,341 @@
+"""Fused, graph-replayed data-parallel training step for the reference MNIST CNN on MI355X.
+
+This is the flagship path (bench.py ``--impl fused``). One step is nine HIP launches (+ the RCCL
+allreduce when ``size() > 1``), all hand-written CDNA4 kernels from ``csrc/kernels``:
+
+    conv1_fwd   direct conv + bias + ReLU + 2x2 max-pool (+argmax)             [VALU]
+    conv2_fwd   implicit GEMM, pool-window-major M, pool/ReLU in registers    [MFMA bf16]
+    fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs                    [MFMA bf16]
+    head        slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
+    fc1_bwd     dgrad(+pool mask) | wgrad -> fusion buffer | db3 | dW4/db4   [MFMA bf16]
+    --- bucket "fc" (98.4 % of the gradient bytes) is allreduced from here on a side stream ---
+    conv2_bwd   dgrad(+pool/ReLU routing) | wgrad slabs | db2                 [MFMA bf16]
+    conv1_wgrad dW1/db1 + dW2 slab reduction
+    --- bucket "conv" allreduced; the optimizer waits for both buckets ---
+    adam_step   TF1 Adam over the flat fp32 buffer, 1/size averaging fused, bf16 shadow written
+
+Parameters, gradients and Adam slots live in flat fp32 buffers laid out in TF variable order
+(horovod/tensorflow_mnist.py:49-70); every kernel writes its gradient straight into its slot of
+the gradient buffer, which *is* the fusion buffer — there is no pack/unpack copy. The step counter
+and dropout/data indices are device-resident, so ``build_graph(k)`` captures k whole steps
+(including the RCCL calls) into one HIP graph that the host replays with a single launch.
+
+Numerics: bf16 MFMA operands with fp32 accumulation, fp32 master weights and optimizer state,
+fp32 gradients (the MI355X-native equivalent of the reference's ``mixed_float16`` variant,
+tensorflow_mnist_gpu.py:26-28; no loss scaling is needed for bf16).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .. import _native
+from .mnist import TF_PARAM_ORDER, TF_PARAM_SHAPES, MNISTConvNet
+
+ALIGN = 64  # elements (256 B)
+
+
+def _layout():
+    segs, off = {}, 0
+    for name in TF_PARAM_ORDER:
+        n = math.prod(TF_PARAM_SHAPES[name])
+        segs[name] = (off, n)
+        off += (n + ALIGN - 1) // ALIGN * ALIGN
+    return segs, off
+
+
+SEGMENTS, FLAT_NUMEL = _layout()
+FC_START = SEGMENTS["dense/kernel"][0]  # bucket "fc" = [dense/kernel .. dense_1/bias]
+
+
+class FusedMNISTTrainer:
+    def __init__(self, batch_size: int = 100, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 dropout: float = 0.5, seed: int = 0, device=None, compression: str = "none", op=None,
+                 adam_rule: str = "tf", dropout_seed: int | None = None):
+        _native.require_kernels()
+        from .. import basics
+
+        self.ops = torch.ops.mihvd
+        self.device = torch.device(device) if device is not None else (basics.device() if basics.is_initialized()
+                                                                       else torch.device("cuda"))
+        if self.device.type != "cuda":
+            raise RuntimeError("FusedMNISTTrainer runs on an MI355X (cuda/hip device)")
+        if not 1 <= batch_size <= 128:
+            raise ValueError("fused kernels support per-GPU batch sizes 1..128")
+        self.B = batch_size
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.dropout = dropout
+        self.rule = 0 if adam_rule == "tf" else 1
+        self.seed = int(dropout_seed if dropout_seed is not None else (seed * 7919 + 17)) & 0x7FFFFFFF
+        self.world = basics.size() if basics.is_initialized() else 1
+        self.rank = basics.rank() if basics.is_initialized() else 0
+        self.op = op
+        self.compression = compression
+        self.global_step = 0
+        dev = self.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.params = torch.zeros(FLAT_NUMEL, **f32)
+        self.grads = torch.zeros(FLAT_NUMEL, **f32)
+        self.m = torch.zeros(FLAT_NUMEL, **f32)
+        self.v = torch.zeros(FLAT_NUMEL, **f32)
+        self.shadow = torch.zeros(FLAT_NUMEL, device=dev, dtype=torch.bfloat16)
+        self.state = torch.zeros(4, device=dev, dtype=torch.int64)
+        ref = MNISTConvNet(impl="torch", seed=seed)
+        self.load_model_weights(ref)
+        B = self.B
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        u8 = dict(device=dev, dtype=torch.uint8)
+        self.a1 = torch.empty(B, 14, 14, 32, **bf)
+        self.idx1 = torch.empty(B, 14, 14, 32, **u8)
+        self.a2 = torch.empty(B, 3136, **bf)
+        self.idx2 = torch.empty(B, 3136, **u8)
+        self.zpart = torch.empty(14, B, 1024, **f32)
+        self.h = torch.empty(B, 1024, **bf)
+        self.dz = torch.empty(B, 1024, **bf)
+        self.dlog = torch.empty(B, 10, **f32)
+        self.stats = torch.zeros(B, 2, **f32)
+        self.g2 = torch.empty(B, 3136, **bf)
+        self.g1 = torch.empty(B, 14, 14, 32, **bf)
+        self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
+        self.x_buf = torch.zeros(B, 784, **f32)
+        self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
+        self.X = self.Y = self.rows = None
+        self.graph = None
+        self.steps_per_replay = 1
+        self._side = torch.cuda.Stream(device=dev) if self.world > 1 else None
+        if compression == "bf16" and self.world > 1:
+            self.wire = torch.empty(FLAT_NUMEL, **bf)
+        else:
+            self.wire = None
+
+    # ----------------------------------------------------------------------------- views
+    def pview(self, name, buf=None):
+        off, n = SEGMENTS[name]
+        return (self.params if buf is None else buf)[off:off + n].view(TF_PARAM_SHAPES[name])
+
+    def gview(self, name):
+        return self.pview(name, self.grads)
+
+    def load_model_weights(self, model: MNISTConvNet):
+        with torch.no_grad():
+            for name, p in model.ordered_parameters():
+                self.pview(name).copy_(p.detach().to(self.device, torch.float32))
+        self._refresh_shadow()
+
+    def _refresh_shadow(self):
+        self.ops.scale_cast_bf16(self.params, self.shadow, 1.0)
+
+    def to_model(self, model: MNISTConvNet | None = None) -> MNISTConvNet:
+        model = model or MNISTConvNet(impl="torch").to(self.device)
+        with torch.no_grad():
+            for name, p in model.ordered_parameters():
+                p.copy_(self.pview(name))
+        return model
+
+    # ----------------------------------------------------------------------------- data
+    def set_device_dataset(self, X: torch.Tensor, Y: torch.Tensor, shuffle: bool = True, seed: int = 0):
+        """Keep a dataset resident on the device; batches are gathered by index inside conv1/head."""
+        n = (X.shape[0] // self.B) * self.B
+        if n < self.B:
+            raise ValueError("dataset smaller than one batch")
+        self.X = X[:n].to(self.device, torch.float32).contiguous()
+        self.Y = Y[:n].to(self.device, torch.int64).contiguous()
+        self._shuffle = shuffle
+        self._rng = np.random.default_rng(seed + 1000 * self.rank)
+        self.rows = torch.empty(n, device=self.device, dtype=torch.int32)
+        self._reshuffle()
+        self._epoch_steps = n // self.B
+
+    def _reshuffle(self):
+        n = self.X.shape[0]
+        perm = self._rng.permutation(n) if self._shuffle else np.arange(n)
+        self.rows.copy_(torch.from_numpy(perm.astype(np.int32)))
+
+    # ----------------------------------------------------------------------------- step
+    def _launch_step(self, x, rows, labels):
+        o = self.ops
+        B = self.B
+        st = self.state
+        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
+                    self.a1, self.idx1)
+        o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
+                    self.a2, self.idx2)
+        o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
+        o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
+                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        o.fc1_bwd(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.h, self.dlog, self.g2,
+                  self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
+                  self.gview("dense_1/bias"))
+        main = torch.cuda.current_stream(self.device)
+        fc_bucket = self.grads[FC_START:]
+        conv_bucket = self.grads[:FC_START]
+        if self.world > 1:
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                self._allreduce(fc_bucket, FC_START, FLAT_NUMEL)
+        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1, self.slab,
+                    self.gview("conv_layer2/conv2d/bias"), self.gview("conv_layer1/conv2d/kernel"),
+                    self.gview("conv_layer1/conv2d/bias"))
+        o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),
+                      self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/kernel"))
+        if self.world > 1:
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                self._allreduce(conv_bucket, 0, FC_START)
+            main.wait_stream(self._side)
+        b1, b2 = self.betas
+        o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
+                    1.0 / self.world, self.rule)
+
+    def _allreduce(self, bucket, lo, hi):
+        import torch.distributed as dist
+
+        from ..basics import ReduceOp
+
+        if self.op is not None and ReduceOp(self.op) == ReduceOp.Adasum:
+            from ..parallel.collectives import adasum_dispatch_
+
+            segs = [(o - lo, o - lo + n) for o, n in SEGMENTS.values() if lo <= o < hi]
+            adasum_dispatch_(bucket, segs)
+            bucket.mul_(self.world)  # adam divides by size; Adasum output is already the combined gradient
+            return
+        if self.wire is not None:
+            w = self.wire[lo:hi]
+            self.ops.scale_cast_bf16(bucket, w, 1.0)
+            dist.all_reduce(w)
+            self.ops.bf16_to_f32(w, bucket, 1.0)
+        else:
+            dist.all_reduce(bucket)
+
+    def train_step(self, x: torch.Tensor, y: torch.Tensor):
+        """One eager step on a host-fed batch (x: [B,784] in [0,1], y: [B] labels)."""
+        self.x_buf.copy_(x.reshape(self.B, 784), non_blocking=True)
+        self.y_buf.copy_(y.reshape(self.B), non_blocking=True)
+        # Host-fed batches index rows 0..B-1 of x_buf (rows=None); the step counter still advances.
+        self._launch_step(self.x_buf, None, self.y_buf)
+        self.global_step += 1
+        return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
+
+    def device_step(self):
+        """One eager step on the resident dataset."""
+        if self.X is None:
+            raise RuntimeError("call set_device_dataset() first")
+        self._maybe_reshuffle(1)
+        self._launch_step(self.X, self.rows, self.Y)
+        self.global_step += 1
+        return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
+
+    def _maybe_reshuffle(self, k):
+        if self.X is None:
+            return
+        e0 = self.global_step // self._epoch_steps
+        e1 = (self.global_step + k - 1) // self._epoch_steps
+        if e1 != e0 or (self.global_step % self._epoch_steps == 0 and self.global_step > 0):
+            torch.cuda.current_stream(self.device).synchronize()
+            self._reshuffle()
+
+    # ----------------------------------------------------------------------------- graphs
+    def build_graph(self, steps_per_replay: int = 10, warmup: int = 2):
+        """Capture ``steps_per_replay`` whole training steps (resident data) into one HIP graph.
+
+        Warm-up steps run eagerly first (they also initialise RCCL communicators). If capture is not
+        possible (e.g. Adasum's data-dependent exchanges), training stays eager."""
+        if self.X is None:
+            raise RuntimeError("call set_device_dataset() before build_graph()")
+        for _ in range(warmup):
+            self.device_step()
+        torch.cuda.synchronize(self.device)
+        self.steps_per_replay = steps_per_replay
+        if self.op is not None and int(self.op) == 2:  # Adasum: eager
+            self.graph = None
+            return False
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(steps_per_replay):
+                        self._launch_step(self.X, self.rows, self.Y)
+        except Exception as e:  # pragma: no cover - depends on the RCCL build
+            import warnings
+
+            warnings.warn(f"HIP graph capture failed ({e!r}); falling back to eager steps")
+            self.graph = None
+            torch.cuda.synchronize(self.device)
+            return False
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        # Capture does not execute: the device step counter is untouched, so replays continue
+        # from the current global_step.
+        self.graph = g
+        return True
+
+    def run_graph(self):
+        """Advance ``steps_per_replay`` steps (graph replay, or eager steps if capture failed)."""
+        if self.graph is None:
+            for _ in range(self.steps_per_replay):
+                self.device_step()
+            return
+        self._maybe_reshuffle(self.steps_per_replay)
+        self.graph.replay()
+        self.global_step += self.steps_per_replay
+
+    def last_loss(self) -> float:
+        return float(self.stats[:, 0].mean())
+
+    def last_accuracy(self) -> float:
+        return float(self.stats[:, 1].mean())
+
+    # ----------------------------------------------------------------------------- state
+    def sync(self):
+        torch.cuda.synchronize(self.device)
+
+    def variables(self) -> dict[str, torch.Tensor]:
+        """TF1 global variables (names of tensorflow_mnist.py's graph) for the checkpoint layout."""
+        self.sync()
+        out = {}
+        for name in TF_PARAM_ORDER:
+            out[name] = self.pview(name).detach().clone()
+            out[name + "/Adam"] = self.pview(name, self.m).detach().clone()
+            out[name + "/Adam_1"] = self.pview(name, self.v).detach().clone()
+        t = int(self.state[1].item())
+        b1, b2 = self.betas
+        out["beta1_power"] = torch.tensor(b1 ** (t + 1), dtype=torch.float32)
+        out["beta2_power"] = torch.tensor(b2 ** (t + 1), dtype=torch.float32)
+        out["global_step"] = torch.tensor(self.global_step, dtype=torch.int64)
+        return out
+
+    def load_variables(self, variables: dict[str, torch.Tensor]):
+        with torch.no_grad():
+            for name in TF_PARAM_ORDER:
+                self.pview(name).copy_(variables[name].to(self.device))
+                if name + "/Adam" in variables:
+                    self.pview(name, self.m).copy_(variables[name + "/Adam"].to(self.device))
+                    self.pview(name, self.v).copy_(variables[name + "/Adam_1"].to(self.device))
+        self.global_step = int(variables.get("global_step", torch.tensor(0)))
+        t = self.global_step
+        if "beta1_power" in variables:
+            bp = float(variables["beta1_power"])
+            if 0 < bp < 1:
+                t = round(math.log(bp) / math.log(self.betas[0])) - 1
+        self.state.copy_(torch.tensor([self.global_step, t, 0, 0], dtype=torch.int64))
+        self._refresh_shadow()
+
+    def broadcast(self, root_rank: int = 0):
+        """Broadcast weights, Adam slots and counters from ``root_rank`` (BroadcastGlobalVariablesHook)."""
+        from .. import basics
+
+        if not basics.is_initialized() or basics.size() == 1:
+            return
+        import torch.distributed as dist
+
+        for buf in (self.params, self.m, self.v, self.state):
+            dist.broadcast(buf, src=root_rank)
+        from ..parallel.collectives import broadcast_object
+
+        self.global_step = int(broadcast_object(self.global_step, root_rank))
+        self._refresh_shadow()
