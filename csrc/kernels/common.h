@@ -74,6 +74,37 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Stage a [rows][cpr x 16 B] tile from global (row stride gstride elements) into LDS (row stride
+// lstride elements, 16-byte aligned). Rows >= valid_rows are zero-filled. Every load is issued
+// before any LDS store and none is predicated (addresses are clamped, the value is selected after),
+// so the whole tile costs one memory latency instead of one per iteration.
+template <int NT, int MAXIT>
+__device__ __forceinline__ void stage_tile(u16* lds, int lstride, const u16* __restrict__ g, int64_t gstride, int rows,
+                                           int valid_rows, int cpr, int t) {
+  const int total = rows * cpr;
+  uint4 buf[MAXIT];
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int i = min(t + it * NT, total - 1);
+    const int r = i / cpr, c = i - r * cpr;
+    const int rr = min(r, valid_rows - 1);
+    const uint4 v = *reinterpret_cast<const uint4*>(g + (int64_t)rr * gstride + c * 8);
+    buf[it] = (r < valid_rows) ? v : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int i = t + it * NT;
+    if (i < total) {
+      const int r = i / cpr, c = i - r * cpr;
+      *reinterpret_cast<uint4*>(lds + r * lstride + c * 8) = buf[it];
+    }
+  }
+}
+
+__device__ __forceinline__ uint2 pack4bf(float a, float b, float c, float d) {
+  return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
+}
+
 // Step-state words kept on the device so a whole training step replays from a HIP graph:
 //   state[0] = forward step index (read by data/dropout kernels, bumped by the optimizer)
 //   state[1] = optimizer step t   (bumped by the head kernel, read by the optimizer)

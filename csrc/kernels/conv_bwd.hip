@@ -1,17 +1,17 @@
 // Backward convolutions of the MNIST CNN.
 //
-// conv2_bwd (one launch, three block roles):
-//   dgrad  : dA1 = full-correlation of dY2 with W2 (implicit GEMM, K = 25 taps x 64 channels), with
-//            the max-pool routing of conv1's output and its ReLU fused into the epilogue -> g1.
-//            dY2 is never materialised in HBM: each block expands the pooled gradient g2 through the
-//            argmax indices idx2 straight into an LDS image with a zero halo.
-//   wgrad  : dW2 per kernel row kh and group of images as an MFMA GEMM over pixels; both operands are
-//            read with ds_read_b64_tr_b16 from their natural NHWC images. Each block writes an fp32
-//            partial slab (deterministic, no atomics); conv1_wgrad's launch reduces the slabs.
-//   misc   : db2 and zeroing of the conv1 gradient (accumulated with atomics next).
-// conv1_wgrad (one launch): dW1/db1 from the sparse routed gradient (1 of 4 conv1 outputs per
-//   window is non-zero, so it is computed directly on VALU from the pooled gradient) + the dW2 slab
-//   reduction into the fusion buffer.
+// conv2_bwd (one launch, 512-thread blocks, two roles):
+//   * The routed conv2 output gradient dY2 is built on the fly in LDS: the four fc1-dgrad split-K
+//     slabs are summed, masked with conv2's pooled ReLU (a2 > 0) and scattered through the argmax
+//     indices idx2 (4 co per lane -> four 8-byte LDS writes). dY2 never exists in HBM.
+//   * dgrad (one block per image): dA1 = full correlation of dY2 with W2 as an implicit GEMM
+//     (K = 25 taps x 64 channels), W2 resident in LDS (115 KB), output features on the MFMA row
+//     axis; conv1's pooled ReLU mask is applied in the epilogue -> g1 (bf16). db2 is reduced here.
+//   * wgrad (kernel row kh x group of 4 images): dW2 as an MFMA GEMM over pixels with both operands
+//     read by ds_read_b64_tr_b16 from natural NHWC images; two 4-wave groups take two images each
+//     and are summed in LDS; one fp32 partial slab per block (deterministic, no atomics).
+// conv1_wgrad: dW1/db1 from the sparse routed gradient (one of four conv1 outputs per pooling
+//   window is non-zero, so VALU on the pooled gradient), plus the dW2 slab reduction.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -19,171 +19,268 @@
 
 namespace mihvd {
 
-constexpr int CB_IPB = 4;                  // images per wgrad block
-constexpr int CB_DSTR = 64;                // dgrad dY2 image: pixel stride (elements)
-constexpr int CB_DROWS = 11;               // dY2 rows held by a dgrad block
-constexpr int CB_DG_LDS = CB_DROWS * 18 * CB_DSTR * 2;          // 25,344 B
-constexpr int CB_APIX = 18 * 18 + 6;                             // padded a1 image + zero pixels
-constexpr int CB_WSTR = 72;                                      // wgrad dY2 image stride
-constexpr int CB_WG_LDS = (CB_APIX * 32 + 224 * CB_WSTR) * 2;    // 53,568 B
-constexpr int CB_LDS = CB_WG_LDS > CB_DG_LDS ? CB_WG_LDS : CB_DG_LDS;
+constexpr int CB_IPB = 4;               // images per wgrad block (2 per wave group)
+constexpr int CB_KQ = 4;                // fc1 dgrad split-K slabs
+constexpr int CB_WSTR = 72;             // W2 image row stride (dgrad) and dY2 image row stride (wgrad)
+// dgrad LDS: W2 [800][72] | D [18*18][64]
+constexpr int CB_DG_W = 800 * CB_WSTR;
+constexpr int CB_DG_D = 324 * 64;
+constexpr int CB_DG_LDS = (CB_DG_W + CB_DG_D) * 2;                 // 156,672 B
+// wgrad LDS per wave group: A [325][32] | Dm [197][72]
+constexpr int CB_WG_A = 325 * 32;
+constexpr int CB_WG_D = 197 * CB_WSTR;
+constexpr int CB_WG_GRP = CB_WG_A + CB_WG_D;                       // elements
+constexpr int CB_WG_LDS = 2 * CB_WG_GRP * 2;                       // 98,336 B
+constexpr int CB_LDS = CB_DG_LDS > CB_WG_LDS ? CB_DG_LDS : CB_WG_LDS;
 
-__global__ void __launch_bounds__(256) conv2_bwd_kernel(
-    const u16* __restrict__ g2, const uint8_t* __restrict__ idx2, const u16* __restrict__ a1,
-    const u16* __restrict__ w2bf, u16* __restrict__ g1, float* __restrict__ slab, float* __restrict__ gb2,
-    float* __restrict__ gW1, float* __restrict__ gb1, int B, int n_dgrad, int n_wgrad) {
+struct DyItem {
+  float4 s[CB_KQ];
+  uint2 a2;
+  uint32_t idx;
+};
+
+// Loads for one dY2 build item: 4 consecutive channels of one pooling window of image b.
+__device__ __forceinline__ DyItem load_dy_item(const float* __restrict__ dap, const u16* __restrict__ a2,
+                                               const uint8_t* __restrict__ idx2, int B, int b, int e) {
+  DyItem it;
+#pragma unroll
+  for (int k = 0; k < CB_KQ; ++k)
+    it.s[k] = *reinterpret_cast<const float4*>(dap + ((int64_t)k * B + b) * 3136 + e);
+  it.a2 = *reinterpret_cast<const uint2*>(a2 + (int64_t)b * 3136 + e);
+  it.idx = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)b * 3136 + e);
+  return it;
+}
+
+// Reduce + mask an item: g[c] is the bf16 gradient of channel c, d[c] its argmax slot.
+__device__ __forceinline__ void finish_dy_item(const DyItem& it, u16 g[4], int d[4], float gf[4]) {
+  const float sx = it.s[0].x + it.s[1].x + it.s[2].x + it.s[3].x;
+  const float sy = it.s[0].y + it.s[1].y + it.s[2].y + it.s[3].y;
+  const float sz = it.s[0].z + it.s[1].z + it.s[2].z + it.s[3].z;
+  const float sw = it.s[0].w + it.s[1].w + it.s[2].w + it.s[3].w;
+  const float s[4] = {sx, sy, sz, sw};
+  const u16 av[4] = {(u16)(it.a2.x & 0xffff), (u16)(it.a2.x >> 16), (u16)(it.a2.y & 0xffff), (u16)(it.a2.y >> 16)};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    g[c] = bf2f(av[c]) > 0.f ? f2bf(s[c]) : (u16)0;
+    gf[c] = bf2f(g[c]);
+    d[c] = (it.idx >> (8 * c)) & 3;
+  }
+}
+
+// Write the 4 pixels of window `win` (value at the argmax slot, zero elsewhere) for 4 channels.
+__device__ __forceinline__ void scatter_window(u16* img, int pix_stride, int win, int co4, const u16 g[4], const int d[4],
+                                               bool padded18) {
+  const int py = win / 7, px = win - py * 7;
+#pragma unroll
+  for (int dd = 0; dd < 4; ++dd) {
+    const int y = 2 * py + (dd >> 1), x = 2 * px + (dd & 1);
+    const int pix = padded18 ? (y + 2) * 18 + (x + 2) : y * 14 + x;
+    const uint32_t lo = (uint32_t)(d[0] == dd ? g[0] : 0) | ((uint32_t)(d[1] == dd ? g[1] : 0) << 16);
+    const uint32_t hi = (uint32_t)(d[2] == dd ? g[2] : 0) | ((uint32_t)(d[3] == dd ? g[3] : 0) << 16);
+    *reinterpret_cast<uint2*>(img + pix * pix_stride + co4) = make_uint2(lo, hi);
+  }
+}
+
+__global__ void __launch_bounds__(512) conv2_bwd_kernel(
+    const float* __restrict__ dap, const u16* __restrict__ a2, const uint8_t* __restrict__ idx2,
+    const u16* __restrict__ a1, const u16* __restrict__ w2bf, u16* __restrict__ g1, float* __restrict__ slab,
+    float* __restrict__ gb2, int B, int n_dgrad) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
-  int bid = blockIdx.x;
-  if (bid < n_dgrad) {
-    // ------------------------------------------------------------------ dgrad (b, half r)
-    const int b = bid >> 1, r = bid & 1;
-    u16* D = smem;  // [11][18][64]: local row = y' - (7r-2), local col = x' + 2
-    for (int i = t; i < CB_DROWS * 18 * CB_DSTR / 8; i += 256) reinterpret_cast<uint4*>(D)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    const int ybase = 7 * r - 2;
-    for (int i = t; i < 49 * 64; i += 256) {
-      const int win = i >> 6, co = i & 63;
-      const int64_t gi = (int64_t)b * 3136 + i;
-      const u16 g = g2[gi];
-      if (g == 0) continue;
-      const int d = idx2[gi];
-      const int y = 2 * (win / 7) + (d >> 1), x = 2 * (win % 7) + (d & 1);
-      const int yl = y - ybase;
-      if (yl < 0 || yl >= CB_DROWS) continue;
-      D[(yl * 18 + x + 2) * CB_DSTR + co] = g;
+  if ((int)blockIdx.x < n_dgrad) {
+    // ===================================================================== dgrad: image b
+    const int b = blockIdx.x;
+    u16* Ws = smem;              // [800][72]  row = kk*32 + ci, cols = co
+    u16* D = smem + CB_DG_W;     // [18*18][64] padded dY2 image
+    // Issue every load of the block first: W2 (13 x 16 B per thread) and 2 dY2 items.
+    DyItem items[2];
+    int ie[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = min(t + 512 * k, 783);
+      ie[k] = t + 512 * k;
+      items[k] = load_dy_item(dap, a2, idx2, B, b, (i >> 4) * 64 + (i & 15) * 4);
+    }
+    stage_tile<512, 13>(Ws, CB_WSTR, w2bf, 64, 800, 800, 8, t);
+    // zero halo pixels of D (interior pixels are fully written by the scatter)
+    for (int i = t; i < 324 * 8; i += 512) {
+      const int pix = i >> 3, c = i & 7;
+      const int y = pix / 18, x = pix - y * 18;
+      if (y < 2 || y >= 16 || x < 2 || x >= 16) *reinterpret_cast<uint4*>(D + pix * 64 + c * 8) = make_uint4(0, 0, 0, 0);
+    }
+    float db[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (ie[k] < 784) {
+        u16 g[4];
+        int d[4];
+        float gf[4];
+        finish_dy_item(items[k], g, d, gf);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) db[c] += gf[c];
+        scatter_window(D, 64, ie[k] >> 4, (ie[k] & 15) * 4, g, d, true);
+      }
     }
     __syncthreads();
+    // GEMM: rows = ci (2 tiles), cols = pixels (13 tiles: wave w, w+8), K = (kh, kw, co) = 1600.
     f32x4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int ntl = (wave + 8 < 13) ? 2 : 1;
     int pbase[2];
-    const int ntl = (wave + 4 < 7) ? 2 : 1;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      int m = (wave + 4 * i) * 16 + lr;
-      if (m >= 98) m = 0;
-      const int yl = m / 14, x = m % 14;
-      pbase[i] = ((yl + 4) * 18 + (x + 4)) * CB_DSTR + 8 * lg;
+      int m = (wave + 8 * i) * 16 + lr;
+      if (m >= 196) m = 0;
+      const int y = m / 14, x = m - (m / 14) * 14;
+      pbase[i] = ((y + 4) * 18 + (x + 4)) * 64 + 8 * lg;
     }
     for (int kk = 0; kk < 25; ++kk) {
       const int kh = kk / 5, kw = kk - kh * 5;
-      const int aoff = -(kh * 18 + kw) * CB_DSTR;
+      const int aoff = -(kh * 18 + kw) * 64;
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
-        // B[k = co][n = ci] = W2[kh][kw][ci][co]
-        const u16* wp = w2bf + ((int64_t)(kk * 32 + lr) * 64 + ch * 32 + 8 * lg);
-        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(wp);
-        const bf16x8 b1v = *reinterpret_cast<const bf16x8*>(wp + 16 * 64);
+        const u16* wr = Ws + (kk * 32 + lr) * CB_WSTR + ch * 32 + 8 * lg;
+        const bf16x8 w0 = frag_ld128(wr);
+        const bf16x8 w1 = frag_ld128(wr + 16 * CB_WSTR);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           if (i < ntl) {
-            const bf16x8 a = frag_ld128(D + pbase[i] + aoff + ch * 32);
-            acc[i][0] = mfma16(a, b0, acc[i][0]);
-            acc[i][1] = mfma16(a, b1v, acc[i][1]);
+            const bf16x8 bx = frag_ld128(D + pbase[i] + aoff + ch * 32);
+            acc[i][0] = mfma16(w0, bx, acc[i][0]);
+            acc[i][1] = mfma16(w1, bx, acc[i][1]);
           }
         }
       }
     }
+    // Epilogue: lane holds ci = 16*nt + 4*lg .. +3 of pixel (tile*16 + lr).
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i >= ntl) continue;
+      const int m = (wave + 8 * i) * 16 + lr;
+      if (m >= 196) continue;
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = (wave + 4 * i) * 16 + 4 * lg + e;
-          if (m >= 98) continue;
-          const int y = 7 * r + m / 14, x = m % 14, ci = nt * 16 + lr;
-          const int64_t o = (((int64_t)b * 14 + y) * 14 + x) * 32 + ci;
-          g1[o] = (bf2f(a1[o]) > 0.f) ? f2bf(acc[i][nt][e]) : (u16)0;
-        }
+      for (int nt = 0; nt < 2; ++nt) {
+        const int64_t o = ((int64_t)b * 196 + m) * 32 + nt * 16 + 4 * lg;
+        const uint2 av = *reinterpret_cast<const uint2*>(a1 + o);
+        const float m0 = bf2f((u16)(av.x & 0xffff)) > 0.f ? acc[i][nt][0] : 0.f;
+        const float m1 = bf2f((u16)(av.x >> 16)) > 0.f ? acc[i][nt][1] : 0.f;
+        const float m2 = bf2f((u16)(av.y & 0xffff)) > 0.f ? acc[i][nt][2] : 0.f;
+        const float m3 = bf2f((u16)(av.y >> 16)) > 0.f ? acc[i][nt][3] : 0.f;
+        *reinterpret_cast<uint2*>(g1 + o) = pack4bf(m0, m1, m2, m3);
+      }
+    }
+    // db2: per-thread partials (a thread's items share one channel group) -> LDS -> atomics
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(D);  // [512][4]
+    *reinterpret_cast<float4*>(red + t * 4) = make_float4(db[0], db[1], db[2], db[3]);
+    __syncthreads();
+    if (t < 64) {
+      const int co4 = t >> 2, c = t & 3;  // channel co4*4 + c, summed over the 32 threads with (tid & 15) == co4
+      float s = 0.f;
+      for (int r = co4; r < 512; r += 16) s += red[r * 4 + c];
+      atomicAdd(gb2 + co4 * 4 + c, s);
     }
     return;
   }
-  bid -= n_dgrad;
-  if (bid < n_wgrad) {
-    // ------------------------------------------------------------------ wgrad (kh, group)
-    const int kh = bid % 5, grp = bid / 5;
-    u16* A = smem;                   // [18*18 + 6 zero pixels][32]
-    u16* Dm = smem + CB_APIX * 32;   // [224][72]
-    f32x4 acc[10];
+  // ======================================================================= wgrad
+  const int bid = blockIdx.x - n_dgrad;
+  const int kh = bid % 5, grp = bid / 5;
+  const int h = wave >> 2, lw = wave & 3, th = t & 255;
+  u16* A = smem + h * CB_WG_GRP;   // [325][32] padded a1 image (+ zero pixel 324)
+  u16* Dm = A + CB_WG_A;           // [197][72] dY2 rows = pixels (+ zero row 196)
+  f32x4 acc[10];
 #pragma unroll
-    for (int i = 0; i < 10; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int b_end = min(B, (grp + 1) * CB_IPB);
-    for (int b = grp * CB_IPB; b < b_end; ++b) {
-      __syncthreads();  // previous image fully consumed
-      const uint4* src = reinterpret_cast<const uint4*>(a1 + (int64_t)b * 6272);
-      for (int i = t; i < CB_APIX * 4; i += 256) {
-        const int pix = i >> 2, c = i & 3;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (pix < 324) {
-          const int y = pix / 18 - 2, x = pix % 18 - 2;
-          if (y >= 0 && y < 14 && x >= 0 && x < 14) v = src[(y * 14 + x) * 4 + c];
-        }
-        reinterpret_cast<uint4*>(A)[i] = v;
+  for (int i = 0; i < 10; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ii = 0; ii < 2; ++ii) {
+    const int b = grp * CB_IPB + h * 2 + ii;
+    const bool active = b < B;
+    const int bb = active ? b : 0;
+    // loads first: a1 image chunks (interior pixels) and the dY2 items of this image
+    uint4 av[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int i = min(th + 256 * k, 1299);
+      const int pix = i >> 2, c = i & 3;
+      const int y = pix / 18 - 2, x = pix % 18 - 2;
+      const bool in = pix < 324 && y >= 0 && y < 14 && x >= 0 && x < 14;
+      const int yc = in ? y : 0, xc = in ? x : 0;
+      const uint4 v = *reinterpret_cast<const uint4*>(a1 + ((int64_t)bb * 196 + yc * 14 + xc) * 32 + c * 8);
+      av[k] = in ? v : make_uint4(0, 0, 0, 0);
+    }
+    DyItem items[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = min(th + 256 * k, 783);
+      items[k] = load_dy_item(dap, a2, idx2, B, bb, (i >> 4) * 64 + (i & 15) * 4);
+    }
+    __syncthreads();  // the previous image's operands are no longer read
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int i = th + 256 * k;
+      if (i < 1300) reinterpret_cast<uint4*>(A)[i] = av[k];
+    }
+    if (th < 9) reinterpret_cast<uint4*>(Dm + 196 * CB_WSTR)[th] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = th + 256 * k;
+      if (i < 784) {
+        u16 g[4];
+        int d[4];
+        float gf[4];
+        finish_dy_item(items[k], g, d, gf);
+        scatter_window(Dm, CB_WSTR, i >> 4, (i & 15) * 4, g, d, false);
       }
-      for (int i = t; i < 224 * CB_WSTR / 8; i += 256) reinterpret_cast<uint4*>(Dm)[i] = make_uint4(0, 0, 0, 0);
-      __syncthreads();
-      for (int i = t; i < 49 * 64; i += 256) {
-        const int win = i >> 6, co = i & 63;
-        const int64_t gi = (int64_t)b * 3136 + i;
-        const u16 g = g2[gi];
-        if (g == 0) continue;
-        const int d = idx2[gi];
-        const int pix = (2 * (win / 7) + (d >> 1)) * 14 + 2 * (win % 7) + (d & 1);
-        Dm[pix * CB_WSTR + co] = g;
-      }
-      __syncthreads();
+    }
+    __syncthreads();
+    if (active) {
       for (int k0 = 0; k0 < 224; k0 += 32) {
+        // A' = dY2^T: rows = co (16 per wave), k = pixels
+        const int r0 = min(k0 + 8 * lg + q, 196), r1 = min(k0 + 8 * lg + q + 4, 196);
+        const bf16x8 af = frag_tr(Dm + r0 * CB_WSTR + lw * 16 + 4 * p, Dm + r1 * CB_WSTR + lw * 16 + 4 * p);
         int poff[2];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int pix = k0 + 8 * lg + q + 4 * h;
-          if (pix < 196) {
-            const int y = pix / 14, x = pix % 14;
-            poff[h] = ((y + kh) * 18 + x) * 32;
-          } else {
-            poff[h] = 324 * 32;  // zero pixels (6 of them cover +kw*32 + ci)
-          }
+        for (int hh = 0; hh < 2; ++hh) {
+          const int pix = k0 + 8 * lg + q + 4 * hh;
+          const int y = pix / 14, x = pix - (pix / 14) * 14;
+          poff[hh] = pix < 196 ? ((y + kh) * 18 + x) * 32 : -1;
         }
-        const u16* br = Dm + (k0 + 8 * lg + q) * CB_WSTR + wave * 16 + 4 * p;
-        const bf16x8 bfr = frag_tr(br, br + 4 * CB_WSTR);
 #pragma unroll
         for (int mt = 0; mt < 10; ++mt) {
           const int kw = mt >> 1, ci0 = (mt & 1) * 16;
-          const int add = (poff[0] == 324 * 32 ? 0 : kw * 32) + ci0 + 4 * p;
-          const int add1 = (poff[1] == 324 * 32 ? 0 : kw * 32) + ci0 + 4 * p;
-          const bf16x8 a = frag_tr(A + poff[0] + add, A + poff[1] + add1);
-          acc[mt] = mfma16(a, bfr, acc[mt]);
+          const int o0 = poff[0] >= 0 ? poff[0] + kw * 32 : 324 * 32;
+          const int o1 = poff[1] >= 0 ? poff[1] + kw * 32 : 324 * 32;
+          const bf16x8 bx = frag_tr(A + o0 + ci0 + 4 * p, A + o1 + ci0 + 4 * p);
+          acc[mt] = mfma16(af, bx, acc[mt]);
         }
       }
     }
+  }
+  // Sum the two wave groups, then one float4 per lane per tile into the slab.
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // group 1 -> [40][256] floats
+  if (h == 1) {
+#pragma unroll
+    for (int mt = 0; mt < 10; ++mt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(mt * 4 + e) * 256 + th] = acc[mt][e];
+  }
+  __syncthreads();
+  if (h == 0) {
     float* out = slab + (int64_t)grp * 51200;
 #pragma unroll
     for (int mt = 0; mt < 10; ++mt) {
-      const int kw = mt >> 1, ci0 = (mt & 1) * 16;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ci = ci0 + 4 * lg + e, co = wave * 16 + lr;
-        out[((kh * 5 + kw) * 32 + ci) * 64 + co] = acc[mt][e];
-      }
+      const int kw = mt >> 1, ci = (mt & 1) * 16 + lr;
+      const int co = lw * 16 + 4 * lg;
+      float4 v;
+      v.x = acc[mt][0] + red[(mt * 4 + 0) * 256 + th];
+      v.y = acc[mt][1] + red[(mt * 4 + 1) * 256 + th];
+      v.z = acc[mt][2] + red[(mt * 4 + 2) * 256 + th];
+      v.w = acc[mt][3] + red[(mt * 4 + 3) * 256 + th];
+      *reinterpret_cast<float4*>(out + ((kh * 5 + kw) * 32 + ci) * 64 + co) = v;
     }
-    return;
   }
-  // ------------------------------------------------------------------ db2 + zero conv1 grads
-  float* red = reinterpret_cast<float*>(smem);
-  {
-    const int co = t & 63, part = t >> 6;
-    float s = 0.f;
-    for (int row = part; row < B * 49; row += 4) s += bf2f(g2[(int64_t)row * 64 + co]);
-    red[part * 64 + co] = s;
-  }
-  for (int i = t; i < 800; i += 256) gW1[i] = 0.f;
-  if (t < 32) gb1[t] = 0.f;
-  __syncthreads();
-  if (t < 64) gb2[t] = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -200,7 +297,15 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
     const int i = ((int)blockIdx.x - B) * 256 + t;  // float4 index, 12800 total
     if (i < 51200 / 4) {
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int g = 0; g < nslab; ++g) {
+      int g = 0;
+      for (; g + 5 <= nslab; g += 5) {
+        float4 v[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) v[u] = reinterpret_cast<const float4*>(slab + (int64_t)(g + u) * 51200)[i];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+      }
+      for (; g < nslab; ++g) {
         const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)g * 51200)[i];
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       }
@@ -214,29 +319,48 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
     const int64_t step = state ? state[ST_FWD] : 0;
     row = rows[(int)((step * (int64_t)B + b) % n_pool)];
   }
+  const int co = t & 31, grp = t >> 5;
+  // loads first: this thread's 25 pooled gradients + argmax slots, and the image
+  u16 gv[25];
+  uint8_t dv[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) {
+    const int pos = min(grp + 8 * i, 195);
+    const int64_t o = (int64_t)b * 6272 + pos * 32 + co;
+    gv[i] = g1[o];
+    dv[i] = idx1[o];
+  }
   const float* xi = x + (int64_t)row * 784;
-  for (int i = t; i < 32 * 32; i += 256) {
+  float xv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = t + 256 * k;
     const int r = i >> 5, c = i & 31;
     const int gy = r - 2, gx = c - 2;
-    img[r][c] = (gy >= 0 && gy < 28 && gx >= 0 && gx < 28) ? xi[gy * 28 + gx] : 0.f;
+    const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
+    const float v = xi[in ? gy * 28 + gx : 0];
+    xv[k] = in ? v : 0.f;
   }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) img[(t + 256 * k) >> 5][(t + 256 * k) & 31] = xv[k];
   __syncthreads();
-  const int co = t & 31, grp = t >> 5;
   float acc[25], accb = 0.f;
 #pragma unroll
   for (int k = 0; k < 25; ++k) acc[k] = 0.f;
-  for (int pos = grp; pos < 196; pos += 8) {
-    const int64_t o = (int64_t)b * 6272 + pos * 32 + co;
-    const float g = bf2f(g1[o]);
-    if (g == 0.f) continue;
-    const int d = idx1[o];
-    const int py = pos / 14, px = pos - py * 14;
-    const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
-    accb += g;
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh)
+  for (int i = 0; i < 25; ++i) {
+    const int pos = grp + 8 * i;
+    const float g = bf2f(gv[i]);
+    if (pos < 196 && g != 0.f) {
+      const int d = dv[i];
+      const int py = pos / 14, px = pos - py * 14;
+      const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
+      accb += g;
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(g, img[y + kh][xx + kw], acc[kh * 5 + kw]);
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(g, img[y + kh][xx + kw], acc[kh * 5 + kw]);
+    }
   }
 #pragma unroll
   for (int k = 0; k < 25; ++k) red[grp][k][co] = acc[k];
@@ -255,26 +379,25 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
 // ------------------------------------------------------------------------------------------ //
 int64_t conv2_wgrad_groups(int64_t B) { return (B + CB_IPB - 1) / CB_IPB; }
 
-void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf, at::Tensor& g1,
-               at::Tensor& slab, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1) {
+void conv2_bwd(const at::Tensor& dap, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a1,
+               const at::Tensor& w2bf, at::Tensor& g1, at::Tensor& slab, at::Tensor& gb2) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
-  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
+  TORCH_CHECK(dap.dtype() == at::kFloat && dap.numel() == (int64_t)CB_KQ * B * 3136, "conv2_bwd: dap [4][B][3136] fp32");
+  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * 3136 && idx2.numel() == a2.numel(), "conv2_bwd: a2/idx2");
   TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && g1.numel() == a1.numel(), "conv2_bwd: a1/g1");
   TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200, "conv2_bwd: w2");
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_bwd: slab must hold ceil(B/4) x 51200");
-  TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "conv2_bwd: grads");
+  TORCH_CHECK(gb2.numel() == 64 && gb2.dtype() == at::kFloat, "conv2_bwd: gb2");
   static bool attr = [] {
     hipFuncSetAttribute((const void*)conv2_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
     return true;
   }();
   (void)attr;
-  const int n_dgrad = 2 * B, n_wgrad = 5 * G;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv2_bwd_kernel<<<n_dgrad + n_wgrad + 1, 256, CB_LDS, stream>>>(
-      (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
-      (u16*)g1.data_ptr(), slab.data_ptr<float>(), gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), B,
-      n_dgrad, n_wgrad);
+  conv2_bwd_kernel<<<B + 5 * G, 512, CB_LDS, stream>>>(
+      dap.data_ptr<float>(), (const u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(),
+      (const u16*)w2bf.data_ptr(), (u16*)g1.data_ptr(), slab.data_ptr<float>(), gb2.data_ptr<float>(), B, B);
 }
 
 void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,

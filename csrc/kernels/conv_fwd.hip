@@ -19,56 +19,63 @@ namespace mihvd {
 
 // ------------------------------------------------------------------------------------------ //
 // conv1: x[row][784] fp32 -> a1[b][14][14][32] bf16 + argmax idx1 (0..3, u8)
-// grid (2, B): blockIdx.x = half of the pooled rows, blockIdx.y = image. 256 threads.
+// grid (7, B): blockIdx.x = pair of pooled rows, blockIdx.y = image. 256 threads:
+// lane co = t & 31 owns an output channel (25 weights in registers), t >> 5 picks the position.
 // ------------------------------------------------------------------------------------------ //
 __global__ void __launch_bounds__(256) conv1_fwd_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const float* __restrict__ w1, const float* __restrict__ b1, u16* __restrict__ a1, uint8_t* __restrict__ idx1,
     int B) {
-  __shared__ float img[18][33];  // 18 input rows (14 + 2*2 halo) x 32 cols (28 + 2*2), padded
-  const int half = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  __shared__ float img[8][33];  // 8 input rows (4 conv rows + 2*2 halo) x 32 cols (28 + 2*2)
+  const int pr = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   int row = b;
   if (rows != nullptr) {
     const int64_t step = state ? state[ST_FWD] : 0;
     row = rows[(int)((step * (int64_t)B + b) % n_pool)];
   }
   const float* xi = x + (int64_t)row * 784;
-  const int y0 = half * 14 - 2;  // first input row held in LDS
-  for (int i = t; i < 18 * 32; i += 256) {
-    int r = i >> 5, c = i & 31;
-    int gy = y0 + r, gx = c - 2;
-    float v = 0.f;
-    if (gy >= 0 && gy < 28 && gx >= 0 && gx < 28) v = xi[gy * 28 + gx];
-    img[r][c] = v;
-  }
   const int co = t & 31, g = t >> 5;
   float w[25];
 #pragma unroll
   for (int k = 0; k < 25; ++k) w[k] = w1[k * 32 + co];
   const float bias = b1[co];
+  const int y0 = pr * 4 - 2;  // first input row held in LDS
+  {
+    const int r = t >> 5, c = t & 31;  // 256 threads = 8 rows x 32 cols
+    const int gy = y0 + r, gx = c - 2;
+    const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
+    const float v = xi[in ? gy * 28 + gx : 0];
+    img[r][c] = in ? v : 0.f;
+  }
   __syncthreads();
-  for (int pos = g; pos < 98; pos += 8) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pos = g + 8 * i;  // 0..27: local pooled row pos/14, col pos%14
+    if (pos >= 28) break;
     const int pyl = pos / 14, px = pos - pyl * 14;
+    float win[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) win[r][c] = img[2 * pyl + r][2 * px + c];
     float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
+    for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
       for (int kw = 0; kw < 5; ++kw) {
         const float wk = w[kh * 5 + kw];
-        const int r = 2 * pyl + kh, c = 2 * px + kw;
-        s[0] = fmaf(img[r][c], wk, s[0]);
-        s[1] = fmaf(img[r][c + 1], wk, s[1]);
-        s[2] = fmaf(img[r + 1][c], wk, s[2]);
-        s[3] = fmaf(img[r + 1][c + 1], wk, s[3]);
+        s[0] = fmaf(win[kh][kw], wk, s[0]);
+        s[1] = fmaf(win[kh][kw + 1], wk, s[1]);
+        s[2] = fmaf(win[kh + 1][kw], wk, s[2]);
+        s[3] = fmaf(win[kh + 1][kw + 1], wk, s[3]);
       }
-    }
     int best = 0;
     float m = s[0];
 #pragma unroll
-    for (int i = 1; i < 4; ++i)
-      if (s[i] > m) { m = s[i]; best = i; }
+    for (int j = 1; j < 4; ++j)
+      if (s[j] > m) { m = s[j]; best = j; }
     const float y = fmaxf(m + bias, 0.f);
-    const int py = half * 7 + pyl;
+    const int py = pr * 2 + pyl;
     const int64_t o = (((int64_t)b * 14 + py) * 14 + px) * 32 + co;
     a1[o] = f2bf(y);
     idx1[o] = (uint8_t)best;
@@ -91,21 +98,23 @@ __global__ void __launch_bounds__(256) conv2_fwd_kernel(
   u16* img = smem;            // [18][18][32]
   u16* wim = smem + C2_IMG;   // [800][C2_WROW] (k = (kh*5+kw)*32 + ci, n = co - 32*half)
   const int half = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  // Stage the image with a zero halo (16-byte chunks: 4 per pixel).
-  const uint4* src = reinterpret_cast<const uint4*>(a1 + (int64_t)b * 14 * 14 * 32);
-  for (int i = t; i < 18 * 18 * 4; i += 256) {
+  // Issue every load first (image: 6 x 16 B, weights: 13 x 16 B per thread), then write LDS.
+  const u16* src = a1 + (int64_t)b * 14 * 14 * 32;
+  uint4 iv[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int i = min(t + 256 * k, 18 * 18 * 4 - 1);
     const int pix = i >> 2, ch = i & 3;
     const int y = pix / 18 - 2, x = pix % 18 - 2;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (y >= 0 && y < 14 && x >= 0 && x < 14) v = src[(y * 14 + x) * 4 + ch];
-    reinterpret_cast<uint4*>(img)[i] = v;
+    const bool in = y >= 0 && y < 14 && x >= 0 && x < 14;
+    const uint4 v = *reinterpret_cast<const uint4*>(src + ((in ? y : 0) * 14 + (in ? x : 0)) * 32 + ch * 8);
+    iv[k] = in ? v : make_uint4(0, 0, 0, 0);
   }
-  // Stage this block's 32 output channels of W2 (bf16 [800][64]) -> [800][C2_WROW].
-  for (int i = t; i < 800 * 4; i += 256) {
-    const int k = i >> 2, ch = i & 3;
-    const uint4 v = reinterpret_cast<const uint4*>(w2bf + (int64_t)k * 64 + half * 32)[ch];
-    *reinterpret_cast<uint2*>(wim + k * C2_WROW + ch * 8) = make_uint2(v.x, v.y);
-    *reinterpret_cast<uint2*>(wim + k * C2_WROW + ch * 8 + 4) = make_uint2(v.z, v.w);
+  stage_tile<256, 13>(wim, C2_WROW, w2bf + half * 32, 64, 800, 800, 4, t);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int i = t + 256 * k;
+    if (i < 18 * 18 * 4) reinterpret_cast<uint4*>(img)[i] = iv[k];
   }
   __syncthreads();
 
@@ -186,7 +195,7 @@ void conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const
   }
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv1_fwd_kernel<<<dim3(2, B), 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(),
+  conv1_fwd_kernel<<<dim3(7, B), 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(),
                                                    b1.data_ptr<float>(), (u16*)a1.data_ptr(), idx1.data_ptr<uint8_t>(), B);
 }
 

@@ -13,10 +13,11 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats);
 void fc1_bwd(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, const at::Tensor& h,
-             const at::Tensor& dlog, at::Tensor& g2, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4);
+             const at::Tensor& dlog, at::Tensor& dap, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4,
+             at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1);
 int64_t conv2_wgrad_groups(int64_t B);
-void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf, at::Tensor& g1,
-               at::Tensor& slab, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1);
+void conv2_bwd(const at::Tensor& dap, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a1,
+               const at::Tensor& w2bf, at::Tensor& g1, at::Tensor& slab, at::Tensor& gb2);
 void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                  const at::Tensor& g1, const at::Tensor& idx1, const at::Tensor& slab, at::Tensor& gW1, at::Tensor& gb1,
                  at::Tensor& gW2);
@@ -41,12 +42,13 @@ static void head_op(const at::Tensor& zpart, const at::Tensor& b3, const at::Ten
   mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats);
 }
 static void fc1_bwd_op(const at::Tensor& dz, const at::Tensor& w3, const at::Tensor& a2, const at::Tensor& h,
-                       const at::Tensor& dlog, at::Tensor g2, at::Tensor gW3, at::Tensor gb3, at::Tensor gW4, at::Tensor gb4) {
-  mihvd::fc1_bwd(dz, w3, a2, h, dlog, g2, gW3, gb3, gW4, gb4);
+                       const at::Tensor& dlog, at::Tensor dap, at::Tensor gW3, at::Tensor gb3, at::Tensor gW4, at::Tensor gb4,
+                       at::Tensor gb2, at::Tensor gW1, at::Tensor gb1) {
+  mihvd::fc1_bwd(dz, w3, a2, h, dlog, dap, gW3, gb3, gW4, gb4, gb2, gW1, gb1);
 }
-static void conv2_bwd_op(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2,
-                         at::Tensor g1, at::Tensor slab, at::Tensor gb2, at::Tensor gW1, at::Tensor gb1) {
-  mihvd::conv2_bwd(g2, idx2, a1, w2, g1, slab, gb2, gW1, gb1);
+static void conv2_bwd_op(const at::Tensor& dap, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a1,
+                         const at::Tensor& w2, at::Tensor g1, at::Tensor slab, at::Tensor gb2) {
+  mihvd::conv2_bwd(dap, a2, idx2, a1, w2, g1, slab, gb2);
 }
 static void conv1_wgrad_op(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                            const at::Tensor& g1, const at::Tensor& idx1, const at::Tensor& slab, at::Tensor gW1,
@@ -67,11 +69,11 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
-  m.def("fc1_bwd(Tensor dz, Tensor w3bf, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) g2, Tensor(b!) gW3, "
-        "Tensor(c!) gb3, Tensor(d!) gW4, Tensor(e!) gb4) -> ()");
+  m.def("fc1_bwd(Tensor dz, Tensor w3bf, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) dap, Tensor(b!) gW3, "
+        "Tensor(c!) gb3, Tensor(d!) gW4, Tensor(e!) gb4, Tensor(f!) gb2, Tensor(g!) gW1, Tensor(h!) gb1) -> ()");
   m.def("conv2_wgrad_groups(int B) -> int", &mihvd::conv2_wgrad_groups);
-  m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor(a!) g1, Tensor(b!) slab, Tensor(c!) gb2, "
-        "Tensor(d!) gW1, Tensor(e!) gb1) -> ()");
+  m.def("conv2_bwd(Tensor dap, Tensor a2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor(a!) g1, Tensor(b!) slab, "
+        "Tensor(c!) gb2) -> ()");
   m.def("conv1_wgrad(Tensor x, Tensor? rows, Tensor? state, Tensor g1, Tensor idx1, Tensor slab, Tensor(a!) gW1, "
         "Tensor(b!) gb1, Tensor(c!) gW2) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "

@@ -35,7 +35,8 @@ BucketPlan plan_buckets(const std::vector<TensorSpec>& specs, const std::vector<
     int b = -1;
     if (it != open.end()) {
       b = it->second;
-      if (threshold_bytes > 0 && bytes[b] > 0 && bytes[b] + tbytes > threshold_bytes) b = -1;
+      const int64_t aligned_end = ((plan.numel[b] + align_el - 1) / align_el * align_el) * s.elem_size;
+      if (threshold_bytes > 0 && bytes[b] > 0 && aligned_end + tbytes > threshold_bytes) b = -1;
     }
     if (b == -1) {
       b = static_cast<int>(plan.members.size());

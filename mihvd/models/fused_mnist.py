@@ -98,7 +98,7 @@ class FusedMNISTTrainer:
         self.dz = torch.empty(B, 1024, **bf)
         self.dlog = torch.empty(B, 10, **f32)
         self.stats = torch.zeros(B, 2, **f32)
-        self.g2 = torch.empty(B, 3136, **bf)
+        self.dap = torch.empty(4, B, 3136, **f32)   # fc1 dgrad split-K partial slabs
         self.g1 = torch.empty(B, 14, 14, 32, **bf)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
         self.x_buf = torch.zeros(B, 784, **f32)
@@ -167,9 +167,10 @@ class FusedMNISTTrainer:
         o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
-        o.fc1_bwd(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.h, self.dlog, self.g2,
+        o.fc1_bwd(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.h, self.dlog, self.dap,
                   self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
-                  self.gview("dense_1/bias"))
+                  self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
+                  self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
         main = torch.cuda.current_stream(self.device)
         fc_bucket = self.grads[FC_START:]
         conv_bucket = self.grads[:FC_START]
@@ -177,9 +178,8 @@ class FusedMNISTTrainer:
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
                 self._allreduce(fc_bucket, FC_START, FLAT_NUMEL)
-        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1, self.slab,
-                    self.gview("conv_layer2/conv2d/bias"), self.gview("conv_layer1/conv2d/kernel"),
-                    self.gview("conv_layer1/conv2d/bias"))
+        o.conv2_bwd(self.dap, self.a2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1,
+                    self.slab, self.gview("conv_layer2/conv2d/bias"))
         o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),
                       self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/kernel"))
         if self.world > 1:

@@ -1,0 +1,303 @@
+"""CPU unit tests: native runtime (planner, controller, timeline, stall inspector, faults), env
+discovery, launcher argv compatibility, checkpoint layout, TF1-session and Keras-fit plumbing."""
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from mihvd import _native
+from mihvd.runner import launch as L
+from mihvd.utils import checkpoint as ckpt
+from mihvd.utils import env as envmod
+
+rt = _native.runtime()
+
+REFERENCE_ARGV = ("-np 2 --allow-run-as-root -bind-to none -map-by slot -x LD_LIBRARY_PATH -x PATH "
+                  "-mca pml ob1 -mca btl ^openib python /examples/tensorflow_mnist.py").split()
+
+
+# ------------------------------------------------------------------------------ planner
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.tuples(st.integers(1, 5000), st.integers(0, 1)), min_size=1, max_size=30),
+       st.integers(0, 40000), st.sampled_from([4, 16, 256]))
+def test_plan_buckets_properties(raw, threshold, align):
+    tensors = [(n, 4 if dt == 0 else 2, dt) for n, dt in raw]  # dtype code fixes the element size
+    specs = [rt.TensorSpec(n, es, dt, 0) for n, es, dt in tensors]
+    order = list(range(len(specs)))[::-1]
+    plan = rt.plan_buckets(specs, order, threshold, align)
+    seen = set()
+    for b, (mem, offs) in enumerate(zip(plan.members, plan.offsets)):
+        dts = {tensors[i][2] for i in mem}
+        assert len(dts) == 1  # never mixes dtypes
+        esz = tensors[mem[0]][1]
+        ends = []
+        for i, o in zip(mem, offs):
+            assert (o * esz) % align == 0
+            assert o >= (ends[-1] if ends else 0)  # no overlap, pack order preserved
+            ends.append(o + tensors[i][0])
+            seen.add(i)
+            assert plan.tensor_bucket[i] == b and plan.tensor_offset[i] == o
+        assert plan.numel[b] >= ends[-1]
+        if threshold > 0 and len(mem) > 1:
+            assert ends[-1] * esz <= threshold
+    assert seen == set(range(len(specs)))
+    # deterministic
+    plan2 = rt.plan_buckets(specs, order, threshold, align)
+    assert list(plan2.members) == list(plan.members)
+
+
+def test_controller_releases_buckets_in_order():
+    c = rt.Controller([0, 0, 1, 2], 3, 1)
+    assert c.mark_ready(2) == []          # bucket 1 complete but bucket 0 not launched yet
+    assert c.mark_ready(0) == []
+    assert c.mark_ready(1) == [0, 1]      # releases 0 then the already-complete 1
+    assert c.mark_ready(3) == [2]
+    with pytest.raises(RuntimeError):
+        c.mark_ready(3)
+    c.reset()
+    assert c.flush() == [0, 1, 2]
+
+
+def test_controller_backward_passes():
+    c = rt.Controller([0, 0], 1, 2)
+    assert c.mark_ready(0) == [] and c.mark_ready(1) == []
+    assert c.mark_ready(0) == [] and c.mark_ready(1) == [0]
+
+
+def test_signature_sensitivity():
+    s1 = rt.tensor_signature(["a", "b"], [[2, 3], [4]], ["float32", "float32"])
+    assert s1 == rt.tensor_signature(["a", "b"], [[2, 3], [4]], ["float32", "float32"])
+    assert s1 != rt.tensor_signature(["a", "b"], [[3, 2], [4]], ["float32", "float32"])
+    assert s1 != rt.tensor_signature(["a", "c"], [[2, 3], [4]], ["float32", "float32"])
+
+
+# ------------------------------------------------------------------------------ timeline / stall / faults
+def test_timeline_writes_valid_chrome_trace(tmp_path):
+    p = tmp_path / "tl.json"
+    tl = rt.Timeline(str(p), 3)
+    tl.begin("allreduce.bucket0", "ALLREDUCE", 1)
+    tl.end("allreduce.bucket0", "ALLREDUCE", 1)
+    tl.complete("fc1_fwd", "COMPUTE", 0, 10.0, 5.5)
+    tl.instant("step", "STEP", 0)
+    tl.counter("loss", 0.25)
+    tl.close()
+    ev = json.loads(p.read_text())
+    names = [e["name"] for e in ev]
+    assert "process_name" in names and "allreduce.bucket0" in names and "loss" in names
+    assert all(e["pid"] == 3 for e in ev)
+    x = [e for e in ev if e["ph"] == "X"][0]
+    assert x["dur"] == pytest.approx(5.5)
+
+
+def test_stall_inspector_reports_old_ops():
+    si = rt.StallInspector(0.2, 0.0, 0.05, 0)
+    si.set_hard_abort(False)
+    si.start()
+    a = si.submit("allreduce.bucket0")
+    b = si.submit("allreduce.bucket1")
+    si.complete(b)
+    time.sleep(0.5)
+    out = si.outstanding(0.1)
+    assert [r.name for r in out] == ["allreduce.bucket0"]
+    assert si.stalled and si.warnings_emitted == 1
+    si.complete(a)
+    assert si.num_outstanding() == 0
+    si.stop()
+
+
+def test_fault_plan_parsing():
+    fp = rt.FaultPlan("kill:rank=1:step=50:code=3;delay:step=2:ms=10")
+    assert [a.kind for a in fp.due(1, 50)] == ["kill"]
+    assert fp.due(1, 50)[0].args["code"] == "3"
+    assert [a.kind for a in fp.due(0, 2)] == ["delay"]
+    assert fp.due(0, 3) == []
+    with pytest.raises(Exception):
+        rt.FaultPlan("explode:rank=0")
+
+
+def test_step_stats():
+    s = rt.StepStats(4)
+    for v in (1, 2, 3, 4, 100):
+        s.add(v)
+    assert s.count == 5 and s.mean() == pytest.approx((2 + 3 + 4 + 100) / 4)
+    assert s.percentile(50) == pytest.approx(3.5)
+
+
+# ------------------------------------------------------------------------------ env / launcher
+def test_env_discovery_sources():
+    t = envmod.discover({"OMPI_COMM_WORLD_RANK": "3", "OMPI_COMM_WORLD_SIZE": "8", "OMPI_COMM_WORLD_LOCAL_RANK": "1",
+                         "OMPI_COMM_WORLD_LOCAL_SIZE": "2"})
+    assert (t.rank, t.size, t.local_rank, t.local_size, t.cross_rank, t.cross_size, t.source) == (3, 8, 1, 2, 1, 4, "ompi")
+    t = envmod.discover({"RANK": "1", "WORLD_SIZE": "2", "LOCAL_RANK": "1", "LOCAL_WORLD_SIZE": "2",
+                         "MASTER_ADDR": "10.0.0.1", "MASTER_PORT": "1234"})
+    assert (t.rank, t.master_addr, t.master_port, t.source) == (1, "10.0.0.1", 1234, "native")
+    t = envmod.discover({"PMI_RANK": "2", "PMI_SIZE": "4"})
+    assert (t.rank, t.size, t.source) == (2, 4, "pmi")
+    assert envmod.discover({}).source == "single"
+    with pytest.raises(ValueError):
+        envmod.discover({"RANK": "5", "WORLD_SIZE": "2"})
+
+
+def test_launcher_accepts_reference_mpirun_argv():
+    spec = L.parse_args(REFERENCE_ARGV)
+    assert spec.np == 2 and spec.map_by == "slot"
+    assert spec.command == ["python", "/examples/tensorflow_mnist.py"]
+    assert set(spec.env_forward) == {"LD_LIBRARY_PATH", "PATH"}
+    assert ("pml", "ob1") in spec.mca and ("btl", "^openib") in spec.mca
+    assert "--allow-run-as-root" in spec.ignored
+
+
+def test_launcher_hosts_and_layout(tmp_path):
+    spec = L.parse_args(["-np", "4", "-H", "a:2,b:2", "python", "x.py"])
+    lay = L.assign_ranks(spec.hosts, spec.np, "slot")
+    assert [(r, h, lr, ls, n) for r, h, lr, ls, n in lay] == [(0, "a", 0, 2, 0), (1, "a", 1, 2, 0), (2, "b", 0, 2, 1),
+                                                              (3, "b", 1, 2, 1)]
+    lay = L.assign_ranks(spec.hosts, spec.np, "node")
+    assert [(r, h) for r, h, *_ in lay] == [(0, "a"), (1, "b"), (2, "a"), (3, "b")]
+    hf = tmp_path / "hostfile"
+    hf.write_text("worker-0.svc slots=8\nworker-1.svc slots=8\n# comment\n")
+    spec = L.parse_args(["--hostfile", str(hf), "python", "t.py"])
+    assert spec.hosts == [("worker-0.svc", 8), ("worker-1.svc", 8)] and spec.np == 16
+    with pytest.raises(SystemExit):
+        L.assign_ranks([("a", 1)], 2)
+
+
+def test_launcher_rank_env():
+    spec = L.parse_args(["-np", "2", "-x", "FOO=bar", "-x", "HOME", "--fusion-threshold-mb", "16", "python", "t.py"])
+    e = L.build_rank_env(spec, 1, 1, 2, 0, "127.0.0.1", 29501, base_env={"HOME": "/h"})
+    assert e["RANK"] == "1" and e["OMPI_COMM_WORLD_LOCAL_RANK"] == "1" and e["MASTER_PORT"] == "29501"
+    assert e["FOO"] == "bar" and e["HOME"] == "/h" and e["MIHVD_FUSION_THRESHOLD"] == str(16 * 1024 * 1024)
+
+
+# ------------------------------------------------------------------------------ checkpoints
+def test_checkpoint_layout_and_rotation(tmp_path):
+    s = ckpt.Saver(max_to_keep=3)
+    for step in (10, 20, 30, 40):
+        s.save(str(tmp_path), {"w": torch.full((2,), float(step)), "global_step": torch.tensor(step)}, step)
+    latest, allp = ckpt.read_index(str(tmp_path))
+    assert latest == "model.ckpt-40" and allp == ["model.ckpt-20", "model.ckpt-30", "model.ckpt-40"]
+    assert sorted(os.listdir(tmp_path)) == ["checkpoint", "model.ckpt-20.pt", "model.ckpt-30.pt", "model.ckpt-40.pt"]
+    v = ckpt.Saver.restore(ckpt.latest_checkpoint(str(tmp_path)))
+    assert float(v["w"][0]) == 40.0 and int(v["global_step"]) == 40
+
+
+def test_tf_variable_mapping_roundtrip():
+    from mihvd.models.mnist import NUM_PARAMS, MNISTConvNet
+    from mihvd.optim import TFAdam
+
+    m = MNISTConvNet(seed=0)
+    assert sum(p.numel() for p in m.parameters()) == NUM_PARAMS == 3274634
+    opt = TFAdam(m.parameters(), lr=1e-3)
+    m(torch.rand(2, 784)).sum().backward()
+    opt.step()
+    v = ckpt.adam_to_tf_vars(m.ordered_parameters(), opt, 7)
+    assert v["dense/kernel"].shape == (3136, 1024) and "dense/kernel/Adam_1" in v
+    assert int(v["global_step"]) == 7 and float(v["beta1_power"]) == pytest.approx(0.9 ** 2)
+    m2 = MNISTConvNet(seed=1)
+    opt2 = TFAdam(m2.parameters(), lr=1e-3)
+    step = ckpt.tf_vars_to_adam(v, m2.ordered_parameters(), opt2)
+    assert step == 7
+    for (n, a), (_, b) in zip(m.ordered_parameters(), m2.ordered_parameters()):
+        assert torch.equal(a, b)
+    assert float(opt2.state[m2.dense.kernel]["step"]) == 1.0
+
+
+def test_tfadam_matches_tf1_formula():
+    from mihvd.optim import TFAdam
+
+    p = torch.nn.Parameter(torch.tensor([1.0, -2.0]))
+    opt = TFAdam([p], lr=0.1)
+    g = torch.tensor([0.5, -1.0])
+    m = v = torch.zeros(2)
+    ref = p.detach().clone()
+    for t in (1, 2):
+        p.grad = g.clone()
+        opt.step()
+        m = 0.9 * m + 0.1 * g
+        v = 0.999 * v + 0.001 * g * g
+        lr_t = 0.1 * np.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        ref = ref - lr_t * m / (v.sqrt() + 1e-8)
+    assert torch.allclose(p.detach(), ref, atol=1e-6)
+
+
+# ------------------------------------------------------------------------------ session / keras (single process)
+def test_monitored_session_single_rank(tmp_path, hvd_single):
+    import mihvd.tensorflow as htf
+    from mihvd.models.mnist import MNISTConvNet, softmax_cross_entropy
+    from mihvd.optim import TFAdam
+
+    model = MNISTConvNet(seed=0)
+    opt = hvd_single.DistributedOptimizer(TFAdam(model.parameters(), lr=1e-3), named_parameters=model.named_parameters())
+    state = htf.TorchTrainState(model, opt)
+    log = htf.LoggingTensorHook({"step": "global_step", "loss": "loss"}, every_n_iter=2)
+
+    def train_op(image, label):
+        opt.zero_grad()
+        loss = softmax_cross_entropy(model(image), label)
+        loss.backward()
+        opt.step()
+        return {"loss": loss.detach()}
+
+    hooks = [htf.BroadcastGlobalVariablesHook(0), htf.StopAtStepHook(last_step=5), log]
+    with htf.MonitoredTrainingSession(checkpoint_dir=str(tmp_path), hooks=hooks, state=state) as s:
+        while not s.should_stop():
+            s.run(train_op, feed_dict={"image": torch.rand(4, 784), "label": torch.randint(0, 10, (4,))})
+    assert state.global_step == 5 and len(log.lines) == 3
+    assert ckpt.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-5")
+    # restart resumes at 5 and stops immediately
+    state2 = htf.TorchTrainState(MNISTConvNet(seed=9), None)
+    with htf.MonitoredTrainingSession(checkpoint_dir=str(tmp_path), hooks=[htf.StopAtStepHook(last_step=5)],
+                                      state=state2) as s:
+        assert s.should_stop() and s.restored_from is not None
+    assert state2.global_step == 5
+    assert torch.equal(state2.model.dense.kernel, model.dense.kernel)
+
+
+def test_keras_fit_single_rank(tmp_path, hvd_single):
+    import mihvd.keras as hk
+    from mihvd.models.mnist import MNISTConvNet
+    from mihvd.optim import TFAdam
+    from mihvd.utils.data import synthetic_mnist
+
+    (x, y), (xt, yt) = synthetic_mnist(n_train=600, n_test=200, seed=3)
+    x = x.reshape(-1, 784).astype(np.float32) / 255
+    xt = xt.reshape(-1, 784).astype(np.float32) / 255
+    model = hk.Model(MNISTConvNet(seed=0))
+    opt = hk.DistributedOptimizer(TFAdam(model.module.parameters(), lr=1e-3), named_parameters=model.module.named_parameters())
+    model.compile(opt, torch.nn.functional.cross_entropy, ["accuracy"])
+    cbs = [hk.callbacks.BroadcastGlobalVariablesCallback(0), hk.callbacks.MetricAverageCallback(),
+           hk.callbacks.TensorBoard(str(tmp_path / "logs")),
+           hk.callbacks.ModelCheckpoint(str(tmp_path / "ckpt" / "mnist-{epoch}.h5"), save_best_only=True)]
+    model.fit(x, y, batch_size=50, epochs=2, steps_per_epoch=6, validation_data=(xt, yt), validation_steps=2,
+              callbacks=cbs, verbose=0)
+    assert cbs[0].broadcast_done and len(model.history["loss"]) == 2
+    assert os.path.exists(tmp_path / "ckpt" / "mnist-1.h5")
+    assert (tmp_path / "logs" / "metrics.jsonl").exists()
+    path = model.save(str(tmp_path / "final_model"))
+    assert path.endswith("model.pt")
+    m2 = hk.Model.load_weights(MNISTConvNet(seed=5), str(tmp_path / "final_model"))
+    assert torch.equal(m2.dense.bias, model.module.dense.bias)
+
+
+def test_lr_scaler_rule(hvd_single):
+    # tensorflow_mnist.py:123-127
+    hvd = hvd_single
+    scaler = hvd.size()
+    assert scaler == 1
+    adasum_scaler = hvd.local_size() if hvd.nccl_built() else 1
+    assert adasum_scaler == 1
+
+
+def test_synthetic_data_and_generator():
+    from mihvd.utils.data import synthetic_mnist, train_input_generator
+
+    (x, y), (xt, yt) = synthetic_mnist(n_train=1000, n_test=100)
+    assert x.shape == (1000, 28, 28) and x.dtype == np.uint8 and set(np.unique(y)) <= set(range(10))
+    gen = train_input_generator(x.reshape(-1, 784), y, batch_size=300, rng=np.random.default_rng(0))
+    batches = [next(gen) for _ in range(4)]
+    assert all(b[0].shape == (300, 784) for b in batches)  # tail of 100 dropped each pass
