@@ -78,27 +78,46 @@ __device__ __forceinline__ float wave_max(float v) {
 // lstride elements, 16-byte aligned). Rows >= valid_rows are zero-filled. Every load is issued
 // before any LDS store and none is predicated (addresses are clamped, the value is selected after),
 // so the whole tile costs one memory latency instead of one per iteration.
-template <int NT, int MAXIT>
-__device__ __forceinline__ void stage_tile(u16* lds, int lstride, const u16* __restrict__ g, int64_t gstride, int rows,
-                                           int valid_rows, int cpr, int t) {
-  const int total = rows * cpr;
-  uint4 buf[MAXIT];
+//
+// Split in two phases so several tiles' loads can all be in flight before the first LDS store:
+//   TileLoad<NT, MAXIT, CPR> a, w;  a.load(...); w.load(...); a.store(...); w.store(...);
+// Out-of-range rows are zeroed with a bit mask, never with a select: hipcc turns a select on a
+// loaded value into a branch around the load, which serialises the loads (one wait per load).
+template <int NT, int MAXIT, int CPR>
+struct TileLoad {
+  uint4 v[MAXIT];
+  __device__ __forceinline__ void load(const u16* __restrict__ g, int64_t gstride, int rows, int valid_rows, int t) {
+    const int total = rows * CPR;
 #pragma unroll
-  for (int it = 0; it < MAXIT; ++it) {
-    const int i = min(t + it * NT, total - 1);
-    const int r = i / cpr, c = i - r * cpr;
-    const int rr = min(r, valid_rows - 1);
-    const uint4 v = *reinterpret_cast<const uint4*>(g + (int64_t)rr * gstride + c * 8);
-    buf[it] = (r < valid_rows) ? v : make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (int it = 0; it < MAXIT; ++it) {
-    const int i = t + it * NT;
-    if (i < total) {
-      const int r = i / cpr, c = i - r * cpr;
-      *reinterpret_cast<uint4*>(lds + r * lstride + c * 8) = buf[it];
+    for (int it = 0; it < MAXIT; ++it) {
+      const int i = min(t + it * NT, total - 1);
+      const int r = i / CPR, c = i - r * CPR;
+      const int rr = min(r, valid_rows - 1);
+      const uint32_t mask = (r < valid_rows) ? 0xffffffffu : 0u;
+      const uint4 x = *reinterpret_cast<const uint4*>(g + (int64_t)rr * gstride + c * 8);
+      v[it] = make_uint4(x.x & mask, x.y & mask, x.z & mask, x.w & mask);
     }
   }
+  __device__ __forceinline__ void store(u16* lds, int lstride, int rows, int t) const {
+    const int total = rows * CPR;
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int i = t + it * NT;
+      if (i < total) {
+        const int r = i / CPR, c = i - r * CPR;
+        *reinterpret_cast<uint4*>(lds + r * lstride + c * 8) = v[it];
+      }
+    }
+  }
+};
+
+// Zero a loaded value when `keep` is false without a select (see TileLoad).
+__device__ __forceinline__ uint4 mask_u4(uint4 v, bool keep) {
+  const uint32_t m = keep ? 0xffffffffu : 0u;
+  return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+__device__ __forceinline__ float mask_f(float v, bool keep) {
+  return __uint_as_float(__float_as_uint(v) & (keep ? 0xffffffffu : 0u));
 }
 
 __device__ __forceinline__ uint2 pack4bf(float a, float b, float c, float d) {

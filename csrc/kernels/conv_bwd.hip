@@ -102,7 +102,9 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       ie[k] = t + 512 * k;
       items[k] = load_dy_item(dap, a2, idx2, B, b, (i >> 4) * 64 + (i & 15) * 4);
     }
-    stage_tile<512, 13>(Ws, CB_WSTR, w2bf, 64, 800, 800, 8, t);
+    TileLoad<512, 13, 8> lw;
+    lw.load(w2bf, 64, 800, 800, t);
+    lw.store(Ws, CB_WSTR, 800, t);
     // zero halo pixels of D (interior pixels are fully written by the scatter)
     for (int i = t; i < 324 * 8; i += 512) {
       const int pix = i >> 3, c = i & 7;
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       const bool in = pix < 324 && y >= 0 && y < 14 && x >= 0 && x < 14;
       const int yc = in ? y : 0, xc = in ? x : 0;
       const uint4 v = *reinterpret_cast<const uint4*>(a1 + ((int64_t)bb * 196 + yc * 14 + xc) * 32 + c * 8);
-      av[k] = in ? v : make_uint4(0, 0, 0, 0);
+      av[k] = mask_u4(v, in);
     }
     DyItem items[4];
 #pragma unroll
@@ -296,19 +298,17 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
   if ((int)blockIdx.x >= B) {
     const int i = ((int)blockIdx.x - B) * 256 + t;  // float4 index, 12800 total
     if (i < 51200 / 4) {
+      // all (<= 32) slab loads in flight at once; absent slabs are masked, not branched around
+      float4 v[32];
+#pragma unroll
+      for (int g = 0; g < 32; ++g) {
+        const float4 x = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[i];
+        const bool k = g < nslab;
+        v[g] = make_float4(mask_f(x.x, k), mask_f(x.y, k), mask_f(x.z, k), mask_f(x.w, k));
+      }
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      int g = 0;
-      for (; g + 5 <= nslab; g += 5) {
-        float4 v[5];
 #pragma unroll
-        for (int u = 0; u < 5; ++u) v[u] = reinterpret_cast<const float4*>(slab + (int64_t)(g + u) * 51200)[i];
-#pragma unroll
-        for (int u = 0; u < 5; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
-      }
-      for (; g < nslab; ++g) {
-        const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)g * 51200)[i];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
+      for (int g = 0; g < 32; ++g) { s.x += v[g].x; s.y += v[g].y; s.z += v[g].z; s.w += v[g].w; }
       reinterpret_cast<float4*>(gW2)[i] = s;
     }
     return;
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
     const int gy = r - 2, gx = c - 2;
     const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
     const float v = xi[in ? gy * 28 + gx : 0];
-    xv[k] = in ? v : 0.f;
+    xv[k] = mask_f(v, in);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) img[(t + 256 * k) >> 5][(t + 256 * k) & 31] = xv[k];

@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(256) conv1_fwd_kernel(
     const int gy = y0 + r, gx = c - 2;
     const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
     const float v = xi[in ? gy * 28 + gx : 0];
-    img[r][c] = in ? v : 0.f;
+    img[r][c] = mask_f(v, in);
   }
   __syncthreads();
 #pragma unroll
@@ -108,14 +108,16 @@ __global__ void __launch_bounds__(256) conv2_fwd_kernel(
     const int y = pix / 18 - 2, x = pix % 18 - 2;
     const bool in = y >= 0 && y < 14 && x >= 0 && x < 14;
     const uint4 v = *reinterpret_cast<const uint4*>(src + ((in ? y : 0) * 14 + (in ? x : 0)) * 32 + ch * 8);
-    iv[k] = in ? v : make_uint4(0, 0, 0, 0);
+    iv[k] = mask_u4(v, in);
   }
-  stage_tile<256, 13>(wim, C2_WROW, w2bf + half * 32, 64, 800, 800, 4, t);
+  TileLoad<256, 13, 4> lw;
+  lw.load(w2bf + half * 32, 64, 800, 800, t);
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     const int i = t + 256 * k;
     if (i < 18 * 18 * 4) reinterpret_cast<uint4*>(img)[i] = iv[k];
   }
+  lw.store(wim, C2_WROW, 800, t);
   __syncthreads();
 
   const int lane = t & 63, wave = t >> 6;

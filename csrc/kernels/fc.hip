@@ -37,9 +37,14 @@ __global__ void __launch_bounds__(256) fc1_fwd_kernel(const u16* __restrict__ a2
   const int nt = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
   const int MT = (B + 15) >> 4, Mpad = MT * 16;
   const int k0 = ks * FC1_KSL;
-  stage_tile<256, (MAXB * FC1_KSL / 8 + 255) / 256>(As, F1_ASTR, a2 + k0, FC1_K, Mpad, B, FC1_KSL / 8, t);
-  stage_tile<256, (FC1_KSL * FC1_NT / 8 + 255) / 256>(Ws, F1_WSTR, w3 + (int64_t)k0 * FC1_N + nt * FC1_NT, FC1_N,
-                                                      FC1_KSL, FC1_KSL, FC1_NT / 8, t);
+  {
+    TileLoad<256, (MAXB * FC1_KSL / 8 + 255) / 256, FC1_KSL / 8> la;
+    TileLoad<256, (FC1_KSL * FC1_NT / 8 + 255) / 256, FC1_NT / 8> lw;
+    lw.load(w3 + (int64_t)k0 * FC1_N + nt * FC1_NT, FC1_N, FC1_KSL, FC1_KSL, t);
+    la.load(a2 + k0, FC1_K, Mpad, B, t);
+    lw.store(Ws, F1_WSTR, FC1_KSL, t);
+    la.store(As, F1_ASTR, Mpad, t);
+  }
   __syncthreads();
   const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4, q = lr >> 2, p = lr & 3;
   f32x4 acc[8];
@@ -84,11 +89,18 @@ __global__ void __launch_bounds__(256) head_kernel(
   float4 parts[FC1_KS];
 #pragma unroll
   for (int s = 0; s < FC1_KS; ++s) parts[s] = *reinterpret_cast<const float4*>(zpart + ((int64_t)s * B + b) * FC1_N + n0);
-  float w4r[4][10];
+  float w4r[4][10];  // this thread's 4 rows of W4 = 40 contiguous floats = 10 x 16 B
+  {
+    float4 wv[10];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int k = 0; k < 10; ++k) wv[k] = reinterpret_cast<const float4*>(w4 + n0 * 10)[k];
 #pragma unroll
-    for (int c = 0; c < 10; ++c) w4r[i][c] = w4[(n0 + i) * 10 + c];
+    for (int k = 0; k < 10; ++k) {
+      const float e[4] = {wv[k].x, wv[k].y, wv[k].z, wv[k].w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w4r[(4 * k + u) / 10][(4 * k + u) % 10] = e[u];
+    }
+  }
   const float4 bb = *reinterpret_cast<const float4*>(b3 + n0);
   float z[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
@@ -175,21 +187,26 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ w3, const u16* __restrict__ a2, const u16* __restrict__ h,
     const float* __restrict__ dlog, float* __restrict__ dap, float* __restrict__ gW3, float* __restrict__ gb3,
     float* __restrict__ gW4, float* __restrict__ gb4, float* __restrict__ gb2, float* __restrict__ gW1,
-    float* __restrict__ gb1, int B) {
+    float* __restrict__ gb1, int B, int role_base) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
   const int MT = (B + 15) >> 4, Mpad = MT * 16;
-  int bid = blockIdx.x;
+  int bid = blockIdx.x + role_base;
   if (bid < FB_DGRAD) {
     // dAp^T[j][b] = sum_n W3[j][n] dz[b][n] over this block's K quarter.
     const int jt = bid >> 2, kq = bid & 3;
     const int j0 = jt * 64, n0 = kq * FB_KQL;
-    u16* Ds = smem;                    // dz   [Mpad][264]  rows = samples
-    u16* Ws = smem + MAXB * FB_DSTR;   // W3   [64][264]    rows = j
-    stage_tile<256, (MAXB * FB_KQL / 8 + 255) / 256>(Ds, FB_DSTR, dz + n0, FC1_N, Mpad, B, FB_KQL / 8, t);
-    stage_tile<256, (64 * FB_KQL / 8 + 255) / 256>(Ws, FB_DSTR, w3 + (int64_t)j0 * FC1_N + n0, FC1_N, 64, 64,
-                                                   FB_KQL / 8, t);
+    u16* Ws = smem;                    // W3   [64][264]    rows = j
+    u16* Ds = smem + 64 * FB_DSTR;     // dz   [Mpad][264]  rows = samples
+    {
+      TileLoad<256, (MAXB * FB_KQL / 8 + 255) / 256, FB_KQL / 8> ld;
+      TileLoad<256, (64 * FB_KQL / 8 + 255) / 256, FB_KQL / 8> lw;
+      lw.load(w3 + (int64_t)j0 * FC1_N + n0, FC1_N, 64, 64, t);
+      ld.load(dz + n0, FC1_N, Mpad, B, t);
+      lw.store(Ws, FB_DSTR, 64, t);
+      ld.store(Ds, FB_DSTR, Mpad, t);
+    }
     __syncthreads();
     f32x4 acc[8];
 #pragma unroll
@@ -223,8 +240,13 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
     u16* Zim = smem;                   // [Kpad][72]  rows b, cols n
     u16* Aim = smem + MAXB * FB_TSTR;  // [Kpad][72]  rows b, cols j
     const int Kpad = (B + 31) & ~31;
-    stage_tile<256, (MAXB * 8 + 255) / 256>(Zim, FB_TSTR, dz + n0, FC1_N, Kpad, B, 8, t);
-    stage_tile<256, (MAXB * 8 + 255) / 256>(Aim, FB_TSTR, a2 + j0, FC1_K, Kpad, B, 8, t);
+    {
+      TileLoad<256, (MAXB * 8 + 255) / 256, 8> lz, la;
+      lz.load(dz + n0, FC1_N, Kpad, B, t);
+      la.load(a2 + j0, FC1_K, Kpad, B, t);
+      lz.store(Zim, FB_TSTR, Kpad, t);
+      la.store(Aim, FB_TSTR, Kpad, t);
+    }
     __syncthreads();
     const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;  // wave's 32 (n) x 32 (j) sub-tile
     f32x4 acc[2][2];
@@ -350,27 +372,50 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                                      stats.data_ptr<float>(), B);
 }
 
-void fc1_bwd(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, const at::Tensor& h,
-             const at::Tensor& dlog, at::Tensor& dap, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4,
-             at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1) {
-  const int B = dz.size(0);
-  TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_bwd: batch");
-  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_bwd: dz");
-  TORCH_CHECK(a2.numel() == (int64_t)B * FC1_K && a2.dtype() == at::kBFloat16, "fc1_bwd: a2");
-  TORCH_CHECK(dap.dtype() == at::kFloat && dap.numel() == (int64_t)FB_KQ * B * FC1_K, "fc1_bwd: dap must be fp32 [4][B][3136]");
-  TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_bwd: gW3");
-  TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_bwd: fc grads");
-  TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "fc1_bwd: conv grads");
+// Two launches of one kernel so each gets its own LDS budget: the weight-gradient roles (37 KB:
+// several blocks per CU) and the dgrad split-K role ((Mpad + 64) x 528 B: one block per CU).
+// The wgrad launch completes the whole "fc" gradient bucket, so its allreduce can start while
+// dgrad and the conv backward still run.
+static void fc1_bwd_attr() {
   static bool attr = [] {
     hipFuncSetAttribute((const void*)fc1_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, FB_LDS);
     return true;
   }();
   (void)attr;
+}
+
+void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
+               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1) {
+  const int B = dz.size(0);
+  TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_wgrad: batch");
+  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
+  TORCH_CHECK(a2.numel() == (int64_t)B * FC1_K && a2.dtype() == at::kBFloat16, "fc1_wgrad: a2");
+  TORCH_CHECK(h.numel() == (int64_t)B * FC1_N && h.dtype() == at::kBFloat16 && dlog.numel() == B * 10, "fc1_wgrad: h/dlog");
+  TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_wgrad: gW3");
+  TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_wgrad: fc grads");
+  TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "fc1_wgrad: conv grads");
+  fc1_bwd_attr();
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  fc1_bwd_kernel<<<FB_TOTAL, 256, FB_LDS, stream>>>(
-      (const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(),
-      dlog.data_ptr<float>(), dap.data_ptr<float>(), gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(),
-      gb4.data_ptr<float>(), gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), B);
+  fc1_bwd_kernel<<<FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC, 256, FB_LDS_WG, stream>>>(
+      (const u16*)dz.data_ptr(), nullptr, (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
+      nullptr, gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(),
+      gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, FB_DGRAD);
+}
+
+void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, at::Tensor& dap) {
+  const int B = dz.size(0);
+  TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_dgrad: batch");
+  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_dgrad: dz");
+  TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N, "fc1_dgrad: w3");
+  TORCH_CHECK(dap.dtype() == at::kFloat && dap.numel() == (int64_t)FB_KQ * B * FC1_K, "fc1_dgrad: dap must be fp32 [4][B][3136]");
+  fc1_bwd_attr();
+  const int Mpad = ((B + 15) >> 4) * 16;
+  // The dz image sits after the 64 W3 rows, so only the rows of this batch need LDS.
+  const int lds = (64 + Mpad) * FB_DSTR * 2;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  fc1_bwd_kernel<<<FB_DGRAD, 256, lds, stream>>>((const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(), nullptr,
+                                                  nullptr, nullptr, dap.data_ptr<float>(), nullptr, nullptr, nullptr,
+                                                  nullptr, nullptr, nullptr, nullptr, B, 0);
 }
 
 }  // namespace mihvd

@@ -7,7 +7,8 @@ allreduce when ``size() > 1``), all hand-written CDNA4 kernels from ``csrc/kerne
     conv2_fwd   implicit GEMM, pool-window-major M, pool/ReLU in registers    [MFMA bf16]
     fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs                    [MFMA bf16]
     head        slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
-    fc1_bwd     dgrad(+pool mask) | wgrad -> fusion buffer | db3 | dW4/db4   [MFMA bf16]
+    fc1_wgrad   dW3 -> fusion buffer | db3 | dW4/db4 (bucket "fc" complete)  [MFMA bf16]
+    fc1_dgrad   split-K dz.W3^T -> fp32 partial slabs (reduced in conv2_bwd) [MFMA bf16]
     --- bucket "fc" (98.4 % of the gradient bytes) is allreduced from here on a side stream ---
     conv2_bwd   dgrad(+pool/ReLU routing) | wgrad slabs | db2                 [MFMA bf16]
     conv1_wgrad dW1/db1 + dW2 slab reduction
@@ -167,17 +168,18 @@ class FusedMNISTTrainer:
         o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
-        o.fc1_bwd(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.h, self.dlog, self.dap,
-                  self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
-                  self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
-                  self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
+        o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
+                    self.gview("dense_1/kernel"), self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
+                    self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
         main = torch.cuda.current_stream(self.device)
         fc_bucket = self.grads[FC_START:]
         conv_bucket = self.grads[:FC_START]
         if self.world > 1:
+            # bucket "fc" is complete: reduce it on the side stream while the conv backward runs
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
                 self._allreduce(fc_bucket, FC_START, FLAT_NUMEL)
+        o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.dap)
         o.conv2_bwd(self.dap, self.a2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1,
                     self.slab, self.gview("conv_layer2/conv2d/bias"))
         o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),

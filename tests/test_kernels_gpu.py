@@ -153,8 +153,9 @@ def test_fc1_bwd(ops, B):
     gb3, gW4, gb4 = torch.empty(1024, device="cuda"), torch.empty(1024, 10, device="cuda"), torch.empty(10, device="cuda")
     gb2, gW1, gb1 = (torch.full((64,), 3.0, device="cuda"), torch.full((800,), 3.0, device="cuda"),
                      torch.full((32,), 3.0, device="cuda"))
-    ops.fc1_bwd(dz.to(torch.bfloat16), w3.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, dap, gW3,
-                gb3, gW4, gb4, gb2, gW1, gb1)
+    ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3, gb3, gW4, gb4, gb2,
+                  gW1, gb1)
+    ops.fc1_dgrad(dz.to(torch.bfloat16), w3.to(torch.bfloat16), dap)
     assert rel_err(dap.sum(0), dz @ w3.t()) < 1e-4
     assert rel_err(gW3, a2.t() @ dz) < 1e-4
     assert rel_err(gb3, dz.sum(0)) < 1e-4
