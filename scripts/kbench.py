@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmark of the fused MNIST step (no profiler): each op is replayed N times
+back to back inside a HIP graph and timed with events, so launch overhead is excluded and the
+number is the kernel's own duration. Usage: python scripts/kbench.py [--iters 200] [--batch 100]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    B = args.batch
+    tr = FusedMNISTTrainer(batch_size=B, seed=0, device="cuda")
+    x = torch.rand(B, 784, device="cuda")
+    y = torch.randint(0, 10, (B,), device="cuda")
+    tr.train_step(x, y)
+    torch.cuda.synchronize()
+    o = tr.ops
+    st = tr.state
+    sh = tr.shadow
+    ops = {
+        "conv1_fwd": lambda: o.conv1_fwd(tr.x_buf, None, st, tr.pview("conv_layer1/conv2d/kernel"),
+                                         tr.pview("conv_layer1/conv2d/bias"), tr.a1, tr.idx1),
+        "conv2_fwd": lambda: o.conv2_fwd(tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh),
+                                         tr.pview("conv_layer2/conv2d/bias"), tr.a2, tr.idx2),
+        "fc1_fwd": lambda: o.fc1_fwd(tr.a2, tr.pview("dense/kernel", sh), tr.zpart),
+        "head": lambda: o.head_fwd_bwd(tr.zpart, tr.pview("dense/bias"), tr.pview("dense_1/kernel"),
+                                       tr.pview("dense_1/bias"), tr.y_buf, None, st, tr.seed, 0.5, tr.h, tr.dz, tr.dlog,
+                                       tr.stats),
+        "fc1_wgrad": lambda: o.fc1_wgrad(tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"),
+                                         tr.gview("dense_1/kernel"), tr.gview("dense_1/bias"),
+                                         tr.gview("conv_layer2/conv2d/bias"), tr.gview("conv_layer1/conv2d/kernel"),
+                                         tr.gview("conv_layer1/conv2d/bias")),
+        "fc1_dgrad": lambda: o.fc1_dgrad(tr.dz, tr.pview("dense/kernel", sh), tr.dap),
+        "conv2_bwd": lambda: o.conv2_bwd(tr.dap, tr.a2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.g1,
+                                         tr.slab, tr.gview("conv_layer2/conv2d/bias")),
+        "conv1_wgrad": lambda: o.conv1_wgrad(tr.x_buf, None, st, tr.g1, tr.idx1, tr.slab,
+                                             tr.gview("conv_layer1/conv2d/kernel"), tr.gview("conv_layer1/conv2d/bias"),
+                                             tr.gview("conv_layer2/conv2d/kernel")),
+        "adam": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, sh, st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
+    }
+    res = {}
+    s = torch.cuda.Stream()
+    for name, fn in ops.items():
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(args.iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = e0.elapsed_time(e1) * 1000.0 / args.iters
+        print(f"{name:12s} {res[name]:8.2f} us", flush=True)
+    # whole step, graph-replayed
+    from mihvd.utils.data import synthetic_mnist
+
+    (xs, ys), _ = synthetic_mnist(n_train=6000, n_test=10)
+    tr.set_device_dataset(torch.from_numpy(xs.reshape(-1, 784)).float().cuda() / 255,
+                          torch.from_numpy(ys.astype("int64")).cuda())
+    tr.build_graph(steps_per_replay=20)
+    for _ in range(3):
+        tr.run_graph()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        tr.run_graph()
+    e1.record()
+    torch.cuda.synchronize()
+    res["step"] = e0.elapsed_time(e1) * 1000.0 / 200
+    res["sum_kernels"] = sum(v for k, v in res.items() if k != "step")
+    print(f"{'step':12s} {res['step']:8.2f} us   (sum of kernels {res['sum_kernels']:.2f} us)", flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
