@@ -22,11 +22,8 @@ typedef unsigned short u16;
 
 #define LDS_PTR(T) __attribute__((address_space(3))) T*
 
-__device__ __forceinline__ u16 f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (inputs are finite)
-  return (u16)(u >> 16);
-}
+// Plain cast: hipcc emits v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN preserved).
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
 __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {

@@ -147,12 +147,10 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
         const bf16x8 w0 = frag_ld128(wr);
         const bf16x8 w1 = frag_ld128(wr + 16 * CB_WSTR);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (i < ntl) {
-            const bf16x8 bx = frag_ld128(D + pbase[i] + aoff + ch * 32);
-            acc[i][0] = mfma16(w0, bx, acc[i][0]);
-            acc[i][1] = mfma16(w1, bx, acc[i][1]);
-          }
+        for (int i = 0; i < 2; ++i) {  // waves 5-7 compute a dummy second tile (no guard on MFMAs)
+          const bf16x8 bx = frag_ld128(D + pbase[i] + aoff + ch * 32);
+          acc[i][0] = mfma16(w0, bx, acc[i][0]);
+          acc[i][1] = mfma16(w1, bx, acc[i][1]);
         }
       }
     }
@@ -209,13 +207,17 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       const bool in = pix < 324 && y >= 0 && y < 14 && x >= 0 && x < 14;
       const int yc = in ? y : 0, xc = in ? x : 0;
       const uint4 v = *reinterpret_cast<const uint4*>(a1 + ((int64_t)bb * 196 + yc * 14 + xc) * 32 + c * 8);
-      av[k] = mask_u4(v, in);
+      av[k] = mask_u4(v, in && active);
     }
     DyItem items[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = min(th + 256 * k, 783);
       items[k] = load_dy_item(dap, a2, idx2, B, bb, (i >> 4) * 64 + (i & 15) * 4);
+      // a missing image (B not a multiple of 4) contributes zeros: mask its ReLU gate to 0
+      const uint32_t m = active ? 0xffffffffu : 0u;
+      items[k].a2.x &= m;
+      items[k].a2.y &= m;
     }
     __syncthreads();  // the previous image's operands are no longer read
 #pragma unroll
@@ -236,26 +238,25 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       }
     }
     __syncthreads();
-    if (active) {
-      for (int k0 = 0; k0 < 224; k0 += 32) {
-        // A' = dY2^T: rows = co (16 per wave), k = pixels
-        const int r0 = min(k0 + 8 * lg + q, 196), r1 = min(k0 + 8 * lg + q + 4, 196);
-        const bf16x8 af = frag_tr(Dm + r0 * CB_WSTR + lw * 16 + 4 * p, Dm + r1 * CB_WSTR + lw * 16 + 4 * p);
-        int poff[2];
+    // (an absent image was staged as zeros, so it is computed unconditionally: no MFMA guard)
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int pix = k0 + 8 * lg + q + 4 * hh;
-          const int y = pix / 14, x = pix - (pix / 14) * 14;
-          poff[hh] = pix < 196 ? ((y + kh) * 18 + x) * 32 : -1;
-        }
+    for (int k0 = 0; k0 < 224; k0 += 32) {
+      // A' = dY2^T: rows = co (16 per wave), k = pixels
+      const int r0 = min(k0 + 8 * lg + q, 196), r1 = min(k0 + 8 * lg + q + 4, 196);
+      const bf16x8 af = frag_tr(Dm + r0 * CB_WSTR + lw * 16 + 4 * p, Dm + r1 * CB_WSTR + lw * 16 + 4 * p);
+      int poff[2], kwm[2];
 #pragma unroll
-        for (int mt = 0; mt < 10; ++mt) {
-          const int kw = mt >> 1, ci0 = (mt & 1) * 16;
-          const int o0 = poff[0] >= 0 ? poff[0] + kw * 32 : 324 * 32;
-          const int o1 = poff[1] >= 0 ? poff[1] + kw * 32 : 324 * 32;
-          const bf16x8 bx = frag_tr(A + o0 + ci0 + 4 * p, A + o1 + ci0 + 4 * p);
-          acc[mt] = mfma16(af, bx, acc[mt]);
-        }
+      for (int hh = 0; hh < 2; ++hh) {
+        const int pix = k0 + 8 * lg + q + 4 * hh;
+        const int y = pix / 14, x = pix - (pix / 14) * 14;
+        poff[hh] = pix < 196 ? ((y + kh) * 18 + x) * 32 : 324 * 32;  // pixel 324 = zeros
+        kwm[hh] = pix < 196 ? 32 : 0;
+      }
+#pragma unroll
+      for (int mt = 0; mt < 10; ++mt) {
+        const int kw = mt >> 1, ci0 = (mt & 1) * 16;
+        const bf16x8 bx = frag_tr(A + poff[0] + kw * kwm[0] + ci0 + 4 * p, A + poff[1] + kw * kwm[1] + ci0 + 4 * p);
+        acc[mt] = mfma16(af, bx, acc[mt]);
       }
     }
   }

@@ -138,7 +138,8 @@ __global__ void __launch_bounds__(256) conv2_fwd_kernel(
     const int y = 2 * (win / 7) + (d >> 1), x = 2 * (win % 7) + (d & 1);
     abase[i] = (y * 18 + x) * 32 + 8 * lg;
   }
-  const int ntiles = (wave == 0) ? 4 : 3;
+  // Every wave computes 4 tiles (tiles 13..15 are dummies on clamped rows, discarded below): no
+  // runtime guard around an MFMA, which would make hipcc shuttle the accumulators.
   const int q = lr >> 2, p = lr & 3;
   for (int kk = 0; kk < 25; ++kk) {  // (kh, kw): 32 input channels = one K step
     const int kh = kk / 5, kw = kk - kh * 5;
@@ -148,17 +149,14 @@ __global__ void __launch_bounds__(256) conv2_fwd_kernel(
     const bf16x8 b1f = frag_tr(wr0 + 16, wr0 + 16 + 4 * C2_WROW);
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      if (i < ntiles) {
-        const bf16x8 a = frag_ld128(img + abase[i] + aoff);
-        acc[i][0] = mfma16(a, b0, acc[i][0]);
-        acc[i][1] = mfma16(a, b1f, acc[i][1]);
-      }
+      const bf16x8 a = frag_ld128(img + abase[i] + aoff);
+      acc[i][0] = mfma16(a, b0, acc[i][0]);
+      acc[i][1] = mfma16(a, b1f, acc[i][1]);
     }
   }
   // Epilogue: lane holds rows 4*lg..4*lg+3 of its tile = one pooling window, column lr.
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    if (i >= ntiles) continue;
     const int tile = wave + 4 * i;
     const int win = tile * 4 + lg;
     if (win >= 49) continue;

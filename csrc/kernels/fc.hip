@@ -29,16 +29,18 @@ constexpr int F1_WSTR = FC1_NT + 8;    // W3 image rows: 72 elements (144 B)
 constexpr int F1_LDS = (MAXB * F1_ASTR + FC1_KSL * F1_WSTR) * 2;
 
 // grid (16, 14): blockIdx.x = 64-column tile, blockIdx.y = K slice. 256 threads = 4 waves.
+// MT = ceil(B/16) sample tiles, a template parameter (no runtime guard around any MFMA).
+template <int MT>
 __global__ void __launch_bounds__(256) fc1_fwd_kernel(const u16* __restrict__ a2, const u16* __restrict__ w3,
                                                       float* __restrict__ zpart, int B) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  u16* As = smem;                     // [Mpad][F1_ASTR]   rows = samples, k contiguous
-  u16* Ws = smem + MAXB * F1_ASTR;    // [224][F1_WSTR]    rows = k, n contiguous
+  constexpr int Mpad = MT * 16;
+  u16* Ws = smem;                     // [224][F1_WSTR]    rows = k, n contiguous
+  u16* As = smem + FC1_KSL * F1_WSTR; // [Mpad][F1_ASTR]   rows = samples, k contiguous
   const int nt = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
-  const int MT = (B + 15) >> 4, Mpad = MT * 16;
   const int k0 = ks * FC1_KSL;
   {
-    TileLoad<256, (MAXB * FC1_KSL / 8 + 255) / 256, FC1_KSL / 8> la;
+    TileLoad<256, (Mpad * FC1_KSL / 8 + 255) / 256, FC1_KSL / 8> la;
     TileLoad<256, (FC1_KSL * FC1_NT / 8 + 255) / 256, FC1_NT / 8> lw;
     lw.load(w3 + (int64_t)k0 * FC1_N + nt * FC1_NT, FC1_N, FC1_KSL, FC1_KSL, t);
     la.load(a2 + k0, FC1_K, Mpad, B, t);
@@ -47,28 +49,26 @@ __global__ void __launch_bounds__(256) fc1_fwd_kernel(const u16* __restrict__ a2
   }
   __syncthreads();
   const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4, q = lr >> 2, p = lr & 3;
-  f32x4 acc[8];
+  f32x4 acc[MT];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kk = 0; kk < FC1_KSL / 32; ++kk) {
     // A = W3^T (rows = features n), read transposed from the [k][n] image.
     const u16* wr = Ws + (kk * 32 + 8 * lg + q) * F1_WSTR + wave * 16 + 4 * p;
     const bf16x8 afr = frag_tr(wr, wr + 4 * F1_WSTR);
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      if (mt < MT) {
-        const bf16x8 bfr = frag_ld128(As + (mt * 16 + lr) * F1_ASTR + kk * 32 + 8 * lg);
-        acc[mt] = mfma16(afr, bfr, acc[mt]);
-      }
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf16x8 bfr = frag_ld128(As + (mt * 16 + lr) * F1_ASTR + kk * 32 + 8 * lg);
+      acc[mt] = mfma16(afr, bfr, acc[mt]);
     }
   }
   float* out = zpart + (int64_t)ks * B * FC1_N;
   const int n = nt * FC1_NT + wave * 16 + 4 * lg;
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
+  for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + lr;
-    if (mt < MT && m < B)
+    if (m < B)
       *reinterpret_cast<float4*>(out + (int64_t)m * FC1_N + n) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
   }
 }
@@ -183,6 +183,9 @@ constexpr int FB_LDS_DG = (MAXB + 64) * FB_DSTR * 2;             // 101,376 B
 constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
 constexpr int FB_LDS = FB_LDS_DG;
 
+// MT (= ceil(B/16) sample tiles) is a template parameter: a runtime guard around an MFMA makes
+// hipcc shuttle every accumulator between AGPRs and VGPRs at each guard (thousands of moves).
+template <int MT>
 __global__ void __launch_bounds__(256) fc1_bwd_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ w3, const u16* __restrict__ a2, const u16* __restrict__ h,
     const float* __restrict__ dlog, float* __restrict__ dap, float* __restrict__ gW3, float* __restrict__ gb3,
@@ -191,7 +194,7 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
-  const int MT = (B + 15) >> 4, Mpad = MT * 16;
+  constexpr int Mpad = MT * 16;
   int bid = blockIdx.x + role_base;
   if (bid < FB_DGRAD) {
     // dAp^T[j][b] = sum_n W3[j][n] dz[b][n] over this block's K quarter.
@@ -200,7 +203,7 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
     u16* Ws = smem;                    // W3   [64][264]    rows = j
     u16* Ds = smem + 64 * FB_DSTR;     // dz   [Mpad][264]  rows = samples
     {
-      TileLoad<256, (MAXB * FB_KQL / 8 + 255) / 256, FB_KQL / 8> ld;
+      TileLoad<256, (Mpad * FB_KQL / 8 + 255) / 256, FB_KQL / 8> ld;
       TileLoad<256, (64 * FB_KQL / 8 + 255) / 256, FB_KQL / 8> lw;
       lw.load(w3 + (int64_t)j0 * FC1_N + n0, FC1_N, 64, 64, t);
       ld.load(dz + n0, FC1_N, Mpad, B, t);
@@ -208,26 +211,24 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
       ld.store(Ds, FB_DSTR, Mpad, t);
     }
     __syncthreads();
-    f32x4 acc[8];
+    f32x4 acc[MT];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < FB_KQL / 32; ++kk) {
       const bf16x8 afr = frag_ld128(Ws + (wave * 16 + lr) * FB_DSTR + kk * 32 + 8 * lg);
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        if (mt < MT) {
-          const bf16x8 bfr = frag_ld128(Ds + (mt * 16 + lr) * FB_DSTR + kk * 32 + 8 * lg);
-          acc[mt] = mfma16(afr, bfr, acc[mt]);
-        }
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8 bfr = frag_ld128(Ds + (mt * 16 + lr) * FB_DSTR + kk * 32 + 8 * lg);
+        acc[mt] = mfma16(afr, bfr, acc[mt]);
       }
     }
     float* out = dap + (int64_t)kq * B * FC1_K;
     const int j = j0 + wave * 16 + 4 * lg;
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+    for (int mt = 0; mt < MT; ++mt) {
       const int m = mt * 16 + lr;
-      if (mt < MT && m < B)
+      if (m < B)
         *reinterpret_cast<float4*>(out + (int64_t)m * FC1_K + j) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
     }
     return;
@@ -332,20 +333,37 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------ //
+#define MIHVD_MT_SWITCH(MTV, ...)                         \
+  switch (MTV) {                                          \
+    case 1: { constexpr int MT_ = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int MT_ = 2; __VA_ARGS__; } break; \
+    case 3: { constexpr int MT_ = 3; __VA_ARGS__; } break; \
+    case 4: { constexpr int MT_ = 4; __VA_ARGS__; } break; \
+    case 5: { constexpr int MT_ = 5; __VA_ARGS__; } break; \
+    case 6: { constexpr int MT_ = 6; __VA_ARGS__; } break; \
+    case 7: { constexpr int MT_ = 7; __VA_ARGS__; } break; \
+    default: { constexpr int MT_ = 8; __VA_ARGS__; } break; \
+  }
+
+template <typename K>
+static void set_max_lds(K kernel, int bytes) {
+  (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
 void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
   const int B = a2.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_fwd: batch must be in [1, 128] (got ", B, ")");
   TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_fwd: a2");
   TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_fwd: w3");
   TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "fc1_fwd: zpart [14][B][1024]");
-  static bool attr = [] {
-    hipFuncSetAttribute((const void*)fc1_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, F1_LDS);
-    return true;
-  }();
-  (void)attr;
+  const int MT = (B + 15) >> 4;
+  const int lds = (FC1_KSL * F1_WSTR + MT * 16 * F1_ASTR) * 2;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  fc1_fwd_kernel<<<dim3(FC1_N / FC1_NT, FC1_KS), 256, F1_LDS, stream>>>((const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(),
-                                                                       zpart.data_ptr<float>(), B);
+  MIHVD_MT_SWITCH(MT, {
+    set_max_lds(fc1_fwd_kernel<MT_>, F1_LDS);
+    fc1_fwd_kernel<MT_><<<dim3(FC1_N / FC1_NT, FC1_KS), 256, lds, stream>>>(
+        (const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(), zpart.data_ptr<float>(), B);
+  })
 }
 
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
@@ -373,17 +391,9 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
 }
 
 // Two launches of one kernel so each gets its own LDS budget: the weight-gradient roles (37 KB:
-// several blocks per CU) and the dgrad split-K role ((Mpad + 64) x 528 B: one block per CU).
-// The wgrad launch completes the whole "fc" gradient bucket, so its allreduce can start while
-// dgrad and the conv backward still run.
-static void fc1_bwd_attr() {
-  static bool attr = [] {
-    hipFuncSetAttribute((const void*)fc1_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, FB_LDS);
-    return true;
-  }();
-  (void)attr;
-}
-
+// several blocks per CU) and the dgrad split-K role ((Mpad + 64) x 528 B). The wgrad launch
+// completes the whole "fc" gradient bucket, so its allreduce can start while dgrad and the conv
+// backward still run.
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1) {
   const int B = dz.size(0);
@@ -394,9 +404,8 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_wgrad: gW3");
   TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_wgrad: fc grads");
   TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "fc1_wgrad: conv grads");
-  fc1_bwd_attr();
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  fc1_bwd_kernel<<<FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC, 256, FB_LDS_WG, stream>>>(
+  fc1_bwd_kernel<1><<<FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC, 256, FB_LDS_WG, stream>>>(
       (const u16*)dz.data_ptr(), nullptr, (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
       nullptr, gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(),
       gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, FB_DGRAD);
@@ -408,14 +417,16 @@ void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, at::Tensor& dap) {
   TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_dgrad: dz");
   TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N, "fc1_dgrad: w3");
   TORCH_CHECK(dap.dtype() == at::kFloat && dap.numel() == (int64_t)FB_KQ * B * FC1_K, "fc1_dgrad: dap must be fp32 [4][B][3136]");
-  fc1_bwd_attr();
-  const int Mpad = ((B + 15) >> 4) * 16;
+  const int MT = (B + 15) >> 4;
   // The dz image sits after the 64 W3 rows, so only the rows of this batch need LDS.
-  const int lds = (64 + Mpad) * FB_DSTR * 2;
+  const int lds = (64 + MT * 16) * FB_DSTR * 2;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  fc1_bwd_kernel<<<FB_DGRAD, 256, lds, stream>>>((const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(), nullptr,
-                                                  nullptr, nullptr, dap.data_ptr<float>(), nullptr, nullptr, nullptr,
-                                                  nullptr, nullptr, nullptr, nullptr, B, 0);
+  MIHVD_MT_SWITCH(MT, {
+    set_max_lds(fc1_bwd_kernel<MT_>, FB_LDS);
+    fc1_bwd_kernel<MT_><<<FB_DGRAD, 256, lds, stream>>>((const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(), nullptr,
+                                                        nullptr, nullptr, dap.data_ptr<float>(), nullptr, nullptr,
+                                                        nullptr, nullptr, nullptr, nullptr, nullptr, B, 0);
+  })
 }
 
 }  // namespace mihvd

@@ -28,6 +28,7 @@ tensorflow_mnist_gpu.py:26-28; no loss scaling is needed for bf16).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -54,7 +55,7 @@ FC_START = SEGMENTS["dense/kernel"][0]  # bucket "fc" = [dense/kernel .. dense_1
 class FusedMNISTTrainer:
     def __init__(self, batch_size: int = 100, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  dropout: float = 0.5, seed: int = 0, device=None, compression: str = "none", op=None,
-                 adam_rule: str = "tf", dropout_seed: int | None = None):
+                 adam_rule: str = "tf", dropout_seed: int | None = None, world_size: int | None = None):
         _native.require_kernels()
         from .. import basics
 
@@ -72,7 +73,11 @@ class FusedMNISTTrainer:
         self.dropout = dropout
         self.rule = 0 if adam_rule == "tf" else 1
         self.seed = int(dropout_seed if dropout_seed is not None else (seed * 7919 + 17)) & 0x7FFFFFFF
-        self.world = basics.size() if basics.is_initialized() else 1
+        if world_size is None:
+            world_size = basics.size() if basics.is_initialized() else 1
+        self.world = int(world_size)
+        # MIHVD_FORCE_COLLECTIVES=1 keeps the allreduce path even at size 1 (tests of the RCCL path)
+        self.collectives = self.world > 1 or os.environ.get("MIHVD_FORCE_COLLECTIVES") == "1"
         self.rank = basics.rank() if basics.is_initialized() else 0
         self.op = op
         self.compression = compression
@@ -107,8 +112,8 @@ class FusedMNISTTrainer:
         self.X = self.Y = self.rows = None
         self.graph = None
         self.steps_per_replay = 1
-        self._side = torch.cuda.Stream(device=dev) if self.world > 1 else None
-        if compression == "bf16" and self.world > 1:
+        self._side = torch.cuda.Stream(device=dev) if self.collectives else None
+        if compression == "bf16" and self.collectives:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
         else:
             self.wire = None
@@ -174,7 +179,7 @@ class FusedMNISTTrainer:
         main = torch.cuda.current_stream(self.device)
         fc_bucket = self.grads[FC_START:]
         conv_bucket = self.grads[:FC_START]
-        if self.world > 1:
+        if self.collectives:
             # bucket "fc" is complete: reduce it on the side stream while the conv backward runs
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
@@ -184,7 +189,7 @@ class FusedMNISTTrainer:
                     self.slab, self.gview("conv_layer2/conv2d/bias"))
         o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),
                       self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/kernel"))
-        if self.world > 1:
+        if self.collectives:
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
                 self._allreduce(conv_bucket, 0, FC_START)

@@ -1,0 +1,76 @@
+"""GPU multi-process scenarios for the fused trainer (launched by tests/test_fused_distributed_gpu.py).
+
+usage: python fused_worker.py <scenario> <outdir>
+  rccl_graph : world 1 over RCCL with MIHVD_FORCE_COLLECTIVES=1 — the allreduce is captured in the
+               HIP graph; results must equal a trainer without collectives.
+  dp_gloo    : 2 ranks (gloo, both on cuda:0), B=50 each == one trainer with B=100 (dropout off).
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import mihvd.torch as hvd  # noqa: E402
+from mihvd.models.fused_mnist import FusedMNISTTrainer  # noqa: E402
+from mihvd.utils.data import synthetic_mnist  # noqa: E402
+
+
+def data(n, seed=3):
+    (x, y), _ = synthetic_mnist(n_train=n, n_test=10, seed=seed)
+    return torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0, torch.from_numpy(y.astype("int64")).cuda()
+
+
+def sc_rccl_graph(outdir):
+    X, Y = data(2000)
+    a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda")
+    assert a.collectives, "MIHVD_FORCE_COLLECTIVES should enable the allreduce path"
+    a.set_device_dataset(X, Y, seed=4)
+    captured = a.build_graph(steps_per_replay=5)
+    for _ in range(4):
+        a.run_graph()
+    os.environ["MIHVD_FORCE_COLLECTIVES"] = "0"
+    b = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda")
+    b.set_device_dataset(X, Y, seed=4)
+    b.build_graph(steps_per_replay=5)
+    for _ in range(4):
+        b.run_graph()
+    torch.cuda.synchronize()
+    diff = (a.params - b.params).abs().max().item()
+    with open(os.path.join(outdir, "rccl_graph.json"), "w") as f:
+        json.dump({"captured": captured, "diff": diff, "steps": a.global_step, "loss": a.last_loss()}, f)
+
+
+def sc_dp_gloo(outdir):
+    r = hvd.rank()
+    X, Y = data(600)
+    tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda")
+    tr.broadcast(0)
+    for step in range(3):
+        xb = X[step * 100:(step + 1) * 100]
+        yb = Y[step * 100:(step + 1) * 100]
+        tr.train_step(xb[r * 50:(r + 1) * 50], yb[r * 50:(r + 1) * 50])
+    torch.cuda.synchronize()
+    ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", world_size=1)
+    for step in range(3):
+        ref.train_step(X[step * 100:(step + 1) * 100], Y[step * 100:(step + 1) * 100])
+    torch.cuda.synchronize()
+    rel = ((tr.params - ref.params).norm() / ref.params.norm()).item()
+    mx = (tr.params - ref.params).abs().max().item()
+    spread = hvd.allgather(tr.params[:4096].cpu().view(1, -1))
+    with open(os.path.join(outdir, f"dp_gloo.{r}.json"), "w") as f:
+        json.dump({"rel": rel, "max": mx, "rank_spread": (spread - spread[0]).abs().max().item()}, f)
+
+
+def main():
+    scenario, outdir = sys.argv[1], sys.argv[2]
+    hvd.init()
+    globals()["sc_" + scenario](outdir)
+    hvd.shutdown()
+
+
+if __name__ == "__main__":
+    main()
