@@ -23,7 +23,7 @@ void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, con
                  at::Tensor& gW2);
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
-               double grad_scale, int64_t rule);
+               double grad_scale, int64_t rule, int64_t bump);
 void scale_cast_bf16(const at::Tensor& src, at::Tensor& dst, double scale);
 void bf16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale);
 }  // namespace mihvd
@@ -58,8 +58,8 @@ void conv1_wgrad_op(const Tensor& x, const OptT& rows, const OptT& state, const 
   mihvd::conv1_wgrad(x, rows, state, g1, idx1, slab, gW1, gb1, gW2);
 }
 void adam_op(Tensor p, const Tensor& g, Tensor m, Tensor v, const OptT& shadow, const OptT& state, int64_t host_step,
-             double lr, double b1, double b2, double eps, double grad_scale, int64_t rule) {
-  mihvd::adam_step(p, g, m, v, shadow, state, host_step, lr, b1, b2, eps, grad_scale, rule);
+             double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, int64_t bump) {
+  mihvd::adam_step(p, g, m, v, shadow, state, host_step, lr, b1, b2, eps, grad_scale, rule, bump);
 }
 void scale_cast_op(const Tensor& src, Tensor dst, double scale) { mihvd::scale_cast_bf16(src, dst, scale); }
 void bf16_to_f32_op(const Tensor& src, Tensor dst, double scale) { mihvd::bf16_to_f32(src, dst, scale); }
@@ -80,7 +80,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("conv1_wgrad(Tensor x, Tensor? rows, Tensor? state, Tensor g1, Tensor idx1, Tensor slab, Tensor(a!) gW1, "
         "Tensor(b!) gb1, Tensor(c!) gW2) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
-        "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule) -> ()");
+        "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
 }

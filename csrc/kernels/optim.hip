@@ -17,7 +17,7 @@ namespace mihvd {
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, u16* __restrict__ shadow,
                                                    int64_t n4, int64_t* __restrict__ state, int64_t host_t, float lr,
-                                                   float b1, float b2, float eps, float gscale, int rule) {
+                                                   float b1, float b2, float eps, float gscale, int rule, int bump) {
   const float t = (float)(state ? state[ST_OPT] : host_t);
   const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
   // rule 0: TF1 (eps outside the bias-corrected sqrt); rule 1: torch.optim.Adam
@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const 
       reinterpret_cast<uint2*>(shadow)[i] = make_uint2((uint32_t)sh[0] | ((uint32_t)sh[1] << 16),
                                                        (uint32_t)sh[2] | ((uint32_t)sh[3] << 16));
   }
-  if (state && blockIdx.x == 0 && threadIdx.x == 0) state[ST_FWD] += 1;
+  if (bump && state && blockIdx.x == 0 && threadIdx.x == 0) state[ST_FWD] += 1;
 }
 
 __global__ void __launch_bounds__(256) scale_cast_kernel(const float* __restrict__ src, u16* __restrict__ dst, int64_t n4,
@@ -77,7 +77,7 @@ static int grid_for(int64_t n4) {
 
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
-               double grad_scale, int64_t rule) {
+               double grad_scale, int64_t rule, int64_t bump) {
   const int64_t n = p.numel();
   TORCH_CHECK(p.dtype() == at::kFloat && g.dtype() == at::kFloat && m.dtype() == at::kFloat && v.dtype() == at::kFloat,
               "adam_step: fp32 buffers expected");
@@ -94,7 +94,7 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
   auto stream = c10::hip::getCurrentHIPStream().stream();
   adam_kernel<<<grid_for(n / 4), 256, 0, stream>>>(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                                                    v.data_ptr<float>(), sp, n / 4, st, host_step, (float)lr, (float)b1,
-                                                   (float)b2, (float)eps, (float)grad_scale, (int)rule);
+                                                   (float)b2, (float)eps, (float)grad_scale, (int)rule, (int)bump);
 }
 
 void scale_cast_bf16(const at::Tensor& src, at::Tensor& dst, double scale) {

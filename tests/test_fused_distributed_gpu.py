@@ -30,7 +30,7 @@ def test_rccl_allreduce_inside_hip_graph(tmp_path):
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     r = json.loads((tmp_path / "rccl_graph.json").read_text())
     assert r["captured"], "RCCL allreduce could not be captured into the HIP graph"
-    assert r["steps"] == 22 and r["diff"] == 0.0
+    assert r["steps"] == 22 and r["rel_update_diff"] < 0.05, r
 
 
 def test_fused_data_parallel_equivalence_two_ranks(tmp_path):
@@ -42,4 +42,5 @@ def test_fused_data_parallel_equivalence_two_ranks(tmp_path):
     for r in range(2):
         o = json.loads((tmp_path / f"dp_gloo.{r}.json").read_text())
         assert o["rank_spread"] == 0.0
-        assert o["rel"] < 1e-4, o
+        assert o["grad_rel"] < 1e-4, o
+        assert o["rel_update_diff"] < 0.05, o

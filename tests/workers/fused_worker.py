@@ -29,6 +29,7 @@ def sc_rccl_graph(outdir):
     a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda")
     assert a.collectives, "MIHVD_FORCE_COLLECTIVES should enable the allreduce path"
     a.set_device_dataset(X, Y, seed=4)
+    p0 = a.params.clone()
     captured = a.build_graph(steps_per_replay=5)
     for _ in range(4):
         a.run_graph()
@@ -39,9 +40,12 @@ def sc_rccl_graph(outdir):
     for _ in range(4):
         b.run_graph()
     torch.cuda.synchronize()
-    diff = (a.params - b.params).abs().max().item()
+    # conv1's weight gradient is accumulated with float atomics (order-dependent in the last bits),
+    # so compare the parameter *updates* in norm rather than bitwise.
+    rel = ((a.params - b.params).norm() / (b.params - p0).norm()).item()
     with open(os.path.join(outdir, "rccl_graph.json"), "w") as f:
-        json.dump({"captured": captured, "diff": diff, "steps": a.global_step, "loss": a.last_loss()}, f)
+        json.dump({"captured": captured, "rel_update_diff": rel, "steps": a.global_step, "loss": a.last_loss(),
+                   "loss_ref": b.last_loss()}, f)
 
 
 def sc_dp_gloo(outdir):
@@ -49,20 +53,24 @@ def sc_dp_gloo(outdir):
     X, Y = data(600)
     tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda")
     tr.broadcast(0)
+    ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", world_size=1)
+    p0 = ref.params.clone()
+    grel = None
     for step in range(3):
         xb = X[step * 100:(step + 1) * 100]
         yb = Y[step * 100:(step + 1) * 100]
         tr.train_step(xb[r * 50:(r + 1) * 50], yb[r * 50:(r + 1) * 50])
-    torch.cuda.synchronize()
-    ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", world_size=1)
-    for step in range(3):
-        ref.train_step(X[step * 100:(step + 1) * 100], Y[step * 100:(step + 1) * 100])
-    torch.cuda.synchronize()
-    rel = ((tr.params - ref.params).norm() / ref.params.norm()).item()
+        ref.train_step(xb, yb)
+        torch.cuda.synchronize()
+        if step == 0:
+            # allreduced SUM of the two per-rank batch means == 2 x the 100-sample batch mean
+            grel = ((tr.grads / 2 - ref.grads).norm() / ref.grads.norm()).item()
+    rel = ((tr.params - ref.params).norm() / (ref.params - p0).norm()).item()
     mx = (tr.params - ref.params).abs().max().item()
     spread = hvd.allgather(tr.params[:4096].cpu().view(1, -1))
     with open(os.path.join(outdir, f"dp_gloo.{r}.json"), "w") as f:
-        json.dump({"rel": rel, "max": mx, "rank_spread": (spread - spread[0]).abs().max().item()}, f)
+        json.dump({"grad_rel": grel, "rel_update_diff": rel, "max": mx,
+                   "rank_spread": (spread - spread[0]).abs().max().item()}, f)
 
 
 def main():
