@@ -34,34 +34,26 @@ constexpr int CB_WG_LDS = 2 * CB_WG_GRP * 2;                       // 98,336 B
 constexpr int CB_LDS = CB_DG_LDS > CB_WG_LDS ? CB_DG_LDS : CB_WG_LDS;
 
 struct DyItem {
-  float4 s[CB_KQ];
-  uint2 a2;
-  uint32_t idx;
+  uint2 g;       // 4 bf16 pooled gradients (already masked by conv2's pooled ReLU)
+  uint32_t idx;  // 4 argmax slots
 };
 
 // Loads for one dY2 build item: 4 consecutive channels of one pooling window of image b.
-__device__ __forceinline__ DyItem load_dy_item(const float* __restrict__ dap, const u16* __restrict__ a2,
-                                               const uint8_t* __restrict__ idx2, int B, int b, int e) {
+__device__ __forceinline__ DyItem load_dy_item(const u16* __restrict__ g2, const uint8_t* __restrict__ idx2, int b,
+                                               int e) {
   DyItem it;
-#pragma unroll
-  for (int k = 0; k < CB_KQ; ++k)
-    it.s[k] = *reinterpret_cast<const float4*>(dap + ((int64_t)k * B + b) * 3136 + e);
-  it.a2 = *reinterpret_cast<const uint2*>(a2 + (int64_t)b * 3136 + e);
+  it.g = *reinterpret_cast<const uint2*>(g2 + (int64_t)b * 3136 + e);
   it.idx = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)b * 3136 + e);
   return it;
 }
 
-// Reduce + mask an item: g[c] is the bf16 gradient of channel c, d[c] its argmax slot.
 __device__ __forceinline__ void finish_dy_item(const DyItem& it, u16 g[4], int d[4], float gf[4]) {
-  const float sx = it.s[0].x + it.s[1].x + it.s[2].x + it.s[3].x;
-  const float sy = it.s[0].y + it.s[1].y + it.s[2].y + it.s[3].y;
-  const float sz = it.s[0].z + it.s[1].z + it.s[2].z + it.s[3].z;
-  const float sw = it.s[0].w + it.s[1].w + it.s[2].w + it.s[3].w;
-  const float s[4] = {sx, sy, sz, sw};
-  const u16 av[4] = {(u16)(it.a2.x & 0xffff), (u16)(it.a2.x >> 16), (u16)(it.a2.y & 0xffff), (u16)(it.a2.y >> 16)};
+  g[0] = (u16)(it.g.x & 0xffff);
+  g[1] = (u16)(it.g.x >> 16);
+  g[2] = (u16)(it.g.y & 0xffff);
+  g[3] = (u16)(it.g.y >> 16);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    g[c] = bf2f(av[c]) > 0.f ? f2bf(s[c]) : (u16)0;
     gf[c] = bf2f(g[c]);
     d[c] = (it.idx >> (8 * c)) & 3;
   }
@@ -82,7 +74,7 @@ __device__ __forceinline__ void scatter_window(u16* img, int pix_stride, int win
 }
 
 __global__ void __launch_bounds__(512) conv2_bwd_kernel(
-    const float* __restrict__ dap, const u16* __restrict__ a2, const uint8_t* __restrict__ idx2,
+    const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, u16* __restrict__ g1, float* __restrict__ slab,
     float* __restrict__ gb2, int B, int n_dgrad) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
@@ -100,7 +92,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     for (int k = 0; k < 2; ++k) {
       const int i = min(t + 512 * k, 783);
       ie[k] = t + 512 * k;
-      items[k] = load_dy_item(dap, a2, idx2, B, b, (i >> 4) * 64 + (i & 15) * 4);
+      items[k] = load_dy_item(g2, idx2, b, (i >> 4) * 64 + (i & 15) * 4);
     }
     TileLoad<512, 13, 8> lw;
     lw.load(w2bf, 64, 800, 800, t);
@@ -213,11 +205,11 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = min(th + 256 * k, 783);
-      items[k] = load_dy_item(dap, a2, idx2, B, bb, (i >> 4) * 64 + (i & 15) * 4);
-      // a missing image (B not a multiple of 4) contributes zeros: mask its ReLU gate to 0
+      items[k] = load_dy_item(g2, idx2, bb, (i >> 4) * 64 + (i & 15) * 4);
+      // a missing image (B not a multiple of 4) contributes zeros
       const uint32_t m = active ? 0xffffffffu : 0u;
-      items[k].a2.x &= m;
-      items[k].a2.y &= m;
+      items[k].g.x &= m;
+      items[k].g.y &= m;
     }
     __syncthreads();  // the previous image's operands are no longer read
 #pragma unroll
@@ -297,20 +289,28 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
   __shared__ float red[8][26][32];
   const int t = threadIdx.x;
   if ((int)blockIdx.x >= B) {
-    const int i = ((int)blockIdx.x - B) * 256 + t;  // float4 index, 12800 total
-    if (i < 51200 / 4) {
-      // all (<= 32) slab loads in flight at once; absent slabs are masked, not branched around
-      float4 v[32];
+    // dW2 = sum of the (<= 32) wgrad slabs. Block = 64 float4 outputs x 4 slab groups of 8, every
+    // load in flight at once (absent slabs masked, not branched around), then a 4-way LDS sum.
+    const int o = ((int)blockIdx.x - B) * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
+    float4 v[8];
 #pragma unroll
-      for (int g = 0; g < 32; ++g) {
-        const float4 x = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[i];
-        const bool k = g < nslab;
-        v[g] = make_float4(mask_f(x.x, k), mask_f(x.y, k), mask_f(x.z, k), mask_f(x.w, k));
-      }
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < 8; ++k) {
+      const int g = sg * 8 + k;
+      const float4 x = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[min(o, 12799)];
+      const bool keep = g < nslab;
+      v[k] = make_float4(mask_f(x.x, keep), mask_f(x.y, keep), mask_f(x.z, keep), mask_f(x.w, keep));
+    }
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int g = 0; g < 32; ++g) { s.x += v[g].x; s.y += v[g].y; s.z += v[g].z; s.w += v[g].w; }
-      reinterpret_cast<float4*>(gW2)[i] = s;
+    for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
+    float4* r4 = reinterpret_cast<float4*>(&red[0][0][0]);
+    r4[t] = s;
+    __syncthreads();
+    if (t < 64 && o < 12800) {
+      const float4 a = r4[t], b = r4[64 + t], c = r4[128 + t], d = r4[192 + t];
+      reinterpret_cast<float4*>(gW2)[o] =
+          make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                      (a.w + b.w) + (c.w + d.w));
     }
     return;
   }
@@ -380,12 +380,11 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
 // ------------------------------------------------------------------------------------------ //
 int64_t conv2_wgrad_groups(int64_t B) { return (B + CB_IPB - 1) / CB_IPB; }
 
-void conv2_bwd(const at::Tensor& dap, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a1,
-               const at::Tensor& w2bf, at::Tensor& g1, at::Tensor& slab, at::Tensor& gb2) {
+void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf, at::Tensor& g1,
+               at::Tensor& slab, at::Tensor& gb2) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
-  TORCH_CHECK(dap.dtype() == at::kFloat && dap.numel() == (int64_t)CB_KQ * B * 3136, "conv2_bwd: dap [4][B][3136] fp32");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * 3136 && idx2.numel() == a2.numel(), "conv2_bwd: a2/idx2");
+  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
   TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && g1.numel() == a1.numel(), "conv2_bwd: a1/g1");
   TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200, "conv2_bwd: w2");
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_bwd: slab must hold ceil(B/4) x 51200");
@@ -397,7 +396,7 @@ void conv2_bwd(const at::Tensor& dap, const at::Tensor& a2, const at::Tensor& id
   (void)attr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   conv2_bwd_kernel<<<B + 5 * G, 512, CB_LDS, stream>>>(
-      dap.data_ptr<float>(), (const u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(),
+      (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(),
       (const u16*)w2bf.data_ptr(), (u16*)g1.data_ptr(), slab.data_ptr<float>(), gb2.data_ptr<float>(), B, B);
 }
 
@@ -415,7 +414,8 @@ void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, con
   if (rows.has_value() && rows->defined()) rp = rows->data_ptr<int>();
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv1_wgrad_kernel<<<B + 50, 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (const u16*)g1.data_ptr(),
+  TORCH_CHECK(G <= 32, "conv1_wgrad: at most 32 wgrad slabs");
+  conv1_wgrad_kernel<<<B + 200, 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (const u16*)g1.data_ptr(),
                                                  idx1.data_ptr<uint8_t>(), slab.data_ptr<float>(), G, gW1.data_ptr<float>(),
                                                  gb1.data_ptr<float>(), gW2.data_ptr<float>(), B);
 }

@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(256) head_kernel(
 constexpr int FB_KQ = 4, FB_KQL = FC1_N / FB_KQ;                 // 256
 constexpr int FB_DGRAD = (FC1_K / 64) * FB_KQ;                   // 196
 constexpr int FB_WGRAD = (FC1_K / 64) * (FC1_N / 64);            // 784
-constexpr int FB_DB3 = 4, FB_DW4 = 4, FB_MISC = 1;
+constexpr int FB_DB3 = FC1_N / 64, FB_DW4 = FC1_N / 64, FB_MISC = 1;  // 16 + 16 + 1 blocks
 constexpr int FB_TOTAL = FB_DGRAD + FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC;
 constexpr int FB_DSTR = FB_KQL + 8;                              // 264 elements (528 B)
 constexpr int FB_TSTR = 64 + 8;                                  // 72 elements
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ w3, const u16* __restrict__ a2, const u16* __restrict__ h,
     const float* __restrict__ dlog, float* __restrict__ dap, float* __restrict__ gW3, float* __restrict__ gb3,
     float* __restrict__ gW4, float* __restrict__ gb4, float* __restrict__ gb2, float* __restrict__ gW1,
-    float* __restrict__ gb1, int B, int role_base) {
+    float* __restrict__ gb1, u16* __restrict__ g2, int* __restrict__ cnt, int B, int role_base) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
@@ -230,6 +230,55 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
       const int m = mt * 16 + lr;
       if (m < B)
         *reinterpret_cast<float4*>(out + (int64_t)m * FC1_K + j) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
+    }
+    // In-launch split-K combine (cdna_hip_programming.md §6 Guideline 16, counter form): every
+    // storing wave drains, the block releases at agent scope and takes a ticket; the fourth
+    // arriver of this column tile acquires, sums the four fp32 slabs, applies conv2's pooled-ReLU
+    // mask (a2 > 0) and writes g2 in bf16. Correct for any placement of the four blocks.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);  // the one LDS array (no second __shared__ object)
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(cnt + jt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = (ticket == FB_KQ - 1);
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cnt[jt] = 0;  // re-arm for the next launch (the buffer is zeroed once at allocation)
+    }
+    __syncthreads();
+    // thread -> (row m, 4 columns): 16 float4 per row of the tile, B rows
+    constexpr int IT = (MT * 16 * 16 + 255) / 256;
+    float4 part[IT][FB_KQ];
+    uint2 mk[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int e = min(t + 256 * it, B * 16 - 1);
+      const int m = e >> 4, c4 = (e & 15) * 4;
+#pragma unroll
+      for (int k = 0; k < FB_KQ; ++k)
+        part[it][k] = *reinterpret_cast<const float4*>(dap + ((int64_t)k * B + m) * FC1_K + j0 + c4);
+      mk[it] = *reinterpret_cast<const uint2*>(a2 + (int64_t)m * FC1_K + j0 + c4);
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int e = t + 256 * it;
+      if (e >= B * 16) continue;
+      const int m = e >> 4, c4 = (e & 15) * 4;
+      float s[4];
+      s[0] = (part[it][0].x + part[it][1].x) + (part[it][2].x + part[it][3].x);
+      s[1] = (part[it][0].y + part[it][1].y) + (part[it][2].y + part[it][3].y);
+      s[2] = (part[it][0].z + part[it][1].z) + (part[it][2].z + part[it][3].z);
+      s[3] = (part[it][0].w + part[it][1].w) + (part[it][2].w + part[it][3].w);
+      const u16 av[4] = {(u16)(mk[it].x & 0xffff), (u16)(mk[it].x >> 16), (u16)(mk[it].y & 0xffff), (u16)(mk[it].y >> 16)};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[c] = bf2f(av[c]) > 0.f ? s[c] : 0.f;
+      *reinterpret_cast<uint2*>(g2 + (int64_t)m * FC1_K + j0 + c4) = pack4bf(s[0], s[1], s[2], s[3]);
     }
     return;
   }
@@ -279,57 +328,84 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(
     return;
   }
   bid -= FB_WGRAD;
+  // Small reductions over the batch: thread = (feature n in a 64-wide tile, row group rg of 32
+  // samples); every row load of a thread is issued at once (masked past B), then a 4-way LDS sum.
+  const int nn = t & 63, rg = t >> 6;
   if (bid < FB_DB3) {
-    const int n = bid * 256 + t;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int b = 0;
-    for (; b + 4 <= B; b += 4) {
-      s0 += bf2f(dz[(int64_t)(b + 0) * FC1_N + n]);
-      s1 += bf2f(dz[(int64_t)(b + 1) * FC1_N + n]);
-      s2 += bf2f(dz[(int64_t)(b + 2) * FC1_N + n]);
-      s3 += bf2f(dz[(int64_t)(b + 3) * FC1_N + n]);
+    const int n = bid * 64 + nn;
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int b = rg * 32 + i;
+      v[i] = mask_f(bf2f(dz[(int64_t)min(b, B - 1) * FC1_N + n]), b < B);
     }
-    for (; b < B; ++b) s0 += bf2f(dz[(int64_t)b * FC1_N + n]);
-    gb3[n] = (s0 + s1) + (s2 + s3);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) s += v[i];
+    float* red = reinterpret_cast<float*>(smem);
+    red[rg * 64 + nn] = s;
+    __syncthreads();
+    if (t < 64) gb3[n] = (red[nn] + red[64 + nn]) + (red[128 + nn] + red[192 + nn]);
     return;
   }
   bid -= FB_DB3;
   if (bid < FB_DW4) {
     float* dls = reinterpret_cast<float*>(smem);  // [B][10]
+    float* red = dls + MAXB * 10;                  // [4][64][10]
+    const int n = bid * 64 + nn;
+    float hv[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int b = rg * 32 + i;
+      hv[i] = mask_f(bf2f(h[(int64_t)min(b, B - 1) * FC1_N + n]), b < B);
+    }
     for (int i = t; i < B * 10; i += 256) dls[i] = dlog[i];
+    for (int i = B * 10 + t; i < MAXB * 10; i += 256) dls[i] = 0.f;
     __syncthreads();
-    const int n = bid * 256 + t;
     float s[10];
 #pragma unroll
     for (int c = 0; c < 10; ++c) s[c] = 0.f;
-    int b = 0;
-    for (; b + 4 <= B; b += 4) {
-      float hv[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) hv[u] = bf2f(h[(int64_t)(b + u) * FC1_N + n]);
+    for (int i = 0; i < 32; ++i)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int c = 0; c < 10; ++c) s[c] = fmaf(hv[i], dls[(rg * 32 + i) * 10 + c], s[c]);
 #pragma unroll
-        for (int c = 0; c < 10; ++c) s[c] = fmaf(hv[u], dls[(b + u) * 10 + c], s[c]);
+    for (int c = 0; c < 10; ++c) red[(rg * 64 + nn) * 10 + c] = s[c];
+    __syncthreads();
+    for (int i = t; i < 640; i += 256) {
+      const int n2 = i / 10, c = i - n2 * 10;
+      gW4[(bid * 64 + n2) * 10 + c] = (red[n2 * 10 + c] + red[(64 + n2) * 10 + c]) +
+                                      (red[(128 + n2) * 10 + c] + red[(192 + n2) * 10 + c]);
     }
-    for (; b < B; ++b) {
-      const float hv = bf2f(h[(int64_t)b * FC1_N + n]);
-#pragma unroll
-      for (int c = 0; c < 10; ++c) s[c] = fmaf(hv, dls[b * 10 + c], s[c]);
-    }
-#pragma unroll
-    for (int c = 0; c < 10; ++c) gW4[n * 10 + c] = s[c];
     return;
   }
-  // misc: db4, and zero the gradients that conv2_bwd / conv1_wgrad accumulate with atomics
-  if (t < 10) {
+  // misc: db4 (thread = class c, row group), and zero the gradients that conv2_bwd / conv1_wgrad
+  // accumulate with atomics
+  {
+    float* red = reinterpret_cast<float*>(smem);
+    const int c = t % 10, g = t / 10;  // 25 groups x 10 classes = 250 threads
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dlog[b * 10 + t];
-    gb4[t] = s;
+    if (g < 25) {
+      float v[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int b = g * 6 + i;  // 25 x 6 = 150 >= MAXB rows
+        v[i] = mask_f(dlog[min(b, B - 1) * 10 + c], b < B);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) s += v[i];
+    }
+    red[t] = s;
+    if (t < 64) gb2[t] = 0.f;
+    if (t < 32) gb1[t] = 0.f;
+    for (int i = t; i < 800; i += 256) gW1[i] = 0.f;
+    __syncthreads();
+    if (t < 10) {
+      float tot = 0.f;
+      for (int gg = 0; gg < 25; ++gg) tot += red[gg * 10 + t];
+      gb4[t] = tot;
+    }
   }
-  if (t < 64) gb2[t] = 0.f;
-  if (t < 32) gb1[t] = 0.f;
-  for (int i = t; i < 800; i += 256) gW1[i] = 0.f;
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -408,24 +484,32 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   fc1_bwd_kernel<1><<<FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC, 256, FB_LDS_WG, stream>>>(
       (const u16*)dz.data_ptr(), nullptr, (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
       nullptr, gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(),
-      gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, FB_DGRAD);
+      gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), nullptr, nullptr, B, FB_DGRAD);
 }
 
-void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, at::Tensor& dap) {
+// dgrad: split-K partials into `dap` (workspace), combined in-launch into g2 = (a2 > 0) * dz.W3^T
+// (bf16). `cnt` holds one arrival counter per 64-column tile (49 ints, zero at allocation; the
+// combining block re-arms it).
+void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& dap, at::Tensor& g2,
+               at::Tensor& cnt) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_dgrad: batch");
   TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_dgrad: dz");
   TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N, "fc1_dgrad: w3");
+  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K, "fc1_dgrad: a2");
+  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * FC1_K, "fc1_dgrad: g2");
   TORCH_CHECK(dap.dtype() == at::kFloat && dap.numel() == (int64_t)FB_KQ * B * FC1_K, "fc1_dgrad: dap must be fp32 [4][B][3136]");
+  TORCH_CHECK(cnt.dtype() == at::kInt && cnt.numel() >= FC1_K / 64, "fc1_dgrad: cnt must be int32 [>=49]");
   const int MT = (B + 15) >> 4;
   // The dz image sits after the 64 W3 rows, so only the rows of this batch need LDS.
   const int lds = (64 + MT * 16) * FB_DSTR * 2;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   MIHVD_MT_SWITCH(MT, {
     set_max_lds(fc1_bwd_kernel<MT_>, FB_LDS);
-    fc1_bwd_kernel<MT_><<<FB_DGRAD, 256, lds, stream>>>((const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(), nullptr,
-                                                        nullptr, nullptr, dap.data_ptr<float>(), nullptr, nullptr,
-                                                        nullptr, nullptr, nullptr, nullptr, nullptr, B, 0);
+    fc1_bwd_kernel<MT_><<<FB_DGRAD, 256, lds, stream>>>(
+        (const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(), (const u16*)a2.data_ptr(), nullptr, nullptr,
+        dap.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, (u16*)g2.data_ptr(),
+        cnt.data_ptr<int>(), B, 0);
   })
 }
 

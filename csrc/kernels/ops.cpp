@@ -14,10 +14,11 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1);
-void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, at::Tensor& dap);
+void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& dap, at::Tensor& g2,
+               at::Tensor& cnt);
 int64_t conv2_wgrad_groups(int64_t B);
-void conv2_bwd(const at::Tensor& dap, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a1,
-               const at::Tensor& w2bf, at::Tensor& g1, at::Tensor& slab, at::Tensor& gb2);
+void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf, at::Tensor& g1,
+               at::Tensor& slab, at::Tensor& gb2);
 void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                  const at::Tensor& g1, const at::Tensor& idx1, const at::Tensor& slab, at::Tensor& gW1, at::Tensor& gb1,
                  at::Tensor& gW2);
@@ -48,10 +49,12 @@ void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Ten
                   Tensor gW4, Tensor gb4, Tensor gb2, Tensor gW1, Tensor gb1) {
   mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, gb2, gW1, gb1);
 }
-void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, Tensor dap) { mihvd::fc1_dgrad(dz, w3, dap); }
-void conv2_bwd_op(const Tensor& dap, const Tensor& a2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, Tensor g1,
-                  Tensor slab, Tensor gb2) {
-  mihvd::conv2_bwd(dap, a2, idx2, a1, w2, g1, slab, gb2);
+void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, const Tensor& a2, Tensor dap, Tensor g2, Tensor cnt) {
+  mihvd::fc1_dgrad(dz, w3, a2, dap, g2, cnt);
+}
+void conv2_bwd_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, Tensor g1, Tensor slab,
+                  Tensor gb2) {
+  mihvd::conv2_bwd(g2, idx2, a1, w2, g1, slab, gb2);
 }
 void conv1_wgrad_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& g1, const Tensor& idx1,
                     const Tensor& slab, Tensor gW1, Tensor gb1, Tensor gW2) {
@@ -73,10 +76,9 @@ TORCH_LIBRARY(mihvd, m) {
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
   m.def("fc1_wgrad(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
         "Tensor(d!) gb4, Tensor(e!) gb2, Tensor(f!) gW1, Tensor(g!) gb1) -> ()");
-  m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor(a!) dap) -> ()");
+  m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor a2, Tensor(a!) dap, Tensor(b!) g2, Tensor(c!) cnt) -> ()");
   m.def("conv2_wgrad_groups(int B) -> int", &mihvd::conv2_wgrad_groups);
-  m.def("conv2_bwd(Tensor dap, Tensor a2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor(a!) g1, Tensor(b!) slab, "
-        "Tensor(c!) gb2) -> ()");
+  m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor(a!) g1, Tensor(b!) slab, Tensor(c!) gb2) -> ()");
   m.def("conv1_wgrad(Tensor x, Tensor? rows, Tensor? state, Tensor g1, Tensor idx1, Tensor slab, Tensor(a!) gW1, "
         "Tensor(b!) gb1, Tensor(c!) gW2) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "

@@ -104,7 +104,9 @@ class FusedMNISTTrainer:
         self.dz = torch.empty(B, 1024, **bf)
         self.dlog = torch.empty(B, 10, **f32)
         self.stats = torch.zeros(B, 2, **f32)
-        self.dap = torch.empty(4, B, 3136, **f32)   # fc1 dgrad split-K partial slabs
+        self.dap = torch.empty(4, B, 3136, **f32)   # fc1 dgrad split-K partial slabs (workspace)
+        self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
+        self.cnt = torch.zeros(64, device=dev, dtype=torch.int32)  # split-K arrival counters
         self.g1 = torch.empty(B, 14, 14, 32, **bf)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
         self.x_buf = torch.zeros(B, 784, **f32)
@@ -112,7 +114,10 @@ class FusedMNISTTrainer:
         self.X = self.Y = self.rows = None
         self.graph = None
         self.steps_per_replay = 1
-        self._side = torch.cuda.Stream(device=dev)  # fc-bucket allreduce + fc-segment optimizer
+        # Overlap the "fc" bucket's allreduce with the conv backward on a side stream (N > 1). A
+        # stream fork/join costs a few us inside a HIP graph, so it is only used with collectives.
+        self.overlap = os.environ.get("MIHVD_OVERLAP", "1") != "0"
+        self._side = torch.cuda.Stream(device=dev) if self.collectives else None
         if compression == "bf16" and self.collectives:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
         else:
@@ -177,31 +182,27 @@ class FusedMNISTTrainer:
                     self.gview("dense_1/kernel"), self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
                     self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
         main = torch.cuda.current_stream(self.device)
-        side = self._side
         fc_bucket = self.grads[FC_START:]
         conv_bucket = self.grads[:FC_START]
-        b1, b2 = self.betas
-        side.wait_stream(main)
-        if self.collectives:
+        overlap = self.collectives and self.overlap
+        if overlap:
             # bucket "fc" is complete: reduce it on the side stream while the conv backward runs
-            with torch.cuda.stream(side):
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
                 self._allreduce(fc_bucket, FC_START, FLAT_NUMEL)
-        o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.dap)  # last reader of W3
-        # Optimizer for the fc segment (98 % of the state bytes) on the side stream, concurrent with
-        # the conv backward; it must follow fc1_dgrad, which reads the W3 shadow it rewrites.
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            o.adam_step(self.params[FC_START:], fc_bucket, self.m[FC_START:], self.v[FC_START:],
-                        self.shadow[FC_START:], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 0)
-        o.conv2_bwd(self.dap, self.a2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1,
-                    self.slab, self.gview("conv_layer2/conv2d/bias"))
+        o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.dap, self.g2, self.cnt)
+        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1, self.slab,
+                    self.gview("conv_layer2/conv2d/bias"))
         o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),
                       self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/kernel"))
-        if self.collectives:
+        if overlap:
             self._allreduce(conv_bucket, 0, FC_START)
-        o.adam_step(self.params[:FC_START], conv_bucket, self.m[:FC_START], self.v[:FC_START], self.shadow[:FC_START],
-                    st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-        main.wait_stream(side)
+            main.wait_stream(self._side)
+        elif self.collectives:
+            self._allreduce(self.grads, 0, FLAT_NUMEL)  # one fused collective for the whole buffer
+        b1, b2 = self.betas
+        o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
+                    1.0 / self.world, self.rule, 1)
 
     def _allreduce(self, bucket, lo, hi):
         import torch.distributed as dist

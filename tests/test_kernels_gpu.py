@@ -155,8 +155,14 @@ def test_fc1_bwd(ops, B):
                      torch.full((32,), 3.0, device="cuda"))
     ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3, gb3, gW4, gb4, gb2,
                   gW1, gb1)
-    ops.fc1_dgrad(dz.to(torch.bfloat16), w3.to(torch.bfloat16), dap)
-    assert rel_err(dap.sum(0), dz @ w3.t()) < 1e-4
+    g2 = torch.empty(B, 3136, device="cuda", dtype=torch.bfloat16)
+    cnt = torch.zeros(64, device="cuda", dtype=torch.int32)
+    for _ in range(2):  # second call checks that the split-K counters re-arm themselves
+        ops.fc1_dgrad(dz.to(torch.bfloat16), w3.to(torch.bfloat16), a2.to(torch.bfloat16), dap, g2, cnt)
+        torch.cuda.synchronize()
+        assert rel_err(dap.sum(0), dz @ w3.t()) < 1e-4
+        assert rel_err(g2, (dz @ w3.t()) * (a2 > 0)) < 5e-3
+        assert int(cnt.abs().sum()) == 0
     assert rel_err(gW3, a2.t() @ dz) < 1e-4
     assert rel_err(gb3, dz.sum(0)) < 1e-4
     assert rel_err(gW4, h.t() @ dlog) < 1e-4
@@ -179,14 +185,14 @@ def test_conv2_bwd_and_conv1_wgrad(ops, B):
     a2 = torch.empty(B, 3136, device="cuda", dtype=torch.bfloat16)
     idx2 = torch.empty_like(a2, dtype=torch.uint8)
     ops.conv2_fwd(a1, w2.to(torch.bfloat16).reshape(-1), b2, a2, idx2)
-    dap = torch.randn(4, B, 3136, device="cuda", generator=g) * 0.005
-    g2 = (dap.sum(0) * (a2.float() > 0)).to(torch.bfloat16)  # what conv2_bwd builds internally
+    dA2 = torch.randn(B, 3136, device="cuda", generator=g) * 0.01
+    g2 = (dA2 * (a2.float() > 0)).to(torch.bfloat16)  # what fc1_dgrad hands to conv2_bwd
     G = int(ops.conv2_wgrad_groups(B))
     g1 = torch.empty_like(a1)
     slab = torch.empty(G, 51200, device="cuda")
     gb2, gW1, gb1, gW2 = (torch.zeros(64, device="cuda"), torch.zeros(800, device="cuda"),
                           torch.zeros(32, device="cuda"), torch.empty(51200, device="cuda"))
-    ops.conv2_bwd(dap, a2, idx2, a1, w2.to(torch.bfloat16).reshape(-1), g1, slab, gb2)
+    ops.conv2_bwd(g2, idx2, a1, w2.to(torch.bfloat16).reshape(-1), g1, slab, gb2)
     ops.conv1_wgrad(x, None, None, g1, idx1, slab, gW1, gb1, gW2)
     # Reference: autograd through conv2 (+relu+pool) on the same bf16 a1, and conv1 on fp32 x.
     a1r = a1.float().requires_grad_(True)
