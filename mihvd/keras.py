@@ -233,6 +233,14 @@ class Model:
     def train_on_batch(self, xb, yb):
         self.module.train()
         self.optimizer.zero_grad()
+        if getattr(self.module, "impl", None) == "hip":
+            # whole forward+backward in the CDNA4 kernels, one autograd node (bf16 MFMA inside)
+            from .ops.functional import fused_mnist_loss
+
+            loss, acc = fused_mnist_loss(self.module, xb, yb, training=True, return_accuracy=True)
+            loss.backward()
+            self.optimizer.step()
+            return loss.detach(), acc
         with self._autocast():
             logits = self.module(xb)
         loss = self.loss_fn(logits.float(), yb)

@@ -116,9 +116,11 @@ class MNISTConvNet(nn.Module):
     def forward(self, images: torch.Tensor) -> torch.Tensor:
         """images: [B, 784] or [B, 28, 28] floats in [0, 1]. Returns [B, 10] logits."""
         if self.impl == "hip":
+            # inference through the HIP kernels; training goes through
+            # mihvd.ops.functional.fused_mnist_loss (forward + backward in one fused node)
             from ..ops import functional as HF
 
-            return HF.mnist_forward(self, images)
+            return HF.mnist_logits(self, images)
         x = images.reshape(-1, 28, 28, 1).permute(0, 3, 1, 2)  # NHWC view -> NCHW for torch conv
         cd = self.compute_dtype
         w1 = self.conv_layer1.conv2d.kernel.permute(3, 2, 0, 1)  # HWIO -> OIHW
