@@ -324,3 +324,28 @@ def test_fused_training_converges_and_graph_replays(ops):
     assert int(tr.state[0].item()) == tr.global_step and int(tr.state[1].item()) == tr.global_step
     assert tr.last_loss() < first * 0.5, (first, tr.last_loss())
     assert tr.last_accuracy() > 0.8
+
+
+def test_fused_loss_autograd_matches_trainer(ops):
+    """ops.functional.fused_mnist_loss (one autograd node) gives the trainer's gradients, and the
+    HIP inference logits agree with the torch model."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.models.mnist import MNISTConvNet
+    from mihvd.ops.functional import fused_mnist_loss, mnist_logits
+
+    B = 64
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.rand(B, 784, device="cuda", generator=g)
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    model = MNISTConvNet(impl="hip", seed=3).cuda()
+    loss, acc = fused_mnist_loss(model, x, y, training=False, return_accuracy=True)
+    loss.backward()
+    tr = FusedMNISTTrainer(batch_size=B, lr=0.0, dropout=0.0, seed=3, device="cuda")
+    out = tr.train_step(x, y)
+    torch.cuda.synchronize()
+    assert abs(loss.item() - out["loss"].item()) < 1e-5
+    for name, p in model.ordered_parameters():
+        assert rel_err(p.grad, tr.gview(name)) < 1e-3, name
+    ref = MNISTConvNet(impl="torch", seed=3).cuda().eval()
+    with torch.no_grad():
+        assert rel_err(mnist_logits(model, x), ref(x)) < 2e-2
