@@ -11,9 +11,10 @@
 //           28 KB slice of W3 and writes an fp32 partial slab — the step is weight-bandwidth bound.
 // head    : one block per sample: slab sum + bias + ReLU + counter-based dropout, fc2, softmax
 //           cross-entropy and the fc2 backward into dz (K9-K11 of SURVEY.md §2.5, one kernel).
-// fc1_bwd : one launch, five block roles: dgrad (split-K into fp32 slabs, reduced and masked by
-//           conv2_bwd), wgrad (dW3 straight into the fusion buffer), db3, dW4, db4 (+ zeroing of
-//           the gradients the next launch accumulates atomically).
+// fc1_wgrad: one launch, four block roles: dW3 straight into the fusion buffer, db3, dW4, db4
+//           (+ zeroing of the gradients conv2_bwd / conv1_wgrad accumulate atomically).
+// fc1_dgrad: full-K tiles (W3 rows in registers, dz in LDS) with the pooled-ReLU mask and the
+//           bf16 cast fused into the epilogue.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -167,122 +168,103 @@ __global__ void __launch_bounds__(256) head_kernel(
 }
 
 // ------------------------------------------------------------------------------------------ //
-// fc1_bwd roles by blockIdx.x:
-//   [0, 196)       dgrad : (64 rows j, K quarter) -> dAp[kq][b][j] fp32 partial (split-K)
-//   [196, 980)     wgrad : 64x64 tile of dW3 = a2^T dz   (K = batch, zero padded)
-//   next 4         db3   ; next 4: dW4 ; last: db4 + zero gb2/gW1/gb1 (atomic targets)
+// fc1_dgrad: g2[b][j] = (a2[b][j] > 0) * sum_n dz[b][n] W3[j][n]     (no split-K, no combine)
+//
+// Block = 64 features j x 32 samples x the full K = 1024. Both operands are K-contiguous, so each
+// wave keeps its 16 rows of W3 (32 KB) in registers straight from global memory — one 32-byte
+// load per lane per 64-wide K step, all 32 loads in flight at once — while the block's 32 dz rows
+// (64 KB) are staged once in LDS. The K order inside a 64-wide step is permuted identically for
+// both operands (lane group lg owns K = 64s + 16lg + [0,16)), which lets a lane load 32 contiguous
+// bytes. The four sample groups of a feature tile are mapped to the same XCD (blockIdx & 7), so
+// W3 comes from HBM once per XCD L2 and three of its four reads hit.
 // ------------------------------------------------------------------------------------------ //
-constexpr int FB_KQ = 4, FB_KQL = FC1_N / FB_KQ;                 // 256
-constexpr int FB_DGRAD = (FC1_K / 64) * FB_KQ;                   // 196
-constexpr int FB_WGRAD = (FC1_K / 64) * (FC1_N / 64);            // 784
-constexpr int FB_DB3 = FC1_N / 64, FB_DW4 = FC1_N / 64, FB_MISC = 1;  // 16 + 16 + 1 blocks
-constexpr int FB_TOTAL = FB_DGRAD + FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC;
-constexpr int FB_DSTR = FB_KQL + 8;                              // 264 elements (528 B)
-constexpr int FB_TSTR = 64 + 8;                                  // 72 elements
-constexpr int FB_LDS_DG = (MAXB + 64) * FB_DSTR * 2;             // 101,376 B
-constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
-constexpr int FB_LDS = FB_LDS_DG;
+constexpr int DG_ROWS = 32, DG_JT = FC1_K / 64;         // 49 feature tiles
+constexpr int DG_DSTR = FC1_N + 8;                      // dz image row stride (2064 B)
+constexpr int DG_LDS = DG_ROWS * DG_DSTR * 2;           // 66,048 B
 
-// MT (= ceil(B/16) sample tiles) is a template parameter: a runtime guard around an MFMA makes
-// hipcc shuttle every accumulator between AGPRs and VGPRs at each guard (thousands of moves).
-template <int MT>
-__global__ void __launch_bounds__(256) fc1_bwd_kernel(
-    const u16* __restrict__ dz, const u16* __restrict__ w3, const u16* __restrict__ a2, const u16* __restrict__ h,
-    const float* __restrict__ dlog, float* __restrict__ dap, float* __restrict__ gW3, float* __restrict__ gb3,
-    float* __restrict__ gW4, float* __restrict__ gb4, float* __restrict__ gb2, float* __restrict__ gW1,
-    float* __restrict__ gb1, u16* __restrict__ g2, int* __restrict__ cnt, int B, int role_base) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) fc1_dgrad_kernel(const u16* __restrict__ dz, const u16* __restrict__ w3,
+                                                        const u16* __restrict__ a2, u16* __restrict__ g2, int B, int G) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
-  const int q = lr >> 2, p = lr & 3;
-  constexpr int Mpad = MT * 16;
-  int bid = blockIdx.x + role_base;
-  if (bid < FB_DGRAD) {
-    // dAp^T[j][b] = sum_n W3[j][n] dz[b][n] over this block's K quarter.
-    const int jt = bid >> 2, kq = bid & 3;
-    const int j0 = jt * 64, n0 = kq * FB_KQL;
-    u16* Ws = smem;                    // W3   [64][264]    rows = j
-    u16* Ds = smem + 64 * FB_DSTR;     // dz   [Mpad][264]  rows = samples
-    {
-      TileLoad<256, (Mpad * FB_KQL / 8 + 255) / 256, FB_KQL / 8> ld;
-      TileLoad<256, (64 * FB_KQL / 8 + 255) / 256, FB_KQL / 8> lw;
-      lw.load(w3 + (int64_t)j0 * FC1_N + n0, FC1_N, 64, 64, t);
-      ld.load(dz + n0, FC1_N, Mpad, B, t);
-      lw.store(Ws, FB_DSTR, 64, t);
-      ld.store(Ds, FB_DSTR, Mpad, t);
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int mg = slot % G, jt = (slot / G) * 8 + xcd;
+  if (jt >= DG_JT) return;
+  const int j0 = jt * 64, m0 = mg * DG_ROWS;
+  const int rows = min(DG_ROWS, B - m0);
+  // Load order matters: vmcnt retires in issue order, so the dz tile (needed first, for the LDS
+  // image) is issued before the 32 W3 loads, which then land while the image is written.
+  // 1. the block's dz rows (rows past B zero-filled)
+  TileLoad<256, DG_ROWS * (FC1_N / 8) / 256, FC1_N / 8> ld;
+  ld.load(dz + (int64_t)m0 * FC1_N, FC1_N, DG_ROWS, rows, t);
+  // 2. this wave's W3 rows: j = j0 + 16*wave + lr, K chunk [64s + 16lg, +16) for s = 0..15
+  uint4 wv[16][2];
+  {
+    const u16* wr = w3 + (int64_t)(j0 + wave * 16 + lr) * FC1_N + 16 * lg;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      wv[s][0] = *reinterpret_cast<const uint4*>(wr + 64 * s);
+      wv[s][1] = *reinterpret_cast<const uint4*>(wr + 64 * s + 8);
     }
-    __syncthreads();
-    f32x4 acc[MT];
+  }
+  // 3. pooled-ReLU mask for the epilogue rows (a2 > 0), 4 features per lane
+  uint2 mk[2];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int mt = 0; mt < 2; ++mt) {
+    const int m = m0 + mt * 16 + lr;
+    const uint2 x = *reinterpret_cast<const uint2*>(a2 + (int64_t)min(m, B - 1) * FC1_K + j0 + wave * 16 + 4 * lg);
+    const uint32_t keep = m < B ? 0xffffffffu : 0u;
+    mk[mt] = make_uint2(x.x & keep, x.y & keep);
+  }
+  u16* Ds = smem;
+  ld.store(Ds, DG_DSTR, DG_ROWS, t);
+  __syncthreads();
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int kk = 0; kk < FB_KQL / 32; ++kk) {
-      const bf16x8 afr = frag_ld128(Ws + (wave * 16 + lr) * FB_DSTR + kk * 32 + 8 * lg);
+  for (int s = 0; s < 16; ++s) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 bfr = frag_ld128(Ds + (mt * 16 + lr) * FB_DSTR + kk * 32 + 8 * lg);
+    for (int hh = 0; hh < 2; ++hh) {
+      const bf16x8 afr = __builtin_bit_cast(bf16x8, wv[s][hh]);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const bf16x8 bfr = frag_ld128(Ds + (mt * 16 + lr) * DG_DSTR + 64 * s + 16 * lg + 8 * hh);
         acc[mt] = mfma16(afr, bfr, acc[mt]);
       }
     }
-    float* out = dap + (int64_t)kq * B * FC1_K;
-    const int j = j0 + wave * 16 + 4 * lg;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int m = mt * 16 + lr;
-      if (m < B)
-        *reinterpret_cast<float4*>(out + (int64_t)m * FC1_K + j) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
-    }
-    // In-launch split-K combine (cdna_hip_programming.md §6 Guideline 16, counter form): every
-    // storing wave drains, the block releases at agent scope and takes a ticket; the fourth
-    // arriver of this column tile acquires, sums the four fp32 slabs, applies conv2's pooled-ReLU
-    // mask (a2 > 0) and writes g2 in bf16. Correct for any placement of the four blocks.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);  // the one LDS array (no second __shared__ object)
-    if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int ticket = __hip_atomic_fetch_add(cnt + jt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = (ticket == FB_KQ - 1);
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      cnt[jt] = 0;  // re-arm for the next launch (the buffer is zeroed once at allocation)
-    }
-    __syncthreads();
-    // thread -> (row m, 4 columns): 16 float4 per row of the tile, B rows
-    constexpr int IT = (MT * 16 * 16 + 255) / 256;
-    float4 part[IT][FB_KQ];
-    uint2 mk[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int e = min(t + 256 * it, B * 16 - 1);
-      const int m = e >> 4, c4 = (e & 15) * 4;
-#pragma unroll
-      for (int k = 0; k < FB_KQ; ++k)
-        part[it][k] = *reinterpret_cast<const float4*>(dap + ((int64_t)k * B + m) * FC1_K + j0 + c4);
-      mk[it] = *reinterpret_cast<const uint2*>(a2 + (int64_t)m * FC1_K + j0 + c4);
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int e = t + 256 * it;
-      if (e >= B * 16) continue;
-      const int m = e >> 4, c4 = (e & 15) * 4;
-      float s[4];
-      s[0] = (part[it][0].x + part[it][1].x) + (part[it][2].x + part[it][3].x);
-      s[1] = (part[it][0].y + part[it][1].y) + (part[it][2].y + part[it][3].y);
-      s[2] = (part[it][0].z + part[it][1].z) + (part[it][2].z + part[it][3].z);
-      s[3] = (part[it][0].w + part[it][1].w) + (part[it][2].w + part[it][3].w);
-      const u16 av[4] = {(u16)(mk[it].x & 0xffff), (u16)(mk[it].x >> 16), (u16)(mk[it].y & 0xffff), (u16)(mk[it].y >> 16)};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s[c] = bf2f(av[c]) > 0.f ? s[c] : 0.f;
-      *reinterpret_cast<uint2*>(g2 + (int64_t)m * FC1_K + j0 + c4) = pack4bf(s[0], s[1], s[2], s[3]);
-    }
-    return;
   }
-  bid -= FB_DGRAD;
+  // C[row = 4lg + i][col = lr] = feature j0 + 16*wave + 4lg + i, sample m0 + 16mt + lr
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int m = m0 + mt * 16 + lr;
+    if (m < B) {
+      const uint2 x = mk[mt];
+      const u16 av[4] = {(u16)(x.x & 0xffff), (u16)(x.x >> 16), (u16)(x.y & 0xffff), (u16)(x.y >> 16)};
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = bf2f(av[i]) > 0.f ? acc[mt][i] : 0.f;
+      *reinterpret_cast<uint2*>(g2 + (int64_t)m * FC1_K + j0 + wave * 16 + 4 * lg) = pack4bf(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ //
+// fc1_wgrad roles by blockIdx.x:
+//   [0, 784)       wgrad : 64x64 tile of dW3 = a2^T dz   (K = batch, zero padded)
+//   next 16        db3   ; next 16: dW4 ; last: db4 + zero gb2/gW1/gb1 (atomic targets)
+// ------------------------------------------------------------------------------------------ //
+constexpr int FB_WGRAD = (FC1_K / 64) * (FC1_N / 64);            // 784
+constexpr int FB_DB3 = FC1_N / 64, FB_DW4 = FC1_N / 64, FB_MISC = 1;  // 16 + 16 + 1 blocks
+constexpr int FB_TOTAL = FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC;
+constexpr int FB_TSTR = 64 + 8;                                  // 72 elements
+constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
+
+__global__ void __launch_bounds__(256) fc1_wgrad_kernel(
+    const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
+    float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4, float* __restrict__ gb4,
+    float* __restrict__ gb2, float* __restrict__ gW1, float* __restrict__ gb1, int B) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int q = lr >> 2, p = lr & 3;
+  int bid = blockIdx.x;
   if (bid < FB_WGRAD) {
     // dW3^T[n][j] tile = sum_b dz[b][n] a2[b][j]  -> stored as gW3[j][n..n+3] (float4 per lane)
     const int jt = bid >> 4, ntile = bid & 15;
@@ -466,10 +448,8 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                                      stats.data_ptr<float>(), B);
 }
 
-// Two launches of one kernel so each gets its own LDS budget: the weight-gradient roles (37 KB:
-// several blocks per CU) and the dgrad split-K role ((Mpad + 64) x 528 B). The wgrad launch
-// completes the whole "fc" gradient bucket, so its allreduce can start while dgrad and the conv
-// backward still run.
+// The wgrad launch completes the whole "fc" gradient bucket, so its allreduce can start while
+// dgrad and the conv backward still run.
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1) {
   const int B = dz.size(0);
@@ -481,36 +461,26 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_wgrad: fc grads");
   TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "fc1_wgrad: conv grads");
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  fc1_bwd_kernel<1><<<FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC, 256, FB_LDS_WG, stream>>>(
-      (const u16*)dz.data_ptr(), nullptr, (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
-      nullptr, gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(),
-      gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), nullptr, nullptr, B, FB_DGRAD);
+  fc1_wgrad_kernel<<<FB_TOTAL, 256, FB_LDS_WG, stream>>>(
+      (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
+      gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), gb2.data_ptr<float>(),
+      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B);
 }
 
-// dgrad: split-K partials into `dap` (workspace), combined in-launch into g2 = (a2 > 0) * dz.W3^T
-// (bf16). `cnt` holds one arrival counter per 64-column tile (49 ints, zero at allocation; the
-// combining block re-arms it).
-void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& dap, at::Tensor& g2,
-               at::Tensor& cnt) {
+// dgrad: g2 = (a2 > 0) * dz.W3^T in bf16, the gradient conv2_bwd routes through the pool argmax.
+void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& g2) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_dgrad: batch");
-  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_dgrad: dz");
-  TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N, "fc1_dgrad: w3");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K, "fc1_dgrad: a2");
-  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * FC1_K, "fc1_dgrad: g2");
-  TORCH_CHECK(dap.dtype() == at::kFloat && dap.numel() == (int64_t)FB_KQ * B * FC1_K, "fc1_dgrad: dap must be fp32 [4][B][3136]");
-  TORCH_CHECK(cnt.dtype() == at::kInt && cnt.numel() >= FC1_K / 64, "fc1_dgrad: cnt must be int32 [>=49]");
-  const int MT = (B + 15) >> 4;
-  // The dz image sits after the 64 W3 rows, so only the rows of this batch need LDS.
-  const int lds = (64 + MT * 16) * FB_DSTR * 2;
+  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N && dz.is_contiguous(), "fc1_dgrad: dz");
+  TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_dgrad: w3");
+  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_dgrad: a2");
+  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * FC1_K && g2.is_contiguous(), "fc1_dgrad: g2");
+  const int G = (B + DG_ROWS - 1) / DG_ROWS;
+  const int grid = 8 * ((DG_JT + 7) / 8) * G;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  MIHVD_MT_SWITCH(MT, {
-    set_max_lds(fc1_bwd_kernel<MT_>, FB_LDS);
-    fc1_bwd_kernel<MT_><<<FB_DGRAD, 256, lds, stream>>>(
-        (const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(), (const u16*)a2.data_ptr(), nullptr, nullptr,
-        dap.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, (u16*)g2.data_ptr(),
-        cnt.data_ptr<int>(), B, 0);
-  })
+  set_max_lds(fc1_dgrad_kernel, DG_LDS);
+  fc1_dgrad_kernel<<<grid, 256, DG_LDS, stream>>>((const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(),
+                                                   (const u16*)a2.data_ptr(), (u16*)g2.data_ptr(), B, G);
 }
 
 }  // namespace mihvd

@@ -14,8 +14,7 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1);
-void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& dap, at::Tensor& g2,
-               at::Tensor& cnt);
+void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& g2);
 int64_t conv2_wgrad_groups(int64_t B);
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf, at::Tensor& g1,
                at::Tensor& slab, at::Tensor& gb2);
@@ -24,9 +23,16 @@ void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, con
                  at::Tensor& gW2);
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
-               double grad_scale, int64_t rule, int64_t bump);
+               double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale);
 void scale_cast_bf16(const at::Tensor& src, at::Tensor& dst, double scale);
 void bf16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale);
+void segment_dots(const at::Tensor& a, const at::Tensor& b, const at::Tensor& offs_dev, int64_t max_seg_len,
+                  at::Tensor& out);
+void adasum_combine(const at::Tensor& a, const at::Tensor& b, const at::Tensor& offs_dev, int64_t max_seg_len,
+                    const at::Tensor& dots, at::Tensor& out);
+void grad_check_(at::TensorList grads, at::Tensor& ls, bool unscale);
+void update_scale_(at::Tensor& ls, at::Tensor& tracker, double growth, double backoff, int64_t interval,
+                   double min_scale);
 }  // namespace mihvd
 
 namespace {
@@ -49,9 +55,7 @@ void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Ten
                   Tensor gW4, Tensor gb4, Tensor gb2, Tensor gW1, Tensor gb1) {
   mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, gb2, gW1, gb1);
 }
-void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, const Tensor& a2, Tensor dap, Tensor g2, Tensor cnt) {
-  mihvd::fc1_dgrad(dz, w3, a2, dap, g2, cnt);
-}
+void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, const Tensor& a2, Tensor g2) { mihvd::fc1_dgrad(dz, w3, a2, g2); }
 void conv2_bwd_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, Tensor g1, Tensor slab,
                   Tensor gb2) {
   mihvd::conv2_bwd(g2, idx2, a1, w2, g1, slab, gb2);
@@ -61,11 +65,23 @@ void conv1_wgrad_op(const Tensor& x, const OptT& rows, const OptT& state, const 
   mihvd::conv1_wgrad(x, rows, state, g1, idx1, slab, gW1, gb1, gW2);
 }
 void adam_op(Tensor p, const Tensor& g, Tensor m, Tensor v, const OptT& shadow, const OptT& state, int64_t host_step,
-             double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, int64_t bump) {
-  mihvd::adam_step(p, g, m, v, shadow, state, host_step, lr, b1, b2, eps, grad_scale, rule, bump);
+             double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, int64_t bump,
+             const OptT& loss_scale) {
+  mihvd::adam_step(p, g, m, v, shadow, state, host_step, lr, b1, b2, eps, grad_scale, rule, bump, loss_scale);
 }
 void scale_cast_op(const Tensor& src, Tensor dst, double scale) { mihvd::scale_cast_bf16(src, dst, scale); }
 void bf16_to_f32_op(const Tensor& src, Tensor dst, double scale) { mihvd::bf16_to_f32(src, dst, scale); }
+void segment_dots_op(const Tensor& a, const Tensor& b, const Tensor& offs, int64_t max_len, Tensor out) {
+  mihvd::segment_dots(a, b, offs, max_len, out);
+}
+void adasum_combine_op(const Tensor& a, const Tensor& b, const Tensor& offs, int64_t max_len, const Tensor& dots,
+                       Tensor out) {
+  mihvd::adasum_combine(a, b, offs, max_len, dots, out);
+}
+void grad_check_op(at::TensorList grads, Tensor ls, bool unscale) { mihvd::grad_check_(grads, ls, unscale); }
+void update_scale_op(Tensor ls, Tensor tracker, double growth, double backoff, int64_t interval, double min_scale) {
+  mihvd::update_scale_(ls, tracker, growth, backoff, interval, min_scale);
+}
 }  // namespace
 
 TORCH_LIBRARY(mihvd, m) {
@@ -76,15 +92,21 @@ TORCH_LIBRARY(mihvd, m) {
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
   m.def("fc1_wgrad(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
         "Tensor(d!) gb4, Tensor(e!) gb2, Tensor(f!) gW1, Tensor(g!) gb1) -> ()");
-  m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor a2, Tensor(a!) dap, Tensor(b!) g2, Tensor(c!) cnt) -> ()");
+  m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor a2, Tensor(a!) g2) -> ()");
   m.def("conv2_wgrad_groups(int B) -> int", &mihvd::conv2_wgrad_groups);
   m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor(a!) g1, Tensor(b!) slab, Tensor(c!) gb2) -> ()");
   m.def("conv1_wgrad(Tensor x, Tensor? rows, Tensor? state, Tensor g1, Tensor idx1, Tensor slab, Tensor(a!) gW1, "
         "Tensor(b!) gb1, Tensor(c!) gW2) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
-        "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1) -> ()");
+        "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1, "
+        "Tensor? loss_scale=None) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
+  m.def("segment_dots(Tensor a, Tensor b, Tensor offs, int max_seg_len, Tensor(a!) out) -> ()");
+  m.def("adasum_combine(Tensor a, Tensor b, Tensor offs, int max_seg_len, Tensor dots, Tensor(a!) out) -> ()");
+  m.def("grad_check_(Tensor(a!)[] grads, Tensor(b!) ls, bool unscale) -> ()");
+  m.def("update_scale_(Tensor(a!) ls, Tensor(b!) tracker, float growth, float backoff, int interval, "
+        "float min_scale) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
@@ -99,4 +121,8 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("adam_step", &adam_op);
   m.impl("scale_cast_bf16", &scale_cast_op);
   m.impl("bf16_to_f32", &bf16_to_f32_op);
+  m.impl("segment_dots", &segment_dots_op);
+  m.impl("adasum_combine", &adasum_combine_op);
+  m.impl("grad_check_", &grad_check_op);
+  m.impl("update_scale_", &update_scale_op);
 }

@@ -6,7 +6,8 @@
 // (horovod/tensorflow_mnist.py:130):
 //     lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t);  p -= lr_t * m / (sqrt(v) + eps)
 // With a device step-state tensor the step t is read on the device (graph-replayable) and the
-// forward step counter is advanced by block 0.
+// forward step counter is advanced by block 0. An optional device loss-scale pair [scale, found]
+// (dp_kernels.hip) makes the update skip itself after an overflow and divides by the scale.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -17,7 +18,13 @@ namespace mihvd {
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, u16* __restrict__ shadow,
                                                    int64_t n4, int64_t* __restrict__ state, int64_t host_t, float lr,
-                                                   float b1, float b2, float eps, float gscale, int rule, int bump) {
+                                                   float b1, float b2, float eps, float gscale, int rule, int bump,
+                                                   const float* __restrict__ ls) {
+  if (bump && state && blockIdx.x == 0 && threadIdx.x == 0) state[ST_FWD] += 1;
+  if (ls) {  // dynamic loss scaling (dp_kernels.hip): skip on overflow, unscale fused into gscale
+    if (ls[1] != 0.f) return;
+    gscale /= ls[0];
+  }
   const float t = (float)(state ? state[ST_OPT] : host_t);
   const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
   // rule 0: TF1 (eps outside the bias-corrected sqrt); rule 1: torch.optim.Adam
@@ -49,7 +56,6 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const 
       reinterpret_cast<uint2*>(shadow)[i] = make_uint2((uint32_t)sh[0] | ((uint32_t)sh[1] << 16),
                                                        (uint32_t)sh[2] | ((uint32_t)sh[3] << 16));
   }
-  if (bump && state && blockIdx.x == 0 && threadIdx.x == 0) state[ST_FWD] += 1;
 }
 
 __global__ void __launch_bounds__(256) scale_cast_kernel(const float* __restrict__ src, u16* __restrict__ dst, int64_t n4,
@@ -77,7 +83,7 @@ static int grid_for(int64_t n4) {
 
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
-               double grad_scale, int64_t rule, int64_t bump) {
+               double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale) {
   const int64_t n = p.numel();
   TORCH_CHECK(p.dtype() == at::kFloat && g.dtype() == at::kFloat && m.dtype() == at::kFloat && v.dtype() == at::kFloat,
               "adam_step: fp32 buffers expected");
@@ -91,10 +97,15 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
   }
   int64_t* st = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   TORCH_CHECK(st != nullptr || host_step >= 1, "adam_step: step must be >= 1");
+  const float* ls = nullptr;
+  if (loss_scale.has_value() && loss_scale->defined()) {
+    TORCH_CHECK(loss_scale->dtype() == at::kFloat && loss_scale->numel() == 2, "adam_step: loss_scale is float32 [2]");
+    ls = loss_scale->data_ptr<float>();
+  }
   auto stream = c10::hip::getCurrentHIPStream().stream();
   adam_kernel<<<grid_for(n / 4), 256, 0, stream>>>(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                                                    v.data_ptr<float>(), sp, n / 4, st, host_step, (float)lr, (float)b1,
-                                                   (float)b2, (float)eps, (float)grad_scale, (int)rule, (int)bump);
+                                                   (float)b2, (float)eps, (float)grad_scale, (int)rule, (int)bump, ls);
 }
 
 void scale_cast_bf16(const at::Tensor& src, at::Tensor& dst, double scale) {

@@ -172,27 +172,64 @@ callbacks = _CallbacksNS()
 # Model
 # ------------------------------------------------------------------------------------------ #
 class _LossScaler:
-    """Dynamic loss scaling for the fp16 policy (Keras LossScaleOptimizer semantics)."""
+    """Dynamic loss scaling for the fp16 policy (Keras LossScaleOptimizer semantics: start at
+    2**15, halve on overflow and skip the step, double after ``growth_interval`` clean steps).
+
+    On a GPU the state is the device pair ``ls = [scale, found_nonfinite]`` driven by the HIP
+    kernels ``grad_check_`` (multi-tensor unscale + non-finite test) and ``update_scale_``
+    (csrc/kernels/dp_kernels.hip); the host reads one flag per step to decide
+    whether to apply the update. On the CPU the same rule runs in plain torch."""
 
     def __init__(self, init_scale=2.0 ** 15, growth_interval=2000):
-        self.scale = init_scale
+        self.init_scale = float(init_scale)
         self.growth_interval = growth_interval
         self.good_steps = 0
+        self._scale = float(init_scale)
+        self._ls = None
+        self._tracker = None
+
+    def _device_state(self, device):
+        if device.type != "cuda":
+            return None
+        if self._ls is None:
+            from . import _native
+
+            _native.require_kernels()
+            self._ls = torch.tensor([self._scale, 0.0], dtype=torch.float32, device=device)
+            self._tracker = torch.zeros(1, dtype=torch.int32, device=device)
+        return self._ls
+
+    @property
+    def scale(self):
+        return self._ls[0] if self._ls is not None else self._scale
+
+    def scale_loss(self, loss):
+        ls = self._device_state(loss.device)
+        return loss * (ls[0] if ls is not None else self._scale)
 
     def unscale_and_check(self, params) -> bool:
+        grads = [p.grad for p in params if p.grad is not None]
+        if not grads:
+            return True
+        ls = self._device_state(grads[0].device)
+        if ls is not None:
+            ops = torch.ops.mihvd
+            ops.grad_check_([g for g in grads if g.dtype == torch.float32], ls, True)
+            finite = float(ls[1].item()) == 0.0
+            ops.update_scale_(ls, self._tracker, 2.0, 0.5, self.growth_interval, 1.0)
+            return finite
         finite = True
-        for p in params:
-            if p.grad is not None:
-                p.grad.div_(self.scale)
-                if not torch.isfinite(p.grad).all():
-                    finite = False
+        for g in grads:
+            g.div_(self._scale)
+            if not torch.isfinite(g).all():
+                finite = False
         if finite:
             self.good_steps += 1
             if self.good_steps >= self.growth_interval:
-                self.scale *= 2
+                self._scale *= 2
                 self.good_steps = 0
         else:
-            self.scale = max(1.0, self.scale / 2)
+            self._scale = max(1.0, self._scale / 2)
             self.good_steps = 0
         return finite
 
@@ -245,7 +282,7 @@ class Model:
             logits = self.module(xb)
         loss = self.loss_fn(logits.float(), yb)
         if self._scaler is not None:
-            (loss * self._scaler.scale).backward()
+            self._scaler.scale_loss(loss).backward()
             self.optimizer.synchronize()
             ok = self._scaler.unscale_and_check([p for g in self.optimizer.param_groups for p in g["params"]])
             if ok:

@@ -7,13 +7,19 @@ allreduce when ``size() > 1``), all hand-written CDNA4 kernels from ``csrc/kerne
     conv2_fwd   implicit GEMM, pool-window-major M, pool/ReLU in registers    [MFMA bf16]
     fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs                    [MFMA bf16]
     head        slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
-    fc1_wgrad   dW3 -> fusion buffer | db3 | dW4/db4 (bucket "fc" complete)  [MFMA bf16]
-    fc1_dgrad   split-K dz.W3^T -> fp32 partial slabs (reduced in conv2_bwd) [MFMA bf16]
-    --- bucket "fc" (98.4 % of the gradient bytes) is allreduced from here on a side stream ---
-    conv2_bwd   dgrad(+pool/ReLU routing) | wgrad slabs | db2                 [MFMA bf16]
+    fc1_wgrad   dW3 -> fusion buffer | db3 | dW4/db4 | db4 (bucket "fc" complete) [MFMA bf16]
+    --- size() > 1: bucket "fc" (98.4 % of the gradient bytes) is allreduced from here on a
+        side stream (MIHVD_OVERLAP=1, default) while the conv backward runs ---
+    fc1_dgrad   full-K dz.W3^T tiles (W3 rows in registers, dz in LDS, XCD-aware tile map)
+                with the pooled-ReLU mask and bf16 cast fused: writes g2         [MFMA bf16]
+    conv2_bwd   dgrad (g2 routed through the pool argmax, ReLU mask) | wgrad slabs | db2
+                                                                                [MFMA bf16]
     conv1_wgrad dW1/db1 + dW2 slab reduction
     --- bucket "conv" allreduced; the optimizer waits for both buckets ---
     adam_step   TF1 Adam over the flat fp32 buffer, 1/size averaging fused, bf16 shadow written
+
+At N=1 everything runs on one stream (a fork/join inside a HIP graph costs more than the
+overlap it would buy when there is no collective to hide).
 
 Parameters, gradients and Adam slots live in flat fp32 buffers laid out in TF variable order
 (horovod/tensorflow_mnist.py:49-70); every kernel writes its gradient straight into its slot of
@@ -104,9 +110,7 @@ class FusedMNISTTrainer:
         self.dz = torch.empty(B, 1024, **bf)
         self.dlog = torch.empty(B, 10, **f32)
         self.stats = torch.zeros(B, 2, **f32)
-        self.dap = torch.empty(4, B, 3136, **f32)   # fc1 dgrad split-K partial slabs (workspace)
         self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
-        self.cnt = torch.zeros(64, device=dev, dtype=torch.int32)  # split-K arrival counters
         self.g1 = torch.empty(B, 14, 14, 32, **bf)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
         self.x_buf = torch.zeros(B, 784, **f32)
@@ -190,7 +194,7 @@ class FusedMNISTTrainer:
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
                 self._allreduce(fc_bucket, FC_START, FLAT_NUMEL)
-        o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.dap, self.g2, self.cnt)
+        o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
         o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1, self.slab,
                     self.gview("conv_layer2/conv2d/bias"))
         o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),

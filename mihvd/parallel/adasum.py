@@ -40,11 +40,60 @@ def _segment_dots(a: torch.Tensor, b: torch.Tensor, segments: Sequence[tuple[int
     return ab[:-1], aa[:-1], bb[:-1]
 
 
+_OFFS_CACHE: dict = {}
+
+
+def _covering_offsets(segments: Sequence[tuple[int, int]], n: int) -> list[int]:
+    """Offsets of a segment table that covers [0, n): gaps become segments of their own (zero
+    padding in a fusion buffer, which the combine then simply sums)."""
+    offs = [0]
+    for s, e in sorted(segments):
+        if s > offs[-1]:
+            offs.append(s)
+        if e > offs[-1]:
+            offs.append(e)
+    if offs[-1] < n:
+        offs.append(n)
+    return offs
+
+
+def _hip_pair(a: torch.Tensor, b: torch.Tensor, segments) -> torch.Tensor:
+    """The CDNA4 path (csrc/kernels/dp_kernels.hip): one fp64-accumulated dot/norm launch and one
+    streaming combine launch for all segments."""
+    key = (tuple(segments), a.numel(), a.device)
+    hit = _OFFS_CACHE.get(key)
+    if hit is None:
+        offs = _covering_offsets(segments, a.numel())
+        max_len = max(e - s for s, e in zip(offs[:-1], offs[1:]))
+        hit = (torch.tensor(offs, dtype=torch.int64, device=a.device), max_len,
+               torch.empty(3 * (len(offs) - 1), dtype=torch.float64, device=a.device))
+        _OFFS_CACHE[key] = hit
+    offs_dev, max_len, dots = hit
+    ops = torch.ops.mihvd
+    a, b = a.contiguous(), b.contiguous()
+    ops.segment_dots(a, b, offs_dev, max_len, dots)
+    out = torch.empty_like(a)
+    ops.adasum_combine(a, b, offs_dev, max_len, dots, out)
+    return out
+
+
+def _use_hip(a: torch.Tensor) -> bool:
+    if not (a.is_cuda and a.dtype == torch.float32):
+        return False
+    from .. import _native
+
+    _native.require_kernels()  # a GPU tensor must take the HIP path: fail loudly if it is missing
+    return True
+
+
 def adasum_pair(a: torch.Tensor, b: torch.Tensor, segments: Sequence[tuple[int, int]] | None = None) -> torch.Tensor:
     """Combine two flat vectors segment by segment. ``a`` must be the lower-rank operand so both
-    partners compute bit-identical results."""
+    partners compute bit-identical results. fp32 GPU vectors run the HIP kernels; everything else
+    (CPU/gloo, other dtypes) the torch formulation below, which is also the test oracle."""
     if segments is None:
         segments = [(0, a.numel())]
+    if _use_hip(a):
+        return _hip_pair(a, b, segments)
     ab, aa, bb = _segment_dots(a, b, segments)
     ca = torch.where(aa > 0, 1.0 - ab / (2.0 * aa), torch.zeros_like(aa))
     cb = torch.where(bb > 0, 1.0 - ab / (2.0 * bb), torch.zeros_like(bb))

@@ -42,7 +42,7 @@ def main():
                                          tr.gview("dense_1/kernel"), tr.gview("dense_1/bias"),
                                          tr.gview("conv_layer2/conv2d/bias"), tr.gview("conv_layer1/conv2d/kernel"),
                                          tr.gview("conv_layer1/conv2d/bias")),
-        "fc1_dgrad": lambda: o.fc1_dgrad(tr.dz, tr.pview("dense/kernel", sh), tr.a2, tr.dap, tr.g2, tr.cnt),
+        "fc1_dgrad": lambda: o.fc1_dgrad(tr.dz, tr.pview("dense/kernel", sh), tr.a2, tr.g2),
         "conv2_bwd": lambda: o.conv2_bwd(tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.g1,
                                          tr.slab, tr.gview("conv_layer2/conv2d/bias")),
         "conv1_wgrad": lambda: o.conv1_wgrad(tr.x_buf, None, st, tr.g1, tr.idx1, tr.slab,

@@ -301,3 +301,11 @@ def test_synthetic_data_and_generator():
     gen = train_input_generator(x.reshape(-1, 784), y, batch_size=300, rng=np.random.default_rng(0))
     batches = [next(gen) for _ in range(4)]
     assert all(b[0].shape == (300, 784) for b in batches)  # tail of 100 dropped each pass
+
+
+def test_adasum_covering_offsets():
+    from mihvd.parallel.adasum import _covering_offsets
+
+    assert _covering_offsets([(0, 5), (8, 10)], 12) == [0, 5, 8, 10, 12]
+    assert _covering_offsets([(0, 12)], 12) == [0, 12]
+    assert _covering_offsets([(2, 4)], 4) == [0, 2, 4]
