@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace mihvd {
 
@@ -119,6 +120,14 @@ __device__ __forceinline__ float mask_f(float v, bool keep) {
 
 __device__ __forceinline__ uint2 pack4bf(float a, float b, float c, float d) {
   return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
+}
+
+// Profiling aid (scripts/kbench.py --roles): MIHVD_ROLE_ONLY=<r> makes a launch that packs several
+// block roles run only the blocks of role r, so each role can be timed on its own. Unset (the
+// normal case) every role runs.
+inline int debug_role_only() {
+  const char* e = getenv("MIHVD_ROLE_ONLY");
+  return e ? atoi(e) : -1;
 }
 
 // Step-state words kept on the device so a whole training step replays from a HIP graph:

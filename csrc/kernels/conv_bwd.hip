@@ -284,14 +284,15 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
 __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const u16* __restrict__ g1, const uint8_t* __restrict__ idx1, const float* __restrict__ slab, int nslab,
-    float* __restrict__ gW1, float* __restrict__ gb1, float* __restrict__ gW2, int B) {
+    float* __restrict__ gW1, float* __restrict__ gb1, float* __restrict__ gW2, int B, int role_base) {
   __shared__ float img[32][33];
   __shared__ float red[8][26][32];
   const int t = threadIdx.x;
-  if ((int)blockIdx.x >= B) {
+  const int bid = (int)blockIdx.x + role_base;
+  if (bid >= B) {
     // dW2 = sum of the (<= 32) wgrad slabs. Block = 64 float4 outputs x 4 slab groups of 8, every
     // load in flight at once (absent slabs masked, not branched around), then a 4-way LDS sum.
-    const int o = ((int)blockIdx.x - B) * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
+    const int o = (bid - B) * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
     float4 v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -314,7 +315,7 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
     }
     return;
   }
-  const int b = blockIdx.x;
+  const int b = bid;
   int row = b;
   if (rows != nullptr) {
     const int64_t step = state ? state[ST_FWD] : 0;
@@ -395,9 +396,12 @@ void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a
   }();
   (void)attr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv2_bwd_kernel<<<B + 5 * G, 512, CB_LDS, stream>>>(
+  const int role = debug_role_only();  // 0: dgrad blocks only, 1: wgrad blocks only
+  const int n_dgrad = role == 1 ? 0 : B;
+  const int grid = role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
+  conv2_bwd_kernel<<<grid, 512, CB_LDS, stream>>>(
       (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(),
-      (const u16*)w2bf.data_ptr(), (u16*)g1.data_ptr(), slab.data_ptr<float>(), gb2.data_ptr<float>(), B, B);
+      (const u16*)w2bf.data_ptr(), (u16*)g1.data_ptr(), slab.data_ptr<float>(), gb2.data_ptr<float>(), B, n_dgrad);
 }
 
 void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
@@ -415,9 +419,11 @@ void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, con
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   TORCH_CHECK(G <= 32, "conv1_wgrad: at most 32 wgrad slabs");
-  conv1_wgrad_kernel<<<B + 200, 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (const u16*)g1.data_ptr(),
-                                                 idx1.data_ptr<uint8_t>(), slab.data_ptr<float>(), G, gW1.data_ptr<float>(),
-                                                 gb1.data_ptr<float>(), gW2.data_ptr<float>(), B);
+  const int role = debug_role_only();  // 0: image blocks only, 1: dW2 slab-reduce blocks only
+  const int grid = role == 0 ? B : role == 1 ? 200 : B + 200;
+  conv1_wgrad_kernel<<<grid, 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (const u16*)g1.data_ptr(),
+                                               idx1.data_ptr<uint8_t>(), slab.data_ptr<float>(), G, gW1.data_ptr<float>(),
+                                               gb1.data_ptr<float>(), gW2.data_ptr<float>(), B, role == 1 ? B : 0);
 }
 
 }  // namespace mihvd

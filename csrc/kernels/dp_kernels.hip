@@ -9,8 +9,8 @@
 //                   adds the block total into fp64 accumulators (global fp64 atomics on gfx950).
 //   adasum_combine — same grid; each block turns the segment's (ab, aa, bb) into the two
 //                   coefficients and streams out = ca*a + cb*b (float4 when the segment allows).
-// Segments are given as an int64 offset table; the host wrapper covers gaps with extra segments so
-// padding (zero in a fusion buffer) is simply summed.
+// Segments are given as an int64 table [S+1 offsets | S flags]; the host wrapper covers gaps with
+// extra segments flagged "plain sum" (padding between tensors of a fusion buffer is not a tensor).
 //
 // Loss scaling (reference mixed_float16 policy, horovod/tensorflow_mnist_gpu.py:26-28; Keras wraps
 // the optimizer in a dynamic LossScaleOptimizer) keeps its whole state on the device in a float32
@@ -44,9 +44,10 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 }
 
 // Per-segment [lo, hi) -> this block's chunk [c0, c1).
-__device__ __forceinline__ bool chunk_of(const int64_t* offs, int64_t& c0, int64_t& c1) {
+__device__ __forceinline__ bool chunk_of(const int64_t* offs, int64_t& c0, int64_t& c1, bool skip_sum_segments) {
   const int s = blockIdx.y;
   const int64_t lo = offs[s], hi = offs[s + 1];
+  if (skip_sum_segments && offs[gridDim.y + 1 + s]) return false;  // plain-sum segment: no dots needed
   c0 = lo + (int64_t)blockIdx.x * kChunk;
   c1 = c0 + kChunk < hi ? c0 + kChunk : hi;
   return c0 < hi;
@@ -58,7 +59,7 @@ __global__ void __launch_bounds__(kDotThreads) segment_dots_kernel(const float* 
                                                                    double* __restrict__ out) {
   __shared__ float red[kDotThreads / 64];
   int64_t c0, c1;
-  if (!chunk_of(offs, c0, c1)) return;
+  if (!chunk_of(offs, c0, c1, true)) return;
   float ab = 0.f, aa = 0.f, bb = 0.f;
   // Scalar head until 16-byte alignment, float4 body, scalar tail: all loads of the body are
   // issued before any use (8 independent float4 per operand per thread).
@@ -112,11 +113,12 @@ __global__ void __launch_bounds__(kDotThreads) adasum_combine_kernel(const float
                                                                      const double* __restrict__ dots,
                                                                      float* __restrict__ out) {
   int64_t c0, c1;
-  if (!chunk_of(offs, c0, c1)) return;
+  if (!chunk_of(offs, c0, c1, false)) return;
+  const bool plain = offs[gridDim.y + 1 + blockIdx.y] != 0;
   const double ab = dots[3 * blockIdx.y], aa = dots[3 * blockIdx.y + 1], bb = dots[3 * blockIdx.y + 2];
   // |a| = 0 -> b ; |b| = 0 -> a ; both zero -> a + b (padding).
-  const float ca = bb > 0.0 ? (aa > 0.0 ? (float)(1.0 - ab / (2.0 * aa)) : 0.f) : 1.f;
-  const float cb = aa > 0.0 ? (bb > 0.0 ? (float)(1.0 - ab / (2.0 * bb)) : 0.f) : 1.f;
+  const float ca = plain ? 1.f : bb > 0.0 ? (aa > 0.0 ? (float)(1.0 - ab / (2.0 * aa)) : 0.f) : 1.f;
+  const float cb = plain ? 1.f : aa > 0.0 ? (bb > 0.0 ? (float)(1.0 - ab / (2.0 * bb)) : 0.f) : 1.f;
   const bool vec = (((c0 | c1) & 3) == 0) && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
                                                 reinterpret_cast<uintptr_t>(out)) & 15) == 0;
   if (vec) {
@@ -192,9 +194,10 @@ void segment_dots(const at::Tensor& a, const at::Tensor& b, const at::Tensor& of
   check_f32_cuda(a, "segment_dots(a)");
   check_f32_cuda(b, "segment_dots(b)");
   TORCH_CHECK(a.numel() == b.numel(), "segment_dots: size mismatch");
-  TORCH_CHECK(offs_dev.is_cuda() && offs_dev.dtype() == at::kLong && offs_dev.dim() == 1 && offs_dev.numel() >= 2,
-              "segment_dots: offs must be an int64 GPU vector of S+1 offsets");
-  const int64_t S = offs_dev.numel() - 1;
+  TORCH_CHECK(offs_dev.is_cuda() && offs_dev.dtype() == at::kLong && offs_dev.dim() == 1 && offs_dev.numel() >= 3 &&
+                  offs_dev.numel() % 2 == 1,
+              "segment_dots: offs must be an int64 GPU vector [S+1 offsets | S plain-sum flags]");
+  const int64_t S = offs_dev.numel() / 2;
   TORCH_CHECK(out.is_cuda() && out.dtype() == at::kDouble && out.numel() == 3 * S && out.is_contiguous(),
               "segment_dots: out must be fp64 [S,3]");
   TORCH_CHECK(S <= 65535, "segment_dots: too many segments");
@@ -211,7 +214,8 @@ void adasum_combine(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
   check_f32_cuda(b, "adasum_combine(b)");
   check_f32_cuda(out, "adasum_combine(out)");
   TORCH_CHECK(a.numel() == b.numel() && out.numel() == a.numel(), "adasum_combine: size mismatch");
-  const int64_t S = offs_dev.numel() - 1;
+  TORCH_CHECK(offs_dev.numel() % 2 == 1 && offs_dev.numel() >= 3, "adasum_combine: offs table");
+  const int64_t S = offs_dev.numel() / 2;
   TORCH_CHECK(dots.dtype() == at::kDouble && dots.numel() == 3 * S, "adasum_combine: dots must be fp64 [S,3]");
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const dim3 grid((unsigned)std::max<int64_t>(1, (max_seg_len + kChunk - 1) / kChunk), (unsigned)S);

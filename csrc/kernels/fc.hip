@@ -260,11 +260,11 @@ constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
 __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
     float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4, float* __restrict__ gb4,
-    float* __restrict__ gb2, float* __restrict__ gW1, float* __restrict__ gb1, int B) {
+    float* __restrict__ gb2, float* __restrict__ gW1, float* __restrict__ gb1, int B, int role_base) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
-  int bid = blockIdx.x;
+  int bid = blockIdx.x + role_base;
   if (bid < FB_WGRAD) {
     // dW3^T[n][j] tile = sum_b dz[b][n] a2[b][j]  -> stored as gW3[j][n..n+3] (float4 per lane)
     const int jt = bid >> 4, ntile = bid & 15;
@@ -461,10 +461,12 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_wgrad: fc grads");
   TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "fc1_wgrad: conv grads");
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  fc1_wgrad_kernel<<<FB_TOTAL, 256, FB_LDS_WG, stream>>>(
+  const int role = debug_role_only();  // 0: dW3 tiles only, 1: the small reductions only
+  const int grid = role == 0 ? FB_WGRAD : role == 1 ? FB_TOTAL - FB_WGRAD : FB_TOTAL;
+  fc1_wgrad_kernel<<<grid, 256, FB_LDS_WG, stream>>>(
       (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
       gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), gb2.data_ptr<float>(),
-      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B);
+      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, role == 1 ? FB_WGRAD : 0);
 }
 
 // dgrad: g2 = (a2 > 0) * dz.W3^T in bf16, the gradient conv2_bwd routes through the pool argmax.

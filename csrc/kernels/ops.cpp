@@ -23,7 +23,8 @@ void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, con
                  at::Tensor& gW2);
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
-               double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale);
+               double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale,
+               int64_t max_blocks);
 void scale_cast_bf16(const at::Tensor& src, at::Tensor& dst, double scale);
 void bf16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale);
 void segment_dots(const at::Tensor& a, const at::Tensor& b, const at::Tensor& offs_dev, int64_t max_seg_len,
@@ -66,8 +67,9 @@ void conv1_wgrad_op(const Tensor& x, const OptT& rows, const OptT& state, const 
 }
 void adam_op(Tensor p, const Tensor& g, Tensor m, Tensor v, const OptT& shadow, const OptT& state, int64_t host_step,
              double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, int64_t bump,
-             const OptT& loss_scale) {
-  mihvd::adam_step(p, g, m, v, shadow, state, host_step, lr, b1, b2, eps, grad_scale, rule, bump, loss_scale);
+             const OptT& loss_scale, int64_t max_blocks) {
+  mihvd::adam_step(p, g, m, v, shadow, state, host_step, lr, b1, b2, eps, grad_scale, rule, bump, loss_scale,
+                   max_blocks);
 }
 void scale_cast_op(const Tensor& src, Tensor dst, double scale) { mihvd::scale_cast_bf16(src, dst, scale); }
 void bf16_to_f32_op(const Tensor& src, Tensor dst, double scale) { mihvd::bf16_to_f32(src, dst, scale); }
@@ -99,7 +101,7 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(b!) gb1, Tensor(c!) gW2) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
         "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1, "
-        "Tensor? loss_scale=None) -> ()");
+        "Tensor? loss_scale=None, int max_blocks=0) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("segment_dots(Tensor a, Tensor b, Tensor offs, int max_seg_len, Tensor(a!) out) -> ()");

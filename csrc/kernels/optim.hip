@@ -83,7 +83,8 @@ static int grid_for(int64_t n4) {
 
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
-               double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale) {
+               double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale,
+               int64_t max_blocks) {
   const int64_t n = p.numel();
   TORCH_CHECK(p.dtype() == at::kFloat && g.dtype() == at::kFloat && m.dtype() == at::kFloat && v.dtype() == at::kFloat,
               "adam_step: fp32 buffers expected");
@@ -103,7 +104,11 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
     ls = loss_scale->data_ptr<float>();
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  adam_kernel<<<grid_for(n / 4), 256, 0, stream>>>(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+  // max_blocks > 0 caps the grid (grid-stride loop): a capped update sharing the GPU with
+  // another stream's kernels leaves CUs to them instead of queueing thousands of blocks ahead.
+  int grid = grid_for(n / 4);
+  if (max_blocks > 0) grid = std::min<int>(grid, (int)max_blocks);
+  adam_kernel<<<grid, 256, 0, stream>>>(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                                                    v.data_ptr<float>(), sp, n / 4, st, host_step, (float)lr, (float)b1,
                                                    (float)b2, (float)eps, (float)grad_scale, (int)rule, (int)bump, ls);
 }

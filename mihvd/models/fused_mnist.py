@@ -121,7 +121,12 @@ class FusedMNISTTrainer:
         # Overlap the "fc" bucket's allreduce with the conv backward on a side stream (N > 1). A
         # stream fork/join costs a few us inside a HIP graph, so it is only used with collectives.
         self.overlap = os.environ.get("MIHVD_OVERLAP", "1") != "0"
-        self._side = torch.cuda.Stream(device=dev) if self.collectives else None
+        # MIHVD_ADAM_PIPELINE=1: the "fc" part of the Adam update runs on a side stream after the
+        # last reader of W3 (fc1_dgrad) and overlaps the conv backward and the next step's convs.
+        self.pipeline = os.environ.get("MIHVD_ADAM_PIPELINE", "0") == "1"
+        self.adam_blocks = int(os.environ.get("MIHVD_ADAM_BLOCKS", "0"))
+        self._fc_update_pending = False
+        self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline) else None
         if compression == "bf16" and self.collectives:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
         else:
@@ -173,40 +178,70 @@ class FusedMNISTTrainer:
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
         o = self.ops
-        B = self.B
         st = self.state
+        main = torch.cuda.current_stream(self.device)
         o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
                     self.a1, self.idx1)
         o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
                     self.a2, self.idx2)
+        if self._fc_update_pending:
+            # the previous step's "fc" Adam update (side stream) overlapped the two convolutions above
+            main.wait_stream(self._side)
+            self._fc_update_pending = False
         o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
                     self.gview("dense_1/kernel"), self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
                     self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
-        main = torch.cuda.current_stream(self.device)
         fc_bucket = self.grads[FC_START:]
         conv_bucket = self.grads[:FC_START]
         overlap = self.collectives and self.overlap
+        ar_done = None
         if overlap:
             # bucket "fc" is complete: reduce it on the side stream while the conv backward runs
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
                 self._allreduce(fc_bucket, FC_START, FLAT_NUMEL)
+                if self.pipeline:
+                    ar_done = torch.cuda.Event()
+                    ar_done.record(self._side)
         o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
+        b1, b2 = self.betas
+        if self.pipeline:
+            # fc1_dgrad was the last reader of W3: the "fc" update (98 % of the optimizer bytes) runs
+            # on the side stream, overlapping the conv backward and the next step's convolutions.
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                o.adam_step(self.params[FC_START:], fc_bucket, self.m[FC_START:], self.v[FC_START:],
+                            self.shadow[FC_START:], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 0,
+                            None, self.adam_blocks)
+            self._fc_update_pending = True
         o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1, self.slab,
                     self.gview("conv_layer2/conv2d/bias"))
         o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),
                       self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/kernel"))
+        if self.pipeline:
+            if self.collectives:
+                if ar_done is not None:
+                    main.wait_event(ar_done)  # one collective at a time on the communicator
+                self._allreduce(conv_bucket, 0, FC_START)
+            o.adam_step(self.params[:FC_START], conv_bucket, self.m[:FC_START], self.v[:FC_START],
+                        self.shadow[:FC_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+            return
         if overlap:
             self._allreduce(conv_bucket, 0, FC_START)
             main.wait_stream(self._side)
         elif self.collectives:
             self._allreduce(self.grads, 0, FLAT_NUMEL)  # one fused collective for the whole buffer
-        b1, b2 = self.betas
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
+
+    def _join(self):
+        """Make the current stream wait for any side-stream work of the last step."""
+        if self._fc_update_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._fc_update_pending = False
 
     def _allreduce(self, bucket, lo, hi):
         import torch.distributed as dist
@@ -234,6 +269,7 @@ class FusedMNISTTrainer:
         self.y_buf.copy_(y.reshape(self.B), non_blocking=True)
         # Host-fed batches index rows 0..B-1 of x_buf (rows=None); the step counter still advances.
         self._launch_step(self.x_buf, None, self.y_buf)
+        self._join()
         self.global_step += 1
         return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
 
@@ -243,6 +279,7 @@ class FusedMNISTTrainer:
             raise RuntimeError("call set_device_dataset() first")
         self._maybe_reshuffle(1)
         self._launch_step(self.X, self.rows, self.Y)
+        self._join()
         self.global_step += 1
         return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
 
@@ -278,11 +315,13 @@ class FusedMNISTTrainer:
                 with torch.cuda.graph(g, stream=s):
                     for _ in range(steps_per_replay):
                         self._launch_step(self.X, self.rows, self.Y)
+                    self._join()
         except Exception as e:  # pragma: no cover - depends on the RCCL build
             import warnings
 
             warnings.warn(f"HIP graph capture failed ({e!r}); falling back to eager steps")
             self.graph = None
+            self._fc_update_pending = False
             torch.cuda.synchronize(self.device)
             return False
         torch.cuda.current_stream(self.device).wait_stream(s)

@@ -43,18 +43,22 @@ def _segment_dots(a: torch.Tensor, b: torch.Tensor, segments: Sequence[tuple[int
 _OFFS_CACHE: dict = {}
 
 
-def _covering_offsets(segments: Sequence[tuple[int, int]], n: int) -> list[int]:
-    """Offsets of a segment table that covers [0, n): gaps become segments of their own (zero
-    padding in a fusion buffer, which the combine then simply sums)."""
-    offs = [0]
+def _covering_offsets(segments: Sequence[tuple[int, int]], n: int) -> tuple[list[int], list[int]]:
+    """(offsets, plain_sum_flags) of a segment table covering [0, n): gaps between the given
+    segments become segments of their own that are summed, not Adasum-combined (as in
+    ``adasum_pair``'s torch path)."""
+    offs, flags = [0], []
     for s, e in sorted(segments):
         if s > offs[-1]:
             offs.append(s)
+            flags.append(1)
         if e > offs[-1]:
             offs.append(e)
+            flags.append(0)
     if offs[-1] < n:
         offs.append(n)
-    return offs
+        flags.append(1)
+    return offs, flags
 
 
 def _hip_pair(a: torch.Tensor, b: torch.Tensor, segments) -> torch.Tensor:
@@ -63,9 +67,9 @@ def _hip_pair(a: torch.Tensor, b: torch.Tensor, segments) -> torch.Tensor:
     key = (tuple(segments), a.numel(), a.device)
     hit = _OFFS_CACHE.get(key)
     if hit is None:
-        offs = _covering_offsets(segments, a.numel())
+        offs, flags = _covering_offsets(segments, a.numel())
         max_len = max(e - s for s, e in zip(offs[:-1], offs[1:]))
-        hit = (torch.tensor(offs, dtype=torch.int64, device=a.device), max_len,
+        hit = (torch.tensor(offs + flags, dtype=torch.int64, device=a.device), max_len,
                torch.empty(3 * (len(offs) - 1), dtype=torch.float64, device=a.device))
         _OFFS_CACHE[key] = hit
     offs_dev, max_len, dots = hit

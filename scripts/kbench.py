@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--json", default="")
+    ap.add_argument("--roles", action="store_true", help="also time each block role of multi-role launches")
     args = ap.parse_args()
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
@@ -50,9 +51,17 @@ def main():
                                              tr.gview("conv_layer2/conv2d/kernel")),
         "adam": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, sh, st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
     }
+    jobs = [(name, fn, None) for name, fn in ops.items()]
+    if args.roles:  # MIHVD_ROLE_ONLY is read by the host wrappers at launch (i.e. capture) time
+        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv1_wgrad", 2)):
+            jobs += [(f"{name}[role{r}]", ops[name], r) for r in range(n_roles)]
     res = {}
     s = torch.cuda.Stream()
-    for name, fn in ops.items():
+    for name, fn, role in jobs:
+        if role is None:
+            os.environ.pop("MIHVD_ROLE_ONLY", None)
+        else:
+            os.environ["MIHVD_ROLE_ONLY"] = str(role)
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -68,7 +77,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         res[name] = e0.elapsed_time(e1) * 1000.0 / args.iters
-        print(f"{name:12s} {res[name]:8.2f} us", flush=True)
+        print(f"{name:18s} {res[name]:8.2f} us", flush=True)
+    os.environ.pop("MIHVD_ROLE_ONLY", None)
     # whole step, graph-replayed
     from mihvd.utils.data import synthetic_mnist
 
@@ -86,7 +96,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     res["step"] = e0.elapsed_time(e1) * 1000.0 / 200
-    res["sum_kernels"] = sum(v for k, v in res.items() if k != "step")
+    res["sum_kernels"] = sum(v for k, v in res.items() if k != "step" and "[" not in k)
     print(f"{'step':12s} {res['step']:8.2f} us   (sum of kernels {res['sum_kernels']:.2f} us)", flush=True)
     if args.json:
         with open(args.json, "w") as f:

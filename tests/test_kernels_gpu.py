@@ -398,3 +398,28 @@ def test_adam_loss_scale_fused(ops):
         outs.append(p)
     assert torch.allclose(outs[0], outs[1], atol=1e-7)
     assert torch.equal(outs[2], p0)  # overflow step skipped
+
+
+def test_adam_pipeline_matches_serial(ops, monkeypatch):
+    """MIHVD_ADAM_PIPELINE=1 (fc Adam on a side stream, overlapping the conv backward and the next
+    step's convolutions, graph-captured) trains like the serial step."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    g = torch.Generator(device="cuda").manual_seed(21)
+    X = torch.rand(400, 784, device="cuda", generator=g)
+    Y = torch.randint(0, 10, (400,), device="cuda", generator=g)
+    out = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("MIHVD_ADAM_PIPELINE", pipe)
+        monkeypatch.setenv("MIHVD_ADAM_BLOCKS", "128" if pipe == "1" else "0")
+        tr = FusedMNISTTrainer(batch_size=100, seed=4, device="cuda", dropout=0.0)
+        assert tr.pipeline == (pipe == "1")
+        tr.set_device_dataset(X, Y, shuffle=False)
+        tr.build_graph(steps_per_replay=4, warmup=2)
+        tr.run_graph()
+        torch.cuda.synchronize()
+        out.append((tr.params.clone(), tr.last_loss(), int(tr.state[0]), int(tr.state[1])))
+    (p0, l0, f0, t0), (p1, l1, f1, t1) = out
+    assert (f0, t0) == (f1, t1) == (6, 6)
+    assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0))
+    assert rel_err(p1, p0) < 1e-5

@@ -306,6 +306,6 @@ def test_synthetic_data_and_generator():
 def test_adasum_covering_offsets():
     from mihvd.parallel.adasum import _covering_offsets
 
-    assert _covering_offsets([(0, 5), (8, 10)], 12) == [0, 5, 8, 10, 12]
-    assert _covering_offsets([(0, 12)], 12) == [0, 12]
-    assert _covering_offsets([(2, 4)], 4) == [0, 2, 4]
+    assert _covering_offsets([(0, 5), (8, 10)], 12) == ([0, 5, 8, 10, 12], [0, 1, 0, 1])
+    assert _covering_offsets([(0, 12)], 12) == ([0, 12], [0])
+    assert _covering_offsets([(2, 4)], 4) == ([0, 2, 4], [1, 0])
