@@ -10,8 +10,8 @@
 //   * wgrad (kernel row kh x group of 4 images): dW2 as an MFMA GEMM over pixels with both operands
 //     read by ds_read_b64_tr_b16 from natural NHWC images; two 4-wave groups take two images each
 //     and are summed in LDS; one fp32 partial slab per block (deterministic, no atomics).
-// conv1_wgrad: dW1/db1 from the sparse routed gradient (one of four conv1 outputs per pooling
-//   window is non-zero, so VALU on the pooled gradient), plus the dW2 slab reduction.
+// conv1_wgrad: dW1/db1 as an MFMA GEMM over full-resolution pixels (the routed gradient is
+//   scattered into LDS, im2col(x) is read from kw-shifted image copies), plus the dW2 slab reduction.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -22,10 +22,14 @@ namespace mihvd {
 constexpr int CB_IPB = 4;               // images per wgrad block (2 per wave group)
 constexpr int CB_KQ = 4;                // fc1 dgrad split-K slabs
 constexpr int CB_WSTR = 72;             // W2 image row stride (dgrad) and dY2 image row stride (wgrad)
-// dgrad LDS: W2 [800][72] | D [18*18][64]
+// dgrad LDS: W2 [800][72] | D [18*18][72]. Both row strides are 144 B (36 banks): the 16
+// consecutive rows a ds_read_b128 lane group touches land on distinct banks (a 128-B pixel stride
+// would put every other pixel on the same banks: 8-way conflicts on each B-fragment read).
+constexpr int CB_DSTR = 72;
 constexpr int CB_DG_W = 800 * CB_WSTR;
-constexpr int CB_DG_D = 324 * 64;
-constexpr int CB_DG_LDS = (CB_DG_W + CB_DG_D) * 2;                 // 156,672 B
+constexpr int CB_DG_D = 324 * CB_DSTR;
+constexpr int CB_DG_LDS = (CB_DG_W + CB_DG_D) * 2;                 // 161,856 B
+static_assert(CB_DG_LDS <= 163840, "dgrad LDS");
 // wgrad LDS per wave group: A [325][32] | Dm [197][72]
 constexpr int CB_WG_A = 325 * 32;
 constexpr int CB_WG_D = 197 * CB_WSTR;
@@ -84,7 +88,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     // ===================================================================== dgrad: image b
     const int b = blockIdx.x;
     u16* Ws = smem;              // [800][72]  row = kk*32 + ci, cols = co
-    u16* D = smem + CB_DG_W;     // [18*18][64] padded dY2 image
+    u16* D = smem + CB_DG_W;     // [18*18][72] padded dY2 image
     // Issue every load of the block first: W2 (13 x 16 B per thread) and 2 dY2 items.
     DyItem items[2];
     int ie[2];
@@ -101,7 +105,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     for (int i = t; i < 324 * 8; i += 512) {
       const int pix = i >> 3, c = i & 7;
       const int y = pix / 18, x = pix - y * 18;
-      if (y < 2 || y >= 16 || x < 2 || x >= 16) *reinterpret_cast<uint4*>(D + pix * 64 + c * 8) = make_uint4(0, 0, 0, 0);
+      if (y < 2 || y >= 16 || x < 2 || x >= 16) *reinterpret_cast<uint4*>(D + pix * CB_DSTR + c * 8) = make_uint4(0, 0, 0, 0);
     }
     float db[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -113,10 +117,19 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
         finish_dy_item(items[k], g, d, gf);
 #pragma unroll
         for (int c = 0; c < 4; ++c) db[c] += gf[c];
-        scatter_window(D, 64, ie[k] >> 4, (ie[k] & 15) * 4, g, d, true);
+        scatter_window(D, CB_DSTR, ie[k] >> 4, (ie[k] & 15) * 4, g, d, true);
       }
     }
     __syncthreads();
+    // conv1's pooled-ReLU mask for the epilogue, fetched now so its latency hides under the GEMM
+    uint2 amask[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = min((wave + 8 * i) * 16 + lr, 195);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        amask[i][nt] = *reinterpret_cast<const uint2*>(a1 + ((int64_t)b * 196 + m) * 32 + nt * 16 + 4 * lg);
+    }
     // GEMM: rows = ci (2 tiles), cols = pixels (13 tiles: wave w, w+8), K = (kh, kw, co) = 1600.
     f32x4 acc[2][2];
 #pragma unroll
@@ -128,11 +141,11 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       int m = (wave + 8 * i) * 16 + lr;
       if (m >= 196) m = 0;
       const int y = m / 14, x = m - (m / 14) * 14;
-      pbase[i] = ((y + 4) * 18 + (x + 4)) * 64 + 8 * lg;
+      pbase[i] = ((y + 4) * 18 + (x + 4)) * CB_DSTR + 8 * lg;
     }
     for (int kk = 0; kk < 25; ++kk) {
       const int kh = kk / 5, kw = kk - kh * 5;
-      const int aoff = -(kh * 18 + kw) * 64;
+      const int aoff = -(kh * 18 + kw) * CB_DSTR;
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
         const u16* wr = Ws + (kk * 32 + lr) * CB_WSTR + ch * 32 + 8 * lg;
@@ -155,7 +168,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int64_t o = ((int64_t)b * 196 + m) * 32 + nt * 16 + 4 * lg;
-        const uint2 av = *reinterpret_cast<const uint2*>(a1 + o);
+        const uint2 av = amask[i][nt];
         const float m0 = bf2f((u16)(av.x & 0xffff)) > 0.f ? acc[i][nt][0] : 0.f;
         const float m1 = bf2f((u16)(av.x >> 16)) > 0.f ? acc[i][nt][1] : 0.f;
         const float m2 = bf2f((u16)(av.y & 0xffff)) > 0.f ? acc[i][nt][2] : 0.f;
@@ -279,14 +292,31 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------ //
-// conv1_wgrad: blocks [0, B): one image each -> atomics into gW1/gb1; blocks [B, B+50): dW2 slabs.
+// conv1_wgrad: blocks [0, B): one image each, dW1/db1 -> atomics; blocks [B, B+200): dW2 slabs.
+//
+// The image role is an MFMA GEMM over the full-resolution pixels of the image:
+//     dW1^T[co][tap] = sum_pix dY1^T[co][pix] * im2col(x)[pix][tap]      (M = 32, N = 25 -> 32)
+// with K = 28 rows x 32 columns (columns 28..31 are dummy pixels whose dY1 row is the zero row).
+//   * dY1 ([785][40] bf16, pixel rows) is scattered from the pooled gradient g1 through the argmax
+//     slots idx1 (each pooling window writes its four sub-pixels, value or zero), so every pixel
+//     row is written once and only the zero row needs clearing; it is read by transposed LDS
+//     reads (ds_read_b64_tr_b16) as the A operand.
+//   * im2col(x) is never built: the B fragment of tap (kh, kw) for 8 consecutive pixels of a row
+//     is 8 consecutive elements of the zero-padded image row y + kh starting at column x0 + kw.
+//     Five copies of the bf16 image shifted by kw = 0..4 make that one aligned ds_read_b128.
+//   * the four waves split K (7 image rows each) and are summed through LDS before the atomics.
 // ------------------------------------------------------------------------------------------ //
+constexpr int C1_DSTR = 40;                          // dY1 row stride (32 co + 8 pad)
+constexpr int C1_DY = 785 * C1_DSTR;                 // elements; row 784 = zeros
+constexpr int C1_XS = 32 * 32;                       // one shifted bf16 image copy [32][32]
+constexpr int C1_LDS = (C1_DY + 5 * C1_XS + 8) * 2 + 32 * 36 * 4;  // + zero chunk + fp32 staging
+static_assert(4 * 64 * 16 * 4 <= C1_DY * 2, "wave partials reuse the dY1 image");
+
 __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const u16* __restrict__ g1, const uint8_t* __restrict__ idx1, const float* __restrict__ slab, int nslab,
     float* __restrict__ gW1, float* __restrict__ gb1, float* __restrict__ gW2, int B, int role_base) {
-  __shared__ float img[32][33];
-  __shared__ float red[8][26][32];
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x;
   const int bid = (int)blockIdx.x + role_base;
   if (bid >= B) {
@@ -297,14 +327,14 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int g = sg * 8 + k;
-      const float4 x = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[min(o, 12799)];
+      const float4 xv = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[min(o, 12799)];
       const bool keep = g < nslab;
-      v[k] = make_float4(mask_f(x.x, keep), mask_f(x.y, keep), mask_f(x.z, keep), mask_f(x.w, keep));
+      v[k] = make_float4(mask_f(xv.x, keep), mask_f(xv.y, keep), mask_f(xv.z, keep), mask_f(xv.w, keep));
     }
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
-    float4* r4 = reinterpret_cast<float4*>(&red[0][0][0]);
+    float4* r4 = reinterpret_cast<float4*>(smem);
     r4[t] = s;
     __syncthreads();
     if (t < 64 && o < 12800) {
@@ -321,60 +351,127 @@ __global__ void __launch_bounds__(256) conv1_wgrad_kernel(
     const int64_t step = state ? state[ST_FWD] : 0;
     row = rows[(int)((step * (int64_t)B + b) % n_pool)];
   }
-  const int co = t & 31, grp = t >> 5;
-  // loads first: this thread's 25 pooled gradients + argmax slots, and the image
-  u16 gv[25];
-  uint8_t dv[25];
-#pragma unroll
-  for (int i = 0; i < 25; ++i) {
-    const int pos = min(grp + 8 * i, 195);
-    const int64_t o = (int64_t)b * 6272 + pos * 32 + co;
-    gv[i] = g1[o];
-    dv[i] = idx1[o];
-  }
-  const float* xi = x + (int64_t)row * 784;
+  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int q = lr >> 2, p = lr & 3;
+  u16* Dy = smem;                                          // [785][40]
+  u16* Xs = smem + C1_DY;                                  // 5 x [32][32] shifted bf16 images
+  u16* Zc = Xs + 5 * C1_XS;                                // 8 zero elements (dummy taps)
+  float* Xf = reinterpret_cast<float*>(Zc + 8);            // [32][36] fp32 padded image
+  // ---- loads first: the image (4 values per thread) and 6 pooled-gradient items (4 co each)
   float xv[4];
+  const float* xi = x + (int64_t)row * 784;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int i = t + 256 * k;
+    const int i = t + 256 * k;  // [32][32] padded positions
     const int r = i >> 5, c = i & 31;
     const int gy = r - 2, gx = c - 2;
     const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
-    const float v = xi[in ? gy * 28 + gx : 0];
-    xv[k] = mask_f(v, in);
+    xv[k] = mask_f(xi[in ? gy * 28 + gx : 0], in);
   }
+  uint2 gv[7];
+  uint32_t dv[7];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) img[(t + 256 * k) >> 5][(t + 256 * k) & 31] = xv[k];
-  __syncthreads();
-  float acc[25], accb = 0.f;
+  for (int k = 0; k < 7; ++k) {  // 196 windows x 8 channel quads = 1568 items
+    const int i = min(t + 256 * k, 1567);
+    const int64_t o = (int64_t)b * 6272 + (i >> 3) * 32 + (i & 7) * 4;
+    gv[k] = *reinterpret_cast<const uint2*>(g1 + o);
+    dv[k] = *reinterpret_cast<const uint32_t*>(idx1 + o);
+  }
+  // ---- LDS images
 #pragma unroll
-  for (int k = 0; k < 25; ++k) acc[k] = 0.f;
+  for (int k = 0; k < 4; ++k) {
+    const int i = t + 256 * k;
+    Xf[(i >> 5) * 36 + (i & 31)] = xv[k];
+  }
+  if (t < 32) Xf[t * 36 + 32] = Xf[t * 36 + 33] = Xf[t * 36 + 34] = Xf[t * 36 + 35] = 0.f;
+  if (t < 5) reinterpret_cast<uint4*>(Dy + 784 * C1_DSTR)[t] = make_uint4(0, 0, 0, 0);
+  if (t == 5) *reinterpret_cast<uint4*>(Zc) = make_uint4(0, 0, 0, 0);
+  float db[4] = {0.f, 0.f, 0.f, 0.f};  // every item of a thread has channel quad (t & 7)
 #pragma unroll
-  for (int i = 0; i < 25; ++i) {
-    const int pos = grp + 8 * i;
-    const float g = bf2f(gv[i]);
-    if (pos < 196 && g != 0.f) {
-      const int d = dv[i];
-      const int py = pos / 14, px = pos - py * 14;
-      const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
-      accb += g;
+  for (int k = 0; k < 7; ++k) {
+    const int i = t + 256 * k;
+    if (i < 1568) {
+      const int win = i >> 3, co4 = (i & 7) * 4;
+      const int py = win / 14, px = win - py * 14;
+      const u16 g[4] = {(u16)(gv[k].x & 0xffff), (u16)(gv[k].x >> 16), (u16)(gv[k].y & 0xffff), (u16)(gv[k].y >> 16)};
+      int d[4];
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
+      for (int c = 0; c < 4; ++c) {
+        d[c] = (dv[k] >> (8 * c)) & 3;
+        db[c] += bf2f(g[c]);
+      }
 #pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(g, img[y + kh][xx + kw], acc[kh * 5 + kw]);
+      for (int dd = 0; dd < 4; ++dd) {
+        const int pix = (2 * py + (dd >> 1)) * 28 + 2 * px + (dd & 1);
+        const uint32_t lo = (uint32_t)(d[0] == dd ? g[0] : 0) | ((uint32_t)(d[1] == dd ? g[1] : 0) << 16);
+        const uint32_t hi = (uint32_t)(d[2] == dd ? g[2] : 0) | ((uint32_t)(d[3] == dd ? g[3] : 0) << 16);
+        *reinterpret_cast<uint2*>(Dy + pix * C1_DSTR + co4) = make_uint2(lo, hi);
+      }
     }
   }
-#pragma unroll
-  for (int k = 0; k < 25; ++k) red[grp][k][co] = acc[k];
-  red[grp][25][co] = accb;
   __syncthreads();
-  for (int i = t; i < 26 * 32; i += 256) {
-    const int k = i >> 5, c = i & 31;
-    float s = 0.f;
+  // five kw-shifted bf16 copies: Xs[kw][r][c] = P[r][c + kw]  (640 chunks of 8 elements)
+  for (int i = t; i < 5 * 32 * 4; i += 256) {
+    const int kw = i >> 7, r = (i >> 2) & 31, c0 = (i & 3) * 8;
+    const float* src = Xf + r * 36 + c0 + kw;
+    *reinterpret_cast<uint4*>(Xs + kw * C1_XS + r * 32 + c0) =
+        make_uint4((uint32_t)f2bf(src[0]) | ((uint32_t)f2bf(src[1]) << 16), (uint32_t)f2bf(src[2]) | ((uint32_t)f2bf(src[3]) << 16),
+                   (uint32_t)f2bf(src[4]) | ((uint32_t)f2bf(src[5]) << 16), (uint32_t)f2bf(src[6]) | ((uint32_t)f2bf(src[7]) << 16));
+  }
+  __syncthreads();
+  // ---- GEMM: wave w takes image rows y = 7w .. 7w+6 (one 32-pixel K step each)
+  int boff[2];  // B fragment base per tap tile: copy kw, row offset kh, this lane's 8-pixel group
 #pragma unroll
-    for (int g = 0; g < 8; ++g) s += red[g][k][c];
-    if (k < 25) atomicAdd(gW1 + k * 32 + c, s);
-    else atomicAdd(gb1 + c, s);
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = nt * 16 + lr;
+    const int kh = n / 5, kw = n - (n / 5) * 5;
+    boff[nt] = n < 25 ? kw * C1_XS + kh * 32 + 8 * lg : -1;
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int yy = 0; yy < 7; ++yy) {
+    const int y = wave * 7 + yy;
+    const int x0 = 8 * lg + q, x1 = x0 + 4;
+    const int r0 = x0 < 28 ? y * 28 + x0 : 784, r1 = x1 < 28 ? y * 28 + x1 : 784;
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+      af[mt] = frag_tr(Dy + r0 * C1_DSTR + mt * 16 + 4 * p, Dy + r1 * C1_DSTR + mt * 16 + 4 * p);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bfr[nt] = frag_ld128(boff[nt] >= 0 ? Xs + boff[nt] + y * 32 : Zc);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16(af[mt], bfr[nt], acc[mt][nt]);
+  }
+  // ---- sum the four waves (partials reuse the dY1 image) and the db1 partials, then atomics
+  __syncthreads();
+  float* part = reinterpret_cast<float*>(smem);  // [4 waves][64 lanes][16]
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      *reinterpret_cast<float4*>(part + (wave * 64 + lane) * 16 + (mt * 2 + nt) * 4) =
+          make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
+  float* dbp = part + 4 * 64 * 16;  // [256][4]
+  *reinterpret_cast<float4*>(dbp + t * 4) = make_float4(db[0], db[1], db[2], db[3]);
+  __syncthreads();
+  // C[row = co = 16mt + 4lg' + i][col = tap = 16nt + lr'] lives in lane (lg', lr') slot (mt, nt, i)
+  for (int o = t; o < 800; o += 256) {
+    const int tap = o >> 5, co = o & 31;
+    const int nt = tap >> 4, lrr = tap & 15, mt = co >> 4, lgg = (co >> 2) & 3, i = co & 3;
+    const int ln = lgg * 16 + lrr, slot = (mt * 2 + nt) * 4 + i;
+    const float v = (part[(0 * 64 + ln) * 16 + slot] + part[(1 * 64 + ln) * 16 + slot]) +
+                    (part[(2 * 64 + ln) * 16 + slot] + part[(3 * 64 + ln) * 16 + slot]);
+    atomicAdd(gW1 + o, v);  // HWIO: tap * 32 + co
+  }
+  if (t < 32) {
+    // channel t: quad t >> 2 was accumulated by the 32 threads with (tid & 7) == t >> 2
+    float sdb = 0.f;
+    for (int r = t >> 2; r < 256; r += 8) sdb += dbp[r * 4 + (t & 3)];
+    atomicAdd(gb1 + t, sdb);
   }
 }
 
@@ -421,7 +518,12 @@ void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, con
   TORCH_CHECK(G <= 32, "conv1_wgrad: at most 32 wgrad slabs");
   const int role = debug_role_only();  // 0: image blocks only, 1: dW2 slab-reduce blocks only
   const int grid = role == 0 ? B : role == 1 ? 200 : B + 200;
-  conv1_wgrad_kernel<<<grid, 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (const u16*)g1.data_ptr(),
+  static bool attr = [] {
+    hipFuncSetAttribute((const void*)conv1_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, C1_LDS);
+    return true;
+  }();
+  (void)attr;
+  conv1_wgrad_kernel<<<grid, 256, C1_LDS, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (const u16*)g1.data_ptr(),
                                                idx1.data_ptr<uint8_t>(), slab.data_ptr<float>(), G, gW1.data_ptr<float>(),
                                                gb1.data_ptr<float>(), gW2.data_ptr<float>(), B, role == 1 ? B : 0);
 }

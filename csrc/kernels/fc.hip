@@ -247,9 +247,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 }
 
 // ------------------------------------------------------------------------------------------ //
-// fc1_wgrad roles by blockIdx.x:
-//   [0, 784)       wgrad : 64x64 tile of dW3 = a2^T dz   (K = batch, zero padded)
-//   next 16        db3   ; next 16: dW4 ; last: db4 + zero gb2/gW1/gb1 (atomic targets)
+// fc1_wgrad roles (dispatch order: the 33 small blocks first, then the 784 dW3 tiles):
+//   wgrad : 64x64 tile of dW3 = a2^T dz   (K = batch, zero padded)
+//   db3 (16 blocks), dW4 (16 blocks), misc: db4 + zero gb2/gW1/gb1 (atomic targets)
 // ------------------------------------------------------------------------------------------ //
 constexpr int FB_WGRAD = (FC1_K / 64) * (FC1_N / 64);            // 784
 constexpr int FB_DB3 = FC1_N / 64, FB_DW4 = FC1_N / 64, FB_MISC = 1;  // 16 + 16 + 1 blocks
@@ -264,7 +264,11 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
+  // The 33 small-reduction blocks come first in dispatch order so they run alongside the dW3 tiles
+  // instead of trailing them.
+  constexpr int NS = FB_TOTAL - FB_WGRAD;
   int bid = blockIdx.x + role_base;
+  bid = bid < NS ? FB_WGRAD + bid : bid - NS;
   if (bid < FB_WGRAD) {
     // dW3^T[n][j] tile = sum_b dz[b][n] a2[b][j]  -> stored as gW3[j][n..n+3] (float4 per lane)
     const int jt = bid >> 4, ntile = bid & 15;
@@ -466,7 +470,7 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   fc1_wgrad_kernel<<<grid, 256, FB_LDS_WG, stream>>>(
       (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
       gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), gb2.data_ptr<float>(),
-      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, role == 1 ? FB_WGRAD : 0);
+      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, role == 0 ? FB_TOTAL - FB_WGRAD : 0);
 }
 
 // dgrad: g2 = (a2 > 0) * dz.W3^T in bf16, the gradient conv2_bwd routes through the pool argmax.

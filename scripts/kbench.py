@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--json", default="")
     ap.add_argument("--roles", action="store_true", help="also time each block role of multi-role launches")
+    ap.add_argument("--only", default="", help="comma-separated job names (e.g. 'conv2_bwd[role0]'); skips the step")
     args = ap.parse_args()
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
@@ -55,6 +56,9 @@ def main():
     if args.roles:  # MIHVD_ROLE_ONLY is read by the host wrappers at launch (i.e. capture) time
         for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv1_wgrad", 2)):
             jobs += [(f"{name}[role{r}]", ops[name], r) for r in range(n_roles)]
+    if args.only:
+        keep = set(args.only.split(","))
+        jobs = [j for j in jobs if j[0] in keep]
     res = {}
     s = torch.cuda.Stream()
     for name, fn, role in jobs:
@@ -79,6 +83,11 @@ def main():
         res[name] = e0.elapsed_time(e1) * 1000.0 / args.iters
         print(f"{name:18s} {res[name]:8.2f} us", flush=True)
     os.environ.pop("MIHVD_ROLE_ONLY", None)
+    if args.only:
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     # whole step, graph-replayed
     from mihvd.utils.data import synthetic_mnist
 
