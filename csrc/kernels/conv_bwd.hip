@@ -1,12 +1,13 @@
 // Backward convolutions of the MNIST CNN.
 //
 // conv2_bwd (one launch, 512-thread blocks, two roles):
-//   * The routed conv2 output gradient dY2 is built on the fly in LDS: the four fc1-dgrad split-K
-//     slabs are summed, masked with conv2's pooled ReLU (a2 > 0) and scattered through the argmax
-//     indices idx2 (4 co per lane -> four 8-byte LDS writes). dY2 never exists in HBM.
+//   * The routed conv2 output gradient dY2 is built on the fly in LDS from g2 (fc1_dgrad's bf16
+//     output, already masked with conv2's pooled ReLU) scattered through the argmax indices idx2
+//     (4 co per lane -> four 8-byte LDS writes). dY2 never exists in HBM.
 //   * dgrad (one block per image): dA1 = full correlation of dY2 with W2 as an implicit GEMM
-//     (K = 25 taps x 64 channels), W2 resident in LDS (115 KB), output features on the MFMA row
-//     axis; conv1's pooled ReLU mask is applied in the epilogue -> g1 (bf16). db2 is reduced here.
+//     (K = 25 taps x 64 channels), W2 resident in LDS (100 KB, swizzled), output features on the
+//     MFMA row axis and one image row per pixel tile; conv1's pooled ReLU mask is applied in the
+//     epilogue -> g1 (bf16). db2 is reduced here.
 //   * wgrad (kernel row kh x group of 4 images): dW2 as an MFMA GEMM over pixels with both operands
 //     read by ds_read_b64_tr_b16 from natural NHWC images; two 4-wave groups take two images each
 //     and are summed in LDS; one fp32 partial slab per block (deterministic, no atomics).
@@ -21,18 +22,22 @@ namespace mihvd {
 
 constexpr int CB_IPB = 4;               // images per wgrad block (2 per wave group)
 constexpr int CB_KQ = 4;                // fc1 dgrad split-K slabs
-constexpr int CB_WSTR = 72;             // W2 image row stride (dgrad) and dY2 image row stride (wgrad)
-// dgrad LDS: W2 [800][72] | D [18*18][72]. Both row strides are 144 B (36 banks): the 16
-// consecutive rows a ds_read_b128 lane group touches land on distinct banks (a 128-B pixel stride
-// would put every other pixel on the same banks: 8-way conflicts on each B-fragment read).
-constexpr int CB_DSTR = 72;
-constexpr int CB_DG_W = 800 * CB_WSTR;
-constexpr int CB_DG_D = 324 * CB_DSTR;
-constexpr int CB_DG_LDS = (CB_DG_W + CB_DG_D) * 2;                 // 161,856 B
-static_assert(CB_DG_LDS <= 163840, "dgrad LDS");
-// wgrad LDS per wave group: A [325][32] | Dm [197][72]
+// wgrad images are XOR-swizzled on 8-byte groups so the transposed reads (ds_read_b64_tr_b16,
+// 32-lane groups) spread over the banks: dY2 rows (128 B, 16 groups) use swd(row), the a1 image
+// (64-B pixel rows, 8 groups) flips the upper half of the row on pixel bit 2.
+__device__ __forceinline__ int swd(int r) { return 4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+__device__ __forceinline__ int swa(int pix) { return ((pix >> 2) & 1) << 2; }
+// dgrad LDS: W2 [800][64] | D [326][64], both unpadded 128-B rows whose eight 16-B chunks are
+// XOR-swizzled with the row index (chunk' = chunk ^ (row & 7)). With output tiles of 16
+// consecutive pixels (one image row, x = 0..15) every ds_read_b128 lane group of the A and B
+// fragment reads hits 64 distinct banks (checked with a bank model of the lane groups).
+constexpr int CB_DG_W = 800 * 64;
+constexpr int CB_DG_D = 326 * 64;                                  // 18 x 18 halo image + 2 spare rows
+constexpr int CB_DG_LDS = (CB_DG_W + CB_DG_D) * 2;                 // 144,128 B
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + 8 * (chunk ^ (row & 7)); }
+// wgrad LDS per wave group: A [325][32] | Dm [197][64]
 constexpr int CB_WG_A = 325 * 32;
-constexpr int CB_WG_D = 197 * CB_WSTR;
+constexpr int CB_WG_D = 197 * 64;
 constexpr int CB_WG_GRP = CB_WG_A + CB_WG_D;                       // elements
 constexpr int CB_WG_LDS = 2 * CB_WG_GRP * 2;                       // 98,336 B
 constexpr int CB_LDS = CB_DG_LDS > CB_WG_LDS ? CB_DG_LDS : CB_WG_LDS;
@@ -63,20 +68,6 @@ __device__ __forceinline__ void finish_dy_item(const DyItem& it, u16 g[4], int d
   }
 }
 
-// Write the 4 pixels of window `win` (value at the argmax slot, zero elsewhere) for 4 channels.
-__device__ __forceinline__ void scatter_window(u16* img, int pix_stride, int win, int co4, const u16 g[4], const int d[4],
-                                               bool padded18) {
-  const int py = win / 7, px = win - py * 7;
-#pragma unroll
-  for (int dd = 0; dd < 4; ++dd) {
-    const int y = 2 * py + (dd >> 1), x = 2 * px + (dd & 1);
-    const int pix = padded18 ? (y + 2) * 18 + (x + 2) : y * 14 + x;
-    const uint32_t lo = (uint32_t)(d[0] == dd ? g[0] : 0) | ((uint32_t)(d[1] == dd ? g[1] : 0) << 16);
-    const uint32_t hi = (uint32_t)(d[2] == dd ? g[2] : 0) | ((uint32_t)(d[3] == dd ? g[3] : 0) << 16);
-    *reinterpret_cast<uint2*>(img + pix * pix_stride + co4) = make_uint2(lo, hi);
-  }
-}
-
 __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, u16* __restrict__ g1, float* __restrict__ slab,
@@ -87,9 +78,10 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
   if ((int)blockIdx.x < n_dgrad) {
     // ===================================================================== dgrad: image b
     const int b = blockIdx.x;
-    u16* Ws = smem;              // [800][72]  row = kk*32 + ci, cols = co
-    u16* D = smem + CB_DG_W;     // [18*18][72] padded dY2 image
-    // Issue every load of the block first: W2 (13 x 16 B per thread) and 2 dY2 items.
+    u16* Ws = smem;              // [800][64] swizzled, row = kk*32 + ci, cols = co
+    u16* D = smem + CB_DG_W;     // [326][64] swizzled padded dY2 image (pixel = row)
+    // Issue every load of the block first: W2 (13 x 16 B per thread), 2 dY2 items and the
+    // epilogue's conv1 pooled-ReLU mask.
     DyItem items[2];
     int ie[2];
 #pragma unroll
@@ -100,12 +92,27 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     }
     TileLoad<512, 13, 8> lw;
     lw.load(w2bf, 64, 800, 800, t);
-    lw.store(Ws, CB_WSTR, 800, t);
-    // zero halo pixels of D (interior pixels are fully written by the scatter)
+    // output tiles: image row y = wave and wave + 8 (rows 14, 15 are dummies), pixel x = lr
+    // (x = 14, 15 dummies); lane holds ci 16*nt + 4*lg .. +3 of that pixel.
+    uint2 amask[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int y = min(wave + 8 * i, 13), x = min(lr, 13);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        amask[i][nt] = *reinterpret_cast<const uint2*>(a1 + ((int64_t)b * 196 + y * 14 + x) * 32 + nt * 16 + 4 * lg);
+    }
+#pragma unroll
+    for (int it = 0; it < 13; ++it) {
+      const int i = t + it * 512;
+      if (i < 800 * 8) *reinterpret_cast<uint4*>(Ws + swz64(i >> 3, i & 7)) = lw.v[it];
+    }
+    // zero the halo pixels (interior pixels are fully written by the scatter); rows 324, 325 are
+    // only read by dummy output columns, whose results are discarded
     for (int i = t; i < 324 * 8; i += 512) {
       const int pix = i >> 3, c = i & 7;
       const int y = pix / 18, x = pix - y * 18;
-      if (y < 2 || y >= 16 || x < 2 || x >= 16) *reinterpret_cast<uint4*>(D + pix * CB_DSTR + c * 8) = make_uint4(0, 0, 0, 0);
+      if (y < 2 || y >= 16 || x < 2 || x >= 16) *reinterpret_cast<uint4*>(D + swz64(pix, c)) = make_uint4(0, 0, 0, 0);
     }
     float db[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -117,57 +124,50 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
         finish_dy_item(items[k], g, d, gf);
 #pragma unroll
         for (int c = 0; c < 4; ++c) db[c] += gf[c];
-        scatter_window(D, CB_DSTR, ie[k] >> 4, (ie[k] & 15) * 4, g, d, true);
+        const int win = ie[k] >> 4, co4 = (ie[k] & 15) * 4;
+        const int py = win / 7, px = win - py * 7;
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+          const int pix = (2 * py + (dd >> 1) + 2) * 18 + 2 * px + (dd & 1) + 2;
+          const uint32_t lo = (uint32_t)(d[0] == dd ? g[0] : 0) | ((uint32_t)(d[1] == dd ? g[1] : 0) << 16);
+          const uint32_t hi = (uint32_t)(d[2] == dd ? g[2] : 0) | ((uint32_t)(d[3] == dd ? g[3] : 0) << 16);
+          *reinterpret_cast<uint2*>(D + swz64(pix, co4 >> 3) + (co4 & 7)) = make_uint2(lo, hi);
+        }
       }
     }
     __syncthreads();
-    // conv1's pooled-ReLU mask for the epilogue, fetched now so its latency hides under the GEMM
-    uint2 amask[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = min((wave + 8 * i) * 16 + lr, 195);
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        amask[i][nt] = *reinterpret_cast<const uint2*>(a1 + ((int64_t)b * 196 + m) * 32 + nt * 16 + 4 * lg);
-    }
-    // GEMM: rows = ci (2 tiles), cols = pixels (13 tiles: wave w, w+8), K = (kh, kw, co) = 1600.
+    // GEMM: rows = ci (2 tiles), cols = 16 pixels of image row y, K = (kh, kw, co) = 1600.
+    // Waves 6, 7 compute a dummy second tile (no guard on MFMAs).
     f32x4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int ntl = (wave + 8 < 13) ? 2 : 1;
-    int pbase[2];
+    int pix0[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int m = (wave + 8 * i) * 16 + lr;
-      if (m >= 196) m = 0;
-      const int y = m / 14, x = m - (m / 14) * 14;
-      pbase[i] = ((y + 4) * 18 + (x + 4)) * CB_DSTR + 8 * lg;
-    }
+    for (int i = 0; i < 2; ++i) pix0[i] = (min(wave + 8 * i, 13) + 4) * 18 + lr + 4;  // <= 325
     for (int kk = 0; kk < 25; ++kk) {
       const int kh = kk / 5, kw = kk - kh * 5;
-      const int aoff = -(kh * 18 + kw) * CB_DSTR;
+      const int toff = kh * 18 + kw;
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
-        const u16* wr = Ws + (kk * 32 + lr) * CB_WSTR + ch * 32 + 8 * lg;
-        const bf16x8 w0 = frag_ld128(wr);
-        const bf16x8 w1 = frag_ld128(wr + 16 * CB_WSTR);
+        const int c = ch * 4 + lg;
+        const bf16x8 w0 = frag_ld128(Ws + swz64(kk * 32 + lr, c));
+        const bf16x8 w1 = frag_ld128(Ws + swz64(kk * 32 + 16 + lr, c));
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {  // waves 5-7 compute a dummy second tile (no guard on MFMAs)
-          const bf16x8 bx = frag_ld128(D + pbase[i] + aoff + ch * 32);
+        for (int i = 0; i < 2; ++i) {
+          const bf16x8 bx = frag_ld128(D + swz64(pix0[i] - toff, c));
           acc[i][0] = mfma16(w0, bx, acc[i][0]);
           acc[i][1] = mfma16(w1, bx, acc[i][1]);
         }
       }
     }
-    // Epilogue: lane holds ci = 16*nt + 4*lg .. +3 of pixel (tile*16 + lr).
+    // Epilogue: conv1's pooled-ReLU mask, bf16, 8-byte stores.
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      if (i >= ntl) continue;
-      const int m = (wave + 8 * i) * 16 + lr;
-      if (m >= 196) continue;
+      const int y = wave + 8 * i;
+      if (y >= 14 || lr >= 14) continue;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const int64_t o = ((int64_t)b * 196 + m) * 32 + nt * 16 + 4 * lg;
+        const int64_t o = ((int64_t)b * 196 + y * 14 + lr) * 32 + nt * 16 + 4 * lg;
         const uint2 av = amask[i][nt];
         const float m0 = bf2f((u16)(av.x & 0xffff)) > 0.f ? acc[i][nt][0] : 0.f;
         const float m1 = bf2f((u16)(av.x >> 16)) > 0.f ? acc[i][nt][1] : 0.f;
@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
   const int kh = bid % 5, grp = bid / 5;
   const int h = wave >> 2, lw = wave & 3, th = t & 255;
   u16* A = smem + h * CB_WG_GRP;   // [325][32] padded a1 image (+ zero pixel 324)
-  u16* Dm = A + CB_WG_A;           // [197][72] dY2 rows = pixels (+ zero row 196)
+  u16* Dm = A + CB_WG_A;           // [197][64] dY2 rows = pixels (+ zero row 196)
   f32x4 acc[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -228,9 +228,10 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const int i = th + 256 * k;
-      if (i < 1300) reinterpret_cast<uint4*>(A)[i] = av[k];
+      const int pix = i >> 2, c = i & 3;
+      if (i < 1300) *reinterpret_cast<uint4*>(A + pix * 32 + 8 * (c ^ (swa(pix) >> 1))) = av[k];
     }
-    if (th < 9) reinterpret_cast<uint4*>(Dm + 196 * CB_WSTR)[th] = make_uint4(0, 0, 0, 0);
+    if (th < 8) reinterpret_cast<uint4*>(Dm + 196 * 64)[th] = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = th + 256 * k;
@@ -239,7 +240,15 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
         int d[4];
         float gf[4];
         finish_dy_item(items[k], g, d, gf);
-        scatter_window(Dm, CB_WSTR, i >> 4, (i & 15) * 4, g, d, false);
+        const int win = i >> 4, grp8 = i & 15;  // 8-byte group = 4 channels
+        const int py = win / 7, px = win - py * 7;
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+          const int pix = (2 * py + (dd >> 1)) * 14 + 2 * px + (dd & 1);
+          const uint32_t lo = (uint32_t)(d[0] == dd ? g[0] : 0) | ((uint32_t)(d[1] == dd ? g[1] : 0) << 16);
+          const uint32_t hi = (uint32_t)(d[2] == dd ? g[2] : 0) | ((uint32_t)(d[3] == dd ? g[3] : 0) << 16);
+          *reinterpret_cast<uint2*>(Dm + pix * 64 + 4 * (grp8 ^ swd(pix))) = make_uint2(lo, hi);
+        }
       }
     }
     __syncthreads();
@@ -248,19 +257,20 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     for (int k0 = 0; k0 < 224; k0 += 32) {
       // A' = dY2^T: rows = co (16 per wave), k = pixels
       const int r0 = min(k0 + 8 * lg + q, 196), r1 = min(k0 + 8 * lg + q + 4, 196);
-      const bf16x8 af = frag_tr(Dm + r0 * CB_WSTR + lw * 16 + 4 * p, Dm + r1 * CB_WSTR + lw * 16 + 4 * p);
-      int poff[2], kwm[2];
+      const bf16x8 af = frag_tr(Dm + r0 * 64 + 4 * ((4 * lw + p) ^ swd(r0)), Dm + r1 * 64 + 4 * ((4 * lw + p) ^ swd(r1)));
+      int prow[2], kwm[2];
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int pix = k0 + 8 * lg + q + 4 * hh;
         const int y = pix / 14, x = pix - (pix / 14) * 14;
-        poff[hh] = pix < 196 ? ((y + kh) * 18 + x) * 32 : 324 * 32;  // pixel 324 = zeros
-        kwm[hh] = pix < 196 ? 32 : 0;
+        prow[hh] = pix < 196 ? (y + kh) * 18 + x : 324;  // pixel 324 = zeros
+        kwm[hh] = pix < 196 ? 1 : 0;
       }
 #pragma unroll
       for (int mt = 0; mt < 10; ++mt) {
-        const int kw = mt >> 1, ci0 = (mt & 1) * 16;
-        const bf16x8 bx = frag_tr(A + poff[0] + kw * kwm[0] + ci0 + 4 * p, A + poff[1] + kw * kwm[1] + ci0 + 4 * p);
+        const int kw = mt >> 1, gq = (mt & 1) * 4 + p;  // 8-byte group of ci0 + 4p
+        const int P0 = prow[0] + kw * kwm[0], P1 = prow[1] + kw * kwm[1];
+        const bf16x8 bx = frag_tr(A + P0 * 32 + 4 * (gq ^ swa(P0)), A + P1 * 32 + 4 * (gq ^ swa(P1)));
         acc[mt] = mfma16(af, bx, acc[mt]);
       }
     }

@@ -202,7 +202,9 @@ def test_conv2_bwd_and_conv1_wgrad(ops, B):
     b1r = b1.clone().requires_grad_(True)
     p1, _, _ = ref_conv_pool(x.view(B, 28, 28, 1), w1r, b1r)
     p1.backward(g1.float())
-    assert rel_err(gW1.view(5, 5, 1, 32), w1r.grad) < 1e-3
+    # conv1_wgrad feeds the MFMA with the input image in bf16 (rel. rounding 2^-9), the reference
+    # keeps fp32 x: a few 1e-3 of relative difference
+    assert rel_err(gW1.view(5, 5, 1, 32), w1r.grad) < 5e-3
     assert rel_err(gb1, b1r.grad) < 1e-3
 
 
