@@ -11,8 +11,10 @@
 //   * wgrad (kernel row kh x group of 4 images): dW2 as an MFMA GEMM over pixels with both operands
 //     read by ds_read_b64_tr_b16 from natural NHWC images; two 4-wave groups take two images each
 //     and are summed in LDS; one fp32 partial slab per block (deterministic, no atomics).
-// conv1_wgrad: dW1/db1 as an MFMA GEMM over full-resolution pixels (the routed gradient is
-//   scattered into LDS, im2col(x) is read from kw-shifted image copies), plus the dW2 slab reduction.
+//   The dgrad role then computes conv1's weight gradient for its image from g1 still on chip: dW1/db1
+//   as an MFMA GEMM over full-resolution pixels (the routed gradient is scattered into LDS,
+//   im2col(x) is read from kw-shifted image copies).
+// conv2_wgrad_reduce: dW2 = sum of the wgrad slabs.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -22,11 +24,9 @@ namespace mihvd {
 
 constexpr int CB_IPB = 4;               // images per wgrad block (2 per wave group)
 constexpr int CB_KQ = 4;                // fc1 dgrad split-K slabs
-// wgrad images are XOR-swizzled on 8-byte groups so the transposed reads (ds_read_b64_tr_b16,
-// 32-lane groups) spread over the banks: dY2 rows (128 B, 16 groups) use swd(row), the a1 image
-// (64-B pixel rows, 8 groups) flips the upper half of the row on pixel bit 2.
+// The wgrad dY2 image (128-B pixel rows, 16 groups of 8 B) is XOR-swizzled on its 8-byte groups
+// so the transposed reads (ds_read_b64_tr_b16, 32-lane groups) hit distinct banks.
 __device__ __forceinline__ int swd(int r) { return 4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
-__device__ __forceinline__ int swa(int pix) { return ((pix >> 2) & 1) << 2; }
 // dgrad LDS: W2 [800][64] | D [326][64], both unpadded 128-B rows whose eight 16-B chunks are
 // XOR-swizzled with the row index (chunk' = chunk ^ (row & 7)). With output tiles of 16
 // consecutive pixels (one image row, x = 0..15) every ds_read_b128 lane group of the A and B
@@ -41,6 +41,28 @@ constexpr int CB_WG_D = 197 * 64;
 constexpr int CB_WG_GRP = CB_WG_A + CB_WG_D;                       // elements
 constexpr int CB_WG_LDS = 2 * CB_WG_GRP * 2;                       // 98,336 B
 constexpr int CB_LDS = CB_DG_LDS > CB_WG_LDS ? CB_DG_LDS : CB_WG_LDS;
+
+// ------------------------------------------------------------------------------------------ //
+// Fused conv1 weight gradient (tail of the conv2 dgrad role, one image per block): dW1/db1 -> atomics.
+//
+// It is an MFMA GEMM over the full-resolution pixels of the image:
+//     dW1^T[co][tap] = sum_pix dY1^T[co][pix] * im2col(x)[pix][tap]      (M = 32, N = 25 -> 32)
+// with K = 28 rows x 32 columns (columns 28..31 are dummy pixels whose dY1 row is the zero row).
+//   * dY1 ([785][40] bf16, pixel rows) is scattered from the pooled gradient g1 (the dgrad
+//     epilogue's registers, never re-read from HBM) through the argmax slots idx1 (each pooling window writes its four sub-pixels, value or zero), so every pixel
+//     row is written once and only the zero row needs clearing; it is read by transposed LDS
+//     reads (ds_read_b64_tr_b16) as the A operand.
+//   * im2col(x) is never built: the B fragment of tap (kh, kw) for 8 consecutive pixels of a row
+//     is 8 consecutive elements of the zero-padded image row y + kh starting at column x0 + kw.
+//     Five copies of the bf16 image shifted by kw = 0..4 make that one aligned ds_read_b128.
+//   * the eight waves split K (image rows w, w+8, ...) and are summed through LDS before the atomics.
+// ------------------------------------------------------------------------------------------ //
+constexpr int C1_DSTR = 40;                          // dY1 row stride (32 co + 8 pad)
+constexpr int C1_DY = 785 * C1_DSTR;                 // elements; row 784 = zeros
+constexpr int C1_XS = 32 * 32;                       // one shifted bf16 image copy [32][32]
+constexpr int C1_LDS = (C1_DY + 5 * C1_XS + 8) * 2 + 32 * 36 * 4;  // + zero chunk + fp32 staging
+static_assert(C1_LDS <= CB_DG_W * 2, "the conv1 images fit in the dead W2 image");
+static_assert(8 * 64 * 16 * 4 <= CB_DG_D * 2 && (512 * 4 + 256) * 4 <= CB_DG_D * 2, "partials fit in the dY2 image");
 
 struct DyItem {
   uint2 g;       // 4 bf16 pooled gradients (already masked by conv2's pooled ReLU)
@@ -70,8 +92,10 @@ __device__ __forceinline__ void finish_dy_item(const DyItem& it, u16 g[4], int d
 
 __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
-    const u16* __restrict__ a1, const u16* __restrict__ w2bf, u16* __restrict__ g1, float* __restrict__ slab,
-    float* __restrict__ gb2, int B, int n_dgrad) {
+    const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
+    int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
+    float* __restrict__ slab, float* __restrict__ gb2, float* __restrict__ gW1, float* __restrict__ gb1, int B,
+    int n_dgrad) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
@@ -95,12 +119,33 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     // output tiles: image row y = wave and wave + 8 (rows 14, 15 are dummies), pixel x = lr
     // (x = 14, 15 dummies); lane holds ci 16*nt + 4*lg .. +3 of that pixel.
     uint2 amask[2][2];
+    uint32_t dsel[2][2];  // conv1 pool argmax slots of the same 4 channels (fused conv1 wgrad)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int y = min(wave + 8 * i, 13), x = min(lr, 13);
+      const int y = min(wave + 8 * i, 13), xx = min(lr, 13);
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        amask[i][nt] = *reinterpret_cast<const uint2*>(a1 + ((int64_t)b * 196 + y * 14 + x) * 32 + nt * 16 + 4 * lg);
+      for (int nt = 0; nt < 2; ++nt) {
+        const int64_t o = ((int64_t)b * 196 + y * 14 + xx) * 32 + nt * 16 + 4 * lg;
+        amask[i][nt] = *reinterpret_cast<const uint2*>(a1 + o);
+        dsel[i][nt] = *reinterpret_cast<const uint32_t*>(idx1 + o);
+      }
+    }
+    // the input image for conv1's weight gradient: 2 of the [32][32] zero-padded positions each
+    float xv[2];
+    {
+      int row = b;
+      if (rows != nullptr) {
+        const int64_t step = state ? state[ST_FWD] : 0;
+        row = rows[(int)((step * (int64_t)B + b) % n_pool)];
+      }
+      const float* xi = x + (int64_t)row * 784;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = t + 512 * k;
+        const int gy = (i >> 5) - 2, gx = (i & 31) - 2;
+        const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
+        xv[k] = mask_f(xi[in ? gy * 28 + gx : 0], in);
+      }
     }
 #pragma unroll
     for (int it = 0; it < 13; ++it) {
@@ -144,6 +189,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     int pix0[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) pix0[i] = (min(wave + 8 * i, 13) + 4) * 18 + lr + 4;  // <= 325
+#pragma unroll 5
     for (int kk = 0; kk < 25; ++kk) {
       const int kh = kk / 5, kw = kk - kh * 5;
       const int toff = kh * 18 + kw;
@@ -160,32 +206,145 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
         }
       }
     }
-    // Epilogue: conv1's pooled-ReLU mask, bf16, 8-byte stores.
+    // Epilogue: conv1's pooled-ReLU mask and bf16 rounding -> g1 (kept on chip; written to HBM
+    // only when the caller asks for it, e.g. numerics tests).
+    uint2 gq[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int y = wave + 8 * i;
-      if (y >= 14 || lr >= 14) continue;
+      const bool valid = wave + 8 * i < 14 && lr < 14;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const int64_t o = ((int64_t)b * 196 + y * 14 + lr) * 32 + nt * 16 + 4 * lg;
         const uint2 av = amask[i][nt];
         const float m0 = bf2f((u16)(av.x & 0xffff)) > 0.f ? acc[i][nt][0] : 0.f;
         const float m1 = bf2f((u16)(av.x >> 16)) > 0.f ? acc[i][nt][1] : 0.f;
         const float m2 = bf2f((u16)(av.y & 0xffff)) > 0.f ? acc[i][nt][2] : 0.f;
         const float m3 = bf2f((u16)(av.y >> 16)) > 0.f ? acc[i][nt][3] : 0.f;
-        *reinterpret_cast<uint2*>(g1 + o) = pack4bf(m0, m1, m2, m3);
+        const uint2 v = pack4bf(m0, m1, m2, m3);
+        gq[i][nt] = make_uint2(valid ? v.x : 0u, valid ? v.y : 0u);
+        if (g1 != nullptr && valid)
+          *reinterpret_cast<uint2*>(g1 + ((int64_t)b * 196 + (wave + 8 * i) * 14 + lr) * 32 + nt * 16 + 4 * lg) = v;
       }
     }
-    // db2: per-thread partials (a thread's items share one channel group) -> LDS -> atomics
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(D);  // [512][4]
+    // ---- fused conv1 weight gradient (see conv1 section below for the GEMM layout)
+    __syncthreads();  // W2 and dY2 images are dead: reuse their LDS
+    u16* Dy = smem;                                          // [785][40] full-resolution dY1
+    u16* Xs = smem + C1_DY;                                  // 5 x [32][32] kw-shifted bf16 images
+    u16* Zc = Xs + 5 * C1_XS;                                // zero chunk (dummy taps)
+    float* Xf = reinterpret_cast<float*>(Zc + 8);            // [32][36] fp32 padded image
+    float* red = reinterpret_cast<float*>(D);                // [512][4] db2 | [8 waves][4 lg][8] db1
+    float* red1 = red + 512 * 4;
+    float d1[8];                                             // db1 partial: (nt, i) channel 16nt+4lg+i
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int y = min(wave + 8 * i, 13);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const uint2 v = gq[i][nt];
+        const u16 g[4] = {(u16)(v.x & 0xffff), (u16)(v.x >> 16), (u16)(v.y & 0xffff), (u16)(v.y >> 16)};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d1[nt * 4 + c] = (i == 0 ? 0.f : d1[nt * 4 + c]) + bf2f(g[c]);
+        if (wave + 8 * i < 14 && lr < 14) {
+          int d[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) d[c] = (dsel[i][nt] >> (8 * c)) & 3;
+#pragma unroll
+          for (int dd = 0; dd < 4; ++dd) {
+            const int pix = (2 * y + (dd >> 1)) * 28 + 2 * lr + (dd & 1);
+            const uint32_t lo = (uint32_t)(d[0] == dd ? g[0] : 0) | ((uint32_t)(d[1] == dd ? g[1] : 0) << 16);
+            const uint32_t hi = (uint32_t)(d[2] == dd ? g[2] : 0) | ((uint32_t)(d[3] == dd ? g[3] : 0) << 16);
+            *reinterpret_cast<uint2*>(Dy + pix * C1_DSTR + nt * 16 + 4 * lg) = make_uint2(lo, hi);
+          }
+        }
+      }
+    }
+    // db1: sum the 16 pixels (lanes lr) of each lane group, then one slot per (wave, lg)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float v = d1[c];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      d1[c] = v;
+    }
+    if (lr == 0) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) red1[(wave * 4 + lg) * 8 + c] = d1[c];
+    }
     *reinterpret_cast<float4*>(red + t * 4) = make_float4(db[0], db[1], db[2], db[3]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) Xf[((t + 512 * k) >> 5) * 36 + ((t + 512 * k) & 31)] = xv[k];
+    if (t < 32) Xf[t * 36 + 32] = Xf[t * 36 + 33] = Xf[t * 36 + 34] = Xf[t * 36 + 35] = 0.f;
+    if (t < 5) reinterpret_cast<uint4*>(Dy + 784 * C1_DSTR)[t] = make_uint4(0, 0, 0, 0);
+    if (t == 5) *reinterpret_cast<uint4*>(Zc) = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (t < 64) {
-      const int co4 = t >> 2, c = t & 3;  // channel co4*4 + c, summed over the 32 threads with (tid & 15) == co4
-      float s = 0.f;
-      for (int r = co4; r < 512; r += 16) s += red[r * 4 + c];
-      atomicAdd(gb2 + co4 * 4 + c, s);
+      // db2 channel co4*4 + c, summed over the 32 threads with (tid & 15) == co4
+      const int co4 = t >> 2, c = t & 3;
+      float sacc = 0.f;
+      for (int r = co4; r < 512; r += 16) sacc += red[r * 4 + c];
+      atomicAdd(gb2 + co4 * 4 + c, sacc);
+    } else if (t < 96) {
+      // db1 channel ch = 16nt + 4lg + i
+      const int ch = t - 64, nt = ch >> 4, lgg = (ch >> 2) & 3, i = ch & 3;
+      float sacc = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sacc += red1[(w * 4 + lgg) * 8 + nt * 4 + i];
+      atomicAdd(gb1 + ch, sacc);
+    }
+    for (int i = t; i < 5 * 32 * 4; i += 512) {
+      const int kw = i >> 7, r = (i >> 2) & 31, c0 = (i & 3) * 8;
+      const float* src = Xf + r * 36 + c0 + kw;
+      *reinterpret_cast<uint4*>(Xs + kw * C1_XS + r * 32 + c0) =
+          make_uint4((uint32_t)f2bf(src[0]) | ((uint32_t)f2bf(src[1]) << 16), (uint32_t)f2bf(src[2]) | ((uint32_t)f2bf(src[3]) << 16),
+                     (uint32_t)f2bf(src[4]) | ((uint32_t)f2bf(src[5]) << 16), (uint32_t)f2bf(src[6]) | ((uint32_t)f2bf(src[7]) << 16));
+    }
+    __syncthreads();
+    // GEMM dW1^T[co][tap] = sum_pix dY1^T[co][pix] im2col(x)[pix][tap]: wave w takes image rows
+    // w, w+8, w+16, w+24 (rows >= 28 read the zero dY1 row: no guard around the MFMAs).
+    int boff[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int n = nt * 16 + lr;
+      const int kh = n / 5, kw = n - (n / 5) * 5;
+      boff[nt] = n < 25 ? kw * C1_XS + kh * 32 + 8 * lg : -1;
+    }
+    f32x4 c1[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) c1[i][0] = c1[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int y = wave + 8 * j;
+      const int yb = min(y, 27);
+      const int x0 = 8 * lg + q, x1 = x0 + 4;
+      const int r0 = (y < 28 && x0 < 28) ? y * 28 + x0 : 784, r1 = (y < 28 && x1 < 28) ? y * 28 + x1 : 784;
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        af[mt] = frag_tr(Dy + r0 * C1_DSTR + mt * 16 + 4 * p, Dy + r1 * C1_DSTR + mt * 16 + 4 * p);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) bfr[nt] = frag_ld128(boff[nt] >= 0 ? Xs + boff[nt] + yb * 32 : Zc);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) c1[mt][nt] = mfma16(af[mt], bfr[nt], c1[mt][nt]);
+    }
+    float* part = reinterpret_cast<float*>(D);  // [8 waves][64 lanes][16] (db areas are consumed)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        *reinterpret_cast<float4*>(part + (wave * 64 + lane) * 16 + (mt * 2 + nt) * 4) =
+            make_float4(c1[mt][nt][0], c1[mt][nt][1], c1[mt][nt][2], c1[mt][nt][3]);
+    __syncthreads();
+    for (int o = t; o < 800; o += 512) {
+      const int tap = o >> 5, co = o & 31;
+      const int nt = tap >> 4, lrr = tap & 15, mt = co >> 4, lgg = (co >> 2) & 3, i = co & 3;
+      const int slot = (lgg * 16 + lrr) * 16 + (mt * 2 + nt) * 4 + i;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += part[w * 64 * 16 + slot];
+      atomicAdd(gW1 + o, v);  // HWIO: tap * 32 + co
     }
     return;
   }
@@ -229,7 +388,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     for (int k = 0; k < 6; ++k) {
       const int i = th + 256 * k;
       const int pix = i >> 2, c = i & 3;
-      if (i < 1300) *reinterpret_cast<uint4*>(A + pix * 32 + 8 * (c ^ (swa(pix) >> 1))) = av[k];
+      if (i < 1300) *reinterpret_cast<uint4*>(A + pix * 32 + 8 * c) = av[k];
     }
     if (th < 8) reinterpret_cast<uint4*>(Dm + 196 * 64)[th] = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -258,19 +417,18 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       // A' = dY2^T: rows = co (16 per wave), k = pixels
       const int r0 = min(k0 + 8 * lg + q, 196), r1 = min(k0 + 8 * lg + q + 4, 196);
       const bf16x8 af = frag_tr(Dm + r0 * 64 + 4 * ((4 * lw + p) ^ swd(r0)), Dm + r1 * 64 + 4 * ((4 * lw + p) ^ swd(r1)));
-      int prow[2], kwm[2];
+      int poff[2], kwm[2];
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int pix = k0 + 8 * lg + q + 4 * hh;
         const int y = pix / 14, x = pix - (pix / 14) * 14;
-        prow[hh] = pix < 196 ? (y + kh) * 18 + x : 324;  // pixel 324 = zeros
-        kwm[hh] = pix < 196 ? 1 : 0;
+        poff[hh] = pix < 196 ? ((y + kh) * 18 + x) * 32 : 324 * 32;  // pixel 324 = zeros
+        kwm[hh] = pix < 196 ? 32 : 0;
       }
 #pragma unroll
       for (int mt = 0; mt < 10; ++mt) {
-        const int kw = mt >> 1, gq = (mt & 1) * 4 + p;  // 8-byte group of ci0 + 4p
-        const int P0 = prow[0] + kw * kwm[0], P1 = prow[1] + kw * kwm[1];
-        const bf16x8 bx = frag_tr(A + P0 * 32 + 4 * (gq ^ swa(P0)), A + P1 * 32 + 4 * (gq ^ swa(P1)));
+        const int kw = mt >> 1, ci0 = (mt & 1) * 16;
+        const bf16x8 bx = frag_tr(A + poff[0] + kw * kwm[0] + ci0 + 4 * p, A + poff[1] + kw * kwm[1] + ci0 + 4 * p);
         acc[mt] = mfma16(af, bx, acc[mt]);
       }
     }
@@ -301,202 +459,61 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
   }
 }
 
-// ------------------------------------------------------------------------------------------ //
-// conv1_wgrad: blocks [0, B): one image each, dW1/db1 -> atomics; blocks [B, B+200): dW2 slabs.
-//
-// The image role is an MFMA GEMM over the full-resolution pixels of the image:
-//     dW1^T[co][tap] = sum_pix dY1^T[co][pix] * im2col(x)[pix][tap]      (M = 32, N = 25 -> 32)
-// with K = 28 rows x 32 columns (columns 28..31 are dummy pixels whose dY1 row is the zero row).
-//   * dY1 ([785][40] bf16, pixel rows) is scattered from the pooled gradient g1 through the argmax
-//     slots idx1 (each pooling window writes its four sub-pixels, value or zero), so every pixel
-//     row is written once and only the zero row needs clearing; it is read by transposed LDS
-//     reads (ds_read_b64_tr_b16) as the A operand.
-//   * im2col(x) is never built: the B fragment of tap (kh, kw) for 8 consecutive pixels of a row
-//     is 8 consecutive elements of the zero-padded image row y + kh starting at column x0 + kw.
-//     Five copies of the bf16 image shifted by kw = 0..4 make that one aligned ds_read_b128.
-//   * the four waves split K (7 image rows each) and are summed through LDS before the atomics.
-// ------------------------------------------------------------------------------------------ //
-constexpr int C1_DSTR = 40;                          // dY1 row stride (32 co + 8 pad)
-constexpr int C1_DY = 785 * C1_DSTR;                 // elements; row 784 = zeros
-constexpr int C1_XS = 32 * 32;                       // one shifted bf16 image copy [32][32]
-constexpr int C1_LDS = (C1_DY + 5 * C1_XS + 8) * 2 + 32 * 36 * 4;  // + zero chunk + fp32 staging
-static_assert(4 * 64 * 16 * 4 <= C1_DY * 2, "wave partials reuse the dY1 image");
-
-__global__ void __launch_bounds__(256) conv1_wgrad_kernel(
-    const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
-    const u16* __restrict__ g1, const uint8_t* __restrict__ idx1, const float* __restrict__ slab, int nslab,
-    float* __restrict__ gW1, float* __restrict__ gb1, float* __restrict__ gW2, int B, int role_base) {
-  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+// dW2 = sum of the (<= 32) conv2 wgrad slabs. Block = 64 float4 outputs x 4 slab groups of 8, every
+// load in flight at once (absent slabs masked, not branched around), then a 4-way LDS sum.
+__global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab,
+                                                                 float* __restrict__ gW2) {
+  __shared__ float4 r4[256];
   const int t = threadIdx.x;
-  const int bid = (int)blockIdx.x + role_base;
-  if (bid >= B) {
-    // dW2 = sum of the (<= 32) wgrad slabs. Block = 64 float4 outputs x 4 slab groups of 8, every
-    // load in flight at once (absent slabs masked, not branched around), then a 4-way LDS sum.
-    const int o = (bid - B) * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
-    float4 v[8];
+  const int o = (int)blockIdx.x * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
+  float4 v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int g = sg * 8 + k;
-      const float4 xv = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[min(o, 12799)];
-      const bool keep = g < nslab;
-      v[k] = make_float4(mask_f(xv.x, keep), mask_f(xv.y, keep), mask_f(xv.z, keep), mask_f(xv.w, keep));
-    }
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
-    float4* r4 = reinterpret_cast<float4*>(smem);
-    r4[t] = s;
-    __syncthreads();
-    if (t < 64 && o < 12800) {
-      const float4 a = r4[t], b = r4[64 + t], c = r4[128 + t], d = r4[192 + t];
-      reinterpret_cast<float4*>(gW2)[o] =
-          make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
-                      (a.w + b.w) + (c.w + d.w));
-    }
-    return;
+  for (int k = 0; k < 8; ++k) {
+    const int g = sg * 8 + k;
+    const float4 xv = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[min(o, 12799)];
+    const bool keep = g < nslab;
+    v[k] = make_float4(mask_f(xv.x, keep), mask_f(xv.y, keep), mask_f(xv.z, keep), mask_f(xv.w, keep));
   }
-  const int b = bid;
-  int row = b;
-  if (rows != nullptr) {
-    const int64_t step = state ? state[ST_FWD] : 0;
-    row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-  }
-  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
-  const int q = lr >> 2, p = lr & 3;
-  u16* Dy = smem;                                          // [785][40]
-  u16* Xs = smem + C1_DY;                                  // 5 x [32][32] shifted bf16 images
-  u16* Zc = Xs + 5 * C1_XS;                                // 8 zero elements (dummy taps)
-  float* Xf = reinterpret_cast<float*>(Zc + 8);            // [32][36] fp32 padded image
-  // ---- loads first: the image (4 values per thread) and 6 pooled-gradient items (4 co each)
-  float xv[4];
-  const float* xi = x + (int64_t)row * 784;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = t + 256 * k;  // [32][32] padded positions
-    const int r = i >> 5, c = i & 31;
-    const int gy = r - 2, gx = c - 2;
-    const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
-    xv[k] = mask_f(xi[in ? gy * 28 + gx : 0], in);
-  }
-  uint2 gv[7];
-  uint32_t dv[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {  // 196 windows x 8 channel quads = 1568 items
-    const int i = min(t + 256 * k, 1567);
-    const int64_t o = (int64_t)b * 6272 + (i >> 3) * 32 + (i & 7) * 4;
-    gv[k] = *reinterpret_cast<const uint2*>(g1 + o);
-    dv[k] = *reinterpret_cast<const uint32_t*>(idx1 + o);
-  }
-  // ---- LDS images
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = t + 256 * k;
-    Xf[(i >> 5) * 36 + (i & 31)] = xv[k];
-  }
-  if (t < 32) Xf[t * 36 + 32] = Xf[t * 36 + 33] = Xf[t * 36 + 34] = Xf[t * 36 + 35] = 0.f;
-  if (t < 5) reinterpret_cast<uint4*>(Dy + 784 * C1_DSTR)[t] = make_uint4(0, 0, 0, 0);
-  if (t == 5) *reinterpret_cast<uint4*>(Zc) = make_uint4(0, 0, 0, 0);
-  float db[4] = {0.f, 0.f, 0.f, 0.f};  // every item of a thread has channel quad (t & 7)
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const int i = t + 256 * k;
-    if (i < 1568) {
-      const int win = i >> 3, co4 = (i & 7) * 4;
-      const int py = win / 14, px = win - py * 14;
-      const u16 g[4] = {(u16)(gv[k].x & 0xffff), (u16)(gv[k].x >> 16), (u16)(gv[k].y & 0xffff), (u16)(gv[k].y >> 16)};
-      int d[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        d[c] = (dv[k] >> (8 * c)) & 3;
-        db[c] += bf2f(g[c]);
-      }
-#pragma unroll
-      for (int dd = 0; dd < 4; ++dd) {
-        const int pix = (2 * py + (dd >> 1)) * 28 + 2 * px + (dd & 1);
-        const uint32_t lo = (uint32_t)(d[0] == dd ? g[0] : 0) | ((uint32_t)(d[1] == dd ? g[1] : 0) << 16);
-        const uint32_t hi = (uint32_t)(d[2] == dd ? g[2] : 0) | ((uint32_t)(d[3] == dd ? g[3] : 0) << 16);
-        *reinterpret_cast<uint2*>(Dy + pix * C1_DSTR + co4) = make_uint2(lo, hi);
-      }
-    }
-  }
+  for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
+  r4[t] = s;
   __syncthreads();
-  // five kw-shifted bf16 copies: Xs[kw][r][c] = P[r][c + kw]  (640 chunks of 8 elements)
-  for (int i = t; i < 5 * 32 * 4; i += 256) {
-    const int kw = i >> 7, r = (i >> 2) & 31, c0 = (i & 3) * 8;
-    const float* src = Xf + r * 36 + c0 + kw;
-    *reinterpret_cast<uint4*>(Xs + kw * C1_XS + r * 32 + c0) =
-        make_uint4((uint32_t)f2bf(src[0]) | ((uint32_t)f2bf(src[1]) << 16), (uint32_t)f2bf(src[2]) | ((uint32_t)f2bf(src[3]) << 16),
-                   (uint32_t)f2bf(src[4]) | ((uint32_t)f2bf(src[5]) << 16), (uint32_t)f2bf(src[6]) | ((uint32_t)f2bf(src[7]) << 16));
-  }
-  __syncthreads();
-  // ---- GEMM: wave w takes image rows y = 7w .. 7w+6 (one 32-pixel K step each)
-  int boff[2];  // B fragment base per tap tile: copy kw, row offset kh, this lane's 8-pixel group
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int n = nt * 16 + lr;
-    const int kh = n / 5, kw = n - (n / 5) * 5;
-    boff[nt] = n < 25 ? kw * C1_XS + kh * 32 + 8 * lg : -1;
-  }
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int yy = 0; yy < 7; ++yy) {
-    const int y = wave * 7 + yy;
-    const int x0 = 8 * lg + q, x1 = x0 + 4;
-    const int r0 = x0 < 28 ? y * 28 + x0 : 784, r1 = x1 < 28 ? y * 28 + x1 : 784;
-    bf16x8 af[2], bfr[2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-      af[mt] = frag_tr(Dy + r0 * C1_DSTR + mt * 16 + 4 * p, Dy + r1 * C1_DSTR + mt * 16 + 4 * p);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) bfr[nt] = frag_ld128(boff[nt] >= 0 ? Xs + boff[nt] + y * 32 : Zc);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16(af[mt], bfr[nt], acc[mt][nt]);
-  }
-  // ---- sum the four waves (partials reuse the dY1 image) and the db1 partials, then atomics
-  __syncthreads();
-  float* part = reinterpret_cast<float*>(smem);  // [4 waves][64 lanes][16]
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      *reinterpret_cast<float4*>(part + (wave * 64 + lane) * 16 + (mt * 2 + nt) * 4) =
-          make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
-  float* dbp = part + 4 * 64 * 16;  // [256][4]
-  *reinterpret_cast<float4*>(dbp + t * 4) = make_float4(db[0], db[1], db[2], db[3]);
-  __syncthreads();
-  // C[row = co = 16mt + 4lg' + i][col = tap = 16nt + lr'] lives in lane (lg', lr') slot (mt, nt, i)
-  for (int o = t; o < 800; o += 256) {
-    const int tap = o >> 5, co = o & 31;
-    const int nt = tap >> 4, lrr = tap & 15, mt = co >> 4, lgg = (co >> 2) & 3, i = co & 3;
-    const int ln = lgg * 16 + lrr, slot = (mt * 2 + nt) * 4 + i;
-    const float v = (part[(0 * 64 + ln) * 16 + slot] + part[(1 * 64 + ln) * 16 + slot]) +
-                    (part[(2 * 64 + ln) * 16 + slot] + part[(3 * 64 + ln) * 16 + slot]);
-    atomicAdd(gW1 + o, v);  // HWIO: tap * 32 + co
-  }
-  if (t < 32) {
-    // channel t: quad t >> 2 was accumulated by the 32 threads with (tid & 7) == t >> 2
-    float sdb = 0.f;
-    for (int r = t >> 2; r < 256; r += 8) sdb += dbp[r * 4 + (t & 3)];
-    atomicAdd(gb1 + t, sdb);
+  if (t < 64 && o < 12800) {
+    const float4 a = r4[t], b = r4[64 + t], c = r4[128 + t], d = r4[192 + t];
+    reinterpret_cast<float4*>(gW2)[o] = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
+                                                    (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
   }
 }
 
 // ------------------------------------------------------------------------------------------ //
 int64_t conv2_wgrad_groups(int64_t B) { return (B + CB_IPB - 1) / CB_IPB; }
 
-void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf, at::Tensor& g1,
-               at::Tensor& slab, at::Tensor& gb2) {
+void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+               const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1,
+               const c10::optional<at::Tensor>& g1) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
-  TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && g1.numel() == a1.numel(), "conv2_bwd: a1/g1");
+  TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && idx1.numel() == a1.numel() &&
+                  idx1.dtype() == at::kByte, "conv2_bwd: a1/idx1");
   TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200, "conv2_bwd: w2");
+  TORCH_CHECK(x.dtype() == at::kFloat && x.size(-1) == 784 && x.is_contiguous(), "conv2_bwd: x");
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_bwd: slab must hold ceil(B/4) x 51200");
   TORCH_CHECK(gb2.numel() == 64 && gb2.dtype() == at::kFloat, "conv2_bwd: gb2");
+  TORCH_CHECK(gW1.numel() == 800 && gb1.numel() == 32 && gW1.dtype() == at::kFloat && gb1.dtype() == at::kFloat,
+              "conv2_bwd: gW1/gb1");
+  u16* g1p = nullptr;
+  if (g1.has_value() && g1->defined()) {
+    TORCH_CHECK(g1->dtype() == at::kBFloat16 && g1->numel() == a1.numel(), "conv2_bwd: g1");
+    g1p = (u16*)g1->data_ptr();
+  }
+  const int* rp = nullptr;
+  int n_pool = x.size(0);
+  if (rows.has_value() && rows->defined()) rp = rows->data_ptr<int>();
+  else TORCH_CHECK(n_pool >= B, "conv2_bwd: x has fewer rows than the batch");
+  const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   static bool attr = [] {
     hipFuncSetAttribute((const void*)conv2_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
     return true;
@@ -507,35 +524,18 @@ void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a
   const int n_dgrad = role == 1 ? 0 : B;
   const int grid = role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
   conv2_bwd_kernel<<<grid, 512, CB_LDS, stream>>>(
-      (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(),
-      (const u16*)w2bf.data_ptr(), (u16*)g1.data_ptr(), slab.data_ptr<float>(), gb2.data_ptr<float>(), B, n_dgrad);
+      (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
+      x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(), gb2.data_ptr<float>(),
+      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, n_dgrad);
 }
 
-void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                 const at::Tensor& g1, const at::Tensor& idx1, const at::Tensor& slab, at::Tensor& gW1, at::Tensor& gb1,
-                 at::Tensor& gW2) {
-  const int B = g1.size(0);
+void conv2_wgrad_reduce(const at::Tensor& slab, int64_t B, at::Tensor& gW2) {
   const int G = (int)conv2_wgrad_groups(B);
-  TORCH_CHECK(x.dtype() == at::kFloat && x.size(-1) == 784, "conv1_wgrad: x");
-  TORCH_CHECK(g1.numel() == (int64_t)B * 6272 && idx1.numel() == g1.numel(), "conv1_wgrad: g1/idx1");
-  TORCH_CHECK(slab.numel() >= (int64_t)G * 51200 && gW2.numel() == 51200 && gW2.is_contiguous(), "conv1_wgrad: slab/gW2");
-  TORCH_CHECK(gW1.numel() == 800 && gb1.numel() == 32, "conv1_wgrad: gW1/gb1");
-  const int* rp = nullptr;
-  int n_pool = x.size(0);
-  if (rows.has_value() && rows->defined()) rp = rows->data_ptr<int>();
-  const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  TORCH_CHECK(G >= 1 && G <= 32, "conv2_wgrad_reduce: at most 32 wgrad slabs");
+  TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_wgrad_reduce: slab");
+  TORCH_CHECK(gW2.dtype() == at::kFloat && gW2.numel() == 51200 && gW2.is_contiguous(), "conv2_wgrad_reduce: gW2");
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  TORCH_CHECK(G <= 32, "conv1_wgrad: at most 32 wgrad slabs");
-  const int role = debug_role_only();  // 0: image blocks only, 1: dW2 slab-reduce blocks only
-  const int grid = role == 0 ? B : role == 1 ? 200 : B + 200;
-  static bool attr = [] {
-    hipFuncSetAttribute((const void*)conv1_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, C1_LDS);
-    return true;
-  }();
-  (void)attr;
-  conv1_wgrad_kernel<<<grid, 256, C1_LDS, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (const u16*)g1.data_ptr(),
-                                               idx1.data_ptr<uint8_t>(), slab.data_ptr<float>(), G, gW1.data_ptr<float>(),
-                                               gb1.data_ptr<float>(), gW2.data_ptr<float>(), B, role == 1 ? B : 0);
+  conv2_wgrad_reduce_kernel<<<200, 256, 0, stream>>>(slab.data_ptr<float>(), G, gW2.data_ptr<float>());
 }
 
 }  // namespace mihvd

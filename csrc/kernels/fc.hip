@@ -12,7 +12,7 @@
 // head    : one block per sample: slab sum + bias + ReLU + counter-based dropout, fc2, softmax
 //           cross-entropy and the fc2 backward into dz (K9-K11 of SURVEY.md §2.5, one kernel).
 // fc1_wgrad: one launch, four block roles: dW3 straight into the fusion buffer, db3, dW4, db4
-//           (+ zeroing of the gradients conv2_bwd / conv1_wgrad accumulate atomically).
+//           (+ zeroing of the gradients conv2_bwd accumulates atomically).
 // fc1_dgrad: full-K tiles (W3 rows in registers, dz in LDS) with the pooled-ReLU mask and the
 //           bf16 cast fused into the epilogue.
 #include <ATen/ATen.h>
@@ -365,7 +365,7 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     }
     return;
   }
-  // misc: db4 (thread = class c, row group), and zero the gradients that conv2_bwd / conv1_wgrad
+  // misc: db4 (thread = class c, row group), and zero the gradients that conv2_bwd
   // accumulate with atomics
   {
     float* red = reinterpret_cast<float*>(smem);

@@ -16,11 +16,11 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1);
 void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& g2);
 int64_t conv2_wgrad_groups(int64_t B);
-void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf, at::Tensor& g1,
-               at::Tensor& slab, at::Tensor& gb2);
-void conv1_wgrad(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                 const at::Tensor& g1, const at::Tensor& idx1, const at::Tensor& slab, at::Tensor& gW1, at::Tensor& gb1,
-                 at::Tensor& gW2);
+void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+               const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1,
+               const c10::optional<at::Tensor>& g1);
+void conv2_wgrad_reduce(const at::Tensor& slab, int64_t B, at::Tensor& gW2);
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
                double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale,
@@ -57,14 +57,12 @@ void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Ten
   mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, gb2, gW1, gb1);
 }
 void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, const Tensor& a2, Tensor g2) { mihvd::fc1_dgrad(dz, w3, a2, g2); }
-void conv2_bwd_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, Tensor g1, Tensor slab,
-                  Tensor gb2) {
-  mihvd::conv2_bwd(g2, idx2, a1, w2, g1, slab, gb2);
+void conv2_bwd_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, const Tensor& x,
+                  const OptT& rows, const OptT& state, const Tensor& idx1, Tensor slab, Tensor gb2, Tensor gW1, Tensor gb1,
+                  const OptT& g1) {
+  mihvd::conv2_bwd(g2, idx2, a1, w2, x, rows, state, idx1, slab, gb2, gW1, gb1, g1);
 }
-void conv1_wgrad_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& g1, const Tensor& idx1,
-                    const Tensor& slab, Tensor gW1, Tensor gb1, Tensor gW2) {
-  mihvd::conv1_wgrad(x, rows, state, g1, idx1, slab, gW1, gb1, gW2);
-}
+void conv2_wgrad_reduce_op(const Tensor& slab, int64_t B, Tensor gW2) { mihvd::conv2_wgrad_reduce(slab, B, gW2); }
 void adam_op(Tensor p, const Tensor& g, Tensor m, Tensor v, const OptT& shadow, const OptT& state, int64_t host_step,
              double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, int64_t bump,
              const OptT& loss_scale, int64_t max_blocks) {
@@ -96,9 +94,9 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(d!) gb4, Tensor(e!) gb2, Tensor(f!) gW1, Tensor(g!) gb1) -> ()");
   m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor a2, Tensor(a!) g2) -> ()");
   m.def("conv2_wgrad_groups(int B) -> int", &mihvd::conv2_wgrad_groups);
-  m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor(a!) g1, Tensor(b!) slab, Tensor(c!) gb2) -> ()");
-  m.def("conv1_wgrad(Tensor x, Tensor? rows, Tensor? state, Tensor g1, Tensor idx1, Tensor slab, Tensor(a!) gW1, "
-        "Tensor(b!) gb1, Tensor(c!) gW2) -> ()");
+  m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, Tensor? state, Tensor idx1, "
+        "Tensor(a!) slab, Tensor(b!) gb2, Tensor(c!) gW1, Tensor(d!) gb1, Tensor(e!)? g1=None) -> ()");
+  m.def("conv2_wgrad_reduce(Tensor slab, int B, Tensor(a!) gW2) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
         "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1, "
         "Tensor? loss_scale=None, int max_blocks=0) -> ()");
@@ -119,7 +117,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("fc1_wgrad", &fc1_wgrad_op);
   m.impl("fc1_dgrad", &fc1_dgrad_op);
   m.impl("conv2_bwd", &conv2_bwd_op);
-  m.impl("conv1_wgrad", &conv1_wgrad_op);
+  m.impl("conv2_wgrad_reduce", &conv2_wgrad_reduce_op);
   m.impl("adam_step", &adam_op);
   m.impl("scale_cast_bf16", &scale_cast_op);
   m.impl("bf16_to_f32", &bf16_to_f32_op);

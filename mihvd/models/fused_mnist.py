@@ -12,9 +12,9 @@ allreduce when ``size() > 1``), all hand-written CDNA4 kernels from ``csrc/kerne
         side stream (MIHVD_OVERLAP=1, default) while the conv backward runs ---
     fc1_dgrad   full-K dz.W3^T tiles (W3 rows in registers, dz in LDS, XCD-aware tile map)
                 with the pooled-ReLU mask and bf16 cast fused: writes g2         [MFMA bf16]
-    conv2_bwd   dgrad (g2 routed through the pool argmax, ReLU mask) | wgrad slabs | db2
-                                                                                [MFMA bf16]
-    conv1_wgrad dW1/db1 + dW2 slab reduction
+    conv2_bwd   dgrad (g2 routed through the pool argmax, ReLU mask) -> g1 on chip -> fused
+                conv1 wgrad (dW1/db1) | conv2 wgrad slabs | db2                  [MFMA bf16]
+    conv2_wgrad_reduce  dW2 = sum of the wgrad slabs
     --- bucket "conv" allreduced; the optimizer waits for both buckets ---
     adam_step   TF1 Adam over the flat fp32 buffer, 1/size averaging fused, bf16 shadow written
 
@@ -111,7 +111,6 @@ class FusedMNISTTrainer:
         self.dlog = torch.empty(B, 10, **f32)
         self.stats = torch.zeros(B, 2, **f32)
         self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
-        self.g1 = torch.empty(B, 14, 14, 32, **bf)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
@@ -217,10 +216,10 @@ class FusedMNISTTrainer:
                             self.shadow[FC_START:], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 0,
                             None, self.adam_blocks)
             self._fc_update_pending = True
-        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.g1, self.slab,
-                    self.gview("conv_layer2/conv2d/bias"))
-        o.conv1_wgrad(x, rows, st, self.g1, self.idx1, self.slab, self.gview("conv_layer1/conv2d/kernel"),
-                      self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/kernel"))
+        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows, st,
+                    self.idx1, self.slab, self.gview("conv_layer2/conv2d/bias"), self.gview("conv_layer1/conv2d/kernel"),
+                    self.gview("conv_layer1/conv2d/bias"))
+        o.conv2_wgrad_reduce(self.slab, self.B, self.gview("conv_layer2/conv2d/kernel"))
         if self.pipeline:
             if self.collectives:
                 if ar_done is not None:

@@ -2,7 +2,8 @@
 
 ``load()`` loads ``mihvd/_native/libmihvd_kernels.so`` (built in-tree by ``python -m mihvd._build``)
 and raises if it is unavailable. Kernels: conv1_fwd, conv2_fwd, fc1_fwd, head_fwd_bwd, fc1_wgrad,
-fc1_dgrad, conv2_bwd, conv1_wgrad, adam_step, scale_cast_bf16, bf16_to_f32 (csrc/kernels/*.hip).
+fc1_dgrad, conv2_bwd (+ fused conv1 wgrad), conv2_wgrad_reduce, adam_step, scale_cast_bf16, bf16_to_f32,
+segment_dots, adasum_combine, grad_check_, update_scale_ (csrc/kernels/*.hip).
 """
 from .. import _native
 

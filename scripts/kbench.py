@@ -45,16 +45,15 @@ def main():
                                          tr.gview("conv_layer2/conv2d/bias"), tr.gview("conv_layer1/conv2d/kernel"),
                                          tr.gview("conv_layer1/conv2d/bias")),
         "fc1_dgrad": lambda: o.fc1_dgrad(tr.dz, tr.pview("dense/kernel", sh), tr.a2, tr.g2),
-        "conv2_bwd": lambda: o.conv2_bwd(tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.g1,
-                                         tr.slab, tr.gview("conv_layer2/conv2d/bias")),
-        "conv1_wgrad": lambda: o.conv1_wgrad(tr.x_buf, None, st, tr.g1, tr.idx1, tr.slab,
-                                             tr.gview("conv_layer1/conv2d/kernel"), tr.gview("conv_layer1/conv2d/bias"),
-                                             tr.gview("conv_layer2/conv2d/kernel")),
+        "conv2_bwd": lambda: o.conv2_bwd(tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf,
+                                         None, st, tr.idx1, tr.slab, tr.gview("conv_layer2/conv2d/bias"),
+                                         tr.gview("conv_layer1/conv2d/kernel"), tr.gview("conv_layer1/conv2d/bias")),
+        "conv2_wgrad_reduce": lambda: o.conv2_wgrad_reduce(tr.slab, B, tr.gview("conv_layer2/conv2d/kernel")),
         "adam": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, sh, st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
     }
     jobs = [(name, fn, None) for name, fn in ops.items()]
     if args.roles:  # MIHVD_ROLE_ONLY is read by the host wrappers at launch (i.e. capture) time
-        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv1_wgrad", 2)):
+        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2)):
             jobs += [(f"{name}[role{r}]", ops[name], r) for r in range(n_roles)]
     if args.only:
         keep = set(args.only.split(","))
