@@ -148,6 +148,16 @@ def main():
     loss_val = None
     if args.impl == "fused":
         loss_val = float(tr.last_loss())
+    if args.impl != "fused":
+        comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
+    elif n == 1:
+        comm_desc = "none (1 GPU)"
+    elif getattr(tr, "gather", False):
+        comm_desc = ("RCCL all-gather of the bf16 fc1 factors (a2, dz) -> exact dW3 over all samples; RCCL "
+                     "allreduce of the other fp32 gradients; every step, in the HIP graph")
+    else:
+        comm_desc = "RCCL allreduce of the fp32 gradient fusion buffer every step" + (
+            " (bf16 wire)" if args.compression == "bf16" else "")
     if hvd.rank() == 0:
         rec = {
             "metric": METRIC, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": steps_timed,
@@ -157,8 +167,7 @@ def main():
                        "global_batch": args.batch_size * n, "per_gpu_batch": args.batch_size, "seq_len": None,
                        "image_shape": [28, 28, 1], "parallelism": f"dp{n}", "impl": args.impl,
                        "optimizer": "Adam (TF1 rule), lr=%g x size" % args.lr,
-                       "allreduce": "RCCL allreduce of the fp32 gradient fusion buffer every step" +
-                                    (" (bf16 wire)" if args.compression == "bf16" else ""),
+                       "allreduce": comm_desc,
                        "steps_per_graph": per_call, "final_loss": loss_val},
         }
         print(json.dumps(rec), flush=True)

@@ -259,48 +259,60 @@ constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
 
 __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
-    float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4, float* __restrict__ gb4,
-    float* __restrict__ gb2, float* __restrict__ gW1, float* __restrict__ gb1, int B, int role_base) {
+    const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
+    float* __restrict__ gW4, float* __restrict__ gb4, float* __restrict__ gb2, float* __restrict__ gW1,
+    float* __restrict__ gb1, int B, int role_base, int n_small) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
-  // The 33 small-reduction blocks come first in dispatch order so they run alongside the dW3 tiles
-  // instead of trailing them.
-  constexpr int NS = FB_TOTAL - FB_WGRAD;
+  // The small-reduction blocks (n_small = 33, or 0 when they are not launched) come first in
+  // dispatch order so they run alongside the dW3 tiles instead of trailing them.
   int bid = blockIdx.x + role_base;
-  bid = bid < NS ? FB_WGRAD + bid : bid - NS;
+  bid = bid < n_small ? FB_WGRAD + bid : bid - n_small;
   if (bid < FB_WGRAD) {
-    // dW3^T[n][j] tile = sum_b dz[b][n] a2[b][j]  -> stored as gW3[j][n..n+3] (float4 per lane)
+    // dW3^T[n][j] tile = sum_k dzw[k][n] a2w[k][j] over Kw rows (the local batch, or the batch of
+    // every rank when the factors were all-gathered) -> stored as gW3[j][n..n+3] (float4 per lane).
+    // K streams through LDS in chunks of 128 rows; the next chunk's loads are in flight while the
+    // current one is multiplied.
     const int jt = bid >> 4, ntile = bid & 15;
     const int j0 = jt * 64, n0 = ntile * 64;
-    u16* Zim = smem;                   // [Kpad][72]  rows b, cols n
-    u16* Aim = smem + MAXB * FB_TSTR;  // [Kpad][72]  rows b, cols j
-    const int Kpad = (B + 31) & ~31;
-    {
-      TileLoad<256, (MAXB * 8 + 255) / 256, 8> lz, la;
-      lz.load(dz + n0, FC1_N, Kpad, B, t);
-      la.load(a2 + j0, FC1_K, Kpad, B, t);
-      lz.store(Zim, FB_TSTR, Kpad, t);
-      la.store(Aim, FB_TSTR, Kpad, t);
-    }
-    __syncthreads();
+    u16* Zim = smem;                   // [128][72]  rows k, cols n
+    u16* Aim = smem + MAXB * FB_TSTR;  // [128][72]  rows k, cols j
     const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;  // wave's 32 (n) x 32 (j) sub-tile
     f32x4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < Kpad; k0 += 32) {
-      bf16x8 af[2], bfv[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const u16* zr = Zim + (k0 + 8 * lg + q) * FB_TSTR + wm + i * 16 + 4 * p;
-        af[i] = frag_tr(zr, zr + 4 * FB_TSTR);
-        const u16* ar = Aim + (k0 + 8 * lg + q) * FB_TSTR + wn + i * 16 + 4 * p;
-        bfv[i] = frag_tr(ar, ar + 4 * FB_TSTR);
+    TileLoad<256, (MAXB * 8 + 255) / 256, 8> lz, la;
+    {
+      const int rows = min(MAXB, Kw);
+      lz.load(dzw + n0, FC1_N, (rows + 31) & ~31, rows, t);
+      la.load(a2w + j0, FC1_K, (rows + 31) & ~31, rows, t);
+    }
+    for (int kc = 0; kc < Kw; kc += MAXB) {
+      const int rows = min(MAXB, Kw - kc), Kpad = (rows + 31) & ~31;
+      if (kc > 0) __syncthreads();  // the previous chunk's fragments have been read
+      lz.store(Zim, FB_TSTR, Kpad, t);
+      la.store(Aim, FB_TSTR, Kpad, t);
+      __syncthreads();
+      if (kc + MAXB < Kw) {
+        const int nrows = min(MAXB, Kw - kc - MAXB);
+        lz.load(dzw + (int64_t)(kc + MAXB) * FC1_N + n0, FC1_N, (nrows + 31) & ~31, nrows, t);
+        la.load(a2w + (int64_t)(kc + MAXB) * FC1_K + j0, FC1_K, (nrows + 31) & ~31, nrows, t);
       }
+      for (int k0 = 0; k0 < Kpad; k0 += 32) {
+        bf16x8 af[2], bfv[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i) {
+          const u16* zr = Zim + (k0 + 8 * lg + q) * FB_TSTR + wm + i * 16 + 4 * p;
+          af[i] = frag_tr(zr, zr + 4 * FB_TSTR);
+          const u16* ar = Aim + (k0 + 8 * lg + q) * FB_TSTR + wn + i * 16 + 4 * p;
+          bfv[i] = frag_tr(ar, ar + 4 * FB_TSTR);
+        }
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mfma16(af[i], bfv[jj], acc[i][jj]);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mfma16(af[i], bfv[jj], acc[i][jj]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -452,10 +464,13 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                                      stats.data_ptr<float>(), B);
 }
 
-// The wgrad launch completes the whole "fc" gradient bucket, so its allreduce can start while
-// dgrad and the conv backward still run.
+// roles: bit 0 = the dW3 tiles, bit 1 = the small reductions (db3, dW4, db4 + zeroing of the
+// atomic targets). dW3 multiplies dz_w3^T a2_w3 over their rows: the local dz/a2 by default, or the
+// all-gathered factors of every rank (data-parallel "factor gather": dW3 = sum over all samples,
+// exactly what the allreduce of per-rank dW3 would produce, for a fraction of the bytes).
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
-               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1) {
+               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1,
+               int64_t roles, const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_wgrad: batch");
   TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
@@ -464,13 +479,32 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_wgrad: gW3");
   TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_wgrad: fc grads");
   TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "fc1_wgrad: conv grads");
+  TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_wgrad: roles must be 1, 2 or 3");
+  const u16* dzw = (const u16*)dz.data_ptr();
+  const u16* a2w = (const u16*)a2.data_ptr();
+  int Kw = B;
+  if (dz_w3.has_value() && dz_w3->defined()) {
+    TORCH_CHECK(a2_w3.has_value() && a2_w3->defined(), "fc1_wgrad: dz_w3 and a2_w3 go together");
+    Kw = dz_w3->size(0);
+    TORCH_CHECK(dz_w3->dtype() == at::kBFloat16 && dz_w3->numel() == (int64_t)Kw * FC1_N && dz_w3->is_contiguous(),
+                "fc1_wgrad: dz_w3 [K][1024] bf16");
+    TORCH_CHECK(a2_w3->dtype() == at::kBFloat16 && a2_w3->numel() == (int64_t)Kw * FC1_K && a2_w3->is_contiguous(),
+                "fc1_wgrad: a2_w3 [K][3136] bf16");
+    TORCH_CHECK(Kw >= 1 && Kw <= 65536, "fc1_wgrad: K");
+    dzw = (const u16*)dz_w3->data_ptr();
+    a2w = (const u16*)a2_w3->data_ptr();
+  }
+  int role = debug_role_only();  // kbench: 0 = dW3 tiles only, 1 = small reductions only
+  if (role == 0) roles &= 1;
+  if (role == 1) roles &= 2;
+  const int n_small = (roles & 2) ? FB_TOTAL - FB_WGRAD : 0;
+  const int grid = n_small + ((roles & 1) ? FB_WGRAD : 0);
+  if (grid == 0) return;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  const int role = debug_role_only();  // 0: dW3 tiles only, 1: the small reductions only
-  const int grid = role == 0 ? FB_WGRAD : role == 1 ? FB_TOTAL - FB_WGRAD : FB_TOTAL;
   fc1_wgrad_kernel<<<grid, 256, FB_LDS_WG, stream>>>(
-      (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
-      gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), gb2.data_ptr<float>(),
-      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, role == 0 ? FB_TOTAL - FB_WGRAD : 0);
+      (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(), dzw, a2w,
+      Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(),
+      gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, 0, n_small);
 }
 
 // dgrad: g2 = (a2 > 0) * dz.W3^T in bf16, the gradient conv2_bwd routes through the pool argmax.

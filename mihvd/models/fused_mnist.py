@@ -45,9 +45,15 @@ from .mnist import TF_PARAM_ORDER, TF_PARAM_SHAPES, MNISTConvNet
 ALIGN = 64  # elements (256 B)
 
 
+# Flat-buffer order: TF variable order (horovod/tensorflow_mnist.py:49-70) except that dense/kernel
+# (98 % of the bytes) is moved to the end, so bucket "fc" = {dense/bias, dense_1/*, dense/kernel} is
+# one contiguous tail and "everything but dense/kernel" one contiguous head.
+LAYOUT_ORDER = [n for n in TF_PARAM_ORDER if n != "dense/kernel"] + ["dense/kernel"]
+
+
 def _layout():
     segs, off = {}, 0
-    for name in TF_PARAM_ORDER:
+    for name in LAYOUT_ORDER:
         n = math.prod(TF_PARAM_SHAPES[name])
         segs[name] = (off, n)
         off += (n + ALIGN - 1) // ALIGN * ALIGN
@@ -55,7 +61,8 @@ def _layout():
 
 
 SEGMENTS, FLAT_NUMEL = _layout()
-FC_START = SEGMENTS["dense/kernel"][0]  # bucket "fc" = [dense/kernel .. dense_1/bias]
+FC_START = SEGMENTS["dense/bias"][0]    # bucket "fc" = [dense/bias .. dense/kernel]
+W3_START = SEGMENTS["dense/kernel"][0]  # [0, W3_START) = every gradient except dense/kernel
 
 
 class FusedMNISTTrainer:
@@ -103,11 +110,25 @@ class FusedMNISTTrainer:
         u8 = dict(device=dev, dtype=torch.uint8)
         self.a1 = torch.empty(B, 14, 14, 32, **bf)
         self.idx1 = torch.empty(B, 14, 14, 32, **u8)
-        self.a2 = torch.empty(B, 3136, **bf)
+        # Data-parallel "factor gather" (size > 1, op Average/Sum): dW3 = a2^T dz has rank B, so
+        # instead of allreducing the 12.8 MB dW3 every rank all-gathers the bf16 factors a2 and dz
+        # (832 KB per rank at B=100) and multiplies them over the batch of every rank — the exact
+        # sum the allreduce would produce (fp32 accumulation over all samples), 4-16x fewer bytes.
+        from ..basics import ReduceOp
+
+        self.gather = (self.collectives and compression == "none" and os.environ.get("MIHVD_FC_GATHER", "1") != "0"
+                       and (op is None or ReduceOp(op) in (ReduceOp.Average, ReduceOp.Sum)))
+        if self.gather:
+            self.a2_all = torch.empty(self.world * B, 3136, **bf)
+            self.dz_all = torch.empty(self.world * B, 1024, **bf)
+            self.a2 = self.a2_all[self.rank * B:(self.rank + 1) * B]   # conv2_fwd writes its rows in place
+            self.dz = self.dz_all[self.rank * B:(self.rank + 1) * B]   # head writes its rows in place
+        else:
+            self.a2 = torch.empty(B, 3136, **bf)
+            self.dz = torch.empty(B, 1024, **bf)
         self.idx2 = torch.empty(B, 3136, **u8)
         self.zpart = torch.empty(14, B, 1024, **f32)
         self.h = torch.empty(B, 1024, **bf)
-        self.dz = torch.empty(B, 1024, **bf)
         self.dlog = torch.empty(B, 10, **f32)
         self.stats = torch.zeros(B, 2, **f32)
         self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
@@ -122,7 +143,7 @@ class FusedMNISTTrainer:
         self.overlap = os.environ.get("MIHVD_OVERLAP", "1") != "0"
         # MIHVD_ADAM_PIPELINE=1: the "fc" part of the Adam update runs on a side stream after the
         # last reader of W3 (fc1_dgrad) and overlaps the conv backward and the next step's convs.
-        self.pipeline = os.environ.get("MIHVD_ADAM_PIPELINE", "0") == "1"
+        self.pipeline = os.environ.get("MIHVD_ADAM_PIPELINE", "0") == "1" and not self.gather
         self.adam_blocks = int(os.environ.get("MIHVD_ADAM_BLOCKS", "0"))
         self._fc_update_pending = False
         self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline) else None
@@ -176,6 +197,8 @@ class FusedMNISTTrainer:
 
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
+        if self.gather:
+            return self._launch_step_gather(x, rows, labels)
         o = self.ops
         st = self.state
         main = torch.cuda.current_stream(self.device)
@@ -235,6 +258,58 @@ class FusedMNISTTrainer:
             self._allreduce(self.grads, 0, FLAT_NUMEL)  # one fused collective for the whole buffer
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
+
+    def _launch_step_gather(self, x, rows, labels):
+        """Step with the factor-gather data plane (see ``__init__``). Collectives run one at a time
+        on the side stream, each overlapping compute on the main stream:
+
+            main: conv1 conv2 | fc1_fwd head | fc1 small grads, fc1_dgrad, conv2_bwd, dW2 | dW3 (K = size*B) | adam
+            side:             AG(a2)        AG(dz)                                        AR(every other grad)
+        """
+        o = self.ops
+        st = self.state
+        main = torch.cuda.current_stream(self.device)
+        side = self._side
+        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
+                    self.a1, self.idx1)
+        o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
+                    self.a2, self.idx2)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._all_gather_rows(self.a2_all, self.a2)
+        o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
+        o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
+                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._all_gather_rows(self.dz_all, self.dz)
+        gW3 = self.gview("dense/kernel")
+        small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
+                 self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
+                 self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
+        o.fc1_wgrad(*small, 2)  # db3, dW4, db4 of the local batch (+ zero conv2_bwd's atomic targets)
+        o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
+        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows, st,
+                    self.idx1, self.slab, self.gview("conv_layer2/conv2d/bias"), self.gview("conv_layer1/conv2d/kernel"),
+                    self.gview("conv_layer1/conv2d/bias"))
+        o.conv2_wgrad_reduce(self.slab, self.B, self.gview("conv_layer2/conv2d/kernel"))
+        main.wait_stream(side)   # both gathers done: the communicator is free
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._allreduce(self.grads[:W3_START], 0, W3_START)
+        o.fc1_wgrad(*small, 1, self.dz_all, self.a2_all)  # dW3 summed over every rank's samples
+        main.wait_stream(side)
+        b1, b2 = self.betas
+        o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
+                    1.0 / self.world, self.rule, 1)
+
+    def _all_gather_rows(self, full, mine):
+        import torch.distributed as dist
+
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(full, mine)  # in place: `mine` is this rank's slice of `full`
+        else:
+            dist.all_gather(list(full.chunk(self.world)), mine.clone())
 
     def _join(self):
         """Make the current stream wait for any side-stream work of the last step."""

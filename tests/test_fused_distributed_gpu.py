@@ -33,9 +33,11 @@ def test_rccl_allreduce_inside_hip_graph(tmp_path):
     assert r["steps"] == 22 and r["rel_update_diff"] < 0.05, r
 
 
-def test_fused_data_parallel_equivalence_two_ranks(tmp_path):
+@pytest.mark.parametrize("gather", ["1", "0"])
+def test_fused_data_parallel_equivalence_two_ranks(tmp_path, gather):
+    """gather=1: dW3 from all-gathered factors (the default data plane); gather=0: bucket allreduce."""
     _gpu()
-    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT)
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather)
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]

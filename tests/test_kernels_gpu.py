@@ -158,6 +158,14 @@ def test_fc1_bwd(ops, B):
     ops.fc1_dgrad(dz.to(torch.bfloat16), w3.to(torch.bfloat16), a2.to(torch.bfloat16), g2)
     assert rel_err(g2, (dz @ w3.t()) * (a2 > 0)) < 5e-3
     assert rel_err(gW3, a2.t() @ dz) < 1e-4
+    # dW3 over gathered factors (K = 3 ranks x B rows, streamed through LDS in 128-row chunks)
+    K = 3 * B
+    dzk = bf(torch.randn(K, 1024, device="cuda", generator=g) * 0.01)
+    a2k = bf(F.relu(torch.randn(K, 3136, device="cuda", generator=g)))
+    gW3k = torch.empty_like(gW3)
+    ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3k, gb3, gW4, gb4, gb2,
+                  gW1, gb1, 1, dzk.to(torch.bfloat16), a2k.to(torch.bfloat16))
+    assert rel_err(gW3k, a2k.t() @ dzk) < 1e-4
     assert rel_err(gb3, dz.sum(0)) < 1e-4
     assert rel_err(gW4, h.t() @ dlog) < 1e-4
     assert rel_err(gb4, dlog.sum(0)) < 1e-4

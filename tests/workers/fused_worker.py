@@ -52,6 +52,7 @@ def sc_dp_gloo(outdir):
     r = hvd.rank()
     X, Y = data(600)
     tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda")
+    assert tr.gather == (os.environ.get("MIHVD_FC_GATHER", "1") != "0")
     tr.broadcast(0)
     ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", world_size=1)
     p0 = ref.params.clone()
@@ -69,7 +70,7 @@ def sc_dp_gloo(outdir):
     mx = (tr.params - ref.params).abs().max().item()
     spread = hvd.allgather(tr.params[:4096].cpu().view(1, -1))
     with open(os.path.join(outdir, f"dp_gloo.{r}.json"), "w") as f:
-        json.dump({"grad_rel": grel, "rel_update_diff": rel, "max": mx,
+        json.dump({"gather": tr.gather, "grad_rel": grel, "rel_update_diff": rel, "max": mx,
                    "rank_spread": (spread - spread[0]).abs().max().item()}, f)
 
 
