@@ -48,6 +48,11 @@ class Config:
     fault: str = ""                       # fault-injection spec (tests)
     log_level: str = "INFO"
     timeout_s: float = 600.0              # process-group timeout
+    autotune: bool = False                # grid-search the fusion threshold during the first steps
+    autotune_candidates: str = "1,4,16,64"  # MiB
+    autotune_warmup_steps: int = 3
+    autotune_trial_steps: int = 8
+    roctx: bool = False                   # roctx ranges around collectives / steps (rocprofv3 --marker-trace)
 
     @staticmethod
     def from_env(env=None) -> "Config":
@@ -67,4 +72,9 @@ class Config:
             fault=_get("FAULT", "", str, env),
             log_level=_get("LOG_LEVEL", "INFO", str, env).upper(),
             timeout_s=_get("TIMEOUT_SECONDS", 600.0, float, env),
+            autotune=_get("AUTOTUNE", False, bool, env),
+            autotune_candidates=_get("AUTOTUNE_CANDIDATES", "1,4,16,64", str, env),
+            autotune_warmup_steps=_get("AUTOTUNE_WARMUP_STEPS", 3, int, env),
+            autotune_trial_steps=_get("AUTOTUNE_TRIAL_STEPS", 8, int, env),
+            roctx=_get("ROCTX", False, bool, env),
         )

@@ -40,6 +40,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from ..utils.tracing import trace_range
 from .mnist import TF_PARAM_ORDER, TF_PARAM_SHAPES, MNISTConvNet
 
 ALIGN = 64  # elements (256 B)
@@ -342,8 +343,9 @@ class FusedMNISTTrainer:
         self.x_buf.copy_(x.reshape(self.B, 784), non_blocking=True)
         self.y_buf.copy_(y.reshape(self.B), non_blocking=True)
         # Host-fed batches index rows 0..B-1 of x_buf (rows=None); the step counter still advances.
-        self._launch_step(self.x_buf, None, self.y_buf)
-        self._join()
+        with trace_range("mihvd.fused_step"):
+            self._launch_step(self.x_buf, None, self.y_buf)
+            self._join()
         self.global_step += 1
         return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
 
@@ -352,8 +354,9 @@ class FusedMNISTTrainer:
         if self.X is None:
             raise RuntimeError("call set_device_dataset() first")
         self._maybe_reshuffle(1)
-        self._launch_step(self.X, self.rows, self.Y)
-        self._join()
+        with trace_range("mihvd.fused_step"):
+            self._launch_step(self.X, self.rows, self.Y)
+            self._join()
         self.global_step += 1
         return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
 
@@ -411,7 +414,8 @@ class FusedMNISTTrainer:
                 self.device_step()
             return
         self._maybe_reshuffle(self.steps_per_replay)
-        self.graph.replay()
+        with trace_range(f"mihvd.graph_replay[{self.steps_per_replay} steps]"):
+            self.graph.replay()
         self.global_step += self.steps_per_replay
 
     def last_loss(self) -> float:

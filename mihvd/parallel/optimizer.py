@@ -28,6 +28,7 @@ import torch.distributed as dist
 from .. import basics
 from ..basics import ReduceOp
 from . import collectives as C
+from ..utils.tracing import trace_range
 from .compression import Compression
 
 _DTYPE_CODES: dict[torch.dtype, int] = {}
@@ -89,14 +90,34 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._params = params
         self._names = [names.get(id(p), f"param.{i}") for i, p in enumerate(params)]
         self._index = {id(p): i for i, p in enumerate(params)}
+        cfg = basics.config()
+        thresh = cfg.fusion_threshold if fusion_threshold is None else int(fusion_threshold)
+        self._tuner = None
+        if cfg.autotune and fusion_threshold is None and basics.size() > 1:
+            from .autotune import FusionAutotuner
+
+            self._tuner = FusionAutotuner.from_config(cfg)
+            thresh = self._tuner.first()
+        self._plan(thresh)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
+        self._synchronized = False
+        self._should_sync = True
+        self._consistency_checked = not cfg.consistency_check
+        self._check_consistency()
+
+    def _plan(self, thresh: int):
+        """(Re)build the fusion buckets for ``thresh`` bytes and point every ``param.grad`` at its
+        slot (current gradient values are carried over)."""
+        from .._native import runtime
+
+        params = self._params
         rt = runtime()
         specs = [rt.TensorSpec(p.numel(), p.element_size(), _dtype_code(p.dtype),
                                (p.device.index if p.device.index is not None else -1) if p.is_cuda else -2)
                  for p in params]
-        cfg = basics.config()
-        thresh = cfg.fusion_threshold if fusion_threshold is None else int(fusion_threshold)
         order = list(range(len(params)))[::-1]
-        plan = rt.plan_buckets(specs, order, thresh, cfg.bucket_align) if params else None
+        plan = rt.plan_buckets(specs, order, int(thresh), basics.config().bucket_align) if params else None
+        self._fusion_threshold = int(thresh)
         self._buckets: list[_Bucket] = []
         if plan is not None:
             for b in range(len(plan)):
@@ -107,14 +128,9 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self._tensor_bucket = list(plan.tensor_bucket)
             self._tensor_offset = list(plan.tensor_offset)
             self._controller = rt.Controller(self._tensor_bucket, len(self._buckets), self._passes)
+            self._install_grad_views()
         else:
             self._controller = None
-        self._install_grad_views()
-        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
-        self._synchronized = False
-        self._should_sync = True
-        self._consistency_checked = not cfg.consistency_check
-        self._check_consistency()
 
     # -- gradient views --------------------------------------------------------------------
     def _install_grad_views(self):
@@ -171,6 +187,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         return hook
 
     def _launch(self, bid: int):
+        with trace_range(f"mihvd.bucket{bid}.allreduce"):
+            self._launch_impl(bid)
+
+    def _launch_impl(self, bid: int):
         b = self._buckets[bid]
         if self._op == ReduceOp.Average and self._predivide != 1.0:
             pre, post = 1.0 / self._predivide, self._predivide
@@ -189,12 +209,13 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             return
         if not self._views_intact():
             self._install_grad_views()
-        for bid in self._controller.flush():
-            self._launch(bid)
-        for b in self._buckets:
-            if b.handle is not None:
-                C.synchronize(b.handle)
-                b.handle = None
+        with trace_range("mihvd.synchronize"):
+            for bid in self._controller.flush():
+                self._launch(bid)
+            for b in self._buckets:
+                if b.handle is not None:
+                    C.synchronize(b.handle)
+                    b.handle = None
         self._controller.reset()
         self._synchronized = True
 
@@ -213,7 +234,17 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 warnings.warn("optimizer.step() called without a backward pass since the last synchronize()")
             self.synchronize()
         self._synchronized = False
-        return super(self.__class__, self).step(closure)
+        with trace_range("mihvd.optimizer_step"):
+            out = super(self.__class__, self).step(closure)
+        if self._tuner is not None:
+            new = self._tuner.on_step()
+            if new is not None and new != self._fusion_threshold:
+                self._plan(new)
+        return out
+
+    @property
+    def fusion_threshold(self) -> int:
+        return self._fusion_threshold
 
     def zero_grad(self, set_to_none: bool = True):
         # Gradients live inside the fusion buffers: zero them in place and keep the views.

@@ -64,6 +64,16 @@ def test_dp_equivalence_four_ranks(tmp_path):
     assert all(o["maxdiff_0"] < 1e-5 for o in outs)
 
 
+def test_fusion_autotune(tmp_path):
+    env = {"MIHVD_AUTOTUNE": "1", "MIHVD_AUTOTUNE_CANDIDATES": "0.0001,64", "MIHVD_AUTOTUNE_WARMUP_STEPS": "1",
+           "MIHVD_AUTOTUNE_TRIAL_STEPS": "3"}
+    _, (a, b) = run_scenario(tmp_path, "autotune", env=env)
+    for o in (a, b):
+        assert o["done"] and o["final"] == o["best"] and o["maxdiff"] < 1e-5
+        assert len(o["seen"]) == 2  # both candidates were tried
+    assert a["best"] == b["best"]  # every rank chose the same threshold
+
+
 def test_backward_passes_per_step(tmp_path):
     _, outs = run_scenario(tmp_path, "bpps")
     assert all(o["diff"] < 1e-4 for o in outs)

@@ -309,3 +309,30 @@ def test_adasum_covering_offsets():
     assert _covering_offsets([(0, 5), (8, 10)], 12) == ([0, 5, 8, 10, 12], [0, 1, 0, 1])
     assert _covering_offsets([(0, 12)], 12) == ([0, 12], [0])
     assert _covering_offsets([(2, 4)], 4) == ([0, 2, 4], [1, 0])
+
+
+def test_autotuner_picks_fastest(monkeypatch, hvd_single):
+    from mihvd.parallel.autotune import FusionAutotuner
+
+    tu = FusionAutotuner(["1", "4", "16"], warmup_steps=1, trial_steps=2)
+    cost = {1: 3.0, 4: 1.0, 16: 2.0}
+    clock = [0.0]
+    cur = [tu.first()]
+    monkeypatch.setattr(tu, "_now", lambda: clock[0])
+    decided = None
+    for _ in range(40):
+        clock[0] += cost[cur[0] // 2 ** 20]
+        new = tu.on_step()
+        if new is not None:
+            cur[0] = new
+            if tu.done:
+                decided = new
+                break
+    assert tu.done and decided == 4 * 2 ** 20
+
+
+def test_trace_range_noop_without_roctx():
+    from mihvd.utils.tracing import trace_range
+
+    with trace_range("x"):
+        pass

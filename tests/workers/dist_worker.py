@@ -87,6 +87,31 @@ def sc_dp_equivalence(outdir):
     out(outdir, "dp_equivalence", res)
 
 
+def sc_autotune(outdir):
+    """MIHVD_AUTOTUNE=1: the optimizer tries each fusion threshold, every rank settles on the same
+    one, re-plans its buckets once, and training still equals the single-process reference."""
+    r, n = hvd.rank(), hvd.size()
+    gen = torch.Generator().manual_seed(9)
+    X = torch.randn(n * 4, 8, generator=gen)
+    Y = torch.randn(n * 4, 4, generator=gen)
+    m = _model(seed=3)
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.05), named_parameters=m.named_parameters())
+    ref = _model(seed=3)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05)
+    seen = set()
+    for step in range(20):
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(m(X[r * 4:(r + 1) * 4]), Y[r * 4:(r + 1) * 4]).backward()
+        opt.step()
+        seen.add(opt.fusion_threshold)
+        ropt.zero_grad()
+        torch.nn.functional.mse_loss(ref(X), Y).backward()
+        ropt.step()
+    diff = max((a - b).abs().max().item() for a, b in zip(m.parameters(), ref.parameters()))
+    out(outdir, "autotune", {"done": opt._tuner.done, "best": opt._tuner.best, "final": opt.fusion_threshold,
+                             "seen": sorted(seen), "maxdiff": diff, "nbuckets": len(opt.buckets)})
+
+
 def sc_bpps(outdir):
     """backward_passes_per_step=2 accumulates locally, then one allreduce."""
     r, n = hvd.rank(), hvd.size()
