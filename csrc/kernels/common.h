@@ -130,6 +130,13 @@ inline int debug_role_only() {
   return e ? atoi(e) : -1;
 }
 
+// Profiling aid: MIHVD_DEBUG_EXIT=<phase> makes instrumented kernels return after that phase
+// (results are then incomplete), so the cost of each phase can be read off kernel times.
+inline int debug_phase_exit() {
+  const char* e = getenv("MIHVD_DEBUG_EXIT");
+  return e ? atoi(e) : 0;
+}
+
 // Step-state words kept on the device so a whole training step replays from a HIP graph:
 //   state[0] = forward step index (read by data/dropout kernels, bumped by the optimizer)
 //   state[1] = optimizer step t   (bumped by the head kernel, read by the optimizer)

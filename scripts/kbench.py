@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--json", default="")
     ap.add_argument("--roles", action="store_true", help="also time each block role of multi-role launches")
+    ap.add_argument("--phases", action="store_true", help="time conv2_bwd's dgrad role cut after each phase")
     ap.add_argument("--only", default="", help="comma-separated job names (e.g. 'conv2_bwd[role0]'); skips the step")
     args = ap.parse_args()
     from mihvd.models.fused_mnist import FusedMNISTTrainer
@@ -55,14 +56,20 @@ def main():
     if args.roles:  # MIHVD_ROLE_ONLY is read by the host wrappers at launch (i.e. capture) time
         for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2)):
             jobs += [(f"{name}[role{r}]", ops[name], r) for r in range(n_roles)]
+    if args.phases:  # MIHVD_DEBUG_EXIT: conv2_bwd dgrad role cut after phase p (1 staging, 2 GEMM, 3 epilogue)
+        jobs += [(f"conv2_bwd[role0,exit{p}]", ops["conv2_bwd"], (0, p)) for p in (1, 2, 3)]
     if args.only:
         keep = set(args.only.split(","))
         jobs = [j for j in jobs if j[0] in keep]
     res = {}
     s = torch.cuda.Stream()
     for name, fn, role in jobs:
+        os.environ.pop("MIHVD_DEBUG_EXIT", None)
         if role is None:
             os.environ.pop("MIHVD_ROLE_ONLY", None)
+        elif isinstance(role, tuple):
+            os.environ["MIHVD_ROLE_ONLY"] = str(role[0])
+            os.environ["MIHVD_DEBUG_EXIT"] = str(role[1])
         else:
             os.environ["MIHVD_ROLE_ONLY"] = str(role)
         for _ in range(3):
@@ -80,8 +87,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         res[name] = e0.elapsed_time(e1) * 1000.0 / args.iters
-        print(f"{name:18s} {res[name]:8.2f} us", flush=True)
+        print(f"{name:24s} {res[name]:8.2f} us", flush=True)
     os.environ.pop("MIHVD_ROLE_ONLY", None)
+    os.environ.pop("MIHVD_DEBUG_EXIT", None)
     if args.only:
         if args.json:
             with open(args.json, "w") as f:
