@@ -57,6 +57,9 @@ constexpr int CB_LDS = CB_DG_LDS > CB_WG_LDS ? CB_DG_LDS : CB_WG_LDS;
 //     Five copies of the bf16 image shifted by kw = 0..4 make that one aligned ds_read_b128.
 //   * the eight waves split K (image rows w, w+8, ...) and are summed through LDS before the atomics.
 // ------------------------------------------------------------------------------------------ //
+// Per-image partial row of the small conv gradients, reduced (in a fixed order: deterministic, no
+// atomics contending for the same few cache lines) by conv2_wgrad_reduce.
+constexpr int CP_DB1 = 800, CP_DB2 = 832, CP_W = 896;  // [dW1 (800) | db1 (32) | db2 (64)]
 constexpr int C1_DSTR = 40;                          // dY1 row stride (32 co + 8 pad)
 constexpr int C1_DY = 785 * C1_DSTR;                 // elements; row 784 = zeros
 constexpr int C1_XS = 32 * 32;                       // one shifted bf16 image copy [32][32]
@@ -94,8 +97,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
-    float* __restrict__ slab, float* __restrict__ gb2, float* __restrict__ gW1, float* __restrict__ gb1, int B,
-    int n_dgrad, int dbg_exit) {
+    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
@@ -287,14 +289,14 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       const int co4 = t >> 2, c = t & 3;
       float sacc = 0.f;
       for (int r = co4; r < 512; r += 16) sacc += red[r * 4 + c];
-      atomicAdd(gb2 + co4 * 4 + c, sacc);
+      cpart[(int64_t)b * CP_W + CP_DB2 + co4 * 4 + c] = sacc;
     } else if (t < 96) {
       // db1 channel ch = 16nt + 4lg + i
       const int ch = t - 64, nt = ch >> 4, lgg = (ch >> 2) & 3, i = ch & 3;
       float sacc = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) sacc += red1[(w * 4 + lgg) * 8 + nt * 4 + i];
-      atomicAdd(gb1 + ch, sacc);
+      cpart[(int64_t)b * CP_W + CP_DB1 + ch] = sacc;
     }
     for (int i = t; i < 5 * 32 * 4; i += 512) {
       const int kw = i >> 7, r = (i >> 2) & 31, c0 = (i & 3) * 8;
@@ -348,7 +350,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) v += part[w * 64 * 16 + slot];
-      atomicAdd(gW1 + o, v);  // HWIO: tap * 32 + co
+      cpart[(int64_t)b * CP_W + o] = v;  // dW1 in HWIO order: tap * 32 + co
     }
     return;
   }
@@ -463,12 +465,41 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
   }
 }
 
-// dW2 = sum of the (<= 32) conv2 wgrad slabs. Block = 64 float4 outputs x 4 slab groups of 8, every
-// load in flight at once (absent slabs masked, not branched around), then a 4-way LDS sum.
+// Blocks [0, 200): dW2 = sum of the (<= 32) conv2 wgrad slabs; 64 float4 outputs x 4 slab groups of
+// 8 per block, every load in flight at once (absent slabs masked, not branched around), then a
+// 4-way LDS sum. Blocks [200, 214): dW1 | db1 | db2 = sum over images of the per-image partial rows;
+// 64 outputs x 4 row groups per block, 8 rows per load batch.
+constexpr int CR_SLAB_BLOCKS = 200, CR_PART_BLOCKS = CP_W / 64;
 __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab,
-                                                                 float* __restrict__ gW2) {
+                                                                 const float* __restrict__ cpart, int B,
+                                                                 float* __restrict__ gW2, float* __restrict__ gW1,
+                                                                 float* __restrict__ gb1, float* __restrict__ gb2) {
   __shared__ float4 r4[256];
   const int t = threadIdx.x;
+  if ((int)blockIdx.x >= CR_SLAB_BLOCKS) {
+    float* r1 = reinterpret_cast<float*>(r4);
+    const int o = ((int)blockIdx.x - CR_SLAB_BLOCKS) * 64 + (t & 63), rg = t >> 6;
+    float acc = 0.f;
+    for (int r0 = rg * 8; r0 < B; r0 += 32) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = r0 + k;
+        v[k] = mask_f(cpart[(int64_t)min(r, B - 1) * CP_W + o], r < B);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+    r1[t] = acc;
+    __syncthreads();
+    if (t < 64) {
+      const float s = (r1[t] + r1[64 + t]) + (r1[128 + t] + r1[192 + t]);
+      if (o < CP_DB1) gW1[o] = s;
+      else if (o < CP_DB2) gb1[o - CP_DB1] = s;
+      else gb2[o - CP_DB2] = s;
+    }
+    return;
+  }
   const int o = (int)blockIdx.x * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
   float4 v[8];
 #pragma unroll
@@ -495,8 +526,7 @@ int64_t conv2_wgrad_groups(int64_t B) { return (B + CB_IPB - 1) / CB_IPB; }
 
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1,
-               const c10::optional<at::Tensor>& g1) {
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
@@ -505,9 +535,8 @@ void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a
   TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200, "conv2_bwd: w2");
   TORCH_CHECK(x.dtype() == at::kFloat && x.size(-1) == 784 && x.is_contiguous(), "conv2_bwd: x");
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_bwd: slab must hold ceil(B/4) x 51200");
-  TORCH_CHECK(gb2.numel() == 64 && gb2.dtype() == at::kFloat, "conv2_bwd: gb2");
-  TORCH_CHECK(gW1.numel() == 800 && gb1.numel() == 32 && gW1.dtype() == at::kFloat && gb1.dtype() == at::kFloat,
-              "conv2_bwd: gW1/gb1");
+  TORCH_CHECK(cpart.dtype() == at::kFloat && cpart.numel() >= (int64_t)B * CP_W && cpart.is_contiguous(),
+              "conv2_bwd: cpart must hold B x 896 floats (per-image dW1 | db1 | db2)");
   u16* g1p = nullptr;
   if (g1.has_value() && g1->defined()) {
     TORCH_CHECK(g1->dtype() == at::kBFloat16 && g1->numel() == a1.numel(), "conv2_bwd: g1");
@@ -529,17 +558,23 @@ void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a
   const int grid = role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
   conv2_bwd_kernel<<<grid, 512, CB_LDS, stream>>>(
       (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
-      x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(), gb2.data_ptr<float>(),
-      gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, n_dgrad, debug_phase_exit());
+      x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
+      cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit());
 }
 
-void conv2_wgrad_reduce(const at::Tensor& slab, int64_t B, at::Tensor& gW2) {
+void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2, at::Tensor& gW1,
+                        at::Tensor& gb1, at::Tensor& gb2) {
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(G >= 1 && G <= 32, "conv2_wgrad_reduce: at most 32 wgrad slabs");
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_wgrad_reduce: slab");
+  TORCH_CHECK(cpart.dtype() == at::kFloat && cpart.numel() >= B * CP_W, "conv2_wgrad_reduce: cpart");
   TORCH_CHECK(gW2.dtype() == at::kFloat && gW2.numel() == 51200 && gW2.is_contiguous(), "conv2_wgrad_reduce: gW2");
+  TORCH_CHECK(gW1.numel() == 800 && gb1.numel() == 32 && gb2.numel() == 64 && gW1.dtype() == at::kFloat &&
+                  gb1.dtype() == at::kFloat && gb2.dtype() == at::kFloat, "conv2_wgrad_reduce: gW1/gb1/gb2");
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv2_wgrad_reduce_kernel<<<200, 256, 0, stream>>>(slab.data_ptr<float>(), G, gW2.data_ptr<float>());
+  conv2_wgrad_reduce_kernel<<<CR_SLAB_BLOCKS + CR_PART_BLOCKS, 256, 0, stream>>>(
+      slab.data_ptr<float>(), G, cpart.data_ptr<float>(), (int)B, gW2.data_ptr<float>(), gW1.data_ptr<float>(),
+      gb1.data_ptr<float>(), gb2.data_ptr<float>());
 }
 
 }  // namespace mihvd

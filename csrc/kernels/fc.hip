@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 // ------------------------------------------------------------------------------------------ //
 // fc1_wgrad roles (dispatch order: the 33 small blocks first, then the 784 dW3 tiles):
 //   wgrad : 64x64 tile of dW3 = a2^T dz   (K = batch, zero padded)
-//   db3 (16 blocks), dW4 (16 blocks), misc: db4 + zero gb2/gW1/gb1 (atomic targets)
+//   db3 (16 blocks), dW4 (16 blocks), misc: db4
 // ------------------------------------------------------------------------------------------ //
 constexpr int FB_WGRAD = (FC1_K / 64) * (FC1_N / 64);            // 784
 constexpr int FB_DB3 = FC1_N / 64, FB_DW4 = FC1_N / 64, FB_MISC = 1;  // 16 + 16 + 1 blocks
@@ -260,8 +260,7 @@ constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
 __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
     const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
-    float* __restrict__ gW4, float* __restrict__ gb4, float* __restrict__ gb2, float* __restrict__ gW1,
-    float* __restrict__ gb1, int B, int role_base, int n_small) {
+    float* __restrict__ gW4, float* __restrict__ gb4, int B, int role_base, int n_small) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
@@ -377,8 +376,7 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     }
     return;
   }
-  // misc: db4 (thread = class c, row group), and zero the gradients that conv2_bwd
-  // accumulate with atomics
+  // misc: db4 (thread = class c, row group)
   {
     float* red = reinterpret_cast<float*>(smem);
     const int c = t % 10, g = t / 10;  // 25 groups x 10 classes = 250 threads
@@ -394,9 +392,6 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
       for (int i = 0; i < 6; ++i) s += v[i];
     }
     red[t] = s;
-    if (t < 64) gb2[t] = 0.f;
-    if (t < 32) gb1[t] = 0.f;
-    for (int i = t; i < 800; i += 256) gW1[i] = 0.f;
     __syncthreads();
     if (t < 10) {
       float tot = 0.f;
@@ -464,13 +459,11 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                                      stats.data_ptr<float>(), B);
 }
 
-// roles: bit 0 = the dW3 tiles, bit 1 = the small reductions (db3, dW4, db4 + zeroing of the
-// atomic targets). dW3 multiplies dz_w3^T a2_w3 over their rows: the local dz/a2 by default, or the
+// roles: bit 0 = the dW3 tiles, bit 1 = the small reductions (db3, dW4, db4). dW3 multiplies dz_w3^T a2_w3 over their rows: the local dz/a2 by default, or the
 // all-gathered factors of every rank (data-parallel "factor gather": dW3 = sum over all samples,
 // exactly what the allreduce of per-rank dW3 would produce, for a fraction of the bytes).
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
-               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1,
-               int64_t roles, const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3) {
+               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_wgrad: batch");
   TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
@@ -478,7 +471,6 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   TORCH_CHECK(h.numel() == (int64_t)B * FC1_N && h.dtype() == at::kBFloat16 && dlog.numel() == B * 10, "fc1_wgrad: h/dlog");
   TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_wgrad: gW3");
   TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_wgrad: fc grads");
-  TORCH_CHECK(gb2.numel() == 64 && gW1.numel() == 800 && gb1.numel() == 32, "fc1_wgrad: conv grads");
   TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_wgrad: roles must be 1, 2 or 3");
   const u16* dzw = (const u16*)dz.data_ptr();
   const u16* a2w = (const u16*)a2.data_ptr();
@@ -504,7 +496,7 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   fc1_wgrad_kernel<<<grid, 256, FB_LDS_WG, stream>>>(
       (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(), dzw, a2w,
       Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(),
-      gb2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), B, 0, n_small);
+      B, 0, n_small);
 }
 
 // dgrad: g2 = (a2 > 0) * dz.W3^T in bf16, the gradient conv2_bwd routes through the pool argmax.

@@ -13,15 +13,15 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
-               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1,
-               int64_t roles, const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3);
+               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
+               const c10::optional<at::Tensor>& a2_w3);
 void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& g2);
 int64_t conv2_wgrad_groups(int64_t B);
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& gb2, at::Tensor& gW1, at::Tensor& gb1,
-               const c10::optional<at::Tensor>& g1);
-void conv2_wgrad_reduce(const at::Tensor& slab, int64_t B, at::Tensor& gW2);
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1);
+void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2, at::Tensor& gW1,
+                        at::Tensor& gb1, at::Tensor& gb2);
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
                double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale,
@@ -54,17 +54,18 @@ void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tens
   mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats);
 }
 void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, Tensor gW3, Tensor gb3,
-                  Tensor gW4, Tensor gb4, Tensor gb2, Tensor gW1, Tensor gb1, int64_t roles, const OptT& dz_w3,
-                  const OptT& a2_w3) {
-  mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, gb2, gW1, gb1, roles, dz_w3, a2_w3);
+                  Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3) {
+  mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3);
 }
 void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, const Tensor& a2, Tensor g2) { mihvd::fc1_dgrad(dz, w3, a2, g2); }
 void conv2_bwd_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, const Tensor& x,
-                  const OptT& rows, const OptT& state, const Tensor& idx1, Tensor slab, Tensor gb2, Tensor gW1, Tensor gb1,
-                  const OptT& g1) {
-  mihvd::conv2_bwd(g2, idx2, a1, w2, x, rows, state, idx1, slab, gb2, gW1, gb1, g1);
+                  const OptT& rows, const OptT& state, const Tensor& idx1, Tensor slab, Tensor cpart, const OptT& g1) {
+  mihvd::conv2_bwd(g2, idx2, a1, w2, x, rows, state, idx1, slab, cpart, g1);
 }
-void conv2_wgrad_reduce_op(const Tensor& slab, int64_t B, Tensor gW2) { mihvd::conv2_wgrad_reduce(slab, B, gW2); }
+void conv2_wgrad_reduce_op(const Tensor& slab, const Tensor& cpart, int64_t B, Tensor gW2, Tensor gW1, Tensor gb1,
+                           Tensor gb2) {
+  mihvd::conv2_wgrad_reduce(slab, cpart, B, gW2, gW1, gb1, gb2);
+}
 void adam_op(Tensor p, const Tensor& g, Tensor m, Tensor v, const OptT& shadow, const OptT& state, int64_t host_step,
              double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, int64_t bump,
              const OptT& loss_scale, int64_t max_blocks) {
@@ -93,13 +94,13 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
   m.def("fc1_wgrad(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
-        "Tensor(d!) gb4, Tensor(e!) gb2, Tensor(f!) gW1, Tensor(g!) gb1, int roles=3, Tensor? dz_w3=None, "
-        "Tensor? a2_w3=None) -> ()");
+        "Tensor(d!) gb4, int roles=3, Tensor? dz_w3=None, Tensor? a2_w3=None) -> ()");
   m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor a2, Tensor(a!) g2) -> ()");
   m.def("conv2_wgrad_groups(int B) -> int", &mihvd::conv2_wgrad_groups);
   m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, Tensor? state, Tensor idx1, "
-        "Tensor(a!) slab, Tensor(b!) gb2, Tensor(c!) gW1, Tensor(d!) gb1, Tensor(e!)? g1=None) -> ()");
-  m.def("conv2_wgrad_reduce(Tensor slab, int B, Tensor(a!) gW2) -> ()");
+        "Tensor(a!) slab, Tensor(b!) cpart, Tensor(c!)? g1=None) -> ()");
+  m.def("conv2_wgrad_reduce(Tensor slab, Tensor cpart, int B, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
+        "Tensor(d!) gb2) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
         "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1, "
         "Tensor? loss_scale=None, int max_blocks=0) -> ()");

@@ -134,6 +134,7 @@ class FusedMNISTTrainer:
         self.stats = torch.zeros(B, 2, **f32)
         self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
+        self.cpart = torch.empty(B, 896, **f32)     # per-image dW1 | db1 | db2 partial rows
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
@@ -215,8 +216,7 @@ class FusedMNISTTrainer:
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
-                    self.gview("dense_1/kernel"), self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
-                    self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
+                    self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
         fc_bucket = self.grads[FC_START:]
         conv_bucket = self.grads[:FC_START]
         overlap = self.collectives and self.overlap
@@ -240,10 +240,7 @@ class FusedMNISTTrainer:
                             self.shadow[FC_START:], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 0,
                             None, self.adam_blocks)
             self._fc_update_pending = True
-        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows, st,
-                    self.idx1, self.slab, self.gview("conv_layer2/conv2d/bias"), self.gview("conv_layer1/conv2d/kernel"),
-                    self.gview("conv_layer1/conv2d/bias"))
-        o.conv2_wgrad_reduce(self.slab, self.B, self.gview("conv_layer2/conv2d/kernel"))
+        self._conv_backward(x, rows, st)
         if self.pipeline:
             if self.collectives:
                 if ar_done is not None:
@@ -286,14 +283,10 @@ class FusedMNISTTrainer:
             self._all_gather_rows(self.dz_all, self.dz)
         gW3 = self.gview("dense/kernel")
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
-                 self.gview("dense_1/bias"), self.gview("conv_layer2/conv2d/bias"),
-                 self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"))
-        o.fc1_wgrad(*small, 2)  # db3, dW4, db4 of the local batch (+ zero conv2_bwd's atomic targets)
+                 self.gview("dense_1/bias"))
+        o.fc1_wgrad(*small, 2)  # db3, dW4, db4 of the local batch
         o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
-        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows, st,
-                    self.idx1, self.slab, self.gview("conv_layer2/conv2d/bias"), self.gview("conv_layer1/conv2d/kernel"),
-                    self.gview("conv_layer1/conv2d/bias"))
-        o.conv2_wgrad_reduce(self.slab, self.B, self.gview("conv_layer2/conv2d/kernel"))
+        self._conv_backward(x, rows, st)
         main.wait_stream(side)   # both gathers done: the communicator is free
         side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -303,6 +296,14 @@ class FusedMNISTTrainer:
         b1, b2 = self.betas
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
+
+    def _conv_backward(self, x, rows, st):
+        o = self.ops
+        o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows, st,
+                    self.idx1, self.slab, self.cpart)
+        o.conv2_wgrad_reduce(self.slab, self.cpart, self.B, self.gview("conv_layer2/conv2d/kernel"),
+                             self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"),
+                             self.gview("conv_layer2/conv2d/bias"))
 
     def _all_gather_rows(self, full, mine):
         import torch.distributed as dist

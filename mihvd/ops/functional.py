@@ -35,7 +35,7 @@ class _Workspace:
                 a2=torch.empty(B, 3136, **bf), idx2=torch.empty(B, 3136, **u8), zpart=torch.empty(14, B, 1024, **f32),
                 h=torch.empty(B, 1024, **bf), dz=torch.empty(B, 1024, **bf), dlog=torch.empty(B, 10, **f32),
                 stats=torch.empty(B, 2, **f32), g2=torch.empty(B, 3136, **bf),
-                slab=torch.empty(int(ops.conv2_wgrad_groups(B)), 51200, **f32),
+                cpart=torch.empty(B, 896, **f32), slab=torch.empty(int(ops.conv2_wgrad_groups(B)), 51200, **f32),
                 state=torch.zeros(4, device=device, dtype=torch.int64),
                 w2bf=torch.empty(51200, **bf), w3bf=torch.empty(3136 * 1024, **bf),
             )
@@ -83,11 +83,10 @@ class _FusedMNISTLoss(torch.autograd.Function):
         ops.fc1_fwd(ws["a2"], ws["w3bf"], ws["zpart"])
         ops.head_fwd_bwd(ws["zpart"], b3, w4, b4, labels, None, st, int(seed), float(dropout), ws["h"], ws["dz"],
                          ws["dlog"], ws["stats"])
-        ops.fc1_wgrad(ws["dz"], ws["a2"], ws["h"], ws["dlog"], gW3, gb3, gW4, gb4, gb2, gW1.reshape(-1), gb1)
+        ops.fc1_wgrad(ws["dz"], ws["a2"], ws["h"], ws["dlog"], gW3, gb3, gW4, gb4)
         ops.fc1_dgrad(ws["dz"], ws["w3bf"], ws["a2"], ws["g2"])
-        ops.conv2_bwd(ws["g2"], ws["idx2"], ws["a1"], ws["w2bf"], x, None, st, ws["idx1"], ws["slab"], gb2,
-                      gW1.reshape(-1), gb1)
-        ops.conv2_wgrad_reduce(ws["slab"], B, gW2.reshape(-1))
+        ops.conv2_bwd(ws["g2"], ws["idx2"], ws["a1"], ws["w2bf"], x, None, st, ws["idx1"], ws["slab"], ws["cpart"])
+        ops.conv2_wgrad_reduce(ws["slab"], ws["cpart"], B, gW2.reshape(-1), gW1.reshape(-1), gb1, gb2)
         st[0] += 1  # next call draws a fresh dropout mask
         ctx.save_for_backward(*grads)
         acc = ws["stats"][:, 1].mean()

@@ -42,14 +42,14 @@ def main():
                                        tr.pview("dense_1/bias"), tr.y_buf, None, st, tr.seed, 0.5, tr.h, tr.dz, tr.dlog,
                                        tr.stats),
         "fc1_wgrad": lambda: o.fc1_wgrad(tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"),
-                                         tr.gview("dense_1/kernel"), tr.gview("dense_1/bias"),
-                                         tr.gview("conv_layer2/conv2d/bias"), tr.gview("conv_layer1/conv2d/kernel"),
-                                         tr.gview("conv_layer1/conv2d/bias")),
+                                         tr.gview("dense_1/kernel"), tr.gview("dense_1/bias")),
         "fc1_dgrad": lambda: o.fc1_dgrad(tr.dz, tr.pview("dense/kernel", sh), tr.a2, tr.g2),
         "conv2_bwd": lambda: o.conv2_bwd(tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf,
-                                         None, st, tr.idx1, tr.slab, tr.gview("conv_layer2/conv2d/bias"),
-                                         tr.gview("conv_layer1/conv2d/kernel"), tr.gview("conv_layer1/conv2d/bias")),
-        "conv2_wgrad_reduce": lambda: o.conv2_wgrad_reduce(tr.slab, B, tr.gview("conv_layer2/conv2d/kernel")),
+                                         None, st, tr.idx1, tr.slab, tr.cpart),
+        "conv2_wgrad_reduce": lambda: o.conv2_wgrad_reduce(tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"),
+                                                           tr.gview("conv_layer1/conv2d/kernel"),
+                                                           tr.gview("conv_layer1/conv2d/bias"),
+                                                           tr.gview("conv_layer2/conv2d/bias")),
         "adam": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, sh, st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
     }
     jobs = [(name, fn, None) for name, fn in ops.items()]

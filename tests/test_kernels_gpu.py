@@ -150,10 +150,7 @@ def test_fc1_bwd(ops, B):
     dlog = torch.randn(B, 10, device="cuda", generator=g) * 0.01
     gW3 = torch.empty(3136, 1024, device="cuda")
     gb3, gW4, gb4 = torch.empty(1024, device="cuda"), torch.empty(1024, 10, device="cuda"), torch.empty(10, device="cuda")
-    gb2, gW1, gb1 = (torch.full((64,), 3.0, device="cuda"), torch.full((800,), 3.0, device="cuda"),
-                     torch.full((32,), 3.0, device="cuda"))
-    ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3, gb3, gW4, gb4, gb2,
-                  gW1, gb1)
+    ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3, gb3, gW4, gb4)
     g2 = torch.empty(B, 3136, device="cuda", dtype=torch.bfloat16)
     ops.fc1_dgrad(dz.to(torch.bfloat16), w3.to(torch.bfloat16), a2.to(torch.bfloat16), g2)
     assert rel_err(g2, (dz @ w3.t()) * (a2 > 0)) < 5e-3
@@ -163,13 +160,12 @@ def test_fc1_bwd(ops, B):
     dzk = bf(torch.randn(K, 1024, device="cuda", generator=g) * 0.01)
     a2k = bf(F.relu(torch.randn(K, 3136, device="cuda", generator=g)))
     gW3k = torch.empty_like(gW3)
-    ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3k, gb3, gW4, gb4, gb2,
-                  gW1, gb1, 1, dzk.to(torch.bfloat16), a2k.to(torch.bfloat16))
+    ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3k, gb3, gW4, gb4, 1,
+                  dzk.to(torch.bfloat16), a2k.to(torch.bfloat16))
     assert rel_err(gW3k, a2k.t() @ dzk) < 1e-4
     assert rel_err(gb3, dz.sum(0)) < 1e-4
     assert rel_err(gW4, h.t() @ dlog) < 1e-4
     assert rel_err(gb4, dlog.sum(0)) < 1e-4
-    assert gb2.abs().sum() == 0 and gW1.abs().sum() == 0 and gb1.abs().sum() == 0
 
 
 @pytest.mark.parametrize("B", [7, 100])
@@ -192,10 +188,11 @@ def test_conv2_bwd_fused_conv1_wgrad(ops, B):
     G = int(ops.conv2_wgrad_groups(B))
     g1 = torch.empty_like(a1)
     slab = torch.empty(G, 51200, device="cuda")
-    gb2, gW1, gb1, gW2 = (torch.zeros(64, device="cuda"), torch.zeros(800, device="cuda"),
-                          torch.zeros(32, device="cuda"), torch.empty(51200, device="cuda"))
-    ops.conv2_bwd(g2, idx2, a1, w2.to(torch.bfloat16).reshape(-1), x, None, None, idx1, slab, gb2, gW1, gb1, g1)
-    ops.conv2_wgrad_reduce(slab, B, gW2)
+    gb2, gW1, gb1, gW2 = (torch.empty(64, device="cuda"), torch.empty(800, device="cuda"),
+                          torch.empty(32, device="cuda"), torch.empty(51200, device="cuda"))
+    cpart = torch.full((B, 896), float("nan"), device="cuda")  # every entry must be written
+    ops.conv2_bwd(g2, idx2, a1, w2.to(torch.bfloat16).reshape(-1), x, None, None, idx1, slab, cpart, g1)
+    ops.conv2_wgrad_reduce(slab, cpart, B, gW2, gW1, gb1, gb2)
     # Reference: autograd through conv2 (+relu+pool) on the same bf16 a1, and conv1 on fp32 x.
     a1r = a1.float().requires_grad_(True)
     w2r = w2.clone().requires_grad_(True)
@@ -435,6 +432,5 @@ def test_adam_pipeline_matches_serial(ops, monkeypatch):
     (p0, l0, f0, t0), (p1, l1, f1, t1) = out
     assert (f0, t0) == (f1, t1) == (6, 6)
     assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0))
-    # conv2_bwd's atomics (dW1, db1, db2) make runs differ in the last bits, which Adam's normalisation turns into
-    # O(lr) steps on near-zero-gradient weights: compare the updates, not the bits
-    assert rel_err(p1 - p_init, p0 - p_init) < 0.05
+    # no atomics anywhere in the step: the overlapped schedule is bitwise identical to the serial one
+    assert torch.equal(p1, p0)
