@@ -4,9 +4,6 @@
 // conv1 (1 -> 32 channels, K = 25) has too little reduction depth for MFMA: it is a direct VALU
 // convolution with the 25 weights of a channel in registers and the image tile (+halo) in LDS.
 //
-// conv_fwd fuses both per image (the training step's forward); conv1_fwd / conv2_fwd remain as
-// separate launches for inference and tests.
-//
 // conv2 (32 -> 64, K = 800) is an implicit GEMM on v_mfma_f32_16x16x32_bf16. The M dimension
 // (output pixels) is enumerated *pool-window-major* (m = 4*window + 2*dy + dx), so each 16-row
 // MFMA tile holds 4 complete 2x2 windows and a lane's 4 accumulator rows ARE one window of one
@@ -94,11 +91,35 @@ constexpr int C2_WROW = 32 + 8;          // weight image row stride (elements): 
 constexpr int C2_W = 800 * C2_WROW;
 constexpr int C2_LDS_BYTES = (C2_IMG + C2_W) * 2;
 
-// conv2 GEMM + fused bias/ReLU/2x2-pool epilogue for one image and one 32-channel half, with the
-// image ([18][18][32] bf16, zero halo) and the weight half ([800][C2_WROW]) already in LDS.
-__device__ __forceinline__ void conv2_gemm_pool(const u16* img, const u16* wim, const float* __restrict__ b2,
-                                                u16* __restrict__ a2, uint8_t* __restrict__ idx2, int half, int b,
-                                                int t) {
+__global__ void __launch_bounds__(256) conv2_fwd_kernel(
+    const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ b2, u16* __restrict__ a2,
+    uint8_t* __restrict__ idx2) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  u16* img = smem;            // [18][18][32]
+  u16* wim = smem + C2_IMG;   // [800][C2_WROW] (k = (kh*5+kw)*32 + ci, n = co - 32*half)
+  const int half = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  // Issue every load first (image: 6 x 16 B, weights: 13 x 16 B per thread), then write LDS.
+  const u16* src = a1 + (int64_t)b * 14 * 14 * 32;
+  uint4 iv[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int i = min(t + 256 * k, 18 * 18 * 4 - 1);
+    const int pix = i >> 2, ch = i & 3;
+    const int y = pix / 18 - 2, x = pix % 18 - 2;
+    const bool in = y >= 0 && y < 14 && x >= 0 && x < 14;
+    const uint4 v = *reinterpret_cast<const uint4*>(src + ((in ? y : 0) * 14 + (in ? x : 0)) * 32 + ch * 8);
+    iv[k] = mask_u4(v, in);
+  }
+  TileLoad<256, 13, 4> lw;
+  lw.load(w2bf + half * 32, 64, 800, 800, t);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int i = t + 256 * k;
+    if (i < 18 * 18 * 4) reinterpret_cast<uint4*>(img)[i] = iv[k];
+  }
+  lw.store(wim, C2_WROW, 800, t);
+  __syncthreads();
+
   const int lane = t & 63, wave = t >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   // This wave's M tiles: wave, wave+4, wave+8, (12 for wave 0). 13 tiles x 16 = 208 >= 196.
@@ -120,7 +141,6 @@ __device__ __forceinline__ void conv2_gemm_pool(const u16* img, const u16* wim, 
   // Every wave computes 4 tiles (tiles 13..15 are dummies on clamped rows, discarded below): no
   // runtime guard around an MFMA, which would make hipcc shuttle the accumulators.
   const int q = lr >> 2, p = lr & 3;
-#pragma unroll 5
   for (int kk = 0; kk < 25; ++kk) {  // (kh, kw): 32 input channels = one K step
     const int kh = kk / 5, kw = kk - kh * 5;
     const int aoff = (kh * 18 + kw) * 32;
@@ -155,141 +175,6 @@ __device__ __forceinline__ void conv2_gemm_pool(const u16* img, const u16* wim, 
       idx2[o] = (uint8_t)best;
     }
   }
-}
-
-__global__ void __launch_bounds__(256) conv2_fwd_kernel(
-    const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ b2, u16* __restrict__ a2,
-    uint8_t* __restrict__ idx2) {
-  extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  u16* img = smem;            // [18][18][32]
-  u16* wim = smem + C2_IMG;   // [800][C2_WROW] (k = (kh*5+kw)*32 + ci, n = co - 32*half)
-  const int half = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  // Issue every load first (image: 6 x 16 B, weights: 13 x 16 B per thread), then write LDS.
-  const u16* src = a1 + (int64_t)b * 14 * 14 * 32;
-  uint4 iv[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const int i = min(t + 256 * k, 18 * 18 * 4 - 1);
-    const int pix = i >> 2, ch = i & 3;
-    const int y = pix / 18 - 2, x = pix % 18 - 2;
-    const bool in = y >= 0 && y < 14 && x >= 0 && x < 14;
-    const uint4 v = *reinterpret_cast<const uint4*>(src + ((in ? y : 0) * 14 + (in ? x : 0)) * 32 + ch * 8);
-    iv[k] = mask_u4(v, in);
-  }
-  TileLoad<256, 13, 4> lw;
-  lw.load(w2bf + half * 32, 64, 800, 800, t);
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const int i = t + 256 * k;
-    if (i < 18 * 18 * 4) reinterpret_cast<uint4*>(img)[i] = iv[k];
-  }
-  lw.store(wim, C2_WROW, 800, t);
-  __syncthreads();
-
-  conv2_gemm_pool(img, wim, b2, a2, idx2, half, b, t);
-}
-
-// ------------------------------------------------------------------------------------------ //
-// conv_fwd: conv1 + conv2 of one image in one block (grid (2, B): blockIdx.x = conv2 channel half).
-// The conv1 output never round-trips through HBM for conv2: it is written as bf16 straight into
-// the LDS image conv2 reads (block half 0 also stores a1/idx1 for the backward pass). conv1 uses a
-// register sliding window: each thread owns a channel and a pooled row and moves a 6x6 input
-// window two columns per pooled pixel (12 new LDS reads instead of 36). Both halves compute conv1
-// (it is cheap VALU work); the conv2 weight half streams into LDS while conv1 runs.
-// ------------------------------------------------------------------------------------------ //
-constexpr int CF_XS = 36;                                   // fp32 padded-image row stride
-constexpr int CF_LDS = C2_LDS_BYTES + 32 * CF_XS * 4;        // + [32][36] fp32 input image
-
-__global__ void __launch_bounds__(256) conv_fwd_kernel(
-    const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
-    const float* __restrict__ w1, const float* __restrict__ b1, const u16* __restrict__ w2bf,
-    const float* __restrict__ b2, u16* __restrict__ a1, uint8_t* __restrict__ idx1, u16* __restrict__ a2,
-    uint8_t* __restrict__ idx2, int B) {
-  extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  u16* img = smem;                                          // [18][18][32] conv2 input, zero halo
-  u16* wim = smem + C2_IMG;                                 // [800][C2_WROW] conv2 weight half
-  float* xs = reinterpret_cast<float*>(wim + C2_W);         // [32][36]: xs[r][c] = x[r-2][c-2]
-  const int half = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  int row = b;
-  if (rows != nullptr) {
-    const int64_t step = state ? state[ST_FWD] : 0;
-    row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-  }
-  const int co = t & 31, g = t >> 5;
-  // ---- every load first: W2 half (13 x 16 B), the image (4 values), this channel's conv1 weights
-  TileLoad<256, 13, 4> lw;
-  lw.load(w2bf + half * 32, 64, 800, 800, t);
-  const float* xi = x + (int64_t)row * 784;
-  float xv[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = t + 256 * k;
-    const int gy = (i >> 5) - 2, gx = (i & 31) - 2;
-    const bool in = gy >= 0 && gy < 28 && gx >= 0 && gx < 28;
-    xv[k] = mask_f(xi[in ? gy * 28 + gx : 0], in);
-  }
-  float w[25];
-#pragma unroll
-  for (int k = 0; k < 25; ++k) w[k] = w1[k * 32 + co];
-  const float bias1 = b1[co];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) xs[((t + 256 * k) >> 5) * CF_XS + ((t + 256 * k) & 31)] = xv[k];
-  if (t < 32) xs[t * CF_XS + 32] = xs[t * CF_XS + 33] = xs[t * CF_XS + 34] = xs[t * CF_XS + 35] = 0.f;
-  // zero the conv2 image halo (128 pixels x 4 chunks)
-  for (int i = t; i < 324 * 4; i += 256) {
-    const int pix = i >> 2, y = pix / 18, xx = pix - y * 18;
-    if (y < 2 || y >= 16 || xx < 2 || xx >= 16) reinterpret_cast<uint4*>(img)[i] = make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  // ---- conv1: thread = (channel co, pooled rows g and g + 8); waves are uniform in row validity
-#pragma unroll 1
-  for (int rr = 0; rr < 2; ++rr) {
-    const int py = g + 8 * rr;
-    if (py >= 14) break;
-    float win[6][6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) win[r][c + 2] = xs[(2 * py + r) * CF_XS + c];
-#pragma unroll
-    for (int px = 0; px < 14; ++px) {
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {  // slide two columns: keep 4, load 2
-        win[r][0] = win[r][2];
-        win[r][1] = win[r][3];
-        win[r][2] = win[r][4];
-        win[r][3] = win[r][5];
-        win[r][4] = xs[(2 * py + r) * CF_XS + 2 * px + 4];
-        win[r][5] = xs[(2 * py + r) * CF_XS + 2 * px + 5];
-      }
-      float s4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < 5; ++kw) {
-          const float wk = w[kh * 5 + kw];
-          s4[0] = fmaf(win[kh][kw], wk, s4[0]);
-          s4[1] = fmaf(win[kh][kw + 1], wk, s4[1]);
-          s4[2] = fmaf(win[kh + 1][kw], wk, s4[2]);
-          s4[3] = fmaf(win[kh + 1][kw + 1], wk, s4[3]);
-        }
-      int best = 0;
-      float m = s4[0];
-#pragma unroll
-      for (int j = 1; j < 4; ++j)
-        if (s4[j] > m) { m = s4[j]; best = j; }
-      const u16 yb = f2bf(fmaxf(m + bias1, 0.f));
-      img[((py + 2) * 18 + px + 2) * 32 + co] = yb;
-      if (half == 0) {
-        const int64_t o = (((int64_t)b * 14 + py) * 14 + px) * 32 + co;
-        a1[o] = yb;
-        idx1[o] = (uint8_t)best;
-      }
-    }
-  }
-  lw.store(wim, C2_WROW, 800, t);
-  __syncthreads();
-  conv2_gemm_pool(img, wim, b2, a2, idx2, half, b, t);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -329,39 +214,6 @@ void conv2_fwd(const at::Tensor& a1, const at::Tensor& w2bf, const at::Tensor& b
   conv2_fwd_kernel<<<dim3(2, B), 256, C2_LDS_BYTES, stream>>>((const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
                                                               b2.data_ptr<float>(), (u16*)a2.data_ptr(),
                                                               idx2.data_ptr<uint8_t>());
-}
-
-void conv_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-              const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a1,
-              at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2) {
-  const int B = a1.size(0);
-  TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "conv_fwd: x");
-  TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && a1.is_contiguous(), "conv_fwd: a1");
-  TORCH_CHECK(idx1.dtype() == at::kByte && idx1.numel() == a1.numel(), "conv_fwd: idx1");
-  TORCH_CHECK(w1.numel() == 800 && b1.numel() == 32 && w1.dtype() == at::kFloat && b1.dtype() == at::kFloat,
-              "conv_fwd: conv1 weights");
-  TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200 && w2bf.is_contiguous(), "conv_fwd: w2 (bf16)");
-  TORCH_CHECK(b2.dtype() == at::kFloat && b2.numel() == 64, "conv_fwd: b2");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * 3136 && idx2.numel() == a2.numel(), "conv_fwd: out");
-  const int* rp = nullptr;
-  int n_pool = x.size(0);
-  if (rows.has_value() && rows->defined()) {
-    TORCH_CHECK(rows->dtype() == at::kInt && rows->numel() == n_pool, "conv_fwd: rows must be int32 [n_pool]");
-    rp = rows->data_ptr<int>();
-  } else {
-    TORCH_CHECK(n_pool >= B, "conv_fwd: x has fewer rows than the batch");
-  }
-  const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
-  static bool attr = [] {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CF_LDS);
-    return true;
-  }();
-  (void)attr;
-  auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv_fwd_kernel<<<dim3(2, B), 256, CF_LDS, stream>>>(
-      x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(), b1.data_ptr<float>(), (const u16*)w2bf.data_ptr(),
-      b2.data_ptr<float>(), (u16*)a1.data_ptr(), idx1.data_ptr<uint8_t>(), (u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(),
-      B);
 }
 
 }  // namespace mihvd

@@ -3,9 +3,8 @@
 This is the flagship path (bench.py ``--impl fused``). One step is nine HIP launches (+ the RCCL
 allreduce when ``size() > 1``), all hand-written CDNA4 kernels from ``csrc/kernels``:
 
-    conv_fwd    per image: conv1 (direct, sliding register window) + bias + ReLU + pool
-                [VALU] -> bf16 image in LDS -> conv2 implicit GEMM, pool-window-major M,
-                pool/ReLU in registers                                          [MFMA bf16]
+    conv1_fwd   direct conv + bias + ReLU + 2x2 max-pool (+argmax)             [VALU]
+    conv2_fwd   implicit GEMM, pool-window-major M, pool/ReLU in registers    [MFMA bf16]
     fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs                    [MFMA bf16]
     head        slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
     fc1_wgrad   dW3 -> fusion buffer | db3 | dW4/db4 | db4 (bucket "fc" complete) [MFMA bf16]
@@ -205,7 +204,10 @@ class FusedMNISTTrainer:
         o = self.ops
         st = self.state
         main = torch.cuda.current_stream(self.device)
-        self._conv_forward(x, rows, st)
+        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
+                    self.a1, self.idx1)
+        o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
+                    self.a2, self.idx2)
         if self._fc_update_pending:
             # the previous step's "fc" Adam update (side stream) overlapped the two convolutions above
             main.wait_stream(self._side)
@@ -266,7 +268,10 @@ class FusedMNISTTrainer:
         st = self.state
         main = torch.cuda.current_stream(self.device)
         side = self._side
-        self._conv_forward(x, rows, st)
+        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
+                    self.a1, self.idx1)
+        o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
+                    self.a2, self.idx2)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self._all_gather_rows(self.a2_all, self.a2)
@@ -291,11 +296,6 @@ class FusedMNISTTrainer:
         b1, b2 = self.betas
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
-
-    def _conv_forward(self, x, rows, st):
-        self.ops.conv_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
-                          self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
-                          self.a1, self.idx1, self.a2, self.idx2)
 
     def _conv_backward(self, x, rows, st):
         o = self.ops

@@ -73,29 +73,6 @@ def test_conv2_fwd(ops, B):
     assert (idx.long()[pos] == rd.reshape(B, 3136)[pos]).float().mean() > 0.99
 
 
-@pytest.mark.parametrize("B", [7, 100])
-def test_conv_fwd_fused_equals_separate(ops, B):
-    """conv_fwd (conv1 + conv2 per image, a1 kept in LDS) == conv1_fwd then conv2_fwd, bit for bit,
-    including the device-side row gather."""
-    g = torch.Generator(device="cuda").manual_seed(8)
-    X = torch.rand(3 * B, 784, device="cuda", generator=g)
-    rows = torch.randperm(3 * B, device="cuda", generator=g).to(torch.int32)
-    st = torch.tensor([1, 0, 0, 0], device="cuda", dtype=torch.int64)  # step 1 -> rows[B:2B]
-    w1 = torch.randn(800, device="cuda", generator=g) * 0.2
-    b1 = torch.randn(32, device="cuda", generator=g) * 0.05
-    w2 = (torch.randn(51200, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
-    b2 = torch.randn(64, device="cuda", generator=g) * 0.05
-    bf16 = dict(device="cuda", dtype=torch.bfloat16)
-    u8 = dict(device="cuda", dtype=torch.uint8)
-    out = [[torch.empty(B, 14, 14, 32, **bf16), torch.empty(B, 14, 14, 32, **u8), torch.empty(B, 3136, **bf16),
-            torch.empty(B, 3136, **u8)] for _ in range(2)]
-    ops.conv1_fwd(X, rows, st, w1, b1, out[0][0], out[0][1])
-    ops.conv2_fwd(out[0][0], w2, b2, out[0][2], out[0][3])
-    ops.conv_fwd(X, rows, st, w1, b1, w2, b2, *out[1])
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("B", [7, 100, 128])
 def test_fc1_fwd(ops, B):
     g = torch.Generator(device="cuda").manual_seed(3)
