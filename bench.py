@@ -103,9 +103,13 @@ def make_fused_step(args, hvd, device):
     tr.set_device_dataset(X, Y)
     k = args.graph_steps or 10
     tr.build_graph(steps_per_replay=k)
+    # remainders of --steps / --warmup that are not multiples of k replay a shorter graph, so the
+    # timed region is exactly K steps
+    for r in {args.steps % k, args.warmup % k} - {0}:
+        tr.build_graph(steps_per_replay=r, warmup=0, primary=False)
 
-    def step():
-        tr.run_graph()
+    def step(n=None):
+        tr.run_graph(n)
 
     return step, "bf16", tr
 
@@ -123,18 +127,24 @@ def main():
     else:
         step, dtype, _ = make_torch_step(args, hvd, device, ddp=args.impl == "ddp")
         per_call = 1
-    calls_warm = max(1, -(-args.warmup // per_call))
-    calls = max(1, -(-args.steps // per_call))
-    steps_timed = calls * per_call
-    for _ in range(calls_warm):
-        step()
+
+    def run(n):
+        """Exactly n steps: whole graphs of per_call steps, then one replay of the remainder."""
+        for _ in range(n // per_call):
+            step()
+        if n % per_call:
+            step(n % per_call)
+
+    if args.steps < 1:
+        raise SystemExit("--steps must be >= 1")
+    steps_timed = args.steps
+    run(args.warmup)
     sync = (lambda: torch.cuda.synchronize()) if device.type == "cuda" else (lambda: None)
     sync()
     hvd.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(calls):
-        step()
+    run(steps_timed)
     sync()
     hvd.barrier()
     sync()
@@ -161,7 +171,7 @@ def main():
     if hvd.rank() == 0:
         rec = {
             "metric": METRIC, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": steps_timed,
-            "warmup": calls_warm * per_call, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": dtype, "data": "synthetic 28x28 uint8-derived images, device-resident; random-init weights",
             "config": {"model": "tensorflow_mnist 2-conv CNN (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.5-fc10, 3,274,634 params)",
                        "global_batch": args.batch_size * n, "per_gpu_batch": args.batch_size, "seq_len": None,

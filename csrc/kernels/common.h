@@ -122,6 +122,54 @@ __device__ __forceinline__ uint2 pack4bf(float a, float b, float c, float d) {
   return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
 }
 
+// Adam update of four consecutive elements (K12 of SURVEY.md §2.5), shared by the flat-buffer
+// optimizer (optim.hip) and the dW3 tiles of fc1_wgrad that update W3 straight from the MFMA
+// accumulators; both run exactly this code, so the two paths agree bit for bit.
+//   rule 0 (TF1, horovod/tensorflow_mnist.py:130): lr_t = lr sqrt(1-b2^t)/(1-b1^t), eps outside
+//   rule 1 (torch.optim.Adam): eps added to sqrt(v_hat)
+struct AdamCoef {
+  float lr_t, eps_t, inv_sqrt_bc2, b1, b2, gscale;
+};
+__device__ __forceinline__ AdamCoef adam_coef(float t, float lr, float b1, float b2, float eps, float gscale, int rule) {
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  AdamCoef c;
+  c.lr_t = rule == 0 ? lr * sqrtf(bc2) / bc1 : lr / bc1;
+  c.eps_t = rule == 0 ? eps : eps * sqrtf(bc2);
+  c.inv_sqrt_bc2 = rule == 0 ? 1.f : 1.f / sqrtf(bc2);
+  c.b1 = b1;
+  c.b2 = b2;
+  c.gscale = gscale;
+  return c;
+}
+__device__ __forceinline__ uint2 adam4(float4& pp, float4& mm, float4& vv, const float4 gg, const AdamCoef& c) {
+  float* pa = &pp.x;
+  float* ma = &mm.x;
+  float* va = &vv.x;
+  const float* ga = &gg.x;
+  u16 sh[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gk = ga[k] * c.gscale;
+    ma[k] = fmaf(c.b1, ma[k], (1.f - c.b1) * gk);
+    va[k] = fmaf(c.b2, va[k], (1.f - c.b2) * gk * gk);
+    pa[k] -= c.lr_t * ma[k] / (sqrtf(va[k]) * c.inv_sqrt_bc2 + c.eps_t);
+    sh[k] = f2bf(pa[k]);
+  }
+  return make_uint2((uint32_t)sh[0] | ((uint32_t)sh[1] << 16), (uint32_t)sh[2] | ((uint32_t)sh[3] << 16));
+}
+
+// Arguments of an Adam update fused into a gradient-producing kernel (p, m, v, shadow are the
+// slices of the flat buffers that the kernel's gradient covers).
+struct AdamArgs {
+  float* p;
+  float* m;
+  float* v;
+  u16* shadow;
+  const int64_t* state;
+  float lr, b1, b2, eps, gscale;
+  int rule;
+};
+
 // Profiling aid (scripts/kbench.py --roles): MIHVD_ROLE_ONLY=<r> makes a launch that packs several
 // block roles run only the blocks of role r, so each role can be timed on its own. Unset (the
 // normal case) every role runs.

@@ -257,10 +257,15 @@ constexpr int FB_TOTAL = FB_WGRAD + FB_DB3 + FB_DW4 + FB_MISC;
 constexpr int FB_TSTR = 64 + 8;                                  // 72 elements
 constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
 
+// ADAM: the dW3 tiles apply the optimizer to W3 in their epilogue (p, m, v, bf16 shadow of the
+// dense/kernel segment) straight from the accumulators, so dW3 never round-trips through HBM; the
+// gradient is stored too only when write_grad is set (tests). Valid whenever the tile's dW3 is
+// already the full data-parallel sum: world size 1, or the all-gathered factors (Kw = size * B).
+template <bool ADAM>
 __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
     const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
-    float* __restrict__ gW4, float* __restrict__ gb4, int B, int role_base, int n_small) {
+    float* __restrict__ gW4, float* __restrict__ gb4, int B, int role_base, int n_small, AdamArgs ad, int write_grad) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
@@ -287,12 +292,29 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
       lz.load(dzw + n0, FC1_N, (rows + 31) & ~31, rows, t);
       la.load(a2w + j0, FC1_K, (rows + 31) & ~31, rows, t);
     }
+    float4 pp[2][2], mm[2][2], vv[2][2];
     for (int kc = 0; kc < Kw; kc += MAXB) {
       const int rows = min(MAXB, Kw - kc), Kpad = (rows + 31) & ~31;
       if (kc > 0) __syncthreads();  // the previous chunk's fragments have been read
       lz.store(Zim, FB_TSTR, Kpad, t);
       la.store(Aim, FB_TSTR, Kpad, t);
       __syncthreads();
+      if constexpr (ADAM) {
+        // Optimizer operands of this lane's four float4 outputs: issued once the first operand
+        // chunk is in LDS (vmcnt retires in order, so issuing them earlier would make the operand
+        // wait include them) and in flight during the MFMA loop.
+        if (kc == 0) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+              const int64_t o = (int64_t)(j0 + wn + jj * 16 + lr) * FC1_N + n0 + wm + i * 16 + 4 * lg;
+              pp[i][jj] = *reinterpret_cast<const float4*>(ad.p + o);
+              mm[i][jj] = *reinterpret_cast<const float4*>(ad.m + o);
+              vv[i][jj] = *reinterpret_cast<const float4*>(ad.v + o);
+            }
+        }
+      }
       if (kc + MAXB < Kw) {
         const int nrows = min(MAXB, Kw - kc - MAXB);
         lz.load(dzw + (int64_t)(kc + MAXB) * FC1_N + n0, FC1_N, (nrows + 31) & ~31, nrows, t);
@@ -312,6 +334,23 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mfma16(af[i], bfv[jj], acc[i][jj]);
       }
+    }
+    if constexpr (ADAM) {
+      const AdamCoef c = adam_coef((float)ad.state[ST_OPT], ad.lr, ad.b1, ad.b2, ad.eps, ad.gscale, ad.rule);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int64_t o = (int64_t)(j0 + wn + jj * 16 + lr) * FC1_N + n0 + wm + i * 16 + 4 * lg;
+          const float4 g = make_float4(acc[i][jj][0], acc[i][jj][1], acc[i][jj][2], acc[i][jj][3]);
+          if (write_grad) *reinterpret_cast<float4*>(gW3 + o) = g;
+          const uint2 sh = adam4(pp[i][jj], mm[i][jj], vv[i][jj], g, c);
+          *reinterpret_cast<float4*>(ad.p + o) = pp[i][jj];
+          *reinterpret_cast<float4*>(ad.m + o) = mm[i][jj];
+          *reinterpret_cast<float4*>(ad.v + o) = vv[i][jj];
+          *reinterpret_cast<uint2*>(ad.shadow + o) = sh;
+        }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -462,8 +501,10 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
 // roles: bit 0 = the dW3 tiles, bit 1 = the small reductions (db3, dW4, db4). dW3 multiplies dz_w3^T a2_w3 over their rows: the local dz/a2 by default, or the
 // all-gathered factors of every rank (data-parallel "factor gather": dW3 = sum over all samples,
 // exactly what the allreduce of per-rank dW3 would produce, for a fraction of the bytes).
-void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
-               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3) {
+static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
+                             at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
+                             const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3,
+                             const AdamArgs* ad, bool write_grad) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_wgrad: batch");
   TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
@@ -493,10 +534,42 @@ void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, 
   const int grid = n_small + ((roles & 1) ? FB_WGRAD : 0);
   if (grid == 0) return;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  fc1_wgrad_kernel<<<grid, 256, FB_LDS_WG, stream>>>(
-      (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(), dzw, a2w,
-      Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(),
-      B, 0, n_small);
+  const u16 *pdz = (const u16*)dz.data_ptr(), *pa2 = (const u16*)a2.data_ptr(), *ph = (const u16*)h.data_ptr();
+  if (ad != nullptr) {
+    fc1_wgrad_kernel<true><<<grid, 256, FB_LDS_WG, stream>>>(
+        pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, 0, n_small, *ad, write_grad ? 1 : 0);
+  } else {
+    fc1_wgrad_kernel<false><<<grid, 256, FB_LDS_WG, stream>>>(
+        pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, 0, n_small, AdamArgs{}, 1);
+  }
+}
+
+void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
+               at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
+               const c10::optional<at::Tensor>& a2_w3) {
+  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, nullptr, true);
+}
+
+// fc1_wgrad with the Adam update of dense/kernel fused into the dW3 tiles (see the kernel). p3, m3,
+// v3 (fp32) and shadow3 (bf16) are the dense/kernel segments of the flat buffers; state is the
+// device step state (the optimizer step t is read from it; this op does not advance it).
+void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
+                    at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
+                    const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3, at::Tensor& p3,
+                    at::Tensor& m3, at::Tensor& v3, at::Tensor& shadow3, const at::Tensor& state, double lr, double b1,
+                    double b2, double eps, double grad_scale, int64_t rule, bool write_grad) {
+  const int64_t n = (int64_t)FC1_K * FC1_N;
+  for (const at::Tensor* t : {&p3, &m3, &v3})
+    TORCH_CHECK(t->dtype() == at::kFloat && t->numel() == n && t->is_contiguous(), "fc1_wgrad_adam: p3/m3/v3 fp32 [3136*1024]");
+  TORCH_CHECK(shadow3.dtype() == at::kBFloat16 && shadow3.numel() == n && shadow3.is_contiguous(), "fc1_wgrad_adam: shadow3");
+  TORCH_CHECK(state.dtype() == at::kLong && state.numel() >= ST_WORDS, "fc1_wgrad_adam: state");
+  for (const at::Tensor* t : {&p3, &m3, &v3, &shadow3})
+    TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "fc1_wgrad_adam: 16-byte aligned segments required");
+  AdamArgs ad{p3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(), (u16*)shadow3.data_ptr(),
+              state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale, (int)rule};
+  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, &ad, write_grad);
 }
 
 // dgrad: g2 = (a2 > 0) * dz.W3^T in bf16, the gradient conv2_bwd routes through the pool argmax.

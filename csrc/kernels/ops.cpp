@@ -15,6 +15,11 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
                const c10::optional<at::Tensor>& a2_w3);
+void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
+                    at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
+                    const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3, at::Tensor& p3,
+                    at::Tensor& m3, at::Tensor& v3, at::Tensor& shadow3, const at::Tensor& state, double lr, double b1,
+                    double b2, double eps, double grad_scale, int64_t rule, bool write_grad);
 void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& g2);
 int64_t conv2_wgrad_groups(int64_t B);
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
@@ -57,6 +62,13 @@ void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Ten
                   Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3) {
   mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3);
 }
+void fc1_wgrad_adam_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, Tensor gW3, Tensor gb3,
+                       Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3, Tensor p3, Tensor m3,
+                       Tensor v3, Tensor shadow3, const Tensor& state, double lr, double b1, double b2, double eps,
+                       double grad_scale, int64_t rule, bool write_grad) {
+  mihvd::fc1_wgrad_adam(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, p3, m3, v3, shadow3, state, lr, b1, b2,
+                        eps, grad_scale, rule, write_grad);
+}
 void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, const Tensor& a2, Tensor g2) { mihvd::fc1_dgrad(dz, w3, a2, g2); }
 void conv2_bwd_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, const Tensor& x,
                   const OptT& rows, const OptT& state, const Tensor& idx1, Tensor slab, Tensor cpart, const OptT& g1) {
@@ -95,6 +107,10 @@ TORCH_LIBRARY(mihvd, m) {
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
   m.def("fc1_wgrad(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
         "Tensor(d!) gb4, int roles=3, Tensor? dz_w3=None, Tensor? a2_w3=None) -> ()");
+  m.def("fc1_wgrad_adam(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
+        "Tensor(d!) gb4, int roles, Tensor? dz_w3, Tensor? a2_w3, Tensor(e!) p3, Tensor(f!) m3, Tensor(g!) v3, "
+        "Tensor(h!) shadow3, Tensor state, float lr, float b1, float b2, float eps, float grad_scale, int rule, "
+        "bool write_grad=False) -> ()");
   m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor a2, Tensor(a!) g2) -> ()");
   m.def("conv2_wgrad_groups(int B) -> int", &mihvd::conv2_wgrad_groups);
   m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, Tensor? state, Tensor idx1, "
@@ -119,6 +135,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("fc1_fwd", &fc1_fwd_op);
   m.impl("head_fwd_bwd", &head_op);
   m.impl("fc1_wgrad", &fc1_wgrad_op);
+  m.impl("fc1_wgrad_adam", &fc1_wgrad_adam_op);
   m.impl("fc1_dgrad", &fc1_dgrad_op);
   m.impl("conv2_bwd", &conv2_bwd_op);
   m.impl("conv2_wgrad_reduce", &conv2_wgrad_reduce_op);

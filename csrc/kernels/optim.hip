@@ -25,36 +25,17 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const 
     if (ls[1] != 0.f) return;
     gscale /= ls[0];
   }
-  const float t = (float)(state ? state[ST_OPT] : host_t);
-  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
-  // rule 0: TF1 (eps outside the bias-corrected sqrt); rule 1: torch.optim.Adam
-  const float lr_t = rule == 0 ? lr * sqrtf(bc2) / bc1 : lr / bc1;
-  const float eps_t = rule == 0 ? eps : eps * sqrtf(bc2);
-  const float inv_sqrt_bc2 = rule == 0 ? 1.f : 1.f / sqrtf(bc2);
+  const AdamCoef c = adam_coef((float)(state ? state[ST_OPT] : host_t), lr, b1, b2, eps, gscale, rule);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
     const float4 gg = reinterpret_cast<const float4*>(g)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* pa = &pp.x;
-    const float* ga = &gg.x;
-    float* ma = &mm.x;
-    float* va = &vv.x;
-    u16 sh[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gk = ga[k] * gscale;
-      ma[k] = fmaf(b1, ma[k], (1.f - b1) * gk);
-      va[k] = fmaf(b2, va[k], (1.f - b2) * gk * gk);
-      pa[k] -= lr_t * ma[k] / (sqrtf(va[k]) * inv_sqrt_bc2 + eps_t);
-      sh[k] = f2bf(pa[k]);
-    }
+    const uint2 sh = adam4(pp, mm, vv, gg, c);
     reinterpret_cast<float4*>(p)[i] = pp;
     reinterpret_cast<float4*>(m)[i] = mm;
     reinterpret_cast<float4*>(v)[i] = vv;
-    if (shadow)
-      reinterpret_cast<uint2*>(shadow)[i] = make_uint2((uint32_t)sh[0] | ((uint32_t)sh[1] << 16),
-                                                       (uint32_t)sh[2] | ((uint32_t)sh[3] << 16));
+    if (shadow) reinterpret_cast<uint2*>(shadow)[i] = sh;
   }
 }
 

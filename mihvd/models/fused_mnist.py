@@ -139,6 +139,7 @@ class FusedMNISTTrainer:
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
         self.graph = None
+        self._graphs = {}
         self.steps_per_replay = 1
         # Overlap the "fc" bucket's allreduce with the conv backward on a side stream (N > 1). A
         # stream fork/join costs a few us inside a HIP graph, so it is only used with collectives.
@@ -147,6 +148,16 @@ class FusedMNISTTrainer:
         # last reader of W3 (fc1_dgrad) and overlaps the conv backward and the next step's convs.
         self.pipeline = os.environ.get("MIHVD_ADAM_PIPELINE", "0") == "1" and not self.gather
         self.adam_blocks = int(os.environ.get("MIHVD_ADAM_BLOCKS", "0"))
+        # MIHVD_FUSE_W3_ADAM=1: the dW3 tiles of fc1_wgrad apply Adam to dense/kernel (98 %
+        # of the parameters) from their accumulators, so dW3 never goes through HBM and the flat
+        # optimizer only covers the other 65 K parameters. Needs dW3 to be complete on this rank:
+        # size 1, or the factor-gather data plane (dW3 over every rank's samples).
+        # Measured on MI355X (B=100): fused 21.4 us vs fc1_wgrad 7.1 + flat Adam 16.2 us; the fused
+        # epilogue streams p/m/v at ~5.9 TB/s in 256-B row pieces but does not hide the dW3 chain,
+        # so the step is 1-2 us slower and the option is off by default.
+        self.fuse_w3 = (os.environ.get("MIHVD_FUSE_W3_ADAM", "0") == "1" and not self.pipeline
+                        and (not self.collectives or self.gather))
+        self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when fused
         self._fc_update_pending = False
         self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline) else None
         if compression == "bf16" and self.collectives:
@@ -215,6 +226,15 @@ class FusedMNISTTrainer:
         o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        if self.fuse_w3:
+            # W3 is updated in place by the dW3 tiles: its last reader (fc1_dgrad) goes first
+            o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
+            self._fc1_wgrad_w3_adam(3, None, None)
+            self._conv_backward(x, rows, st)
+            b1, b2 = self.betas
+            o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START],
+                        self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+            return
         o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
                     self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
         fc_bucket = self.grads[FC_START:]
@@ -291,11 +311,26 @@ class FusedMNISTTrainer:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self._allreduce(self.grads[:W3_START], 0, W3_START)
+        b1, b2 = self.betas
+        if self.fuse_w3:
+            # dW3 summed over every rank's samples, Adam applied to W3 in the same tiles
+            self._fc1_wgrad_w3_adam(1, self.dz_all, self.a2_all)
+            main.wait_stream(side)
+            o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START],
+                        self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+            return
         o.fc1_wgrad(*small, 1, self.dz_all, self.a2_all)  # dW3 summed over every rank's samples
         main.wait_stream(side)
-        b1, b2 = self.betas
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
+
+    def _fc1_wgrad_w3_adam(self, roles, dz_all, a2_all):
+        b1, b2 = self.betas
+        w3 = slice(W3_START, FLAT_NUMEL)
+        self.ops.fc1_wgrad_adam(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
+                                self.gview("dense_1/kernel"), self.gview("dense_1/bias"), roles, dz_all, a2_all,
+                                self.params[w3], self.m[w3], self.v[w3], self.shadow[w3], self.state, self.lr, b1, b2,
+                                self.eps, 1.0 / self.world, self.rule, self.keep_w3_grad)
 
     def _conv_backward(self, x, rows, st):
         o = self.ops
@@ -371,19 +406,23 @@ class FusedMNISTTrainer:
             self._reshuffle()
 
     # ----------------------------------------------------------------------------- graphs
-    def build_graph(self, steps_per_replay: int = 10, warmup: int = 2):
+    def build_graph(self, steps_per_replay: int = 10, warmup: int = 2, primary: bool = True):
         """Capture ``steps_per_replay`` whole training steps (resident data) into one HIP graph.
 
         Warm-up steps run eagerly first (they also initialise RCCL communicators). If capture is not
-        possible (e.g. Adasum's data-dependent exchanges), training stays eager."""
+        possible (e.g. Adasum's data-dependent exchanges), training stays eager. ``primary=False``
+        keeps an additional graph of that length (``run_graph(steps)``) next to the main one, e.g.
+        for the remainder of a step count that is not a multiple of the main graph's length."""
         if self.X is None:
             raise RuntimeError("call set_device_dataset() before build_graph()")
         for _ in range(warmup):
             self.device_step()
         torch.cuda.synchronize(self.device)
-        self.steps_per_replay = steps_per_replay
+        if primary:
+            self.steps_per_replay = steps_per_replay
         if self.op is not None and int(self.op) == 2:  # Adasum: eager
-            self.graph = None
+            if primary:
+                self.graph = None
             return False
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.device)
@@ -398,26 +437,32 @@ class FusedMNISTTrainer:
             import warnings
 
             warnings.warn(f"HIP graph capture failed ({e!r}); falling back to eager steps")
-            self.graph = None
+            if primary:
+                self.graph = None
             self._fc_update_pending = False
             torch.cuda.synchronize(self.device)
             return False
         torch.cuda.current_stream(self.device).wait_stream(s)
         # Capture does not execute: the device step counter is untouched, so replays continue
         # from the current global_step.
-        self.graph = g
+        self._graphs[steps_per_replay] = g
+        if primary:
+            self.graph = g
         return True
 
-    def run_graph(self):
-        """Advance ``steps_per_replay`` steps (graph replay, or eager steps if capture failed)."""
-        if self.graph is None:
-            for _ in range(self.steps_per_replay):
+    def run_graph(self, steps: int | None = None):
+        """Advance ``steps_per_replay`` steps (or ``steps``, for which a graph was built with
+        ``primary=False``) by one graph replay, or eagerly if capture failed."""
+        k = self.steps_per_replay if steps is None else int(steps)
+        g = self.graph if steps is None else self._graphs.get(k)
+        if g is None:
+            for _ in range(k):
                 self.device_step()
             return
-        self._maybe_reshuffle(self.steps_per_replay)
-        with trace_range(f"mihvd.graph_replay[{self.steps_per_replay} steps]"):
-            self.graph.replay()
-        self.global_step += self.steps_per_replay
+        self._maybe_reshuffle(k)
+        with trace_range(f"mihvd.graph_replay[{k} steps]"):
+            g.replay()
+        self.global_step += k
 
     def last_loss(self) -> float:
         return float(self.stats[:, 0].mean())

@@ -290,6 +290,7 @@ def test_fused_step_matches_emulated_reference(ops, B):
     from mihvd.models.mnist import MNISTConvNet, TF_PARAM_ORDER
 
     tr = FusedMNISTTrainer(batch_size=B, lr=0.0, dropout=0.0, seed=3, device="cuda")
+    tr.keep_w3_grad = True  # dW3 is consumed by the fused W3 Adam; also store it for the comparison
     g = torch.Generator(device="cuda").manual_seed(8)
     x = torch.rand(B, 784, device="cuda", generator=g)
     y = torch.randint(0, 10, (B,), device="cuda", generator=g)
@@ -342,6 +343,7 @@ def test_fused_loss_autograd_matches_trainer(ops):
     loss, acc = fused_mnist_loss(model, x, y, training=False, return_accuracy=True)
     loss.backward()
     tr = FusedMNISTTrainer(batch_size=B, lr=0.0, dropout=0.0, seed=3, device="cuda")
+    tr.keep_w3_grad = True
     out = tr.train_step(x, y)
     torch.cuda.synchronize()
     assert abs(loss.item() - out["loss"].item()) < 1e-5
@@ -434,3 +436,31 @@ def test_adam_pipeline_matches_serial(ops, monkeypatch):
     assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0))
     # no atomics anywhere in the step: the overlapped schedule is bitwise identical to the serial one
     assert torch.equal(p1, p0)
+
+
+def test_fused_w3_adam_matches_separate_optimizer(ops, monkeypatch):
+    """fc1_wgrad_adam (Adam on dense/kernel applied from the dW3 accumulators) against the unfused
+    step (dW3 stored, then the flat Adam kernel): both run the same adam4() on the same fp32
+    gradient values, so parameters, Adam slots and the bf16 shadow agree bit for bit; the stored
+    dW3 (write_grad) equals the unfused gradient."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    g = torch.Generator(device="cuda").manual_seed(23)
+    X = torch.rand(600, 784, device="cuda", generator=g)
+    Y = torch.randint(0, 10, (600,), device="cuda", generator=g)
+    out = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("MIHVD_FUSE_W3_ADAM", fuse)
+        tr = FusedMNISTTrainer(batch_size=100, seed=4, device="cuda")
+        assert tr.fuse_w3 == (fuse == "1")
+        tr.keep_w3_grad = True
+        tr.set_device_dataset(X, Y, shuffle=False)
+        tr.build_graph(steps_per_replay=3, warmup=2)
+        tr.run_graph()
+        torch.cuda.synchronize()
+        out.append((tr.params.clone(), tr.m.clone(), tr.v.clone(), tr.shadow.clone(), tr.grads.clone(),
+                    int(tr.state[0]), int(tr.state[1])))
+    a, b = out
+    assert a[5:] == b[5:] == (5, 5)
+    for x0, x1, name in zip(a[:5], b[:5], ("params", "m", "v", "shadow", "grads")):
+        assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())

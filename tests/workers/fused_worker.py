@@ -54,8 +54,10 @@ def sc_dp_gloo(outdir):
     X, Y = data(600)
     tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda")
     assert tr.gather == (os.environ.get("MIHVD_FC_GATHER", "1") != "0")
+    tr.keep_w3_grad = True  # gradients are compared below
     tr.broadcast(0)
     ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", world_size=1)
+    ref.keep_w3_grad = True
     p0 = ref.params.clone()
     grel = None
     for step in range(3):
