@@ -2,13 +2,15 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "control.h"
 #include "runtime.h"
 
 namespace py = pybind11;
 using namespace mihvd;
 
 PYBIND11_MODULE(_mihvd_runtime, m) {
-  m.doc() = "mihvd native host runtime: bucket planner, controller, timeline, stall inspector";
+  m.doc() = "mihvd native host runtime: bucket planner, controller, timeline, stall inspector, "
+            "TCP key-value store, collective negotiation engine";
 
   py::class_<TensorSpec>(m, "TensorSpec")
       .def(py::init<>())
@@ -105,4 +107,85 @@ PYBIND11_MODULE(_mihvd_runtime, m) {
       .def("percentile", &StepStats::percentile)
       .def("reset", &StepStats::reset)
       .def_property_readonly("count", &StepStats::count);
+
+  // ---- control plane: key-value store + negotiation engine (control.h) ----
+  using gil_release = py::call_guard<py::gil_scoped_release>;
+  py::class_<StoreServer>(m, "StoreServer")
+      .def(py::init<const std::string&, int>(), py::arg("host") = "0.0.0.0", py::arg("port") = 0)
+      .def_property_readonly("port", &StoreServer::port)
+      .def_property_readonly("num_connections", &StoreServer::num_connections)
+      .def("num_keys", &StoreServer::num_keys)
+      .def("stop", &StoreServer::stop, gil_release());
+
+  py::class_<StoreClient>(m, "StoreClient")
+      .def(py::init<const std::string&, int, double>(), py::arg("host"), py::arg("port"),
+           py::arg("connect_timeout_s") = 60.0, gil_release())
+      .def("set", [](StoreClient& c, const std::string& k, const std::string& v) {
+             py::gil_scoped_release nogil;
+             c.set(k, v);
+           })
+      .def("get", [](StoreClient& c, const std::string& k, double timeout_s) {
+             std::string v;
+             {
+               py::gil_scoped_release nogil;
+               v = c.get(k, timeout_s);
+             }
+             return py::bytes(v);
+           }, py::arg("key"), py::arg("timeout_s") = -1.0)
+      .def("try_get", [](StoreClient& c, const std::string& k, double timeout_s) -> py::object {
+             std::string v;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = c.try_get(k, timeout_s, &v);
+             }
+             if (!ok) return py::none();
+             return py::bytes(v);
+           }, py::arg("key"), py::arg("timeout_s") = 0.0)
+      .def("add", &StoreClient::add, gil_release())
+      .def("check", &StoreClient::check, gil_release())
+      .def("wait", &StoreClient::wait, py::arg("keys"), py::arg("timeout_s") = -1.0, gil_release())
+      .def("compare_set", [](StoreClient& c, const std::string& k, const std::string& e, const std::string& d) {
+             std::string v;
+             {
+               py::gil_scoped_release nogil;
+               v = c.compare_set(k, e, d);
+             }
+             return py::bytes(v);
+           })
+      .def("delete", &StoreClient::del, gil_release())
+      .def("append", [](StoreClient& c, const std::string& k, const std::string& v) {
+             py::gil_scoped_release nogil;
+             c.append(k, v);
+           })
+      .def("num_keys", &StoreClient::num_keys, gil_release())
+      .def("close", &StoreClient::close, gil_release())
+      .def_property_readonly("host", &StoreClient::host)
+      .def_property_readonly("port", &StoreClient::port);
+
+  py::class_<Response>(m, "NegotiationResponse")
+      .def_readonly("name", &Response::name)
+      .def_readonly("generation", &Response::generation)
+      .def_readonly("error", &Response::error)
+      .def_readonly("batch", &Response::batch);
+
+  py::class_<StallEntry>(m, "StallEntry")
+      .def_readonly("name", &StallEntry::name)
+      .def_readonly("generation", &StallEntry::generation)
+      .def_readonly("age_s", &StallEntry::age_s)
+      .def_readonly("ready_ranks", &StallEntry::ready_ranks)
+      .def_readonly("missing_ranks", &StallEntry::missing_ranks);
+
+  py::class_<Negotiator>(m, "Negotiator")
+      .def(py::init<const std::string&, int, int, int, const std::string&, double, double, double>(),
+           py::arg("host"), py::arg("port"), py::arg("rank"), py::arg("size"), py::arg("prefix") = "mihvd/neg",
+           py::arg("cycle_s") = 0.005, py::arg("warn_s") = 60.0, py::arg("shutdown_s") = 0.0, gil_release())
+      .def("submit", &Negotiator::submit, gil_release())
+      .def("poll", &Negotiator::poll, gil_release())
+      .def("wait", &Negotiator::wait, py::arg("timeout_s") = -1.0, gil_release())
+      .def("stalled", &Negotiator::stalled, py::arg("older_than_s") = 0.0, gil_release())
+      .def("stop", &Negotiator::stop, gil_release())
+      .def_property_readonly("submitted", &Negotiator::submitted)
+      .def_property_readonly("responses", &Negotiator::responses)
+      .def_property_readonly("warnings", &Negotiator::warnings);
 }

@@ -60,6 +60,9 @@ class _Context:
         self.timeline = None
         self.stall = None
         self.fault_plan = None
+        self.store = None          # NativeStore (C++ TCP store) when launched by mihvdrun
+        self.store_server = None   # StoreServer this process hosts (negotiation without mihvdrun)
+        self.engine = None         # negotiated-collective Engine (MIHVD_NEGOTIATE=1)
         self.lock = threading.RLock()
 
 
@@ -118,11 +121,22 @@ def init(comm=None, process_sets=None, config: Config | None = None):
                                     **({"device_id": device} if backend == "nccl" else {}))
             _ctx.owns_pg = True
         else:
-            port = topo.master_port or 29500
-            url = f"tcp://{topo.master_addr}:{port}"
             kwargs = {"device_id": device} if backend == "nccl" else {}
-            dist.init_process_group(backend, init_method=url, rank=topo.rank, world_size=topo.size,
-                                    timeout=timeout, **kwargs)
+            native = None
+            if cfg.store != "torch":
+                from .runner.store import NativeStore
+
+                native = NativeStore.from_env(timeout)
+            if native is not None:
+                # mihvdrun's rendezvous server (C++): RCCL's unique-id exchange runs over it
+                _ctx.store = native
+                dist.init_process_group(backend, store=dist.PrefixStore("mihvd/pg", native), rank=topo.rank,
+                                        world_size=topo.size, timeout=timeout, **kwargs)
+            else:
+                port = topo.master_port or 29500
+                url = f"tcp://{topo.master_addr}:{port}"
+                dist.init_process_group(backend, init_method=url, rank=topo.rank, world_size=topo.size,
+                                        timeout=timeout, **kwargs)
             _ctx.owns_pg = True
         _ctx.topology = topo
         _ctx.config = cfg
@@ -131,6 +145,8 @@ def init(comm=None, process_sets=None, config: Config | None = None):
         _ctx.world_group = dist.group.WORLD
         _build_subgroups(topo)
         _start_observability(cfg, topo)
+        if cfg.negotiate and topo.size > 1:
+            _start_engine(cfg, topo, backend, device)
         _ctx.initialized = True
         atexit.register(shutdown)
         if topo.rank == 0:
@@ -188,6 +204,34 @@ def _start_observability(cfg: Config, topo: _env.Topology):
         _ctx.fault_plan = rt.FaultPlan(cfg.fault)
 
 
+def _start_engine(cfg: Config, topo: _env.Topology, backend: str, device: torch.device):
+    """Negotiated collectives (``mihvd/parallel/engine.py``): a native Negotiator per rank whose
+    coordinator runs on rank 0, over mihvdrun's store or a store server rank 0 starts here."""
+    import uuid
+
+    from ._native import runtime
+    from .parallel.engine import Engine
+    from .runner.store import parse_addr, start_server
+
+    if _ctx.store is not None:
+        addr = f"{_ctx.store.host}:{_ctx.store.port}"
+    elif topo.rank == 0:
+        _ctx.store_server = start_server("0.0.0.0", 0)
+        addr = f"{topo.master_addr}:{_ctx.store_server.port}"
+    else:
+        addr = None
+    # rank 0 names the negotiation domain, so a re-init on the same store starts a fresh log
+    obj = [(addr, f"mihvd/neg/{uuid.uuid4().hex[:12]}")] if topo.rank == 0 else [None]
+    dist.broadcast_object_list(obj, src=0, device=device if backend == "nccl" else None)
+    if _ctx.store is None:
+        addr = obj[0][0]
+    host, port = parse_addr(addr)
+    warn = 0.0 if cfg.stall_check_disable else cfg.stall_check_s
+    neg = runtime().Negotiator(host, port, topo.rank, topo.size, obj[0][1], cfg.cycle_time_ms / 1000.0, warn,
+                               cfg.stall_shutdown_s)
+    _ctx.engine = Engine(neg, cfg.fusion_threshold, topo.rank)
+
+
 def shutdown():
     """Tear down the world (``hvd.shutdown``). Safe to call more than once."""
     with _ctx.lock:
@@ -199,6 +243,10 @@ def shutdown():
             collectives._drain_all()
         except Exception:  # pragma: no cover
             pass
+        if _ctx.engine is not None:
+            _ctx.engine.flush(timeout=30)
+            _ctx.engine.stop()
+            _ctx.engine = None
         if _ctx.stall is not None:
             _ctx.stall.stop()
             _ctx.stall = None
@@ -210,6 +258,10 @@ def shutdown():
                 dist.destroy_process_group()
             except Exception:  # pragma: no cover
                 pass
+        if _ctx.store_server is not None:
+            _ctx.store_server.stop()
+            _ctx.store_server = None
+        _ctx.store = None
         _ctx.initialized = False
         _ctx.world_group = _ctx.local_group = _ctx.cross_group = None
 

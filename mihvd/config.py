@@ -19,6 +19,7 @@ _ALIASES = {
     "HIERARCHICAL_ALLREDUCE": "HOROVOD_HIERARCHICAL_ALLREDUCE",
     "AUTOTUNE": "HOROVOD_AUTOTUNE",
     "LOG_LEVEL": "HOROVOD_LOG_LEVEL",
+    "NEGOTIATE": "HOROVOD_NEGOTIATE",
 }
 
 
@@ -37,7 +38,7 @@ class Config:
     backend: str = "auto"                 # auto | nccl (=RCCL on ROCm) | gloo
     fusion_threshold: int = 64 * 1024 * 1024  # bytes per fusion bucket (Horovod default 64 MiB)
     bucket_align: int = 256               # bytes; every gradient view starts 256-B aligned
-    cycle_time_ms: float = 1.0            # kept for HOROVOD_CYCLE_TIME compatibility (unused: no polling loop)
+    cycle_time_ms: float = 1.0            # HOROVOD_CYCLE_TIME compatibility (the negotiator pushes, it does not poll)
     timeline: str = ""                    # Chrome-trace path; "{rank}" is substituted
     stall_check_s: float = 60.0
     stall_shutdown_s: float = 0.0
@@ -53,6 +54,8 @@ class Config:
     autotune_warmup_steps: int = 3
     autotune_trial_steps: int = 8
     roctx: bool = False                   # roctx ranges around collectives / steps (rocprofv3 --marker-trace)
+    negotiate: bool = False               # route async collectives through the native negotiation engine
+    store: str = "native"                 # rendezvous: native (mihvdrun's C++ store, if present) | torch
 
     @staticmethod
     def from_env(env=None) -> "Config":
@@ -77,4 +80,6 @@ class Config:
             autotune_warmup_steps=_get("AUTOTUNE_WARMUP_STEPS", 3, int, env),
             autotune_trial_steps=_get("AUTOTUNE_TRIAL_STEPS", 8, int, env),
             roctx=_get("ROCTX", False, bool, env),
+            negotiate=_get("NEGOTIATE", False, bool, env),
+            store=_get("STORE", "native", str, env),
         )

@@ -127,15 +127,20 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
     op = ReduceOp(op)
     n = _group_size(group)
     if op == ReduceOp.Adasum:
-        from .adasum import adasum_allreduce_
-
         if out is not tensor:
             out.copy_(tensor)
         if prescale_factor != 1.0:
             out.mul_(prescale_factor)
-        adasum_dispatch_(out, segments)
-        if postscale_factor != 1.0:
-            out.mul_(postscale_factor)
+
+        def run_adasum(out=out):
+            adasum_dispatch_(out, segments)
+            if postscale_factor != 1.0:
+                out.mul_(postscale_factor)
+
+        if ctx.engine is not None and n > 1:
+            work = ctx.engine.collective(f"allreduce.{name}", "adasum", f"{out.dtype}|{tuple(out.shape)}", run_adasum)
+            return _register(work, out, None, f"allreduce.{name}")
+        run_adasum()
         return _register(None, out, None, f"allreduce.{name}")
     wire, cctx = compression.compress(tensor)
     if wire is tensor and out is not tensor:
@@ -143,7 +148,13 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
         wire = out
     if prescale_factor != 1.0:
         wire.mul_(prescale_factor)
-    work = dist.all_reduce(wire, op=_torch_op(op), group=group, async_op=True) if n > 1 else None
+    if n == 1:
+        work = None
+    elif ctx.engine is not None:
+        # negotiated: launched by the engine thread in the coordinator's order, possibly fused
+        work = ctx.engine.allreduce(f"allreduce.{name}", wire, _torch_op(op), group)
+    else:
+        work = dist.all_reduce(wire, op=_torch_op(op), group=group, async_op=True)
     scale = postscale_factor / n if op == ReduceOp.Average else postscale_factor
 
     def post(_o, wire=wire, cctx=cctx, out=out, scale=scale):
@@ -228,11 +239,25 @@ def grouped_allreduce(tensors: Sequence[torch.Tensor], average=None, name=None, 
 # ------------------------------------------------------------------------------------------ #
 # broadcast / allgather / alltoall / reducescatter
 # ------------------------------------------------------------------------------------------ #
+def _flush_engine():
+    """Direct (non-negotiated) collectives first wait until every negotiated one was launched."""
+    ctx = basics._ctx
+    if ctx.engine is not None:
+        ctx.engine.flush()
+
+
 def broadcast_async_(tensor, root_rank, name=None, process_set=None) -> int:
-    basics._require()
+    ctx = basics._require()
     group = _group(process_set)
-    work = dist.broadcast(tensor, src=root_rank, group=group, async_op=True) if _group_size(group) > 1 else None
-    return _register(work, tensor, None, f"broadcast.{name or 'tensor'}")
+    name = f"broadcast.{name or 'tensor'}"
+    if _group_size(group) == 1:
+        work = None
+    elif ctx.engine is not None:
+        work = ctx.engine.collective(name, "broadcast", f"{tensor.dtype}|{tuple(tensor.shape)}|{root_rank}",
+                                     lambda: dist.broadcast(tensor, src=root_rank, group=group, async_op=True))
+    else:
+        work = dist.broadcast(tensor, src=root_rank, group=group, async_op=True)
+    return _register(work, tensor, None, name)
 
 
 def broadcast_async(tensor, root_rank, name=None, process_set=None) -> int:
@@ -250,29 +275,40 @@ def broadcast_(tensor, root_rank, name=None, process_set=None):
 
 def allgather_async(tensor, name=None, process_set=None) -> int:
     """Concatenate every rank's tensor along dim 0 (first dimensions may differ)."""
-    basics._require()
+    ctx = basics._require()
     group = _group(process_set)
     n = _group_size(group)
+    name = f"allgather.{name or 'tensor'}"
     if n == 1:
-        return _register(None, tensor.clone(), None, f"allgather.{name or 'tensor'}")
+        return _register(None, tensor.clone(), None, name)
     t = tensor.contiguous()
     if t.dim() == 0:
         t = t.view(1)
-    dim0 = torch.tensor([t.shape[0]], dtype=torch.long, device=t.device)
-    sizes = [torch.empty_like(dim0) for _ in range(n)]
-    dist.all_gather(sizes, dim0, group=group)
-    sizes = [int(s.item()) for s in sizes]
-    mx = max(sizes)
-    if mx != t.shape[0]:
-        pad = torch.zeros((mx - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        t = torch.cat([t, pad])
-    bufs = [torch.empty_like(t) for _ in range(n)]
-    work = dist.all_gather(bufs, t, group=group, async_op=True)
+    res: dict = {}
 
-    def post(_o, bufs=bufs, sizes=sizes):
-        return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+    def launch(t=t):
+        dim0 = torch.tensor([t.shape[0]], dtype=torch.long, device=t.device)
+        sizes = [torch.empty_like(dim0) for _ in range(n)]
+        dist.all_gather(sizes, dim0, group=group)
+        sizes = [int(s.item()) for s in sizes]
+        mx = max(sizes)
+        if mx != t.shape[0]:
+            pad = torch.zeros((mx - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            t = torch.cat([t, pad])
+        res["bufs"] = [torch.empty_like(t) for _ in range(n)]
+        res["sizes"] = sizes
+        return dist.all_gather(res["bufs"], t, group=group, async_op=True)
 
-    return _register(work, None, post, f"allgather.{name or 'tensor'}")
+    if ctx.engine is not None:
+        # dim 0 may differ across ranks: the signature carries only dtype and trailing dims
+        work = ctx.engine.collective(name, "allgather", f"{t.dtype}|{tuple(t.shape[1:])}", launch)
+    else:
+        work = launch()
+
+    def post(_o, res=res):
+        return torch.cat([b[:s] for b, s in zip(res["bufs"], res["sizes"])])
+
+    return _register(work, None, post, name)
 
 
 def allgather(tensor, name=None, process_set=None):
@@ -283,6 +319,7 @@ def alltoall(tensor, splits=None, name=None, process_set=None):
     """Scatter slices of dim 0 to every rank and gather what they send back (``hvd.alltoall``).
     Returns ``(output, received_splits)``."""
     basics._require()
+    _flush_engine()
     group = _group(process_set)
     n = _group_size(group)
     if splits is None:
@@ -321,6 +358,7 @@ def alltoall(tensor, splits=None, name=None, process_set=None):
 def reducescatter(tensor, op=ReduceOp.Average, name=None, process_set=None):
     """Reduce across ranks, then return this rank's dim-0 slice (``hvd.reducescatter``)."""
     basics._require()
+    _flush_engine()
     group = _group(process_set)
     n = _group_size(group)
     if n == 1:
@@ -346,6 +384,7 @@ def reducescatter(tensor, op=ReduceOp.Average, name=None, process_set=None):
 
 def barrier(process_set=None):
     basics._require()
+    _flush_engine()
     if basics.size() > 1:
         if basics.backend() == "nccl":
             dist.barrier(device_ids=[basics.device().index])
@@ -356,6 +395,7 @@ def barrier(process_set=None):
 def join(device=-1) -> int:
     """Horovod ``join``: block until every rank arrives; returns the last rank to join."""
     basics._require()
+    _flush_engine()
     t = torch.tensor([basics.rank()], dtype=torch.long, device=basics.device())
     if basics.size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -364,6 +404,7 @@ def join(device=-1) -> int:
 
 def broadcast_object(obj, root_rank=0, name=None, process_set=None):
     basics._require()
+    _flush_engine()
     if basics.size() == 1:
         return obj
     lst = [obj]
@@ -374,6 +415,7 @@ def broadcast_object(obj, root_rank=0, name=None, process_set=None):
 
 def allgather_object(obj, name=None, process_set=None):
     basics._require()
+    _flush_engine()
     if basics.size() == 1:
         return [obj]
     out = [None] * basics.size()

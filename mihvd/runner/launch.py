@@ -7,7 +7,8 @@ The reference's MPIJob launcher runs (horovod/tensorflow-mnist.yaml:17-38)::
 
 ``mihvdrun`` accepts exactly that argv (plus horovodrun's ``-np N -H host:slots``). MPI transport
 flags (``-mca``, ``-bind-to``) are accepted and ignored — the data plane is RCCL over xGMI, the
-bootstrap is torch's TCP store at ``MASTER_ADDR:MASTER_PORT``. Ranks are laid out by
+bootstrap is the launcher's own C++ key-value store (``MIHVD_STORE_ADDR``, mihvd/runner/store.py;
+``MIHVD_STORE=torch`` falls back to torch's TCPStore at ``MASTER_ADDR:MASTER_PORT``). Ranks are laid out by
 ``-map-by slot`` (fill each host) or ``-map-by node`` (round robin); local ranks on a host get
 consecutive GPUs. Remote hosts are reached over ssh, as mpirun does inside an MPIJob (hostfile from
 ``--hostfile`` or ``$OMPI_MCA_orte_default_hostfile``, which the MPI Operator mounts).
@@ -267,10 +268,19 @@ def launch(spec: LaunchSpec) -> int:
             print(f"mihvdrun: ignoring MPI option {m}", file=sys.stderr)
         for k, v in spec.mca:
             print(f"mihvdrun: ignoring MCA parameter {k}={v} (data plane is RCCL)", file=sys.stderr)
+    # The rendezvous server (C++ StoreServer, csrc/runtime/store.cc) lives in the launcher, like
+    # horovodrun's: ranks build their process group and the negotiation engine over it.
+    server = None
+    if os.environ.get("MIHVD_STORE", "native") != "torch":
+        from .store import start_server
+
+        server = start_server("127.0.0.1" if all_local else "0.0.0.0", 0)
     procs: list[_Proc] = []
     threads = []
     for rank, host, lr, ls, node in layout:
         renv = build_rank_env(spec, rank, lr, ls, node, master_addr, master_port)
+        if server is not None:
+            renv["MIHVD_STORE_ADDR"] = f"{master_addr}:{server.port}"
         if _is_local(host):
             env = dict(os.environ)
             env.update(renv)
@@ -325,6 +335,8 @@ def launch(spec: LaunchSpec) -> int:
             signal.signal(s, h)
         for t in threads:
             t.join(timeout=5)
+        if server is not None:
+            server.stop()
     return exit_code
 
 

@@ -110,3 +110,49 @@ def test_fault_kill_tears_down_job(tmp_path):
     assert p.returncode == 7
     assert "rank 1 exited with code 7" in p.stderr
     assert outs == [None, None]
+
+
+NEG = {"MIHVD_NEGOTIATE": "1"}
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_negotiated_collectives_any_order(tmp_path, np_):
+    """Native negotiation engine (csrc/runtime/negotiator.cc) over mihvdrun's C++ store: ranks
+    enqueue named collectives in different orders and still all agree; compatible allreduces are
+    fused within a coordinator record."""
+    _, outs = run_scenario(tmp_path, "negotiated_order", np_=np_, env=NEG)
+    for o in outs:
+        assert o["ok"], o
+        assert o["bc"] == [float(np_ - 1)] * 5
+        assert o["ag"] == [[float(q)] * 2 for q in range(np_) for _ in range(q + 1)]
+        assert o["submitted"] == 14
+    assert len({o["launches"] for o in outs}) == 1  # identical launch sequence on every rank
+    assert len({o["fused"] for o in outs}) == 1
+
+
+def test_negotiation_stall_report_names_missing_rank(tmp_path):
+    env = dict(NEG, MIHVD_STALL_CHECK_TIME_SECONDS="1")
+    p, (a, b) = run_scenario(tmp_path, "negotiated_stall", env=env)
+    assert a["value"] == [3.0, 3.0] == b["value"]
+    assert "collective 'allreduce.late' (generation 0) was submitted by ranks [0] but not by ranks [1]" in p.stderr
+    assert a["warnings"] >= 1
+
+
+def test_negotiation_rejects_mismatched_shapes(tmp_path):
+    _, (a, b) = run_scenario(tmp_path, "negotiated_mismatch", env=NEG)
+    for o in (a, b):
+        assert o["error"] and "mismatched collective 'allreduce.shape_mismatch'" in o["error"]
+        assert o["after"] == [2.0] * 3
+
+
+def test_dp_equivalence_negotiated(tmp_path):
+    """DistributedOptimizer bucket allreduces through the negotiation engine."""
+    _, outs = run_scenario(tmp_path, "dp_equivalence", env=NEG)
+    for o in outs:
+        assert o["maxdiff_0"] < 1e-5 and o["maxdiff_67108864"] < 1e-5
+
+
+def test_torch_store_fallback(tmp_path):
+    """MIHVD_STORE=torch: the launcher does not start its store; init uses torch's TCPStore."""
+    _, (a, b) = run_scenario(tmp_path, "collectives", env={"MIHVD_STORE": "torch"})
+    assert a["sum"] == b["sum"]

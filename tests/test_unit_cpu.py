@@ -336,3 +336,107 @@ def test_trace_range_noop_without_roctx():
 
     with trace_range("x"):
         pass
+
+
+# ---------------------------------------------------------------------------------------------
+# control plane: C++ key-value store + negotiation engine (csrc/runtime/store.cc, negotiator.cc)
+# ---------------------------------------------------------------------------------------------
+def test_native_store_semantics():
+    import threading
+    import time
+
+    from mihvd._native import runtime
+
+    rt = runtime()
+    srv = rt.StoreServer("127.0.0.1", 0)
+    try:
+        c = rt.StoreClient("127.0.0.1", srv.port)
+        c.set("bin", b"a\x00b")
+        assert c.get("bin") == b"a\x00b"
+        assert c.add("ctr", 5) == 5 and c.add("ctr", -7) == -2
+        assert c.try_get("nope", 0.05) is None
+        with pytest.raises(RuntimeError, match="timeout"):
+            c.get("nope", 0.05)
+        # a blocking get is parked on the server until another client sets the key
+        t0 = time.time()
+        threading.Timer(0.2, lambda: rt.StoreClient("127.0.0.1", srv.port).set("late", b"v")).start()
+        assert c.get("late", 5.0) == b"v" and time.time() - t0 >= 0.15
+        # torch.distributed compare_set semantics
+        assert c.compare_set("cs", "", "x") == b"x"
+        assert c.compare_set("cs", "wrong", "y") == b"x"
+        assert c.compare_set("cs", "x", "y") == b"y"
+        assert c.check(["bin", "ctr"]) and not c.check(["bin", "zz"])
+        assert not c.wait(["zz"], 0.05)
+        c.append("ap", b"12")
+        c.append("ap", b"34")
+        assert c.get("ap") == b"1234"
+        assert c.delete("bin") and not c.delete("bin")
+        assert c.num_keys() == srv.num_keys() == 4  # ctr, late, cs, ap
+    finally:
+        srv.stop()
+
+
+def test_native_store_backs_torch_process_group():
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+
+    from mihvd.runner.store import NativeStore, start_server
+
+    srv = start_server("127.0.0.1", 0)
+    try:
+        st = NativeStore("127.0.0.1", srv.port, datetime.timedelta(seconds=30))
+        dist.init_process_group("gloo", store=dist.PrefixStore("t", st), rank=0, world_size=1)
+        try:
+            t = torch.ones(3)
+            dist.all_reduce(t)
+            assert t.tolist() == [1.0] * 3
+        finally:
+            dist.destroy_process_group()
+    finally:
+        srv.stop()
+
+
+def test_negotiator_orders_and_validates():
+    import random
+    import time
+
+    from mihvd._native import runtime
+
+    rt = runtime()
+    srv = rt.StoreServer("127.0.0.1", 0)
+    W = 3
+    negs = [rt.Negotiator("127.0.0.1", srv.port, r, W, "u", 0.001, 0.3, 0.0) for r in range(W)]
+    try:
+        names = [f"n{i}" for i in range(25)]
+        for r in range(W):
+            order = names[:]
+            random.Random(r).shuffle(order)
+            for nm in order:
+                negs[r].submit(nm, "sig")
+            negs[r].submit("n0", "sig")  # generation 1 of a reused name
+        got = [[] for _ in range(W)]
+        deadline = time.time() + 20
+        while any(len(g) < 26 for g in got) and time.time() < deadline:
+            for r in range(W):
+                got[r] += [(x.name, x.generation, x.batch) for x in negs[r].wait(0.05)]
+        assert all(g == got[0] for g in got)            # same order AND same batches on all ranks
+        assert sorted(n for n, gen, _ in got[0] if gen == 0) == sorted(names)
+        assert [n for n, gen, _ in got[0] if gen == 1] == ["n0"]
+        # stall view: only ranks 0 and 2 submit
+        negs[0].submit("stuck", "s")
+        negs[2].submit("stuck", "s")
+        time.sleep(0.8)
+        st = negs[0].stalled(0.0)
+        assert [(e.name, e.ready_ranks, e.missing_ranks) for e in st] == [("stuck", [0, 2], [1])]
+        assert negs[0].warnings >= 1
+        negs[1].submit("stuck", "other")  # signature mismatch is reported on every rank
+        errs = []
+        while not errs and time.time() < deadline:
+            errs = [x.error for x in negs[1].wait(0.1)]
+        assert "mismatched collective 'stuck'" in errs[0]
+    finally:
+        for n in negs:
+            n.stop()
+        srv.stop()

@@ -196,6 +196,60 @@ def sc_fault(outdir):
     out(outdir, "fault", {"completed": True})
 
 
+def sc_negotiated_order(outdir):
+    """MIHVD_NEGOTIATE=1: every rank enqueues the same named collectives in a different order
+    (allreduces of different shapes, a broadcast and an allgather interleaved). Without negotiation
+    gloo would pair mismatched calls; the coordinator's order makes every rank agree."""
+    import random
+
+    from mihvd import basics
+
+    r, n = hvd.rank(), hvd.size()
+    eng = basics._ctx.engine
+    assert eng is not None and basics._ctx.store is not None
+    names = [f"t{i}" for i in range(12)]
+    order = names[:]
+    random.Random(100 + r).shuffle(order)
+    handles = {}
+    for i, nm in enumerate(order):
+        k = int(nm[1:])
+        handles[nm] = hvd.allreduce_async(torch.full((k + 1, 3), float(r + k)), name=nm, op=hvd.Sum)
+        if i == 3 + r:  # the broadcast / allgather land at different positions on each rank
+            handles["bc"] = hvd.broadcast_async(torch.full((5,), float(r)), root_rank=n - 1, name="bc")
+        if i == 7 - r:
+            handles["ag"] = hvd.allgather_async(torch.full((r + 1, 2), float(r)), name="ag")
+    res = {nm: hvd.synchronize(h).tolist() for nm, h in handles.items()}
+    ok = all(res[f"t{k}"] == torch.full((k + 1, 3), float(sum(q + k for q in range(n)))).tolist() for k in range(12))
+    out(outdir, "negotiated_order", {"ok": ok, "bc": res["bc"], "ag": res["ag"], "launches": eng.launches,
+                                     "fused": eng.fused_launches, "submitted": eng.neg.submitted})
+
+
+def sc_negotiated_stall(outdir):
+    """Rank 1 submits 'late' 3 s after rank 0: the coordinator names the missing rank, then the
+    collective completes once rank 1 arrives."""
+    r = hvd.rank()
+    if r == 1:
+        time.sleep(3.0)
+    v = hvd.allreduce(torch.ones(2) * (r + 1), name="late", op=hvd.Sum)
+    from mihvd import basics
+
+    st = basics._ctx.engine.neg
+    out(outdir, "negotiated_stall", {"value": v.tolist(), "warnings": st.warnings})
+
+
+def sc_negotiated_mismatch(outdir):
+    """Same name, different shapes on the two ranks: the coordinator refuses to launch it and
+    every rank gets the error instead of a corrupted or hung collective."""
+    r = hvd.rank()
+    err = None
+    try:
+        hvd.allreduce(torch.ones(4 + r), name="shape_mismatch")
+    except RuntimeError as e:
+        err = str(e)
+    ok = hvd.allreduce(torch.ones(3), name="after", op=hvd.Sum).tolist()
+    out(outdir, "negotiated_mismatch", {"error": err, "after": ok})
+
+
 def main():
     scenario, outdir = sys.argv[1], sys.argv[2]
     hvd.init()
