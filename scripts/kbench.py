@@ -32,6 +32,8 @@ def main():
     o = tr.ops
     st = tr.state
     sh = tr.shadow
+    dz8 = tr.dz.repeat(8, 1).contiguous()
+    a28 = tr.a2.repeat(8, 1).contiguous()
     ops = {
         "conv1_fwd": lambda: o.conv1_fwd(tr.x_buf, None, st, tr.pview("conv_layer1/conv2d/kernel"),
                                          tr.pview("conv_layer1/conv2d/bias"), tr.a1, tr.idx1),
@@ -54,6 +56,10 @@ def main():
             tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
             tr.gview("dense_1/bias"), 3, None, None, tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], st, 0.0, 0.9,
             0.999, 1e-8, 1.0, 0, False),
+        # dW3 over the all-gathered factors of 8 ranks (the N=8 factor-gather data plane, Kw = 800)
+        "fc1_wgrad_k8x": lambda: o.fc1_wgrad(tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"),
+                                             tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
+                                             tr.gview("dense_1/bias"), 1, dz8, a28),
         "adam": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, sh, st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
         "adam_small": lambda: o.adam_step(tr.params[:W3], tr.grads[:W3], tr.m[:W3], tr.v[:W3], sh[:W3], st, 0, 0.0,
                                           0.9, 0.999, 1e-8, 1.0, 0),

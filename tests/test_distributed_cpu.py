@@ -156,3 +156,17 @@ def test_torch_store_fallback(tmp_path):
     """MIHVD_STORE=torch: the launcher does not start its store; init uses torch's TCPStore."""
     _, (a, b) = run_scenario(tmp_path, "collectives", env={"MIHVD_STORE": "torch"})
     assert a["sum"] == b["sum"]
+
+
+def test_collective_custom_ops_autograd(tmp_path):
+    """torch.ops.mihvd_dist: allreduce grad = allreduce(grad); allgather grad = this rank's slice of
+    the summed grad; broadcast grad = sum on the root, zero elsewhere (Horovod's rules)."""
+    _, (a, b) = run_scenario(tmp_path, "torch_ops")
+    assert a["y"] == [3.0] * 3                      # mean of 2*1 and 2*2
+    assert a["wgrad"] == b["wgrad"] == [2.0] * 3    # d/dw sum(avg(2w)) over both ranks' losses
+    assert a["g"] == [[0.0, 0.0], [1.0, 1.0], [1.0, 1.0]]
+    # loss_r = sum_i i * g_i on both ranks -> d/dx = 2 * i for this rank's rows
+    assert a["xgrad"] == [[0.0, 0.0]] and b["xgrad"] == [[2.0, 2.0], [4.0, 4.0]]
+    assert a["bb"] == b["bb"] == [0.0, 0.0]
+    assert a["bgrad"] == [3.0, 3.0] and b["bgrad"] == [0.0, 0.0]
+    assert a["t"] == [3.0] * 4

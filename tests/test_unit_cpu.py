@@ -440,3 +440,20 @@ def test_negotiator_orders_and_validates():
         for n in negs:
             n.stop()
         srv.stop()
+
+
+def test_collective_custom_ops_trace_single_rank(hvd_single):
+    """torch.ops.mihvd_dist ops run at world size 1 and trace through make_fx as single nodes."""
+    import torch
+    from torch.fx.experimental.proxy_tensor import make_fx
+
+    from mihvd.ops import collective_ops  # noqa: F401
+
+    ops = torch.ops.mihvd_dist
+    x = torch.randn(4, 3, requires_grad=True)
+    y = ops.allreduce(x, 0, "x")
+    y.sum().backward()
+    assert torch.equal(y, x) and torch.equal(x.grad, torch.ones(4, 3))
+    gm = make_fx(lambda t: ops.allreduce(t * 2, 1, "t") + 1)(torch.randn(5))
+    assert "mihvd_dist.allreduce" in gm.code
+    assert ops.allgather(torch.ones(2, 2), "g").shape == (2, 2)

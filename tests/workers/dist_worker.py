@@ -250,6 +250,27 @@ def sc_negotiated_mismatch(outdir):
     out(outdir, "negotiated_mismatch", {"error": err, "after": ok})
 
 
+def sc_torch_ops(outdir):
+    """torch.ops.mihvd_dist.* custom ops: values and Horovod's autograd rules across ranks."""
+    from mihvd.ops import collective_ops  # noqa: F401  (registers torch.ops.mihvd_dist)
+
+    ops = torch.ops.mihvd_dist
+    r, n = hvd.rank(), hvd.size()
+    w = torch.full((3,), float(r + 1), requires_grad=True)
+    y = ops.allreduce(w * 2.0, int(hvd.Average), "w")
+    y.sum().backward()
+    x = torch.full((r + 1, 2), float(r), requires_grad=True)
+    g = ops.allgather(x, "x")
+    (g * torch.arange(g.shape[0], dtype=torch.float32).unsqueeze(1)).sum().backward()
+    b = torch.full((2,), float(r), requires_grad=True)
+    bb = ops.broadcast(b, 0, "b")
+    (bb * (r + 1)).sum().backward()
+    t = torch.ones(4) * (r + 1)
+    ops.allreduce_(t, int(hvd.Sum), "inplace")
+    out(outdir, "torch_ops", {"y": y.tolist(), "wgrad": w.grad.tolist(), "g": g.tolist(), "xgrad": x.grad.tolist(),
+                              "bb": bb.tolist(), "bgrad": b.grad.tolist(), "t": t.tolist()})
+
+
 def main():
     scenario, outdir = sys.argv[1], sys.argv[2]
     hvd.init()
