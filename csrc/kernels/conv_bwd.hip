@@ -93,7 +93,7 @@ __device__ __forceinline__ void finish_dy_item(const DyItem& it, u16 g[4], int d
   }
 }
 
-__global__ void __launch_bounds__(512) conv2_bwd_kernel(
+__device__ __forceinline__ void conv2_bwd_block(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
@@ -465,17 +465,69 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
   }
 }
 
+// TAIL: the launch also carries the dense/kernel Adam update (AdamTail, common.h). Blocks
+// [n_conv, grid) have no conv work and start on it at once (they sit on the CUs the conv roles
+// leave idle); every conv block joins in when its own work is done.
+template <bool TAIL>
+__global__ void __launch_bounds__(512) conv2_bwd_kernel(
+    const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
+    const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
+    int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
+    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int n_conv, AdamTail at) {
+  if ((int)blockIdx.x < n_conv)
+    conv2_bwd_block(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit);
+  if constexpr (TAIL) adam_tail_run(at);
+}
+
 // Blocks [0, 200): dW2 = sum of the (<= 32) conv2 wgrad slabs; 64 float4 outputs x 4 slab groups of
 // 8 per block, every load in flight at once (absent slabs masked, not branched around), then a
 // 4-way LDS sum. Blocks [200, 214): dW1 | db1 | db2 = sum over images of the per-image partial rows;
 // 64 outputs x 4 row groups per block, 8 rows per load batch.
+//
+// ADAM (world size 1): the same launch is the optimizer for every parameter except dense/kernel
+// (whose update rode on conv2_bwd's tail): each reduced conv gradient is applied to its slot of the
+// flat p/m/v/shadow buffers right away, blocks [214, 214 + n_fc) update the fc slice
+// [fc_lo4, fc_hi4) (float4 indices: dense/bias, dense_1/*) from the gradient buffer, and block 0
+// advances the forward step and re-arms the tail counter — the step's last launch.
 constexpr int CR_SLAB_BLOCKS = 200, CR_PART_BLOCKS = CP_W / 64;
+struct ReduceAdam {
+  AdamArgs ad;             // p/m/v/shadow = flat buffer bases; state = the step state (read + written)
+  const float* gflat;      // flat gradient buffer
+  int64_t o_w2, o_w1, o_b1, o_b2;  // element offsets of the conv segments in the flat buffers
+  int64_t fc_lo4, fc_hi4;  // float4 range of the fc segments updated from gflat
+};
+template <bool ADAM>
 __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab,
                                                                  const float* __restrict__ cpart, int B,
                                                                  float* __restrict__ gW2, float* __restrict__ gW1,
-                                                                 float* __restrict__ gb1, float* __restrict__ gb2) {
+                                                                 float* __restrict__ gb1, float* __restrict__ gb2,
+                                                                 ReduceAdam ra) {
   __shared__ float4 r4[256];
   const int t = threadIdx.x;
+  AdamCoef c;
+  if constexpr (ADAM) {
+    c = adam_coef((float)ra.ad.state[ST_OPT], ra.ad.lr, ra.ad.b1, ra.ad.b2, ra.ad.eps, ra.ad.gscale, ra.ad.rule);
+    if (blockIdx.x == 0 && t < 8) {
+      int64_t* st = const_cast<int64_t*>(ra.ad.state);
+      if (t == 0) st[ST_FWD] += 1;
+      st[ST_TAILQ + 16 * t] = 0;  // re-arm the Adam-tail counters of the next conv2_bwd
+    }
+    if ((int)blockIdx.x >= CR_SLAB_BLOCKS + CR_PART_BLOCKS) {
+      for (int64_t i = ra.fc_lo4 + ((int64_t)blockIdx.x - CR_SLAB_BLOCKS - CR_PART_BLOCKS) * 256 + t; i < ra.fc_hi4;
+           i += (int64_t)(gridDim.x - CR_SLAB_BLOCKS - CR_PART_BLOCKS) * 256) {
+        float4 pp = reinterpret_cast<const float4*>(ra.ad.p)[i];
+        const float4 gg = reinterpret_cast<const float4*>(ra.gflat)[i];
+        float4 mm = reinterpret_cast<const float4*>(ra.ad.m)[i];
+        float4 vv = reinterpret_cast<const float4*>(ra.ad.v)[i];
+        const uint2 sh = adam4(pp, mm, vv, gg, c);
+        reinterpret_cast<float4*>(ra.ad.p)[i] = pp;
+        reinterpret_cast<float4*>(ra.ad.m)[i] = mm;
+        reinterpret_cast<float4*>(ra.ad.v)[i] = vv;
+        reinterpret_cast<uint2*>(ra.ad.shadow)[i] = sh;
+      }
+      return;
+    }
+  }
   if ((int)blockIdx.x >= CR_SLAB_BLOCKS) {
     float* r1 = reinterpret_cast<float*>(r4);
     const int o = ((int)blockIdx.x - CR_SLAB_BLOCKS) * 64 + (t & 63), rg = t >> 6;
@@ -497,6 +549,15 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
       if (o < CP_DB1) gW1[o] = s;
       else if (o < CP_DB2) gb1[o - CP_DB1] = s;
       else gb2[o - CP_DB2] = s;
+      if constexpr (ADAM) {
+        const int64_t f = o < CP_DB1 ? ra.o_w1 + o : o < CP_DB2 ? ra.o_b1 + (o - CP_DB1) : ra.o_b2 + (o - CP_DB2);
+        float pv = ra.ad.p[f], mv = ra.ad.m[f], vv = ra.ad.v[f];
+        adam1(pv, mv, vv, s, c);
+        ra.ad.p[f] = pv;
+        ra.ad.m[f] = mv;
+        ra.ad.v[f] = vv;
+        ra.ad.shadow[f] = f2bf(pv);
+      }
     }
     return;
   }
@@ -515,18 +576,31 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
   r4[t] = s;
   __syncthreads();
   if (t < 64 && o < 12800) {
-    const float4 a = r4[t], b = r4[64 + t], c = r4[128 + t], d = r4[192 + t];
-    reinterpret_cast<float4*>(gW2)[o] = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
-                                                    (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
+    const float4 a = r4[t], b = r4[64 + t], cc = r4[128 + t], d = r4[192 + t];
+    const float4 g = make_float4((a.x + b.x) + (cc.x + d.x), (a.y + b.y) + (cc.y + d.y), (a.z + b.z) + (cc.z + d.z),
+                                 (a.w + b.w) + (cc.w + d.w));
+    reinterpret_cast<float4*>(gW2)[o] = g;
+    if constexpr (ADAM) {
+      const int64_t f4 = ra.o_w2 / 4 + o;
+      float4 pp = reinterpret_cast<const float4*>(ra.ad.p)[f4];
+      float4 mm = reinterpret_cast<const float4*>(ra.ad.m)[f4];
+      float4 vv = reinterpret_cast<const float4*>(ra.ad.v)[f4];
+      const uint2 sh = adam4(pp, mm, vv, g, c);
+      reinterpret_cast<float4*>(ra.ad.p)[f4] = pp;
+      reinterpret_cast<float4*>(ra.ad.m)[f4] = mm;
+      reinterpret_cast<float4*>(ra.ad.v)[f4] = vv;
+      reinterpret_cast<uint2*>(ra.ad.shadow)[f4] = sh;
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------ //
 int64_t conv2_wgrad_groups(int64_t B) { return (B + CB_IPB - 1) / CB_IPB; }
 
-void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
-               const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1) {
+static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+                             const at::Tensor& x, const c10::optional<at::Tensor>& rows,
+                             const c10::optional<at::Tensor>& state, const at::Tensor& idx1, at::Tensor& slab,
+                             at::Tensor& cpart, const c10::optional<at::Tensor>& g1, const AdamTail* tail) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
@@ -548,18 +622,65 @@ void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a
   else TORCH_CHECK(n_pool >= B, "conv2_bwd: x has fewer rows than the batch");
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   static bool attr = [] {
-    hipFuncSetAttribute((const void*)conv2_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
+    hipFuncSetAttribute((const void*)conv2_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
+    hipFuncSetAttribute((const void*)conv2_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
     return true;
   }();
   (void)attr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const int role = debug_role_only();  // 0: dgrad blocks only, 1: wgrad blocks only
   const int n_dgrad = role == 1 ? 0 : B;
-  const int grid = role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
-  conv2_bwd_kernel<<<grid, 512, CB_LDS, stream>>>(
-      (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
-      x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-      cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit());
+  const int n_conv = role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
+  if (tail == nullptr) {
+    conv2_bwd_kernel<false><<<n_conv, 512, CB_LDS, stream>>>(
+        (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
+        x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{});
+  } else {
+    // one 512-thread block per CU (144 KB of LDS): the extra tail-only blocks take the CUs the
+    // conv roles leave free, so the update streams from the first cycle
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = std::max(n_conv + 8, ncu);
+    conv2_bwd_kernel<true><<<grid, 512, CB_LDS, stream>>>(
+        (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
+        x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, *tail);
+  }
+}
+
+void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+               const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1) {
+  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, g1, nullptr);
+}
+
+static void check_flat(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* what) {
+  TORCH_CHECK(t.scalar_type() == dt && t.numel() == n && t.is_contiguous() && ((uintptr_t)t.data_ptr() & 15) == 0, what);
+}
+
+// conv2_bwd + the Adam update of a flat slice (p3/g3/m3/v3/shadow3: the dense/kernel segment) in
+// the launch's tail. The tail counters state[ST_TAILQ..] must be 0 on entry
+// (conv2_wgrad_reduce_adam re-arms them).
+void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, at::Tensor& state, const at::Tensor& idx1,
+                    at::Tensor& slab, at::Tensor& cpart, at::Tensor& p3, const at::Tensor& g3, at::Tensor& m3,
+                    at::Tensor& v3, at::Tensor& shadow3, double lr, double b1, double b2, double eps, double grad_scale,
+                    int64_t rule) {
+  const int64_t n = p3.numel();
+  TORCH_CHECK(n % 4 == 0 && n > 0, "conv2_bwd_adam: slice length must be a positive multiple of 4");
+  check_flat(p3, at::kFloat, n, "conv2_bwd_adam: p3");
+  check_flat(g3, at::kFloat, n, "conv2_bwd_adam: g3");
+  check_flat(m3, at::kFloat, n, "conv2_bwd_adam: m3");
+  check_flat(v3, at::kFloat, n, "conv2_bwd_adam: v3");
+  check_flat(shadow3, at::kBFloat16, n, "conv2_bwd_adam: shadow3");
+  TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_TAIL_WORDS,
+              "conv2_bwd_adam: state must hold ST_TAIL_WORDS (160) int64 words");
+  AdamTail at{p3.data_ptr<float>(), g3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(),
+              (u16*)shadow3.data_ptr(), n / 4, state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2,
+              (float)eps, (float)grad_scale, (int)rule};
+  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, &at);
 }
 
 void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2, at::Tensor& gW1,
@@ -572,9 +693,57 @@ void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t
   TORCH_CHECK(gW1.numel() == 800 && gb1.numel() == 32 && gb2.numel() == 64 && gW1.dtype() == at::kFloat &&
                   gb1.dtype() == at::kFloat && gb2.dtype() == at::kFloat, "conv2_wgrad_reduce: gW1/gb1/gb2");
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv2_wgrad_reduce_kernel<<<CR_SLAB_BLOCKS + CR_PART_BLOCKS, 256, 0, stream>>>(
+  conv2_wgrad_reduce_kernel<false><<<CR_SLAB_BLOCKS + CR_PART_BLOCKS, 256, 0, stream>>>(
       slab.data_ptr<float>(), G, cpart.data_ptr<float>(), (int)B, gW2.data_ptr<float>(), gW1.data_ptr<float>(),
-      gb1.data_ptr<float>(), gb2.data_ptr<float>());
+      gb1.data_ptr<float>(), gb2.data_ptr<float>(), ReduceAdam{});
+}
+
+// conv2_wgrad_reduce + Adam for every parameter outside [w3_lo, end) of the flat buffers: the conv
+// gradients straight from the reduction, [fc_lo, w3_lo) from the gradient buffer. gW2/gW1/gb1/gb2
+// must be views of `grads` (their offsets locate the parameters). Advances state[ST_FWD] and
+// re-arms the Adam-tail counters: the last launch of a world-size-1 step.
+void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2,
+                             at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads, at::Tensor& p,
+                             at::Tensor& m, at::Tensor& v, at::Tensor& shadow, at::Tensor& state, int64_t fc_lo,
+                             int64_t w3_lo, double lr, double b1, double b2, double eps, double grad_scale,
+                             int64_t rule) {
+  const int G = (int)conv2_wgrad_groups(B);
+  TORCH_CHECK(G >= 1 && G <= 32, "conv2_wgrad_reduce_adam: at most 32 wgrad slabs");
+  TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_wgrad_reduce_adam: slab");
+  TORCH_CHECK(cpart.dtype() == at::kFloat && cpart.numel() >= B * CP_W, "conv2_wgrad_reduce_adam: cpart");
+  const int64_t n = grads.numel();
+  check_flat(grads, at::kFloat, n, "conv2_wgrad_reduce_adam: grads");
+  check_flat(p, at::kFloat, n, "conv2_wgrad_reduce_adam: p");
+  check_flat(m, at::kFloat, n, "conv2_wgrad_reduce_adam: m");
+  check_flat(v, at::kFloat, n, "conv2_wgrad_reduce_adam: v");
+  check_flat(shadow, at::kBFloat16, n, "conv2_wgrad_reduce_adam: shadow");
+  TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_TAIL_WORDS,
+              "conv2_wgrad_reduce_adam: state must hold ST_TAIL_WORDS (160) int64 words");
+  TORCH_CHECK(fc_lo % 4 == 0 && w3_lo % 4 == 0 && 0 <= fc_lo && fc_lo <= w3_lo && w3_lo <= n,
+              "conv2_wgrad_reduce_adam: fc_lo/w3_lo");
+  const float* g0 = grads.data_ptr<float>();
+  auto off = [&](const at::Tensor& t, int64_t len, const char* what) {
+    TORCH_CHECK(t.dtype() == at::kFloat && t.numel() == len && t.is_contiguous(), what);
+    const int64_t o = t.data_ptr<float>() - g0;
+    TORCH_CHECK(o >= 0 && o + len <= fc_lo, what, " must be a view of grads below fc_lo");
+    return o;
+  };
+  ReduceAdam ra;
+  ra.ad = AdamArgs{p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (u16*)shadow.data_ptr(),
+                   state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale, (int)rule};
+  ra.gflat = g0;
+  ra.o_w2 = off(gW2, 51200, "conv2_wgrad_reduce_adam: gW2");
+  TORCH_CHECK(ra.o_w2 % 4 == 0, "conv2_wgrad_reduce_adam: gW2 must be 16-byte aligned");
+  ra.o_w1 = off(gW1, 800, "conv2_wgrad_reduce_adam: gW1");
+  ra.o_b1 = off(gb1, 32, "conv2_wgrad_reduce_adam: gb1");
+  ra.o_b2 = off(gb2, 64, "conv2_wgrad_reduce_adam: gb2");
+  ra.fc_lo4 = fc_lo / 4;
+  ra.fc_hi4 = w3_lo / 4;
+  const int n_fc = (int)std::max<int64_t>(1, std::min<int64_t>(64, (ra.fc_hi4 - ra.fc_lo4 + 255) / 256));
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  conv2_wgrad_reduce_kernel<true><<<CR_SLAB_BLOCKS + CR_PART_BLOCKS + n_fc, 256, 0, stream>>>(
+      slab.data_ptr<float>(), G, cpart.data_ptr<float>(), (int)B, gW2.data_ptr<float>(), gW1.data_ptr<float>(),
+      gb1.data_ptr<float>(), gb2.data_ptr<float>(), ra);
 }
 
 }  // namespace mihvd

@@ -103,7 +103,9 @@ class FusedMNISTTrainer:
         self.m = torch.zeros(FLAT_NUMEL, **f32)
         self.v = torch.zeros(FLAT_NUMEL, **f32)
         self.shadow = torch.zeros(FLAT_NUMEL, device=dev, dtype=torch.bfloat16)
-        self.state = torch.zeros(4, device=dev, dtype=torch.int64)
+        # device step state: [0] forward step, [1] optimizer step t, [32 + 16 q] Adam-tail chunk
+        # counters (csrc/kernels/common.h ST_*); 160 int64 words
+        self.state = torch.zeros(160, device=dev, dtype=torch.int64)
         ref = MNISTConvNet(impl="torch", seed=seed)
         self.load_model_weights(ref)
         B = self.B
@@ -158,6 +160,12 @@ class FusedMNISTTrainer:
         self.fuse_w3 = (os.environ.get("MIHVD_FUSE_W3_ADAM", "0") == "1" and not self.pipeline
                         and (not self.collectives or self.gather))
         self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when fused
+        # MIHVD_FUSED_OPT=1 (default at world size 1): no separate optimizer launch. The dense/kernel
+        # update (98 % of the optimizer's HBM traffic) streams in the tail of the conv2_bwd launch —
+        # tail-only blocks on the CUs the conv roles leave idle, conv blocks joining as they finish —
+        # and conv2_wgrad_reduce applies Adam to every other parameter as it produces the gradients.
+        self.fused_opt = (os.environ.get("MIHVD_FUSED_OPT", "1") != "0" and not self.collectives
+                          and not self.pipeline and not self.fuse_w3)
         self._fc_update_pending = False
         self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline) else None
         if compression == "bf16" and self.collectives:
@@ -226,6 +234,20 @@ class FusedMNISTTrainer:
         o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        if self.fused_opt:
+            b1, b2 = self.betas
+            o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
+                        self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
+            o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)  # last reader of W3
+            w3 = slice(W3_START, FLAT_NUMEL)
+            o.conv2_bwd_adam(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows,
+                             st, self.idx1, self.slab, self.cpart, self.params[w3], self.grads[w3], self.m[w3],
+                             self.v[w3], self.shadow[w3], self.lr, b1, b2, self.eps, 1.0, self.rule)
+            o.conv2_wgrad_reduce_adam(self.slab, self.cpart, self.B, self.gview("conv_layer2/conv2d/kernel"),
+                                      self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"),
+                                      self.gview("conv_layer2/conv2d/bias"), self.grads, self.params, self.m, self.v,
+                                      self.shadow, st, FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
+            return
         if self.fuse_w3:
             # W3 is updated in place by the dW3 tiles: its last reader (fc1_dgrad) goes first
             o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
@@ -502,7 +524,8 @@ class FusedMNISTTrainer:
             bp = float(variables["beta1_power"])
             if 0 < bp < 1:
                 t = round(math.log(bp) / math.log(self.betas[0])) - 1
-        self.state.copy_(torch.tensor([self.global_step, t, 0, 0], dtype=torch.int64))
+        self.state.zero_()
+        self.state[:2].copy_(torch.tensor([self.global_step, t], dtype=torch.int64))
         self._refresh_shadow()
 
     def broadcast(self, root_rank: int = 0):

@@ -464,3 +464,62 @@ def test_fused_w3_adam_matches_separate_optimizer(ops, monkeypatch):
     assert a[5:] == b[5:] == (5, 5)
     for x0, x1, name in zip(a[:5], b[:5], ("params", "m", "v", "shadow", "grads")):
         assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
+
+
+def test_fused_optimizer_tail_matches_separate_adam(ops, monkeypatch):
+    """MIHVD_FUSED_OPT=1 (default at size 1): dense/kernel's Adam streams in conv2_bwd's tail and
+    conv2_wgrad_reduce applies Adam to the other parameters; every element runs the same adam1()
+    on the same gradient as the flat adam_step, so the two schedules agree bit for bit."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    g = torch.Generator(device="cuda").manual_seed(31)
+    X = torch.rand(700, 784, device="cuda", generator=g)
+    Y = torch.randint(0, 10, (700,), device="cuda", generator=g)
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("MIHVD_FUSED_OPT", fused)
+        tr = FusedMNISTTrainer(batch_size=100, seed=5, device="cuda")
+        assert tr.fused_opt == (fused == "1")
+        tr.set_device_dataset(X, Y, shuffle=False)
+        tr.build_graph(steps_per_replay=5, warmup=2)
+        tr.run_graph()
+        tr.run_graph()
+        torch.cuda.synchronize()
+        out.append((tr.params.clone(), tr.m.clone(), tr.v.clone(), tr.shadow.clone(), tr.last_loss(),
+                    [int(v) for v in tr.state.tolist()]))
+    a, b = out
+    assert a[5][:2] == b[5][:2] == [12, 12] and not any(b[5][32::16])   # tail counters re-armed
+    assert a[4] == b[4]
+    for x0, x1, name in zip(a[:4], b[:4], ("params", "m", "v", "shadow")):
+        assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("B", [8, 100])
+def test_conv2_bwd_adam_tail_covers_slice(ops, B):
+    """The tail's chunk counter hands out every float4 of the slice exactly once (any B, any grid),
+    including a slice length that is not a multiple of the 1024-element chunk."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    tr = FusedMNISTTrainer(batch_size=B, seed=2, device="cuda", dropout=0.0)
+    x = torch.rand(B, 784, device="cuda")
+    y = torch.randint(0, 10, (B,), device="cuda")
+    tr.train_step(x, y)
+    torch.cuda.synchronize()
+    n = 1024 * 37 + 12
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    p = torch.randn(n, device="cuda", generator=gen)
+    gr = torch.randn(n, device="cuda", generator=gen)
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    st = tr.state.clone()
+    st[32::16] = 0
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    ops.adam_step(pr, gr, mr, vr, None, st, 0, 1e-3, 0.9, 0.999, 1e-8, 1.0, 0, 0)
+    ops.conv2_bwd_adam(tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", tr.shadow), tr.x_buf, None, st,
+                       tr.idx1, tr.slab, tr.cpart, p, gr, m, v, sh, 1e-3, 0.9, 0.999, 1e-8, 1.0, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(p, pr) and torch.equal(m, mr) and torch.equal(v, vr)
+    assert torch.equal(sh, p.to(torch.bfloat16))
+    nchunks = (n // 4 + 2047) // 2048
+    assert int(st[32::16].sum()) >= nchunks  # every chunk taken (plus the failed grabs)
