@@ -191,16 +191,14 @@ inline int debug_phase_exit() {
 // Step-state words kept on the device so a whole training step replays from a HIP graph:
 //   state[0] = forward step index (read by data/dropout kernels, bumped by the optimizer)
 //   state[1] = optimizer step t   (bumped by the head kernel, read by the optimizer)
-//   state[ST_TAILQ + 16 q], q = 0..7: work counters of the Adam tail in conv2_bwd (one per XCD,
-//   128 B apart; re-armed by the optimizer kernel). Tail-capable state tensors hold ST_TAIL_WORDS.
-enum { ST_FWD = 0, ST_OPT = 1, ST_WORDS = 4, ST_TAILQ = 32, ST_TAIL_WORDS = ST_TAILQ + 16 * 8 };
+enum { ST_FWD = 0, ST_OPT = 1, ST_WORDS = 4 };
 
-// A memory-streaming Adam update appended to a compute-bound launch: after their own work, blocks
-// take chunks of 512 x 4 float4 of the flat range [0, 4*n4) until none are left, so the update
-// fills the gaps between (and after) the compute blocks instead of running as a separate kernel.
-// Chunks are handed out by eight counters, one per XCD (block b starts on queue b & 7 — the XCD
-// the dispatcher placed it on — and steals from the others when its queue is empty), one atomic
-// per block and chunk: a single counter for every wave serialises ~5000 device-scope atomics.
+// A memory-streaming Adam update appended to a compute-bound launch (conv2_bwd): after its own
+// work every wave of the launch updates the float4 groups w, w + W, w + 2W, ... (256 per group,
+// W = waves in the launch) of the flat range [0, 4*n4). Blocks without compute work (on the CUs
+// the compute roles leave idle) start at once. Measured on MI355X, the static interleave beats
+// work stealing through device-scope atomic counters (per-XCD, one atomic per block and chunk):
+// 78.4 vs 79.6 us per step, with no counters to re-arm.
 struct AdamTail {
   float* p;
   const float* g;
@@ -208,60 +206,36 @@ struct AdamTail {
   float* v;
   u16* shadow;
   int64_t n4;
-  int64_t* state;  // ST_OPT read, ST_TAILQ.. are the chunk counters
+  const int64_t* state;  // ST_OPT: the optimizer step t
   float lr, b1, b2, eps, gscale;
   int rule;
 };
 
-__device__ __forceinline__ int64_t adam_tail_grab(const AdamTail& at, int& q, int& tried, int64_t per_q,
-                                                  int64_t nchunks) {
-  while (tried < 8) {
-    unsigned long long* ctr = reinterpret_cast<unsigned long long*>(at.state + ST_TAILQ + 16 * q);
-    const int64_t i = (int64_t)atomicAdd(ctr, 1ull);
-    if (i < per_q && q * per_q + i < nchunks) return q * per_q + i;
-    q = (q + 1) & 7;
-    ++tried;
-  }
-  return -1;
-}
-
 __device__ __forceinline__ void adam_tail_run(const AdamTail& at) {
-  __shared__ int64_t tail_next[2];
-  constexpr int CH = 512 * 4;  // float4 per chunk (a 512-thread block, 4 float4 per lane)
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63;
+  const int waves = (int)blockDim.x >> 6;
   const AdamCoef c = adam_coef((float)at.state[ST_OPT], at.lr, at.b1, at.b2, at.eps, at.gscale, at.rule);
-  const int64_t nchunks = (at.n4 + CH - 1) / CH;
-  const int64_t per_q = (nchunks + 7) / 8;
-  int q = blockIdx.x & 7, tried = 0, buf = 0;  // q/tried: thread 0's grab state
-  __syncthreads();  // every thread is done with the block's own work (LDS reuse below is static)
-  if (t == 0) tail_next[0] = adam_tail_grab(at, q, tried, per_q, nchunks);
-  __syncthreads();
-  for (;;) {
-    const int64_t chunk = tail_next[buf];
-    if (chunk < 0) break;
+  const int64_t nw = (int64_t)gridDim.x * waves, n256 = (at.n4 + 255) / 256;
+  for (int64_t w = (int64_t)blockIdx.x * waves + (t >> 6); w < n256; w += nw) {
     float4 pp[4], gg[4], mm[4], vv[4];
     int64_t idx[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      idx[k] = min(chunk * CH + k * 512 + t, at.n4 - 1);
+      idx[k] = min(w * 256 + k * 64 + lane, at.n4 - 1);
       pp[k] = reinterpret_cast<const float4*>(at.p)[idx[k]];
       gg[k] = reinterpret_cast<const float4*>(at.g)[idx[k]];
       mm[k] = reinterpret_cast<const float4*>(at.m)[idx[k]];
       vv[k] = reinterpret_cast<const float4*>(at.v)[idx[k]];
     }
-    // the next chunk's atomic is in flight together with this chunk's loads
-    if (t == 0) tail_next[buf ^ 1] = adam_tail_grab(at, q, tried, per_q, nchunks);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (chunk * CH + k * 512 + t >= at.n4) continue;
+      if (w * 256 + k * 64 + lane >= at.n4) continue;
       const uint2 sh = adam4(pp[k], mm[k], vv[k], gg[k], c);
       reinterpret_cast<float4*>(at.p)[idx[k]] = pp[k];
       reinterpret_cast<float4*>(at.m)[idx[k]] = mm[k];
       reinterpret_cast<float4*>(at.v)[idx[k]] = vv[k];
       reinterpret_cast<uint2*>(at.shadow)[idx[k]] = sh;
     }
-    __syncthreads();  // tail_next[buf ^ 1] is visible; tail_next[buf] has been read by all
-    buf ^= 1;
   }
 }
 

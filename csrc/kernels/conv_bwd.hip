@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
 // (whose update rode on conv2_bwd's tail): each reduced conv gradient is applied to its slot of the
 // flat p/m/v/shadow buffers right away, blocks [214, 214 + n_fc) update the fc slice
 // [fc_lo4, fc_hi4) (float4 indices: dense/bias, dense_1/*) from the gradient buffer, and block 0
-// advances the forward step and re-arms the tail counter — the step's last launch.
+// advances the forward step — the step's last launch.
 constexpr int CR_SLAB_BLOCKS = 200, CR_PART_BLOCKS = CP_W / 64;
 struct ReduceAdam {
   AdamArgs ad;             // p/m/v/shadow = flat buffer bases; state = the step state (read + written)
@@ -507,11 +507,7 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
   AdamCoef c;
   if constexpr (ADAM) {
     c = adam_coef((float)ra.ad.state[ST_OPT], ra.ad.lr, ra.ad.b1, ra.ad.b2, ra.ad.eps, ra.ad.gscale, ra.ad.rule);
-    if (blockIdx.x == 0 && t < 8) {
-      int64_t* st = const_cast<int64_t*>(ra.ad.state);
-      if (t == 0) st[ST_FWD] += 1;
-      st[ST_TAILQ + 16 * t] = 0;  // re-arm the Adam-tail counters of the next conv2_bwd
-    }
+    if (blockIdx.x == 0 && t == 0) const_cast<int64_t*>(ra.ad.state)[ST_FWD] += 1;
     if ((int)blockIdx.x >= CR_SLAB_BLOCKS + CR_PART_BLOCKS) {
       for (int64_t i = ra.fc_lo4 + ((int64_t)blockIdx.x - CR_SLAB_BLOCKS - CR_PART_BLOCKS) * 256 + t; i < ra.fc_hi4;
            i += (int64_t)(gridDim.x - CR_SLAB_BLOCKS - CR_PART_BLOCKS) * 256) {
@@ -628,9 +624,9 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
   }();
   (void)attr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  const int role = debug_role_only();  // 0: dgrad blocks only, 1: wgrad blocks only
+  const int role = debug_role_only();  // 0: dgrad blocks only, 1: wgrad blocks only, 2: no conv blocks
   const int n_dgrad = role == 1 ? 0 : B;
-  const int n_conv = role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
+  const int n_conv = role == 2 ? 0 : role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
   if (tail == nullptr) {
     conv2_bwd_kernel<false><<<n_conv, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
@@ -661,8 +657,7 @@ static void check_flat(const at::Tensor& t, at::ScalarType dt, int64_t n, const 
 }
 
 // conv2_bwd + the Adam update of a flat slice (p3/g3/m3/v3/shadow3: the dense/kernel segment) in
-// the launch's tail. The tail counters state[ST_TAILQ..] must be 0 on entry
-// (conv2_wgrad_reduce_adam re-arms them).
+// the launch's tail (AdamTail, common.h).
 void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                     const at::Tensor& x, const c10::optional<at::Tensor>& rows, at::Tensor& state, const at::Tensor& idx1,
                     at::Tensor& slab, at::Tensor& cpart, at::Tensor& p3, const at::Tensor& g3, at::Tensor& m3,
@@ -675,8 +670,7 @@ void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tens
   check_flat(m3, at::kFloat, n, "conv2_bwd_adam: m3");
   check_flat(v3, at::kFloat, n, "conv2_bwd_adam: v3");
   check_flat(shadow3, at::kBFloat16, n, "conv2_bwd_adam: shadow3");
-  TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_TAIL_WORDS,
-              "conv2_bwd_adam: state must hold ST_TAIL_WORDS (160) int64 words");
+  TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_WORDS, "conv2_bwd_adam: state");
   AdamTail at{p3.data_ptr<float>(), g3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(),
               (u16*)shadow3.data_ptr(), n / 4, state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2,
               (float)eps, (float)grad_scale, (int)rule};
@@ -700,8 +694,8 @@ void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t
 
 // conv2_wgrad_reduce + Adam for every parameter outside [w3_lo, end) of the flat buffers: the conv
 // gradients straight from the reduction, [fc_lo, w3_lo) from the gradient buffer. gW2/gW1/gb1/gb2
-// must be views of `grads` (their offsets locate the parameters). Advances state[ST_FWD] and
-// re-arms the Adam-tail counters: the last launch of a world-size-1 step.
+// must be views of `grads` (their offsets locate the parameters). Advances state[ST_FWD]: the
+// last launch of a world-size-1 step.
 void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2,
                              at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads, at::Tensor& p,
                              at::Tensor& m, at::Tensor& v, at::Tensor& shadow, at::Tensor& state, int64_t fc_lo,
@@ -717,8 +711,7 @@ void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, in
   check_flat(m, at::kFloat, n, "conv2_wgrad_reduce_adam: m");
   check_flat(v, at::kFloat, n, "conv2_wgrad_reduce_adam: v");
   check_flat(shadow, at::kBFloat16, n, "conv2_wgrad_reduce_adam: shadow");
-  TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_TAIL_WORDS,
-              "conv2_wgrad_reduce_adam: state must hold ST_TAIL_WORDS (160) int64 words");
+  TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_WORDS, "conv2_wgrad_reduce_adam: state");
   TORCH_CHECK(fc_lo % 4 == 0 && w3_lo % 4 == 0 && 0 <= fc_lo && fc_lo <= w3_lo && w3_lo <= n,
               "conv2_wgrad_reduce_adam: fc_lo/w3_lo");
   const float* g0 = grads.data_ptr<float>();

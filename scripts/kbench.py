@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--roles", action="store_true", help="also time each block role of multi-role launches")
     ap.add_argument("--phases", action="store_true", help="time conv2_bwd's dgrad role cut after each phase")
-    ap.add_argument("--only", default="", help="comma-separated job names (e.g. 'conv2_bwd[role0]'); skips the step")
+    ap.add_argument("--only", default="", help="';'-separated job names (e.g. 'conv2_bwd[role0]'); skips the step")
     args = ap.parse_args()
     from mihvd.models.fused_mnist import FC_START as FC, W3_START as W3, FusedMNISTTrainer
 
@@ -74,12 +74,12 @@ def main():
     }
     jobs = [(name, fn, None) for name, fn in ops.items()]
     if args.roles:  # MIHVD_ROLE_ONLY is read by the host wrappers at launch (i.e. capture) time
-        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2)):
+        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv2_bwd_adam+reduce_adam", 3)):
             jobs += [(f"{name}[role{r}]", ops[name], r) for r in range(n_roles)]
     if args.phases:  # MIHVD_DEBUG_EXIT: conv2_bwd dgrad role cut after phase p (1 staging, 2 GEMM, 3 epilogue)
         jobs += [(f"conv2_bwd[role0,exit{p}]", ops["conv2_bwd"], (0, p)) for p in (1, 2, 3)]
     if args.only:
-        keep = set(args.only.split(","))
+        keep = set(args.only.split(";"))
         jobs = [j for j in jobs if j[0] in keep]
     res = {}
     s = torch.cuda.Stream()
