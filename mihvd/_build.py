@@ -130,6 +130,52 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int | None =
     return KERNELS_SO
 
 
+SANITIZERS = {
+    "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+def _sanitizer_cxx() -> str:
+    # ROCm's clang: its TSan runtime intercepts pthread_cond_clockwait (libstdc++'s
+    # condition_variable::wait_for), which GCC 11's libtsan misses — that produces false
+    # "double lock" reports on every cv wait.
+    for c in (os.environ.get("MIHVD_SANITIZER_CXX"), "/opt/rocm/llvm/bin/clang++", shutil.which("clang++"),
+              shutil.which("g++")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("no C++ compiler for the sanitizer self-test")
+
+
+def build_selftest(kind: str = "asan", force: bool = False) -> str:
+    """Build the host-runtime self-test (csrc/runtime/tests/selftest.cc) under a sanitizer
+    (SURVEY.md §5.2): ``asan`` = AddressSanitizer + UndefinedBehaviorSanitizer, ``tsan`` =
+    ThreadSanitizer. Host code only: GPU sanitizers are not available for gfx950 on this pool."""
+    flags = SANITIZERS[kind]
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cc"))) + [os.path.join(CSRC, "runtime", "tests",
+                                                                                    "selftest.cc")]
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.h")))
+    out_dir = os.path.join(BUILD, "selftest_" + kind)
+    exe = os.path.join(out_dir, "selftest")
+    srcs = [s for s in srcs if not s.endswith("bindings.cc")]  # pybind11 module entry point
+    if not force and not _newer(exe, srcs + hdrs + [__file__]):
+        return exe
+    os.makedirs(out_dir, exist_ok=True)
+    cxx = _sanitizer_cxx()
+    common = ["-std=c++17", "-O1", "-g", "-pthread", "-I" + os.path.join(CSRC, "runtime"), *flags]
+
+    def compile_one(src):
+        obj = os.path.join(out_dir, os.path.basename(src) + ".o")
+        _run([cxx, *common, "-c", src, "-o", obj])
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    _run([cxx, *flags, "-pthread", *objs, "-o", exe + ".tmp"])
+    os.replace(exe + ".tmp", exe)
+    return exe
+
+
 def build_all(force: bool = False, verbose: bool = False):
     r = build_runtime(force=force, verbose=verbose)
     k = build_kernels(force=force, verbose=verbose)
@@ -143,3 +189,6 @@ if __name__ == "__main__":
         print(build_runtime(force=force, verbose=True))
     if "kernels" in what or "all" in what:
         print(build_kernels(force=force, verbose=True))
+    for kind in ("asan", "tsan"):
+        if "selftest-" + kind in what:
+            print(build_selftest(kind, force=force))
