@@ -56,6 +56,7 @@ class Config:
     roctx: bool = False                   # roctx ranges around collectives / steps (rocprofv3 --marker-trace)
     negotiate: bool = False               # route async collectives through the native negotiation engine
     store: str = "native"                 # rendezvous: native (mihvdrun's C++ store, if present) | torch
+    debug_sync: bool = False              # serialized bisection mode: sync after every kernel / collective
 
     @staticmethod
     def from_env(env=None) -> "Config":
@@ -82,4 +83,5 @@ class Config:
             roctx=_get("ROCTX", False, bool, env),
             negotiate=_get("NEGOTIATE", False, bool, env),
             store=_get("STORE", "native", str, env),
+            debug_sync=_get("DEBUG_SYNC", False, bool, env),
         )

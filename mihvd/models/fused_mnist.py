@@ -66,6 +66,26 @@ FC_START = SEGMENTS["dense/bias"][0]    # bucket "fc" = [dense/bias .. dense/ker
 W3_START = SEGMENTS["dense/kernel"][0]  # [0, W3_START) = every gradient except dense/kernel
 
 
+class _SyncOps:
+    """torch.ops.mihvd with a synchronize + error check after every launch (MIHVD_DEBUG_SYNC)."""
+
+    def __init__(self, ops):
+        self._ops = ops
+
+    def __getattr__(self, name):
+        fn = getattr(self._ops, name)
+
+        def call(*args, **kw):
+            out = fn(*args, **kw)
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:  # the asynchronous fault, attributed to its kernel
+                raise RuntimeError(f"mihvd kernel {name} failed: {e}") from e
+            return out
+
+        return call
+
+
 class FusedMNISTTrainer:
     def __init__(self, batch_size: int = 100, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  dropout: float = 0.5, seed: int = 0, device=None, compression: str = "none", op=None,
@@ -74,6 +94,12 @@ class FusedMNISTTrainer:
         from .. import basics
 
         self.ops = torch.ops.mihvd
+        # MIHVD_DEBUG_SYNC=1: serialized bisection mode (the HIP_LAUNCH_BLOCKING of this engine):
+        # every kernel is followed by a device synchronize, a failure names the kernel, and steps
+        # run eagerly (build_graph captures nothing).
+        self.debug_sync = os.environ.get("MIHVD_DEBUG_SYNC", "0") == "1"
+        if self.debug_sync:
+            self.ops = _SyncOps(self.ops)
         self.device = torch.device(device) if device is not None else (basics.device() if basics.is_initialized()
                                                                        else torch.device("cuda"))
         if self.device.type != "cuda":
@@ -441,7 +467,7 @@ class FusedMNISTTrainer:
         torch.cuda.synchronize(self.device)
         if primary:
             self.steps_per_replay = steps_per_replay
-        if self.op is not None and int(self.op) == 2:  # Adasum: eager
+        if (self.op is not None and int(self.op) == 2) or self.debug_sync:  # Adasum / serialized: eager
             if primary:
                 self.graph = None
             return False

@@ -39,8 +39,14 @@ class _Handle:
 
 def _register(work, output, post, name) -> int:
     h = next(_next)
+    handle = _Handle(work, output, post, name)
     with _hlock:
-        _handles[h] = _Handle(work, output, post, name)
+        _handles[h] = handle
+    if basics._ctx.config is not None and basics._ctx.config.debug_sync:
+        # serialized bisection mode: every collective completes before the call returns
+        _finish(handle)
+        if basics._ctx.device.type == "cuda":
+            torch.cuda.synchronize()
     return h
 
 

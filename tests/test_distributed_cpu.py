@@ -170,3 +170,9 @@ def test_collective_custom_ops_autograd(tmp_path):
     assert a["bb"] == b["bb"] == [0.0, 0.0]
     assert a["bgrad"] == [3.0, 3.0] and b["bgrad"] == [0.0, 0.0]
     assert a["t"] == [3.0] * 4
+
+
+def test_collectives_debug_sync_mode(tmp_path):
+    """MIHVD_DEBUG_SYNC=1: every collective completes inside the call (bisection mode)."""
+    _, (a, b) = run_scenario(tmp_path, "collectives", env={"MIHVD_DEBUG_SYNC": "1"})
+    assert a["sum"] == b["sum"] and a["async"] == [1.0] * 4

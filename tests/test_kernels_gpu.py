@@ -520,3 +520,23 @@ def test_conv2_bwd_adam_tail_covers_slice(ops, B):
     torch.cuda.synchronize()
     assert torch.equal(p, pr) and torch.equal(m, mr) and torch.equal(v, vr)
     assert torch.equal(sh, p.to(torch.bfloat16))
+
+
+def test_debug_sync_mode_matches_graph(ops, monkeypatch):
+    """MIHVD_DEBUG_SYNC=1 (serialized bisection mode): eager steps with a synchronize after every
+    kernel; same results as the graph-replayed step."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    g = torch.Generator(device="cuda").manual_seed(41)
+    X = torch.rand(300, 784, device="cuda", generator=g)
+    Y = torch.randint(0, 10, (300,), device="cuda", generator=g)
+    out = []
+    for dbg in ("0", "1"):
+        monkeypatch.setenv("MIHVD_DEBUG_SYNC", dbg)
+        tr = FusedMNISTTrainer(batch_size=100, seed=6, device="cuda")
+        tr.set_device_dataset(X, Y, shuffle=False)
+        assert tr.build_graph(steps_per_replay=3, warmup=1) == (dbg == "0")
+        tr.run_graph()
+        torch.cuda.synchronize()
+        out.append(tr.params.clone())
+    assert torch.equal(out[0], out[1])
