@@ -97,7 +97,8 @@ def make_fused_step(args, hvd, device):
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
     tr = FusedMNISTTrainer(batch_size=args.batch_size, lr=args.lr * hvd.size(), seed=42, device=device,
-                           compression=args.compression)
+                           compression=args.compression,
+                           shard_optimizer=os.environ.get("MIHVD_SHARD_W3", "1") != "0")
     tr.broadcast(0)
     X, Y = synthetic_pool(args.pool_batches, args.batch_size, device, seed=hvd.rank())
     tr.set_device_dataset(X, Y)
@@ -162,6 +163,11 @@ def main():
         comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
     elif n == 1:
         comm_desc = "none (1 GPU)"
+    elif getattr(tr, "shard_w3", False):
+        comm_desc = ("RCCL all-gather of the bf16 fc1 factors (a2, dz) -> each rank computes the exact dW3 "
+                     "(all samples) for its 1/N of dense/kernel's rows and applies Adam to them; RCCL all-gather "
+                     "of the updated bf16 rows (overlapping the next step's convolutions); RCCL allreduce of the "
+                     "other fp32 gradients; every step, in the HIP graph")
     elif getattr(tr, "gather", False):
         comm_desc = ("RCCL all-gather of the bf16 fc1 factors (a2, dz) -> exact dW3 over all samples; RCCL "
                      "allreduce of the other fp32 gradients; every step, in the HIP graph")

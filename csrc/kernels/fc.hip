@@ -265,14 +265,16 @@ template <bool ADAM>
 __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
     const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
-    float* __restrict__ gW4, float* __restrict__ gb4, int B, int role_base, int n_small, AdamArgs ad, int write_grad) {
+    float* __restrict__ gW4, float* __restrict__ gb4, int B, int tile_base, int n_small, AdamArgs ad, int write_grad) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
   // The small-reduction blocks (n_small = 33, or 0 when they are not launched) come first in
   // dispatch order so they run alongside the dW3 tiles instead of trailing them.
-  int bid = blockIdx.x + role_base;
-  bid = bid < n_small ? FB_WGRAD + bid : bid - n_small;
+  // dW3 tiles launched: [tile_base, tile_base + gridDim.x - n_small) (a row-slice of dW3 when the
+  // optimizer of dense/kernel is sharded across ranks).
+  int bid = blockIdx.x;
+  bid = bid < n_small ? FB_WGRAD + bid : tile_base + (bid - n_small);
   if (bid < FB_WGRAD) {
     // dW3^T[n][j] tile = sum_k dzw[k][n] a2w[k][j] over Kw rows (the local batch, or the batch of
     // every rank when the factors were all-gathered) -> stored as gW3[j][n..n+3] (float4 per lane).
@@ -504,7 +506,7 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
 static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
                              at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
                              const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3,
-                             const AdamArgs* ad, bool write_grad) {
+                             const AdamArgs* ad, bool write_grad, int64_t jt_lo = 0, int64_t jt_hi = FC1_K / 64) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_wgrad: batch");
   TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
@@ -530,26 +532,28 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   int role = debug_role_only();  // kbench: 0 = dW3 tiles only, 1 = small reductions only
   if (role == 0) roles &= 1;
   if (role == 1) roles &= 2;
+  TORCH_CHECK(0 <= jt_lo && jt_lo <= jt_hi && jt_hi <= FC1_K / 64, "fc1_wgrad: dW3 row-tile range must lie in [0, 49]");
   const int n_small = (roles & 2) ? FB_TOTAL - FB_WGRAD : 0;
-  const int grid = n_small + ((roles & 1) ? FB_WGRAD : 0);
+  const int tile_base = (int)jt_lo * (FC1_N / 64);
+  const int grid = n_small + ((roles & 1) ? (int)(jt_hi - jt_lo) * (FC1_N / 64) : 0);
   if (grid == 0) return;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const u16 *pdz = (const u16*)dz.data_ptr(), *pa2 = (const u16*)a2.data_ptr(), *ph = (const u16*)h.data_ptr();
   if (ad != nullptr) {
     fc1_wgrad_kernel<true><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, 0, n_small, *ad, write_grad ? 1 : 0);
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0);
   } else {
     fc1_wgrad_kernel<false><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, 0, n_small, AdamArgs{}, 1);
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, AdamArgs{}, 1);
   }
 }
 
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
-               const c10::optional<at::Tensor>& a2_w3) {
-  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, nullptr, true);
+               const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi) {
+  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, nullptr, true, jt_lo, jt_hi);
 }
 
 // fc1_wgrad with the Adam update of dense/kernel fused into the dW3 tiles (see the kernel). p3, m3,

@@ -14,7 +14,7 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
-               const c10::optional<at::Tensor>& a2_w3);
+               const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi);
 void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
                     at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
                     const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3, at::Tensor& p3,
@@ -69,8 +69,9 @@ void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tens
   mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats);
 }
 void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, Tensor gW3, Tensor gb3,
-                  Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3) {
-  mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3);
+                  Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3, int64_t jt_lo,
+                  int64_t jt_hi) {
+  mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, jt_lo, jt_hi);
 }
 void fc1_wgrad_adam_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, Tensor gW3, Tensor gb3,
                        Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3, Tensor p3, Tensor m3,
@@ -130,7 +131,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
   m.def("fc1_wgrad(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
-        "Tensor(d!) gb4, int roles=3, Tensor? dz_w3=None, Tensor? a2_w3=None) -> ()");
+        "Tensor(d!) gb4, int roles=3, Tensor? dz_w3=None, Tensor? a2_w3=None, int jt_lo=0, int jt_hi=49) -> ()");
   m.def("fc1_wgrad_adam(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
         "Tensor(d!) gb4, int roles, Tensor? dz_w3, Tensor? a2_w3, Tensor(e!) p3, Tensor(f!) m3, Tensor(g!) v3, "
         "Tensor(h!) shadow3, Tensor state, float lr, float b1, float b2, float eps, float grad_scale, int rule, "

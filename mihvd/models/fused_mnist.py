@@ -89,7 +89,8 @@ class _SyncOps:
 class FusedMNISTTrainer:
     def __init__(self, batch_size: int = 100, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  dropout: float = 0.5, seed: int = 0, device=None, compression: str = "none", op=None,
-                 adam_rule: str = "tf", dropout_seed: int | None = None, world_size: int | None = None):
+                 adam_rule: str = "tf", dropout_seed: int | None = None, world_size: int | None = None,
+                 shard_optimizer: bool | None = None):
         _native.require_kernels()
         from .. import basics
 
@@ -130,6 +131,7 @@ class FusedMNISTTrainer:
         self.v = torch.zeros(FLAT_NUMEL, **f32)
         self.shadow = torch.zeros(FLAT_NUMEL, device=dev, dtype=torch.bfloat16)
         self.state = torch.zeros(4, device=dev, dtype=torch.int64)  # [fwd step, opt step t, -, -]
+        self.shard_w3 = False
         ref = MNISTConvNet(impl="torch", seed=seed)
         self.load_model_weights(ref)
         B = self.B
@@ -153,6 +155,25 @@ class FusedMNISTTrainer:
         else:
             self.a2 = torch.empty(B, 3136, **bf)
             self.dz = torch.empty(B, 1024, **bf)
+        # Sharded dense/kernel optimizer (factor-gather plane only; shard_optimizer=True or
+        # MIHVD_SHARD_W3=1): rank r owns W3 row tiles [r*T, (r+1)*T) of the 49 64-row tiles
+        # (T = ceil(49/size)). It computes dW3 for those rows only (over every rank's samples, so the
+        # result is the exact allreduced sum), applies Adam to them, and all-gathers the updated bf16
+        # rows into a padded shadow [size*T*64][1024] on the side stream — overlapping the next
+        # step's convolutions — instead of every rank computing all of dW3 and updating all of W3.
+        # fp32 master rows / Adam slots of other ranks' rows are not maintained here; call
+        # gather_full_state() on every rank before variables()/to_model().
+        if shard_optimizer is None:
+            shard_optimizer = os.environ.get("MIHVD_SHARD_W3", "0") == "1"
+        self.shard_w3 = bool(shard_optimizer) and self.gather and not self.fuse_w3_requested()
+        self._shadow_ev = None
+        self._full_state_valid = True
+        if self.shard_w3:
+            self._T = -(-49 // self.world)
+            lo, hi = self.rank * self._T, min((self.rank + 1) * self._T, 49)
+            self._w3_tiles = (lo, max(lo, hi))
+            self.shadow3 = torch.zeros(self.world * self._T * 64, 1024, **bf)
+            self._refresh_shadow()
         self.idx2 = torch.empty(B, 3136, **u8)
         self.zpart = torch.empty(14, B, 1024, **f32)
         self.h = torch.empty(B, 1024, **bf)
@@ -199,6 +220,16 @@ class FusedMNISTTrainer:
             self.wire = None
 
     # ----------------------------------------------------------------------------- views
+    @staticmethod
+    def fuse_w3_requested() -> bool:
+        return os.environ.get("MIHVD_FUSE_W3_ADAM", "0") == "1"
+
+    def w3_shadow(self) -> torch.Tensor:
+        """The bf16 dense/kernel the MFMA kernels read ([3136][1024], contiguous)."""
+        if self.shard_w3:
+            return self.shadow3[:3136]
+        return self.pview("dense/kernel", self.shadow)
+
     def pview(self, name, buf=None):
         off, n = SEGMENTS[name]
         return (self.params if buf is None else buf)[off:off + n].view(TF_PARAM_SHAPES[name])
@@ -214,8 +245,16 @@ class FusedMNISTTrainer:
 
     def _refresh_shadow(self):
         self.ops.scale_cast_bf16(self.params, self.shadow, 1.0)
+        if self.shard_w3:
+            self.shadow3[:3136].copy_(self.pview("dense/kernel", self.shadow))
+
+    def _require_full_state(self):
+        if not self._full_state_valid:
+            raise RuntimeError("the dense/kernel optimizer is sharded across ranks: call gather_full_state() on "
+                               "every rank first")
 
     def to_model(self, model: MNISTConvNet | None = None) -> MNISTConvNet:
+        self._require_full_state()
         model = model or MNISTConvNet(impl="torch").to(self.device)
         with torch.no_grad():
             for name, p in model.ordered_parameters():
@@ -342,7 +381,11 @@ class FusedMNISTTrainer:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self._all_gather_rows(self.a2_all, self.a2)
-        o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
+        if self._shadow_ev is not None:
+            # the previous step's W3 row gather (side stream) must land before the first reader
+            main.wait_event(self._shadow_ev)
+            self._shadow_ev = None
+        o.fc1_fwd(self.a2, self.w3_shadow(), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         side.wait_stream(main)
@@ -352,13 +395,35 @@ class FusedMNISTTrainer:
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
                  self.gview("dense_1/bias"))
         o.fc1_wgrad(*small, 2)  # db3, dW4, db4 of the local batch
-        o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
+        o.fc1_dgrad(self.dz, self.w3_shadow(), self.a2, self.g2)
         self._conv_backward(x, rows, st)
         main.wait_stream(side)   # both gathers done: the communicator is free
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self._allreduce(self.grads[:W3_START], 0, W3_START)
         b1, b2 = self.betas
+        if self.shard_w3:
+            ar_done = torch.cuda.Event()
+            ar_done.record(side)
+            lo, hi = self._w3_tiles
+            if hi > lo:
+                # dW3 rows of this rank's tiles over every rank's samples, then Adam on those rows
+                o.fc1_wgrad(*small, 1, self.dz_all, self.a2_all, lo, hi)
+                a, b = W3_START + lo * 64 * 1024, W3_START + hi * 64 * 1024
+                o.adam_step(self.params[a:b], self.grads[a:b], self.m[a:b], self.v[a:b],
+                            self.shadow3[lo * 64:hi * 64].view(-1), st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world,
+                            self.rule, 0)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                T64 = self._T * 64
+                self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
+                self._shadow_ev = torch.cuda.Event()
+                self._shadow_ev.record(side)
+            main.wait_event(ar_done)
+            o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START],
+                        self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+            self._full_state_valid = False
+            return
         if self.fuse_w3:
             # dW3 summed over every rank's samples, Adam applied to W3 in the same tiles
             self._fc1_wgrad_w3_adam(1, self.dz_all, self.a2_all)
@@ -400,6 +465,26 @@ class FusedMNISTTrainer:
         if self._fc_update_pending:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             self._fc_update_pending = False
+        if self._shadow_ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._shadow_ev)
+            self._shadow_ev = None
+
+    def gather_full_state(self):
+        """Sharded optimizer: collect every rank's dense/kernel rows of the fp32 weights and Adam
+        slots, so variables()/to_model() see the complete state. Collective: call on every rank."""
+        if not self.shard_w3 or self._full_state_valid:
+            return
+        self._join()
+        T64 = self._T * 64
+        lo, hi = self._w3_tiles
+        for buf in (self.params, self.m, self.v):
+            w3 = buf[W3_START:].view(3136, 1024)
+            tmp = torch.zeros(self.world * T64, 1024, device=self.device, dtype=torch.float32)
+            mine = tmp[self.rank * T64:(self.rank + 1) * T64]
+            mine[:(hi - lo) * 64].copy_(w3[lo * 64:hi * 64])
+            self._all_gather_rows(tmp, mine)
+            w3.copy_(tmp[:3136])
+        self._full_state_valid = True
 
     def _allreduce(self, bucket, lo, hi):
         import torch.distributed as dist
@@ -523,6 +608,7 @@ class FusedMNISTTrainer:
 
     def variables(self) -> dict[str, torch.Tensor]:
         """TF1 global variables (names of tensorflow_mnist.py's graph) for the checkpoint layout."""
+        self._require_full_state()
         self.sync()
         out = {}
         for name in TF_PARAM_ORDER:
@@ -551,6 +637,7 @@ class FusedMNISTTrainer:
                 t = round(math.log(bp) / math.log(self.betas[0])) - 1
         self.state.copy_(torch.tensor([self.global_step, t, 0, 0], dtype=torch.int64))
         self._refresh_shadow()
+        self._full_state_valid = True
 
     def broadcast(self, root_rank: int = 0):
         """Broadcast weights, Adam slots and counters from ``root_rank`` (BroadcastGlobalVariablesHook)."""
@@ -560,6 +647,7 @@ class FusedMNISTTrainer:
             return
         import torch.distributed as dist
 
+        self.gather_full_state()  # collective; no-op unless the dense/kernel optimizer is sharded
         for buf in (self.params, self.m, self.v, self.state):
             dist.broadcast(buf, src=root_rank)
         from ..parallel.collectives import broadcast_object

@@ -68,6 +68,19 @@ def main():
             tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
             tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
             sh, st, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0)),
+        "fc1_wgrad_adam_k8x": lambda: o.fc1_wgrad_adam(
+            tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
+            tr.gview("dense_1/bias"), 1, dz8, a28, tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], st, 0.0, 0.9,
+            0.999, 1e-8, 1.0, 0, False),
+        # the sharded optimizer at N=8: this rank's 7 of 49 row tiles of dW3 (K = 800), Adam on them
+        "fc1_wgrad_k8x_slice": lambda: o.fc1_wgrad(tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"),
+                                                   tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
+                                                   tr.gview("dense_1/bias"), 1, dz8, a28, 0, 7),
+        "adam_w3_slice8": lambda: o.adam_step(tr.params[W3:W3 + 7 * 65536], tr.grads[W3:W3 + 7 * 65536],
+                                              tr.m[W3:W3 + 7 * 65536], tr.v[W3:W3 + 7 * 65536],
+                                              sh[W3:W3 + 7 * 65536], st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0, 0),
+        "adam_w3": lambda: o.adam_step(tr.params[W3:], tr.grads[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], st, 0, 0.0,
+                                       0.9, 0.999, 1e-8, 1.0, 0, 0),
         "adam": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, sh, st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
         "adam_small": lambda: o.adam_step(tr.params[:W3], tr.grads[:W3], tr.m[:W3], tr.v[:W3], sh[:W3], st, 0, 0.0,
                                           0.9, 0.999, 1e-8, 1.0, 0),

@@ -20,9 +20,12 @@ def _gpu():
         pytest.skip("needs a GPU")
 
 
-def test_rccl_allreduce_inside_hip_graph(tmp_path):
+@pytest.mark.parametrize("shard", ["0", "1"])
+def test_rccl_allreduce_inside_hip_graph(tmp_path, shard):
+    """shard=1: the sharded dense/kernel optimizer, whose bf16 row gather runs on the side stream
+    across step boundaries inside the graph."""
     _gpu()
-    env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl")
+    env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3=shard)
     for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
         env.pop(k, None)
     p = subprocess.run([sys.executable, WORKER, "rccl_graph", str(tmp_path)], env=env, capture_output=True, text=True,
@@ -31,6 +34,7 @@ def test_rccl_allreduce_inside_hip_graph(tmp_path):
     r = json.loads((tmp_path / "rccl_graph.json").read_text())
     assert r["captured"], "RCCL allreduce could not be captured into the HIP graph"
     assert r["steps"] == 22 and r["bitwise"], r
+    assert r["shard"] == (shard == "1")
 
 
 @pytest.mark.parametrize("gather", ["1", "0"])
@@ -46,3 +50,15 @@ def test_fused_data_parallel_equivalence_two_ranks(tmp_path, gather):
         assert o["rank_spread"] == 0.0
         assert o["grad_rel"] < 1e-4, o
         assert o["rel_update_diff"] < 0.05, o
+
+
+def test_sharded_optimizer_matches_unsharded_two_ranks(tmp_path):
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo_shard", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(2):
+        o = json.loads((tmp_path / f"dp_gloo_shard.{r}.json").read_text())
+        assert all(o["same"].values()), o
+        assert o["loss"] == o["loss_ref"]

@@ -4,6 +4,7 @@ usage: python fused_worker.py <scenario> <outdir>
   rccl_graph : world 1 over RCCL with MIHVD_FORCE_COLLECTIVES=1 — the allreduce is captured in the
                HIP graph; results must equal a trainer without collectives.
   dp_gloo    : 2 ranks (gloo, both on cuda:0), B=50 each == one trainer with B=100 (dropout off).
+  dp_gloo_shard : 2 ranks, sharded dense/kernel optimizer == the unsharded factor-gather step.
 """
 import json
 import os
@@ -26,7 +27,8 @@ def data(n, seed=3):
 
 def sc_rccl_graph(outdir):
     X, Y = data(2000)
-    a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda")
+    a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda",
+                          shard_optimizer=os.environ.get("MIHVD_SHARD_W3") == "1")
     assert a.collectives, "MIHVD_FORCE_COLLECTIVES should enable the allreduce path"
     a.set_device_dataset(X, Y, seed=4)
     p0 = a.params.clone()
@@ -42,10 +44,12 @@ def sc_rccl_graph(outdir):
     torch.cuda.synchronize()
     # the step has no atomics: with a world of one, the collective data plane (factor gather + RCCL
     # allreduce, captured in the graph) must reproduce the local step bit for bit
+    a.gather_full_state()
     rel = ((a.params - b.params).norm() / (b.params - p0).norm()).item()
     bitwise = bool(torch.equal(a.params, b.params))
     with open(os.path.join(outdir, "rccl_graph.json"), "w") as f:
-        json.dump({"captured": captured, "bitwise": bitwise, "rel_update_diff": rel, "steps": a.global_step, "loss": a.last_loss(),
+        json.dump({"captured": captured, "bitwise": bitwise, "rel_update_diff": rel, "steps": a.global_step,
+                   "shard": a.shard_w3, "loss": a.last_loss(),
                    "loss_ref": b.last_loss()}, f)
 
 
@@ -75,6 +79,28 @@ def sc_dp_gloo(outdir):
     with open(os.path.join(outdir, f"dp_gloo.{r}.json"), "w") as f:
         json.dump({"gather": tr.gather, "grad_rel": grel, "rel_update_diff": rel, "max": mx,
                    "rank_spread": (spread - spread[0]).abs().max().item()}, f)
+
+
+def sc_dp_gloo_shard(outdir):
+    """Sharded dense/kernel optimizer == unsharded factor-gather step, bit for bit (2 ranks)."""
+    r = hvd.rank()
+    X, Y = data(600)
+    trs = [FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", shard_optimizer=sh)
+           for sh in (False, True)]
+    for tr in trs:
+        tr.broadcast(0)
+    assert not trs[0].shard_w3 and trs[1].shard_w3
+    for step in range(3):
+        xb = X[step * 100:(step + 1) * 100]
+        yb = Y[step * 100:(step + 1) * 100]
+        for tr in trs:
+            tr.train_step(xb[r * 50:(r + 1) * 50], yb[r * 50:(r + 1) * 50])
+    torch.cuda.synchronize()
+    trs[1].gather_full_state()
+    same = {name: bool(torch.equal(getattr(trs[0], name), getattr(trs[1], name))) for name in ("params", "m", "v")}
+    same["shadow_w3"] = bool(torch.equal(trs[0].w3_shadow(), trs[1].w3_shadow()))
+    with open(os.path.join(outdir, f"dp_gloo_shard.{r}.json"), "w") as f:
+        json.dump({"same": same, "loss": trs[1].last_loss(), "loss_ref": trs[0].last_loss()}, f)
 
 
 def main():
