@@ -63,6 +63,7 @@ class _Context:
         self.store = None          # NativeStore (C++ TCP store) when launched by mihvdrun
         self.store_server = None   # StoreServer this process hosts (negotiation without mihvdrun)
         self.engine = None         # negotiated-collective Engine (MIHVD_NEGOTIATE=1)
+        self.elastic_gen = None    # elastic: membership generation of the current world (kept across re-inits)
         self.lock = threading.RLock()
 
 
@@ -93,7 +94,26 @@ def init(comm=None, process_sets=None, config: Config | None = None):
         if _ctx.initialized:
             return
         cfg = config or Config.from_env()
-        topo = _env.discover()
+        elastic = os.environ.get("MIHVD_ELASTIC") == "1"
+        # elastic workers take rank/size from the membership below, not from the launch env
+        topo = _env.discover() if not elastic else _env.Topology(
+            0, 1, 0, 1, 0, 1, os.environ.get("MASTER_ADDR", "127.0.0.1"),
+            int(os.environ["MASTER_PORT"]) if os.environ.get("MASTER_PORT") else None, "elastic")
+        native = None
+        if elastic:
+            # mihvd.elastic: rank/size come from the newest membership generation that includes
+            # this worker (published by mihvdrun in its store), not from the launch environment
+            from .elastic import wait_for_membership
+            from .runner.store import NativeStore
+
+            native = NativeStore.from_env(datetime.timedelta(seconds=cfg.timeout_s))
+            if native is None:
+                raise RuntimeError("MIHVD_ELASTIC=1 needs mihvdrun's store (MIHVD_STORE_ADDR)")
+            wid = int(os.environ["MIHVD_WORKER_ID"])
+            prev = -1 if _ctx.elastic_gen is None else _ctx.elastic_gen
+            g, r, n, lr, ls = wait_for_membership(native, wid, prev, cfg.elastic_timeout_s)
+            _ctx.elastic_gen = g
+            topo = _env.Topology(r, n, lr, ls, 0, 1, topo.master_addr, topo.master_port, "elastic")
         backend = _choose_backend(cfg)
         logging.basicConfig(level=getattr(logging, cfg.log_level, logging.INFO),
                             format="[%(asctime)s] [rank " + str(topo.rank) + "] %(message)s")
@@ -101,7 +121,9 @@ def init(comm=None, process_sets=None, config: Config | None = None):
             ndev = torch.cuda.device_count()
             if ndev == 0:
                 raise RuntimeError("backend nccl (RCCL) requested but no GPU is visible")
-            device = torch.device("cuda", topo.local_rank % ndev)
+            # an elastic worker keeps the GPU of its launch slot whatever its current rank
+            dev_index = int(os.environ.get("MIHVD_DEVICE_INDEX", topo.local_rank)) if elastic else topo.local_rank
+            device = torch.device("cuda", dev_index % ndev)
             torch.cuda.set_device(device)
         else:
             device = torch.device("cpu")
@@ -115,10 +137,16 @@ def init(comm=None, process_sets=None, config: Config | None = None):
                                  topo.local_size if topo.source != "single" else dist.get_world_size(),
                                  topo.cross_rank, topo.cross_size, topo.master_addr, topo.master_port, "existing")
             backend = dist.get_backend()
-        elif topo.size == 1 and topo.master_port is None:
+        elif topo.size == 1 and topo.master_port is None and not elastic:
             # Single process without a launcher: an in-memory store, no sockets needed.
             dist.init_process_group(backend, store=dist.HashStore(), rank=0, world_size=1, timeout=timeout,
                                     **({"device_id": device} if backend == "nccl" else {}))
+            _ctx.owns_pg = True
+        elif elastic:
+            kwargs = {"device_id": device} if backend == "nccl" else {}
+            _ctx.store = native
+            dist.init_process_group(backend, store=dist.PrefixStore(f"mihvd/pg/gen{_ctx.elastic_gen}", native),
+                                    rank=topo.rank, world_size=topo.size, timeout=timeout, **kwargs)
             _ctx.owns_pg = True
         else:
             kwargs = {"device_id": device} if backend == "nccl" else {}

@@ -57,6 +57,8 @@ class Config:
     negotiate: bool = False               # route async collectives through the native negotiation engine
     store: str = "native"                 # rendezvous: native (mihvdrun's C++ store, if present) | torch
     debug_sync: bool = False              # serialized bisection mode: sync after every kernel / collective
+    elastic_grace_s: float = 30.0         # elastic: how long a failed collective waits for a new membership
+    elastic_timeout_s: float = 600.0      # elastic: how long a worker waits to be included in a generation
 
     @staticmethod
     def from_env(env=None) -> "Config":
@@ -84,4 +86,6 @@ class Config:
             negotiate=_get("NEGOTIATE", False, bool, env),
             store=_get("STORE", "native", str, env),
             debug_sync=_get("DEBUG_SYNC", False, bool, env),
+            elastic_grace_s=_get("ELASTIC_GRACE_SECONDS", 30.0, float, env),
+            elastic_timeout_s=_get("ELASTIC_TIMEOUT_SECONDS", 600.0, float, env),
         )

@@ -103,7 +103,11 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._synchronized = False
         self._should_sync = True
         self._consistency_checked = not cfg.consistency_check
-        self._check_consistency()
+        if basics._ctx.elastic_gen is None:
+            self._check_consistency()
+        # elastic worlds: a worker joining mid-training constructs its optimizer while the others
+        # are already training, so the (collective) check runs at the first synchronize() after
+        # every re-formed world instead, where all ranks meet
 
     def _plan(self, thresh: int):
         """(Re)build the fusion buckets for ``thresh`` bytes and point every ``param.grad`` at its
@@ -209,6 +213,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             return
         if not self._views_intact():
             self._install_grad_views()
+        if not self._consistency_checked:
+            self._check_consistency()
         with trace_range("mihvd.synchronize"):
             for bid in self._controller.flush():
                 self._launch(bid)
@@ -241,6 +247,16 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             if new is not None and new != self._fusion_threshold:
                 self._plan(new)
         return out
+
+    def _elastic_reset(self):
+        """Forget in-flight bucket allreduces of a step interrupted by a failed or re-formed world
+        (mihvd.elastic): the next backward starts with every bucket un-launched."""
+        if self._controller is not None:
+            for b in self._buckets:
+                b.handle = None
+            self._controller.reset()
+        self._synchronized = False
+        self._consistency_checked = not basics.config().consistency_check
 
     @property
     def fusion_threshold(self) -> int:

@@ -16,7 +16,10 @@ consecutive GPUs. Remote hosts are reached over ssh, as mpirun does inside an MP
 Each rank receives ``RANK WORLD_SIZE LOCAL_RANK LOCAL_WORLD_SIZE GROUP_RANK MASTER_ADDR
 MASTER_PORT`` and the Open MPI equivalents ``OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK,LOCAL_SIZE}``.
 If any rank exits non-zero the others are terminated and that exit code is returned (mpirun
-semantics: one dead rank aborts the job).
+semantics: one dead rank aborts the job) — unless the job is elastic (``--min-np M [--max-np N]
+[--respawn]``, see mihvd/elastic.py): then the launcher publishes a new membership generation
+without the dead worker (or with a replacement) and only aborts below M workers; SIGUSR1 asks it to
+add a worker (up to N).
 """
 from __future__ import annotations
 
@@ -53,6 +56,9 @@ class LaunchSpec:
     ssh_port: int | None = None
     extra_env: dict[str, str] = field(default_factory=dict)
     start_timeout: float = 120.0
+    min_np: int | None = None          # elastic (mihvd.elastic): keep going while >= min_np workers live
+    max_np: int | None = None
+    respawn: bool = False              # elastic: replace a dead worker (same slot) with a new one
     verbose: bool = False
     command: list[str] = field(default_factory=list)
 
@@ -142,6 +148,12 @@ def parse_args(argv: list[str]) -> LaunchSpec:
             spec.start_timeout = float(need(a)); i += 2; continue
         if a in ("--verbose",):
             spec.verbose = True; i += 1; continue
+        if a in ("--min-np", "--min_np"):
+            spec.min_np = int(need(a)); i += 2; continue
+        if a in ("--max-np", "--max_np"):
+            spec.max_np = int(need(a)); i += 2; continue
+        if a in ("--respawn", "--elastic-respawn"):
+            spec.respawn = True; i += 1; continue
         if a in ("--timeline-filename",):
             spec.extra_env["MIHVD_TIMELINE"] = need(a); i += 2; continue
         if a in ("--fusion-threshold-mb",):
@@ -270,17 +282,42 @@ def launch(spec: LaunchSpec) -> int:
             print(f"mihvdrun: ignoring MCA parameter {k}={v} (data plane is RCCL)", file=sys.stderr)
     # The rendezvous server (C++ StoreServer, csrc/runtime/store.cc) lives in the launcher, like
     # horovodrun's: ranks build their process group and the negotiation engine over it.
-    server = None
-    if os.environ.get("MIHVD_STORE", "native") != "torch":
+    elastic = spec.min_np is not None or spec.max_np is not None
+    server = client = None
+    if os.environ.get("MIHVD_STORE", "native") != "torch" or elastic:
         from .store import start_server
 
         server = start_server("127.0.0.1" if all_local else "0.0.0.0", 0)
+    min_np = spec.min_np if spec.min_np is not None else spec.np
+    max_np = spec.max_np if spec.max_np is not None else spec.np
+    if elastic:
+        from .._native import runtime
+        from ..elastic import GEN_KEY, format_members, members_key
+
+        if not 1 <= min_np <= spec.np <= max_np:
+            raise SystemExit(f"mihvdrun: need 1 <= --min-np ({min_np}) <= -np ({spec.np}) <= --max-np ({max_np})")
+        client = runtime().StoreClient("127.0.0.1" if all_local else master_addr, server.port, 30.0)
     procs: list[_Proc] = []
     threads = []
-    for rank, host, lr, ls, node in layout:
+    slots = {}     # worker id -> (host, local_rank, local_size, node)
+    members = []   # current generation: [(worker id, host)] in rank order
+    gen = [-1]
+
+    def publish(new_members):
+        gen[0] += 1
+        client.set(members_key(gen[0]), format_members(new_members))
+        client.set(GEN_KEY, str(gen[0]))
+        if spec.verbose or gen[0] > 0:
+            print(f"mihvdrun: elastic generation {gen[0]}: {len(new_members)} workers "
+                  f"{[w for w, _ in new_members]}", file=sys.stderr, flush=True)
+
+    def spawn(wid, rank, host, lr, ls, node):
         renv = build_rank_env(spec, rank, lr, ls, node, master_addr, master_port)
         if server is not None:
             renv["MIHVD_STORE_ADDR"] = f"{master_addr}:{server.port}"
+        if elastic:
+            renv.update({"MIHVD_ELASTIC": "1", "MIHVD_WORKER_ID": str(wid), "MIHVD_DEVICE_INDEX": str(lr),
+                         "WORLD_SIZE": str(max(len(members), rank + 1)), "OMPI_COMM_WORLD_SIZE": str(max(len(members), rank + 1))})
         if _is_local(host):
             env = dict(os.environ)
             env.update(renv)
@@ -291,13 +328,20 @@ def launch(spec: LaunchSpec) -> int:
             cmd = ["ssh", "-o", "StrictHostKeyChecking=no"] + (["-p", str(spec.ssh_port)] if spec.ssh_port else []) + [host, remote]
             env = dict(os.environ)
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
-        procs.append(_Proc(rank, p))
-        pre_o = f"[1,{rank}]<stdout>:" if spec.tag_output else ""
-        pre_e = f"[1,{rank}]<stderr>:" if spec.tag_output else ""
-        for s, o, pre in ((p.stdout, sys.stdout, pre_o), (p.stderr, sys.stderr, pre_e)):
-            t = threading.Thread(target=_pump, args=(s, o, pre), daemon=True)
+        procs.append(_Proc(wid, p))
+        slots[wid] = (host, lr, ls, node)
+        pre_o = f"[1,{wid}]<stdout>:" if spec.tag_output else ""
+        pre_e = f"[1,{wid}]<stderr>:" if spec.tag_output else ""
+        for st, o, pre in ((p.stdout, sys.stdout, pre_o), (p.stderr, sys.stderr, pre_e)):
+            t = threading.Thread(target=_pump, args=(st, o, pre), daemon=True)
             t.start()
             threads.append(t)
+
+    if elastic:
+        publish([(rank, host) for rank, host, *_ in layout])
+        members = [(rank, host) for rank, host, *_ in layout]
+    for rank, host, lr, ls, node in layout:
+        spawn(rank, rank, host, lr, ls, node)
 
     def terminate_all(sig=signal.SIGTERM):
         for pr in procs:
@@ -310,31 +354,83 @@ def launch(spec: LaunchSpec) -> int:
     def on_signal(signum, frame):
         terminate_all(signal.SIGTERM)
 
+    def abort(code, why):
+        print(f"mihvdrun: {why}; terminating the job", file=sys.stderr, flush=True)
+        terminate_all(signal.SIGTERM)
+        deadline = time.time() + 10
+        while time.time() < deadline and any(p.popen.poll() is None for p in procs):
+            time.sleep(0.05)
+        terminate_all(signal.SIGKILL)
+        return code
+
+    grow = [0]
+
+    def on_grow(signum, frame):  # elastic scale-up request (e.g. from a host-discovery hook)
+        grow[0] += 1
+
     old = {s: signal.signal(s, on_signal) for s in (signal.SIGINT, signal.SIGTERM)}
+    if elastic:
+        old[signal.SIGUSR1] = signal.signal(signal.SIGUSR1, on_grow)
     exit_code = 0
+    succeeded = 0
+    next_wid = spec.np
     try:
         remaining = set(range(len(procs)))
         while remaining:
+            while elastic and grow[0] > 0 and not succeeded and exit_code == 0:
+                grow[0] -= 1
+                if len(members) >= max_np:
+                    print(f"mihvdrun: scale-up ignored: already --max-np {max_np} workers", file=sys.stderr, flush=True)
+                    continue
+                host, lr, ls, node = slots[members[0][0]]
+                lr = len(members) % max(1, ls)
+                new = next_wid
+                next_wid += 1
+                members.append((new, host))
+                publish(members)
+                spawn(new, len(members) - 1, host, lr, ls, node)
+                remaining.add(len(procs) - 1)
             for i in list(remaining):
                 rc = procs[i].popen.poll()
                 if rc is None:
                     continue
                 remaining.discard(i)
-                if rc != 0 and exit_code == 0:
-                    exit_code = rc if rc > 0 else 128 - rc
-                    print(f"mihvdrun: rank {procs[i].rank} exited with code {rc}; terminating the job",
+                wid = procs[i].rank
+                if rc == 0:
+                    succeeded += 1
+                    continue
+                code = rc if rc > 0 else 128 - rc
+                if not elastic or succeeded:
+                    if exit_code == 0:
+                        exit_code = abort(code, f"rank {wid} exited with code {rc}")
+                    continue
+                # elastic: drop the dead worker (optionally replace it) and publish a new generation
+                members = [(w, h) for w, h in members if w != wid]
+                if spec.respawn and len(members) < max_np:
+                    host, lr, ls, node = slots[wid]
+                    new = next_wid
+                    next_wid += 1
+                    members.append((new, host))
+                    publish(members)
+                    spawn(new, len(members) - 1, host, lr, ls, node)
+                    remaining.add(len(procs) - 1)
+                    print(f"mihvdrun: worker {wid} exited with code {rc}; respawned as worker {new}",
                           file=sys.stderr, flush=True)
-                    terminate_all(signal.SIGTERM)
-                    deadline = time.time() + 10
-                    while time.time() < deadline and any(p.popen.poll() is None for p in procs):
-                        time.sleep(0.05)
-                    terminate_all(signal.SIGKILL)
+                elif len(members) >= min_np:
+                    print(f"mihvdrun: worker {wid} exited with code {rc}; continuing with {len(members)} workers "
+                          f"(--min-np {min_np})", file=sys.stderr, flush=True)
+                    publish(members)
+                elif exit_code == 0:
+                    exit_code = abort(code, f"worker {wid} exited with code {rc} and fewer than --min-np {min_np} "
+                                            "workers remain")
             time.sleep(0.02)
     finally:
         for s, h in old.items():
             signal.signal(s, h)
         for t in threads:
             t.join(timeout=5)
+        if client is not None:
+            client.close()
         if server is not None:
             server.stop()
     return exit_code

@@ -14,3 +14,4 @@ from .parallel.collectives import (allgather, allgather_async, allgather_object,
 from .parallel.compression import Compression
 from .parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters
 from .ops import collective_ops as mpi_ops  # noqa: E402,F401  registers torch.ops.mihvd_dist.* (Horovod's mpi_ops)
+from . import elastic  # noqa: E402,F401  hvd.elastic.run / TorchState / ObjectState
