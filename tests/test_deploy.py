@@ -72,3 +72,14 @@ def test_deploy_script_dry_run():
 def test_dockerfile_builds_native_for_gfx950():
     text = open(os.path.join(DEPLOY, "Dockerfile")).read()
     assert "mihvd._build all" in text and "gfx950" in text and "openssh-server" in text
+
+
+def test_elastic_mpijob():
+    (job,) = _load("mpijob-mi355x-elastic.yaml")
+    spec = job["spec"]
+    assert job["apiVersion"] == "kubeflow.org/v2beta1" and spec["slotsPerWorker"] == 8
+    c = spec["mpiReplicaSpecs"]["Launcher"]["template"]["spec"]["containers"][0]
+    ls = L.parse_args([str(a) for a in c["args"]])
+    assert (ls.np, ls.min_np, ls.max_np, ls.respawn) == (16, 8, 16, True)
+    assert ls.command[:2] == ["python", "/examples/tensorflow_mnist_elastic.py"]
+    assert spec["mpiReplicaSpecs"]["Worker"]["replicas"] * 8 >= ls.max_np
