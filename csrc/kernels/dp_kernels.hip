@@ -252,4 +252,34 @@ void update_scale_(at::Tensor& ls, at::Tensor& tracker, double growth, double ba
                                            (float)backoff, (int)interval, (float)min_scale);
 }
 
+// ------------------------------------------------------------------------------------------ //
+// Column-slice gather for the sharded dense/kernel optimizer's all-to-all (fused_mnist.py):
+//   dst[q][r][c] = src[r][col0 + q*C + c]   (0 past the last column K)
+// 8 bf16 (16 B) per thread; K, C and col0 are multiples of 8, so a chunk is all in or all out.
+__global__ void __launch_bounds__(256) gather_cols_kernel(const uint4* __restrict__ src, int K8, int R, int col08,
+                                                          int C8, int Q, uint4* __restrict__ dst) {
+  const int64_t total = (int64_t)Q * R * C8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C8);
+    const int64_t qr = i / C8;
+    const int r = (int)(qr % R), q = (int)(qr / R);
+    const int col = col08 + q * C8 + c;
+    dst[i] = col < K8 ? src[(int64_t)r * K8 + col] : make_uint4(0, 0, 0, 0);
+  }
+}
+
+void gather_cols_bf16(const at::Tensor& src, int64_t col0, at::Tensor& dst) {
+  TORCH_CHECK(src.dtype() == at::kBFloat16 && dst.dtype() == at::kBFloat16 && src.dim() == 2 && dst.dim() == 3 &&
+                  src.is_contiguous() && dst.is_contiguous(), "gather_cols_bf16: src [R][K], dst [Q][R][C] bf16");
+  const int64_t R = src.size(0), K = src.size(1), Q = dst.size(0), C = dst.size(2);
+  TORCH_CHECK(dst.size(1) == R && K % 8 == 0 && C % 8 == 0 && col0 % 8 == 0 && col0 >= 0,
+              "gather_cols_bf16: shapes (K, C, col0 must be multiples of 8)");
+  const int64_t total = Q * R * (C / 8);
+  if (total == 0) return;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  gather_cols_kernel<<<grid, 256, 0, stream>>>((const uint4*)src.data_ptr(), (int)(K / 8), (int)R, (int)(col0 / 8),
+                                               (int)(C / 8), (int)Q, (uint4*)dst.data_ptr());
+}
+
 }  // namespace mihvd

@@ -265,7 +265,8 @@ template <bool ADAM>
 __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
     const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
-    float* __restrict__ gW4, float* __restrict__ gb4, int B, int tile_base, int n_small, AdamArgs ad, int write_grad) {
+    float* __restrict__ gW4, float* __restrict__ gb4, int B, int tile_base, int n_small, AdamArgs ad, int write_grad,
+    int a2s, int a2c0) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
@@ -292,7 +293,7 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     {
       const int rows = min(MAXB, Kw);
       lz.load(dzw + n0, FC1_N, (rows + 31) & ~31, rows, t);
-      la.load(a2w + j0, FC1_K, (rows + 31) & ~31, rows, t);
+      la.load(a2w + (j0 - a2c0), a2s, (rows + 31) & ~31, rows, t);
     }
     float4 pp[2][2], mm[2][2], vv[2][2];
     for (int kc = 0; kc < Kw; kc += MAXB) {
@@ -320,7 +321,7 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
       if (kc + MAXB < Kw) {
         const int nrows = min(MAXB, Kw - kc - MAXB);
         lz.load(dzw + (int64_t)(kc + MAXB) * FC1_N + n0, FC1_N, (nrows + 31) & ~31, nrows, t);
-        la.load(a2w + (int64_t)(kc + MAXB) * FC1_K + j0, FC1_K, (nrows + 31) & ~31, nrows, t);
+        la.load(a2w + (int64_t)(kc + MAXB) * a2s + (j0 - a2c0), a2s, (nrows + 31) & ~31, nrows, t);
       }
       for (int k0 = 0; k0 < Kpad; k0 += 32) {
         bf16x8 af[2], bfv[2];
@@ -517,14 +518,22 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_wgrad: roles must be 1, 2 or 3");
   const u16* dzw = (const u16*)dz.data_ptr();
   const u16* a2w = (const u16*)a2.data_ptr();
+  int a2s = FC1_K, a2c0 = 0;
   int Kw = B;
   if (dz_w3.has_value() && dz_w3->defined()) {
     TORCH_CHECK(a2_w3.has_value() && a2_w3->defined(), "fc1_wgrad: dz_w3 and a2_w3 go together");
     Kw = dz_w3->size(0);
     TORCH_CHECK(dz_w3->dtype() == at::kBFloat16 && dz_w3->numel() == (int64_t)Kw * FC1_N && dz_w3->is_contiguous(),
                 "fc1_wgrad: dz_w3 [K][1024] bf16");
-    TORCH_CHECK(a2_w3->dtype() == at::kBFloat16 && a2_w3->numel() == (int64_t)Kw * FC1_K && a2_w3->is_contiguous(),
-                "fc1_wgrad: a2_w3 [K][3136] bf16");
+    TORCH_CHECK(a2_w3->dtype() == at::kBFloat16 && a2_w3->is_contiguous() && a2_w3->numel() % Kw == 0,
+                "fc1_wgrad: a2_w3 [K][3136] (or [K][C] columns of the row-tile range) bf16");
+    a2s = (int)(a2_w3->numel() / Kw);
+    if (a2s != FC1_K) {
+      // only the columns of the dW3 row tiles [jt_lo, jt_hi), starting at column jt_lo * 64
+      a2c0 = (int)jt_lo * 64;
+      TORCH_CHECK(a2s % 8 == 0 && a2s >= (int)(jt_hi - jt_lo) * 64,
+                  "fc1_wgrad: a2_w3 column slice must cover the row-tile range (and be a multiple of 8)");
+    }
     TORCH_CHECK(Kw >= 1 && Kw <= 65536, "fc1_wgrad: K");
     dzw = (const u16*)dz_w3->data_ptr();
     a2w = (const u16*)a2_w3->data_ptr();
@@ -542,11 +551,11 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   if (ad != nullptr) {
     fc1_wgrad_kernel<true><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0);
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0, a2s, a2c0);
   } else {
     fc1_wgrad_kernel<false><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, AdamArgs{}, 1);
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, AdamArgs{}, 1, a2s, a2c0);
   }
 }
 

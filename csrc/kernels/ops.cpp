@@ -50,6 +50,7 @@ void adasum_combine(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
 void grad_check_(at::TensorList grads, at::Tensor& ls, bool unscale);
 void update_scale_(at::Tensor& ls, at::Tensor& tracker, double growth, double backoff, int64_t interval,
                    double min_scale);
+void gather_cols_bf16(const at::Tensor& src, int64_t col0, at::Tensor& dst);
 }  // namespace mihvd
 
 namespace {
@@ -122,6 +123,7 @@ void grad_check_op(at::TensorList grads, Tensor ls, bool unscale) { mihvd::grad_
 void update_scale_op(Tensor ls, Tensor tracker, double growth, double backoff, int64_t interval, double min_scale) {
   mihvd::update_scale_(ls, tracker, growth, backoff, interval, min_scale);
 }
+void gather_cols_op(const Tensor& src, int64_t col0, Tensor dst) { mihvd::gather_cols_bf16(src, col0, dst); }
 }  // namespace
 
 TORCH_LIBRARY(mihvd, m) {
@@ -151,6 +153,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
         "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1, "
         "Tensor? loss_scale=None, int max_blocks=0) -> ()");
+  m.def("gather_cols_bf16(Tensor src, int col0, Tensor(a!) dst) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("segment_dots(Tensor a, Tensor b, Tensor offs, int max_seg_len, Tensor(a!) out) -> ()");
@@ -173,6 +176,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("conv2_bwd_adam", &conv2_bwd_adam_op);
   m.impl("conv2_wgrad_reduce_adam", &conv2_wgrad_reduce_adam_op);
   m.impl("adam_step", &adam_op);
+  m.impl("gather_cols_bf16", &gather_cols_op);
   m.impl("scale_cast_bf16", &scale_cast_op);
   m.impl("bf16_to_f32", &bf16_to_f32_op);
   m.impl("segment_dots", &segment_dots_op);

@@ -378,6 +378,9 @@ class FusedMNISTTrainer:
                     self.a1, self.idx1)
         o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
                     self.a2, self.idx2)
+        # (an all-to-all of only the column slice each rank needs would move 1/N of these bytes,
+        # but torch's RCCL process group cannot capture all_to_all_single into a HIP graph: its
+        # watchdog queries the captured event and aborts)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self._all_gather_rows(self.a2_all, self.a2)

@@ -540,3 +540,31 @@ def test_debug_sync_mode_matches_graph(ops, monkeypatch):
         torch.cuda.synchronize()
         out.append(tr.params.clone())
     assert torch.equal(out[0], out[1])
+
+
+def test_gather_cols_and_column_slice_wgrad(ops):
+    """gather_cols_bf16 (column slices with zero padding past K) and fc1_wgrad reading a [K][C]
+    column slice of a2 for a row-tile range: equal to the full-width computation on those rows."""
+    g = torch.Generator(device="cuda").manual_seed(51)
+    B, N = 40, 3
+    a2 = torch.randn(N * B, 3136, device="cuda", generator=g).to(torch.bfloat16)
+    dz = torch.randn(N * B, 1024, device="cuda", generator=g).to(torch.bfloat16)
+    T64 = 17 * 64                              # ceil(49 / 3) tiles per rank
+    out = torch.empty(N, N * B, T64, device="cuda", dtype=torch.bfloat16)
+    ops.gather_cols_bf16(a2, 0, out)
+    for q in range(N):
+        lo, hi = q * T64, min((q + 1) * T64, 3136)
+        assert torch.equal(out[q, :, :hi - lo], a2[:, lo:hi])
+        assert not out[q, :, hi - lo:].any()
+    h = torch.zeros(B, 1024, device="cuda", dtype=torch.bfloat16)
+    dlog = torch.zeros(B, 10, device="cuda")
+    full = torch.zeros(3136, 1024, device="cuda")
+    part = torch.zeros(3136, 1024, device="cuda")
+    small = [torch.zeros(n, device="cuda") for n in (1024, 10240, 10)]
+    ops.fc1_wgrad(dz[:B], a2[:B], h, dlog, full, *small, 1, dz, a2, 0, 49)
+    ops.fc1_wgrad(dz[:B], a2[:B], h, dlog, part, *small, 1, dz, out[1].contiguous(), 17, 34)
+    torch.cuda.synchronize()
+    assert torch.equal(part[17 * 64:34 * 64], full[17 * 64:34 * 64])
+    assert not part[:17 * 64].any() and not part[34 * 64:].any()
+    ref = a2.float().t() @ dz.float()
+    assert rel_err(full, ref) < 1e-4
