@@ -281,13 +281,16 @@ class MonitoredTrainingSession:
         ctx = SessionRunContext(self)
         for h in self.hooks:
             h.before_run(ctx)
+        before = self.state.global_step
         if feed_dict is None:
             res = train_op()
         elif isinstance(feed_dict, dict):
             res = train_op(**feed_dict)
         else:
             res = train_op(*feed_dict)
-        self.state.global_step += 1
+        if self.state.global_step == before:
+            # states that count their own steps (the fused trainer) are not advanced twice
+            self.state.global_step += 1
         if res is not None and not isinstance(res, dict):
             res = {"result": res}
         vals = SessionRunValues(res)

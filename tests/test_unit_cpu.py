@@ -457,3 +457,25 @@ def test_collective_custom_ops_trace_single_rank(hvd_single):
     gm = make_fx(lambda t: ops.allreduce(t * 2, 1, "t") + 1)(torch.randn(5))
     assert "mihvd_dist.allreduce" in gm.code
     assert ops.allgather(torch.ones(2, 2), "g").shape == (2, 2)
+
+
+def test_monitored_session_counts_self_advancing_state_once(tmp_path, hvd_single):
+    """A train state that advances its own global_step (FusedMNISTTrainer.train_step) is not
+    advanced a second time by the session: StopAtStepHook(last_step=N) runs exactly N steps."""
+    import mihvd.tensorflow as tfh
+
+    class SelfCounting:
+        def __init__(self):
+            self.global_step = 0
+            self.calls = 0
+
+        def step(self):
+            self.calls += 1
+            self.global_step += 1
+            return {"loss": 0.0}
+
+    st = SelfCounting()
+    with tfh.MonitoredTrainingSession(state=st, hooks=[tfh.StopAtStepHook(last_step=25)]) as sess:
+        while not sess.should_stop():
+            sess.run(st.step)
+    assert st.calls == 25 and st.global_step == 25
