@@ -177,6 +177,11 @@ def init(comm=None, process_sets=None, config: Config | None = None):
             _start_engine(cfg, topo, backend, device)
         _ctx.initialized = True
         atexit.register(shutdown)
+        if process_sets:
+            from .process_sets import add_process_set
+
+            for ps in process_sets:
+                add_process_set(ps)
         if topo.rank == 0:
             log.debug("mihvd initialised: %s backend=%s device=%s config=%s", topo, backend, device, cfg)
 
@@ -281,6 +286,9 @@ def shutdown():
         if _ctx.timeline is not None:
             _ctx.timeline.close()
             _ctx.timeline = None
+        from .process_sets import _reset as _reset_process_sets
+
+        _reset_process_sets()
         if _ctx.owns_pg and dist.is_initialized():
             try:
                 dist.destroy_process_group()

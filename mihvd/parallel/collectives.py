@@ -117,7 +117,9 @@ def _resolve_op(average, op):
 
 
 def _group(process_set=None):
-    return None if process_set is None else process_set
+    from ..process_sets import resolve
+
+    return resolve(process_set)
 
 
 def _group_size(group) -> int:
@@ -350,10 +352,11 @@ def alltoall(tensor, splits=None, name=None, process_set=None):
             if p == me:
                 outs[p].copy_(ins[p])
                 continue
+            peer = dist.get_global_rank(group, p) if group is not None else p  # P2POp takes global ranks
             if ins[p].numel():
-                ops.append(dist.P2POp(dist.isend, ins[p].contiguous(), p, group))
+                ops.append(dist.P2POp(dist.isend, ins[p].contiguous(), peer, group))
             if outs[p].numel():
-                ops.append(dist.P2POp(dist.irecv, outs[p], p, group))
+                ops.append(dist.P2POp(dist.irecv, outs[p], peer, group))
         for w in (dist.batch_isend_irecv(ops) if ops else []):
             w.wait()
     else:

@@ -15,3 +15,6 @@ from .parallel.compression import Compression
 from .parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters
 from .ops import collective_ops as mpi_ops  # noqa: E402,F401  registers torch.ops.mihvd_dist.* (Horovod's mpi_ops)
 from . import elastic  # noqa: E402,F401  hvd.elastic.run / TorchState / ObjectState
+from .process_sets import (ProcessSet, add_process_set, get_process_set_ids_and_ranks,  # noqa: E402,F401
+                           global_process_set, remove_process_set)
+from torch.nn import SyncBatchNorm  # noqa: E402,F401  (hvd.SyncBatchNorm: batch statistics over the process group)

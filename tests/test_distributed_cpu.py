@@ -176,3 +176,17 @@ def test_collectives_debug_sync_mode(tmp_path):
     """MIHVD_DEBUG_SYNC=1: every collective completes inside the call (bisection mode)."""
     _, (a, b) = run_scenario(tmp_path, "collectives", env={"MIHVD_DEBUG_SYNC": "1"})
     assert a["sum"] == b["sum"] and a["async"] == [1.0] * 4
+
+
+def test_process_sets_three_ranks(tmp_path):
+    _, (a, b, c) = run_scenario(tmp_path, "process_sets", np_=3)
+    assert a["ids"] == {"0": [0, 1, 2], "1": [1, 2], "2": [0, 2]}
+    assert (a["included"], b["included"], c["included"]) == (True, False, True)
+    assert (a["set_rank"], c["set_rank"], a["set_size"]) == (0, 1, 2)
+    assert a["avg"] == c["avg"] == [1.0] * 3               # mean of ranks 0 and 2
+    assert a["bcast"] == c["bcast"] == [2.0, 2.0]
+    assert a["gather"] == [[0.0, 0.0], [2.0, 2.0]]
+    assert a["alltoall"] == [0.0, 1.0, 20.0, 21.0] and c["alltoall"] == [2.0, 3.0, 22.0, 23.0]
+    assert "not part of" in b["error"]
+    assert b["sum2"] == c["sum2"] == [5.0, 5.0] and "sum2" not in a
+    assert a["world"] == b["world"] == [3.0]

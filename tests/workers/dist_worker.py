@@ -271,9 +271,41 @@ def sc_torch_ops(outdir):
                               "bb": bb.tolist(), "bgrad": b.grad.tolist(), "t": t.tolist()})
 
 
+def sc_process_sets(outdir):
+    """Horovod process sets on 3 ranks: {0, 2} registered through add_process_set, {1, 2} through
+    init(process_sets=...) in main()."""
+    r = hvd.rank()
+    ps = hvd.add_process_set([0, 2])
+    res = {"ids": {str(k): v for k, v in hvd.get_process_set_ids_and_ranks().items()}, "included": ps.included(),
+           "set_rank": ps.rank(), "set_size": ps.size()}
+    if ps.included():
+        res["avg"] = hvd.allreduce(torch.full((3,), float(r)), process_set=ps).tolist()
+        res["bcast"] = hvd.broadcast(torch.full((2,), float(r)), root_rank=2, process_set=ps).tolist()
+        res["gather"] = hvd.allgather(torch.full((1, 2), float(r)), process_set=ps).tolist()
+        o, _ = hvd.alltoall(torch.arange(4, dtype=torch.float32) + 10 * r, process_set=ps)
+        res["alltoall"] = o.tolist()
+    else:
+        try:
+            hvd.allreduce(torch.ones(1), process_set=ps)
+        except ValueError as e:
+            res["error"] = str(e)
+    ps2 = PS_INIT[0]
+    if ps2.included():
+        res["sum2"] = hvd.allreduce(torch.ones(2) * (r + 1), op=hvd.Sum, process_set=ps2).tolist()
+    res["world"] = hvd.allreduce(torch.ones(1), op=hvd.Sum).tolist()
+    out(outdir, "process_sets", res)
+
+
+PS_INIT = []
+
+
 def main():
     scenario, outdir = sys.argv[1], sys.argv[2]
-    hvd.init()
+    if scenario == "process_sets":
+        PS_INIT.append(hvd.ProcessSet([1, 2]))
+        hvd.init(process_sets=PS_INIT)
+    else:
+        hvd.init()
     globals()["sc_" + scenario](outdir)
     hvd.shutdown()
 
