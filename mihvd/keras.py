@@ -113,6 +113,40 @@ class LearningRateWarmupCallback(Callback):
             g["lr"] = lr
 
 
+class LearningRateScheduleCallback(Callback):
+    """Horovod's ``LearningRateScheduleCallback``: between ``start_epoch`` and ``end_epoch`` the LR is
+    ``initial_lr * multiplier(epoch)`` — per epoch (``staircase=True``) or per batch with a fractional
+    epoch. ``multiplier`` may be a constant."""
+
+    def __init__(self, initial_lr, multiplier, start_epoch=0, end_epoch=None, staircase=True,
+                 momentum_correction=True, steps_per_epoch=None, verbose=0):
+        self.initial_lr = initial_lr
+        self.multiplier = multiplier if callable(multiplier) else (lambda epoch, m=multiplier: m)
+        self.start_epoch = start_epoch
+        self.end_epoch = end_epoch
+        self.staircase = staircase
+        self.steps_per_epoch = steps_per_epoch
+        self._epoch = 0
+
+    def _active(self, epoch) -> bool:
+        return epoch >= self.start_epoch and (self.end_epoch is None or epoch < self.end_epoch)
+
+    def _set(self, lr):
+        for g in self.model.optimizer.param_groups:
+            g["lr"] = lr
+
+    def on_epoch_begin(self, epoch, logs=None):
+        self._epoch = epoch
+        if self.staircase and self._active(epoch):
+            self._set(self.initial_lr * self.multiplier(epoch))
+
+    def on_batch_begin(self, batch, logs=None):
+        if self.staircase or not self._active(self._epoch):
+            return
+        spe = self.steps_per_epoch or self.model._steps_per_epoch or 1
+        self._set(self.initial_lr * self.multiplier(self._epoch + batch / spe))
+
+
 class ModelCheckpoint(Callback):
     def __init__(self, filepath, monitor="val_loss", save_best_only=False, mode="min", verbose=0):
         self.filepath = filepath
@@ -160,6 +194,7 @@ class _CallbacksNS:
     BroadcastGlobalVariablesCallback = BroadcastGlobalVariablesCallback
     MetricAverageCallback = MetricAverageCallback
     LearningRateWarmupCallback = LearningRateWarmupCallback
+    LearningRateScheduleCallback = LearningRateScheduleCallback
     ModelCheckpoint = ModelCheckpoint
     TensorBoard = TensorBoard
     Callback = Callback

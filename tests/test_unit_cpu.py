@@ -479,3 +479,27 @@ def test_monitored_session_counts_self_advancing_state_once(tmp_path, hvd_single
         while not sess.should_stop():
             sess.run(st.step)
     assert st.calls == 25 and st.global_step == 25
+
+
+def test_keras_lr_schedule_callback():
+    import mihvd.keras as khvd
+
+    class _Opt:
+        param_groups = [{"lr": 0.0}]
+
+    class _M:
+        optimizer = _Opt()
+        _steps_per_epoch = 10
+
+    cb = khvd.callbacks.LearningRateScheduleCallback(0.1, lambda e: 0.5 ** e, start_epoch=1, end_epoch=3)
+    cb.set_model(_M())
+    lrs = []
+    for epoch in range(4):
+        cb.on_epoch_begin(epoch)
+        lrs.append(_M.optimizer.param_groups[0]["lr"])
+    assert lrs == [0.0, 0.05, 0.025, 0.025]  # inactive before 1 and from 3 on
+    smooth = khvd.callbacks.LearningRateScheduleCallback(1.0, lambda e: e, staircase=False)
+    smooth.set_model(_M())
+    smooth.on_epoch_begin(2)
+    smooth.on_batch_begin(5)
+    assert _M.optimizer.param_groups[0]["lr"] == 2.5
