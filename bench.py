@@ -13,7 +13,10 @@ Implementations:
   fused  — mihvd's hand-written CDNA4 HIP kernels: bf16 MFMA forward/backward with fp32 master
            weights, gradients written straight into the fusion buffer, RCCL allreduce on it,
            fused TF1-Adam; the whole step (incl. the allreduce) replayed as one HIP graph.
-  torch  — stock PyTorch-ROCm ops (fp32) + mihvd DistributedOptimizer (bucketed RCCL allreduce).
+  torch  — stock PyTorch-ROCm ops (fp32) + mihvd DistributedOptimizer (bucketed RCCL allreduce) +
+           TF1 Adam on the multi-tensor HIP kernel.
+  torch-graph — the same step (data gather, forward, backward, bucket allreduces, FusedAdam with a
+           device step count) captured in one HIP graph (mihvd.graphs.CapturedStep).
   ddp    — stock PyTorch-ROCm ops (fp32) + torch DDP + torch Adam: the measured comparator
            (the reference publishes no images/sec).
 
@@ -43,7 +46,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--impl", choices=["fused", "torch", "ddp"], default=os.environ.get("MIHVD_BENCH_IMPL", "fused"))
+    ap.add_argument("--impl", choices=["fused", "torch", "torch-graph", "ddp"],
+                    default=os.environ.get("MIHVD_BENCH_IMPL", "fused"))
     ap.add_argument("--batch-size", type=int, default=PER_GPU_BATCH)
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--graph-steps", type=int, default=0, help="fused: steps captured per HIP graph (0=auto)")
@@ -93,6 +97,45 @@ def make_torch_step(args, hvd, device, ddp=False):
     return step, "fp32", lambda: None
 
 
+def make_torch_graph_step(args, hvd, device):
+    """Stock PyTorch-ROCm layers + mihvd DistributedOptimizer + FusedAdam (TF1 rule, device step
+    count), the whole step (data gather, forward, backward, bucket allreduces, optimizer) captured
+    in one HIP graph by mihvd.graphs.CapturedStep."""
+    from mihvd.graphs import CapturedStep
+    from mihvd.models.mnist import MNISTConvNet, softmax_cross_entropy
+    from mihvd.optim import FusedAdam
+
+    model = MNISTConvNet(impl="torch", seed=42).to(device)
+    hvd.broadcast_parameters(model.state_dict(), 0)
+    opt = hvd.DistributedOptimizer(FusedAdam(model.parameters(), lr=args.lr * hvd.size(), rule="tf"),
+                                   named_parameters=model.named_parameters())
+    X, Y = synthetic_pool(args.pool_batches, args.batch_size, device, seed=hvd.rank())
+    B = args.batch_size
+    X = X.view(args.pool_batches, B, 784)
+    Y = Y.view(args.pool_batches, B)
+    ctr = torch.zeros(1, dtype=torch.int64, device=device)
+    xb = torch.empty(B, 784, device=device)
+    yb = torch.empty(B, dtype=torch.int64, device=device)
+
+    def step():
+        i = ctr % args.pool_batches
+        xb.copy_(X.index_select(0, i).squeeze(0))
+        yb.copy_(Y.index_select(0, i).squeeze(0))
+        opt.zero_grad(set_to_none=False)
+        loss = softmax_cross_entropy(model(xb), yb)
+        loss.backward()
+        opt.step()
+        ctr.add_(1)
+        return loss
+
+    graphed = CapturedStep(step, warmup=3)
+
+    def run_step(n=None):
+        graphed()
+
+    return run_step, "fp32", None
+
+
 def make_fused_step(args, hvd, device):
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
@@ -125,6 +168,9 @@ def main():
     if args.impl == "fused":
         step, dtype, tr = make_fused_step(args, hvd, device)
         per_call = tr.steps_per_replay
+    elif args.impl == "torch-graph":
+        step, dtype, _ = make_torch_graph_step(args, hvd, device)
+        per_call = 1
     else:
         step, dtype, _ = make_torch_step(args, hvd, device, ddp=args.impl == "ddp")
         per_call = 1

@@ -51,6 +51,14 @@ void grad_check_(at::TensorList grads, at::Tensor& ls, bool unscale);
 void update_scale_(at::Tensor& ls, at::Tensor& tracker, double growth, double backoff, int64_t interval,
                    double min_scale);
 void gather_cols_bf16(const at::Tensor& src, int64_t col0, at::Tensor& dst);
+void multi_tensor_adam(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std::vector<at::Tensor> m,
+                       std::vector<at::Tensor> v, const c10::optional<at::Tensor>& step, int64_t host_step, double lr,
+                       double b1, double b2, double eps, double weight_decay, bool decoupled, int64_t rule,
+                       double grad_scale);
+void multi_tensor_sgd(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std::vector<at::Tensor> bufs, double lr,
+                      double momentum, double dampening, double weight_decay, bool nesterov, bool first,
+                      double grad_scale);
+void bump_step_(at::Tensor& step);
 }  // namespace mihvd
 
 namespace {
@@ -124,6 +132,17 @@ void update_scale_op(Tensor ls, Tensor tracker, double growth, double backoff, i
   mihvd::update_scale_(ls, tracker, growth, backoff, interval, min_scale);
 }
 void gather_cols_op(const Tensor& src, int64_t col0, Tensor dst) { mihvd::gather_cols_bf16(src, col0, dst); }
+void mt_adam_op(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v, const OptT& step,
+                int64_t host_step, double lr, double b1, double b2, double eps, double wd, bool decoupled, int64_t rule,
+                double grad_scale) {
+  mihvd::multi_tensor_adam(p.vec(), g.vec(), m.vec(), v.vec(), step, host_step, lr, b1, b2, eps, wd, decoupled, rule,
+                           grad_scale);
+}
+void mt_sgd_op(at::TensorList p, at::TensorList g, at::TensorList bufs, double lr, double momentum, double dampening,
+               double wd, bool nesterov, bool first, double grad_scale) {
+  mihvd::multi_tensor_sgd(p.vec(), g.vec(), bufs.vec(), lr, momentum, dampening, wd, nesterov, first, grad_scale);
+}
+void bump_step_op(Tensor step) { mihvd::bump_step_(step); }
 }  // namespace
 
 TORCH_LIBRARY(mihvd, m) {
@@ -153,6 +172,11 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
         "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1, "
         "Tensor? loss_scale=None, int max_blocks=0) -> ()");
+  m.def("multi_tensor_adam(Tensor(a!)[] p, Tensor[] g, Tensor(b!)[] m, Tensor(c!)[] v, Tensor? step, int host_step, "
+        "float lr, float b1, float b2, float eps, float weight_decay, bool decoupled, int rule, float grad_scale) -> ()");
+  m.def("multi_tensor_sgd(Tensor(a!)[] p, Tensor[] g, Tensor(b!)[] bufs, float lr, float momentum, float dampening, "
+        "float weight_decay, bool nesterov, bool first, float grad_scale) -> ()");
+  m.def("bump_step_(Tensor(a!) step) -> ()");
   m.def("gather_cols_bf16(Tensor src, int col0, Tensor(a!) dst) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
@@ -177,6 +201,9 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("conv2_wgrad_reduce_adam", &conv2_wgrad_reduce_adam_op);
   m.impl("adam_step", &adam_op);
   m.impl("gather_cols_bf16", &gather_cols_op);
+  m.impl("multi_tensor_adam", &mt_adam_op);
+  m.impl("multi_tensor_sgd", &mt_sgd_op);
+  m.impl("bump_step_", &bump_step_op);
   m.impl("scale_cast_bf16", &scale_cast_op);
   m.impl("bf16_to_f32", &bf16_to_f32_op);
   m.impl("segment_dots", &segment_dots_op);

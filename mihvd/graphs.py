@@ -1,0 +1,54 @@
+"""Whole-step HIP-graph capture for models trained through the generic engine.
+
+The fused MNIST trainer replays its hand-written kernels from a HIP graph. ``CapturedStep`` does
+the same for any PyTorch model: forward, backward (whose gradient hooks launch the
+DistributedOptimizer's bucket allreduces — RCCL calls are captured), the allreduce waits and a
+capturable optimizer (``mihvd.optim.FusedAdam`` / ``FusedSGD``: device-side step count, no host
+synchronisation) become one graph that the host launches with a single call — the MI355X
+replacement for a tracing compiler on launch-bound models.
+
+    x, y = static input buffers (copy each batch into them, or gather on the device)
+    def step():
+        opt.zero_grad(set_to_none=False)
+        loss = loss_fn(model(x), y)
+        loss.backward()
+        opt.step()
+        return loss
+    graphed = CapturedStep(step)        # warm-up runs + capture
+    for batch in data:
+        x.copy_(batch.x); y.copy_(batch.y)
+        loss = graphed()                # replay
+
+Tensors the step allocates are owned by the graph's private memory pool and are overwritten by the
+next replay; ``graphed()`` returns the step's (static) output.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class CapturedStep:
+    def __init__(self, step_fn, warmup: int = 3, pool=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("CapturedStep needs a GPU")
+        self.step_fn = step_fn
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up on a side stream, as graph capture of autograd requires
+            for _ in range(warmup):
+                out = step_fn()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=pool):
+            self.output = step_fn()
+        self.warmup_output = out if warmup else None
+        self.replays = 0
+
+    def __call__(self):
+        self.graph.replay()
+        self.replays += 1
+        return self.output
+
+    def pool(self):
+        return self.graph.pool()

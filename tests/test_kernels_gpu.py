@@ -568,3 +568,87 @@ def test_gather_cols_and_column_slice_wgrad(ops):
     assert not part[:17 * 64].any() and not part[34 * 64:].any()
     ref = a2.float().t() @ dz.float()
     assert rel_err(full, ref) < 1e-4
+
+
+@pytest.mark.parametrize("kind", ["adam", "adamw", "tf", "sgd", "nesterov"])
+def test_multi_tensor_optimizers_match_torch(ops, kind):
+    """multi_tensor_adam / multi_tensor_sgd (via FusedAdam / FusedSGD) vs torch.optim on GPU
+    tensors of awkward sizes (not multiples of 4, > 1 chunk, > 24 tensors per launch), including a
+    channels_last parameter whose gradient shares its layout."""
+    from mihvd.optim import FusedAdam, FusedSGD, TFAdam
+
+    g = torch.Generator(device="cuda").manual_seed(61)
+    shapes = [(70001,), (3,), (1031, 7), (64, 32, 3, 3)] + [(257,)] * 30
+    a = [torch.randn(s, device="cuda", generator=g) for s in shapes]
+    a[3] = a[3].to(memory_format=torch.channels_last)
+    a = [x.requires_grad_(True) for x in a]
+    b = [x.detach().clone().requires_grad_(True) for x in a]
+    mk = {"adam": (lambda ps: FusedAdam(ps, lr=1e-2, weight_decay=0.01), lambda ps: torch.optim.Adam(ps, lr=1e-2, weight_decay=0.01)),
+          "adamw": (lambda ps: FusedAdam(ps, lr=1e-2, weight_decay=0.1, adamw=True), lambda ps: torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.1)),
+          "tf": (lambda ps: FusedAdam(ps, lr=1e-2, rule="tf"), lambda ps: TFAdam(ps, lr=1e-2)),
+          "sgd": (lambda ps: FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-3), lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-3)),
+          "nesterov": (lambda ps: FusedSGD(ps, lr=0.1, momentum=0.9, nesterov=True), lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, nesterov=True))}[kind]
+    oa, ob = mk[0](a), mk[1](b)
+    if kind == "tf":  # reference: TFAdam's torch foreach path, on CPU copies
+        b = [x.detach().cpu().clone().requires_grad_(True) for x in b]
+        ob = TFAdam(b, lr=1e-2)
+    for step in range(3):
+        for ps, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            sum((x.float() * (i + 1 + step)).cos().sum() for i, x in enumerate(ps)).backward()
+            o.step()
+    for x, y in zip(a, b):
+        assert rel_err(x.detach().cpu(), y.detach().cpu()) < 1e-5, kind
+
+
+def test_captured_step_matches_eager(ops):
+    """mihvd.graphs.CapturedStep: forward + backward + DistributedOptimizer (bucketed) + FusedAdam
+    captured in one HIP graph and replayed == the same steps run eagerly."""
+    import mihvd.torch as hvd
+    from mihvd.graphs import CapturedStep
+    from mihvd.optim import FusedAdam
+
+    hvd.init()
+    try:
+        torch.manual_seed(5)
+        X = torch.randn(12, 64, 32, device="cuda")
+        Y = torch.randn(12, 64, 4, device="cuda")
+
+        def build():
+            torch.manual_seed(1)
+            m = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.GELU(), torch.nn.Linear(64, 4)).cuda()
+            o = hvd.DistributedOptimizer(FusedAdam(m.parameters(), lr=1e-2, rule="tf"),
+                                         named_parameters=m.named_parameters())
+            return m, o
+
+        m1, o1 = build()
+        x = torch.zeros(64, 32, device="cuda")
+        y = torch.zeros(64, 4, device="cuda")
+        ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+        def step():
+            i = ctr % 12
+            x.copy_(X.index_select(0, i).squeeze(0))
+            y.copy_(Y.index_select(0, i).squeeze(0))
+            o1.zero_grad(set_to_none=False)
+            loss = torch.nn.functional.mse_loss(m1(x), y)
+            loss.backward()
+            o1.step()
+            ctr.add_(1)
+            return loss
+
+        graphed = CapturedStep(step, warmup=3)
+        for _ in range(9):
+            graphed()
+        torch.cuda.synchronize()
+        m2, o2 = build()
+        for i in range(12):  # 3 warm-up steps + 9 replays (capture itself does not execute)
+            o2.zero_grad(set_to_none=False)
+            torch.nn.functional.mse_loss(m2(X[i % 12]), Y[i % 12]).backward()
+            o2.step()
+        torch.cuda.synchronize()
+        assert int(ctr) == 12
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            assert torch.equal(p1, p2)
+    finally:
+        hvd.shutdown()

@@ -503,3 +503,32 @@ def test_keras_lr_schedule_callback():
     smooth.on_epoch_begin(2)
     smooth.on_batch_begin(5)
     assert _M.optimizer.param_groups[0]["lr"] == 2.5
+
+
+def test_fused_optimizers_torch_path_match_torch_optim():
+    """FusedAdam / FusedSGD on CPU tensors (torch fallback) follow torch.optim semantics."""
+    import torch
+
+    from mihvd.optim import FusedAdam, FusedSGD
+
+    torch.manual_seed(0)
+    cases = [
+        (lambda ps: FusedAdam(ps, lr=1e-2, weight_decay=0.1), lambda ps: torch.optim.Adam(ps, lr=1e-2, weight_decay=0.1)),
+        (lambda ps: FusedAdam(ps, lr=1e-2, weight_decay=0.1, adamw=True),
+         lambda ps: torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.1)),
+        (lambda ps: FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True),
+         lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True)),
+        (lambda ps: FusedSGD(ps, lr=0.1, momentum=0.9, dampening=0.1),
+         lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, dampening=0.1)),
+    ]
+    for mk, mk_ref in cases:
+        a = [torch.randn(7, 5, requires_grad=True), torch.randn(3, requires_grad=True)]
+        b = [x.detach().clone().requires_grad_(True) for x in a]
+        oa, ob = mk(a), mk_ref(b)
+        for _ in range(4):
+            for ps, o in ((a, oa), (b, ob)):
+                o.zero_grad()
+                (ps[0].sin().sum() + (ps[1] ** 2).sum()).backward()
+                o.step()
+        for x, y in zip(a, b):
+            assert torch.allclose(x, y, atol=1e-6, rtol=1e-5)
