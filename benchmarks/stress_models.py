@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--compression", choices=["none", "fp16", "bf16"], default="")
     ap.add_argument("--fusion-mib", type=float, default=0, help="fusion threshold (0 = engine default)")
+    ap.add_argument("--optimizer", choices=["torch", "fused"], default="fused",
+                    help="fused: mihvd multi-tensor HIP optimizer (FusedSGD / FusedAdam(adamw))")
+    ap.add_argument("--graph", action="store_true", help="capture the whole step in one HIP graph")
     return ap.parse_args()
 
 
@@ -59,7 +62,12 @@ def main():
         model = ResNet50().to(dev).to(memory_format=torch.channels_last)
         x = torch.randn(B, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last)
         y = torch.randint(0, 1000, (B,), device=dev, generator=g)
-        base = torch.optim.SGD(model.parameters(), lr=0.1 * n, momentum=0.9, weight_decay=5e-5)
+        if args.optimizer == "fused":
+            from mihvd.optim import FusedSGD
+
+            base = FusedSGD(model.parameters(), lr=0.1 * n, momentum=0.9, weight_decay=5e-5)
+        else:
+            base = torch.optim.SGD(model.parameters(), lr=0.1 * n, momentum=0.9, weight_decay=5e-5)
 
         def loss_fn():
             with torch.autocast(dev.type, dtype=torch.bfloat16):
@@ -74,7 +82,12 @@ def main():
         c = BertConfig(max_len=max(512, args.seq_len))
         model = BertForMaskedLM(c).to(dev)
         ids, labels = synthetic_mlm_batch(B, args.seq_len, c.vocab_size, dev, generator=g)
-        base = torch.optim.AdamW(model.parameters(), lr=1e-4 * n, weight_decay=0.01)
+        if args.optimizer == "fused":
+            from mihvd.optim import FusedAdam
+
+            base = FusedAdam(model.parameters(), lr=1e-4 * n, weight_decay=0.01, adamw=True)
+        else:
+            base = torch.optim.AdamW(model.parameters(), lr=1e-4 * n, weight_decay=0.01)
 
         def loss_fn():
             with torch.autocast(dev.type, dtype=torch.bfloat16):
@@ -87,12 +100,16 @@ def main():
                                    fusion_threshold=int(args.fusion_mib * 2 ** 20) if args.fusion_mib else None)
 
     def step():
-        opt.zero_grad()
+        opt.zero_grad(set_to_none=False)
         loss = loss_fn()
         loss.backward()
         opt.step()
         return loss
 
+    if args.graph:
+        from mihvd.graphs import CapturedStep
+
+        step = CapturedStep(step, warmup=max(3, args.warmup))
     for _ in range(args.warmup):
         step()
     sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
@@ -113,7 +130,7 @@ def main():
         params = sum(p.numel() for p in model.parameters())
         cfg.update({"parallelism": f"dp{n}", "per_gpu_batch": B, "params": params,
                     "grad_bytes_fp32": params * 4, "buckets": len(opt.buckets), "compression": comp_name,
-                    "final_loss": float(loss)})
+                    "optimizer": args.optimizer, "hip_graph": bool(args.graph), "final_loss": float(loss)})
         print(json.dumps({"metric": metric, "value": round(args.steps * B * per_sample * n / el, 1), "unit": unit,
                           "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
