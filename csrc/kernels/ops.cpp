@@ -43,6 +43,8 @@ void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                int64_t max_blocks);
 void scale_cast_bf16(const at::Tensor& src, at::Tensor& dst, double scale);
 void bf16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale);
+void scale_cast_f16(const at::Tensor& src, at::Tensor& dst, double scale);
+void f16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale);
 void segment_dots(const at::Tensor& a, const at::Tensor& b, const at::Tensor& offs_dev, int64_t max_seg_len,
                   at::Tensor& out);
 void adasum_combine(const at::Tensor& a, const at::Tensor& b, const at::Tensor& offs_dev, int64_t max_seg_len,
@@ -120,6 +122,8 @@ void adam_op(Tensor p, const Tensor& g, Tensor m, Tensor v, const OptT& shadow, 
 }
 void scale_cast_op(const Tensor& src, Tensor dst, double scale) { mihvd::scale_cast_bf16(src, dst, scale); }
 void bf16_to_f32_op(const Tensor& src, Tensor dst, double scale) { mihvd::bf16_to_f32(src, dst, scale); }
+void scale_cast_f16_op(const Tensor& src, Tensor dst, double scale) { mihvd::scale_cast_f16(src, dst, scale); }
+void f16_to_f32_op(const Tensor& src, Tensor dst, double scale) { mihvd::f16_to_f32(src, dst, scale); }
 void segment_dots_op(const Tensor& a, const Tensor& b, const Tensor& offs, int64_t max_len, Tensor out) {
   mihvd::segment_dots(a, b, offs, max_len, out);
 }
@@ -180,6 +184,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("gather_cols_bf16(Tensor src, int col0, Tensor(a!) dst) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
+  m.def("scale_cast_f16(Tensor src, Tensor(a!) dst, float scale) -> ()");
+  m.def("f16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("segment_dots(Tensor a, Tensor b, Tensor offs, int max_seg_len, Tensor(a!) out) -> ()");
   m.def("adasum_combine(Tensor a, Tensor b, Tensor offs, int max_seg_len, Tensor dots, Tensor(a!) out) -> ()");
   m.def("grad_check_(Tensor(a!)[] grads, Tensor(b!) ls, bool unscale) -> ()");
@@ -206,6 +212,8 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("bump_step_", &bump_step_op);
   m.impl("scale_cast_bf16", &scale_cast_op);
   m.impl("bf16_to_f32", &bf16_to_f32_op);
+  m.impl("scale_cast_f16", &scale_cast_f16_op);
+  m.impl("f16_to_f32", &f16_to_f32_op);
   m.impl("segment_dots", &segment_dots_op);
   m.impl("adasum_combine", &adasum_combine_op);
   m.impl("grad_check_", &grad_check_op);

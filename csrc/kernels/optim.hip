@@ -11,6 +11,8 @@
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 
+#include <hip/hip_fp16.h>
+
 #include "common.h"
 
 namespace mihvd {
@@ -54,6 +56,26 @@ __global__ void __launch_bounds__(256) bf16_to_f32_kernel(const u16* __restrict_
     const uint2 s = reinterpret_cast<const uint2*>(src)[i];
     reinterpret_cast<float4*>(dst)[i] = make_float4(bf2f((u16)(s.x & 0xffff)) * scale, bf2f((u16)(s.x >> 16)) * scale,
                                                     bf2f((u16)(s.y & 0xffff)) * scale, bf2f((u16)(s.y >> 16)) * scale);
+  }
+}
+
+// fp16 wire format of Compression.fp16 (the same pack/unpack with scale as the bf16 pair above).
+__global__ void __launch_bounds__(256) scale_cast_f16_kernel(const float* __restrict__ src, __half* __restrict__ dst,
+                                                             int64_t n4, float scale) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 s = reinterpret_cast<const float4*>(src)[i];
+    __half2* d = reinterpret_cast<__half2*>(dst) + 2 * i;
+    d[0] = __floats2half2_rn(s.x * scale, s.y * scale);
+    d[1] = __floats2half2_rn(s.z * scale, s.w * scale);
+  }
+}
+
+__global__ void __launch_bounds__(256) f16_to_f32_kernel(const __half* __restrict__ src, float* __restrict__ dst,
+                                                         int64_t n4, float scale) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const __half2* s = reinterpret_cast<const __half2*>(src) + 2 * i;
+    const float2 a = __half22float2(s[0]), b = __half22float2(s[1]);
+    reinterpret_cast<float4*>(dst)[i] = make_float4(a.x * scale, a.y * scale, b.x * scale, b.y * scale);
   }
 }
 
@@ -108,6 +130,22 @@ void bf16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale) {
   auto stream = c10::hip::getCurrentHIPStream().stream();
   bf16_to_f32_kernel<<<grid_for(src.numel() / 4), 256, 0, stream>>>((const u16*)src.data_ptr(), dst.data_ptr<float>(),
                                                                      src.numel() / 4, (float)scale);
+}
+
+void scale_cast_f16(const at::Tensor& src, at::Tensor& dst, double scale) {
+  TORCH_CHECK(src.dtype() == at::kFloat && dst.dtype() == at::kHalf && src.numel() == dst.numel() && src.numel() % 4 == 0,
+              "scale_cast_f16");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  scale_cast_f16_kernel<<<grid_for(src.numel() / 4), 256, 0, stream>>>(src.data_ptr<float>(), (__half*)dst.data_ptr(),
+                                                                       src.numel() / 4, (float)scale);
+}
+
+void f16_to_f32(const at::Tensor& src, at::Tensor& dst, double scale) {
+  TORCH_CHECK(src.dtype() == at::kHalf && dst.dtype() == at::kFloat && src.numel() == dst.numel() && src.numel() % 4 == 0,
+              "f16_to_f32");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  f16_to_f32_kernel<<<grid_for(src.numel() / 4), 256, 0, stream>>>((const __half*)src.data_ptr(), dst.data_ptr<float>(),
+                                                                   src.numel() / 4, (float)scale);
 }
 
 }  // namespace mihvd

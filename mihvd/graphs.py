@@ -36,13 +36,12 @@ class CapturedStep:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up on a side stream, as graph capture of autograd requires
             for _ in range(warmup):
-                out = step_fn()
+                _detach(step_fn())  # drop the autograd graph: no AccumulateGrad node outlives its step
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
-            self.output = step_fn()
-        self.warmup_output = out if warmup else None
+            self.output = _detach(step_fn())
         self.replays = 0
 
     def __call__(self):
@@ -52,3 +51,13 @@ class CapturedStep:
 
     def pool(self):
         return self.graph.pool()
+
+
+def _detach(out):
+    if torch.is_tensor(out):
+        return out.detach()
+    if isinstance(out, (list, tuple)):
+        return type(out)(_detach(o) for o in out)
+    if isinstance(out, dict):
+        return {k: _detach(v) for k, v in out.items()}
+    return out

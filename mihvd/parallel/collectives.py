@@ -16,7 +16,7 @@ import torch.distributed as dist
 
 from .. import basics
 from ..basics import ReduceOp
-from .compression import Compression
+from .compression import Compression, hip_pack, hip_pack_ok, hip_unpack
 
 _handles: dict[int, "_Handle"] = {}
 _hlock = threading.Lock()
@@ -150,6 +150,16 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
             return _register(work, out, None, f"allreduce.{name}")
         run_adasum()
         return _register(None, out, None, f"allreduce.{name}")
+    if n > 1 and hip_pack_ok(compression, tensor) and out.is_contiguous():
+        # fused HIP pack (cast + prescale) -> collective on the 16-bit wire -> unpack (cast + scale)
+        wire = hip_pack(compression, tensor, prescale_factor)
+        scale = postscale_factor / n if op == ReduceOp.Average else postscale_factor
+        if ctx.engine is not None:
+            work = ctx.engine.allreduce(f"allreduce.{name}", wire, _torch_op(op), group, fuse_extra=("hip-pack",))
+        else:
+            work = dist.all_reduce(wire, op=_torch_op(op), group=group, async_op=True)
+        return _register(work, out, lambda _o, wire=wire, out=out, scale=scale: hip_unpack(wire, out, scale),
+                         f"allreduce.{name}")
     wire, cctx = compression.compress(tensor)
     if wire is tensor and out is not tensor:
         out.copy_(tensor)

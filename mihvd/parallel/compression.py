@@ -45,6 +45,31 @@ class BF16Compressor(_CastCompressor):
     wire_dtype = torch.bfloat16
 
 
+def hip_pack_ok(compression, tensor) -> bool:
+    """Compression.bf16/fp16 of a contiguous fp32 GPU tensor runs on the fused HIP pack/unpack
+    kernels (cast + scale in one pass each way; csrc/kernels/optim.hip)."""
+    if compression.wire_dtype not in (torch.bfloat16, torch.float16):
+        return False
+    if not (tensor.is_cuda and tensor.dtype == torch.float32 and tensor.is_contiguous() and tensor.numel() % 4 == 0):
+        return False
+    from .. import _native
+
+    return _native.load_kernels()
+
+
+def hip_pack(compression, tensor, scale: float = 1.0):
+    wire = torch.empty(tensor.numel(), dtype=compression.wire_dtype, device=tensor.device)
+    op = torch.ops.mihvd.scale_cast_bf16 if compression.wire_dtype == torch.bfloat16 else torch.ops.mihvd.scale_cast_f16
+    op(tensor.view(-1), wire, float(scale))
+    return wire
+
+
+def hip_unpack(wire, out, scale: float = 1.0):
+    op = torch.ops.mihvd.bf16_to_f32 if wire.dtype == torch.bfloat16 else torch.ops.mihvd.f16_to_f32
+    op(wire, out.view(-1), float(scale))
+    return out
+
+
 class Compression:
     none = NoneCompressor
     fp16 = FP16Compressor

@@ -652,3 +652,18 @@ def test_captured_step_matches_eager(ops):
             assert torch.equal(p1, p2)
     finally:
         hvd.shutdown()
+
+
+@pytest.mark.parametrize("wire", [torch.bfloat16, torch.float16])
+def test_hip_pack_unpack_matches_torch_casts(ops, wire):
+    """Compression pack/unpack kernels (cast + scale fused) == torch casts then scale."""
+    from mihvd.parallel.compression import Compression, hip_pack, hip_unpack
+
+    comp = Compression.bf16 if wire == torch.bfloat16 else Compression.fp16
+    g = torch.Generator(device="cuda").manual_seed(71)
+    x = torch.randn(4 * 9999, device="cuda", generator=g)
+    w = hip_pack(comp, x, 0.5)
+    assert w.dtype == wire and torch.equal(w, (x * 0.5).to(wire))
+    out = torch.empty_like(x)
+    hip_unpack(w, out, 0.25)
+    assert torch.equal(out, w.float() * 0.25)
