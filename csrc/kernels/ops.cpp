@@ -8,6 +8,9 @@ namespace mihvd {
 void conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1);
 void conv2_fwd(const at::Tensor& a1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
+void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                const at::Tensor& w1bf, const at::Tensor& b1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a1,
+                at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2);
 void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart);
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
@@ -73,6 +76,11 @@ void conv1_fwd_op(const Tensor& x, const OptT& rows, const OptT& state, const Te
 }
 void conv2_fwd_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2) {
   mihvd::conv2_fwd(a1, w2, b2, a2, idx2);
+}
+void conv12_fwd_op(const Tensor& x, const c10::optional<Tensor>& rows, const c10::optional<Tensor>& state,
+                   const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2, Tensor a1, Tensor idx1,
+                   Tensor a2, Tensor idx2) {
+  mihvd::conv12_fwd(x, rows, state, w1, b1, w2, b2, a1, idx1, a2, idx2);
 }
 void fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::fc1_fwd(a2, w3, zpart); }
 void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
@@ -152,6 +160,8 @@ void bump_step_op(Tensor step) { mihvd::bump_step_(step); }
 TORCH_LIBRARY(mihvd, m) {
   m.def("conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
   m.def("conv2_fwd(Tensor a1, Tensor w2bf, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
+  m.def("conv12_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1bf, Tensor b1, Tensor w2bf, Tensor b2, "
+        "Tensor(a!) a1, Tensor(b!) idx1, Tensor(c!) a2, Tensor(d!) idx2) -> ()");
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
@@ -196,6 +206,7 @@ TORCH_LIBRARY(mihvd, m) {
 TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("conv1_fwd", &conv1_fwd_op);
   m.impl("conv2_fwd", &conv2_fwd_op);
+  m.impl("conv12_fwd", &conv12_fwd_op);
   m.impl("fc1_fwd", &fc1_fwd_op);
   m.impl("head_fwd_bwd", &head_op);
   m.impl("fc1_wgrad", &fc1_wgrad_op);

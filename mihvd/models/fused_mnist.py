@@ -1,10 +1,12 @@
 """Fused, graph-replayed data-parallel training step for the reference MNIST CNN on MI355X.
 
-This is the flagship path (bench.py ``--impl fused``). One step is nine HIP launches (+ the RCCL
+This is the flagship path (bench.py ``--impl fused``). One step is seven HIP launches at world size 1 (+ the RCCL
 allreduce when ``size() > 1``), all hand-written CDNA4 kernels from ``csrc/kernels``:
 
-    conv1_fwd   direct conv + bias + ReLU + 2x2 max-pool (+argmax)             [VALU]
-    conv2_fwd   implicit GEMM, pool-window-major M, pool/ReLU in registers    [MFMA bf16]
+    conv12_fwd  conv1 (implicit GEMM, K = 25 taps in one MFMA step) -> pooled activations
+                written into conv2's LDS image -> conv2 implicit GEMM, pool-window-major M,
+                bias/ReLU/pool/argmax in registers (MIHVD_CONV12=0: two launches,
+                conv1 as an fp32 VALU direct convolution)                  [MFMA bf16]
     fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs                    [MFMA bf16]
     head        slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
     fc1_wgrad   dW3 -> fusion buffer | db3 | dW4/db4 | db4 (bucket "fc" complete) [MFMA bf16]
@@ -195,6 +197,9 @@ class FusedMNISTTrainer:
         # last reader of W3 (fc1_dgrad) and overlaps the conv backward and the next step's convs.
         self.pipeline = os.environ.get("MIHVD_ADAM_PIPELINE", "0") == "1" and not self.gather
         self.adam_blocks = int(os.environ.get("MIHVD_ADAM_BLOCKS", "0"))
+        # conv1 + conv2 forward in one launch (conv1 on MFMA with bf16 operands); 0 = separate
+        # launches with conv1 as an fp32 VALU convolution
+        self.conv12 = os.environ.get("MIHVD_CONV12", "1") != "0"
         # MIHVD_FUSE_W3_ADAM=1: the dW3 tiles of fc1_wgrad apply Adam to dense/kernel (98 %
         # of the parameters) from their accumulators, so dW3 never goes through HBM and the flat
         # optimizer only covers the other 65 K parameters. Needs dW3 to be complete on this rank:
@@ -287,10 +292,7 @@ class FusedMNISTTrainer:
         o = self.ops
         st = self.state
         main = torch.cuda.current_stream(self.device)
-        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
-                    self.a1, self.idx1)
-        o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
-                    self.a2, self.idx2)
+        self._conv_forward(x, rows, st)
         if self._fc_update_pending:
             # the previous step's "fc" Adam update (side stream) overlapped the two convolutions above
             main.wait_stream(self._side)
@@ -374,10 +376,7 @@ class FusedMNISTTrainer:
         st = self.state
         main = torch.cuda.current_stream(self.device)
         side = self._side
-        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
-                    self.a1, self.idx1)
-        o.conv2_fwd(self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), self.pview("conv_layer2/conv2d/bias"),
-                    self.a2, self.idx2)
+        self._conv_forward(x, rows, st)
         # (an all-to-all of only the column slice each rank needs would move 1/N of these bytes,
         # but torch's RCCL process group cannot capture all_to_all_single into a HIP graph: its
         # watchdog queries the captured event and aborts)
@@ -446,6 +445,19 @@ class FusedMNISTTrainer:
                                 self.gview("dense_1/kernel"), self.gview("dense_1/bias"), roles, dz_all, a2_all,
                                 self.params[w3], self.m[w3], self.v[w3], self.shadow[w3], self.state, self.lr, b1, b2,
                                 self.eps, 1.0 / self.world, self.rule, self.keep_w3_grad)
+
+    def _conv_forward(self, x, rows, st):
+        o = self.ops
+        w2 = self.pview("conv_layer2/conv2d/kernel", self.shadow)
+        b2 = self.pview("conv_layer2/conv2d/bias")
+        if self.conv12:
+            # one launch: conv1 on MFMA into conv2's LDS input image (a1/idx1 still stored for the backward)
+            o.conv12_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel", self.shadow),
+                         self.pview("conv_layer1/conv2d/bias"), w2, b2, self.a1, self.idx1, self.a2, self.idx2)
+            return
+        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
+                    self.a1, self.idx1)
+        o.conv2_fwd(self.a1, w2, b2, self.a2, self.idx2)
 
     def _conv_backward(self, x, rows, st):
         o = self.ops

@@ -1,7 +1,7 @@
 """Autograd-facing wrappers of the CDNA4 kernels (``torch.ops.mihvd.*``) for the MNIST CNN.
 
-* ``mnist_logits(model, images)`` — inference forward through the HIP kernels (conv1, conv2 with
-  fused bias/ReLU/pool, fc1 split-K MFMA) and a small torch epilogue for fc2.
+* ``mnist_logits(model, images)`` — inference forward through the HIP kernels (conv1 + conv2 in one
+  launch with fused bias/ReLU/pool, fc1 split-K MFMA) and a small torch epilogue for fc2.
 * ``fused_mnist_loss(model, images, labels)`` — the whole forward+backward in HIP kernels,
   exposed as one autograd node: it returns the mean softmax cross-entropy and, on ``backward()``,
   hands the kernel-computed parameter gradients to autograd. This is how a stock optimizer loop
@@ -9,6 +9,8 @@
   fused graph-replayed loop lives in ``mihvd.models.fused_mnist``.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -37,10 +39,21 @@ class _Workspace:
                 stats=torch.empty(B, 2, **f32), g2=torch.empty(B, 3136, **bf),
                 cpart=torch.empty(B, 896, **f32), slab=torch.empty(int(ops.conv2_wgrad_groups(B)), 51200, **f32),
                 state=torch.zeros(4, device=device, dtype=torch.int64),
-                w2bf=torch.empty(51200, **bf), w3bf=torch.empty(3136 * 1024, **bf),
+                w1bf=torch.empty(800, **bf), w2bf=torch.empty(51200, **bf), w3bf=torch.empty(3136 * 1024, **bf),
             )
             cls._cache[key] = ws
         return ws
+
+
+def _conv_forward(ops, ws, x, st, w1, b1, b2):
+    """conv1 + conv2 forward: one conv12 launch (conv1 on MFMA, bf16 operands, like the fused
+    trainer) unless MIHVD_CONV12=0 (conv1 as an fp32 VALU convolution, then conv2)."""
+    if os.environ.get("MIHVD_CONV12", "1") != "0":
+        ops.scale_cast_bf16(w1.reshape(-1), ws["w1bf"], 1.0)
+        ops.conv12_fwd(x, None, st, ws["w1bf"], b1, ws["w2bf"], b2, ws["a1"], ws["idx1"], ws["a2"], ws["idx2"])
+        return
+    ops.conv1_fwd(x, None, st, w1.reshape(-1), b1, ws["a1"], ws["idx1"])
+    ops.conv2_fwd(ws["a1"], ws["w2bf"], b2, ws["a2"], ws["idx2"])
 
 
 def _params(model):
@@ -60,8 +73,7 @@ def mnist_logits(model, images: torch.Tensor) -> torch.Tensor:
     ws = _Workspace.get(x.device, B)
     ops.scale_cast_bf16(w2.detach().reshape(-1), ws["w2bf"], 1.0)
     ops.scale_cast_bf16(w3.detach().reshape(-1), ws["w3bf"], 1.0)
-    ops.conv1_fwd(x, None, None, w1.detach().reshape(-1), b1.detach(), ws["a1"], ws["idx1"])
-    ops.conv2_fwd(ws["a1"], ws["w2bf"], b2.detach(), ws["a2"], ws["idx2"])
+    _conv_forward(ops, ws, x, None, w1.detach(), b1.detach(), b2.detach())
     ops.fc1_fwd(ws["a2"], ws["w3bf"], ws["zpart"])
     h = torch.relu(ws["zpart"].sum(0) + b3)
     return (h.to(torch.bfloat16).float() @ w4 + b4).float()
@@ -78,8 +90,7 @@ class _FusedMNISTLoss(torch.autograd.Function):
         ops.scale_cast_bf16(w2.reshape(-1), ws["w2bf"], 1.0)
         ops.scale_cast_bf16(w3.reshape(-1), ws["w3bf"], 1.0)
         st = ws["state"]
-        ops.conv1_fwd(x, None, st, w1.reshape(-1), b1, ws["a1"], ws["idx1"])
-        ops.conv2_fwd(ws["a1"], ws["w2bf"], b2, ws["a2"], ws["idx2"])
+        _conv_forward(ops, ws, x, st, w1, b1, b2)
         ops.fc1_fwd(ws["a2"], ws["w3bf"], ws["zpart"])
         ops.head_fwd_bwd(ws["zpart"], b3, w4, b4, labels, None, st, int(seed), float(dropout), ws["h"], ws["dz"],
                          ws["dlog"], ws["stats"])

@@ -39,6 +39,10 @@ def main():
                                          tr.pview("conv_layer1/conv2d/bias"), tr.a1, tr.idx1),
         "conv2_fwd": lambda: o.conv2_fwd(tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh),
                                          tr.pview("conv_layer2/conv2d/bias"), tr.a2, tr.idx2),
+        "conv12_fwd": lambda: o.conv12_fwd(tr.x_buf, None, st, tr.pview("conv_layer1/conv2d/kernel", sh),
+                                           tr.pview("conv_layer1/conv2d/bias"),
+                                           tr.pview("conv_layer2/conv2d/kernel", sh),
+                                           tr.pview("conv_layer2/conv2d/bias"), tr.a1, tr.idx1, tr.a2, tr.idx2),
         "fc1_fwd": lambda: o.fc1_fwd(tr.a2, tr.pview("dense/kernel", sh), tr.zpart),
         "head": lambda: o.head_fwd_bwd(tr.zpart, tr.pview("dense/bias"), tr.pview("dense_1/kernel"),
                                        tr.pview("dense_1/bias"), tr.y_buf, None, st, tr.seed, 0.5, tr.h, tr.dz, tr.dlog,
@@ -145,7 +149,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     res["step"] = e0.elapsed_time(e1) * 1000.0 / 200
-    step_ops = ["conv1_fwd", "conv2_fwd", "fc1_fwd", "head", "fc1_dgrad"]
+    step_ops = (["conv12_fwd"] if tr.conv12 else ["conv1_fwd", "conv2_fwd"]) + ["fc1_fwd", "head", "fc1_dgrad"]
     if tr.fused_opt:
         step_ops += ["fc1_wgrad", "conv2_bwd_adam+reduce_adam"]
     elif tr.fuse_w3:

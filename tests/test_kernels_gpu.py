@@ -73,6 +73,41 @@ def test_conv2_fwd(ops, B):
     assert (idx.long()[pos] == rd.reshape(B, 3136)[pos]).float().mean() > 0.99
 
 
+@pytest.mark.parametrize("B", [7, 100])
+def test_conv12_fwd(ops, B):
+    """conv1 on MFMA (bf16 operands) feeding conv2 through LDS in one launch: a1 matches the fp32
+    reference on bf16-rounded inputs, a2/idx2 are bitwise those of conv2_fwd on the same a1, and the
+    data gather (rows + device step) picks the same images as conv1_fwd."""
+    g = torch.Generator(device="cuda").manual_seed(12)
+    n_pool = 300
+    xs = torch.rand(n_pool, 784, device="cuda", generator=g)
+    rows = torch.randperm(n_pool, device="cuda", generator=g).to(torch.int32)
+    st = torch.zeros(4, dtype=torch.int64, device="cuda")
+    st[0] = 2
+    w1 = torch.randn(5, 5, 1, 32, device="cuda", generator=g) * 0.2
+    b1 = torch.randn(32, device="cuda", generator=g) * 0.1
+    w2 = bf(torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    b2 = torch.randn(64, device="cuda", generator=g) * 0.1
+    a1 = torch.empty(B, 14, 14, 32, device="cuda", dtype=torch.bfloat16)
+    idx1 = torch.empty(B, 14, 14, 32, device="cuda", dtype=torch.uint8)
+    a2 = torch.empty(B, 3136, device="cuda", dtype=torch.bfloat16)
+    idx2 = torch.empty(B, 3136, device="cuda", dtype=torch.uint8)
+    ops.conv12_fwd(xs, rows, st, w1.reshape(800).to(torch.bfloat16), b1, w2.reshape(-1), b2, a1, idx1, a2, idx2)
+    xb = xs[rows[(2 * B + torch.arange(B, device="cuda")) % n_pool].long()]
+    ref, rd, _ = ref_conv_pool(bf(xb).view(B, 28, 28, 1), bf(w1), b1)
+    assert rel_err(a1, ref) < 5e-3
+    pos = ref > 1e-2
+    assert (idx1.long()[pos] == rd[pos]).float().mean() > 0.99
+    a2r = torch.empty_like(a2)
+    idx2r = torch.empty_like(idx2)
+    ops.conv2_fwd(a1, w2.reshape(-1), b2, a2r, idx2r)
+    assert torch.equal(a2, a2r) and torch.equal(idx2, idx2r)
+    # same images as the fp32 VALU conv1 with the same gather
+    a1v = torch.empty_like(a1)
+    ops.conv1_fwd(xs, rows, st, w1.reshape(800), b1, a1v, torch.empty_like(idx1))
+    assert rel_err(a1, a1v) < 1e-2
+
+
 @pytest.mark.parametrize("B", [7, 100, 128])
 def test_fc1_fwd(ops, B):
     g = torch.Generator(device="cuda").manual_seed(3)
@@ -263,12 +298,16 @@ def _pool_by_index(y_nhwc, idx):
     return y.gather(-1, idx.long().unsqueeze(-1)).squeeze(-1)
 
 
-def _emulated_reference(params, x, y, idx1, idx2):
-    """The fused step's exact math in fp32 autograd: same bf16 rounding points, same pool routing."""
+def _emulated_reference(params, x, y, idx1, idx2, conv1_bf16=False):
+    """The fused step's exact math in fp32 autograd: same bf16 rounding points, same pool routing
+    (conv1_bf16: conv1 reads bf16-rounded images and weights, as the one-launch conv12 does)."""
     P = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
     B = x.shape[0]
-    y1 = F.conv2d(x.view(B, 1, 28, 28), P["conv_layer1/conv2d/kernel"].permute(3, 2, 0, 1),
-                  P["conv_layer1/conv2d/bias"], padding=2).permute(0, 2, 3, 1)
+    w1 = P["conv_layer1/conv2d/kernel"]
+    if conv1_bf16:
+        x, w1 = bf(x), _RoundFwd.apply(w1)
+    y1 = F.conv2d(x.view(B, 1, 28, 28), w1.permute(3, 2, 0, 1), P["conv_layer1/conv2d/bias"],
+                  padding=2).permute(0, 2, 3, 1)
     a1 = _RoundBF.apply(F.relu(_pool_by_index(y1, idx1)))
     w2 = _RoundFwd.apply(P["conv_layer2/conv2d/kernel"])
     y2 = F.conv2d(a1.permute(0, 3, 1, 2), w2.permute(3, 2, 0, 1), P["conv_layer2/conv2d/bias"], padding=2)
@@ -297,7 +336,7 @@ def test_fused_step_matches_emulated_reference(ops, B):
     params = {n: tr.pview(n).clone() for n in TF_PARAM_ORDER}
     out = tr.train_step(x, y)
     torch.cuda.synchronize()
-    loss, grads = _emulated_reference(params, x, y, tr.idx1, tr.idx2)
+    loss, grads = _emulated_reference(params, x, y, tr.idx1, tr.idx2, conv1_bf16=tr.conv12)
     assert abs(out["loss"].item() - loss.item()) < 1e-3 * max(1.0, loss.item())
     for name in TF_PARAM_ORDER:
         e = rel_err(tr.gview(name), grads[name])
