@@ -527,6 +527,17 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
   if ((int)blockIdx.x >= CR_SLAB_BLOCKS) {
     float* r1 = reinterpret_cast<float*>(r4);
     const int o = ((int)blockIdx.x - CR_SLAB_BLOCKS) * 64 + (t & 63), rg = t >> 6;
+    // optimizer operands first: their loads fly with the reduction's instead of after it
+    int64_t f = 0;
+    float pv = 0.f, mv = 0.f, vv = 0.f;
+    if constexpr (ADAM) {
+      if (t < 64) {
+        f = o < CP_DB1 ? ra.o_w1 + o : o < CP_DB2 ? ra.o_b1 + (o - CP_DB1) : ra.o_b2 + (o - CP_DB2);
+        pv = ra.ad.p[f];
+        mv = ra.ad.m[f];
+        vv = ra.ad.v[f];
+      }
+    }
     float acc = 0.f;
     for (int r0 = rg * 8; r0 < B; r0 += 32) {
       float v[8];
@@ -546,8 +557,6 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
       else if (o < CP_DB2) gb1[o - CP_DB1] = s;
       else gb2[o - CP_DB2] = s;
       if constexpr (ADAM) {
-        const int64_t f = o < CP_DB1 ? ra.o_w1 + o : o < CP_DB2 ? ra.o_b1 + (o - CP_DB1) : ra.o_b2 + (o - CP_DB2);
-        float pv = ra.ad.p[f], mv = ra.ad.m[f], vv = ra.ad.v[f];
         adam1(pv, mv, vv, s, c);
         ra.ad.p[f] = pv;
         ra.ad.m[f] = mv;
@@ -558,6 +567,15 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
     return;
   }
   const int o = (int)blockIdx.x * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
+  float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
+  if constexpr (ADAM) {
+    if (t < 64) {  // optimizer operands in flight with the slab loads
+      const int64_t f4 = ra.o_w2 / 4 + min(o, 12799);
+      pp = reinterpret_cast<const float4*>(ra.ad.p)[f4];
+      mm = reinterpret_cast<const float4*>(ra.ad.m)[f4];
+      vv = reinterpret_cast<const float4*>(ra.ad.v)[f4];
+    }
+  }
   float4 v[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -578,9 +596,6 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
     reinterpret_cast<float4*>(gW2)[o] = g;
     if constexpr (ADAM) {
       const int64_t f4 = ra.o_w2 / 4 + o;
-      float4 pp = reinterpret_cast<const float4*>(ra.ad.p)[f4];
-      float4 mm = reinterpret_cast<const float4*>(ra.ad.m)[f4];
-      float4 vv = reinterpret_cast<const float4*>(ra.ad.v)[f4];
       const uint2 sh = adam4(pp, mm, vv, g, c);
       reinterpret_cast<float4*>(ra.ad.p)[f4] = pp;
       reinterpret_cast<float4*>(ra.ad.m)[f4] = mm;
@@ -639,10 +654,19 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     const int grid = std::max(n_conv + 8, ncu);
+    // The tail-only blocks stream for the whole conv phase, so they first take a head range of
+    // the update alone (MIHVD_TAIL_HEAD: its fraction of the update, tuned on MI355X).
+    static const double head_frac = [] {
+      const char* e = getenv("MIHVD_TAIL_HEAD");
+      return e ? atof(e) : 0.2;
+    }();
+    AdamTail at = *tail;
+    at.first_free = n_conv;
+    at.head = (int64_t)(head_frac * (double)((at.n4 + 255) / 256));
     conv2_bwd_kernel<true><<<grid, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, *tail);
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at);
   }
 }
 
@@ -673,7 +697,7 @@ void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tens
   TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_WORDS, "conv2_bwd_adam: state");
   AdamTail at{p3.data_ptr<float>(), g3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(),
               (u16*)shadow3.data_ptr(), n / 4, state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2,
-              (float)eps, (float)grad_scale, (int)rule};
+              (float)eps, (float)grad_scale, (int)rule, 0, 0};
   conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, &at);
 }
 
