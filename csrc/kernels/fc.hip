@@ -182,11 +182,11 @@ constexpr int DG_ROWS = 32, DG_JT = FC1_K / 64;         // 49 feature tiles
 constexpr int DG_DSTR = FC1_N + 8;                      // dz image row stride (2064 B)
 constexpr int DG_LDS = DG_ROWS * DG_DSTR * 2;           // 66,048 B
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) fc1_dgrad_kernel(const u16* __restrict__ dz, const u16* __restrict__ w3,
-                                                        const u16* __restrict__ a2, u16* __restrict__ g2, int B, int G) {
-  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+__device__ __forceinline__ void fc1_dgrad_block(int bx, const u16* __restrict__ dz, const u16* __restrict__ w3,
+                                                const u16* __restrict__ a2, u16* __restrict__ g2, int B, int G,
+                                                u16* smem) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int xcd = bx & 7, slot = bx >> 3;
   const int mg = slot % G, jt = (slot / G) * 8 + xcd;
   if (jt >= DG_JT) return;
   const int j0 = jt * 64, m0 = mg * DG_ROWS;
@@ -246,6 +246,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   }
 }
 
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) fc1_dgrad_kernel(
+    const u16* __restrict__ dz, const u16* __restrict__ w3, const u16* __restrict__ a2, u16* __restrict__ g2, int B,
+    int G) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  fc1_dgrad_block(blockIdx.x, dz, w3, a2, g2, B, G, smem);
+}
+
 // ------------------------------------------------------------------------------------------ //
 // fc1_wgrad roles (dispatch order: the 33 small blocks first, then the 784 dW3 tiles):
 //   wgrad : 64x64 tile of dW3 = a2^T dz   (K = batch, zero padded)
@@ -262,19 +269,18 @@ constexpr int FB_LDS_WG = 2 * MAXB * FB_TSTR * 2;                // 36,864 B
 // gradient is stored too only when write_grad is set (tests). Valid whenever the tile's dW3 is
 // already the full data-parallel sum: world size 1, or the all-gathered factors (Kw = size * B).
 template <bool ADAM>
-__global__ void __launch_bounds__(256) fc1_wgrad_kernel(
-    const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
-    const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
-    float* __restrict__ gW4, float* __restrict__ gb4, int B, int tile_base, int n_small, AdamArgs ad, int write_grad,
-    int a2s, int a2c0) {
-  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+__device__ __forceinline__ void fc1_wgrad_block(
+    int bx, const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h,
+    const float* __restrict__ dlog, const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw,
+    float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4, float* __restrict__ gb4, int B,
+    int tile_base, int n_small, const AdamArgs& ad, int write_grad, int a2s, int a2c0, u16* smem) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
   // The small-reduction blocks (n_small = 33, or 0 when they are not launched) come first in
   // dispatch order so they run alongside the dW3 tiles instead of trailing them.
   // dW3 tiles launched: [tile_base, tile_base + gridDim.x - n_small) (a row-slice of dW3 when the
   // optimizer of dense/kernel is sharded across ranks).
-  int bid = blockIdx.x;
+  int bid = bx;
   bid = bid < n_small ? FB_WGRAD + bid : tile_base + (bid - n_small);
   if (bid < FB_WGRAD) {
     // dW3^T[n][j] tile = sum_k dzw[k][n] a2w[k][j] over Kw rows (the local batch, or the batch of
@@ -443,6 +449,34 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
   }
 }
 
+template <bool ADAM>
+__global__ void __launch_bounds__(256) fc1_wgrad_kernel(
+    const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
+    const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
+    float* __restrict__ gW4, float* __restrict__ gb4, int B, int tile_base, int n_small, AdamArgs ad, int write_grad,
+    int a2s, int a2c0) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  fc1_wgrad_block<ADAM>(blockIdx.x, dz, a2, h, dlog, dzw, a2w, Kw, gW3, gb3, gW4, gb4, B, tile_base, n_small, ad,
+                        write_grad, a2s, a2c0, smem);
+}
+
+// fc1_bwd: the dgrad tiles and every fc1_wgrad role (local batch) in one launch. The dgrad blocks
+// come first (they are the longest and keep the blockIdx -> XCD map their tiles rely on).
+__global__ void __launch_bounds__(256) fc1_bwd_kernel(const u16* __restrict__ dz, const u16* __restrict__ a2,
+                                                      const u16* __restrict__ h, const float* __restrict__ dlog,
+                                                      const u16* __restrict__ w3, u16* __restrict__ g2,
+                                                      float* __restrict__ gW3, float* __restrict__ gb3,
+                                                      float* __restrict__ gW4, float* __restrict__ gb4, int B, int G,
+                                                      int n_dg, int n_small) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  if ((int)blockIdx.x < n_dg) {
+    fc1_dgrad_block(blockIdx.x, dz, w3, a2, g2, B, G, smem);
+    return;
+  }
+  fc1_wgrad_block<false>((int)blockIdx.x - n_dg, dz, a2, h, dlog, dz, a2, B, gW3, gb3, gW4, gb4, B, 0, n_small,
+                         AdamArgs{}, 1, FC1_K, 0, smem);
+}
+
 // ------------------------------------------------------------------------------------------ //
 #define MIHVD_MT_SWITCH(MTV, ...)                         \
   switch (MTV) {                                          \
@@ -599,6 +633,33 @@ void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a
   set_max_lds(fc1_dgrad_kernel, DG_LDS);
   fc1_dgrad_kernel<<<grid, 256, DG_LDS, stream>>>((const u16*)dz.data_ptr(), (const u16*)w3bf.data_ptr(),
                                                    (const u16*)a2.data_ptr(), (u16*)g2.data_ptr(), B, G);
+}
+
+// fc1_wgrad (every role, local batch) + fc1_dgrad in one launch (fc1_bwd_kernel).
+// roles as fc1_wgrad: bit 0 = the dW3 tiles, bit 1 = db3 / dW4 / db4.
+void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
+             const at::Tensor& w3bf, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& g2,
+             int64_t roles) {
+  TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_bwd: roles must be 1, 2 or 3");
+  const int B = dz.size(0);
+  TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_bwd: batch");
+  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N && dz.is_contiguous(), "fc1_bwd: dz");
+  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_bwd: a2");
+  TORCH_CHECK(h.numel() == (int64_t)B * FC1_N && h.dtype() == at::kBFloat16 && dlog.numel() == B * 10, "fc1_bwd: h/dlog");
+  TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_bwd: w3");
+  TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_bwd: gW3");
+  TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_bwd: fc grads");
+  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * FC1_K && g2.is_contiguous(), "fc1_bwd: g2");
+  const int G = (B + DG_ROWS - 1) / DG_ROWS;
+  const int n_dg = 8 * ((DG_JT + 7) / 8) * G;
+  const int n_small = (roles & 2) ? FB_TOTAL - FB_WGRAD : 0;
+  const int grid = n_dg + n_small + ((roles & 1) ? FB_WGRAD : 0);
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  set_max_lds(fc1_bwd_kernel, DG_LDS);
+  fc1_bwd_kernel<<<grid, 256, DG_LDS, stream>>>(
+      (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
+      (const u16*)w3bf.data_ptr(), (u16*)g2.data_ptr(), gW3.data_ptr<float>(), gb3.data_ptr<float>(),
+      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg, n_small);
 }
 
 }  // namespace mihvd

@@ -12,6 +12,9 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
                 const at::Tensor& w1bf, const at::Tensor& b1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a1,
                 at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2);
 void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart);
+void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
+             const at::Tensor& w3bf, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& g2,
+             int64_t roles);
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats);
@@ -81,6 +84,10 @@ void conv12_fwd_op(const Tensor& x, const c10::optional<Tensor>& rows, const c10
                    const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2, Tensor a1, Tensor idx1,
                    Tensor a2, Tensor idx2) {
   mihvd::conv12_fwd(x, rows, state, w1, b1, w2, b2, a1, idx1, a2, idx2);
+}
+void fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, const Tensor& w3, Tensor gW3,
+               Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles) {
+  mihvd::fc1_bwd(dz, a2, h, dlog, w3, gW3, gb3, gW4, gb4, g2, roles);
 }
 void fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::fc1_fwd(a2, w3, zpart); }
 void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
@@ -162,6 +169,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("conv2_fwd(Tensor a1, Tensor w2bf, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
   m.def("conv12_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1bf, Tensor b1, Tensor w2bf, Tensor b2, "
         "Tensor(a!) a1, Tensor(b!) idx1, Tensor(c!) a2, Tensor(d!) idx2) -> ()");
+  m.def("fc1_bwd(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor w3bf, Tensor(a!) gW3, Tensor(b!) gb3, "
+        "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3) -> ()");
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
@@ -207,6 +216,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("conv1_fwd", &conv1_fwd_op);
   m.impl("conv2_fwd", &conv2_fwd_op);
   m.impl("conv12_fwd", &conv12_fwd_op);
+  m.impl("fc1_bwd", &fc1_bwd_op);
   m.impl("fc1_fwd", &fc1_fwd_op);
   m.impl("head_fwd_bwd", &head_op);
   m.impl("fc1_wgrad", &fc1_wgrad_op);

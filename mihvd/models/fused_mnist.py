@@ -200,6 +200,8 @@ class FusedMNISTTrainer:
         # conv1 + conv2 forward in one launch (conv1 on MFMA with bf16 operands); 0 = separate
         # launches with conv1 as an fp32 VALU convolution
         self.conv12 = os.environ.get("MIHVD_CONV12", "1") != "0"
+        # fc1 dgrad tiles and the fc1 wgrad roles in one launch (0 = two launches)
+        self.fc1_merged = os.environ.get("MIHVD_FC1_BWD", "1") != "0"
         # MIHVD_FUSE_W3_ADAM=1: the dW3 tiles of fc1_wgrad apply Adam to dense/kernel (98 %
         # of the parameters) from their accumulators, so dW3 never goes through HBM and the flat
         # optimizer only covers the other 65 K parameters. Needs dW3 to be complete on this rank:
@@ -302,9 +304,14 @@ class FusedMNISTTrainer:
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         if self.fused_opt:
             b1, b2 = self.betas
-            o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
-                        self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
-            o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)  # last reader of W3
+            if self.fc1_merged:  # dgrad tiles and every wgrad role in one launch
+                o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.pview("dense/kernel", self.shadow),
+                          self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
+                          self.gview("dense_1/bias"), self.g2)
+            else:
+                o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
+                            self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
+                o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)  # last reader of W3
             w3 = slice(W3_START, FLAT_NUMEL)
             o.conv2_bwd_adam(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows,
                              st, self.idx1, self.slab, self.cpart, self.params[w3], self.grads[w3], self.m[w3],
@@ -396,8 +403,11 @@ class FusedMNISTTrainer:
         gW3 = self.gview("dense/kernel")
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
                  self.gview("dense_1/bias"))
-        o.fc1_wgrad(*small, 2)  # db3, dW4, db4 of the local batch
-        o.fc1_dgrad(self.dz, self.w3_shadow(), self.a2, self.g2)
+        if self.fc1_merged:  # db3, dW4, db4 of the local batch + the dgrad tiles, one launch
+            o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2)
+        else:
+            o.fc1_wgrad(*small, 2)  # db3, dW4, db4 of the local batch
+            o.fc1_dgrad(self.dz, self.w3_shadow(), self.a2, self.g2)
         self._conv_backward(x, rows, st)
         main.wait_stream(side)   # both gathers done: the communicator is free
         side.wait_stream(main)

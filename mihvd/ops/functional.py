@@ -94,8 +94,7 @@ class _FusedMNISTLoss(torch.autograd.Function):
         ops.fc1_fwd(ws["a2"], ws["w3bf"], ws["zpart"])
         ops.head_fwd_bwd(ws["zpart"], b3, w4, b4, labels, None, st, int(seed), float(dropout), ws["h"], ws["dz"],
                          ws["dlog"], ws["stats"])
-        ops.fc1_wgrad(ws["dz"], ws["a2"], ws["h"], ws["dlog"], gW3, gb3, gW4, gb4)
-        ops.fc1_dgrad(ws["dz"], ws["w3bf"], ws["a2"], ws["g2"])
+        ops.fc1_bwd(ws["dz"], ws["a2"], ws["h"], ws["dlog"], ws["w3bf"], gW3, gb3, gW4, gb4, ws["g2"])
         ops.conv2_bwd(ws["g2"], ws["idx2"], ws["a1"], ws["w2bf"], x, None, st, ws["idx1"], ws["slab"], ws["cpart"])
         ops.conv2_wgrad_reduce(ws["slab"], ws["cpart"], B, gW2.reshape(-1), gW1.reshape(-1), gb1, gb2)
         st[0] += 1  # next call draws a fresh dropout mask

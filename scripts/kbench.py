@@ -50,6 +50,8 @@ def main():
         "fc1_wgrad": lambda: o.fc1_wgrad(tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"),
                                          tr.gview("dense_1/kernel"), tr.gview("dense_1/bias")),
         "fc1_dgrad": lambda: o.fc1_dgrad(tr.dz, tr.pview("dense/kernel", sh), tr.a2, tr.g2),
+        "fc1_bwd": lambda: o.fc1_bwd(tr.dz, tr.a2, tr.h, tr.dlog, tr.pview("dense/kernel", sh), tr.gview("dense/kernel"),
+                                     tr.gview("dense/bias"), tr.gview("dense_1/kernel"), tr.gview("dense_1/bias"), tr.g2),
         "conv2_bwd": lambda: o.conv2_bwd(tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf,
                                          None, st, tr.idx1, tr.slab, tr.cpart),
         "conv2_wgrad_reduce": lambda: o.conv2_wgrad_reduce(tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"),
@@ -151,7 +153,8 @@ def main():
     res["step"] = e0.elapsed_time(e1) * 1000.0 / 200
     step_ops = (["conv12_fwd"] if tr.conv12 else ["conv1_fwd", "conv2_fwd"]) + ["fc1_fwd", "head", "fc1_dgrad"]
     if tr.fused_opt:
-        step_ops += ["fc1_wgrad", "conv2_bwd_adam+reduce_adam"]
+        step_ops = [k for k in step_ops if not (tr.fc1_merged and k == "fc1_dgrad")]
+        step_ops += ["fc1_bwd" if tr.fc1_merged else "fc1_wgrad", "conv2_bwd_adam+reduce_adam"]
     elif tr.fuse_w3:
         step_ops += ["fc1_wgrad_adam", "conv2_bwd", "conv2_wgrad_reduce", "adam_small"]
     else:

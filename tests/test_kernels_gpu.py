@@ -201,6 +201,15 @@ def test_fc1_bwd(ops, B):
     assert rel_err(gb3, dz.sum(0)) < 1e-4
     assert rel_err(gW4, h.t() @ dlog) < 1e-4
     assert rel_err(gb4, dlog.sum(0)) < 1e-4
+    # the one-launch fc1_bwd runs the same block code: bitwise equal to the two launches
+    ops.fc1_wgrad(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, gW3, gb3, gW4, gb4)
+    outs = [torch.full_like(t, float("nan")) for t in (gW3, gb3, gW4, gb4)]
+    g2m = torch.empty_like(g2)
+    ops.fc1_bwd(dz.to(torch.bfloat16), a2.to(torch.bfloat16), h.to(torch.bfloat16), dlog, w3.to(torch.bfloat16),
+                *outs, g2m, 3)
+    assert torch.equal(g2m, g2)
+    for a, b in zip(outs, (gW3, gb3, gW4, gb4)):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("B", [7, 100])
