@@ -1,24 +1,27 @@
 """Fused, graph-replayed data-parallel training step for the reference MNIST CNN on MI355X.
 
-This is the flagship path (bench.py ``--impl fused``). One step is seven HIP launches at world size 1 (+ the RCCL
-allreduce when ``size() > 1``), all hand-written CDNA4 kernels from ``csrc/kernels``:
+This is the flagship path (bench.py ``--impl fused``). At world size 1 a step is six HIP launches,
+all hand-written CDNA4 kernels from ``csrc/kernels``:
 
     conv12_fwd  conv1 (implicit GEMM, K = 25 taps in one MFMA step) -> pooled activations
                 written into conv2's LDS image -> conv2 implicit GEMM, pool-window-major M,
                 bias/ReLU/pool/argmax in registers (MIHVD_CONV12=0: two launches,
-                conv1 as an fp32 VALU direct convolution)                  [MFMA bf16]
+                conv1 as an fp32 VALU direct convolution)                      [MFMA bf16]
     fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs                    [MFMA bf16]
     head        slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
-    fc1_wgrad   dW3 -> fusion buffer | db3 | dW4/db4 | db4 (bucket "fc" complete) [MFMA bf16]
-    --- size() > 1: bucket "fc" (98.4 % of the gradient bytes) is allreduced from here on a
-        side stream (MIHVD_OVERLAP=1, default) while the conv backward runs ---
-    fc1_dgrad   full-K dz.W3^T tiles (W3 rows in registers, dz in LDS, XCD-aware tile map)
-                with the pooled-ReLU mask and bf16 cast fused: writes g2         [MFMA bf16]
+    fc1_bwd     full-K dz.W3^T tiles (W3 rows in registers, dz in LDS, XCD-aware tile map,
+                pooled-ReLU mask + bf16 cast fused: g2) and, in the same launch, dW3 tiles
+                -> fusion buffer | db3 | dW4 | db4 (MIHVD_FC1_BWD=0: two launches)  [MFMA bf16]
     conv2_bwd   dgrad (g2 routed through the pool argmax, ReLU mask) -> g1 on chip -> fused
                 conv1 wgrad (dW1/db1) | conv2 wgrad slabs | db2                  [MFMA bf16]
-    conv2_wgrad_reduce  dW2 = sum of the wgrad slabs
-    --- bucket "conv" allreduced; the optimizer waits for both buckets ---
-    adam_step   TF1 Adam over the flat fp32 buffer, 1/size averaging fused, bf16 shadow written
+                + the dense/kernel Adam update streaming in the launch tail
+    conv2_wgrad_reduce  dW2 = sum of the wgrad slabs + Adam for every other parameter
+
+With size() > 1 the data plane is either the factor gather (default: all-gather of the bf16
+factors a2/dz so every rank forms the exact all-sample dW3 for the rows whose optimizer it owns,
+then an all-gather of the updated bf16 rows) or bucketed allreduce of the flat gradient buffer
+(bucket "fc", 98.4 % of the bytes, reduced on a side stream while the conv backward runs); the
+optimizer then runs as separate adam_step launches.
 
 At N=1 everything runs on one stream (a fork/join inside a HIP graph costs more than the
 overlap it would buy when there is no collective to hide).
