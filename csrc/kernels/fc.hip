@@ -103,6 +103,14 @@ __global__ void __launch_bounds__(256) head_kernel(
     }
   }
   const float4 bb = *reinterpret_cast<const float4*>(b3 + n0);
+  // the label (step -> rows[] -> labels[]: dependent loads) is fetched now, so its latency hides
+  // under the fc2 partial sums instead of following the first barrier
+  int y = 0;
+  if (t < 64) {
+    int row = b;
+    if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
+    y = (int)labels[row];
+  }
   float z[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
   for (int s = 0; s < FC1_KS; ++s) {
@@ -130,9 +138,6 @@ __global__ void __launch_bounds__(256) head_kernel(
   __syncthreads();
   if (t < 64) {
     // one wave finishes the 10-way softmax; lanes 0..9 own a class each
-    int row = b;
-    if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-    const int y = (int)labels[row];
     const int c = min(lane, 9);
     const float lg = red[0][c] + red[1][c] + red[2][c] + red[3][c] + b4[c];
     const float v = lane < 10 ? lg : -INFINITY;
