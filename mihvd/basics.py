@@ -125,6 +125,11 @@ def init(comm=None, process_sets=None, config: Config | None = None):
             dev_index = int(os.environ.get("MIHVD_DEVICE_INDEX", topo.local_rank)) if elastic else topo.local_rank
             device = torch.device("cuda", dev_index % ndev)
             torch.cuda.set_device(device)
+        elif os.environ.get("MIHVD_GLOO_ON_GPU") == "1" and torch.cuda.device_count() > 0:
+            # rehearsal mode: gloo collectives between ranks that share the GPU(s) of one box
+            # (multi-rank code paths on a single-GPU machine; RCCL refuses two ranks per GPU)
+            device = torch.device("cuda", topo.local_rank % torch.cuda.device_count())
+            torch.cuda.set_device(device)
         else:
             device = torch.device("cpu")
         timeout = datetime.timedelta(seconds=cfg.timeout_s)

@@ -580,7 +580,8 @@ class FusedMNISTTrainer:
         torch.cuda.synchronize(self.device)
         if primary:
             self.steps_per_replay = steps_per_replay
-        if (self.op is not None and int(self.op) == 2) or self.debug_sync:  # Adasum / serialized: eager
+        if (self.op is not None and int(self.op) == 2) or self.debug_sync or self._host_collectives():
+            # Adasum / serialized mode / gloo collectives (host-side, not capturable): eager
             if primary:
                 self.graph = None
             return False
@@ -609,6 +610,13 @@ class FusedMNISTTrainer:
         if primary:
             self.graph = g
         return True
+
+    def _host_collectives(self) -> bool:
+        if not self.collectives:
+            return False
+        import torch.distributed as dist
+
+        return dist.is_initialized() and dist.get_backend() != "nccl"
 
     def run_graph(self, steps: int | None = None):
         """Advance ``steps_per_replay`` steps (or ``steps``, for which a graph was built with
