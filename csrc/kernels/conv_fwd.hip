@@ -91,13 +91,14 @@ constexpr int C2_WROW = 32 + 8;          // weight image row stride (elements): 
 constexpr int C2_W = 800 * C2_WROW;
 constexpr int C2_LDS_BYTES = (C2_IMG + C2_W) * 2;
 
-// The conv2 GEMM + pool epilogue of one (image b, 32-channel half) block, from the LDS images.
+// The conv2 GEMM + pool epilogue of one (image b, 32-channel half) block, from the LDS images,
+// with NW waves: wave w owns the M tiles w, w + NW, ... (13 tiles x 16 = 208 >= 196 pixels).
+template <int NW = 4>
 __device__ __forceinline__ void conv2_core(const u16* img, const u16* wim, const float* __restrict__ b2,
                                            u16* __restrict__ a2, uint8_t* __restrict__ idx2, int half, int b, int t) {
   const int lane = t & 63, wave = t >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  // This wave's M tiles: wave, wave+4, wave+8, (12 for wave 0). 13 tiles x 16 = 208 >= 196.
-  constexpr int MT = 4;
+  constexpr int MT = (13 + NW - 1) / NW;
   f32x4 acc[MT][2];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -105,14 +106,14 @@ __device__ __forceinline__ void conv2_core(const u16* img, const u16* wim, const
   int abase[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    const int tile = wave + 4 * i;
+    const int tile = wave + NW * i;
     int m = tile * 16 + lr;
     if (m >= 196) m = 0;  // padded rows read a valid pixel; their results are discarded
     const int win = m >> 2, d = m & 3;
     const int y = 2 * (win / 7) + (d >> 1), x = 2 * (win % 7) + (d & 1);
     abase[i] = (y * 18 + x) * 32 + 8 * lg;
   }
-  // Every wave computes 4 tiles (tiles 13..15 are dummies on clamped rows, discarded below): no
+  // Every wave computes MT tiles (tiles 13+ are dummies on clamped rows, discarded below): no
   // runtime guard around an MFMA, which would make hipcc shuttle the accumulators.
   const int q = lr >> 2, p = lr & 3;
   for (int kk = 0; kk < 25; ++kk) {  // (kh, kw): 32 input channels = one K step
@@ -131,7 +132,7 @@ __device__ __forceinline__ void conv2_core(const u16* img, const u16* wim, const
   // Epilogue: lane holds rows 4*lg..4*lg+3 of its tile = one pooling window, column lr.
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    const int tile = wave + 4 * i;
+    const int tile = wave + NW * i;
     const int win = tile * 4 + lg;
     if (win >= 49) continue;
 #pragma unroll
@@ -194,7 +195,8 @@ __global__ void __launch_bounds__(256) conv2_fwd_kernel(
 constexpr int C12_XW = 32;                                  // padded bf16 input image: 32 x 32
 constexpr int C12_LDS_BYTES = C2_LDS_BYTES + C12_XW * C12_XW * 2;
 
-__global__ void __launch_bounds__(256) conv12_fwd_kernel(
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) conv12_fwd_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const u16* __restrict__ w1bf, const float* __restrict__ b1, const u16* __restrict__ w2bf,
     const float* __restrict__ b2, u16* __restrict__ a1, uint8_t* __restrict__ idx1, u16* __restrict__ a2,
@@ -207,7 +209,8 @@ __global__ void __launch_bounds__(256) conv12_fwd_kernel(
   const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   // 1. loads. The weights do not depend on the data gather, so they are issued first and land
   //    while the dependent chain step -> rows[] -> image runs.
-  TileLoad<256, 13, 4> lw;
+  constexpr int T = NW * 64;
+  TileLoad<T, (3200 + T - 1) / T, 4> lw;
   lw.load(w2bf + half * 32, 64, 800, 800, t);
   // B[k][n] = W1[k = kh*5 + kw][n], k >= 25 zero: lane holds k = 8lg + j, n = 16nt + lr
   uint32_t wb[2][4];
@@ -227,25 +230,25 @@ __global__ void __launch_bounds__(256) conv12_fwd_kernel(
     row = rows[(int)((step * (int64_t)B + b) % n_pool)];
   }
   const float* xi = x + (int64_t)row * 784;
-  float xv[4];
+  float xv[1024 / T];
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int i = t + 256 * it, Y = (i >> 5) - 2, X = (i & 31) - 2;
+  for (int it = 0; it < 1024 / T; ++it) {
+    const int i = t + T * it, Y = (i >> 5) - 2, X = (i & 31) - 2;
     const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
     xv[it] = mask_f(xi[in ? Y * 28 + X : 0], in);
   }
   // 2. LDS: bf16 input image; zero halo ring of conv2's input image (its interior is written by
   //    the conv1 epilogue below)
 #pragma unroll
-  for (int it = 0; it < 6; ++it) {
-    const int i = t + 256 * it;
+  for (int it = 0; it < (1296 + T - 1) / T; ++it) {
+    const int i = t + T * it;
     if (i < 18 * 18 * 4) {
       const int pix = i >> 2, Y = pix / 18, X = pix - Y * 18;
       if (Y < 2 || Y >= 16 || X < 2 || X >= 16) reinterpret_cast<uint4*>(img)[i] = make_uint4(0, 0, 0, 0);
     }
   }
 #pragma unroll
-  for (int it = 0; it < 4; ++it) xim[t + 256 * it] = f2bf(xv[it]);
+  for (int it = 0; it < 1024 / T; ++it) xim[t + T * it] = f2bf(xv[it]);
   __syncthreads();
   // 3. conv1 on MFMA. Lane row m = 16*tile + lr -> window 4*tile + (lr >> 2), pixel d = lr & 3.
   //    Tap offsets of this lane's 8 k values in the padded image (k >= 25 masked to zero).
@@ -259,17 +262,17 @@ __global__ void __launch_bounds__(256) conv12_fwd_kernel(
   }
   const bf16x8 bw0 = __builtin_bit_cast(bf16x8, make_uint4(wb[0][0], wb[0][1], wb[0][2], wb[0][3]));
   const bf16x8 bw1 = __builtin_bit_cast(bf16x8, make_uint4(wb[1][0], wb[1][1], wb[1][2], wb[1][3]));
-  // The wave's tiles wave + 4i (i = 0..12; tile 49+ is a clamped dummy whose results are dropped)
-  // go in batches of 4: every LDS gather of a batch is issued before its MFMAs, so the latency is
-  // paid once per batch rather than once per tile.
-  constexpr int C1_BATCH = 4;
+  // The wave's tiles wave + NW*i (i < C1_NT; tile 49+ is a clamped dummy whose results are
+  // dropped) go in batches of 4: every LDS gather of a batch is issued before its MFMAs, so the
+  // latency is paid once per batch rather than once per tile.
+  constexpr int C1_BATCH = 4, C1_NT = (49 + NW - 1) / NW;
 #pragma unroll
-  for (int i0 = 0; i0 < 13; i0 += C1_BATCH) {
+  for (int i0 = 0; i0 < C1_NT; i0 += C1_BATCH) {
     bf16x8 af[C1_BATCH];
 #pragma unroll
     for (int q = 0; q < C1_BATCH; ++q) {
-      if (i0 + q < 13) {
-        const int tile = min(wave + 4 * (i0 + q), 48);
+      if (i0 + q < C1_NT) {
+        const int tile = min(wave + NW * (i0 + q), 48);
         const int win_a = 4 * tile + (lr >> 2), d = lr & 3;
         const int py_a = win_a / 14, px_a = win_a - py_a * 14;
         const int base = (2 * py_a + (d >> 1)) * C12_XW + 2 * px_a + (d & 1);
@@ -284,7 +287,7 @@ __global__ void __launch_bounds__(256) conv12_fwd_kernel(
     f32x4 cc[C1_BATCH][2];
 #pragma unroll
     for (int q = 0; q < C1_BATCH; ++q) {
-      if (i0 + q < 13) {
+      if (i0 + q < C1_NT) {
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         cc[q][0] = mfma16(af[q], bw0, z);
         cc[q][1] = mfma16(af[q], bw1, z);
@@ -292,8 +295,8 @@ __global__ void __launch_bounds__(256) conv12_fwd_kernel(
     }
 #pragma unroll
     for (int q = 0; q < C1_BATCH; ++q) {
-      const int tile = wave + 4 * (i0 + q);
-      if (i0 + q >= 13 || tile >= 49) continue;
+      const int tile = wave + NW * (i0 + q);
+      if (i0 + q >= C1_NT || tile >= 49) continue;
       // C[row 4lg + i][col lr]: window 4*tile + lg, pixel i of its 2x2 window, channel 16nt + lr
       const int win = 4 * tile + lg, py = win / 14, px = win - py * 14;
 #pragma unroll
@@ -317,7 +320,7 @@ __global__ void __launch_bounds__(256) conv12_fwd_kernel(
   }
   lw.store(wim, C2_WROW, 800, t);
   __syncthreads();
-  conv2_core(img, wim, b2, a2, idx2, half, b, t);
+  conv2_core<NW>(img, wim, b2, a2, idx2, half, b, t);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -382,15 +385,26 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
   }
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   static bool attr = [] {
-    hipFuncSetAttribute((const void*)conv12_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, C12_LDS_BYTES);
+    hipFuncSetAttribute((const void*)conv12_fwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, C12_LDS_BYTES);
+    hipFuncSetAttribute((const void*)conv12_fwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, C12_LDS_BYTES);
     return true;
   }();
   (void)attr;
+  // waves per block (MIHVD_CONV12_WAVES, 4 or 8): one block per CU either way (LDS), more waves
+  // hide more of the gather/MFMA latency chains
+  static const int nw = [] {
+    const char* e = getenv("MIHVD_CONV12_WAVES");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  conv12_fwd_kernel<<<dim3(2, B), 256, C12_LDS_BYTES, stream>>>(
-      x.data_ptr<float>(), rp, n_pool, sp, (const u16*)w1bf.data_ptr(), b1.data_ptr<float>(),
-      (const u16*)w2bf.data_ptr(), b2.data_ptr<float>(), (u16*)a1.data_ptr(), idx1.data_ptr<uint8_t>(),
-      (u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(), B);
+  auto launch = [&](auto kern, int threads) {
+    kern<<<dim3(2, B), threads, C12_LDS_BYTES, stream>>>(
+        x.data_ptr<float>(), rp, n_pool, sp, (const u16*)w1bf.data_ptr(), b1.data_ptr<float>(),
+        (const u16*)w2bf.data_ptr(), b2.data_ptr<float>(), (u16*)a1.data_ptr(), idx1.data_ptr<uint8_t>(),
+        (u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(), B);
+  };
+  if (nw == 4) launch(conv12_fwd_kernel<4>, 256);
+  else launch(conv12_fwd_kernel<8>, 512);
 }
 
 }  // namespace mihvd
