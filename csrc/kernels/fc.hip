@@ -29,20 +29,23 @@ constexpr int F1_ASTR = FC1_KSL + 8;   // a2 image rows: 232 elements (464 B)
 constexpr int F1_WSTR = FC1_NT + 8;    // W3 image rows: 72 elements (144 B)
 constexpr int F1_LDS = (MAXB * F1_ASTR + FC1_KSL * F1_WSTR) * 2;
 
-// grid (16, 14): blockIdx.x = 64-column tile, blockIdx.y = K slice. 256 threads = 4 waves.
-// MT = ceil(B/16) sample tiles, a template parameter (no runtime guard around any MFMA).
-template <int MT>
-__global__ void __launch_bounds__(256) fc1_fwd_kernel(const u16* __restrict__ a2, const u16* __restrict__ w3,
-                                                      float* __restrict__ zpart, int B) {
+// grid (16, 14): blockIdx.x = 64-column tile, blockIdx.y = K slice. NW = 4 or 8 waves: wave w
+// owns the 16 features (w & 3) and, with 8 waves, half of the sample tiles (w >> 2).
+// MT = ceil(B/16) sample tiles, a template parameter (no runtime guard around any MFMA: the odd
+// half's spare tile recomputes the last real one and is not stored).
+template <int MT, int NW = 4>
+__global__ void __launch_bounds__(NW * 64) fc1_fwd_kernel(const u16* __restrict__ a2, const u16* __restrict__ w3,
+                                                          float* __restrict__ zpart, int B) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  constexpr int Mpad = MT * 16;
+  constexpr int Mpad = MT * 16, T = NW * 64;
+  constexpr int MTW = NW == 8 ? (MT + 1) / 2 : MT;  // sample tiles per wave
   u16* Ws = smem;                     // [224][F1_WSTR]    rows = k, n contiguous
   u16* As = smem + FC1_KSL * F1_WSTR; // [Mpad][F1_ASTR]   rows = samples, k contiguous
   const int nt = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
   const int k0 = ks * FC1_KSL;
   {
-    TileLoad<256, (Mpad * FC1_KSL / 8 + 255) / 256, FC1_KSL / 8> la;
-    TileLoad<256, (FC1_KSL * FC1_NT / 8 + 255) / 256, FC1_NT / 8> lw;
+    TileLoad<T, (Mpad * FC1_KSL / 8 + T - 1) / T, FC1_KSL / 8> la;
+    TileLoad<T, (FC1_KSL * FC1_NT / 8 + T - 1) / T, FC1_NT / 8> lw;
     lw.load(w3 + (int64_t)k0 * FC1_N + nt * FC1_NT, FC1_N, FC1_KSL, FC1_KSL, t);
     la.load(a2 + k0, FC1_K, Mpad, B, t);
     lw.store(Ws, F1_WSTR, FC1_KSL, t);
@@ -50,27 +53,29 @@ __global__ void __launch_bounds__(256) fc1_fwd_kernel(const u16* __restrict__ a2
   }
   __syncthreads();
   const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4, q = lr >> 2, p = lr & 3;
-  f32x4 acc[MT];
+  const int wn = wave & 3, mt0 = NW == 8 ? (wave >> 2) * MTW : 0;
+  f32x4 acc[MTW];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kk = 0; kk < FC1_KSL / 32; ++kk) {
     // A = W3^T (rows = features n), read transposed from the [k][n] image.
-    const u16* wr = Ws + (kk * 32 + 8 * lg + q) * F1_WSTR + wave * 16 + 4 * p;
+    const u16* wr = Ws + (kk * 32 + 8 * lg + q) * F1_WSTR + wn * 16 + 4 * p;
     const bf16x8 afr = frag_tr(wr, wr + 4 * F1_WSTR);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int i = 0; i < MTW; ++i) {
+      const int mt = min(mt0 + i, MT - 1);
       const bf16x8 bfr = frag_ld128(As + (mt * 16 + lr) * F1_ASTR + kk * 32 + 8 * lg);
-      acc[mt] = mfma16(afr, bfr, acc[mt]);
+      acc[i] = mfma16(afr, bfr, acc[i]);
     }
   }
   float* out = zpart + (int64_t)ks * B * FC1_N;
-  const int n = nt * FC1_NT + wave * 16 + 4 * lg;
+  const int n = nt * FC1_NT + wn * 16 + 4 * lg;
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int m = mt * 16 + lr;
-    if (m < B)
-      *reinterpret_cast<float4*>(out + (int64_t)m * FC1_N + n) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
+  for (int i = 0; i < MTW; ++i) {
+    const int m = (mt0 + i) * 16 + lr;
+    if (mt0 + i < MT && m < B)
+      *reinterpret_cast<float4*>(out + (int64_t)m * FC1_N + n) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
   }
 }
 
@@ -509,11 +514,24 @@ void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
   const int MT = (B + 15) >> 4;
   const int lds = (FC1_KSL * F1_WSTR + MT * 16 * F1_ASTR) * 2;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  MIHVD_MT_SWITCH(MT, {
-    set_max_lds(fc1_fwd_kernel<MT_>, F1_LDS);
-    fc1_fwd_kernel<MT_><<<dim3(FC1_N / FC1_NT, FC1_KS), 256, lds, stream>>>(
-        (const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(), zpart.data_ptr<float>(), B);
-  })
+  // waves per block (MIHVD_FC1_FWD_WAVES, 4 or 8); one block per CU either way (LDS)
+  static const int nw = [] {
+    const char* e = getenv("MIHVD_FC1_FWD_WAVES");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  if (nw == 4) {
+    MIHVD_MT_SWITCH(MT, {
+      set_max_lds(fc1_fwd_kernel<MT_, 4>, F1_LDS);
+      fc1_fwd_kernel<MT_, 4><<<dim3(FC1_N / FC1_NT, FC1_KS), 256, lds, stream>>>(
+          (const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(), zpart.data_ptr<float>(), B);
+    })
+  } else {
+    MIHVD_MT_SWITCH(MT, {
+      set_max_lds(fc1_fwd_kernel<MT_, 8>, F1_LDS);
+      fc1_fwd_kernel<MT_, 8><<<dim3(FC1_N / FC1_NT, FC1_KS), 512, lds, stream>>>(
+          (const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(), zpart.data_ptr<float>(), B);
+    })
+  }
 }
 
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
