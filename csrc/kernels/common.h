@@ -210,23 +210,26 @@ struct AdamTail {
   float lr, b1, b2, eps, gscale;
   int rule;
   int first_free;        // blocks [first_free, grid) have no compute work ...
-  int64_t head;          // ... and alone take the 256-float4 groups [0, head) before the shared range
+  int64_t head;          // ... and alone take the groups [0, head) before the shared range
+  int kpl;               // float4 per lane per array in one group (4 or 8)
 };
 
+// One group: K float4 per lane per array (64 K float4, all loads in flight before any update).
+template <int K>
 __device__ __forceinline__ void adam_tail_group(const AdamTail& at, const AdamCoef& c, int64_t w, int lane) {
-  float4 pp[4], gg[4], mm[4], vv[4];
-  int64_t idx[4];
+  float4 pp[K], gg[K], mm[K], vv[K];
+  int64_t idx[K];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    idx[k] = min(w * 256 + k * 64 + lane, at.n4 - 1);
+  for (int k = 0; k < K; ++k) {
+    idx[k] = min(w * (64 * K) + k * 64 + lane, at.n4 - 1);
     pp[k] = reinterpret_cast<const float4*>(at.p)[idx[k]];
     gg[k] = reinterpret_cast<const float4*>(at.g)[idx[k]];
     mm[k] = reinterpret_cast<const float4*>(at.m)[idx[k]];
     vv[k] = reinterpret_cast<const float4*>(at.v)[idx[k]];
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (w * 256 + k * 64 + lane >= at.n4) continue;
+  for (int k = 0; k < K; ++k) {
+    if (w * (64 * K) + k * 64 + lane >= at.n4) continue;
     const uint2 sh = adam4(pp[k], mm[k], vv[k], gg[k], c);
     reinterpret_cast<float4*>(at.p)[idx[k]] = pp[k];
     reinterpret_cast<float4*>(at.m)[idx[k]] = mm[k];
@@ -236,20 +239,27 @@ __device__ __forceinline__ void adam_tail_group(const AdamTail& at, const AdamCo
 }
 
 // Blocks without compute work start at once and run for the whole compute phase, so they take a
-// head range of their own (sized by the caller) before every wave of the launch shares the rest.
-__device__ __forceinline__ void adam_tail_run(const AdamTail& at) {
+// head range of their own (at.head groups, sized by the caller) before every wave of the launch
+// shares the rest.
+template <int K>
+__device__ __forceinline__ void adam_tail_run_k(const AdamTail& at) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int waves = (int)blockDim.x >> 6;
   const AdamCoef c = adam_coef((float)at.state[ST_OPT], at.lr, at.b1, at.b2, at.eps, at.gscale, at.rule);
-  const int64_t n256 = (at.n4 + 255) / 256;
-  const int64_t head = min(at.head, n256);
+  const int64_t ng = (at.n4 + 64 * K - 1) / (64 * K);
+  const int64_t head = min(at.head, ng);
   const int n_free = (int)gridDim.x - at.first_free;
   if ((int)blockIdx.x >= at.first_free && n_free > 0) {
     for (int64_t w = (int64_t)((int)blockIdx.x - at.first_free) * waves + wave; w < head; w += (int64_t)n_free * waves)
-      adam_tail_group(at, c, w, lane);
+      adam_tail_group<K>(at, c, w, lane);
   }
   const int64_t nw = (int64_t)gridDim.x * waves;
-  for (int64_t w = head + (int64_t)blockIdx.x * waves + wave; w < n256; w += nw) adam_tail_group(at, c, w, lane);
+  for (int64_t w = head + (int64_t)blockIdx.x * waves + wave; w < ng; w += nw) adam_tail_group<K>(at, c, w, lane);
+}
+
+__device__ __forceinline__ void adam_tail_run(const AdamTail& at) {
+  if (at.kpl == 8) adam_tail_run_k<8>(at);
+  else adam_tail_run_k<4>(at);
 }
 
 }  // namespace mihvd
