@@ -190,3 +190,29 @@ def test_process_sets_three_ranks(tmp_path):
     assert "not part of" in b["error"]
     assert b["sum2"] == c["sum2"] == [5.0, 5.0] and "sum2" not in a
     assert a["world"] == b["world"] == [3.0]
+
+
+def test_collective_bandwidth_benchmark_two_ranks(tmp_path):
+    """scripts/allreduce_bw.py under torch.distributed.run (gloo, 2 ranks): one JSON row per op and
+    size from rank 0, bus bandwidth = algbw x the nccl-tests factor, unsupported ops reported."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, MIHVD_BACKEND="gloo")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29641", os.path.join(root, "scripts", "allreduce_bw.py"), "--sizes", "4K,64K",
+           "--iters", "3", "--warmup", "1", "--engine"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=tmp_path)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    timed = [r for r in rows if "us" in r]
+    assert {r["op"] for r in timed} >= {"allreduce", "hvd.allreduce", "allgather", "broadcast"}
+    for r in timed:
+        assert r["world"] == 2 and r["us"] > 0
+        f = {"allreduce": 1.0, "hvd.allreduce": 1.0, "allgather": 0.5, "broadcast": 1.0}.get(r["op"])
+        if f is not None:
+            assert abs(r["busbw_GBs"] - f * r["algbw_GBs"]) < 1e-9 * max(1.0, r["algbw_GBs"])
