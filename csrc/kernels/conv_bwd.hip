@@ -277,7 +277,14 @@ __device__ __forceinline__ void conv2_bwd_block(
 #pragma unroll
       for (int c = 0; c < 8; ++c) red1[(wave * 4 + lg) * 8 + c] = d1[c];
     }
-    *reinterpret_cast<float4*>(red + t * 4) = make_float4(db[0], db[1], db[2], db[3]);
+    // db2: lanes l, l+16, l+32, l+48 of a wave hold the same channel group (t & 15): fold them with
+    // two shuffles, then one slot per (wave, group), so the final sum is 8 terms, not 32
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      db[c] += __shfl_xor(db[c], 16, 64);
+      db[c] += __shfl_xor(db[c], 32, 64);
+    }
+    if (lane < 16) *reinterpret_cast<float4*>(red + (wave * 16 + lane) * 4) = make_float4(db[0], db[1], db[2], db[3]);
 #pragma unroll
     for (int k = 0; k < 2; ++k) Xf[((t + 512 * k) >> 5) * 36 + ((t + 512 * k) & 31)] = xv[k];
     if (t < 32) Xf[t * 36 + 32] = Xf[t * 36 + 33] = Xf[t * 36 + 34] = Xf[t * 36 + 35] = 0.f;
@@ -288,7 +295,7 @@ __device__ __forceinline__ void conv2_bwd_block(
       // db2 channel co4*4 + c, summed over the 32 threads with (tid & 15) == co4
       const int co4 = t >> 2, c = t & 3;
       float sacc = 0.f;
-      for (int r = co4; r < 512; r += 16) sacc += red[r * 4 + c];
+      for (int w = 0; w < 8; ++w) sacc += red[(w * 16 + co4) * 4 + c];  // 8 per-wave folds
       cpart[(int64_t)b * CP_W + CP_DB2 + co4 * 4 + c] = sacc;
     } else if (t < 96) {
       // db1 channel ch = 16nt + 4lg + i
