@@ -286,9 +286,27 @@ class FusedMNISTTrainer:
         self._epoch_steps = n // self.B
 
     def _reshuffle(self):
+        """New epoch permutation of the resident dataset. The copy into ``rows`` is queued on the
+        compute stream (stream order keeps it behind every step still reading the old order), from
+        one of two pinned host buffers, so an epoch boundary costs no host synchronisation."""
         n = self.X.shape[0]
         perm = self._rng.permutation(n) if self._shuffle else np.arange(n)
-        self.rows.copy_(torch.from_numpy(perm.astype(np.int32)))
+        if not self.rows.is_cuda:
+            self.rows.copy_(torch.from_numpy(perm.astype(np.int32)))
+            return
+        if getattr(self, "_pin", None) is None or self._pin[0].numel() != n:
+            self._pin = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(2)]
+            self._pin_ev = [None, None]
+            self._pin_i = 0
+        i = self._pin_i
+        self._pin_i ^= 1
+        if self._pin_ev[i] is not None:
+            self._pin_ev[i].synchronize()  # that buffer's copy (an epoch ago) has long finished
+        self._pin[i].numpy()[:] = perm
+        self.rows.copy_(self._pin[i], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._pin_ev[i] = ev
 
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
@@ -562,8 +580,7 @@ class FusedMNISTTrainer:
         e0 = self.global_step // self._epoch_steps
         e1 = (self.global_step + k - 1) // self._epoch_steps
         if e1 != e0 or (self.global_step % self._epoch_steps == 0 and self.global_step > 0):
-            torch.cuda.current_stream(self.device).synchronize()
-            self._reshuffle()
+            self._reshuffle()  # stream-ordered: no host synchronisation
 
     # ----------------------------------------------------------------------------- graphs
     def build_graph(self, steps_per_replay: int = 10, warmup: int = 2, primary: bool = True):
