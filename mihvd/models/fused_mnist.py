@@ -228,6 +228,16 @@ class FusedMNISTTrainer:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
         else:
             self.wire = None
+        # MIHVD_XGMI_ALLREDUCE=1: the fp32 gradient buckets go through the direct xGMI one-shot
+        # allreduce (mihvd/parallel/xgmi.py, csrc/kernels/xgmi.hip) instead of RCCL: one hop over
+        # the point-to-point mesh for these latency-bound (< 1 MB with the factor gather) buckets.
+        # One context per bucket: the "fc" and "conv" buckets can be in flight on two streams at
+        # once, and a context's calls must be ordered (one epoch counter, one pair of slots).
+        # Contexts are created (collectively) on a bucket's first use, in the eager warm-up steps.
+        self.xgmi = None
+        if (os.environ.get("MIHVD_XGMI_ALLREDUCE", "0") == "1" and self.collectives and self.wire is None
+                and self.world <= 8 and dev.type == "cuda" and (op is None or ReduceOp(op) != ReduceOp.Adasum)):
+            self.xgmi = {}
 
     # ----------------------------------------------------------------------------- views
     @staticmethod
@@ -543,6 +553,15 @@ class FusedMNISTTrainer:
             segs = [(o - lo, o - lo + n) for o, n in SEGMENTS.values() if lo <= o < hi]
             adasum_dispatch_(bucket, segs)
             bucket.mul_(self.world)  # adam divides by size; Adasum output is already the combined gradient
+            return
+        if self.xgmi is not None:
+            ctx = self.xgmi.get((lo, hi))
+            if ctx is None:
+                from ..parallel.xgmi import XGMIAllreduce
+
+                idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+                ctx = self.xgmi[(lo, hi)] = XGMIAllreduce(hi - lo, device=torch.device("cuda", idx))
+            ctx.allreduce_(bucket)  # sum; Adam applies the 1/size of Average
             return
         if self.wire is not None:
             w = self.wire[lo:hi]

@@ -3,14 +3,15 @@
 
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \\
         --master-port 29600 scripts/allreduce_bw.py [--ops allreduce,allgather,reduce_scatter,broadcast]
-        [--sizes 4K,64K,1M,13M,64M,256M] [--dtype bf16|fp32] [--graph] [--engine]
+        [--sizes 4K,64K,1M,13M,64M,256M] [--dtype bf16|fp32] [--graph] [--engine] [--xgmi]
 
 Per op and message size: time per call (median over --iters after --warmup), algorithm bandwidth
 (bytes / time) and bus bandwidth (the nccl-tests convention: allreduce x 2(n-1)/n, allgather and
 reduce-scatter x (n-1)/n, broadcast x 1), the numbers that decide bucket sizes on a point-to-point
 xGMI mesh (13.1 MB is the MNIST gradient bucket). --graph replays the calls from a
 HIP graph (how the fused trainer issues them); --engine also times mihvd's allreduce entry point
-(hvd.allreduce: negotiation/fusion bookkeeping + the same RCCL call). Rank 0 prints one JSON line
+(hvd.allreduce: negotiation/fusion bookkeeping + the same RCCL call); --xgmi also times the direct
+xGMI one-shot allreduce (mihvd.parallel.xgmi, fp32 sizes). Rank 0 prints one JSON line
 per (op, size) and a table.
 """
 from __future__ import annotations
@@ -62,6 +63,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph", action="store_true", help="replay the calls from a HIP graph")
     ap.add_argument("--engine", action="store_true", help="also time hvd.allreduce (mihvd entry point)")
+    ap.add_argument("--xgmi", action="store_true",
+                    help="also time the direct xGMI one-shot allreduce (mihvd.parallel.xgmi, fp32)")
     args = ap.parse_args()
 
     import mihvd.torch as hvd
@@ -73,6 +76,12 @@ def main():
     on_gpu = dev.type == "cuda"
     sync = (lambda: torch.cuda.synchronize(dev)) if on_gpu else (lambda: None)
     rows = []
+    xgmi = None
+    if args.xgmi and on_gpu and world > 1:
+        from mihvd.parallel.xgmi import XGMIAllreduce
+
+        cap = max(parse_size(sz) for sz in args.sizes.split(",")) // 4 + world
+        xgmi = XGMIAllreduce(cap)
     for op in args.ops.split(","):
         for sz in args.sizes.split(","):
             nbytes = parse_size(sz)
@@ -135,6 +144,36 @@ def main():
                 rows.append(dict(row, op="hvd.allreduce", us=float(t.item()) * 1e6,
                                  algbw_GBs=n * esize / float(t.item()) / 1e9,
                                  busbw_GBs=n * esize / float(t.item()) / 1e9 * bus_factor("allreduce", world)))
+            if xgmi is not None and op == "allreduce" and dtype == torch.float32 and n <= xgmi.capacity:
+                xcall = lambda: xgmi.allreduce_(buf)  # noqa: E731
+                for _ in range(args.warmup):
+                    xcall()
+                sync()
+                xgmi.check()
+                if args.graph:
+                    g = torch.cuda.CUDAGraph()
+                    s = torch.cuda.Stream(device=dev)
+                    s.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+                        xcall()
+                    torch.cuda.current_stream(dev).wait_stream(s)
+                    xcall = g.replay
+                xt = []
+                for _ in range(args.iters):
+                    dist.barrier()
+                    sync()
+                    t0 = time.perf_counter()
+                    xcall()
+                    sync()
+                    xt.append(time.perf_counter() - t0)
+                xgmi.check()
+                t = torch.tensor([statistics.median(xt)], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                xs = float(t.item())
+                rows.append(dict(row, op="xgmi_oneshot", us=xs * 1e6, algbw_GBs=n * esize / xs / 1e9,
+                                 busbw_GBs=n * esize / xs / 1e9 * bus_factor("allreduce", world)))
+    if xgmi is not None:
+        xgmi.close()
     if rank == 0:
         for r in rows:
             print(json.dumps(r))

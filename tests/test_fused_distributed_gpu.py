@@ -52,6 +52,23 @@ def test_fused_data_parallel_equivalence_two_ranks(tmp_path, gather):
         assert o["rel_update_diff"] < 0.05, o
 
 
+@pytest.mark.parametrize("gather", ["1", "0"])
+def test_fused_data_parallel_xgmi_allreduce_two_ranks(tmp_path, gather):
+    """The fused trainer's gradient buckets over the direct xGMI one-shot allreduce
+    (MIHVD_XGMI_ALLREDUCE=1; gloo only carries the factor gather and the IPC handle exchange)."""
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_XGMI_ALLREDUCE="1")
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(2):
+        o = json.loads((tmp_path / f"dp_gloo.{r}.json").read_text())
+        assert o["xgmi"], o
+        assert o["rank_spread"] == 0.0
+        assert o["grad_rel"] < 1e-4, o
+        assert o["rel_update_diff"] < 0.05, o
+
+
 def test_sharded_optimizer_matches_unsharded_two_ranks(tmp_path):
     _gpu()
     env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT)

@@ -77,7 +77,7 @@ def sc_dp_gloo(outdir):
     mx = (tr.params - ref.params).abs().max().item()
     spread = hvd.allgather(tr.params[:4096].cpu().view(1, -1))
     with open(os.path.join(outdir, f"dp_gloo.{r}.json"), "w") as f:
-        json.dump({"gather": tr.gather, "grad_rel": grel, "rel_update_diff": rel, "max": mx,
+        json.dump({"gather": tr.gather, "xgmi": tr.xgmi is not None, "grad_rel": grel, "rel_update_diff": rel, "max": mx,
                    "rank_spread": (spread - spread[0]).abs().max().item()}, f)
 
 
