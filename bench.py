@@ -145,6 +145,9 @@ def make_fused_step(args, hvd, device):
     tr.broadcast(0)
     X, Y = synthetic_pool(args.pool_batches, args.batch_size, device, seed=hvd.rank())
     tr.set_device_dataset(X, Y)
+    # N > 1: data plane of the factor gather (MIHVD_XGMI=auto: validate the direct xGMI collectives
+    # against RCCL, time both planes, keep the faster; these steps are untimed and counted apart)
+    tr.plane_report = tr.select_data_plane() if tr.collectives else {"plane": "none"}
     k = args.graph_steps or 20  # steps per HIP-graph replay (20: measured 66.6 vs 67.5 us at 10)
     tr.build_graph(steps_per_replay=k)
     # remainders of --steps / --warmup that are not multiples of k replay a shorter graph, so the
@@ -209,14 +212,21 @@ def main():
         comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
     elif n == 1:
         comm_desc = "none (1 GPU)"
+    elif getattr(tr, "shard_w3", False) and tr.data_plane() == "xgmi":
+        comm_desc = ("direct xGMI one-shot collectives (hipIpc peer memory, device-side phase barriers): each rank "
+                     "reads the peers' bf16 fc1 factors (dz, and the a2 columns of its own dense/kernel rows), "
+                     "computes the exact dW3 (all samples) for its 1/N of the rows and applies Adam to them, then "
+                     "reads the peers' updated bf16 rows (overlapping the next step's convolutions); one-shot sum of "
+                     "the other fp32 gradients; every step, in the HIP graph")
     elif getattr(tr, "shard_w3", False):
         comm_desc = ("RCCL all-gather of the bf16 fc1 factors (a2, dz) -> each rank computes the exact dW3 "
                      "(all samples) for its 1/N of dense/kernel's rows and applies Adam to them; RCCL all-gather "
                      "of the updated bf16 rows (overlapping the next step's convolutions); RCCL allreduce of the "
                      "other fp32 gradients; every step, in the HIP graph")
     elif getattr(tr, "gather", False):
-        comm_desc = ("RCCL all-gather of the bf16 fc1 factors (a2, dz) -> exact dW3 over all samples; RCCL "
-                     "allreduce of the other fp32 gradients; every step, in the HIP graph")
+        comm_desc = ("%s gather of the bf16 fc1 factors (a2, dz) -> exact dW3 over all samples; %s reduction of "
+                     "the other fp32 gradients; every step, in the HIP graph"
+                     % (("direct xGMI", "xGMI one-shot") if tr.data_plane() == "xgmi" else ("RCCL", "RCCL")))
     else:
         comm_desc = "RCCL allreduce of the fp32 gradient fusion buffer every step" + (
             " (bf16 wire)" if args.compression == "bf16" else "")
@@ -232,7 +242,11 @@ def main():
                        "allreduce": comm_desc,
                        "steps_per_graph": per_call, "final_loss": loss_val},
         }
+        if args.impl == "fused" and n > 1:
+            rec["config"]["data_plane"] = tr.plane_report
         print(json.dumps(rec), flush=True)
+    if args.impl == "fused":
+        tr.close()
     hvd.shutdown()
 
 

@@ -152,14 +152,6 @@ class FusedMNISTTrainer:
 
         self.gather = (self.collectives and compression == "none" and os.environ.get("MIHVD_FC_GATHER", "1") != "0"
                        and (op is None or ReduceOp(op) in (ReduceOp.Average, ReduceOp.Sum)))
-        if self.gather:
-            self.a2_all = torch.empty(self.world * B, 3136, **bf)
-            self.dz_all = torch.empty(self.world * B, 1024, **bf)
-            self.a2 = self.a2_all[self.rank * B:(self.rank + 1) * B]   # conv2_fwd writes its rows in place
-            self.dz = self.dz_all[self.rank * B:(self.rank + 1) * B]   # head writes its rows in place
-        else:
-            self.a2 = torch.empty(B, 3136, **bf)
-            self.dz = torch.empty(B, 1024, **bf)
         # Sharded dense/kernel optimizer (factor-gather plane only; shard_optimizer=True or
         # MIHVD_SHARD_W3=1): rank r owns W3 row tiles [r*T, (r+1)*T) of the 49 64-row tiles
         # (T = ceil(49/size)). It computes dW3 for those rows only (over every rank's samples, so the
@@ -177,7 +169,52 @@ class FusedMNISTTrainer:
             self._T = -(-49 // self.world)
             lo, hi = self.rank * self._T, min((self.rank + 1) * self._T, 49)
             self._w3_tiles = (lo, max(lo, hi))
-            self.shadow3 = torch.zeros(self.world * self._T * 64, 1024, **bf)
+        # Direct xGMI data plane for the factor gather (MIHVD_XGMI=auto|on|off, mihvd/parallel/xgmi.py):
+        # a2, dz, the gradient buffer and the W3 row shadow live in one hipIpc-shared region per rank,
+        # and the plane's four collectives per step are one-shot launches that read the peers'
+        # copies in place over xGMI — a2 only for the columns this rank's W3 rows need — instead of
+        # RCCL all-gathers/allreduce. "auto" validates it against RCCL and times both
+        # (select_data_plane); ranks on several nodes or a failed IPC setup fall back to RCCL.
+        self.xplane = None
+        self.use_xgmi = False
+        self._xgmi_mode = "off"
+        if self.gather:
+            from ..parallel import xgmi as _xg
+
+            self._xgmi_mode = _xg.env_mode()
+            if self._xgmi_mode != "off" and self.world <= _xg.MAX_RANKS:
+                import torch.distributed as dist
+
+                if dist.is_initialized():
+                    layout = {"a2": (self.world * B * 3136, torch.bfloat16), "dz": (self.world * B * 1024, torch.bfloat16),
+                              "grads": (FLAT_NUMEL, torch.float32)}
+                    if self.shard_w3:
+                        layout["shadow3"] = (self.world * self._T * 64 * 1024, torch.bfloat16)
+                    try:
+                        self.xplane = _xg.XGMIRegion(layout, device=dev)
+                    except _xg.XGMIUnavailable as e:
+                        _xg.warn_fallback(str(e))
+            # "on": use it from the first step; "auto": RCCL until select_data_plane() validated it
+            self.use_xgmi = self.xplane is not None and self._xgmi_mode == "on"
+        if self.gather:
+            if self.xplane is not None:
+                self.a2_all = self.xplane.view("a2").view(self.world * B, 3136)
+                self.dz_all = self.xplane.view("dz").view(self.world * B, 1024)
+                self.grads = self.xplane.view("grads")
+                self.gred = torch.zeros(W3_START, **f32)  # xGMI sum of the small gradients
+            else:
+                self.a2_all = torch.empty(self.world * B, 3136, **bf)
+                self.dz_all = torch.empty(self.world * B, 1024, **bf)
+            self.a2 = self.a2_all[self.rank * B:(self.rank + 1) * B]   # conv2_fwd writes its rows in place
+            self.dz = self.dz_all[self.rank * B:(self.rank + 1) * B]   # head writes its rows in place
+        else:
+            self.a2 = torch.empty(B, 3136, **bf)
+            self.dz = torch.empty(B, 1024, **bf)
+        if self.shard_w3:
+            if self.xplane is not None:
+                self.shadow3 = self.xplane.view("shadow3").view(self.world * self._T * 64, 1024)
+            else:
+                self.shadow3 = torch.zeros(self.world * self._T * 64, 1024, **bf)
             self._refresh_shadow()
         self.idx2 = torch.empty(B, 3136, **u8)
         self.zpart = torch.empty(14, B, 1024, **f32)
@@ -228,16 +265,17 @@ class FusedMNISTTrainer:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
         else:
             self.wire = None
-        # MIHVD_XGMI_ALLREDUCE=1: the fp32 gradient buckets go through the direct xGMI one-shot
-        # allreduce (mihvd/parallel/xgmi.py, csrc/kernels/xgmi.hip) instead of RCCL: one hop over
-        # the point-to-point mesh for these latency-bound (< 1 MB with the factor gather) buckets.
-        # One context per bucket: the "fc" and "conv" buckets can be in flight on two streams at
-        # once, and a context's calls must be ordered (one epoch counter, one pair of slots).
-        # Contexts are created (collectively) on a bucket's first use, in the eager warm-up steps.
+        # Bucket-allreduce plane (MIHVD_FC_GATHER=0) with MIHVD_XGMI_ALLREDUCE=1: the fp32 gradient
+        # buckets go through the direct xGMI one-shot allreduce (mihvd/parallel/xgmi.py) instead of
+        # RCCL. One context per bucket: the "fc" and "conv" buckets can be in flight on two streams
+        # at once. Contexts are created (collectively) on a bucket's first use, in the eager warm-up
+        # steps; ranks on several nodes fall back to RCCL (XGMIUnavailable on every rank alike).
         self.xgmi = None
-        if (os.environ.get("MIHVD_XGMI_ALLREDUCE", "0") == "1" and self.collectives and self.wire is None
-                and self.world <= 8 and dev.type == "cuda" and (op is None or ReduceOp(op) != ReduceOp.Adasum)):
+        if (not self.gather and os.environ.get("MIHVD_XGMI_ALLREDUCE", "0") == "1" and self.collectives
+                and self.wire is None and self.world <= 8 and dev.type == "cuda"
+                and (op is None or ReduceOp(op) != ReduceOp.Adasum)):
             self.xgmi = {}
+        self._closed = False
 
     # ----------------------------------------------------------------------------- views
     @staticmethod
@@ -415,12 +453,20 @@ class FusedMNISTTrainer:
         main = torch.cuda.current_stream(self.device)
         side = self._side
         self._conv_forward(x, rows, st)
-        # (an all-to-all of only the column slice each rank needs would move 1/N of these bytes,
-        # but torch's RCCL process group cannot capture all_to_all_single into a HIP graph: its
-        # watchdog queries the captured event and aborts)
+        # (with RCCL this gathers whole a2 rows: an all-to-all of only the column slice each rank
+        # needs cannot be captured, torch's RCCL process group watchdog queries the captured event
+        # and aborts; the xGMI plane reads just those columns from the peers)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self._all_gather_rows(self.a2_all, self.a2)
+            self._gather_a2()
+            a_done = None
+            if self.use_xgmi and not self.shard_w3:
+                # the peers read this rank's small gradients in place (xGMI phase 2 of the last
+                # step); they are rewritten by fc1_bwd below, which therefore waits until every peer
+                # entered this step's phase 0 (and so finished phase 2). With the sharded optimizer
+                # the wait on the W3 row gather (phase 3) below already implies it.
+                a_done = torch.cuda.Event()
+                a_done.record(side)
         if self._shadow_ev is not None:
             # the previous step's W3 row gather (side stream) must land before the first reader
             main.wait_event(self._shadow_ev)
@@ -430,10 +476,15 @@ class FusedMNISTTrainer:
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self._all_gather_rows(self.dz_all, self.dz)
+            if self.use_xgmi:
+                self.xplane.gather_rows("dz", 1, 1024 * 2, self.B)
+            else:
+                self._all_gather_rows(self.dz_all, self.dz)
         gW3 = self.gview("dense/kernel")
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
                  self.gview("dense_1/bias"))
+        if a_done is not None:
+            main.wait_event(a_done)
         if self.fc1_merged:  # db3, dW4, db4 of the local batch + the dgrad tiles, one launch
             o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2)
         else:
@@ -443,7 +494,11 @@ class FusedMNISTTrainer:
         main.wait_stream(side)   # both gathers done: the communicator is free
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self._allreduce(self.grads[:W3_START], 0, W3_START)
+            if self.use_xgmi:
+                self.xplane.reduce("grads", 2, self.gred)  # sum; Adam applies the 1/size of Average
+            else:
+                self._allreduce(self.grads[:W3_START], 0, W3_START)
+        gsmall = self.gred if self.use_xgmi else self.grads[:W3_START]
         b1, b2 = self.betas
         if self.shard_w3:
             ar_done = torch.cuda.Event()
@@ -459,11 +514,14 @@ class FusedMNISTTrainer:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 T64 = self._T * 64
-                self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
+                if self.use_xgmi:
+                    self.xplane.gather_rows("shadow3", 3, 1024 * 2, T64, total_rows=min(self.world * T64, 3136))
+                else:
+                    self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
                 self._shadow_ev = torch.cuda.Event()
                 self._shadow_ev.record(side)
             main.wait_event(ar_done)
-            o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START],
+            o.adam_step(self.params[:W3_START], gsmall, self.m[:W3_START], self.v[:W3_START],
                         self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
             self._full_state_valid = False
             return
@@ -471,13 +529,29 @@ class FusedMNISTTrainer:
             # dW3 summed over every rank's samples, Adam applied to W3 in the same tiles
             self._fc1_wgrad_w3_adam(1, self.dz_all, self.a2_all)
             main.wait_stream(side)
-            o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START],
+            o.adam_step(self.params[:W3_START], gsmall, self.m[:W3_START], self.v[:W3_START],
                         self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
             return
         o.fc1_wgrad(*small, 1, self.dz_all, self.a2_all)  # dW3 summed over every rank's samples
         main.wait_stream(side)
+        if self.use_xgmi:
+            w3 = slice(W3_START, FLAT_NUMEL)
+            o.adam_step(self.params[w3], self.grads[w3], self.m[w3], self.v[w3], self.shadow[w3], st, 0, self.lr, b1, b2,
+                        self.eps, 1.0 / self.world, self.rule, 0)
+            o.adam_step(self.params[:W3_START], gsmall, self.m[:W3_START], self.v[:W3_START], self.shadow[:W3_START],
+                        st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+            return
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
+
+    def _gather_a2(self):
+        """All ranks' a2 rows (the fc1 input factors) into a2_all: with xGMI only the byte columns
+        of this rank's W3 row tiles (all that its dW3 rows read), else whole rows over RCCL."""
+        if self.use_xgmi:
+            lo, hi = self._w3_tiles if self.shard_w3 else (0, 49)
+            self.xplane.gather_rows("a2", 0, 3136 * 2, self.B, col_lo=lo * 128, col_hi=hi * 128)
+        else:
+            self._all_gather_rows(self.a2_all, self.a2)
 
     def _fc1_wgrad_w3_adam(self, roles, dz_all, a2_all):
         b1, b2 = self.betas
@@ -555,14 +629,20 @@ class FusedMNISTTrainer:
             bucket.mul_(self.world)  # adam divides by size; Adasum output is already the combined gradient
             return
         if self.xgmi is not None:
-            ctx = self.xgmi.get((lo, hi))
-            if ctx is None:
-                from ..parallel.xgmi import XGMIAllreduce
+            ctx = self.xgmi.get((lo, hi), False)
+            if ctx is False:
+                from ..parallel import xgmi as _xg
 
                 idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-                ctx = self.xgmi[(lo, hi)] = XGMIAllreduce(hi - lo, device=torch.device("cuda", idx))
-            ctx.allreduce_(bucket)  # sum; Adam applies the 1/size of Average
-            return
+                try:
+                    ctx = _xg.XGMIAllreduce(hi - lo, device=torch.device("cuda", idx))
+                except _xg.XGMIUnavailable as e:
+                    _xg.warn_fallback(str(e))
+                    ctx = None
+                self.xgmi[(lo, hi)] = ctx
+            if ctx is not None:
+                ctx.allreduce_(bucket)  # sum; Adam applies the 1/size of Average
+                return
         if self.wire is not None:
             w = self.wire[lo:hi]
             self.ops.scale_cast_bf16(bucket, w, 1.0)
@@ -669,14 +749,182 @@ class FusedMNISTTrainer:
         self.global_step += k
 
     def last_loss(self) -> float:
+        self.check_xgmi()
         return float(self.stats[:, 0].mean())
 
     def last_accuracy(self) -> float:
+        self.check_xgmi()
         return float(self.stats[:, 1].mean())
+
+    # ----------------------------------------------------------------------------- xGMI plane
+    def check_xgmi(self):
+        """Raise if a direct-xGMI collective of this trainer timed out waiting for a peer (its
+        outputs, and those of every later xGMI collective, are NaN). Waits for the current stream."""
+        if self.xplane is not None:
+            self.xplane.check()
+        for ctx in (self.xgmi or {}).values():
+            if ctx is not None:
+                ctx.check()
+
+    def _validate_xgmi(self, rounds: int = 2) -> bool:
+        """Run the plane's four xGMI collectives on random data and compare them with the same
+        collectives over the process group (gathers bitwise, the reduction to fp32 rounding).
+        Clobbers a2 and dz (every step recomputes them); the gradients and the W3 row shadow are restored."""
+        import torch.distributed as dist
+
+        W, B, r = self.world, self.B, self.rank
+        ok = True
+        g = torch.Generator(device="cpu").manual_seed(9173 + r)
+        saved_shadow3 = self.shadow3.clone() if self.shard_w3 else None
+        saved_grads = self.grads[:W3_START].clone()  # (the alignment gaps are never rewritten by a step)
+        lo, hi = self._w3_tiles if self.shard_w3 else (0, 49)
+        cols = slice(lo * 64, hi * 64)
+        others = [q for q in range(W) if q != r]
+        for _ in range(rounds):
+            self.a2.copy_(torch.randn(B, 3136, generator=g).to(torch.bfloat16))
+            self.dz.copy_(torch.randn(B, 1024, generator=g).to(torch.bfloat16))
+            self.grads[:W3_START].copy_(torch.randn(W3_START, generator=g))
+            ref_a2 = self.a2_all.clone()
+            ref_dz = self.dz_all.clone()
+            self._all_gather_rows(ref_a2, ref_a2[r * B:(r + 1) * B])
+            self._all_gather_rows(ref_dz, ref_dz[r * B:(r + 1) * B])
+            ref_g = self.grads[:W3_START].clone()
+            dist.all_reduce(ref_g)
+            self._gather_a2()
+            self.xplane.gather_rows("dz", 1, 1024 * 2, B)
+            self.xplane.reduce("grads", 2, self.gred)
+            if self.shard_w3:
+                T64 = self._T * 64
+                mine = self.shadow3[r * T64:(r + 1) * T64]
+                mine.copy_(torch.randn(T64, 1024, generator=g).to(torch.bfloat16))
+                ref_s = self.shadow3.clone()
+                self._all_gather_rows(ref_s, ref_s[r * T64:(r + 1) * T64])
+                self.xplane.gather_rows("shadow3", 3, 1024 * 2, T64, total_rows=min(W * T64, 3136))
+            torch.cuda.synchronize(self.device)
+            for q in others:
+                rows = slice(q * B, (q + 1) * B)
+                ok &= torch.equal(self.a2_all[rows, cols], ref_a2[rows, cols])
+                ok &= torch.equal(self.dz_all[rows], ref_dz[rows])
+                if self.shard_w3:
+                    srows = slice(q * T64, min((q + 1) * T64, 3136))
+                    ok &= torch.equal(self.shadow3[srows], ref_s[srows])
+            ok &= bool(torch.allclose(self.gred, ref_g, rtol=1e-5, atol=1e-5))
+        try:
+            self.xplane.check()
+        except RuntimeError:
+            ok = False
+        from ..parallel.xgmi import _group_ok
+
+        ok = _group_ok(ok, None, self.device)
+        if saved_shadow3 is not None:
+            self.shadow3.copy_(saved_shadow3)
+        self.grads[:W3_START].copy_(saved_grads)
+        return ok
+
+    def select_data_plane(self, steps: int = 40, steps_per_replay: int = 20) -> dict:
+        """Pick the data plane of the factor gather (MIHVD_XGMI=auto): validate the direct xGMI
+        collectives against the process group's, then time ``steps`` training steps on each plane
+        (graph-replayed when capturable) and keep the faster one. Collective; the decision is the
+        same on every rank (max time over ranks). Runs real training steps. Returns a report."""
+        import time
+
+        import torch.distributed as dist
+
+        rep = {"mode": self._xgmi_mode, "available": self.xplane is not None}
+        if self.xplane is None or self._xgmi_mode == "off":
+            self.use_xgmi = False
+            rep["plane"] = "rccl" if self.collectives else "none"
+            return rep
+        valid = self._validate_xgmi()
+        rep["valid"] = valid
+        if not valid:
+            from ..parallel.xgmi import warn_fallback
+
+            warn_fallback("validation against the process group's collectives failed")
+            self.use_xgmi = False
+            rep["plane"] = "rccl"
+            return rep
+        if self._xgmi_mode == "on" or self._host_collectives():
+            self.use_xgmi = True
+            rep["plane"] = "xgmi"
+            return rep
+        times = {}
+        k = max(1, min(steps_per_replay, steps))
+        for plane in (True, False):
+            self.use_xgmi = plane
+            self._graphs = {}
+            self.graph = None
+            captured = self.build_graph(steps_per_replay=k, warmup=1)
+            torch.cuda.synchronize(self.device)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(max(1, steps // k)):
+                self.run_graph()
+            torch.cuda.synchronize(self.device)
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.device)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            times["xgmi" if plane else "rccl"] = float(el.item()) / (max(1, steps // k) * k) * 1e6
+            rep["captured"] = captured
+        self.check_xgmi()
+        self.use_xgmi = times["xgmi"] <= times["rccl"]
+        self._graphs = {}
+        self.graph = None
+        rep["us_per_step"] = {p: round(t, 2) for p, t in times.items()}
+        rep["plane"] = "xgmi" if self.use_xgmi else "rccl"
+        return rep
+
+    def reduced_grads(self) -> torch.Tensor:
+        """The flat gradient buffer after the step's reduction (sums over ranks; the xGMI plane
+        reduces the small gradients into a separate buffer instead of in place)."""
+        if self.use_xgmi and self.gather:
+            return torch.cat([self.gred, self.grads[W3_START:]])
+        return self.grads
+
+    def data_plane(self) -> str:
+        if not self.collectives:
+            return "none"
+        if self.gather:
+            return "xgmi" if self.use_xgmi else "rccl"
+        return "xgmi" if self.xgmi and any(c is not None for c in self.xgmi.values()) else "rccl"
+
+    def close(self):
+        """Release the direct-xGMI regions (collective when they exist: peers may still read this
+        rank's region, so every rank synchronises and meets at a barrier first). The trainer is
+        unusable afterwards."""
+        if self._closed:
+            return
+        self._closed = True
+        ctxs = [c for c in (self.xgmi or {}).values() if c is not None]
+        if self.xplane is None and not ctxs:
+            return
+        import torch.distributed as dist
+
+        torch.cuda.synchronize(self.device)
+        self.graph = None
+        self._graphs = {}
+        if dist.is_initialized():
+            dist.barrier()
+        for c in ctxs:
+            c.close()
+        self.xgmi = {}
+        if self.xplane is not None:
+            for name in ("a2_all", "dz_all", "a2", "dz", "grads", "shadow3"):
+                if hasattr(self, name):
+                    setattr(self, name, None)
+            self.xplane.close()
+            self.xplane = None
+            self.use_xgmi = False
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     # ----------------------------------------------------------------------------- state
     def sync(self):
         torch.cuda.synchronize(self.device)
+        self.check_xgmi()
 
     def variables(self) -> dict[str, torch.Tensor]:
         """TF1 global variables (names of tensorflow_mnist.py's graph) for the checkpoint layout."""

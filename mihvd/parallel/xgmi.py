@@ -1,63 +1,223 @@
-"""Direct xGMI one-shot allreduce (SURVEY.md §2.3 N4 "optional xGMI direct allreduce", §5.8).
+"""Direct xGMI collectives over hipIpc-shared device memory (SURVEY.md §2.3 N4 "optional xGMI
+direct allreduce", §5.8).
 
-RCCL's ring/tree allreduce pays one link latency per hop; for the small, latency-bound gradient
-buckets of a B=100 MNIST step (horovod/tensorflow_mnist.py:133 reduces 8 tensors every step, all
-but ``dense/kernel`` under 250 KB) a one-shot exchange over the fully connected xGMI mesh of an
-MI355X node is shorter: every rank publishes its buffer, waits at a device-side barrier, then
-reads all peers' buffers over its own point-to-point links and sums them in rank order
-(``csrc/kernels/xgmi.hip``). No host involvement per call, so it can be captured in a HIP graph.
+RCCL's ring/tree collectives pay one link latency per hop; the messages of a B=100 MNIST step
+(horovod/tensorflow_mnist.py:133 reduces 8 tensors every step, all but ``dense/kernel`` under
+250 KB; the factor-gather plane moves sub-MB bf16 activations) are latency-bound, and on an MI355X
+node every GPU has its own xGMI link to every other GPU. So the one-shot shape is shorter: every
+rank reads all peers' copies over its own links at once (``csrc/kernels/xgmi.hip``). Each
+collective is one launch with a device-side phase barrier (epochs on the device, so it replays
+from a HIP graph).
 
-    ar = XGMIAllreduce(capacity_numel=1 << 20)       # collective: every rank of the group
-    ar.allreduce_(t, average=True)                   # fp32, contiguous, numel <= capacity
-    ar.check()                                       # raises if a device-side barrier timed out
+Two objects:
 
-Opt-in: the fused trainer uses it for its small-gradient bucket with ``MIHVD_XGMI_ALLREDUCE=1``;
-``scripts/allreduce_bw.py --xgmi`` compares it against RCCL. Every rank of the group must sit on
-one node (IPC handles), at most 8 ranks.
+* :class:`XGMIRegion` — a node-local communicator over one IPC-shared region per rank in which
+  callers place named buffers (same offsets on every rank). Collectives read peers' buffers in
+  place: ``gather_rows`` (every rank's row block of a ``[world*R][C]`` buffer into the local copy,
+  optionally only a column range) and ``reduce`` (sum of a buffer over ranks into a local tensor).
+  Phases: each call site uses its own phase id; see ``csrc/kernels/xgmi.hip`` for what entering a
+  phase promises the peers.
+* :class:`XGMIAllreduce` — allreduce of arbitrary fp32 tensors (staged into a double-buffered slot).
+
+Both need every rank of the group on ONE node (IPC handles do not cross hosts): construction
+checks that collectively (hostname + kernel boot id) and raises :class:`XGMIUnavailable`
+everywhere otherwise, so callers fall back to RCCL consistently. At most 8 ranks.
 """
 from __future__ import annotations
+
+import os
+import socket
+import warnings
 
 import torch
 import torch.distributed as dist
 
 from .. import ops as _ops
 
+MAX_RANKS = 8
+N_PHASES = 64
 
-class XGMIAllreduce:
-    def __init__(self, capacity_numel: int, group=None, device: torch.device | None = None):
+
+class XGMIUnavailable(RuntimeError):
+    """The direct xGMI path cannot be used by this group (raised on every rank alike)."""
+
+
+def _node_id() -> str:
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:  # pragma: no cover - non-Linux
+        boot = ""
+    return f"{socket.gethostname()}/{boot}"
+
+
+def check_single_node(group=None) -> bool:
+    """Collective: True on every rank iff every rank of ``group`` runs on this node."""
+    ids = [None] * dist.get_world_size(group)
+    dist.all_gather_object(ids, _node_id(), group=group)
+    return len(set(ids)) == 1
+
+
+def _group_ok(ok: bool, group, device) -> bool:
+    """Collective AND of a per-rank flag."""
+    backend = dist.get_backend(group)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+class XGMIRegion:
+    """Node-local peer-memory communicator. ``layout`` maps buffer names to ``(numel, dtype)``;
+    ``extra_bytes`` reserves raw space (e.g. allreduce slots) at :attr:`extra_offset`.
+    Collective: every rank of ``group`` constructs it with the same layout."""
+
+    def __init__(self, layout: dict, group=None, device: torch.device | None = None, extra_bytes: int = 0):
         if not dist.is_initialized():
-            raise RuntimeError("XGMIAllreduce needs an initialised process group")
+            raise XGMIUnavailable("the xGMI path needs an initialised process group")
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        if self.world > 8:
-            raise ValueError("XGMIAllreduce supports at most 8 ranks (one MI355X node)")
-        self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.capacity = int(capacity_numel)
-        o = _ops.load()
-        self._o = o
-        self.ctx = int(o.xgmi_create(self.device.index, self.capacity, self.rank, self.world))
-        mine = o.xgmi_handle(self.ctx)
+        if self.world > MAX_RANKS:
+            raise XGMIUnavailable(f"the xGMI path supports at most {MAX_RANKS} ranks (one MI355X node)")
+        device = torch.device(device) if device is not None else torch.device("cuda")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        if not check_single_node(group):
+            raise XGMIUnavailable("ranks span several nodes: IPC handles do not cross hosts")
+        self._o = _ops.load()
+        self.offsets, off = {}, 0
+        self.shapes = {}
+        for name, (numel, dtype) in layout.items():
+            self.offsets[name] = off
+            self.shapes[name] = (int(numel), dtype)
+            off += (int(numel) * torch.empty((), dtype=dtype).element_size() + 255) // 256 * 256
+        self.extra_offset = off
+        self.nbytes = off + (int(extra_bytes) + 255) // 256 * 256
+        err = None
+        self.ctx = None
+        try:
+            self.ctx = int(self._o.xgmi_create(self.device.index, max(self.nbytes, 256), self.rank, self.world))
+            mine = bytes(self._o.xgmi_handle(self.ctx).numpy().tobytes())
+        except Exception as e:  # pragma: no cover - depends on the driver
+            err, mine = e, b""
         handles = [None] * self.world
-        dist.all_gather_object(handles, bytes(mine.numpy().tobytes()), group=group)
-        table = torch.frombuffer(bytearray(b"".join(handles)), dtype=torch.uint8).view(self.world, -1).clone()
-        o.xgmi_open(self.ctx, table)
-        dist.barrier(group=group)  # every peer has opened every buffer before the first signal
+        dist.all_gather_object(handles, mine, group=group)
+        if err is None and any(not h for h in handles):
+            err = RuntimeError("a peer could not export its region")
+        if err is None:
+            try:
+                table = torch.frombuffer(bytearray(b"".join(handles)), dtype=torch.uint8).view(self.world, -1).clone()
+                self._o.xgmi_open(self.ctx, table)
+            except Exception as e:  # pragma: no cover - depends on the driver / peer access
+                err = e
+        if not _group_ok(err is None, group, self.device):
+            if self.ctx is not None:
+                self._o.xgmi_destroy(self.ctx)
+                self.ctx = None
+            raise XGMIUnavailable(f"IPC setup failed on at least one rank ({err!r})")
+        dist.barrier(group=group)  # every peer opened every region before the first signal
+        self._views = {}
         self._closed = False
 
+    # ------------------------------------------------------------------ buffers
+    def view(self, name: str) -> torch.Tensor:
+        """The 1-D tensor of buffer ``name`` in this rank's region (cached)."""
+        v = self._views.get(name)
+        if v is None:
+            numel, dtype = self.shapes[name]
+            v = self._views[name] = self._o.xgmi_view(self.ctx, self.offsets[name], numel, dtype)
+        return v
+
+    def raw_view(self, offset: int, numel: int, dtype=torch.float32) -> torch.Tensor:
+        return self._o.xgmi_view(self.ctx, offset, numel, dtype)
+
+    # ------------------------------------------------------------------ collectives
+    def gather_rows(self, name: str, phase: int, row_bytes: int, rows_per_rank: int, total_rows: int | None = None,
+                    col_lo: int = 0, col_hi: int | None = None):
+        """Copy every peer's rows ``[p*R, (p+1)*R)`` (capped at ``total_rows``) of buffer ``name``
+        (viewed as rows of ``row_bytes``), byte columns ``[col_lo, col_hi)``, into this rank's copy."""
+        total = self.world * rows_per_rank if total_rows is None else int(total_rows)
+        col_hi = row_bytes if col_hi is None else int(col_hi)
+        self._o.xgmi_gather_(self.ctx, phase, self.offsets[name], row_bytes, rows_per_rank, total, col_lo,
+                             col_hi - col_lo)
+
+    def reduce(self, name: str, phase: int, out: torch.Tensor, scale: float = 1.0, offset_elems: int = 0):
+        """``out = scale * sum over ranks`` of buffer ``name`` (fp32) starting at ``offset_elems``."""
+        self._o.xgmi_reduce_(self.ctx, phase, self.offsets[name] + 4 * int(offset_elems), out, scale)
+
+    def check(self):
+        """Wait for the current stream and raise if a device-side phase barrier timed out."""
+        if self.ctx is None:
+            return
+        err = int(self._o.xgmi_error(self.ctx))
+        if err:
+            ranks = [r for r in range(MAX_RANKS) if err & (1 << r)]
+            raise RuntimeError(f"xGMI collective timed out waiting for rank(s) {ranks} (error word {err:#x}); "
+                               "the outputs of this and every later xGMI collective are NaN")
+
+    def close(self):
+        if not self._closed and self.ctx is not None:
+            self._views.clear()
+            self._o.xgmi_destroy(self.ctx)
+            self._closed = True
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            if not getattr(self, "_closed", True) and torch.cuda.is_initialized():
+                self.close()
+        except Exception:
+            pass
+
+
+class XGMIAllreduce:
+    """Allreduce of any contiguous fp32 tensor of at most ``capacity_numel`` elements over the
+    direct xGMI path (stage into a double-buffered slot + one reduce launch)::
+
+        ar = XGMIAllreduce(capacity_numel=1 << 20)   # collective: every rank of the group
+        ar.allreduce_(t, average=True)               # in place, on the current stream
+        ar.check()                                   # raises if a device-side barrier timed out
+    """
+
+    def __init__(self, capacity_numel: int, group=None, device: torch.device | None = None, phase: int = 0):
+        self.capacity = int(capacity_numel)
+        self._slot = (self.capacity * 4 + 255) // 256 * 256
+        self.region = XGMIRegion({}, group=group, device=device, extra_bytes=2 * self._slot)
+        self.world = self.region.world
+        self.rank = self.region.rank
+        self.device = self.region.device
+        self.phase = int(phase)
+
+    @property
+    def ctx(self):
+        return self.region.ctx
+
     def allreduce_(self, t: torch.Tensor, average: bool = False, scale: float = 1.0) -> torch.Tensor:
-        """In-place sum (or average) of ``t`` over the group, on the current stream."""
         s = scale / self.world if average else scale
-        self._o.xgmi_allreduce_(self.ctx, t, s)
+        self.region._o.xgmi_allreduce_(self.region.ctx, self.phase, t, self.region.extra_offset, self._slot, s)
         return t
 
     def check(self):
-        """Synchronise the device and raise if any device-side barrier timed out."""
-        err = int(self._o.xgmi_error(self.ctx))
-        if err:
-            raise RuntimeError(f"xGMI allreduce barrier timed out waiting for peers (mask {err:#x})")
+        self.region.check()
 
     def close(self):
-        if not self._closed:
-            self._o.xgmi_destroy(self.ctx)
-            self._closed = True
+        self.region.close()
+
+
+def env_mode() -> str:
+    """``MIHVD_XGMI``: ``0``/``off`` (RCCL only), ``1``/``on`` (use it), ``auto`` (validate and time
+    against RCCL during warm-up, keep the faster; the default for the fused trainer)."""
+    v = os.environ.get("MIHVD_XGMI", os.environ.get("MIHVD_XGMI_ALLREDUCE", "auto")).strip().lower()
+    if v in ("0", "off", "false", "no", "rccl"):
+        return "off"
+    if v in ("1", "on", "true", "yes", "force"):
+        return "on"
+    return "auto"
+
+
+def warn_fallback(reason: str):
+    warnings.warn(f"direct xGMI data plane unavailable, using RCCL: {reason}", RuntimeWarning, stacklevel=2)
+
+
+__all__ = ["XGMIRegion", "XGMIAllreduce", "XGMIUnavailable", "check_single_node", "env_mode", "N_PHASES",
+           "MAX_RANKS"]

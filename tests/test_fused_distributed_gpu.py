@@ -20,21 +20,32 @@ def _gpu():
         pytest.skip("needs a GPU")
 
 
-@pytest.mark.parametrize("shard", ["0", "1"])
-def test_rccl_allreduce_inside_hip_graph(tmp_path, shard):
-    """shard=1: the sharded dense/kernel optimizer, whose bf16 row gather runs on the side stream
-    across step boundaries inside the graph."""
+@pytest.mark.parametrize("shard,xgmi", [("0", "off"), ("1", "off"), ("0", "on"), ("1", "on"), ("1", "auto")])
+def test_collectives_inside_hip_graph(tmp_path, shard, xgmi):
+    """World 1 with the collective data plane forced on, captured in the trainer's HIP graph and
+    replayed; must equal the trainer without collectives bit for bit. shard=1: the sharded
+    dense/kernel optimizer, whose bf16 row gather runs on the side stream across step boundaries.
+    xgmi=off: RCCL; on: the direct xGMI plane (all four collectives in the graph); auto: plane
+    selection (validation against RCCL + timed replays of both planes) first."""
     _gpu()
-    env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3=shard)
+    env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3=shard,
+               MIHVD_XGMI=xgmi)
     for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
         env.pop(k, None)
     p = subprocess.run([sys.executable, WORKER, "rccl_graph", str(tmp_path)], env=env, capture_output=True, text=True,
                        timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     r = json.loads((tmp_path / "rccl_graph.json").read_text())
-    assert r["captured"], "RCCL allreduce could not be captured into the HIP graph"
-    assert r["steps"] == 22 and r["bitwise"], r
+    assert r["captured"], "the collectives could not be captured into the HIP graph"
+    assert r["steps"] == r["pre_steps"] + 22 and r["bitwise"], r
     assert r["shard"] == (shard == "1")
+    if xgmi == "on":
+        assert r["plane"] == "xgmi", r
+    elif xgmi == "off":
+        assert r["plane"] == "rccl", r
+    else:
+        assert r["select"]["valid"] and r["plane"] in ("xgmi", "rccl"), r
+        assert set(r["select"]["us_per_step"]) == {"xgmi", "rccl"}, r
 
 
 @pytest.mark.parametrize("gather", ["1", "0"])
@@ -53,11 +64,13 @@ def test_fused_data_parallel_equivalence_two_ranks(tmp_path, gather):
 
 
 @pytest.mark.parametrize("gather", ["1", "0"])
-def test_fused_data_parallel_xgmi_allreduce_two_ranks(tmp_path, gather):
-    """The fused trainer's gradient buckets over the direct xGMI one-shot allreduce
-    (MIHVD_XGMI_ALLREDUCE=1; gloo only carries the factor gather and the IPC handle exchange)."""
+def test_fused_data_parallel_xgmi_two_ranks(tmp_path, gather):
+    """gather=1: the factor-gather plane over the direct xGMI collectives (a2/dz gathers and the
+    small-gradient reduction read the peer's region in place); gather=0: the gradient buckets over
+    the staged xGMI allreduce (MIHVD_XGMI_ALLREDUCE=1). gloo only carries the IPC handle exchange."""
     _gpu()
-    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_XGMI_ALLREDUCE="1")
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_XGMI_ALLREDUCE="1",
+               MIHVD_XGMI="on")
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -69,14 +82,17 @@ def test_fused_data_parallel_xgmi_allreduce_two_ranks(tmp_path, gather):
         assert o["rel_update_diff"] < 0.05, o
 
 
-def test_sharded_optimizer_matches_unsharded_two_ranks(tmp_path):
+@pytest.mark.parametrize("xgmi", ["off", "on"])
+def test_sharded_optimizer_matches_unsharded_two_ranks(tmp_path, xgmi):
+    """xgmi=on: both trainers on the direct xGMI plane (the W3 row gather too)."""
     _gpu()
-    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT)
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI=xgmi)
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo_shard", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(2):
         o = json.loads((tmp_path / f"dp_gloo_shard.{r}.json").read_text())
+        assert o["planes"] == (["xgmi", "xgmi"] if xgmi == "on" else ["rccl", "rccl"]), o
         assert all(o["same"].values()), o
         assert o["loss"] == o["loss_ref"]
 

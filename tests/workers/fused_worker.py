@@ -26,18 +26,27 @@ def data(n, seed=3):
 
 
 def sc_rccl_graph(outdir):
-    X, Y = data(2000)
+    # 50 steps per epoch: no reshuffle inside the (up to 44) steps, so eager and graph-replayed
+    # schedules of different lengths see the same batches
+    X, Y = data(5000)
     a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda",
                           shard_optimizer=os.environ.get("MIHVD_SHARD_W3") == "1")
     assert a.collectives, "MIHVD_FORCE_COLLECTIVES should enable the allreduce path"
     a.set_device_dataset(X, Y, seed=4)
     p0 = a.params.clone()
+    select = None
+    if os.environ.get("MIHVD_XGMI") == "auto":
+        # plane selection: validation against the process group + timed graph replays of both planes
+        select = a.select_data_plane(steps=10, steps_per_replay=5)
+    pre = a.global_step
     captured = a.build_graph(steps_per_replay=5)
     for _ in range(4):
         a.run_graph()
     os.environ["MIHVD_FORCE_COLLECTIVES"] = "0"
     b = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda")
     b.set_device_dataset(X, Y, seed=4)
+    for _ in range(pre):
+        b.device_step()
     b.build_graph(steps_per_replay=5)
     for _ in range(4):
         b.run_graph()
@@ -49,8 +58,10 @@ def sc_rccl_graph(outdir):
     bitwise = bool(torch.equal(a.params, b.params))
     with open(os.path.join(outdir, "rccl_graph.json"), "w") as f:
         json.dump({"captured": captured, "bitwise": bitwise, "rel_update_diff": rel, "steps": a.global_step,
-                   "shard": a.shard_w3, "loss": a.last_loss(),
+                   "pre_steps": pre, "select": select,
+                   "shard": a.shard_w3, "plane": a.data_plane(), "loss": a.last_loss(),
                    "loss_ref": b.last_loss()}, f)
+    a.close()
 
 
 def sc_dp_gloo(outdir):
@@ -72,13 +83,16 @@ def sc_dp_gloo(outdir):
         torch.cuda.synchronize()
         if step == 0:
             # allreduced SUM of the two per-rank batch means == 2 x the 100-sample batch mean
-            grel = ((tr.grads / 2 - ref.grads).norm() / ref.grads.norm()).item()
+            grel = ((tr.reduced_grads() / 2 - ref.grads).norm() / ref.grads.norm()).item()
     rel = ((tr.params - ref.params).norm() / (ref.params - p0).norm()).item()
     mx = (tr.params - ref.params).abs().max().item()
     spread = hvd.allgather(tr.params[:4096].cpu().view(1, -1))
+    tr.check_xgmi()
+    rec = {"gather": tr.gather, "xgmi": tr.data_plane() == "xgmi", "grad_rel": grel, "rel_update_diff": rel, "max": mx,
+           "rank_spread": (spread - spread[0]).abs().max().item()}
+    tr.close()
     with open(os.path.join(outdir, f"dp_gloo.{r}.json"), "w") as f:
-        json.dump({"gather": tr.gather, "xgmi": tr.xgmi is not None, "grad_rel": grel, "rel_update_diff": rel, "max": mx,
-                   "rank_spread": (spread - spread[0]).abs().max().item()}, f)
+        json.dump(rec, f)
 
 
 def sc_dp_gloo_shard(outdir):
@@ -99,8 +113,12 @@ def sc_dp_gloo_shard(outdir):
     trs[1].gather_full_state()
     same = {name: bool(torch.equal(getattr(trs[0], name), getattr(trs[1], name))) for name in ("params", "m", "v")}
     same["shadow_w3"] = bool(torch.equal(trs[0].w3_shadow(), trs[1].w3_shadow()))
+    rec = {"same": same, "loss": trs[1].last_loss(), "loss_ref": trs[0].last_loss(),
+           "planes": [tr.data_plane() for tr in trs]}
+    for tr in trs:
+        tr.close()
     with open(os.path.join(outdir, f"dp_gloo_shard.{r}.json"), "w") as f:
-        json.dump({"same": same, "loss": trs[1].last_loss(), "loss_ref": trs[0].last_loss()}, f)
+        json.dump(rec, f)
 
 
 def main():
