@@ -210,7 +210,7 @@ def main():
         loss_val = float(tr.last_loss())
     if args.impl != "fused":
         comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
-    elif n == 1:
+    elif n == 1 and not tr.collectives:
         comm_desc = "none (1 GPU)"
     elif getattr(tr, "shard_w3", False) and tr.data_plane() == "xgmi":
         comm_desc = ("direct xGMI one-shot collectives (hipIpc peer memory, device-side phase barriers): each rank "
@@ -242,7 +242,7 @@ def main():
                        "allreduce": comm_desc,
                        "steps_per_graph": per_call, "final_loss": loss_val},
         }
-        if args.impl == "fused" and n > 1:
+        if args.impl == "fused" and tr.collectives:
             rec["config"]["data_plane"] = tr.plane_report
         print(json.dumps(rec), flush=True)
     if args.impl == "fused":

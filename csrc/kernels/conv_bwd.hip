@@ -19,6 +19,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include "common.h"
+#include "xgmi_role.h"
 
 namespace mihvd {
 
@@ -97,13 +98,13 @@ __device__ __forceinline__ void conv2_bwd_block(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
-    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit) {
+    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int bx) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
-  if ((int)blockIdx.x < n_dgrad) {
+  if (bx < n_dgrad) {
     // ===================================================================== dgrad: image b
-    const int b = blockIdx.x;
+    const int b = bx;
     u16* Ws = smem;              // [800][64] swizzled, row = kk*32 + ci, cols = co
     u16* D = smem + CB_DG_W;     // [326][64] swizzled padded dY2 image (pixel = row)
     // Issue every load of the block first: W2 (13 x 16 B per thread), 2 dY2 items and the
@@ -362,7 +363,7 @@ __device__ __forceinline__ void conv2_bwd_block(
     return;
   }
   // ======================================================================= wgrad
-  const int bid = blockIdx.x - n_dgrad;
+  const int bid = bx - n_dgrad;
   const int kh = bid % 5, grp = bid / 5;
   const int h = wave >> 2, lw = wave & 3, th = t & 255;
   u16* A = smem + h * CB_WG_GRP;   // [325][32] padded a1 image (+ zero pixel 324)
@@ -480,9 +481,17 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
-    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int n_conv, AdamTail at) {
-  if ((int)blockIdx.x < n_conv)
-    conv2_bwd_block(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit);
+    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int n_conv, AdamTail at,
+    CollRole cr) {
+  // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk blocks (the CUs the 225 conv
+  // blocks of a B = 100 step leave idle)
+  if ((int)blockIdx.x < cr.nblk) {
+    coll_role_run(cr, blockIdx.x);
+    return;
+  }
+  const int bx = (int)blockIdx.x - cr.nblk;
+  if (bx < n_conv)
+    conv2_bwd_block(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit, bx);
   if constexpr (TAIL) adam_tail_run(at);
 }
 
@@ -618,7 +627,8 @@ int64_t conv2_wgrad_groups(int64_t B) { return (B + CB_IPB - 1) / CB_IPB; }
 static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                              const at::Tensor& x, const c10::optional<at::Tensor>& rows,
                              const c10::optional<at::Tensor>& state, const at::Tensor& idx1, at::Tensor& slab,
-                             at::Tensor& cpart, const c10::optional<at::Tensor>& g1, const AdamTail* tail) {
+                             at::Tensor& cpart, const c10::optional<at::Tensor>& g1, const AdamTail* tail,
+                             int64_t coll) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
@@ -649,11 +659,12 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
   const int role = debug_role_only();  // 0: dgrad blocks only, 1: wgrad blocks only, 2: no conv blocks
   const int n_dgrad = role == 1 ? 0 : B;
   const int n_conv = role == 2 ? 0 : role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
+  const CollRole cr = xgmi_role_lookup(coll);
   if (tail == nullptr) {
-    conv2_bwd_kernel<false><<<n_conv, 512, CB_LDS, stream>>>(
+    conv2_bwd_kernel<false><<<cr.nblk + n_conv, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{});
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, cr);
   } else {
     // one 512-thread block per CU (144 KB of LDS): the extra tail-only blocks take the CUs the
     // conv roles leave free, so the update streams from the first cycle
@@ -675,17 +686,19 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     at.first_free = n_conv;
     at.kpl = kpl;
     at.head = (int64_t)(head_frac * (double)((at.n4 + 64 * kpl - 1) / (64 * kpl)));
+    TORCH_CHECK(cr.nblk == 0, "conv2_bwd_adam: no co-launched collective with the optimizer tail");
     conv2_bwd_kernel<true><<<grid, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at);
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at, cr);
   }
 }
 
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1) {
-  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, g1, nullptr);
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1,
+               int64_t coll) {
+  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, g1, nullptr, coll);
 }
 
 static void check_flat(const at::Tensor& t, at::ScalarType dt, int64_t n, const char* what) {
@@ -710,7 +723,7 @@ void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tens
   AdamTail at{p3.data_ptr<float>(), g3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(),
               (u16*)shadow3.data_ptr(), n / 4, state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2,
               (float)eps, (float)grad_scale, (int)rule, 0, 0, 4};
-  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, &at);
+  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, &at, -1);
 }
 
 void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2, at::Tensor& gW1,

@@ -14,6 +14,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include "common.h"
+#include "xgmi_role.h"
 
 namespace mihvd {
 
@@ -200,12 +201,18 @@ __global__ void __launch_bounds__(NW * 64) conv12_fwd_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const u16* __restrict__ w1bf, const float* __restrict__ b1, const u16* __restrict__ w2bf,
     const float* __restrict__ b2, u16* __restrict__ a1, uint8_t* __restrict__ idx1, u16* __restrict__ a2,
-    uint8_t* __restrict__ idx2, int B) {
+    uint8_t* __restrict__ idx2, int B, CollRole cr) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   u16* img = smem;                    // [18][18][32] conv2 input (pooled conv1 output + zero halo)
   u16* wim = smem + C2_IMG;           // [800][C2_WROW]
   u16* xim = smem + C2_IMG + C2_W;    // [32][32] bf16 input image, 2-pixel zero halo
-  const int half = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk / 2 grid rows (on the CUs the
+  // 2 x B image blocks leave idle)
+  if ((int)blockIdx.y < (cr.nblk >> 1)) {
+    coll_role_run(cr, blockIdx.y * 2 + blockIdx.x);
+    return;
+  }
+  const int half = blockIdx.x, b = blockIdx.y - (cr.nblk >> 1), t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   // 1. loads. The weights do not depend on the data gather, so they are issued first and land
   //    while the dependent chain step -> rows[] -> image runs.
@@ -364,7 +371,7 @@ void conv2_fwd(const at::Tensor& a1, const at::Tensor& w2bf, const at::Tensor& b
 
 void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                 const at::Tensor& w1bf, const at::Tensor& b1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a1,
-                at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2) {
+                at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2, int64_t coll) {
   const int B = a1.size(0);
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "conv12_fwd: x");
   TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && a1.is_contiguous(), "conv12_fwd: a1");
@@ -397,11 +404,13 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
     return (e && atoi(e) == 4) ? 4 : 8;
   }();
   auto stream = c10::hip::getCurrentHIPStream().stream();
+  CollRole cr = xgmi_role_lookup(coll);
+  TORCH_CHECK(cr.nblk % 2 == 0, "conv12_fwd: a co-launched collective needs an even number of blocks");
   auto launch = [&](auto kern, int threads) {
-    kern<<<dim3(2, B), threads, C12_LDS_BYTES, stream>>>(
+    kern<<<dim3(2, B + cr.nblk / 2), threads, C12_LDS_BYTES, stream>>>(
         x.data_ptr<float>(), rp, n_pool, sp, (const u16*)w1bf.data_ptr(), b1.data_ptr<float>(),
         (const u16*)w2bf.data_ptr(), b2.data_ptr<float>(), (u16*)a1.data_ptr(), idx1.data_ptr<uint8_t>(),
-        (u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(), B);
+        (u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(), B, cr);
   };
   if (nw == 4) launch(conv12_fwd_kernel<4>, 256);
   else launch(conv12_fwd_kernel<8>, 512);

@@ -19,6 +19,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include "common.h"
+#include "xgmi_role.h"
 
 namespace mihvd {
 
@@ -86,10 +87,15 @@ __global__ void __launch_bounds__(256) head_kernel(
     const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, u16* __restrict__ h_out,
-    u16* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B) {
+    u16* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B, CollRole cr) {
   __shared__ float red[4][10];
   __shared__ float dl[10];
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk blocks
+  if ((int)blockIdx.x < cr.nblk) {
+    coll_role_run(cr, blockIdx.x);
+    return;
+  }
+  const int b = blockIdx.x - cr.nblk, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t step = state ? state[ST_FWD] : 0;
   const int n0 = t * 4;
   float4 parts[FC1_KS];
@@ -464,10 +470,14 @@ __global__ void __launch_bounds__(256) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
     const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
     float* __restrict__ gW4, float* __restrict__ gb4, int B, int tile_base, int n_small, AdamArgs ad, int write_grad,
-    int a2s, int a2c0) {
+    int a2s, int a2c0, CollRole cr) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  fc1_wgrad_block<ADAM>(blockIdx.x, dz, a2, h, dlog, dzw, a2w, Kw, gW3, gb3, gW4, gb4, B, tile_base, n_small, ad,
-                        write_grad, a2s, a2c0, smem);
+  if ((int)blockIdx.x < cr.nblk) {  // co-launched xGMI collective (xgmi_role.h)
+    coll_role_run(cr, blockIdx.x);
+    return;
+  }
+  fc1_wgrad_block<ADAM>((int)blockIdx.x - cr.nblk, dz, a2, h, dlog, dzw, a2w, Kw, gW3, gb3, gW4, gb4, B, tile_base,
+                        n_small, ad, write_grad, a2s, a2c0, smem);
 }
 
 // fc1_bwd: the dgrad tiles and every fc1_wgrad role (local batch) in one launch. The dgrad blocks
@@ -477,14 +487,21 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(const u16* __restrict__ dz
                                                       const u16* __restrict__ w3, u16* __restrict__ g2,
                                                       float* __restrict__ gW3, float* __restrict__ gb3,
                                                       float* __restrict__ gW4, float* __restrict__ gb4, int B, int G,
-                                                      int n_dg, int n_small) {
+                                                      int n_dg, int n_small, CollRole cr) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  if ((int)blockIdx.x < n_dg) {
-    fc1_dgrad_block(blockIdx.x, dz, w3, a2, g2, B, G, smem);
+  // co-launched xGMI collective on the first cr.nblk blocks (a multiple of 8, so the dgrad tiles
+  // keep their blockIdx -> XCD map)
+  if ((int)blockIdx.x < cr.nblk) {
+    coll_role_run(cr, blockIdx.x);
     return;
   }
-  fc1_wgrad_block<false>((int)blockIdx.x - n_dg, dz, a2, h, dlog, dz, a2, B, gW3, gb3, gW4, gb4, B, 0, n_small,
-                         AdamArgs{}, 1, FC1_K, 0, smem);
+  const int bx = (int)blockIdx.x - cr.nblk;
+  if (bx < n_dg) {
+    fc1_dgrad_block(bx, dz, w3, a2, g2, B, G, smem);
+    return;
+  }
+  fc1_wgrad_block<false>(bx - n_dg, dz, a2, h, dlog, dz, a2, B, gW3, gb3, gW4, gb4, B, 0, n_small, AdamArgs{}, 1,
+                         FC1_K, 0, smem);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -536,7 +553,8 @@ void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
 
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                  int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats) {
+                  int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
+                  int64_t coll) {
   const int B = h.size(0);
   TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "head: zpart");
   TORCH_CHECK(b3.numel() == FC1_N && w4.numel() == FC1_N * 10 && b4.numel() == 10 && w4.dtype() == at::kFloat, "head: params");
@@ -552,10 +570,12 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
   const uint32_t thresh = (uint32_t)(rate * 16777216.0);
   const float keep_scale = (float)(1.0 / (1.0 - rate));
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  head_kernel<<<B, 256, 0, stream>>>(zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(),
-                                     b4.data_ptr<float>(), labels.data_ptr<int64_t>(), rp, n_pool, sp, (uint32_t)seed,
-                                     thresh, keep_scale, (u16*)h.data_ptr(), (u16*)dz.data_ptr(), dlog.data_ptr<float>(),
-                                     stats.data_ptr<float>(), B);
+  const CollRole cr = xgmi_role_lookup(coll);
+  head_kernel<<<B + cr.nblk, 256, 0, stream>>>(zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(),
+                                               b4.data_ptr<float>(), labels.data_ptr<int64_t>(), rp, n_pool, sp,
+                                               (uint32_t)seed, thresh, keep_scale, (u16*)h.data_ptr(),
+                                               (u16*)dz.data_ptr(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B,
+                                               cr);
 }
 
 // roles: bit 0 = the dW3 tiles, bit 1 = the small reductions (db3, dW4, db4). dW3 multiplies dz_w3^T a2_w3 over their rows: the local dz/a2 by default, or the
@@ -564,7 +584,7 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
 static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
                              at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
                              const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3,
-                             const AdamArgs* ad, bool write_grad, int64_t jt_lo = 0, int64_t jt_hi = FC1_K / 64) {
+                             const AdamArgs* ad, bool write_grad, int64_t jt_lo, int64_t jt_hi, int64_t coll) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_wgrad: batch");
   TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
@@ -601,35 +621,38 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   TORCH_CHECK(0 <= jt_lo && jt_lo <= jt_hi && jt_hi <= FC1_K / 64, "fc1_wgrad: dW3 row-tile range must lie in [0, 49]");
   const int n_small = (roles & 2) ? FB_TOTAL - FB_WGRAD : 0;
   const int tile_base = (int)jt_lo * (FC1_N / 64);
-  const int grid = n_small + ((roles & 1) ? (int)(jt_hi - jt_lo) * (FC1_N / 64) : 0);
+  const CollRole cr = xgmi_role_lookup(coll);
+  const int grid = n_small + ((roles & 1) ? (int)(jt_hi - jt_lo) * (FC1_N / 64) : 0) + cr.nblk;
   if (grid == 0) return;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const u16 *pdz = (const u16*)dz.data_ptr(), *pa2 = (const u16*)a2.data_ptr(), *ph = (const u16*)h.data_ptr();
   if (ad != nullptr) {
     fc1_wgrad_kernel<true><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0, a2s, a2c0);
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0, a2s, a2c0, cr);
   } else {
     fc1_wgrad_kernel<false><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, AdamArgs{}, 1, a2s, a2c0);
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, AdamArgs{}, 1, a2s, a2c0, cr);
   }
 }
 
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
-               const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi) {
-  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, nullptr, true, jt_lo, jt_hi);
+               const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi, int64_t coll) {
+  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, nullptr, true, jt_lo, jt_hi, coll);
 }
 
 // fc1_wgrad with the Adam update of dense/kernel fused into the dW3 tiles (see the kernel). p3, m3,
-// v3 (fp32) and shadow3 (bf16) are the dense/kernel segments of the flat buffers; state is the
-// device step state (the optimizer step t is read from it; this op does not advance it).
+// v3 (fp32) and shadow3 (bf16) are the dense/kernel segments of the flat buffers (indexed by W3 row:
+// only the rows of the tiles [jt_lo, jt_hi) are touched); state is the device step state (the
+// optimizer step t is read from it; this op does not advance it).
 void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
                     at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
                     const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3, at::Tensor& p3,
                     at::Tensor& m3, at::Tensor& v3, at::Tensor& shadow3, const at::Tensor& state, double lr, double b1,
-                    double b2, double eps, double grad_scale, int64_t rule, bool write_grad) {
+                    double b2, double eps, double grad_scale, int64_t rule, bool write_grad, int64_t jt_lo,
+                    int64_t jt_hi, int64_t coll) {
   const int64_t n = (int64_t)FC1_K * FC1_N;
   for (const at::Tensor* t : {&p3, &m3, &v3})
     TORCH_CHECK(t->dtype() == at::kFloat && t->numel() == n && t->is_contiguous(), "fc1_wgrad_adam: p3/m3/v3 fp32 [3136*1024]");
@@ -639,7 +662,7 @@ void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor
     TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "fc1_wgrad_adam: 16-byte aligned segments required");
   AdamArgs ad{p3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(), (u16*)shadow3.data_ptr(),
               state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale, (int)rule};
-  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, &ad, write_grad);
+  fc1_wgrad_launch(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, &ad, write_grad, jt_lo, jt_hi, coll);
 }
 
 // dgrad: g2 = (a2 > 0) * dz.W3^T in bf16, the gradient conv2_bwd routes through the pool argmax.
@@ -662,7 +685,7 @@ void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a
 // roles as fc1_wgrad: bit 0 = the dW3 tiles, bit 1 = db3 / dW4 / db4.
 void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
              const at::Tensor& w3bf, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& g2,
-             int64_t roles) {
+             int64_t roles, int64_t coll) {
   TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_bwd: roles must be 1, 2 or 3");
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_bwd: batch");
@@ -676,13 +699,15 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
   const int G = (B + DG_ROWS - 1) / DG_ROWS;
   const int n_dg = 8 * ((DG_JT + 7) / 8) * G;
   const int n_small = (roles & 2) ? FB_TOTAL - FB_WGRAD : 0;
-  const int grid = n_dg + n_small + ((roles & 1) ? FB_WGRAD : 0);
+  CollRole cr = xgmi_role_lookup(coll);
+  TORCH_CHECK(cr.nblk % 8 == 0, "fc1_bwd: a co-launched collective needs a multiple of 8 blocks (XCD map)");
+  const int grid = cr.nblk + n_dg + n_small + ((roles & 1) ? FB_WGRAD : 0);
   auto stream = c10::hip::getCurrentHIPStream().stream();
   set_max_lds(fc1_bwd_kernel, DG_LDS);
   fc1_bwd_kernel<<<grid, 256, DG_LDS, stream>>>(
       (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
       (const u16*)w3bf.data_ptr(), (u16*)g2.data_ptr(), gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg, n_small);
+      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg, n_small, cr);
 }
 
 }  // namespace mihvd

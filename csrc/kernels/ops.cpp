@@ -10,27 +10,30 @@ void conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const
 void conv2_fwd(const at::Tensor& a1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
 void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                 const at::Tensor& w1bf, const at::Tensor& b1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a1,
-                at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2);
+                at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2, int64_t coll);
 void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart);
 void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
              const at::Tensor& w3bf, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& g2,
-             int64_t roles);
+             int64_t roles, int64_t coll);
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                  int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats);
+                  int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
+                  int64_t coll);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
-               const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi);
+               const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi, int64_t coll);
 void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
                     at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles,
                     const c10::optional<at::Tensor>& dz_w3, const c10::optional<at::Tensor>& a2_w3, at::Tensor& p3,
                     at::Tensor& m3, at::Tensor& v3, at::Tensor& shadow3, const at::Tensor& state, double lr, double b1,
-                    double b2, double eps, double grad_scale, int64_t rule, bool write_grad);
+                    double b2, double eps, double grad_scale, int64_t rule, bool write_grad, int64_t jt_lo,
+                    int64_t jt_hi, int64_t coll);
 void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& g2);
 int64_t conv2_wgrad_groups(int64_t B);
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1);
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1,
+               int64_t coll);
 void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2, at::Tensor& gW1,
                         at::Tensor& gb1, at::Tensor& gb2);
 void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
@@ -82,34 +85,36 @@ void conv2_fwd_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a
 }
 void conv12_fwd_op(const Tensor& x, const c10::optional<Tensor>& rows, const c10::optional<Tensor>& state,
                    const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2, Tensor a1, Tensor idx1,
-                   Tensor a2, Tensor idx2) {
-  mihvd::conv12_fwd(x, rows, state, w1, b1, w2, b2, a1, idx1, a2, idx2);
+                   Tensor a2, Tensor idx2, int64_t coll) {
+  mihvd::conv12_fwd(x, rows, state, w1, b1, w2, b2, a1, idx1, a2, idx2, coll);
 }
 void fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, const Tensor& w3, Tensor gW3,
-               Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles) {
-  mihvd::fc1_bwd(dz, a2, h, dlog, w3, gW3, gb3, gW4, gb4, g2, roles);
+               Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles, int64_t coll) {
+  mihvd::fc1_bwd(dz, a2, h, dlog, w3, gW3, gb3, gW4, gb4, g2, roles, coll);
 }
 void fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::fc1_fwd(a2, w3, zpart); }
 void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
-             const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog, Tensor stats) {
-  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats);
+             const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog, Tensor stats,
+             int64_t coll) {
+  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll);
 }
 void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, Tensor gW3, Tensor gb3,
                   Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3, int64_t jt_lo,
-                  int64_t jt_hi) {
-  mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, jt_lo, jt_hi);
+                  int64_t jt_hi, int64_t coll) {
+  mihvd::fc1_wgrad(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, jt_lo, jt_hi, coll);
 }
 void fc1_wgrad_adam_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, Tensor gW3, Tensor gb3,
                        Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3, Tensor p3, Tensor m3,
                        Tensor v3, Tensor shadow3, const Tensor& state, double lr, double b1, double b2, double eps,
-                       double grad_scale, int64_t rule, bool write_grad) {
+                       double grad_scale, int64_t rule, bool write_grad, int64_t jt_lo, int64_t jt_hi, int64_t coll) {
   mihvd::fc1_wgrad_adam(dz, a2, h, dlog, gW3, gb3, gW4, gb4, roles, dz_w3, a2_w3, p3, m3, v3, shadow3, state, lr, b1, b2,
-                        eps, grad_scale, rule, write_grad);
+                        eps, grad_scale, rule, write_grad, jt_lo, jt_hi, coll);
 }
 void fc1_dgrad_op(const Tensor& dz, const Tensor& w3, const Tensor& a2, Tensor g2) { mihvd::fc1_dgrad(dz, w3, a2, g2); }
 void conv2_bwd_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, const Tensor& x,
-                  const OptT& rows, const OptT& state, const Tensor& idx1, Tensor slab, Tensor cpart, const OptT& g1) {
-  mihvd::conv2_bwd(g2, idx2, a1, w2, x, rows, state, idx1, slab, cpart, g1);
+                  const OptT& rows, const OptT& state, const Tensor& idx1, Tensor slab, Tensor cpart, const OptT& g1,
+                  int64_t coll) {
+  mihvd::conv2_bwd(g2, idx2, a1, w2, x, rows, state, idx1, slab, cpart, g1, coll);
 }
 void conv2_wgrad_reduce_op(const Tensor& slab, const Tensor& cpart, int64_t B, Tensor gW2, Tensor gW1, Tensor gb1,
                            Tensor gb2) {
@@ -168,22 +173,23 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
   m.def("conv2_fwd(Tensor a1, Tensor w2bf, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
   m.def("conv12_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1bf, Tensor b1, Tensor w2bf, Tensor b2, "
-        "Tensor(a!) a1, Tensor(b!) idx1, Tensor(c!) a2, Tensor(d!) idx2) -> ()");
+        "Tensor(a!) a1, Tensor(b!) idx1, Tensor(c!) a2, Tensor(d!) idx2, int coll=-1) -> ()");
   m.def("fc1_bwd(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor w3bf, Tensor(a!) gW3, Tensor(b!) gb3, "
-        "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3) -> ()");
+        "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3, int coll=-1) -> ()");
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
-        "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
+        "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, int coll=-1) -> ()");
   m.def("fc1_wgrad(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
-        "Tensor(d!) gb4, int roles=3, Tensor? dz_w3=None, Tensor? a2_w3=None, int jt_lo=0, int jt_hi=49) -> ()");
+        "Tensor(d!) gb4, int roles=3, Tensor? dz_w3=None, Tensor? a2_w3=None, int jt_lo=0, int jt_hi=49, "
+        "int coll=-1) -> ()");
   m.def("fc1_wgrad_adam(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
         "Tensor(d!) gb4, int roles, Tensor? dz_w3, Tensor? a2_w3, Tensor(e!) p3, Tensor(f!) m3, Tensor(g!) v3, "
         "Tensor(h!) shadow3, Tensor state, float lr, float b1, float b2, float eps, float grad_scale, int rule, "
-        "bool write_grad=False) -> ()");
+        "bool write_grad=False, int jt_lo=0, int jt_hi=49, int coll=-1) -> ()");
   m.def("fc1_dgrad(Tensor dz, Tensor w3bf, Tensor a2, Tensor(a!) g2) -> ()");
   m.def("conv2_wgrad_groups(int B) -> int", &mihvd::conv2_wgrad_groups);
   m.def("conv2_bwd(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, Tensor? state, Tensor idx1, "
-        "Tensor(a!) slab, Tensor(b!) cpart, Tensor(c!)? g1=None) -> ()");
+        "Tensor(a!) slab, Tensor(b!) cpart, Tensor(c!)? g1=None, int coll=-1) -> ()");
   m.def("conv2_wgrad_reduce(Tensor slab, Tensor cpart, int B, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
         "Tensor(d!) gb2) -> ()");
   m.def("conv2_bwd_adam(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, Tensor(s!) state, "

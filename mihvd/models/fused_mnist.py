@@ -155,29 +155,32 @@ class FusedMNISTTrainer:
         # Sharded dense/kernel optimizer (factor-gather plane only; shard_optimizer=True or
         # MIHVD_SHARD_W3=1): rank r owns W3 row tiles [r*T, (r+1)*T) of the 49 64-row tiles
         # (T = ceil(49/size)). It computes dW3 for those rows only (over every rank's samples, so the
-        # result is the exact allreduced sum), applies Adam to them, and all-gathers the updated bf16
-        # rows into a padded shadow [size*T*64][1024] on the side stream — overlapping the next
-        # step's convolutions — instead of every rank computing all of dW3 and updating all of W3.
-        # fp32 master rows / Adam slots of other ranks' rows are not maintained here; call
-        # gather_full_state() on every rank before variables()/to_model().
+        # result is the exact allreduced sum), applies Adam to them, and gathers the updated bf16
+        # rows of the other ranks into a padded shadow [size*T*64][1024] before the next fc1_fwd,
+        # instead of every rank computing all of dW3 and updating all of W3. fp32 master rows / Adam
+        # slots of other ranks' rows are not maintained here; call gather_full_state() on every
+        # rank before variables()/to_model(). Unsharded, every rank owns all 49 tiles. The flag can
+        # change between steps (set_sharding, collective): the row gather moves (size-1)/size of the
+        # 6.4 MB bf16 W3 per step over size-1 links, so it pays at 8 GPUs, not at 2.
         if shard_optimizer is None:
             shard_optimizer = os.environ.get("MIHVD_SHARD_W3", "0") == "1"
         self.shard_w3 = bool(shard_optimizer) and self.gather and not self.fuse_w3_requested()
         self._shadow_ev = None
         self._full_state_valid = True
-        if self.shard_w3:
-            self._T = -(-49 // self.world)
-            lo, hi = self.rank * self._T, min((self.rank + 1) * self._T, 49)
-            self._w3_tiles = (lo, max(lo, hi))
+        self._T = -(-49 // self.world)
+        lo, hi = self.rank * self._T, min((self.rank + 1) * self._T, 49)
+        self._w3_mine = (lo, max(lo, hi))
         # Direct xGMI data plane for the factor gather (MIHVD_XGMI=auto|on|off, mihvd/parallel/xgmi.py):
-        # a2, dz, the gradient buffer and the W3 row shadow live in one hipIpc-shared region per rank,
-        # and the plane's four collectives per step are one-shot launches that read the peers'
-        # copies in place over xGMI — a2 only for the columns this rank's W3 rows need — instead of
-        # RCCL all-gathers/allreduce. "auto" validates it against RCCL and times both
-        # (select_data_plane); ranks on several nodes or a failed IPC setup fall back to RCCL.
+        # a2, dz, the gradient buffer and the W3 row shadow live in one hipIpc-shared region per rank;
+        # the plane's collectives read the peers' copies in place over xGMI (a2 only for the columns
+        # this rank's W3 rows need) and run as the first blocks of compute launches of the step
+        # (co-launch: no extra launch, no stream fork/join), instead of RCCL all-gathers/allreduce on
+        # a side stream. "auto" validates it against RCCL and times both (select_data_plane); ranks
+        # on several nodes or a failed IPC setup fall back to RCCL.
         self.xplane = None
         self.use_xgmi = False
         self._xgmi_mode = "off"
+        self._roles = None
         if self.gather:
             from ..parallel import xgmi as _xg
 
@@ -187,9 +190,8 @@ class FusedMNISTTrainer:
 
                 if dist.is_initialized():
                     layout = {"a2": (self.world * B * 3136, torch.bfloat16), "dz": (self.world * B * 1024, torch.bfloat16),
-                              "grads": (FLAT_NUMEL, torch.float32)}
-                    if self.shard_w3:
-                        layout["shadow3"] = (self.world * self._T * 64 * 1024, torch.bfloat16)
+                              "grads": (FLAT_NUMEL, torch.float32),
+                              "shadow3": (self.world * self._T * 64 * 1024, torch.bfloat16)}
                     try:
                         self.xplane = _xg.XGMIRegion(layout, device=dev)
                     except _xg.XGMIUnavailable as e:
@@ -201,21 +203,18 @@ class FusedMNISTTrainer:
                 self.a2_all = self.xplane.view("a2").view(self.world * B, 3136)
                 self.dz_all = self.xplane.view("dz").view(self.world * B, 1024)
                 self.grads = self.xplane.view("grads")
+                self.shadow3 = self.xplane.view("shadow3").view(self.world * self._T * 64, 1024)
                 self.gred = torch.zeros(W3_START, **f32)  # xGMI sum of the small gradients
             else:
                 self.a2_all = torch.empty(self.world * B, 3136, **bf)
                 self.dz_all = torch.empty(self.world * B, 1024, **bf)
+                self.shadow3 = torch.zeros(self.world * self._T * 64, 1024, **bf)
             self.a2 = self.a2_all[self.rank * B:(self.rank + 1) * B]   # conv2_fwd writes its rows in place
             self.dz = self.dz_all[self.rank * B:(self.rank + 1) * B]   # head writes its rows in place
+            self._refresh_shadow()
         else:
             self.a2 = torch.empty(B, 3136, **bf)
             self.dz = torch.empty(B, 1024, **bf)
-        if self.shard_w3:
-            if self.xplane is not None:
-                self.shadow3 = self.xplane.view("shadow3").view(self.world * self._T * 64, 1024)
-            else:
-                self.shadow3 = torch.zeros(self.world * self._T * 64, 1024, **bf)
-            self._refresh_shadow()
         self.idx2 = torch.empty(B, 3136, **u8)
         self.zpart = torch.empty(14, B, 1024, **f32)
         self.h = torch.empty(B, 1024, **bf)
@@ -283,10 +282,16 @@ class FusedMNISTTrainer:
         return os.environ.get("MIHVD_FUSE_W3_ADAM", "0") == "1"
 
     def w3_shadow(self) -> torch.Tensor:
-        """The bf16 dense/kernel the MFMA kernels read ([3136][1024], contiguous)."""
-        if self.shard_w3:
+        """The bf16 dense/kernel the MFMA kernels read ([3136][1024], contiguous): on the
+        factor-gather plane the first 3136 rows of the (row-gathered) shadow3 buffer."""
+        if self.gather:
             return self.shadow3[:3136]
         return self.pview("dense/kernel", self.shadow)
+
+    @property
+    def _w3_tiles(self):
+        """The dense/kernel 64-row tiles whose dW3 and Adam update this rank computes."""
+        return self._w3_mine if self.shard_w3 else (0, 49)
 
     def pview(self, name, buf=None):
         off, n = SEGMENTS[name]
@@ -303,7 +308,7 @@ class FusedMNISTTrainer:
 
     def _refresh_shadow(self):
         self.ops.scale_cast_bf16(self.params, self.shadow, 1.0)
-        if self.shard_w3:
+        if getattr(self, "shadow3", None) is not None:
             self.shadow3[:3136].copy_(self.pview("dense/kernel", self.shadow))
 
     def _require_full_state(self):
@@ -442,31 +447,27 @@ class FusedMNISTTrainer:
                     1.0 / self.world, self.rule, 1)
 
     def _launch_step_gather(self, x, rows, labels):
-        """Step with the factor-gather data plane (see ``__init__``). Collectives run one at a time
-        on the side stream, each overlapping compute on the main stream:
+        """Step with the factor-gather data plane over the process group (RCCL; see ``__init__``).
+        Collectives run one at a time on the side stream, each overlapping compute on main
+        (sharded optimizer shown):
 
-            main: conv1 conv2 | fc1_fwd head | fc1 small grads, fc1_dgrad, conv2_bwd, dW2 | dW3 (K = size*B) | adam
-            side:             AG(a2)        AG(dz)                                        AR(every other grad)
+            main: conv12 | fc1_fwd head | fc1_bwd (small grads + dgrad), conv2_bwd, dW2 | dW3 rows, Adam rows |
+            side:        AG(a2)        AG(dz)                                          AR(other grads)    AG(W3 rows) ->
+                                                                                                next step's fc1_fwd
+        The xGMI plane runs the same collectives co-launched in one stream (_launch_step_xgmi).
         """
+        if self.use_xgmi:
+            return self._launch_step_xgmi(x, rows, labels)
         o = self.ops
         st = self.state
         main = torch.cuda.current_stream(self.device)
         side = self._side
         self._conv_forward(x, rows, st)
-        # (with RCCL this gathers whole a2 rows: an all-to-all of only the column slice each rank
-        # needs cannot be captured, torch's RCCL process group watchdog queries the captured event
-        # and aborts; the xGMI plane reads just those columns from the peers)
+        # (whole a2 rows: an all-to-all of only the column slice each rank needs cannot be captured,
+        # torch's RCCL process group watchdog queries the captured event and aborts)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self._gather_a2()
-            a_done = None
-            if self.use_xgmi and not self.shard_w3:
-                # the peers read this rank's small gradients in place (xGMI phase 2 of the last
-                # step); they are rewritten by fc1_bwd below, which therefore waits until every peer
-                # entered this step's phase 0 (and so finished phase 2). With the sharded optimizer
-                # the wait on the W3 row gather (phase 3) below already implies it.
-                a_done = torch.cuda.Event()
-                a_done.record(side)
+            self._all_gather_rows(self.a2_all, self.a2)
         if self._shadow_ev is not None:
             # the previous step's W3 row gather (side stream) must land before the first reader
             main.wait_event(self._shadow_ev)
@@ -476,15 +477,10 @@ class FusedMNISTTrainer:
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            if self.use_xgmi:
-                self.xplane.gather_rows("dz", 1, 1024 * 2, self.B)
-            else:
-                self._all_gather_rows(self.dz_all, self.dz)
+            self._all_gather_rows(self.dz_all, self.dz)
         gW3 = self.gview("dense/kernel")
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
                  self.gview("dense_1/bias"))
-        if a_done is not None:
-            main.wait_event(a_done)
         if self.fc1_merged:  # db3, dW4, db4 of the local batch + the dgrad tiles, one launch
             o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2)
         else:
@@ -494,72 +490,111 @@ class FusedMNISTTrainer:
         main.wait_stream(side)   # both gathers done: the communicator is free
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            if self.use_xgmi:
-                self.xplane.reduce("grads", 2, self.gred)  # sum; Adam applies the 1/size of Average
-            else:
-                self._allreduce(self.grads[:W3_START], 0, W3_START)
-        gsmall = self.gred if self.use_xgmi else self.grads[:W3_START]
+            self._allreduce(self.grads[:W3_START], 0, W3_START)
+        ar_done = torch.cuda.Event()
+        ar_done.record(side)
         b1, b2 = self.betas
+        lo, hi = self._w3_tiles
+        if self.fuse_w3:
+            # dW3 summed over every rank's samples, Adam applied to W3 in the same tiles
+            self._fc1_wgrad_w3_adam(1, self.dz_all, self.a2_all, lo, hi)
+        elif hi > lo:
+            # dW3 rows of this rank's tiles over every rank's samples, then Adam on those rows
+            o.fc1_wgrad(*small, 1, self.dz_all, self.a2_all, lo, hi)
+            a, b = W3_START + lo * 64 * 1024, W3_START + hi * 64 * 1024
+            o.adam_step(self.params[a:b], self.grads[a:b], self.m[a:b], self.v[a:b],
+                        self.shadow3[lo * 64:hi * 64].view(-1), st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world,
+                        self.rule, 0)
         if self.shard_w3:
-            ar_done = torch.cuda.Event()
-            ar_done.record(side)
-            lo, hi = self._w3_tiles
-            if hi > lo:
-                # dW3 rows of this rank's tiles over every rank's samples, then Adam on those rows
-                o.fc1_wgrad(*small, 1, self.dz_all, self.a2_all, lo, hi)
-                a, b = W3_START + lo * 64 * 1024, W3_START + hi * 64 * 1024
-                o.adam_step(self.params[a:b], self.grads[a:b], self.m[a:b], self.v[a:b],
-                            self.shadow3[lo * 64:hi * 64].view(-1), st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world,
-                            self.rule, 0)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 T64 = self._T * 64
-                if self.use_xgmi:
-                    self.xplane.gather_rows("shadow3", 3, 1024 * 2, T64, total_rows=min(self.world * T64, 3136))
-                else:
-                    self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
+                self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
                 self._shadow_ev = torch.cuda.Event()
                 self._shadow_ev.record(side)
-            main.wait_event(ar_done)
-            o.adam_step(self.params[:W3_START], gsmall, self.m[:W3_START], self.v[:W3_START],
-                        self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
             self._full_state_valid = False
-            return
-        if self.fuse_w3:
-            # dW3 summed over every rank's samples, Adam applied to W3 in the same tiles
-            self._fc1_wgrad_w3_adam(1, self.dz_all, self.a2_all)
-            main.wait_stream(side)
-            o.adam_step(self.params[:W3_START], gsmall, self.m[:W3_START], self.v[:W3_START],
-                        self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-            return
-        o.fc1_wgrad(*small, 1, self.dz_all, self.a2_all)  # dW3 summed over every rank's samples
-        main.wait_stream(side)
-        if self.use_xgmi:
-            w3 = slice(W3_START, FLAT_NUMEL)
-            o.adam_step(self.params[w3], self.grads[w3], self.m[w3], self.v[w3], self.shadow[w3], st, 0, self.lr, b1, b2,
-                        self.eps, 1.0 / self.world, self.rule, 0)
-            o.adam_step(self.params[:W3_START], gsmall, self.m[:W3_START], self.v[:W3_START], self.shadow[:W3_START],
-                        st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-            return
-        o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
-                    1.0 / self.world, self.rule, 1)
+        main.wait_event(ar_done)
+        o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START],
+                    self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
 
-    def _gather_a2(self):
-        """All ranks' a2 rows (the fc1 input factors) into a2_all: with xGMI only the byte columns
-        of this rank's W3 row tiles (all that its dW3 rows read), else whole rows over RCCL."""
-        if self.use_xgmi:
-            lo, hi = self._w3_tiles if self.shard_w3 else (0, 49)
-            self.xplane.gather_rows("a2", 0, 3136 * 2, self.B, col_lo=lo * 128, col_hi=hi * 128)
-        else:
-            self._all_gather_rows(self.a2_all, self.a2)
+    # xGMI phase ids of the factor-gather plane (csrc/kernels/xgmi_role.h), in step order
+    PH_W3, PH_DZ, PH_A2, PH_SMALL = 3, 1, 0, 2
 
-    def _fc1_wgrad_w3_adam(self, roles, dz_all, a2_all):
+    def _prepare_roles(self):
+        """Descriptors of the plane's xGMI collectives (built once; they hold the buffers' pointers
+        and the optimizer hyper-parameters, so a new learning rate prepares them again)."""
+        xp, W, B = self.xplane, self.world, self.B
+        b1, b2 = self.betas
+        lo, hi = self._w3_mine
+        h = slice(0, W3_START)
+        T64 = self._T * 64
+        r = {"lr": self.lr}
+        # dz rows, in fc1_bwd's launch (a multiple of 8 blocks: its dgrad tiles keep their XCD map)
+        r["dz"] = xp.prepare_gather("dz", self.PH_DZ, 1024 * 2, B, nblk=64)
+        # a2 columns of this rank's W3 row tiles (sharded) / whole rows (627 KB per peer), in the
+        # launch with the longest window, conv2_bwd, on the CUs its 225 blocks leave idle (one
+        # 512-thread block per CU: 144 KB of LDS)
+        nb = max(2, 256 - (B + 5 * ((B + 3) // 4)) - 1)
+        r["a2_shard"] = xp.prepare_gather("a2", self.PH_A2, 3136 * 2, B, col_lo=lo * 128, col_hi=hi * 128, nblk=nb)
+        r["a2_full"] = xp.prepare_gather("a2", self.PH_A2, 3136 * 2, B, nblk=nb)
+        # small gradients: one-shot sum + their Adam update (1/size of Average = the Adam gradient
+        # scale) + the forward step bump, in fc1_wgrad's launch
+        r["small"] = xp.prepare_reduce("grads", self.PH_SMALL, self.gred, 1.0, nblk=64, adam=dict(
+            p=self.params[h], m=self.m[h], v=self.v[h], shadow=self.shadow[h], state=self.state, lr=self.lr, b1=b1,
+            b2=b2, eps=self.eps, grad_scale=1.0 / W, rule=self.rule))
+        # the other ranks' updated W3 rows (sharded), in the next step's conv12_fwd launch, on the
+        # CUs its 2 x B image blocks leave idle
+        r["w3"] = xp.prepare_gather("shadow3", self.PH_W3, 1024 * 2, T64, total_rows=min(W * T64, 3136),
+                                    nblk=max(2, (256 - 2 * B) // 2 * 2))
+        # replicated optimizer: the same phase moving no bytes (a fence): fc1_bwd rewrites the small
+        # gradients the peers summed in the last step's phase PH_SMALL, so a phase must separate them
+        r["fence"] = xp.prepare_gather("shadow3", self.PH_W3, 1024 * 2, T64, total_rows=0, col_lo=0, col_hi=0, nblk=2)
+        self._roles = r
+
+    def _launch_step_xgmi(self, x, rows, labels):
+        """Factor-gather step on the direct xGMI plane: ONE stream, every collective co-launched
+        with a compute kernel (csrc/kernels/xgmi_role.h), seven launches:
+
+            conv12_fwd [+ W3 rows of the other ranks (sharded)] | fc1_fwd | head |
+            fc1_bwd dgrad + db3/dW4/db4 [+ dz] | conv2_bwd [+ a2 columns] | conv2_wgrad_reduce |
+            dW3 tiles of this rank with Adam in the epilogue [+ small-gradient sum + their Adam]
+
+        Each bracketed collective reads what the peers produced in earlier launches; the phase
+        order (W3 rows, dz, a2, small) gives every buffer rewrite a later phase that proves the
+        peers finished reading it (docs/ARCHITECTURE.md, "xGMI plane")."""
+        o = self.ops
+        st = self.state
+        if self._roles is None or self._roles["lr"] != self.lr:
+            self._prepare_roles()
+        R = self._roles
+        b1, b2 = self.betas
+        w2 = self.pview("conv_layer2/conv2d/kernel", self.shadow)
+        o.conv12_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel", self.shadow),
+                     self.pview("conv_layer1/conv2d/bias"), w2, self.pview("conv_layer2/conv2d/bias"), self.a1, self.idx1,
+                     self.a2, self.idx2, R["w3"] if self.shard_w3 else R["fence"])
+        o.fc1_fwd(self.a2, self.w3_shadow(), self.zpart)
+        o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
+                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        gW3 = self.gview("dense/kernel")
+        small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
+                 self.gview("dense_1/bias"))
+        o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2, R["dz"])
+        self._conv_backward(x, rows, st, R["a2_shard"] if self.shard_w3 else R["a2_full"])
+        lo, hi = self._w3_tiles
+        w3 = slice(W3_START, FLAT_NUMEL)
+        o.fc1_wgrad_adam(*small, 1, self.dz_all, self.a2_all, self.params[w3], self.m[w3], self.v[w3],
+                         self.shadow3[:3136].view(-1), st, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule,
+                         self.keep_w3_grad, lo, hi, R["small"])
+        if self.shard_w3:
+            self._full_state_valid = False
+
+    def _fc1_wgrad_w3_adam(self, roles, dz_all, a2_all, lo=0, hi=49):
         b1, b2 = self.betas
         w3 = slice(W3_START, FLAT_NUMEL)
         self.ops.fc1_wgrad_adam(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
                                 self.gview("dense_1/kernel"), self.gview("dense_1/bias"), roles, dz_all, a2_all,
-                                self.params[w3], self.m[w3], self.v[w3], self.shadow[w3], self.state, self.lr, b1, b2,
-                                self.eps, 1.0 / self.world, self.rule, self.keep_w3_grad)
+                                self.params[w3], self.m[w3], self.v[w3], self.w3_shadow().reshape(-1), self.state,
+                                self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, self.keep_w3_grad, lo, hi)
 
     def _conv_forward(self, x, rows, st):
         o = self.ops
@@ -574,10 +609,10 @@ class FusedMNISTTrainer:
                     self.a1, self.idx1)
         o.conv2_fwd(self.a1, w2, b2, self.a2, self.idx2)
 
-    def _conv_backward(self, x, rows, st):
+    def _conv_backward(self, x, rows, st, coll=-1):
         o = self.ops
         o.conv2_bwd(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows, st,
-                    self.idx1, self.slab, self.cpart)
+                    self.idx1, self.slab, self.cpart, None, coll)
         o.conv2_wgrad_reduce(self.slab, self.cpart, self.B, self.gview("conv_layer2/conv2d/kernel"),
                              self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"),
                              self.gview("conv_layer2/conv2d/bias"))
@@ -614,6 +649,9 @@ class FusedMNISTTrainer:
             mine[:(hi - lo) * 64].copy_(w3[lo * 64:hi * 64])
             self._all_gather_rows(tmp, mine)
             w3.copy_(tmp[:3136])
+        # the bf16 rows too (on the xGMI plane the other ranks' rows of the last update arrive
+        # with the next step's conv12_fwd launch): the same rounding of the same fp32 values
+        self._refresh_shadow()
         self._full_state_valid = True
 
     def _allreduce(self, bucket, lo, hi):
@@ -767,47 +805,52 @@ class FusedMNISTTrainer:
                 ctx.check()
 
     def _validate_xgmi(self, rounds: int = 2) -> bool:
-        """Run the plane's four xGMI collectives on random data and compare them with the same
-        collectives over the process group (gathers bitwise, the reduction to fp32 rounding).
-        Clobbers a2 and dz (every step recomputes them); the gradients and the W3 row shadow are restored."""
+        """Run the plane's prepared xGMI collectives (the descriptors the step co-launches, here
+        launched on their own; the small-gradient sum without its Adam update) on random data and
+        compare them with the same collectives over the process group: gathers bitwise, the sum to
+        fp32 rounding. Collective. Clobbers a2 and dz (every step recomputes them); the gradients
+        and the W3 row shadow are restored."""
         import torch.distributed as dist
 
+        if self._roles is None or self._roles["lr"] != self.lr:
+            self._prepare_roles()
+        R = self._roles
         W, B, r = self.world, self.B, self.rank
+        T64 = self._T * 64
         ok = True
         g = torch.Generator(device="cpu").manual_seed(9173 + r)
-        saved_shadow3 = self.shadow3.clone() if self.shard_w3 else None
+        saved_shadow3 = self.shadow3.clone()
         saved_grads = self.grads[:W3_START].clone()  # (the alignment gaps are never rewritten by a step)
-        lo, hi = self._w3_tiles if self.shard_w3 else (0, 49)
-        cols = slice(lo * 64, hi * 64)
         others = [q for q in range(W) if q != r]
-        for _ in range(rounds):
+        for it in range(rounds):
+            shard = it % 2 == 0  # both a2 descriptors: this rank's columns, whole rows
+            lo, hi = self._w3_mine if shard else (0, 49)
+            cols = slice(lo * 64, hi * 64)
             self.a2.copy_(torch.randn(B, 3136, generator=g).to(torch.bfloat16))
             self.dz.copy_(torch.randn(B, 1024, generator=g).to(torch.bfloat16))
             self.grads[:W3_START].copy_(torch.randn(W3_START, generator=g))
+            mine = self.shadow3[r * T64:(r + 1) * T64]
+            mine.copy_(torch.randn(T64, 1024, generator=g).to(torch.bfloat16))
             ref_a2 = self.a2_all.clone()
             ref_dz = self.dz_all.clone()
+            ref_s = self.shadow3.clone()
             self._all_gather_rows(ref_a2, ref_a2[r * B:(r + 1) * B])
             self._all_gather_rows(ref_dz, ref_dz[r * B:(r + 1) * B])
+            self._all_gather_rows(ref_s, ref_s[r * T64:(r + 1) * T64])
             ref_g = self.grads[:W3_START].clone()
             dist.all_reduce(ref_g)
-            self._gather_a2()
-            self.xplane.gather_rows("dz", 1, 1024 * 2, B)
-            self.xplane.reduce("grads", 2, self.gred)
-            if self.shard_w3:
-                T64 = self._T * 64
-                mine = self.shadow3[r * T64:(r + 1) * T64]
-                mine.copy_(torch.randn(T64, 1024, generator=g).to(torch.bfloat16))
-                ref_s = self.shadow3.clone()
-                self._all_gather_rows(ref_s, ref_s[r * T64:(r + 1) * T64])
-                self.xplane.gather_rows("shadow3", 3, 1024 * 2, T64, total_rows=min(W * T64, 3136))
+            torch.cuda.synchronize(self.device)
+            self.xplane.run(R["w3"])
+            self.xplane.run(R["a2_shard"] if shard else R["a2_full"])
+            self.xplane.run(R["dz"])
+            self.xplane.reduce("grads", self.PH_SMALL, self.gred)
             torch.cuda.synchronize(self.device)
             for q in others:
-                rows = slice(q * B, (q + 1) * B)
-                ok &= torch.equal(self.a2_all[rows, cols], ref_a2[rows, cols])
-                ok &= torch.equal(self.dz_all[rows], ref_dz[rows])
-                if self.shard_w3:
-                    srows = slice(q * T64, min((q + 1) * T64, 3136))
-                    ok &= torch.equal(self.shadow3[srows], ref_s[srows])
+                rws = slice(q * B, (q + 1) * B)
+                ok &= torch.equal(self.a2_all[rws, cols], ref_a2[rws, cols])
+                ok &= torch.equal(self.dz_all[rws], ref_dz[rws])
+                srows = slice(q * T64, min((q + 1) * T64, 3136))
+                ok &= torch.equal(self.shadow3[srows], ref_s[srows])
             ok &= bool(torch.allclose(self.gred, ref_g, rtol=1e-5, atol=1e-5))
         try:
             self.xplane.check()
@@ -816,44 +859,80 @@ class FusedMNISTTrainer:
         from ..parallel.xgmi import _group_ok
 
         ok = _group_ok(ok, None, self.device)
-        if saved_shadow3 is not None:
-            self.shadow3.copy_(saved_shadow3)
+        # every peer finished reading this rank's buffers before they are restored
+        dist.barrier()
+        self.shadow3.copy_(saved_shadow3)
         self.grads[:W3_START].copy_(saved_grads)
         return ok
 
-    def select_data_plane(self, steps: int = 40, steps_per_replay: int = 20) -> dict:
-        """Pick the data plane of the factor gather (MIHVD_XGMI=auto): validate the direct xGMI
-        collectives against the process group's, then time ``steps`` training steps on each plane
-        (graph-replayed when capturable) and keep the faster one. Collective; the decision is the
-        same on every rank (max time over ranks). Runs real training steps. Returns a report."""
+    def _set_plane(self, xgmi: bool, shard: bool):
+        """Switch data plane and sharding between steps (collective). Leaving the sharded xGMI
+        plane, whose row gather of the last update would run in the next conv12_fwd launch,
+        gathers the rows now."""
+        self._join()
+        if self.use_xgmi and self.shard_w3 and not (xgmi and shard):
+            torch.cuda.synchronize(self.device)
+            T64 = self._T * 64
+            self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
+            torch.cuda.synchronize(self.device)
+        self.use_xgmi = bool(xgmi) and self.xplane is not None
+        self.set_sharding(shard)
+        self._graphs = {}
+        self.graph = None
+
+    def set_sharding(self, shard: bool):
+        """Switch the dense/kernel optimizer between sharded and replicated (factor-gather plane;
+        collective). Sharded -> replicated first collects every rank's fp32 rows and Adam slots."""
+        shard = bool(shard) and self.gather and not self.fuse_w3_requested()
+        if shard == self.shard_w3:
+            return
+        self._join()
+        if not shard:
+            self.gather_full_state()
+            self._refresh_shadow()
+        self.shard_w3 = shard
+        self._graphs = {}
+        self.graph = None
+
+    def select_data_plane(self, steps: int = 40, steps_per_replay: int = 20, shard_options=None) -> dict:
+        """Pick the data plane of the factor gather (MIHVD_XGMI=auto) and whether the dense/kernel
+        optimizer is sharded: validate the direct xGMI collectives against the process group's,
+        then time ``steps`` training steps of each candidate (graph-replayed when capturable) and
+        keep the fastest. Collective; the decision is the same on every rank (max time over
+        ranks). Runs real training steps. ``shard_options``: the sharding settings to try (default:
+        MIHVD_SHARD_W3 if set, else both). Returns a report."""
         import time
 
         import torch.distributed as dist
 
         rep = {"mode": self._xgmi_mode, "available": self.xplane is not None}
-        if self.xplane is None or self._xgmi_mode == "off":
-            self.use_xgmi = False
+        if not self.gather:
             rep["plane"] = "rccl" if self.collectives else "none"
             return rep
-        valid = self._validate_xgmi()
-        rep["valid"] = valid
-        if not valid:
-            from ..parallel.xgmi import warn_fallback
+        if shard_options is None:
+            env = os.environ.get("MIHVD_SHARD_W3")
+            # (one rank owns every tile either way: replicated, which has no row gather)
+            shard_options = [env != "0"] if env is not None else ([True, False] if self.world > 1 else [False])
+        shard_options = [bool(x) and not self.fuse_w3_requested() for x in shard_options]
+        planes = ["rccl"]
+        if self.xplane is not None and self._xgmi_mode != "off":
+            valid = self._validate_xgmi()
+            rep["valid"] = valid
+            if valid:
+                planes = ["xgmi"] if self._xgmi_mode == "on" else ["xgmi", "rccl"]
+            else:
+                from ..parallel.xgmi import warn_fallback
 
-            warn_fallback("validation against the process group's collectives failed")
-            self.use_xgmi = False
-            rep["plane"] = "rccl"
-            return rep
-        if self._xgmi_mode == "on" or self._host_collectives():
-            self.use_xgmi = True
-            rep["plane"] = "xgmi"
+                warn_fallback("validation against the process group's collectives failed")
+        cands = [(p, sh) for p in planes for sh in dict.fromkeys(shard_options)]
+        if len(cands) == 1 or self._host_collectives():
+            self._set_plane(cands[0][0] == "xgmi", cands[0][1])
+            rep["plane"], rep["shard"] = cands[0]
             return rep
         times = {}
         k = max(1, min(steps_per_replay, steps))
-        for plane in (True, False):
-            self.use_xgmi = plane
-            self._graphs = {}
-            self.graph = None
+        for plane, sh in cands:
+            self._set_plane(plane == "xgmi", sh)
             captured = self.build_graph(steps_per_replay=k, warmup=1)
             torch.cuda.synchronize(self.device)
             dist.barrier()
@@ -863,19 +942,19 @@ class FusedMNISTTrainer:
             torch.cuda.synchronize(self.device)
             el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.device)
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
-            times["xgmi" if plane else "rccl"] = float(el.item()) / (max(1, steps // k) * k) * 1e6
+            times[(plane, sh)] = float(el.item()) / (max(1, steps // k) * k) * 1e6
             rep["captured"] = captured
         self.check_xgmi()
-        self.use_xgmi = times["xgmi"] <= times["rccl"]
-        self._graphs = {}
-        self.graph = None
-        rep["us_per_step"] = {p: round(t, 2) for p, t in times.items()}
-        rep["plane"] = "xgmi" if self.use_xgmi else "rccl"
+        plane, sh = min(times, key=times.get)
+        self._set_plane(plane == "xgmi", sh)
+        rep["us_per_step"] = {f"{p}{'-shard' if s else '-replicated'}": round(t, 2) for (p, s), t in times.items()}
+        rep["plane"], rep["shard"] = plane, sh
         return rep
 
     def reduced_grads(self) -> torch.Tensor:
         """The flat gradient buffer after the step's reduction (sums over ranks; the xGMI plane
-        reduces the small gradients into a separate buffer instead of in place)."""
+        reduces the small gradients into a separate buffer instead of in place, and dW3 reaches
+        the gradient buffer only with keep_w3_grad)."""
         if self.use_xgmi and self.gather:
             return torch.cat([self.gred, self.grads[W3_START:]])
         return self.grads

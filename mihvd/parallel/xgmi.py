@@ -146,6 +146,33 @@ class XGMIRegion:
         """``out = scale * sum over ranks`` of buffer ``name`` (fp32) starting at ``offset_elems``."""
         self._o.xgmi_reduce_(self.ctx, phase, self.offsets[name] + 4 * int(offset_elems), out, scale)
 
+    # ------------------------------------------------------------------ prepared collectives
+    # A prepared collective is a descriptor id (csrc/kernels/xgmi_role.h CollRole) that either runs
+    # on its own (run) or is handed to a compute op's `coll` argument, whose launch then runs it on
+    # its first nblk blocks (co-launch: no extra launch, no stream fork in the step's HIP graph).
+    # Descriptors hold raw pointers: the tensors they name must outlive them.
+    def prepare_gather(self, name: str, phase: int, row_bytes: int, rows_per_rank: int, total_rows: int | None = None,
+                       col_lo: int = 0, col_hi: int | None = None, nblk: int = 0) -> int:
+        total = self.world * rows_per_rank if total_rows is None else int(total_rows)
+        col_hi = row_bytes if col_hi is None else int(col_hi)
+        return int(self._o.xgmi_role_gather(self.ctx, phase, self.offsets[name], row_bytes, rows_per_rank, total,
+                                            col_lo, col_hi - col_lo, nblk))
+
+    def prepare_reduce(self, name: str, phase: int, out: torch.Tensor, scale: float = 1.0, adam: dict | None = None,
+                       nblk: int = 0, offset_elems: int = 0) -> int:
+        """``out = scale * sum over ranks`` of buffer ``name``; with ``adam`` (keys p, m, v, shadow,
+        state, lr, b1, b2, eps, grad_scale, rule) also the Adam update of those parameters from the
+        sum, in the same launch, advancing the forward step counter like ``adam_step(bump=1)``."""
+        a = adam or {}
+        return int(self._o.xgmi_role_reduce(self.ctx, phase, self.offsets[name] + 4 * int(offset_elems), out, scale,
+                                            a.get("p"), a.get("m"), a.get("v"), a.get("shadow"), a.get("state"),
+                                            a.get("lr", 0.0), a.get("b1", 0.0), a.get("b2", 0.0), a.get("eps", 0.0),
+                                            a.get("grad_scale", 1.0), a.get("rule", 0), nblk))
+
+    def run(self, role: int):
+        """Launch a prepared collective on its own (current stream)."""
+        self._o.xgmi_run(role)
+
     def check(self):
         """Wait for the current stream and raise if a device-side phase barrier timed out."""
         if self.ctx is None:

@@ -45,7 +45,7 @@ def test_collectives_inside_hip_graph(tmp_path, shard, xgmi):
         assert r["plane"] == "rccl", r
     else:
         assert r["select"]["valid"] and r["plane"] in ("xgmi", "rccl"), r
-        assert set(r["select"]["us_per_step"]) == {"xgmi", "rccl"}, r
+        assert set(r["select"]["us_per_step"]) == {"xgmi-shard", "rccl-shard"}, r
 
 
 @pytest.mark.parametrize("gather", ["1", "0"])
@@ -93,6 +93,21 @@ def test_sharded_optimizer_matches_unsharded_two_ranks(tmp_path, xgmi):
     for r in range(2):
         o = json.loads((tmp_path / f"dp_gloo_shard.{r}.json").read_text())
         assert o["planes"] == (["xgmi", "xgmi"] if xgmi == "on" else ["rccl", "rccl"]), o
+        assert all(o["same"].values()), o
+        assert o["loss"] == o["loss_ref"]
+
+
+def test_plane_and_sharding_switches_two_ranks(tmp_path):
+    """select_data_plane switches the data plane and the optimizer sharding between steps; the
+    trainer must stay bitwise equal to one that never switches."""
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="auto")
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo_switch", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(2):
+        o = json.loads((tmp_path / f"dp_gloo_switch.{r}.json").read_text())
+        assert o["planes"] == ["xgmi-shard", "rccl-replicated", "xgmi-replicated", "xgmi-shard", "rccl-shard"], o
         assert all(o["same"].values()), o
         assert o["loss"] == o["loss_ref"]
 

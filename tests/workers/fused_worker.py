@@ -121,6 +121,39 @@ def sc_dp_gloo_shard(outdir):
         json.dump(rec, f)
 
 
+def sc_dp_gloo_switch(outdir):
+    """Plane / sharding switches between steps (xGMI sharded -> RCCL replicated -> xGMI replicated
+    -> xGMI sharded -> RCCL sharded) == a trainer that stays on the process group, unsharded, bit for
+    bit (2 ranks: the two-term sums commute exactly)."""
+    r = hvd.rank()
+    X, Y = data(1200)
+    a = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", shard_optimizer=True)
+    ref = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", shard_optimizer=False)
+    for tr in (a, ref):
+        tr.broadcast(0)
+    ref._set_plane(False, False)
+    plan = [(True, True), (False, False), (True, False), (True, True), (False, True)]
+    step, planes = 0, []
+    for xg, sh in plan:
+        a._set_plane(xg, sh)
+        planes.append(a.data_plane() + ("-shard" if a.shard_w3 else "-replicated"))
+        for _ in range(2):
+            xb = X[step * 100:(step + 1) * 100]
+            yb = Y[step * 100:(step + 1) * 100]
+            for tr in (a, ref):
+                tr.train_step(xb[r * 50:(r + 1) * 50], yb[r * 50:(r + 1) * 50])
+            step += 1
+    torch.cuda.synchronize()
+    a.gather_full_state()
+    same = {name: bool(torch.equal(getattr(a, name), getattr(ref, name))) for name in ("params", "m", "v")}
+    same["shadow_w3"] = bool(torch.equal(a.w3_shadow(), ref.w3_shadow()))
+    rec = {"same": same, "planes": planes, "loss": a.last_loss(), "loss_ref": ref.last_loss()}
+    for tr in (a, ref):
+        tr.close()
+    with open(os.path.join(outdir, f"dp_gloo_switch.{r}.json"), "w") as f:
+        json.dump(rec, f)
+
+
 def main():
     scenario, outdir = sys.argv[1], sys.argv[2]
     hvd.init()
