@@ -19,6 +19,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include "common.h"
+#include "w3_tail.h"
 #include "xgmi_role.h"
 
 namespace mihvd {
@@ -473,16 +474,18 @@ __device__ __forceinline__ void conv2_bwd_block(
   }
 }
 
-// TAIL: the launch also carries the dense/kernel Adam update (AdamTail, common.h). Blocks
-// [n_conv, grid) have no conv work and start on it at once (they sit on the CUs the conv roles
-// leave idle); every conv block joins in when its own work is done.
-template <bool TAIL>
+// TAIL: the launch also carries the dense/kernel Adam update — 1: from the dW3 gradient in HBM
+// (AdamTail, common.h), 2: from dW3 tiles computed here from the bf16 factors (W3TileTail,
+// w3_tail.h). Blocks [n_conv, grid) have no conv work and start on it at once (they sit on the CUs
+// the conv roles leave idle); every conv block joins in when its own work is done.
+enum { TAIL_NONE = 0, TAIL_ADAM = 1, TAIL_W3 = 2 };
+template <int TAIL>
 __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
     float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int n_conv, AdamTail at,
-    CollRole cr) {
+    W3TileTail wt, CollRole cr) {
   // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk blocks (the CUs the 225 conv
   // blocks of a B = 100 step leave idle)
   if ((int)blockIdx.x < cr.nblk) {
@@ -492,7 +495,8 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
   const int bx = (int)blockIdx.x - cr.nblk;
   if (bx < n_conv)
     conv2_bwd_block(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit, bx);
-  if constexpr (TAIL) adam_tail_run(at);
+  if constexpr (TAIL == TAIL_ADAM) adam_tail_run(at);
+  if constexpr (TAIL == TAIL_W3) w3_tail_run(wt);  // independent waves, no LDS
 }
 
 // Blocks [0, 200): dW2 = sum of the (<= 32) conv2 wgrad slabs; 64 float4 outputs x 4 slab groups of
@@ -628,7 +632,7 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
                              const at::Tensor& x, const c10::optional<at::Tensor>& rows,
                              const c10::optional<at::Tensor>& state, const at::Tensor& idx1, at::Tensor& slab,
                              at::Tensor& cpart, const c10::optional<at::Tensor>& g1, const AdamTail* tail,
-                             int64_t coll) {
+                             int64_t coll, const W3TileTail* w3t = nullptr) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
@@ -650,8 +654,9 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
   else TORCH_CHECK(n_pool >= B, "conv2_bwd: x has fewer rows than the batch");
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   static bool attr = [] {
-    hipFuncSetAttribute((const void*)conv2_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
-    hipFuncSetAttribute((const void*)conv2_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
+    hipFuncSetAttribute((const void*)conv2_bwd_kernel<TAIL_NONE>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
+    hipFuncSetAttribute((const void*)conv2_bwd_kernel<TAIL_ADAM>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
+    hipFuncSetAttribute((const void*)conv2_bwd_kernel<TAIL_W3>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
     return true;
   }();
   (void)attr;
@@ -660,11 +665,31 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
   const int n_dgrad = role == 1 ? 0 : B;
   const int n_conv = role == 2 ? 0 : role == 0 ? B : role == 1 ? 5 * G : B + 5 * G;
   const CollRole cr = xgmi_role_lookup(coll);
-  if (tail == nullptr) {
-    conv2_bwd_kernel<false><<<cr.nblk + n_conv, 512, CB_LDS, stream>>>(
+  if (w3t != nullptr) {
+    // one 512-thread block per CU (144 KB of LDS): the tail-only blocks take the CUs the conv roles
+    // leave free and start on the dW3 tiles at once (MIHVD_W3T_HEAD: their share, tuned on MI355X)
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = std::max(n_conv + 8, ncu);
+    static const double head_frac = [] {
+      const char* e = getenv("MIHVD_W3T_HEAD");
+      return e ? atof(e) : 0.25;
+    }();
+    W3TileTail wtl = *w3t;
+    wtl.first_free = n_conv;
+    wtl.head = (int)(head_frac * W3T_TILES);
+    if (role == 2) wtl.first_free = 0;  // kbench: the tail alone
+    TORCH_CHECK(cr.nblk == 0, "conv2_bwd_w3adam: no co-launched collective with the optimizer tail");
+    conv2_bwd_kernel<TAIL_W3><<<grid, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, cr);
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, wtl, cr);
+  } else if (tail == nullptr) {
+    conv2_bwd_kernel<TAIL_NONE><<<cr.nblk + n_conv, 512, CB_LDS, stream>>>(
+        (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
+        x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, W3TileTail{}, cr);
   } else {
     // one 512-thread block per CU (144 KB of LDS): the extra tail-only blocks take the CUs the
     // conv roles leave free, so the update streams from the first cycle
@@ -687,10 +712,10 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     at.kpl = kpl;
     at.head = (int64_t)(head_frac * (double)((at.n4 + 64 * kpl - 1) / (64 * kpl)));
     TORCH_CHECK(cr.nblk == 0, "conv2_bwd_adam: no co-launched collective with the optimizer tail");
-    conv2_bwd_kernel<true><<<grid, 512, CB_LDS, stream>>>(
+    conv2_bwd_kernel<TAIL_ADAM><<<grid, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at, cr);
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at, W3TileTail{}, cr);
   }
 }
 
@@ -724,6 +749,39 @@ void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tens
               (u16*)shadow3.data_ptr(), n / 4, state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2,
               (float)eps, (float)grad_scale, (int)rule, 0, 0, 4};
   conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, &at, -1);
+}
+
+// conv2_bwd + the dense/kernel Adam update from dW3 = a2^T dz tiles computed in the launch's tail
+// (W3TileTail, w3_tail.h): dzT [1024][128] and a2T [3136][128] bf16 are this step's fc1 factors,
+// transposed by fc1_bwd's dgrad blocks (zero past the batch); p3/m3/v3/shadow3 the dense/kernel
+// segments of the flat buffers; gW3 (optional) also receives dW3.
+void conv2_bwd_w3adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+                      const at::Tensor& x, const c10::optional<at::Tensor>& rows, at::Tensor& state,
+                      const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const at::Tensor& dzT,
+                      const at::Tensor& a2T, at::Tensor& p3, at::Tensor& m3, at::Tensor& v3, at::Tensor& shadow3,
+                      const c10::optional<at::Tensor>& gW3, double lr, double b1, double b2, double eps,
+                      double grad_scale, int64_t rule) {
+  const int B = a1.size(0);
+  const int64_t n = (int64_t)W3T_K * W3T_N;
+  TORCH_CHECK(B >= 1 && B <= W3T_KP, "conv2_bwd_w3adam: batch must be in [1, 128]");
+  check_flat(dzT, at::kBFloat16, (int64_t)W3T_N * W3T_KP, "conv2_bwd_w3adam: dzT [1024][128] bf16");
+  check_flat(a2T, at::kBFloat16, (int64_t)W3T_K * W3T_KP, "conv2_bwd_w3adam: a2T [3136][128] bf16");
+  check_flat(p3, at::kFloat, n, "conv2_bwd_w3adam: p3");
+  check_flat(m3, at::kFloat, n, "conv2_bwd_w3adam: m3");
+  check_flat(v3, at::kFloat, n, "conv2_bwd_w3adam: v3");
+  check_flat(shadow3, at::kBFloat16, n, "conv2_bwd_w3adam: shadow3");
+  float* gp = nullptr;
+  if (gW3.has_value() && gW3->defined()) {
+    check_flat(*gW3, at::kFloat, n, "conv2_bwd_w3adam: gW3");
+    gp = gW3->data_ptr<float>();
+  }
+  TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_WORDS, "conv2_bwd_w3adam: state");
+  W3TileTail wt{(const u16*)dzT.data_ptr(), (const u16*)a2T.data_ptr(),
+                AdamArgs{p3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(), (u16*)shadow3.data_ptr(),
+                         state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale,
+                         (int)rule},
+                gp, 0, 0};
+  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, nullptr, -1, &wt);
 }
 
 void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2, at::Tensor& gW1,

@@ -198,9 +198,15 @@ constexpr int DG_ROWS = 32, DG_JT = FC1_K / 64;         // 49 feature tiles
 constexpr int DG_DSTR = FC1_N + 8;                      // dz image row stride (2064 B)
 constexpr int DG_LDS = DG_ROWS * DG_DSTR * 2;           // 66,048 B
 
+// FT_KP: row length of the transposed factor copies a2T [3136][128] / dzT [1024][128] that the
+// dgrad blocks can leave for conv2_bwd's dW3 tail (w3_tail.h): K-contiguous rows make every MFMA
+// fragment there one 16-byte load. Columns past the batch are never written (zero-initialised).
+constexpr int FT_KP = MAXB;
+
 __device__ __forceinline__ void fc1_dgrad_block(int bx, const u16* __restrict__ dz, const u16* __restrict__ w3,
                                                 const u16* __restrict__ a2, u16* __restrict__ g2, int B, int G,
-                                                u16* smem) {
+                                                u16* smem, u16* __restrict__ a2T = nullptr,
+                                                u16* __restrict__ dzT = nullptr) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int xcd = bx & 7, slot = bx >> 3;
   const int mg = slot % G, jt = (slot / G) * 8 + xcd;
@@ -259,6 +265,32 @@ __device__ __forceinline__ void fc1_dgrad_block(int bx, const u16* __restrict__ 
       for (int i = 0; i < 4; ++i) o[i] = bf2f(av[i]) > 0.f ? acc[mt][i] : 0.f;
       *reinterpret_cast<uint2*>(g2 + (int64_t)m * FC1_K + j0 + wave * 16 + 4 * lg) = pack4bf(o[0], o[1], o[2], o[3]);
     }
+  }
+  if (a2T != nullptr) {
+    // a2T[j][m] for this block's 64 features x 32 samples (zero past B: mk is masked): lanes lr
+    // hold 16 consecutive samples, so each store instruction writes 32 contiguous bytes per row.
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int m = m0 + mt * 16 + lr;
+      const uint2 x = mk[mt];
+      const u16 av[4] = {(u16)(x.x & 0xffff), (u16)(x.x >> 16), (u16)(x.y & 0xffff), (u16)(x.y >> 16)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a2T[(int64_t)(j0 + wave * 16 + 4 * lg + i) * FT_KP + m] = av[i];
+    }
+  }
+  if (dzT != nullptr && jt < FC1_N / 64) {
+    // dzT[n][m] for n in [64 jt, 64 jt + 64), this block's 32 samples, read from the dz image
+    // (rows past B are zero-filled): 8 consecutive samples -> one 16-byte store per thread.
+    const int n = jt * 64 + (t & 63), mq = t >> 6;
+    u16 e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = Ds[(8 * mq + k) * DG_DSTR + n];
+    uint4 v;
+    v.x = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
+    v.y = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
+    v.z = (uint32_t)e[4] | ((uint32_t)e[5] << 16);
+    v.w = (uint32_t)e[6] | ((uint32_t)e[7] << 16);
+    *reinterpret_cast<uint4*>(dzT + (int64_t)n * FT_KP + m0 + 8 * mq) = v;
   }
 }
 
@@ -465,8 +497,8 @@ __device__ __forceinline__ void fc1_wgrad_block(
   }
 }
 
-template <bool ADAM>
-__global__ void __launch_bounds__(256) fc1_wgrad_kernel(
+template <bool ADAM, int MINW = 1>
+__global__ void __launch_bounds__(256, MINW) fc1_wgrad_kernel(
     const u16* __restrict__ dz, const u16* __restrict__ a2, const u16* __restrict__ h, const float* __restrict__ dlog,
     const u16* __restrict__ dzw, const u16* __restrict__ a2w, int Kw, float* __restrict__ gW3, float* __restrict__ gb3,
     float* __restrict__ gW4, float* __restrict__ gb4, int B, int tile_base, int n_small, AdamArgs ad, int write_grad,
@@ -487,7 +519,8 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(const u16* __restrict__ dz
                                                       const u16* __restrict__ w3, u16* __restrict__ g2,
                                                       float* __restrict__ gW3, float* __restrict__ gb3,
                                                       float* __restrict__ gW4, float* __restrict__ gb4, int B, int G,
-                                                      int n_dg, int n_small, CollRole cr) {
+                                                      int n_dg, int n_small, CollRole cr, u16* __restrict__ a2T,
+                                                      u16* __restrict__ dzT) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   // co-launched xGMI collective on the first cr.nblk blocks (a multiple of 8, so the dgrad tiles
   // keep their blockIdx -> XCD map)
@@ -497,7 +530,7 @@ __global__ void __launch_bounds__(256) fc1_bwd_kernel(const u16* __restrict__ dz
   }
   const int bx = (int)blockIdx.x - cr.nblk;
   if (bx < n_dg) {
-    fc1_dgrad_block(bx, dz, w3, a2, g2, B, G, smem);
+    fc1_dgrad_block(bx, dz, w3, a2, g2, B, G, smem, a2T, dzT);
     return;
   }
   fc1_wgrad_block<false>(bx - n_dg, dz, a2, h, dlog, dz, a2, B, gW3, gb3, gW4, gb4, B, 0, n_small, AdamArgs{}, 1,
@@ -626,7 +659,16 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   if (grid == 0) return;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const u16 *pdz = (const u16*)dz.data_ptr(), *pa2 = (const u16*)a2.data_ptr(), *ph = (const u16*)h.data_ptr();
-  if (ad != nullptr) {
+  // MIHVD_WGRAD_ADAM_OCC=4: registers capped for 4 blocks per CU (784 tiles resident at once)
+  static const int occ = [] {
+    const char* e = getenv("MIHVD_WGRAD_ADAM_OCC");
+    return e ? atoi(e) : 0;
+  }();
+  if (ad != nullptr && occ == 4) {
+    fc1_wgrad_kernel<true, 4><<<grid, 256, FB_LDS_WG, stream>>>(
+        pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
+        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0, a2s, a2c0, cr);
+  } else if (ad != nullptr) {
     fc1_wgrad_kernel<true><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
         gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0, a2s, a2c0, cr);
@@ -685,7 +727,8 @@ void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a
 // roles as fc1_wgrad: bit 0 = the dW3 tiles, bit 1 = db3 / dW4 / db4.
 void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
              const at::Tensor& w3bf, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& g2,
-             int64_t roles, int64_t coll) {
+             int64_t roles, int64_t coll, const c10::optional<at::Tensor>& a2T,
+             const c10::optional<at::Tensor>& dzT) {
   TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_bwd: roles must be 1, 2 or 3");
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_bwd: batch");
@@ -702,12 +745,22 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
   CollRole cr = xgmi_role_lookup(coll);
   TORCH_CHECK(cr.nblk % 8 == 0, "fc1_bwd: a co-launched collective needs a multiple of 8 blocks (XCD map)");
   const int grid = cr.nblk + n_dg + n_small + ((roles & 1) ? FB_WGRAD : 0);
+  u16 *pa2T = nullptr, *pdzT = nullptr;
+  if (a2T.has_value() && a2T->defined()) {
+    TORCH_CHECK(dzT.has_value() && dzT->defined(), "fc1_bwd: a2T and dzT go together");
+    TORCH_CHECK(a2T->dtype() == at::kBFloat16 && a2T->numel() == (int64_t)FC1_K * FT_KP && a2T->is_contiguous(),
+                "fc1_bwd: a2T must be bf16 [3136][128]");
+    TORCH_CHECK(dzT->dtype() == at::kBFloat16 && dzT->numel() == (int64_t)FC1_N * FT_KP && dzT->is_contiguous(),
+                "fc1_bwd: dzT must be bf16 [1024][128]");
+    pa2T = (u16*)a2T->data_ptr();
+    pdzT = (u16*)dzT->data_ptr();
+  }
   auto stream = c10::hip::getCurrentHIPStream().stream();
   set_max_lds(fc1_bwd_kernel, DG_LDS);
   fc1_bwd_kernel<<<grid, 256, DG_LDS, stream>>>(
       (const u16*)dz.data_ptr(), (const u16*)a2.data_ptr(), (const u16*)h.data_ptr(), dlog.data_ptr<float>(),
       (const u16*)w3bf.data_ptr(), (u16*)g2.data_ptr(), gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg, n_small, cr);
+      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg, n_small, cr, pa2T, pdzT);
 }
 
 }  // namespace mihvd

@@ -14,7 +14,8 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
 void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart);
 void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
              const at::Tensor& w3bf, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& g2,
-             int64_t roles, int64_t coll);
+             int64_t roles, int64_t coll, const c10::optional<at::Tensor>& a2T,
+             const c10::optional<at::Tensor>& dzT);
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
@@ -41,6 +42,12 @@ void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tens
                     at::Tensor& slab, at::Tensor& cpart, at::Tensor& p3, const at::Tensor& g3, at::Tensor& m3,
                     at::Tensor& v3, at::Tensor& shadow3, double lr, double b1, double b2, double eps, double grad_scale,
                     int64_t rule);
+void conv2_bwd_w3adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+                      const at::Tensor& x, const c10::optional<at::Tensor>& rows, at::Tensor& state,
+                      const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const at::Tensor& dzT,
+                      const at::Tensor& a2T, at::Tensor& p3, at::Tensor& m3, at::Tensor& v3, at::Tensor& shadow3,
+                      const c10::optional<at::Tensor>& gW3, double lr, double b1, double b2, double eps,
+                      double grad_scale, int64_t rule);
 void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2,
                              at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads, at::Tensor& p,
                              at::Tensor& m, at::Tensor& v, at::Tensor& shadow, at::Tensor& state, int64_t fc_lo,
@@ -89,8 +96,9 @@ void conv12_fwd_op(const Tensor& x, const c10::optional<Tensor>& rows, const c10
   mihvd::conv12_fwd(x, rows, state, w1, b1, w2, b2, a1, idx1, a2, idx2, coll);
 }
 void fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, const Tensor& w3, Tensor gW3,
-               Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles, int64_t coll) {
-  mihvd::fc1_bwd(dz, a2, h, dlog, w3, gW3, gb3, gW4, gb4, g2, roles, coll);
+               Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles, int64_t coll, const OptT& a2T,
+               const OptT& dzT) {
+  mihvd::fc1_bwd(dz, a2, h, dlog, w3, gW3, gb3, gW4, gb4, g2, roles, coll, a2T, dzT);
 }
 void fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::fc1_fwd(a2, w3, zpart); }
 void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
@@ -126,6 +134,13 @@ void conv2_bwd_adam_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, c
                        double eps, double grad_scale, int64_t rule) {
   mihvd::conv2_bwd_adam(g2, idx2, a1, w2, x, rows, state, idx1, slab, cpart, p3, g3, m3, v3, shadow3, lr, b1, b2, eps,
                         grad_scale, rule);
+}
+void conv2_bwd_w3adam_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, const Tensor& x,
+                         const OptT& rows, Tensor state, const Tensor& idx1, Tensor slab, Tensor cpart, const Tensor& dzT,
+                         const Tensor& a2T, Tensor p3, Tensor m3, Tensor v3, Tensor shadow3, const OptT& gW3, double lr,
+                         double b1, double b2, double eps, double grad_scale, int64_t rule) {
+  mihvd::conv2_bwd_w3adam(g2, idx2, a1, w2, x, rows, state, idx1, slab, cpart, dzT, a2T, p3, m3, v3, shadow3, gW3, lr, b1,
+                          b2, eps, grad_scale, rule);
 }
 void conv2_wgrad_reduce_adam_op(const Tensor& slab, const Tensor& cpart, int64_t B, Tensor gW2, Tensor gW1, Tensor gb1,
                                 Tensor gb2, const Tensor& grads, Tensor p, Tensor m, Tensor v, Tensor shadow,
@@ -175,7 +190,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("conv12_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1bf, Tensor b1, Tensor w2bf, Tensor b2, "
         "Tensor(a!) a1, Tensor(b!) idx1, Tensor(c!) a2, Tensor(d!) idx2, int coll=-1) -> ()");
   m.def("fc1_bwd(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor w3bf, Tensor(a!) gW3, Tensor(b!) gb3, "
-        "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3, int coll=-1) -> ()");
+        "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3, int coll=-1, Tensor(f!)? a2T=None, "
+        "Tensor(g!)? dzT=None) -> ()");
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, int coll=-1) -> ()");
@@ -195,6 +211,10 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("conv2_bwd_adam(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, Tensor(s!) state, "
         "Tensor idx1, Tensor(a!) slab, Tensor(b!) cpart, Tensor(c!) p3, Tensor g3, Tensor(d!) m3, Tensor(e!) v3, "
         "Tensor(f!) shadow3, float lr, float b1, float b2, float eps, float grad_scale, int rule) -> ()");
+  m.def("conv2_bwd_w3adam(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, Tensor(s!) state, "
+        "Tensor idx1, Tensor(a!) slab, Tensor(b!) cpart, Tensor dzT, Tensor a2T, Tensor(c!) p3, Tensor(d!) m3, "
+        "Tensor(e!) v3, Tensor(f!) shadow3, Tensor(g!)? gW3, float lr, float b1, float b2, float eps, "
+        "float grad_scale, int rule) -> ()");
   m.def("conv2_wgrad_reduce_adam(Tensor slab, Tensor cpart, int B, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
         "Tensor(d!) gb2, Tensor grads, Tensor(e!) p, Tensor(f!) m, Tensor(g!) v, Tensor(h!) shadow, Tensor(s!) state, "
         "int fc_lo, int w3_lo, float lr, float b1, float b2, float eps, float grad_scale, int rule) -> ()");
@@ -231,6 +251,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("conv2_bwd", &conv2_bwd_op);
   m.impl("conv2_wgrad_reduce", &conv2_wgrad_reduce_op);
   m.impl("conv2_bwd_adam", &conv2_bwd_adam_op);
+  m.impl("conv2_bwd_w3adam", &conv2_bwd_w3adam_op);
   m.impl("conv2_wgrad_reduce_adam", &conv2_wgrad_reduce_adam_op);
   m.impl("adam_step", &adam_op);
   m.impl("gather_cols_bf16", &gather_cols_op);

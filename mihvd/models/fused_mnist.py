@@ -258,6 +258,16 @@ class FusedMNISTTrainer:
         # Measured (B=100): 78.4 us/step vs 80.0 us with the flat adam_step launch.
         self.fused_opt = (os.environ.get("MIHVD_FUSED_OPT", "1") != "0" and not self.collectives
                           and not self.pipeline and not self.fuse_w3)
+        # MIHVD_W3_TAIL=1 (opt-in, with the fused optimizer): conv2_bwd's tail computes dW3 = a2^T dz tile by
+        # tile on MFMA from the bf16 factors and applies Adam to dense/kernel from the accumulators
+        # (csrc/kernels/w3_tail.h), so fc1_bwd only runs the dgrad tiles and the small reductions and
+        # dW3 never goes through HBM (25.7 MB less per step); bitwise equal to the stored-dW3 tail.
+        self.w3_tail = self.fused_opt and os.environ.get("MIHVD_W3_TAIL", "0") == "1"
+        if self.w3_tail:
+            # the fc1 factors transposed (K-contiguous, zero past the batch), left by fc1_bwd's dgrad
+            # blocks for the tail's MFMA fragments
+            self.a2T = torch.zeros(3136, 128, **bf)
+            self.dzT = torch.zeros(1024, 128, **bf)
         self._fc_update_pending = False
         self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline) else None
         if compression == "bf16" and self.collectives:
@@ -378,7 +388,12 @@ class FusedMNISTTrainer:
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         if self.fused_opt:
             b1, b2 = self.betas
-            if self.fc1_merged:  # dgrad tiles and every wgrad role in one launch
+            if self.w3_tail:  # dgrad tiles (+ the transposed factors) and the small reductions; dW3 runs in
+                # conv2_bwd's tail
+                o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.pview("dense/kernel", self.shadow),
+                          self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
+                          self.gview("dense_1/bias"), self.g2, 2, -1, self.a2T, self.dzT)
+            elif self.fc1_merged:  # dgrad tiles and every wgrad role in one launch
                 o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.pview("dense/kernel", self.shadow),
                           self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
                           self.gview("dense_1/bias"), self.g2)
@@ -387,9 +402,16 @@ class FusedMNISTTrainer:
                             self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
                 o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)  # last reader of W3
             w3 = slice(W3_START, FLAT_NUMEL)
-            o.conv2_bwd_adam(self.g2, self.idx2, self.a1, self.pview("conv_layer2/conv2d/kernel", self.shadow), x, rows,
-                             st, self.idx1, self.slab, self.cpart, self.params[w3], self.grads[w3], self.m[w3],
-                             self.v[w3], self.shadow[w3], self.lr, b1, b2, self.eps, 1.0, self.rule)
+            w2 = self.pview("conv_layer2/conv2d/kernel", self.shadow)
+            if self.w3_tail:
+                o.conv2_bwd_w3adam(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
+                                   self.dzT, self.a2T, self.params[w3], self.m[w3], self.v[w3], self.shadow[w3],
+                                   self.grads[w3] if self.keep_w3_grad else None, self.lr, b1, b2, self.eps, 1.0,
+                                   self.rule)
+            else:
+                o.conv2_bwd_adam(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
+                                 self.params[w3], self.grads[w3], self.m[w3], self.v[w3], self.shadow[w3], self.lr, b1,
+                                 b2, self.eps, 1.0, self.rule)
             o.conv2_wgrad_reduce_adam(self.slab, self.cpart, self.B, self.gview("conv_layer2/conv2d/kernel"),
                                       self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"),
                                       self.gview("conv_layer2/conv2d/bias"), self.grads, self.params, self.m, self.v,

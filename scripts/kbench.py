@@ -33,6 +33,10 @@ def main():
     st = tr.state
     sh = tr.shadow
     dz8 = tr.dz.repeat(8, 1).contiguous()
+    a2T = torch.zeros(3136, 128, device="cuda", dtype=torch.bfloat16)
+    dzT = torch.zeros(1024, 128, device="cuda", dtype=torch.bfloat16)
+    a2T[:, :B].copy_(tr.a2.t())
+    dzT[:, :B].copy_(tr.dz.t())
     a28 = tr.a2.repeat(8, 1).contiguous()
     ops = {
         "conv1_fwd": lambda: o.conv1_fwd(tr.x_buf, None, st, tr.pview("conv_layer1/conv2d/kernel"),
@@ -74,6 +78,17 @@ def main():
             tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
             tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
             sh, st, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0)),
+        "fc1_bwd[roles=2]": lambda: o.fc1_bwd(tr.dz, tr.a2, tr.h, tr.dlog, tr.pview("dense/kernel", sh),
+                                              tr.gview("dense/kernel"), tr.gview("dense/bias"),
+                                              tr.gview("dense_1/kernel"), tr.gview("dense_1/bias"), tr.g2, 2, -1,
+                                              a2T, dzT),
+        "conv2_bwd_w3adam+reduce_adam": lambda: (o.conv2_bwd_w3adam(
+            tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf, None, st, tr.idx1, tr.slab,
+            tr.cpart, dzT, a2T, tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], None, 0.0, 0.9, 0.999, 1e-8, 1.0,
+            0), o.conv2_wgrad_reduce_adam(
+            tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
+            tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
+            sh, st, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0)),
         "fc1_wgrad_adam_k8x": lambda: o.fc1_wgrad_adam(
             tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
             tr.gview("dense_1/bias"), 1, dz8, a28, tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], st, 0.0, 0.9,
@@ -93,7 +108,8 @@ def main():
     }
     jobs = [(name, fn, None) for name, fn in ops.items()]
     if args.roles:  # MIHVD_ROLE_ONLY is read by the host wrappers at launch (i.e. capture) time
-        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv2_bwd_adam+reduce_adam", 3)):
+        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv2_bwd_adam+reduce_adam", 3),
+                              ("conv2_bwd_w3adam+reduce_adam", 3)):
             jobs += [(f"{name}[role{r}]", ops[name], r) for r in range(n_roles)]
     if args.phases:  # MIHVD_DEBUG_EXIT: conv2_bwd dgrad role cut after phase p (1 staging, 2 GEMM, 3 epilogue)
         jobs += [(f"conv2_bwd[role0,exit{p}]", ops["conv2_bwd"], (0, p)) for p in (1, 2, 3)]
@@ -152,7 +168,10 @@ def main():
     torch.cuda.synchronize()
     res["step"] = e0.elapsed_time(e1) * 1000.0 / 200
     step_ops = (["conv12_fwd"] if tr.conv12 else ["conv1_fwd", "conv2_fwd"]) + ["fc1_fwd", "head", "fc1_dgrad"]
-    if tr.fused_opt:
+    if tr.fused_opt and getattr(tr, "w3_tail", False):
+        step_ops = [k for k in step_ops if not (tr.fc1_merged and k == "fc1_dgrad")]
+        step_ops += ["fc1_bwd[roles=2]", "conv2_bwd_w3adam+reduce_adam"]
+    elif tr.fused_opt:
         step_ops = [k for k in step_ops if not (tr.fc1_merged and k == "fc1_dgrad")]
         step_ops += ["fc1_bwd" if tr.fc1_merged else "fc1_wgrad", "conv2_bwd_adam+reduce_adam"]
     elif tr.fuse_w3:

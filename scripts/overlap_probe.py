@@ -79,14 +79,53 @@ def main():
     for blocks in (0, 256, 512, 1024):
         jobs[f"fork conv2_bwd | adam_w3[{blocks or 'all'}]"] = forked(blocks)
         jobs[f"fork conv2_bwd+reduce_adam | adam_w3[{blocks or 'all'}]"] = forked(blocks, with_reduce=True)
+
+    def streams(n, blocks, main_fn):
+        # one fork/join around n kernels per stream: the concurrent throughput without the fork cost
+        def fn():
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for _ in range(n):
+                    adam(blocks)
+            for _ in range(n):
+                main_fn()
+            main.wait_stream(side)
+        return fn
+
+    conv12 = lambda: o.conv12_fwd(tr.x_buf, None, st, tr.pview("conv_layer1/conv2d/kernel", sh),  # noqa: E731
+                                  tr.pview("conv_layer1/conv2d/bias"), w2, tr.pview("conv_layer2/conv2d/bias"), tr.a1,
+                                  tr.idx1, tr.a2, tr.idx2)
+    jobs["conv12_fwd"] = conv12
+    jobs["conv2_bwd; reduce_adam; conv12_fwd"] = lambda: (conv(), reduce_adam(), conv12())
+    for blocks in (128, 256, 512, 2048):
+        jobs[f"20x[conv2_bwd] | 20x[adam_w3[{blocks}]] /20"] = streams(20, blocks, conv)
+        jobs[f"20x[conv2_bwd;reduce;conv12] | 20x[adam_w3[{blocks}]] /20"] = streams(
+            20, blocks, lambda: (conv(), reduce_adam(), conv12()))
+
+    def tiny_streams():
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            for _ in range(20):
+                st[3:4].add_(0)
+        for _ in range(20):
+            st[2:3].add_(0)
+        main.wait_stream(side)
+    jobs["20x[tiny] | 20x[tiny] /20"] = tiny_streams
+    div = {k: (20 if k.startswith("20x") else 1) for k in jobs}
     s = torch.cuda.Stream()
+    only = os.environ.get("PROBE_ONLY")
     for name, fn in jobs.items():
+        if only and only not in name:
+            continue
+        iters = max(1, args.iters // div[name])
         for _ in range(2):
             fn()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
-            for _ in range(args.iters):
+            for _ in range(iters):
                 fn()
         g.replay()
         torch.cuda.synchronize()
@@ -96,7 +135,8 @@ def main():
             g.replay()
         e1.record()
         torch.cuda.synchronize()
-        print(f"{name:48s} {e0.elapsed_time(e1) * 1000.0 / (3 * args.iters):8.2f} us", flush=True)
+        us = e0.elapsed_time(e1) * 1000.0 / (3 * iters * div[name])
+        print(f"{name:56s} {us:8.2f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -542,6 +542,37 @@ def test_fused_optimizer_tail_matches_separate_adam(ops, monkeypatch):
         assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
 
 
+@pytest.mark.parametrize("B", [1, 37, 100, 128])
+def test_w3_tile_tail_matches_stored_dw3_tail(ops, monkeypatch, B):
+    """MIHVD_W3_TAIL=1: conv2_bwd's tail multiplies the bf16 fc1 factors into
+    dW3 tiles and applies Adam to dense/kernel from the accumulators, fc1_bwd skips its dW3 tiles.
+    Against fc1_bwd storing dW3 and the plain Adam tail: same MFMA tile code, same adam4(), so
+    parameters, slots, shadow, the stored dW3 (keep_w3_grad) and the loss agree bit for bit, for
+    batch sizes that leave partial K chunks."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    g = torch.Generator(device="cuda").manual_seed(41)
+    X = torch.rand(7 * B, 784, device="cuda", generator=g)
+    Y = torch.randint(0, 10, (7 * B,), device="cuda", generator=g)
+    out = []
+    for tail in ("0", "1"):
+        monkeypatch.setenv("MIHVD_W3_TAIL", tail)
+        tr = FusedMNISTTrainer(batch_size=B, seed=6, device="cuda")
+        assert tr.fused_opt and tr.w3_tail == (tail == "1")
+        tr.keep_w3_grad = True
+        tr.set_device_dataset(X, Y, shuffle=False)
+        tr.build_graph(steps_per_replay=4, warmup=2)
+        tr.run_graph()
+        torch.cuda.synchronize()
+        out.append((tr.params.clone(), tr.m.clone(), tr.v.clone(), tr.shadow.clone(), tr.grads.clone(),
+                    tr.last_loss(), [int(v) for v in tr.state.tolist()][:2]))
+    a, b = out
+    assert a[6] == b[6] == [6, 6]
+    assert a[5] == b[5]
+    for x0, x1, name in zip(a[:5], b[:5], ("params", "m", "v", "shadow", "grads")):
+        assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
+
+
 @pytest.mark.parametrize("B", [8, 100])
 def test_conv2_bwd_adam_tail_covers_slice(ops, B):
     """The tail covers every float4 of the slice exactly once (any B, any grid), including a slice
