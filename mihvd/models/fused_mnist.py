@@ -819,8 +819,9 @@ class FusedMNISTTrainer:
     # ----------------------------------------------------------------------------- xGMI plane
     def check_xgmi(self):
         """Raise if a direct-xGMI collective of this trainer timed out waiting for a peer (its
-        outputs, and those of every later xGMI collective, are NaN). Waits for the current stream."""
-        if self.xplane is not None:
+        outputs, and those of every later xGMI collective, are NaN). Waits for the current stream.
+        A plane that select_data_plane() dropped after such a timeout is not checked again."""
+        if self.xplane is not None and not getattr(self, "_xplane_failed", False):
             self.xplane.check()
         for ctx in (self.xgmi or {}).values():
             if ctx is not None:
@@ -897,7 +898,7 @@ class FusedMNISTTrainer:
             T64 = self._T * 64
             self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
             torch.cuda.synchronize(self.device)
-        self.use_xgmi = bool(xgmi) and self.xplane is not None
+        self.use_xgmi = bool(xgmi) and self.xplane is not None and not getattr(self, "_xplane_failed", False)
         self.set_sharding(shard)
         self._graphs = {}
         self.graph = None
@@ -953,6 +954,9 @@ class FusedMNISTTrainer:
             return rep
         times = {}
         k = max(1, min(steps_per_replay, steps))
+        # the timed candidates run real training steps: the model, optimizer and step state are
+        # restored afterwards, so selection leaves no trace (nor NaN from a poisoned collective)
+        snap = self._snapshot()
         for plane, sh in cands:
             self._set_plane(plane == "xgmi", sh)
             captured = self.build_graph(steps_per_replay=k, warmup=1)
@@ -966,12 +970,42 @@ class FusedMNISTTrainer:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
             times[(plane, sh)] = float(el.item()) / (max(1, steps // k) * k) * 1e6
             rep["captured"] = captured
-        self.check_xgmi()
-        plane, sh = min(times, key=times.get)
+        if any(p == "xgmi" for p, _ in cands):
+            # a device-side phase barrier that timed out (a peer that never arrived) poisoned its
+            # outputs: every rank then drops the plane for good and keeps RCCL
+            from ..parallel.xgmi import _group_ok, warn_fallback
+            err = int(self.ops.xgmi_error(self.xplane.ctx)) if self.xplane is not None else 1
+            if not _group_ok(err == 0, None, self.device):
+                times = {key: t for key, t in times.items() if key[0] != "xgmi"}
+                self._xplane_failed = True
+                rep["timing_error"] = True
+                warn_fallback("a collective timed out while the plane was timed")
+                if not times:  # pragma: no cover - 'on' mode: nothing else was timed
+                    times = {("rccl", cands[0][1]): float("nan")}
+        plane, sh = min(times, key=lambda key: (times[key] != times[key], times[key]))
         self._set_plane(plane == "xgmi", sh)
+        self._restore(snap)
         rep["us_per_step"] = {f"{p}{'-shard' if s else '-replicated'}": round(t, 2) for (p, s), t in times.items()}
         rep["plane"], rep["shard"] = plane, sh
         return rep
+
+    def _snapshot(self) -> dict:
+        """Device copies of everything a training step changes (weights, Adam slots, step state)."""
+        self._join()
+        self.gather_full_state()
+        return {"params": self.params.clone(), "m": self.m.clone(), "v": self.v.clone(), "state": self.state.clone(),
+                "global_step": self.global_step}
+
+    def _restore(self, snap: dict):
+        """Back to a _snapshot() (collective when the dense/kernel optimizer is sharded)."""
+        self._join()
+        torch.cuda.synchronize(self.device)
+        for name in ("params", "m", "v", "state"):
+            getattr(self, name).copy_(snap[name])
+        self.global_step = snap["global_step"]
+        self._full_state_valid = True
+        self._refresh_shadow()  # (and the full W3 row shadow of the factor-gather plane)
+        torch.cuda.synchronize(self.device)
 
     def reduced_grads(self) -> torch.Tensor:
         """The flat gradient buffer after the step's reduction (sums over ranks; the xGMI plane
