@@ -18,6 +18,7 @@ _ALIASES = {
     "STALL_CHECK_DISABLE": "HOROVOD_STALL_CHECK_DISABLE",
     "HIERARCHICAL_ALLREDUCE": "HOROVOD_HIERARCHICAL_ALLREDUCE",
     "AUTOTUNE": "HOROVOD_AUTOTUNE",
+    "AUTOTUNE_LOG": "HOROVOD_AUTOTUNE_LOG",
     "LOG_LEVEL": "HOROVOD_LOG_LEVEL",
     "NEGOTIATE": "HOROVOD_NEGOTIATE",
 }
@@ -53,6 +54,7 @@ class Config:
     autotune_candidates: str = "1,4,16,64"  # MiB
     autotune_warmup_steps: int = 3
     autotune_trial_steps: int = 8
+    autotune_log: str = ""                # horovodrun --autotune-log-file: CSV of the candidates
     roctx: bool = False                   # roctx ranges around collectives / steps (rocprofv3 --marker-trace)
     negotiate: bool = False               # route async collectives through the native negotiation engine
     store: str = "native"                 # rendezvous: native (mihvdrun's C++ store, if present) | torch
@@ -82,6 +84,7 @@ class Config:
             autotune_candidates=_get("AUTOTUNE_CANDIDATES", "1,4,16,64", str, env),
             autotune_warmup_steps=_get("AUTOTUNE_WARMUP_STEPS", 3, int, env),
             autotune_trial_steps=_get("AUTOTUNE_TRIAL_STEPS", 8, int, env),
+            autotune_log=_get("AUTOTUNE_LOG", "", str, env),
             roctx=_get("ROCTX", False, bool, env),
             negotiate=_get("NEGOTIATE", False, bool, env),
             store=_get("STORE", "native", str, env),

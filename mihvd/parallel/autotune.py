@@ -19,7 +19,7 @@ from ..utils.logging import log_kv
 
 
 class FusionAutotuner:
-    def __init__(self, candidates_mib, warmup_steps: int = 3, trial_steps: int = 8):
+    def __init__(self, candidates_mib, warmup_steps: int = 3, trial_steps: int = 8, log_file: str | None = None):
         self.candidates = [int(float(c) * 1024 * 1024) for c in candidates_mib]
         if not self.candidates:
             raise ValueError("autotune: no candidates")
@@ -31,10 +31,12 @@ class FusionAutotuner:
         self.done = False
         self.best: int | None = None
         self._t = None
+        self.log_file = log_file or None  # horovodrun --autotune-log-file: one CSV row per candidate
 
     @classmethod
     def from_config(cls, cfg):
-        return cls(cfg.autotune_candidates.split(","), cfg.autotune_warmup_steps, cfg.autotune_trial_steps)
+        return cls(cfg.autotune_candidates.split(","), cfg.autotune_warmup_steps, cfg.autotune_trial_steps,
+                   getattr(cfg, "autotune_log", "") or None)
 
     def first(self) -> int:
         return self.candidates[0]
@@ -75,4 +77,15 @@ class FusionAutotuner:
         if basics.rank() == 0:
             log_kv("autotune", fusion_threshold_mib=round(self.best / 2 ** 20, 3),
                    **{f"ms@{c / 2 ** 20:g}MiB": round(float(m) * 1e3, 3) for c, m in zip(self.candidates, med)})
+            if self.log_file:
+                import csv
+                import os
+
+                new = not os.path.exists(self.log_file)
+                with open(self.log_file, "a", newline="") as f:
+                    w = csv.writer(f)
+                    if new:
+                        w.writerow(["fusion_threshold_bytes", "median_step_ms", "trial_steps", "chosen"])
+                    for c, m in zip(self.candidates, med):
+                        w.writerow([c, round(float(m) * 1e3, 4), self.trials, int(c == self.best)])
         return self.best

@@ -34,12 +34,14 @@ import threading
 import time
 from dataclasses import dataclass, field
 
-_IGNORED_WITH_ARG = {"-bind-to", "--bind-to", "-map-by", "--map-by", "-rank-by", "--rank-by", "--output-filename",
-                     "-output-filename", "--prefix", "-prefix", "-wdir", "--wdir", "-wd"}
+_IGNORED_WITH_ARG = {"-bind-to", "--bind-to", "-map-by", "--map-by", "-rank-by", "--rank-by", "--prefix", "-prefix",
+                     "-wdir", "--wdir", "-wd", "--network-interface", "--network-interfaces", "--gloo-timeout-seconds",
+                     "--config-file"}
 _IGNORED_FLAGS = {"--allow-run-as-root", "-allow-run-as-root", "--oversubscribe", "-oversubscribe",
                   "--report-bindings", "-report-bindings", "--display-map", "-display-map", "-q", "--quiet",
                   "--gloo", "--mpi", "--nccl", "--rccl", "--use-hwthread-cpus", "-use-hwthread-cpus",
-                  "--bind-to-core", "-bind-to-core", "--enable-recovery", "-v"}
+                  "--bind-to-core", "-bind-to-core", "--enable-recovery", "-v", "--disable-cache",
+                  "--mpi-threads-disable"}
 
 
 @dataclass
@@ -60,6 +62,7 @@ class LaunchSpec:
     max_np: int | None = None
     respawn: bool = False              # elastic: replace a dead worker (same slot) with a new one
     verbose: bool = False
+    output_dir: str | None = None      # mpirun --output-filename: rank r's output also goes to <dir>/1/rank.r/
     command: list[str] = field(default_factory=list)
 
 
@@ -168,6 +171,14 @@ def parse_args(argv: list[str]) -> LaunchSpec:
             spec.extra_env["MIHVD_STALL_CHECK_DISABLE"] = "1"; i += 1; continue
         if a in ("--hierarchical-allreduce",):
             spec.extra_env["MIHVD_HIERARCHICAL_ALLREDUCE"] = "1"; i += 1; continue
+        if a in ("--autotune",):
+            spec.extra_env["MIHVD_AUTOTUNE"] = "1"; i += 1; continue
+        if a in ("--autotune-log-file",):
+            spec.extra_env["MIHVD_AUTOTUNE_LOG"] = need(a); i += 2; continue
+        if a in ("--log-level",):
+            spec.extra_env["MIHVD_LOG_LEVEL"] = need(a).upper(); i += 2; continue
+        if a in ("--output-filename", "-output-filename"):
+            spec.output_dir = need(a); i += 2; continue
         if a in _IGNORED_WITH_ARG:
             spec.ignored.append(f"{a} {need(a)}"); i += 2; continue
         if a in _IGNORED_FLAGS:
@@ -259,14 +270,22 @@ class _Proc:
         self.popen = popen
 
 
-def _pump(stream, out, prefix):
-    for line in iter(stream.readline, b""):
-        if prefix:
-            out.buffer.write(prefix.encode() + line)
-        else:
-            out.buffer.write(line)
-        out.flush()
-    stream.close()
+def _pump(stream, out, prefix, copy_path=None):
+    copy = open(copy_path, "ab") if copy_path else None
+    try:
+        for line in iter(stream.readline, b""):
+            if prefix:
+                out.buffer.write(prefix.encode() + line)
+            else:
+                out.buffer.write(line)
+            out.flush()
+            if copy is not None:
+                copy.write(line)
+                copy.flush()
+    finally:
+        stream.close()
+        if copy is not None:
+            copy.close()
 
 
 def launch(spec: LaunchSpec) -> int:
@@ -332,8 +351,13 @@ def launch(spec: LaunchSpec) -> int:
         slots[wid] = (host, lr, ls, node)
         pre_o = f"[1,{wid}]<stdout>:" if spec.tag_output else ""
         pre_e = f"[1,{wid}]<stderr>:" if spec.tag_output else ""
-        for st, o, pre in ((p.stdout, sys.stdout, pre_o), (p.stderr, sys.stderr, pre_e)):
-            t = threading.Thread(target=_pump, args=(st, o, pre), daemon=True)
+        rank_dir = None
+        if spec.output_dir:  # Open MPI's layout: <dir>/1/rank.<r>/{stdout,stderr}
+            rank_dir = os.path.join(spec.output_dir, "1", f"rank.{wid}")
+            os.makedirs(rank_dir, exist_ok=True)
+        for st, o, pre, name in ((p.stdout, sys.stdout, pre_o, "stdout"), (p.stderr, sys.stderr, pre_e, "stderr")):
+            t = threading.Thread(target=_pump, args=(st, o, pre, os.path.join(rank_dir, name) if rank_dir else None),
+                                 daemon=True)
             t.start()
             threads.append(t)
 
@@ -436,10 +460,53 @@ def launch(spec: LaunchSpec) -> int:
     return exit_code
 
 
+def check_build() -> str:
+    """``horovodrun --check-build``: what this installation can run (frameworks, controllers,
+    tensor operations), probed without initialising a GPU."""
+    import importlib.util
+
+    def box(ok):
+        return "[X]" if ok else "[ ]"
+
+    try:
+        import torch
+        torch_ok = True
+        rocm = getattr(torch.version, "hip", None) is not None
+        dist_ok = torch.distributed.is_available()
+        nccl = dist_ok and torch.distributed.is_nccl_available()
+        gloo = dist_ok and torch.distributed.is_gloo_available()
+        mpi = dist_ok and torch.distributed.is_mpi_available()
+    except Exception:  # pragma: no cover
+        torch_ok = rocm = nccl = gloo = mpi = False
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    native = os.path.isdir(os.path.join(here, "_native"))
+    kernels = native and os.path.exists(os.path.join(here, "_native", "libmihvd_kernels.so"))
+    runtime = native and any(f.startswith("_mihvd_runtime") for f in os.listdir(os.path.join(here, "_native")))
+    from .. import __version__
+
+    lines = [f"mihvd v{__version__}:", "", "Available Frameworks:",
+             f"    {box(torch_ok)} PyTorch{' (ROCm)' if rocm else ''}  (mihvd.torch)",
+             f"    {box(torch_ok)} TensorFlow-shaped API on PyTorch  (mihvd.tensorflow: hooks, MonitoredTrainingSession)",
+             f"    {box(torch_ok)} Keras-shaped API on PyTorch  (mihvd.keras: callbacks, fit)",
+             f"    {box(importlib.util.find_spec('mxnet') is not None)} MXNet",
+             "", "Available Controllers:",
+             f"    {box(runtime)} native C++ store + negotiation engine",
+             f"    {box(gloo)} Gloo", f"    {box(mpi)} MPI",
+             "", "Available Tensor Operations:",
+             f"    {box(nccl and rocm)} RCCL  (torch.distributed 'nccl' backend on ROCm)",
+             f"    {box(kernels)} direct xGMI (hipIpc peer memory, csrc/kernels/xgmi.hip)",
+             f"    {box(kernels)} CDNA4 HIP kernels (gfx950: fused MNIST step, multi-tensor optimizers, Adasum)",
+             f"    {box(gloo)} Gloo", f"    {box(mpi)} MPI", f"    {box(False)} DDL", f"    {box(False)} CCL"]
+    return "\n".join(lines)
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     if argv and argv[0] in ("-h", "--help"):
         print(__doc__)
+        return 0
+    if argv and argv[0] in ("-cb", "--check-build"):
+        print(check_build())
         return 0
     spec = parse_args(argv)
     return launch(spec)

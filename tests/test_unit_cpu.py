@@ -2,6 +2,7 @@
 discovery, launcher argv compatibility, checkpoint layout, TF1-session and Keras-fit plumbing."""
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -172,6 +173,43 @@ def test_launcher_rank_env():
     e = L.build_rank_env(spec, 1, 1, 2, 0, "127.0.0.1", 29501, base_env={"HOME": "/h"})
     assert e["RANK"] == "1" and e["OMPI_COMM_WORLD_LOCAL_RANK"] == "1" and e["MASTER_PORT"] == "29501"
     assert e["FOO"] == "bar" and e["HOME"] == "/h" and e["MIHVD_FUSION_THRESHOLD"] == str(16 * 1024 * 1024)
+
+
+def test_launcher_horovodrun_knobs(tmp_path):
+    """horovodrun's tuning/diagnostic flags map onto the engine's MIHVD_* knobs; --output-filename
+    writes every rank's output under <dir>/1/rank.<r>/ (Open MPI's layout); --check-build lists
+    what this installation runs."""
+    spec = L.parse_args(["-np", "1", "--autotune", "--autotune-log-file", "at.csv", "--log-level", "debug",
+                         "--output-filename", str(tmp_path / "logs"), "--network-interface", "eth0", "--disable-cache",
+                         sys.executable, "-c", "import os,sys; print('hello', os.environ['MIHVD_LOG_LEVEL']); "
+                         "print('err', file=sys.stderr)"])
+    assert spec.extra_env == {"MIHVD_AUTOTUNE": "1", "MIHVD_AUTOTUNE_LOG": "at.csv", "MIHVD_LOG_LEVEL": "DEBUG"}
+    assert "--disable-cache" in spec.ignored and "--network-interface eth0" in spec.ignored
+    assert L.launch(spec) == 0
+    assert (tmp_path / "logs" / "1" / "rank.0" / "stdout").read_text() == "hello DEBUG\n"
+    assert (tmp_path / "logs" / "1" / "rank.0" / "stderr").read_text() == "err\n"
+    text = L.check_build()
+    assert "[X] PyTorch" in text and "Available Tensor Operations:" in text and "RCCL" in text
+
+
+def test_autotuner_writes_log_file(monkeypatch, hvd_single, tmp_path):
+    from mihvd.parallel.autotune import FusionAutotuner
+
+    log = tmp_path / "autotune.csv"
+    tu = FusionAutotuner(["1", "2"], warmup_steps=0, trial_steps=1, log_file=str(log))
+    clock = [0.0]
+    monkeypatch.setattr(tu, "_now", lambda: clock[0])
+    cur = tu.first()
+    for _ in range(20):
+        clock[0] += 1.0 if cur == 2 ** 21 else 2.0
+        new = tu.on_step()
+        if new is not None:
+            cur = new
+            if tu.done:
+                break
+    rows = log.read_text().splitlines()
+    assert rows[0] == "fusion_threshold_bytes,median_step_ms,trial_steps,chosen" and len(rows) == 3
+    assert rows[2].startswith(str(2 ** 21)) and rows[2].endswith(",1")
 
 
 # ------------------------------------------------------------------------------ checkpoints
