@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--optimizer", choices=["torch", "fused"], default="fused",
                     help="fused: mihvd multi-tensor HIP optimizer (FusedSGD / FusedAdam(adamw))")
     ap.add_argument("--graph", action="store_true", help="capture the whole step in one HIP graph")
+    ap.add_argument("--no-dp", action="store_true",
+                    help="plain optimizer without mihvd's DistributedOptimizer (world size 1: engine overhead)")
+    ap.add_argument("--mlm-all-positions", action="store_true",
+                    help="bert-base: MLM head on every position (default: the masked positions only)")
     return ap.parse_args()
 
 
@@ -82,6 +86,9 @@ def main():
         c = BertConfig(max_len=max(512, args.seq_len))
         model = BertForMaskedLM(c).to(dev)
         ids, labels = synthetic_mlm_batch(B, args.seq_len, c.vocab_size, dev, generator=g)
+        from mihvd.models.bert import masked_positions
+
+        mpos = None if args.mlm_all_positions else masked_positions(labels)
         if args.optimizer == "fused":
             from mihvd.optim import FusedAdam
 
@@ -91,13 +98,19 @@ def main():
 
         def loss_fn():
             with torch.autocast(dev.type, dtype=torch.bfloat16):
-                return model(ids, labels)
+                return model(ids, labels, masked_positions=mpos)
         unit, per_sample = "tokens/sec", args.seq_len
         metric = "tokens/sec (whole node) BERT-base MLM synthetic seq=%d bf16" % args.seq_len
         cfg = {"model": "BERT-base (12x768, 110M)", "global_batch": B * n, "seq_len": args.seq_len}
     hvd.broadcast_parameters(model.state_dict(), root_rank=0)
-    opt = hvd.DistributedOptimizer(base, named_parameters=model.named_parameters(), compression=comp,
-                                   fusion_threshold=int(args.fusion_mib * 2 ** 20) if args.fusion_mib else None)
+    if args.no_dp:
+        if n > 1:
+            raise SystemExit("--no-dp is a world-size-1 measurement")
+        opt = base
+        opt.buckets = []
+    else:
+        opt = hvd.DistributedOptimizer(base, named_parameters=model.named_parameters(), compression=comp,
+                                       fusion_threshold=int(args.fusion_mib * 2 ** 20) if args.fusion_mib else None)
 
     def step():
         opt.zero_grad(set_to_none=False)
@@ -130,7 +143,10 @@ def main():
         params = sum(p.numel() for p in model.parameters())
         cfg.update({"parallelism": f"dp{n}", "per_gpu_batch": B, "params": params,
                     "grad_bytes_fp32": params * 4, "buckets": len(opt.buckets), "compression": comp_name,
-                    "optimizer": args.optimizer, "hip_graph": bool(args.graph), "final_loss": float(loss)})
+                    "optimizer": args.optimizer, "hip_graph": bool(args.graph), "final_loss": float(loss),
+                    "distributed_optimizer": not args.no_dp})
+        if args.model == "bert-base":
+            cfg["mlm_head"] = "all positions" if args.mlm_all_positions else "masked positions"
         print(json.dumps({"metric": metric, "value": round(args.steps * B * per_sample * n / el, 1), "unit": unit,
                           "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,

@@ -75,18 +75,32 @@ class BertForMaskedLM(nn.Module):
         if isinstance(m, nn.Linear) and m.bias is not None:
             nn.init.zeros_(m.bias)
 
-    def forward(self, ids, labels=None):
+    def forward(self, ids, labels=None, masked_positions=None):
+        """``masked_positions`` (flat indices into B*S, e.g. from :func:`masked_positions`): apply the
+        MLM head only at those positions, as BERT pretraining implementations do — the vocabulary
+        projection and its softmax then cost ~15 % of the all-position form. Fixed-size, so the step
+        stays free of host synchronisation (HIP-graph capturable)."""
         B, S = ids.shape
         pos = torch.arange(S, device=ids.device)
         x = self.tok(ids) + self.pos(pos)[None] + self.typ(torch.zeros_like(ids))
         x = self.drop(self.ln(x))
         for layer in self.layers:
             x = layer(x)
+        if masked_positions is not None:
+            x = x.reshape(B * S, -1).index_select(0, masked_positions)
+            if labels is not None:
+                labels = labels.reshape(-1).index_select(0, masked_positions)
         h = self.head_ln(F.gelu(self.head_dense(x)))
         logits = h @ self.tok.weight.t() + self.head_bias
         if labels is None:
             return logits
-        return F.cross_entropy(logits.float().view(-1, logits.size(-1)), labels.view(-1), ignore_index=-100)
+        return F.cross_entropy(logits.float().view(-1, logits.size(-1)), labels.reshape(-1), ignore_index=-100)
+
+
+def masked_positions(labels: torch.Tensor) -> torch.Tensor:
+    """Flat indices of the positions that carry an MLM label (one host sync: call once per batch
+    layout, not per step)."""
+    return (labels.reshape(-1) != -100).nonzero().squeeze(1)
 
 
 def synthetic_mlm_batch(batch: int, seq: int, vocab: int, device, generator=None, mask_prob: float = 0.15):
