@@ -99,6 +99,10 @@ bool read_all(int fd, char* p, size_t n) {
   return true;
 }
 
+// Frames are small control messages (keys, ranks' signatures, membership lists); a length past this
+// is a corrupt or foreign stream: the connection is dropped instead of buffering without bound.
+constexpr uint32_t kMaxFrame = 64u << 20;
+
 void set_nodelay(int fd) {
   int one = 1;
   ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
@@ -355,6 +359,11 @@ void StoreServer::loop() {
         while (c->in.size() - pos >= 5) {
           uint32_t len;
           std::memcpy(&len, c->in.data() + pos, 4);
+          if (len < 1 || len > kMaxFrame) {
+            c->dead = true;
+            pos = c->in.size();
+            break;
+          }
           if (c->in.size() - pos - 4 < len) break;
           uint8_t op = (uint8_t)c->in[pos + 4];
           std::string payload = c->in.substr(pos + 5, len - 1);
@@ -441,6 +450,7 @@ uint8_t StoreClient::request(uint8_t op, const std::string& payload, std::string
   if (!write_all(fd_, frame.data(), frame.size())) throw std::runtime_error("StoreClient: connection lost (send)");
   uint32_t len;
   if (!read_all(fd_, (char*)&len, 4) || len < 1) throw std::runtime_error("StoreClient: connection lost (recv)");
+  if (len > kMaxFrame) throw std::runtime_error("StoreClient: corrupt reply frame");
   std::string body(len, '\0');
   if (!read_all(fd_, &body[0], len)) throw std::runtime_error("StoreClient: connection lost (recv)");
   uint8_t status = (uint8_t)body[0];

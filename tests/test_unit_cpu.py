@@ -410,6 +410,16 @@ def test_native_store_semantics():
         assert c.get("ap") == b"1234"
         assert c.delete("bin") and not c.delete("bin")
         assert c.num_keys() == srv.num_keys() == 4  # ctr, late, cs, ap
+        # a corrupt frame (length past the limit) drops that connection, not the server
+        import socket
+        import struct
+
+        raw = socket.create_connection(("127.0.0.1", srv.port))
+        raw.sendall(struct.pack("<I", 0xFFFFFFF0) + b"\x01")
+        raw.settimeout(5.0)
+        assert raw.recv(16) == b""  # closed by the server
+        raw.close()
+        assert c.get("ap") == b"1234"
     finally:
         srv.stop()
 
