@@ -97,6 +97,12 @@ def main():
         "fc1_wgrad_k8x_slice": lambda: o.fc1_wgrad(tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"),
                                                    tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
                                                    tr.gview("dense_1/bias"), 1, dz8, a28, 0, 7),
+        # the sharded xGMI plane's last launch at N=8: dW3 of this rank's 7 row tiles over all ranks'
+        # samples (K = 800) with Adam fused into the tiles
+        "fc1_wgrad_adam_k8x_slice": lambda: o.fc1_wgrad_adam(
+            tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
+            tr.gview("dense_1/bias"), 1, dz8, a28, tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], st, 0.0, 0.9,
+            0.999, 1e-8, 1.0, 0, False, 0, 7),
         "adam_w3_slice8": lambda: o.adam_step(tr.params[W3:W3 + 7 * 65536], tr.grads[W3:W3 + 7 * 65536],
                                               tr.m[W3:W3 + 7 * 65536], tr.v[W3:W3 + 7 * 65536],
                                               sh[W3:W3 + 7 * 65536], st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0, 0),

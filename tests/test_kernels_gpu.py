@@ -573,6 +573,51 @@ def test_w3_tile_tail_matches_stored_dw3_tail(ops, monkeypatch, B):
         assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
 
 
+@pytest.mark.parametrize("K", [200, 237, 800])
+def test_fc1_wgrad_long_k_two_group_tiles(ops, K):
+    """dW3 over a long K (the all-gathered factors of N ranks: Kw = N*B > 128) runs as two-group
+    tiles (K chunks split between two 4-wave groups, partial tiles combined in a fixed order):
+    close to the fp32 product, a row slice [lo, hi) reproduces those rows of the full range bit for
+    bit (sharded and replicated optimizers agree), and the fused Adam epilogue equals adam_step on
+    the stored gradient bit for bit."""
+    g = torch.Generator(device="cuda").manual_seed(K)
+    B = 100
+    bf = torch.bfloat16
+    dz = torch.randn(B, 1024, device="cuda", generator=g).to(bf)
+    a2 = torch.rand(B, 3136, device="cuda", generator=g).to(bf)
+    h = torch.rand(B, 1024, device="cuda", generator=g).to(bf)
+    dlog = torch.randn(B, 10, device="cuda", generator=g)
+    dzw = torch.randn(K, 1024, device="cuda", generator=g).to(bf)
+    a2w = torch.rand(K, 3136, device="cuda", generator=g).to(bf)
+    small = [torch.zeros(n, device="cuda") for n in (1024, 10240, 10)]
+
+    def wgrad(lo=0, hi=49):
+        out = torch.zeros(3136 * 1024, device="cuda")
+        ops.fc1_wgrad(dz, a2, h, dlog, out, *small, 1, dzw, a2w, lo, hi)
+        return out.view(3136, 1024)
+
+    full = wgrad()
+    ref = a2w.float().t() @ dzw.float()
+    assert ((full - ref).norm() / ref.norm()).item() < 1e-5
+    part = wgrad(7, 14)
+    assert torch.equal(part[448:896], full[448:896]) and not part[:448].any() and not part[896:].any()
+    n = 3136 * 1024
+    p = torch.randn(n, device="cuda", generator=g)
+    m = torch.randn(n, device="cuda", generator=g).abs() * 1e-3
+    v = torch.rand(n, device="cuda", generator=g) * 1e-4
+    st = torch.tensor([0, 3, 0, 0], device="cuda", dtype=torch.int64)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    sh = torch.empty(n, device="cuda", dtype=bf)
+    sh2 = torch.empty_like(sh)
+    gst = torch.zeros(n, device="cuda")
+    ops.fc1_wgrad_adam(dz, a2, h, dlog, gst, *small, 1, dzw, a2w, p, m, v, sh, st, 1e-3, 0.9, 0.999, 1e-8, 0.125, 0,
+                       True)
+    ops.adam_step(p2, full.reshape(-1), m2, v2, sh2, st, 0, 1e-3, 0.9, 0.999, 1e-8, 0.125, 0, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(gst, full.reshape(-1))
+    assert torch.equal(p, p2) and torch.equal(m, m2) and torch.equal(v, v2) and torch.equal(sh, sh2)
+
+
 @pytest.mark.parametrize("B", [8, 100])
 def test_conv2_bwd_adam_tail_covers_slice(ops, B):
     """The tail covers every float4 of the slice exactly once (any B, any grid), including a slice
