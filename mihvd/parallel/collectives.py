@@ -1,5 +1,5 @@
 """Tensor collectives with Horovod semantics (``hvd.allreduce / allgather / broadcast / alltoall /
-reducescatter``, their ``_async`` forms, ``synchronize`` and ``poll``).
+reducescatter``, their grouped and ``_async`` forms, sparse allreduce, ``synchronize`` and ``poll``).
 
 Each call is one RCCL collective on the process group (``nccl`` backend = RCCL over xGMI on
 MI355X; ``gloo`` on CPU). Async calls return an integer handle; the native stall inspector tracks
@@ -83,8 +83,26 @@ def poll(handle: int) -> bool:
         h = _handles.get(handle)
     if h is None:
         raise ValueError(f"unknown handle {handle}")
+    if h.done:
+        return True
     works = h.work if isinstance(h.work, (list, tuple)) else [h.work]
     return all(w is None or w.is_completed() for w in works)
+
+
+class _Children:
+    """Work object of a handle built from other handles (grouped / sparse forms): ``poll`` on
+    the parent reports completion only when every child collective has completed."""
+
+    def __init__(self, handles):
+        self.handles = list(handles)
+
+    def is_completed(self) -> bool:
+        with _hlock:
+            live = [c for c in self.handles if c in _handles]  # absent: already synchronized
+        return all(poll(c) for c in live)
+
+    def wait(self):
+        pass  # the parent's post() synchronizes the children in order
 
 
 def _drain_all():
@@ -232,14 +250,15 @@ def allreduce_(tensor, average=None, name=None, op=None, prescale_factor=1.0, po
                                         process_set=process_set))
 
 
-def grouped_allreduce(tensors: Sequence[torch.Tensor], average=None, name=None, compression=Compression.none,
-                      op=None, prescale_factor=1.0, postscale_factor=1.0, process_set=None):
-    """Fused allreduce of many tensors: one flat buffer per dtype, one collective each."""
-    op = _resolve_op(average, op)
-    outs: list[Any] = [None] * len(tensors)
+def _grouped_allreduce_async(tensors, op, name, compression, prescale_factor, postscale_factor, process_set,
+                             inplace: bool) -> int:
+    """One flat buffer and one collective per dtype; the handle's output is the list of results
+    (views of the flat buffers, or the input tensors themselves when ``inplace``)."""
+    tensors = list(tensors)
     by_dtype: dict[torch.dtype, list[int]] = {}
     for i, t in enumerate(tensors):
         by_dtype.setdefault(t.dtype, []).append(i)
+    parts = []
     for dt, idxs in by_dtype.items():
         flat = torch.cat([tensors[i].reshape(-1) for i in idxs])
         segs, off = [], 0
@@ -248,10 +267,68 @@ def grouped_allreduce(tensors: Sequence[torch.Tensor], average=None, name=None, 
             off += tensors[i].numel()
         h = _allreduce_impl(flat, flat, name or "grouped", op, compression, prescale_factor, postscale_factor,
                             _group(process_set), segments=segs)
-        flat = synchronize(h)
-        for i, (s, e) in zip(idxs, segs):
-            outs[i] = flat[s:e].view_as(tensors[i])
-    return outs
+        parts.append((h, idxs, segs))
+
+    def post(_o, parts=parts):
+        outs: list[Any] = [None] * len(tensors)
+        for h, idxs, segs in parts:
+            flat = synchronize(h)
+            for i, (s, e) in zip(idxs, segs):
+                outs[i] = flat[s:e].view_as(tensors[i])
+                if inplace:
+                    tensors[i].copy_(outs[i])
+                    outs[i] = tensors[i]
+        return outs
+
+    return _register(_Children(h for h, _, _ in parts), None, post, f"grouped_allreduce.{name or 'grouped'}")
+
+
+def grouped_allreduce_async(tensors: Sequence[torch.Tensor], average=None, name=None, op=None,
+                            prescale_factor=1.0, postscale_factor=1.0, compression=Compression.none,
+                            process_set=None) -> int:
+    return _grouped_allreduce_async(tensors, _resolve_op(average, op), name, compression, prescale_factor,
+                                    postscale_factor, process_set, inplace=False)
+
+
+def grouped_allreduce_async_(tensors: Sequence[torch.Tensor], average=None, name=None, op=None,
+                             prescale_factor=1.0, postscale_factor=1.0, process_set=None) -> int:
+    return _grouped_allreduce_async(tensors, _resolve_op(average, op), name, Compression.none, prescale_factor,
+                                    postscale_factor, process_set, inplace=True)
+
+
+def grouped_allreduce(tensors: Sequence[torch.Tensor], average=None, name=None, compression=Compression.none,
+                      op=None, prescale_factor=1.0, postscale_factor=1.0, process_set=None):
+    """Fused allreduce of many tensors: one flat buffer per dtype, one collective each."""
+    return synchronize(grouped_allreduce_async(tensors, average, name, op, prescale_factor, postscale_factor,
+                                               compression, process_set))
+
+
+def grouped_allreduce_(tensors: Sequence[torch.Tensor], average=None, name=None, op=None, prescale_factor=1.0,
+                       postscale_factor=1.0, process_set=None):
+    return synchronize(grouped_allreduce_async_(tensors, average, name, op, prescale_factor, postscale_factor,
+                                                process_set))
+
+
+def sparse_allreduce_async(tensor: torch.Tensor, name=None, op=ReduceOp.Average, process_set=None) -> int:
+    """Allreduce of a sparse COO tensor (Horovod's ``sparse_allreduce_async``, used for
+    ``sparse_as_dense=False`` embedding gradients): every rank's indices and values are
+    all-gathered and summed into one coalesced tensor (``Average`` divides by the group size)."""
+    op = ReduceOp(op)
+    if op not in (ReduceOp.Average, ReduceOp.Sum):
+        raise ValueError("sparse_allreduce supports Average and Sum")
+    t = tensor.coalesce()
+    hi = allgather_async(t.indices().t().contiguous(), name=f"{name or 'sparse'}.indices", process_set=process_set)
+    hv = allgather_async(t.values().contiguous(), name=f"{name or 'sparse'}.values", process_set=process_set)
+    n = _group_size(_group(process_set))
+
+    def post(_o, hi=hi, hv=hv, shape=t.shape):
+        idx = synchronize(hi).t()
+        val = synchronize(hv)
+        if op == ReduceOp.Average:
+            val = val / n
+        return torch.sparse_coo_tensor(idx, val, shape).coalesce()
+
+    return _register(_Children((hi, hv)), None, post, f"sparse_allreduce.{name or 'sparse'}")
 
 
 # ------------------------------------------------------------------------------------------ #
@@ -372,6 +449,28 @@ def alltoall(tensor, splits=None, name=None, process_set=None):
     else:
         dist.all_to_all_single(out, tensor.contiguous(), rsplits, splits, group=group)
     return out, torch.tensor(rsplits)
+
+
+def alltoall_async(tensor, splits=None, name=None, process_set=None) -> int:
+    """``hvd.alltoall_async``: the exchange runs at once (its split negotiation is itself a
+    collective); ``synchronize`` returns ``(output, received_splits)``."""
+    res = alltoall(tensor, splits, name, process_set)
+    return _register(None, res, None, f"alltoall.{name or 'tensor'}")
+
+
+def reducescatter_async(tensor, op=ReduceOp.Average, name=None, process_set=None) -> int:
+    return _register(None, reducescatter(tensor, op, name, process_set), None, f"reducescatter.{name or 'tensor'}")
+
+
+def grouped_reducescatter(tensors: Sequence[torch.Tensor], op=ReduceOp.Average, name=None, process_set=None):
+    """Reduce-scatter of several tensors (each split along its own dim 0)."""
+    return [reducescatter(t, op, f"{name or 'grouped'}.{i}", process_set) for i, t in enumerate(tensors)]
+
+
+def grouped_reducescatter_async(tensors: Sequence[torch.Tensor], op=ReduceOp.Average, name=None,
+                                process_set=None) -> int:
+    return _register(None, grouped_reducescatter(tensors, op, name, process_set), None,
+                     f"grouped_reducescatter.{name or 'grouped'}")
 
 
 def reducescatter(tensor, op=ReduceOp.Average, name=None, process_set=None):

@@ -56,17 +56,18 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     """Mixin body; instances are created through :func:`DistributedOptimizer`."""
 
     def _mihvd_setup(self, named_parameters, compression, backward_passes_per_step, op,
-                     gradient_predivide_factor, fusion_threshold, sparse_as_dense):
+                     gradient_predivide_factor, fusion_threshold, sparse_as_dense, local_params=()):
         from .._native import runtime
 
         basics._require()
+        local = {id(p) for p in local_params}  # PartialDistributedOptimizer: never reduced
         self._compression = compression
         self._op = ReduceOp(op)
         self._predivide = float(gradient_predivide_factor)
         if self._predivide != 1.0 and self._op != ReduceOp.Average:
             raise ValueError("gradient_predivide_factor requires op=Average")
         self._passes = int(backward_passes_per_step)
-        params = [p for g in self.param_groups for p in g["params"] if p.requires_grad]
+        params = [p for g in self.param_groups for p in g["params"] if p.requires_grad and id(p) not in local]
         seen = set()
         uniq = []
         for p in params:
@@ -82,7 +83,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             dups = {n for n, _ in named_parameters if sum(1 for m, _ in named_parameters if m == n) > 1}
             if dups:
                 raise ValueError(f"parameter names must be unique; duplicates: {sorted(dups)}")
-            names = {id(p): n for n, p in named_parameters}
+            names = {id(p): n for n, p in named_parameters if id(p) not in local}
             missing = [p for p in params if id(p) not in names]
             if missing:
                 raise ValueError("named_parameters was specified, but one or more model parameters "
@@ -273,6 +274,14 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 b.flat.zero_()
             if not self._views_intact():
                 self._install_grad_views()
+            reduced = {id(p) for p in self._params}
+            for g in self.param_groups:  # parameters kept local (PartialDistributedOptimizer)
+                for p in g["params"]:
+                    if id(p) not in reduced and p.grad is not None:
+                        if set_to_none:
+                            p.grad = None
+                        else:
+                            p.grad.zero_()
         else:
             super(self.__class__, self).zero_grad(set_to_none)
 
@@ -292,6 +301,24 @@ def DistributedOptimizer(optimizer: torch.optim.Optimizer, named_parameters=None
     obj.__dict__.update(optimizer.__dict__)
     obj._mihvd_setup(named_parameters, compression, backward_passes_per_step, op, gradient_predivide_factor,
                      fusion_threshold, sparse_as_dense)
+    return obj
+
+
+def PartialDistributedOptimizer(optimizer: torch.optim.Optimizer, named_parameters=None, compression=Compression.none,
+                                backward_passes_per_step: int = 1, op=ReduceOp.Average, gradient_predivide_factor=1.0,
+                                fusion_threshold=None, sparse_as_dense=False, local_layers=None, process_set=None):
+    """Horovod's ``PartialDistributedOptimizer``: like :func:`DistributedOptimizer`, but the
+    parameters of ``local_layers`` (modules, or an iterable of modules) keep their per-rank
+    gradients — they are updated by the wrapped optimizer without any allreduce (e.g. rank-local
+    heads or embeddings trained on rank-specific data)."""
+    mods = [] if local_layers is None else (
+        [local_layers] if isinstance(local_layers, torch.nn.Module) else list(local_layers))
+    local_params = [p for m in mods for p in m.parameters()]
+    cls = type(optimizer.__class__.__name__, (optimizer.__class__,), dict(_DistributedOptimizer.__dict__))
+    obj = cls.__new__(cls)
+    obj.__dict__.update(optimizer.__dict__)
+    obj._mihvd_setup(named_parameters, compression, backward_passes_per_step, op, gradient_predivide_factor,
+                     fusion_threshold, sparse_as_dense, local_params=local_params)
     return obj
 
 

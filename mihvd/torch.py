@@ -8,11 +8,14 @@ from .basics import (Adasum, Average, Max, Min, Product, ReduceOp, Sum, backend,
                      local_size, mpi_built, mpi_enabled, mpi_threads_supported, nccl_built, rank, rccl_built,
                      rocm_built, shutdown, size, start_timeline, stop_timeline)
 from .parallel.collectives import (allgather, allgather_async, allgather_object, allreduce, allreduce_,
-                                   allreduce_async, allreduce_async_, alltoall, barrier, broadcast, broadcast_,
-                                   broadcast_async, broadcast_async_, broadcast_object, grouped_allreduce, join, poll,
-                                   reducescatter, synchronize)
+                                   allreduce_async, allreduce_async_, alltoall, alltoall_async, barrier, broadcast,
+                                   broadcast_, broadcast_async, broadcast_async_, broadcast_object, grouped_allreduce,
+                                   grouped_allreduce_, grouped_allreduce_async, grouped_allreduce_async_,
+                                   grouped_reducescatter, grouped_reducescatter_async, join, poll, reducescatter,
+                                   reducescatter_async, sparse_allreduce_async, synchronize)
 from .parallel.compression import Compression
-from .parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters
+from .parallel.optimizer import (DistributedOptimizer, PartialDistributedOptimizer, broadcast_optimizer_state,
+                                 broadcast_parameters)
 from .ops import collective_ops as mpi_ops  # noqa: E402,F401  registers torch.ops.mihvd_dist.* (Horovod's mpi_ops)
 from . import elastic  # noqa: E402,F401  hvd.elastic.run / TorchState / ObjectState
 from .process_sets import (ProcessSet, add_process_set, get_process_set_ids_and_ranks,  # noqa: E402,F401

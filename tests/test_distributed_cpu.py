@@ -216,3 +216,29 @@ def test_collective_bandwidth_benchmark_two_ranks(tmp_path):
         f = {"allreduce": 1.0, "hvd.allreduce": 1.0, "allgather": 0.5, "broadcast": 1.0}.get(r["op"])
         if f is not None:
             assert abs(r["busbw_GBs"] - f * r["algbw_GBs"]) < 1e-9 * max(1.0, r["algbw_GBs"])
+
+
+def test_api_extras_two_ranks(tmp_path):
+    """Grouped / async / in-place / sparse collectives and PartialDistributedOptimizer."""
+    _, (a, b) = run_scenario(tmp_path, "api_extras")
+    assert a["grouped_async"] == b["grouped_async"] == [[3.0] * 3, [[1.0, 1.0], [1.0, 1.0]], [0.0, 3.0, 6.0, 9.0]]
+    assert a["grouped_unchanged"] == [1.0] * 3                      # the non-in-place form leaves inputs alone
+    assert a["grouped_inplace"] == b["grouped_inplace"] == [[1.5] * 3, [[0.5, 0.5], [0.5, 0.5]], [0.0, 1.5, 3.0, 4.5]]
+    assert a["alltoall_async"] == [0.0, 1.0, 100.0, 101.0] and b["alltoall_async"] == [2.0, 3.0, 102.0, 103.0]
+    assert a["alltoall_splits"] == [2, 2]
+    assert a["reducescatter_async"] == b["reducescatter_async"] == [[3.0] * 3] * 2
+    assert a["grouped_reducescatter"] == b["grouped_reducescatter"] == [[[1.5, 1.5]], [0.5] * 3]
+    assert a["grouped_reducescatter_async"] == [[3.0]]
+    assert a["sparse_sum"] == b["sparse_sum"] == [[2.0, 1.0], [0.0, 2.0], [0.0, 0.0]]
+    assert a["sparse_avg"] == [[1.0, 0.5], [0.0, 1.0], [0.0, 0.0]]
+    for r in (a, b):
+        assert r["reduced_params"] == 2                              # body weight + bias only
+        assert r["head_grad"] == pytest.approx(r["head_ref"])        # local: this rank's own gradient
+        assert r["body_grad"] == pytest.approx(r["body_ref"], rel=1e-5)
+    assert a["head_grad"] != b["head_grad"]
+
+
+def test_api_extras_debug_sync_mode(tmp_path):
+    """Composite handles (grouped / sparse) stay pollable when every collective completes eagerly."""
+    _, (a, b) = run_scenario(tmp_path, "api_extras", env={"MIHVD_DEBUG_SYNC": "1"})
+    assert a["grouped_async"] == b["grouped_async"] and a["sparse_sum"] == [[2.0, 1.0], [0.0, 2.0], [0.0, 0.0]]

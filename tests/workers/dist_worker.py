@@ -296,6 +296,59 @@ def sc_process_sets(outdir):
     out(outdir, "process_sets", res)
 
 
+def sc_api_extras(outdir):
+    """Grouped / async / in-place / sparse forms of the collectives and PartialDistributedOptimizer."""
+    r, n = hvd.rank(), hvd.size()
+    res = {}
+    ts = [torch.ones(3) * (r + 1), torch.full((2, 2), float(r)), torch.arange(4, dtype=torch.float64) * (r + 1)]
+    h = hvd.grouped_allreduce_async(ts, op=hvd.Sum, name="ga")
+    while not hvd.poll(h):
+        time.sleep(0.001)
+    res["grouped_async"] = [x.tolist() for x in hvd.synchronize(h)]
+    res["grouped_unchanged"] = ts[0].tolist()
+    hvd.grouped_allreduce_(ts, op=hvd.Average)
+    res["grouped_inplace"] = [x.tolist() for x in ts]
+    h = hvd.alltoall_async(torch.arange(n * 2, dtype=torch.float32) + 100 * r)
+    o, splits = hvd.synchronize(h)
+    res["alltoall_async"] = o.tolist()
+    res["alltoall_splits"] = splits.tolist()
+    h = hvd.reducescatter_async(torch.ones(n * 2, 3) * (r + 1), op=hvd.Sum)
+    res["reducescatter_async"] = hvd.synchronize(h).tolist()
+    g = hvd.grouped_reducescatter([torch.ones(n, 2) * (r + 1), torch.ones(n * 3) * r], op=hvd.Average)
+    res["grouped_reducescatter"] = [x.tolist() for x in g]
+    h = hvd.grouped_reducescatter_async([torch.ones(n) * (r + 1)], op=hvd.Sum)
+    res["grouped_reducescatter_async"] = [x.tolist() for x in hvd.synchronize(h)]
+    # sparse: rank r holds value (r+1) at row r and 1.0 at row 0 of a (n+1)x2 tensor
+    idx = torch.tensor([[0, r], [0, 1]])
+    sp = torch.sparse_coo_tensor(idx, torch.tensor([1.0, float(r + 1)]), (n + 1, 2))
+    h = hvd.sparse_allreduce_async(sp, name="emb", op=hvd.Sum)
+    res["sparse_sum"] = hvd.synchronize(h).to_dense().tolist()
+    res["sparse_avg"] = hvd.synchronize(hvd.sparse_allreduce_async(sp, name="emb2")).to_dense().tolist()
+    # PartialDistributedOptimizer: the head stays rank-local, the body is averaged
+    torch.manual_seed(0)
+    body, head = torch.nn.Linear(4, 4), torch.nn.Linear(4, 1)
+    model = torch.nn.Sequential(body, torch.nn.Tanh(), head)
+    opt = hvd.PartialDistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.0),
+                                          named_parameters=model.named_parameters(), local_layers=[head], op=hvd.Sum)
+    for _ in range(2):
+        opt.zero_grad()
+        model(torch.ones(2, 4) * (r + 1)).sum().backward()
+        opt.step()
+    res["head_grad"] = head.weight.grad.flatten().tolist()
+    res["body_grad"] = body.bias.grad.tolist()
+    ref_body = []
+    for rr in range(n):
+        torch.manual_seed(0)
+        b2, h2 = torch.nn.Linear(4, 4), torch.nn.Linear(4, 1)
+        torch.nn.Sequential(b2, torch.nn.Tanh(), h2)(torch.ones(2, 4) * (rr + 1)).sum().backward()
+        ref_body.append(b2.bias.grad)
+        if rr == r:
+            res["head_ref"] = h2.weight.grad.flatten().tolist()
+    res["body_ref"] = torch.stack(ref_body).sum(0).tolist()
+    res["reduced_params"] = len(opt._params)
+    out(outdir, "api_extras", res)
+
+
 PS_INIT = []
 
 
