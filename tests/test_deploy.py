@@ -83,3 +83,59 @@ def test_elastic_mpijob():
     assert (ls.np, ls.min_np, ls.max_np, ls.respawn) == (16, 8, 16, True)
     assert ls.command[:2] == ["python", "/examples/tensorflow_mnist_elastic.py"]
     assert spec["mpiReplicaSpecs"]["Worker"]["replicas"] * 8 >= ls.max_np
+
+
+def _logql_regexes(expr):
+    """The RE2 patterns inside `...` of a LogQL query (`regexp` stages and `|~` filters)."""
+    import re
+
+    return re.findall(r"`([^`]*)`", expr)
+
+
+def test_loki_values_and_dashboard_parse_the_training_logs():
+    """Promtail's rank-label stage and every Grafana panel query match the lines the framework
+    writes (mihvd/utils/logging.py via LoggingTensorHook / StepCounterHook)."""
+    import json
+    import re
+
+    from mihvd.utils.logging import fmt_kv
+
+    (vals,) = _load("loki-stack-values.yaml")
+    assert vals["loki"]["persistence"] == {"enabled": True, "size": "5Gi"}
+    assert vals["grafana"]["sidecar"]["dashboards"]["label"] == "grafana_dashboard"
+    stages = vals["promtail"]["config"]["snippets"]["pipelineStages"]
+    match = [s["match"] for s in stages if "match" in s][0]
+    rx = [s["regex"]["expression"] for s in match["stages"] if "regex" in s][0]
+    lines = ["[rank 3/8] " + fmt_kv(step=120, loss=0.0421, sec=0.012),
+             "[rank 0/8] " + fmt_kv(**{"global_step/sec": 14210.5, "img_per_sec": 11368400.0}),
+             "[rank 1/8] " + fmt_kv(step=7, val_loss=9.5, loss=1.5)]
+    m = re.match(rx, lines[0])
+    assert m and m.group("rank") == "3" and m.group("world") == "8"
+
+    dash = json.load(open(os.path.join(DEPLOY, "grafana", "mihvd-dashboard.json")))
+    assert dash["uid"] == "mihvd-mnist" and len(dash["panels"]) >= 5
+    want = {"loss": {0: 0.0421, 2: 1.5}, "step": {0: 120.0, 2: 7.0}, "img_per_sec": {1: 11368400.0},
+            "global_step/sec": {1: 14210.5}}
+    seen = set()
+    for p in dash["panels"]:
+        for t in p["targets"]:
+            for pat in _logql_regexes(t["expr"]):
+                if "(?P<v>" not in pat:
+                    assert re.search(pat, "[rank 1/8] RuntimeError: stall detected")
+                    continue
+                key = re.search(r"\)(.+)=\(\?P<v>", pat).group(1)
+                seen.add(key)
+                for i, line in enumerate(lines):
+                    m = re.search(pat, line)
+                    if i in want[key]:
+                        assert m and float(m.group("v")) == want[key][i], (key, line)
+                    else:
+                        assert m is None, (key, line)   # `loss` never picks up `val_loss`
+    assert seen == set(want)
+
+
+def test_deploy_script_provisions_dashboard():
+    out = subprocess.run(["bash", os.path.join(DEPLOY, "deploy_stack.sh")], env={**os.environ, "DRY_RUN": "1"},
+                         capture_output=True, text=True, check=True).stdout
+    assert "-f " in out and "loki-stack-values.yaml" in out
+    assert "create configmap mihvd-dashboard -n loki" in out and "grafana_dashboard=1" in out
