@@ -72,6 +72,21 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Direct global -> LDS copy of an image of 128-byte rows into the row-XOR-swizzled layout
+// lds[row * 64 + 8 * (chunk ^ (row & 7))] (bf16 elements; 8 16-byte chunks per row). One
+// global_load_lds_dwordx4 per wave and 64 chunks: the LDS destination of a wave-instruction is
+// lane-linear, so the swizzle is applied to the per-lane SOURCE address. No VGPR round trip and no
+// ds_write pass; the copy has landed after the next __syncthreads() (its vmcnt(0) covers it).
+template <int NT>
+__device__ __forceinline__ void glds_swz128(const u16* __restrict__ g, u16* lds, int nchunks, int t) {
+  const int lane = t & 63, w0 = (t >> 6) * 64;
+  for (int i0 = w0; i0 < nchunks; i0 += NT) {  // wave-uniform bounds
+    const int i = i0 + lane, row = i >> 3;
+    __builtin_amdgcn_global_load_lds((const void*)(g + row * 64 + 8 * ((i & 7) ^ (row & 7))),
+                                     (void __attribute__((address_space(3)))*)(lds + i0 * 8), 16, 0, 0);
+  }
+}
+
 // Stage a [rows][cpr x 16 B] tile from global (row stride gstride elements) into LDS (row stride
 // lstride elements, 16-byte aligned). Rows >= valid_rows are zero-filled. Every load is issued
 // before any LDS store and none is predicated (addresses are clamped, the value is selected after),
@@ -210,56 +225,49 @@ struct AdamTail {
   float lr, b1, b2, eps, gscale;
   int rule;
   int first_free;        // blocks [first_free, grid) have no compute work ...
-  int64_t head;          // ... and alone take the groups [0, head) before the shared range
-  int kpl;               // float4 per lane per array in one group (4 or 8)
+  int64_t head;          // ... and alone take the chunks [0, head) (64 float4 each) before the shared range
 };
 
-// One group: K float4 per lane per array (64 K float4, all loads in flight before any update).
-template <int K>
-__device__ __forceinline__ void adam_tail_group(const AdamTail& at, const AdamCoef& c, int64_t w, int lane) {
-  float4 pp[K], gg[K], mm[K], vv[K];
-  int64_t idx[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    idx[k] = min(w * (64 * K) + k * 64 + lane, at.n4 - 1);
-    pp[k] = reinterpret_cast<const float4*>(at.p)[idx[k]];
-    gg[k] = reinterpret_cast<const float4*>(at.g)[idx[k]];
-    mm[k] = reinterpret_cast<const float4*>(at.m)[idx[k]];
-    vv[k] = reinterpret_cast<const float4*>(at.v)[idx[k]];
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    if (w * (64 * K) + k * 64 + lane >= at.n4) continue;
-    const uint2 sh = adam4(pp[k], mm[k], vv[k], gg[k], c);
-    reinterpret_cast<float4*>(at.p)[idx[k]] = pp[k];
-    reinterpret_cast<float4*>(at.m)[idx[k]] = mm[k];
-    reinterpret_cast<float4*>(at.v)[idx[k]] = vv[k];
-    reinterpret_cast<uint2*>(at.shadow)[idx[k]] = sh;
+// One float4 of every array per lane per iteration, grid-stride — the loop of the standalone
+// adam_kernel (optim.hip), which streams at full HBM rate even on one 4-wave block per CU; the
+// arrays are restrict-qualified locals so loads may be hoisted past the previous stores.
+__device__ __forceinline__ void adam_tail_stream(const AdamTail& at, const AdamCoef& c, int64_t i, int64_t end,
+                                                 int64_t stride) {
+  float* __restrict__ p = at.p;
+  const float* __restrict__ g = at.g;
+  float* __restrict__ m = at.m;
+  float* __restrict__ v = at.v;
+  u16* __restrict__ sh = at.shadow;
+  for (; i < end; i += stride) {
+    float4 pp = reinterpret_cast<const float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<const float4*>(m)[i];
+    float4 vv = reinterpret_cast<const float4*>(v)[i];
+    const uint2 s2 = adam4(pp, mm, vv, gg, c);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    reinterpret_cast<uint2*>(sh)[i] = s2;
   }
 }
 
-// Blocks without compute work start at once and run for the whole compute phase, so they take a
-// head range of their own (at.head groups, sized by the caller) before every wave of the launch
-// shares the rest.
-template <int K>
-__device__ __forceinline__ void adam_tail_run_k(const AdamTail& at) {
+// Waves without compute work start at once and run for the whole compute phase, so they take a
+// head range of their own (at.head float4 chunks of 64, sized by the caller) before every wave of
+// the launch shares the rest. Free waves: every wave of the blocks [first_free, grid), and the
+// streamer waves (index >= 8) that blocks of more than 512 threads add to the compute blocks.
+__device__ __forceinline__ void adam_tail_run(const AdamTail& at) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int waves = (int)blockDim.x >> 6;
+  const int sw = waves - 8 > 0 ? waves - 8 : 0;  // streamer waves per compute block
   const AdamCoef c = adam_coef((float)at.state[ST_OPT], at.lr, at.b1, at.b2, at.eps, at.gscale, at.rule);
-  const int64_t ng = (at.n4 + 64 * K - 1) / (64 * K);
-  const int64_t head = min(at.head, ng);
+  const int64_t head4 = min(at.head * 64, at.n4);
   const int n_free = (int)gridDim.x - at.first_free;
-  if ((int)blockIdx.x >= at.first_free && n_free > 0) {
-    for (int64_t w = (int64_t)((int)blockIdx.x - at.first_free) * waves + wave; w < head; w += (int64_t)n_free * waves)
-      adam_tail_group<K>(at, c, w, lane);
-  }
-  const int64_t nw = (int64_t)gridDim.x * waves;
-  for (int64_t w = head + (int64_t)blockIdx.x * waves + wave; w < ng; w += nw) adam_tail_group<K>(at, c, w, lane);
-}
-
-__device__ __forceinline__ void adam_tail_run(const AdamTail& at) {
-  if (at.kpl == 8) adam_tail_run_k<8>(at);
-  else adam_tail_run_k<4>(at);
+  const int64_t nfw = (int64_t)at.first_free * sw + (int64_t)n_free * waves;
+  int64_t fw = -1;
+  if ((int)blockIdx.x >= at.first_free) fw = (int64_t)at.first_free * sw + (int64_t)((int)blockIdx.x - at.first_free) * waves + wave;
+  else if (wave >= 8) fw = (int64_t)blockIdx.x * sw + (wave - 8);
+  if (fw >= 0) adam_tail_stream(at, c, fw * 64 + lane, head4, nfw * 64);
+  adam_tail_stream(at, c, head4 + ((int64_t)blockIdx.x * waves + wave) * 64 + lane, at.n4, (int64_t)gridDim.x * waves * 64);
 }
 
 }  // namespace mihvd

@@ -35,7 +35,14 @@ __device__ __forceinline__ int swd(int r) { return 4 * (((r >> 1) & 1) | (((r >>
 // fragment reads hits 64 distinct banks (checked with a bank model of the lane groups).
 constexpr int CB_DG_W = 800 * 64;
 constexpr int CB_DG_D = 326 * 64;                                  // 18 x 18 halo image + 2 spare rows
-constexpr int CB_DG_LDS = (CB_DG_W + CB_DG_D) * 2;                 // 144,128 B
+// + conv1-tail operands staged with the dgrad operands, outside the W2 / dY2 images: the five
+// kw-shifted bf16 input images [5][32][32], a zero chunk and the bias fold slots (db2 [8 waves][16]
+// float4, db1 [8 waves][4 lg][8]), 13,328 B. The launch adds the kernel's static LDS (the
+// co-launched roles) and checks the sum against the CU's 163,840 B.
+constexpr int CB_X_OFF = CB_DG_W + CB_DG_D;                        // elements
+constexpr int CB_X_LDS = (5 * 32 * 32 + 8) * 2 + (512 + 256) * 4;
+constexpr int CB_DG_LDS = (CB_DG_W + CB_DG_D) * 2 + CB_X_LDS;      // 157,456 B
+static_assert(CB_DG_LDS <= 163840 - 1024, "dgrad LDS fits one CU with room for static LDS");
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + 8 * (chunk ^ (row & 7)); }
 // wgrad LDS per wave group: A [325][32] | Dm [197][64]
 constexpr int CB_WG_A = 325 * 32;
@@ -65,9 +72,22 @@ constexpr int CP_DB1 = 800, CP_DB2 = 832, CP_W = 896;  // [dW1 (800) | db1 (32) 
 constexpr int C1_DSTR = 40;                          // dY1 row stride (32 co + 8 pad)
 constexpr int C1_DY = 785 * C1_DSTR;                 // elements; row 784 = zeros
 constexpr int C1_XS = 32 * 32;                       // one shifted bf16 image copy [32][32]
-constexpr int C1_LDS = (C1_DY + 5 * C1_XS + 8) * 2 + 32 * 36 * 4;  // + zero chunk + fp32 staging
-static_assert(C1_LDS <= CB_DG_W * 2, "the conv1 images fit in the dead W2 image");
-static_assert(8 * 64 * 16 * 4 <= CB_DG_D * 2 && (512 * 4 + 256) * 4 <= CB_DG_D * 2, "partials fit in the dY2 image");
+static_assert(C1_DY * 2 <= CB_DG_W * 2, "dY1 fits in the dead W2 image");
+static_assert(8 * 64 * 16 * 4 <= CB_DG_D * 2, "the GEMM partials fit in the dead dY2 image");
+
+// Sum over the 16 lanes of a DPP row (every lane gets the row's sum): quad xor 1, quad xor 2,
+// half-row mirror, row mirror — four v_add_f32 with DPP operands instead of LDS permutes.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
 
 struct DyItem {
   uint2 g;       // 4 bf16 pooled gradients (already masked by conv2's pooled ReLU)
@@ -95,12 +115,38 @@ __device__ __forceinline__ void finish_dy_item(const DyItem& it, u16 g[4], int d
   }
 }
 
+// Barrier of the conv roles' eight waves. With streamer waves in the block (TAIL_ADAM launches
+// of 512 + 64 * SW threads, below) a hardware s_barrier would also wait for the streamers, so
+// the eight conv waves meet on an LDS counter instead: each wave adds 1 after its LDS accesses
+// have completed (workgroup release) and waits until the counter reaches 8 x its barrier count.
+template <bool SWB>
+struct ConvBarrier {
+  unsigned* ctr;
+  unsigned gen = 0;
+  __device__ __forceinline__ void sync() {
+    if constexpr (!SWB) {
+      __syncthreads();
+    } else {
+      gen += 8;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // bounded: a broken count ends the wait (wrong results, not a hung GPU) after ~30 ms
+      for (int spin = 0; spin < (1 << 20) && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen;
+           ++spin)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+  }
+};
+
+template <bool SWB>
 __device__ __forceinline__ void conv2_bwd_block(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
-    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int bx) {
+    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int bx, unsigned* bar_ctr) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  ConvBarrier<SWB> bar{bar_ctr};
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
   if (bx < n_dgrad) {
@@ -108,8 +154,8 @@ __device__ __forceinline__ void conv2_bwd_block(
     const int b = bx;
     u16* Ws = smem;              // [800][64] swizzled, row = kk*32 + ci, cols = co
     u16* D = smem + CB_DG_W;     // [326][64] swizzled padded dY2 image (pixel = row)
-    // Issue every load of the block first: W2 (13 x 16 B per thread), 2 dY2 items and the
-    // epilogue's conv1 pooled-ReLU mask.
+    // Issue every load of the block first: W2 (direct to LDS), 2 dY2 items and the epilogue's
+    // conv1 pooled-ReLU mask.
     DyItem items[2];
     int ie[2];
 #pragma unroll
@@ -118,8 +164,7 @@ __device__ __forceinline__ void conv2_bwd_block(
       ie[k] = t + 512 * k;
       items[k] = load_dy_item(g2, idx2, b, (i >> 4) * 64 + (i & 15) * 4);
     }
-    TileLoad<512, 13, 8> lw;
-    lw.load(w2bf, 64, 800, 800, t);
+    glds_swz128<512>(w2bf, Ws, 800 * 8, t);  // W2 straight into its swizzled LDS image
     // output tiles: image row y = wave and wave + 8 (rows 14, 15 are dummies), pixel x = lr
     // (x = 14, 15 dummies); lane holds ci 16*nt + 4*lg .. +3 of that pixel.
     uint2 amask[2][2];
@@ -151,11 +196,6 @@ __device__ __forceinline__ void conv2_bwd_block(
         xv[k] = mask_f(xi[in ? gy * 28 + gx : 0], in);
       }
     }
-#pragma unroll
-    for (int it = 0; it < 13; ++it) {
-      const int i = t + it * 512;
-      if (i < 800 * 8) *reinterpret_cast<uint4*>(Ws + swz64(i >> 3, i & 7)) = lw.v[it];
-    }
     // zero the halo pixels (interior pixels are fully written by the scatter); rows 324, 325 are
     // only read by dummy output columns, whose results are discarded
     for (int i = t; i < 324 * 8; i += 512) {
@@ -184,7 +224,30 @@ __device__ __forceinline__ void conv2_bwd_block(
         }
       }
     }
-    __syncthreads();
+    // The epilogue / conv1-tail operands must have landed here, with the staging loads: left to
+    // itself the compiler sinks these loads to their first use after the GEMM and exposes their
+    // full latency there.
+    // conv1 tail operands: the five kw-shifted bf16 copies of the zero-padded input image,
+    // Xs[kw][r][c] = P[r][c + kw] with P = x padded by 2 (columns 32..35 of P are zero)
+    u16* Xs = smem + CB_X_OFF;
+    u16* Zc = Xs + 5 * C1_XS;  // zero chunk (dummy taps)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = t + 512 * k, r = i >> 5, col = i & 31;
+      const u16 v = f2bf(xv[k]);
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw)
+        if (col >= kw) Xs[kw * C1_XS + r * 32 + col - kw] = v;
+    }
+    if (t < 320) {  // the 10 entries per row that read P's zero columns: (kw, c) with c + kw >= 32
+      const int r = t / 10, e = t - r * 10;
+      const int kw = e < 1 ? 1 : e < 3 ? 2 : e < 6 ? 3 : 4;
+      const int c = 32 - kw + (e - (kw * (kw - 1)) / 2);
+      Xs[kw * C1_XS + r * 32 + c] = 0;
+    } else if (t == 320) {
+      *reinterpret_cast<uint4*>(Zc) = make_uint4(0, 0, 0, 0);
+    }
+    bar.sync();
     if (dbg_exit == 1) return;  // profiling: staging only
     // GEMM: rows = ci (2 tiles), cols = 16 pixels of image row y, K = (kh, kw, co) = 1600.
     // Waves 6, 7 compute a dummy second tile (no guard on MFMAs).
@@ -234,13 +297,11 @@ __device__ __forceinline__ void conv2_bwd_block(
     }
     if (dbg_exit == 3) return;  // profiling: no conv1 tail
     // ---- fused conv1 weight gradient (see conv1 section below for the GEMM layout)
-    __syncthreads();  // W2 and dY2 images are dead: reuse their LDS
+    bar.sync();  // W2 and dY2 images are dead: reuse their LDS
+    if (dbg_exit == 7) return;  // profiling: conv1 tail cut after its first barrier
     u16* Dy = smem;                                          // [785][40] full-resolution dY1
-    u16* Xs = smem + C1_DY;                                  // 5 x [32][32] kw-shifted bf16 images
-    u16* Zc = Xs + 5 * C1_XS;                                // zero chunk (dummy taps)
-    float* Xf = reinterpret_cast<float*>(Zc + 8);            // [32][36] fp32 padded image
-    float* red = reinterpret_cast<float*>(D);                // [512][4] db2 | [8 waves][4 lg][8] db1
-    float* red1 = red + 512 * 4;
+    float* red = reinterpret_cast<float*>(Zc + 8);           // [8 waves][16] float4 db2 | [8 waves][4 lg][8] db1
+    float* red1 = red + 512;
     float d1[8];                                             // db1 partial: (nt, i) channel 16nt+4lg+i
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -265,16 +326,10 @@ __device__ __forceinline__ void conv2_bwd_block(
         }
       }
     }
-    // db1: sum the 16 pixels (lanes lr) of each lane group, then one slot per (wave, lg)
+    if (dbg_exit == 8) return;  // profiling: ... after the dY1 scatter stores
+    // db1: sum the 16 pixels (lanes lr = one DPP row) of each lane group, then one slot per (wave, lg)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      float v = d1[c];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      d1[c] = v;
-    }
+    for (int c = 0; c < 8; ++c) d1[c] = row_sum16(d1[c]);
     if (lr == 0) {
 #pragma unroll
       for (int c = 0; c < 8; ++c) red1[(wave * 4 + lg) * 8 + c] = d1[c];
@@ -287,12 +342,9 @@ __device__ __forceinline__ void conv2_bwd_block(
       db[c] += __shfl_xor(db[c], 32, 64);
     }
     if (lane < 16) *reinterpret_cast<float4*>(red + (wave * 16 + lane) * 4) = make_float4(db[0], db[1], db[2], db[3]);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) Xf[((t + 512 * k) >> 5) * 36 + ((t + 512 * k) & 31)] = xv[k];
-    if (t < 32) Xf[t * 36 + 32] = Xf[t * 36 + 33] = Xf[t * 36 + 34] = Xf[t * 36 + 35] = 0.f;
     if (t < 5) reinterpret_cast<uint4*>(Dy + 784 * C1_DSTR)[t] = make_uint4(0, 0, 0, 0);
-    if (t == 5) *reinterpret_cast<uint4*>(Zc) = make_uint4(0, 0, 0, 0);
-    __syncthreads();
+    bar.sync();
+    if (dbg_exit == 4) return;  // profiling: conv1 tail cut after the dY1 scatter
     if (t < 64) {
       // db2 channel co4*4 + c, summed over the 32 threads with (tid & 15) == co4
       const int co4 = t >> 2, c = t & 3;
@@ -307,14 +359,7 @@ __device__ __forceinline__ void conv2_bwd_block(
       for (int w = 0; w < 8; ++w) sacc += red1[(w * 4 + lgg) * 8 + nt * 4 + i];
       cpart[(int64_t)b * CP_W + CP_DB1 + ch] = sacc;
     }
-    for (int i = t; i < 5 * 32 * 4; i += 512) {
-      const int kw = i >> 7, r = (i >> 2) & 31, c0 = (i & 3) * 8;
-      const float* src = Xf + r * 36 + c0 + kw;
-      *reinterpret_cast<uint4*>(Xs + kw * C1_XS + r * 32 + c0) =
-          make_uint4((uint32_t)f2bf(src[0]) | ((uint32_t)f2bf(src[1]) << 16), (uint32_t)f2bf(src[2]) | ((uint32_t)f2bf(src[3]) << 16),
-                     (uint32_t)f2bf(src[4]) | ((uint32_t)f2bf(src[5]) << 16), (uint32_t)f2bf(src[6]) | ((uint32_t)f2bf(src[7]) << 16));
-    }
-    __syncthreads();
+    if (dbg_exit == 5) return;  // profiling: ... after the bias sums
     // GEMM dW1^T[co][tap] = sum_pix dY1^T[co][pix] im2col(x)[pix][tap]: wave w takes image rows
     // w, w+8, w+16, w+24 (rows >= 28 read the zero dY1 row: no guard around the MFMAs).
     int boff[2];
@@ -351,7 +396,8 @@ __device__ __forceinline__ void conv2_bwd_block(
       for (int nt = 0; nt < 2; ++nt)
         *reinterpret_cast<float4*>(part + (wave * 64 + lane) * 16 + (mt * 2 + nt) * 4) =
             make_float4(c1[mt][nt][0], c1[mt][nt][1], c1[mt][nt][2], c1[mt][nt][3]);
-    __syncthreads();
+    bar.sync();
+    if (dbg_exit == 6) return;  // profiling: ... after the GEMM (no wave sum, no stores)
     for (int o = t; o < 800; o += 512) {
       const int tap = o >> 5, co = o & 31;
       const int nt = tap >> 4, lrr = tap & 15, mt = co >> 4, lgg = (co >> 2) & 3, i = co & 3;
@@ -398,7 +444,7 @@ __device__ __forceinline__ void conv2_bwd_block(
       items[k].g.x &= m;
       items[k].g.y &= m;
     }
-    __syncthreads();  // the previous image's operands are no longer read
+    bar.sync();  // the previous image's operands are no longer read
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const int i = th + 256 * k;
@@ -425,7 +471,7 @@ __device__ __forceinline__ void conv2_bwd_block(
         }
       }
     }
-    __syncthreads();
+    bar.sync();
     // (an absent image was staged as zeros, so it is computed unconditionally: no MFMA guard)
 #pragma unroll
     for (int k0 = 0; k0 < 224; k0 += 32) {
@@ -449,7 +495,7 @@ __device__ __forceinline__ void conv2_bwd_block(
     }
   }
   // Sum the two wave groups, then one float4 per lane per tile into the slab.
-  __syncthreads();
+  bar.sync();
   float* red = reinterpret_cast<float*>(smem);  // group 1 -> [40][256] floats
   if (h == 1) {
 #pragma unroll
@@ -457,7 +503,7 @@ __device__ __forceinline__ void conv2_bwd_block(
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[(mt * 4 + e) * 256 + th] = acc[mt][e];
   }
-  __syncthreads();
+  bar.sync();
   if (h == 0) {
     float* out = slab + (int64_t)grp * 51200;
 #pragma unroll
@@ -479,8 +525,13 @@ __device__ __forceinline__ void conv2_bwd_block(
 // w3_tail.h). Blocks [n_conv, grid) have no conv work and start on it at once (they sit on the CUs
 // the conv roles leave idle); every conv block joins in when its own work is done.
 enum { TAIL_NONE = 0, TAIL_ADAM = 1, TAIL_W3 = 2 };
+// TAIL_ADAM launches may add SW streamer waves (waves 8 .. 8 + SW - 1) to every block: they stream
+// the update from the first cycle on the CUs the conv roles occupy (latency-bound work that leaves
+// HBM idle), while the conv waves meet on the LDS counter barrier above.
+constexpr int CB_MAX_THREADS = 768;
+constexpr int CB_LDS_SW = CB_LDS + 16;  // + the conv waves' barrier counter
 template <int TAIL>
-__global__ void __launch_bounds__(512) conv2_bwd_kernel(
+__global__ void __launch_bounds__(TAIL == TAIL_ADAM ? CB_MAX_THREADS : 512) conv2_bwd_kernel(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
@@ -493,8 +544,18 @@ __global__ void __launch_bounds__(512) conv2_bwd_kernel(
     return;
   }
   const int bx = (int)blockIdx.x - cr.nblk;
-  if (bx < n_conv)
-    conv2_bwd_block(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit, bx);
+  if (TAIL == TAIL_ADAM && blockDim.x > 512) {
+    extern __shared__ __attribute__((aligned(16))) u16 smem[];
+    unsigned* ctr = reinterpret_cast<unsigned*>(smem + CB_LDS / 2);
+    if (threadIdx.x == 0) *ctr = 0u;
+    __syncthreads();  // the only block-wide barrier: every later one is the conv waves' own
+    if (bx < n_conv && threadIdx.x < 512)
+      conv2_bwd_block<true>(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit,
+                            bx, ctr);
+  } else if (bx < n_conv) {
+    conv2_bwd_block<false>(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit, bx,
+                           nullptr);
+  }
   if constexpr (TAIL == TAIL_ADAM) adam_tail_run(at);
   if constexpr (TAIL == TAIL_W3) w3_tail_run(wt);  // independent waves, no LDS
 }
@@ -654,9 +715,15 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
   else TORCH_CHECK(n_pool >= B, "conv2_bwd: x has fewer rows than the batch");
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   static bool attr = [] {
-    hipFuncSetAttribute((const void*)conv2_bwd_kernel<TAIL_NONE>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
-    hipFuncSetAttribute((const void*)conv2_bwd_kernel<TAIL_ADAM>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
-    hipFuncSetAttribute((const void*)conv2_bwd_kernel<TAIL_W3>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS);
+    for (const void* f : {(const void*)conv2_bwd_kernel<TAIL_NONE>, (const void*)conv2_bwd_kernel<TAIL_ADAM>,
+                          (const void*)conv2_bwd_kernel<TAIL_W3>}) {
+      hipFuncAttributes fa;
+      TORCH_CHECK(hipFuncGetAttributes(&fa, f) == hipSuccess, "conv2_bwd: hipFuncGetAttributes");
+      TORCH_CHECK(fa.sharedSizeBytes + CB_LDS_SW <= 163840, "conv2_bwd: static (", fa.sharedSizeBytes, ") + dynamic (",
+                  CB_LDS_SW, ") LDS exceeds the CU's 163,840 B");
+      TORCH_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, CB_LDS_SW) == hipSuccess,
+                  "conv2_bwd: hipFuncSetAttribute");
+    }
     return true;
   }();
   (void)attr;
@@ -691,28 +758,30 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
         cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, W3TileTail{}, cr);
   } else {
-    // one 512-thread block per CU (144 KB of LDS): the extra tail-only blocks take the CUs the
-    // conv roles leave free, so the update streams from the first cycle
+    // one block per CU (the conv roles' LDS): the extra tail-only blocks take the CUs the conv
+    // roles leave free, and every conv block carries streamer waves, so the update streams from
+    // the first cycle on every CU (the conv roles are latency-bound and leave HBM idle)
     int dev = 0, ncu = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     const int grid = std::max(n_conv + 8, ncu);
-    // The tail-only blocks stream for the whole conv phase, so they first take a head range of
-    // the update alone (MIHVD_TAIL_HEAD: its fraction of the update, tuned on MI355X).
+    // MIHVD_TAIL_STREAMERS: streamer waves per compute block (0 .. 4; 768 threads at most)
+    static const int sw = [] {
+      const char* e = getenv("MIHVD_TAIL_STREAMERS");
+      return e ? std::max(0, std::min(4, atoi(e))) : 4;
+    }();
+    const int nthr = debug_phase_exit() ? 512 : 512 + 64 * sw;  // profiling cuts: conv waves alone
+    // The free waves' head range (MIHVD_TAIL_HEAD: its fraction of the update), tuned on MI355X:
+    // with streamers they carry most of the update while the conv roles run.
     static const double head_frac = [] {
       const char* e = getenv("MIHVD_TAIL_HEAD");
-      return e ? atof(e) : 0.2;
-    }();
-    static const int kpl = [] {
-      const char* e = getenv("MIHVD_TAIL_KPL");  // 8 measured 0.7 us slower per launch
-      return (e && atoi(e) == 8) ? 8 : 4;
+      return e ? atof(e) : (sw > 0 ? 0.8 : 0.2);
     }();
     AdamTail at = *tail;
     at.first_free = n_conv;
-    at.kpl = kpl;
-    at.head = (int64_t)(head_frac * (double)((at.n4 + 64 * kpl - 1) / (64 * kpl)));
+    at.head = (int64_t)(head_frac * (double)((at.n4 + 63) / 64));
     TORCH_CHECK(cr.nblk == 0, "conv2_bwd_adam: no co-launched collective with the optimizer tail");
-    conv2_bwd_kernel<TAIL_ADAM><<<grid, 512, CB_LDS, stream>>>(
+    conv2_bwd_kernel<TAIL_ADAM><<<grid, nthr, nthr > 512 ? CB_LDS_SW : CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
         cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at, W3TileTail{}, cr);
@@ -747,7 +816,7 @@ void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tens
   TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_WORDS, "conv2_bwd_adam: state");
   AdamTail at{p3.data_ptr<float>(), g3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(),
               (u16*)shadow3.data_ptr(), n / 4, state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2,
-              (float)eps, (float)grad_scale, (int)rule, 0, 0, 4};
+              (float)eps, (float)grad_scale, (int)rule, 0, 0};
   conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, &at, -1);
 }
 

@@ -78,6 +78,13 @@ def main():
             tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
             tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
             sh, st, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0)),
+        "conv2_bwd_adam": lambda: o.conv2_bwd_adam(
+            tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf, None, st, tr.idx1, tr.slab,
+            tr.cpart, tr.params[W3:], tr.grads[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
+        "reduce_adam": lambda: o.conv2_wgrad_reduce_adam(
+            tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
+            tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
+            sh, st, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
         "fc1_bwd[roles=2]": lambda: o.fc1_bwd(tr.dz, tr.a2, tr.h, tr.dlog, tr.pview("dense/kernel", sh),
                                               tr.gview("dense/kernel"), tr.gview("dense/bias"),
                                               tr.gview("dense_1/kernel"), tr.gview("dense_1/bias"), tr.g2, 2, -1,
@@ -109,16 +116,23 @@ def main():
         "adam_w3": lambda: o.adam_step(tr.params[W3:], tr.grads[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], st, 0, 0.0,
                                        0.9, 0.999, 1e-8, 1.0, 0, 0),
         "adam": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, sh, st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
+        # the same update on a capped grid (grid-stride loop): how the streaming rate depends on the
+        # number of resident waves (the optimizer tail of conv2_bwd has one block per CU)
+        **{f"adam_w3[blocks={nb}]": (lambda nb=nb: o.adam_step(tr.params[W3:], tr.grads[W3:], tr.m[W3:], tr.v[W3:],
+                                                               sh[W3:], st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0, 0,
+                                                               None, nb)) for nb in (256, 512, 1024)},
         "adam_small": lambda: o.adam_step(tr.params[:W3], tr.grads[:W3], tr.m[:W3], tr.v[:W3], sh[:W3], st, 0, 0.0,
                                           0.9, 0.999, 1e-8, 1.0, 0),
     }
     jobs = [(name, fn, None) for name, fn in ops.items()]
     if args.roles:  # MIHVD_ROLE_ONLY is read by the host wrappers at launch (i.e. capture) time
-        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv2_bwd_adam+reduce_adam", 3),
+        for name, n_roles in (("fc1_wgrad", 2), ("conv2_bwd", 2), ("conv2_bwd_adam+reduce_adam", 3), ("conv2_bwd_adam", 3),
                               ("conv2_bwd_w3adam+reduce_adam", 3)):
             jobs += [(f"{name}[role{r}]", ops[name], r) for r in range(n_roles)]
-    if args.phases:  # MIHVD_DEBUG_EXIT: conv2_bwd dgrad role cut after phase p (1 staging, 2 GEMM, 3 epilogue)
-        jobs += [(f"conv2_bwd[role0,exit{p}]", ops["conv2_bwd"], (0, p)) for p in (1, 2, 3)]
+    if args.phases:  # MIHVD_DEBUG_EXIT: conv2_bwd dgrad role cut after phase p (1 staging, 2 GEMM, 3 epilogue,
+        # then conv1's weight gradient: 7 first barrier, 8 dY1 scatter stores, 4 + bias folds and barrier,
+        # 5 bias sums + shifted images, 6 GEMM)
+        jobs += [(f"conv2_bwd[role0,exit{p}]", ops["conv2_bwd"], (0, p)) for p in (1, 2, 3, 7, 8, 4, 5, 6)]
     if args.only:
         keep = set(args.only.split(";"))
         jobs = [j for j in jobs if j[0] in keep]
