@@ -156,11 +156,16 @@ __device__ __forceinline__ AdamCoef adam_coef(float t, float lr, float b1, float
   c.gscale = gscale;
   return c;
 }
+// The step uses the hardware square root and reciprocal (v_sqrt_f32 / v_rcp_f32, 1 ulp) instead of
+// the IEEE-rounded sqrtf and division: those expand to ~25 VALU instructions per element (scale,
+// div_fmas, fixup, class checks), which made the update VALU-bound wherever it shares CUs with
+// compute. The difference is a few ulp of the step (lr-scaled), far below the bf16 shadow's
+// resolution; every optimizer kernel runs this same code, so all schedules agree bit for bit.
 __device__ __forceinline__ void adam1(float& p, float& m, float& v, const float g, const AdamCoef& c) {
   const float gk = g * c.gscale;
   m = fmaf(c.b1, m, (1.f - c.b1) * gk);
   v = fmaf(c.b2, v, (1.f - c.b2) * gk * gk);
-  p -= c.lr_t * m / (sqrtf(v) * c.inv_sqrt_bc2 + c.eps_t);
+  p -= c.lr_t * m * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(v), c.inv_sqrt_bc2, c.eps_t));
 }
 __device__ __forceinline__ uint2 adam4(float4& pp, float4& mm, float4& vv, const float4 gg, const AdamCoef& c) {
   float* pa = &pp.x;

@@ -908,7 +908,8 @@ void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, in
   ra.o_b2 = off(gb2, 64, "conv2_wgrad_reduce_adam: gb2");
   ra.fc_lo4 = fc_lo / 4;
   ra.fc_hi4 = w3_lo / 4;
-  const int n_fc = (int)std::max<int64_t>(1, std::min<int64_t>(64, (ra.fc_hi4 - ra.fc_lo4 + 255) / 256));
+  // the fc range may include part of dense/kernel (the trainer's split): up to 4 blocks per CU
+  const int n_fc = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (ra.fc_hi4 - ra.fc_lo4 + 255) / 256));
   auto stream = c10::hip::getCurrentHIPStream().stream();
   conv2_wgrad_reduce_kernel<true><<<CR_SLAB_BLOCKS + CR_PART_BLOCKS + n_fc, 256, 0, stream>>>(
       slab.data_ptr<float>(), G, cpart.data_ptr<float>(), (int)B, gW2.data_ptr<float>(), gW1.data_ptr<float>(),

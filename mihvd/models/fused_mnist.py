@@ -258,6 +258,12 @@ class FusedMNISTTrainer:
         # Measured (B=100): 78.4 us/step vs 80.0 us with the flat adam_step launch.
         self.fused_opt = (os.environ.get("MIHVD_FUSED_OPT", "1") != "0" and not self.collectives
                           and not self.pipeline and not self.fuse_w3)
+        # Fused optimizer split of dense/kernel: the first MIHVD_REDUCE_W3 of its rows (a fraction,
+        # rounded to 256 elements) are updated by the gradient-reduction launch next to the conv
+        # reductions, the rest streams inside conv2_bwd. Default 0: moving 10-30 % to the reduce
+        # launch measured 0.4-1.8 us slower per step (the reduce grows more than conv2_bwd shrinks).
+        frac = min(max(float(os.environ.get("MIHVD_REDUCE_W3", "0")), 0.0), 1.0)
+        self.tail_split = W3_START + int(frac * (FLAT_NUMEL - W3_START)) // 256 * 256
         # MIHVD_W3_TAIL=1 (opt-in, with the fused optimizer): conv2_bwd's tail computes dW3 = a2^T dz tile by
         # tile on MFMA from the bf16 factors and applies Adam to dense/kernel from the accumulators
         # (csrc/kernels/w3_tail.h), so fc1_bwd only runs the dgrad tiles and the small reductions and
@@ -408,14 +414,17 @@ class FusedMNISTTrainer:
                                    self.dzT, self.a2T, self.params[w3], self.m[w3], self.v[w3], self.shadow[w3],
                                    self.grads[w3] if self.keep_w3_grad else None, self.lr, b1, b2, self.eps, 1.0,
                                    self.rule)
+                split = W3_START
             else:
+                split = self.tail_split
+                t3 = slice(split, FLAT_NUMEL)
                 o.conv2_bwd_adam(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
-                                 self.params[w3], self.grads[w3], self.m[w3], self.v[w3], self.shadow[w3], self.lr, b1,
+                                 self.params[t3], self.grads[t3], self.m[t3], self.v[t3], self.shadow[t3], self.lr, b1,
                                  b2, self.eps, 1.0, self.rule)
             o.conv2_wgrad_reduce_adam(self.slab, self.cpart, self.B, self.gview("conv_layer2/conv2d/kernel"),
                                       self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"),
                                       self.gview("conv_layer2/conv2d/bias"), self.grads, self.params, self.m, self.v,
-                                      self.shadow, st, FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
+                                      self.shadow, st, FC_START, split, self.lr, b1, b2, self.eps, 1.0, self.rule)
             return
         if self.fuse_w3:
             # W3 is updated in place by the dW3 tiles: its last reader (fc1_dgrad) goes first

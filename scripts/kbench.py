@@ -32,6 +32,7 @@ def main():
     o = tr.ops
     st = tr.state
     sh = tr.shadow
+    TS = tr.tail_split  # dense/kernel rows below it: updated in the reduce launch
     dz8 = tr.dz.repeat(8, 1).contiguous()
     a2T = torch.zeros(3136, 128, device="cuda", dtype=torch.bfloat16)
     dzT = torch.zeros(1024, 128, device="cuda", dtype=torch.bfloat16)
@@ -71,20 +72,21 @@ def main():
                                              tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
                                              tr.gview("dense_1/bias"), 1, dz8, a28),
         # the fused optimizer pair (the reduce re-arms the tail counter, so it is timed as a pair)
+        # the trainer's split of dense/kernel between the reduce launch and conv2_bwd's streamers
         "conv2_bwd_adam+reduce_adam": lambda: (o.conv2_bwd_adam(
             tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf, None, st, tr.idx1, tr.slab,
-            tr.cpart, tr.params[W3:], tr.grads[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
+            tr.cpart, tr.params[TS:], tr.grads[TS:], tr.m[TS:], tr.v[TS:], sh[TS:], 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
             o.conv2_wgrad_reduce_adam(
             tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
             tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
-            sh, st, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0)),
+            sh, st, FC, TS, 0.0, 0.9, 0.999, 1e-8, 1.0, 0)),
         "conv2_bwd_adam": lambda: o.conv2_bwd_adam(
             tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf, None, st, tr.idx1, tr.slab,
-            tr.cpart, tr.params[W3:], tr.grads[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
+            tr.cpart, tr.params[TS:], tr.grads[TS:], tr.m[TS:], tr.v[TS:], sh[TS:], 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
         "reduce_adam": lambda: o.conv2_wgrad_reduce_adam(
             tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
             tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
-            sh, st, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
+            sh, st, FC, TS, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
         "fc1_bwd[roles=2]": lambda: o.fc1_bwd(tr.dz, tr.a2, tr.h, tr.dlog, tr.pview("dense/kernel", sh),
                                               tr.gview("dense/kernel"), tr.gview("dense/bias"),
                                               tr.gview("dense_1/kernel"), tr.gview("dense_1/bias"), tr.g2, 2, -1,
