@@ -264,7 +264,7 @@ __device__ __forceinline__ void adam_tail_run(const AdamTail& at) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int waves = (int)blockDim.x >> 6;
   const int sw = waves - 8 > 0 ? waves - 8 : 0;  // streamer waves per compute block
-  const AdamCoef c = adam_coef((float)at.state[ST_OPT], at.lr, at.b1, at.b2, at.eps, at.gscale, at.rule);
+  const AdamCoef c = adam_coef((float)at.state[ST_OPT], at.lr, at.b1, at.b2, at.eps, at.gscale, at.rule & 0xff);
   const int64_t head4 = min(at.head * 64, at.n4);
   const int n_free = (int)gridDim.x - at.first_free;
   const int64_t nfw = (int64_t)at.first_free * sw + (int64_t)n_free * waves;

@@ -139,14 +139,21 @@ struct ConvBarrier {
   }
 };
 
+// Stores of the outputs that the reduction reads. WT (the folded reduction, below): write-through
+// (sc1) so that another XCD's reduction can read them after the arrival counter with no release.
+__device__ __forceinline__ void out_store1(float* p, float v, bool wt) {
+  if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 template <bool SWB>
 __device__ __forceinline__ void conv2_bwd_block(
     const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
     const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
     int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
-    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int bx, unsigned* bar_ctr) {
+    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int bx,
+    ConvBarrier<SWB>& bar, bool wt = false) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  ConvBarrier<SWB> bar{bar_ctr};
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
   if (bx < n_dgrad) {
@@ -350,14 +357,14 @@ __device__ __forceinline__ void conv2_bwd_block(
       const int co4 = t >> 2, c = t & 3;
       float sacc = 0.f;
       for (int w = 0; w < 8; ++w) sacc += red[(w * 16 + co4) * 4 + c];  // 8 per-wave folds
-      cpart[(int64_t)b * CP_W + CP_DB2 + co4 * 4 + c] = sacc;
+      out_store1(cpart + (int64_t)b * CP_W + CP_DB2 + co4 * 4 + c, sacc, wt);
     } else if (t < 96) {
       // db1 channel ch = 16nt + 4lg + i
       const int ch = t - 64, nt = ch >> 4, lgg = (ch >> 2) & 3, i = ch & 3;
       float sacc = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) sacc += red1[(w * 4 + lgg) * 8 + nt * 4 + i];
-      cpart[(int64_t)b * CP_W + CP_DB1 + ch] = sacc;
+      out_store1(cpart + (int64_t)b * CP_W + CP_DB1 + ch, sacc, wt);
     }
     if (dbg_exit == 5) return;  // profiling: ... after the bias sums
     // GEMM dW1^T[co][tap] = sum_pix dY1^T[co][pix] im2col(x)[pix][tap]: wave w takes image rows
@@ -405,7 +412,7 @@ __device__ __forceinline__ void conv2_bwd_block(
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) v += part[w * 64 * 16 + slot];
-      cpart[(int64_t)b * CP_W + o] = v;  // dW1 in HWIO order: tap * 32 + co
+      out_store1(cpart + (int64_t)b * CP_W + o, v, wt);  // dW1 in HWIO order: tap * 32 + co
     }
     return;
   }
@@ -515,99 +522,65 @@ __device__ __forceinline__ void conv2_bwd_block(
       v.y = acc[mt][1] + red[(mt * 4 + 1) * 256 + th];
       v.z = acc[mt][2] + red[(mt * 4 + 2) * 256 + th];
       v.w = acc[mt][3] + red[(mt * 4 + 3) * 256 + th];
-      *reinterpret_cast<float4*>(out + ((kh * 5 + kw) * 32 + ci) * 64 + co) = v;
+      const int oo = ((kh * 5 + kw) * 32 + ci) * 64 + co;
+      if (wt) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 51200 * 4, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(f4v{v.x, v.y, v.z, v.w}, rs, oo * 4, 0, 16);  // sc1
+      } else {
+        *reinterpret_cast<float4*>(out + oo) = v;
+      }
     }
   }
 }
 
-// TAIL: the launch also carries the dense/kernel Adam update — 1: from the dW3 gradient in HBM
-// (AdamTail, common.h), 2: from dW3 tiles computed here from the bf16 factors (W3TileTail,
-// w3_tail.h). Blocks [n_conv, grid) have no conv work and start on it at once (they sit on the CUs
-// the conv roles leave idle); every conv block joins in when its own work is done.
-enum { TAIL_NONE = 0, TAIL_ADAM = 1, TAIL_W3 = 2 };
-// TAIL_ADAM launches may add SW streamer waves (waves 8 .. 8 + SW - 1) to every block: they stream
-// the update from the first cycle on the CUs the conv roles occupy (latency-bound work that leaves
-// HBM idle), while the conv waves meet on the LDS counter barrier above.
-constexpr int CB_MAX_THREADS = 768;
-constexpr int CB_LDS_SW = CB_LDS + 16;  // + the conv waves' barrier counter
-template <int TAIL>
-__global__ void __launch_bounds__(TAIL == TAIL_ADAM ? CB_MAX_THREADS : 512) conv2_bwd_kernel(
-    const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
-    const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
-    int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
-    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int n_conv, AdamTail at,
-    W3TileTail wt, CollRole cr) {
-  // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk blocks (the CUs the 225 conv
-  // blocks of a B = 100 step leave idle)
-  if ((int)blockIdx.x < cr.nblk) {
-    coll_role_run(cr, blockIdx.x);
-    return;
+// Loads of the conv roles' outputs by the reduction. SC1: the folded form (the reduction runs in
+// the conv2_bwd launch after an arrival counter, cdna_hip_programming.md §6 Guideline 16): the
+// producers stored them write-through (sc1), so every load of them here is an sc1 load too and no
+// acquire is needed; otherwise plain loads behind the kernel boundary.
+template <bool SC1>
+struct ReduceLoads {
+  __amdgpu_buffer_rsrc_t rs;
+  const float* slab;
+  const float* cpart;
+  __device__ __forceinline__ ReduceLoads(const float* slab_, int nslab, const float* cpart_) : slab(slab_), cpart(cpart_) {
+    if constexpr (SC1) rs = __builtin_amdgcn_make_buffer_rsrc((void*)slab_, (short)0, nslab * 51200 * 4, 0x00020000);
   }
-  const int bx = (int)blockIdx.x - cr.nblk;
-  if (TAIL == TAIL_ADAM && blockDim.x > 512) {
-    extern __shared__ __attribute__((aligned(16))) u16 smem[];
-    unsigned* ctr = reinterpret_cast<unsigned*>(smem + CB_LDS / 2);
-    if (threadIdx.x == 0) *ctr = 0u;
-    __syncthreads();  // the only block-wide barrier: every later one is the conv waves' own
-    if (bx < n_conv && threadIdx.x < 512)
-      conv2_bwd_block<true>(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit,
-                            bx, ctr);
-  } else if (bx < n_conv) {
-    conv2_bwd_block<false>(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit, bx,
-                           nullptr);
+  __device__ __forceinline__ float4 slab4(int g, int o) const {  // float4 o of slab g
+    if constexpr (SC1) {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (g * 12800 + o) * 16, 0, 16);
+      return make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      return reinterpret_cast<const float4*>(slab + (int64_t)g * 51200)[o];
+    }
   }
-  if constexpr (TAIL == TAIL_ADAM) adam_tail_run(at);
-  if constexpr (TAIL == TAIL_W3) w3_tail_run(wt);  // independent waves, no LDS
-}
+  __device__ __forceinline__ float part(int64_t i) const {
+    if constexpr (SC1) return __hip_atomic_load(cpart + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return cpart[i];
+  }
+};
 
-// Blocks [0, 200): dW2 = sum of the (<= 32) conv2 wgrad slabs; 64 float4 outputs x 4 slab groups of
-// 8 per block, every load in flight at once (absent slabs masked, not branched around), then a
-// 4-way LDS sum. Blocks [200, 214): dW1 | db1 | db2 = sum over images of the per-image partial rows;
-// 64 outputs x 4 row groups per block, 8 rows per load batch.
-//
-// ADAM (world size 1): the same launch is the optimizer for every parameter except dense/kernel
-// (whose update rode on conv2_bwd's tail): each reduced conv gradient is applied to its slot of the
-// flat p/m/v/shadow buffers right away, blocks [214, 214 + n_fc) update the fc slice
-// [fc_lo4, fc_hi4) (float4 indices: dense/bias, dense_1/*) from the gradient buffer, and block 0
-// advances the forward step — the step's last launch.
-constexpr int CR_SLAB_BLOCKS = 200, CR_PART_BLOCKS = CP_W / 64;
+// One 256-thread reduction item. Items [0, 200): dW2 = sum of the (<= 32) conv2 wgrad slabs; 64
+// float4 outputs x 4 slab groups of 8 per item, every load in flight at once (absent slabs masked,
+// not branched around), then a 4-way LDS sum. Items [200, 214): dW1 | db1 | db2 = sum over images
+// of the per-image partial rows; 64 outputs x 4 row groups per item, 8 rows per load batch. With
+// ADAM each reduced gradient is applied to its slot of the flat p/m/v/shadow buffers right away.
+constexpr int CR_SLAB_BLOCKS = 200, CR_PART_BLOCKS = CP_W / 64, CR_ITEMS = CR_SLAB_BLOCKS + CR_PART_BLOCKS;
 struct ReduceAdam {
   AdamArgs ad;             // p/m/v/shadow = flat buffer bases; state = the step state (read + written)
   const float* gflat;      // flat gradient buffer
   int64_t o_w2, o_w1, o_b1, o_b2;  // element offsets of the conv segments in the flat buffers
   int64_t fc_lo4, fc_hi4;  // float4 range of the fc segments updated from gflat
 };
-template <bool ADAM>
-__global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab,
-                                                                 const float* __restrict__ cpart, int B,
-                                                                 float* __restrict__ gW2, float* __restrict__ gW1,
-                                                                 float* __restrict__ gb1, float* __restrict__ gb2,
-                                                                 ReduceAdam ra) {
-  __shared__ float4 r4[256];
-  const int t = threadIdx.x;
-  AdamCoef c;
-  if constexpr (ADAM) {
-    c = adam_coef((float)ra.ad.state[ST_OPT], ra.ad.lr, ra.ad.b1, ra.ad.b2, ra.ad.eps, ra.ad.gscale, ra.ad.rule);
-    if (blockIdx.x == 0 && t == 0) const_cast<int64_t*>(ra.ad.state)[ST_FWD] += 1;
-    if ((int)blockIdx.x >= CR_SLAB_BLOCKS + CR_PART_BLOCKS) {
-      for (int64_t i = ra.fc_lo4 + ((int64_t)blockIdx.x - CR_SLAB_BLOCKS - CR_PART_BLOCKS) * 256 + t; i < ra.fc_hi4;
-           i += (int64_t)(gridDim.x - CR_SLAB_BLOCKS - CR_PART_BLOCKS) * 256) {
-        float4 pp = reinterpret_cast<const float4*>(ra.ad.p)[i];
-        const float4 gg = reinterpret_cast<const float4*>(ra.gflat)[i];
-        float4 mm = reinterpret_cast<const float4*>(ra.ad.m)[i];
-        float4 vv = reinterpret_cast<const float4*>(ra.ad.v)[i];
-        const uint2 sh = adam4(pp, mm, vv, gg, c);
-        reinterpret_cast<float4*>(ra.ad.p)[i] = pp;
-        reinterpret_cast<float4*>(ra.ad.m)[i] = mm;
-        reinterpret_cast<float4*>(ra.ad.v)[i] = vv;
-        reinterpret_cast<uint2*>(ra.ad.shadow)[i] = sh;
-      }
-      return;
-    }
-  }
-  if ((int)blockIdx.x >= CR_SLAB_BLOCKS) {
+template <bool ADAM, bool SC1, class Sync>
+__device__ __forceinline__ void reduce_item(int item, int t, float4* r4, Sync&& sync, const ReduceLoads<SC1>& ld,
+                                            int nslab, int B, float* __restrict__ gW2, float* __restrict__ gW1,
+                                            float* __restrict__ gb1, float* __restrict__ gb2, const ReduceAdam& ra,
+                                            const AdamCoef& c) {
+  if (item >= CR_SLAB_BLOCKS) {
     float* r1 = reinterpret_cast<float*>(r4);
-    const int o = ((int)blockIdx.x - CR_SLAB_BLOCKS) * 64 + (t & 63), rg = t >> 6;
+    const int o = (item - CR_SLAB_BLOCKS) * 64 + (t & 63), rg = t >> 6;
     // optimizer operands first: their loads fly with the reduction's instead of after it
     int64_t f = 0;
     float pv = 0.f, mv = 0.f, vv = 0.f;
@@ -625,13 +598,13 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int r = r0 + k;
-        v[k] = mask_f(cpart[(int64_t)min(r, B - 1) * CP_W + o], r < B);
+        v[k] = mask_f(ld.part((int64_t)min(r, B - 1) * CP_W + o), r < B);
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc += v[k];
     }
     r1[t] = acc;
-    __syncthreads();
+    sync();
     if (t < 64) {
       const float s = (r1[t] + r1[64 + t]) + (r1[128 + t] + r1[192 + t]);
       if (o < CP_DB1) gW1[o] = s;
@@ -647,7 +620,7 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
     }
     return;
   }
-  const int o = (int)blockIdx.x * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
+  const int o = item * 64 + (t & 63), sg = t >> 6;  // float4 index, 12800 total
   float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
   if constexpr (ADAM) {
     if (t < 64) {  // optimizer operands in flight with the slab loads
@@ -661,7 +634,7 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int g = sg * 8 + k;
-    const float4 xv = reinterpret_cast<const float4*>(slab + (int64_t)min(g, nslab - 1) * 51200)[min(o, 12799)];
+    const float4 xv = ld.slab4(min(g, nslab - 1), min(o, 12799));
     const bool keep = g < nslab;
     v[k] = make_float4(mask_f(xv.x, keep), mask_f(xv.y, keep), mask_f(xv.z, keep), mask_f(xv.w, keep));
   }
@@ -669,7 +642,7 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
   r4[t] = s;
-  __syncthreads();
+  sync();
   if (t < 64 && o < 12800) {
     const float4 a = r4[t], b = r4[64 + t], cc = r4[128 + t], d = r4[192 + t];
     const float4 g = make_float4((a.x + b.x) + (cc.x + d.x), (a.y + b.y) + (cc.y + d.y), (a.z + b.z) + (cc.z + d.z),
@@ -686,14 +659,182 @@ __global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __
   }
 }
 
+// Adam over the fc float4 range [fc_lo4, fc_hi4) from the gradient buffer (no conv dependency).
+__device__ __forceinline__ void reduce_fc_adam(const ReduceAdam& ra, const AdamCoef& c, int64_t i, int64_t stride) {
+  for (; i < ra.fc_hi4; i += stride) {
+    float4 pp = reinterpret_cast<const float4*>(ra.ad.p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(ra.gflat)[i];
+    float4 mm = reinterpret_cast<const float4*>(ra.ad.m)[i];
+    float4 vv = reinterpret_cast<const float4*>(ra.ad.v)[i];
+    const uint2 sh = adam4(pp, mm, vv, gg, c);
+    reinterpret_cast<float4*>(ra.ad.p)[i] = pp;
+    reinterpret_cast<float4*>(ra.ad.m)[i] = mm;
+    reinterpret_cast<float4*>(ra.ad.v)[i] = vv;
+    reinterpret_cast<uint2*>(ra.ad.shadow)[i] = sh;
+  }
+}
+
+// TAIL: the launch also carries the dense/kernel Adam update — 1: from the dW3 gradient in HBM
+// (AdamTail, common.h), 2: from dW3 tiles computed here from the bf16 factors (W3TileTail,
+// w3_tail.h). Blocks [n_conv, grid) have no conv work and start on it at once (they sit on the CUs
+// the conv roles leave idle); every conv block joins in when its own work is done.
+enum { TAIL_NONE = 0, TAIL_ADAM = 1, TAIL_W3 = 2 };
+// TAIL_ADAM launches may add SW streamer waves (waves 8 .. 8 + SW - 1) to every block: they stream
+// the update from the first cycle on the CUs the conv roles occupy (latency-bound work that leaves
+// HBM idle), while the conv waves meet on the LDS counter barrier above.
+constexpr int CB_MAX_THREADS = 768;
+constexpr int CB_LDS_SW = CB_LDS + 16;  // + the conv waves' barrier counter
+// Folded reduction (FoldArgs, TAIL_ADAM launches with streamers): the conv2_wgrad_reduce_adam
+// work runs in this launch. Every conv block stores its slab rows / partial rows write-through,
+// drains them, adds 1 to an arrival counter and waits (one wave polls, bounded) for all n_conv;
+// then its conv waves take reduction items (two per pass, one per 256-thread half) while the
+// streamers keep streaming. The last block to pass the wait resets the counters for the next call.
+struct FoldArgs {
+  ReduceAdam ra;
+  float *gW2, *gW1, *gb1, *gb2;
+  unsigned* sync;  // [arrive, depart, error, -]: zero-initialised, reset in-kernel every call
+  int nslab;
+  int on;
+};
+
+// Arrival: every storing wave drains its write-through stores, then one lane counts the block in.
+__device__ __forceinline__ void conv2_fold_arrive(const FoldArgs& fa, ConvBarrier<true>& bar) {
+  if ((fa.on >> 1) == 3) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores have landed
+  bar.sync();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)fa.sync, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void conv2_fold_reduce(const FoldArgs& fa, ConvBarrier<true>& bar, int bx, int n_conv,
+                                                  const float* slab, const float* cpart, int B) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  typedef __attribute__((address_space(1))) unsigned gu32;
+  gu32* arrive = (gu32*)fa.sync;
+  gu32* depart = arrive + 1;
+  gu32* err = arrive + 2;
+  const int t = threadIdx.x, wave = t >> 6;
+  const int dbg = fa.on >> 1;  // profiling (MIHVD_FOLD_DEBUG): 1 no items, 2 no wait, 3 stores only
+  if (dbg == 3) return;
+  if (wave == 0 && dbg != 2) {
+    // every conv block is resident (grid <= CUs, checked at launch); bounded: ~0.1 s, then an error
+    int spin = 0;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)n_conv) {
+      if (++spin > (1 << 21)) {
+        if ((t & 63) == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(16);  // ~1k cycles: up to 225 pollers share one word
+    }
+  }
+  bar.sync();
+  // every load of the handed-off slabs / partial rows below is an sc1 load: no acquire needed, only
+  // keep the compiler from hoisting them above the poll
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (t == 0) {  // the whole block has passed the wait: the last one to get here resets both words
+    if (__hip_atomic_fetch_add(depart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)n_conv - 1) {
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(depart, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  const ReduceAdam& ra = fa.ra;
+  const AdamCoef c = adam_coef((float)ra.ad.state[ST_OPT], ra.ad.lr, ra.ad.b1, ra.ad.b2, ra.ad.eps, ra.ad.gscale,
+                               ra.ad.rule);
+  if (bx == 0 && t == 0) const_cast<int64_t*>(ra.ad.state)[ST_FWD] += 1;  // every conv block has read it
+  if (dbg == 1) return;
+  const int half = t >> 8, th = t & 255;
+  float4* r4 = reinterpret_cast<float4*>(smem) + half * 256;
+  const ReduceLoads<true> ld(slab, fa.nslab, cpart);
+  // items go to the wgrad blocks first (they finish their conv work before the dgrad blocks)
+  const int n_dg = n_conv - fa.nslab * 5;
+  const int rank = bx >= n_dg ? bx - n_dg : (n_conv - n_dg) + bx;
+  for (int base = 2 * rank; base < CR_ITEMS; base += 2 * n_conv) {
+    const int item = base + half;
+    if (item < CR_ITEMS)
+      reduce_item<true, true>(item, th, r4, [&] { bar.sync(); }, ld, fa.nslab, B, fa.gW2, fa.gW1, fa.gb1, fa.gb2, ra, c);
+    else
+      bar.sync();  // the other half's item: same barrier count
+  }
+  reduce_fc_adam(ra, c, ra.fc_lo4 + (int64_t)bx * 512 + t, (int64_t)n_conv * 512);
+}
+
+template <int TAIL>
+__global__ void __launch_bounds__(TAIL == TAIL_ADAM ? CB_MAX_THREADS : 512) conv2_bwd_kernel(
+    const u16* __restrict__ g2, const uint8_t* __restrict__ idx2,
+    const u16* __restrict__ a1, const u16* __restrict__ w2bf, const float* __restrict__ x, const int* __restrict__ rows,
+    int n_pool, const int64_t* __restrict__ state, const uint8_t* __restrict__ idx1, u16* __restrict__ g1,
+    float* __restrict__ slab, float* __restrict__ cpart, int B, int n_dgrad, int dbg_exit, int n_conv, AdamTail at,
+    W3TileTail wt, CollRole cr, FoldArgs fa) {
+  // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk blocks (the CUs the 225 conv
+  // blocks of a B = 100 step leave idle)
+  if ((int)blockIdx.x < cr.nblk) {
+    coll_role_run(cr, blockIdx.x);
+    return;
+  }
+  const int bx = (int)blockIdx.x - cr.nblk;
+  if (TAIL == TAIL_ADAM && blockDim.x > 512) {
+    extern __shared__ __attribute__((aligned(16))) u16 smem[];
+    unsigned* ctr = reinterpret_cast<unsigned*>(smem + CB_LDS / 2);
+    if (threadIdx.x == 0) *ctr = 0u;
+    __syncthreads();  // the only block-wide barrier: every later one is the conv waves' own
+    if (bx < n_conv && threadIdx.x < 512) {
+      ConvBarrier<true> bar{ctr};
+      conv2_bwd_block<true>(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit,
+                            bx, bar, fa.on != 0);
+      if constexpr (TAIL == TAIL_ADAM) {
+        if (fa.on) {
+          // count in, take this wave's share of the update while the other blocks finish, then reduce
+          conv2_fold_arrive(fa, bar);
+          adam_tail_run(at);
+          conv2_fold_reduce(fa, bar, bx, n_conv, slab, cpart, B);
+          return;
+        }
+      }
+    }
+  } else if (bx < n_conv) {
+    ConvBarrier<false> bar{nullptr};
+    conv2_bwd_block<false>(g2, idx2, a1, w2bf, x, rows, n_pool, state, idx1, g1, slab, cpart, B, n_dgrad, dbg_exit, bx,
+                           bar);
+  }
+  if constexpr (TAIL == TAIL_ADAM) adam_tail_run(at);
+  if constexpr (TAIL == TAIL_W3) w3_tail_run(wt);  // independent waves, no LDS
+}
+
+// Blocks [0, 214): one reduction item each; ADAM (world size 1): blocks [214, 214 + n_fc) update the
+// fc slice, and block 0 advances the forward step — the step's last launch.
+template <bool ADAM>
+__global__ void __launch_bounds__(256) conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nslab,
+                                                                 const float* __restrict__ cpart, int B,
+                                                                 float* __restrict__ gW2, float* __restrict__ gW1,
+                                                                 float* __restrict__ gb1, float* __restrict__ gb2,
+                                                                 ReduceAdam ra) {
+  __shared__ float4 r4[256];
+  const int t = threadIdx.x;
+  AdamCoef c;
+  if constexpr (ADAM) {
+    c = adam_coef((float)ra.ad.state[ST_OPT], ra.ad.lr, ra.ad.b1, ra.ad.b2, ra.ad.eps, ra.ad.gscale, ra.ad.rule);
+    if (blockIdx.x == 0 && t == 0) const_cast<int64_t*>(ra.ad.state)[ST_FWD] += 1;
+    if ((int)blockIdx.x >= CR_ITEMS) {
+      reduce_fc_adam(ra, c, ra.fc_lo4 + ((int64_t)blockIdx.x - CR_ITEMS) * 256 + t,
+                     (int64_t)(gridDim.x - CR_ITEMS) * 256);
+      return;
+    }
+  }
+  const ReduceLoads<false> ld(slab, nslab, cpart);
+  reduce_item<ADAM, false>((int)blockIdx.x, t, r4, [] { __syncthreads(); }, ld, nslab, B, gW2, gW1, gb1, gb2, ra, c);
+}
+
 // ------------------------------------------------------------------------------------------ //
 int64_t conv2_wgrad_groups(int64_t B) { return (B + CB_IPB - 1) / CB_IPB; }
+static int64_t B_of(const at::Tensor& a1) { return a1.size(0); }
 
 static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                              const at::Tensor& x, const c10::optional<at::Tensor>& rows,
                              const c10::optional<at::Tensor>& state, const at::Tensor& idx1, at::Tensor& slab,
                              at::Tensor& cpart, const c10::optional<at::Tensor>& g1, const AdamTail* tail,
-                             int64_t coll, const W3TileTail* w3t = nullptr) {
+                             int64_t coll, const W3TileTail* w3t = nullptr, const FoldArgs* fold = nullptr,
+                             bool* fold_done = nullptr) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
@@ -751,12 +892,12 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     conv2_bwd_kernel<TAIL_W3><<<grid, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, wtl, cr);
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, wtl, cr, FoldArgs{});
   } else if (tail == nullptr) {
     conv2_bwd_kernel<TAIL_NONE><<<cr.nblk + n_conv, 512, CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, W3TileTail{}, cr);
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, AdamTail{}, W3TileTail{}, cr, FoldArgs{});
   } else {
     // one block per CU (the conv roles' LDS): the extra tail-only blocks take the CUs the conv
     // roles leave free, and every conv block carries streamer waves, so the update streams from
@@ -781,10 +922,20 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     at.first_free = n_conv;
     at.head = (int64_t)(head_frac * (double)((at.n4 + 63) / 64));
     TORCH_CHECK(cr.nblk == 0, "conv2_bwd_adam: no co-launched collective with the optimizer tail");
+    // The folded reduction needs every conv block resident at once (they wait for each other) and
+    // the streamer form (its barrier); otherwise the caller's separate reduce launch runs.
+    FoldArgs fa = fold ? *fold : FoldArgs{};
+    fa.on = fold != nullptr && nthr > 512 && role == -1 && n_conv <= grid && grid <= ncu;
+    if (fold) *fold_done = fa.on != 0;
+    static const int fold_dbg = [] {
+      const char* e = getenv("MIHVD_FOLD_DEBUG");
+      return e ? atoi(e) : 0;
+    }();
+    if (fa.on) fa.on |= fold_dbg << 1;
     conv2_bwd_kernel<TAIL_ADAM><<<grid, nthr, nthr > 512 ? CB_LDS_SW : CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),
-        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at, W3TileTail{}, cr);
+        cpart.data_ptr<float>(), B, n_dgrad, debug_phase_exit(), n_conv, at, W3TileTail{}, cr, fa);
   }
 }
 
@@ -872,11 +1023,11 @@ void conv2_wgrad_reduce(const at::Tensor& slab, const at::Tensor& cpart, int64_t
 // gradients straight from the reduction, [fc_lo, w3_lo) from the gradient buffer. gW2/gW1/gb1/gb2
 // must be views of `grads` (their offsets locate the parameters). Advances state[ST_FWD]: the
 // last launch of a world-size-1 step.
-void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2,
-                             at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads, at::Tensor& p,
-                             at::Tensor& m, at::Tensor& v, at::Tensor& shadow, at::Tensor& state, int64_t fc_lo,
-                             int64_t w3_lo, double lr, double b1, double b2, double eps, double grad_scale,
-                             int64_t rule) {
+static ReduceAdam make_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2,
+                                   at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads,
+                                   at::Tensor& p, at::Tensor& m, at::Tensor& v, at::Tensor& shadow, at::Tensor& state,
+                                   int64_t fc_lo, int64_t w3_lo, double lr, double b1, double b2, double eps,
+                                   double grad_scale, int64_t rule) {
   const int G = (int)conv2_wgrad_groups(B);
   TORCH_CHECK(G >= 1 && G <= 32, "conv2_wgrad_reduce_adam: at most 32 wgrad slabs");
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_wgrad_reduce_adam: slab");
@@ -908,12 +1059,53 @@ void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, in
   ra.o_b2 = off(gb2, 64, "conv2_wgrad_reduce_adam: gb2");
   ra.fc_lo4 = fc_lo / 4;
   ra.fc_hi4 = w3_lo / 4;
+  return ra;
+}
+
+static void launch_reduce_adam(const ReduceAdam& ra, const at::Tensor& slab, const at::Tensor& cpart, int64_t B,
+                               at::Tensor& gW2, at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2) {
+  const int G = (int)conv2_wgrad_groups(B);
   // the fc range may include part of dense/kernel (the trainer's split): up to 4 blocks per CU
   const int n_fc = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (ra.fc_hi4 - ra.fc_lo4 + 255) / 256));
   auto stream = c10::hip::getCurrentHIPStream().stream();
   conv2_wgrad_reduce_kernel<true><<<CR_SLAB_BLOCKS + CR_PART_BLOCKS + n_fc, 256, 0, stream>>>(
       slab.data_ptr<float>(), G, cpart.data_ptr<float>(), (int)B, gW2.data_ptr<float>(), gW1.data_ptr<float>(),
       gb1.data_ptr<float>(), gb2.data_ptr<float>(), ra);
+}
+
+void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, int64_t B, at::Tensor& gW2,
+                             at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads, at::Tensor& p,
+                             at::Tensor& m, at::Tensor& v, at::Tensor& shadow, at::Tensor& state, int64_t fc_lo,
+                             int64_t w3_lo, double lr, double b1, double b2, double eps, double grad_scale,
+                             int64_t rule) {
+  const ReduceAdam ra = make_reduce_adam(slab, cpart, B, gW2, gW1, gb1, gb2, grads, p, m, v, shadow, state, fc_lo, w3_lo,
+                                         lr, b1, b2, eps, grad_scale, rule);
+  launch_reduce_adam(ra, slab, cpart, B, gW2, gW1, gb1, gb2);
+}
+
+// conv2_bwd_adam + conv2_wgrad_reduce_adam as ONE launch when the folded reduction applies
+// (FoldArgs: streamer form, every conv block resident); otherwise the same two launches. The
+// dense/kernel update covers [w3_lo, end) of the flat buffers; sync: int32 [4] zeros, owned by the
+// caller (reset in-kernel after every call; word 2 = 1 after a timed-out wait).
+void conv2_bwd_adam_fold(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+                         const at::Tensor& x, const c10::optional<at::Tensor>& rows, at::Tensor& state,
+                         const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, at::Tensor& gW2, at::Tensor& gW1,
+                         at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads, at::Tensor& p, at::Tensor& m,
+                         at::Tensor& v, at::Tensor& shadow, at::Tensor& sync, int64_t fc_lo, int64_t w3_lo, double lr,
+                         double b1, double b2, double eps, double grad_scale, int64_t rule) {
+  const ReduceAdam ra = make_reduce_adam(slab, cpart, B_of(a1), gW2, gW1, gb1, gb2, grads, p, m, v, shadow, state, fc_lo,
+                                         w3_lo, lr, b1, b2, eps, grad_scale, rule);
+  const int64_t n = grads.numel();
+  TORCH_CHECK(n - w3_lo > 0 && (n - w3_lo) % 4 == 0, "conv2_bwd_adam_fold: dense/kernel slice");
+  TORCH_CHECK(sync.scalar_type() == at::kInt && sync.numel() >= 4 && sync.is_contiguous(), "conv2_bwd_adam_fold: sync");
+  AdamTail at{p.data_ptr<float>() + w3_lo, grads.data_ptr<float>() + w3_lo, m.data_ptr<float>() + w3_lo,
+              v.data_ptr<float>() + w3_lo, (u16*)shadow.data_ptr() + w3_lo, (n - w3_lo) / 4, state.data_ptr<int64_t>(),
+              (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale, (int)rule, 0, 0};
+  FoldArgs fa{ra, gW2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(), gb2.data_ptr<float>(),
+              (unsigned*)sync.data_ptr<int>(), (int)conv2_wgrad_groups(B_of(a1)), 1};
+  bool done = false;
+  conv2_bwd_launch(g2, idx2, a1, w2bf, x, rows, state, idx1, slab, cpart, c10::nullopt, &at, -1, nullptr, &fa, &done);
+  if (!done) launch_reduce_adam(ra, slab, cpart, B_of(a1), gW2, gW1, gb1, gb2);
 }
 
 }  // namespace mihvd

@@ -53,6 +53,12 @@ void conv2_wgrad_reduce_adam(const at::Tensor& slab, const at::Tensor& cpart, in
                              at::Tensor& m, at::Tensor& v, at::Tensor& shadow, at::Tensor& state, int64_t fc_lo,
                              int64_t w3_lo, double lr, double b1, double b2, double eps, double grad_scale,
                              int64_t rule);
+void conv2_bwd_adam_fold(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+                         const at::Tensor& x, const c10::optional<at::Tensor>& rows, at::Tensor& state,
+                         const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, at::Tensor& gW2, at::Tensor& gW1,
+                         at::Tensor& gb1, at::Tensor& gb2, const at::Tensor& grads, at::Tensor& p, at::Tensor& m,
+                         at::Tensor& v, at::Tensor& shadow, at::Tensor& sync, int64_t fc_lo, int64_t w3_lo, double lr,
+                         double b1, double b2, double eps, double grad_scale, int64_t rule);
 void adam_step(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v, const c10::optional<at::Tensor>& shadow,
                const c10::optional<at::Tensor>& state, int64_t host_step, double lr, double b1, double b2, double eps,
                double grad_scale, int64_t rule, int64_t bump, const c10::optional<at::Tensor>& loss_scale,
@@ -149,6 +155,14 @@ void conv2_wgrad_reduce_adam_op(const Tensor& slab, const Tensor& cpart, int64_t
   mihvd::conv2_wgrad_reduce_adam(slab, cpart, B, gW2, gW1, gb1, gb2, grads, p, m, v, shadow, state, fc_lo, w3_lo, lr,
                                  b1, b2, eps, grad_scale, rule);
 }
+void conv2_bwd_adam_fold_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, const Tensor& x,
+                            const OptT& rows, Tensor state, const Tensor& idx1, Tensor slab, Tensor cpart, Tensor gW2,
+                            Tensor gW1, Tensor gb1, Tensor gb2, const Tensor& grads, Tensor p, Tensor m, Tensor v,
+                            Tensor shadow, Tensor sync, int64_t fc_lo, int64_t w3_lo, double lr, double b1, double b2,
+                            double eps, double grad_scale, int64_t rule) {
+  mihvd::conv2_bwd_adam_fold(g2, idx2, a1, w2, x, rows, state, idx1, slab, cpart, gW2, gW1, gb1, gb2, grads, p, m, v,
+                             shadow, sync, fc_lo, w3_lo, lr, b1, b2, eps, grad_scale, rule);
+}
 void adam_op(Tensor p, const Tensor& g, Tensor m, Tensor v, const OptT& shadow, const OptT& state, int64_t host_step,
              double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, int64_t bump,
              const OptT& loss_scale, int64_t max_blocks) {
@@ -218,6 +232,11 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("conv2_wgrad_reduce_adam(Tensor slab, Tensor cpart, int B, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
         "Tensor(d!) gb2, Tensor grads, Tensor(e!) p, Tensor(f!) m, Tensor(g!) v, Tensor(h!) shadow, Tensor(s!) state, "
         "int fc_lo, int w3_lo, float lr, float b1, float b2, float eps, float grad_scale, int rule) -> ()");
+  m.def("conv2_bwd_adam_fold(Tensor g2, Tensor idx2, Tensor a1, Tensor w2bf, Tensor x, Tensor? rows, "
+        "Tensor(s!) state, Tensor idx1, Tensor(a!) slab, Tensor(b!) cpart, Tensor(c!) gW2, Tensor(d!) gW1, "
+        "Tensor(e!) gb1, Tensor(f!) gb2, Tensor grads, Tensor(g!) p, Tensor(h!) m, Tensor(i!) v, Tensor(j!) shadow, "
+        "Tensor(k!) sync, int fc_lo, int w3_lo, float lr, float b1, float b2, float eps, float grad_scale, "
+        "int rule) -> ()");
   m.def("adam_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? shadow, Tensor(e!)? state, "
         "int host_step, float lr, float b1, float b2, float eps, float grad_scale, int rule, int bump=1, "
         "Tensor? loss_scale=None, int max_blocks=0) -> ()");
@@ -253,6 +272,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("conv2_bwd_adam", &conv2_bwd_adam_op);
   m.impl("conv2_bwd_w3adam", &conv2_bwd_w3adam_op);
   m.impl("conv2_wgrad_reduce_adam", &conv2_wgrad_reduce_adam_op);
+  m.impl("conv2_bwd_adam_fold", &conv2_bwd_adam_fold_op);
   m.impl("adam_step", &adam_op);
   m.impl("gather_cols_bf16", &gather_cols_op);
   m.impl("multi_tensor_adam", &mt_adam_op);

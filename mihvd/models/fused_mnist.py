@@ -264,6 +264,13 @@ class FusedMNISTTrainer:
         # launch measured 0.4-1.8 us slower per step (the reduce grows more than conv2_bwd shrinks).
         frac = min(max(float(os.environ.get("MIHVD_REDUCE_W3", "0")), 0.0), 1.0)
         self.tail_split = W3_START + int(frac * (FLAT_NUMEL - W3_START)) // 256 * 256
+        # MIHVD_FOLD_REDUCE=1 (opt-in): the gradient reduction + the rest of Adam run inside the conv2_bwd
+        # launch (conv2_bwd_adam_fold: arrival counter, write-through hand-off) instead of a launch of
+        # their own; the kernel falls back to two launches where every conv block cannot be resident.
+        # Bitwise equal, but measured slower on MI355X (35.6 vs 25.0 us for the pair): waiting for the
+        # slowest conv block serialises the reduction behind it (docs/ARCHITECTURE.md).
+        self.fold_reduce = self.fused_opt and os.environ.get("MIHVD_FOLD_REDUCE", "0") == "1"
+        self.fold_sync = torch.zeros(4, dtype=torch.int32, device=self.device)  # [arrive, depart, error, -]
         # MIHVD_W3_TAIL=1 (opt-in, with the fused optimizer): conv2_bwd's tail computes dW3 = a2^T dz tile by
         # tile on MFMA from the bf16 factors and applies Adam to dense/kernel from the accumulators
         # (csrc/kernels/w3_tail.h), so fc1_bwd only runs the dgrad tiles and the small reductions and
@@ -415,6 +422,13 @@ class FusedMNISTTrainer:
                                    self.grads[w3] if self.keep_w3_grad else None, self.lr, b1, b2, self.eps, 1.0,
                                    self.rule)
                 split = W3_START
+            elif self.fold_reduce and self.tail_split == W3_START:
+                o.conv2_bwd_adam_fold(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
+                                      self.gview("conv_layer2/conv2d/kernel"), self.gview("conv_layer1/conv2d/kernel"),
+                                      self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/bias"),
+                                      self.grads, self.params, self.m, self.v, self.shadow, self.fold_sync, FC_START,
+                                      W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
+                return
             else:
                 split = self.tail_split
                 t3 = slice(split, FLAT_NUMEL)
@@ -830,6 +844,9 @@ class FusedMNISTTrainer:
         """Raise if a direct-xGMI collective of this trainer timed out waiting for a peer (its
         outputs, and those of every later xGMI collective, are NaN). Waits for the current stream.
         A plane that select_data_plane() dropped after such a timeout is not checked again."""
+        if getattr(self, "fold_reduce", False) and int(self.fold_sync[2]) != 0:
+            raise RuntimeError("fused step: the folded gradient reduction timed out waiting for the conv blocks "
+                               "(a conv block was not resident); parameters of that step are invalid")
         if self.xplane is not None and not getattr(self, "_xplane_failed", False):
             self.xplane.check()
         for ctx in (self.xgmi or {}).values():

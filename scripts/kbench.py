@@ -80,6 +80,11 @@ def main():
             tr.slab, tr.cpart, B, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
             tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
             sh, st, FC, TS, 0.0, 0.9, 0.999, 1e-8, 1.0, 0)),
+        "conv2_bwd_adam_fold": lambda: o.conv2_bwd_adam_fold(
+            tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf, None, st, tr.idx1, tr.slab,
+            tr.cpart, tr.gview("conv_layer2/conv2d/kernel"), tr.gview("conv_layer1/conv2d/kernel"),
+            tr.gview("conv_layer1/conv2d/bias"), tr.gview("conv_layer2/conv2d/bias"), tr.grads, tr.params, tr.m, tr.v,
+            sh, tr.fold_sync, FC, W3, 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
         "conv2_bwd_adam": lambda: o.conv2_bwd_adam(
             tr.g2, tr.idx2, tr.a1, tr.pview("conv_layer2/conv2d/kernel", sh), tr.x_buf, None, st, tr.idx1, tr.slab,
             tr.cpart, tr.params[TS:], tr.grads[TS:], tr.m[TS:], tr.v[TS:], sh[TS:], 0.0, 0.9, 0.999, 1e-8, 1.0, 0),
@@ -195,7 +200,8 @@ def main():
         step_ops += ["fc1_bwd[roles=2]", "conv2_bwd_w3adam+reduce_adam"]
     elif tr.fused_opt:
         step_ops = [k for k in step_ops if not (tr.fc1_merged and k == "fc1_dgrad")]
-        step_ops += ["fc1_bwd" if tr.fc1_merged else "fc1_wgrad", "conv2_bwd_adam+reduce_adam"]
+        step_ops += ["fc1_bwd" if tr.fc1_merged else "fc1_wgrad",
+                     "conv2_bwd_adam_fold" if tr.fold_reduce else "conv2_bwd_adam+reduce_adam"]
     elif tr.fuse_w3:
         step_ops += ["fc1_wgrad_adam", "conv2_bwd", "conv2_wgrad_reduce", "adam_small"]
     else:

@@ -10,5 +10,6 @@ run() {  # env assignments..., then the kbench --only list
 JOBS=${JOBS:-conv2_bwd_adam+reduce_adam}
 for spec in ${SWEEP:-"4:0.8:0.2"}; do
   IFS=: read -r sw hd rw <<< "$spec"
-  run MIHVD_TAIL_STREAMERS=$sw MIHVD_TAIL_HEAD=$hd MIHVD_REDUCE_W3=${rw:-0}
+  run MIHVD_TAIL_STREAMERS=$sw MIHVD_TAIL_HEAD=$hd MIHVD_REDUCE_W3=${rw:-0} ${EXTRA:-}
 done
+# extra environment for every run: EXTRA="VAR=value ..."

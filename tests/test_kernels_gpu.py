@@ -542,6 +542,39 @@ def test_fused_optimizer_tail_matches_separate_adam(ops, monkeypatch):
         assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
 
 
+@pytest.mark.parametrize("B", [7, 37, 100, 128])
+def test_folded_reduction_matches_separate_launches(ops, monkeypatch, B):
+    """MIHVD_FOLD_REDUCE (default on at size 1): conv2_bwd's conv blocks hand their slab / partial rows
+    write-through to each other through an arrival counter and run the gradient reduction + the rest
+    of Adam inside the same launch. Against the separate-optimizer schedule it must agree bit for bit;
+    B = 128 has more conv blocks than CUs and takes the two-launch fallback. The arrival words are
+    reset by the kernel after every call and the error word stays 0."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    g = torch.Generator(device="cuda").manual_seed(41)
+    X = torch.rand(4 * B + 3, 784, device="cuda", generator=g)
+    Y = torch.randint(0, 10, (4 * B + 3,), device="cuda", generator=g)
+    out = []
+    for fused, fold in (("0", "0"), ("1", "1"), ("1", "0")):
+        monkeypatch.setenv("MIHVD_FUSED_OPT", fused)
+        monkeypatch.setenv("MIHVD_FOLD_REDUCE", fold)
+        tr = FusedMNISTTrainer(batch_size=B, seed=9, device="cuda")
+        assert tr.fold_reduce == (fold == "1")
+        tr.set_device_dataset(X, Y, shuffle=False)
+        tr.build_graph(steps_per_replay=3, warmup=1)
+        for _ in range(3):
+            tr.run_graph()
+        torch.cuda.synchronize()
+        out.append((tr.params.clone(), tr.m.clone(), tr.v.clone(), tr.shadow.clone(),
+                    [int(v) for v in tr.state.tolist()], tr.fold_sync.tolist()))
+    ref = out[0]
+    for o in out[1:]:
+        assert o[4] == ref[4]
+        assert o[5] == [0, 0, 0, 0]
+        for x0, x1, name in zip(ref[:4], o[:4], ("params", "m", "v", "shadow")):
+            assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
+
+
 @pytest.mark.parametrize("B", [1, 37, 100, 128])
 def test_w3_tile_tail_matches_stored_dw3_tail(ops, monkeypatch, B):
     """MIHVD_W3_TAIL=1: conv2_bwd's tail multiplies the bf16 fc1 factors into
