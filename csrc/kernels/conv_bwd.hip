@@ -75,19 +75,7 @@ constexpr int C1_XS = 32 * 32;                       // one shifted bf16 image c
 static_assert(C1_DY * 2 <= CB_DG_W * 2, "dY1 fits in the dead W2 image");
 static_assert(8 * 64 * 16 * 4 <= CB_DG_D * 2, "the GEMM partials fit in the dead dY2 image");
 
-// Sum over the 16 lanes of a DPP row (every lane gets the row's sum): quad xor 1, quad xor 2,
-// half-row mirror, row mirror — four v_add_f32 with DPP operands instead of LDS permutes.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float row_sum16(float v) {
-  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);  // row_half_mirror
-  v += dpp_f<0x140>(v);  // row_mirror
-  return v;
-}
+
 
 struct DyItem {
   uint2 g;       // 4 bf16 pooled gradients (already masked by conv2's pooled ReLU)

@@ -256,6 +256,8 @@ __global__ void __launch_bounds__(NW * 64) conv12_fwd_kernel(
   }
 #pragma unroll
   for (int it = 0; it < 1024 / T; ++it) xim[t + T * it] = f2bf(xv[it]);
+  // W2 (issued first, landed before the image chain) goes to LDS now, off the conv1 -> conv2 seam
+  lw.store(wim, C2_WROW, 800, t);
   __syncthreads();
   // 3. conv1 on MFMA. Lane row m = 16*tile + lr -> window 4*tile + (lr >> 2), pixel d = lr & 3.
   //    Tap offsets of this lane's 8 k values in the padded image (k >= 25 masked to zero).
@@ -325,7 +327,6 @@ __global__ void __launch_bounds__(NW * 64) conv12_fwd_kernel(
       }
     }
   }
-  lw.store(wim, C2_WROW, 800, t);
   __syncthreads();
   conv2_core<NW>(img, wim, b2, a2, idx2, half, b, t);
 }
