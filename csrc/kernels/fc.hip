@@ -23,15 +23,15 @@
 
 namespace mihvd {
 
-constexpr int FC1_K = 3136, FC1_N = 1024, FC1_KS = 14, FC1_KSL = FC1_K / FC1_KS;  // 224 = 7 K steps
-constexpr int FC1_NT = 64;                                                          // columns per block
+constexpr int FC1_K = 3136, FC1_N = 1024, FC1_KS = 7, FC1_KSL = FC1_K / FC1_KS;   // 448 = 14 K steps
+constexpr int FC1_NT = 32;                                                          // columns per block
 constexpr int MAXB = 128;                                                           // batch limit (8 tiles)
 constexpr int F1_ASTR = FC1_KSL + 8;   // a2 image rows: 232 elements (464 B)
 constexpr int F1_WSTR = FC1_NT + 8;    // W3 image rows: 72 elements (144 B)
 constexpr int F1_LDS = (MAXB * F1_ASTR + FC1_KSL * F1_WSTR) * 2;
 
-// grid (16, 14): blockIdx.x = 64-column tile, blockIdx.y = K slice. NW = 4 or 8 waves: wave w
-// owns the 16 features (w & 3) and, with 8 waves, half of the sample tiles (w >> 2).
+// grid (32, 7): blockIdx.x = 32-column tile, blockIdx.y = K slice (448 = 14 K steps). NW = 4 or 8
+// waves: wave w owns the 16 features w % 2 and the sample-tile group w / 2.
 // MT = ceil(B/16) sample tiles, a template parameter (no runtime guard around any MFMA: the odd
 // half's spare tile recomputes the last real one and is not stored).
 template <int MT, int NW = 4>
@@ -39,7 +39,8 @@ __global__ void __launch_bounds__(NW * 64) fc1_fwd_kernel(const u16* __restrict_
                                                           float* __restrict__ zpart, int B) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   constexpr int Mpad = MT * 16, T = NW * 64;
-  constexpr int MTW = NW == 8 ? (MT + 1) / 2 : MT;  // sample tiles per wave
+  constexpr int WN = FC1_NT / 16, MG = NW / WN;     // 16-feature groups, sample-tile groups
+  constexpr int MTW = (MT + MG - 1) / MG;           // sample tiles per wave
   u16* Ws = smem;                     // [224][F1_WSTR]    rows = k, n contiguous
   u16* As = smem + FC1_KSL * F1_WSTR; // [Mpad][F1_ASTR]   rows = samples, k contiguous
   const int nt = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
@@ -54,7 +55,7 @@ __global__ void __launch_bounds__(NW * 64) fc1_fwd_kernel(const u16* __restrict_
   }
   __syncthreads();
   const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4, q = lr >> 2, p = lr & 3;
-  const int wn = wave & 3, mt0 = NW == 8 ? (wave >> 2) * MTW : 0;
+  const int wn = wave % WN, mt0 = (wave / WN) * MTW;
   f32x4 acc[MTW];
 #pragma unroll
   for (int i = 0; i < MTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -671,7 +672,7 @@ void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_fwd: batch must be in [1, 128] (got ", B, ")");
   TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_fwd: a2");
   TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_fwd: w3");
-  TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "fc1_fwd: zpart [14][B][1024]");
+  TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "fc1_fwd: zpart [7][B][1024]");
   const int MT = (B + 15) >> 4;
   const int lds = (FC1_KSL * F1_WSTR + MT * 16 * F1_ASTR) * 2;
   auto stream = c10::hip::getCurrentHIPStream().stream();

@@ -46,7 +46,7 @@ import torch
 
 from .. import _native
 from ..utils.tracing import trace_range
-from .mnist import TF_PARAM_ORDER, TF_PARAM_SHAPES, MNISTConvNet
+from .mnist import FC1_KS, TF_PARAM_ORDER, TF_PARAM_SHAPES, MNISTConvNet
 
 ALIGN = 64  # elements (256 B)
 
@@ -216,7 +216,7 @@ class FusedMNISTTrainer:
             self.a2 = torch.empty(B, 3136, **bf)
             self.dz = torch.empty(B, 1024, **bf)
         self.idx2 = torch.empty(B, 3136, **u8)
-        self.zpart = torch.empty(14, B, 1024, **f32)
+        self.zpart = torch.empty(FC1_KS, B, 1024, **f32)  # fc1 split-K partial slabs
         self.h = torch.empty(B, 1024, **bf)
         self.dlog = torch.empty(B, 10, **f32)
         self.stats = torch.zeros(B, 2, **f32)

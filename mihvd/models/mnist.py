@@ -144,3 +144,6 @@ def softmax_cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.T
 
 def accuracy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     return (logits.argmax(1) == labels.long()).float().mean()
+
+# fc1_fwd split-K slabs of the fused HIP step (csrc/kernels/fc.hip FC1_KS; the ops check the zpart shape)
+FC1_KS = 7

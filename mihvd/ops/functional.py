@@ -15,7 +15,7 @@ import os
 import torch
 
 from .. import _native
-from ..models.mnist import TF_PARAM_ORDER
+from ..models.mnist import FC1_KS, TF_PARAM_ORDER
 
 
 class _Workspace:
@@ -34,7 +34,7 @@ class _Workspace:
             u8 = dict(device=device, dtype=torch.uint8)
             ws = dict(
                 a1=torch.empty(B, 14, 14, 32, **bf), idx1=torch.empty(B, 14, 14, 32, **u8),
-                a2=torch.empty(B, 3136, **bf), idx2=torch.empty(B, 3136, **u8), zpart=torch.empty(14, B, 1024, **f32),
+                a2=torch.empty(B, 3136, **bf), idx2=torch.empty(B, 3136, **u8), zpart=torch.empty(FC1_KS, B, 1024, **f32),
                 h=torch.empty(B, 1024, **bf), dz=torch.empty(B, 1024, **bf), dlog=torch.empty(B, 10, **f32),
                 stats=torch.empty(B, 2, **f32), g2=torch.empty(B, 3136, **bf),
                 cpart=torch.empty(B, 896, **f32), slab=torch.empty(int(ops.conv2_wgrad_groups(B)), 51200, **f32),

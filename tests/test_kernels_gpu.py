@@ -10,6 +10,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from mihvd.models.mnist import FC1_KS
+
 pytestmark = pytest.mark.gpu
 
 
@@ -113,7 +115,7 @@ def test_fc1_fwd(ops, B):
     g = torch.Generator(device="cuda").manual_seed(3)
     a2 = bf(torch.rand(B, 3136, device="cuda", generator=g))
     w = bf(torch.randn(3136, 1024, device="cuda", generator=g) * 0.02)
-    zp = torch.empty(14, B, 1024, device="cuda")
+    zp = torch.empty(FC1_KS, B, 1024, device="cuda")
     ops.fc1_fwd(a2.to(torch.bfloat16), w.to(torch.bfloat16), zp)
     assert rel_err(zp.sum(0), a2 @ w) < 1e-4
 
@@ -121,7 +123,7 @@ def test_fc1_fwd(ops, B):
 def test_head_no_dropout(ops):
     B = 100
     g = torch.Generator(device="cuda").manual_seed(4)
-    zp = torch.randn(14, B, 1024, device="cuda", generator=g) * 0.1
+    zp = torch.randn(FC1_KS, B, 1024, device="cuda", generator=g) * 0.1
     b3 = torch.randn(1024, device="cuda", generator=g) * 0.1
     w4 = torch.randn(1024, 10, device="cuda", generator=g) * 0.05
     b4 = torch.randn(10, device="cuda", generator=g) * 0.1
@@ -144,7 +146,7 @@ def test_head_no_dropout(ops):
 
 def test_head_dropout_rate(ops):
     B = 100
-    zp = torch.ones(14, B, 1024, device="cuda")
+    zp = torch.ones(FC1_KS, B, 1024, device="cuda")
     h = torch.empty(B, 1024, device="cuda", dtype=torch.bfloat16)
     dz, dlog, stats = torch.empty_like(h), torch.empty(B, 10, device="cuda"), torch.empty(B, 2, device="cuda")
     st = torch.zeros(4, device="cuda", dtype=torch.int64)
@@ -153,7 +155,7 @@ def test_head_dropout_rate(ops):
     ops.head_fwd_bwd(zp, *args, h, dz, dlog, stats)
     keep = (h.float() > 0).float()
     assert abs(keep.mean().item() - 0.5) < 0.01
-    assert torch.allclose(h.float()[h.float() > 0], torch.full_like(h.float()[h.float() > 0], 28.0))  # 14*1*2
+    assert torch.allclose(h.float()[h.float() > 0], torch.full_like(h.float()[h.float() > 0], 2.0 * FC1_KS))  # slabs of 1, x2 (dropout)
     h2 = torch.empty_like(h)
     ops.head_fwd_bwd(zp, *args, h2, dz, dlog, stats)
     # head advances only the optimizer counter (state[1]); the mask is keyed on state[0]
@@ -162,7 +164,7 @@ def test_head_dropout_rate(ops):
 
 def test_dropout_mask_depends_on_forward_step(ops):
     B = 16
-    zp = torch.ones(14, B, 1024, device="cuda")
+    zp = torch.ones(FC1_KS, B, 1024, device="cuda")
     st = torch.zeros(4, device="cuda", dtype=torch.int64)
     outs = []
     for step in (0, 0, 1):
