@@ -125,13 +125,27 @@ def main():
         step = CapturedStep(step, warmup=max(3, args.warmup))
     for _ in range(args.warmup):
         step()
-    sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
+    # Graph mode waits on the stream instead of the device: on this ROCm/torch build a device-wide
+    # synchronize between replays of the captured BERT-base step made the following replays produce
+    # NaN (docs/ARCHITECTURE.md, "Generic models"); the replays and the timing are on this stream.
+    if dev.type != "cuda":
+        sync = lambda: None  # noqa: E731
+    elif args.graph:
+        sync = torch.cuda.current_stream().synchronize
+    else:
+        sync = torch.cuda.synchronize
     sync()
     hvd.barrier()
     sync()
     t0 = time.perf_counter()
+    trace = [] if os.environ.get("MIHVD_STRESS_TRACE") else None
+    each = os.environ.get("MIHVD_STRESS_SYNC_EACH") == "1"
     for _ in range(args.steps):
         loss = step()
+        if each:
+            sync()
+        if trace is not None:
+            trace.append(loss.detach().clone())
     sync()
     hvd.barrier()
     sync()
@@ -139,6 +153,8 @@ def main():
     if n > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el)
+    if trace is not None:
+        print("per-step loss:", " ".join("%.4f" % float(v) for v in trace), flush=True)
     if hvd.rank() == 0:
         params = sum(p.numel() for p in model.parameters())
         cfg.update({"parallelism": f"dp{n}", "per_gpu_batch": B, "params": params,

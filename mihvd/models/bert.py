@@ -26,6 +26,7 @@ class BertConfig:
     max_len: int = 512
     type_vocab: int = 2
     dropout: float = 0.1
+    attn_dropout: float | None = None  # attention-probability dropout (None: ``dropout``)
     eps: float = 1e-12
 
 
@@ -41,12 +42,15 @@ class BertLayer(nn.Module):
         self.ln2 = nn.LayerNorm(c.hidden, eps=c.eps)
         self.drop = nn.Dropout(c.dropout)
 
+    def _attn_p(self):
+        return self.c.dropout if self.c.attn_dropout is None else self.c.attn_dropout
+
     def forward(self, x, mask=None):
         B, S, H = x.shape
         nh = self.c.heads
         q, k, v = self.qkv(x).view(B, S, 3, nh, H // nh).permute(2, 0, 3, 1, 4)
         a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask,
-                                           dropout_p=self.c.dropout if self.training else 0.0)
+                                           dropout_p=self._attn_p() if self.training else 0.0)
         a = a.transpose(1, 2).reshape(B, S, H)
         x = self.ln1(x + self.drop(self.proj(a)))  # post-LN, as in BERT
         return self.ln2(x + self.drop(self.fc2(F.gelu(self.fc1(x)))))

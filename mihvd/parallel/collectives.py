@@ -148,7 +148,7 @@ def _group_size(group) -> int:
 # allreduce
 # ------------------------------------------------------------------------------------------ #
 def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postscale_factor, group,
-                    segments=None, async_op=True):
+                    segments=None, async_op=True, wire_buf=None):
     ctx = basics._require()
     op = ReduceOp(op)
     n = _group_size(group)
@@ -168,11 +168,14 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
             return _register(work, out, None, f"allreduce.{name}")
         run_adasum()
         return _register(None, out, None, f"allreduce.{name}")
-    if n > 1 and hip_pack_ok(compression, tensor) and out.is_contiguous():
-        # fused HIP pack (cast + prescale) -> collective on the 16-bit wire -> unpack (cast + scale)
-        wire = hip_pack(compression, tensor, prescale_factor)
+    if hip_pack_ok(compression, tensor) and out.is_contiguous():
+        # fused HIP pack (cast + prescale) -> collective on the 16-bit wire -> unpack (cast + scale);
+        # at size 1 the wire round trip still runs (Horovod compresses at any size)
+        wire = hip_pack(compression, tensor, prescale_factor, out=wire_buf)
         scale = postscale_factor / n if op == ReduceOp.Average else postscale_factor
-        if ctx.engine is not None:
+        if n == 1:
+            work = None
+        elif ctx.engine is not None:
             work = ctx.engine.allreduce(f"allreduce.{name}", wire, _torch_op(op), group, fuse_extra=("hip-pack",))
         else:
             work = dist.all_reduce(wire, op=_torch_op(op), group=group, async_op=True)

@@ -57,8 +57,13 @@ def hip_pack_ok(compression, tensor) -> bool:
     return _native.load_kernels()
 
 
-def hip_pack(compression, tensor, scale: float = 1.0):
-    wire = torch.empty(tensor.numel(), dtype=compression.wire_dtype, device=tensor.device)
+def hip_pack(compression, tensor, scale: float = 1.0, out: torch.Tensor | None = None):
+    """Cast (+ scale) ``tensor`` onto the 16-bit wire; ``out`` is a persistent wire buffer (e.g. the
+    DistributedOptimizer's per-bucket one), so nothing is allocated per step."""
+    if out is not None and out.numel() == tensor.numel() and out.dtype == compression.wire_dtype:
+        wire = out
+    else:
+        wire = torch.empty(tensor.numel(), dtype=compression.wire_dtype, device=tensor.device)
     op = torch.ops.mihvd.scale_cast_bf16 if compression.wire_dtype == torch.bfloat16 else torch.ops.mihvd.scale_cast_f16
     op(tensor.view(-1), wire, float(scale))
     return wire

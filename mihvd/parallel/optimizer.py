@@ -41,15 +41,18 @@ def _dtype_code(dt: torch.dtype) -> int:
 
 
 class _Bucket:
-    __slots__ = ("index", "flat", "members", "offsets", "segments", "handle")
+    __slots__ = ("index", "flat", "members", "offsets", "segments", "handle", "wire")
 
-    def __init__(self, index, flat, members, offsets, segments):
+    def __init__(self, index, flat, members, offsets, segments, wire=None):
         self.index = index
         self.flat = flat
         self.members = members
         self.offsets = offsets
         self.segments = segments
         self.handle = None
+        # persistent 16-bit wire buffer of a compressed bucket: no allocation per step (and none
+        # inside a captured HIP graph, whose private pool would otherwise own it)
+        self.wire = wire
 
 
 class _DistributedOptimizer(torch.optim.Optimizer):
@@ -129,7 +132,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 p0 = params[plan.members[b][0]]
                 flat = torch.zeros(plan.numel[b], dtype=p0.dtype, device=p0.device)
                 segs = [(int(o), int(o) + params[i].numel()) for i, o in zip(plan.members[b], plan.offsets[b])]
-                self._buckets.append(_Bucket(b, flat, list(plan.members[b]), list(plan.offsets[b]), segs))
+                wdt = getattr(self._compression, "wire_dtype", None)
+                wire = (torch.empty(flat.numel(), dtype=wdt, device=flat.device)
+                        if wdt is not None and flat.is_cuda and flat.dtype == torch.float32 else None)
+                self._buckets.append(_Bucket(b, flat, list(plan.members[b]), list(plan.offsets[b]), segs, wire))
             self._tensor_bucket = list(plan.tensor_bucket)
             self._tensor_offset = list(plan.tensor_offset)
             self._controller = rt.Controller(self._tensor_bucket, len(self._buckets), self._passes)
@@ -205,7 +211,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             b.handle = C._allreduce_impl(b.flat, b.flat, f"bucket{bid}", ReduceOp.Adasum, self._compression, pre,
                                          post, None, segments=b.segments)
         else:
-            b.handle = C._allreduce_impl(b.flat, b.flat, f"bucket{bid}", self._op, self._compression, pre, post, None)
+            b.handle = C._allreduce_impl(b.flat, b.flat, f"bucket{bid}", self._op, self._compression, pre, post, None,
+                                         wire_buf=b.wire)
 
     def synchronize(self):
         """Launch any bucket not yet launched, then wait for every bucket's allreduce."""

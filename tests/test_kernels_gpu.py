@@ -813,6 +813,63 @@ def test_captured_step_matches_eager(ops):
         hvd.shutdown()
 
 
+@pytest.mark.parametrize("comp", ["none", "fp16", "bf16"])
+def test_captured_step_compression_survives_device_sync(ops, comp):
+    """CapturedStep + DistributedOptimizer with several compressed buckets: replays, a device-wide
+    synchronize (the bench's barrier), more replays == the same steps eagerly, bitwise. (The wire
+    buffers used to be allocated per step inside the graph's pool; after a device synchronize a few
+    gradient elements of the next replay came out NaN.)"""
+    import mihvd.torch as hvd
+    from mihvd.graphs import CapturedStep
+    from mihvd.optim import FusedAdam
+
+    hvd.init()
+    try:
+        C = {"none": hvd.Compression.none, "fp16": hvd.Compression.fp16, "bf16": hvd.Compression.bf16}[comp]
+        torch.manual_seed(5)
+        X = torch.randn(64, 128, device="cuda")
+        Y = torch.randn(64, 8, device="cuda")
+
+        def build():
+            torch.manual_seed(1)
+            m = torch.nn.Sequential(torch.nn.Linear(128, 256), torch.nn.GELU(), torch.nn.Linear(256, 256),
+                                    torch.nn.GELU(), torch.nn.Linear(256, 8)).cuda()
+            o = hvd.DistributedOptimizer(FusedAdam(m.parameters(), lr=1e-3), named_parameters=m.named_parameters(),
+                                         compression=C, fusion_threshold=64 * 1024)
+            return m, o
+
+        m1, o1 = build()
+        assert len(o1.buckets) >= 3
+
+        def step():
+            o1.zero_grad(set_to_none=False)
+            loss = torch.nn.functional.mse_loss(m1(X), Y)
+            loss.backward()
+            o1.step()
+            return loss
+
+        graphed = CapturedStep(step, warmup=2)
+        for _ in range(3):
+            graphed()
+        torch.cuda.synchronize()
+        hvd.barrier()
+        torch.cuda.synchronize()
+        for _ in range(3):
+            graphed()
+        torch.cuda.synchronize()
+        m2, o2 = build()
+        for _ in range(8):  # 2 warm-up steps + 6 replays
+            o2.zero_grad(set_to_none=False)
+            torch.nn.functional.mse_loss(m2(X), Y).backward()
+            o2.step()
+        torch.cuda.synchronize()
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            assert torch.isfinite(p1).all()
+            assert torch.equal(p1, p2)
+    finally:
+        hvd.shutdown()
+
+
 @pytest.mark.parametrize("wire", [torch.bfloat16, torch.float16])
 def test_hip_pack_unpack_matches_torch_casts(ops, wire):
     """Compression pack/unpack kernels (cast + scale fused) == torch casts then scale."""
