@@ -28,10 +28,16 @@ import torch
 
 
 class CapturedStep:
-    def __init__(self, step_fn, warmup: int = 3, pool=None):
+    """``serialize=True``: each replay is launched only once the previous one has completed (a
+    host wait on an event; costs one launch latency per step)."""
+
+    def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("CapturedStep needs a GPU")
         self.step_fn = step_fn
+        self.serialize = bool(serialize)
+        self._done = torch.cuda.Event() if self.serialize else None
+        self._pending = False
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up on a side stream, as graph capture of autograd requires
@@ -45,7 +51,12 @@ class CapturedStep:
         self.replays = 0
 
     def __call__(self):
+        if self._pending:
+            self._done.synchronize()
         self.graph.replay()
+        if self.serialize:
+            self._done.record()
+            self._pending = True
         self.replays += 1
         return self.output
 

@@ -27,6 +27,7 @@ class BertConfig:
     type_vocab: int = 2
     dropout: float = 0.1
     attn_dropout: float | None = None  # attention-probability dropout (None: ``dropout``)
+    attn_impl: str = "sdpa"  # "sdpa" (F.scaled_dot_product_attention) | "math" (matmul/softmax ops)
     eps: float = 1e-12
 
 
@@ -49,8 +50,14 @@ class BertLayer(nn.Module):
         B, S, H = x.shape
         nh = self.c.heads
         q, k, v = self.qkv(x).view(B, S, 3, nh, H // nh).permute(2, 0, 3, 1, 4)
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask,
-                                           dropout_p=self._attn_p() if self.training else 0.0)
+        p = self._attn_p() if self.training else 0.0
+        if self.c.attn_impl == "math":
+            w = (q @ k.transpose(-2, -1)) * (1.0 / math.sqrt(q.size(-1)))
+            if mask is not None:
+                w = w + mask
+            a = F.dropout(w.softmax(-1), p=p, training=p > 0) @ v
+        else:
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
         a = a.transpose(1, 2).reshape(B, S, H)
         x = self.ln1(x + self.drop(self.proj(a)))  # post-LN, as in BERT
         return self.ln2(x + self.drop(self.fc2(F.gelu(self.fc1(x)))))

@@ -815,10 +815,9 @@ def test_captured_step_matches_eager(ops):
 
 @pytest.mark.parametrize("comp", ["none", "fp16", "bf16"])
 def test_captured_step_compression_survives_device_sync(ops, comp):
-    """CapturedStep + DistributedOptimizer with several compressed buckets: replays, a device-wide
-    synchronize (the bench's barrier), more replays == the same steps eagerly, bitwise. (The wire
-    buffers used to be allocated per step inside the graph's pool; after a device synchronize a few
-    gradient elements of the next replay came out NaN.)"""
+    """CapturedStep + DistributedOptimizer with several compressed buckets (persistent wire
+    buffers, HIP pack/unpack at world size 1 too): replays, a device-wide synchronize and barrier
+    (the benches' timing fence), more replays == the same steps eagerly, bitwise."""
     import mihvd.torch as hvd
     from mihvd.graphs import CapturedStep
     from mihvd.optim import FusedAdam
