@@ -112,21 +112,24 @@ def test_plane_and_sharding_switches_two_ranks(tmp_path):
         assert o["loss"] == o["loss_ref"]
 
 
-def test_bench_multirank_rehearsal_on_one_gpu():
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_multirank_rehearsal_on_one_gpu(n):
     """bench.py's N > 1 flow (torch.distributed.run rendezvous on 127.0.0.1, factor gather +
-    sharded optimizer, barrier-bracketed timing, max over ranks, one JSON line from rank 0) with two
-    ranks sharing this GPU over gloo (MIHVD_GLOO_ON_GPU; RCCL refuses two ranks per GPU)."""
+    sharded optimizer with the N-rank row-tile split, data-plane selection, barrier-bracketed
+    timing, max over ranks, one JSON line from rank 0) with N ranks sharing this GPU over gloo
+    (MIHVD_GLOO_ON_GPU; RCCL refuses two ranks per GPU)."""
     _gpu()
     env = dict(os.environ, MIHVD_BACKEND="gloo", MIHVD_GLOO_ON_GPU="1", PYTHONPATH=ROOT)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
         env.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "7",
-           "--warmup", "2"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(29531 + n), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps",
+           "7", "--warmup", "2"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     r = lines[0]
-    assert r["n_gpus"] == 2 and r["steps"] == 7 and r["warmup"] == 2 and r["value"] > 0
-    assert r["config"]["global_batch"] == 200 and r["config"]["parallelism"] == "dp2"
+    assert r["n_gpus"] == n and r["steps"] == 7 and r["warmup"] == 2 and r["value"] > 0
+    assert r["config"]["global_batch"] == 100 * n and r["config"]["parallelism"] == f"dp{n}"
+    assert r["config"]["final_loss"] == r["config"]["final_loss"]  # finite (NaN != NaN)
