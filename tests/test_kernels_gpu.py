@@ -882,4 +882,3 @@ def test_hip_pack_unpack_matches_torch_casts(ops, wire):
     out = torch.empty_like(x)
     hip_unpack(w, out, 0.25)
     assert torch.equal(out, w.float() * 0.25)
-
