@@ -376,6 +376,16 @@ def mpi_built() -> bool:
     return False
 
 
+def ccl_built() -> bool:
+    """Intel oneCCL: not part of this framework (Horovod API parity)."""
+    return False
+
+
+def ddl_built() -> bool:
+    """IBM DDL: not part of this framework (Horovod API parity)."""
+    return False
+
+
 def mpi_enabled() -> bool:
     return False
 

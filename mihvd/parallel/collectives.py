@@ -413,6 +413,21 @@ def allgather(tensor, name=None, process_set=None):
     return synchronize(allgather_async(tensor, name, process_set))
 
 
+def grouped_allgather_async(tensors: Sequence[torch.Tensor], name=None, process_set=None) -> int:
+    """``hvd.grouped_allgather_async``: every tensor all-gathered along dim 0 (first dims may
+    differ per rank); the handle's output is the list of results in input order."""
+    hs = [allgather_async(t, f"{name or 'grouped'}.{i}", process_set) for i, t in enumerate(tensors)]
+
+    def post(_o, hs=hs):
+        return [synchronize(h) for h in hs]
+
+    return _register(_Children(hs), None, post, f"grouped_allgather.{name or 'grouped'}")
+
+
+def grouped_allgather(tensors: Sequence[torch.Tensor], name=None, process_set=None):
+    return synchronize(grouped_allgather_async(tensors, name, process_set))
+
+
 def alltoall(tensor, splits=None, name=None, process_set=None):
     """Scatter slices of dim 0 to every rank and gather what they send back (``hvd.alltoall``).
     Returns ``(output, received_splits)``."""

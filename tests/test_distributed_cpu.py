@@ -229,6 +229,9 @@ def test_api_extras_two_ranks(tmp_path):
     assert a["reducescatter_async"] == b["reducescatter_async"] == [[3.0] * 3] * 2
     assert a["grouped_reducescatter"] == b["grouped_reducescatter"] == [[[1.5, 1.5]], [0.5] * 3]
     assert a["grouped_reducescatter_async"] == [[3.0]]
+    assert a["grouped_allgather"] == b["grouped_allgather"] == [[[0.0, 0.0], [1.0, 1.0], [1.0, 1.0]], [0, 0, 1]]
+    assert a["grouped_allgather_sync"] == [[0.0, 1.0]]
+    assert a["built"] == [False, False, False]
     assert a["sparse_sum"] == b["sparse_sum"] == [[2.0, 1.0], [0.0, 2.0], [0.0, 0.0]]
     assert a["sparse_avg"] == [[1.0, 0.5], [0.0, 1.0], [0.0, 0.0]]
     for r in (a, b):

@@ -318,6 +318,13 @@ def sc_api_extras(outdir):
     res["grouped_reducescatter"] = [x.tolist() for x in g]
     h = hvd.grouped_reducescatter_async([torch.ones(n) * (r + 1)], op=hvd.Sum)
     res["grouped_reducescatter_async"] = [x.tolist() for x in hvd.synchronize(h)]
+    # grouped allgather: uneven first dims per rank (r+1 rows), two dtypes
+    h = hvd.grouped_allgather_async([torch.full((r + 1, 2), float(r)), torch.arange(r + 1, dtype=torch.int64)])
+    while not hvd.poll(h):
+        time.sleep(0.001)
+    res["grouped_allgather"] = [x.tolist() for x in hvd.synchronize(h)]
+    res["grouped_allgather_sync"] = [x.tolist() for x in hvd.grouped_allgather([torch.ones(1) * r])]
+    res["built"] = [hvd.ccl_built(), hvd.ddl_built(), hvd.mpi_built()]
     # sparse: rank r holds value (r+1) at row r and 1.0 at row 0 of a (n+1)x2 tensor
     idx = torch.tensor([[0, r], [0, 1]])
     sp = torch.sparse_coo_tensor(idx, torch.tensor([1.0, float(r + 1)]), (n + 1, 2))
