@@ -417,3 +417,73 @@ class Model:
         sd = torch.load(target, map_location="cpu", weights_only=True)["model"]
         module.load_state_dict(sd)
         return module
+
+
+# ------------------------------------------------------------------------------------------ #
+# Module-level functions of horovod.tensorflow.keras
+# ------------------------------------------------------------------------------------------ #
+def _as_tensor(value):
+    t = value if torch.is_tensor(value) else torch.as_tensor(np.asarray(value))
+    return t.to(_b.device()) if _b.is_initialized() and _b.backend() == "nccl" else t
+
+
+def _like(value, t: torch.Tensor):
+    """Return ``t`` in the caller's type: a tensor for a tensor, a numpy array otherwise (Keras
+    backend values), a Python scalar for a scalar."""
+    if torch.is_tensor(value):
+        return t.to(value.device)
+    a = t.detach().cpu().numpy()
+    return a.item() if np.ndim(value) == 0 and a.size == 1 else a
+
+
+def allreduce(value, name=None, average=True, prescale_factor=1.0, postscale_factor=1.0, op=None,
+              compression=Compression.none):
+    """``hvd.allreduce`` of a tensor / array / scalar (Average unless ``average=False`` or ``op``)."""
+    t = _as_tensor(value)
+    if not t.is_floating_point():
+        t = t.double() if not torch.is_tensor(value) else t
+    if op is None:
+        op = _b.Average if average else _b.Sum
+    return _like(value, C.allreduce(t, name=name, op=op, prescale_factor=prescale_factor,
+                                    postscale_factor=postscale_factor, compression=compression))
+
+
+def allgather(value, name=None):
+    """``hvd.allgather``: concatenation of every rank's value along the first dimension."""
+    return _like(value, C.allgather(_as_tensor(value), name=name))
+
+
+def broadcast(value, root_rank, name=None):
+    """``hvd.broadcast``: ``root_rank``'s value on every rank."""
+    return _like(value, C.broadcast(_as_tensor(value), root_rank, name=name))
+
+
+def broadcast_global_variables(root_rank: int, model: "Model"):
+    """Broadcast a compiled model's weights and optimizer state from ``root_rank`` (Horovod's
+    Keras form reads them from the global backend session; here the model is passed)."""
+    broadcast_parameters(model.module.state_dict(), root_rank)
+    if model.optimizer is not None:
+        broadcast_optimizer_state(model.optimizer, root_rank)
+
+
+def load_model(filepath: str, module: torch.nn.Module, optimizer=None, loss=None, metrics=(),
+               compression=Compression.none, policy: str = "float32", custom_optimizers=None,
+               custom_objects=None) -> "Model":
+    """``hvd.load_model``: a ``Model`` over ``module`` with the weights saved by ``Model.save`` and,
+    if ``optimizer`` is given (an optimizer over ``module``'s parameters, or a factory / optimizer
+    class called with them; also taken from ``custom_optimizers``), that optimizer wrapped in
+    ``DistributedOptimizer``. The architecture is passed as
+    ``module``: a torch checkpoint holds tensors only (weights-only load)."""
+    Model.load_weights(module, filepath)
+    m = Model(module, policy=policy)
+    if optimizer is None and custom_optimizers:
+        optimizer = custom_optimizers[0] if isinstance(custom_optimizers, (list, tuple)) else custom_optimizers
+    if optimizer is not None and not isinstance(optimizer, torch.optim.Optimizer):
+        optimizer = optimizer(module.parameters())  # a factory / optimizer class over the parameters
+    if optimizer is not None:
+        optimizer = DistributedOptimizer(optimizer, named_parameters=module.named_parameters(), compression=compression)
+    m.compile(optimizer, loss, metrics)
+    return m
+
+
+from . import elastic  # noqa: E402,F401  (hvd.elastic)

@@ -24,8 +24,8 @@ import torch
 
 from .basics import *  # noqa: F401,F403  (init, rank, size, Average, Adasum, ...)
 from . import basics as _b
-from .parallel.collectives import (allgather, allreduce, broadcast, broadcast_object,  # noqa: F401
-                                   broadcast_)
+from .parallel.collectives import (allgather, allreduce, alltoall, barrier, broadcast, broadcast_,  # noqa: F401
+                                   broadcast_object, grouped_allgather, grouped_allreduce, join, reducescatter)
 from .parallel.compression import Compression  # noqa: F401
 from .parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters  # noqa: F401
 from .utils import checkpoint as ckpt
@@ -105,6 +105,22 @@ class SessionRunHook:
 
     def end(self, session):
         pass
+
+
+def broadcast_variables(variables, root_rank: int):
+    """Broadcast tensors in place from ``root_rank`` (``hvd.broadcast_variables``): a mapping of
+    name -> tensor (every rank must pass the same names) or a sequence of tensors."""
+    items = sorted(variables.items()) if isinstance(variables, dict) else list(enumerate(variables))
+    for name, t in items:
+        broadcast_(t, root_rank, name=f"bcast.{name}")
+
+
+def broadcast_global_variables(root_rank: int, state=None):
+    """``hvd.broadcast_global_variables``: every global variable of a train state (weights, Adam
+    slots, global_step; ``TorchTrainState`` / ``FusedMNISTTrainer``) from ``root_rank``."""
+    if state is None:
+        raise ValueError("broadcast_global_variables needs the train state whose variables to broadcast")
+    state.broadcast(root_rank)
 
 
 class BroadcastGlobalVariablesHook(SessionRunHook):
@@ -306,3 +322,6 @@ class MonitoredTrainingSession:
 
     def close(self):
         self.__exit__(None, None, None)
+
+
+from . import elastic  # noqa: E402,F401  (hvd.elastic)

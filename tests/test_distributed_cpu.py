@@ -245,3 +245,16 @@ def test_api_extras_debug_sync_mode(tmp_path):
     """Composite handles (grouped / sparse) stay pollable when every collective completes eagerly."""
     _, (a, b) = run_scenario(tmp_path, "api_extras", env={"MIHVD_DEBUG_SYNC": "1"})
     assert a["grouped_async"] == b["grouped_async"] and a["sparse_sum"] == [[2.0, 1.0], [0.0, 2.0], [0.0, 0.0]]
+
+
+def test_keras_and_tf_module_functions_two_ranks(tmp_path):
+    """hvd.allreduce / allgather / broadcast / broadcast_global_variables / load_model of the Keras
+    API and broadcast_variables of the TF1 API over two gloo ranks."""
+    _, (a, b) = run_scenario(tmp_path, "keras_tf_api")
+    for r in (a, b):
+        assert r["allreduce_scalar"] == 1.5 and r["allreduce_sum"] == [1.0, 1.0]
+        assert r["allgather"] == [[0, 0], [1, 1]] and r["broadcast"] == [10, 11, 12]
+        assert r["tf_bcast"] == [[1.0, 1.0], [1.0], [0.0, 0.0]]
+        assert r["loaded"] == a["weights"] and r["loaded_dp"] is True
+    assert a["weights"] == b["weights"] and a["exp_avg"] == b["exp_avg"]
+

@@ -356,6 +356,43 @@ def sc_api_extras(outdir):
     out(outdir, "api_extras", res)
 
 
+def sc_keras_tf_api(outdir):
+    """Module-level functions of horovod.tensorflow.keras / horovod.tensorflow."""
+    import mihvd.keras as hk
+    import mihvd.tensorflow as htf
+
+    r = hvd.rank()
+    res = {"allreduce_scalar": hk.allreduce(float(r + 1)),
+           "allreduce_sum": hk.allreduce(np.ones(2) * r, average=False).tolist(),
+           "allgather": hk.allgather(np.full((1, 2), r)).tolist(),
+           "broadcast": hk.broadcast(np.arange(3) + 10 * r, 1).tolist()}
+    # broadcast_global_variables(root, model): weights and optimizer state of a compiled Model
+    torch.manual_seed(r)
+    mod = torch.nn.Linear(3, 2)
+    m = hk.Model(mod)
+    m.compile(hvd.DistributedOptimizer(torch.optim.Adam(mod.parameters(), lr=0.1),
+                                       named_parameters=mod.named_parameters()), torch.nn.functional.cross_entropy)
+    m.train_on_batch(torch.ones(4, 3) * (r + 1), torch.tensor([0, 1, 0, 1]))
+    hk.broadcast_global_variables(0, m)
+    res["weights"] = mod.weight.detach().flatten().tolist()
+    res["exp_avg"] = m.optimizer.state[mod.weight]["exp_avg"].flatten().tolist()
+    # load_model: every rank reads rank 0's file into a fresh module, optimizer wrapped for DP
+    path = os.path.join(outdir, "km")
+    if r == 0:
+        m.save(path)
+    hvd.barrier()
+    m2 = hk.load_model(path, torch.nn.Linear(3, 2), optimizer=lambda ps: torch.optim.SGD(ps, lr=0.0))
+    res["loaded"] = m2.module.weight.detach().flatten().tolist()
+    res["loaded_dp"] = hasattr(m2.optimizer, "synchronize") and len(m2.optimizer._params) == 2
+    # horovod.tensorflow: broadcast_variables of a dict / a list
+    v = {"a": torch.ones(2) * r, "b": torch.zeros(1) + r}
+    htf.broadcast_variables(v, 1)
+    lst = [torch.full((2,), float(r))]
+    htf.broadcast_variables(lst, 0)
+    res["tf_bcast"] = [v["a"].tolist(), v["b"].tolist(), lst[0].tolist()]
+    out(outdir, "keras_tf_api", res)
+
+
 PS_INIT = []
 
 
