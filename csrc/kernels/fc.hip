@@ -514,16 +514,20 @@ __global__ void __launch_bounds__(256, MINW) fc1_wgrad_kernel(
 }
 
 // dW3 tiles over a long K (the all-gathered factors of N ranks, Kw = N*B) with the K chunks split
-// between the two 4-wave groups of a 512-thread block: group g streams chunks g, g+2, ... through its
-// own LDS images (the next chunk's loads in flight while it multiplies), so a tile's chunk chain is
-// half as long as in fc1_wgrad_block. The groups then swap half-tiles through LDS and each finishes
-// one half: sum (group 0 + group 1, always in that order: deterministic), then the store or the
-// Adam epilogue. Only the tile geometry of fc1_wgrad_block is reused; results differ from it in the
-// last bits (the K sum is split) but every rank and every row slice computes the same values.
-template <bool ADAM>
-__device__ __forceinline__ void fc1_dw3_tile_kg2(int tile, const u16* __restrict__ dzw, const u16* __restrict__ a2w,
-                                                 int Kw, float* __restrict__ gW3, const AdamArgs& ad, int write_grad,
-                                                 int a2s, int a2c0, u16* smem) {
+// between the G 4-wave groups of a 256*G-thread block (G = 2 or 4): group g streams chunks g, g+G, ...
+// through its own LDS images (the next chunk's loads in flight while it multiplies), so a tile's
+// chunk chain is 1/G as long as in fc1_wgrad_block. The groups then exchange their partial tiles
+// through LDS and each finishes 4/G of the 2x2 sub-tiles: the sum over groups 0, 1, ..., G-1 in that
+// order (deterministic), then the store or the Adam epilogue. Only the tile geometry of
+// fc1_wgrad_block is reused; results differ from it in the last bits (the K sum is split) but every
+// rank and every row slice computes the same values. G = 4 pays where the chunk chain is long (the
+// 8-rank factors: 7 chunks -> 2 per group instead of 4).
+template <bool ADAM, int G>
+__device__ __forceinline__ void fc1_dw3_tile_kg(int tile, const u16* __restrict__ dzw, const u16* __restrict__ a2w,
+                                                int Kw, float* __restrict__ gW3, const AdamArgs& ad, int write_grad,
+                                                int a2s, int a2c0, u16* smem) {
+  static_assert(G == 2 || G == 4, "fc1_dw3_tile_kg: 2 or 4 groups");
+  constexpr int U = 4 / G;  // sub-tiles (i, jj) finished by each group
   const int t = threadIdx.x, g = t >> 8, th = t & 255, lane = th & 63, wave = th >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
   const int jt = tile >> 4, ntile = tile & 15;
@@ -531,7 +535,7 @@ __device__ __forceinline__ void fc1_dw3_tile_kg2(int tile, const u16* __restrict
   u16* Zim = smem + g * (2 * MAXB * FB_TSTR);  // [128][72] rows k, cols n
   u16* Aim = Zim + MAXB * FB_TSTR;             // [128][72] rows k, cols j
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  const int nch = (Kw + MAXB - 1) / MAXB, nit = (nch + 1) / 2;
+  const int nch = (Kw + MAXB - 1) / MAXB, nit = (nch + G - 1) / G;
   auto rows_of = [&](int c) { return c < nch ? min(MAXB, Kw - c * MAXB) : 0; };
   f32x4 acc[2][2];
 #pragma unroll
@@ -544,11 +548,11 @@ __device__ __forceinline__ void fc1_dw3_tile_kg2(int tile, const u16* __restrict
       la.load(a2w + (int64_t)g * MAXB * a2s + (j0 - a2c0), a2s, (rows + 31) & ~31, rows, th);
     }
   }
-  float4 pp[2], mm[2], vv[2];  // Adam operands of this group's half-tile (i == g)
+  float4 pp[U], mm[U], vv[U];  // Adam operands of this group's sub-tiles u = g*U + s (i = u >> 1, jj = u & 1)
   for (int it = 0; it < nit; ++it) {
-    const int c = 2 * it + g;
+    const int c = G * it + g;
     const int rows = rows_of(c), Kpad = (rows + 31) & ~31;
-    if (it > 0) __syncthreads();  // both groups read their previous chunk's fragments
+    if (it > 0) __syncthreads();  // every group read its previous chunk's fragments
     if (rows > 0) {
       lz.store(Zim, FB_TSTR, Kpad, th);
       la.store(Aim, FB_TSTR, Kpad, th);
@@ -557,18 +561,19 @@ __device__ __forceinline__ void fc1_dw3_tile_kg2(int tile, const u16* __restrict
     if constexpr (ADAM) {
       if (it == 0) {
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const int64_t o = (int64_t)(j0 + wn + jj * 16 + lr) * FC1_N + n0 + wm + g * 16 + 4 * lg;
-          pp[jj] = *reinterpret_cast<const float4*>(ad.p + o);
-          mm[jj] = *reinterpret_cast<const float4*>(ad.m + o);
-          vv[jj] = *reinterpret_cast<const float4*>(ad.v + o);
+        for (int s2 = 0; s2 < U; ++s2) {
+          const int u = g * U + s2, i = u >> 1, jj = u & 1;
+          const int64_t o = (int64_t)(j0 + wn + jj * 16 + lr) * FC1_N + n0 + wm + i * 16 + 4 * lg;
+          pp[s2] = *reinterpret_cast<const float4*>(ad.p + o);
+          mm[s2] = *reinterpret_cast<const float4*>(ad.m + o);
+          vv[s2] = *reinterpret_cast<const float4*>(ad.v + o);
         }
       }
     }
-    const int rn = rows_of(c + 2);
+    const int rn = rows_of(c + G);
     if (rn > 0) {
-      lz.load(dzw + (int64_t)(c + 2) * MAXB * FC1_N + n0, FC1_N, (rn + 31) & ~31, rn, th);
-      la.load(a2w + (int64_t)(c + 2) * MAXB * a2s + (j0 - a2c0), a2s, (rn + 31) & ~31, rn, th);
+      lz.load(dzw + (int64_t)(c + G) * MAXB * FC1_N + n0, FC1_N, (rn + 31) & ~31, rn, th);
+      la.load(a2w + (int64_t)(c + G) * MAXB * a2s + (j0 - a2c0), a2s, (rn + 31) & ~31, rn, th);
     }
     for (int k0 = 0; k0 < Kpad; k0 += 32) {
       bf16x8 af[2], bfv[2];
@@ -585,26 +590,27 @@ __device__ __forceinline__ void fc1_dw3_tile_kg2(int tile, const u16* __restrict
         for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mfma16(af[i], bfv[jj], acc[i][jj]);
     }
   }
-  // swap half-tiles: group g keeps i == g and hands its i == 1 - g partials to the other group
+  // exchange: every group stores its four partial sub-tiles, then sums the groups' partials of its own
   __syncthreads();
-  float* xr = reinterpret_cast<float*>(smem);  // [group][256 threads][2 jj][4]
+  f32x4* xr = reinterpret_cast<f32x4*>(smem);  // [group][256 threads][4 sub-tiles]
 #pragma unroll
-  for (int jj = 0; jj < 2; ++jj)
-    *reinterpret_cast<f32x4*>(xr + ((g * 256 + th) * 2 + jj) * 4) = g == 0 ? acc[1][jj] : acc[0][jj];
+  for (int u = 0; u < 4; ++u) xr[(g * 256 + th) * 4 + u] = acc[u >> 1][u & 1];
   __syncthreads();
 #pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const f32x4 other = *reinterpret_cast<const f32x4*>(xr + (((1 - g) * 256 + th) * 2 + jj) * 4);
-    const f32x4 s = g == 0 ? acc[0][jj] + other : other + acc[1][jj];  // group 0's part first
-    const int64_t o = (int64_t)(j0 + wn + jj * 16 + lr) * FC1_N + n0 + wm + g * 16 + 4 * lg;
-    const float4 gv = make_float4(s[0], s[1], s[2], s[3]);
+  for (int s2 = 0; s2 < U; ++s2) {
+    const int u = g * U + s2, jj = u & 1, i = u >> 1;
+    f32x4 sum = xr[th * 4 + u];
+#pragma unroll
+    for (int gg = 1; gg < G; ++gg) sum = sum + xr[(gg * 256 + th) * 4 + u];  // groups in order
+    const int64_t o = (int64_t)(j0 + wn + jj * 16 + lr) * FC1_N + n0 + wm + i * 16 + 4 * lg;
+    const float4 gv = make_float4(sum[0], sum[1], sum[2], sum[3]);
     if constexpr (ADAM) {
       const AdamCoef cf = adam_coef((float)ad.state[ST_OPT], ad.lr, ad.b1, ad.b2, ad.eps, ad.gscale, ad.rule);
       if (write_grad) *reinterpret_cast<float4*>(gW3 + o) = gv;
-      const uint2 sh = adam4(pp[jj], mm[jj], vv[jj], gv, cf);
-      *reinterpret_cast<float4*>(ad.p + o) = pp[jj];
-      *reinterpret_cast<float4*>(ad.m + o) = mm[jj];
-      *reinterpret_cast<float4*>(ad.v + o) = vv[jj];
+      const uint2 sh = adam4(pp[s2], mm[s2], vv[s2], gv, cf);
+      *reinterpret_cast<float4*>(ad.p + o) = pp[s2];
+      *reinterpret_cast<float4*>(ad.m + o) = mm[s2];
+      *reinterpret_cast<float4*>(ad.v + o) = vv[s2];
       *reinterpret_cast<uint2*>(ad.shadow + o) = sh;
     } else {
       *reinterpret_cast<float4*>(gW3 + o) = gv;
@@ -612,16 +618,16 @@ __device__ __forceinline__ void fc1_dw3_tile_kg2(int tile, const u16* __restrict
   }
 }
 
-template <bool ADAM>
-__global__ void __launch_bounds__(512) fc1_dw3_kg2_kernel(const u16* __restrict__ dzw, const u16* __restrict__ a2w,
-                                                          int Kw, float* __restrict__ gW3, int tile_base, AdamArgs ad,
-                                                          int write_grad, int a2s, int a2c0, CollRole cr) {
+template <bool ADAM, int G>
+__global__ void __launch_bounds__(256 * G) fc1_dw3_kg_kernel(const u16* __restrict__ dzw, const u16* __restrict__ a2w,
+                                                             int Kw, float* __restrict__ gW3, int tile_base, AdamArgs ad,
+                                                             int write_grad, int a2s, int a2c0, CollRole cr) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   if ((int)blockIdx.x < cr.nblk) {  // co-launched xGMI collective (xgmi_role.h)
     coll_role_run(cr, blockIdx.x);
     return;
   }
-  fc1_dw3_tile_kg2<ADAM>(tile_base + (int)blockIdx.x - cr.nblk, dzw, a2w, Kw, gW3, ad, write_grad, a2s, a2c0, smem);
+  fc1_dw3_tile_kg<ADAM, G>(tile_base + (int)blockIdx.x - cr.nblk, dzw, a2w, Kw, gW3, ad, write_grad, a2s, a2c0, smem);
 }
 
 // fc1_bwd: the dgrad tiles and every fc1_wgrad role (local batch) in one launch. The dgrad blocks
@@ -771,23 +777,41 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   if (grid == 0) return;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const u16 *pdz = (const u16*)dz.data_ptr(), *pa2 = (const u16*)a2.data_ptr(), *ph = (const u16*)h.data_ptr();
-  // dW3 tiles alone over a K of two or more 128-row chunks (all-gathered factors): the two-group
-  // tiles (MIHVD_WGRAD_KG2=0 keeps the 4-wave tiles)
+  // dW3 tiles alone over a K of two or more 128-row chunks (all-gathered factors): the K-split
+  // group tiles, 2 groups, or 4 from MIHVD_WGRAD_KG4_CHUNKS chunks on (default 5: the 8-rank
+  // factors; 0 = never); MIHVD_WGRAD_KG2=0 keeps the 4-wave tiles
   static const bool kg2 = [] {
     const char* e = getenv("MIHVD_WGRAD_KG2");
     return !(e && atoi(e) == 0);
   }();
+  static const int kg4_from = [] {
+    const char* e = getenv("MIHVD_WGRAD_KG4_CHUNKS");
+    return e ? atoi(e) : 5;
+  }();
   if (kg2 && roles == 1 && Kw > MAXB) {
-    const int lds = 2 * FB_LDS_WG;
-    if (ad != nullptr) {
-      set_max_lds(fc1_dw3_kg2_kernel<true>, lds);
-      fc1_dw3_kg2_kernel<true><<<grid, 512, lds, stream>>>(dzw, a2w, Kw, gW3.data_ptr<float>(), tile_base, *ad,
-                                                           write_grad ? 1 : 0, a2s, a2c0, cr);
-    } else {
-      set_max_lds(fc1_dw3_kg2_kernel<false>, lds);
-      fc1_dw3_kg2_kernel<false><<<grid, 512, lds, stream>>>(dzw, a2w, Kw, gW3.data_ptr<float>(), tile_base,
-                                                            AdamArgs{}, 1, a2s, a2c0, cr);
-    }
+    const int nch = (Kw + MAXB - 1) / MAXB;
+    auto run = [&](auto kt, auto ka, int groups) {
+      const int lds = groups * FB_LDS_WG;
+      if (ad != nullptr) {
+        set_max_lds(ka, lds);
+        ka<<<grid, 256 * groups, lds, stream>>>(dzw, a2w, Kw, gW3.data_ptr<float>(), tile_base, *ad,
+                                                write_grad ? 1 : 0, a2s, a2c0, cr);
+      } else {
+        set_max_lds(kt, lds);
+        kt<<<grid, 256 * groups, lds, stream>>>(dzw, a2w, Kw, gW3.data_ptr<float>(), tile_base, AdamArgs{}, 1,
+                                                a2s, a2c0, cr);
+      }
+    };
+    // four groups only for a row slice that fits the CUs one block each (the sharded optimizer's
+    // 1/N of the rows): over all 784 tiles the 1024-thread blocks cut occupancy (measured 22.3 ->
+    // 29.9 us at the 8-rank K), over the 8-rank slice they win (7.7 -> 7.2 us, with Adam 12.8 -> 11.4)
+    const int tiles = (int)(jt_hi - jt_lo) * (FC1_N / 64);
+    int ncu = 256, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (kg4_from > 0 && nch >= kg4_from && tiles <= ncu)
+      run(fc1_dw3_kg_kernel<false, 4>, fc1_dw3_kg_kernel<true, 4>, 4);
+    else run(fc1_dw3_kg_kernel<false, 2>, fc1_dw3_kg_kernel<true, 2>, 2);
     return;
   }
   // MIHVD_WGRAD_ADAM_OCC=4: registers capped for 4 blocks per CU (784 tiles resident at once)
