@@ -522,25 +522,30 @@ __global__ void __launch_bounds__(256, MINW) fc1_wgrad_kernel(
 // fc1_wgrad_block is reused; results differ from it in the last bits (the K sum is split) but every
 // rank and every row slice computes the same values. G = 4 pays where the chunk chain is long (the
 // 8-rank factors: 7 chunks -> 2 per group instead of 4).
-template <bool ADAM, int G>
+template <bool ADAM, int G, int NTW = 64>
 __device__ __forceinline__ void fc1_dw3_tile_kg(int tile, const u16* __restrict__ dzw, const u16* __restrict__ a2w,
                                                 int Kw, float* __restrict__ gW3, const AdamArgs& ad, int write_grad,
                                                 int a2s, int a2c0, u16* smem) {
   static_assert(G == 2 || G == 4, "fc1_dw3_tile_kg: 2 or 4 groups");
-  constexpr int U = 4 / G;  // sub-tiles (i, jj) finished by each group
+  static_assert(NTW == 64 || NTW == 32, "fc1_dw3_tile_kg: 64- or 32-feature tiles");
+  constexpr int SI = NTW / 32;                 // 16-feature sub-tile rows per wave (2 or 1)
+  constexpr int S = SI * 2;                    // sub-tiles (i, jj) per wave
+  constexpr int U = S / G > 0 ? S / G : 1;     // sub-tiles finished by each group (groups g*U >= S idle)
+  constexpr int NTILES = FC1_N / NTW;          // feature tiles per 64-row tile row
   const int t = threadIdx.x, g = t >> 8, th = t & 255, lane = th & 63, wave = th >> 6, lr = lane & 15, lg = lane >> 4;
   const int q = lr >> 2, p = lr & 3;
-  const int jt = tile >> 4, ntile = tile & 15;
-  const int j0 = jt * 64, n0 = ntile * 64;
-  u16* Zim = smem + g * (2 * MAXB * FB_TSTR);  // [128][72] rows k, cols n
+  const int jt = tile / NTILES, ntile = tile - jt * NTILES;
+  const int j0 = jt * 64, n0 = ntile * NTW;
+  u16* Zim = smem + g * (2 * MAXB * FB_TSTR);  // [128][72] rows k, cols n (NTW used)
   u16* Aim = Zim + MAXB * FB_TSTR;             // [128][72] rows k, cols j
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int wm = (wave >> 1) * (NTW / 2), wn = (wave & 1) * 32;
   const int nch = (Kw + MAXB - 1) / MAXB, nit = (nch + G - 1) / G;
   auto rows_of = [&](int c) { return c < nch ? min(MAXB, Kw - c * MAXB) : 0; };
-  f32x4 acc[2][2];
+  f32x4 acc[SI][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  TileLoad<256, (MAXB * 8 + 255) / 256, 8> lz, la;
+  for (int i = 0; i < SI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TileLoad<256, (MAXB * (NTW / 8) + 255) / 256, NTW / 8> lz;
+  TileLoad<256, (MAXB * 8 + 255) / 256, 8> la;
   {
     const int rows = rows_of(g);
     if (rows > 0) {
@@ -548,6 +553,7 @@ __device__ __forceinline__ void fc1_dw3_tile_kg(int tile, const u16* __restrict_
       la.load(a2w + (int64_t)g * MAXB * a2s + (j0 - a2c0), a2s, (rows + 31) & ~31, rows, th);
     }
   }
+  const bool fin = g * U < S;  // this group finishes sub-tiles
   float4 pp[U], mm[U], vv[U];  // Adam operands of this group's sub-tiles u = g*U + s (i = u >> 1, jj = u & 1)
   for (int it = 0; it < nit; ++it) {
     const int c = G * it + g;
@@ -559,7 +565,7 @@ __device__ __forceinline__ void fc1_dw3_tile_kg(int tile, const u16* __restrict_
     }
     __syncthreads();
     if constexpr (ADAM) {
-      if (it == 0) {
+      if (it == 0 && fin) {
 #pragma unroll
         for (int s2 = 0; s2 < U; ++s2) {
           const int u = g * U + s2, i = u >> 1, jj = u & 1;
@@ -576,32 +582,36 @@ __device__ __forceinline__ void fc1_dw3_tile_kg(int tile, const u16* __restrict_
       la.load(a2w + (int64_t)(c + G) * MAXB * a2s + (j0 - a2c0), a2s, (rn + 31) & ~31, rn, th);
     }
     for (int k0 = 0; k0 < Kpad; k0 += 32) {
-      bf16x8 af[2], bfv[2];
+      bf16x8 af[SI], bfv[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < SI; ++i) {
         const u16* zr = Zim + (k0 + 8 * lg + q) * FB_TSTR + wm + i * 16 + 4 * p;
         af[i] = frag_tr(zr, zr + 4 * FB_TSTR);
-        const u16* ar = Aim + (k0 + 8 * lg + q) * FB_TSTR + wn + i * 16 + 4 * p;
-        bfv[i] = frag_tr(ar, ar + 4 * FB_TSTR);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int jj = 0; jj < 2; ++jj) {
+        const u16* ar = Aim + (k0 + 8 * lg + q) * FB_TSTR + wn + jj * 16 + 4 * p;
+        bfv[jj] = frag_tr(ar, ar + 4 * FB_TSTR);
+      }
+#pragma unroll
+      for (int i = 0; i < SI; ++i)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mfma16(af[i], bfv[jj], acc[i][jj]);
     }
   }
-  // exchange: every group stores its four partial sub-tiles, then sums the groups' partials of its own
+  // exchange: every group stores its partial sub-tiles, then sums the groups' partials of its own
   __syncthreads();
-  f32x4* xr = reinterpret_cast<f32x4*>(smem);  // [group][256 threads][4 sub-tiles]
+  f32x4* xr = reinterpret_cast<f32x4*>(smem);  // [group][256 threads][S sub-tiles]
 #pragma unroll
-  for (int u = 0; u < 4; ++u) xr[(g * 256 + th) * 4 + u] = acc[u >> 1][u & 1];
+  for (int u = 0; u < S; ++u) xr[(g * 256 + th) * S + u] = acc[u >> 1][u & 1];
   __syncthreads();
+  if (!fin) return;
 #pragma unroll
   for (int s2 = 0; s2 < U; ++s2) {
     const int u = g * U + s2, jj = u & 1, i = u >> 1;
-    f32x4 sum = xr[th * 4 + u];
+    f32x4 sum = xr[th * S + u];
 #pragma unroll
-    for (int gg = 1; gg < G; ++gg) sum = sum + xr[(gg * 256 + th) * 4 + u];  // groups in order
+    for (int gg = 1; gg < G; ++gg) sum = sum + xr[(gg * 256 + th) * S + u];  // groups in order
     const int64_t o = (int64_t)(j0 + wn + jj * 16 + lr) * FC1_N + n0 + wm + i * 16 + 4 * lg;
     const float4 gv = make_float4(sum[0], sum[1], sum[2], sum[3]);
     if constexpr (ADAM) {
@@ -618,7 +628,7 @@ __device__ __forceinline__ void fc1_dw3_tile_kg(int tile, const u16* __restrict_
   }
 }
 
-template <bool ADAM, int G>
+template <bool ADAM, int G, int NTW = 64>
 __global__ void __launch_bounds__(256 * G) fc1_dw3_kg_kernel(const u16* __restrict__ dzw, const u16* __restrict__ a2w,
                                                              int Kw, float* __restrict__ gW3, int tile_base, AdamArgs ad,
                                                              int write_grad, int a2s, int a2c0, CollRole cr) {
@@ -627,7 +637,8 @@ __global__ void __launch_bounds__(256 * G) fc1_dw3_kg_kernel(const u16* __restri
     coll_role_run(cr, blockIdx.x);
     return;
   }
-  fc1_dw3_tile_kg<ADAM, G>(tile_base + (int)blockIdx.x - cr.nblk, dzw, a2w, Kw, gW3, ad, write_grad, a2s, a2c0, smem);
+  fc1_dw3_tile_kg<ADAM, G, NTW>(tile_base + (int)blockIdx.x - cr.nblk, dzw, a2w, Kw, gW3, ad, write_grad, a2s, a2c0,
+                                smem);
 }
 
 // fc1_bwd: the dgrad tiles and every fc1_wgrad role (local batch) in one launch. The dgrad blocks
@@ -809,6 +820,28 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
     int ncu = 256, dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    // 32-feature tiles (twice the blocks, each with half the MFMA work and half the Adam epilogue)
+    // when they still fit the CUs one block each: the 8-rank slice dW3 7.2 -> 6.3 us, dW3 + Adam
+    // 11.4 -> 9.0 us (MIHVD_WGRAD_NARROW=0 keeps the 64-feature tiles)
+    static const bool narrow = [] {
+      const char* e = getenv("MIHVD_WGRAD_NARROW");
+      return !(e && atoi(e) == 0);
+    }();
+    if (kg4_from > 0 && nch >= kg4_from && narrow && 2 * tiles <= ncu) {
+      const int grid32 = 2 * tiles + cr.nblk;
+      const int lds = 4 * FB_LDS_WG;
+      const int tb32 = (int)jt_lo * (FC1_N / 32);
+      if (ad != nullptr) {
+        set_max_lds(fc1_dw3_kg_kernel<true, 4, 32>, lds);
+        fc1_dw3_kg_kernel<true, 4, 32><<<grid32, 1024, lds, stream>>>(dzw, a2w, Kw, gW3.data_ptr<float>(), tb32, *ad,
+                                                                      write_grad ? 1 : 0, a2s, a2c0, cr);
+      } else {
+        set_max_lds(fc1_dw3_kg_kernel<false, 4, 32>, lds);
+        fc1_dw3_kg_kernel<false, 4, 32><<<grid32, 1024, lds, stream>>>(dzw, a2w, Kw, gW3.data_ptr<float>(), tb32,
+                                                                       AdamArgs{}, 1, a2s, a2c0, cr);
+      }
+      return;
+    }
     if (kg4_from > 0 && nch >= kg4_from && tiles <= ncu)
       run(fc1_dw3_kg_kernel<false, 4>, fc1_dw3_kg_kernel<true, 4>, 4);
     else run(fc1_dw3_kg_kernel<false, 2>, fc1_dw3_kg_kernel<true, 2>, 2);
