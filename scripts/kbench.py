@@ -117,6 +117,15 @@ def main():
             tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
             tr.gview("dense_1/bias"), 1, dz8, a28, tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:], st, 0.0, 0.9,
             0.999, 1e-8, 1.0, 0, False, 0, 7),
+        # the sharded xGMI plane's last launch at N=2 / N=4 (K = 200 / 400; 25 / 13 row tiles)
+        "fc1_wgrad_adam_k2x_slice": lambda: o.fc1_wgrad_adam(
+            tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
+            tr.gview("dense_1/bias"), 1, dz8[:2 * B], a28[:2 * B], tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:],
+            st, 0.0, 0.9, 0.999, 1e-8, 1.0, 0, False, 0, 25),
+        "fc1_wgrad_adam_k4x_slice": lambda: o.fc1_wgrad_adam(
+            tr.dz, tr.a2, tr.h, tr.dlog, tr.gview("dense/kernel"), tr.gview("dense/bias"), tr.gview("dense_1/kernel"),
+            tr.gview("dense_1/bias"), 1, dz8[:4 * B], a28[:4 * B], tr.params[W3:], tr.m[W3:], tr.v[W3:], sh[W3:],
+            st, 0.0, 0.9, 0.999, 1e-8, 1.0, 0, False, 0, 13),
         "adam_w3_slice8": lambda: o.adam_step(tr.params[W3:W3 + 7 * 65536], tr.grads[W3:W3 + 7 * 65536],
                                               tr.m[W3:W3 + 7 * 65536], tr.v[W3:W3 + 7 * 65536],
                                               sh[W3:W3 + 7 * 65536], st, 0, 0.0, 0.9, 0.999, 1e-8, 1.0, 0, 0),
