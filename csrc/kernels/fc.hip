@@ -789,15 +789,15 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const u16 *pdz = (const u16*)dz.data_ptr(), *pa2 = (const u16*)a2.data_ptr(), *ph = (const u16*)h.data_ptr();
   // dW3 tiles alone over a K of two or more 128-row chunks (all-gathered factors): the K-split
-  // group tiles, 2 groups, or 4 from MIHVD_WGRAD_KG4_CHUNKS chunks on (default 5: the 8-rank
-  // factors; 0 = never); MIHVD_WGRAD_KG2=0 keeps the 4-wave tiles
+  // group tiles, 2 groups, or 4 from MIHVD_WGRAD_KG4_CHUNKS chunks on (default 4: the 4- and
+  // 8-rank factors; 0 = never); MIHVD_WGRAD_KG2=0 keeps the 4-wave tiles
   static const bool kg2 = [] {
     const char* e = getenv("MIHVD_WGRAD_KG2");
     return !(e && atoi(e) == 0);
   }();
   static const int kg4_from = [] {
     const char* e = getenv("MIHVD_WGRAD_KG4_CHUNKS");
-    return e ? atoi(e) : 5;
+    return e ? atoi(e) : 4;
   }();
   if (kg2 && roles == 1 && Kw > MAXB) {
     const int nch = (Kw + MAXB - 1) / MAXB;
@@ -815,7 +815,8 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
     };
     // four groups only for a row slice that fits the CUs one block each (the sharded optimizer's
     // 1/N of the rows): over all 784 tiles the 1024-thread blocks cut occupancy (measured 22.3 ->
-    // 29.9 us at the 8-rank K), over the 8-rank slice they win (7.7 -> 7.2 us, with Adam 12.8 -> 11.4)
+    // 29.9 us at the 8-rank K), over the 8-rank slice they win (7.7 -> 7.2 us, with Adam 12.8 ->
+    // 11.4), over the 4-rank slice (13 row tiles, K = 400) dW3 + Adam 11.2 -> 9.6 us
     const int tiles = (int)(jt_hi - jt_lo) * (FC1_N / 64);
     int ncu = 256, dev = 0;
     (void)hipGetDevice(&dev);

@@ -608,7 +608,7 @@ def test_w3_tile_tail_matches_stored_dw3_tail(ops, monkeypatch, B):
         assert torch.equal(x0, x1), (name, (x0.float() - x1.float()).abs().max().item())
 
 
-@pytest.mark.parametrize("K", [200, 237, 513, 800])
+@pytest.mark.parametrize("K", [200, 237, 400, 513, 800])
 def test_fc1_wgrad_long_k_two_group_tiles(ops, K):
     """dW3 over a long K (the all-gathered factors of N ranks: Kw = N*B > 128) runs as K-split group
     tiles (K chunks split between two — or, from five chunks on, four — 4-wave groups, partial tiles
@@ -637,10 +637,15 @@ def test_fc1_wgrad_long_k_two_group_tiles(ops, K):
     assert ((full - ref).norm() / ref.norm()).item() < 1e-5
     part = wgrad(7, 14)
     assert not part[:448].any() and not part[896:].any()
-    if K <= 4 * 128:
+    # a 13-row-tile slice (the 4-rank shard: 208 64-feature tiles) takes the 64-feature group tiles
+    sl = wgrad(21, 34)
+    assert ((sl[1344:2176] - ref[1344:2176]).norm() / ref[1344:2176].norm()).item() < 1e-5
+    assert not sl[:1344].any() and not sl[2176:].any()
+    if K <= 3 * 128:
         assert torch.equal(part[448:896], full[448:896])  # same group count: bit for bit
+        assert torch.equal(sl[1344:2176], full[1344:2176])
     else:
-        # a slice of at most one tile per CU runs four K groups from five chunks on (the sharded
+        # a slice of at most one tile per CU runs four K groups from four chunks on (the sharded
         # optimizer's rows), all 784 tiles two: same rows, last bits may differ; both close to fp32
         assert ((part[448:896] - ref[448:896]).norm() / ref[448:896].norm()).item() < 1e-5
         assert torch.equal(part[448:896], wgrad(7, 14)[448:896])  # deterministic
