@@ -69,8 +69,10 @@ def test_fused_data_parallel_xgmi_two_ranks(tmp_path, gather):
     small-gradient reduction read the peer's region in place); gather=0: the gradient buckets over
     the staged xGMI allreduce (MIHVD_XGMI_ALLREDUCE=1). gloo only carries the IPC handle exchange."""
     _gpu()
+    # both ranks share this one GPU: a rank's spinning phase barrier can wait for the other process's
+    # kernels to be scheduled, so the device-side timeout is raised from 20 s (a timeout still fails)
     env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_XGMI_ALLREDUCE="1",
-               MIHVD_XGMI="on")
+               MIHVD_XGMI="on", MIHVD_XGMI_TIMEOUT_MS="60000")
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
