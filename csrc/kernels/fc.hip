@@ -828,7 +828,7 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
       const char* e = getenv("MIHVD_WGRAD_NARROW");
       return !(e && atoi(e) == 0);
     }();
-    if (kg4_from > 0 && nch >= kg4_from && narrow && 2 * tiles <= ncu) {
+    if (kg4_from > 0 && nch >= kg4_from && narrow && 2 * tiles + cr.nblk <= ncu) {
       const int grid32 = 2 * tiles + cr.nblk;
       const int lds = 4 * FB_LDS_WG;
       const int tb32 = (int)jt_lo * (FC1_N / 32);
@@ -843,7 +843,7 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
       }
       return;
     }
-    if (kg4_from > 0 && nch >= kg4_from && tiles <= ncu)
+    if (kg4_from > 0 && nch >= kg4_from && tiles + cr.nblk <= ncu)
       run(fc1_dw3_kg_kernel<false, 4>, fc1_dw3_kg_kernel<true, 4>, 4);
     else run(fc1_dw3_kg_kernel<false, 2>, fc1_dw3_kg_kernel<true, 2>, 2);
     return;

@@ -583,8 +583,10 @@ class FusedMNISTTrainer:
         r["a2_shard"] = xp.prepare_gather("a2", self.PH_A2, 3136 * 2, B, col_lo=lo * 128, col_hi=hi * 128, nblk=nb)
         r["a2_full"] = xp.prepare_gather("a2", self.PH_A2, 3136 * 2, B, nblk=nb)
         # small gradients: one-shot sum + their Adam update (1/size of Average = the Adam gradient
-        # scale) + the forward step bump, in fc1_wgrad's launch
-        r["small"] = xp.prepare_reduce("grads", self.PH_SMALL, self.gred, 1.0, nblk=64, adam=dict(
+        # scale) + the forward step bump, in fc1_wgrad's launch: 32 blocks of that launch's 512- or
+        # 1024-thread blocks, so with the 8-rank slice's 224 32-feature tiles every block of the
+        # launch is resident at once (one per CU)
+        r["small"] = xp.prepare_reduce("grads", self.PH_SMALL, self.gred, 1.0, nblk=32, adam=dict(
             p=self.params[h], m=self.m[h], v=self.v[h], shadow=self.shadow[h], state=self.state, lr=self.lr, b1=b1,
             b2=b2, eps=self.eps, grad_scale=1.0 / W, rule=self.rule))
         # the other ranks' updated W3 rows (sharded), in the next step's conv12_fwd launch, on the
