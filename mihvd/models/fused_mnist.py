@@ -251,6 +251,10 @@ class FusedMNISTTrainer:
         self.fuse_w3 = (os.environ.get("MIHVD_FUSE_W3_ADAM", "0") == "1" and not self.pipeline
                         and (not self.collectives or self.gather))
         self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when fused
+        # sharded factor-gather step over RCCL: dW3 of this rank's rows with Adam in the tile epilogue
+        # (the xGMI plane's form; the 8-rank slice 9.0 us vs 6.1 + 4.0 us for dW3 then adam_step,
+        # bit-identical: same tiles, same adam4). MIHVD_FUSE_W3_SLICE=0: the two launches
+        self.fuse_slice = os.environ.get("MIHVD_FUSE_W3_SLICE", "1") != "0"
         # MIHVD_FUSED_OPT=1 (default at world size 1): no separate optimizer launch. The dense/kernel
         # update (98 % of the optimizer's HBM traffic) streams in the tail of the conv2_bwd launch —
         # tail-only blocks on the CUs the conv roles leave idle, conv blocks joining as they finish —
@@ -540,7 +544,7 @@ class FusedMNISTTrainer:
         ar_done.record(side)
         b1, b2 = self.betas
         lo, hi = self._w3_tiles
-        if self.fuse_w3:
+        if self.fuse_w3 or (self.shard_w3 and self.fuse_slice and hi > lo):
             # dW3 summed over every rank's samples, Adam applied to W3 in the same tiles
             self._fc1_wgrad_w3_adam(1, self.dz_all, self.a2_all, lo, hi)
         elif hi > lo:
