@@ -10,9 +10,11 @@ RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment. Model: the reference's
 (:133). Data: synthetic 28×28 images resident on the device (no network for MNIST).
 
 Implementations:
-  fused  — mihvd's hand-written CDNA4 HIP kernels: bf16 MFMA forward/backward with fp32 master
-           weights, gradients written straight into the fusion buffer, RCCL allreduce on it,
-           fused TF1-Adam; the whole step (incl. the allreduce) replayed as one HIP graph.
+  fused  — mihvd's hand-written CDNA4 HIP kernels, gradients written straight into the fusion
+           buffer, RCCL collectives on it, TF1-Adam; the whole step (incl. the collectives) replayed
+           as one HIP graph. --precision fp32 (default, the reference's precision): exact fp32
+           operands on the fp32-input MFMAs (v_mfma_f32_16x16x4_f32 / 32x32x2_f32); --precision
+           bf16: bf16 MFMA operands with fp32 accumulation, master weights and optimizer state.
   torch  — stock PyTorch-ROCm ops (fp32) + mihvd DistributedOptimizer (bucketed RCCL allreduce) +
            TF1 Adam on the multi-tensor HIP kernel.
   torch-graph — the same step (data gather, forward, backward, bucket allreduces, FusedAdam with a
@@ -53,6 +55,10 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=0, help="fused: steps captured per HIP graph (0=auto)")
     ap.add_argument("--pool-batches", type=int, default=60, help="synthetic batches resident on device")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default=os.environ.get("MIHVD_PRECISION", "fp32"),
+                    help="fused: operand precision of the hand-written step. fp32 (default) = the reference's "
+                         "launched config (fp32 placeholders + AdamOptimizer, tensorflow_mnist.py:118-130) on the "
+                         "fp32-input MFMAs; bf16 = bf16 MFMA operands, fp32 accumulation/master weights")
     return ap.parse_args()
 
 
@@ -140,7 +146,7 @@ def make_fused_step(args, hvd, device):
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
     tr = FusedMNISTTrainer(batch_size=args.batch_size, lr=args.lr * hvd.size(), seed=42, device=device,
-                           compression=args.compression,
+                           compression=args.compression, precision=args.precision,
                            shard_optimizer=os.environ.get("MIHVD_SHARD_W3", "1") != "0")
     tr.broadcast(0)
     X, Y = synthetic_pool(args.pool_batches, args.batch_size, device, seed=hvd.rank())
@@ -158,7 +164,7 @@ def make_fused_step(args, hvd, device):
     def step(n=None):
         tr.run_graph(n)
 
-    return step, "bf16", tr
+    return step, args.precision, tr
 
 
 def main():

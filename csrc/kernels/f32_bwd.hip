@@ -1,0 +1,673 @@
+// Exact-fp32 backward kernels of the MNIST CNN (see f32_fwd.hip for the precision contract).
+//
+//   f32_fc1_bwd      one launch, three block roles:
+//                      dgrad: g2 = (dz W3^T) * [a2 > 0], routed through the pool argmax idx2 into
+//                             the full conv2 output gradient dY2 [B][14][14][64] (every element
+//                             written: value or zero), + per-block db2 partial rows
+//                      small: db3, dW4, db4
+//                      wgrad: dW3 = a2^T dz in 64x64 tiles              [MFMA 16x16x4 / 32x32x2]
+//   f32_conv2_bwd    one launch, two block roles:
+//                      dgrad: dA1 = dY2 (x) W2 (implicit GEMM, K = 25 taps x 64) over 16-pixel
+//                             tiles of the batch; conv1's pooled-ReLU mask; the conv1 weight
+//                             gradient of those pixels from the routed gradient (sparse: one 5x5
+//                             x-patch per pooled element) -> per-block partial rows
+//                      wgrad: dW2 partial slabs per (kernel row, 32-channel half, image group)
+//                                                                           [MFMA 16x16x4 / 32x32x2]
+//   f32_conv_reduce  dW2 = sum of slabs; dW1, db1, db2 = sums of the partial rows (fixed order:
+//                    deterministic, no atomics)
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+
+#include "f32_common.h"
+
+namespace mihvd {
+
+// ------------------------------------------------------------------------------------------ //
+// f32_fc1_bwd
+// ------------------------------------------------------------------------------------------ //
+constexpr int F1B_DS = 1028;                       // dz image row stride (floats)
+constexpr int F1B_LDS_DG = 16 * F1B_DS * 4;        // 65,792 B
+constexpr int F1B_LDS_WG = 2 * F32_MAXB * 64 * 4;  // 65,536 B
+constexpr int F1B_LDS = F1B_LDS_DG > F1B_LDS_WG ? F1B_LDS_DG : F1B_LDS_WG;
+constexpr int F1B_SMALL = 33, F1B_WGRAD = 784;
+
+// dgrad block: one pooling window jt (= 64 consecutive features j of the NHWC flatten) x 16 samples,
+// full K = 1024. Both operands are K-contiguous: A = this wave's 16 rows of W3 (float4 chunks
+// streamed from global, 8 chunks in flight), B = the block's dz rows from LDS. Block ids are
+// XCD-interleaved (xcd = bid & 7) so the sample groups of one window share an XCD L2 for W3.
+__device__ __forceinline__ void f32_fc1_dgrad_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
+                                                    const uint8_t* __restrict__ idx2, const float* __restrict__ w3,
+                                                    float* __restrict__ dY2, float* __restrict__ db2p, int B, int G,
+                                                    float* smf) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int xcd = bid & 7, slot = bid >> 3, mg = slot % G, jt = (slot / G) * 8 + xcd;
+  if (jt >= 49) return;
+  const int m0 = 16 * mg;
+  float* Ds = smf;  // [16][1028]
+  float4 dv[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int i = t + 256 * it, r = i >> 8, c = i & 255, m = m0 + r;
+    dv[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)min(m, B - 1) * 1024 + 4 * c), m < B);
+  }
+  const float* wr = w3 + (int64_t)(64 * jt + 16 * wave + lr) * 1024 + 4 * lg;
+  float4 wv[2][8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) wv[0][u] = *reinterpret_cast<const float4*>(wr + 16 * u);
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int i = t + 256 * it;
+    *reinterpret_cast<float4*>(Ds + (i >> 8) * F1B_DS + 4 * (i & 255)) = dv[it];
+  }
+  __syncthreads();
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  const float* dp = Ds + lr * F1B_DS + 4 * lg;
+#pragma unroll
+  for (int c8 = 0; c8 < 8; ++c8) {
+    if (c8 + 1 < 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wv[(c8 + 1) & 1][u] = *reinterpret_cast<const float4*>(wr + 16 * (8 * (c8 + 1) + u));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float4 bq = *reinterpret_cast<const float4*>(dp + 16 * (8 * c8 + u));
+      if (u & 1) acc1 = mfma4_q(wv[c8 & 1][u], bq, acc1);
+      else acc0 = mfma4_q(wv[c8 & 1][u], bq, acc0);
+    }
+  }
+  // C[row 4lg + i][col lr] = channel co + i of window jt, sample m0 + lr
+  const f32x4 acc = acc0 + acc1;
+  const int m = m0 + lr, mc = min(m, B - 1), co = 16 * wave + 4 * lg, j = 64 * jt + co;
+  const bool valid = m < B;
+  const float4 av = *reinterpret_cast<const float4*>(a2 + (int64_t)mc * 3136 + j);
+  const uint32_t ix = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc * 3136 + j);
+  const float ae[4] = {av.x, av.y, av.z, av.w};
+  float g[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = (valid && ae[i] > 0.f) ? acc[i] : 0.f;
+  float s[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s[i] = row_sum16(g[i]);  // over the 16 samples of the block
+  if (lr == 0)
+    *reinterpret_cast<float4*>(db2p + ((int64_t)mg * 49 + jt) * 64 + co) = make_float4(s[0], s[1], s[2], s[3]);
+  if (valid) {
+    const int py = jt / 7, px = jt - 7 * py;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (int)((ix >> (8 * i)) & 0xff) == d ? g[i] : 0.f;
+      const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
+      *reinterpret_cast<float4*>(dY2 + (((int64_t)m * 14 + y) * 14 + x) * 64 + co) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// Small reductions over the batch: db3 (16 blocks of 64 features), dW4 (16 blocks), db4 (1 block).
+__device__ __forceinline__ void f32_fc1_small_block(int bid, const float* __restrict__ dz, const float* __restrict__ h,
+                                                    const float* __restrict__ dlog, float* __restrict__ gb3,
+                                                    float* __restrict__ gW4, float* __restrict__ gb4, int B, float* smf) {
+  const int t = threadIdx.x, nn = t & 63, rg = t >> 6;
+  if (bid < 16) {
+    const int n = bid * 64 + nn;
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int b = rg * 32 + i;
+      v[i] = mask_f(dz[(int64_t)min(b, B - 1) * 1024 + n], b < B);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) s += v[i];
+    smf[rg * 64 + nn] = s;
+    __syncthreads();
+    if (t < 64) gb3[n] = (smf[nn] + smf[64 + nn]) + (smf[128 + nn] + smf[192 + nn]);
+    return;
+  }
+  if (bid < 32) {
+    const int r = bid - 16, n = r * 64 + nn;
+    float* dls = smf;                // [128][10]
+    float* red = smf + F32_MAXB * 10;  // [4][64][10]
+    float hv[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int b = rg * 32 + i;
+      hv[i] = mask_f(h[(int64_t)min(b, B - 1) * 1024 + n], b < B);
+    }
+    for (int i = t; i < F32_MAXB * 10; i += 256) dls[i] = i < B * 10 ? dlog[i] : 0.f;
+    __syncthreads();
+    float s[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) s[c] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+#pragma unroll
+      for (int c = 0; c < 10; ++c) s[c] = fmaf(hv[i], dls[(rg * 32 + i) * 10 + c], s[c]);
+#pragma unroll
+    for (int c = 0; c < 10; ++c) red[(rg * 64 + nn) * 10 + c] = s[c];
+    __syncthreads();
+    for (int i = t; i < 640; i += 256) {
+      const int n2 = i / 10, c = i - n2 * 10;
+      gW4[(r * 64 + n2) * 10 + c] =
+          (red[n2 * 10 + c] + red[(64 + n2) * 10 + c]) + (red[(128 + n2) * 10 + c] + red[(192 + n2) * 10 + c]);
+    }
+    return;
+  }
+  // db4: thread = (class c, row group of 6)
+  const int c = t % 10, gq = t / 10;
+  float s = 0.f;
+  if (gq < 25) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int b = gq * 6 + i;
+      s += mask_f(dlog[min(b, B - 1) * 10 + c], b < B);
+    }
+  }
+  smf[t] = s;
+  __syncthreads();
+  if (t < 10) {
+    float tot = 0.f;
+    for (int q = 0; q < 25; ++q) tot += smf[q * 10 + t];
+    gb4[t] = tot;
+  }
+}
+
+// wgrad block: the 64x64 tile (jt, ntile) of dW3 = a2^T dz over K = the batch. Both operands are
+// K-strided (sample rows), so the tile runs on v_mfma_f32_32x32x2_f32, whose A and B lanes 0-31 /
+// 32-63 read 32 consecutive floats of one sample row each (ds_read_b32, conflict-free without
+// padding). 4 waves x one 32x32 sub-tile; output features n on the MFMA row axis so a lane's four
+// consecutive accumulator rows are one float4 of a dW3 row.
+__device__ __forceinline__ void f32_fc1_wgrad_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
+                                                    float* __restrict__ gW3, int B, float* smf) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int jt = bid >> 4, ntile = bid & 15, j0 = 64 * jt, n0 = 64 * ntile;
+  float* A2s = smf;                   // [128][64] rows b, cols j
+  float* DZs = smf + F32_MAXB * 64;   // [128][64] rows b, cols n
+  const int Kp = (B + 1) & ~1, nchk = Kp * 16;
+  float4 va[8], vz[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int i = min(t + 256 * it, nchk - 1), r = i >> 4, c = i & 15, rc = min(r, B - 1);
+    va[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)rc * 3136 + j0 + 4 * c), r < B);
+    vz[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)rc * 1024 + n0 + 4 * c), r < B);
+  }
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int i = t + 256 * it;
+    if (i < nchk) {
+      *reinterpret_cast<float4*>(A2s + 4 * i) = va[it];
+      *reinterpret_cast<float4*>(DZs + 4 * i) = vz[it];
+    }
+  }
+  __syncthreads();
+  const int wn = wave & 1, wj = wave >> 1, l32 = lane & 31, hh = lane >> 5;
+  const float* ap = DZs + hh * 64 + 32 * wn + l32;  // A[n][k] = dz[k][n]
+  const float* bp = A2s + hh * 64 + 32 * wj + l32;  // B[k][j] = a2[k][j]
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int ns = Kp >> 1;
+#pragma unroll 8
+  for (int s = 0; s < ns; ++s) acc = mfma32(ap[s * 128], bp[s * 128], acc);
+  const int j = j0 + 32 * wj + l32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<float4*>(gW3 + (int64_t)j * 1024 + n0 + 32 * wn + 8 * g + 4 * hh) =
+        make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+}
+
+__global__ void __launch_bounds__(256) f32_fc1_bwd_kernel(
+    const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
+    const float* __restrict__ h, const float* __restrict__ dlog, const float* __restrict__ w3, float* __restrict__ dY2,
+    float* __restrict__ db2p, float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4,
+    float* __restrict__ gb4, int B, int G, int n_dg) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  int bid = blockIdx.x;
+  if (bid < n_dg) {
+    f32_fc1_dgrad_block(bid, dz, a2, idx2, w3, dY2, db2p, B, G, smf);
+    return;
+  }
+  bid -= n_dg;
+  if (bid < F1B_SMALL) {
+    f32_fc1_small_block(bid, dz, h, dlog, gb3, gW4, gb4, B, smf);
+    return;
+  }
+  f32_fc1_wgrad_block(bid - F1B_SMALL, dz, a2, gW3, B, smf);
+}
+
+// ------------------------------------------------------------------------------------------ //
+// f32_conv2_bwd (512-thread blocks)
+// ------------------------------------------------------------------------------------------ //
+constexpr int CBF_PS = 68, CBF_RS = 18 * CBF_PS, CBF_MAXR = 18;
+constexpr int CBF_IMG = CBF_MAXR * CBF_RS;            // floats: tall padded dY2 rows
+constexpr int CBF_WB = 32 * 68;                       // one W2 tap slice [32 ci][68]
+constexpr int CBF_XIM = 2 * 1024;                     // two padded x images [32][32]
+constexpr int CBF_PW = 8 * 26 * 16;                   // per-wave conv1 partials
+constexpr int CBF_LDS_DG = (CBF_IMG + 2 * CBF_WB + CBF_XIM + CBF_PW) * 4;   // 127,040 B
+constexpr int CBF_A1S = 14 * 18 * 32, CBF_DYS = 196 * 32, CBF_WBUF = CBF_A1S + CBF_DYS;
+constexpr int CBF_LDS_WG = 2 * CBF_WBUF * 4;                                // 114,688 B
+constexpr int CBF_LDS = CBF_LDS_DG > CBF_LDS_WG ? CBF_LDS_DG : CBF_LDS_WG;
+constexpr int CBF_MAXCH = (CBF_MAXR * 18 * 16 + 511) / 512;                 // dY2 chunks per thread
+constexpr int CBF_IG = 4;                                                   // images per wgrad block
+constexpr int CP_F32 = 832;                                                 // [dW1 (800) | db1 (32)]
+static_assert(CBF_LDS <= 163840, "f32_conv2_bwd LDS");
+static_assert(4 * 2 * 7 * 64 * 16 <= CBF_IMG * 4, "dgrad partial exchange fits the dY2 image");
+static_assert(4 * 5 * 4 * 64 * 16 <= CBF_LDS_WG, "wgrad partial exchange fits the staging buffers");
+
+// dgrad role. Pixels of the batch (flattened [B][196], raster order) in 16-pixel tiles; block owns
+// tiles [bid TPB, (bid+1) TPB). dA1[p][ci] = sum_{tap, co} dY2pad[p + (4 - kh, 4 - kw)][co] W2[tap][ci][co]:
+// A = the routed gradient (tall padded image rows in LDS, co contiguous -> float4), B = the W2 tap
+// slice read as [ci][co] (co contiguous -> float4): both K-contiguous in their natural layouts.
+// 8 waves: wave w = ci half (w & 1) x co quarter (w >> 1) of K; the four co-quarter partials are
+// summed through LDS before the epilogue.
+template <int TPB>
+__device__ __forceinline__ void f32_conv2_dgrad_block(
+    int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
+    const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
+    const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf) {
+  float* dimg = smf;
+  float* wbuf = smf + CBF_IMG;
+  float* xim = wbuf + 2 * CBF_WB;
+  float* pw = xim + CBF_XIM;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int np = 196 * B, T0 = bid * TPB;
+  const int P0 = 16 * T0, P1 = min(16 * (T0 + TPB), np) - 1;
+  const int b0 = P0 / 196, b1i = P1 / 196;
+  const int R0 = 18 * b0 + (P0 - 196 * b0) / 14, R1 = 18 * b1i + (P1 - 196 * b1i) / 14 + 5;
+  const int nch = (R1 - R0) * 288;  // 18 pixels x 16 float4
+  // 1. loads: tap-0 weights, the dY2 rows, the (at most two) x images
+  float4 wr = *reinterpret_cast<const float4*>(w2 + (t >> 4) * 64 + (t & 15) * 4);
+  float4 iv[CBF_MAXCH];
+#pragma unroll
+  for (int it = 0; it < CBF_MAXCH; ++it) {
+    const int i = min(t + 512 * it, nch - 1);
+    const int rr = i / 288, rem = i - rr * 288, c = rem >> 4, ch = rem & 15;
+    const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
+    const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+    const float4 v = *reinterpret_cast<const float4*>(
+        dY2 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 64 + ch * 4);
+    iv[it] = mask_f4(v, in);
+  }
+  float xv[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int i = t + 512 * it, s = i >> 10, pix = i & 1023, Y = (pix >> 5) - 2, X = (pix & 31) - 2;
+    const int bb = min(b0 + s, B - 1);
+    int row = bb;
+    if (rows != nullptr) {
+      const int64_t step = state ? state[ST_FWD] : 0;
+      row = rows[(int)((step * (int64_t)B + bb) % n_pool)];
+    }
+    const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
+    xv[it] = mask_f(x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
+  }
+#pragma unroll
+  for (int it = 0; it < CBF_MAXCH; ++it) {
+    const int i = t + 512 * it;
+    if (i < nch) {
+      const int rr = i / 288, rem = i - rr * 288;
+      *reinterpret_cast<float4*>(dimg + (rr * 18 + (rem >> 4)) * CBF_PS + (rem & 15) * 4) = iv[it];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
+  *reinterpret_cast<float4*>(wbuf + (t >> 4) * CBF_PS + (t & 15) * 4) = wr;
+  const int nt = wave & 1, cq = wave >> 1;
+  int abase[TPB];
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) {
+    const int P = min(16 * (T0 + i) + lr, np - 1);
+    const int bb = P / 196, p = P - 196 * bb, py = p / 14, px = p - 14 * py;
+    abase[i] = ((18 * bb + py - R0) * 18 + px) * CBF_PS + 16 * cq + 4 * lg;
+  }
+  f32x4 acc[TPB];
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  const float* wq = wbuf + (16 * nt + lr) * CBF_PS + 16 * cq + 4 * lg;
+  for (int tap = 0; tap < 25; ++tap) {
+    if (tap + 1 < 25) wr = *reinterpret_cast<const float4*>(w2 + (tap + 1) * 2048 + (t >> 4) * 64 + (t & 15) * 4);
+    const int kh = tap / 5, kw = tap - 5 * kh;
+    const int aoff = ((4 - kh) * 18 + (4 - kw)) * CBF_PS;
+    const float4 bq = *reinterpret_cast<const float4*>(wq + (tap & 1) * CBF_WB);
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) {
+      const float4 a = *reinterpret_cast<const float4*>(dimg + abase[i] + aoff);
+      acc[i] = mfma4_q(a, bq, acc[i]);
+    }
+    if (tap + 1 < 25)
+      *reinterpret_cast<float4*>(wbuf + ((tap + 1) & 1) * CBF_WB + (t >> 4) * CBF_PS + (t & 15) * 4) = wr;
+    __syncthreads();
+  }
+  // 2. sum the four co-quarter partials (the dY2 image is dead now)
+  f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) red[((cq * 2 + nt) * TPB + i) * 64 + lane] = acc[i];
+  __syncthreads();
+  // 3. epilogue: (nt, tile) pairs p = wave, wave + 8, ...: mask -> g1, the conv1 weight gradient of
+  //    the routed g1 (one 5x5 patch of x per pooled element), db1
+  float s25[26];
+#pragma unroll
+  for (int e = 0; e < 26; ++e) s25[e] = 0.f;
+  const int ci = 16 * nt + lr;
+  for (int p = wave; p < 2 * TPB; p += 8) {  // wave-uniform; p & 1 == nt
+    const int i = p >> 1;
+    const f32x4 sum = ((red[((0 * 2 + nt) * TPB + i) * 64 + lane] + red[((1 * 2 + nt) * TPB + i) * 64 + lane]) +
+                       red[((2 * 2 + nt) * TPB + i) * 64 + lane]) +
+                      red[((3 * 2 + nt) * TPB + i) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int P = 16 * (T0 + i) + 4 * lg + r;
+      if (P < np) {
+        const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
+        const int64_t o = (int64_t)P * 32 + ci;
+        const float g = a1[o] > 0.f ? sum[r] : 0.f;
+        const int ix = idx1[o];
+        const float* xs = xim + (bb - b0) * 1024 + (2 * py + (ix >> 1)) * 32 + 2 * px + (ix & 1);
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) s25[kh * 5 + kw] = fmaf(g, xs[kh * 32 + kw], s25[kh * 5 + kw]);
+        s25[25] += g;
+      }
+    }
+  }
+  // 4. sum over the four lane groups (same channel), then over the four waves of each ci half
+#pragma unroll
+  for (int e = 0; e < 26; ++e) {
+    float v = s25[e];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    s25[e] = v;
+  }
+  if (lg == 0) {
+#pragma unroll
+    for (int e = 0; e < 26; ++e) pw[(wave * 26 + e) * 16 + lr] = s25[e];
+  }
+  __syncthreads();
+  for (int q = t; q < CP_F32; q += 512) {
+    const int e = q >> 5, c = q & 31, h = c >> 4, l = c & 15;
+    const float v = (pw[((h + 0) * 26 + e) * 16 + l] + pw[((h + 2) * 26 + e) * 16 + l]) +
+                    (pw[((h + 4) * 26 + e) * 16 + l] + pw[((h + 6) * 26 + e) * 16 + l]);
+    cpart[(int64_t)bid * CP_F32 + q] = v;  // q = tap * 32 + ci (dW1, HWIO) or 800 + ci (db1)
+  }
+}
+
+// wgrad role: dW2[kh][kw][ci][co] over the images of one group, kernel row kh and output-channel
+// half ch. M = 32 co (A = dY2[q][co], the MFMA row axis, so a lane's four accumulator rows are a
+// float4 of the HWIO slab), N = 32 ci per kw (five accumulator tiles), K = pixels q (two per MFMA).
+// Every operand read is a ds_read_b32 of 32 consecutive floats (conflict-free, no padding).
+// Per image: a1 padded rows kh..kh+13 [14][18][32] and the dY2 channel half [196][32], register-
+// staged double buffering (the next image's loads are in flight while this one is multiplied).
+// 8 waves split the K steps (w, w + 8, ...); their partial tiles are summed through LDS.
+__device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
+                                                      const float* __restrict__ a1, float* __restrict__ slab, int B,
+                                                      float* smf) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
+  const int img0 = CBF_IG * grp, nimg = min(CBF_IG, B - img0);
+  auto load_img = [&](int b, float4 (&v)[7]) {
+#pragma unroll
+    for (int it = 0; it < 7; ++it) {
+      const int i = t + 512 * it;  // < 3584 = 2016 a1 chunks + 1568 dY2 chunks
+      if (i < 2016) {
+        const int ly = i / 144, r2 = i - 144 * ly, c = r2 >> 3, q4 = r2 & 7;
+        const int y = ly + kh - 2, xx = c - 2;
+        const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+        v[it] = mask_f4(*reinterpret_cast<const float4*>(
+                            a1 + (((int64_t)b * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + 4 * q4), in);
+      } else {
+        const int j = i - 2016, q = j >> 3, q4 = j & 7;
+        v[it] = *reinterpret_cast<const float4*>(dY2 + ((int64_t)b * 196 + q) * 64 + 32 * ch + 4 * q4);
+      }
+    }
+  };
+  auto store_img = [&](float* buf, const float4 (&v)[7]) {
+#pragma unroll
+    for (int it = 0; it < 7; ++it) {
+      const int i = t + 512 * it;
+      // a1 chunk i -> A1s[(ly*18 + c)*32 + 4 q4] = buf + 4 i; dY2 chunk j -> DYs[q*32 + 4 q4] = buf + A1S + 4 j
+      *reinterpret_cast<float4*>(buf + 4 * i) = v[it];
+    }
+  };
+  f32x16 acc[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
+  float4 v[7];
+  load_img(img0, v);
+  store_img(smf, v);
+  __syncthreads();
+  for (int n = 0; n < nimg; ++n) {
+    const float* buf = smf + (n & 1) * CBF_WBUF;
+    if (n + 1 < nimg) load_img(img0 + n + 1, v);
+    const float* A1s = buf;
+    const float* DYs = buf + CBF_A1S;
+    for (int s = wave; s < 98; s += 8) {  // K step s: pixels 2s (lanes 0-31) and 2s + 1 (32-63)
+      const int q = 2 * s + hh, qy = q / 14, qx = q - 14 * qy;
+      const float a = DYs[q * 32 + l32];
+      const float* bp = A1s + (qy * 18 + qx) * 32 + l32;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(a, bp[kw * 32], acc[kw]);
+    }
+    if (n + 1 < nimg) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
+    __syncthreads();
+  }
+  // partial exchange: [slot][kw][g][lane] float4, two rounds (waves 4-7 -> 0-3, then 0-3 -> all)
+  float4* xr = reinterpret_cast<float4*>(smf);
+  if (wave >= 4) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        xr[(((wave - 4) * 5 + kw) * 4 + g) * 64 + lane] =
+            make_float4(acc[kw][4 * g], acc[kw][4 * g + 1], acc[kw][4 * g + 2], acc[kw][4 * g + 3]);
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 o = xr[((wave * 5 + kw) * 4 + g) * 64 + lane];
+        acc[kw][4 * g] += o.x;
+        acc[kw][4 * g + 1] += o.y;
+        acc[kw][4 * g + 2] += o.z;
+        acc[kw][4 * g + 3] += o.w;
+      }
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        xr[((wave * 5 + kw) * 4 + g) * 64 + lane] =
+            make_float4(acc[kw][4 * g], acc[kw][4 * g + 1], acc[kw][4 * g + 2], acc[kw][4 * g + 3]);
+  }
+  __syncthreads();
+  for (int it = t; it < 1280; it += 512) {
+    const int kw = it >> 8, g = (it >> 6) & 3, ln = it & 63;
+    const float4 a = xr[((0 * 5 + kw) * 4 + g) * 64 + ln], b = xr[((1 * 5 + kw) * 4 + g) * 64 + ln];
+    const float4 c = xr[((2 * 5 + kw) * 4 + g) * 64 + ln], d = xr[((3 * 5 + kw) * 4 + g) * 64 + ln];
+    const float4 s = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                                 (a.w + b.w) + (c.w + d.w));
+    const int tap = kh * 5 + kw, ci = ln & 31, co = 32 * ch + 8 * g + 4 * (ln >> 5);
+    *reinterpret_cast<float4*>(slab + (int64_t)grp * 51200 + (tap * 32 + ci) * 64 + co) = s;
+  }
+}
+
+template <int TPB>
+__global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
+    const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
+    const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
+    const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const int bid = blockIdx.x;
+  if (bid < n_dg) {
+    f32_conv2_dgrad_block<TPB>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
+    return;
+  }
+  f32_conv2_wgrad_block(bid - n_dg, dY2, a1, slab, B, smf);
+}
+
+// ------------------------------------------------------------------------------------------ //
+// f32_conv_reduce: blocks [0, 50): dW2 (12,800 float4 = sum over the G slabs); [50, 63): dW1/db1
+// (64 elements x 4 row parts of the dgrad blocks' partial rows); 63: db2 (64 channels x 4 parts of
+// the fc1 dgrad blocks' rows).
+// ------------------------------------------------------------------------------------------ //
+__global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __restrict__ slab, int G,
+                                                              const float* __restrict__ cpart, int ncp,
+                                                              const float* __restrict__ db2p, int ndb,
+                                                              float* __restrict__ gW2, float* __restrict__ gW1,
+                                                              float* __restrict__ gb1, float* __restrict__ gb2) {
+  __shared__ float red[256];
+  const int bid = blockIdx.x, t = threadIdx.x;
+  if (bid < 50) {
+    const int i = bid * 256 + t;
+    float4 s = reinterpret_cast<const float4*>(slab)[i];
+    for (int g = 1; g < G; ++g) {
+      const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)g * 51200)[i];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    reinterpret_cast<float4*>(gW2)[i] = s;
+    return;
+  }
+  const int e = t & 63, part = t >> 6;
+  float s = 0.f;
+  if (bid < 63) {
+    const int q = (bid - 50) * 64 + e;  // 0..831
+    for (int r = part; r < ncp; r += 4) s += cpart[(int64_t)r * CP_F32 + q];
+    red[t] = s;
+    __syncthreads();
+    if (t < 64) {
+      const float v = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
+      if (q < 800) gW1[q] = v;
+      else gb1[q - 800] = v;
+    }
+    return;
+  }
+  for (int r = part; r < ndb; r += 4) s += db2p[(int64_t)r * 64 + e];
+  red[t] = s;
+  __syncthreads();
+  if (t < 64) gb2[e] = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
+}
+
+// ------------------------------------------------------------------------------------------ //
+// host wrappers
+// ------------------------------------------------------------------------------------------ //
+static void chk_f32(const at::Tensor& t, int64_t numel, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dtype() == at::kFloat && t.is_contiguous() && t.numel() == numel, what,
+              ": expected a contiguous fp32 device tensor of ", numel, " elements");
+}
+
+int64_t f32_db2_rows(int64_t B) { return 49 * ((B + 15) / 16); }
+int64_t f32_wgrad_groups(int64_t B) { return (B + CBF_IG - 1) / CBF_IG; }
+static int conv2b_tpb(int B) {
+  const int nt = (196 * B + 15) / 16;
+  return std::min(7, std::max(1, (nt + 255) / 256));
+}
+int64_t f32_dgrad_blocks(int64_t B) {
+  const int tpb = conv2b_tpb((int)B), nt = (196 * (int)B + 15) / 16;
+  return (nt + tpb - 1) / tpb;
+}
+
+void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
+                 const at::Tensor& dlog, const at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
+                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4) {
+  const int B = dz.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_bwd: batch 1..128");
+  chk_f32(dz, (int64_t)B * 1024, "f32_fc1_bwd: dz");
+  chk_f32(a2, (int64_t)B * 3136, "f32_fc1_bwd: a2");
+  TORCH_CHECK(idx2.dtype() == at::kByte && idx2.numel() == (int64_t)B * 3136 && idx2.is_contiguous(), "f32_fc1_bwd: idx2");
+  chk_f32(h, (int64_t)B * 1024, "f32_fc1_bwd: h");
+  chk_f32(dlog, (int64_t)B * 10, "f32_fc1_bwd: dlog");
+  chk_f32(w3, 3136 * 1024, "f32_fc1_bwd: w3");
+  chk_f32(dY2, (int64_t)B * 196 * 64, "f32_fc1_bwd: dY2");
+  chk_f32(db2p, f32_db2_rows(B) * 64, "f32_fc1_bwd: db2 partial rows");
+  chk_f32(gW3, 3136 * 1024, "f32_fc1_bwd: gW3");
+  chk_f32(gb3, 1024, "f32_fc1_bwd: gb3");
+  chk_f32(gW4, 10240, "f32_fc1_bwd: gW4");
+  chk_f32(gb4, 10, "f32_fc1_bwd: gb4");
+  const int G = (B + 15) / 16, n_dg = 56 * G;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  static bool attr = [] {
+    hipFuncSetAttribute((const void*)f32_fc1_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, F1B_LDS);
+    return true;
+  }();
+  (void)attr;
+  f32_fc1_bwd_kernel<<<n_dg + F1B_SMALL + F1B_WGRAD, 256, F1B_LDS, stream>>>(
+      dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(), dlog.data_ptr<float>(),
+      w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(), gW3.data_ptr<float>(), gb3.data_ptr<float>(),
+      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg);
+}
+
+void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
+                   const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                   at::Tensor& cpart, at::Tensor& slab) {
+  const int B = a1.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv2_bwd: batch 1..128");
+  chk_f32(dY2, (int64_t)B * 196 * 64, "f32_conv2_bwd: dY2");
+  chk_f32(w2, 51200, "f32_conv2_bwd: w2");
+  chk_f32(a1, (int64_t)B * 6272, "f32_conv2_bwd: a1");
+  TORCH_CHECK(idx1.dtype() == at::kByte && idx1.numel() == (int64_t)B * 6272 && idx1.is_contiguous(), "f32_conv2_bwd: idx1");
+  TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv2_bwd: x");
+  const int n_dg = (int)f32_dgrad_blocks(B), tpb = conv2b_tpb(B);
+  chk_f32(cpart, (int64_t)n_dg * CP_F32, "f32_conv2_bwd: cpart [dgrad blocks][832]");
+  const int ngrp = (int)f32_wgrad_groups(B);
+  chk_f32(slab, (int64_t)ngrp * 51200, "f32_conv2_bwd: slab [groups][51200]");
+  const int n_pool = x.size(0);
+  const int* rp = nullptr;
+  if (rows.has_value() && rows->defined()) {
+    TORCH_CHECK(rows->dtype() == at::kInt && rows->numel() == n_pool, "f32_conv2_bwd: rows must be int32 [n_pool]");
+    rp = rows->data_ptr<int>();
+  } else {
+    TORCH_CHECK(n_pool >= B, "f32_conv2_bwd: x has fewer rows than the batch");
+  }
+  const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  // host check of the dgrad blocks' row spans (the LDS image) and image count (<= 2)
+  for (int blk = 0; blk < n_dg; ++blk) {
+    const int P0 = 16 * blk * tpb, P1 = std::min(16 * (blk + 1) * tpb, 196 * B) - 1;
+    const int r0 = 18 * (P0 / 196) + (P0 % 196) / 14, r1 = 18 * (P1 / 196) + (P1 % 196) / 14 + 5;
+    TORCH_CHECK(r1 - r0 <= CBF_MAXR && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS image");
+  }
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  auto launch = [&](auto kern) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, CBF_LDS);
+    kern<<<n_dg + 10 * ngrp, 512, CBF_LDS, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
+                                                     idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
+                                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, n_dg);
+  };
+  switch (tpb) {
+    case 1: launch(f32_conv2_bwd_kernel<1>); break;
+    case 2: launch(f32_conv2_bwd_kernel<2>); break;
+    case 3: launch(f32_conv2_bwd_kernel<3>); break;
+    case 4: launch(f32_conv2_bwd_kernel<4>); break;
+    case 5: launch(f32_conv2_bwd_kernel<5>); break;
+    case 6: launch(f32_conv2_bwd_kernel<6>); break;
+    default: launch(f32_conv2_bwd_kernel<7>); break;
+  }
+}
+
+void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,
+                     at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2) {
+  TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() % 51200 == 0 && slab.numel() > 0, "f32_conv_reduce: slab");
+  TORCH_CHECK(cpart.dtype() == at::kFloat && cpart.numel() % CP_F32 == 0 && cpart.numel() > 0, "f32_conv_reduce: cpart");
+  TORCH_CHECK(db2p.dtype() == at::kFloat && db2p.numel() % 64 == 0 && db2p.numel() > 0, "f32_conv_reduce: db2p");
+  chk_f32(gW2, 51200, "f32_conv_reduce: gW2");
+  chk_f32(gW1, 800, "f32_conv_reduce: gW1");
+  chk_f32(gb1, 32, "f32_conv_reduce: gb1");
+  chk_f32(gb2, 64, "f32_conv_reduce: gb2");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  f32_conv_reduce_kernel<<<64, 256, 0, stream>>>(slab.data_ptr<float>(), (int)(slab.numel() / 51200),
+                                                 cpart.data_ptr<float>(), (int)(cpart.numel() / CP_F32),
+                                                 db2p.data_ptr<float>(), (int)(db2p.numel() / 64),
+                                                 gW2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(),
+                                                 gb2.data_ptr<float>());
+}
+
+}  // namespace mihvd

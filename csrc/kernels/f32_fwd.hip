@@ -1,0 +1,505 @@
+// Exact-fp32 forward kernels of the MNIST CNN (horovod/tensorflow_mnist.py:38-73).
+//
+// The reference's launched entrypoint trains in fp32 — fp32 placeholders (:118-121) and
+// AdamOptimizer (:130) on fp32 variables — so this step keeps every operand fp32. GEMM-shaped work
+// runs on the fp32-input matrix cores: v_mfma_f32_16x16x4_f32 (one fp32 A and B value per lane,
+// exact products, fp32 accumulation; gfx950 has no reduced-precision xf32 form). Activations,
+// gradients, weights and optimizer state are fp32 throughout.
+//
+// Operand convention (f32_common.h): both operands of a 16x16x4 MFMA are read as float4 chunks of
+// 4 consecutive k per lane where the tensor is K-contiguous; lane group g (= lane >> 4) holds
+// k = 4g + j in element j, and the four MFMAs of the chunk use elements j = 0..3. The same k order
+// on both operands makes the chunk's 16-deep dot product exact (only the fp32 summation order
+// differs from a sequential loop).
+//
+//   f32_conv1_fwd  conv1 (K = 25 taps in 7 MFMAs, x in LDS) + bias + ReLU + 2x2 pool/argmax
+//   f32_conv2_fwd  conv2 over 16-pixel tiles of the whole batch (pool-window-major rows), ~one
+//                  block per CU; a1 rows staged once, W2 streamed tap by tap (double-buffered)
+//   f32_fc1_fwd    split-K (14 slices of 224) partial slabs; W3 fragments held in registers
+//   f32_head       slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+
+#include "f32_common.h"
+
+namespace mihvd {
+
+// ------------------------------------------------------------------------------------------ //
+// conv1: x rows [784] fp32 -> a1 [B][14][14][32] fp32 + argmax idx1 (u8)
+// grid (4, B): block q of an image owns the 16-row tiles [13q, 13q + 13) of its 49 (4 pooling
+// windows per tile, pool-window-major: row m = 4 * window + d, d = 2 * dy + dx). 4 waves, wave w:
+// tiles 13q + w, +4, ... . A = im2col(x) gathered from the padded image in LDS (one ds_read_b32
+// per MFMA), B = W1 in registers (k = 4s + lane group, 25 taps zero-padded to 28).
+// ------------------------------------------------------------------------------------------ //
+__global__ void __launch_bounds__(256) f32_conv1_kernel(
+    const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
+    const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ a1, uint8_t* __restrict__ idx1,
+    int B) {
+  __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
+  const int q = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  int row = b;
+  if (rows != nullptr) {
+    const int64_t step = state ? state[ST_FWD] : 0;
+    row = rows[(int)((step * (int64_t)B + b) % n_pool)];
+  }
+  const float* xi = x + (int64_t)row * 784;
+  float xv[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int i = t + 256 * it, Y = (i >> 5) - 2, X = (i & 31) - 2;
+    const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
+    xv[it] = mask_f(xi[in ? Y * 28 + X : 0], in);
+  }
+  float wb[2][7];
+  int toff[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    const int k = 4 * s + lg, kc = min(k, 24);
+    toff[s] = (kc / 5) * 32 + (kc % 5);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) wb[nt][s] = mask_f(w1[kc * 32 + 16 * nt + lr], k < 25);
+  }
+  const float bias0 = b1[lr], bias1 = b1[16 + lr];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) xim[t + 256 * it] = xv[it];
+  __syncthreads();
+  const int tile_end = min(49, 13 * q + 13);
+  for (int tile = 13 * q + wave; tile < tile_end; tile += 4) {  // wave-uniform
+    const int wa = 4 * tile + (lr >> 2), d = lr & 3;
+    const int pya = wa / 14, pxa = wa - pya * 14;
+    const int base = (2 * pya + (d >> 1)) * 32 + 2 * pxa + (d & 1);
+    float av[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) av[s] = xim[base + toff[s]];
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      c0 = mfma4(av[s], wb[0][s], c0);
+      c1 = mfma4(av[s], wb[1][s], c1);
+    }
+    // C[row 4lg + i][col lr] = pixel i of window 4 * tile + lg, channel 16 nt + lr
+    const int win = 4 * tile + lg, py = win / 14, px = win - py * 14;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const f32x4 c = nt ? c1 : c0;
+      int best;
+      const float m = pool4(c, best);
+      const int64_t o = (((int64_t)b * 14 + py) * 14 + px) * 32 + 16 * nt + lr;
+      a1[o] = fmaxf(m + (nt ? bias1 : bias0), 0.f);
+      idx1[o] = (uint8_t)best;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ //
+// conv2: a1 [B][14][14][32] -> a2 [B][3136] (NHWC flatten of [7][7][64]) + idx2
+//
+// M = the 49 B pooling windows of the batch x 4 pixels (pool-window-major), in 16-row tiles; block
+// b owns tiles [b TPB, (b+1) TPB) (TPB = ceil(tiles / 256): about one block per CU), which span at
+// most two images. The a1 rows those tiles read are staged once as rows of the "tall" padded image
+// (image i = tall rows [18 i, 18 i + 18), padded row r = a1 row r - 2, 18 padded columns, pixel
+// stride 36 floats). W2 streams through LDS one tap ([32 ci][64 co] = 8 KB) at a time,
+// double-buffered, one barrier per tap. 4 waves; wave w owns output channels 16w..16w+15 of every
+// tile: per tap one ds_read_b32 B fragment per MFMA (shared by the TPB tiles) and two float4 A
+// chunks per tile. Epilogue: 2x2 max-pool + argmax + bias + ReLU in registers.
+// ------------------------------------------------------------------------------------------ //
+constexpr int C2F_PS = 36, C2F_RS = 18 * C2F_PS, C2F_MAXR = 22, C2F_WS = 68, C2F_WB = 32 * C2F_WS;
+constexpr int C2F_LDS = (C2F_MAXR * C2F_RS + 2 * C2F_WB) * 4;     // 74,432 B
+constexpr int C2F_MAXCH = (C2F_MAXR * 18 * 8 + 255) / 256;         // image float4 chunks per thread
+
+// two float4 chunks of one [32][64] HWIO tap slice per thread (256 threads)
+__device__ __forceinline__ void w2_tap_load(const float* __restrict__ w2, int tap, int t, float4 (&wr)[2]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = t + 256 * u;
+    wr[u] = *reinterpret_cast<const float4*>(w2 + tap * 2048 + (i >> 4) * 64 + (i & 15) * 4);
+  }
+}
+__device__ __forceinline__ void w2_tap_store(float* dst, int t, const float4 (&wr)[2]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = t + 256 * u;
+    *reinterpret_cast<float4*>(dst + (i >> 4) * C2F_WS + (i & 15) * 4) = wr[u];
+  }
+}
+
+template <int TPB>
+__global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
+                                                            const float* __restrict__ b2, float* __restrict__ a2,
+                                                            uint8_t* __restrict__ idx2, int B) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  float* img = smf;
+  float* wbuf = smf + C2F_MAXR * C2F_RS;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int nwin = 49 * B, T0 = blockIdx.x * TPB;
+  const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
+  const int b0 = gw0 / 49, b1i = gw1 / 49;
+  const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
+  const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
+  const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
+  // 1. every load in flight first: tap-0 weights, then the image rows
+  float4 wr[2];
+  w2_tap_load(w2, 0, t, wr);
+  float4 iv[C2F_MAXCH];
+#pragma unroll
+  for (int it = 0; it < C2F_MAXCH; ++it) {
+    const int i = min(t + 256 * it, nch - 1);
+    const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, ch = rem & 7;
+    const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
+    const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+    const float4 v = *reinterpret_cast<const float4*>(
+        a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
+    iv[it] = mask_f4(v, in);
+  }
+#pragma unroll
+  for (int it = 0; it < C2F_MAXCH; ++it) {
+    const int i = t + 256 * it;
+    if (i < nch) {
+      const int rr = i / 144, rem = i - rr * 144;
+      *reinterpret_cast<float4*>(img + (rr * 18 + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
+    }
+  }
+  w2_tap_store(wbuf, t, wr);
+  // 2. per-lane A row of each tile (clamped past the batch; those results are dropped)
+  int abase[TPB];
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) {
+    const int m = 16 * (T0 + i) + lr;
+    const int gw = min(m >> 2, nwin - 1), d = m & 3;
+    const int bb = gw / 49, win = gw - 49 * bb, py = win / 7, px = win - 7 * py;
+    const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
+    abase[i] = ((18 * bb + y - R0) * 18 + xx) * C2F_PS + 4 * lg;
+  }
+  f32x4 acc[TPB];
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  const float* wcol = wbuf + 4 * lg * C2F_WS + 16 * wave + lr;
+  for (int tap = 0; tap < 25; ++tap) {
+    const float* wb = wcol + (tap & 1) * C2F_WB;
+    if (tap + 1 < 25) w2_tap_load(w2, tap + 1, t, wr);
+    const int kh = tap / 5, kw = tap - 5 * kh;
+    const int aoff = (kh * 18 + kw) * C2F_PS;
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) {
+      float bv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = wb[(16 * c2 + j) * C2F_WS];
+      const float4 bq = make_float4(bv[0], bv[1], bv[2], bv[3]);
+#pragma unroll
+      for (int i = 0; i < TPB; ++i) {
+        const float4 a = *reinterpret_cast<const float4*>(img + abase[i] + aoff + 16 * c2);
+        acc[i] = mfma4_q(a, bq, acc[i]);
+      }
+    }
+    if (tap + 1 < 25) w2_tap_store(wbuf + ((tap + 1) & 1) * C2F_WB, t, wr);
+    __syncthreads();
+  }
+  const int co = 16 * wave + lr;
+  const float bias = b2[co];
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) {
+    const int gw = 4 * (T0 + i) + lg;
+    if (gw < nwin) {
+      const int bb = gw / 49, win = gw - 49 * bb;
+      int best;
+      const float m = pool4(acc[i], best);
+      const int64_t o = (int64_t)bb * 3136 + win * 64 + co;
+      a2[o] = fmaxf(m + bias, 0.f);
+      idx2[o] = (uint8_t)best;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ //
+// fc1 forward: zpart[ks][b][n] = sum_{k in slice ks} a2[b][k] W3[k][n]   (14 slices of 224)
+// grid (16, 14): 64 columns x one K slice per block, 8 waves: wave w = 16 columns (w & 3) x every
+// other 16-sample tile (w >> 2). The transposed product puts features on the MFMA row axis: A =
+// W3^T, whose 56 fragments for the slice (one W3 element per lane per MFMA) are loaded once into
+// registers straight from HBM (every W3 element is read by one block); B = a2^T from the slice's
+// K-contiguous LDS image (one float4 per 4 MFMAs). A lane's 4 accumulators are 4 consecutive
+// features of one sample: 16-byte slab stores.
+// ------------------------------------------------------------------------------------------ //
+constexpr int F1F_KS = 14, F1F_KSL = 224, F1F_AS = 228;
+constexpr int F1F_LDS = 128 * F1F_AS * 4;  // 116,736 B
+
+template <int MT>
+__global__ void __launch_bounds__(512) f32_fc1_fwd_kernel(const float* __restrict__ a2, const float* __restrict__ w3,
+                                                          float* __restrict__ zpart, int B) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  float* As = smf;  // [16 MT][228]: rows = samples, k contiguous
+  const int nb = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int k0 = ks * F1F_KSL, nt = wave & 3, sh = wave >> 2;
+  const int n = nb * 64 + nt * 16 + lr;
+  // A fragments: wa[4q + j] = W3[k0 + 16q + 4lg + j][n]
+  float wa[56];
+  const float* wp = w3 + (int64_t)(k0 + 4 * lg) * 1024 + n;
+#pragma unroll
+  for (int q = 0; q < 14; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[4 * q + j] = wp[(16 * q + j) * 1024];
+  constexpr int NCH = MT * 16 * 56, PER = (NCH + 511) / 512;
+  float4 v[PER];
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = min(t + 512 * it, NCH - 1), r = i / 56, c = i - 56 * r;
+    v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * c), r < B);
+  }
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = t + 512 * it;
+    if (i < NCH) {
+      const int r = i / 56, c = i - 56 * r;
+      *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * c) = v[it];
+    }
+  }
+  __syncthreads();
+  for (int tt = sh; tt < MT; tt += 2) {  // wave-uniform
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    const float* bp = As + (tt * 16 + lr) * F1F_AS + 4 * lg;
+#pragma unroll
+    for (int q = 0; q < 14; q += 2) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bp + 16 * q);
+      const float4 b1 = *reinterpret_cast<const float4*>(bp + 16 * q + 16);
+      acc0 = mfma4_q(make_float4(wa[4 * q], wa[4 * q + 1], wa[4 * q + 2], wa[4 * q + 3]), b0, acc0);
+      acc1 = mfma4_q(make_float4(wa[4 * q + 4], wa[4 * q + 5], wa[4 * q + 6], wa[4 * q + 7]), b1, acc1);
+    }
+    const int m = tt * 16 + lr;
+    if (m < B) {
+      const f32x4 s = acc0 + acc1;
+      *reinterpret_cast<float4*>(zpart + ((int64_t)ks * B + m) * 1024 + nb * 64 + nt * 16 + 4 * lg) =
+          make_float4(s[0], s[1], s[2], s[3]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ //
+// head: one block per sample b, 256 threads x 4 features (K9-K11 of SURVEY.md §2.5):
+//   z = sum of the 14 slabs + b3; h = dropout(relu(z)); logits = h W4 + b4; softmax-xent;
+//   dlogits = (softmax - onehot) / B; dz = (dlogits W4^T) * relu'(z) * dropout mask
+// ------------------------------------------------------------------------------------------ //
+__global__ void __launch_bounds__(256) f32_head_kernel(
+    const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
+    const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
+    int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
+    float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B) {
+  __shared__ float red[4][10];
+  __shared__ float dl[10];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t step = state ? state[ST_FWD] : 0;
+  const int n0 = t * 4;
+  float4 parts[F1F_KS];
+#pragma unroll
+  for (int s = 0; s < F1F_KS; ++s)
+    parts[s] = *reinterpret_cast<const float4*>(zpart + ((int64_t)s * B + b) * 1024 + n0);
+  float w4r[4][10];  // this thread's 4 rows of W4 = 40 contiguous floats
+  {
+    float4 wv[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) wv[k] = reinterpret_cast<const float4*>(w4 + n0 * 10)[k];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const float e[4] = {wv[k].x, wv[k].y, wv[k].z, wv[k].w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w4r[(4 * k + u) / 10][(4 * k + u) % 10] = e[u];
+    }
+  }
+  const float4 bb = *reinterpret_cast<const float4*>(b3 + n0);
+  int y = 0;
+  if (t < 64) {
+    int row = b;
+    if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
+    y = (int)labels[row];
+  }
+  float z[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+  for (int s = 0; s < F1F_KS; ++s) {
+    z[0] += parts[s].x;
+    z[1] += parts[s].y;
+    z[2] += parts[s].z;
+    z[3] += parts[s].w;
+  }
+  float h[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool keep = thresh24 == 0 || dropout_keep(seed, (uint32_t)step, (uint32_t)(b * 1024 + n0 + i), thresh24);
+    h[i] = keep ? fmaxf(z[i], 0.f) * keep_scale : 0.f;
+  }
+  *reinterpret_cast<float4*>(h_out + (int64_t)b * 1024 + n0) = make_float4(h[0], h[1], h[2], h[3]);
+  float part[10];
+#pragma unroll
+  for (int c = 0; c < 10; ++c) part[c] = h[0] * w4r[0][c] + h[1] * w4r[1][c] + h[2] * w4r[2][c] + h[3] * w4r[3][c];
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    const float s = wave_sum(part[c]);
+    if (lane == 0) red[wave][c] = s;
+  }
+  __syncthreads();
+  if (t < 64) {
+    const int c = min(lane, 9);
+    const float lgt = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]) + b4[c];
+    const float v = lane < 10 ? lgt : -INFINITY;
+    const float mx = wave_max(v);
+    const float e = lane < 10 ? expf(lgt - mx) : 0.f;
+    const float se = wave_sum(e);
+    const float lse = mx + logf(se);
+    const unsigned long long ismax = __ballot(lane < 10 && lgt == mx);
+    const int am = __ffsll((long long)ismax) - 1;
+    const float ly = __shfl(lgt, y, 64);
+    if (lane < 10) {
+      const float d = (expf(lgt - lse) - (lane == y ? 1.f : 0.f)) / (float)B;
+      dl[lane] = d;
+      dlog_out[b * 10 + lane] = d;
+    }
+    if (lane == 0) {
+      stats[b * 2 + 0] = lse - ly;
+      stats[b * 2 + 1] = (am == y) ? 1.f : 0.f;
+      if (b == 0 && state != nullptr) state[ST_OPT] += 1;
+    }
+  }
+  __syncthreads();
+  float g[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 10; ++c) s = fmaf(dl[c], w4r[i][c], s);
+    g[i] = h[i] > 0.f ? s * keep_scale : 0.f;
+  }
+  *reinterpret_cast<float4*>(dz_out + (int64_t)b * 1024 + n0) = make_float4(g[0], g[1], g[2], g[3]);
+}
+
+// ------------------------------------------------------------------------------------------ //
+// host wrappers
+// ------------------------------------------------------------------------------------------ //
+static void check_f32(const at::Tensor& t, int64_t numel, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dtype() == at::kFloat && t.is_contiguous() && t.numel() == numel, what,
+              ": expected a contiguous fp32 device tensor of ", numel, " elements");
+}
+static void check_u8(const at::Tensor& t, int64_t numel, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dtype() == at::kByte && t.is_contiguous() && t.numel() == numel, what,
+              ": expected a contiguous uint8 device tensor of ", numel, " elements");
+}
+
+static const int* rows_ptr(const c10::optional<at::Tensor>& rows, int n_pool, int B, const char* what) {
+  if (rows.has_value() && rows->defined()) {
+    TORCH_CHECK(rows->dtype() == at::kInt && rows->numel() == n_pool, what, ": rows must be int32 [n_pool]");
+    return rows->data_ptr<int>();
+  }
+  TORCH_CHECK(n_pool >= B, what, ": x has fewer rows than the batch");
+  return nullptr;
+}
+
+void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                   const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1) {
+  const int B = a1.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv1_fwd: batch 1..128");
+  TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv1_fwd: x");
+  check_f32(a1, (int64_t)B * 6272, "f32_conv1_fwd: a1");
+  check_u8(idx1, (int64_t)B * 6272, "f32_conv1_fwd: idx1");
+  check_f32(w1, 800, "f32_conv1_fwd: w1");
+  check_f32(b1, 32, "f32_conv1_fwd: b1");
+  const int n_pool = x.size(0);
+  const int* rp = rows_ptr(rows, n_pool, B, "f32_conv1_fwd");
+  const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  f32_conv1_kernel<<<dim3(4, B), 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(),
+                                                   b1.data_ptr<float>(), a1.data_ptr<float>(),
+                                                   idx1.data_ptr<uint8_t>(), B);
+}
+
+// tiles per block of f32_conv2_fwd for batch B (about one block per CU), and the block count
+static int conv2f_tpb(int B) {
+  const int nt = (49 * B + 3) / 4;
+  return std::min(7, std::max(1, (nt + 255) / 256));
+}
+
+void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2) {
+  const int B = a2.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv2_fwd: batch 1..128");
+  check_f32(a1, (int64_t)B * 6272, "f32_conv2_fwd: a1");
+  check_f32(w2, 51200, "f32_conv2_fwd: w2");
+  check_f32(b2, 64, "f32_conv2_fwd: b2");
+  check_f32(a2, (int64_t)B * 3136, "f32_conv2_fwd: a2");
+  check_u8(idx2, (int64_t)B * 3136, "f32_conv2_fwd: idx2");
+  const int tpb = conv2f_tpb(B), nt = (49 * B + 3) / 4, nblk = (nt + tpb - 1) / tpb;
+  // every block's tall-row span must fit the LDS image (host check of the kernel's assumption)
+  for (int blk = 0; blk < nblk; ++blk) {
+    const int gw0 = 4 * blk * tpb, gw1 = std::min(4 * (blk + 1) * tpb, 49 * B) - 1;
+    const int r0 = 18 * (gw0 / 49) + 2 * ((gw0 % 49) / 7), r1 = 18 * (gw1 / 49) + 2 * ((gw1 % 49) / 7) + 6;
+    TORCH_CHECK(r1 - r0 <= C2F_MAXR, "f32_conv2_fwd: row span exceeds the LDS image");
+  }
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  auto launch = [&](auto kern) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C2F_LDS);
+    kern<<<nblk, 256, C2F_LDS, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+                                         a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B);
+  };
+  switch (tpb) {
+    case 1: launch(f32_conv2_fwd_kernel<1>); break;
+    case 2: launch(f32_conv2_fwd_kernel<2>); break;
+    case 3: launch(f32_conv2_fwd_kernel<3>); break;
+    case 4: launch(f32_conv2_fwd_kernel<4>); break;
+    case 5: launch(f32_conv2_fwd_kernel<5>); break;
+    case 6: launch(f32_conv2_fwd_kernel<6>); break;
+    default: launch(f32_conv2_fwd_kernel<7>); break;
+  }
+}
+
+void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) {
+  const int B = a2.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_fwd: batch 1..128");
+  check_f32(a2, (int64_t)B * 3136, "f32_fc1_fwd: a2");
+  check_f32(w3, 3136 * 1024, "f32_fc1_fwd: w3");
+  check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_fc1_fwd: zpart [14][B][1024]");
+  const int mt = (B + 15) / 16;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  auto launch = [&](auto kern) {
+    const int lds = mt * 16 * F1F_AS * 4;
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1F_LDS);
+    kern<<<dim3(16, F1F_KS), 512, lds, stream>>>(a2.data_ptr<float>(), w3.data_ptr<float>(), zpart.data_ptr<float>(),
+                                                 B);
+  };
+  switch (mt) {
+    case 1: launch(f32_fc1_fwd_kernel<1>); break;
+    case 2: launch(f32_fc1_fwd_kernel<2>); break;
+    case 3: launch(f32_fc1_fwd_kernel<3>); break;
+    case 4: launch(f32_fc1_fwd_kernel<4>); break;
+    case 5: launch(f32_fc1_fwd_kernel<5>); break;
+    case 6: launch(f32_fc1_fwd_kernel<6>); break;
+    case 7: launch(f32_fc1_fwd_kernel<7>); break;
+    default: launch(f32_fc1_fwd_kernel<8>); break;
+  }
+}
+
+void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
+                      const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
+                      const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
+                      at::Tensor& dlog, at::Tensor& stats) {
+  const int B = h.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_head: batch 1..128");
+  check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_head: zpart");
+  check_f32(b3, 1024, "f32_head: b3");
+  check_f32(w4, 10240, "f32_head: w4");
+  check_f32(b4, 10, "f32_head: b4");
+  check_f32(h, (int64_t)B * 1024, "f32_head: h");
+  check_f32(dz, (int64_t)B * 1024, "f32_head: dz");
+  check_f32(dlog, (int64_t)B * 10, "f32_head: dlog");
+  check_f32(stats, (int64_t)B * 2, "f32_head: stats");
+  TORCH_CHECK(labels.dtype() == at::kLong, "f32_head: labels int64");
+  const int n_pool = labels.size(0);
+  const int* rp = rows_ptr(rows, n_pool, B, "f32_head");
+  int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "f32_head: dropout rate in [0, 1)");
+  const uint32_t thresh = (uint32_t)(rate * 16777216.0);
+  const float keep_scale = rate > 0.0 ? (float)(1.0 / (1.0 - rate)) : 1.f;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  f32_head_kernel<<<B, 256, 0, stream>>>(zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(),
+                                         b4.data_ptr<float>(), labels.data_ptr<int64_t>(), rp, n_pool, sp,
+                                         (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(), dz.data_ptr<float>(),
+                                         dlog.data_ptr<float>(), stats.data_ptr<float>(), B);
+}
+
+}  // namespace mihvd

@@ -83,6 +83,25 @@ void multi_tensor_sgd(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std:
                       double momentum, double dampening, double weight_decay, bool nesterov, bool first,
                       double grad_scale);
 void bump_step_(at::Tensor& step);
+void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                   const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1);
+void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
+void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
+void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
+                      const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
+                      const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
+                      at::Tensor& dlog, at::Tensor& stats);
+void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
+                 const at::Tensor& dlog, const at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
+                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4);
+void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
+                   const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                   at::Tensor& cpart, at::Tensor& slab);
+void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,
+                     at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2);
+int64_t f32_db2_rows(int64_t B);
+int64_t f32_wgrad_groups(int64_t B);
+int64_t f32_dgrad_blocks(int64_t B);
 }  // namespace mihvd
 
 namespace {
@@ -196,6 +215,31 @@ void mt_sgd_op(at::TensorList p, at::TensorList g, at::TensorList bufs, double l
   mihvd::multi_tensor_sgd(p.vec(), g.vec(), bufs.vec(), lr, momentum, dampening, wd, nesterov, first, grad_scale);
 }
 void bump_step_op(Tensor step) { mihvd::bump_step_(step); }
+void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
+                  Tensor idx1) {
+  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1);
+}
+void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2) {
+  mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2);
+}
+void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
+void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
+                 const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
+                 Tensor stats) {
+  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats);
+}
+void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, const Tensor& h, const Tensor& dlog,
+                    const Tensor& w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4) {
+  mihvd::f32_fc1_bwd(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4);
+}
+void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, const Tensor& idx1, const Tensor& x,
+                      const OptT& rows, const OptT& state, Tensor cpart, Tensor slab) {
+  mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab);
+}
+void f32_conv_reduce_op(const Tensor& slab, const Tensor& cpart, const Tensor& db2p, Tensor gW2, Tensor gW1, Tensor gb1,
+                        Tensor gb2) {
+  mihvd::f32_conv_reduce(slab, cpart, db2p, gW2, gW1, gb1, gb2);
+}
 }  // namespace
 
 TORCH_LIBRARY(mihvd, m) {
@@ -245,6 +289,20 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("multi_tensor_sgd(Tensor(a!)[] p, Tensor[] g, Tensor(b!)[] bufs, float lr, float momentum, float dampening, "
         "float weight_decay, bool nesterov, bool first, float grad_scale) -> ()");
   m.def("bump_step_(Tensor(a!) step) -> ()");
+  m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
+  m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
+  m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
+  m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
+        "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
+  m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor w3, Tensor(a!) dY2, "
+        "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4) -> ()");
+  m.def("f32_conv2_bwd(Tensor dY2, Tensor w2, Tensor a1, Tensor idx1, Tensor x, Tensor? rows, Tensor? state, "
+        "Tensor(a!) cpart, Tensor(b!) slab) -> ()");
+  m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
+        "Tensor(d!) gb2) -> ()");
+  m.def("f32_db2_rows(int B) -> int", &mihvd::f32_db2_rows);
+  m.def("f32_wgrad_groups(int B) -> int", &mihvd::f32_wgrad_groups);
+  m.def("f32_dgrad_blocks(int B) -> int", &mihvd::f32_dgrad_blocks);
   m.def("gather_cols_bf16(Tensor src, int col0, Tensor(a!) dst) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");
@@ -278,6 +336,13 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("multi_tensor_adam", &mt_adam_op);
   m.impl("multi_tensor_sgd", &mt_sgd_op);
   m.impl("bump_step_", &bump_step_op);
+  m.impl("f32_conv1_fwd", &f32_conv1_op);
+  m.impl("f32_conv2_fwd", &f32_conv2_op);
+  m.impl("f32_fc1_fwd", &f32_fc1_fwd_op);
+  m.impl("f32_head_fwd_bwd", &f32_head_op);
+  m.impl("f32_fc1_bwd", &f32_fc1_bwd_op);
+  m.impl("f32_conv2_bwd", &f32_conv2_bwd_op);
+  m.impl("f32_conv_reduce", &f32_conv_reduce_op);
   m.impl("scale_cast_bf16", &scale_cast_op);
   m.impl("bf16_to_f32", &bf16_to_f32_op);
   m.impl("scale_cast_f16", &scale_cast_f16_op);

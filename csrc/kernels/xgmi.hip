@@ -113,6 +113,8 @@ CollRole gather_role(Ctx* c, int64_t ph, int64_t offset, int64_t stride, int64_t
   r.col_off = col_off;
   r.col_bytes = col_bytes;
   r.nblk = blocks_for(rows_per_rank * (col_bytes / 16));
+  const char* dbg = std::getenv("MIHVD_XGMI_DEBUG_STALE");
+  r.dbg_stale = (dbg && std::atoi(dbg) != 0) ? 1 : 0;
   return r;
 }
 
@@ -265,8 +267,11 @@ int64_t xgmi_role_reduce(int64_t id, int64_t ph, int64_t offset, at::Tensor& out
 
 // Launch a prepared collective on its own (current stream).
 void xgmi_run(int64_t role) {
-  const CollRole r = xgmi_role_lookup(role);
+  CollRole r = xgmi_role_lookup(role);
   TORCH_CHECK(r.kind != COLL_NONE && r.nblk > 0, "xgmi_run: empty descriptor");
+  // the debug stale-read injection models in-step staleness only: standalone launches (the
+  // start-up validation, _validate_xgmi) stay exact, so the end-to-end check must catch it
+  r.dbg_stale = 0;
   launch_role(r, c10::hip::getCurrentHIPStream().stream());
 }
 

@@ -11,10 +11,19 @@
 //
 // Phase protocol, per launch of phase ph with epoch e = epoch[ph] + 1:
 //   enter: the first kSignalBlocks role blocks store e into flags[ph][rank] of every peer
-//          (system-scope stores over xGMI); every role block polls its own flags[ph][*] until each
-//          peer reached e (relaxed system-scope loads + s_sleep; bounded by tmo wall-clock ticks:
-//          on timeout set err and continue poisoned). The published data of ph must come from
-//          launches that completed before this one (the kernel boundary wrote this GPU's L2s back).
+//          (system-scope stores over xGMI), each after a SYSTEM-scope release fence; every role
+//          block polls its own flags[ph][*] until each peer reached e (relaxed system-scope loads +
+//          s_sleep; bounded by tmo wall-clock ticks: on timeout set err and continue poisoned).
+//          Memory-model argument: the published data of ph was written by launches that completed
+//          before this one on the same stream. Each such launch ends with the dispatch packet's
+//          release fence (agent scope in a captured graph), which writes every XCD's L2 back to the
+//          memory side (the only point where the non-coherent per-XCD L2s meet), and the signal's
+//          own system-scope release orders it after that at the scope the peers read at. Peers
+//          read with system-scope loads (sc0 sc1, below), which miss in their own caches and are
+//          served by this GPU's memory side. The argument is also checked end to end at start-up:
+//          select_data_plane() compares graph-replayed steps on this plane against RCCL from one
+//          snapshot and drops the plane on any mismatch (MIHVD_XGMI_DEBUG_STALE=1 injects stale
+//          reads to show that the check fires).
 //   move:  peer bytes are read with system-scope loads (buffer loads, sc0 sc1), which miss in this
 //          GPU's caches for peer memory, so no line cached in an earlier epoch is returned.
 //   exit:  the last role block to finish (device-scope ticket) publishes epoch[ph] = e.
@@ -66,6 +75,7 @@ struct CollRole {
   float scale = 1.f;
   int adam = 0;
   AdamArgs aa{};
+  int dbg_stale = 0;        // debug (MIHVD_XGMI_DEBUG_STALE): gathers skip odd rows -> stale data
 };
 
 __device__ __forceinline__ unsigned* xg_u32(char* base, int64_t off) { return (unsigned*)(base + off); }
@@ -86,11 +96,13 @@ __device__ __forceinline__ unsigned xg_enter(const CollRole& c, int bid, bool& o
         __hip_atomic_load(xg_u32(mine, kXgEpochOff) + c.ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     s_e = e;
     s_err = __hip_atomic_load(xg_u32(mine, kXgErrOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if ((unsigned)bid < kXgSignalBlocks)
+    if ((unsigned)bid < kXgSignalBlocks) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: before the peers can see e
       for (int p = 0; p < c.world; ++p)
         if (p != c.rank)
           __hip_atomic_store(xg_u32(c.pt.base[p], kXgFlagsOff) + c.ph * kXgMaxRanks + c.rank, e, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   __syncthreads();
   const unsigned e = s_e;
@@ -148,7 +160,7 @@ __device__ __forceinline__ void xg_gather(const CollRole& c, int bid, bool ok) {
     for (int p = 0; p < kXgMaxRanks; ++p) {
       if (p >= c.world || p == c.rank) continue;
       const int64_t row = (int64_t)p * c.R + r;
-      if (row >= c.total_rows) continue;
+      if (row >= c.total_rows || (c.dbg_stale && (r & 1))) continue;
       xg_u32x4 x = v[p];
       if (!ok) x = xg_u32x4{0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u};  // bf16 / f32 NaN
       *(xg_u32x4*)(mine + row * c.stride + c.col_off + cc * 16) = x;

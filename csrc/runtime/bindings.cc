@@ -100,6 +100,26 @@ PYBIND11_MODULE(_mihvd_runtime, m) {
       .def("due", &FaultPlan::due)
       .def_property_readonly("actions", &FaultPlan::actions);
 
+  py::class_<HealthMonitor>(m, "HealthMonitor")
+      .def(py::init<int, double, int>(), py::arg("rank") = 0, py::arg("poll_s") = 0.5, py::arg("exit_code") = 134)
+      .def("attach_rccl", &HealthMonitor::attach_rccl, py::arg("comm"), py::arg("lib_path"))
+      .def("inject_error", &HealthMonitor::inject_error, py::arg("code"), py::arg("what") = "test")
+      .def("poll_once", [](HealthMonitor& h) {
+             std::string what;
+             int e;
+             {
+               py::gil_scoped_release nogil;
+               e = h.poll_once(&what);
+             }
+             return py::make_tuple(e, what);
+           })
+      .def("start", &HealthMonitor::start)
+      .def("stop", &HealthMonitor::stop, py::call_guard<py::gil_scoped_release>())
+      .def("set_abort_process", &HealthMonitor::set_abort_process)
+      .def_property_readonly("error", &HealthMonitor::error)
+      .def_property_readonly("polls", &HealthMonitor::polls)
+      .def_property_readonly("num_comms", &HealthMonitor::num_comms);
+
   py::class_<StepStats>(m, "StepStats")
       .def(py::init<size_t>(), py::arg("window") = 100)
       .def("add", &StepStats::add)
@@ -187,5 +207,7 @@ PYBIND11_MODULE(_mihvd_runtime, m) {
       .def("stop", &Negotiator::stop, gil_release())
       .def_property_readonly("submitted", &Negotiator::submitted)
       .def_property_readonly("responses", &Negotiator::responses)
-      .def_property_readonly("warnings", &Negotiator::warnings);
+      .def_property_readonly("warnings", &Negotiator::warnings)
+      .def_property_readonly("cache_hits", &Negotiator::cache_hits)
+      .def_property_readonly("records_posted", &Negotiator::records_posted);
 }

@@ -144,6 +144,10 @@ class Negotiator {
   int64_t submitted() const { return submitted_.load(); }
   int64_t responses() const { return responded_.load(); }
   int64_t warnings() const { return warnings_.load(); }
+  // response cache: submissions that went out as a bit of a cached-slot vector, and request
+  // records written to the store (full requests + bit-vector records)
+  int64_t cache_hits() const { return cache_hits_.load(); }
+  int64_t records_posted() const { return records_posted_.load(); }
   void stop();
 
  private:
@@ -161,7 +165,19 @@ class Negotiator {
   std::condition_variable cv_;
   std::deque<std::pair<std::string, std::string>> outbox_;
   std::deque<Response> ready_;
-  std::atomic<int64_t> submitted_{0}, responded_{0}, warnings_{0};
+  std::atomic<int64_t> submitted_{0}, responded_{0}, warnings_{0}, cache_hits_{0}, records_posted_{0};
+  // Response cache (Horovod's response_cache.cc): the coordinator gives every (name, signature)
+  // it has published without error a slot; every rank learns the slots from the responses. A
+  // later submission of a cached pair is posted as one bit of a per-batch slot bit vector
+  // ("<rank>\x1d<hex bits>") instead of a full request record, so steady-state negotiation costs
+  // one store write per poster batch, not one per tensor. A pair whose signature changed misses
+  // the cache and goes out in full, so the coordinator still sees (and reports) the mismatch.
+  std::unordered_map<std::string, int> rank_cache_;   // every rank: name \x1f sig -> slot
+  // every rank: signatures of its outstanding submissions per name, in submission order (the
+  // responses of one name come back in generation order, so the front is the response's)
+  std::unordered_map<std::string, std::deque<std::string>> sig_q_;
+  std::unordered_map<std::string, int> coord_cache_;  // rank 0: name \x1f sig -> slot
+  std::vector<std::pair<std::string, std::string>> coord_slots_;  // rank 0: slot -> (name, sig)
 
   // coordinator state (rank 0)
   struct Pending {

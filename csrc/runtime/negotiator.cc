@@ -4,11 +4,15 @@
 // Store keys (under `prefix/`):
 //   req_seq            global request counter (ADD gives every submission a unique, totally
 //                      ordered sequence number across all ranks)
-//   req/<seq>          "<rank>\x1f<name>\x1f<signature>"
-//   resp/<k>           the k-th response record: one or more "<generation>\x1f<name>\x1f<error>"
-//                      entries joined by \x1e — collectives that became ready on all ranks in
-//                      the same coordinator pass. A record is a unit every rank sees identically,
-//                      so it is also the unit inside which the executor may fuse tensors.
+//   req/<seq>          "<rank>\x1f<name>\x1f<signature>" (a full request), or
+//                      "<rank>\x1d<hex bit vector>" (response cache: every set bit i is a
+//                      submission of the (name, signature) cached in slot i)
+//   resp/<k>           the k-th response record: one or more
+//                      "<generation>\x1f<name>\x1f<error>\x1f<slot>" entries joined by \x1e —
+//                      collectives that became ready on all ranks in the same coordinator pass
+//                      (slot: the pair's response-cache slot, -1 after an error). A record is a
+//                      unit every rank sees identically, so it is also the unit inside which the
+//                      executor may fuse tensors.
 //   ack/<rank>         highest response index a rank has consumed (lets the coordinator delete)
 #include <algorithm>
 #include <cstdio>
@@ -37,6 +41,28 @@ std::vector<std::string> split(const std::string& s, char sep) {
     out.push_back(s.substr(a, b - a));
     a = b + 1;
   }
+}
+
+std::string bits_to_hex(const std::vector<uint8_t>& bits) {
+  static const char* hx = "0123456789abcdef";
+  std::string out;
+  for (size_t i = 0; i < bits.size(); i += 4) {
+    int v = 0;
+    for (size_t j = 0; j < 4 && i + j < bits.size(); ++j) v |= (bits[i + j] ? 1 : 0) << j;
+    out += hx[v];
+  }
+  return out;
+}
+
+std::vector<int> hex_to_slots(const std::string& hex) {
+  std::vector<int> out;
+  for (size_t i = 0; i < hex.size(); ++i) {
+    const char c = hex[i];
+    const int v = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10 : 0;
+    for (int j = 0; j < 4; ++j)
+      if (v & (1 << j)) out.push_back((int)(4 * i + j));
+  }
+  return out;
 }
 
 std::string ranks_str(const std::vector<int>& r) {
@@ -80,6 +106,7 @@ void Negotiator::submit(const std::string& name, const std::string& signature) {
   {
     std::lock_guard<std::mutex> g(mu_);
     outbox_.emplace_back(name, signature);
+    sig_q_[name].push_back(signature);
   }
   submitted_.fetch_add(1);
   cv_.notify_all();
@@ -113,10 +140,41 @@ void Negotiator::poster_loop() {
         batch.swap(outbox_);
       }
       if (batch.empty()) continue;
-      const int64_t last = post_->add(key("req_seq"), (int64_t)batch.size());
-      int64_t seq = last - (int64_t)batch.size() + 1;
-      for (auto& e : batch)
-        post_->set(key("req/" + std::to_string(seq++)), std::to_string(rank_) + '\x1f' + e.first + '\x1f' + e.second);
+      // records in submission order; cached pairs accumulate in a bit vector that is flushed
+      // before a full request and before a second submission of the same slot, so every rank's
+      // per-name submission order survives
+      std::vector<std::string> recs;
+      std::vector<uint8_t> bits;
+      bool any = false;
+      auto flush_bits = [&] {
+        if (!any) return;
+        recs.push_back(std::to_string(rank_) + '\x1d' + bits_to_hex(bits));
+        std::fill(bits.begin(), bits.end(), 0);
+        any = false;
+      };
+      for (auto& e : batch) {
+        int slot = -1;
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          auto it = rank_cache_.find(e.first + '\x1f' + e.second);
+          if (it != rank_cache_.end()) slot = it->second;
+        }
+        if (slot < 0) {
+          flush_bits();
+          recs.push_back(std::to_string(rank_) + '\x1f' + e.first + '\x1f' + e.second);
+          continue;
+        }
+        if ((size_t)slot >= bits.size()) bits.resize(slot + 1, 0);
+        if (bits[slot]) flush_bits();
+        bits[slot] = 1;
+        any = true;
+        cache_hits_.fetch_add(1);
+      }
+      flush_bits();
+      const int64_t last = post_->add(key("req_seq"), (int64_t)recs.size());
+      int64_t seq = last - (int64_t)recs.size() + 1;
+      for (auto& r : recs) post_->set(key("req/" + std::to_string(seq++)), r);
+      records_posted_.fetch_add((int64_t)recs.size());
     }
   } catch (const std::exception& e) {
     if (!stop_.load()) std::fprintf(stderr, "[mihvd negotiator rank %d] poster thread stopped: %s\n", rank_, e.what());
@@ -140,6 +198,18 @@ void Negotiator::engine_loop() {
           r.name = f.at(1);
           r.error = f.size() > 2 ? f[2] : "";
           r.batch = next_resp;
+          // learn the pair's cache slot (the signature is the one this rank submitted: a pair
+          // with an error is never cached)
+          auto q = sig_q_.find(r.name);
+          if (q != sig_q_.end() && !q->second.empty()) {
+            const std::string sig = std::move(q->second.front());
+            q->second.pop_front();
+            if (q->second.empty()) sig_q_.erase(q);
+            if (f.size() > 3 && r.error.empty()) {
+              const int slot = std::stoi(f[3]);
+              if (slot >= 0) rank_cache_[r.name + '\x1f' + sig] = slot;
+            }
+          }
           ready_.push_back(std::move(r));
         }
       }
@@ -188,10 +258,22 @@ void Negotiator::coordinator_loop() {
         ++n_in_pass;
         coord_->del(key("req/" + std::to_string(next_req)));
         ++next_req;
-        auto f = split(v, '\x1f');
-        const int r = std::stoi(f.at(0));
-        const std::string& name = f.at(1);
-        const std::string sig = f.size() > 2 ? f[2] : "";
+        // a full request, or a bit vector of cached (name, signature) slots
+        std::vector<std::pair<int, std::pair<std::string, std::string>>> subs;
+        const size_t bv = v.find('\x1d');
+        if (bv != std::string::npos) {
+          const int r = std::stoi(v.substr(0, bv));
+          std::lock_guard<std::mutex> g(mu_);
+          for (int slot : hex_to_slots(v.substr(bv + 1)))
+            if (slot < (int)coord_slots_.size()) subs.push_back({r, coord_slots_[slot]});
+        } else {
+          auto f = split(v, '\x1f');
+          subs.push_back({std::stoi(f.at(0)), {f.at(1), f.size() > 2 ? f[2] : ""}});
+        }
+        for (auto& sub : subs) {
+        const int r = sub.first;
+        const std::string& name = sub.second.first;
+        const std::string& sig = sub.second.second;
         std::string publish;
         {
           std::lock_guard<std::mutex> g(mu_);
@@ -211,13 +293,24 @@ void Negotiator::coordinator_loop() {
           Pending& p = it->second;
           p.have[r] = 1;
           if (++p.count == size_) {
-            publish = std::to_string(gen) + '\x1f' + name + '\x1f' + p.error;
+            int slot = -1;
+            if (p.error.empty()) {
+              const std::string ck = name + '\x1f' + p.signature;
+              auto cit = coord_cache_.find(ck);
+              if (cit == coord_cache_.end()) {
+                cit = coord_cache_.emplace(ck, (int)coord_slots_.size()).first;
+                coord_slots_.push_back({name, p.signature});
+              }
+              slot = cit->second;
+            }
+            publish = std::to_string(gen) + '\x1f' + name + '\x1f' + p.error + '\x1f' + std::to_string(slot);
             pending_.erase(it);
           }
         }
         if (!publish.empty()) {
           if (!record.empty()) record += '\x1e';
           record += publish;
+        }
         }
       }
       if (!record.empty()) coord_->set(key("resp/" + std::to_string(next_out++)), record);

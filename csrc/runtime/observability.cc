@@ -260,7 +260,7 @@ FaultPlan::FaultPlan(const std::string& spec) {
     auto parts = split(item, ':');
     FaultAction a;
     a.kind = parts[0];
-    static const char* kinds[] = {"kill", "delay", "hang", "raise", "nan"};
+    static const char* kinds[] = {"kill", "delay", "hang", "raise", "nan", "collerr"};
     bool ok = false;
     for (auto* k : kinds) ok |= (a.kind == k);
     if (!ok) throw std::invalid_argument("MIHVD_FAULT: unknown fault kind '" + a.kind + "'");

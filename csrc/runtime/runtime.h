@@ -16,6 +16,7 @@
 //                      that have been outstanding too long and can hard-abort the process so the
 //                      launcher tears the job down (mpirun semantics).
 //   * FaultPlan      - env-driven fault injection (MIHVD_FAULT) used by the robustness tests.
+//   * HealthMonitor  - RCCL async-error polling -> communicator abort -> non-zero exit.
 //   * StepStats      - step-time accumulator for img/s and global_step/sec logging.
 #pragma once
 
@@ -189,6 +190,51 @@ class FaultPlan {
 
  private:
   std::vector<FaultAction> actions_;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Communicator health monitor (health.cc): RCCL async-error polling -> abort -> non-zero exit
+// ---------------------------------------------------------------------------------------------
+class HealthMonitor {
+ public:
+  HealthMonitor(int rank, double poll_s, int exit_code);
+  ~HealthMonitor();
+  // Attach an RCCL communicator (ncclComm_t as an integer) created by the library at lib_path
+  // (already loaded by the process). False if the library or its symbols are unavailable.
+  bool attach_rccl(uintptr_t comm, const std::string& lib_path);
+  void inject_error(int code, const std::string& what);  // test hook (MIHVD_FAULT collerr)
+  int poll_once(std::string* what);                      // one check; the first error code or 0
+  void start();
+  void stop();
+  int error() const { return error_.load(); }
+  int64_t polls() const { return polls_.load(); }
+  int64_t num_comms() const;
+  void set_abort_process(bool v) { abort_process_ = v; }  // false: report only (tests)
+
+ private:
+  using GetErrFn = int (*)(void*, int*);
+  using AbortFn = int (*)(void*);
+  using ErrStrFn = const char* (*)(int);
+  void loop();
+  void fail(int code, const std::string& what);
+  int rank_;
+  double poll_s_;
+  int exit_code_;
+  bool abort_process_ = true;
+  void* lib_ = nullptr;
+  GetErrFn get_err_ = nullptr;
+  AbortFn abort_ = nullptr;
+  ErrStrFn err_str_ = nullptr;
+  std::vector<void*> comms_;
+  int injected_ = 0;
+  std::string injected_what_;
+  std::atomic<int> error_{0};
+  std::atomic<int64_t> polls_{0};
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  bool running_ = false;
+  bool stop_ = false;
+  std::thread thread_;
 };
 
 // ---------------------------------------------------------------------------------------------

@@ -59,6 +59,7 @@ class _Context:
         self.owns_pg = False
         self.timeline = None
         self.stall = None
+        self.health = None
         self.fault_plan = None
         self.store = None          # NativeStore (C++ TCP store) when launched by mihvdrun
         self.store_server = None   # StoreServer this process hosts (negotiation without mihvdrun)
@@ -178,6 +179,7 @@ def init(comm=None, process_sets=None, config: Config | None = None):
         _ctx.world_group = dist.group.WORLD
         _build_subgroups(topo)
         _start_observability(cfg, topo)
+        _start_health(topo, backend)
         if cfg.negotiate and topo.size > 1:
             _start_engine(cfg, topo, backend, device)
         _ctx.initialized = True
@@ -242,6 +244,42 @@ def _start_observability(cfg: Config, topo: _env.Topology):
         _ctx.fault_plan = rt.FaultPlan(cfg.fault)
 
 
+def _loaded_rccl_path() -> str | None:
+    """Path of the librccl this process loaded (torch's bundled copy or /opt/rocm's)."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.split()[-1]
+                if "librccl" in os.path.basename(path) and os.path.isfile(path):
+                    return path
+    except OSError:  # pragma: no cover - non-Linux
+        pass
+    return None
+
+
+def _start_health(topo: _env.Topology, backend: str):
+    """Native communicator health monitor (csrc/runtime/health.cc): polls the RCCL communicator's
+    async-error state and, on an error (or a ``collerr`` fault), aborts the communicator and exits
+    with 134 so the launcher tears the job down — MPI's abort semantics, which the reference relies
+    on (tensorflow-mnist.yaml:17-38). ``MIHVD_HEALTH=0`` disables it; ``MIHVD_HEALTH_POLL_S`` sets
+    the poll interval (0.5 s)."""
+    if os.environ.get("MIHVD_HEALTH", "1") == "0":
+        return
+    from ._native import runtime
+
+    mon = runtime().HealthMonitor(topo.rank, float(os.environ.get("MIHVD_HEALTH_POLL_S", "0.5")), 134)
+    if backend == "nccl":
+        try:
+            comm = int(dist.group.WORLD._get_backend(torch.device("cuda"))._comm_ptr())
+            lib = _loaded_rccl_path()
+            if comm and lib and mon.attach_rccl(comm, lib):
+                log.debug("health monitor attached to RCCL communicator %#x (%s)", comm, lib)
+        except Exception as e:  # pragma: no cover - depends on the torch build
+            log.debug("health monitor: no RCCL communicator to attach (%r)", e)
+    mon.start()
+    _ctx.health = mon
+
+
 def _start_engine(cfg: Config, topo: _env.Topology, backend: str, device: torch.device):
     """Negotiated collectives (``mihvd/parallel/engine.py``): a native Negotiator per rank whose
     coordinator runs on rank 0, over mihvdrun's store or a store server rank 0 starts here."""
@@ -288,6 +326,9 @@ def shutdown():
         if _ctx.stall is not None:
             _ctx.stall.stop()
             _ctx.stall = None
+        if getattr(_ctx, "health", None) is not None:
+            _ctx.health.stop()  # before the communicator is destroyed
+            _ctx.health = None
         if _ctx.timeline is not None:
             _ctx.timeline.close()
             _ctx.timeline = None

@@ -95,9 +95,20 @@ class FusedMNISTTrainer:
     def __init__(self, batch_size: int = 100, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  dropout: float = 0.5, seed: int = 0, device=None, compression: str = "none", op=None,
                  adam_rule: str = "tf", dropout_seed: int | None = None, world_size: int | None = None,
-                 shard_optimizer: bool | None = None):
+                 shard_optimizer: bool | None = None, precision: str | None = None):
         _native.require_kernels()
         from .. import basics
+
+        # Operand precision of the hand-written step (MIHVD_PRECISION): "fp32" = exact fp32 operands
+        # on the fp32-input MFMAs (the reference's launched config: fp32 placeholders and
+        # AdamOptimizer, horovod/tensorflow_mnist.py:118-121,130; csrc/kernels/f32_*.hip), "bf16" =
+        # bf16 MFMA operands with fp32 accumulation and fp32 master weights (the MI355X analogue of
+        # the mixed_float16 variant, tensorflow_mnist_gpu.py:26-28).
+        precision = (precision or os.environ.get("MIHVD_PRECISION", "bf16")).lower()
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        self.precision = precision
+        self.f32 = precision == "fp32"
 
         self.ops = torch.ops.mihvd
         # MIHVD_DEBUG_SYNC=1: serialized bisection mode (the HIP_LAUNCH_BLOCKING of this engine):
@@ -134,7 +145,8 @@ class FusedMNISTTrainer:
         self.grads = torch.zeros(FLAT_NUMEL, **f32)
         self.m = torch.zeros(FLAT_NUMEL, **f32)
         self.v = torch.zeros(FLAT_NUMEL, **f32)
-        self.shadow = torch.zeros(FLAT_NUMEL, device=dev, dtype=torch.bfloat16)
+        # bf16 copy of the parameters that the bf16 kernels read (the fp32 kernels read params)
+        self.shadow = None if self.f32 else torch.zeros(FLAT_NUMEL, device=dev, dtype=torch.bfloat16)
         self.state = torch.zeros(4, device=dev, dtype=torch.int64)  # [fwd step, opt step t, -, -]
         self.shard_w3 = False
         ref = MNISTConvNet(impl="torch", seed=seed)
@@ -150,7 +162,8 @@ class FusedMNISTTrainer:
         # sum the allreduce would produce (fp32 accumulation over all samples), 4-16x fewer bytes.
         from ..basics import ReduceOp
 
-        self.gather = (self.collectives and compression == "none" and os.environ.get("MIHVD_FC_GATHER", "1") != "0"
+        self.gather = (self.collectives and compression == "none" and not self.f32
+                       and os.environ.get("MIHVD_FC_GATHER", "1") != "0"
                        and (op is None or ReduceOp(op) in (ReduceOp.Average, ReduceOp.Sum)))
         # Sharded dense/kernel optimizer (factor-gather plane only; shard_optimizer=True or
         # MIHVD_SHARD_W3=1): rank r owns W3 row tiles [r*T, (r+1)*T) of the 49 64-row tiles
@@ -223,6 +236,18 @@ class FusedMNISTTrainer:
         self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
         self.cpart = torch.empty(B, 896, **f32)     # per-image dW1 | db1 | db2 partial rows
+        if self.f32:
+            ops = self.ops
+            self.a1 = torch.empty(B, 14, 14, 32, **f32)
+            self.a2 = torch.empty(B, 3136, **f32)
+            self.zpart = torch.empty(14, B, 1024, **f32)   # fc1 split-K slabs (14 x 224)
+            self.h = torch.empty(B, 1024, **f32)
+            self.dz = torch.empty(B, 1024, **f32)
+            self.dY2 = torch.empty(B, 14, 14, 64, **f32)   # routed conv2 output gradient
+            self.db2p = torch.empty(int(ops.f32_db2_rows(B)), 64, **f32)
+            self.slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, **f32)
+            self.cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, **f32)
+            self.g2 = None
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
@@ -260,7 +285,7 @@ class FusedMNISTTrainer:
         # tail-only blocks on the CUs the conv roles leave idle, conv blocks joining as they finish —
         # and conv2_wgrad_reduce applies Adam to every other parameter as it produces the gradients.
         # Measured (B=100): 78.4 us/step vs 80.0 us with the flat adam_step launch.
-        self.fused_opt = (os.environ.get("MIHVD_FUSED_OPT", "1") != "0" and not self.collectives
+        self.fused_opt = (os.environ.get("MIHVD_FUSED_OPT", "1") != "0" and not self.collectives and not self.f32
                           and not self.pipeline and not self.fuse_w3)
         # Fused optimizer split of dense/kernel: the first MIHVD_REDUCE_W3 of its rows (a fraction,
         # rounded to 256 elements) are updated by the gradient-reduction launch next to the conv
@@ -334,6 +359,8 @@ class FusedMNISTTrainer:
         self._refresh_shadow()
 
     def _refresh_shadow(self):
+        if self.shadow is None:  # fp32 step: the kernels read the fp32 parameters
+            return
         self.ops.scale_cast_bf16(self.params, self.shadow, 1.0)
         if getattr(self, "shadow3", None) is not None:
             self.shadow3[:3136].copy_(self.pview("dense/kernel", self.shadow))
@@ -390,6 +417,8 @@ class FusedMNISTTrainer:
 
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
+        if self.f32:
+            return self._launch_step_f32(x, rows, labels)
         if self.gather:
             return self._launch_step_gather(x, rows, labels)
         o = self.ops
@@ -494,6 +523,45 @@ class FusedMNISTTrainer:
             self._allreduce(self.grads, 0, FLAT_NUMEL)  # one fused collective for the whole buffer
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
+
+    def _launch_step_f32(self, x, rows, labels):
+        """Exact-fp32 step (csrc/kernels/f32_fwd.hip, f32_bwd.hip), one stream at world size 1:
+
+            conv1 | conv2 | fc1_fwd | head | fc1_bwd (dgrad -> dY2, dW3, db3, dW4, db4) |
+            conv2_bwd (dgrad + fused conv1 wgrad, conv2 wgrad slabs) | conv reduce | adam
+
+        With collectives the "fc" bucket (dense/*, dense_1/*: 98.4 % of the bytes) is complete
+        after fc1_bwd and is allreduced on the side stream while the conv backward runs; the conv
+        bucket follows the reduction; Adam applies the 1/size of Average."""
+        o = self.ops
+        st = self.state
+        P, G = self.pview, self.gview
+        main = torch.cuda.current_stream(self.device)
+        w2 = P("conv_layer2/conv2d/kernel")
+        w3 = P("dense/kernel")
+        o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1, self.idx1)
+        o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
+        o.f32_fc1_fwd(self.a2, w3, self.zpart)
+        o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
+                           self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
+                      G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+        overlap = self.collectives and self.overlap
+        if overlap:
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                self._allreduce(self.grads[FC_START:], FC_START, FLAT_NUMEL)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab)
+        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
+                          G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
+        if overlap:
+            self._allreduce(self.grads[:FC_START], 0, FC_START)
+            main.wait_stream(self._side)
+        elif self.collectives:
+            self._allreduce(self.grads, 0, FLAT_NUMEL)
+        b1, b2 = self.betas
+        o.adam_step(self.params, self.grads, self.m, self.v, None, st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world,
+                    self.rule, 1)
 
     def _launch_step_gather(self, x, rows, labels):
         """Step with the factor-gather data plane over the process group (RCCL; see ``__init__``).
@@ -837,6 +905,39 @@ class FusedMNISTTrainer:
             g.replay()
         self.global_step += k
 
+    def run_steps(self, k: int, steps_per_replay: int = 10) -> int:
+        """Advance exactly ``k`` steps on the resident dataset, graph-replayed: the first call
+        captures a graph of ``steps_per_replay`` steps (after one eager warm-up step, which counts),
+        whole replays follow, and a remainder replays a graph of that length (captured once).
+        Falls back to eager steps where capture is impossible. Returns the steps advanced."""
+        k = int(k)
+        done = 0
+        if k <= 0:
+            return 0
+        if self.graph is None and not getattr(self, "_graph_tried", False):
+            self._graph_tried = True
+            self.build_graph(steps_per_replay=steps_per_replay, warmup=1)  # the warm-up step counts
+            done += 1
+        spr = self.steps_per_replay
+        while self.graph is not None and k - done >= spr:
+            self.run_graph()
+            done += spr
+        r = k - done
+        if r > 0:
+            if self.graph is not None:
+                if r not in self._graphs:
+                    self.build_graph(steps_per_replay=r, warmup=0, primary=False)
+                self.run_graph(r)
+            else:
+                for _ in range(r):
+                    self.device_step()
+            done += r
+        return done
+
+    def loss_tensor(self) -> torch.Tensor:
+        """The last step's mean loss as a device scalar (reading it synchronises)."""
+        return self.stats[:, 0].mean()
+
     def last_loss(self) -> float:
         self.check_xgmi()
         return float(self.stats[:, 0].mean())
@@ -980,17 +1081,25 @@ class FusedMNISTTrainer:
 
                 warn_fallback("validation against the process group's collectives failed")
         cands = [(p, sh) for p in planes for sh in dict.fromkeys(shard_options)]
-        if len(cands) == 1 or self._host_collectives():
+        host = self._host_collectives()
+        # host (gloo) collectives cannot be captured or timed meaningfully: the candidates still run
+        # (eagerly) for the consistency check below unless MIHVD_XGMI_CHECK=0, and the first
+        # consistent candidate is kept
+        if len(cands) == 1 or (host and os.environ.get("MIHVD_XGMI_CHECK", "1") == "0"):
             self._set_plane(cands[0][0] == "xgmi", cands[0][1])
             rep["plane"], rep["shard"] = cands[0]
             return rep
         times = {}
+        finals = {}
         k = max(1, min(steps_per_replay, steps))
-        # the timed candidates run real training steps: the model, optimizer and step state are
-        # restored afterwards, so selection leaves no trace (nor NaN from a poisoned collective)
+        # the timed candidates run real training steps: the model, optimizer, step state and data
+        # order are restored before each candidate and afterwards, so every candidate trains the
+        # same steps on the same batches and selection leaves no trace (nor NaN from a poisoned
+        # collective)
         snap = self._snapshot()
         for plane, sh in cands:
             self._set_plane(plane == "xgmi", sh)
+            self._restore(snap)
             captured = self.build_graph(steps_per_replay=k, warmup=1)
             torch.cuda.synchronize(self.device)
             dist.barrier()
@@ -1002,6 +1111,33 @@ class FusedMNISTTrainer:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
             times[(plane, sh)] = float(el.item()) / (max(1, steps // k) * k) * 1e6
             rep["captured"] = captured
+            self.gather_full_state()
+            finals[(plane, sh)] = self.params.clone()
+        # End-to-end check of the xGMI plane's cross-GPU visibility (xgmi_role.h): the graph-replayed
+        # steps of every xGMI candidate must land where RCCL's steps with the same sharding landed,
+        # from the same snapshot on the same batches — to fp32 summation-order differences (the
+        # one-shot sum adds ranks in rank order, RCCL's ring in ring order). A stale peer read
+        # (a gather that saw the previous step's rows) moves the result by the size of a whole
+        # gradient term; on any mismatch, on any rank, every rank drops the plane.
+        cons = {}
+        for (plane, sh), fin in finals.items():
+            ref = finals.get(("rccl", sh))
+            if plane != "xgmi" or ref is None:
+                continue
+            upd = (ref - snap["params"]).norm().item()
+            d = (fin - ref).norm().item() / max(upd, 1e-30)
+            cons[f"xgmi-{'shard' if sh else 'replicated'}"] = d if math.isfinite(d) else float("inf")
+        if cons:
+            from ..parallel.xgmi import _group_ok, warn_fallback
+
+            tol = float(os.environ.get("MIHVD_XGMI_CHECK_TOL", "1e-3"))
+            ok = _group_ok(all(v <= tol for v in cons.values()), None, self.device)
+            rep["consistency"] = {key: round(v, 9) for key, v in cons.items()}
+            rep["consistent"] = ok
+            if not ok:
+                times = {key: t for key, t in times.items() if key[0] != "xgmi"}
+                self._xplane_failed = True
+                warn_fallback("graph-replayed steps on the xGMI plane disagree with RCCL's from the same snapshot")
         if any(p == "xgmi" for p, _ in cands):
             # a device-side phase barrier that timed out (a peer that never arrived) poisoned its
             # outputs: every rank then drops the plane for good and keeps RCCL
@@ -1014,7 +1150,10 @@ class FusedMNISTTrainer:
                 warn_fallback("a collective timed out while the plane was timed")
                 if not times:  # pragma: no cover - 'on' mode: nothing else was timed
                     times = {("rccl", cands[0][1]): float("nan")}
-        plane, sh = min(times, key=lambda key: (times[key] != times[key], times[key]))
+        if host:
+            plane, sh = next(c for c in cands if c in times)
+        else:
+            plane, sh = min(times, key=lambda key: (times[key] != times[key], times[key]))
         self._set_plane(plane == "xgmi", sh)
         self._restore(snap)
         rep["us_per_step"] = {f"{p}{'-shard' if s else '-replicated'}": round(t, 2) for (p, s), t in times.items()}
@@ -1023,10 +1162,17 @@ class FusedMNISTTrainer:
 
     def _snapshot(self) -> dict:
         """Device copies of everything a training step changes (weights, Adam slots, step state)."""
+        import copy
+
         self._join()
         self.gather_full_state()
-        return {"params": self.params.clone(), "m": self.m.clone(), "v": self.v.clone(), "state": self.state.clone(),
+        snap = {"params": self.params.clone(), "m": self.m.clone(), "v": self.v.clone(), "state": self.state.clone(),
                 "global_step": self.global_step}
+        if self.rows is not None:  # the resident dataset's current epoch order and its RNG
+            torch.cuda.synchronize(self.device)
+            snap["rows"] = self.rows.clone()
+            snap["rng"] = copy.deepcopy(self._rng.bit_generator.state)
+        return snap
 
     def _restore(self, snap: dict):
         """Back to a _snapshot() (collective when the dense/kernel optimizer is sharded)."""
@@ -1034,6 +1180,9 @@ class FusedMNISTTrainer:
         torch.cuda.synchronize(self.device)
         for name in ("params", "m", "v", "state"):
             getattr(self, name).copy_(snap[name])
+        if "rows" in snap and self.rows is not None:
+            self.rows.copy_(snap["rows"])
+            self._rng.bit_generator.state = snap["rng"]
         self.global_step = snap["global_step"]
         self._full_state_valid = True
         self._refresh_shadow()  # (and the full W3 row shadow of the factor-gather plane)

@@ -12,8 +12,11 @@ mismatching RCCL/gloo calls, which is what Horovod's coordinator guarantees
 
 Consecutive ready allreduces with the same (dtype, device, op, process set, compression, scale
 factors) are fused into one flat buffer up to the fusion threshold (``MIHVD_FUSION_THRESHOLD``,
-64 MiB): one RCCL call per fused group, copied back into each tensor when its handle is waited on
-(Horovod's MEMCPY_IN_FUSION_BUFFER / MEMCPY_OUT_FUSION_BUFFER). The coordinator also checks that all
+64 MiB): one RCCL call per fused group (Horovod's MEMCPY_IN_FUSION_BUFFER / collective /
+MEMCPY_OUT_FUSION_BUFFER). The fusion buffer is persistent — one per fuse key, allocated on first
+use and only re-allocated to grow — so the negotiated path allocates nothing per step; the copy-out
+is issued by the executor right behind the collective (stream-ordered on GPUs; gloo's CPU work is
+waited for first), which is what makes the single buffer safe to refill for the next group. The coordinator also checks that all
 ranks submitted the same signature (op, dtype, shape) for a name and reports tensors that some ranks
 never submitted (the stall inspector, with the list of missing ranks).
 """
@@ -30,8 +33,7 @@ log = logging.getLogger("mihvd.engine")
 
 
 class _Entry:
-    __slots__ = ("name", "kind", "launch", "fuse_key", "tensor", "nbytes", "work", "flat", "offset", "error",
-                 "launched", "post_copy")
+    __slots__ = ("name", "kind", "launch", "fuse_key", "tensor", "nbytes", "work", "offset", "error", "launched")
 
     def __init__(self, name, kind, launch=None, fuse_key=None, tensor=None):
         self.name = name
@@ -41,7 +43,6 @@ class _Entry:
         self.tensor = tensor          # fusable allreduce: the wire tensor, reduced in place
         self.nbytes = tensor.numel() * tensor.element_size() if tensor is not None else 0
         self.work = None
-        self.flat = None
         self.offset = 0
         self.error = None
         self.launched = threading.Event()
@@ -62,10 +63,6 @@ class DeferredWork:
             raise e.error
         if e.work is not None:
             e.work.wait()
-        if e.flat is not None and not self._copied:
-            n = e.tensor.numel()
-            e.tensor.copy_(e.flat[e.offset:e.offset + n].view_as(e.tensor))
-            self._copied = True
         return True
 
     def is_completed(self) -> bool:
@@ -87,6 +84,8 @@ class Engine:
         self._stop = threading.Event()
         self.fused_launches = 0
         self.launches = 0
+        self._fusion: dict = {}       # fuse key -> persistent flat buffer (grown, never per step)
+        self.fusion_allocs = 0
         self._thread = threading.Thread(target=self._loop, name="mihvd-engine", daemon=True)
         self._thread.start()
 
@@ -191,12 +190,27 @@ class Engine:
             if len(group) == 1:
                 e0.work = dist.all_reduce(e0.tensor, op=torch_op, group=process_group, async_op=True)
             else:
-                flat = torch.cat([g.tensor.reshape(-1) for g in group])   # MEMCPY_IN_FUSION_BUFFER
-                work = dist.all_reduce(flat, op=torch_op, group=process_group, async_op=True)
+                n = sum(g.tensor.numel() for g in group)
+                buf = self._fusion.get(e0.fuse_key)
+                if buf is None or buf.numel() < n:
+                    buf = torch.empty(n, dtype=e0.tensor.dtype, device=e0.tensor.device)
+                    self._fusion[e0.fuse_key] = buf
+                    self.fusion_allocs += 1
+                flat = buf[:n]
                 off = 0
+                for g in group:                                           # MEMCPY_IN_FUSION_BUFFER
+                    k = g.tensor.numel()
+                    flat[off:off + k].copy_(g.tensor.reshape(-1))
+                    g.offset = off
+                    off += k
+                work = dist.all_reduce(flat, op=torch_op, group=process_group, async_op=True)
+                # MEMCPY_OUT_FUSION_BUFFER right behind the collective: on GPUs the wait only orders
+                # the current stream after it; gloo's CPU work completes here
+                work.wait()
                 for g in group:
-                    g.work, g.flat, g.offset = work, flat, off
-                    off += g.tensor.numel()
+                    k = g.tensor.numel()
+                    g.tensor.copy_(flat[g.offset:g.offset + k].view_as(g.tensor))
+                    g.work = None
                 self.fused_launches += 1
         except Exception as exc:
             for g in group:

@@ -80,6 +80,7 @@ class SessionRunContext:
     def __init__(self, session):
         self.session = session
         self._stop = False
+        self.steps = 1  # training steps this run advanced (a graph-replayed run covers several)
 
     def request_stop(self):
         self._stop = True
@@ -174,7 +175,11 @@ class LoggingTensorHook(SessionRunHook):
         self.lines: list[str] = []
 
     def after_run(self, run_context, run_values):
-        if self._iter % self.every_n == 0:
+        # iteration cadence counted in training steps: a run that advanced k steps covers the
+        # iterations [_iter, _iter + k); log if one of them is a multiple of every_n (k = 1: TF's rule)
+        k = max(1, int(getattr(run_context, "steps", 1)))
+        due = (self._iter + k - 1) // self.every_n * self.every_n >= self._iter
+        if due:
             vals = {}
             res = run_values.results or {}
             for name, key in self.tensors.items():
@@ -194,7 +199,7 @@ class LoggingTensorHook(SessionRunHook):
             else:
                 line = log_kv("", **vals, **({"sec": round(el, 3)} if el is not None else {}))
             self.lines.append(line)
-        self._iter += 1
+        self._iter += k
 
 
 class StepCounterHook(SessionRunHook):
@@ -229,24 +234,56 @@ class StepCounterHook(SessionRunHook):
 
 
 class CheckpointSaverHook(SessionRunHook):
-    def __init__(self, checkpoint_dir, save_secs=600, save_steps=None, max_to_keep=5):
+    """Rank-0 checkpoints in the TF1 layout (``checkpoint`` index + ``model.ckpt-<step>``).
+
+    ``collective=True`` (a train state whose variables are sharded across ranks, e.g. the fused
+    trainer's sharded dense/kernel optimizer): the hook runs on EVERY rank, all ranks call the
+    state's collective ``gather_full_state()`` at the same step, and only the rank with a
+    ``checkpoint_dir`` (rank 0) writes. Step triggers are deterministic on every rank; the time
+    trigger is rank 0's clock, broadcast to the others every ``sync_steps`` steps."""
+
+    def __init__(self, checkpoint_dir, save_secs=600, save_steps=None, max_to_keep=5, collective=False,
+                 sync_steps=500):
         self.mgr = ckpt.CheckpointManager(checkpoint_dir, save_secs, save_steps, max_to_keep)
+        self.writer = checkpoint_dir is not None
+        self.collective = collective
+        self.sync_steps = max(1, int(sync_steps))
         self.saved: list[str] = []
+        self._prev = 0
 
     def after_create_session(self, session, coord=None):
         self.mgr._last_step = session.state.global_step
+        self._prev = session.state.global_step
+
+    def _due(self, step: int) -> bool:
+        if not self.collective:
+            return self.mgr.should_save(step)
+        m = self.mgr
+        due = bool(m.save_steps) and (m._last_step is None or step - m._last_step >= m.save_steps)
+        if m.save_secs and step // self.sync_steps != self._prev // self.sync_steps:
+            mine = (time.time() - m._last_t >= m.save_secs) if self.writer else None
+            due = due or bool(broadcast_object(mine, 0))
+        return due
+
+    def _save(self, session, step: int):
+        if self.collective and hasattr(session.state, "gather_full_state"):
+            session.state.gather_full_state()  # collective: every rank, same step
+        if self.writer:
+            session.state_sync()
+            self.saved.append(self.mgr.save(session.state.variables(), step))
+        else:
+            self.mgr._last_step, self.mgr._last_t = step, time.time()
 
     def after_run(self, run_context, run_values):
         step = run_context.session.state.global_step
-        if self.mgr.should_save(step):
-            run_context.session.state_sync()
-            self.saved.append(self.mgr.save(run_context.session.state.variables(), step))
+        if self._due(step):
+            self._save(run_context.session, step)
+        self._prev = step
 
     def end(self, session):
         step = session.state.global_step
         if self.mgr._last_step != step:
-            session.state_sync()
-            self.saved.append(self.mgr.save(session.state.variables(), step))
+            self._save(session, step)
 
 
 # ------------------------------------------------------------------------------------------ #
@@ -265,8 +302,11 @@ class MonitoredTrainingSession:
         self.state = state
         self.checkpoint_dir = checkpoint_dir
         self.hooks = list(hooks)
-        if checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps):
-            self.hooks.append(CheckpointSaverHook(checkpoint_dir, save_checkpoint_secs, save_checkpoint_steps, max_to_keep))
+        # a state sharded across ranks checkpoints collectively: the saver hook runs on every rank
+        collective = (hasattr(state, "gather_full_state") and _b.is_initialized() and _b.size() > 1)
+        if (checkpoint_dir or collective) and (save_checkpoint_secs or save_checkpoint_steps):
+            self.hooks.append(CheckpointSaverHook(checkpoint_dir, save_checkpoint_secs, save_checkpoint_steps, max_to_keep,
+                                                  collective=collective))
         if log_step_count_steps:
             self.hooks.append(StepCounterHook(log_step_count_steps))
         self.hooks.extend(chief_only_hooks)
@@ -307,6 +347,7 @@ class MonitoredTrainingSession:
         if self.state.global_step == before:
             # states that count their own steps (the fused trainer) are not advanced twice
             self.state.global_step += 1
+        ctx.steps = self.state.global_step - before
         if res is not None and not isinstance(res, dict):
             res = {"result": res}
         vals = SessionRunValues(res)

@@ -2,7 +2,9 @@
 
 Spec: ``kind:key=val:...;kind2:...`` with kinds ``kill`` (exit with ``code``, default 1),
 ``delay`` (sleep ``ms``), ``hang`` (sleep ``s``, default 3600 — the stall inspector must catch it),
-``raise`` (RuntimeError) and ``nan`` (returns True so the caller poisons a gradient).
+``raise`` (RuntimeError), ``nan`` (returns True so the caller poisons a gradient) and ``collerr``
+(a communicator async error of ``code``, default 6 = remote error, reported to the native health
+monitor, which aborts the communicator and exits with 134 like a real RCCL failure).
 ``rank=`` and ``step=`` select where it fires (absent = everywhere / every step).
 """
 from __future__ import annotations
@@ -32,4 +34,10 @@ def maybe_inject(step: int) -> bool:
             raise RuntimeError(f"MIHVD_FAULT: injected failure at step {step}")
         elif a.kind == "nan":
             nan = True
+        elif a.kind == "collerr":
+            mon = basics._ctx.health
+            if mon is None:
+                raise RuntimeError("MIHVD_FAULT collerr needs the health monitor (MIHVD_HEALTH=1)")
+            mon.inject_error(int(a.args.get("code", "6")), f"MIHVD_FAULT at step {step}")
+            time.sleep(float(a.args.get("s", "30")))  # the monitor exits the process meanwhile
     return nan

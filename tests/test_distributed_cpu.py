@@ -112,6 +112,24 @@ def test_fault_kill_tears_down_job(tmp_path):
     assert outs == [None, None]
 
 
+def test_collective_async_error_aborts_every_rank(tmp_path):
+    """An asynchronous communicator error on rank 1 (injected into the native health monitor, as
+    RCCL's ncclCommGetAsyncError would report it) makes that rank abort its communicator and exit
+    134; the launcher then tears down rank 0, which is blocked in the next collective (mpirun
+    semantics, tensorflow-mnist.yaml:17-38). Both exit promptly, not at the collective timeout."""
+    import time
+
+    t0 = time.time()
+    p, outs = run_scenario(tmp_path, "fault", env={"MIHVD_FAULT": "collerr:rank=1:step=3",
+                                                   "MIHVD_HEALTH_POLL_S": "0.2"}, expect_ok=False, timeout=120)
+    el = time.time() - t0
+    assert p.returncode == 134, p.stderr[-2000:]
+    assert "mihvd health: RCCL async error 6" in p.stderr
+    assert "rank 1 exited with code 134" in p.stderr
+    assert outs == [None, None]
+    assert el < 60, el
+
+
 NEG = {"MIHVD_NEGOTIATE": "1"}
 
 
@@ -143,6 +161,19 @@ def test_negotiation_rejects_mismatched_shapes(tmp_path):
     for o in (a, b):
         assert o["error"] and "mismatched collective 'allreduce.shape_mismatch'" in o["error"]
         assert o["after"] == [2.0] * 3
+
+
+def test_negotiated_fusion_buffer_is_persistent(tmp_path):
+    """The negotiated path fuses ready allreduces into one persistent buffer: no allocation per step."""
+    _, outs = run_scenario(tmp_path, "negotiated_fusion", env=NEG)
+    for o in outs:
+        assert o["ok"], o
+        assert o["fused"] > 0, o
+        assert o["allocs"][-1] == o["allocs"][1] <= 2, o  # grown at most once, then reused
+        # response cache: after the first step the same 6 names are posted as cached slots, several
+        # per bit-vector record
+        assert o["cache_hits"] >= o["submitted"] - 2 * 6, o
+        assert o["records"] < o["submitted"], o
 
 
 def test_dp_equivalence_negotiated(tmp_path):

@@ -1,0 +1,267 @@
+"""Exact-fp32 fused step (csrc/kernels/f32_fwd.hip, f32_bwd.hip) against plain PyTorch fp32.
+
+The reference's launched entrypoint trains in fp32 (horovod/tensorflow_mnist.py:118-121,130), so
+these kernels take fp32 operands on the fp32-input MFMAs: every comparison here is against the
+stock fp32 model / fp32 torch ops with fp32-rounding tolerances (summation order only). Batch sizes
+include non-multiples of 16 to catch tiling bugs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from mihvd import _native
+
+    _native.require_kernels()
+    return torch.ops.mihvd
+
+
+def rel_err(a, b):
+    return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+
+
+def ref_conv_pool(x_nhwc, w_hwio, b):
+    """conv SAME + bias + ReLU + maxpool 2x2 -> (pooled NHWC, argmax d = 2 dy + dx)."""
+    y = F.relu(F.conv2d(x_nhwc.permute(0, 3, 1, 2), w_hwio.permute(3, 2, 0, 1), b, padding=2))
+    pooled, ind = F.max_pool2d(y, 2, 2, return_indices=True)
+    W = y.shape[-1]
+    d = ((ind // W) % 2) * 2 + (ind % W) % 2
+    return pooled.permute(0, 2, 3, 1), d.permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("B", [7, 100])
+def test_f32_conv1_fwd(ops, B):
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.rand(B, 784, device="cuda", generator=g)
+    w = torch.randn(5, 5, 1, 32, device="cuda", generator=g) * 0.2
+    b = torch.randn(32, device="cuda", generator=g) * 0.1
+    a1 = torch.empty(B, 14, 14, 32, device="cuda")
+    idx = torch.empty(B, 14, 14, 32, device="cuda", dtype=torch.uint8)
+    ops.f32_conv1_fwd(x, None, None, w.reshape(800), b, a1, idx)
+    ref, rd = ref_conv_pool(x.view(B, 28, 28, 1), w, b)
+    assert rel_err(a1, ref) < 1e-6
+    pos = ref > 1e-4
+    assert (idx.long()[pos] == rd[pos]).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("B", [7, 100, 128])
+def test_f32_conv2_fwd(ops, B):
+    g = torch.Generator(device="cuda").manual_seed(2)
+    a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
+    w = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
+    b = torch.randn(64, device="cuda", generator=g) * 0.1
+    a2 = torch.empty(B, 3136, device="cuda")
+    idx = torch.empty(B, 3136, device="cuda", dtype=torch.uint8)
+    ops.f32_conv2_fwd(a1, w, b, a2, idx)
+    ref, rd = ref_conv_pool(a1, w, b)
+    assert rel_err(a2, ref.reshape(B, 3136)) < 1e-6
+    pos = ref.reshape(B, 3136) > 1e-4
+    assert (idx.long()[pos] == rd.reshape(B, 3136)[pos]).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("B", [7, 100])
+def test_f32_fc1_fwd_and_head(ops, B):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    a2 = torch.rand(B, 3136, device="cuda", generator=g)
+    w3 = torch.randn(3136, 1024, device="cuda", generator=g) * 0.02
+    zpart = torch.empty(14, B, 1024, device="cuda")
+    ops.f32_fc1_fwd(a2, w3, zpart)
+    z = a2.double() @ w3.double()
+    assert rel_err(zpart.sum(0), z) < 1e-6
+    b3 = torch.randn(1024, device="cuda", generator=g) * 0.1
+    w4 = torch.randn(1024, 10, device="cuda", generator=g) * 0.05
+    b4 = torch.randn(10, device="cuda", generator=g) * 0.1
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    h = torch.empty(B, 1024, device="cuda")
+    dz = torch.empty(B, 1024, device="cuda")
+    dlog = torch.empty(B, 10, device="cuda")
+    stats = torch.empty(B, 2, device="cuda")
+    ops.f32_head_fwd_bwd(zpart, b3, w4, b4, y, None, None, 0, 0.0, h, dz, dlog, stats)
+    zr = (z.float() + b3).requires_grad_(True)
+    hr = F.relu(zr)
+    logits = hr @ w4 + b4
+    loss = F.cross_entropy(logits, y)
+    loss.backward()
+    assert rel_err(h, hr) < 1e-6
+    assert abs(stats[:, 0].mean().item() - loss.item()) < 1e-5
+    assert rel_err(dz, zr.grad) < 1e-5
+    assert rel_err(dlog, torch.softmax(logits, 1).sub(F.one_hot(y, 10).float()).div(B)) < 1e-5
+
+
+@pytest.mark.parametrize("B", [7, 100])
+def test_f32_fc1_bwd(ops, B):
+    """dgrad routed into dY2 (and the db2 partial rows), dW3, db3, dW4, db4 vs autograd."""
+    g = torch.Generator(device="cuda").manual_seed(4)
+    a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
+    w2 = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
+    b2 = torch.randn(64, device="cuda", generator=g) * 0.1
+    a2 = torch.empty(B, 3136, device="cuda")
+    idx2 = torch.empty(B, 3136, device="cuda", dtype=torch.uint8)
+    ops.f32_conv2_fwd(a1, w2, b2, a2, idx2)
+    w3 = torch.randn(3136, 1024, device="cuda", generator=g) * 0.02
+    dz = torch.randn(B, 1024, device="cuda", generator=g)
+    h = torch.rand(B, 1024, device="cuda", generator=g)
+    dlog = torch.randn(B, 10, device="cuda", generator=g)
+    dY2 = torch.full((B, 14, 14, 64), float("nan"), device="cuda")
+    db2p = torch.empty(int(ops.f32_db2_rows(B)), 64, device="cuda")
+    gW3 = torch.empty(3136, 1024, device="cuda")
+    gb3, gW4, gb4 = torch.empty(1024, device="cuda"), torch.empty(1024, 10, device="cuda"), torch.empty(10, device="cuda")
+    ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4)
+    # reference: y2 pre-pool through autograd
+    a1r = a1.permute(0, 3, 1, 2)
+    y2 = F.conv2d(a1r, w2.permute(3, 2, 0, 1), b2, padding=2).requires_grad_(True)
+    p2 = F.max_pool2d(F.relu(y2), 2, 2).permute(0, 2, 3, 1).reshape(B, 3136)
+    p2.backward(dz @ w3.t())
+    ref_dY2 = y2.grad.permute(0, 2, 3, 1)
+    assert torch.isfinite(dY2).all()
+    assert rel_err(dY2, ref_dY2) < 1e-5
+    assert rel_err(db2p.sum(0), ref_dY2.sum((0, 1, 2))) < 1e-5
+    assert rel_err(gW3, a2.double().t() @ dz.double()) < 1e-6
+    assert rel_err(gb3, dz.sum(0)) < 1e-6
+    assert rel_err(gW4, h.double().t() @ dlog.double()) < 1e-6
+    assert rel_err(gb4, dlog.sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("B", [7, 100])
+def test_f32_conv2_bwd_and_reduce(ops, B):
+    """conv2 dgrad + fused conv1 wgrad, conv2 wgrad slabs, and the reduction, vs autograd of
+    conv1 -> pool -> conv2 with the routed conv2 gradient."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.rand(B, 784, device="cuda", generator=g)
+    w1 = torch.randn(5, 5, 1, 32, device="cuda", generator=g) * 0.2
+    b1 = torch.randn(32, device="cuda", generator=g) * 0.1
+    w2 = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
+    a1 = torch.empty(B, 14, 14, 32, device="cuda")
+    idx1 = torch.empty(B, 14, 14, 32, device="cuda", dtype=torch.uint8)
+    ops.f32_conv1_fwd(x, None, None, w1.reshape(800), b1, a1, idx1)
+    dY2 = torch.randn(B, 14, 14, 64, device="cuda", generator=g)
+    cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, device="cuda")
+    slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, device="cuda")
+    ops.f32_conv2_bwd(dY2, w2, a1, idx1, x, None, None, cpart, slab)
+    db2p = torch.randn(int(ops.f32_db2_rows(B)), 64, device="cuda", generator=g)
+    gW2, gW1, gb1, gb2 = (torch.empty(51200, device="cuda"), torch.empty(800, device="cuda"),
+                          torch.empty(32, device="cuda"), torch.empty(64, device="cuda"))
+    ops.f32_conv_reduce(slab, cpart, db2p, gW2, gW1, gb1, gb2)
+    w1r = w1.clone().requires_grad_(True)
+    b1r = b1.clone().requires_grad_(True)
+    w2r = w2.clone().requires_grad_(True)
+    y1 = F.conv2d(x.view(B, 1, 28, 28), w1r.permute(3, 2, 0, 1), b1r, padding=2)
+    p1 = F.max_pool2d(F.relu(y1), 2, 2)
+    y2 = F.conv2d(p1, w2r.permute(3, 2, 0, 1), None, padding=2)
+    y2.backward(dY2.permute(0, 3, 1, 2))
+    assert rel_err(gW2.view(5, 5, 32, 64), w2r.grad) < 1e-5
+    assert rel_err(gW1.view(5, 5, 1, 32), w1r.grad) < 1e-5
+    assert rel_err(gb1, b1r.grad) < 1e-5
+    assert rel_err(gb2, db2p.sum(0)) < 1e-6
+
+
+def _tf_adam_(p, grad, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
+    """TF1 AdamOptimizer (tensorflow_mnist.py:130) in float64 on the host side of the test."""
+    m.mul_(b1).add_(grad, alpha=1 - b1)
+    v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+    lr_t = lr * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
+    p.sub_(lr_t * m / (v.sqrt() + eps))
+
+
+def _reference_model(seed):
+    from mihvd.models.mnist import MNISTConvNet
+
+    return MNISTConvNet(impl="torch", seed=seed, dropout_rate=0.0).cuda()
+
+
+@pytest.mark.parametrize("B", [8, 100])
+def test_f32_step_matches_fp32_model(ops, B):
+    """One fp32 fused step (dropout off) == the stock fp32 model: loss, every gradient and the TF1
+    Adam update, to fp32 summation-order tolerances."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.models.mnist import TF_PARAM_ORDER, softmax_cross_entropy
+
+    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, dropout=0.0, seed=3, device="cuda", precision="fp32")
+    g = torch.Generator(device="cuda").manual_seed(8)
+    x = torch.rand(B, 784, device="cuda", generator=g)
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    ref = _reference_model(3)
+    loss = softmax_cross_entropy(ref(x), y)
+    loss.backward()
+    out = tr.train_step(x, y)
+    torch.cuda.synchronize()
+    assert abs(out["loss"].item() - loss.item()) < 1e-5 * max(1.0, loss.item())
+    named = dict(ref.ordered_parameters())
+    for name in TF_PARAM_ORDER:
+        e = rel_err(tr.gview(name), named[name].grad)
+        assert e < 2e-5, (name, e)
+    for name in TF_PARAM_ORDER:
+        p = named[name].detach().double().clone()
+        m, v = torch.zeros_like(p), torch.zeros_like(p)
+        _tf_adam_(p, named[name].grad.double(), m, v, 1, 1e-3)
+        # |update| = lr for every element with a gradient: compare the update itself
+        d_ref = p - named[name].detach().double()
+        d_tr = tr.pview(name).double() - named[name].detach().double()
+        assert rel_err(d_tr, d_ref) < 1e-3, name
+
+
+def test_f32_trajectory_tracks_fp32_model_200_steps(ops):
+    """200 steps from the same init on the same batches (dropout off): the fused fp32 step and the
+    stock fp32 model + TF1 Adam stay on the same loss curve."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.models.mnist import TF_PARAM_ORDER, softmax_cross_entropy
+    from mihvd.utils.data import synthetic_mnist
+
+    B, steps = 100, 200
+    (xs, ys), _ = synthetic_mnist(n_train=20 * B, n_test=10, seed=11)
+    X = torch.from_numpy(xs.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(ys.astype("int64")).cuda()
+    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, dropout=0.0, seed=5, device="cuda", precision="fp32")
+    ref = _reference_model(5)
+    params = [p for _, p in ref.ordered_parameters()]
+    st = [(torch.zeros_like(p, dtype=torch.float64), torch.zeros_like(p, dtype=torch.float64)) for p in params]
+    master = [p.detach().double().clone() for p in params]
+    lt, lr_ = [], []
+    for s in range(steps):
+        i = s % 20
+        xb, yb = X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B]
+        lt.append(tr.train_step(xb, yb)["loss"].item())
+        for p in params:
+            p.grad = None
+        loss = softmax_cross_entropy(ref(xb), yb)
+        loss.backward()
+        lr_.append(loss.item())
+        with torch.no_grad():
+            for p, mp, (m, v) in zip(params, master, st):
+                _tf_adam_(mp, p.grad.double(), m, v, s + 1, 1e-3)
+                p.copy_(mp.float())
+    lt, lr_ = torch.tensor(lt), torch.tensor(lr_)
+    assert lr_[-20:].mean() < 0.5 * lr_[:5].mean()  # it trains
+    dev = ((lt - lr_).abs() / lr_.clamp_min(1e-3)).max().item()
+    assert dev < 2e-2, dev
+    named = dict(ref.ordered_parameters())
+    for name in TF_PARAM_ORDER:
+        assert rel_err(tr.pview(name), named[name].detach()) < 1e-2, name
+
+
+def test_f32_graph_replay_converges(ops):
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    (x, y), _ = synthetic_mnist(n_train=3000, n_test=10, seed=5)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    tr = FusedMNISTTrainer(batch_size=100, lr=1e-3, seed=0, device="cuda", precision="fp32")
+    tr.set_device_dataset(X, Y)
+    assert tr.build_graph(steps_per_replay=10)
+    first = None
+    for _ in range(30):
+        tr.run_graph()
+        if first is None:
+            first = tr.last_loss()
+    torch.cuda.synchronize()
+    assert tr.global_step == 2 + 300
+    assert int(tr.state[0].item()) == tr.global_step and int(tr.state[1].item()) == tr.global_step
+    assert tr.last_loss() < first * 0.5, (first, tr.last_loss())
+    assert tr.last_accuracy() > 0.8

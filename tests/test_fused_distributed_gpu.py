@@ -135,3 +135,67 @@ def test_bench_multirank_rehearsal_on_one_gpu(n):
     assert r["n_gpus"] == n and r["steps"] == 7 and r["warmup"] == 2 and r["value"] > 0
     assert r["config"]["global_batch"] == 100 * n and r["config"]["parallelism"] == f"dp{n}"
     assert r["config"]["final_loss"] == r["config"]["final_loss"]  # finite (NaN != NaN)
+
+
+@pytest.mark.parametrize("n,prec,gather,shard,xgmi", [
+    (4, "fp32", "0", "0", "off"), (8, "fp32", "0", "0", "off"),
+    (4, "bf16", "1", "1", "off"), (8, "bf16", "1", "1", "off"), (8, "bf16", "1", "0", "off"),
+    (8, "bf16", "0", "0", "off"), (8, "bf16", "1", "1", "on")])
+def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shard, xgmi):
+    """N ranks x B=50 sharing this GPU over gloo: the reduced gradient of the first step equals the
+    sum of the N single-process gradients (gradient rel < 1e-4), the update equals TF1 Adam on their
+    average, every rank holds identical parameters, and training makes progress. At 8 ranks the
+    factor-gather dW3 runs over Kw = 400 rows (the 4-group K-split tiles of the sharded slice)."""
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_SHARD_W3=shard,
+               MIHVD_XGMI=xgmi, MIHVD_TEST_PRECISION=prec, MIHVD_TEST_B="50", MIHVD_XGMI_TIMEOUT_MS="60000")
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", str(n), sys.executable, WORKER, "dp_gloo_n", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(n):
+        o = json.loads((tmp_path / f"dp_gloo_n.{r}.json").read_text())
+        assert o["rank_spread"] == 0.0, o
+        assert o["grad_rel"] < 1e-4, o
+        assert o["upd_rel"] < (1e-3 if prec == "fp32" else 1e-2), o
+        assert o["losses"][-1] < o["losses"][0], o
+        assert o["shard"] == (shard == "1" and prec == "bf16"), o
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_sharded_state_checkpoint_restore_broadcast_two_ranks(tmp_path, prec):
+    """tensorflow_mnist.py:143,157-167 with the optimizer state sharded across ranks: every rank
+    gathers before rank 0 saves; a new session restores on rank 0 and broadcasts; bitwise equal."""
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="off", MIHVD_TEST_PRECISION=prec)
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "ckpt_shard", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(2):
+        o = json.loads((tmp_path / f"ckpt_shard.{r}.json").read_text())
+        assert o["sharded"] == (prec == "bf16"), o
+        assert all(o["same"].values()), o
+        assert o["step"] == 5, o
+        if r == 0:
+            assert o["restored"].endswith("model.ckpt-5"), o
+            assert "model.ckpt-2.pt" in o["saved"] and "model.ckpt-4.pt" in o["saved"], o
+
+
+@pytest.mark.parametrize("stale", ["0", "1"])
+def test_xgmi_selection_consistency_check(tmp_path, stale):
+    """select_data_plane replays the same steps on the xGMI plane and on the process group from one
+    snapshot and compares the parameters; with stale peer reads injected (MIHVD_XGMI_DEBUG_STALE=1:
+    the gathers skip every other row, which keeps the previous step's values) the check fails on
+    every rank and the plane falls back to the process group."""
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="auto", MIHVD_XGMI_DEBUG_STALE=stale,
+               MIHVD_XGMI_TIMEOUT_MS="60000")
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "select_check", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(2):
+        o = json.loads((tmp_path / f"select_check.{r}.json").read_text())
+        assert o["valid"], o
+        if stale == "1":
+            assert o["consistent"] is False and o["final_plane"] == "rccl", o
+        else:
+            assert o["consistent"] is True and o["final_plane"] == "xgmi", o

@@ -87,6 +87,27 @@ def sc_dp_equivalence(outdir):
     out(outdir, "dp_equivalence", res)
 
 
+def sc_negotiated_fusion(outdir):
+    """MIHVD_NEGOTIATE=1: groups of small allreduces submitted together are fused by the engine
+    into its persistent fusion buffer — allocated once, reused every step."""
+    from mihvd import basics
+
+    r, n = hvd.rank(), hvd.size()
+    eng = basics._ctx.engine
+    allocs, ok = [], True
+    for step in range(6):
+        ts = [torch.full((k + 3,), float(r + step + k)) for k in range(6)]
+        hs = [hvd.allreduce_async(t, name=f"fz{k}", op=hvd.Sum) for k, t in enumerate(ts)]
+        outs = [hvd.synchronize(h) for h in hs]
+        for k, o in enumerate(outs):
+            ok &= bool(torch.allclose(o, torch.full((k + 3,), float(sum(q + step + k for q in range(n))))))
+        allocs.append(eng.fusion_allocs)
+    neg = eng.neg
+    out(outdir, "negotiated_fusion", {"ok": ok, "allocs": allocs, "fused": eng.fused_launches,
+                                      "submitted": neg.submitted, "cache_hits": neg.cache_hits,
+                                      "records": neg.records_posted})
+
+
 def sc_autotune(outdir):
     """MIHVD_AUTOTUNE=1: the optimizer tries each fusion threshold, every rank settles on the same
     one, re-plans its buckets once, and training still equals the single-process reference."""

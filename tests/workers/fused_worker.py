@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import mihvd.torch as hvd  # noqa: E402
-from mihvd.models.fused_mnist import FusedMNISTTrainer  # noqa: E402
+from mihvd.models.fused_mnist import W3_START as FLAT_W3, FusedMNISTTrainer  # noqa: E402
 from mihvd.utils.data import synthetic_mnist  # noqa: E402
 
 
@@ -152,6 +152,126 @@ def sc_dp_gloo_switch(outdir):
         tr.close()
     with open(os.path.join(outdir, f"dp_gloo_switch.{r}.json"), "w") as f:
         json.dump(rec, f)
+
+
+def _tf_adam_host(p, g, t, lr, b1=0.9, b2=0.999, eps=1e-8):
+    """One TF1 Adam step from zero slots, float64 (tensorflow_mnist.py:130)."""
+    m = (1 - b1) * g
+    v = (1 - b2) * g * g
+    lr_t = lr * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
+    return p - lr_t * m / (v.sqrt() + eps)
+
+
+def sc_dp_gloo_n(outdir):
+    """N ranks (gloo, all on cuda:0) x B=MIHVD_TEST_B samples: the first step's reduced gradient
+    equals the sum of N single-process gradients on the same per-rank batches (each from a world-1
+    trainer with the same weights), its update equals TF1 Adam on their average, and 10 more steps
+    keep every rank identical and the loss falling. Precision / data plane / sharding from env."""
+    r, n = hvd.rank(), hvd.size()
+    B = int(os.environ.get("MIHVD_TEST_B", "50"))
+    prec = os.environ.get("MIHVD_TEST_PRECISION", "bf16")
+    shard = os.environ.get("MIHVD_SHARD_W3", "0") == "1"
+    lr = 1e-3 * n
+    X, Y = data(n * B * 12, seed=7)
+    tr = FusedMNISTTrainer(batch_size=B, lr=lr, dropout=0.0, seed=1, device="cuda", precision=prec,
+                           shard_optimizer=shard)
+    tr.keep_w3_grad = True
+    tr.broadcast(0)
+    if os.environ.get("MIHVD_XGMI", "off") != "off" and tr.xplane is not None:
+        tr._set_plane(True, tr.shard_w3)
+    p0 = tr.params.clone()
+    ref = FusedMNISTTrainer(batch_size=B, lr=lr, dropout=0.0, seed=1, device="cuda", world_size=1, precision=prec)
+    ref.keep_w3_grad = True
+    snap = ref._snapshot()
+    gsum = torch.zeros_like(ref.grads)
+    for q in range(n):
+        ref._restore(snap)
+        ref.train_step(X[q * B:(q + 1) * B], Y[q * B:(q + 1) * B])
+        torch.cuda.synchronize()
+        gsum += ref.grads
+    tr.train_step(X[r * B:(r + 1) * B], Y[r * B:(r + 1) * B])
+    torch.cuda.synchronize()
+    red = tr.reduced_grads()
+    if tr.gather:
+        # the factor-gather plane forms dW3 only for the rows whose optimizer this rank owns
+        lo, hi = tr._w3_tiles
+        rows = slice(FLAT_W3 + lo * 64 * 1024, FLAT_W3 + min(hi * 64, 3136) * 1024)
+        red = torch.cat([red[:FLAT_W3], red[rows]])
+        gsum_c = torch.cat([gsum[:FLAT_W3], gsum[rows]])
+    else:
+        gsum_c = gsum
+    grel = ((red - gsum_c).norm() / gsum_c.norm()).item()
+    tr.gather_full_state()
+    upd = tr.params.double() - p0.double()
+    upd_ref = _tf_adam_host(p0.double(), gsum.double() / n, 1, lr) - p0.double()
+    urel = ((upd - upd_ref).norm() / upd_ref.norm()).item()
+    losses = []
+    for step in range(1, 11):
+        i = (step * n + r) * B
+        tr.train_step(X[i:i + B], Y[i:i + B])
+        losses.append(tr.last_loss())
+    tr.gather_full_state()
+    spread = hvd.allgather(tr.params.cpu().view(1, -1))
+    rec = {"grad_rel": grel, "upd_rel": urel, "losses": losses, "plane": tr.data_plane(), "shard": tr.shard_w3,
+           "gather": tr.gather, "rank_spread": (spread - spread[0]).abs().max().item(), "n": n}
+    tr.close()
+    with open(os.path.join(outdir, f"dp_gloo_n.{r}.json"), "w") as f:
+        json.dump(rec, f)
+
+
+def sc_ckpt_shard(outdir):
+    """2 ranks, sharded dense/kernel optimizer: MonitoredTrainingSession checkpoints (collective
+    gather on every rank, rank 0 writes), a fresh session restores on rank 0 and broadcasts; the
+    restored state equals the trained full state bit for bit on every rank."""
+    import mihvd.tensorflow as tfh
+
+    r = hvd.rank()
+    X, Y = data(1200, seed=9)
+    ck = os.path.join(outdir, "ckpt")
+    prec = os.environ.get("MIHVD_TEST_PRECISION", "bf16")
+
+    def session(tr, last):
+        hooks = [tfh.BroadcastGlobalVariablesHook(0), tfh.StopAtStepHook(last_step=last)]
+        with tfh.MonitoredTrainingSession(checkpoint_dir=ck if r == 0 else None, hooks=hooks, state=tr,
+                                          save_checkpoint_steps=2) as sess:
+            while not sess.should_stop():
+                s = tr.global_step
+                sess.run(lambda: tr.train_step(X[(2 * s + r) * 50:(2 * s + r + 1) * 50],
+                                               Y[(2 * s + r) * 50:(2 * s + r + 1) * 50]))
+        return sess
+
+    a = FusedMNISTTrainer(batch_size=50, lr=2e-3, dropout=0.0, seed=1, device="cuda", shard_optimizer=True,
+                          precision=prec)
+    sharded = a.shard_w3
+    session(a, 5)
+    a.gather_full_state()
+    full = {k: getattr(a, k).clone() for k in ("params", "m", "v")}
+    saved = sorted(os.listdir(ck)) if r == 0 else []
+    hvd.barrier()
+    b = FusedMNISTTrainer(batch_size=50, lr=2e-3, dropout=0.0, seed=2, device="cuda", shard_optimizer=True,
+                          precision=prec)
+    sess = session(b, 5)  # restores step 5 on rank 0, broadcasts, runs no step
+    b.gather_full_state()
+    same = {k: bool(torch.equal(getattr(b, k), full[k])) for k in full}
+    rec = {"sharded": sharded, "same": same, "restored": sess.restored_from, "step": b.global_step, "saved": saved}
+    a.close()
+    b.close()
+    with open(os.path.join(outdir, f"ckpt_shard.{r}.json"), "w") as f:
+        json.dump(rec, f)
+
+
+def sc_select_check(outdir):
+    """2 ranks: plane selection's end-to-end consistency check (xGMI vs RCCL steps from one snapshot)."""
+    r = hvd.rank()
+    X, Y = data(2000, seed=5)
+    tr = FusedMNISTTrainer(batch_size=50, lr=2e-3, seed=1, device="cuda", shard_optimizer=True)
+    tr.broadcast(0)
+    tr.set_device_dataset(X, Y, seed=3 + r)
+    rep = tr.select_data_plane(steps=6, steps_per_replay=3, shard_options=[True])
+    rep["final_plane"] = tr.data_plane()
+    tr.close()
+    with open(os.path.join(outdir, f"select_check.{r}.json"), "w") as f:
+        json.dump(rep, f)
 
 
 def main():
