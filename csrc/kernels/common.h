@@ -216,6 +216,21 @@ struct AdamArgs {
   int rule;
 };
 
+// CU count of the current device, queried once per device (launch-time grid sizing; a
+// hipDeviceGetAttribute per launch costs host time on every step of an eager loop).
+inline int device_cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] == 0) {
+    int n = 256;
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    cache[dev] = n > 0 ? n : 256;
+  }
+  return cache[dev];
+}
+
 // Profiling aid (scripts/kbench.py --roles): MIHVD_ROLE_ONLY=<r> makes a launch that packs several
 // block roles run only the blocks of role r, so each role can be timed on its own. Unset (the
 // normal case) every role runs.

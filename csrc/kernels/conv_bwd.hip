@@ -107,6 +107,10 @@ __device__ __forceinline__ void finish_dy_item(const DyItem& it, u16 g[4], int d
 // of 512 + 64 * SW threads, below) a hardware s_barrier would also wait for the streamers, so
 // the eight conv waves meet on an LDS counter instead: each wave adds 1 after its LDS accesses
 // have completed (workgroup release) and waits until the counter reaches 8 x its barrier count.
+// Set (atomic OR) by a ConvBarrier whose bounded wait ran out: the conv gradients of that launch
+// are invalid. Read and cleared by conv_barrier_error() (the trainer's check after every replay).
+__device__ unsigned g_conv_barrier_err = 0;
+
 template <bool SWB>
 struct ConvBarrier {
   unsigned* ctr;
@@ -118,10 +122,12 @@ struct ConvBarrier {
       gen += 8;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      // bounded: a broken count ends the wait (wrong results, not a hung GPU) after ~30 ms
-      for (int spin = 0; spin < (1 << 20) && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen;
-           ++spin)
+      // bounded: a broken count ends the wait (wrong results, not a hung GPU) after ~30 ms, and
+      // raises the device error word so the host reports it instead of training on it
+      int spin = 0;
+      for (; spin < (1 << 20) && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen; ++spin)
         __builtin_amdgcn_s_sleep(1);
+      if (spin == (1 << 20)) __hip_atomic_fetch_or(&g_conv_barrier_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
   }
@@ -864,9 +870,7 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
   if (w3t != nullptr) {
     // one 512-thread block per CU (144 KB of LDS): the tail-only blocks take the CUs the conv roles
     // leave free and start on the dW3 tiles at once (MIHVD_W3T_HEAD: their share, tuned on MI355X)
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int ncu = device_cu_count();
     const int grid = std::max(n_conv + 8, ncu);
     static const double head_frac = [] {
       const char* e = getenv("MIHVD_W3T_HEAD");
@@ -890,9 +894,7 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     // one block per CU (the conv roles' LDS): the extra tail-only blocks take the CUs the conv
     // roles leave free, and every conv block carries streamer waves, so the update streams from
     // the first cycle on every CU (the conv roles are latency-bound and leave HBM idle)
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int ncu = device_cu_count();
     const int grid = std::max(n_conv + 8, ncu);
     // MIHVD_TAIL_STREAMERS: streamer waves per compute block (0 .. 4; 768 threads at most)
     static const int sw = [] {
@@ -1096,4 +1098,21 @@ void conv2_bwd_adam_fold(const at::Tensor& g2, const at::Tensor& idx2, const at:
   if (!done) launch_reduce_adam(ra, slab, cpart, B_of(a1), gW2, gW1, gb1, gb2);
 }
 
+}  // namespace mihvd
+
+namespace mihvd {
+// Read (and with reset, clear) the conv barrier error word; waits for the current stream.
+int64_t conv_barrier_error(bool reset) {
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  unsigned v = 0;
+  TORCH_CHECK(hipStreamSynchronize(stream) == hipSuccess, "conv_barrier_error: stream sync failed");
+  TORCH_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_conv_barrier_err), sizeof(v)) == hipSuccess,
+              "conv_barrier_error: read failed");
+  if (reset && v) {
+    const unsigned z = 0;
+    TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_conv_barrier_err), &z, sizeof(z)) == hipSuccess,
+                "conv_barrier_error: reset failed");
+  }
+  return (int64_t)v;
+}
 }  // namespace mihvd

@@ -515,15 +515,33 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
 // ------------------------------------------------------------------------------------------ //
 // f32_conv_reduce: blocks [0, 50): dW2 (12,800 float4 = sum over the G slabs); [50, 63): dW1/db1
 // (64 elements x 4 row parts of the dgrad blocks' partial rows); 63: db2 (64 channels x 4 parts of
-// the fc1 dgrad blocks' rows).
+// the fc1 dgrad blocks' rows). With the optimizer fused (world size 1: the gradients are final
+// here) every block applies Adam to the elements it just produced, blocks [64, 64 + n_fc) apply it
+// to the small fc parameters [fc_lo, fc_hi) (dense/bias, dense_1/*, produced by fc1_bwd), and
+// block 0 advances the forward step counter (adam_step's bump): one launch for the gradient
+// reduction and the whole optimizer except dense/kernel (whose update is deferred into the next
+// conv2_fwd launch, f32_fwd.hip).
 // ------------------------------------------------------------------------------------------ //
+struct F32SmallAdam {
+  F32Adam a;               // p, g, m, v: the FLAT buffers (a.n4 unused); a.nblk = 0: no optimizer
+  int o_w1 = 0, o_b1 = 0, o_w2 = 0, o_b2 = 0;   // element offsets of the conv segments
+  int fc_lo = 0, fc_hi = 0;                     // the small fc range (multiple-of-4 bounds)
+};
+
 __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __restrict__ slab, int G,
                                                               const float* __restrict__ cpart, int ncp,
                                                               const float* __restrict__ db2p, int ndb,
                                                               float* __restrict__ gW2, float* __restrict__ gW1,
-                                                              float* __restrict__ gb1, float* __restrict__ gb2) {
+                                                              float* __restrict__ gb1, float* __restrict__ gb2,
+                                                              F32SmallAdam sa) {
   __shared__ float red[256];
   const int bid = blockIdx.x, t = threadIdx.x;
+  const bool opt = sa.a.nblk > 0;
+  AdamCoef c{};
+  if (opt) {
+    c = f32_adam_coef(sa.a);
+    if (bid == 0 && t == 0) const_cast<int64_t*>(sa.a.state)[ST_FWD] += 1;
+  }
   if (bid < 50) {
     const int i = bid * 256 + t;
     float4 s = reinterpret_cast<const float4*>(slab)[i];
@@ -535,26 +553,62 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       s.w += v.w;
     }
     reinterpret_cast<float4*>(gW2)[i] = s;
+    if (opt) {
+      const int64_t o = sa.o_w2 + 4 * i;
+      float4 pp = *reinterpret_cast<const float4*>(sa.a.p + o);
+      float4 mm = *reinterpret_cast<const float4*>(sa.a.m + o);
+      float4 vv = *reinterpret_cast<const float4*>(sa.a.v + o);
+      adam4_f32(pp, mm, vv, s, c);
+      *reinterpret_cast<float4*>(sa.a.p + o) = pp;
+      *reinterpret_cast<float4*>(sa.a.m + o) = mm;
+      *reinterpret_cast<float4*>(sa.a.v + o) = vv;
+    }
+    return;
+  }
+  if (bid >= 64) {  // small fc parameters: gradients already final (fc1_bwd)
+    const int64_t i = sa.fc_lo / 4 + (int64_t)(bid - 64) * 256 + t;
+    if (opt && i < sa.fc_hi / 4) {
+      float4 pp = reinterpret_cast<const float4*>(sa.a.p)[i];
+      const float4 gg = reinterpret_cast<const float4*>(sa.a.g)[i];
+      float4 mm = reinterpret_cast<const float4*>(sa.a.m)[i];
+      float4 vv = reinterpret_cast<const float4*>(sa.a.v)[i];
+      adam4_f32(pp, mm, vv, gg, c);
+      reinterpret_cast<float4*>(sa.a.p)[i] = pp;
+      reinterpret_cast<float4*>(sa.a.m)[i] = mm;
+      reinterpret_cast<float4*>(sa.a.v)[i] = vv;
+    }
     return;
   }
   const int e = t & 63, part = t >> 6;
   float s = 0.f;
+  int64_t po = -1;  // flat offset of the element this thread finishes (optimizer)
+  float gv = 0.f;
   if (bid < 63) {
     const int q = (bid - 50) * 64 + e;  // 0..831
     for (int r = part; r < ncp; r += 4) s += cpart[(int64_t)r * CP_F32 + q];
     red[t] = s;
     __syncthreads();
     if (t < 64) {
-      const float v = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
-      if (q < 800) gW1[q] = v;
-      else gb1[q - 800] = v;
+      gv = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
+      if (q < 800) {
+        gW1[q] = gv;
+        po = sa.o_w1 + q;
+      } else {
+        gb1[q - 800] = gv;
+        po = sa.o_b1 + (q - 800);
+      }
     }
-    return;
+  } else {
+    for (int r = part; r < ndb; r += 4) s += db2p[(int64_t)r * 64 + e];
+    red[t] = s;
+    __syncthreads();
+    if (t < 64) {
+      gv = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
+      gb2[e] = gv;
+      po = sa.o_b2 + e;
+    }
   }
-  for (int r = part; r < ndb; r += 4) s += db2p[(int64_t)r * 64 + e];
-  red[t] = s;
-  __syncthreads();
-  if (t < 64) gb2[e] = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
+  if (opt && po >= 0) adam1(sa.a.p[po], sa.a.m[po], sa.a.v[po], gv, c);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -654,7 +708,11 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
 }
 
 void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,
-                     at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2) {
+                     at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const c10::optional<at::Tensor>& params,
+                     const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
+                     const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, int64_t o_w1,
+                     int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo, int64_t fc_hi, double lr, double b1,
+                     double b2, double eps, double grad_scale, int64_t rule) {
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() % 51200 == 0 && slab.numel() > 0, "f32_conv_reduce: slab");
   TORCH_CHECK(cpart.dtype() == at::kFloat && cpart.numel() % CP_F32 == 0 && cpart.numel() > 0, "f32_conv_reduce: cpart");
   TORCH_CHECK(db2p.dtype() == at::kFloat && db2p.numel() % 64 == 0 && db2p.numel() > 0, "f32_conv_reduce: db2p");
@@ -662,12 +720,51 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
   chk_f32(gW1, 800, "f32_conv_reduce: gW1");
   chk_f32(gb1, 32, "f32_conv_reduce: gb1");
   chk_f32(gb2, 64, "f32_conv_reduce: gb2");
+  F32SmallAdam sa;
+  int n_fc = 0;
+  if (params.has_value() && params->defined()) {
+    TORCH_CHECK(grads.has_value() && m.has_value() && v.has_value() && state.has_value() && state->defined(),
+                "f32_conv_reduce: the fused optimizer needs params, grads, m, v and the step state");
+    const int64_t n = params->numel();
+    for (const at::Tensor* t : {&*params, &*grads, &*m, &*v})
+      TORCH_CHECK(t->is_cuda() && t->dtype() == at::kFloat && t->is_contiguous() && t->numel() == n &&
+                      ((uintptr_t)t->data_ptr() & 15) == 0,
+                  "f32_conv_reduce: flat fp32 buffers of one length expected");
+    TORCH_CHECK(o_w2 % 4 == 0 && fc_lo % 4 == 0 && fc_hi % 4 == 0 && 0 <= fc_lo && fc_lo <= fc_hi && fc_hi <= n,
+                "f32_conv_reduce: segment offsets");
+    TORCH_CHECK(o_w1 + 800 <= n && o_b1 + 32 <= n && o_w2 + 51200 <= n && o_b2 + 64 <= n,
+                "f32_conv_reduce: conv segments exceed the flat buffers");
+    TORCH_CHECK(gW2.data_ptr<float>() == grads->data_ptr<float>() + o_w2 &&
+                    gW1.data_ptr<float>() == grads->data_ptr<float>() + o_w1 &&
+                    gb1.data_ptr<float>() == grads->data_ptr<float>() + o_b1 &&
+                    gb2.data_ptr<float>() == grads->data_ptr<float>() + o_b2,
+                "f32_conv_reduce: the gradient outputs must be the flat gradient buffer at the given offsets");
+    sa.a.p = params->data_ptr<float>();
+    sa.a.g = grads->data_ptr<float>();
+    sa.a.m = m->data_ptr<float>();
+    sa.a.v = v->data_ptr<float>();
+    sa.a.state = state->data_ptr<int64_t>();
+    sa.a.lr = (float)lr;
+    sa.a.b1 = (float)b1;
+    sa.a.b2 = (float)b2;
+    sa.a.eps = (float)eps;
+    sa.a.gscale = (float)grad_scale;
+    sa.a.rule = (int)rule;
+    sa.a.nblk = 1;
+    sa.o_w1 = (int)o_w1;
+    sa.o_b1 = (int)o_b1;
+    sa.o_w2 = (int)o_w2;
+    sa.o_b2 = (int)o_b2;
+    sa.fc_lo = (int)fc_lo;
+    sa.fc_hi = (int)fc_hi;
+    n_fc = (int)((fc_hi - fc_lo) / 4 + 255) / 256;
+  }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  f32_conv_reduce_kernel<<<64, 256, 0, stream>>>(slab.data_ptr<float>(), (int)(slab.numel() / 51200),
-                                                 cpart.data_ptr<float>(), (int)(cpart.numel() / CP_F32),
-                                                 db2p.data_ptr<float>(), (int)(db2p.numel() / 64),
-                                                 gW2.data_ptr<float>(), gW1.data_ptr<float>(), gb1.data_ptr<float>(),
-                                                 gb2.data_ptr<float>());
+  f32_conv_reduce_kernel<<<64 + n_fc, 256, 0, stream>>>(slab.data_ptr<float>(), (int)(slab.numel() / 51200),
+                                                        cpart.data_ptr<float>(), (int)(cpart.numel() / CP_F32),
+                                                        db2p.data_ptr<float>(), (int)(db2p.numel() / 64),
+                                                        gW2.data_ptr<float>(), gW1.data_ptr<float>(),
+                                                        gb1.data_ptr<float>(), gb2.data_ptr<float>(), sa);
 }
 
 }  // namespace mihvd

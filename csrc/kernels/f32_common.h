@@ -55,4 +55,50 @@ __device__ __forceinline__ float pool4(const f32x4& c, int& best) {
   return m;
 }
 
+// Adam over a flat fp32 range with no bf16 shadow (the fp32 step's kernels read the fp32
+// parameters): the same adam1() as adam_step, so every schedule of the update agrees bit for bit.
+struct F32Adam {
+  float* p = nullptr;
+  const float* g = nullptr;
+  float* m = nullptr;
+  float* v = nullptr;
+  int64_t n4 = 0;              // float4 groups of the range
+  const int64_t* state = nullptr;
+  float lr = 0.f, b1 = 0.f, b2 = 0.f, eps = 0.f, gscale = 1.f;
+  int rule = 0;
+  int nblk = 0;                // blocks of the launch that stream this range (0: none)
+};
+
+__device__ __forceinline__ AdamCoef f32_adam_coef(const F32Adam& a) {
+  return adam_coef((float)a.state[ST_OPT], a.lr, a.b1, a.b2, a.eps, a.gscale, a.rule);
+}
+
+__device__ __forceinline__ void adam4_f32(float4& pp, float4& mm, float4& vv, const float4& gg, const AdamCoef& c) {
+  adam1(pp.x, mm.x, vv.x, gg.x, c);
+  adam1(pp.y, mm.y, vv.y, gg.y, c);
+  adam1(pp.z, mm.z, vv.z, gg.z, c);
+  adam1(pp.w, mm.w, vv.w, gg.w, c);
+}
+
+// Grid-stride stream of the range by blocks [0, a.nblk) of a launch (one float4 of each array per
+// lane per iteration, restrict-qualified locals: the loads of an iteration are all in flight).
+__device__ __forceinline__ void f32_adam_stream(const F32Adam& a, int bid) {
+  const AdamCoef c = f32_adam_coef(a);
+  float* __restrict__ p = a.p;
+  const float* __restrict__ g = a.g;
+  float* __restrict__ m = a.m;
+  float* __restrict__ v = a.v;
+  const int64_t stride = (int64_t)a.nblk * blockDim.x;
+  for (int64_t i = (int64_t)bid * blockDim.x + threadIdx.x; i < a.n4; i += stride) {
+    float4 pp = reinterpret_cast<const float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<const float4*>(m)[i];
+    float4 vv = reinterpret_cast<const float4*>(v)[i];
+    adam4_f32(pp, mm, vv, gg, c);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+}
+
 }  // namespace mihvd

@@ -124,15 +124,25 @@ __device__ __forceinline__ void w2_tap_store(float* dst, int t, const float4 (&w
   }
 }
 
-template <int TPB>
+// TAIL: the first ad.nblk blocks of the launch stream an Adam update instead (the previous step's
+// dense/kernel update, deferred into this MFMA-bound launch, which leaves HBM idle). They are first
+// in dispatch order, so they take the CUs before the conv blocks; a tail block and a conv block fit
+// one CU together (2 x 74 KB of LDS, 4 + 4 waves).
+template <int TPB, bool TAIL>
 __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, float* __restrict__ a2,
-                                                            uint8_t* __restrict__ idx2, int B) {
+                                                            uint8_t* __restrict__ idx2, int B, F32Adam ad) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
+  if constexpr (TAIL) {
+    if ((int)blockIdx.x < ad.nblk) {
+      f32_adam_stream(ad, blockIdx.x);
+      return;
+    }
+  }
   float* img = smf;
   float* wbuf = smf + C2F_MAXR * C2F_RS;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
-  const int nwin = 49 * B, T0 = blockIdx.x * TPB;
+  const int nwin = 49 * B, T0 = ((int)blockIdx.x - (TAIL ? ad.nblk : 0)) * TPB;
   const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
   const int b0 = gw0 / 49, b1i = gw1 / 49;
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
@@ -416,7 +426,43 @@ static int conv2f_tpb(int B) {
   return std::min(7, std::max(1, (nt + 255) / 256));
 }
 
-void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2) {
+// Adam operands of a flat fp32 range (p, g, m, v: same length, multiple of 4) for a fused update;
+// nblk = 0 when p is absent.
+static F32Adam f32_adam_args(const c10::optional<at::Tensor>& p, const c10::optional<at::Tensor>& g,
+                             const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
+                             const c10::optional<at::Tensor>& state, double lr, double b1, double b2, double eps,
+                             double gscale, int64_t rule, int nblk, const char* what) {
+  F32Adam a;
+  if (!(p.has_value() && p->defined())) return a;
+  TORCH_CHECK(g.has_value() && m.has_value() && v.has_value() && state.has_value() && state->defined(), what,
+              ": fused Adam needs p, g, m, v and the step state");
+  const int64_t n = p->numel();
+  for (const at::Tensor* t : {&*p, &*g, &*m, &*v})
+    TORCH_CHECK(t->is_cuda() && t->dtype() == at::kFloat && t->is_contiguous() && t->numel() == n &&
+                    ((uintptr_t)t->data_ptr() & 15) == 0,
+                what, ": Adam operands must be 16-byte aligned contiguous fp32 tensors of one length");
+  TORCH_CHECK(n % 4 == 0, what, ": Adam range must be a multiple of 4 elements");
+  a.p = p->data_ptr<float>();
+  a.g = g->data_ptr<float>();
+  a.m = m->data_ptr<float>();
+  a.v = v->data_ptr<float>();
+  a.n4 = n / 4;
+  a.state = state->data_ptr<int64_t>();
+  a.lr = (float)lr;
+  a.b1 = (float)b1;
+  a.b2 = (float)b2;
+  a.eps = (float)eps;
+  a.gscale = (float)gscale;
+  a.rule = (int)rule;
+  a.nblk = nblk;
+  return a;
+}
+
+void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
+                   const c10::optional<at::Tensor>& p3, const c10::optional<at::Tensor>& g3,
+                   const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
+                   const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
+                   double grad_scale, int64_t rule, int64_t tail_blocks) {
   const int B = a2.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv2_fwd: batch 1..128");
   check_f32(a1, (int64_t)B * 6272, "f32_conv2_fwd: a1");
@@ -431,21 +477,32 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
     const int r0 = 18 * (gw0 / 49) + 2 * ((gw0 % 49) / 7), r1 = 18 * (gw1 / 49) + 2 * ((gw1 % 49) / 7) + 6;
     TORCH_CHECK(r1 - r0 <= C2F_MAXR, "f32_conv2_fwd: row span exceeds the LDS image");
   }
+  const int nt_tail = tail_blocks > 0 ? (int)tail_blocks : device_cu_count();
+  const F32Adam ad =
+      f32_adam_args(p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule, nt_tail, "f32_conv2_fwd");
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  auto launch = [&](auto kern) {
+  auto launch = [&](auto kern, int extra) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C2F_LDS);
-    kern<<<nblk, 256, C2F_LDS, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
-                                         a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B);
+    kern<<<nblk + extra, 256, C2F_LDS, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+                                                 a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, ad);
   };
+#define C2F_CASE(T)                                                                  \
+  case T:                                                                            \
+    if (ad.nblk > 0) launch(f32_conv2_fwd_kernel<T, true>, ad.nblk);                 \
+    else launch(f32_conv2_fwd_kernel<T, false>, 0);                                  \
+    break;
   switch (tpb) {
-    case 1: launch(f32_conv2_fwd_kernel<1>); break;
-    case 2: launch(f32_conv2_fwd_kernel<2>); break;
-    case 3: launch(f32_conv2_fwd_kernel<3>); break;
-    case 4: launch(f32_conv2_fwd_kernel<4>); break;
-    case 5: launch(f32_conv2_fwd_kernel<5>); break;
-    case 6: launch(f32_conv2_fwd_kernel<6>); break;
-    default: launch(f32_conv2_fwd_kernel<7>); break;
+    C2F_CASE(1)
+    C2F_CASE(2)
+    C2F_CASE(3)
+    C2F_CASE(4)
+    C2F_CASE(5)
+    C2F_CASE(6)
+    default:
+      if (ad.nblk > 0) launch(f32_conv2_fwd_kernel<7, true>, ad.nblk);
+      else launch(f32_conv2_fwd_kernel<7, false>, 0);
   }
+#undef C2F_CASE
 }
 
 void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) {

@@ -26,9 +26,10 @@ namespace mihvd {
 constexpr int FC1_K = 3136, FC1_N = 1024, FC1_KS = 7, FC1_KSL = FC1_K / FC1_KS;   // 448 = 14 K steps
 constexpr int FC1_NT = 32;                                                          // columns per block
 constexpr int MAXB = 128;                                                           // batch limit (8 tiles)
-constexpr int F1_ASTR = FC1_KSL + 8;   // a2 image rows: 232 elements (464 B)
-constexpr int F1_WSTR = FC1_NT + 8;    // W3 image rows: 72 elements (144 B)
-constexpr int F1_LDS = (MAXB * F1_ASTR + FC1_KSL * F1_WSTR) * 2;
+constexpr int F1_ASTR = FC1_KSL + 8;   // a2 image rows: 456 elements (912 B)
+constexpr int F1_WSTR = FC1_NT + 8;    // W3 image rows: 40 elements (80 B)
+constexpr int F1_LDS = (MAXB * F1_ASTR + FC1_KSL * F1_WSTR) * 2;   // 152,576 B
+static_assert(F1_LDS <= 163840, "fc1_fwd LDS image exceeds the CU's 160 KiB");
 
 // grid (32, 7): blockIdx.x = 32-column tile, blockIdx.y = K slice (448 = 14 K steps). NW = 4 or 8
 // waves: wave w owns the 16 features w % 2 and the sample-tile group w / 2.
@@ -41,7 +42,7 @@ __global__ void __launch_bounds__(NW * 64) fc1_fwd_kernel(const u16* __restrict_
   constexpr int Mpad = MT * 16, T = NW * 64;
   constexpr int WN = FC1_NT / 16, MG = NW / WN;     // 16-feature groups, sample-tile groups
   constexpr int MTW = (MT + MG - 1) / MG;           // sample tiles per wave
-  u16* Ws = smem;                     // [224][F1_WSTR]    rows = k, n contiguous
+  u16* Ws = smem;                     // [448][F1_WSTR]    rows = k, n contiguous
   u16* As = smem + FC1_KSL * F1_WSTR; // [Mpad][F1_ASTR]   rows = samples, k contiguous
   const int nt = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
   const int k0 = ks * FC1_KSL;
@@ -818,9 +819,7 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
     // 29.9 us at the 8-rank K), over the 8-rank slice they win (7.7 -> 7.2 us, with Adam 12.8 ->
     // 11.4), over the 4-rank slice (13 row tiles, K = 400) dW3 + Adam 11.2 -> 9.6 us
     const int tiles = (int)(jt_hi - jt_lo) * (FC1_N / 64);
-    int ncu = 256, dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int ncu = device_cu_count();
     // 32-feature tiles (twice the blocks, each with half the MFMA work and half the Adam epilogue)
     // when they still fit the CUs one block each: the 8-rank slice dW3 7.2 -> 6.3 us, dW3 + Adam
     // 11.4 -> 9.0 us (MIHVD_WGRAD_NARROW=0 keeps the 64-feature tiles)

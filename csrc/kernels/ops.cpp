@@ -85,7 +85,11 @@ void multi_tensor_sgd(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std:
 void bump_step_(at::Tensor& step);
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1);
-void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
+void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
+                   const c10::optional<at::Tensor>& p3, const c10::optional<at::Tensor>& g3,
+                   const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
+                   const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
+                   double grad_scale, int64_t rule, int64_t tail_blocks);
 void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
@@ -98,10 +102,15 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    at::Tensor& cpart, at::Tensor& slab);
 void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,
-                     at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2);
+                     at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const c10::optional<at::Tensor>& params,
+                     const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
+                     const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, int64_t o_w1,
+                     int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo, int64_t fc_hi, double lr, double b1,
+                     double b2, double eps, double grad_scale, int64_t rule);
 int64_t f32_db2_rows(int64_t B);
 int64_t f32_wgrad_groups(int64_t B);
 int64_t f32_dgrad_blocks(int64_t B);
+int64_t conv_barrier_error(bool reset);
 }  // namespace mihvd
 
 namespace {
@@ -219,8 +228,11 @@ void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Te
                   Tensor idx1) {
   mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1);
 }
-void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2) {
-  mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2);
+void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& p3,
+                  const OptT& g3, const OptT& m3, const OptT& v3, const OptT& state, double lr, double beta1,
+                  double beta2, double eps, double grad_scale, int64_t rule, int64_t tail_blocks) {
+  mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule,
+                       tail_blocks);
 }
 void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
@@ -237,8 +249,11 @@ void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, con
   mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab);
 }
 void f32_conv_reduce_op(const Tensor& slab, const Tensor& cpart, const Tensor& db2p, Tensor gW2, Tensor gW1, Tensor gb1,
-                        Tensor gb2) {
-  mihvd::f32_conv_reduce(slab, cpart, db2p, gW2, gW1, gb1, gb2);
+                        Tensor gb2, const OptT& params, const OptT& grads, const OptT& m, const OptT& v,
+                        const OptT& state, int64_t o_w1, int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo,
+                        int64_t fc_hi, double lr, double b1, double b2, double eps, double grad_scale, int64_t rule) {
+  mihvd::f32_conv_reduce(slab, cpart, db2p, gW2, gW1, gb1, gb2, params, grads, m, v, state, o_w1, o_b1, o_w2, o_b2,
+                         fc_lo, fc_hi, lr, b1, b2, eps, grad_scale, rule);
 }
 }  // namespace
 
@@ -290,7 +305,9 @@ TORCH_LIBRARY(mihvd, m) {
         "float weight_decay, bool nesterov, bool first, float grad_scale) -> ()");
   m.def("bump_step_(Tensor(a!) step) -> ()");
   m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
-  m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
+  m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor(c!)? p3=None, "
+        "Tensor? g3=None, Tensor(d!)? m3=None, Tensor(e!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., "
+        "float beta2=0., float eps=0., float grad_scale=1., int rule=0, int tail_blocks=0) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
@@ -299,10 +316,13 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_conv2_bwd(Tensor dY2, Tensor w2, Tensor a1, Tensor idx1, Tensor x, Tensor? rows, Tensor? state, "
         "Tensor(a!) cpart, Tensor(b!) slab) -> ()");
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
-        "Tensor(d!) gb2) -> ()");
+        "Tensor(d!) gb2, Tensor(e!)? params=None, Tensor? grads=None, Tensor(f!)? m=None, Tensor(g!)? v=None, "
+        "Tensor(s!)? state=None, int o_w1=0, int o_b1=0, int o_w2=0, int o_b2=0, int fc_lo=0, int fc_hi=0, "
+        "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0) -> ()");
   m.def("f32_db2_rows(int B) -> int", &mihvd::f32_db2_rows);
   m.def("f32_wgrad_groups(int B) -> int", &mihvd::f32_wgrad_groups);
   m.def("f32_dgrad_blocks(int B) -> int", &mihvd::f32_dgrad_blocks);
+  m.def("conv_barrier_error(bool reset=True) -> int", &mihvd::conv_barrier_error);
   m.def("gather_cols_bf16(Tensor src, int col0, Tensor(a!) dst) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bf16_to_f32(Tensor src, Tensor(a!) dst, float scale) -> ()");

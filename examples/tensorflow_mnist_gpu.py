@@ -9,6 +9,12 @@ fp16 with dynamic loss scaling); LR scaling as the reference; callbacks
 ``steps_per_epoch = max(1, 60000 // (batch*size))``, ``validation_steps = max(1, 10000 // batch)``,
 ``epochs = max(1, num_steps // steps_per_epoch)``; rank 0 evaluates, prints Test loss/accuracy and
 saves ``./final_model``.
+
+On an MI355X the model trains through the hand-written CDNA4 kernels (``--impl hip``, the default
+with a GPU): every ``fit`` batch is one fused forward+backward of ``csrc/kernels`` (bf16 MFMA
+operands under ``mixed_bfloat16``, the exact-fp32 kernels under ``--policy float32``), the gradients
+go through ``hvd.DistributedOptimizer``'s RCCL buckets and TF1/Keras Adam runs as the multi-tensor
+HIP kernel. ``--impl torch`` runs stock PyTorch-ROCm layers instead.
 """
 import argparse
 import os
@@ -30,6 +36,7 @@ parser.add_argument("--lr", default=0.001, type=float, help="Adam learning rate"
 parser.add_argument("--num-steps", default=20000, type=int, help="Number of training steps")
 parser.add_argument("--batch-size", default=100, type=int, help="Batch size")
 parser.add_argument("--policy", default="mixed_bfloat16", choices=["float32", "mixed_bfloat16", "mixed_float16"])
+parser.add_argument("--impl", default="auto", choices=["auto", "hip", "torch"], help="compute path")
 args = parser.parse_args()
 
 
@@ -42,7 +49,8 @@ def main():
     x_test = np.reshape(x_test.astype(np.float32) / 255.0, (-1, 784))
 
     policy = args.policy if device.type == "cuda" else "float32"
-    model = hvd.Model(MNISTConvNet(impl="torch", seed=hvd.rank()).to(device), policy=policy)
+    impl = args.impl if args.impl != "auto" else ("hip" if device.type == "cuda" else "torch")
+    model = hvd.Model(MNISTConvNet(impl=impl, seed=hvd.rank()).to(device), policy=policy)
     lr_scaler = hvd.size()
     if args.use_adasum:
         lr_scaler = hvd.local_size() if hvd.nccl_built() else 1

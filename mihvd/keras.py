@@ -270,9 +270,20 @@ class _LossScaler:
 
 
 class Model:
+    """``policy`` is the Keras mixed-precision policy (tensorflow_mnist_gpu.py:26-28). A module with
+    ``impl == "hip"`` (``MNISTConvNet(impl="hip")``) trains through the hand-written CDNA4 kernels
+    (one fused forward+backward autograd node per batch): ``float32`` runs the exact-fp32 kernels,
+    ``mixed_bfloat16`` the bf16-operand kernels (fp32 accumulation and master weights);
+    ``mixed_float16`` has no fp16-operand kernel set and runs stock fp16 autocast ops with the HIP
+    dynamic loss scaler."""
+
     def __init__(self, module: torch.nn.Module, policy: str = "float32"):
         self.module = module
         self.policy = policy
+        if getattr(module, "impl", None) == "hip":
+            if policy == "mixed_float16":
+                module.impl = "torch"  # no fp16-operand kernel set: stock fp16 autocast + HIP loss scaler
+            module.hip_precision = "fp32" if policy == "float32" else "bf16"
         self.optimizer = None
         self.loss_fn = None
         self.metrics = []
@@ -305,7 +316,7 @@ class Model:
     def train_on_batch(self, xb, yb):
         self.module.train()
         self.optimizer.zero_grad()
-        if getattr(self.module, "impl", None) == "hip":
+        if getattr(self.module, "impl", None) == "hip" and self.policy != "mixed_float16":
             # whole forward+backward in the CDNA4 kernels, one autograd node (bf16 MFMA inside)
             from .ops.functional import fused_mnist_loss
 

@@ -236,6 +236,13 @@ class FusedMNISTTrainer:
         self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
         self.cpart = torch.empty(B, 896, **f32)     # per-image dW1 | db1 | db2 partial rows
+        # fp32 step: MIHVD_FUSED_OPT=1 (default) folds the optimizer into the step's kernels — the
+        # small parameters' Adam into the gradient-reduction launch (world size 1) and dense/kernel's
+        # into tail blocks of the next step's conv2_fwd launch; MIHVD_F32_TAIL_BLOCKS sets their count
+        # (default: one per CU)
+        self.f32_fused_opt = self.f32 and os.environ.get("MIHVD_FUSED_OPT", "1") != "0"
+        self.f32_tail_blocks = int(os.environ.get("MIHVD_F32_TAIL_BLOCKS", "0"))
+        self._w3_pending = False
         if self.f32:
             ops = self.ops
             self.a1 = torch.empty(B, 14, 14, 32, **f32)
@@ -372,6 +379,7 @@ class FusedMNISTTrainer:
 
     def to_model(self, model: MNISTConvNet | None = None) -> MNISTConvNet:
         self._require_full_state()
+        self._join()
         model = model or MNISTConvNet(impl="torch").to(self.device)
         with torch.no_grad():
             for name, p in model.ordered_parameters():
@@ -537,10 +545,20 @@ class FusedMNISTTrainer:
         st = self.state
         P, G = self.pview, self.gview
         main = torch.cuda.current_stream(self.device)
+        b1, b2 = self.betas
         w2 = P("conv_layer2/conv2d/kernel")
         w3 = P("dense/kernel")
+        s3 = slice(W3_START, FLAT_NUMEL)
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1, self.idx1)
-        o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
+        if self._w3_pending:
+            # the previous step's dense/kernel Adam update (98 % of the optimizer's bytes) streams in
+            # tail blocks of this MFMA-bound launch; fc1_fwd below is its first reader
+            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, self.params[s3],
+                            self.grads[s3], self.m[s3], self.v[s3], st, self.lr, b1, b2, self.eps, 1.0 / self.world,
+                            self.rule, self.f32_tail_blocks)
+            self._w3_pending = False
+        else:
+            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
         o.f32_fc1_fwd(self.a2, w3, self.zpart)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
@@ -552,16 +570,38 @@ class FusedMNISTTrainer:
             with torch.cuda.stream(self._side):
                 self._allreduce(self.grads[FC_START:], FC_START, FLAT_NUMEL)
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab)
-        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
-                          G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
-        if overlap:
-            self._allreduce(self.grads[:FC_START], 0, FC_START)
-            main.wait_stream(self._side)
-        elif self.collectives:
-            self._allreduce(self.grads, 0, FLAT_NUMEL)
+        gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
+                 G("conv_layer2/conv2d/bias"))
+        if self.f32_fused_opt and not self.collectives:
+            # gradient reduction + Adam of every parameter but dense/kernel + the step bump, one launch
+            o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv, self.params, self.grads, self.m, self.v, st,
+                              SEGMENTS["conv_layer1/conv2d/kernel"][0], SEGMENTS["conv_layer1/conv2d/bias"][0],
+                              SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0],
+                              FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
+        else:
+            o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
+            if overlap:
+                self._allreduce(self.grads[:FC_START], 0, FC_START)
+                main.wait_stream(self._side)
+            elif self.collectives:
+                self._allreduce(self.grads, 0, FLAT_NUMEL)
+            hi = W3_START if self.f32_fused_opt else FLAT_NUMEL
+            o.adam_step(self.params[:hi], self.grads[:hi], self.m[:hi], self.v[:hi], None, st, 0, self.lr, b1, b2,
+                        self.eps, 1.0 / self.world, self.rule, 1)
+        if self.f32_fused_opt:
+            # dense/kernel's update is deferred into the next step's conv2_fwd launch (or applied by
+            # _flush_w3 when no step follows: end of an eager step or of a captured graph)
+            self._w3_pending = True
+
+    def _flush_w3(self):
+        """Apply a deferred dense/kernel Adam update now (fp32 step; see _launch_step_f32)."""
+        if not getattr(self, "_w3_pending", False):
+            return
         b1, b2 = self.betas
-        o.adam_step(self.params, self.grads, self.m, self.v, None, st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world,
-                    self.rule, 1)
+        s3 = slice(W3_START, FLAT_NUMEL)
+        self.ops.adam_step(self.params[s3], self.grads[s3], self.m[s3], self.v[s3], None, self.state, 0, self.lr, b1,
+                           b2, self.eps, 1.0 / self.world, self.rule, 0)
+        self._w3_pending = False
 
     def _launch_step_gather(self, x, rows, labels):
         """Step with the factor-gather data plane over the process group (RCCL; see ``__init__``).
@@ -745,7 +785,9 @@ class FusedMNISTTrainer:
             dist.all_gather(list(full.chunk(self.world)), mine.clone())
 
     def _join(self):
-        """Make the current stream wait for any side-stream work of the last step."""
+        """Make the current stream wait for any side-stream work of the last step, and apply a
+        deferred optimizer update (the step's results are then complete)."""
+        self._flush_w3()
         if self._fc_update_pending:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             self._fc_update_pending = False
@@ -951,6 +993,9 @@ class FusedMNISTTrainer:
         """Raise if a direct-xGMI collective of this trainer timed out waiting for a peer (its
         outputs, and those of every later xGMI collective, are NaN). Waits for the current stream.
         A plane that select_data_plane() dropped after such a timeout is not checked again."""
+        if not self.f32 and self.fused_opt and int(self.ops.conv_barrier_error(True)) != 0:
+            raise RuntimeError("fused step: a conv2_bwd LDS barrier timed out (a broken wave count); the conv "
+                               "gradients and optimizer state of that step are invalid")
         if getattr(self, "fold_reduce", False) and int(self.fold_sync[2]) != 0:
             raise RuntimeError("fused step: the folded gradient reduction timed out waiting for the conv blocks "
                                "(a conv block was not resident); parameters of that step are invalid")
@@ -1190,8 +1235,11 @@ class FusedMNISTTrainer:
 
     def reduced_grads(self) -> torch.Tensor:
         """The flat gradient buffer after the step's reduction (sums over ranks; the xGMI plane
-        reduces the small gradients into a separate buffer instead of in place, and dW3 reaches
-        the gradient buffer only with keep_w3_grad)."""
+        reduces the small gradients into a separate buffer instead of in place). On the
+        factor-gather plane (both the xGMI and the RCCL form: MIHVD_FUSE_W3_SLICE=1, the default,
+        computes dW3 + Adam in one tile epilogue) the dense/kernel segment is written only with
+        keep_w3_grad=True, and then only for the rows whose optimizer this rank owns; otherwise it
+        holds stale values."""
         if self.use_xgmi and self.gather:
             return torch.cat([self.gred, self.grads[W3_START:]])
         return self.grads
@@ -1239,6 +1287,7 @@ class FusedMNISTTrainer:
 
     # ----------------------------------------------------------------------------- state
     def sync(self):
+        self._join()
         torch.cuda.synchronize(self.device)
         self.check_xgmi()
 
@@ -1283,6 +1332,7 @@ class FusedMNISTTrainer:
             return
         import torch.distributed as dist
 
+        self._join()
         self.gather_full_state()  # collective; no-op unless the dense/kernel optimizer is sharded
         for buf in (self.params, self.m, self.v, self.state):
             dist.broadcast(buf, src=root_rank)

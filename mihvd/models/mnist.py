@@ -76,6 +76,8 @@ class MNISTConvNet(nn.Module):
         self.impl = impl
         self.dropout_rate = dropout_rate
         self.compute_dtype = compute_dtype
+        # impl="hip": operand precision of the HIP kernels ("bf16" MFMA operands or exact "fp32")
+        self.hip_precision = "bf16"
         self.conv_layer1 = _Scope(_Layer((5, 5, 1, 32), (32,)))
         self.conv_layer2 = _Scope(_Layer((5, 5, 32, 64), (64,)))
         self.dense = _Layer((3136, 1024), (1024,))

@@ -7,6 +7,10 @@
   hands the kernel-computed parameter gradients to autograd. This is how a stock optimizer loop
   (e.g. ``hvd.DistributedOptimizer`` with its per-parameter hooks) drives the HIP path; the fully
   fused graph-replayed loop lives in ``mihvd.models.fused_mnist``.
+
+Both take ``precision``: ``"bf16"`` (bf16 MFMA operands, fp32 accumulation; the default) or
+``"fp32"`` (the exact-fp32 kernels of csrc/kernels/f32_*.hip); ``MNISTConvNet.hip_precision``
+sets it for the model's own forward.
 """
 from __future__ import annotations
 
@@ -45,6 +49,33 @@ class _Workspace:
         return ws
 
 
+class _WorkspaceF32:
+    """Per-(device, batch) buffers of the exact-fp32 kernels."""
+
+    _cache: dict = {}
+
+    @classmethod
+    def get(cls, device, B):
+        key = (str(device), B)
+        ws = cls._cache.get(key)
+        if ws is None:
+            ops = torch.ops.mihvd
+            f32 = dict(device=device, dtype=torch.float32)
+            u8 = dict(device=device, dtype=torch.uint8)
+            ws = dict(
+                a1=torch.empty(B, 14, 14, 32, **f32), idx1=torch.empty(B, 14, 14, 32, **u8),
+                a2=torch.empty(B, 3136, **f32), idx2=torch.empty(B, 3136, **u8), zpart=torch.empty(14, B, 1024, **f32),
+                h=torch.empty(B, 1024, **f32), dz=torch.empty(B, 1024, **f32), dlog=torch.empty(B, 10, **f32),
+                stats=torch.empty(B, 2, **f32), dY2=torch.empty(B, 14, 14, 64, **f32),
+                db2p=torch.empty(int(ops.f32_db2_rows(B)), 64, **f32),
+                slab=torch.empty(int(ops.f32_wgrad_groups(B)), 51200, **f32),
+                cpart=torch.empty(int(ops.f32_dgrad_blocks(B)), 832, **f32),
+                state=torch.zeros(4, device=device, dtype=torch.int64),
+            )
+            cls._cache[key] = ws
+        return ws
+
+
 def _conv_forward(ops, ws, x, st, w1, b1, b2):
     """conv1 + conv2 forward: one conv12 launch (conv1 on MFMA, bf16 operands, like the fused
     trainer) unless MIHVD_CONV12=0 (conv1 as an fp32 VALU convolution, then conv2)."""
@@ -62,14 +93,22 @@ def _params(model):
 
 
 @torch.no_grad()
-def mnist_logits(model, images: torch.Tensor) -> torch.Tensor:
+def mnist_logits(model, images: torch.Tensor, precision: str | None = None) -> torch.Tensor:
     _native.require_kernels()
     ops = torch.ops.mihvd
     x = images.reshape(-1, 784).float().contiguous()
     B = x.shape[0]
+    precision = precision or getattr(model, "hip_precision", "bf16")
     if B > 128:
-        return torch.cat([mnist_logits(model, x[i:i + 128]) for i in range(0, B, 128)])
+        return torch.cat([mnist_logits(model, x[i:i + 128], precision) for i in range(0, B, 128)])
     w1, b1, w2, b2, w3, b3, w4, b4 = _params(model)
+    if precision == "fp32":
+        ws = _WorkspaceF32.get(x.device, B)
+        ops.f32_conv1_fwd(x, None, None, w1.detach().reshape(-1), b1.detach(), ws["a1"], ws["idx1"])
+        ops.f32_conv2_fwd(ws["a1"], w2.detach(), b2.detach(), ws["a2"], ws["idx2"])
+        ops.f32_fc1_fwd(ws["a2"], w3.detach(), ws["zpart"])
+        h = torch.relu(ws["zpart"].sum(0) + b3)
+        return h @ w4 + b4
     ws = _Workspace.get(x.device, B)
     ops.scale_cast_bf16(w2.detach().reshape(-1), ws["w2bf"], 1.0)
     ops.scale_cast_bf16(w3.detach().reshape(-1), ws["w3bf"], 1.0)
@@ -77,6 +116,39 @@ def mnist_logits(model, images: torch.Tensor) -> torch.Tensor:
     ops.fc1_fwd(ws["a2"], ws["w3bf"], ws["zpart"])
     h = torch.relu(ws["zpart"].sum(0) + b3)
     return (h.to(torch.bfloat16).float() @ w4 + b4).float()
+
+
+class _FusedMNISTLossF32(torch.autograd.Function):
+    """The exact-fp32 step's kernels (csrc/kernels/f32_fwd.hip, f32_bwd.hip) as one autograd node."""
+
+    @staticmethod
+    def forward(ctx, x, labels, dropout, seed, w1, b1, w2, b2, w3, b3, w4, b4):
+        ops = torch.ops.mihvd
+        B = x.shape[0]
+        ws = _WorkspaceF32.get(x.device, B)
+        grads = [torch.empty_like(p, dtype=torch.float32) for p in (w1, b1, w2, b2, w3, b3, w4, b4)]
+        gW1, gb1, gW2, gb2, gW3, gb3, gW4, gb4 = grads
+        st = ws["state"]
+        w2c, w3c = w2.contiguous(), w3.contiguous()
+        ops.f32_conv1_fwd(x, None, st, w1.reshape(-1), b1, ws["a1"], ws["idx1"])
+        ops.f32_conv2_fwd(ws["a1"], w2c, b2, ws["a2"], ws["idx2"])
+        ops.f32_fc1_fwd(ws["a2"], w3c, ws["zpart"])
+        ops.f32_head_fwd_bwd(ws["zpart"], b3, w4.contiguous(), b4, labels, None, st, int(seed), float(dropout), ws["h"],
+                             ws["dz"], ws["dlog"], ws["stats"])
+        ops.f32_fc1_bwd(ws["dz"], ws["a2"], ws["idx2"], ws["h"], ws["dlog"], w3c, ws["dY2"], ws["db2p"], gW3, gb3, gW4,
+                        gb4)
+        ops.f32_conv2_bwd(ws["dY2"], w2c, ws["a1"], ws["idx1"], x, None, st, ws["cpart"], ws["slab"])
+        ops.f32_conv_reduce(ws["slab"], ws["cpart"], ws["db2p"], gW2.reshape(-1), gW1.reshape(-1), gb1, gb2)
+        st[0] += 1  # next call draws a fresh dropout mask
+        ctx.save_for_backward(*grads)
+        acc = ws["stats"][:, 1].mean()
+        ctx.mark_non_differentiable(acc)
+        return ws["stats"][:, 0].mean(), acc
+
+    @staticmethod
+    def backward(ctx, gout, _gacc):
+        grads = [g * gout for g in ctx.saved_tensors]
+        return (None, None, None, None, *grads)
 
 
 class _FusedMNISTLoss(torch.autograd.Function):
@@ -110,12 +182,14 @@ class _FusedMNISTLoss(torch.autograd.Function):
 
 
 def fused_mnist_loss(model, images: torch.Tensor, labels: torch.Tensor, training: bool = True, seed: int = 17,
-                     return_accuracy: bool = False):
+                     return_accuracy: bool = False, precision: str | None = None):
     """Mean softmax cross-entropy of the reference CNN, forward and backward in HIP kernels."""
     _native.require_kernels()
     x = images.reshape(-1, 784).float().contiguous()
     if x.shape[0] > 128:
         raise ValueError("fused_mnist_loss: per-call batch must be <= 128")
     rate = model.dropout_rate if training else 0.0
-    loss, acc = _FusedMNISTLoss.apply(x, labels.long().contiguous(), rate, seed, *_params(model))
+    precision = precision or getattr(model, "hip_precision", "bf16")
+    fn = _FusedMNISTLossF32 if precision == "fp32" else _FusedMNISTLoss
+    loss, acc = fn.apply(x, labels.long().contiguous(), rate, seed, *_params(model))
     return (loss, acc) if return_accuracy else loss
