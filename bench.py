@@ -218,6 +218,14 @@ def main():
         comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
     elif n == 1 and not tr.collectives:
         comm_desc = "none (1 GPU)"
+    elif tr.f32 and tr.shard_w3:
+        comm_desc = ("RCCL reduce-scatter of dense/kernel's fp32 gradient by rows (overlapping the conv backward) -> "
+                     "each rank's Adam on its 1/N of the rows -> RCCL all-gather of the updated fp32 rows "
+                     "(overlapping the next step's convolutions); RCCL allreduce of the other fp32 gradients; every "
+                     "step, in the HIP graph")
+    elif tr.f32:
+        comm_desc = ("RCCL allreduce of the fp32 gradient fusion buffer every step: the fc bucket (98.4 % of the "
+                     "bytes) on a side stream overlapping the conv backward, then the conv bucket; in the HIP graph")
     elif getattr(tr, "shard_w3", False) and tr.data_plane() == "xgmi":
         comm_desc = ("direct xGMI one-shot collectives (hipIpc peer memory, device-side phase barriers): each rank "
                      "reads the peers' bf16 fc1 factors (dz, and the a2 columns of its own dense/kernel rows), "

@@ -178,6 +178,14 @@ class FusedMNISTTrainer:
         if shard_optimizer is None:
             shard_optimizer = os.environ.get("MIHVD_SHARD_W3", "0") == "1"
         self.shard_w3 = bool(shard_optimizer) and self.gather and not self.fuse_w3_requested()
+        # fp32 step over RCCL: the same option as a reduce-scatter of dW3 by rows, Adam on this rank's
+        # 3136/size rows, and an all-gather of the updated fp32 rows overlapping the next step's
+        # convolutions (instead of allreducing dW3 and every rank updating all of W3)
+        self._f32_can_shard = (self.f32 and self.collectives and self.world > 1 and 3136 % self.world == 0
+                               and compression == "none" and (op is None or ReduceOp(op) in (ReduceOp.Average,
+                                                                                              ReduceOp.Sum)))
+        if self.f32:
+            self.shard_w3 = bool(shard_optimizer) and self._f32_can_shard
         self._shadow_ev = None
         self._full_state_valid = True
         self._T = -(-49 // self.world)
@@ -255,6 +263,9 @@ class FusedMNISTTrainer:
             self.slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, **f32)
             self.cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, **f32)
             self.g2 = None
+            # sharded dense/kernel optimizer: this rank's rows of the reduce-scattered dW3
+            self._f32_R = 3136 // self.world if self.world > 0 and 3136 % self.world == 0 else 0
+            self.gshard = torch.empty(max(self._f32_R, 1), 1024, **f32) if self._f32_can_shard else None
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
@@ -549,6 +560,8 @@ class FusedMNISTTrainer:
         w2 = P("conv_layer2/conv2d/kernel")
         w3 = P("dense/kernel")
         s3 = slice(W3_START, FLAT_NUMEL)
+        if self.shard_w3:
+            return self._launch_step_f32_shard(x, rows, labels)
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1, self.idx1)
         if self._w3_pending:
             # the previous step's dense/kernel Adam update (98 % of the optimizer's bytes) streams in
@@ -592,6 +605,68 @@ class FusedMNISTTrainer:
             # dense/kernel's update is deferred into the next step's conv2_fwd launch (or applied by
             # _flush_w3 when no step follows: end of an eager step or of a captured graph)
             self._w3_pending = True
+
+    def _launch_step_f32_shard(self, x, rows, labels):
+        """fp32 step with the dense/kernel optimizer sharded over RCCL (size > 1):
+
+            main: conv1 conv2 | fc1_fwd head fc1_bwd | conv2_bwd reduce | Adam (small + my rows) |
+            side:  AG(W3 rows) ->|   (prev. step)      RS(dW3 rows)      AR(small)              AG(W3 rows) -> next
+
+        The row all-gather of the updated fp32 W3 overlaps the next step's convolutions (an event
+        joins it before fc1_fwd, W3's first reader); the reduce-scatter overlaps the conv backward.
+        Adam slots of other ranks' rows are not maintained (gather_full_state() collects them)."""
+        o = self.ops
+        st = self.state
+        P, G = self.pview, self.gview
+        main = torch.cuda.current_stream(self.device)
+        side = self._side
+        b1, b2 = self.betas
+        w2 = P("conv_layer2/conv2d/kernel")
+        w3 = P("dense/kernel")
+        R, r = self._f32_R, self.rank
+        o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1, self.idx1)
+        o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
+        if self._shadow_ev is not None:  # the previous step's W3 row gather
+            main.wait_event(self._shadow_ev)
+            self._shadow_ev = None
+        o.f32_fc1_fwd(self.a2, w3, self.zpart)
+        o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
+                           self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        gW3 = G("dense/kernel")
+        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3, G("dense/bias"),
+                      G("dense_1/kernel"), G("dense_1/bias"))
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._reduce_scatter_rows(gW3, self.gshard, R)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab)
+        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
+                          G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._allreduce(self.grads[:W3_START], 0, W3_START)
+        main.wait_stream(side)
+        o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START], None, st, 0,
+                    self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+        mine = slice(W3_START + r * R * 1024, W3_START + (r + 1) * R * 1024)
+        o.adam_step(self.params[mine], self.gshard.view(-1), self.m[mine], self.v[mine], None, st, 0, self.lr, b1, b2,
+                    self.eps, 1.0 / self.world, self.rule, 0)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            p3 = self.params[W3_START:].view(3136, 1024)
+            self._all_gather_rows(p3, p3[r * R:(r + 1) * R])
+            self._shadow_ev = torch.cuda.Event()
+            self._shadow_ev.record(side)
+        self._full_state_valid = False
+
+    def _reduce_scatter_rows(self, full, out, R):
+        """out = this rank's R rows of the sum over ranks of ``full`` (rows x 1024)."""
+        import torch.distributed as dist
+
+        if dist.get_backend() == "nccl":
+            dist.reduce_scatter_tensor(out, full.view(self.world * R, -1))
+        else:  # gloo has no reduce-scatter: allreduce in place, keep this rank's rows
+            dist.all_reduce(full)
+            out.copy_(full.view(self.world * R, -1)[self.rank * R:(self.rank + 1) * R])
 
     def _flush_w3(self):
         """Apply a deferred dense/kernel Adam update now (fp32 step; see _launch_step_f32)."""
@@ -801,6 +876,13 @@ class FusedMNISTTrainer:
         if not self.shard_w3 or self._full_state_valid:
             return
         self._join()
+        if self.f32:  # the fp32 rows are gathered every step; the Adam slots here
+            R = self._f32_R
+            for buf in (self.m, self.v):
+                w3 = buf[W3_START:].view(3136, 1024)
+                self._all_gather_rows(w3, w3[self.rank * R:(self.rank + 1) * R])
+            self._full_state_valid = True
+            return
         T64 = self._T * 64
         lo, hi = self._w3_tiles
         for buf in (self.params, self.m, self.v):
@@ -1084,7 +1166,10 @@ class FusedMNISTTrainer:
     def set_sharding(self, shard: bool):
         """Switch the dense/kernel optimizer between sharded and replicated (factor-gather plane;
         collective). Sharded -> replicated first collects every rank's fp32 rows and Adam slots."""
-        shard = bool(shard) and self.gather and not self.fuse_w3_requested()
+        if self.f32:
+            shard = bool(shard) and self._f32_can_shard
+        else:
+            shard = bool(shard) and self.gather and not self.fuse_w3_requested()
         if shard == self.shard_w3:
             return
         self._join()
@@ -1107,7 +1192,12 @@ class FusedMNISTTrainer:
         import torch.distributed as dist
 
         rep = {"mode": self._xgmi_mode, "available": self.xplane is not None}
-        if not self.gather:
+        if self.f32 and self._f32_can_shard and shard_options is None:
+            # fp32 over RCCL: dW3 bucket allreduce + every rank's full Adam, or reduce-scatter +
+            # sharded Adam + row all-gather; timed like the factor-gather planes below
+            env = os.environ.get("MIHVD_SHARD_W3")
+            shard_options = [env != "0"] if env is not None else [True, False]
+        elif not self.gather:
             rep["plane"] = "rccl" if self.collectives else "none"
             return rep
         if shard_options is None:

@@ -265,3 +265,32 @@ def test_f32_graph_replay_converges(ops):
     assert int(tr.state[0].item()) == tr.global_step and int(tr.state[1].item()) == tr.global_step
     assert tr.last_loss() < first * 0.5, (first, tr.last_loss())
     assert tr.last_accuracy() > 0.8
+
+
+def test_f32_fused_optimizer_matches_separate_adam(ops, monkeypatch):
+    """MIHVD_FUSED_OPT=1 (small-parameter Adam inside the reduction launch, dense/kernel's update
+    deferred into the next step's conv2_fwd tail blocks, flushed at the end of each graph / eager
+    step) is bitwise equal to a separate adam_step after every step, graph-replayed and eager."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    (x, y), _ = synthetic_mnist(n_train=2000, n_test=10, seed=6)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    trs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MIHVD_FUSED_OPT", fused)
+        tr = FusedMNISTTrainer(batch_size=100, lr=2e-3, seed=4, device="cuda", precision="fp32")
+        assert tr.f32_fused_opt == (fused == "1")
+        tr.set_device_dataset(X, Y, seed=2)
+        tr.build_graph(steps_per_replay=5)
+        for _ in range(3):
+            tr.run_graph()
+        tr.device_step()
+        tr.run_graph()
+        trs.append(tr)
+    torch.cuda.synchronize()
+    a, b = trs
+    assert a.global_step == b.global_step == 2 + 21
+    for name in ("params", "m", "v", "state"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name

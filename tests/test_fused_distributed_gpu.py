@@ -114,8 +114,8 @@ def test_plane_and_sharding_switches_two_ranks(tmp_path):
         assert o["loss"] == o["loss_ref"]
 
 
-@pytest.mark.parametrize("n", [2, 4])
-def test_bench_multirank_rehearsal_on_one_gpu(n):
+@pytest.mark.parametrize("n,prec", [(2, "fp32"), (4, "fp32"), (2, "bf16"), (4, "bf16")])
+def test_bench_multirank_rehearsal_on_one_gpu(n, prec):
     """bench.py's N > 1 flow (torch.distributed.run rendezvous on 127.0.0.1, factor gather +
     sharded optimizer with the N-rank row-tile split, data-plane selection, barrier-bracketed
     timing, max over ranks, one JSON line from rank 0) with N ranks sharing this GPU over gloo
@@ -126,19 +126,21 @@ def test_bench_multirank_rehearsal_on_one_gpu(n):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
            "127.0.0.1", "--master-port", str(29531 + n), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps",
-           "7", "--warmup", "2"]
-    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+           "40", "--warmup", "2", "--precision", prec]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150, cwd=ROOT)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     r = lines[0]
-    assert r["n_gpus"] == n and r["steps"] == 7 and r["warmup"] == 2 and r["value"] > 0
+    assert r["n_gpus"] == n and r["steps"] == 40 and r["warmup"] == 2 and r["value"] > 0 and r["dtype"] == prec
     assert r["config"]["global_batch"] == 100 * n and r["config"]["parallelism"] == f"dp{n}"
-    assert r["config"]["final_loss"] == r["config"]["final_loss"]  # finite (NaN != NaN)
+    # trains: well below chance (ln 10 = 2.30) after the selection + warm-up + timed steps at lr 1e-3 x n
+    assert r["config"]["final_loss"] < 2.0, r
 
 
 @pytest.mark.parametrize("n,prec,gather,shard,xgmi", [
-    (4, "fp32", "0", "0", "off"), (8, "fp32", "0", "0", "off"),
+    (4, "fp32", "0", "0", "off"), (8, "fp32", "0", "0", "off"), (4, "fp32", "0", "1", "off"),
+    (8, "fp32", "0", "1", "off"),
     (4, "bf16", "1", "1", "off"), (8, "bf16", "1", "1", "off"), (8, "bf16", "1", "0", "off"),
     (8, "bf16", "0", "0", "off"), (8, "bf16", "1", "1", "on")])
 def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shard, xgmi):
@@ -158,7 +160,7 @@ def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shar
         assert o["grad_rel"] < 1e-4, o
         assert o["upd_rel"] < (1e-3 if prec == "fp32" else 1e-2), o
         assert o["losses"][-1] < o["losses"][0], o
-        assert o["shard"] == (shard == "1" and prec == "bf16"), o
+        assert o["shard"] == (shard == "1"), o
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])
@@ -172,7 +174,7 @@ def test_sharded_state_checkpoint_restore_broadcast_two_ranks(tmp_path, prec):
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(2):
         o = json.loads((tmp_path / f"ckpt_shard.{r}.json").read_text())
-        assert o["sharded"] == (prec == "bf16"), o
+        assert o["sharded"], o
         assert all(o["same"].values()), o
         assert o["step"] == 5, o
         if r == 0:

@@ -192,10 +192,15 @@ def sc_dp_gloo_n(outdir):
     tr.train_step(X[r * B:(r + 1) * B], Y[r * B:(r + 1) * B])
     torch.cuda.synchronize()
     red = tr.reduced_grads()
-    if tr.gather:
-        # the factor-gather plane forms dW3 only for the rows whose optimizer this rank owns
-        lo, hi = tr._w3_tiles
-        rows = slice(FLAT_W3 + lo * 64 * 1024, FLAT_W3 + min(hi * 64, 3136) * 1024)
+    if tr.gather or (tr.f32 and tr.shard_w3):
+        # the factor-gather plane forms dW3 only for the rows whose optimizer this rank owns; the
+        # fp32 sharded optimizer reduce-scatters them
+        if tr.f32:
+            R = tr._f32_R
+            rows = slice(FLAT_W3 + r * R * 1024, FLAT_W3 + (r + 1) * R * 1024)
+        else:
+            lo, hi = tr._w3_tiles
+            rows = slice(FLAT_W3 + lo * 64 * 1024, FLAT_W3 + min(hi * 64, 3136) * 1024)
         red = torch.cat([red[:FLAT_W3], red[rows]])
         gsum_c = torch.cat([gsum[:FLAT_W3], gsum[rows]])
     else:
