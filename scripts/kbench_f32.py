@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Per-kernel times of the exact-fp32 step (csrc/kernels/f32_*.hip) at one batch size.
+
+Each kernel of the step is captured alone N times in a HIP graph and replayed, so the figure is the
+kernel's own time in a back-to-back stream (no host launch gaps); the whole step is timed the same
+way. Prints a table and writes JSON (``--json``).
+
+    python scripts/kbench_f32.py [--batch 100] [--reps 50] [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, reps):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b) * 1000.0 / reps)
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    from mihvd.models.fused_mnist import FC_START, FLAT_NUMEL, SEGMENTS, W3_START, FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    B = args.batch
+    (x, y), _ = synthetic_mnist(n_train=B * 20, n_test=10, seed=1)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, seed=0, device="cuda", precision="fp32")
+    tr.set_device_dataset(X, Y)
+    for _ in range(3):
+        tr.device_step()
+    torch.cuda.synchronize()
+    o, st, P, G = tr.ops, tr.state, tr.pview, tr.gview
+    b1, b2 = tr.betas
+    s3 = slice(W3_START, FLAT_NUMEL)
+    gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
+             G("conv_layer2/conv2d/bias"))
+    w2, w3 = P("conv_layer2/conv2d/kernel"), P("dense/kernel")
+    # lr 0 keeps the weights fixed while the optimizer kernels are timed
+    ks = {
+        "conv1_fwd": lambda: o.f32_conv1_fwd(tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"),
+                                             P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1),
+        "conv2_fwd": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2),
+        "conv2_fwd+W3 adam tail": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
+                                                          tr.params[s3], tr.grads[s3], tr.m[s3], tr.v[s3], st, 0.0,
+                                                          b1, b2, tr.eps, 1.0, tr.rule, tr.f32_tail_blocks),
+        "fc1_fwd": lambda: o.f32_fc1_fwd(tr.a2, w3, tr.zpart),
+        "head": lambda: o.f32_head_fwd_bwd(tr.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), tr.Y,
+                                           tr.rows, st, tr.seed, tr.dropout, tr.h, tr.dz, tr.dlog, tr.stats),
+        "fc1_bwd": lambda: o.f32_fc1_bwd(tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"),
+                                         G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias")),
+        "conv2_bwd": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab),
+        "conv_reduce": lambda: o.f32_conv_reduce(tr.slab, tr.cpart, tr.db2p, *gconv),
+        "conv_reduce+adam": lambda: o.f32_conv_reduce(
+            tr.slab, tr.cpart, tr.db2p, *gconv, tr.params, tr.grads, tr.m, tr.v, st,
+            SEGMENTS["conv_layer1/conv2d/kernel"][0], SEGMENTS["conv_layer1/conv2d/bias"][0],
+            SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0], FC_START, W3_START, 0.0,
+            b1, b2, tr.eps, 1.0, tr.rule),
+        "adam_step (all)": lambda: o.adam_step(tr.params, tr.grads, tr.m, tr.v, None, st, 0, 0.0, b1, b2, tr.eps, 1.0,
+                                               tr.rule, 0),
+        "adam_step (W3)": lambda: o.adam_step(tr.params[s3], tr.grads[s3], tr.m[s3], tr.v[s3], None, st, 0, 0.0, b1,
+                                              b2, tr.eps, 1.0, tr.rule, 0),
+    }
+    res = {}
+    for name, fn in ks.items():
+        res[name] = timed(fn, args.reps)
+    saved = tr.lr
+    tr.lr = 0.0
+    res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
+    tr._join()
+    tr.lr = saved
+    width = max(len(k) for k in res)
+    for k, v in res.items():
+        print(f"{k:<{width}}  {v:8.2f} us")
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump({"batch": B, "us": res, "device": torch.cuda.get_device_name()}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
