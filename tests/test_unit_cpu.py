@@ -296,6 +296,49 @@ def test_monitored_session_single_rank(tmp_path, hvd_single):
     assert torch.equal(state2.model.dense.kernel, model.dense.kernel)
 
 
+def test_session_multi_step_runs_keep_step_cadence(tmp_path, hvd_single):
+    """A run that advances several steps (the fused trainer's graph replay) keeps the hooks'
+    step-based semantics: LoggingTensorHook logs once per 10 steps, StopAtStepHook stops exactly at
+    the last step, step-triggered checkpoints land on the run boundaries that cross them."""
+    import mihvd.tensorflow as htf
+
+    class State:
+        def __init__(self):
+            self.global_step = 0
+            self.w = torch.zeros(3)
+
+        def variables(self):
+            return {"w": self.w.clone(), "global_step": torch.tensor(self.global_step)}
+
+        def load_variables(self, v):
+            self.w.copy_(v["w"])
+            self.global_step = int(v["global_step"])
+
+        def broadcast(self, root):
+            pass
+
+    st = State()
+    last = 47
+    log = htf.LoggingTensorHook({"step": "global_step", "loss": "loss"}, every_n_iter=10)
+
+    def train_op():
+        k = min(10, last - st.global_step)  # graph-replayed run of up to 10 steps
+        st.global_step += k
+        st.w += k
+        return {"loss": torch.tensor(1.0 / st.global_step)}
+
+    hooks = [htf.BroadcastGlobalVariablesHook(0), htf.StopAtStepHook(last_step=last), log]
+    with htf.MonitoredTrainingSession(checkpoint_dir=str(tmp_path), hooks=hooks, state=st,
+                                      save_checkpoint_steps=20) as s:
+        while not s.should_stop():
+            s.run(train_op)
+    assert st.global_step == last
+    steps = [int(line.split("step=")[1].split()[0]) for line in log.lines]
+    assert steps == [10, 20, 30, 40, 47], log.lines  # one line per 10 steps (iterations 0, 10, 20, ...)
+    saved = sorted(f for f in os.listdir(tmp_path) if f.endswith(".pt"))
+    assert saved == ["model.ckpt-20.pt", "model.ckpt-40.pt", "model.ckpt-47.pt"], saved
+
+
 def test_keras_fit_single_rank(tmp_path, hvd_single):
     import mihvd.keras as hk
     from mihvd.models.mnist import MNISTConvNet
