@@ -40,6 +40,8 @@ struct Ctx {
   bool open = false;
   uint64_t timeout_ticks = 0;
   std::vector<void*> opened;
+  unsigned* herr = nullptr;      // host-coherent mirror of the error word (health monitor), or null
+  unsigned* herr_dev = nullptr;  // its device address
 };
 
 std::mutex g_mu;
@@ -92,6 +94,7 @@ CollRole base_role(Ctx* c, int64_t ph) {
   r.rank = c->rank;
   r.world = c->world;
   r.tmo = c->timeout_ticks;
+  r.herr = c->herr_dev;
   return r;
 }
 
@@ -176,6 +179,20 @@ int64_t xgmi_create(int64_t device, int64_t data_bytes, int64_t rank, int64_t wo
   const size_t bytes = kXgCtlBytes + c->data_bytes;
   XGMI_HIP(hipMalloc((void**)&c->base, bytes));
   XGMI_HIP(hipMemset(c->base, 0, bytes));
+  // the timeout mirror lives in fine-grained host memory: a device system-scope store reaches it
+  // while kernels are still running, so the health monitor's thread sees it without a sync
+  void* h = nullptr;
+  if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess && h != nullptr) {
+    std::memset(h, 0, 64);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess && d != nullptr) {
+      c->herr = (unsigned*)h;
+      c->herr_dev = (unsigned*)d;
+    } else {
+      (void)hipHostFree(h);
+    }
+  }
+  (void)hipGetLastError();
   XGMI_HIP(hipDeviceSynchronize());
   c->peers.base[c->rank] = c->base;
   std::lock_guard<std::mutex> lk(g_mu);
@@ -326,6 +343,9 @@ int64_t xgmi_error(int64_t id) {
   return (int64_t)err;
 }
 
+// Host address of the error word's host-coherent mirror (0: none), for HealthMonitor.watch_word.
+int64_t xgmi_error_word(int64_t id) { return (int64_t)(uintptr_t)get(id)->herr; }
+
 void xgmi_destroy(int64_t id) {
   Ctx* c = get(id);
   {
@@ -333,6 +353,7 @@ void xgmi_destroy(int64_t id) {
     XGMI_HIP(hipDeviceSynchronize());
     for (void* p : c->opened) (void)hipIpcCloseMemHandle(p);
     (void)hipFree(c->base);
+    if (c->herr != nullptr) (void)hipHostFree(c->herr);
   }
   std::lock_guard<std::mutex> lk(g_mu);
   for (size_t i = 0; i < g_role_ctx.size(); ++i)
@@ -363,5 +384,6 @@ TORCH_LIBRARY_FRAGMENT(mihvd, m) {
   m.def("xgmi_allreduce_(int ctx, int phase, Tensor(a!) t, int slot_off, int slot_bytes, float scale) -> ()",
         &mihvd::xgmi_allreduce_);
   m.def("xgmi_error(int ctx) -> int", &mihvd::xgmi_error);
+  m.def("xgmi_error_word(int ctx) -> int", &mihvd::xgmi_error_word);
   m.def("xgmi_destroy(int ctx) -> ()", &mihvd::xgmi_destroy);
 }

@@ -13,7 +13,9 @@
 //   enter: the first kSignalBlocks role blocks store e into flags[ph][rank] of every peer
 //          (system-scope stores over xGMI), each after a SYSTEM-scope release fence; every role
 //          block polls its own flags[ph][*] until each peer reached e (relaxed system-scope loads +
-//          s_sleep; bounded by tmo wall-clock ticks: on timeout set err and continue poisoned).
+//          s_sleep; bounded by tmo wall-clock ticks: on timeout set err and its host-coherent mirror,
+//          which the health monitor watches, and continue poisoned: gathers write NaN, a fused
+//          Adam leaves the parameters at their last good values).
 //          Memory-model argument: the published data of ph was written by launches that completed
 //          before this one on the same stream. Each such launch ends with the dispatch packet's
 //          release fence (agent scope in a captured graph), which writes every XCD's L2 back to the
@@ -76,6 +78,7 @@ struct CollRole {
   int adam = 0;
   AdamArgs aa{};
   int dbg_stale = 0;        // debug (MIHVD_XGMI_DEBUG_STALE): gathers skip odd rows -> stale data
+  unsigned* herr = nullptr; // host-coherent mirror of err (the health monitor's watched word)
 };
 
 __device__ __forceinline__ unsigned* xg_u32(char* base, int64_t off) { return (unsigned*)(base + off); }
@@ -115,6 +118,9 @@ __device__ __forceinline__ unsigned xg_enter(const CollRole& c, int bid, bool& o
       if (wall_clock64() - t0 > c.tmo) {
         __hip_atomic_fetch_or(xg_u32(mine, kXgErrOff), (1u << t) | kXgPoison, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_SYSTEM);
+        // the host's health monitor polls this copy (no PCIe atomic: any nonzero value is the signal)
+        if (c.herr != nullptr)
+          __hip_atomic_store(c.herr, (1u << t) | kXgPoison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         good = 0;
         break;
       }
@@ -203,7 +209,7 @@ __device__ __forceinline__ void xg_reduce(const CollRole& c, int bid, bool ok, u
     a.x *= c.scale; a.y *= c.scale; a.z *= c.scale; a.w *= c.scale;
     if (!ok) a = make_float4(nan, nan, nan, nan);
     if (c.out) ((float4*)c.out)[i] = a;
-    if (c.adam) {
+    if (c.adam && ok) {  // poisoned: the parameters keep their last good values (no NaN update)
       float4 pp = ((const float4*)c.aa.p)[i], mm = ((const float4*)c.aa.m)[i], vv = ((const float4*)c.aa.v)[i];
       const uint2 sh = adam4(pp, mm, vv, a, ac);
       ((float4*)c.aa.p)[i] = pp;

@@ -10,6 +10,10 @@
 // (ncclCommAbort: in-flight kernels are cancelled instead of spinning) and terminates the process
 // with a non-zero code, so mihvdrun / mpirun kill the remaining ranks promptly.
 //
+// The direct-xGMI plane has no communicator: its device-side phase barriers mirror a timeout into a
+// host-coherent error word (csrc/kernels/xgmi.hip), which the same thread watches (watch_word), so
+// a peer that never arrives ends the job within one poll interval instead of at the next host sync.
+//
 // inject_error() (driven by MIHVD_FAULT="collerr:...") sets the same error from a test, which is how
 // the path is exercised on CPU-only machines.
 #include <dlfcn.h>
@@ -26,6 +30,7 @@ namespace {
 // ncclResult_t values of rccl.h (RCCL 2.27): 0 success, 7 in progress (non-blocking init)
 constexpr int kNcclSuccess = 0;
 constexpr int kNcclInProgress = 7;
+constexpr int kWordError = 6;  // a watched error word: reported as a remote error (a peer never arrived)
 const char* fallback_name(int code) {
   switch (code) {
     case 1: return "unhandled HIP error";
@@ -75,6 +80,28 @@ void HealthMonitor::inject_error(int code, const std::string& what) {
   cv_.notify_all();
 }
 
+void HealthMonitor::watch_word(uintptr_t addr, const std::string& label) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (addr == 0) return;
+  for (auto& w : words_)
+    if (w.first == reinterpret_cast<const uint32_t*>(addr)) return;
+  words_.emplace_back(reinterpret_cast<const uint32_t*>(addr), label);
+}
+
+void HealthMonitor::unwatch_word(uintptr_t addr) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (size_t i = 0; i < words_.size(); ++i)
+    if (words_[i].first == reinterpret_cast<const uint32_t*>(addr)) {
+      words_.erase(words_.begin() + (ptrdiff_t)i);
+      return;
+    }
+}
+
+int64_t HealthMonitor::num_words() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return (int64_t)words_.size();
+}
+
 int64_t HealthMonitor::num_comms() const {
   std::lock_guard<std::mutex> lk(mu_);
   return (int64_t)comms_.size();
@@ -119,6 +146,18 @@ int HealthMonitor::poll_once(std::string* what) {
       return e;
     }
   }
+  for (const auto& w : words_) {
+    // written by device code with system-scope stores into host-coherent memory
+    const uint32_t v = __atomic_load_n(w.first, __ATOMIC_ACQUIRE);
+    if (v != 0u) {
+      if (what) {
+        char buf[32];
+        std::snprintf(buf, sizeof(buf), " (error word %#x)", v);
+        *what = w.second + buf;
+      }
+      return kWordError;
+    }
+  }
   return kNcclSuccess;
 }
 
@@ -130,7 +169,7 @@ void HealthMonitor::fail(int code, const std::string& what) {
     if (err_str_ != nullptr) name = err_str_(code);
   }
   std::fprintf(stderr,
-               "[rank %d] mihvd health: RCCL async error %d (%s) on %s; aborting the communicator(s) and "
+               "[rank %d] mihvd health: collective error %d (%s) on %s; aborting the communicator(s) and "
                "exiting with %d so the launcher tears the job down\n",
                rank_, code, name ? name : fallback_name(code), what.c_str(), exit_code_);
   std::fflush(stderr);

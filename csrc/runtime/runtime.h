@@ -203,6 +203,12 @@ class HealthMonitor {
   // (already loaded by the process). False if the library or its symbols are unavailable.
   bool attach_rccl(uintptr_t comm, const std::string& lib_path);
   void inject_error(int code, const std::string& what);  // test hook (MIHVD_FAULT collerr)
+  // Watch a 32-bit error word in host-visible memory (e.g. the xGMI plane's host-mapped timeout
+  // mirror, csrc/kernels/xgmi.hip): nonzero is a collective failure like an RCCL async error.
+  // The word must stay valid until unwatch_word().
+  void watch_word(uintptr_t addr, const std::string& label);
+  void unwatch_word(uintptr_t addr);
+  int64_t num_words() const;
   int poll_once(std::string* what);                      // one check; the first error code or 0
   void start();
   void stop();
@@ -226,6 +232,7 @@ class HealthMonitor {
   AbortFn abort_ = nullptr;
   ErrStrFn err_str_ = nullptr;
   std::vector<void*> comms_;
+  std::vector<std::pair<const uint32_t*, std::string>> words_;
   int injected_ = 0;
   std::string injected_what_;
   std::atomic<int> error_{0};

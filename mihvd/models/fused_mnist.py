@@ -219,6 +219,8 @@ class FusedMNISTTrainer:
                         _xg.warn_fallback(str(e))
             # "on": use it from the first step; "auto": RCCL until select_data_plane() validated it
             self.use_xgmi = self.xplane is not None and self._xgmi_mode == "on"
+            if self.use_xgmi:
+                self.xplane.watch(True)
         if self.gather:
             if self.xplane is not None:
                 self.a2_all = self.xplane.view("a2").view(self.world * B, 3136)
@@ -1207,6 +1209,7 @@ class FusedMNISTTrainer:
         shard_options = [bool(x) and not self.fuse_w3_requested() for x in shard_options]
         planes = ["rccl"]
         if self.xplane is not None and self._xgmi_mode != "off":
+            self.xplane.watch(False)  # a timeout while the plane is on trial means "use RCCL"
             valid = self._validate_xgmi()
             rep["valid"] = valid
             if valid:
@@ -1223,6 +1226,7 @@ class FusedMNISTTrainer:
         if len(cands) == 1 or (host and os.environ.get("MIHVD_XGMI_CHECK", "1") == "0"):
             self._set_plane(cands[0][0] == "xgmi", cands[0][1])
             rep["plane"], rep["shard"] = cands[0]
+            self._watch_plane()
             return rep
         times = {}
         finals = {}
@@ -1293,7 +1297,13 @@ class FusedMNISTTrainer:
         self._restore(snap)
         rep["us_per_step"] = {f"{p}{'-shard' if s else '-replicated'}": round(t, 2) for (p, s), t in times.items()}
         rep["plane"], rep["shard"] = plane, sh
+        self._watch_plane()
         return rep
+
+    def _watch_plane(self):
+        """Arm (or disarm) the health monitor's watch of the xGMI timeout word for the chosen plane."""
+        if self.xplane is not None:
+            self.xplane.watch(self.use_xgmi)
 
     def _snapshot(self) -> dict:
         """Device copies of everything a training step changes (weights, Adam slots, step state)."""

@@ -183,8 +183,30 @@ class XGMIRegion:
             raise RuntimeError(f"xGMI collective timed out waiting for rank(s) {ranks} (error word {err:#x}); "
                                "the outputs of this and every later xGMI collective are NaN")
 
+    def watch(self, on: bool = True) -> bool:
+        """Hand the host-coherent mirror of the error word to the native health monitor
+        (csrc/runtime/health.cc): a phase barrier that times out mid-replay then aborts the process
+        within one poll interval (exit 134, so the launcher tears the job down) instead of surfacing
+        at the next host sync. Arm it once the plane is chosen for training: during
+        ``select_data_plane`` a timeout means "fall back to RCCL", not "abort". False when there
+        is no monitor (``MIHVD_HEALTH=0``) or no mirror."""
+        from .. import basics
+
+        mon = getattr(basics._ctx, "health", None)
+        addr = int(self._o.xgmi_error_word(self.ctx)) if self.ctx is not None else 0
+        if mon is None or not addr:
+            return False
+        if on:
+            mon.watch_word(addr, f"xGMI phase barrier (rank {self.rank} of {self.world})")
+        else:
+            mon.unwatch_word(addr)
+        self._watched = bool(on)
+        return True
+
     def close(self):
         if not self._closed and self.ctx is not None:
+            if getattr(self, "_watched", False):
+                self.watch(False)  # before the word is freed
             self._views.clear()
             self._o.xgmi_destroy(self.ctx)
             self._closed = True

@@ -124,10 +124,45 @@ def test_collective_async_error_aborts_every_rank(tmp_path):
                                                    "MIHVD_HEALTH_POLL_S": "0.2"}, expect_ok=False, timeout=120)
     el = time.time() - t0
     assert p.returncode == 134, p.stderr[-2000:]
-    assert "mihvd health: RCCL async error 6" in p.stderr
+    assert "mihvd health: collective error 6" in p.stderr
     assert "rank 1 exited with code 134" in p.stderr
     assert outs == [None, None]
     assert el < 60, el
+
+
+def test_health_monitor_watches_error_words():
+    """The xGMI plane mirrors a phase-barrier timeout into a host-coherent word that the native
+    health monitor polls (csrc/runtime/health.cc watch_word): zero is healthy, any nonzero value is
+    a collective failure reported like RCCL's remote error (6), naming the word's label; an
+    unwatched word is ignored (here the word is host memory written by the test instead of a kernel)."""
+    import numpy as np
+
+    from mihvd._native import runtime
+
+    mon = runtime().HealthMonitor(0, 0.05, 134)
+    mon.set_abort_process(False)
+    word = np.zeros(16, dtype=np.uint32)
+    addr = word.ctypes.data
+    mon.watch_word(addr, "xGMI phase barrier (test)")
+    mon.watch_word(addr, "again")  # idempotent
+    assert mon.num_words == 1
+    assert mon.poll_once() == (0, "")
+    word[0] = 0x80000002
+    code, what = mon.poll_once()
+    assert code == 6 and "xGMI phase barrier (test)" in what and "0x80000002" in what
+    mon.unwatch_word(addr)
+    assert mon.num_words == 0 and mon.poll_once() == (0, "")
+    # the background thread reports it too (report-only mode: no exit)
+    mon.watch_word(addr, "bg")
+    mon.start()
+    import time
+
+    t0 = time.time()
+    while mon.error == 0 and time.time() - t0 < 10:
+        time.sleep(0.02)
+    mon.stop()
+    mon.unwatch_word(addr)
+    assert mon.error == 6
 
 
 NEG = {"MIHVD_NEGOTIATE": "1"}
