@@ -55,3 +55,7 @@ def test_xgmi_peer_timeout_poisons_and_raises(tmp_path):
     assert r0["first_s"] < 2.5, r0           # bounded by the timeout, not by the late peer
     assert r0["second_nan"] and r0["second_s"] < 1.0, r0  # poisoned: no second wait
     assert not r1["first_nan"] and not r1["raised"], r1   # the late rank found its peer's signal
+    # the timeout reached the host-coherent mirror the health monitor watches (bit 1 + poison)
+    assert r0["mirror"] == 0x80000002, r0
+    assert r0["monitor"][0] == 6 and "xgmi test" in r0["monitor"][1], r0
+    assert r1["mirror"] == 0 and r1["monitor"] == [0, ""], r1

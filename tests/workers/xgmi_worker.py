@@ -155,6 +155,18 @@ def sc_timeout(r, w):
     torch.cuda.synchronize()
     res["first_s"] = time.perf_counter() - t0
     res["first_nan"] = bool(torch.isnan(out).all())
+    # the host-coherent mirror of the error word, and the health monitor's view of it
+    import ctypes
+
+    from mihvd._native import runtime
+
+    addr = int(reg._o.xgmi_error_word(reg.ctx))
+    res["mirror"] = ctypes.c_uint32.from_address(addr).value if addr else -1
+    mon = runtime().HealthMonitor(r, 0.05, 134)
+    mon.set_abort_process(False)
+    mon.watch_word(addr, "xgmi test")
+    res["monitor"] = list(mon.poll_once())
+    mon.unwatch_word(addr)
     try:
         reg.check()
         res["raised"] = False
