@@ -10,6 +10,8 @@
 //   so every global tensor is staged in its natural layout and never transposed in HBM.
 #pragma once
 
+#include <cstdlib>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -218,6 +220,12 @@ struct AdamArgs {
 
 // CU count of the current device, queried once per device (launch-time grid sizing; a
 // hipDeviceGetAttribute per launch costs host time on every step of an eager loop).
+// Integer knob from the environment (kernel-study switches read at launch/capture time), or def.
+inline int env_knob(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return (v != nullptr && *v != '\0') ? std::atoi(v) : def;
+}
+
 inline int device_cu_count() {
   static int cache[64] = {0};
   int dev = 0;

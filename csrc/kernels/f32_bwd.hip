@@ -50,31 +50,46 @@ __device__ __forceinline__ void f32_fc1_dgrad_block(int bid, const float* __rest
     const int i = t + 256 * it, r = i >> 8, c = i & 255, m = m0 + r;
     dv[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)min(m, B - 1) * 1024 + 4 * c), m < B);
   }
+  // W3 streams from HBM / L2 in 8 chunks of 128 k (8 float4 per lane each) through a 4-deep
+  // register ring: three chunks (24 loads per lane) stay in flight ahead of the MFMAs
   const float* wr = w3 + (int64_t)(64 * jt + 16 * wave + lr) * 1024 + 4 * lg;
-  float4 wv[2][8];
+  float4 wv[4][8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) wv[0][u] = *reinterpret_cast<const float4*>(wr + 16 * u);
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) wv[c][u] = *reinterpret_cast<const float4*>(wr + 16 * (8 * c + u));
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
     const int i = t + 256 * it;
     *reinterpret_cast<float4*>(Ds + (i >> 8) * F1B_DS + 4 * (i & 255)) = dv[it];
   }
   __syncthreads();
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  f32x4 accq[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                  f32x4{0.f, 0.f, 0.f, 0.f}};
   const float* dp = Ds + lr * F1B_DS + 4 * lg;
 #pragma unroll
   for (int c8 = 0; c8 < 8; ++c8) {
-    if (c8 + 1 < 8) {
+    if (c8 + 3 < 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) wv[(c8 + 1) & 1][u] = *reinterpret_cast<const float4*>(wr + 16 * (8 * (c8 + 1) + u));
+      for (int u = 0; u < 8; ++u) wv[(c8 + 3) & 3][u] = *reinterpret_cast<const float4*>(wr + 16 * (8 * (c8 + 3) + u));
     }
+    float4 bq[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float4 bq = *reinterpret_cast<const float4*>(dp + 16 * (8 * c8 + u));
-      if (u & 1) acc1 = mfma4_q(wv[c8 & 1][u], bq, acc1);
-      else acc0 = mfma4_q(wv[c8 & 1][u], bq, acc0);
+    for (int u = 0; u < 8; ++u) bq[u] = *reinterpret_cast<const float4*>(dp + 16 * (8 * c8 + u));
+    // four accumulators, k-element outer: no two consecutive MFMAs share one
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].x, bq[4 * h + u].x, accq[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].y, bq[4 * h + u].y, accq[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].z, bq[4 * h + u].z, accq[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].w, bq[4 * h + u].w, accq[u]);
     }
   }
+  const f32x4 acc0 = accq[0] + accq[2], acc1 = accq[1] + accq[3];
   // C[row 4lg + i][col lr] = channel co + i of window jt, sample m0 + lr
   const f32x4 acc = acc0 + acc1;
   const int m = m0 + lr, mc = min(m, B - 1), co = 16 * wave + 4 * lg, j = 64 * jt + co;
@@ -240,10 +255,9 @@ __global__ void __launch_bounds__(256) f32_fc1_bwd_kernel(
 // ------------------------------------------------------------------------------------------ //
 constexpr int CBF_PS = 68, CBF_RS = 18 * CBF_PS, CBF_MAXR = 18;
 constexpr int CBF_IMG = CBF_MAXR * CBF_RS;            // floats: tall padded dY2 rows
-constexpr int CBF_WB = 32 * 68;                       // one W2 tap slice [32 ci][68]
 constexpr int CBF_XIM = 2 * 1024;                     // two padded x images [32][32]
 constexpr int CBF_PW = 8 * 26 * 16;                   // per-wave conv1 partials
-constexpr int CBF_LDS_DG = (CBF_IMG + 2 * CBF_WB + CBF_XIM + CBF_PW) * 4;   // 127,040 B
+constexpr int CBF_LDS_DG = (CBF_IMG + CBF_XIM + CBF_PW) * 4;               // 109,632 B
 constexpr int CBF_A1S = 14 * 18 * 32, CBF_DYS = 196 * 32, CBF_WBUF = CBF_A1S + CBF_DYS;
 constexpr int CBF_LDS_WG = 2 * CBF_WBUF * 4;                                // 114,688 B
 constexpr int CBF_LDS = CBF_LDS_DG > CBF_LDS_WG ? CBF_LDS_DG : CBF_LDS_WG;
@@ -257,17 +271,17 @@ static_assert(4 * 5 * 4 * 64 * 16 <= CBF_LDS_WG, "wgrad partial exchange fits th
 // dgrad role. Pixels of the batch (flattened [B][196], raster order) in 16-pixel tiles; block owns
 // tiles [bid TPB, (bid+1) TPB). dA1[p][ci] = sum_{tap, co} dY2pad[p + (4 - kh, 4 - kw)][co] W2[tap][ci][co]:
 // A = the routed gradient (tall padded image rows in LDS, co contiguous -> float4), B = the W2 tap
-// slice read as [ci][co] (co contiguous -> float4): both K-contiguous in their natural layouts.
-// 8 waves: wave w = ci half (w & 1) x co quarter (w >> 1) of K; the four co-quarter partials are
-// summed through LDS before the epilogue.
+// slice read as [ci][co] (co contiguous -> float4): a wave's whole B (25 taps x 16 co x 16 ci =
+// 100 floats per lane) is loaded into registers once, so the tap loop has no global load and no
+// barrier. 8 waves: wave w = ci half (w & 1) x co
+// quarter (w >> 1) of K; the four co-quarter partials are summed through LDS before the epilogue.
 template <int TPB>
 __device__ __forceinline__ void f32_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf) {
   float* dimg = smf;
-  float* wbuf = smf + CBF_IMG;
-  float* xim = wbuf + 2 * CBF_WB;
+  float* xim = smf + CBF_IMG;
   float* pw = xim + CBF_XIM;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int np = 196 * B, T0 = bid * TPB;
@@ -275,8 +289,8 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   const int b0 = P0 / 196, b1i = P1 / 196;
   const int R0 = 18 * b0 + (P0 - 196 * b0) / 14, R1 = 18 * b1i + (P1 - 196 * b1i) / 14 + 5;
   const int nch = (R1 - R0) * 288;  // 18 pixels x 16 float4
-  // 1. loads: tap-0 weights, the dY2 rows, the (at most two) x images
-  float4 wr = *reinterpret_cast<const float4*>(w2 + (t >> 4) * 64 + (t & 15) * 4);
+  const int nt = wave & 1, cq = wave >> 1;
+  // 1. loads: the first two taps' weight fragments, the dY2 rows, the (at most two) x images
   float4 iv[CBF_MAXCH];
 #pragma unroll
   for (int it = 0; it < CBF_MAXCH; ++it) {
@@ -301,6 +315,11 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
     xv[it] = mask_f(x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
   }
+  // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3]
+  const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
+  float4 wb[25];
+#pragma unroll
+  for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
 #pragma unroll
   for (int it = 0; it < CBF_MAXCH; ++it) {
     const int i = t + 512 * it;
@@ -311,8 +330,6 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   }
 #pragma unroll
   for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
-  *reinterpret_cast<float4*>(wbuf + (t >> 4) * CBF_PS + (t & 15) * 4) = wr;
-  const int nt = wave & 1, cq = wave >> 1;
   int abase[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) {
@@ -323,22 +340,25 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   f32x4 acc[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-  const float* wq = wbuf + (16 * nt + lr) * CBF_PS + 16 * cq + 4 * lg;
-  for (int tap = 0; tap < 25; ++tap) {
-    if (tap + 1 < 25) wr = *reinterpret_cast<const float4*>(w2 + (tap + 1) * 2048 + (t >> 4) * 64 + (t & 15) * 4);
+  __syncthreads();  // the images are complete; no barrier in the tap loop
+#pragma unroll
+  for (int tap = 0; tap < 25; ++tap) {  // fully unrolled: constant LDS offsets, static register indices
     const int kh = tap / 5, kw = tap - 5 * kh;
     const int aoff = ((4 - kh) * 18 + (4 - kw)) * CBF_PS;
-    const float4 bq = *reinterpret_cast<const float4*>(wq + (tap & 1) * CBF_WB);
+    float4 a[TPB];
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) {
-      const float4 a = *reinterpret_cast<const float4*>(dimg + abase[i] + aoff);
-      acc[i] = mfma4_q(a, bq, acc[i]);
-    }
-    if (tap + 1 < 25)
-      *reinterpret_cast<float4*>(wbuf + ((tap + 1) & 1) * CBF_WB + (t >> 4) * CBF_PS + (t & 15) * 4) = wr;
-    __syncthreads();
+    for (int i = 0; i < TPB; ++i) a[i] = *reinterpret_cast<const float4*>(dimg + abase[i] + aoff);
+    // k-element j outer, tiles inner: consecutive MFMAs use different accumulators
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].x, wb[tap].x, acc[i]);
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].y, wb[tap].y, acc[i]);
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].z, wb[tap].z, acc[i]);
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].w, wb[tap].w, acc[i]);
   }
+  __syncthreads();  // every wave is done with the dY2 image
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
 #pragma unroll
@@ -444,12 +464,18 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     if (n + 1 < nimg) load_img(img0 + n + 1, v);
     const float* A1s = buf;
     const float* DYs = buf + CBF_A1S;
-    for (int s = wave; s < 98; s += 8) {  // K step s: pixels 2s (lanes 0-31) and 2s + 1 (32-63)
-      const int q = 2 * s + hh, qy = q / 14, qx = q - 14 * qy;
-      const float a = DYs[q * 32 + l32];
-      const float* bp = A1s + (qy * 18 + qx) * 32 + l32;
+    // K steps s = wave + 8u (pixels 2s: lanes 0-31, 2s + 1: lanes 32-63), unrolled so the LDS
+    // reads of later steps are in flight while earlier steps' MFMAs issue
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(a, bp[kw * 32], acc[kw]);
+    for (int u = 0; u < 13; ++u) {
+      const int s = wave + 8 * u;
+      if (u < 12 || s < 98) {  // wave-uniform (98 = 12 x 8 + 2)
+        const int q = 2 * s + hh, qy = q / 14, qx = q - 14 * qy;
+        const float a = DYs[q * 32 + l32];
+        const float* bp = A1s + (qy * 18 + qx) * 32 + l32;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(a, bp[kw * 32], acc[kw]);
+      }
     }
     if (n + 1 < nimg) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
@@ -513,20 +539,55 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------ //
-// f32_conv_reduce: blocks [0, 50): dW2 (12,800 float4 = sum over the G slabs); [50, 63): dW1/db1
-// (64 elements x 4 row parts of the dgrad blocks' partial rows); 63: db2 (64 channels x 4 parts of
-// the fc1 dgrad blocks' rows). With the optimizer fused (world size 1: the gradients are final
-// here) every block applies Adam to the elements it just produced, blocks [64, 64 + n_fc) apply it
-// to the small fc parameters [fc_lo, fc_hi) (dense/bias, dense_1/*, produced by fc1_bwd), and
-// block 0 advances the forward step counter (adam_step's bump): one launch for the gradient
-// reduction and the whole optimizer except dense/kernel (whose update is deferred into the next
-// conv2_fwd launch, f32_fwd.hip).
+// f32_conv_reduce: a latency-bound gather of partial sums (the slabs were just written by
+// conv2_bwd on every XCD, so most reads miss this XCD's L2), written for memory-level
+// parallelism: each thread keeps 8 independent loads in flight and the partial sums meet in LDS.
+//   blocks [0, 200):   dW2, 64 float4 per block x 4 slab quarters (sum over the G slabs)
+//   blocks [200, 213): dW1 | db1, 16 float4 columns (64 of the 832) x 16 row parts of cpart
+//   block  213:        db2, 16 float4 columns x 16 row parts of db2p
+//   blocks [214, 214 + n_fc): Adam of the small fc parameters [fc_lo, fc_hi)
+// With the optimizer fused (world size 1: the gradients are final here) every element is updated
+// by the thread that finishes its gradient and block 0 advances the forward step counter
+// (adam_step's bump): one launch for the gradient reduction and the whole optimizer except
+// dense/kernel (whose update is deferred into the next conv2_fwd launch, f32_fwd.hip).
+// Fixed summation order (deterministic, no atomics).
 // ------------------------------------------------------------------------------------------ //
 struct F32SmallAdam {
   F32Adam a;               // p, g, m, v: the FLAT buffers (a.n4 unused); a.nblk = 0: no optimizer
   int o_w1 = 0, o_b1 = 0, o_w2 = 0, o_b2 = 0;   // element offsets of the conv segments
   int fc_lo = 0, fc_hi = 0;                     // the small fc range (multiple-of-4 bounds)
 };
+constexpr int CR_W2 = 200, CR_CP = 13, CR_DB = 1, CR_FC0 = CR_W2 + CR_CP + CR_DB;
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// sum of rows r0, r0 + step, ... (< n) of a float4 column, 8 loads in flight per round
+__device__ __forceinline__ float4 strided_sum8(const float4* __restrict__ p, int64_t stride4, int r0, int step, int n) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = r0; r < n; r += 8 * step) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int rr = r + u * step;
+      v[u] = rr < n ? p[(int64_t)rr * stride4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = f4add(acc, v[u]);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void adam_flat4(const F32SmallAdam& sa, int64_t o, float4 g, const AdamCoef& c) {
+  float4 pp = *reinterpret_cast<const float4*>(sa.a.p + o);
+  float4 mm = *reinterpret_cast<const float4*>(sa.a.m + o);
+  float4 vv = *reinterpret_cast<const float4*>(sa.a.v + o);
+  adam4_f32(pp, mm, vv, g, c);
+  *reinterpret_cast<float4*>(sa.a.p + o) = pp;
+  *reinterpret_cast<float4*>(sa.a.m + o) = mm;
+  *reinterpret_cast<float4*>(sa.a.v + o) = vv;
+}
 
 __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __restrict__ slab, int G,
                                                               const float* __restrict__ cpart, int ncp,
@@ -534,7 +595,7 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
                                                               float* __restrict__ gW2, float* __restrict__ gW1,
                                                               float* __restrict__ gb1, float* __restrict__ gb2,
                                                               F32SmallAdam sa) {
-  __shared__ float red[256];
+  __shared__ float4 red[256];
   const int bid = blockIdx.x, t = threadIdx.x;
   const bool opt = sa.a.nblk > 0;
   AdamCoef c{};
@@ -542,73 +603,65 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
     c = f32_adam_coef(sa.a);
     if (bid == 0 && t == 0) const_cast<int64_t*>(sa.a.state)[ST_FWD] += 1;
   }
-  if (bid < 50) {
-    const int i = bid * 256 + t;
-    float4 s = reinterpret_cast<const float4*>(slab)[i];
-    for (int g = 1; g < G; ++g) {
-      const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)g * 51200)[i];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-    }
-    reinterpret_cast<float4*>(gW2)[i] = s;
-    if (opt) {
-      const int64_t o = sa.o_w2 + 4 * i;
-      float4 pp = *reinterpret_cast<const float4*>(sa.a.p + o);
-      float4 mm = *reinterpret_cast<const float4*>(sa.a.m + o);
-      float4 vv = *reinterpret_cast<const float4*>(sa.a.v + o);
-      adam4_f32(pp, mm, vv, s, c);
-      *reinterpret_cast<float4*>(sa.a.p + o) = pp;
-      *reinterpret_cast<float4*>(sa.a.m + o) = mm;
-      *reinterpret_cast<float4*>(sa.a.v + o) = vv;
-    }
-    return;
-  }
-  if (bid >= 64) {  // small fc parameters: gradients already final (fc1_bwd)
-    const int64_t i = sa.fc_lo / 4 + (int64_t)(bid - 64) * 256 + t;
+  if (bid >= CR_FC0) {  // small fc parameters: gradients already final (fc1_bwd)
+    const int64_t i = sa.fc_lo / 4 + (int64_t)(bid - CR_FC0) * 256 + t;
     if (opt && i < sa.fc_hi / 4) {
-      float4 pp = reinterpret_cast<const float4*>(sa.a.p)[i];
       const float4 gg = reinterpret_cast<const float4*>(sa.a.g)[i];
-      float4 mm = reinterpret_cast<const float4*>(sa.a.m)[i];
-      float4 vv = reinterpret_cast<const float4*>(sa.a.v)[i];
-      adam4_f32(pp, mm, vv, gg, c);
-      reinterpret_cast<float4*>(sa.a.p)[i] = pp;
-      reinterpret_cast<float4*>(sa.a.m)[i] = mm;
-      reinterpret_cast<float4*>(sa.a.v)[i] = vv;
+      adam_flat4(sa, 4 * i, gg, c);
     }
     return;
   }
-  const int e = t & 63, part = t >> 6;
-  float s = 0.f;
-  int64_t po = -1;  // flat offset of the element this thread finishes (optimizer)
-  float gv = 0.f;
-  if (bid < 63) {
-    const int q = (bid - 50) * 64 + e;  // 0..831
-    for (int r = part; r < ncp; r += 4) s += cpart[(int64_t)r * CP_F32 + q];
-    red[t] = s;
-    __syncthreads();
+  const int col = t & 63, part = t >> 6;  // dW2 blocks: 64 float4 x 4 slab quarters
+  const int col16 = t & 15, part16 = t >> 4;  // cpart / db2 blocks: 16 float4 columns x 16 row parts
+  float4 s;
+  if (bid < CR_W2) {
+    const int64_t i = (int64_t)bid * 64 + col;
+    s = strided_sum8(reinterpret_cast<const float4*>(slab) + i, 51200 / 4, part, 4, G);
+  } else if (bid < CR_W2 + CR_CP) {
+    const int c4 = (bid - CR_W2) * 16 + col16;  // float4 column of the 208
+    s = strided_sum8(reinterpret_cast<const float4*>(cpart) + c4, CP_F32 / 4, part16, 16, ncp);
+  } else {
+    s = strided_sum8(reinterpret_cast<const float4*>(db2p) + col16, 16, part16, 16, ndb);
+  }
+  red[t] = s;
+  __syncthreads();
+  if (bid < CR_W2) {
     if (t < 64) {
-      gv = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
-      if (q < 800) {
-        gW1[q] = gv;
-        po = sa.o_w1 + q;
+      const float4 g = f4add(f4add(red[t], red[64 + t]), f4add(red[128 + t], red[192 + t]));
+      const int64_t i = (int64_t)bid * 64 + t;
+      reinterpret_cast<float4*>(gW2)[i] = g;
+      if (opt) adam_flat4(sa, sa.o_w2 + 4 * i, g, c);
+    }
+    return;
+  }
+  if (t < 16) {
+    float4 g = red[t];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) g = f4add(g, red[16 * q + t]);
+    const float ge[4] = {g.x, g.y, g.z, g.w};
+    if (bid < CR_W2 + CR_CP) {
+      const int q0 = ((bid - CR_W2) * 16 + t) * 4;  // 0..831, a float4 never straddles 800
+      if (q0 < 800) {
+        *reinterpret_cast<float4*>(gW1 + q0) = g;
       } else {
-        gb1[q - 800] = gv;
-        po = sa.o_b1 + (q - 800);
+        *reinterpret_cast<float4*>(gb1 + (q0 - 800)) = g;
+      }
+      if (opt) {
+        const int64_t o = q0 < 800 ? sa.o_w1 + q0 : sa.o_b1 + (q0 - 800);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) adam1(sa.a.p[o + e], sa.a.m[o + e], sa.a.v[o + e], ge[e], c);
+      }
+    } else {
+      *reinterpret_cast<float4*>(gb2 + 4 * t) = g;
+      if (opt) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t o = sa.o_b2 + 4 * t + e;
+          adam1(sa.a.p[o], sa.a.m[o], sa.a.v[o], ge[e], c);
+        }
       }
     }
-  } else {
-    for (int r = part; r < ndb; r += 4) s += db2p[(int64_t)r * 64 + e];
-    red[t] = s;
-    __syncthreads();
-    if (t < 64) {
-      gv = (red[e] + red[64 + e]) + (red[128 + e] + red[192 + e]);
-      gb2[e] = gv;
-      po = sa.o_b2 + e;
-    }
   }
-  if (opt && po >= 0) adam1(sa.a.p[po], sa.a.m[po], sa.a.v[po], gv, c);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -654,10 +707,14 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
     return true;
   }();
   (void)attr;
-  f32_fc1_bwd_kernel<<<n_dg + F1B_SMALL + F1B_WGRAD, 256, F1B_LDS, stream>>>(
+  // study knob: MIHVD_F32_F1B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only
+  const int role = env_knob("MIHVD_F32_F1B_ROLE", 0);
+  const int grid = role == 1 ? n_dg : role == 2 ? F1B_WGRAD : n_dg + F1B_SMALL + F1B_WGRAD;
+  const int ndg_arg = role == 2 ? -F1B_SMALL : n_dg;  // wgrad only: bid - n_dg - 33 = bid
+  f32_fc1_bwd_kernel<<<grid, 256, F1B_LDS, stream>>>(
       dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(), dlog.data_ptr<float>(),
       w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(), gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg);
+      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, ndg_arg);
 }
 
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
@@ -690,11 +747,17 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
     TORCH_CHECK(r1 - r0 <= CBF_MAXR && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS image");
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
+  // study knobs: MIHVD_F32_C2B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only (the other role's
+  // outputs are then stale); MIHVD_F32_C2B_LDS requests more dynamic LDS than the roles need
+  const int role = env_knob("MIHVD_F32_C2B_ROLE", 0);
+  const int lds = std::max(CBF_LDS, std::min(env_knob("MIHVD_F32_C2B_LDS", 0), 163840));
+  const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
+  const int ndg_arg = role == 2 ? 0 : n_dg;
   auto launch = [&](auto kern) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, CBF_LDS);
-    kern<<<n_dg + 10 * ngrp, 512, CBF_LDS, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
-                                                     idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
-                                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, n_dg);
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
+                                     idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
+                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg);
   };
   switch (tpb) {
     case 1: launch(f32_conv2_bwd_kernel<1>); break;
@@ -720,6 +783,9 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
   chk_f32(gW1, 800, "f32_conv_reduce: gW1");
   chk_f32(gb1, 32, "f32_conv_reduce: gb1");
   chk_f32(gb2, 64, "f32_conv_reduce: gb2");
+  for (const at::Tensor* t : {(const at::Tensor*)&gW2, (const at::Tensor*)&gW1, (const at::Tensor*)&gb1,
+                              (const at::Tensor*)&gb2, &slab, &cpart, &db2p})
+    TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "f32_conv_reduce: operands must be 16-byte aligned");
   F32SmallAdam sa;
   int n_fc = 0;
   if (params.has_value() && params->defined()) {
@@ -760,7 +826,7 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
     n_fc = (int)((fc_hi - fc_lo) / 4 + 255) / 256;
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  f32_conv_reduce_kernel<<<64 + n_fc, 256, 0, stream>>>(slab.data_ptr<float>(), (int)(slab.numel() / 51200),
+  f32_conv_reduce_kernel<<<CR_FC0 + n_fc, 256, 0, stream>>>(slab.data_ptr<float>(), (int)(slab.numel() / 51200),
                                                         cpart.data_ptr<float>(), (int)(cpart.numel() / CP_F32),
                                                         db2p.data_ptr<float>(), (int)(db2p.numel() / 64),
                                                         gW2.data_ptr<float>(), gW1.data_ptr<float>(),

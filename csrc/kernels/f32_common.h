@@ -80,24 +80,37 @@ __device__ __forceinline__ void adam4_f32(float4& pp, float4& mm, float4& vv, co
   adam1(pp.w, mm.w, vv.w, gg.w, c);
 }
 
-// Grid-stride stream of the range by blocks [0, a.nblk) of a launch (one float4 of each array per
-// lane per iteration, restrict-qualified locals: the loads of an iteration are all in flight).
+// Grid-stride stream of the range by blocks [0, a.nblk) of a launch: four float4 of each array
+// per lane per round, all 16 loads issued before the first is used (an HBM-latency-bound stream
+// needs that many bytes in flight per CU), restrict-qualified locals.
 __device__ __forceinline__ void f32_adam_stream(const F32Adam& a, int bid) {
+  constexpr int U = 4;
   const AdamCoef c = f32_adam_coef(a);
   float* __restrict__ p = a.p;
   const float* __restrict__ g = a.g;
   float* __restrict__ m = a.m;
   float* __restrict__ v = a.v;
-  const int64_t stride = (int64_t)a.nblk * blockDim.x;
-  for (int64_t i = (int64_t)bid * blockDim.x + threadIdx.x; i < a.n4; i += stride) {
-    float4 pp = reinterpret_cast<const float4*>(p)[i];
-    const float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<const float4*>(m)[i];
-    float4 vv = reinterpret_cast<const float4*>(v)[i];
-    adam4_f32(pp, mm, vv, gg, c);
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
+  const int64_t nthr = (int64_t)a.nblk * blockDim.x;
+  for (int64_t i0 = (int64_t)bid * blockDim.x + threadIdx.x; i0 < a.n4; i0 += U * nthr) {
+    float4 pp[U], gg[U], mm[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = min(i0 + u * nthr, a.n4 - 1);
+      pp[u] = reinterpret_cast<const float4*>(p)[i];
+      gg[u] = reinterpret_cast<const float4*>(g)[i];
+      mm[u] = reinterpret_cast<const float4*>(m)[i];
+      vv[u] = reinterpret_cast<const float4*>(v)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * nthr;
+      if (i < a.n4) {
+        adam4_f32(pp[u], mm[u], vv[u], gg[u], c);
+        reinterpret_cast<float4*>(p)[i] = pp[u];
+        reinterpret_cast<float4*>(m)[i] = mm[u];
+        reinterpret_cast<float4*>(v)[i] = vv[u];
+      }
+    }
   }
 }
 

@@ -14,7 +14,7 @@
 //
 //   f32_conv1_fwd  conv1 (K = 25 taps in 7 MFMAs, x in LDS) + bias + ReLU + 2x2 pool/argmax
 //   f32_conv2_fwd  conv2 over 16-pixel tiles of the whole batch (pool-window-major rows), ~one
-//                  block per CU; a1 rows staged once, W2 streamed tap by tap (double-buffered)
+//                  block per CU; a1 rows staged once in LDS, W2 fragments from L2 two taps ahead
 //   f32_fc1_fwd    split-K (14 slices of 224) partial slabs; W3 fragments held in registers
 //   f32_head       slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
 #include <ATen/ATen.h>
@@ -99,35 +99,57 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
 // b owns tiles [b TPB, (b+1) TPB) (TPB = ceil(tiles / 256): about one block per CU), which span at
 // most two images. The a1 rows those tiles read are staged once as rows of the "tall" padded image
 // (image i = tall rows [18 i, 18 i + 18), padded row r = a1 row r - 2, 18 padded columns, pixel
-// stride 36 floats). W2 streams through LDS one tap ([32 ci][64 co] = 8 KB) at a time,
-// double-buffered, one barrier per tap. 4 waves; wave w owns output channels 16w..16w+15 of every
-// tile: per tap one ds_read_b32 B fragment per MFMA (shared by the TPB tiles) and two float4 A
-// chunks per tile. Epilogue: 2x2 max-pool + argmax + bias + ReLU in registers.
+// stride 36 floats). 4 waves, one per SIMD; wave w owns output channels 16w..16w+15.
+//
+// Weights stay in registers: a wave's whole B operand (W2[tap][ci][16w..16w+15], 800 k x 16 co =
+// 200 floats per lane) is loaded once, so the MFMA loop has no global load and no barrier; only
+// the A chunks come from LDS (one ds_read_b128 per 4 MFMAs, shared by the 4 waves). Tiles are
+// processed in pairs with alternating accumulators (16x16x4 f32: 32-cycle issue, 40-cycle
+// dependent latency), the 25 taps fully unrolled (constant LDS offsets, static register indices).
+// Epilogue: 2x2 max-pool + argmax + bias + ReLU in registers.
 // ------------------------------------------------------------------------------------------ //
-constexpr int C2F_PS = 36, C2F_RS = 18 * C2F_PS, C2F_MAXR = 22, C2F_WS = 68, C2F_WB = 32 * C2F_WS;
-constexpr int C2F_LDS = (C2F_MAXR * C2F_RS + 2 * C2F_WB) * 4;     // 74,432 B
+constexpr int C2F_PS = 36, C2F_RS = 18 * C2F_PS, C2F_MAXR = 22;
+constexpr int C2F_LDS = C2F_MAXR * C2F_RS * 4;                     // 57,024 B
 constexpr int C2F_MAXCH = (C2F_MAXR * 18 * 8 + 255) / 256;         // image float4 chunks per thread
 
-// two float4 chunks of one [32][64] HWIO tap slice per thread (256 threads)
-__device__ __forceinline__ void w2_tap_load(const float* __restrict__ w2, int tap, int t, float4 (&wr)[2]) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = t + 256 * u;
-    wr[u] = *reinterpret_cast<const float4*>(w2 + tap * 2048 + (i >> 4) * 64 + (i & 15) * 4);
-  }
+// A row (tall-image offset) of lane row lr of tile `tile` (clamped past the batch)
+__device__ __forceinline__ int c2f_abase(int tile, int lr, int lg, int nwin, int R0) {
+  const int m = 16 * tile + lr;
+  const int gw = min(m >> 2, nwin - 1), d = m & 3;
+  const int bb = gw / 49, win = gw - 49 * bb, py = win / 7, px = win - 7 * py;
+  const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
+  return ((18 * bb + y - R0) * 18 + xx) * C2F_PS + 4 * lg;
 }
-__device__ __forceinline__ void w2_tap_store(float* dst, int t, const float4 (&wr)[2]) {
+
+// NT (1 or 2) tiles against the register-resident weights: acc[u] += A(tile u) x W2
+template <int NT>
+__device__ __forceinline__ void c2f_tiles(const float* img, const int (&ab)[2], const float (&wb)[200],
+                                          f32x4 (&acc)[2]) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = t + 256 * u;
-    *reinterpret_cast<float4*>(dst + (i >> 4) * C2F_WS + (i & 15) * 4) = wr[u];
+  for (int tap = 0; tap < 25; ++tap) {
+    const int kh = tap / 5, kw = tap - 5 * kh, aoff = (kh * 18 + kw) * C2F_PS;
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) {
+      float4 a[NT];
+#pragma unroll
+      for (int u = 0; u < NT; ++u) a[u] = *reinterpret_cast<const float4*>(img + ab[u] + aoff + 16 * c2);
+      const float* w = wb + tap * 8 + 4 * c2;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].x, w[0], acc[u]);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].y, w[1], acc[u]);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].z, w[2], acc[u]);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].w, w[3], acc[u]);
+    }
   }
 }
 
 // TAIL: the first ad.nblk blocks of the launch stream an Adam update instead (the previous step's
 // dense/kernel update, deferred into this MFMA-bound launch, which leaves HBM idle). They are first
 // in dispatch order, so they take the CUs before the conv blocks; a tail block and a conv block fit
-// one CU together (2 x 74 KB of LDS, 4 + 4 waves).
+// one CU together (2 x 57 KB of LDS, 4 + 4 waves).
 template <int TPB, bool TAIL>
 __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, float* __restrict__ a2,
@@ -140,7 +162,6 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
     }
   }
   float* img = smf;
-  float* wbuf = smf + C2F_MAXR * C2F_RS;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int nwin = 49 * B, T0 = ((int)blockIdx.x - (TAIL ? ad.nblk : 0)) * TPB;
   const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
@@ -148,9 +169,7 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
   const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
   const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
-  // 1. every load in flight first: tap-0 weights, then the image rows
-  float4 wr[2];
-  w2_tap_load(w2, 0, t, wr);
+  // 1. every load in flight first: the image rows, then this wave's weights (into registers)
   float4 iv[C2F_MAXCH];
 #pragma unroll
   for (int it = 0; it < C2F_MAXCH; ++it) {
@@ -162,6 +181,14 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
         a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
     iv[it] = mask_f4(v, in);
   }
+  float wb[200];  // wb[8 tap + 4 c2 + j] = W2[tap][16 c2 + 4 lg + j][16 w + lr]
+  const float* wp = w2 + (4 * lg) * 64 + 16 * wave + lr;
+#pragma unroll
+  for (int tap = 0; tap < 25; ++tap)
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wb[8 * tap + 4 * c2 + j] = wp[tap * 2048 + (16 * c2 + j) * 64];
 #pragma unroll
   for (int it = 0; it < C2F_MAXCH; ++it) {
     const int i = t + 256 * it;
@@ -170,54 +197,27 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
       *reinterpret_cast<float4*>(img + (rr * 18 + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
     }
   }
-  w2_tap_store(wbuf, t, wr);
-  // 2. per-lane A row of each tile (clamped past the batch; those results are dropped)
-  int abase[TPB];
-#pragma unroll
-  for (int i = 0; i < TPB; ++i) {
-    const int m = 16 * (T0 + i) + lr;
-    const int gw = min(m >> 2, nwin - 1), d = m & 3;
-    const int bb = gw / 49, win = gw - 49 * bb, py = win / 7, px = win - 7 * py;
-    const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
-    abase[i] = ((18 * bb + y - R0) * 18 + xx) * C2F_PS + 4 * lg;
-  }
-  f32x4 acc[TPB];
-#pragma unroll
-  for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-  const float* wcol = wbuf + 4 * lg * C2F_WS + 16 * wave + lr;
-  for (int tap = 0; tap < 25; ++tap) {
-    const float* wb = wcol + (tap & 1) * C2F_WB;
-    if (tap + 1 < 25) w2_tap_load(w2, tap + 1, t, wr);
-    const int kh = tap / 5, kw = tap - 5 * kh;
-    const int aoff = (kh * 18 + kw) * C2F_PS;
-#pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2) {
-      float bv[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = wb[(16 * c2 + j) * C2F_WS];
-      const float4 bq = make_float4(bv[0], bv[1], bv[2], bv[3]);
-#pragma unroll
-      for (int i = 0; i < TPB; ++i) {
-        const float4 a = *reinterpret_cast<const float4*>(img + abase[i] + aoff + 16 * c2);
-        acc[i] = mfma4_q(a, bq, acc[i]);
-      }
-    }
-    if (tap + 1 < 25) w2_tap_store(wbuf + ((tap + 1) & 1) * C2F_WB, t, wr);
-    __syncthreads();
-  }
+  __syncthreads();  // the image is complete; no barrier below
   const int co = 16 * wave + lr;
   const float bias = b2[co];
+  for (int i = 0; i < TPB; i += 2) {  // block-uniform
+    const int tile0 = T0 + i, tile1 = T0 + min(i + 1, TPB - 1);
+    const int ab[2] = {c2f_abase(tile0, lr, lg, nwin, R0), c2f_abase(tile1, lr, lg, nwin, R0)};
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int nt = min(2, TPB - i);
+    if (nt == 2) c2f_tiles<2>(img, ab, wb, acc);
+    else c2f_tiles<1>(img, ab, wb, acc);
 #pragma unroll
-  for (int i = 0; i < TPB; ++i) {
-    const int gw = 4 * (T0 + i) + lg;
-    if (gw < nwin) {
-      const int bb = gw / 49, win = gw - 49 * bb;
-      int best;
-      const float m = pool4(acc[i], best);
-      const int64_t o = (int64_t)bb * 3136 + win * 64 + co;
-      a2[o] = fmaxf(m + bias, 0.f);
-      idx2[o] = (uint8_t)best;
+    for (int u = 0; u < 2; ++u) {
+      const int gw = 4 * (T0 + i + u) + lg;
+      if (u < nt && gw < nwin) {
+        const int bb = gw / 49, win = gw - 49 * bb;
+        int best;
+        const float m = pool4(acc[u], best);
+        const int64_t o = (int64_t)bb * 3136 + win * 64 + co;
+        a2[o] = fmaxf(m + bias, 0.f);
+        idx2[o] = (uint8_t)best;
+      }
     }
   }
 }
@@ -481,9 +481,12 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   const F32Adam ad =
       f32_adam_args(p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule, nt_tail, "f32_conv2_fwd");
   auto stream = c10::hip::getCurrentHIPStream().stream();
+  // MIHVD_F32_C2F_LDS (study knob): request more dynamic LDS than the image needs, which caps
+  // how many blocks share a CU
+  const int lds = std::max(C2F_LDS, std::min(env_knob("MIHVD_F32_C2F_LDS", 0), 163840));
   auto launch = [&](auto kern, int extra) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C2F_LDS);
-    kern<<<nblk + extra, 256, C2F_LDS, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    kern<<<nblk + extra, 256, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
                                                  a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, ad);
   };
 #define C2F_CASE(T)                                                                  \

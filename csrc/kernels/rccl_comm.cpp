@@ -1,0 +1,284 @@
+// Native RCCL communicator owned by the framework ("ncclCommInitRank,
+// the side stream and async-error polling in the C++ runtime").
+//
+// The reference's data plane is Horovod's native core (built at horovod/Dockerfile:51-65), which
+// owns its NCCL communicator and enqueues the fused allreduce of every step
+// (horovod/tensorflow_mnist.py:133, hvd.DistributedOptimizer) on its own stream. Here the fused
+// trainer's collectives (bucket allreduce, dW3 row reduce-scatter / all-gather, state broadcast)
+// go through this communicator instead of torch.distributed's process group: one RCCL comm per
+// rank, created from a unique id that rank 0 draws and the ranks exchange over the bootstrap
+// store, and ops that enqueue straight onto the caller's HIP stream (the trainer's side stream, or
+// a stream being captured into the step's HIP graph) with no process-group bookkeeping around them.
+//
+// The RCCL entry points are resolved from the librccl the process already loaded (torch links it;
+// /proc/self/maps names the file), so this communicator, torch's and the health monitor's view of
+// them share one library instance; rccl.h is used for the types and enum values only.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+#include <torch/library.h>
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace mihvd {
+namespace {
+
+struct Rccl {
+  void* lib = nullptr;
+  std::string path;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclCommAbort) abort = nullptr;
+  decltype(&ncclCommGetAsyncError) async_error = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+};
+
+std::string loaded_rccl_path() {
+  std::ifstream maps("/proc/self/maps");
+  std::string line;
+  while (std::getline(maps, line)) {
+    const auto pos = line.find('/');
+    if (pos == std::string::npos) continue;
+    const std::string p = line.substr(pos);
+    const auto slash = p.rfind('/');
+    if (p.compare(slash + 1, 9, "librccl.s") == 0) return p;
+  }
+  return "";
+}
+
+Rccl& rccl() {
+  static std::once_flag once;
+  static Rccl r;
+  std::call_once(once, [] {
+    std::string p = loaded_rccl_path();
+    void* h = p.empty() ? nullptr : dlopen(p.c_str(), RTLD_NOW | RTLD_NOLOAD);
+    if (h == nullptr) {
+      p = "librccl.so.1";
+      h = dlopen(p.c_str(), RTLD_NOW | RTLD_LOCAL);
+    }
+    if (h == nullptr) return;
+    r.lib = h;
+    r.path = p;
+#define MIHVD_SYM(field, name) r.field = reinterpret_cast<decltype(r.field)>(dlsym(h, #name))
+    MIHVD_SYM(get_unique_id, ncclGetUniqueId);
+    MIHVD_SYM(init_rank, ncclCommInitRank);
+    MIHVD_SYM(destroy, ncclCommDestroy);
+    MIHVD_SYM(abort, ncclCommAbort);
+    MIHVD_SYM(async_error, ncclCommGetAsyncError);
+    MIHVD_SYM(error_string, ncclGetErrorString);
+    MIHVD_SYM(all_reduce, ncclAllReduce);
+    MIHVD_SYM(all_gather, ncclAllGather);
+    MIHVD_SYM(reduce_scatter, ncclReduceScatter);
+    MIHVD_SYM(broadcast, ncclBroadcast);
+    MIHVD_SYM(group_start, ncclGroupStart);
+    MIHVD_SYM(group_end, ncclGroupEnd);
+#undef MIHVD_SYM
+  });
+  TORCH_CHECK(r.lib != nullptr && r.init_rank != nullptr && r.all_reduce != nullptr && r.all_gather != nullptr &&
+                  r.reduce_scatter != nullptr && r.broadcast != nullptr && r.get_unique_id != nullptr &&
+                  r.destroy != nullptr,
+              "rccl_comm: librccl is not loaded in this process or lacks the expected entry points");
+  return r;
+}
+
+void check(ncclResult_t e, const char* what) {
+  if (e == ncclSuccess) return;
+  const Rccl& r = rccl();
+  TORCH_CHECK(false, "rccl_comm: ", what, " failed: ", r.error_string ? r.error_string(e) : "error", " (", (int)e,
+              ")");
+}
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1, device = -1;
+};
+
+std::mutex g_mu;
+std::vector<Comm*> g_comms;
+
+Comm* get(int64_t h) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(h >= 0 && h < (int64_t)g_comms.size() && g_comms[h] != nullptr, "rccl_comm: bad handle ", h);
+  return g_comms[h];
+}
+
+ncclDataType_t dtype_of(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    case at::kChar: return ncclInt8;
+    default: TORCH_CHECK(false, "rccl_comm: unsupported dtype ", t.scalar_type());
+  }
+}
+
+ncclRedOp_t op_of(int64_t op) {
+  switch (op) {
+    case 0: return ncclSum;
+    case 1: return ncclProd;
+    case 2: return ncclMax;
+    case 3: return ncclMin;
+    case 4: return ncclAvg;
+    default: TORCH_CHECK(false, "rccl_comm: reduce op must be 0 sum, 1 prod, 2 max, 3 min, 4 avg");
+  }
+}
+
+void check_dev(const Comm* c, const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.get_device() == c->device && t.is_contiguous(), what,
+              ": expected a contiguous tensor on the communicator's device ", c->device);
+}
+
+}  // namespace
+
+// 128-byte ncclUniqueId drawn on this rank (rank 0 shares it with the others).
+at::Tensor rccl_unique_id() {
+  ncclUniqueId id;
+  check(rccl().get_unique_id(&id), "ncclGetUniqueId");
+  auto t = at::empty({(int64_t)sizeof(id)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &id, sizeof(id));
+  return t;
+}
+
+// Collective over the `world` ranks that pass the same id. Returns a handle.
+int64_t rccl_comm_init(const at::Tensor& uid, int64_t rank, int64_t world, int64_t device) {
+  TORCH_CHECK(uid.device().is_cpu() && uid.dtype() == at::kByte && uid.numel() == (int64_t)sizeof(ncclUniqueId),
+              "rccl_comm_init: uid must be the CPU uint8[128] from rccl_unique_id");
+  TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rccl_comm_init: bad rank / world");
+  ncclUniqueId id;
+  std::memcpy(&id, uid.contiguous().data_ptr(), sizeof(id));
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  auto* c = new Comm();
+  c->rank = (int)rank;
+  c->world = (int)world;
+  c->device = (int)device;
+  const ncclResult_t e = rccl().init_rank(&c->comm, (int)world, id, (int)rank);
+  if (e != ncclSuccess) {
+    delete c;
+    check(e, "ncclCommInitRank");
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms.push_back(c);
+  return (int64_t)g_comms.size() - 1;
+}
+
+// ncclComm_t as an integer (for the health monitor's async-error polling, HealthMonitor.attach_rccl).
+int64_t rccl_comm_ptr(int64_t h) { return (int64_t)(uintptr_t)get(h)->comm; }
+
+std::string rccl_library_path() { return rccl().path; }
+
+// ---- collectives: enqueued on the current HIP stream (capturable into a HIP graph) ----
+void rccl_all_reduce_(int64_t h, at::Tensor& t, int64_t op) {
+  Comm* c = get(h);
+  check_dev(c, t, "rccl_all_reduce_");
+  if (t.numel() == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  check(rccl().all_reduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), op_of(op), c->comm, stream),
+        "ncclAllReduce");
+}
+
+// out = concatenation over ranks of `in` (out may alias in at rank offset: in-place all-gather).
+void rccl_all_gather(int64_t h, at::Tensor& out, const at::Tensor& in) {
+  Comm* c = get(h);
+  check_dev(c, out, "rccl_all_gather: out");
+  check_dev(c, in, "rccl_all_gather: in");
+  TORCH_CHECK(out.scalar_type() == in.scalar_type() && out.numel() == in.numel() * c->world,
+              "rccl_all_gather: out must hold world x in elements of in's dtype");
+  if (in.numel() == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  check(rccl().all_gather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), dtype_of(in), c->comm, stream),
+        "ncclAllGather");
+}
+
+// out = this rank's block of the reduction over ranks of `in` (world x out elements).
+void rccl_reduce_scatter(int64_t h, at::Tensor& out, const at::Tensor& in, int64_t op) {
+  Comm* c = get(h);
+  check_dev(c, out, "rccl_reduce_scatter: out");
+  check_dev(c, in, "rccl_reduce_scatter: in");
+  TORCH_CHECK(out.scalar_type() == in.scalar_type() && in.numel() == out.numel() * c->world,
+              "rccl_reduce_scatter: in must hold world x out elements of out's dtype");
+  if (out.numel() == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  check(rccl().reduce_scatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), dtype_of(out), op_of(op), c->comm,
+                              stream),
+        "ncclReduceScatter");
+}
+
+void rccl_broadcast_(int64_t h, at::Tensor& t, int64_t root) {
+  Comm* c = get(h);
+  check_dev(c, t, "rccl_broadcast_");
+  TORCH_CHECK(root >= 0 && root < c->world, "rccl_broadcast_: bad root");
+  if (t.numel() == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  check(rccl().broadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), (int)root, c->comm, stream),
+        "ncclBroadcast");
+}
+
+// Several all-reduces as one RCCL group (one launch for a list of buckets).
+void rccl_all_reduce_many_(int64_t h, at::TensorList ts, int64_t op) {
+  Comm* c = get(h);
+  for (const auto& t : ts) check_dev(c, t, "rccl_all_reduce_many_");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  Rccl& r = rccl();
+  check(r.group_start(), "ncclGroupStart");
+  for (const auto& t : ts)
+    if (t.numel() > 0)
+      check(r.all_reduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), op_of(op), c->comm, stream),
+            "ncclAllReduce");
+  check(r.group_end(), "ncclGroupEnd");
+}
+
+// 0 healthy, else the ncclResult_t of an asynchronous failure of the communicator.
+int64_t rccl_async_error(int64_t h) {
+  Comm* c = get(h);
+  if (rccl().async_error == nullptr) return 0;
+  ncclResult_t e = ncclSuccess;
+  check(rccl().async_error(c->comm, &e), "ncclCommGetAsyncError");
+  return e == ncclInProgress ? 0 : (int64_t)e;
+}
+
+void rccl_comm_destroy(int64_t h, bool abort) {
+  Comm* c = get(h);
+  {
+    c10::hip::HIPGuard guard((c10::DeviceIndex)c->device);
+    if (abort && rccl().abort != nullptr) (void)rccl().abort(c->comm);
+    else (void)rccl().destroy(c->comm);
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms[h] = nullptr;
+  delete c;
+}
+
+}  // namespace mihvd
+
+TORCH_LIBRARY_FRAGMENT(mihvd, m) {
+  m.def("rccl_unique_id() -> Tensor", &mihvd::rccl_unique_id);
+  m.def("rccl_comm_init(Tensor uid, int rank, int world, int device) -> int", &mihvd::rccl_comm_init);
+  m.def("rccl_comm_ptr(int comm) -> int", &mihvd::rccl_comm_ptr);
+  m.def("rccl_library_path() -> str", &mihvd::rccl_library_path);
+  m.def("rccl_all_reduce_(int comm, Tensor(a!) t, int op=0) -> ()", &mihvd::rccl_all_reduce_);
+  m.def("rccl_all_gather(int comm, Tensor(a!) out, Tensor input) -> ()", &mihvd::rccl_all_gather);
+  m.def("rccl_reduce_scatter(int comm, Tensor(a!) out, Tensor input, int op=0) -> ()", &mihvd::rccl_reduce_scatter);
+  m.def("rccl_broadcast_(int comm, Tensor(a!) t, int root=0) -> ()", &mihvd::rccl_broadcast_);
+  m.def("rccl_all_reduce_many_(int comm, Tensor(a!)[] ts, int op=0) -> ()", &mihvd::rccl_all_reduce_many_);
+  m.def("rccl_async_error(int comm) -> int", &mihvd::rccl_async_error);
+  m.def("rccl_comm_destroy(int comm, bool abort=False) -> ()", &mihvd::rccl_comm_destroy);
+}

@@ -252,6 +252,10 @@ class FusedMNISTTrainer:
         # (default: one per CU)
         self.f32_fused_opt = self.f32 and os.environ.get("MIHVD_FUSED_OPT", "1") != "0"
         self.f32_tail_blocks = int(os.environ.get("MIHVD_F32_TAIL_BLOCKS", "0"))
+        # where dense/kernel's fused Adam update runs (world size 1): "side" = on the side stream
+        # concurrently with the MFMA-bound conv backward of the same step (HBM-bound next to
+        # MFMA-bound: they share the CUs), "tail" = deferred into tail blocks of the next conv2_fwd
+        self.f32_w3 = os.environ.get("MIHVD_F32_W3", "side")
         self._w3_pending = False
         if self.f32:
             ops = self.ops
@@ -331,7 +335,7 @@ class FusedMNISTTrainer:
             self.a2T = torch.zeros(3136, 128, **bf)
             self.dzT = torch.zeros(1024, 128, **bf)
         self._fc_update_pending = False
-        self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline) else None
+        self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline or self.f32) else None
         if compression == "bf16" and self.collectives:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
         else:
@@ -580,10 +584,18 @@ class FusedMNISTTrainer:
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
                       G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
         overlap = self.collectives and self.overlap
+        w3_side = self.f32_fused_opt and not self.collectives and self.f32_w3 == "side"
         if overlap:
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
                 self._allreduce(self.grads[FC_START:], FC_START, FLAT_NUMEL)
+        elif w3_side:
+            # dense/kernel's Adam (98 % of the optimizer's bytes, HBM-bound) runs beside the
+            # MFMA-bound conv backward; the step's end joins it
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                o.adam_step(self.params[s3], self.grads[s3], self.m[s3], self.v[s3], None, st, 0, self.lr, b1, b2,
+                            self.eps, 1.0, self.rule, 0)
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab)
         gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
                  G("conv_layer2/conv2d/bias"))
@@ -603,7 +615,9 @@ class FusedMNISTTrainer:
             hi = W3_START if self.f32_fused_opt else FLAT_NUMEL
             o.adam_step(self.params[:hi], self.grads[:hi], self.m[:hi], self.v[:hi], None, st, 0, self.lr, b1, b2,
                         self.eps, 1.0 / self.world, self.rule, 1)
-        if self.f32_fused_opt:
+        if w3_side:
+            main.wait_stream(self._side)
+        elif self.f32_fused_opt:
             # dense/kernel's update is deferred into the next step's conv2_fwd launch (or applied by
             # _flush_w3 when no step follows: end of an eager step or of a captured graph)
             self._w3_pending = True

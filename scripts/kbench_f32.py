@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="comma-separated entries: run each --eager times, eagerly "
+                    "(for counter collection), and exit")
+    ap.add_argument("--eager", type=int, default=20)
     args = ap.parse_args()
     from mihvd.models.fused_mnist import FC_START, FLAT_NUMEL, SEGMENTS, W3_START, FusedMNISTTrainer
     from mihvd.utils.data import synthetic_mnist
@@ -91,13 +94,49 @@ def main():
         "adam_step (W3)": lambda: o.adam_step(tr.params[s3], tr.grads[s3], tr.m[s3], tr.v[s3], None, st, 0, 0.0, b1,
                                               b2, tr.eps, 1.0, tr.rule, 0),
     }
+    study_env = {"dg": {"MIHVD_F32_C2B_ROLE": "1"}, "wg": {"MIHVD_F32_C2B_ROLE": "2"},
+                 "fdg": {"MIHVD_F32_F1B_ROLE": "1"}, "fwg": {"MIHVD_F32_F1B_ROLE": "2"}}
+    if args.only:
+        for item in args.only.split(","):
+            name, _, variant = item.partition(":")
+            os.environ.update(study_env.get(variant, {}))
+            for _ in range(args.eager):
+                ks[name]()
+            torch.cuda.synchronize()
+            for k in study_env.get(variant, {}):
+                os.environ.pop(k, None)
+        return
     res = {}
     for name, fn in ks.items():
         res[name] = timed(fn, args.reps)
+    # study variants (host knobs read at capture time, csrc/kernels/f32_*.hip): placement and roles
+    study = {
+        "conv2_fwd [LDS 96 KB: 1 block/CU]": ({"MIHVD_F32_C2F_LDS": "98304"}, ks["conv2_fwd"]),
+        "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
+        "conv2_bwd [wgrad role only]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd"]),
+        "fc1_bwd [dgrad role only]": ({"MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
+        "fc1_bwd [wgrad role only]": ({"MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
+    }
+    for name, (env, fn) in study.items():
+        old_env = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            res[name] = timed(fn, args.reps)
+        finally:
+            for k, v in old_env.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     saved = tr.lr
     tr.lr = 0.0
     res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
     tr._join()
+    mode = tr.f32_w3
+    tr.f32_w3 = "tail" if mode == "side" else "side"
+    res[f"whole step [dense/kernel Adam: {tr.f32_w3}]"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
+    tr._join()
+    tr.f32_w3 = mode
     tr.lr = saved
     width = max(len(k) for k in res)
     for k, v in res.items():

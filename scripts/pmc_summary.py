@@ -1,24 +1,43 @@
 #!/usr/bin/env python3
-"""Average rocprofv3 PMC counters per mihvd kernel from the CSVs written by pmc_bench.sh."""
+"""Median per-dispatch PMC values per kernel (and study variant) from rocprofv3 --pmc CSV dirs.
+
+    python scripts/pmc_summary.py gpurun_out/pmcA gpurun_out/pmcB ...
+"""
 import collections
 import csv
 import glob
+import os
 import sys
 
-out = sys.argv[1]
-acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        name = r.get("Kernel_Name", "").split("(")[0]
-        grid = r.get("Grid_Size") or r.get("Grid_Size_X")
-        if grid:
-            name += "/g" + grid
-        if "mihvd" not in name:
+
+def load(d):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            key = (r["Kernel_Name"].split("(")[0][-44:], r["Grid_Size"])
+            out[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    agg = collections.defaultdict(dict)
+    for d in sys.argv[1:]:
+        for k, cs in load(d).items():
+            for c, v in cs.items():
+                agg[k][c] = sorted(v)[len(v) // 2]
+    for (name, grid), cs in sorted(agg.items()):
+        if "mihvd" not in name and "f32" not in name:
             continue
-        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-cols = sys.argv[2:] or ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
-        "SQ_LDS_BANK_CONFLICT", "FETCH_SIZE", "TCC_HIT_sum", "GRBM_GUI_ACTIVE"]
-print("%-28s" % "kernel" + "".join("%14s" % c.replace("SQ_", "")[:13] for c in cols))
-for k, d in sorted(acc.items()):
-    print("%-28s" % k.replace("mihvd::", "")[:28] + "".join(
-        "%14.0f" % (sum(d[c]) / len(d[c])) if d.get(c) else "%14s" % "-" for c in cols))
+        wc = cs.get("SQ_WAVE_CYCLES")
+        line = f"{name:44s} grid {grid:>7s}"
+        if wc:
+            line += (f" | wait {cs['SQ_WAIT_ANY'] / wc:.2f} waitInst {cs['SQ_WAIT_INST_ANY'] / wc:.2f}"
+                     f" active {cs['SQ_ACTIVE_INST_ANY'] / wc:.2f} waitLDS {cs['SQ_WAIT_INST_LDS'] / wc:.2f}")
+        rest = {c: v for c, v in cs.items() if c not in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                                          "SQ_WAIT_INST_LDS")}
+        line += " | " + " ".join(f"{c.replace('SQ_', '')}={v:.3g}" for c, v in sorted(rest.items()))
+        print(line)
+
+
+if __name__ == "__main__":
+    main()

@@ -272,16 +272,19 @@ def test_f32_graph_replay_converges(ops):
     assert tr.last_accuracy() > 0.8
 
 
-def test_f32_fused_optimizer_matches_separate_adam(ops, monkeypatch):
-    """MIHVD_FUSED_OPT=1 (small-parameter Adam inside the reduction launch, dense/kernel's update
-    deferred into the next step's conv2_fwd tail blocks, flushed at the end of each graph / eager
-    step) is bitwise equal to a separate adam_step after every step, graph-replayed and eager."""
+@pytest.mark.parametrize("w3_mode", ["side", "tail"])
+def test_f32_fused_optimizer_matches_separate_adam(ops, monkeypatch, w3_mode):
+    """MIHVD_FUSED_OPT=1 (small-parameter Adam inside the reduction launch; dense/kernel's update
+    on the side stream beside the conv backward, or deferred into the next step's conv2_fwd tail
+    blocks and flushed at the end of each graph / eager step) is bitwise equal to a separate
+    adam_step after every step, graph-replayed and eager."""
     from mihvd.models.fused_mnist import FusedMNISTTrainer
     from mihvd.utils.data import synthetic_mnist
 
     (x, y), _ = synthetic_mnist(n_train=2000, n_test=10, seed=6)
     X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
     Y = torch.from_numpy(y.astype("int64")).cuda()
+    monkeypatch.setenv("MIHVD_F32_W3", w3_mode)
     trs = []
     for fused in ("1", "0"):
         monkeypatch.setenv("MIHVD_FUSED_OPT", fused)
