@@ -302,19 +302,6 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
         dY2 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 64 + ch * 4);
     iv[it] = mask_f4(v, in);
   }
-  float xv[4];
-#pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int i = t + 512 * it, s = i >> 10, pix = i & 1023, Y = (pix >> 5) - 2, X = (pix & 31) - 2;
-    const int bb = min(b0 + s, B - 1);
-    int row = bb;
-    if (rows != nullptr) {
-      const int64_t step = state ? state[ST_FWD] : 0;
-      row = rows[(int)((step * (int64_t)B + bb) % n_pool)];
-    }
-    const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
-    xv[it] = mask_f(x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
-  }
   // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3]
   const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
   float4 wb[25];
@@ -328,8 +315,6 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
       *reinterpret_cast<float4*>(dimg + (rr * 18 + (rem >> 4)) * CBF_PS + (rem & 15) * 4) = iv[it];
     }
   }
-#pragma unroll
-  for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
   int abase[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) {
@@ -340,7 +325,22 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   f32x4 acc[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();  // the images are complete; no barrier in the tap loop
+  __syncthreads();  // the dY2 image is complete; no barrier in the tap loop
+  // the x patches are needed only by the epilogue: their gather (state -> rows -> x, three
+  // dependent loads) is issued here and lands during the tap loop instead of before the barrier
+  float xv[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int i = t + 512 * it, s = i >> 10, pix = i & 1023, Y = (pix >> 5) - 2, X = (pix & 31) - 2;
+    const int bb = min(b0 + s, B - 1);
+    int row = bb;
+    if (rows != nullptr) {
+      const int64_t step = state ? state[ST_FWD] : 0;
+      row = rows[(int)((step * (int64_t)B + bb) % n_pool)];
+    }
+    const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
+    xv[it] = mask_f(x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
+  }
 #pragma unroll
   for (int tap = 0; tap < 25; ++tap) {  // fully unrolled: constant LDS offsets, static register indices
     const int kh = tap / 5, kw = tap - 5 * kh;
@@ -358,7 +358,9 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
     for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].w, wb[tap].w, acc[i]);
   }
-  __syncthreads();  // every wave is done with the dY2 image
+#pragma unroll
+  for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
+  __syncthreads();  // every wave is done with the dY2 image; the x images are complete
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
 #pragma unroll

@@ -98,8 +98,9 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
 // M = the 49 B pooling windows of the batch x 4 pixels (pool-window-major), in 16-row tiles; block
 // b owns tiles [b TPB, (b+1) TPB) (TPB = ceil(tiles / 256): about one block per CU), which span at
 // most two images. The a1 rows those tiles read are staged once as rows of the "tall" padded image
-// (image i = tall rows [18 i, 18 i + 18), padded row r = a1 row r - 2, 18 padded columns, pixel
-// stride 36 floats). 4 waves, one per SIMD; wave w owns output channels 16w..16w+15.
+// (image i = tall rows [18 i, 18 i + 18), padded row r = a1 row r - 2, 18 padded columns of a
+// 24-pixel row, pixel stride 36 floats). 4 waves, one per SIMD; wave w owns output channels
+// 16w..16w+15.
 //
 // Weights stay in registers: a wave's whole B operand (W2[tap][ci][16w..16w+15], 800 k x 16 co =
 // 200 floats per lane) is loaded once, so the MFMA loop has no global load and no barrier; only
@@ -108,8 +109,11 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
 // dependent latency), the 25 taps fully unrolled (constant LDS offsets, static register indices).
 // Epilogue: 2x2 max-pool + argmax + bias + ReLU in registers.
 // ------------------------------------------------------------------------------------------ //
-constexpr int C2F_PS = 36, C2F_RS = 18 * C2F_PS, C2F_MAXR = 22;
-constexpr int C2F_LDS = C2F_MAXR * C2F_RS * 4;                     // 57,024 B
+// pixel stride 36 floats, 24 pixels per tall row (18 used): a tile's 16 rows (4 windows x 2x2
+// pixels: pixel offsets 2w + 24 dy + dx) then fall on 16 distinct 16-byte bank groups, so its
+// ds_read_b128 is conflict-free (with 18 pixels per row the 2x2 windows alias pairwise)
+constexpr int C2F_PS = 36, C2F_RW = 24, C2F_RS = C2F_RW * C2F_PS, C2F_MAXR = 22;
+constexpr int C2F_LDS = C2F_MAXR * C2F_RS * 4;                     // 76,032 B
 constexpr int C2F_MAXCH = (C2F_MAXR * 18 * 8 + 255) / 256;         // image float4 chunks per thread
 
 // A row (tall-image offset) of lane row lr of tile `tile` (clamped past the batch)
@@ -118,7 +122,7 @@ __device__ __forceinline__ int c2f_abase(int tile, int lr, int lg, int nwin, int
   const int gw = min(m >> 2, nwin - 1), d = m & 3;
   const int bb = gw / 49, win = gw - 49 * bb, py = win / 7, px = win - 7 * py;
   const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
-  return ((18 * bb + y - R0) * 18 + xx) * C2F_PS + 4 * lg;
+  return ((18 * bb + y - R0) * C2F_RW + xx) * C2F_PS + 4 * lg;
 }
 
 // NT (1 or 2) tiles against the register-resident weights: acc[u] += A(tile u) x W2
@@ -127,7 +131,7 @@ __device__ __forceinline__ void c2f_tiles(const float* img, const int (&ab)[2], 
                                           f32x4 (&acc)[2]) {
 #pragma unroll
   for (int tap = 0; tap < 25; ++tap) {
-    const int kh = tap / 5, kw = tap - 5 * kh, aoff = (kh * 18 + kw) * C2F_PS;
+    const int kh = tap / 5, kw = tap - 5 * kh, aoff = (kh * C2F_RW + kw) * C2F_PS;
 #pragma unroll
     for (int c2 = 0; c2 < 2; ++c2) {
       float4 a[NT];
@@ -149,7 +153,7 @@ __device__ __forceinline__ void c2f_tiles(const float* img, const int (&ab)[2], 
 // TAIL: the first ad.nblk blocks of the launch stream an Adam update instead (the previous step's
 // dense/kernel update, deferred into this MFMA-bound launch, which leaves HBM idle). They are first
 // in dispatch order, so they take the CUs before the conv blocks; a tail block and a conv block fit
-// one CU together (2 x 57 KB of LDS, 4 + 4 waves).
+// one CU together when registers allow (2 x 76 KB of LDS).
 template <int TPB, bool TAIL>
 __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, float* __restrict__ a2,
@@ -194,7 +198,7 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
     const int i = t + 256 * it;
     if (i < nch) {
       const int rr = i / 144, rem = i - rr * 144;
-      *reinterpret_cast<float4*>(img + (rr * 18 + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
+      *reinterpret_cast<float4*>(img + (rr * C2F_RW + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
     }
   }
   __syncthreads();  // the image is complete; no barrier below
@@ -234,38 +238,91 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
 constexpr int F1F_KS = 14, F1F_KSL = 224, F1F_AS = 228;
 constexpr int F1F_LDS = 128 * F1F_AS * 4;  // 116,736 B
 
-template <int MT>
-__global__ void __launch_bounds__(512) f32_fc1_fwd_kernel(const float* __restrict__ a2, const float* __restrict__ w3,
-                                                          float* __restrict__ zpart, int B) {
+// ADAM: dense/kernel's deferred Adam update (the previous step's gradient) is applied here, where
+// W3 is read anyway (one read of p instead of two): the block first streams Adam over its
+// [224 k][64 n] tile of W3 with coalesced float4 accesses (p, g, m, v in; p, m, v out), keeps the
+// new tile in LDS and takes the MFMA fragments from there. Every W3 element belongs to exactly one
+// block. LDS: the a2 slice + the tile, so MT <= 7 (B <= 112).
+constexpr int F1F_WS = 64;                          // W3 tile row stride in LDS (floats)
+constexpr int F1F_LDS_ADAM = 7 * 16 * F1F_AS * 4 + F1F_KSL * F1F_WS * 4;   // 159,488 B
+
+template <int MT, bool ADAM>
+__global__ void __launch_bounds__(512) f32_fc1_fwd_kernel(const float* __restrict__ a2, float* __restrict__ w3,
+                                                          float* __restrict__ zpart, int B, F32Adam ad) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   float* As = smf;  // [16 MT][228]: rows = samples, k contiguous
   const int nb = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int k0 = ks * F1F_KSL, nt = wave & 3, sh = wave >> 2;
   const int n = nb * 64 + nt * 16 + lr;
-  // A fragments: wa[4q + j] = W3[k0 + 16q + 4lg + j][n]
-  float wa[56];
-  const float* wp = w3 + (int64_t)(k0 + 4 * lg) * 1024 + n;
-#pragma unroll
-  for (int q = 0; q < 14; ++q)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wa[4 * q + j] = wp[(16 * q + j) * 1024];
   constexpr int NCH = MT * 16 * 56, PER = (NCH + 511) / 512;
-  float4 v[PER];
+  float wa[56];  // A fragments: wa[4q + j] = W3[k0 + 16q + 4lg + j][n]
+  const int64_t wo = (int64_t)(k0 + 4 * lg) * 1024 + n;
+  if constexpr (ADAM) {
+    static_assert(MT <= 7, "the fused update needs the a2 slice and the W3 tile in LDS");
+    float* Ws = smf + 7 * 16 * F1F_AS;  // [224][64]: the updated tile
+    const AdamCoef c = f32_adam_coef(ad);
+    // tile float4 i (0..3583): row i >> 4, float4 column i & 15; 7 per thread, all 28 loads in flight
+    float4 pv[7], gv[7], mv[7], vv[7];
 #pragma unroll
-  for (int it = 0; it < PER; ++it) {
-    const int i = min(t + 512 * it, NCH - 1), r = i / 56, c = i - 56 * r;
-    v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * c), r < B);
-  }
-#pragma unroll
-  for (int it = 0; it < PER; ++it) {
-    const int i = t + 512 * it;
-    if (i < NCH) {
-      const int r = i / 56, c = i - 56 * r;
-      *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * c) = v[it];
+    for (int u = 0; u < 7; ++u) {
+      const int i = t + 512 * u;
+      const int64_t o = (int64_t)(k0 + (i >> 4)) * 1024 + nb * 64 + 4 * (i & 15);
+      pv[u] = *reinterpret_cast<const float4*>(w3 + o);
+      gv[u] = *reinterpret_cast<const float4*>(ad.g + o);
+      mv[u] = *reinterpret_cast<const float4*>(ad.m + o);
+      vv[u] = *reinterpret_cast<const float4*>(ad.v + o);
     }
+    float4 v[PER];
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = min(t + 512 * it, NCH - 1), r = i / 56, cc = i - 56 * r;
+      v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc), r < B);
+    }
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      const int i = t + 512 * u;
+      const int64_t o = (int64_t)(k0 + (i >> 4)) * 1024 + nb * 64 + 4 * (i & 15);
+      adam4_f32(pv[u], mv[u], vv[u], gv[u], c);
+      *reinterpret_cast<float4*>(w3 + o) = pv[u];
+      *reinterpret_cast<float4*>(ad.m + o) = mv[u];
+      *reinterpret_cast<float4*>(ad.v + o) = vv[u];
+      *reinterpret_cast<float4*>(Ws + (i >> 4) * F1F_WS + 4 * (i & 15)) = pv[u];
+    }
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = t + 512 * it;
+      if (i < NCH) {
+        const int r = i / 56, cc = i - 56 * r;
+        *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 14; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wa[4 * q + j] = Ws[(16 * q + 4 * lg + j) * F1F_WS + nt * 16 + lr];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 14; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wa[4 * q + j] = w3[wo + (16 * q + j) * 1024];
+    float4 v[PER];
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = min(t + 512 * it, NCH - 1), r = i / 56, cc = i - 56 * r;
+      v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc), r < B);
+    }
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = t + 512 * it;
+      if (i < NCH) {
+        const int r = i / 56, cc = i - 56 * r;
+        *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int tt = sh; tt < MT; tt += 2) {  // wave-uniform
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
     const float* bp = As + (tt * 16 + lr) * F1F_AS + 4 * lg;
@@ -508,30 +565,43 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
 #undef C2F_CASE
 }
 
-void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) {
+void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const c10::optional<at::Tensor>& g3,
+                 const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
+                 const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
+                 double grad_scale, int64_t rule) {
   const int B = a2.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_fwd: batch 1..128");
   check_f32(a2, (int64_t)B * 3136, "f32_fc1_fwd: a2");
   check_f32(w3, 3136 * 1024, "f32_fc1_fwd: w3");
   check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_fc1_fwd: zpart [14][B][1024]");
+  const c10::optional<at::Tensor> p3 = g3.has_value() && g3->defined() ? c10::optional<at::Tensor>(w3) : c10::nullopt;
+  const F32Adam ad = f32_adam_args(p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule, 1, "f32_fc1_fwd");
   const int mt = (B + 15) / 16;
+  TORCH_CHECK(ad.nblk == 0 || mt <= 7, "f32_fc1_fwd: the fused dense/kernel update needs B <= 112");
   auto stream = c10::hip::getCurrentHIPStream().stream();
   auto launch = [&](auto kern) {
-    const int lds = mt * 16 * F1F_AS * 4;
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1F_LDS);
+    const int lds = ad.nblk > 0 ? F1F_LDS_ADAM : mt * 16 * F1F_AS * 4;
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<dim3(16, F1F_KS), 512, lds, stream>>>(a2.data_ptr<float>(), w3.data_ptr<float>(), zpart.data_ptr<float>(),
-                                                 B);
+                                                 B, ad);
   };
+#define F1F_CASE(T)                                           \
+  case T:                                                     \
+    if (ad.nblk > 0) launch(f32_fc1_fwd_kernel<T, true>);     \
+    else launch(f32_fc1_fwd_kernel<T, false>);                \
+    break;
   switch (mt) {
-    case 1: launch(f32_fc1_fwd_kernel<1>); break;
-    case 2: launch(f32_fc1_fwd_kernel<2>); break;
-    case 3: launch(f32_fc1_fwd_kernel<3>); break;
-    case 4: launch(f32_fc1_fwd_kernel<4>); break;
-    case 5: launch(f32_fc1_fwd_kernel<5>); break;
-    case 6: launch(f32_fc1_fwd_kernel<6>); break;
-    case 7: launch(f32_fc1_fwd_kernel<7>); break;
-    default: launch(f32_fc1_fwd_kernel<8>); break;
+    F1F_CASE(1)
+    F1F_CASE(2)
+    F1F_CASE(3)
+    F1F_CASE(4)
+    F1F_CASE(5)
+    F1F_CASE(6)
+    F1F_CASE(7)
+    default:
+      launch(f32_fc1_fwd_kernel<8, false>);
   }
+#undef F1F_CASE
 }
 
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,

@@ -90,7 +90,10 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
                    const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
                    const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
                    double grad_scale, int64_t rule, int64_t tail_blocks);
-void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
+void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const c10::optional<at::Tensor>& g3,
+                 const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
+                 const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
+                 double grad_scale, int64_t rule);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
@@ -234,7 +237,11 @@ void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a
   mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule,
                        tail_blocks);
 }
-void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
+void f32_fc1_fwd_op(const Tensor& a2, Tensor w3, Tensor zpart, const OptT& g3, const OptT& m3, const OptT& v3,
+                    const OptT& state, double lr, double beta1, double beta2, double eps, double grad_scale,
+                    int64_t rule) {
+  mihvd::f32_fc1_fwd(a2, w3, zpart, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule);
+}
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
                  Tensor stats) {
@@ -308,7 +315,9 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor(c!)? p3=None, "
         "Tensor? g3=None, Tensor(d!)? m3=None, Tensor(e!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., "
         "float beta2=0., float eps=0., float grad_scale=1., int rule=0, int tail_blocks=0) -> ()");
-  m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
+  m.def("f32_fc1_fwd(Tensor a2, Tensor(w!) w3, Tensor(a!) zpart, Tensor? g3=None, Tensor(m!)? m3=None, "
+        "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
+        "float grad_scale=1., int rule=0) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
   m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor w3, Tensor(a!) dY2, "

@@ -103,6 +103,7 @@ PYBIND11_MODULE(_mihvd_runtime, m) {
   py::class_<HealthMonitor>(m, "HealthMonitor")
       .def(py::init<int, double, int>(), py::arg("rank") = 0, py::arg("poll_s") = 0.5, py::arg("exit_code") = 134)
       .def("attach_rccl", &HealthMonitor::attach_rccl, py::arg("comm"), py::arg("lib_path"))
+      .def("detach_rccl", &HealthMonitor::detach_rccl, py::arg("comm"))
       .def("inject_error", &HealthMonitor::inject_error, py::arg("code"), py::arg("what") = "test")
       .def("watch_word", &HealthMonitor::watch_word, py::arg("addr"), py::arg("label"))
       .def("unwatch_word", &HealthMonitor::unwatch_word, py::arg("addr"))

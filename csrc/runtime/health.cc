@@ -73,6 +73,15 @@ bool HealthMonitor::attach_rccl(uintptr_t comm, const std::string& lib_path) {
   return true;
 }
 
+void HealthMonitor::detach_rccl(uintptr_t comm) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (size_t i = 0; i < comms_.size(); ++i)
+    if (comms_[i] == reinterpret_cast<void*>(comm)) {
+      comms_.erase(comms_.begin() + (ptrdiff_t)i);
+      return;
+    }
+}
+
 void HealthMonitor::inject_error(int code, const std::string& what) {
   std::lock_guard<std::mutex> lk(mu_);
   injected_ = code;

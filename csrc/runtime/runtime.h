@@ -202,6 +202,7 @@ class HealthMonitor {
   // Attach an RCCL communicator (ncclComm_t as an integer) created by the library at lib_path
   // (already loaded by the process). False if the library or its symbols are unavailable.
   bool attach_rccl(uintptr_t comm, const std::string& lib_path);
+  void detach_rccl(uintptr_t comm);  // before the communicator is destroyed
   void inject_error(int code, const std::string& what);  // test hook (MIHVD_FAULT collerr)
   // Watch a 32-bit error word in host-visible memory (e.g. the xGMI plane's host-mapped timeout
   // mirror, csrc/kernels/xgmi.hip): nonzero is a collective failure like an RCCL async error.

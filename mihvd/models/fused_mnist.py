@@ -135,6 +135,17 @@ class FusedMNISTTrainer:
         self.world = int(world_size)
         # MIHVD_FORCE_COLLECTIVES=1 keeps the allreduce path even at size 1 (tests of the RCCL path)
         self.collectives = self.world > 1 or os.environ.get("MIHVD_FORCE_COLLECTIVES") == "1"
+        # MIHVD_COMM=native: the step's collectives go through a framework-owned RCCL communicator
+        # (mihvd/parallel/rccl.py) instead of the process group's
+        self.ncomm = None
+        if self.collectives:
+            from ..parallel import rccl as _rccl
+
+            if _rccl.env_mode() == "native":
+                import torch.distributed as dist
+
+                if dist.is_initialized() and dist.get_backend() == "nccl":
+                    self.ncomm = _rccl.NativeComm(device=self.device)
         self.rank = basics.rank() if basics.is_initialized() else 0
         self.op = op
         self.compression = compression
@@ -252,10 +263,14 @@ class FusedMNISTTrainer:
         # (default: one per CU)
         self.f32_fused_opt = self.f32 and os.environ.get("MIHVD_FUSED_OPT", "1") != "0"
         self.f32_tail_blocks = int(os.environ.get("MIHVD_F32_TAIL_BLOCKS", "0"))
-        # where dense/kernel's fused Adam update runs (world size 1): "side" = on the side stream
-        # concurrently with the MFMA-bound conv backward of the same step (HBM-bound next to
-        # MFMA-bound: they share the CUs), "tail" = deferred into tail blocks of the next conv2_fwd
-        self.f32_w3 = os.environ.get("MIHVD_F32_W3", "side")
+        # where dense/kernel's fused Adam update runs: "fc1" = deferred into the next step's fc1_fwd,
+        # which reads W3 anyway (each lane updates the fragment it multiplies with: one read of p
+        # instead of two); "tail" = deferred into tail blocks of the next conv2_fwd; "side" = on the
+        # side stream beside the conv backward of the same step (world size 1 only; the cross-queue
+        # join of a captured graph costs more than it hides here)
+        self.f32_w3 = os.environ.get("MIHVD_F32_W3", "fc1")
+        if self.f32_w3 == "fc1" and B > 112:  # the fused update keeps the a2 slice + a W3 tile in LDS
+            self.f32_w3 = "tail"
         self._w3_pending = False
         if self.f32:
             ops = self.ops
@@ -569,7 +584,7 @@ class FusedMNISTTrainer:
         if self.shard_w3:
             return self._launch_step_f32_shard(x, rows, labels)
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1, self.idx1)
-        if self._w3_pending:
+        if self._w3_pending and self.f32_w3 == "tail":
             # the previous step's dense/kernel Adam update (98 % of the optimizer's bytes) streams in
             # tail blocks of this MFMA-bound launch; fc1_fwd below is its first reader
             o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, self.params[s3],
@@ -578,7 +593,13 @@ class FusedMNISTTrainer:
             self._w3_pending = False
         else:
             o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
-        o.f32_fc1_fwd(self.a2, w3, self.zpart)
+        if self._w3_pending:
+            # ... or inside fc1_fwd, W3's first reader: the update of each fragment in registers
+            o.f32_fc1_fwd(self.a2, w3, self.zpart, self.grads[s3], self.m[s3], self.v[s3], st, self.lr, b1, b2,
+                          self.eps, 1.0 / self.world, self.rule)
+            self._w3_pending = False
+        else:
+            o.f32_fc1_fwd(self.a2, w3, self.zpart)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
@@ -678,7 +699,9 @@ class FusedMNISTTrainer:
         """out = this rank's R rows of the sum over ranks of ``full`` (rows x 1024)."""
         import torch.distributed as dist
 
-        if dist.get_backend() == "nccl":
+        if self.ncomm is not None:
+            self.ncomm.reduce_scatter(out, full.view(self.world * R, -1))
+        elif dist.get_backend() == "nccl":
             dist.reduce_scatter_tensor(out, full.view(self.world * R, -1))
         else:  # gloo has no reduce-scatter: allreduce in place, keep this rank's rows
             dist.all_reduce(full)
@@ -870,7 +893,9 @@ class FusedMNISTTrainer:
     def _all_gather_rows(self, full, mine):
         import torch.distributed as dist
 
-        if dist.get_backend() == "nccl":
+        if self.ncomm is not None:
+            self.ncomm.all_gather_into(full, mine)
+        elif dist.get_backend() == "nccl":
             dist.all_gather_into_tensor(full, mine)  # in place: `mine` is this rank's slice of `full`
         else:
             dist.all_gather(list(full.chunk(self.world)), mine.clone())
@@ -940,13 +965,14 @@ class FusedMNISTTrainer:
             if ctx is not None:
                 ctx.allreduce_(bucket)  # sum; Adam applies the 1/size of Average
                 return
+        reduce_ = self.ncomm.all_reduce_ if self.ncomm is not None else dist.all_reduce
         if self.wire is not None:
             w = self.wire[lo:hi]
             self.ops.scale_cast_bf16(bucket, w, 1.0)
-            dist.all_reduce(w)
+            reduce_(w)
             self.ops.bf16_to_f32(w, bucket, 1.0)
         else:
-            dist.all_reduce(bucket)
+            reduce_(bucket)
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor):
         """One eager step on a host-fed batch (x: [B,784] in [0,1], y: [B] labels)."""
@@ -1372,6 +1398,9 @@ class FusedMNISTTrainer:
         if self._closed:
             return
         self._closed = True
+        if self.ncomm is not None:
+            self.ncomm.close()
+            self.ncomm = None
         ctxs = [c for c in (self.xgmi or {}).values() if c is not None]
         if self.xplane is None and not ctxs:
             return

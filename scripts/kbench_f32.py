@@ -78,6 +78,8 @@ def main():
                                                           tr.params[s3], tr.grads[s3], tr.m[s3], tr.v[s3], st, 0.0,
                                                           b1, b2, tr.eps, 1.0, tr.rule, tr.f32_tail_blocks),
         "fc1_fwd": lambda: o.f32_fc1_fwd(tr.a2, w3, tr.zpart),
+        "fc1_fwd+W3 adam": lambda: o.f32_fc1_fwd(tr.a2, w3, tr.zpart, tr.grads[s3], tr.m[s3], tr.v[s3], st, 0.0, b1,
+                                                 b2, tr.eps, 1.0, tr.rule),
         "head": lambda: o.f32_head_fwd_bwd(tr.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), tr.Y,
                                            tr.rows, st, tr.seed, tr.dropout, tr.h, tr.dz, tr.dlog, tr.stats),
         "fc1_bwd": lambda: o.f32_fc1_bwd(tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"),
@@ -133,9 +135,11 @@ def main():
     res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
     tr._join()
     mode = tr.f32_w3
-    tr.f32_w3 = "tail" if mode == "side" else "side"
-    res[f"whole step [dense/kernel Adam: {tr.f32_w3}]"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
-    tr._join()
+    for alt in ("fc1", "tail", "side"):
+        if alt != mode:
+            tr.f32_w3 = alt
+            res[f"whole step [dense/kernel Adam: {alt}]"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
+            tr._join()
     tr.f32_w3 = mode
     tr.lr = saved
     width = max(len(k) for k in res)

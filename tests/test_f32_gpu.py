@@ -272,12 +272,12 @@ def test_f32_graph_replay_converges(ops):
     assert tr.last_accuracy() > 0.8
 
 
-@pytest.mark.parametrize("w3_mode", ["side", "tail"])
+@pytest.mark.parametrize("w3_mode", ["fc1", "side", "tail"])
 def test_f32_fused_optimizer_matches_separate_adam(ops, monkeypatch, w3_mode):
     """MIHVD_FUSED_OPT=1 (small-parameter Adam inside the reduction launch; dense/kernel's update
-    on the side stream beside the conv backward, or deferred into the next step's conv2_fwd tail
-    blocks and flushed at the end of each graph / eager step) is bitwise equal to a separate
-    adam_step after every step, graph-replayed and eager."""
+    deferred into the next step's fc1_fwd or conv2_fwd tail blocks and flushed at the end of each
+    graph / eager step, or on the side stream beside the conv backward) is bitwise equal to a
+    separate adam_step after every step, graph-replayed and eager."""
     from mihvd.models.fused_mnist import FusedMNISTTrainer
     from mihvd.utils.data import synthetic_mnist
 

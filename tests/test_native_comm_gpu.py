@@ -1,0 +1,40 @@
+"""Framework-owned RCCL communicator (csrc/kernels/rccl_comm.cpp, mihvd/parallel/rccl.py) on the
+box's one GPU: every collective eagerly and replayed from a HIP graph, and the fused fp32 trainer's
+collective path over it (MIHVD_COMM=native, MIHVD_FORCE_COLLECTIVES=1) against the trainer with no
+collectives. Multi-GPU runs of it are the driver's (RCCL refuses two ranks on one GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_native_rccl_comm_one_gpu(tmp_path):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    out = tmp_path / "res.json"
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "tests", "workers", "native_comm_worker.py"),
+           str(out)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = json.loads(out.read_text())
+    assert r["world"] == 1
+    for k in ("allreduce_sum", "allreduce_avg", "allreduce_bf16", "all_gather", "reduce_scatter", "broadcast", "many"):
+        assert r[k], (k, r)
+    assert r["graph"] == 1024.0, r
+    assert r["async_error"] == 0
+    assert r["trainer_native_comm"]
+    # the same collective-free arithmetic (world-1 sums are exact): the updates agree to fp32
+    # summation order (the collective path applies the dense/kernel update in a different launch)
+    assert r["trainer_rel_diff"] < 1e-5, r
