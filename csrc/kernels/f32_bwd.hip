@@ -341,22 +341,40 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
     xv[it] = mask_f(x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
   }
-#pragma unroll
-  for (int tap = 0; tap < 25; ++tap) {  // fully unrolled: constant LDS offsets, static register indices
+  // Software pipeline, fully unrolled: the A chunks of tap t + 1 are read into the other register
+  // set before tap t's MFMAs issue; sched_barrier pins that order (left alone, the scheduler
+  // reuses one register set and waits on each read right before its MFMAs).
+  float4 ra[TPB], rb[TPB];
+  auto load_a = [&](float4 (&a)[TPB], int tap) {
     const int kh = tap / 5, kw = tap - 5 * kh;
     const int aoff = ((4 - kh) * 18 + (4 - kw)) * CBF_PS;
-    float4 a[TPB];
 #pragma unroll
     for (int i = 0; i < TPB; ++i) a[i] = *reinterpret_cast<const float4*>(dimg + abase[i] + aoff);
+  };
+  auto mfma_tap = [&](const float4 (&a)[TPB], const float4& w) {
     // k-element j outer, tiles inner: consecutive MFMAs use different accumulators
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].x, wb[tap].x, acc[i]);
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].x, w.x, acc[i]);
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].y, wb[tap].y, acc[i]);
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].y, w.y, acc[i]);
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].z, wb[tap].z, acc[i]);
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].z, w.z, acc[i]);
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].w, wb[tap].w, acc[i]);
+    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].w, w.w, acc[i]);
+  };
+  load_a(ra, 0);
+#pragma unroll
+  for (int tap = 0; tap < 25; tap += 2) {
+    if (tap + 1 < 25) load_a(rb, tap + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_tap(ra, wb[tap]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (tap + 1 < 25) {
+      if (tap + 2 < 25) load_a(ra, tap + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_tap(rb, wb[tap + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 #pragma unroll
   for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];

@@ -125,28 +125,41 @@ __device__ __forceinline__ int c2f_abase(int tile, int lr, int lg, int nwin, int
   return ((18 * bb + y - R0) * C2F_RW + xx) * C2F_PS + 4 * lg;
 }
 
-// NT (1 or 2) tiles against the register-resident weights: acc[u] += A(tile u) x W2
+// NT (1 or 2) tiles against the register-resident weights: acc[u] += A(tile u) x W2. Software
+// pipeline over the 50 (tap, 16-channel) steps, fully unrolled: the A chunks of step s + 1 are read
+// into the other register set before step s's MFMAs issue (sched_barrier pins the order).
 template <int NT>
 __device__ __forceinline__ void c2f_tiles(const float* img, const int (&ab)[2], const float (&wb)[200],
                                           f32x4 (&acc)[2]) {
+  float4 ra[NT], rb[NT];
+  auto load_a = [&](float4 (&a)[NT], int st) {
+    const int tap = st >> 1, c2 = st & 1, kh = tap / 5, kw = tap - 5 * kh;
+    const int off = (kh * C2F_RW + kw) * C2F_PS + 16 * c2;
 #pragma unroll
-  for (int tap = 0; tap < 25; ++tap) {
-    const int kh = tap / 5, kw = tap - 5 * kh, aoff = (kh * C2F_RW + kw) * C2F_PS;
+    for (int u = 0; u < NT; ++u) a[u] = *reinterpret_cast<const float4*>(img + ab[u] + off);
+  };
+  auto mfma_step = [&](const float4 (&a)[NT], int st) {
+    const float* w = wb + 4 * st;  // wb[8 tap + 4 c2 + j]
 #pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2) {
-      float4 a[NT];
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].x, w[0], acc[u]);
 #pragma unroll
-      for (int u = 0; u < NT; ++u) a[u] = *reinterpret_cast<const float4*>(img + ab[u] + aoff + 16 * c2);
-      const float* w = wb + tap * 8 + 4 * c2;
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].y, w[1], acc[u]);
 #pragma unroll
-      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].x, w[0], acc[u]);
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].z, w[2], acc[u]);
 #pragma unroll
-      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].y, w[1], acc[u]);
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].w, w[3], acc[u]);
+  };
+  load_a(ra, 0);
 #pragma unroll
-      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].z, w[2], acc[u]);
-#pragma unroll
-      for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].w, w[3], acc[u]);
-    }
+  for (int st = 0; st < 50; st += 2) {
+    load_a(rb, st + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_step(ra, st);
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 2 < 50) load_a(ra, st + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_step(rb, st + 1);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
