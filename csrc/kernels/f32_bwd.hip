@@ -22,6 +22,15 @@
 
 namespace mihvd {
 
+// Phase stamps (study instrument, off unless f32_stamps_enable set the buffer): thread 0 of each
+// block of f32_conv2_bwd records the shader clock (s_memtime) at its phase boundaries into
+// stamps[block][8] with vector stores.
+__device__ unsigned long long* g_c2b_stamps = nullptr;
+__device__ __forceinline__ void c2b_stamp(int k) {
+  unsigned long long* p = g_c2b_stamps;
+  if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memtime();
+}
+
 // ------------------------------------------------------------------------------------------ //
 // f32_fc1_bwd
 // ------------------------------------------------------------------------------------------ //
@@ -326,6 +335,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
   for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // the dY2 image is complete; no barrier in the tap loop
+  c2b_stamp(1);
   // the x patches are needed only by the epilogue: their gather (state -> rows -> x, three
   // dependent loads) is issued here and lands during the tap loop instead of before the barrier
   float xv[4];
@@ -378,6 +388,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   }
 #pragma unroll
   for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
+  c2b_stamp(2);
   __syncthreads();  // every wave is done with the dY2 image; the x images are complete
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
@@ -431,6 +442,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
                     (pw[((h + 4) * 26 + e) * 16 + l] + pw[((h + 6) * 26 + e) * 16 + l]);
     cpart[(int64_t)bid * CP_F32 + q] = v;  // q = tap * 32 + ci (dW1, HWIO) or 800 + ci (db1)
   }
+  c2b_stamp(3);
 }
 
 // wgrad role: dW2[kh][kw][ci][co] over the images of one group, kernel row kh and output-channel
@@ -477,6 +489,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
   float4 v[7];
   load_img(img0, v);
+  c2b_stamp(4);
   store_img(smf, v);
   __syncthreads();
   for (int n = 0; n < nimg; ++n) {
@@ -500,6 +513,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     if (n + 1 < nimg) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
   }
+  c2b_stamp(5);
   // partial exchange: [slot][kw][g][lane] float4, two rounds (waves 4-7 -> 0-3, then 0-3 -> all)
   float4* xr = reinterpret_cast<float4*>(smf);
   if (wave >= 4) {
@@ -542,6 +556,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     const int tap = kh * 5 + kw, ci = ln & 31, co = 32 * ch + 8 * g + 4 * (ln >> 5);
     *reinterpret_cast<float4*>(slab + (int64_t)grp * 51200 + (tap * 32 + ci) * 64 + co) = s;
   }
+  c2b_stamp(6);
 }
 
 template <int TPB>
@@ -551,6 +566,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
+  c2b_stamp(0);
   if (bid < n_dg) {
     f32_conv2_dgrad_block<TPB>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
     return;
@@ -690,6 +706,21 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
 static void chk_f32(const at::Tensor& t, int64_t numel, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.dtype() == at::kFloat && t.is_contiguous() && t.numel() == numel, what,
               ": expected a contiguous fp32 device tensor of ", numel, " elements");
+}
+
+// Study instrument: a device buffer of [n_blocks][8] shader-clock stamps that f32_conv2_bwd fills
+// from now on (n_blocks = 0: off). Returns the buffer (int64).
+at::Tensor f32_stamps_enable(int64_t n_blocks) {
+  static at::Tensor buf;
+  unsigned long long* p = nullptr;
+  if (n_blocks > 0) {
+    buf = at::zeros({n_blocks * 8}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA));
+    p = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
+  } else {
+    buf = at::Tensor();
+  }
+  TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_c2b_stamps), &p, sizeof(p)) == hipSuccess, "f32_stamps_enable");
+  return n_blocks > 0 ? buf : at::zeros({0}, at::TensorOptions().dtype(at::kLong));
 }
 
 int64_t f32_db2_rows(int64_t B) { return 49 * ((B + 15) / 16); }

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Phase timing of f32_conv2_bwd blocks from in-kernel shader-clock stamps (f32_stamps_enable).
+
+Prints, per role, the median and max cycles of each phase and when blocks start relative to the
+first block (second-round blocks start late), plus the kernel's event-timed duration for scale.
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    B = 100
+    (x, y), _ = synthetic_mnist(n_train=B * 20, n_test=10, seed=1)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, seed=0, device="cuda", precision="fp32")
+    tr.set_device_dataset(X, Y)
+    for _ in range(3):
+        tr.device_step()
+    torch.cuda.synchronize()
+    o, st, P = tr.ops, tr.state, tr.pview
+    n_dg = int(o.f32_dgrad_blocks(B))
+    n_wg = 10 * int(o.f32_wgrad_groups(B))
+    w2 = P("conv_layer2/conv2d/kernel")
+    run = lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab)
+    for _ in range(5):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    run()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000
+    buf = o.f32_stamps_enable(n_dg + n_wg)
+    run()
+    torch.cuda.synchronize()
+    s = buf.view(-1, 8).cpu().double()
+    o.f32_stamps_enable(0)
+    t0 = s[:, 0].min()
+    span = (torch.maximum(s[:n_dg, 3], torch.zeros(1)).max().item(), s[n_dg:, 6].max().item())
+    total = max(span) - t0.item()
+    print(f"conv2_bwd B={B}: {us:.1f} us (event), {total:.0f} cycles first start -> last end "
+          f"({total / us:.0f} cycles/us)")
+
+    def show(name, rows, marks):
+        print(f"  {name}: {rows.shape[0]} blocks")
+        st_ = rows[:, 0] - t0
+        print(f"    start offset   median {st_.median():8.0f}  max {st_.max():8.0f}")
+        for a, b, label in marks:
+            d = rows[:, b] - rows[:, a]
+            print(f"    {label:14s} median {d.median():8.0f}  max {d.max():8.0f}")
+
+    show("dgrad", s[:n_dg], [(0, 1, "staging"), (1, 2, "tap loop"), (2, 3, "epilogue"), (0, 3, "block total")])
+    show("wgrad", s[n_dg:], [(0, 4, "first image"), (4, 5, "image loop"), (5, 6, "reduction"), (0, 6, "block total")])
+
+
+if __name__ == "__main__":
+    main()
