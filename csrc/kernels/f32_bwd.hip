@@ -24,11 +24,16 @@ namespace mihvd {
 
 // Phase stamps (study instrument, off unless f32_stamps_enable set the buffer): thread 0 of each
 // block of f32_conv2_bwd records the shader clock (s_memtime) at its phase boundaries into
-// stamps[block][8] with vector stores.
+// stamps[block][16] with vector stores (slots 8..15: each wave's end of the dgrad tap loop).
 __device__ unsigned long long* g_c2b_stamps = nullptr;
 __device__ __forceinline__ void c2b_stamp(int k) {
   unsigned long long* p = g_c2b_stamps;
-  if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memtime();
+  if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memtime();
+}
+// per-wave stamp (lane 0 of every wave): slot 8 + wave
+__device__ __forceinline__ void c2b_stamp_wave() {
+  unsigned long long* p = g_c2b_stamps;
+  if (p != nullptr && (threadIdx.x & 63) == 0) p[blockIdx.x * 16 + 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -311,11 +316,6 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
         dY2 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 64 + ch * 4);
     iv[it] = mask_f4(v, in);
   }
-  // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3]
-  const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
-  float4 wb[25];
-#pragma unroll
-  for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
 #pragma unroll
   for (int it = 0; it < CBF_MAXCH; ++it) {
     const int i = t + 512 * it;
@@ -336,6 +336,27 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // the dY2 image is complete; no barrier in the tap loop
   c2b_stamp(1);
+  // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3].
+  // Issued after the barrier (whose vmcnt(0) would otherwise wait for all 25 loads): the tap loop
+  // consumes them in issue order, so tap t waits only for its own.
+  const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
+  float4 wb[25];
+#pragma unroll
+  for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
+  // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched
+  constexpr int NP = (2 * TPB + 7) / 8;  // (nt, tile) pairs per wave
+  float ea[NP][4];
+  int ex[NP][4];
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pp = wave + 8 * k, P = 16 * (T0 + (pp >> 1)) + 4 * lg + r;
+      const bool ok = pp < 2 * TPB && P < np;
+      const int64_t o = (int64_t)min(P, np - 1) * 32 + 16 * nt + lr;
+      ea[k][r] = mask_f(a1[o], ok);
+      ex[k][r] = idx1[o];
+    }
   // the x patches are needed only by the epilogue: their gather (state -> rows -> x, three
   // dependent loads) is issued here and lands during the tap loop instead of before the barrier
   float xv[4];
@@ -389,7 +410,9 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
   for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
   c2b_stamp(2);
+  c2b_stamp_wave();
   __syncthreads();  // every wave is done with the dY2 image; the x images are complete
+  c2b_stamp(7);
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
 #pragma unroll
@@ -401,7 +424,10 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
   for (int e = 0; e < 26; ++e) s25[e] = 0.f;
   const int ci = 16 * nt + lr;
-  for (int p = wave; p < 2 * TPB; p += 8) {  // wave-uniform; p & 1 == nt
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int p = wave + 8 * k;  // wave-uniform; p & 1 == nt
+    if (p >= 2 * TPB) break;
     const int i = p >> 1;
     const f32x4 sum = ((red[((0 * 2 + nt) * TPB + i) * 64 + lane] + red[((1 * 2 + nt) * TPB + i) * 64 + lane]) +
                        red[((2 * 2 + nt) * TPB + i) * 64 + lane]) +
@@ -411,9 +437,8 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
       const int P = 16 * (T0 + i) + 4 * lg + r;
       if (P < np) {
         const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
-        const int64_t o = (int64_t)P * 32 + ci;
-        const float g = a1[o] > 0.f ? sum[r] : 0.f;
-        const int ix = idx1[o];
+        const float g = ea[k][r] > 0.f ? sum[r] : 0.f;
+        const int ix = ex[k][r];
         const float* xs = xim + (bb - b0) * 1024 + (2 * py + (ix >> 1)) * 32 + 2 * px + (ix & 1);
 #pragma unroll
         for (int kh = 0; kh < 5; ++kh)
@@ -708,13 +733,13 @@ static void chk_f32(const at::Tensor& t, int64_t numel, const char* what) {
               ": expected a contiguous fp32 device tensor of ", numel, " elements");
 }
 
-// Study instrument: a device buffer of [n_blocks][8] shader-clock stamps that f32_conv2_bwd fills
+// Study instrument: a device buffer of [n_blocks][16] shader-clock stamps that f32_conv2_bwd fills
 // from now on (n_blocks = 0: off). Returns the buffer (int64).
 at::Tensor f32_stamps_enable(int64_t n_blocks) {
   static at::Tensor buf;
   unsigned long long* p = nullptr;
   if (n_blocks > 0) {
-    buf = at::zeros({n_blocks * 8}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA));
+    buf = at::zeros({n_blocks * 16}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA));
     p = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
   } else {
     buf = at::Tensor();

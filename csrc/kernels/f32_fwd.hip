@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
   const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
   const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
-  // 1. every load in flight first: the image rows, then this wave's weights (into registers)
+  // 1. the image rows
   float4 iv[C2F_MAXCH];
 #pragma unroll
   for (int it = 0; it < C2F_MAXCH; ++it) {
@@ -198,14 +198,6 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
         a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
     iv[it] = mask_f4(v, in);
   }
-  float wb[200];  // wb[8 tap + 4 c2 + j] = W2[tap][16 c2 + 4 lg + j][16 w + lr]
-  const float* wp = w2 + (4 * lg) * 64 + 16 * wave + lr;
-#pragma unroll
-  for (int tap = 0; tap < 25; ++tap)
-#pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wb[8 * tap + 4 * c2 + j] = wp[tap * 2048 + (16 * c2 + j) * 64];
 #pragma unroll
   for (int it = 0; it < C2F_MAXCH; ++it) {
     const int i = t + 256 * it;
@@ -215,6 +207,16 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
     }
   }
   __syncthreads();  // the image is complete; no barrier below
+  // the weights, issued after the barrier (whose vmcnt(0) would otherwise wait for all 200 loads):
+  // the MFMA steps consume them in issue order, each waiting only for its own
+  float wb[200];  // wb[8 tap + 4 c2 + j] = W2[tap][16 c2 + 4 lg + j][16 w + lr]
+  const float* wp = w2 + (4 * lg) * 64 + 16 * wave + lr;
+#pragma unroll
+  for (int tap = 0; tap < 25; ++tap)
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wb[8 * tap + 4 * c2 + j] = wp[tap * 2048 + (16 * c2 + j) * 64];
   const int co = 16 * wave + lr;
   const float bias = b2[co];
   for (int i = 0; i < TPB; i += 2) {  // block-uniform

@@ -42,7 +42,7 @@ def main():
     buf = o.f32_stamps_enable(n_dg + n_wg)
     run()
     torch.cuda.synchronize()
-    s = buf.view(-1, 8).cpu().double()
+    s = buf.view(-1, 16).cpu().double()
     o.f32_stamps_enable(0)
     t0 = s[:, 0].min()
     span = (torch.maximum(s[:n_dg, 3], torch.zeros(1)).max().item(), s[n_dg:, 6].max().item())
@@ -58,7 +58,10 @@ def main():
             d = rows[:, b] - rows[:, a]
             print(f"    {label:14s} median {d.median():8.0f}  max {d.max():8.0f}")
 
-    show("dgrad", s[:n_dg], [(0, 1, "staging"), (1, 2, "tap loop"), (2, 3, "epilogue"), (0, 3, "block total")])
+    show("dgrad", s[:n_dg], [(0, 1, "staging"), (1, 2, "tap loop w0"), (2, 7, "loop skew"), (7, 3, "epilogue"),
+                             (0, 3, "block total")])
+    d = s[:n_dg, 8:16] - s[:n_dg, 1:2]
+    print("    tap loop per wave (median over blocks): " + " ".join(f"{v:.0f}" for v in d.median(0).values))
     show("wgrad", s[n_dg:], [(0, 4, "first image"), (4, 5, "image loop"), (5, 6, "reduction"), (0, 6, "block total")])
 
 
