@@ -63,9 +63,11 @@ def parse():
 
 
 def synthetic_pool(n_batches, batch, device, seed=0):
+    """This rank's resident batches: the class templates are shared by every rank (one dataset),
+    the samples are drawn per rank (``seed`` = rank), like shards of MNIST."""
     from mihvd.utils.data import synthetic_mnist
 
-    (x, y), _ = synthetic_mnist(n_train=n_batches * batch, n_test=10, seed=seed)
+    (x, y), _ = synthetic_mnist(n_train=n_batches * batch, n_test=10, seed=1234, sample_seed=seed)
     xt = torch.from_numpy(x.reshape(-1, 784)).to(device=device, dtype=torch.float32).div_(255.0)
     yt = torch.from_numpy(y.astype("int64")).to(device)
     return xt, yt

@@ -60,7 +60,12 @@ def load_idx_dir(dirname: str):
     return (xtr, ytr), (xte, yte)
 
 
-def synthetic_mnist(n_train: int = 60000, n_test: int = 10000, seed: int = 1234):
+def synthetic_mnist(n_train: int = 60000, n_test: int = 10000, seed: int = 1234, sample_seed: int | None = None):
+    """MNIST-shaped synthetic data: 10 class templates (random strokes, drawn from ``seed``), samples
+    = a template shifted by up to 2 px, scaled and noised. ``sample_seed`` draws the samples from a
+    separate generator with the SAME templates: data-parallel ranks must share the class templates
+    and differ only in their samples (per-rank templates would give each rank its own labelling of
+    the classes, and the averaged gradient of N conflicting labellings trains towards chance)."""
     rng = np.random.default_rng(seed)
     templates = np.zeros((10, 28, 28), dtype=np.float32)
     for c in range(10):
@@ -87,8 +92,9 @@ def synthetic_mnist(n_train: int = 60000, n_test: int = 10000, seed: int = 1234)
         out += rs.normal(0, 0.15, size=out.shape).astype(np.float32)
         return (np.clip(out, 0, 1) * 255).astype(np.uint8), labels
 
-    xtr, ytr = make(n_train, np.random.default_rng(seed + 1))
-    xte, yte = make(n_test, np.random.default_rng(seed + 2))
+    s0 = seed if sample_seed is None else 7919 * sample_seed + 104729
+    xtr, ytr = make(n_train, np.random.default_rng(s0 + 1))
+    xte, yte = make(n_test, np.random.default_rng(s0 + 2))
     return (xtr, ytr), (xte, yte)
 
 

@@ -138,6 +138,23 @@ def test_bench_multirank_rehearsal_on_one_gpu(n, prec):
     assert r["config"]["final_loss"] < 2.0, r
 
 
+@pytest.mark.parametrize("n,prec", [(8, "bf16"), (8, "fp32")])
+def test_bench_flow_trains_at_8_ranks(tmp_path, n, prec):
+    """The bench's fused flow (data-plane selection, 20-step graphs) at 8 ranks sharing this GPU
+    over gloo, with per-rank synthetic shards that share the class templates: training reaches well
+    below chance (ln 10 = 2.30). Round 2's 8-rank rehearsal sat at 2.31 because every rank drew its
+    own class templates (seed = rank): 8 conflicting labellings whose averaged gradient cancels."""
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_TEST_PRECISION=prec,
+               MIHVD_XGMI_TIMEOUT_MS="60000")
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", str(n), sys.executable, WORKER, "bench_flow", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(n):
+        o = json.loads((tmp_path / f"bench_flow.{r}.json").read_text())
+        assert o["losses"][-1] < 1.0, o
+
+
 @pytest.mark.parametrize("n,prec,gather,shard,xgmi", [
     (4, "fp32", "0", "0", "off"), (8, "fp32", "0", "0", "off"), (4, "fp32", "0", "1", "off"),
     (8, "fp32", "0", "1", "off"),

@@ -623,3 +623,25 @@ def test_fused_optimizers_torch_path_match_torch_optim():
                 o.step()
         for x, y in zip(a, b):
             assert torch.allclose(x, y, atol=1e-6, rtol=1e-5)
+
+
+def test_synthetic_shards_share_class_templates():
+    """Data-parallel shards of the synthetic set (sample_seed = rank) share the class templates: the
+    per-class mean images of two shards match; independently seeded sets (the old per-rank seed)
+    do not."""
+    import numpy as np
+
+    from mihvd.utils.data import synthetic_mnist
+
+    def class_means(x, y):
+        return np.stack([x[y == c].astype(np.float64).mean(0) for c in range(10)])
+
+    (a, ya), _ = synthetic_mnist(3000, 10, seed=1234, sample_seed=0)
+    (b, yb), _ = synthetic_mnist(3000, 10, seed=1234, sample_seed=1)
+    (c, yc), _ = synthetic_mnist(3000, 10, seed=1)
+    assert not np.array_equal(a, b)
+    ma, mb, mc = class_means(a, ya), class_means(b, yb), class_means(c, yc)
+    same = np.corrcoef(ma.reshape(10, -1), mb.reshape(10, -1))[np.arange(10), 10 + np.arange(10)]
+    other = np.corrcoef(ma.reshape(10, -1), mc.reshape(10, -1))[np.arange(10), 10 + np.arange(10)]
+    assert same.min() > 0.95, same
+    assert other.mean() < 0.5, other

@@ -224,6 +224,30 @@ def sc_dp_gloo_n(outdir):
         json.dump(rec, f)
 
 
+def sc_bench_flow(outdir):
+    """bench.py's fused flow at N ranks without bench.py: per-rank synthetic shards (shared class
+    templates), lr 1e-3 x N, dropout 0.5, select_data_plane, 20-step graphs, 2 replays."""
+    from mihvd.utils.data import synthetic_mnist
+
+    r, n = hvd.rank(), hvd.size()
+    prec = os.environ.get("MIHVD_TEST_PRECISION", "fp32")
+    (x, y), _ = synthetic_mnist(n_train=60 * 100, n_test=10, seed=1234, sample_seed=r)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    tr = FusedMNISTTrainer(batch_size=100, lr=1e-3 * n, seed=42, device="cuda", precision=prec)
+    tr.set_device_dataset(X, Y)
+    rep = tr.select_data_plane() if tr.collectives else {"plane": "none"}
+    tr.build_graph(steps_per_replay=20)
+    losses = []
+    for _ in range(3):
+        tr.run_graph()
+        losses.append(tr.last_loss())
+    rec = {"losses": losses, "plane": rep.get("plane"), "shard": tr.shard_w3, "n": n}
+    tr.close()
+    with open(os.path.join(outdir, f"bench_flow.{r}.json"), "w") as f:
+        json.dump(rec, f)
+
+
 def sc_ckpt_shard(outdir):
     """2 ranks, sharded dense/kernel optimizer: MonitoredTrainingSession checkpoints (collective
     gather on every rank, rank 0 writes), a fresh session restores on rank 0 and broadcasts; the
