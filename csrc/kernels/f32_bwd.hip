@@ -735,17 +735,24 @@ static void chk_f32(const at::Tensor& t, int64_t numel, const char* what) {
 
 // Study instrument: a device buffer of [n_blocks][16] shader-clock stamps that f32_conv2_bwd fills
 // from now on (n_blocks = 0: off). Returns the buffer (int64).
-at::Tensor f32_stamps_enable(int64_t n_blocks) {
-  static at::Tensor buf;
+void f32_fwd_stamps_set(unsigned long long* p);  // f32_fwd.hip
+
+at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel) {
+  static at::Tensor buf[2];
+  TORCH_CHECK(kernel == 0 || kernel == 1, "f32_stamps_enable: kernel 0 = conv2_bwd, 1 = conv2_fwd");
   unsigned long long* p = nullptr;
   if (n_blocks > 0) {
-    buf = at::zeros({n_blocks * 16}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA));
-    p = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
+    buf[kernel] = at::zeros({n_blocks * 16}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA));
+    p = reinterpret_cast<unsigned long long*>(buf[kernel].data_ptr<int64_t>());
   } else {
-    buf = at::Tensor();
+    buf[kernel] = at::Tensor();
   }
-  TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_c2b_stamps), &p, sizeof(p)) == hipSuccess, "f32_stamps_enable");
-  return n_blocks > 0 ? buf : at::zeros({0}, at::TensorOptions().dtype(at::kLong));
+  if (kernel == 0) {
+    TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_c2b_stamps), &p, sizeof(p)) == hipSuccess, "f32_stamps_enable");
+  } else {
+    f32_fwd_stamps_set(p);
+  }
+  return n_blocks > 0 ? buf[kernel] : at::zeros({0}, at::TensorOptions().dtype(at::kLong));
 }
 
 int64_t f32_db2_rows(int64_t B) { return 49 * ((B + 15) / 16); }

@@ -24,6 +24,17 @@
 
 namespace mihvd {
 
+// Phase stamps of f32_conv2_fwd blocks (study instrument; f32_stamps_enable(1, n) in f32_bwd.hip
+// sets the buffer): slots 0 start, 1 staging barrier, 2 + pair index: end of each tile pair.
+__device__ unsigned long long* g_c2f_stamps = nullptr;
+__device__ __forceinline__ void c2f_stamp(int k) {
+  unsigned long long* p = g_c2f_stamps;
+  if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memtime();
+}
+void f32_fwd_stamps_set(unsigned long long* p) {
+  TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_c2f_stamps), &p, sizeof(p)) == hipSuccess, "c2f stamps");
+}
+
 // ------------------------------------------------------------------------------------------ //
 // conv1: x rows [784] fp32 -> a1 [B][14][14][32] fp32 + argmax idx1 (u8)
 // grid (4, B): block q of an image owns the 16-row tiles [13q, 13q + 13) of its 49 (4 pooling
@@ -179,6 +190,7 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
     }
   }
   float* img = smf;
+  c2f_stamp(0);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int nwin = 49 * B, T0 = ((int)blockIdx.x - (TAIL ? ad.nblk : 0)) * TPB;
   const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
@@ -207,6 +219,7 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
     }
   }
   __syncthreads();  // the image is complete; no barrier below
+  c2f_stamp(1);
   // the weights, issued after the barrier (whose vmcnt(0) would otherwise wait for all 200 loads):
   // the MFMA steps consume them in issue order, each waiting only for its own
   float wb[200];  // wb[8 tap + 4 c2 + j] = W2[tap][16 c2 + 4 lg + j][16 w + lr]
@@ -238,6 +251,7 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
         idx2[o] = (uint8_t)best;
       }
     }
+    c2f_stamp(2 + (i >> 1));
   }
 }
 

@@ -103,10 +103,33 @@ def bert_tiny():
     return W()
 
 
+def bert_base(mpos=False):
+    """The stress config's model (BERT-base 12x768) at this script's B and S; mpos: the MLM head on
+    the masked positions only, index list computed outside the capture (as benchmarks/stress_models.py)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from mihvd.models.bert import BertConfig, BertForMaskedLM, masked_positions
+
+    class W(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.m = BertForMaskedLM(BertConfig(max_len=512))
+            self.mp = None
+
+        def forward(self, ids, labels):
+            if mpos and self.mp is None:
+                self.mp = masked_positions(labels)
+            return self.m(ids, labels, masked_positions=self.mp if mpos else None)
+
+    return W()
+
+
 VARIANTS = {
     "emb": lambda: Emb(False), "emb_tied": lambda: Emb(True), "ln_gelu": LnGelu, "sdpa": lambda: Attn(True),
     "math_attn": lambda: Attn(False), "sdpa_dropout": lambda: Attn(True, 0.1), "dropout": Dropout,
-    "bert_tiny": bert_tiny,
+    "bert_tiny": bert_tiny, "bert_base": lambda: bert_base(False), "bert_base_mpos": lambda: bert_base(True),
 }
 
 

@@ -64,6 +64,21 @@ def main():
     print("    tap loop per wave (median over blocks): " + " ".join(f"{v:.0f}" for v in d.median(0).values))
     show("wgrad", s[n_dg:], [(0, 4, "first image"), (4, 5, "image loop"), (5, 6, "reduction"), (0, 6, "block total")])
 
+    # conv2_fwd: staging, then one stamp per tile pair
+    a2, idx2 = tr.a2, tr.idx2
+    runf = lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), a2, idx2)
+    nblk = -(-((49 * B + 3) // 4) // 5)
+    buf = o.f32_stamps_enable(nblk, 1)
+    runf()
+    torch.cuda.synchronize()
+    f = buf.view(-1, 16).cpu().double()
+    o.f32_stamps_enable(0, 1)
+    print(f"conv2_fwd: {nblk} blocks")
+    for a, b, label in [(0, 1, "staging"), (1, 2, "tile pair 1"), (2, 3, "tile pair 2"), (3, 4, "tile 5"),
+                        (0, 4, "block total")]:
+        d = f[:, b] - f[:, a]
+        print(f"    {label:14s} median {d.median():8.0f}  max {d.max():8.0f}")
+
 
 if __name__ == "__main__":
     main()
