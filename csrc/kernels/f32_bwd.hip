@@ -132,6 +132,104 @@ __device__ __forceinline__ void f32_fc1_dgrad_block(int bid, const float* __rest
   }
 }
 
+// dgrad block, K-split form (default): 16 features f0..f0+15 (window jt = bid >> 2, channels
+// 16 (bid & 3) ..) x every 16-sample tile of the batch (G <= 8) x the full K, one K quarter per
+// wave (wave w: k in [256 w, 256 w + 256)). Each W3 fragment a wave loads serves all G sample
+// tiles (G independent accumulators: no dependent MFMA pair closer than G issues), so W3 is read
+// once and the MFMA pipe, not the operand fetch, sets the pace; 196 blocks x 4 waves of 16 G
+// MFMAs per 16-deep chunk. Operands stream from L2 through a 4-deep register ring (3 chunks in
+// flight). The quarters meet in LDS and are summed in a fixed order (deterministic).
+constexpr int F1B_DG2 = 196;
+template <int G>
+__device__ __forceinline__ void f32_fc1_dgrad_ks_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
+                                                       const uint8_t* __restrict__ idx2, const float* __restrict__ w3,
+                                                       float* __restrict__ dY2, float* __restrict__ db2p, int B,
+                                                       float* smf) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int f0 = 16 * bid, kb = 256 * wave;
+  const float* wr = w3 + (int64_t)(f0 + lr) * 1024 + kb + 4 * lg;
+  const float* zr[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) zr[u] = dz + (int64_t)min(16 * u + lr, B - 1) * 1024 + kb + 4 * lg;
+  // sample columns >= B read row B - 1 and are never stored (MFMA columns are independent)
+  constexpr int NC = 16, D = 4;
+  float4 wv[D], zv[D][G];
+#pragma unroll
+  for (int c = 0; c < D - 1; ++c) {
+    wv[c] = *reinterpret_cast<const float4*>(wr + 16 * c);
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      zv[c][u] = *reinterpret_cast<const float4*>(zr[u] + 16 * c);
+  }
+  f32x4 acc[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fully unrolled; sched_barrier pins the order [loads of chunk c + 3] [MFMAs of chunk c, element
+  // by element, tile-inner] so the scheduler neither hoists every chunk's loads (register blow-up)
+  // nor sinks them next to their use (exposed latency), and no two consecutive MFMAs share an
+  // accumulator
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c + D - 1 < NC) {
+      const int s = (c + D - 1) % D, cn = c + D - 1;
+      wv[s] = *reinterpret_cast<const float4*>(wr + 16 * cn);
+#pragma unroll
+      for (int u = 0; u < G; ++u) zv[s][u] = *reinterpret_cast<const float4*>(zr[u] + 16 * cn);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = c % D;
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].x, zv[s][u].x, acc[u]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].y, zv[s][u].y, acc[u]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].z, zv[s][u].z, acc[u]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].w, zv[s][u].w, acc[u]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // C[row 4 lg + i][col lr] of tile u = channel 4 lg + i of this block's 16, sample 16 u + lr
+  float4* red = reinterpret_cast<float4*>(smf);  // [4 waves][8 tiles][64 lanes]
+#pragma unroll
+  for (int u = 0; u < G; ++u)
+    red[(wave * 8 + u) * 64 + lane] = make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+  __syncthreads();
+  const int jt = bid >> 2, py = jt / 7, px = jt - 7 * py;
+  for (int i = t; i < G * 64; i += 256) {  // wave-uniform trip count: i >> 6 is one tile per wave
+    const int u = i >> 6, ln = i & 63, r = ln & 15, q = ln >> 4;
+    const float4 s0 = red[(0 * 8 + u) * 64 + ln], s1 = red[(1 * 8 + u) * 64 + ln];
+    const float4 s2 = red[(2 * 8 + u) * 64 + ln], s3 = red[(3 * 8 + u) * 64 + ln];
+    const float sv[4] = {(s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y), (s0.z + s1.z) + (s2.z + s3.z),
+                         (s0.w + s1.w) + (s2.w + s3.w)};
+    const int m = 16 * u + r, mc = min(m, B - 1), co = 16 * (bid & 3) + 4 * q, j = 64 * jt + co;
+    const bool valid = m < B;
+    const float4 av = *reinterpret_cast<const float4*>(a2 + (int64_t)mc * 3136 + j);
+    const uint32_t ix = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc * 3136 + j);
+    const float ae[4] = {av.x, av.y, av.z, av.w};
+    float g[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[e] = (valid && ae[e] > 0.f) ? sv[e] : 0.f;
+    float sm[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sm[e] = row_sum16(g[e]);  // over the 16 samples of tile u
+    if (r == 0)
+      *reinterpret_cast<float4*>(db2p + ((int64_t)u * 49 + jt) * 64 + co) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+    if (valid) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (int)((ix >> (8 * e)) & 0xff) == d ? g[e] : 0.f;
+        const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
+        *reinterpret_cast<float4*>(dY2 + (((int64_t)m * 14 + y) * 14 + x) * 64 + co) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+}
+
 // Small reductions over the batch: db3 (16 blocks of 64 features), dW4 (16 blocks), db4 (1 block).
 __device__ __forceinline__ void f32_fc1_small_block(int bid, const float* __restrict__ dz, const float* __restrict__ h,
                                                     const float* __restrict__ dlog, float* __restrict__ gb3,
@@ -206,13 +304,17 @@ __device__ __forceinline__ void f32_fc1_small_block(int bid, const float* __rest
 // 32-63 read 32 consecutive floats of one sample row each (ds_read_b32, conflict-free without
 // padding). 4 waves x one 32x32 sub-tile; output features n on the MFMA row axis so a lane's four
 // consecutive accumulator rows are one float4 of a dW3 row.
+// G > 0: K padded to the 16 G rows of whole sample tiles (zero rows) and the MFMA chain fully
+// unrolled, so the LDS operand reads run ahead of the dependent MFMAs (the runtime-length loop
+// waited on every ds_read pair before its MFMA).
+template <int G>
 __device__ __forceinline__ void f32_fc1_wgrad_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
                                                     float* __restrict__ gW3, int B, float* smf) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int jt = bid >> 4, ntile = bid & 15, j0 = 64 * jt, n0 = 64 * ntile;
   float* A2s = smf;                   // [128][64] rows b, cols j
   float* DZs = smf + F32_MAXB * 64;   // [128][64] rows b, cols n
-  const int Kp = (B + 1) & ~1, nchk = Kp * 16;
+  const int Kp = G > 0 ? 16 * G : (B + 1) & ~1, nchk = Kp * 16;
   float4 va[8], vz[8];
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
@@ -235,9 +337,30 @@ __device__ __forceinline__ void f32_fc1_wgrad_block(int bid, const float* __rest
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int ns = Kp >> 1;
+  if constexpr (G > 0) {
+    // operand reads run 6 steps ahead of the MFMA that uses them (ring of 8 register pairs)
+    constexpr int NS = 8 * G, R = 8, AH = 6;
+    float ar[R], br[R];
+#pragma unroll
+    for (int s = 0; s < AH; ++s) {
+      ar[s] = ap[s * 128];
+      br[s] = bp[s * 128];
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + AH < NS) {
+        ar[(s + AH) % R] = ap[(s + AH) * 128];
+        br[(s + AH) % R] = bp[(s + AH) * 128];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      acc = mfma32(ar[s % R], br[s % R], acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    const int ns = Kp >> 1;
 #pragma unroll 8
-  for (int s = 0; s < ns; ++s) acc = mfma32(ap[s * 128], bp[s * 128], acc);
+    for (int s = 0; s < ns; ++s) acc = mfma32(ap[s * 128], bp[s * 128], acc);
+  }
   const int j = j0 + 32 * wj + l32;
 #pragma unroll
   for (int g = 0; g < 4; ++g)
@@ -245,6 +368,8 @@ __device__ __forceinline__ void f32_fc1_wgrad_block(int bid, const float* __rest
         make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
 }
 
+// GT: 0 = the earlier dgrad form, 1..8 = the K-split form for G = GT sample tiles
+template <int GT>
 __global__ void __launch_bounds__(256) f32_fc1_bwd_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, const float* __restrict__ w3, float* __restrict__ dY2,
@@ -253,7 +378,10 @@ __global__ void __launch_bounds__(256) f32_fc1_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float smf[];
   int bid = blockIdx.x;
   if (bid < n_dg) {
-    f32_fc1_dgrad_block(bid, dz, a2, idx2, w3, dY2, db2p, B, G, smf);
+    if constexpr (GT > 0)
+      f32_fc1_dgrad_ks_block<GT>(bid, dz, a2, idx2, w3, dY2, db2p, B, smf);
+    else
+      f32_fc1_dgrad_block(bid, dz, a2, idx2, w3, dY2, db2p, B, G, smf);
     return;
   }
   bid -= n_dg;
@@ -261,7 +389,7 @@ __global__ void __launch_bounds__(256) f32_fc1_bwd_kernel(
     f32_fc1_small_block(bid, dz, h, dlog, gb3, gW4, gb4, B, smf);
     return;
   }
-  f32_fc1_wgrad_block(bid - F1B_SMALL, dz, a2, gW3, B, smf);
+  f32_fc1_wgrad_block<GT>(bid - F1B_SMALL, dz, a2, gW3, B, smf);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -783,21 +911,33 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   chk_f32(gb3, 1024, "f32_fc1_bwd: gb3");
   chk_f32(gW4, 10240, "f32_fc1_bwd: gW4");
   chk_f32(gb4, 10, "f32_fc1_bwd: gb4");
-  const int G = (B + 15) / 16, n_dg = 56 * G;
+  // MIHVD_F32_F1B_KS=1 selects the K-split dgrad form with the unrolled wgrad chain (study: same
+  // dgrad time, fc1_bwd 27.0 vs 25.5 us at B = 100, so the window form stays the default)
+  const int dg_ks = env_knob("MIHVD_F32_F1B_KS", 0) != 0;
+  const int G = (B + 15) / 16, n_dg = dg_ks ? F1B_DG2 : 56 * G;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  static bool attr = [] {
-    hipFuncSetAttribute((const void*)f32_fc1_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, F1B_LDS);
-    return true;
-  }();
-  (void)attr;
   // study knob: MIHVD_F32_F1B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only
   const int role = env_knob("MIHVD_F32_F1B_ROLE", 0);
   const int grid = role == 1 ? n_dg : role == 2 ? F1B_WGRAD : n_dg + F1B_SMALL + F1B_WGRAD;
   const int ndg_arg = role == 2 ? -F1B_SMALL : n_dg;  // wgrad only: bid - n_dg - 33 = bid
-  f32_fc1_bwd_kernel<<<grid, 256, F1B_LDS, stream>>>(
-      dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(), dlog.data_ptr<float>(),
-      w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(), gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-      gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, ndg_arg);
+  auto launch = [&](auto kern) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1B_LDS);
+    kern<<<grid, 256, F1B_LDS, stream>>>(
+        dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
+        dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
+        gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, ndg_arg);
+  };
+  switch (dg_ks ? G : 0) {
+    case 0: launch(f32_fc1_bwd_kernel<0>); break;
+    case 1: launch(f32_fc1_bwd_kernel<1>); break;
+    case 2: launch(f32_fc1_bwd_kernel<2>); break;
+    case 3: launch(f32_fc1_bwd_kernel<3>); break;
+    case 4: launch(f32_fc1_bwd_kernel<4>); break;
+    case 5: launch(f32_fc1_bwd_kernel<5>); break;
+    case 6: launch(f32_fc1_bwd_kernel<6>); break;
+    case 7: launch(f32_fc1_bwd_kernel<7>); break;
+    default: launch(f32_fc1_bwd_kernel<8>); break;
+  }
 }
 
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,

@@ -371,6 +371,163 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd_kernel(const float* __restric
   }
 }
 
+// fc1 forward, pipelined form (default; MIHVD_F32_F1F=0 selects the form above). Same grid,
+// slabs and operand layouts; two changes:
+//  * MFMA core: a wave's NT tiles (sh, sh + 2, ...) are interleaved element-outer, tile-inner, so
+//    dependent MFMAs sit NT issues apart (the form above alternated two accumulators: 2 x 32 cycles
+//    against the 40-cycle dependent latency), and the a2 chunks are read from LDS two chunks ahead.
+//  * ADAM: the update streams in 7 parts of 32 rows (one float4 of p/g/m/v per thread per part);
+//    part p + 1's update and part p + 2's loads run while the MFMAs of part p issue, so the HBM
+//    stream and the matrix cores overlap instead of taking turns (the form above applied the whole
+//    tile's update, then ran every MFMA).
+template <int NT, int Q0, int Q1>
+__device__ __forceinline__ void f1f_mma(const float (&wa)[56], const float* __restrict__ bp, f32x4 (&acc)[4]) {
+  if constexpr (NT > 0) {
+    constexpr int NQ = Q1 - Q0, DQ = 2, R = DQ + 1;
+    float4 bq[R][NT];
+#pragma unroll
+    for (int j = 0; j < DQ; ++j)
+      if (j < NQ) {
+#pragma unroll
+        for (int u = 0; u < NT; ++u) bq[j][u] = *reinterpret_cast<const float4*>(bp + u * 32 * F1F_AS + 16 * (Q0 + j));
+      }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      if (j + DQ < NQ) {
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+          bq[(j + DQ) % R][u] = *reinterpret_cast<const float4*>(bp + u * 32 * F1F_AS + 16 * (Q0 + j + DQ));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const int q = Q0 + j, s = j % R;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(wa[4 * q + 0], bq[s][u].x, acc[u]);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(wa[4 * q + 1], bq[s][u].y, acc[u]);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(wa[4 * q + 2], bq[s][u].z, acc[u]);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma4(wa[4 * q + 3], bq[s][u].w, acc[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <int MT, bool ADAM>
+__global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restrict__ a2, float* __restrict__ w3,
+                                                           float* __restrict__ zpart, int B, F32Adam ad) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  float* As = smf;  // [16 MT][228]: rows = samples, k contiguous
+  const int nb = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int k0 = ks * F1F_KSL, nt = wave & 3, sh = wave >> 2;
+  const int n = nb * 64 + nt * 16 + lr;
+  constexpr int NCH = MT * 16 * 56, PER = (NCH + 511) / 512;
+  constexpr int NT0 = (MT + 1) / 2, NT1 = MT / 2;  // tiles of the sh = 0 / sh = 1 waves
+  const float* bp = As + (sh * 16 + lr) * F1F_AS + 4 * lg;
+  float wa[56];  // A fragments: wa[4q + j] = W3[k0 + 16q + 4lg + j][n]
+  f32x4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 v[PER];
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = min(t + 512 * it, NCH - 1), r = i / 56, cc = i - 56 * r;
+    v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc), r < B);
+  }
+  if constexpr (!ADAM) {
+    const int64_t wo = (int64_t)(k0 + 4 * lg) * 1024 + n;
+#pragma unroll
+    for (int q = 0; q < 14; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wa[4 * q + j] = w3[wo + (16 * q + j) * 1024];
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = t + 512 * it;
+      if (i < NCH) {
+        const int r = i / 56, cc = i - 56 * r;
+        *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
+      }
+    }
+    __syncthreads();
+    if (sh == 0)
+      f1f_mma<NT0, 0, 14>(wa, bp, acc);
+    else
+      f1f_mma<NT1, 0, 14>(wa, bp, acc);
+  } else {
+    static_assert(MT <= 7, "the fused update needs the a2 slice and the W3 tile in LDS");
+    float* Ws = smf + 7 * 16 * F1F_AS;  // [224][64]: the updated tile
+    const AdamCoef c = f32_adam_coef(ad);
+    // part p: rows [32 p, 32 p + 32) of the slice; thread t owns row 32 p + (t >> 4), float4 column t & 15
+    const int64_t o0 = (int64_t)(k0 + (t >> 4)) * 1024 + nb * 64 + 4 * (t & 15);
+    float* wsp = Ws + (t >> 4) * F1F_WS + 4 * (t & 15);
+    float4 P[3], Gv[3], M[3], V[3];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int64_t o = o0 + (int64_t)p * 32 * 1024;
+      P[p] = *reinterpret_cast<const float4*>(w3 + o);
+      Gv[p] = *reinterpret_cast<const float4*>(ad.g + o);
+      M[p] = *reinterpret_cast<const float4*>(ad.m + o);
+      V[p] = *reinterpret_cast<const float4*>(ad.v + o);
+    }
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = t + 512 * it;
+      if (i < NCH) {
+        const int r = i / 56, cc = i - 56 * r;
+        *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
+      }
+    }
+    auto update = [&](int p, int s) {
+      const int64_t o = o0 + (int64_t)p * 32 * 1024;
+      adam4_f32(P[s], M[s], V[s], Gv[s], c);
+      *reinterpret_cast<float4*>(w3 + o) = P[s];
+      *reinterpret_cast<float4*>(ad.m + o) = M[s];
+      *reinterpret_cast<float4*>(ad.v + o) = V[s];
+      *reinterpret_cast<float4*>(wsp + p * 32 * F1F_WS) = P[s];
+    };
+    update(0, 0);
+    __syncthreads();
+    // part p (compile-time, so the q range of the MFMA core is static)
+    auto part = [&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      if constexpr (p + 2 < 7) {
+        constexpr int s = (p + 2) % 3;
+        const int64_t o = o0 + (int64_t)(p + 2) * 32 * 1024;
+        P[s] = *reinterpret_cast<const float4*>(w3 + o);
+        Gv[s] = *reinterpret_cast<const float4*>(ad.g + o);
+        M[s] = *reinterpret_cast<const float4*>(ad.m + o);
+        V[s] = *reinterpret_cast<const float4*>(ad.v + o);
+      }
+#pragma unroll
+      for (int q = 2 * p; q < 2 * p + 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wa[4 * q + j] = Ws[(16 * q + 4 * lg + j) * F1F_WS + nt * 16 + lr];
+      if (sh == 0)
+        f1f_mma<NT0, 2 * p, 2 * p + 2>(wa, bp, acc);
+      else
+        f1f_mma<NT1, 2 * p, 2 * p + 2>(wa, bp, acc);
+      if constexpr (p + 1 < 7) update(p + 1, (p + 1) % 3);
+      __syncthreads();
+    };
+    part(std::integral_constant<int, 0>{});
+    part(std::integral_constant<int, 1>{});
+    part(std::integral_constant<int, 2>{});
+    part(std::integral_constant<int, 3>{});
+    part(std::integral_constant<int, 4>{});
+    part(std::integral_constant<int, 5>{});
+    part(std::integral_constant<int, 6>{});
+  }
+  const int ntl = sh == 0 ? NT0 : NT1;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int tt = sh + 2 * u, m = tt * 16 + lr;
+    if (u < ntl && m < B)
+      *reinterpret_cast<float4*>(zpart + ((int64_t)ks * B + m) * 1024 + nb * 64 + nt * 16 + 4 * lg) =
+          make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+  }
+}
+
 // ------------------------------------------------------------------------------------------ //
 // head: one block per sample b, 256 threads x 4 features (K9-K11 of SURVEY.md §2.5):
 //   z = sum of the 14 slabs + b3; h = dropout(relu(z)); logits = h W4 + b4; softmax-xent;
@@ -614,10 +771,12 @@ void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const 
     kern<<<dim3(16, F1F_KS), 512, lds, stream>>>(a2.data_ptr<float>(), w3.data_ptr<float>(), zpart.data_ptr<float>(),
                                                  B, ad);
   };
-#define F1F_CASE(T)                                           \
-  case T:                                                     \
-    if (ad.nblk > 0) launch(f32_fc1_fwd_kernel<T, true>);     \
-    else launch(f32_fc1_fwd_kernel<T, false>);                \
+  // MIHVD_F32_F1F=0 selects the earlier form (whole-tile update, then the MFMAs) for comparison
+  const bool v2 = env_knob("MIHVD_F32_F1F", 1) != 0;
+#define F1F_CASE(T)                                                                                 \
+  case T:                                                                                           \
+    if (ad.nblk > 0) v2 ? launch(f32_fc1_fwd2_kernel<T, true>) : launch(f32_fc1_fwd_kernel<T, true>); \
+    else v2 ? launch(f32_fc1_fwd2_kernel<T, false>) : launch(f32_fc1_fwd_kernel<T, false>);           \
     break;
   switch (mt) {
     F1F_CASE(1)
@@ -628,7 +787,7 @@ void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const 
     F1F_CASE(6)
     F1F_CASE(7)
     default:
-      launch(f32_fc1_fwd_kernel<8, false>);
+      v2 ? launch(f32_fc1_fwd2_kernel<8, false>) : launch(f32_fc1_fwd_kernel<8, false>);
   }
 #undef F1F_CASE
 }

@@ -118,6 +118,10 @@ def main():
         "conv2_bwd [wgrad role only]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd"]),
         "fc1_bwd [dgrad role only]": ({"MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [wgrad role only]": ({"MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
+        "fc1_fwd [earlier form]": ({"MIHVD_F32_F1F": "0"}, ks["fc1_fwd"]),
+        "fc1_fwd+W3 adam [earlier form]": ({"MIHVD_F32_F1F": "0"}, ks["fc1_fwd+W3 adam"]),
+        "fc1_bwd [K-split dgrad form]": ({"MIHVD_F32_F1B_KS": "1"}, ks["fc1_bwd"]),
+        "fc1_bwd [K-split dgrad form, dgrad only]": ({"MIHVD_F32_F1B_KS": "1", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
     }
     for name, (env, fn) in study.items():
         old_env = {k: os.environ.get(k) for k in env}
