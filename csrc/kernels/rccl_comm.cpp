@@ -255,6 +255,21 @@ int64_t rccl_async_error(int64_t h) {
   return e == ncclInProgress ? 0 : (int64_t)e;
 }
 
+// ---- for the native engine (engine.cpp): raw access on the engine's own stream ----
+void* rccl_comm_raw(int64_t h) { return (void*)get(h)->comm; }
+int rccl_comm_world(int64_t h) { return get(h)->world; }
+int rccl_comm_device(int64_t h) { return get(h)->device; }
+
+// 0 on success; otherwise the ncclResult_t with its message in *err
+int rccl_all_reduce_raw(void* buf, size_t count, int dtype, int op, void* comm, hipStream_t stream, std::string* err) {
+  if (count == 0) return 0;
+  Rccl& r = rccl();
+  const ncclResult_t e =
+      r.all_reduce(buf, buf, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, (ncclComm_t)comm, stream);
+  if (e != ncclSuccess && err != nullptr) *err = r.error_string ? r.error_string(e) : "RCCL error";
+  return (int)e;
+}
+
 void rccl_comm_destroy(int64_t h, bool abort) {
   Comm* c = get(h);
   {

@@ -180,7 +180,7 @@ def init(comm=None, process_sets=None, config: Config | None = None):
         _build_subgroups(topo)
         _start_observability(cfg, topo)
         _start_health(topo, backend)
-        if cfg.negotiate and topo.size > 1:
+        if cfg.engine == "native" or (cfg.negotiate and topo.size > 1):
             _start_engine(cfg, topo, backend, device)
         _ctx.initialized = True
         atexit.register(shutdown)
@@ -281,9 +281,20 @@ def _start_health(topo: _env.Topology, backend: str):
 
 
 def _start_engine(cfg: Config, topo: _env.Topology, backend: str, device: torch.device):
-    """Negotiated collectives (``mihvd/parallel/engine.py``): a native Negotiator per rank whose
-    coordinator runs on rank 0, over mihvdrun's store or a store server rank 0 starts here."""
+    """Negotiated collectives. On the RCCL backend (``MIHVD_ENGINE`` auto/native): the native engine
+    (``csrc/kernels/engine.cpp``, a C++ thread that owns an RCCL communicator and a high-priority
+    stream, negotiates over the GPU and fuses into a persistent buffer). Otherwise
+    (``MIHVD_ENGINE=python`` or gloo): ``mihvd/parallel/engine.py``, a native Negotiator per rank
+    whose coordinator runs on rank 0, over mihvdrun's store or a store server rank 0 starts here."""
     import uuid
+
+    if cfg.engine == "native" and backend != "nccl":
+        raise RuntimeError("MIHVD_ENGINE=native needs the nccl (RCCL) backend")
+    if backend == "nccl" and cfg.engine in ("auto", "native"):
+        from .parallel.native_engine import NativeEngine
+
+        _ctx.engine = NativeEngine(cfg, device)
+        return
 
     from ._native import runtime
     from .parallel.engine import Engine

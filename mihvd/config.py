@@ -57,6 +57,7 @@ class Config:
     autotune_log: str = ""                # horovodrun --autotune-log-file: CSV of the candidates
     roctx: bool = False                   # roctx ranges around collectives / steps (rocprofv3 --marker-trace)
     negotiate: bool = False               # route async collectives through the native negotiation engine
+    engine: str = "auto"                  # auto | native (C++ engine thread over RCCL) | python (negotiator + executor thread)
     store: str = "native"                 # rendezvous: native (mihvdrun's C++ store, if present) | torch
     debug_sync: bool = False              # serialized bisection mode: sync after every kernel / collective
     elastic_grace_s: float = 30.0         # elastic: how long a failed collective waits for a new membership
@@ -87,6 +88,7 @@ class Config:
             autotune_log=_get("AUTOTUNE_LOG", "", str, env),
             roctx=_get("ROCTX", False, bool, env),
             negotiate=_get("NEGOTIATE", False, bool, env),
+            engine=_get("ENGINE", "auto", str, env).strip().lower(),
             store=_get("STORE", "native", str, env),
             debug_sync=_get("DEBUG_SYNC", False, bool, env),
             elastic_grace_s=_get("ELASTIC_GRACE_SECONDS", 30.0, float, env),

@@ -173,12 +173,10 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
         # at size 1 the wire round trip still runs (Horovod compresses at any size)
         wire = hip_pack(compression, tensor, prescale_factor, out=wire_buf)
         scale = postscale_factor / n if op == ReduceOp.Average else postscale_factor
-        if n == 1:
+        if n == 1 and not getattr(ctx.engine, "world_one", False):
             work = None
-        elif ctx.engine is not None:
-            work = ctx.engine.allreduce(f"allreduce.{name}", wire, _torch_op(op), group, fuse_extra=("hip-pack",))
         else:
-            work = dist.all_reduce(wire, op=_torch_op(op), group=group, async_op=True)
+            work = _engine_allreduce(ctx, f"allreduce.{name}", wire, _torch_op(op), group, ("hip-pack",))
         return _register(work, out, lambda _o, wire=wire, out=out, scale=scale: hip_unpack(wire, out, scale),
                          f"allreduce.{name}")
     wire, cctx = compression.compress(tensor)
@@ -187,13 +185,10 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
         wire = out
     if prescale_factor != 1.0:
         wire.mul_(prescale_factor)
-    if n == 1:
+    if n == 1 and not getattr(ctx.engine, "world_one", False):
         work = None
-    elif ctx.engine is not None:
-        # negotiated: launched by the engine thread in the coordinator's order, possibly fused
-        work = ctx.engine.allreduce(f"allreduce.{name}", wire, _torch_op(op), group)
     else:
-        work = dist.all_reduce(wire, op=_torch_op(op), group=group, async_op=True)
+        work = _engine_allreduce(ctx, f"allreduce.{name}", wire, _torch_op(op), group, ())
     scale = postscale_factor / n if op == ReduceOp.Average else postscale_factor
 
     def post(_o, wire=wire, cctx=cctx, out=out, scale=scale):
@@ -205,6 +200,21 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
         return out
 
     return _register(work, out, post, f"allreduce.{name}")
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _engine_allreduce(ctx, name, wire, torch_op, group, fuse_extra):
+    """Negotiated (launched by the engine thread in an order every rank agrees on, possibly fused)
+    when an engine runs and the call is not being captured into a HIP graph; else on the process
+    group. The native engine declines what it does not handle (sub-groups, other ops)."""
+    if ctx.engine is not None and not _capturing():
+        work = ctx.engine.allreduce(name, wire, torch_op, group, fuse_extra=fuse_extra)
+        if work is not None:
+            return work
+    return dist.all_reduce(wire, op=torch_op, group=group, async_op=True)
 
 
 def adasum_dispatch_(flat: torch.Tensor, segments=None):

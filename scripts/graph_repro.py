@@ -133,7 +133,7 @@ VARIANTS = {
 }
 
 
-def run(name, steps, graph, dropout_eval=False):
+def run(name, steps, graph, dropout_eval=False, sync_each=True):
     torch.manual_seed(0)
     model = VARIANTS[name]().cuda()
     if dropout_eval:
@@ -166,21 +166,35 @@ def run(name, steps, graph, dropout_eval=False):
     gr = torch.cuda.CUDAGraph()
     with torch.cuda.graph(gr):
         out = step()
+    if sync_each:
+        for _ in range(steps - 3):
+            gr.replay()
+            losses.append(float(out))
+        return losses, model
+    # back-to-back replays (the stress bench's pattern): each loss is cloned on the stream behind
+    # its replay, read only at the end
+    outs = []
     for _ in range(steps - 3):
         gr.replay()
-        losses.append(float(out))
+        outs.append(out.detach().clone())
+    losses += [float(o) for o in outs]
     return losses, model
 
 
 def main():
+    global B, S
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--batch", type=int, default=B)
+    ap.add_argument("--seq", type=int, default=S)
+    ap.add_argument("--no-sync", action="store_true", help="replays back to back, losses read at the end")
     args = ap.parse_args()
+    B, S = args.batch, args.seq
     res = {}
     for name in args.variants.split(","):
         le, me = run(name, args.steps, graph=False)
-        lg, mg = run(name, args.steps, graph=True)
+        lg, mg = run(name, args.steps, graph=True, sync_each=not args.no_sync)
         finite = all(math.isfinite(v) for v in lg) and all(torch.isfinite(p).all() for p in mg.parameters())
         pd = max(((a - b).norm() / (b.norm() + 1e-12)).item() for a, b in zip(mg.parameters(), me.parameters()))
         rel = max(abs(a - b) / max(abs(b), 1e-6) for a, b in zip(lg, le))

@@ -38,3 +38,27 @@ def test_native_rccl_comm_one_gpu(tmp_path):
     # the same collective-free arithmetic (world-1 sums are exact): the updates agree to fp32
     # summation order (the collective path applies the dense/kernel update in a different launch)
     assert r["trainer_rel_diff"] < 1e-5, r
+
+
+def test_native_engine_one_gpu(tmp_path):
+    """The C++ engine thread (csrc/kernels/engine.cpp) at world size 1: negotiation cycles, fusion,
+    in-place big tensors, stream ordering, DistributedOptimizer bit-equality, clean shutdown."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    out = tmp_path / "eng.json"
+    env = dict(os.environ, PYTHONPATH=ROOT, MIHVD_ENGINE="native", MIHVD_FUSION_THRESHOLD=str(1 << 20))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", "29563", os.path.join(ROOT, "tests", "workers", "native_engine_worker.py"),
+           str(out)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = json.loads(out.read_text())
+    assert r["engine"] == "NativeEngine" and r["world"] == 1, r
+    assert r["values_exact"] and r["small_exact"] and r["big_exact"], r
+    assert r["small_tensors"] == 24 and r["small_collectives"] < 24, r  # fused
+    assert r["optimizer_bitwise"] and r["optimizer_collectives"] >= 6, r
+    assert r["stats"]["cycles"] > 0 and r["stopped"], r

@@ -645,3 +645,42 @@ def test_synthetic_shards_share_class_templates():
     other = np.corrcoef(ma.reshape(10, -1), mc.reshape(10, -1))[np.arange(10), 10 + np.arange(10)]
     assert same.min() > 0.95, same
     assert other.mean() < 0.5, other
+
+
+def _engine_ctrl(world, counts, hashes_by_rank):
+    """Summed control vector of the native engine (csrc/kernels/engine.cpp) for S slots."""
+    S = len(counts)
+    v = np.zeros(2 + 2 * S, dtype=np.int64)
+    v[2:2 + S] = counts
+    v[2 + S:] = np.sum(hashes_by_rank, axis=0)
+    return ((v + 2 ** 31) % 2 ** 32 - 2 ** 31).astype(np.int32)  # int32 wrap-around, as RCCL's sum
+
+
+def test_native_engine_plan_fusion_and_stalls():
+    """The engine's planning step (the same C++ function the engine thread runs on the summed
+    control vector): ready slots fused in slot order by (dtype, op) up to the threshold, tensors
+    above the threshold alone, slots pending on some ranks reported, signature mismatch fatal."""
+    if not _native.load_kernels():
+        pytest.skip("kernel library not built")
+    from mihvd.parallel.native_engine import plan, signature_hash
+
+    world = 4
+    h = [signature_hash(f"g{i}", 6, 100, 0) for i in range(7)]
+    nbytes = [400, 400, 400, 5000, 400, 400, 400]
+    keys = [1, 1, 1, 1, 1, 2, 1]
+    counts = [4, 4, 0, 4, 4, 4, 2]
+    per_rank = [[h[s] if (counts[s] == world or (counts[s] and r < counts[s])) else 0 for s in range(7)]
+                for r in range(world)]
+    groups, partial = plan(_engine_ctrl(world, counts, per_rank), world, h, nbytes, keys, threshold=1000)
+    # slot 2 has nothing pending; slot 3 exceeds the threshold (alone); slot 5 differs in key; slot 6 is partial
+    assert groups == [[0, 1], [3], [4], [5]], groups
+    assert partial == [6]
+    # a rank that put a different signature in a full slot: every rank detects it
+    bad = [list(r) for r in per_rank]
+    bad[2][1] = signature_hash("other", 6, 100, 0)
+    with pytest.raises(RuntimeError, match="different collectives"):
+        plan(_engine_ctrl(world, counts, bad), world, h, nbytes, keys, threshold=1000)
+    # the fused groups never exceed the threshold
+    many = [signature_hash(f"m{i}", 6, 64, 0) for i in range(10)]
+    groups, _ = plan(_engine_ctrl(2, [2] * 10, [many, many]), 2, many, [300] * 10, [0] * 10, threshold=1000)
+    assert groups == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9]]
