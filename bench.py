@@ -171,6 +171,10 @@ def make_fused_step(args, hvd, device):
 
 def main():
     args = parse()
+    if args.impl == "fused":
+        # the fused trainer issues its own collectives (in its HIP graph): no engine thread cycling
+        # beside the timed steps
+        os.environ.setdefault("MIHVD_ENGINE", "torch")
     import mihvd.torch as hvd
 
     hvd.init()

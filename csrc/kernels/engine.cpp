@@ -294,7 +294,9 @@ class Engine {
     bool stop_seen = false;
     try {
       while (!stop_seen) {
-        next += std::chrono::microseconds((int64_t)(cycle_ * 1e6));
+        // a world with nothing pending anywhere for 100 cycles backs off to 10x the cycle time
+        // (every rank sees the same summed vectors, so all back off together); work ends it
+        next += std::chrono::microseconds((int64_t)(cycle_ * 1e6 * (idle_ > 100 ? 10 : 1)));
         std::this_thread::sleep_until(next);
         if (Clock::now() > next + std::chrono::milliseconds(50)) next = Clock::now();
         bool stopping;
@@ -332,6 +334,9 @@ class Engine {
           ++cycles_;
         }
         if (hv[0] == world_) stop_seen = true;  // every rank asked to stop with nothing pending
+        bool idle = true;
+        for (int s = 0; s < S && idle; ++s) idle = hv[2 + s] == 0;
+        idle_ = idle ? idle_ + 1 : 0;
         // 3. plan + execute
         std::vector<uint32_t> hash(S, 0);
         std::vector<int64_t> bytes(S, 0), key(S, 0);
@@ -473,6 +478,7 @@ class Engine {
   int64_t next_id_ = 1;
   bool stopping_ = false;
   std::string fatal_;
+  int64_t idle_ = 0;
   int64_t cycles_ = 0, collectives_ = 0, tensors_ = 0, fused_bytes_ = 0, stalls_warned_ = 0;
   std::thread thread_;
 };

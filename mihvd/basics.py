@@ -180,7 +180,11 @@ def init(comm=None, process_sets=None, config: Config | None = None):
         _build_subgroups(topo)
         _start_observability(cfg, topo)
         _start_health(topo, backend)
-        if cfg.engine == "native" or (cfg.negotiate and topo.size > 1):
+        # Horovod's background engine: on by default on the RCCL backend at N > 1 (the native C++
+        # engine), opt-in elsewhere (MIHVD_NEGOTIATE=1: the store-negotiated python executor);
+        # MIHVD_ENGINE=torch turns it off (allreduces straight on the process group)
+        if cfg.engine != "torch" and (cfg.engine == "native" or (
+                topo.size > 1 and (cfg.negotiate or cfg.engine == "python" or (cfg.engine == "auto" and backend == "nccl")))):
             _start_engine(cfg, topo, backend, device)
         _ctx.initialized = True
         atexit.register(shutdown)

@@ -133,12 +133,15 @@ VARIANTS = {
 }
 
 
+OPTS = {"lr": 1e-3, "wd": 0.0, "captured_step": False}
+
+
 def run(name, steps, graph, dropout_eval=False, sync_each=True):
     torch.manual_seed(0)
     model = VARIANTS[name]().cuda()
     if dropout_eval:
         model.eval()
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, capturable=True)
+    opt = torch.optim.AdamW(model.parameters(), lr=OPTS["lr"], weight_decay=OPTS["wd"], capturable=True)
     g = torch.Generator(device="cuda").manual_seed(1)
     ids = torch.randint(0, V, (B, S), device="cuda", generator=g)
     labels = torch.where(torch.rand(B, S, device="cuda", generator=g) < 0.15, ids, torch.full_like(ids, -100))
@@ -156,6 +159,18 @@ def run(name, steps, graph, dropout_eval=False, sync_each=True):
     if not graph:
         for _ in range(steps):
             losses.append(float(step()))
+        return losses, model
+    if OPTS["captured_step"]:  # mihvd.graphs.CapturedStep (the stress bench's capture path)
+        import os
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from mihvd.graphs import CapturedStep
+
+        cs = CapturedStep(step, warmup=3)
+        losses += [None] * 3  # its warm-up losses are not returned
+        outs = [cs().clone() for _ in range(steps - 3)]
+        losses += [float(o) for o in outs]
         return losses, model
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -189,15 +204,28 @@ def main():
     ap.add_argument("--batch", type=int, default=B)
     ap.add_argument("--seq", type=int, default=S)
     ap.add_argument("--no-sync", action="store_true", help="replays back to back, losses read at the end")
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--wd", type=float, default=0.0)
+    ap.add_argument("--captured-step", action="store_true", help="capture with mihvd.graphs.CapturedStep")
+    ap.add_argument("--hvd-init", action="store_true", help="mihvd.init() first (health monitor, observability)")
     args = ap.parse_args()
+    OPTS.update(lr=args.lr, wd=args.wd, captured_step=args.captured_step)
+    if args.hvd_init:
+        import os
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import mihvd
+
+        mihvd.init()
     B, S = args.batch, args.seq
     res = {}
     for name in args.variants.split(","):
         le, me = run(name, args.steps, graph=False)
         lg, mg = run(name, args.steps, graph=True, sync_each=not args.no_sync)
-        finite = all(math.isfinite(v) for v in lg) and all(torch.isfinite(p).all() for p in mg.parameters())
+        finite = all(math.isfinite(v) for v in lg if v is not None) and all(torch.isfinite(p).all() for p in mg.parameters())
         pd = max(((a - b).norm() / (b.norm() + 1e-12)).item() for a, b in zip(mg.parameters(), me.parameters()))
-        rel = max(abs(a - b) / max(abs(b), 1e-6) for a, b in zip(lg, le))
+        rel = max(abs(a - b) / max(abs(b), 1e-6) for a, b in zip(lg, le) if a is not None)
         res[name] = {"finite": finite, "loss_rel_diff": rel, "param_rel_diff": pd, "eager": le, "graph": lg}
         print(json.dumps({name: {k: v for k, v in res[name].items() if k not in ("eager", "graph")}}), flush=True)
     print(json.dumps(res))

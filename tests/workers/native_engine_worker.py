@@ -64,20 +64,33 @@ def main(out):
     hvd.synchronize(hvd.allreduce_async_(big, name="big", op=hvd.Sum))
     res["big_exact"] = bool(torch.equal(big, ref))
 
-    # 4. DistributedOptimizer through the engine vs plain training (world 1: identical arithmetic)
+    # 4. DistributedOptimizer through the engine vs plain training (world 1: identical arithmetic).
+    #    An MLP (deterministic GEMMs): bit for bit; the CNN (MIOpen's weight-gradient convolutions
+    #    are not run-to-run deterministic): to fp32 rounding.
     from mihvd.models.mnist import MNISTConvNet
 
     X = torch.randn(6, 32, 784, generator=g).to(dev)
     Y = torch.randint(0, 10, (6, 32), generator=g).to(dev)
-    m1 = MNISTConvNet(impl="torch", seed=1).to(dev)
-    m2 = MNISTConvNet(impl="torch", seed=1).to(dev)
+
+    def mlp():
+        torch.manual_seed(1)
+        return torch.nn.Sequential(torch.nn.Linear(784, 256), torch.nn.ReLU(), torch.nn.Linear(256, 10)).to(dev)
+
     st2 = eng.stats()
+    m1, m2 = mlp(), mlp()
     o1 = hvd.DistributedOptimizer(torch.optim.Adam(m1.parameters(), lr=1e-3), named_parameters=m1.named_parameters())
     p1 = train(m1, o1, X, Y, 6)
     p2 = train(m2, torch.optim.Adam(m2.parameters(), lr=1e-3), X, Y, 6)
+    res["optimizer_bitwise"] = bool(torch.equal(p1, p2))
+    c1 = MNISTConvNet(impl="torch", seed=1).to(dev).eval()  # dropout off: the same function twice
+    c2 = MNISTConvNet(impl="torch", seed=1).to(dev).eval()
+    oc = hvd.DistributedOptimizer(torch.optim.Adam(c1.parameters(), lr=1e-3), named_parameters=c1.named_parameters(),
+                                  backward_passes_per_step=1)
+    q1 = train(c1, oc, X, Y, 6)
+    q2 = train(c2, torch.optim.Adam(c2.parameters(), lr=1e-3), X, Y, 6)
+    res["cnn_rel_diff"] = float((q1 - q2).norm() / q2.norm())
     torch.cuda.synchronize()
     st3 = eng.stats()
-    res["optimizer_bitwise"] = bool(torch.equal(p1, p2))
     res["optimizer_collectives"] = st3["collectives"] - st2["collectives"]
     res["stats"] = st3
     hvd.shutdown()
