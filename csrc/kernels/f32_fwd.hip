@@ -47,60 +47,7 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ a1, uint8_t* __restrict__ idx1,
     int B) {
   __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
-  const int q = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
-  int row = b;
-  if (rows != nullptr) {
-    const int64_t step = state ? state[ST_FWD] : 0;
-    row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-  }
-  const float* xi = x + (int64_t)row * 784;
-  float xv[4];
-#pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int i = t + 256 * it, Y = (i >> 5) - 2, X = (i & 31) - 2;
-    const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
-    xv[it] = mask_f(xi[in ? Y * 28 + X : 0], in);
-  }
-  float wb[2][7];
-  int toff[7];
-#pragma unroll
-  for (int s = 0; s < 7; ++s) {
-    const int k = 4 * s + lg, kc = min(k, 24);
-    toff[s] = (kc / 5) * 32 + (kc % 5);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) wb[nt][s] = mask_f(w1[kc * 32 + 16 * nt + lr], k < 25);
-  }
-  const float bias0 = b1[lr], bias1 = b1[16 + lr];
-#pragma unroll
-  for (int it = 0; it < 4; ++it) xim[t + 256 * it] = xv[it];
-  __syncthreads();
-  const int tile_end = min(49, 13 * q + 13);
-  for (int tile = 13 * q + wave; tile < tile_end; tile += 4) {  // wave-uniform
-    const int wa = 4 * tile + (lr >> 2), d = lr & 3;
-    const int pya = wa / 14, pxa = wa - pya * 14;
-    const int base = (2 * pya + (d >> 1)) * 32 + 2 * pxa + (d & 1);
-    float av[7];
-#pragma unroll
-    for (int s = 0; s < 7; ++s) av[s] = xim[base + toff[s]];
-    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-    for (int s = 0; s < 7; ++s) {
-      c0 = mfma4(av[s], wb[0][s], c0);
-      c1 = mfma4(av[s], wb[1][s], c1);
-    }
-    // C[row 4lg + i][col lr] = pixel i of window 4 * tile + lg, channel 16 nt + lr
-    const int win = 4 * tile + lg, py = win / 14, px = win - py * 14;
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const f32x4 c = nt ? c1 : c0;
-      int best;
-      const float m = pool4(c, best);
-      const int64_t o = (((int64_t)b * 14 + py) * 14 + px) * 32 + 16 * nt + lr;
-      a1[o] = fmaxf(m + (nt ? bias1 : bias0), 0.f);
-      idx1[o] = (uint8_t)best;
-    }
-  }
+  f32_conv1_block<false>(blockIdx.x, blockIdx.y, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim);
 }
 
 // ------------------------------------------------------------------------------------------ //

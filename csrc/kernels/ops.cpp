@@ -109,7 +109,9 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
                      const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
                      const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, int64_t o_w1,
                      int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo, int64_t fc_hi, double lr, double b1,
-                     double b2, double eps, double grad_scale, int64_t rule);
+                     double b2, double eps, double grad_scale, int64_t rule, const c10::optional<at::Tensor>& c1_x,
+                     const c10::optional<at::Tensor>& c1_rows, const c10::optional<at::Tensor>& c1_a1,
+                     const c10::optional<at::Tensor>& c1_idx1, const c10::optional<at::Tensor>& c1_sync);
 int64_t f32_db2_rows(int64_t B);
 at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel);
 int64_t f32_wgrad_groups(int64_t B);
@@ -259,9 +261,11 @@ void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, con
 void f32_conv_reduce_op(const Tensor& slab, const Tensor& cpart, const Tensor& db2p, Tensor gW2, Tensor gW1, Tensor gb1,
                         Tensor gb2, const OptT& params, const OptT& grads, const OptT& m, const OptT& v,
                         const OptT& state, int64_t o_w1, int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo,
-                        int64_t fc_hi, double lr, double b1, double b2, double eps, double grad_scale, int64_t rule) {
+                        int64_t fc_hi, double lr, double b1, double b2, double eps, double grad_scale, int64_t rule,
+                        const OptT& c1_x, const OptT& c1_rows, const OptT& c1_a1, const OptT& c1_idx1,
+                        const OptT& c1_sync) {
   mihvd::f32_conv_reduce(slab, cpart, db2p, gW2, gW1, gb1, gb2, params, grads, m, v, state, o_w1, o_b1, o_w2, o_b2,
-                         fc_lo, fc_hi, lr, b1, b2, eps, grad_scale, rule);
+                         fc_lo, fc_hi, lr, b1, b2, eps, grad_scale, rule, c1_x, c1_rows, c1_a1, c1_idx1, c1_sync);
 }
 }  // namespace
 
@@ -328,7 +332,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
         "Tensor(d!) gb2, Tensor(e!)? params=None, Tensor? grads=None, Tensor(f!)? m=None, Tensor(g!)? v=None, "
         "Tensor(s!)? state=None, int o_w1=0, int o_b1=0, int o_w2=0, int o_b2=0, int fc_lo=0, int fc_hi=0, "
-        "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0) -> ()");
+        "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0, Tensor? c1_x=None, "
+        "Tensor? c1_rows=None, Tensor(h!)? c1_a1=None, Tensor(i!)? c1_idx1=None, Tensor(j!)? c1_sync=None) -> ()");
   m.def("f32_db2_rows(int B) -> int", &mihvd::f32_db2_rows);
   m.def("f32_stamps_enable(int n_blocks, int kernel=0) -> Tensor", &mihvd::f32_stamps_enable);
   m.def("f32_wgrad_groups(int B) -> int", &mihvd::f32_wgrad_groups);

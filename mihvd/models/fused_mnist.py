@@ -272,6 +272,12 @@ class FusedMNISTTrainer:
         if self.f32_w3 == "fc1" and B > 112:  # the fused update keeps the a2 slice + a W3 tile in LDS
             self.f32_w3 = "tail"
         self._w3_pending = False
+        # graph-replayed world-size-1 fp32 steps: the next step's conv1 runs inside this step's
+        # f32_conv_reduce launch (after W1/b1's Adam and the step bump; f32_bwd.hip), so only the
+        # first step of a replay launches conv1 on its own (MIHVD_F32_CONV1_FUSE=0: always separate)
+        self.f32_conv1_fuse = self.f32 and os.environ.get("MIHVD_F32_CONV1_FUSE", "1") != "0"
+        self._c1_ready = False
+        self._c1_sync = torch.zeros(4, device=dev, dtype=torch.int32) if self.f32 else None
         if self.f32:
             ops = self.ops
             self.a1 = torch.empty(B, 14, 14, 32, **f32)
@@ -583,7 +589,11 @@ class FusedMNISTTrainer:
         s3 = slice(W3_START, FLAT_NUMEL)
         if self.shard_w3:
             return self._launch_step_f32_shard(x, rows, labels)
-        o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1, self.idx1)
+        if self._c1_ready:
+            self._c1_ready = False  # the previous step's conv_reduce computed this step's conv1
+        else:
+            o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
+                            self.idx1)
         if self._w3_pending and self.f32_w3 == "tail":
             # the previous step's dense/kernel Adam update (98 % of the optimizer's bytes) streams in
             # tail blocks of this MFMA-bound launch; fc1_fwd below is its first reader
@@ -622,10 +632,14 @@ class FusedMNISTTrainer:
                  G("conv_layer2/conv2d/bias"))
         if self.f32_fused_opt and not self.collectives:
             # gradient reduction + Adam of every parameter but dense/kernel + the step bump, one launch
+            # (+ the next step's conv1 when the steps are being captured back to back)
+            c1 = self.f32_conv1_fuse and torch.cuda.is_current_stream_capturing()
             o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv, self.params, self.grads, self.m, self.v, st,
                               SEGMENTS["conv_layer1/conv2d/kernel"][0], SEGMENTS["conv_layer1/conv2d/bias"][0],
                               SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0],
-                              FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
+                              FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule,
+                              *((x, rows, self.a1, self.idx1, self._c1_sync) if c1 else ()))
+            self._c1_ready = c1
         else:
             o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
             if overlap:
@@ -904,6 +918,7 @@ class FusedMNISTTrainer:
         """Make the current stream wait for any side-stream work of the last step, and apply a
         deferred optimizer update (the step's results are then complete)."""
         self._flush_w3()
+        self._c1_ready = False  # a step launched after this one recomputes its conv1 (idempotent)
         if self._fc_update_pending:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             self._fc_update_pending = False
@@ -1120,6 +1135,9 @@ class FusedMNISTTrainer:
         if not self.f32 and self.fused_opt and int(self.ops.conv_barrier_error(True)) != 0:
             raise RuntimeError("fused step: a conv2_bwd LDS barrier timed out (a broken wave count); the conv "
                                "gradients and optimizer state of that step are invalid")
+        if self._c1_sync is not None and int(self._c1_sync[2]) != 0:
+            raise RuntimeError("fused fp32 step: the next step's conv1 in f32_conv_reduce timed out waiting for the "
+                               "W1/b1 update; a1 of that step is invalid")
         if getattr(self, "fold_reduce", False) and int(self.fold_sync[2]) != 0:
             raise RuntimeError("fused step: the folded gradient reduction timed out waiting for the conv blocks "
                                "(a conv block was not resident); parameters of that step are invalid")

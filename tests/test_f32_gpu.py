@@ -302,3 +302,37 @@ def test_f32_fused_optimizer_matches_separate_adam(ops, monkeypatch, w3_mode):
     assert a.global_step == b.global_step == 2 + 21
     for name in ("params", "m", "v", "state"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+def test_f32_next_conv1_in_reduce_launch_is_bitwise(ops, monkeypatch):
+    """Graph-replayed steps with the next step's conv1 inside f32_conv_reduce (MIHVD_F32_CONV1_FUSE=1:
+    conv1 blocks acquire the W1/b1 update and the step bump of the same launch) train bit for bit like
+    separate conv1 launches, across replays, an eager step in between and a shorter graph; the
+    launch's sync words are back to zero after every replay and never timed out."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    (x, y), _ = synthetic_mnist(n_train=2000, n_test=10, seed=8)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    trs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MIHVD_F32_CONV1_FUSE", fuse)
+        tr = FusedMNISTTrainer(batch_size=100, lr=2e-3, seed=3, device="cuda", precision="fp32")
+        assert tr.f32_conv1_fuse == (fuse == "1")
+        tr.set_device_dataset(X, Y, seed=1)
+        tr.build_graph(steps_per_replay=8)
+        tr.build_graph(steps_per_replay=3, warmup=0, primary=False)
+        for _ in range(3):
+            tr.run_graph()
+        tr.device_step()
+        tr.run_graph(3)
+        tr.run_graph()
+        trs.append(tr)
+    torch.cuda.synchronize()
+    a, b = trs
+    assert a.global_step == b.global_step
+    for name in ("params", "m", "v", "state", "a1"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert a._c1_sync.tolist() == [0, 0, 0, 0], a._c1_sync.tolist()
+    a.check_xgmi()
