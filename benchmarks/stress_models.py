@@ -86,7 +86,8 @@ def main():
         from mihvd.models.bert import BertConfig, BertForMaskedLM, synthetic_mlm_batch
 
         B = args.batch_size or 16
-        c = BertConfig(max_len=max(512, args.seq_len), attn_impl=os.environ.get("MIHVD_BERT_ATTN", "sdpa"))
+        c = BertConfig(max_len=max(512, args.seq_len), attn_impl=os.environ.get("MIHVD_BERT_ATTN", "sdpa"),
+                       embedding_impl=os.environ.get("MIHVD_BERT_EMBEDDING", "gather"))
         model = BertForMaskedLM(c).to(dev)
         ids, labels = synthetic_mlm_batch(B, args.seq_len, c.vocab_size, dev, generator=g)
         from mihvd.models.bert import masked_positions
@@ -123,15 +124,13 @@ def main():
         opt.step()
         return loss
 
-    if args.graph and args.model == "bert-base" and os.environ.get("MIHVD_STRESS_FORCE_GRAPH") != "1":
-        # Whole-step capture of BERT-base turns the loss NaN after the first replay that follows
-        # the warm-up replays on this PyTorch-ROCm build — also with stock torch.optim.AdamW
-        # (capturable=True), without mihvd's DistributedOptimizer (--no-dp) and with matmul/softmax
-        # attention instead of SDPA (MIHVD_BERT_ATTN=math), so it is not mihvd's engine; eager is
-        # also the faster mode here (20.4 vs 25.7 ms/step). MIHVD_STRESS_FORCE_GRAPH=1 runs it anyway.
-        raise SystemExit("stress_models: --graph is not supported for bert-base on this PyTorch-ROCm build "
-                         "(NaN after the first post-warm-up replay, reproducible with stock torch only); "
-                         "set MIHVD_STRESS_FORCE_GRAPH=1 to run it anyway")
+    if args.graph and args.model == "bert-base" and c.embedding_impl == "embedding" and \
+            os.environ.get("MIHVD_STRESS_FORCE_GRAPH") != "1":
+        # F.embedding's backward (sort + rocprim unique_by_key) faults when replayed from a HIP
+        # graph with MLM ids on this ROCm build (scripts/embedding_graph_repro.py, stock torch only);
+        # the default gather lookups (index_select: index_add_ backward) replay correctly
+        raise SystemExit("stress_models: --graph with MIHVD_BERT_EMBEDDING=embedding faults on this ROCm build "
+                         "(scripts/embedding_graph_repro.py); use the default gather lookups")
     if args.graph:
         from mihvd.graphs import CapturedStep
 

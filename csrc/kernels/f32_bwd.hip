@@ -766,12 +766,14 @@ struct F32Conv1Next {
 constexpr int CR_PRODUCERS = CR_CP + 1;
 
 __device__ __forceinline__ void c1n_arrive(const F32Conv1Next& c1) {
-  // every wave's stores of this block are complete and written back before the arrival
-  __threadfence();
+  // the barrier completes every wave's stores (to this XCD's L2); thread 0's release RMW writes
+  // them back (one L2 writeback per producer block). The last arriver acquires the others'
+  // releases once and publishes the ready word.
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(c1.sync, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const int prev = __hip_atomic_fetch_add(c1.sync, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == CR_PRODUCERS - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __hip_atomic_store(c1.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c1.sync + 1, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -818,9 +820,11 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
   const int bid = blockIdx.x, t = threadIdx.x;
   const bool opt = sa.a.nblk > 0;
   if (c1.nblk > 0 && bid >= CR_FC0 + n_fc) {  // the next step's conv1 (opt is on: state, W1 updates)
+    // relaxed agent-scope polling (an acquire per poll would invalidate the L2 under every other
+    // block of the launch); W1/b1/the counter are then read with agent-scope (coherent) loads
     if (t == 0) {
       int spins = 0;
-      while (__hip_atomic_load(c1.sync + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      while (__hip_atomic_load(c1.sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > (1 << 22)) {
           __hip_atomic_fetch_or(c1.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -829,6 +833,7 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       }
     }
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // no load below is hoisted above the poll
     const int cb = bid - CR_FC0 - n_fc;
     f32_conv1_block<true>(cb & 3, cb >> 2, c1.x, c1.rows, c1.n_pool, sa.a.state, sa.a.p + sa.o_w1, sa.a.p + sa.o_b1,
                           c1.a1, c1.idx1, c1.B, reinterpret_cast<float*>(red));

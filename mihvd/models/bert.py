@@ -29,6 +29,11 @@ class BertConfig:
     attn_dropout: float | None = None  # attention-probability dropout (None: ``dropout``)
     attn_impl: str = "sdpa"  # "sdpa" (F.scaled_dot_product_attention) | "math" (matmul/softmax ops)
     eps: float = 1e-12
+    # "gather": lookups as index_select, whose backward is a scatter-add (index_add_); "embedding":
+    # F.embedding, whose backward sorts the ids and segments them with rocprim's unique_by_key —
+    # that partition kernel faults (memory aperture violation) when a whole BERT step is replayed
+    # from a HIP graph on this ROCm build with MLM data (many repeated [MASK] ids)
+    embedding_impl: str = "gather"
 
 
 class BertLayer(nn.Module):
@@ -86,6 +91,11 @@ class BertForMaskedLM(nn.Module):
         if isinstance(m, nn.Linear) and m.bias is not None:
             nn.init.zeros_(m.bias)
 
+    def _lookup(self, emb: nn.Embedding, ids: torch.Tensor) -> torch.Tensor:
+        if self.c.embedding_impl == "embedding":
+            return emb(ids)
+        return emb.weight.index_select(0, ids.reshape(-1)).view(*ids.shape, emb.weight.shape[1])
+
     def forward(self, ids, labels=None, masked_positions=None):
         """``masked_positions`` (flat indices into B*S, e.g. from :func:`masked_positions`): apply the
         MLM head only at those positions, as BERT pretraining implementations do — the vocabulary
@@ -93,7 +103,7 @@ class BertForMaskedLM(nn.Module):
         stays free of host synchronisation (HIP-graph capturable)."""
         B, S = ids.shape
         pos = torch.arange(S, device=ids.device)
-        x = self.tok(ids) + self.pos(pos)[None] + self.typ(torch.zeros_like(ids))
+        x = self._lookup(self.tok, ids) + self._lookup(self.pos, pos)[None] + self._lookup(self.typ, torch.zeros_like(ids))
         x = self.drop(self.ln(x))
         for layer in self.layers:
             x = layer(x)

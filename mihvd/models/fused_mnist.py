@@ -272,10 +272,12 @@ class FusedMNISTTrainer:
         if self.f32_w3 == "fc1" and B > 112:  # the fused update keeps the a2 slice + a W3 tile in LDS
             self.f32_w3 = "tail"
         self._w3_pending = False
-        # graph-replayed world-size-1 fp32 steps: the next step's conv1 runs inside this step's
-        # f32_conv_reduce launch (after W1/b1's Adam and the step bump; f32_bwd.hip), so only the
-        # first step of a replay launches conv1 on its own (MIHVD_F32_CONV1_FUSE=0: always separate)
-        self.f32_conv1_fuse = self.f32 and os.environ.get("MIHVD_F32_CONV1_FUSE", "1") != "0"
+        # MIHVD_F32_CONV1_FUSE=1 (measured alternative, off): in graph-replayed world-size-1 fp32
+        # steps the next step's conv1 runs inside this step's f32_conv_reduce launch (after W1/b1's
+        # Adam and the step bump; f32_bwd.hip). Bitwise equal, but 19.8 us for the merged launch vs
+        # 6.9 + 7.0 us apart (150.7 vs 145.3 us/step): conv1 still waits for the whole reduction,
+        # and the cross-XCD release/acquire costs more than the saved launch
+        self.f32_conv1_fuse = self.f32 and os.environ.get("MIHVD_F32_CONV1_FUSE", "0") == "1"
         self._c1_ready = False
         self._c1_sync = torch.zeros(4, device=dev, dtype=torch.int32) if self.f32 else None
         if self.f32:
