@@ -189,6 +189,11 @@ class Engine {
     TORCH_CHECK(t.is_cuda() && t.get_device() == device_ && t.is_contiguous(),
                 "engine: expected a contiguous tensor on the engine's device ", device_);
     TORCH_CHECK(op >= 0 && op <= 3, "engine: op must be 0 sum, 1 prod, 2 max, 3 min");
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      TORCH_CHECK(!stopping_, "engine: enqueue after stop");
+      TORCH_CHECK(fatal_.empty(), "engine: the engine thread failed: ", fatal_);
+    }
     c10::hip::HIPGuard g((c10::DeviceIndex)device_);
     Req r;
     r.t = t;
