@@ -810,6 +810,7 @@ __device__ __forceinline__ void adam_flat4(const F32SmallAdam& sa, int64_t o, fl
   *reinterpret_cast<float4*>(sa.a.v + o) = vv;
 }
 
+template <bool C1>  // C1: the next step's conv1 role (F32Conv1Next) is compiled in
 __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __restrict__ slab, int G,
                                                               const float* __restrict__ cpart, int ncp,
                                                               const float* __restrict__ db2p, int ndb,
@@ -819,7 +820,7 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
   __shared__ float4 red[256];
   const int bid = blockIdx.x, t = threadIdx.x;
   const bool opt = sa.a.nblk > 0;
-  if (c1.nblk > 0 && bid >= CR_FC0 + n_fc) {  // the next step's conv1 (opt is on: state, W1 updates)
+  if (C1 && bid >= CR_FC0 + n_fc) {  // the next step's conv1 (opt is on: state, W1 updates)
     // relaxed agent-scope polling (an acquire per poll would invalidate the L2 under every other
     // block of the launch); W1/b1/the counter are then read with agent-scope (coherent) loads
     if (t == 0) {
@@ -848,7 +849,7 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
   if (opt) {
     c = f32_adam_coef(sa.a);
     if (bid == 0 && t == 0) const_cast<int64_t*>(sa.a.state)[ST_FWD] += 1;
-    if (bid == 0 && c1.nblk > 0) c1n_arrive(c1);
+    if (C1 && bid == 0) c1n_arrive(c1);
   }
   if (bid >= CR_FC0) {  // small fc parameters: gradients already final (fc1_bwd)
     const int64_t i = sa.fc_lo / 4 + (int64_t)(bid - CR_FC0) * 256 + t;
@@ -909,7 +910,7 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       }
     }
   }
-  if (c1.nblk > 0 && bid < CR_W2 + CR_CP) c1n_arrive(c1);  // a cpart block: W1 / b1 are final
+  if (C1 && bid < CR_W2 + CR_CP) c1n_arrive(c1);  // a cpart block: W1 / b1 are final
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1135,7 +1136,8 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
     c1.sync = sync.data_ptr<int>();
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  f32_conv_reduce_kernel<<<CR_FC0 + n_fc + c1.nblk, 256, 0, stream>>>(
+  auto kern = c1.nblk > 0 ? f32_conv_reduce_kernel<true> : f32_conv_reduce_kernel<false>;
+  kern<<<CR_FC0 + n_fc + c1.nblk, 256, 0, stream>>>(
       slab.data_ptr<float>(), (int)(slab.numel() / 51200), cpart.data_ptr<float>(), (int)(cpart.numel() / CP_F32),
       db2p.data_ptr<float>(), (int)(db2p.numel() / 64), gW2.data_ptr<float>(), gW1.data_ptr<float>(),
       gb1.data_ptr<float>(), gb2.data_ptr<float>(), sa, n_fc, c1);
