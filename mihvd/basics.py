@@ -116,6 +116,11 @@ def init(comm=None, process_sets=None, config: Config | None = None):
             _ctx.elastic_gen = g
             topo = _env.Topology(r, n, lr, ls, 0, 1, topo.master_addr, topo.master_port, "elastic")
         backend = _choose_backend(cfg)
+        # ProcessGroupNCCL's event cache hands a retired work's HIP event to the next collective;
+        # when that collective is being captured into a HIP graph (the fused step's RCCL calls) the
+        # watchdog may still query the event through the old work and abort with
+        # hipErrorCapturedEvent. Fresh events per work avoid the race.
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
         logging.basicConfig(level=getattr(logging, cfg.log_level, logging.INFO),
                             format="[%(asctime)s] [rank " + str(topo.rank) + "] %(message)s")
         if backend == "nccl":
