@@ -31,7 +31,7 @@ class CapturedStep:
     """``serialize=True``: each replay is launched only once the previous one has completed (a
     host wait on an event; costs one launch latency per step)."""
 
-    def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False):
+    def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False, sync_warmup: bool = True):
         if not torch.cuda.is_available():
             raise RuntimeError("CapturedStep needs a GPU")
         self.step_fn = step_fn
@@ -43,6 +43,10 @@ class CapturedStep:
         with torch.cuda.stream(side):  # warm-up on a side stream, as graph capture of autograd requires
             for _ in range(warmup):
                 _detach(step_fn())  # drop the autograd graph: no AccumulateGrad node outlives its step
+                if sync_warmup:
+                    # each warm-up step completes before the next is issued (scripts/bert_graph_bisect.py:
+                    # variant H vs C)
+                    side.synchronize()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
