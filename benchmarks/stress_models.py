@@ -124,7 +124,8 @@ def main():
         opt.step()
         return loss
 
-    if args.graph and args.model == "bert-base" and os.environ.get("MIHVD_STRESS_FORCE_GRAPH") != "1":
+    if args.graph and args.model == "bert-base" and os.environ.get("MIHVD_STRESS_BERT_GRAPH") != "1" and \
+            os.environ.get("MIHVD_STRESS_FORCE_GRAPH") != "1":
         # Whole-step replays of BERT-base are correct only when issued back to back: with the host
         # synchronising between replays the parameters go non-finite at the second one, also with
         # stock torch.optim.AdamW, a manual torch.cuda.graph capture, matmul attention and gather
