@@ -684,3 +684,49 @@ def test_native_engine_plan_fusion_and_stalls():
     many = [signature_hash(f"m{i}", 6, 64, 0) for i in range(10)]
     groups, _ = plan(_engine_ctrl(2, [2] * 10, [many, many]), 2, many, [300] * 10, [0] * 10, threshold=1000)
     assert groups == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9]]
+
+
+def test_native_engine_wrapper_routing():
+    """mihvd.parallel.native_engine.NativeEngine's Python side (no GPU): allreduces on the world go
+    to the engine op, sub-groups / unsupported ops / non-contiguous tensors are declined (the caller
+    launches them on the process group), flush() waits every outstanding handle once."""
+    import torch.distributed as dist
+
+    from mihvd.parallel import native_engine as ne
+
+    class Ops:
+        def __init__(self):
+            self.enq, self.waited, self.n = [], [], 0
+
+        def engine_allreduce_async(self, t, name, op):
+            self.n += 1
+            self.enq.append((name, op))
+            return self.n
+
+        def engine_wait(self, h):
+            self.waited.append(h)
+
+        def engine_poll(self, h):
+            return h in self.waited
+
+    eng = ne.NativeEngine.__new__(ne.NativeEngine)
+    eng._o = Ops()
+    import threading
+
+    eng._lock = threading.Lock()
+    eng._outstanding = set()
+    t = torch.zeros(8)
+    w1 = eng.allreduce("a", t, dist.ReduceOp.SUM, None)
+    w2 = eng.allreduce("b", t, dist.ReduceOp.MAX, dist.group.WORLD)
+    assert isinstance(w1, ne.NativeWork) and isinstance(w2, ne.NativeWork)
+    assert eng._o.enq == [("a", 0), ("b", 2)]
+    assert eng.allreduce("c", t, dist.ReduceOp.SUM, object()) is None            # a sub-group
+    assert eng.allreduce("d", t, dist.ReduceOp.BAND, None) is None              # not an engine op
+    assert eng.allreduce("e", torch.zeros(4, 4).t(), dist.ReduceOp.SUM, None) is None  # not contiguous
+    assert not w1.is_completed()
+    w1.wait()
+    w1.wait()  # idempotent
+    assert w1.is_completed() and eng._o.waited == [1]
+    eng.flush()
+    assert sorted(eng._o.waited) == [1, 2] and not eng._outstanding
+    assert eng.collective("x", "broadcast", "sig", lambda: "launched") == "launched"
