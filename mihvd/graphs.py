@@ -24,6 +24,8 @@ next replay; ``graphed()`` returns the step's (static) output.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 
@@ -40,9 +42,20 @@ class CapturedStep:
         self._pending = False
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        # MIHVD_GRAPH_HOLD_WARMUP=1: keep the last warm-up step's output, autograd graph included, alive
+        # for the life of the captured step, and read each warm-up output back before the next step
+        # (scripts/bert_graph_bisect.py variant H, the form whose BERT-base replays stay finite)
+        hold = os.environ.get("MIHVD_GRAPH_HOLD_WARMUP", "0") == "1"
+        self._held = None
         with torch.cuda.stream(side):  # warm-up on a side stream, as graph capture of autograd requires
             for _ in range(warmup):
-                _detach(step_fn())  # drop the autograd graph: no AccumulateGrad node outlives its step
+                out = step_fn()
+                if hold:
+                    _readback(out)
+                    self._held = out
+                else:
+                    _detach(out)  # drop the autograd graph: no AccumulateGrad node outlives its step
+                del out
                 if sync_warmup:
                     # each warm-up step completes before the next is issued (scripts/bert_graph_bisect.py:
                     # variant H vs C)
@@ -66,6 +79,19 @@ class CapturedStep:
 
     def pool(self):
         return self.graph.pool()
+
+
+def _readback(out):
+    """Copy one element of the first tensor in ``out`` to the host (synchronising its stream)."""
+    if torch.is_tensor(out):
+        if out.numel():
+            out.detach().reshape(-1)[:1].cpu()
+        return True
+    if isinstance(out, (list, tuple)):
+        return any(_readback(o) for o in out)
+    if isinstance(out, dict):
+        return any(_readback(o) for o in out.values())
+    return False
 
 
 def _detach(out):
