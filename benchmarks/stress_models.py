@@ -124,17 +124,6 @@ def main():
         opt.step()
         return loss
 
-    if args.graph and args.model == "bert-base" and os.environ.get("MIHVD_STRESS_BERT_GRAPH") != "1" and \
-            os.environ.get("MIHVD_STRESS_FORCE_GRAPH") != "1":
-        # Whole-step replays of BERT-base are correct only when issued back to back: with the host
-        # synchronising between replays the parameters go non-finite at the second one, also with
-        # stock torch.optim.AdamW, a manual torch.cuda.graph capture, matmul attention and gather
-        # embeddings (scripts/bert_graph_bisect.py; docs/ARCHITECTURE.md "Generic models"). The
-        # timed loop here synchronises around the timed region, so it is refused; eager is faster
-        # anyway (21.1 vs 25.7 ms/step). MIHVD_STRESS_FORCE_GRAPH=1 runs it.
-        raise SystemExit("stress_models: --graph is not supported for bert-base (replays after a host "
-                         "synchronisation go non-finite; scripts/bert_graph_bisect.py); MIHVD_STRESS_FORCE_GRAPH=1 "
-                         "runs it anyway")
     if args.graph:
         from mihvd.graphs import CapturedStep
 

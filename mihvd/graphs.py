@@ -42,10 +42,13 @@ class CapturedStep:
         self._pending = False
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        # MIHVD_GRAPH_HOLD_WARMUP=1: keep the last warm-up step's output, autograd graph included, alive
-        # for the life of the captured step, and read each warm-up output back before the next step
-        # (scripts/bert_graph_bisect.py variant H, the form whose BERT-base replays stay finite)
-        hold = os.environ.get("MIHVD_GRAPH_HOLD_WARMUP", "0") == "1"
+        # The last warm-up step's output, autograd graph included, stays alive for the life of the
+        # captured step, and each warm-up output is read back before the next step is issued. With
+        # the warm-up freed before capture instead, BERT-base's replays go non-finite at the second
+        # replay once the host synchronises between replays (scripts/bert_graph_bisect.py: variants
+        # H vs C, and this class with MIHVD_GRAPH_HOLD_WARMUP=0); held, they track eager. Costs one
+        # step's activations of memory. MIHVD_GRAPH_HOLD_WARMUP=0 restores the freeing form.
+        hold = os.environ.get("MIHVD_GRAPH_HOLD_WARMUP", "1") != "0"
         self._held = None
         with torch.cuda.stream(side):  # warm-up on a side stream, as graph capture of autograd requires
             for _ in range(warmup):

@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("model,extra", [("resnet50", ["--batch-size", "32"]), ("bert-base", ["--batch-size", "2"])])
+@pytest.mark.parametrize("model,extra", [("resnet50", ["--batch-size", "32"]), ("bert-base", ["--batch-size", "2"]),
+                                         ("bert-base", ["--batch-size", "4", "--graph", "--steps", "6"])])
 def test_stress_model_runs(model, extra):
     import torch
 
@@ -21,7 +22,7 @@ def test_stress_model_runs(model, extra):
     for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
         env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "stress_models.py"), "--model", model,
-                        "--steps", "3", "--warmup", "1", *extra], env=env, capture_output=True, text=True, timeout=600)
+                        "--steps", "3", "--warmup", "3", *extra], env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     assert rec["value"] > 0 and rec["n_gpus"] == 1
