@@ -2,36 +2,52 @@
 // runs it inside the Horovod core its image builds, horovod/Dockerfile:51-65, and every step's
 // hvd.DistributedOptimizer allreduce at horovod/tensorflow_mnist.py:133 goes through it).
 //
-// One std::thread per process owns a framework RCCL communicator (rccl_comm.cpp) and a
-// high-priority HIP stream from the PyTorch pool. Callers enqueue allreduces by name from any
-// thread (autograd hooks included); the thread runs *cycles*:
+// One std::thread per process owns two framework RCCL communicators (rccl_comm.cpp): a CONTROL
+// communicator for negotiation on a control stream, and a DATA communicator for the fused
+// allreduces on a high-priority data stream. Callers enqueue allreduces by name from any thread
+// (autograd hooks included). The thread is event-driven: it sleeps on a condition variable while
+// this rank has nothing pending and wakes on enqueue (no fixed clock); while work is pending it runs
+// *cycles* back to back, or re-negotiates after at most the cycle time when its last cycle made no
+// progress (MIHVD_CYCLE_TIME is a bound on that re-poll, not a floor on latency):
 //
-//   1. drain the queue into per-slot FIFOs. A slot is a (name, dtype, numel, op) signature,
-//      numbered in first-enqueue order on each rank.
-//   2. negotiate with ONE small RCCL allreduce of a control vector (int32, summed over ranks):
-//        [0] ranks asking to stop with nothing pending   [1] reserved (0)
+//   1. drain the queue. A signature (name, dtype, numel, op) gets a SLOT that every rank agrees
+//      on: slots are keyed by the signature's 32-bit hash and numbered in an order all ranks derive
+//      from the same data (see 3), never in a rank's local enqueue order — so ranks may enqueue
+//      tensors in different orders.
+//   2. negotiate with ONE small RCCL allreduce of a control vector (int32, summed over ranks) on
+//      the control communicator:
+//        [0] ranks asking to stop with nothing pending   [1] ranks with unannounced signatures
 //        [2 .. 2+S)       1 if this rank has work pending in slot s
-//        [2+S .. 2+2S)    this rank's signature hash of slot s (0 if nothing pending)
-//      Slot s is ready when its count equals the world size and the hash sum equals world x this
-//      rank's hash (every rank enqueued the same signature there). Every rank sees the same
-//      summed vector, so every rank derives the same ready list and issues the same RCCL calls
-//      in the same order — the coordinator's role, as a bit-vector allreduce (Horovod's response
-//      cache fast path) on the GPU instead of MPI messages to rank 0. A full count with a
-//      mismatched hash is a signature error, reported on every rank.
-//   3. fuse: ready slots in slot order, consecutive ones with equal dtype/op, packed into a
-//      persistent device fusion buffer up to the threshold (one buffer, grown, never freed per
-//      step) — copy-in / ncclAllReduce / copy-out on the engine stream; a tensor larger than the
-//      threshold is reduced in place.
-//   4. completion: each request's done event is recorded behind its copy-out and its handle
-//      marked enqueued; wait() blocks the caller until then and makes the caller's current stream
-//      wait for the event (no host-device sync on the caller's side).
-//   5. stall inspector: a slot pending on some but not all ranks for warn_s is reported (with how
-//      many ranks have it); after abort_s every pending handle fails and the process exits 134
-//      so the launcher tears the job down (mpirun's semantics, horovod/tensorflow-mnist.yaml:17-38).
+//        [2+S .. 2+2S)    the slot's hash if pending here (0 otherwise)
+//      Slot s is ready when its count equals the world size (and the hash sum equals world x hash,
+//      a consistency check). Every rank sees the same summed vector, derives the same ready list and
+//      issues the same RCCL calls in the same order — the coordinator's role as a bit-vector
+//      allreduce (Horovod's response-cache fast path) on the GPU instead of MPI messages to rank 0.
+//   3. new signatures (only when [1] > 0): an all-gather of up to K unannounced hashes per rank;
+//      every rank takes the union of the hashes that have no slot yet, sorts it and appends it to
+//      the slot table (engine_new_slot_order) — identical on every rank by construction. A slot
+//      table overflow is detected identically on every rank.
+//   4. fuse: ready slots in slot order, consecutive ones with equal dtype/op, packed into a
+//      persistent device fusion buffer up to the threshold by ONE batched pack kernel, one
+//      ncclAllReduce, ONE batched unpack kernel — on the data stream. The host does not wait for
+//      them: the next cycle's negotiation (control stream) overlaps them.
+//   5. completion: each request's done event (from a pool) is recorded behind its unpack and its
+//      handle marked enqueued; wait() blocks the caller until then and makes the caller's current
+//      stream wait for the event (no host-device sync on the caller's side).
+//   6. stall inspector: a slot pending on some but not all ranks for warn_s is reported (with how
+//      many ranks have it), and so is a negotiation that peers have not joined for warn_s; after
+//      abort_s the process exits 134 so the launcher tears the job down (mpirun's semantics,
+//      horovod/tensorflow-mnist.yaml:17-38).
+//
+// Failures: an error every rank sees identically (a signature mismatch, the slot table overflowing)
+// fails every pending handle on every rank and stops the engine. A failure local to one rank (a HIP
+// or RCCL error) aborts both communicators and exits 134: its peers would otherwise wait forever in
+// the next negotiation, where no stall inspector of theirs can tell them why.
 //
 // Stream ordering: enqueue records an event on the caller's current stream (the producer of the
-// gradient), the engine stream waits on it before reading; the tensor's storage is recorded on the
-// engine stream so the caching allocator cannot hand it out before the engine is done with it.
+// gradient); the data stream waits on it before reading; the tensor's storage is recorded on the data
+// stream so the caching allocator cannot hand it out before the engine is done with it. The fusion
+// buffer is allocated on the data stream (its only user); a replaced buffer is freed stream-ordered.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
@@ -42,6 +58,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -51,9 +68,12 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace mihvd {
@@ -64,6 +84,42 @@ int rccl_comm_world(int64_t h);
 int rccl_comm_device(int64_t h);
 int rccl_all_reduce_raw(void* buf, size_t count, int dtype, int op, void* comm, hipStream_t stream,
                         std::string* err);
+int rccl_all_gather_raw(const void* in, void* out, size_t count, int dtype, void* comm, hipStream_t stream,
+                        std::string* err);
+void rccl_comm_abort_raw(void* comm);
+
+// ------------------------------------------------------------------------------------------------
+// batched pack / unpack: one launch copies up to kCopyMax (src, dst, bytes) pieces; blockIdx.y is
+// the piece, blockIdx.x strides over its bytes with the widest access its alignment allows
+// ------------------------------------------------------------------------------------------------
+constexpr int kCopyMax = 32;
+struct CopyBatch {
+  const char* src[kCopyMax];
+  char* dst[kCopyMax];
+  int64_t bytes[kCopyMax];
+};
+
+template <typename V>
+__device__ __forceinline__ void copy_span(const char* s, char* d, int64_t nbytes) {
+  const int64_t n = nbytes / (int64_t)sizeof(V);
+  const V* sv = reinterpret_cast<const V*>(s);
+  V* dv = reinterpret_cast<V*>(d);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dv[i] = sv[i];
+}
+
+__global__ void __launch_bounds__(256) engine_batched_copy_kernel(CopyBatch b) {
+  const int k = blockIdx.y;
+  const char* s = b.src[k];
+  char* d = b.dst[k];
+  const int64_t nb = b.bytes[k];
+  const uintptr_t a = (uintptr_t)s | (uintptr_t)d | (uintptr_t)nb;
+  if ((a & 15) == 0) copy_span<uint4>(s, d, nb);
+  else if ((a & 7) == 0) copy_span<uint2>(s, d, nb);
+  else if ((a & 3) == 0) copy_span<uint32_t>(s, d, nb);
+  else if ((a & 1) == 0) copy_span<uint16_t>(s, d, nb);
+  else copy_span<uint8_t>(s, d, nb);
+}
 
 namespace {
 
@@ -72,7 +128,7 @@ using Clock = std::chrono::steady_clock;
 uint32_t fnv32(const std::string& s) {
   uint32_t h = 2166136261u;
   for (unsigned char c : s) h = (h ^ c) * 16777619u;
-  return h == 0 ? 1u : h;  // 0 means "nothing pending"
+  return h == 0 ? 1u : h;  // 0 means "nothing pending" / "no signature"
 }
 
 int nccl_dtype(at::ScalarType t) {
@@ -89,12 +145,17 @@ int nccl_dtype(at::ScalarType t) {
   }
 }
 
+// a failure every rank sees identically (computed from the same summed / gathered data)
+struct ConsistentError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 void hip_check(hipError_t e, const char* what) {
-  TORCH_CHECK(e == hipSuccess, "engine: ", what, ": ", hipGetErrorString(e));
+  if (e != hipSuccess) throw std::runtime_error(std::string("engine: ") + what + ": " + hipGetErrorString(e));
 }
 
 struct Handle {
-  int state = 0;  // 0 queued, 1 enqueued on the engine stream, 2 failed
+  int state = 0;  // 0 queued, 1 enqueued on the data stream, 2 failed
   hipEvent_t done = nullptr;
   std::string error;
   std::string name;
@@ -107,8 +168,9 @@ struct Req {
 };
 
 struct Slot {
-  std::string name;
   uint32_t hash = 0;
+  bool known = false;  // dtype/op/numel/name set (from a local enqueue of this signature)
+  std::string name;
   at::ScalarType dtype = at::kFloat;
   int op = 0;
   int64_t numel = 0;
@@ -120,8 +182,8 @@ struct Slot {
 }  // namespace
 
 // Pure planning step, shared by the engine loop and the CPU unit test (engine_plan op): given the
-// summed control vector, this rank's slot hashes and the slots' sizes/fuse keys, return the ready
-// slots grouped for fusion (-1 separates groups), or throw on a signature mismatch.
+// summed control vector, the slots' hashes and sizes/fuse keys, return the ready slots grouped for
+// fusion (-1 separates groups), or an error on a signature mismatch.
 std::vector<int64_t> engine_plan_groups(const int32_t* sum, int nslot, int world, const std::vector<uint32_t>& hash,
                                         const std::vector<int64_t>& bytes, const std::vector<int64_t>& key,
                                         int64_t threshold, std::vector<int>* partial, std::string* error) {
@@ -161,13 +223,29 @@ std::vector<int64_t> engine_plan_groups(const int32_t* sum, int nslot, int world
   return out;
 }
 
+// Slot agreement (step 3): `gathered` holds world x K announced hashes (0 = empty entry). Returns
+// the hashes that get new slots, in the order every rank appends them: the sorted union of the
+// announced hashes that have no slot yet. A pure function of data every rank holds identically.
+std::vector<uint32_t> engine_new_slot_order(const int32_t* gathered, int world, int K,
+                                            const std::unordered_set<uint32_t>& assigned) {
+  std::set<uint32_t> fresh;
+  for (int i = 0; i < world * K; ++i) {
+    const uint32_t h = (uint32_t)gathered[i];
+    if (h != 0 && assigned.count(h) == 0) fresh.insert(h);
+  }
+  return std::vector<uint32_t>(fresh.begin(), fresh.end());
+}
+
 namespace {
+
+constexpr int kAnnounce = 64;  // new signatures announced per rank per cycle
 
 class Engine {
  public:
-  Engine(int64_t comm, int64_t fusion_bytes, double cycle_s, double warn_s, double abort_s, int64_t max_slots)
-      : comm_h_(comm),
-        comm_(rccl_comm_raw(comm)),
+  Engine(int64_t comm, int64_t ctrl_comm, int64_t fusion_bytes, double cycle_s, double warn_s, double abort_s,
+         int64_t max_slots)
+      : comm_(rccl_comm_raw(comm)),
+        ctrl_comm_(rccl_comm_raw(ctrl_comm)),
         world_(rccl_comm_world(comm)),
         device_(rccl_comm_device(comm)),
         threshold_(fusion_bytes),
@@ -175,43 +253,77 @@ class Engine {
         warn_s_(warn_s),
         abort_s_(abort_s),
         cap_((int)max_slots),
-        stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_)) {
+        stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_)),
+        ctrl_stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_)) {
+    TORCH_CHECK(rccl_comm_world(ctrl_comm) == world_ && rccl_comm_device(ctrl_comm) == device_,
+                "engine: the control communicator must span the same ranks and device");
     c10::hip::HIPGuard g((c10::DeviceIndex)device_);
     auto i32 = at::TensorOptions().dtype(at::kInt);
-    ctrl_dev_ = at::zeros({2 + 2 * (int64_t)cap_}, i32.device(at::kCUDA, device_));
-    ctrl_host_ = at::zeros({2 + 2 * (int64_t)cap_}, i32.pinned_memory(true));
+    const int64_t n = 2 + 2 * (int64_t)cap_;
+    ctrl_dev_ = at::zeros({n}, i32.device(at::kCUDA, device_));
+    ctrl_host_ = at::zeros({n}, i32.pinned_memory(true));
+    ann_dev_ = at::zeros({(int64_t)world_ * kAnnounce + kAnnounce}, i32.device(at::kCUDA, device_));
+    ann_host_ = at::zeros({(int64_t)world_ * kAnnounce + kAnnounce}, i32.pinned_memory(true));
+    hip_check(hipEventCreateWithFlags(&ctrl_ev_, hipEventDisableTiming), "hipEventCreate");
     thread_ = std::thread([this] { loop(); });
   }
 
-  ~Engine() { stop(); }
+  ~Engine() {
+    stop();
+    for (hipEvent_t e : pool_) hipEventDestroy(e);
+    if (ctrl_ev_) hipEventDestroy(ctrl_ev_);
+  }
 
   int64_t enqueue(const at::Tensor& t, const std::string& name, int64_t op) {
     TORCH_CHECK(t.is_cuda() && t.get_device() == device_ && t.is_contiguous(),
                 "engine: expected a contiguous tensor on the engine's device ", device_);
     TORCH_CHECK(op >= 0 && op <= 3, "engine: op must be 0 sum, 1 prod, 2 max, 3 min");
+    (void)nccl_dtype(t.scalar_type());
+    const std::string sig =
+        name + "|" + std::to_string((int)t.scalar_type()) + "|" + std::to_string(t.numel()) + "|" + std::to_string(op);
+    const uint32_t h = fnv32(sig);
     {
       std::lock_guard<std::mutex> lk(mu_);
       TORCH_CHECK(!stopping_, "engine: enqueue after stop");
       TORCH_CHECK(fatal_.empty(), "engine: the engine thread failed: ", fatal_);
+      auto it = local_sig_.find(h);
+      if (it == local_sig_.end()) {
+        // the slot cap, checked where the caller can see it (a new signature this rank adds)
+        TORCH_CHECK((int)local_sig_.size() < cap_, "engine: more than ", cap_,
+                    " distinct collectives (MIHVD_ENGINE_SLOTS)");
+        local_sig_.emplace(h, sig);
+      } else {
+        TORCH_CHECK(it->second == sig, "engine: signature hash collision between '", it->second, "' and '", sig, "'");
+      }
     }
     c10::hip::HIPGuard g((c10::DeviceIndex)device_);
     Req r;
     r.t = t;
-    hip_check(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "hipEventCreate");
-    hip_check(hipEventRecord(r.ready, c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream()), "hipEventRecord");
-    auto h = std::make_shared<Handle>();
-    h->name = name;
-    hip_check(hipEventCreateWithFlags(&h->done, hipEventDisableTiming), "hipEventCreate");
-    std::lock_guard<std::mutex> lk(mu_);
-    TORCH_CHECK(!stopping_, "engine: enqueue after stop");
-    TORCH_CHECK(fatal_.empty(), "engine: the engine thread failed: ", fatal_);
-    r.id = next_id_++;
-    handles_[r.id] = h;
-    queue_.push_back({name, (int)op, std::move(r)});
-    return queue_.back().req.id;
+    r.ready = event_get();
+    hip_check(hipEventRecord(r.ready, c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream()),
+              "hipEventRecord");
+    auto hd = std::make_shared<Handle>();
+    hd->name = name;
+    hd->done = event_get();
+    int64_t id = 0;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stopping_ || !fatal_.empty()) {
+        event_put(r.ready);
+        event_put(hd->done);
+        TORCH_CHECK(false, "engine: enqueue after stop", fatal_.empty() ? "" : ": ", fatal_);
+      }
+      id = next_id_++;
+      r.id = id;
+      handles_[id] = hd;
+      queue_.push_back({name, (int)op, h, std::move(r)});
+      ++enqueued_;
+    }
+    cv_work_.notify_one();
+    return id;
   }
 
-  // Blocks until the collective of handle `id` is enqueued on the engine stream, then orders the
+  // Blocks until the collective of handle `id` is enqueued on the data stream, then orders the
   // caller's current stream after it.
   void wait(int64_t id) {
     std::shared_ptr<Handle> h;
@@ -224,13 +336,15 @@ class Engine {
       handles_.erase(it);
     }
     if (h->state == 2) {
-      hipEventDestroy(h->done);
+      event_put(h->done);
       TORCH_CHECK(false, "engine: collective '", h->name, "' failed: ", h->error);
     }
     c10::hip::HIPGuard g((c10::DeviceIndex)device_);
-    hip_check(hipStreamWaitEvent(c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream(), h->done, 0),
-              "hipStreamWaitEvent");
-    hipEventDestroy(h->done);
+    const hipError_t e =
+        hipStreamWaitEvent(c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream(), h->done, 0);
+    // the wait captured the event's current record: re-recording it later (pool reuse) is safe
+    event_put(h->done);
+    TORCH_CHECK(e == hipSuccess, "engine: hipStreamWaitEvent: ", hipGetErrorString(e));
   }
 
   // true once the collective has completed on the device
@@ -243,26 +357,49 @@ class Engine {
     return hipEventQuery(it->second->done) == hipSuccess;
   }
 
+  // (called by one owner: engine_stop moves the engine out of the global first)
   void stop() {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (stopping_) return;
       stopping_ = true;
     }
+    cv_work_.notify_all();
     if (thread_.joinable()) thread_.join();
   }
 
   std::vector<int64_t> stats() {
     std::lock_guard<std::mutex> lk(mu_);
-    return {cycles_, collectives_, tensors_, fused_bytes_, (int64_t)slots_.size(), stalls_warned_};
+    return {cycles_, collectives_, tensors_, fused_bytes_, (int64_t)slots_.size(), stalls_warned_, wakeups_,
+            idle_waits_, announces_};
   }
 
  private:
   struct Item {
     std::string name;
     int op;
+    uint32_t hash;
     Req req;
   };
+
+  hipEvent_t event_get() {
+    {
+      std::lock_guard<std::mutex> lk(pool_mu_);
+      if (!pool_.empty()) {
+        hipEvent_t e = pool_.back();
+        pool_.pop_back();
+        return e;
+      }
+    }
+    hipEvent_t e = nullptr;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    return e;
+  }
+
+  void event_put(hipEvent_t e) {
+    if (e == nullptr) return;
+    std::lock_guard<std::mutex> lk(pool_mu_);
+    pool_.push_back(e);
+  }
 
   void fail_all(const std::string& why) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -275,51 +412,108 @@ class Engine {
     cv_done_.notify_all();
   }
 
-  int slot_of(const Item& it) {
-    const std::string sig = it.name + "|" + std::to_string((int)it.req.t.scalar_type()) + "|" +
-                            std::to_string(it.req.t.numel()) + "|" + std::to_string(it.op);
-    auto f = slot_index_.find(sig);
-    if (f != slot_index_.end()) return f->second;
-    TORCH_CHECK((int)slots_.size() < cap_, "engine: more than ", cap_, " distinct collectives (MIHVD_ENGINE_SLOTS)");
-    Slot s;
-    s.name = it.name;
-    s.hash = fnv32(sig);
-    s.dtype = it.req.t.scalar_type();
-    s.op = it.op;
-    s.numel = it.req.t.numel();
-    slots_.push_back(std::move(s));
-    slot_index_[sig] = (int)slots_.size() - 1;
-    return (int)slots_.size() - 1;
+  bool local_work() const {
+    if (!unassigned_.empty()) return true;
+    for (const auto& s : slots_)
+      if (!s.pending.empty()) return true;
+    return false;
+  }
+
+  Slot& slot_for_local(int s, const Item& it) {
+    Slot& sl = slots_[s];
+    if (!sl.known) {
+      sl.known = true;
+      sl.name = it.name;
+      sl.dtype = it.req.t.scalar_type();
+      sl.op = it.op;
+      sl.numel = it.req.t.numel();
+    }
+    return sl;
+  }
+
+  // the queue -> slot FIFOs (assigned signatures) or the unassigned staging area
+  void drain_locked() {
+    while (!queue_.empty()) {
+      Item it = std::move(queue_.front());
+      queue_.pop_front();
+      auto f = slot_of_hash_.find(it.hash);
+      if (f != slot_of_hash_.end()) {
+        slot_for_local(f->second, it).pending.push_back(std::move(it.req));
+        continue;
+      }
+      auto& st = unassigned_[it.hash];
+      if (st.empty() && std::find(announce_.begin(), announce_.end(), it.hash) == announce_.end())
+        announce_.push_back(it.hash);
+      st.push_back(std::move(it));
+    }
+  }
+
+  // Polls `ev` (control stream) until it completes; meanwhile runs the negotiation stall check.
+  void wait_ctrl(hipEvent_t ev) {
+    const auto t0 = Clock::now();
+    bool warned = false;
+    int spins = 0;
+    for (;;) {
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) hip_check(q, "negotiation event");
+      if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 10));
+      if ((spins & 255) != 0) continue;
+      const double age = std::chrono::duration<double>(Clock::now() - t0).count();
+      if (warn_s_ > 0 && age > warn_s_ && !warned) {
+        warned = true;
+        std::string names;
+        for (const auto& s : slots_)
+          if (!s.pending.empty()) names += (names.empty() ? "" : ", ") + s.name;
+        for (const auto& kv : unassigned_)
+          if (!kv.second.empty()) names += (names.empty() ? "" : ", ") + kv.second.front().name;
+        std::fprintf(stderr,
+                     "[mihvd engine] stall: this rank has waited %.1f s in negotiation for peers that have not "
+                     "submitted any collective (pending here: %s)\n",
+                     age, names.empty() ? "nothing" : names.c_str());
+        std::lock_guard<std::mutex> lk(mu_);
+        ++stalls_warned_;
+      }
+      if (abort_s_ > 0 && age > abort_s_) {
+        std::fprintf(stderr, "[mihvd engine] negotiation stalled for more than %.1f s: aborting (exit 134)\n",
+                     abort_s_);
+        std::fflush(stderr);
+        std::_Exit(134);
+      }
+    }
   }
 
   void loop() {
     c10::hip::HIPGuard g((c10::DeviceIndex)device_);
-    hipStream_t st = stream_.stream();
-    auto next = Clock::now();
-    bool stop_seen = false;
+    // the data stream is this thread's current stream: the fusion buffer is allocated on it
+    c10::hip::HIPStreamGuard sg(stream_);
+    hipStream_t cst = ctrl_stream_.stream();
+    bool progressed = true;
     try {
-      while (!stop_seen) {
-        // a world with nothing pending anywhere for 100 cycles backs off to 10x the cycle time
-        // (every rank sees the same summed vectors, so all back off together); work ends it
-        next += std::chrono::microseconds((int64_t)(cycle_ * 1e6 * (idle_ > 100 ? 10 : 1)));
-        std::this_thread::sleep_until(next);
-        if (Clock::now() > next + std::chrono::milliseconds(50)) next = Clock::now();
+      for (;;) {
         bool stopping;
         {
-          std::lock_guard<std::mutex> lk(mu_);
-          while (!queue_.empty()) {
-            Item it = std::move(queue_.front());
-            queue_.pop_front();
-            const int s = slot_of(it);
-            slots_[s].pending.push_back(std::move(it.req));
+          std::unique_lock<std::mutex> lk(mu_);
+          const bool had_work = local_work();
+          if (!had_work && queue_.empty() && !stopping_) {
+            // idle: sleep until work or stop (no clock)
+            ++idle_waits_;
+            cv_work_.wait(lk, [&] { return !queue_.empty() || stopping_; });
+            ++wakeups_;
+          } else if (had_work && !progressed && queue_.empty() && !stopping_) {
+            // partial work and no progress last cycle: re-negotiate within the cycle time, sooner
+            // on new work
+            cv_work_.wait_for(lk, std::chrono::microseconds((int64_t)(cycle_ * 1e6)),
+                              [&] { return !queue_.empty() || stopping_; });
           }
+          drain_locked();
           stopping = stopping_;
         }
-        // 2. negotiation: one small allreduce of the control vector
+        // 2. negotiation on the control communicator
         int32_t* hv = ctrl_host_.data_ptr<int32_t>();
         const int S = cap_;
         std::fill(hv, hv + 2 + 2 * S, 0);
-        bool any_pending = false;
+        bool any_pending = !unassigned_.empty();
         for (size_t s = 0; s < slots_.size(); ++s)
           if (!slots_[s].pending.empty()) {
             hv[2 + s] = 1;
@@ -328,52 +522,124 @@ class Engine {
           }
         // a stopping rank first drains its own pending work (its peers will match it)
         hv[0] = (stopping && !any_pending) ? 1 : 0;
-        hip_check(hipMemcpyAsync(ctrl_dev_.data_ptr(), hv, (2 + 2 * S) * 4, hipMemcpyHostToDevice, st), "H2D");
+        hv[1] = announce_.empty() ? 0 : 1;
+        hip_check(hipMemcpyAsync(ctrl_dev_.data_ptr(), hv, (2 + 2 * S) * 4, hipMemcpyHostToDevice, cst), "H2D");
         std::string err;
-        if (rccl_all_reduce_raw(ctrl_dev_.data_ptr(), 2 + 2 * S, ncclInt32, ncclSum, comm_, st, &err) != 0)
+        if (rccl_all_reduce_raw(ctrl_dev_.data_ptr(), 2 + 2 * S, ncclInt32, ncclSum, ctrl_comm_, cst, &err) != 0)
           throw std::runtime_error("negotiation allreduce: " + err);
-        hip_check(hipMemcpyAsync(hv, ctrl_dev_.data_ptr(), (2 + 2 * S) * 4, hipMemcpyDeviceToHost, st), "D2H");
-        hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+        hip_check(hipMemcpyAsync(hv, ctrl_dev_.data_ptr(), (2 + 2 * S) * 4, hipMemcpyDeviceToHost, cst), "D2H");
+        hip_check(hipEventRecord(ctrl_ev_, cst), "hipEventRecord");
+        wait_ctrl(ctrl_ev_);
         {
           std::lock_guard<std::mutex> lk(mu_);
           ++cycles_;
         }
-        if (hv[0] == world_) stop_seen = true;  // every rank asked to stop with nothing pending
-        bool idle = true;
-        for (int s = 0; s < S && idle; ++s) idle = hv[2 + s] == 0;
-        idle_ = idle ? idle_ + 1 : 0;
-        // 3. plan + execute
+        if (hv[0] == world_) break;  // every rank asked to stop with nothing pending
+        progressed = false;
+        // 3. new signatures: all-gather the announced hashes, append their sorted union
+        if (hv[1] > 0) {
+          announce_round(cst);
+          progressed = true;
+        }
+        // 4. plan + execute on the data stream
         std::vector<uint32_t> hash(S, 0);
         std::vector<int64_t> bytes(S, 0), key(S, 0);
         for (size_t s = 0; s < slots_.size(); ++s) {
           hash[s] = slots_[s].hash;
-          bytes[s] = slots_[s].numel * (int64_t)c10::elementSize(slots_[s].dtype);
-          key[s] = (int64_t)slots_[s].dtype * 16 + slots_[s].op;
+          if (slots_[s].known) {
+            bytes[s] = slots_[s].numel * (int64_t)c10::elementSize(slots_[s].dtype);
+            key[s] = (int64_t)slots_[s].dtype * 16 + slots_[s].op;
+          }
         }
         std::vector<int> partial;
         std::string perr;
         const auto plan = engine_plan_groups(hv, S, world_, hash, bytes, key, threshold_, &partial, &perr);
-        if (!perr.empty()) throw std::runtime_error(perr);
+        if (!perr.empty()) throw ConsistentError(perr);
         std::vector<int> group;
         for (int64_t e : plan) {
           if (e >= 0) {
             group.push_back((int)e);
             continue;
           }
-          run_group(group, st);
+          run_group(group);
           group.clear();
+          progressed = true;
         }
         inspect_stalls(partial);
       }
-    } catch (const std::exception& e) {
+    } catch (const ConsistentError& e) {
       fail_all(e.what());
-      std::fprintf(stderr, "[mihvd engine] fatal: %s\n", e.what());
+      std::fprintf(stderr, "[mihvd engine] fatal (on every rank): %s\n", e.what());
       return;
+    } catch (const std::exception& e) {
+      // local failure: the peers are (or will be) blocked in a collective with this rank
+      fail_all(e.what());
+      std::fprintf(stderr, "[mihvd engine] fatal on this rank: %s; aborting the engine communicators (exit 134)\n",
+                   e.what());
+      std::fflush(stderr);
+      rccl_comm_abort_raw(ctrl_comm_);
+      rccl_comm_abort_raw(comm_);
+      std::_Exit(134);
     }
     fail_all("engine stopped");
   }
 
-  void run_group(const std::vector<int>& group, hipStream_t st) {
+  void announce_round(hipStream_t cst) {
+    int32_t* ah = ann_host_.data_ptr<int32_t>();
+    const int64_t mine = world_ * (int64_t)kAnnounce;  // this rank's send block lives past the gather area
+    std::fill(ah, ah + world_ * kAnnounce + kAnnounce, 0);
+    for (int i = 0; i < kAnnounce && i < (int)announce_.size(); ++i) ah[mine + i] = (int32_t)announce_[i];
+    int32_t* ad = ann_dev_.data_ptr<int32_t>();
+    hip_check(hipMemcpyAsync(ad + mine, ah + mine, kAnnounce * 4, hipMemcpyHostToDevice, cst), "H2D announce");
+    std::string err;
+    if (rccl_all_gather_raw(ad + mine, ad, kAnnounce, ncclInt32, ctrl_comm_, cst, &err) != 0)
+      throw std::runtime_error("announce all-gather: " + err);
+    hip_check(hipMemcpyAsync(ah, ad, world_ * kAnnounce * 4, hipMemcpyDeviceToHost, cst), "D2H announce");
+    hip_check(hipEventRecord(ctrl_ev_, cst), "hipEventRecord");
+    wait_ctrl(ctrl_ev_);
+    std::unordered_set<uint32_t> assigned;
+    for (const auto& kv : slot_of_hash_) assigned.insert(kv.first);
+    const auto fresh = engine_new_slot_order(ah, world_, kAnnounce, assigned);
+    if ((int)slots_.size() + (int)fresh.size() > cap_)
+      throw ConsistentError("more than " + std::to_string(cap_) +
+                            " distinct collectives across the ranks (MIHVD_ENGINE_SLOTS)");
+    std::lock_guard<std::mutex> lk(mu_);
+    ++announces_;
+    for (uint32_t h : fresh) {
+      const int s = (int)slots_.size();
+      Slot sl;
+      sl.hash = h;
+      slots_.push_back(std::move(sl));
+      slot_of_hash_[h] = s;
+      auto it = unassigned_.find(h);
+      if (it != unassigned_.end()) {
+        for (auto& item : it->second) slot_for_local(s, item).pending.push_back(std::move(item.req));
+        unassigned_.erase(it);
+      }
+      announce_.erase(std::remove(announce_.begin(), announce_.end(), h), announce_.end());
+    }
+  }
+
+  void launch_copies(const std::vector<std::tuple<const char*, char*, int64_t>>& pieces) {
+    hipStream_t st = stream_.stream();
+    for (size_t i = 0; i < pieces.size(); i += kCopyMax) {
+      CopyBatch b{};
+      const int n = (int)std::min<size_t>(kCopyMax, pieces.size() - i);
+      int64_t most = 0;
+      for (int k = 0; k < n; ++k) {
+        b.src[k] = std::get<0>(pieces[i + k]);
+        b.dst[k] = std::get<1>(pieces[i + k]);
+        b.bytes[k] = std::get<2>(pieces[i + k]);
+        most = std::max(most, b.bytes[k]);
+      }
+      const int gx = (int)std::min<int64_t>(256, std::max<int64_t>(1, (most + 256 * 16 * 4 - 1) / (256 * 16 * 4)));
+      hipLaunchKernelGGL(engine_batched_copy_kernel, dim3(gx, n), dim3(256), 0, st, b);
+      hip_check(hipGetLastError(), "pack/unpack launch");
+    }
+  }
+
+  void run_group(const std::vector<int>& group) {
+    hipStream_t st = stream_.stream();
     std::vector<Req> reqs;
     for (int s : group) {
       reqs.push_back(std::move(slots_[s].pending.front()));
@@ -398,25 +664,26 @@ class Engine {
       int64_t nbytes = 0;
       for (auto& r : reqs) nbytes += r.t.numel() * es;
       if (!fusion_.defined() || fusion_.numel() < nbytes) {
-        // grown, never shrunk; the old buffer's last use is on this stream
-        fusion_ = at::empty({std::max<int64_t>(nbytes, threshold_)}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device_));
+        // grown, never shrunk. Allocated with the data stream current, so the old block (whose last
+        // use is on this stream) is freed stream-ordered; recordStream makes that explicit
+        if (fusion_.defined()) c10::hip::HIPCachingAllocator::recordStream(fusion_.storage().data_ptr(), stream_);
+        fusion_ = at::empty({std::max<int64_t>(nbytes, threshold_)},
+                            at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device_));
       }
       char* base = (char*)fusion_.data_ptr();
+      std::vector<std::tuple<const char*, char*, int64_t>> in, out;
       int64_t off = 0;
       for (auto& r : reqs) {
         const int64_t nb = r.t.numel() * es;
-        hip_check(hipMemcpyAsync(base + off, r.t.data_ptr(), nb, hipMemcpyDeviceToDevice, st), "copy-in");
+        in.emplace_back((const char*)r.t.data_ptr(), base + off, nb);
+        out.emplace_back((const char*)(base + off), (char*)r.t.data_ptr(), nb);
         off += nb;
       }
+      launch_copies(in);  // MEMCPY_IN_FUSION_BUFFER: one launch
       total = nbytes / es;
       if (rccl_all_reduce_raw(base, (size_t)total, dt, op, comm_, st, &err) != 0)
         throw std::runtime_error("fused allreduce: " + err);
-      off = 0;
-      for (auto& r : reqs) {
-        const int64_t nb = r.t.numel() * es;
-        hip_check(hipMemcpyAsync(r.t.data_ptr(), base + off, nb, hipMemcpyDeviceToDevice, st), "copy-out");
-        off += nb;
-      }
+      launch_copies(out);  // MEMCPY_OUT_FUSION_BUFFER: one launch
     }
     std::lock_guard<std::mutex> lk(mu_);
     ++collectives_;
@@ -428,7 +695,7 @@ class Engine {
         hip_check(hipEventRecord(it->second->done, st), "hipEventRecord");
         it->second->state = 1;
       }
-      hipEventDestroy(r.ready);
+      event_put(r.ready);  // the data stream's wait above captured it
     }
     cv_done_.notify_all();
   }
@@ -451,13 +718,13 @@ class Engine {
         std::fprintf(stderr,
                      "[mihvd engine] stall: '%s' has been submitted by %d of %d ranks for %.1f s (the others "
                      "have not reached it)\n",
-                     sl.name.c_str(), have, world_, age);
+                     sl.known ? sl.name.c_str() : "(not submitted on this rank)", have, world_, age);
         std::lock_guard<std::mutex> lk(mu_);
         ++stalls_warned_;
       }
       if (abort_s_ > 0 && age > abort_s_) {
-        std::fprintf(stderr, "[mihvd engine] stall on '%s' exceeded %.1f s: aborting (exit 134)\n", sl.name.c_str(),
-                     abort_s_);
+        std::fprintf(stderr, "[mihvd engine] stall on '%s' exceeded %.1f s: aborting (exit 134)\n",
+                     sl.known ? sl.name.c_str() : "(not submitted on this rank)", abort_s_);
         std::fflush(stderr);
         std::_Exit(134);
       }
@@ -466,25 +733,34 @@ class Engine {
       if (!is_partial[s]) slots_[s].partial = slots_[s].warned = false;
   }
 
-  const int64_t comm_h_;
   void* comm_;
+  void* ctrl_comm_;
   const int world_, device_;
   const int64_t threshold_;
   const double cycle_, warn_s_, abort_s_;
   const int cap_;
-  c10::hip::HIPStream stream_;
-  at::Tensor ctrl_dev_, ctrl_host_, fusion_;
+  c10::hip::HIPStream stream_, ctrl_stream_;
+  at::Tensor ctrl_dev_, ctrl_host_, ann_dev_, ann_host_, fusion_;
+  hipEvent_t ctrl_ev_ = nullptr;
+  // engine-thread state
   std::vector<Slot> slots_;
-  std::unordered_map<std::string, int> slot_index_;
+  std::unordered_map<uint32_t, int> slot_of_hash_;
+  std::unordered_map<uint32_t, std::deque<Item>> unassigned_;
+  std::vector<uint32_t> announce_;
+  // shared state (mu_)
   std::mutex mu_;
-  std::condition_variable cv_done_;
+  std::condition_variable cv_done_, cv_work_;
   std::deque<Item> queue_;
+  std::unordered_map<uint32_t, std::string> local_sig_;
   std::map<int64_t, std::shared_ptr<Handle>> handles_;
-  int64_t next_id_ = 1;
+  int64_t next_id_ = 1, enqueued_ = 0;
   bool stopping_ = false;
   std::string fatal_;
-  int64_t idle_ = 0;
-  int64_t cycles_ = 0, collectives_ = 0, tensors_ = 0, fused_bytes_ = 0, stalls_warned_ = 0;
+  int64_t cycles_ = 0, collectives_ = 0, tensors_ = 0, fused_bytes_ = 0, stalls_warned_ = 0, wakeups_ = 0,
+          idle_waits_ = 0, announces_ = 0;
+  // event pool
+  std::mutex pool_mu_;
+  std::vector<hipEvent_t> pool_;
   std::thread thread_;
 };
 
@@ -499,12 +775,12 @@ Engine& engine() {
 
 }  // namespace
 
-void engine_start(int64_t comm, int64_t fusion_bytes, double cycle_s, double warn_s, double abort_s,
-                  int64_t max_slots) {
+void engine_start(int64_t comm, int64_t ctrl_comm, int64_t fusion_bytes, double cycle_s, double warn_s,
+                  double abort_s, int64_t max_slots) {
   TORCH_CHECK(fusion_bytes > 0 && cycle_s > 0 && max_slots > 0, "engine_start: bad arguments");
   std::lock_guard<std::mutex> lk(g_emu);
   TORCH_CHECK(g_engine == nullptr, "engine_start: an engine is already running");
-  g_engine = std::make_unique<Engine>(comm, fusion_bytes, cycle_s, warn_s, abort_s, max_slots);
+  g_engine = std::make_unique<Engine>(comm, ctrl_comm, fusion_bytes, cycle_s, warn_s, abort_s, max_slots);
 }
 
 int64_t engine_allreduce_async(const at::Tensor& t, const std::string& name, int64_t op) {
@@ -531,9 +807,9 @@ bool engine_running() {
   return g_engine != nullptr;
 }
 
-// CPU-testable planning step: `ctrl` is a summed control vector (int32 [2 + 2 S]), `hash` this
-// rank's slot hashes (int64, low 32 bits), `bytes` / `key` per slot. Returns the grouped ready
-// slots (-1 ends a group), -2 followed by the partial slots; throws on a signature mismatch.
+// CPU-testable planning step: `ctrl` is a summed control vector (int32 [2 + 2 S]), `hash` the slot
+// hashes (int64, low 32 bits), `bytes` / `key` per slot. Returns the grouped ready slots (-1 ends a
+// group), -2 followed by the partial slots; throws on a signature mismatch.
 std::vector<int64_t> engine_plan(const at::Tensor& ctrl, int64_t world, const at::Tensor& hash, const at::Tensor& bytes,
                                  const at::Tensor& key, int64_t threshold) {
   const int S = (int)hash.numel();
@@ -556,13 +832,27 @@ std::vector<int64_t> engine_plan(const at::Tensor& ctrl, int64_t world, const at
   return out;
 }
 
+// CPU-testable slot agreement: `gathered` = the all-gathered announce blocks (int32 [world x K]),
+// `assigned` = hashes that already have slots. Returns the hashes appended as new slots, in order.
+std::vector<int64_t> engine_assign(const at::Tensor& gathered, int64_t world, const at::Tensor& assigned) {
+  auto g = gathered.to(at::kInt).contiguous();
+  TORCH_CHECK(world >= 1 && g.numel() % world == 0, "engine_assign: gathered must hold world x K entries");
+  auto a = assigned.to(at::kLong).contiguous();
+  std::unordered_set<uint32_t> as;
+  for (int64_t i = 0; i < a.numel(); ++i) as.insert((uint32_t)a.data_ptr<int64_t>()[i]);
+  const auto fresh = engine_new_slot_order(g.data_ptr<int32_t>(), (int)world, (int)(g.numel() / world), as);
+  return std::vector<int64_t>(fresh.begin(), fresh.end());
+}
+
 int64_t engine_signature_hash(const std::string& sig) { return (int64_t)fnv32(sig); }
 
 }  // namespace mihvd
 
 TORCH_LIBRARY_FRAGMENT(mihvd, m) {
-  m.def("engine_start(int comm, int fusion_bytes, float cycle_s, float warn_s, float abort_s, int max_slots) -> ()",
-        &mihvd::engine_start);
+  m.def(
+      "engine_start(int comm, int ctrl_comm, int fusion_bytes, float cycle_s, float warn_s, float abort_s, "
+      "int max_slots) -> ()",
+      &mihvd::engine_start);
   m.def("engine_allreduce_async(Tensor(a!) t, str name, int op=0) -> int", &mihvd::engine_allreduce_async);
   m.def("engine_wait(int handle) -> ()", &mihvd::engine_wait);
   m.def("engine_poll(int handle) -> bool", &mihvd::engine_poll);
@@ -571,5 +861,6 @@ TORCH_LIBRARY_FRAGMENT(mihvd, m) {
   m.def("engine_running() -> bool", &mihvd::engine_running);
   m.def("engine_plan(Tensor ctrl, int world, Tensor hash, Tensor bytes, Tensor key, int threshold) -> int[]",
         &mihvd::engine_plan);
+  m.def("engine_assign(Tensor gathered, int world, Tensor assigned) -> int[]", &mihvd::engine_assign);
   m.def("engine_signature_hash(str sig) -> int", &mihvd::engine_signature_hash);
 }

@@ -270,6 +270,22 @@ int rccl_all_reduce_raw(void* buf, size_t count, int dtype, int op, void* comm, 
   return (int)e;
 }
 
+int rccl_all_gather_raw(const void* in, void* out, size_t count, int dtype, void* comm, hipStream_t stream,
+                        std::string* err) {
+  if (count == 0) return 0;
+  Rccl& r = rccl();
+  const ncclResult_t e = r.all_gather(in, out, count, (ncclDataType_t)dtype, (ncclComm_t)comm, stream);
+  if (e != ncclSuccess && err != nullptr) *err = r.error_string ? r.error_string(e) : "RCCL error";
+  return (int)e;
+}
+
+// ncclCommAbort of a raw communicator (the engine's local-failure path): peers blocked in a
+// collective with this rank see the communicator fail instead of waiting forever
+void rccl_comm_abort_raw(void* comm) {
+  Rccl& r = rccl();
+  if (r.abort != nullptr && comm != nullptr) (void)r.abort((ncclComm_t)comm);
+}
+
 void rccl_comm_destroy(int64_t h, bool abort) {
   Comm* c = get(h);
   {

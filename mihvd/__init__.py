@@ -10,8 +10,8 @@ kernels), ``models`` (MNIST CNN: reference-semantics torch model + fused HIP tra
 ``utils`` (env discovery, checkpoints, data, logging, timeline), ``runner`` (``mihvdrun``).
 """
 from .basics import (Adasum, Average, Max, Min, Product, ReduceOp, Sum, backend, ccl_built, config, cross_rank,
-                     cross_size, cuda_built, ddl_built, device, gloo_built, gloo_enabled, init, is_homogeneous,
+                     cross_size, cuda_built, ddl_built, device, engine_running, gloo_built, gloo_enabled, init, is_homogeneous,
                      is_initialized, local_rank, local_size, mpi_built, mpi_enabled, mpi_threads_supported, nccl_built,
-                     rank, rccl_built, rocm_built, shutdown, size, start_timeline, stop_timeline)
+                     rank, rccl_built, rocm_built, shutdown, size, start_timeline, stop_timeline, suspend_engine)
 
 __version__ = "0.1.0"

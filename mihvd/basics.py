@@ -117,10 +117,14 @@ def init(comm=None, process_sets=None, config: Config | None = None):
             topo = _env.Topology(r, n, lr, ls, 0, 1, topo.master_addr, topo.master_port, "elastic")
         backend = _choose_backend(cfg)
         # ProcessGroupNCCL's event cache hands a retired work's HIP event to the next collective;
-        # when that collective is being captured into a HIP graph (the fused step's RCCL calls) the
-        # watchdog may still query the event through the old work and abort with
-        # hipErrorCapturedEvent. Fresh events per work avoid the race.
-        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+        # when that collective is being captured into a HIP graph the watchdog may still query the
+        # event through the old work and abort with hipErrorCapturedEvent. The fused trainer's
+        # in-graph collectives run on its own communicator (MIHVD_COMM=native, the default) and
+        # never reach the process group; this setting is for the paths that DO capture process-
+        # group collectives: CapturedStep over DistributedOptimizer (mihvd/graphs.py, bench.py
+        # --impl torch-graph) and MIHVD_COMM=torch. MIHVD_PG_CAPTURE=0 leaves torch's default.
+        if os.environ.get("MIHVD_PG_CAPTURE", "1") == "1":
+            os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
         logging.basicConfig(level=getattr(logging, cfg.log_level, logging.INFO),
                             format="[%(asctime)s] [rank " + str(topo.rank) + "] %(message)s")
         if backend == "nccl":
@@ -185,11 +189,12 @@ def init(comm=None, process_sets=None, config: Config | None = None):
         _build_subgroups(topo)
         _start_observability(cfg, topo)
         _start_health(topo, backend)
-        # Horovod's background engine: on by default on the RCCL backend at N > 1 (the native C++
-        # engine), opt-in elsewhere (MIHVD_NEGOTIATE=1: the store-negotiated python executor);
-        # MIHVD_ENGINE=torch turns it off (allreduces straight on the process group)
-        if cfg.engine != "torch" and (cfg.engine == "native" or (
-                topo.size > 1 and (cfg.negotiate or cfg.engine == "python" or (cfg.engine == "auto" and backend == "nccl")))):
+        # Horovod's background engine, opt-in: MIHVD_ENGINE=native (the C++ engine thread over its
+        # own RCCL communicator) or MIHVD_ENGINE=python / MIHVD_NEGOTIATE=1 (the store-negotiated
+        # python executor). auto / torch: allreduces go straight to the process group, which
+        # already orders them (every rank issues the DistributedOptimizer's buckets in the same
+        # static order)
+        if engine_wanted(cfg, topo.size, backend):
             _start_engine(cfg, topo, backend, device)
         _ctx.initialized = True
         atexit.register(shutdown)
@@ -200,6 +205,15 @@ def init(comm=None, process_sets=None, config: Config | None = None):
                 add_process_set(ps)
         if topo.rank == 0:
             log.debug("mihvd initialised: %s backend=%s device=%s config=%s", topo, backend, device, cfg)
+
+
+def engine_wanted(cfg: Config, world: int, backend: str) -> bool:
+    """Whether ``init()`` starts a background engine (MIHVD_ENGINE / MIHVD_NEGOTIATE)."""
+    if cfg.engine == "torch":
+        return False
+    if cfg.engine == "native":
+        return True
+    return world > 1 and (cfg.negotiate or cfg.engine == "python")
 
 
 def _build_subgroups(topo: _env.Topology):
@@ -277,7 +291,12 @@ def _start_health(topo: _env.Topology, backend: str):
     from ._native import runtime
 
     mon = runtime().HealthMonitor(topo.rank, float(os.environ.get("MIHVD_HEALTH_POLL_S", "0.5")), 134)
-    if backend == "nccl":
+    # The monitor watches the communicators this framework owns (NativeComm and the native engine's
+    # attach themselves, mihvd/parallel/rccl.py). The process group's communicator belongs to torch,
+    # which can free it (destroy_process_group outside hvd.shutdown, or its watchdog's abort) while
+    # the monitor thread still polls it; torch's own watchdog covers that communicator. Opt in with
+    # MIHVD_HEALTH_PG=1 (then hvd.shutdown() must be the only teardown path).
+    if backend == "nccl" and os.environ.get("MIHVD_HEALTH_PG", "0") == "1":
         try:
             comm = int(dist.group.WORLD._get_backend(torch.device("cuda"))._comm_ptr())
             lib = _loaded_rccl_path()
@@ -326,6 +345,26 @@ def _start_engine(cfg: Config, topo: _env.Topology, backend: str, device: torch.
     neg = runtime().Negotiator(host, port, topo.rank, topo.size, obj[0][1], cfg.cycle_time_ms / 1000.0, warn,
                                cfg.stall_shutdown_s)
     _ctx.engine = Engine(neg, cfg.fusion_threshold, topo.rank)
+
+
+def suspend_engine(reason: str = "") -> bool:
+    """Flush and stop the background engine, if one runs (a component that issues its own
+    collectives, such as the fused trainer, calls this: an engine thread cycling RCCL calls on a
+    second communicator beside them is the classic cross-communicator deadlock). Returns True if an
+    engine was stopped. Collectives issued later go straight to the process group."""
+    with _ctx.lock:
+        eng = _ctx.engine
+        if eng is None:
+            return False
+        eng.flush(timeout=30)
+        eng.stop()
+        _ctx.engine = None
+    log.info("mihvd engine stopped%s", f": {reason}" if reason else "")
+    return True
+
+
+def engine_running() -> bool:
+    return _ctx.engine is not None
 
 
 def shutdown():

@@ -57,7 +57,7 @@ class Config:
     autotune_log: str = ""                # horovodrun --autotune-log-file: CSV of the candidates
     roctx: bool = False                   # roctx ranges around collectives / steps (rocprofv3 --marker-trace)
     negotiate: bool = False               # route async collectives through the native negotiation engine
-    engine: str = "auto"                  # auto (native on RCCL at N>1) | native (C++ engine thread over RCCL) | python (negotiator + executor thread, MIHVD_NEGOTIATE) | torch (no engine)
+    engine: str = "auto"                  # auto = torch (no engine thread) | native (C++ engine thread over RCCL) | python (negotiator + executor thread, MIHVD_NEGOTIATE) | torch (no engine)
     store: str = "native"                 # rendezvous: native (mihvdrun's C++ store, if present) | torch
     debug_sync: bool = False              # serialized bisection mode: sync after every kernel / collective
     elastic_grace_s: float = 30.0         # elastic: how long a failed collective waits for a new membership

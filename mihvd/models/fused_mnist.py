@@ -1,40 +1,40 @@
 """Fused, graph-replayed data-parallel training step for the reference MNIST CNN on MI355X.
 
-This is the flagship path (bench.py ``--impl fused``). At world size 1 a step is six HIP launches,
-all hand-written CDNA4 kernels from ``csrc/kernels``:
+This is the flagship path (bench.py ``--impl fused``). The default precision is the reference's:
+``precision="fp32"`` (horovod/tensorflow_mnist.py:118-121,130 train fp32 variables with fp32
+placeholders and AdamOptimizer). Every operand stays fp32 and GEMM-shaped work runs on gfx950's
+fp32-input matrix cores (``v_mfma_f32_16x16x4_f32``: exact products, fp32 accumulation;
+csrc/kernels/f32_fwd.hip, f32_bwd.hip). At world size 1 a step is seven hand-written launches:
 
-    conv12_fwd  conv1 (implicit GEMM, K = 25 taps in one MFMA step) -> pooled activations
-                written into conv2's LDS image -> conv2 implicit GEMM, pool-window-major M,
-                bias/ReLU/pool/argmax in registers (MIHVD_CONV12=0: two launches,
-                conv1 as an fp32 VALU direct convolution)                      [MFMA bf16]
-    fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs                    [MFMA bf16]
-    head        slab sum + bias + ReLU + dropout + fc2 + softmax-xent + fc2 backward -> dz
-    fc1_bwd     full-K dz.W3^T tiles (W3 rows in registers, dz in LDS, XCD-aware tile map,
-                pooled-ReLU mask + bf16 cast fused: g2) and, in the same launch, dW3 tiles
-                -> fusion buffer | db3 | dW4 | db4 (MIHVD_FC1_BWD=0: two launches)  [MFMA bf16]
-    conv2_bwd   dgrad (g2 routed through the pool argmax, ReLU mask) -> g1 on chip -> fused
-                conv1 wgrad (dW1/db1) | conv2 wgrad slabs | db2                  [MFMA bf16]
-                + the dense/kernel Adam update streaming in the launch tail
-    conv2_wgrad_reduce  dW2 = sum of the wgrad slabs + Adam for every other parameter
+    f32_conv1_fwd   conv1 (K = 25 taps on MFMA) + bias + ReLU + 2x2 pool/argmax
+    f32_conv2_fwd   conv2 implicit GEMM (pool-window-major rows), bias/ReLU/pool/argmax in registers
+    f32_fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs; the previous step's dense/kernel Adam
+                    update is applied to each W3 fragment as it is read (one read of W3 for both)
+    f32_head        slab sum + bias + ReLU + dropout(0.5) + fc2 + softmax-xent + fc2 backward -> dz
+    f32_fc1_bwd     dgrad dz.W3^T routed through the pool argmax / ReLU mask -> dY2, and dW3, db3,
+                    dW4, db4 written straight into the flat gradient (= fusion) buffer
+    f32_conv2_bwd   conv2 dgrad -> conv1 gradient on chip -> fused conv1 wgrad; conv2 wgrad slabs
+    f32_conv_reduce slab/partial-row reduction + Adam of every parameter but dense/kernel + step bump
 
-With size() > 1 the data plane is either the factor gather (default: all-gather of the bf16
-factors a2/dz so every rank forms the exact all-sample dW3 for the rows whose optimizer it owns,
-then an all-gather of the updated bf16 rows) or bucketed allreduce of the flat gradient buffer
-(bucket "fc", 98.4 % of the bytes, reduced on a side stream while the conv backward runs); the
-optimizer then runs as separate adam_step launches.
+With collectives (size() > 1, or MIHVD_FORCE_COLLECTIVES=1 at size 1) the step's collectives run
+on a framework-owned RCCL communicator (mihvd/parallel/rccl.py NativeComm, MIHVD_COMM=native, the
+default; MIHVD_COMM=torch uses the process group's) on a side stream, inside the same HIP graph:
+by default dense/kernel's gradient is reduce-scattered by rows while the conv backward runs, every
+rank applies Adam to its 1/N of the rows, and the updated fp32 rows are all-gathered while the next
+step's convolutions run (the sharded optimizer); the other gradients are allreduced.
 
-At N=1 everything runs on one stream (a fork/join inside a HIP graph costs more than the
-overlap it would buy when there is no collective to hide).
+``precision="bf16"`` is the MI355X analogue of the reference's ``mixed_float16`` GPU variant
+(tensorflow_mnist_gpu.py:26-28): bf16 MFMA operands with fp32 accumulation, fp32 master weights,
+gradients and Adam state (no loss scaling). Its multi-GPU data plane is the "factor gather": the
+ranks all-gather the bf16 fc1 factors a2/dz so every rank forms the exact all-sample dW3 for the
+rows whose optimizer it owns (over RCCL, or the direct hipIpc/xGMI plane of
+mihvd/parallel/xgmi.py), then all-gather the updated bf16 rows.
 
 Parameters, gradients and Adam slots live in flat fp32 buffers laid out in TF variable order
 (horovod/tensorflow_mnist.py:49-70); every kernel writes its gradient straight into its slot of
 the gradient buffer, which *is* the fusion buffer — there is no pack/unpack copy. The step counter
 and dropout/data indices are device-resident, so ``build_graph(k)`` captures k whole steps
 (including the RCCL calls) into one HIP graph that the host replays with a single launch.
-
-Numerics: bf16 MFMA operands with fp32 accumulation, fp32 master weights and optimizer state,
-fp32 gradients (the MI355X-native equivalent of the reference's ``mixed_float16`` variant,
-tensorflow_mnist_gpu.py:26-28; no loss scaling is needed for bf16).
 """
 from __future__ import annotations
 
@@ -124,7 +124,7 @@ class FusedMNISTTrainer:
         # AdamOptimizer, horovod/tensorflow_mnist.py:118-121,130; csrc/kernels/f32_*.hip), "bf16" =
         # bf16 MFMA operands with fp32 accumulation and fp32 master weights (the MI355X analogue of
         # the mixed_float16 variant, tensorflow_mnist_gpu.py:26-28).
-        precision = (precision or os.environ.get("MIHVD_PRECISION", "bf16")).lower()
+        precision = (precision or os.environ.get("MIHVD_PRECISION", "fp32")).lower()
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
         self.precision = precision
@@ -155,17 +155,34 @@ class FusedMNISTTrainer:
         self.world = int(world_size)
         # MIHVD_FORCE_COLLECTIVES=1 keeps the allreduce path even at size 1 (tests of the RCCL path)
         self.collectives = self.world > 1 or os.environ.get("MIHVD_FORCE_COLLECTIVES") == "1"
-        # MIHVD_COMM=native: the step's collectives go through a framework-owned RCCL communicator
-        # (mihvd/parallel/rccl.py) instead of the process group's
+        # MIHVD_COMM=native (default): the step's collectives go through a framework-owned RCCL
+        # communicator (mihvd/parallel/rccl.py) instead of the process group's; the process group
+        # is the fallback (MIHVD_COMM=torch, or a communicator that cannot be created)
         self.ncomm = None
         if self.collectives:
             from ..parallel import rccl as _rccl
 
+            # the trainer issues its own collectives inside its HIP graph: no engine thread may run
+            # RCCL calls on another communicator beside them (unordered kernels of two communicators
+            # across ranks can deadlock)
+            basics.suspend_engine("the fused trainer owns the step's collectives")
             if _rccl.env_mode() == "native":
                 import torch.distributed as dist
 
                 if dist.is_initialized() and dist.get_backend() == "nccl":
-                    self.ncomm = _rccl.NativeComm(device=self.device)
+                    try:
+                        self.ncomm = _rccl.NativeComm(device=self.device)
+                    except Exception as e:  # pragma: no cover - depends on the RCCL build
+                        import warnings
+
+                        warnings.warn(f"native RCCL communicator unavailable ({e!r}); using the process group's")
+                        self.ncomm = None
+                    # every rank must use the same communicator: any failure moves all to the fallback
+                    flag = torch.tensor([0 if self.ncomm is not None else 1], device=self.device)
+                    dist.all_reduce(flag)
+                    if int(flag.item()) != 0 and self.ncomm is not None:
+                        self.ncomm.close()
+                        self.ncomm = None
         self.rank = basics.rank() if basics.is_initialized() else 0
         self.op = op
         self.compression = compression
@@ -212,7 +229,9 @@ class FusedMNISTTrainer:
         # fp32 step over RCCL: the same option as a reduce-scatter of dW3 by rows, Adam on this rank's
         # 3136/size rows, and an all-gather of the updated fp32 rows overlapping the next step's
         # convolutions (instead of allreducing dW3 and every rank updating all of W3)
-        self._f32_can_shard = (self.f32 and self.collectives and self.world > 1 and 3136 % self.world == 0
+        # (at size 1 with MIHVD_FORCE_COLLECTIVES the same step runs with R = 3136 rows: the exact
+        # multi-rank launch/collective sequence, capture-testable on one GPU)
+        self._f32_can_shard = (self.f32 and self.collectives and 3136 % self.world == 0
                                and compression == "none" and (op is None or ReduceOp(op) in (ReduceOp.Average,
                                                                                               ReduceOp.Sum)))
         if self.f32:

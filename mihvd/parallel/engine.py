@@ -33,7 +33,8 @@ log = logging.getLogger("mihvd.engine")
 
 
 class _Entry:
-    __slots__ = ("name", "kind", "launch", "fuse_key", "tensor", "nbytes", "work", "offset", "error", "launched")
+    __slots__ = ("name", "kind", "launch", "fuse_key", "tensor", "nbytes", "work", "offset", "error", "launched",
+                 "ready", "done")
 
     def __init__(self, name, kind, launch=None, fuse_key=None, tensor=None):
         self.name = name
@@ -46,6 +47,15 @@ class _Entry:
         self.offset = 0
         self.error = None
         self.launched = threading.Event()
+        # device tensors: `ready` is recorded on the submitting thread's current stream (the
+        # producer of the tensor), the executor's stream waits on it before reading; `done` is
+        # recorded on the executor's stream behind a fused copy-out, and wait() orders the
+        # caller's current stream after it
+        self.ready = None
+        self.done = None
+        if tensor is not None and tensor.is_cuda:
+            self.ready = torch.cuda.Event()
+            self.ready.record(torch.cuda.current_stream(tensor.device))
 
 
 class DeferredWork:
@@ -63,13 +73,17 @@ class DeferredWork:
             raise e.error
         if e.work is not None:
             e.work.wait()
+        if e.done is not None:
+            torch.cuda.current_stream(e.tensor.device).wait_event(e.done)
         return True
 
     def is_completed(self) -> bool:
         e = self._e
         if not e.launched.is_set():
             return False
-        return e.work is None or e.work.is_completed()
+        if e.work is not None and not e.work.is_completed():
+            return False
+        return e.done is None or e.done.query()
 
 
 class Engine:
@@ -187,6 +201,12 @@ class Engine:
         e0 = group[0]
         torch_op, process_group = _decode[e0.fuse_key[2]]
         try:
+            cuda = e0.tensor.is_cuda
+            if cuda:
+                cur = torch.cuda.current_stream(e0.tensor.device)
+                for g in group:  # the producers of every tensor of the group
+                    if g.ready is not None:
+                        cur.wait_event(g.ready)
             if len(group) == 1:
                 e0.work = dist.all_reduce(e0.tensor, op=torch_op, group=process_group, async_op=True)
             else:
@@ -207,10 +227,18 @@ class Engine:
                 # MEMCPY_OUT_FUSION_BUFFER right behind the collective: on GPUs the wait only orders
                 # the current stream after it; gloo's CPU work completes here
                 work.wait()
+                done = None
+                if cuda:
+                    done = torch.cuda.Event()
                 for g in group:
                     k = g.tensor.numel()
                     g.tensor.copy_(flat[g.offset:g.offset + k].view_as(g.tensor))
                     g.work = None
+                if done is not None:
+                    # the callers' streams wait for the copy-out, not just the collective
+                    done.record(torch.cuda.current_stream(e0.tensor.device))
+                    for g in group:
+                        g.done = done
                 self.fused_launches += 1
         except Exception as exc:
             for g in group:

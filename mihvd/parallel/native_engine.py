@@ -1,18 +1,23 @@
 """The native collective engine (``csrc/kernels/engine.cpp``): Horovod's background loop in C++.
 
-``MIHVD_ENGINE=native`` (or ``MIHVD_NEGOTIATE=1`` on the RCCL backend, where ``MIHVD_ENGINE=auto``
-picks it) routes every asynchronous allreduce — the DistributedOptimizer's bucket allreduces issued
-from gradient hooks, ``allreduce_async`` — through one C++ thread per process that owns a
-framework RCCL communicator (:class:`mihvd.parallel.rccl.NativeComm`) and a high-priority HIP
-stream. Each cycle (``HOROVOD_CYCLE_TIME``, 1 ms) the thread negotiates readiness with one small
-RCCL allreduce of a per-slot count + signature-hash vector (Horovod's bit-vector response cache, on
-the GPU), fuses ready tensors into a persistent fusion buffer up to ``HOROVOD_FUSION_THRESHOLD``,
-reduces, copies out, and records a completion event per request; the stall inspector reports
-collectives that only some ranks reached and aborts after ``HOROVOD_STALL_SHUTDOWN_TIME_SECONDS``.
+``MIHVD_ENGINE=native`` (opt-in) routes every asynchronous allreduce — the DistributedOptimizer's
+bucket allreduces issued from gradient hooks, ``allreduce_async`` — through one C++ thread per
+process that owns two framework RCCL communicators (:class:`mihvd.parallel.rccl.NativeComm`): a
+control communicator for negotiation and a data communicator for the fused allreduces, each on its
+own high-priority HIP stream. The thread is event-driven: it sleeps until a tensor is enqueued, then
+negotiates readiness with one small RCCL allreduce of a per-slot count + signature-hash vector
+(Horovod's bit-vector response cache, on the GPU), packs ready tensors into a persistent fusion
+buffer (one batched pack kernel) up to ``HOROVOD_FUSION_THRESHOLD``, reduces, unpacks (one kernel)
+and records a pooled completion event per request, without waiting for the data stream: the next
+negotiation overlaps the previous cycle's collectives. ``HOROVOD_CYCLE_TIME`` only bounds how long
+a rank whose work is partly ready waits before re-negotiating. The stall inspector reports
+collectives that only some ranks reached (and negotiations peers never joined) and aborts after
+``HOROVOD_STALL_SHUTDOWN_TIME_SECONDS``.
 
-Ranks may enqueue tensors in different orders: a collective runs only once every rank enqueued its
-signature (name, dtype, size, op), and every rank derives the same launch order from the same
-summed vector, so mismatched autograd schedules cannot deadlock or mismatch RCCL calls
+Ranks may enqueue tensors in different orders: slots are numbered from data every rank holds (the
+sorted union of newly announced signature hashes, all-gathered), a collective runs only once every
+rank enqueued its signature (name, dtype, size, op), and every rank derives the same launch order
+from the same summed vector, so mismatched autograd schedules cannot deadlock or mismatch RCCL calls
 (horovod/tensorflow_mnist.py:133 relies on this implicitly).
 
 Non-allreduce collectives (broadcast, allgather, Adasum) keep running on the process group's
@@ -61,14 +66,15 @@ class NativeEngine:
 
         self._o = _ops.load()
         self.comm = comm if comm is not None else NativeComm(device=device)
+        self.ctrl_comm = NativeComm(device=self.comm.device)  # negotiation, on its own stream
         self.world = self.comm.world
         # an engine started at world size 1 (MIHVD_ENGINE=native) still carries every allreduce, as
         # Horovod's does: the same negotiation / fusion / completion path as at N ranks
         self.world_one = self.world == 1
         self.fusion_threshold = int(cfg.fusion_threshold)
         warn = 0.0 if cfg.stall_check_disable else float(cfg.stall_check_s)
-        self._o.engine_start(self.comm.handle, self.fusion_threshold, max(cfg.cycle_time_ms, 0.05) / 1000.0, warn,
-                             float(cfg.stall_shutdown_s), int(max_slots))
+        self._o.engine_start(self.comm.handle, self.ctrl_comm.handle, self.fusion_threshold,
+                             max(cfg.cycle_time_ms, 0.05) / 1000.0, warn, float(cfg.stall_shutdown_s), int(max_slots))
         self._lock = threading.Lock()
         self._outstanding: set = set()
 
@@ -95,12 +101,14 @@ class NativeEngine:
             w.wait()
 
     def stats(self) -> dict:
-        c, n, t, fb, slots, stalls = (int(x) for x in self._o.engine_stats())
-        return {"cycles": c, "collectives": n, "tensors": t, "fused_bytes": fb, "slots": slots, "stall_warnings": stalls}
+        c, n, t, fb, slots, stalls, wake, idle, ann = (int(x) for x in self._o.engine_stats())
+        return {"cycles": c, "collectives": n, "tensors": t, "fused_bytes": fb, "slots": slots, "stall_warnings": stalls,
+                "wakeups": wake, "idle_waits": idle, "announce_rounds": ann}
 
     def stop(self):
         self.flush()
         self._o.engine_stop()
+        self.ctrl_comm.close()
         self.comm.close()
 
 
@@ -122,8 +130,16 @@ def plan(ctrl, world: int, hashes, nbytes, keys, threshold: int):
     return groups, [int(s) for s in out[cut + 1:]]
 
 
+def assign(gathered, world: int, assigned=()):
+    """The engine's slot agreement on an all-gathered announce array (CPU; for tests): the hashes
+    that get new slots, in the order every rank appends them."""
+    o = _ops.load()
+    return [int(h) & 0xFFFFFFFF for h in o.engine_assign(torch.as_tensor(gathered, dtype=torch.int64).to(torch.int32),
+                                                         int(world), torch.as_tensor(list(assigned), dtype=torch.int64))]
+
+
 def signature_hash(name: str, dtype_code: int, numel: int, op: int) -> int:
     return int(_ops.load().engine_signature_hash(f"{name}|{dtype_code}|{numel}|{op}"))
 
 
-__all__ = ["NativeEngine", "NativeWork", "plan", "signature_hash"]
+__all__ = ["NativeEngine", "NativeWork", "assign", "plan", "signature_hash"]

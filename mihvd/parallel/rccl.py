@@ -9,8 +9,12 @@ caller's current HIP stream — the trainer's side stream, or a stream being cap
 HIP graph — with no process-group work objects around them, and the communicator is registered
 with the native health monitor (async-error polling → abort, csrc/runtime/health.cc).
 
-``MIHVD_COMM=native`` makes the fused trainer's collectives use it (default ``torch``: the
-process group's RCCL communicator).
+The fused trainer's collectives use it by default (``MIHVD_COMM=native``); ``MIHVD_COMM=torch``
+selects the process group's RCCL communicator instead, which is also the fallback when the
+native communicator cannot be created. The process group then only carries the bootstrap (the
+unique-id broadcast) and host-synchronised control traffic (initial broadcast, barriers), never a
+collective inside the step's HIP graph — so torch's ProcessGroupNCCL watchdog never sees a
+captured event.
 """
 from __future__ import annotations
 
@@ -25,9 +29,10 @@ _OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
 
 
 def env_mode() -> str:
-    """``MIHVD_COMM``: ``torch`` (the process group's communicator, default) or ``native``."""
-    v = os.environ.get("MIHVD_COMM", "torch").strip().lower()
-    return "native" if v in ("native", "rccl", "1", "on") else "torch"
+    """``MIHVD_COMM``: ``native`` (a framework-owned communicator, default) or ``torch`` (the
+    process group's)."""
+    v = os.environ.get("MIHVD_COMM", "native").strip().lower()
+    return "torch" if v in ("torch", "pg", "0", "off") else "native"
 
 
 class NativeComm:

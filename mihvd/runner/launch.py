@@ -245,9 +245,34 @@ def _free_port(addr="127.0.0.1") -> int:
         return s.getsockname()[1]
 
 
+# Variables forwarded to every rank by default, like horovodrun (which forwards the launcher's
+# environment): the framework's and Horovod's knobs, the collective library's, the ROCm runtime's
+# and the Python path. mpirun forwards only its -x list; in an MPIJob the ranks on the worker pods
+# are started over ssh, whose sessions do not inherit the container's Docker ENV, so the settings
+# an operator puts on the launcher must travel with the command. MIHVD_FORWARD_PREFIXES overrides
+# the list ("" forwards nothing beyond -x); *_VISIBLE_DEVICES is never forwarded (the launcher
+# pod's GPU view is not the worker's).
+DEFAULT_FORWARD_PREFIXES = ("MIHVD_", "HOROVOD_", "NCCL_", "RCCL_", "HSA_", "HIP_", "ROCR_", "TORCH_NCCL_",
+                            "PYTORCH_", "OMP_NUM_THREADS", "PYTHONPATH")
+_NEVER_FORWARD = ("MIHVD_LAUNCHED", "MIHVD_STORE_ADDR", "MIHVD_WORKER_ID", "MIHVD_ELASTIC", "MIHVD_DEVICE_INDEX")
+
+
+def forward_prefixes(base=None) -> tuple[str, ...]:
+    base = os.environ if base is None else base
+    v = base.get("MIHVD_FORWARD_PREFIXES")
+    if v is None:
+        return DEFAULT_FORWARD_PREFIXES
+    return tuple(p.strip() for p in v.split(",") if p.strip())
+
+
 def build_rank_env(spec: LaunchSpec, rank, local_rank, local_size, node, master_addr, master_port, base_env=None):
     base = dict(os.environ if base_env is None else base_env)
     env = {}
+    pre = forward_prefixes(base)
+    for k, v in base.items():
+        if (pre and k.startswith(pre) and not k.endswith("_VISIBLE_DEVICES") and k not in _NEVER_FORWARD
+                and k != "MIHVD_FORWARD_PREFIXES"):
+            env[k] = v
     for k, v in spec.env_forward.items():
         if v is not None:
             env[k] = v
@@ -262,6 +287,19 @@ def build_rank_env(spec: LaunchSpec, rank, local_rank, local_size, node, master_
         "MIHVD_LAUNCHED": "1",
     })
     return env
+
+
+def remote_command(spec: LaunchSpec, renv: dict[str, str], cwd: str | None = None) -> str:
+    """The shell command a remote rank runs (after ssh): cd to the launcher's working directory,
+    then the program under exactly ``renv`` on top of the ssh session's own environment."""
+    exports = " ".join(f"{k}={shlex.quote(v)}" for k, v in renv.items())
+    return (f"cd {shlex.quote(cwd or os.getcwd())} && env {exports} " +
+            " ".join(shlex.quote(c) for c in spec.command))
+
+
+def ssh_command(spec: LaunchSpec, host: str, renv: dict[str, str]) -> list[str]:
+    return (["ssh", "-o", "StrictHostKeyChecking=no"] + (["-p", str(spec.ssh_port)] if spec.ssh_port else []) +
+            [host, remote_command(spec, renv)])
 
 
 class _Proc:
@@ -342,9 +380,7 @@ def launch(spec: LaunchSpec) -> int:
             env.update(renv)
             cmd = spec.command
         else:
-            exports = " ".join(f"{k}={shlex.quote(v)}" for k, v in renv.items())
-            remote = f"cd {shlex.quote(os.getcwd())} && env {exports} " + " ".join(shlex.quote(c) for c in spec.command)
-            cmd = ["ssh", "-o", "StrictHostKeyChecking=no"] + (["-p", str(spec.ssh_port)] if spec.ssh_port else []) + [host, remote]
+            cmd = ssh_command(spec, host, renv)
             env = dict(os.environ)
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
         procs.append(_Proc(wid, p))

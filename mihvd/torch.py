@@ -4,9 +4,9 @@ Everything the reference's entrypoints call through ``horovod.tensorflow`` /
 ``horovod.tensorflow.keras`` is available here for PyTorch-ROCm models.
 """
 from .basics import (Adasum, Average, Max, Min, Product, ReduceOp, Sum, backend, ccl_built, config, cross_rank,
-                     cross_size, cuda_built, ddl_built, device, gloo_built, gloo_enabled, init, is_homogeneous,
+                     cross_size, cuda_built, ddl_built, device, engine_running, gloo_built, gloo_enabled, init, is_homogeneous,
                      is_initialized, local_rank, local_size, mpi_built, mpi_enabled, mpi_threads_supported, nccl_built,
-                     rank, rccl_built, rocm_built, shutdown, size, start_timeline, stop_timeline)
+                     rank, rccl_built, rocm_built, shutdown, size, start_timeline, stop_timeline, suspend_engine)
 from .parallel.collectives import (allgather, allgather_async, allgather_object, allreduce, allreduce_,
                                    allreduce_async, allreduce_async_, alltoall, alltoall_async, barrier, broadcast,
                                    broadcast_, broadcast_async, broadcast_async_, broadcast_object, grouped_allgather,

@@ -20,7 +20,7 @@ def main():
     from mihvd.models.fused_mnist import FC_START as FC, W3_START as W3, FusedMNISTTrainer
 
     B = 100
-    tr = FusedMNISTTrainer(batch_size=B, seed=0, device="cuda")
+    tr = FusedMNISTTrainer(batch_size=B, seed=0, device="cuda", precision="bf16")
     x = torch.rand(B, 784, device="cuda")
     y = torch.randint(0, 10, (B,), device="cuda")
     tr.train_step(x, y)

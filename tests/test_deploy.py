@@ -32,15 +32,79 @@ def _check_mpijob(job, np_, slots):
     return worker
 
 
+def _rank_env_of(job):
+    """The environment a rank on a worker pod receives: mihvdrun's forwarded set, built from the
+    launcher container's env (the only env that reaches an ssh-started rank)."""
+    launcher = job["spec"]["mpiReplicaSpecs"]["Launcher"]["template"]["spec"]["containers"][0]
+    ls = L.parse_args([str(a) for a in launcher["args"]])
+    lenv = {"PATH": "/usr/bin:/bin", "LD_LIBRARY_PATH": "/opt/rocm/lib"}
+    lenv.update({e["name"]: str(e["value"]) for e in launcher.get("env", [])})
+    return ls, L.build_rank_env(ls, 9, 1, 8, 1, "10.0.0.1", 29500, base_env=lenv)
+
+
 def test_mi355x_mpijob():
     (job,) = _load("mpijob-mi355x.yaml")
     worker = _check_mpijob(job, 8, 8)
     c = worker["template"]["spec"]["containers"][0]
     assert c["resources"]["limits"]["amd.com/gpu"] == 8
-    env = {e["name"]: e["value"] for e in c["env"]}
-    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # settings on the worker container would only reach its sshd, never an ssh-started rank
+    assert not c.get("env"), "put rank settings on the launcher (mihvdrun forwards them)"
+    ls, renv = _rank_env_of(job)
+    assert renv["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert renv["MIHVD_STALL_CHECK_TIME_SECONDS"] == "60" and renv["MIHVD_STALL_SHUTDOWN_TIME_SECONDS"] == "600"
+    assert "MIHVD_STALL_CHECK_TIME_SECONDS" in ls.env_forward
+    assert renv["RANK"] == "9" and renv["LOCAL_RANK"] == "1"
     vols = {v["name"]: v for v in worker["template"]["spec"]["volumes"]}
     assert vols["checkpoints"]["persistentVolumeClaim"]["claimName"] == "mihvd-checkpoints"
+
+
+def test_mpijob_rank_env_starts_no_engine_thread():
+    """At N > 1 on RCCL the job's ranks start no background engine (the fused trainer issues its
+    own collectives; a second communicator cycling beside it could deadlock)."""
+    from mihvd.basics import engine_wanted
+    from mihvd.config import Config
+
+    for name in ("mpijob-mi355x.yaml", "mpijob-mi355x-elastic.yaml"):
+        (job,) = _load(name)
+        _, renv = _rank_env_of(job)
+        assert not engine_wanted(Config.from_env(renv), 8, "nccl"), name
+    assert not engine_wanted(Config.from_env({}), 8, "nccl")
+    assert engine_wanted(Config.from_env({"MIHVD_ENGINE": "native"}), 8, "nccl")
+    assert engine_wanted(Config.from_env({"MIHVD_NEGOTIATE": "1"}), 2, "gloo")
+
+
+def test_launcher_forwards_framework_env_by_default():
+    """horovodrun-style forwarding: MIHVD_* / HOROVOD_* / NCCL_* / HSA_* and PYTHONPATH reach every
+    rank without -x; *_VISIBLE_DEVICES and launcher-private variables do not; MIHVD_FORWARD_PREFIXES
+    narrows it."""
+    ls = L.parse_args(["-np", "2", "-x", "FOO", "python", "x.py"])
+    base = {"MIHVD_X": "1", "HOROVOD_FUSION_THRESHOLD": "2", "NCCL_DEBUG": "INFO", "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+            "PYTHONPATH": "/opt/mihvd", "HIP_VISIBLE_DEVICES": "3", "MIHVD_STORE_ADDR": "a:1", "FOO": "f",
+            "UNRELATED": "u"}
+    env = L.build_rank_env(ls, 1, 1, 2, 0, "127.0.0.1", 1234, base_env=base)
+    for k in ("MIHVD_X", "HOROVOD_FUSION_THRESHOLD", "NCCL_DEBUG", "HSA_ENABLE_IPC_MODE_LEGACY", "PYTHONPATH", "FOO"):
+        assert env[k] == base[k], k
+    for k in ("HIP_VISIBLE_DEVICES", "MIHVD_STORE_ADDR", "UNRELATED"):
+        assert k not in env, k
+    env = L.build_rank_env(ls, 1, 1, 2, 0, "127.0.0.1", 1234, base_env=dict(base, MIHVD_FORWARD_PREFIXES=""))
+    assert "MIHVD_X" not in env and env["FOO"] == "f"
+
+
+def test_remote_rank_command_imports_mihvd_without_inherited_env(tmp_path):
+    """The command an ssh-started rank runs (launch.remote_command) under an EMPTY environment
+    (`env -i`, as an ssh session on a worker pod: no Docker ENV): the launcher's forwarded set alone
+    makes mihvd importable and carries the rank's settings."""
+    import sys
+
+    ls = L.parse_args(["-np", "2", "-x", "PATH", sys.executable, "-c",
+                       "import os, mihvd, mihvd.runner; print('OK', os.environ['RANK'], "
+                       "os.environ['MIHVD_STALL_CHECK_TIME_SECONDS'])"])
+    base = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"), "PYTHONPATH": ROOT, "MIHVD_STALL_CHECK_TIME_SECONDS": "60"}
+    renv = L.build_rank_env(ls, 1, 1, 2, 1, "127.0.0.1", 1234, base_env=base)
+    cmd = L.remote_command(ls, renv, cwd=str(tmp_path))
+    out = subprocess.run(["env", "-i", "sh", "-c", cmd], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split() == ["OK", "1", "60"], out.stdout
 
 
 def test_cpu_mpijob_matches_reference_topology():
@@ -72,6 +136,10 @@ def test_deploy_script_dry_run():
 def test_dockerfile_builds_native_for_gfx950():
     text = open(os.path.join(DEPLOY, "Dockerfile")).read()
     assert "mihvd._build all" in text and "gfx950" in text and "openssh-server" in text
+    # installed site-wide (a .pth in site-packages), not through Docker ENV, which ssh-started ranks
+    # never see
+    assert "mihvd.pth" in text and "site.getsitepackages()" in text
+    assert "ENV PYTHONPATH" not in text
 
 
 def test_elastic_mpijob():

@@ -337,3 +337,116 @@ def test_f32_next_conv1_in_reduce_launch_is_bitwise(ops, monkeypatch):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     assert a._c1_sync.tolist() == [0, 0, 0, 0], a._c1_sync.tolist()
     a.check_xgmi()
+
+
+def _f32_head_mask(ops, B, step, seed, rate=0.5):
+    """The fp32 head's dropout keep-mask for (seed, step): run it on all-positive pre-activations
+    (zpart slabs of 1/14, so z = 1 + b3 = 1 everywhere) and read which h survived."""
+    zp = torch.full((14, B, 1024), 1.0 / 14, device="cuda")
+    st = torch.tensor([step, 0, 0, 0], device="cuda", dtype=torch.int64)
+    h = torch.empty(B, 1024, device="cuda")
+    ops.f32_head_fwd_bwd(zp, torch.zeros(1024, device="cuda"), torch.zeros(1024, 10, device="cuda"),
+                         torch.zeros(10, device="cuda"), torch.zeros(B, device="cuda", dtype=torch.int64), None, st, seed,
+                         rate, h, torch.empty_like(h), torch.empty(B, 10, device="cuda"), torch.empty(B, 2, device="cuda"))
+    return h > 0, h, st
+
+
+def test_f32_head_dropout_semantics(ops):
+    """The reference's dropout(rate=0.5) when training (tensorflow_mnist.py:65-67) on the fp32 head:
+    keep fraction 0.5, kept values scaled by 2, dz zero exactly where h was dropped, the mask keyed
+    on the forward step state[0] (not on the optimizer counter the head bumps) and identical to the
+    bf16 head's mask for the same (seed, step)."""
+    B = 100
+    keep, h, st = _f32_head_mask(ops, B, 7, 123)
+    assert abs(keep.float().mean().item() - 0.5) < 0.01
+    assert torch.allclose(h[keep], torch.full_like(h[keep], 2.0), rtol=1e-6)
+    assert int(st[1]) == 1 and int(st[0]) == 7
+    keep2, _, _ = _f32_head_mask(ops, B, 7, 123)
+    keep3, _, _ = _f32_head_mask(ops, B, 8, 123)
+    keep4, _, _ = _f32_head_mask(ops, B, 7, 124)
+    assert torch.equal(keep, keep2) and not torch.equal(keep, keep3) and not torch.equal(keep, keep4)
+    # the bf16 head draws the same mask (one RNG, common.h dropout_keep)
+    zp = torch.ones(7, B, 1024, device="cuda")
+    hb = torch.empty(B, 1024, device="cuda", dtype=torch.bfloat16)
+    stb = torch.tensor([7, 0, 0, 0], device="cuda", dtype=torch.int64)
+    ops.head_fwd_bwd(zp, torch.zeros(1024, device="cuda"), torch.zeros(1024, 10, device="cuda"),
+                     torch.zeros(10, device="cuda"), torch.zeros(B, device="cuda", dtype=torch.int64), None, stb, 123,
+                     0.5, hb, torch.empty_like(hb), torch.empty(B, 10, device="cuda"), torch.empty(B, 2, device="cuda"))
+    assert torch.equal(hb.float() > 0, keep)
+    # dz on random data: exactly zero where dropped, and equal to autograd through the same mask
+    g = torch.Generator(device="cuda").manual_seed(31)
+    zpart = torch.randn(14, B, 1024, device="cuda", generator=g) * 0.1
+    b3 = torch.randn(1024, device="cuda", generator=g) * 0.1
+    w4 = torch.randn(1024, 10, device="cuda", generator=g) * 0.05
+    b4 = torch.randn(10, device="cuda", generator=g) * 0.1
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    st = torch.tensor([7, 0, 0, 0], device="cuda", dtype=torch.int64)
+    h = torch.empty(B, 1024, device="cuda")
+    dz = torch.empty_like(h)
+    dlog, stats = torch.empty(B, 10, device="cuda"), torch.empty(B, 2, device="cuda")
+    ops.f32_head_fwd_bwd(zpart, b3, w4, b4, y, None, st, 123, 0.5, h, dz, dlog, stats)
+    assert torch.all(dz[~keep] == 0) and torch.all(h[~keep] == 0)
+    zr = (zpart.sum(0) + b3).requires_grad_(True)
+    hr = F.relu(zr) * keep.float() * 2.0
+    loss = F.cross_entropy(hr @ w4 + b4, y)
+    loss.backward()
+    assert rel_err(h, hr) < 1e-6
+    assert abs(stats[:, 0].mean().item() - loss.item()) < 1e-5
+    assert rel_err(dz, zr.grad) < 1e-5
+
+
+def _masked_reference_loss(model, x, mask):
+    """The stock fp32 model's forward with the dropout mask given (the kernel's, exported)."""
+    B = x.shape[0]
+    xi = x.reshape(B, 28, 28, 1).permute(0, 3, 1, 2)
+    w1 = model.conv_layer1.conv2d.kernel.permute(3, 2, 0, 1)
+    w2 = model.conv_layer2.conv2d.kernel.permute(3, 2, 0, 1)
+    h = F.max_pool2d(F.relu(F.conv2d(xi, w1, model.conv_layer1.conv2d.bias, padding=2)), 2, 2)
+    h = F.max_pool2d(F.relu(F.conv2d(h, w2, model.conv_layer2.conv2d.bias, padding=2)), 2, 2)
+    h = h.permute(0, 2, 3, 1).reshape(B, 3136)
+    h = F.relu(h @ model.dense.kernel + model.dense.bias) * mask.float() * 2.0
+    return h @ model.dense_1.kernel + model.dense_1.bias
+
+
+@pytest.mark.parametrize("B", [8, 100])
+def test_f32_step_with_dropout_matches_fp32_model(ops, B):
+    """One fp32 fused step with the headline's dropout 0.5: the kernel's mask, exported and applied
+    in torch, gives the stock fp32 model the same loss, every gradient and the TF1 Adam update."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.models.mnist import TF_PARAM_ORDER, MNISTConvNet
+
+    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, dropout=0.5, seed=3, device="cuda", precision="fp32")
+    g = torch.Generator(device="cuda").manual_seed(8)
+    x = torch.rand(B, 784, device="cuda", generator=g)
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    step0 = int(tr.state[0].item())
+    mask, _, _ = _f32_head_mask(ops, B, step0, tr.seed)
+    ref = MNISTConvNet(impl="torch", seed=3, dropout_rate=0.0).cuda()
+    loss = F.cross_entropy(_masked_reference_loss(ref, x, mask), y)
+    loss.backward()
+    out = tr.train_step(x, y)
+    torch.cuda.synchronize()
+    assert abs(out["loss"].item() - loss.item()) < 1e-5 * max(1.0, loss.item())
+    named = dict(ref.ordered_parameters())
+    for name in TF_PARAM_ORDER:
+        e = rel_err(tr.gview(name), named[name].grad)
+        assert e < 2e-5, (name, e)
+    for name in TF_PARAM_ORDER:
+        p = named[name].detach().double().clone()
+        m, v = torch.zeros_like(p), torch.zeros_like(p)
+        _tf_adam_(p, named[name].grad.double(), m, v, 1, 1e-3)
+        d_ref = p - named[name].detach().double()
+        d_tr = tr.pview(name).double() - named[name].detach().double()
+        assert rel_err(d_tr, d_ref) < 1e-3, name
+    # the next step draws a new mask (keyed on the advanced forward step)
+    assert int(tr.state[0].item()) == step0 + 1
+
+
+def test_trainer_default_precision_is_fp32(ops, monkeypatch):
+    """The reference trains fp32 (tensorflow_mnist.py:118-121,130): so does a FusedMNISTTrainer built
+    without a precision argument (MIHVD_PRECISION unset)."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    monkeypatch.delenv("MIHVD_PRECISION", raising=False)
+    tr = FusedMNISTTrainer(batch_size=8, device="cuda")
+    assert tr.precision == "fp32" and tr.f32 and tr.shadow is None

@@ -20,16 +20,27 @@ def _gpu():
         pytest.skip("needs a GPU")
 
 
-@pytest.mark.parametrize("shard,xgmi", [("0", "off"), ("1", "off"), ("0", "on"), ("1", "on"), ("1", "auto")])
-def test_collectives_inside_hip_graph(tmp_path, shard, xgmi):
-    """World 1 with the collective data plane forced on, captured in the trainer's HIP graph and
-    replayed; must equal the trainer without collectives bit for bit. shard=1: the sharded
-    dense/kernel optimizer, whose bf16 row gather runs on the side stream across step boundaries.
-    xgmi=off: RCCL; on: the direct xGMI plane (all four collectives in the graph); auto: plane
-    selection (validation against RCCL + timed replays of both planes) first."""
+@pytest.mark.parametrize("prec,shard,xgmi,comm", [
+    ("fp32", "1", "off", "native"), ("fp32", "0", "off", "native"), ("fp32", "1", "off", "torch"),
+    ("bf16", "0", "off", "native"), ("bf16", "1", "off", "native"), ("bf16", "0", "on", "native"),
+    ("bf16", "1", "on", "native"), ("bf16", "1", "auto", "native")])
+def test_collectives_inside_hip_graph(tmp_path, prec, shard, xgmi, comm):
+    """World 1 with the collective data plane forced on, captured in the trainer's HIP graph (2 x
+    5-step graphs... 4 replays) and replayed; must equal the trainer without collectives bit for bit.
+    fp32 shard=1 is the exact step bench.py runs at N > 1 (reduce-scatter of dW3 rows on the side
+    stream, Adam on this rank's rows, all-gather of the updated fp32 rows carried across the step
+    boundary by an event), here with R = 3136 rows. bf16 shard=1: the sharded dense/kernel optimizer
+    of the factor-gather plane, whose bf16 row gather runs on the side stream across step
+    boundaries. xgmi=off: RCCL; on: the direct xGMI plane (all four collectives in the graph); auto:
+    plane selection (validation against RCCL + timed replays of both planes) first. comm=native:
+    the framework-owned communicator (the default); torch: the process group's (the fallback)."""
     _gpu()
     env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3=shard,
-               MIHVD_XGMI=xgmi)
+               MIHVD_XGMI=xgmi, MIHVD_TEST_PRECISION=prec, MIHVD_COMM=comm)
+    if prec == "fp32" and shard == "1" and comm == "native":
+        # an engine thread started by init() must be stopped by the trainer (one communicator
+        # issuing the step's collectives)
+        env["MIHVD_ENGINE"] = "native"
     for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
         env.pop(k, None)
     p = subprocess.run([sys.executable, WORKER, "rccl_graph", str(tmp_path)], env=env, capture_output=True, text=True,
@@ -39,6 +50,8 @@ def test_collectives_inside_hip_graph(tmp_path, shard, xgmi):
     assert r["captured"], "the collectives could not be captured into the HIP graph"
     assert r["steps"] == r["pre_steps"] + 22 and r["bitwise"], r
     assert r["shard"] == (shard == "1")
+    assert r["precision"] == prec and r["native_comm"] == (comm == "native"), r
+    assert r["engine_running"] is False, r
     if xgmi == "on":
         assert r["plane"] == "xgmi", r
     elif xgmi == "off":

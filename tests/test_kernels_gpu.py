@@ -339,7 +339,7 @@ def test_fused_step_matches_emulated_reference(ops, B):
     from mihvd.models.fused_mnist import FusedMNISTTrainer
     from mihvd.models.mnist import MNISTConvNet, TF_PARAM_ORDER
 
-    tr = FusedMNISTTrainer(batch_size=B, lr=0.0, dropout=0.0, seed=3, device="cuda")
+    tr = FusedMNISTTrainer(batch_size=B, lr=0.0, dropout=0.0, seed=3, device="cuda", precision="bf16")
     tr.keep_w3_grad = True  # dW3 is consumed by the fused W3 Adam; also store it for the comparison
     g = torch.Generator(device="cuda").manual_seed(8)
     x = torch.rand(B, 784, device="cuda", generator=g)
@@ -363,7 +363,7 @@ def test_fused_training_converges_and_graph_replays(ops):
     (x, y), _ = synthetic_mnist(n_train=3000, n_test=10, seed=5)
     X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
     Y = torch.from_numpy(y.astype("int64")).cuda()
-    tr = FusedMNISTTrainer(batch_size=100, lr=1e-3, seed=0, device="cuda")
+    tr = FusedMNISTTrainer(batch_size=100, lr=1e-3, seed=0, device="cuda", precision="bf16")
     tr.set_device_dataset(X, Y)
     assert tr.build_graph(steps_per_replay=10)
     first = None
@@ -392,7 +392,7 @@ def test_fused_loss_autograd_matches_trainer(ops):
     model = MNISTConvNet(impl="hip", seed=3).cuda()
     loss, acc = fused_mnist_loss(model, x, y, training=False, return_accuracy=True)
     loss.backward()
-    tr = FusedMNISTTrainer(batch_size=B, lr=0.0, dropout=0.0, seed=3, device="cuda")
+    tr = FusedMNISTTrainer(batch_size=B, lr=0.0, dropout=0.0, seed=3, device="cuda", precision="bf16")
     tr.keep_w3_grad = True
     out = tr.train_step(x, y)
     torch.cuda.synchronize()
@@ -472,7 +472,7 @@ def test_adam_pipeline_matches_serial(ops, monkeypatch):
     for pipe in ("0", "1"):
         monkeypatch.setenv("MIHVD_ADAM_PIPELINE", pipe)
         monkeypatch.setenv("MIHVD_ADAM_BLOCKS", "128" if pipe == "1" else "0")
-        tr = FusedMNISTTrainer(batch_size=100, seed=4, device="cuda", dropout=0.0)
+        tr = FusedMNISTTrainer(batch_size=100, seed=4, device="cuda", precision="bf16", dropout=0.0)
         assert tr.pipeline == (pipe == "1")
         if p_init is None:
             p_init = tr.params.clone()
@@ -501,7 +501,7 @@ def test_fused_w3_adam_matches_separate_optimizer(ops, monkeypatch):
     out = []
     for fuse in ("0", "1"):
         monkeypatch.setenv("MIHVD_FUSE_W3_ADAM", fuse)
-        tr = FusedMNISTTrainer(batch_size=100, seed=4, device="cuda")
+        tr = FusedMNISTTrainer(batch_size=100, seed=4, device="cuda", precision="bf16")
         assert tr.fuse_w3 == (fuse == "1")
         tr.keep_w3_grad = True
         tr.set_device_dataset(X, Y, shuffle=False)
@@ -528,7 +528,7 @@ def test_fused_optimizer_tail_matches_separate_adam(ops, monkeypatch):
     out = []
     for fused in ("0", "1"):
         monkeypatch.setenv("MIHVD_FUSED_OPT", fused)
-        tr = FusedMNISTTrainer(batch_size=100, seed=5, device="cuda")
+        tr = FusedMNISTTrainer(batch_size=100, seed=5, device="cuda", precision="bf16")
         assert tr.fused_opt == (fused == "1")
         tr.set_device_dataset(X, Y, shuffle=False)
         tr.build_graph(steps_per_replay=5, warmup=2)
@@ -560,7 +560,7 @@ def test_folded_reduction_matches_separate_launches(ops, monkeypatch, B):
     for fused, fold in (("0", "0"), ("1", "1"), ("1", "0")):
         monkeypatch.setenv("MIHVD_FUSED_OPT", fused)
         monkeypatch.setenv("MIHVD_FOLD_REDUCE", fold)
-        tr = FusedMNISTTrainer(batch_size=B, seed=9, device="cuda")
+        tr = FusedMNISTTrainer(batch_size=B, seed=9, device="cuda", precision="bf16")
         assert tr.fold_reduce == (fold == "1")
         tr.set_device_dataset(X, Y, shuffle=False)
         tr.build_graph(steps_per_replay=3, warmup=1)
@@ -592,7 +592,7 @@ def test_w3_tile_tail_matches_stored_dw3_tail(ops, monkeypatch, B):
     out = []
     for tail in ("0", "1"):
         monkeypatch.setenv("MIHVD_W3_TAIL", tail)
-        tr = FusedMNISTTrainer(batch_size=B, seed=6, device="cuda")
+        tr = FusedMNISTTrainer(batch_size=B, seed=6, device="cuda", precision="bf16")
         assert tr.fused_opt and tr.w3_tail == (tail == "1")
         tr.keep_w3_grad = True
         tr.set_device_dataset(X, Y, shuffle=False)
@@ -690,7 +690,7 @@ def test_conv2_bwd_adam_tail_covers_slice(ops, B):
     length that is not a multiple of the 1024-element wave group."""
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
-    tr = FusedMNISTTrainer(batch_size=B, seed=2, device="cuda", dropout=0.0)
+    tr = FusedMNISTTrainer(batch_size=B, seed=2, device="cuda", precision="bf16", dropout=0.0)
     x = torch.rand(B, 784, device="cuda")
     y = torch.randint(0, 10, (B,), device="cuda")
     tr.train_step(x, y)
@@ -723,7 +723,7 @@ def test_debug_sync_mode_matches_graph(ops, monkeypatch):
     out = []
     for dbg in ("0", "1"):
         monkeypatch.setenv("MIHVD_DEBUG_SYNC", dbg)
-        tr = FusedMNISTTrainer(batch_size=100, seed=6, device="cuda")
+        tr = FusedMNISTTrainer(batch_size=100, seed=6, device="cuda", precision="bf16")
         tr.set_device_dataset(X, Y, shuffle=False)
         assert tr.build_graph(steps_per_replay=3, warmup=1) == (dbg == "0")
         tr.run_graph()

@@ -686,6 +686,39 @@ def test_native_engine_plan_fusion_and_stalls():
     assert groups == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9]]
 
 
+def test_native_engine_slot_agreement_is_order_independent():
+    """Slot numbering of the native engine (engine_new_slot_order, the function the engine thread
+    runs on the all-gathered announce blocks): two ranks that first enqueue the same tensors in
+    OPPOSITE orders, and in different cycles, derive the same slot table — so the summed control
+    vector lines the same signature up on every rank (round 3's engine numbered slots in each rank's
+    local first-enqueue order, which broke exactly this case)."""
+    if not _native.load_kernels():
+        pytest.skip("kernel library not built")
+    from mihvd.parallel.native_engine import assign, signature_hash
+
+    K = 64
+    a, b, c, d = (signature_hash(n, 6, 100, 0) for n in ("A", "B", "C", "D"))
+
+    def block(hashes):
+        return list(hashes) + [0] * (K - len(hashes))
+
+    # cycle 1: rank 0 announces A, B; rank 1 announces B, A (opposite order) and D
+    g1 = block([a, b]) + block([b, a, d])
+    slots0 = assign(g1, 2)   # what rank 0 appends
+    slots1 = assign(g1, 2)   # what rank 1 appends (same gathered data)
+    assert slots0 == slots1 == sorted({a, b, d})
+    table = list(slots0)
+    # cycle 2: rank 1 announces C; rank 0 (first use of D now, already assigned) announces nothing
+    g2 = block([]) + block([c])
+    new = assign(g2, 2, assigned=table)
+    assert new == [c]
+    table += new
+    # every rank's slot of a signature is its index in the common table
+    assert {h: i for i, h in enumerate(table)} == {a: table.index(a), b: table.index(b), c: 3, d: table.index(d)}
+    # already-assigned hashes announced again (a rank that enqueued them late) add nothing
+    assert assign(block([a, d]) + block([]), 2, assigned=table) == []
+
+
 def test_native_engine_wrapper_routing():
     """mihvd.parallel.native_engine.NativeEngine's Python side (no GPU): allreduces on the world go
     to the engine op, sub-groups / unsupported ops / non-contiguous tensors are declined (the caller

@@ -29,7 +29,8 @@ def sc_rccl_graph(outdir):
     # 50 steps per epoch: no reshuffle inside the (up to 44) steps, so eager and graph-replayed
     # schedules of different lengths see the same batches
     X, Y = data(5000)
-    a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda",
+    prec = os.environ.get("MIHVD_TEST_PRECISION", "bf16")
+    a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda", precision=prec,
                           shard_optimizer=os.environ.get("MIHVD_SHARD_W3") == "1")
     assert a.collectives, "MIHVD_FORCE_COLLECTIVES should enable the allreduce path"
     a.set_device_dataset(X, Y, seed=4)
@@ -43,7 +44,7 @@ def sc_rccl_graph(outdir):
     for _ in range(4):
         a.run_graph()
     os.environ["MIHVD_FORCE_COLLECTIVES"] = "0"
-    b = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda")
+    b = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda", precision=prec)
     b.set_device_dataset(X, Y, seed=4)
     for _ in range(pre):
         b.device_step()
@@ -60,6 +61,8 @@ def sc_rccl_graph(outdir):
         json.dump({"captured": captured, "bitwise": bitwise, "rel_update_diff": rel, "steps": a.global_step,
                    "pre_steps": pre, "select": select,
                    "shard": a.shard_w3, "plane": a.data_plane(), "loss": a.last_loss(),
+                   "native_comm": a.ncomm is not None, "precision": a.precision,
+                   "engine_running": hvd.engine_running() if hasattr(hvd, "engine_running") else None,
                    "loss_ref": b.last_loss()}, f)
     a.close()
 
@@ -67,11 +70,11 @@ def sc_rccl_graph(outdir):
 def sc_dp_gloo(outdir):
     r = hvd.rank()
     X, Y = data(600)
-    tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda")
+    tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="bf16")
     assert tr.gather == (os.environ.get("MIHVD_FC_GATHER", "1") != "0")
     tr.keep_w3_grad = True  # gradients are compared below
     tr.broadcast(0)
-    ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", world_size=1)
+    ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="bf16", world_size=1)
     ref.keep_w3_grad = True
     p0 = ref.params.clone()
     grel = None
@@ -99,7 +102,7 @@ def sc_dp_gloo_shard(outdir):
     """Sharded dense/kernel optimizer == unsharded factor-gather step, bit for bit (2 ranks)."""
     r = hvd.rank()
     X, Y = data(600)
-    trs = [FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", shard_optimizer=sh)
+    trs = [FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="bf16", shard_optimizer=sh)
            for sh in (False, True)]
     for tr in trs:
         tr.broadcast(0)
@@ -127,8 +130,8 @@ def sc_dp_gloo_switch(outdir):
     bit (2 ranks: the two-term sums commute exactly)."""
     r = hvd.rank()
     X, Y = data(1200)
-    a = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", shard_optimizer=True)
-    ref = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", shard_optimizer=False)
+    a = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="bf16", shard_optimizer=True)
+    ref = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="bf16", shard_optimizer=False)
     for tr in (a, ref):
         tr.broadcast(0)
     ref._set_plane(False, False)
@@ -293,7 +296,7 @@ def sc_select_check(outdir):
     """2 ranks: plane selection's end-to-end consistency check (xGMI vs RCCL steps from one snapshot)."""
     r = hvd.rank()
     X, Y = data(2000, seed=5)
-    tr = FusedMNISTTrainer(batch_size=50, lr=2e-3, seed=1, device="cuda", shard_optimizer=True)
+    tr = FusedMNISTTrainer(batch_size=50, lr=2e-3, seed=1, device="cuda", precision="bf16", shard_optimizer=True)
     tr.broadcast(0)
     tr.set_device_dataset(X, Y, seed=3 + r)
     rep = tr.select_data_plane(steps=6, steps_per_replay=3, shard_options=[True])
