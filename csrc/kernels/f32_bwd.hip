@@ -25,15 +25,22 @@ namespace mihvd {
 // Phase stamps (study instrument, off unless f32_stamps_enable set the buffer): thread 0 of each
 // block of f32_conv2_bwd records the shader clock (s_memtime) at its phase boundaries into
 // stamps[block][16] with vector stores (slots 8..15: each wave's end of the dgrad tap loop).
+// Compiled in only by a study build (MIHVD_F32_STAMPS=1 at build time, mihvd/_build.py): each stamp
+// loads the buffer pointer from a __device__ variable and waits for it (s_waitcnt vmcnt(0)), which
+// costs a dependent L2 round trip at every phase boundary of the production kernel.
 __device__ unsigned long long* g_c2b_stamps = nullptr;
 __device__ __forceinline__ void c2b_stamp(int k) {
+#ifdef MIHVD_F32_STAMPS
   unsigned long long* p = g_c2b_stamps;
   if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memtime();
+#endif
 }
 // per-wave stamp (lane 0 of every wave): slot 8 + wave
 __device__ __forceinline__ void c2b_stamp_wave() {
+#ifdef MIHVD_F32_STAMPS
   unsigned long long* p = g_c2b_stamps;
   if (p != nullptr && (threadIdx.x & 63) == 0) p[blockIdx.x * 16 + 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -390,6 +397,246 @@ __global__ void __launch_bounds__(256) f32_fc1_bwd_kernel(
     return;
   }
   f32_fc1_wgrad_block<GT>(bid - F1B_SMALL, dz, a2, gW3, B, smf);
+}
+
+// ------------------------------------------------------------------------------------------ //
+// f32_fc1_bwd, row form (default): one block per 16 rows of W3 (= 16 channels of one pooling
+// window), 8 waves; wave w owns the 128 columns n in [128 w, 128 w + 128) of those rows, in 8
+// chunks of 16. Per chunk the wave holds p = W3[f0 + lr][n .. n + 3] (4 consecutive columns per
+// lane: lane group lg -> n = nn + 4 lg) and uses it twice:
+//   dgrad  g2[b][f] += sum_n W3[f][n] dz[b][n]  (K-split over the waves; p is the K-contiguous A
+//          operand, dz[b][n..n+3] from LDS the B operand; G sample tiles = G accumulators)
+//   wgrad  dW3[f][n] = sum_b a2[b][f] dz[b][n]  (16x16x4, C[row = n][col = f]: the lane's four
+//          accumulator rows are exactly the four columns of p it holds; A = dz^T from LDS, B = the
+//          block's a2 column held in registers for the whole kernel)
+// and then, with ADAM (world size 1: dW3 is final here), applies Adam to those four elements from
+// the accumulators: W3 is read ONCE per step for dgrad, gradient and update, and dW3 never goes
+// through HBM (STORE keeps it in the gradient buffer: N > 1, where it is reduced first, and tests).
+// dz chunks ([B][16] per wave, rows >= B zero) are staged through a per-wave double buffer in LDS
+// (row stride 16 floats: the b32 reads of the wgrad operand are conflict-free) by register loads
+// issued one chunk ahead; p/m/v are loaded two chunks ahead. The eight dgrad partials meet in LDS
+// in a fixed order (deterministic) and the routing epilogue writes dY2 and the db2 partial rows.
+// ------------------------------------------------------------------------------------------ //
+constexpr int F1R_BLOCKS = 196;                       // 3136 / 16 rows
+constexpr int F1R_LDS_BUF = F32_MAXB * 16;            // floats per wave buffer
+constexpr int F1R_LDS = 8 * 2 * F1R_LDS_BUF * 4;      // 131,072 B
+static_assert(8 * 8 * 64 * 16 <= F1R_LDS, "fc1 row form: dgrad partial exchange fits the dz buffers");
+
+__device__ __forceinline__ void lds_wave_fence() {
+  // the wave's own LDS writes before its later reads (LDS executes one wave's ops in order); a
+  // compiler barrier keeps the program order
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Small reductions over the batch for 512-thread blocks: db3 (16 blocks), dW4 (16 blocks), db4.
+__device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restrict__ dz, const float* __restrict__ h,
+                                                 const float* __restrict__ dlog, float* __restrict__ gb3,
+                                                 float* __restrict__ gW4, float* __restrict__ gb4, int B, float* smf) {
+  const int t = threadIdx.x, nn = t & 63, rg = t >> 6;  // 8 row groups of 16 samples
+  if (bid < 16) {
+    const int n = bid * 64 + nn;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int b = rg * 16 + i;
+      s += mask_f(dz[(int64_t)min(b, B - 1) * 1024 + n], b < B);
+    }
+    smf[rg * 64 + nn] = s;
+    __syncthreads();
+    if (t < 64)
+      gb3[n] = ((smf[nn] + smf[64 + nn]) + (smf[128 + nn] + smf[192 + nn])) +
+               ((smf[256 + nn] + smf[320 + nn]) + (smf[384 + nn] + smf[448 + nn]));
+    return;
+  }
+  if (bid < 32) {
+    const int r = bid - 16, n = r * 64 + nn;
+    float* dls = smf;                  // [128][10]
+    float* red = smf + F32_MAXB * 10;  // [8][64][10]
+    float hv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int b = rg * 16 + i;
+      hv[i] = mask_f(h[(int64_t)min(b, B - 1) * 1024 + n], b < B);
+    }
+    for (int i = t; i < F32_MAXB * 10; i += 512) dls[i] = i < B * 10 ? dlog[i] : 0.f;
+    __syncthreads();
+    float s[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) s[c] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int c = 0; c < 10; ++c) s[c] = fmaf(hv[i], dls[(rg * 16 + i) * 10 + c], s[c]);
+#pragma unroll
+    for (int c = 0; c < 10; ++c) red[(rg * 64 + nn) * 10 + c] = s[c];
+    __syncthreads();
+    for (int i = t; i < 640; i += 512) {
+      const int n2 = i / 10, c = i - n2 * 10;
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) v += red[(q * 64 + n2) * 10 + c] + red[((q + 1) * 64 + n2) * 10 + c];
+      gW4[(r * 64 + n2) * 10 + c] = v;
+    }
+    return;
+  }
+  // db4: thread = (class c, row group of 3)
+  const int c = t % 10, gq = t / 10;
+  float s = 0.f;
+  if (gq < 43) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int b = gq * 3 + i;
+      s += mask_f(dlog[min(b, B - 1) * 10 + c], b < B);
+    }
+  }
+  smf[t] = s;
+  __syncthreads();
+  if (t < 10) {
+    float tot = 0.f;
+    for (int q = 0; q < 43; ++q) tot += smf[q * 10 + t];
+    gb4[t] = tot;
+  }
+}
+
+template <int G, bool ADAM, bool STORE>
+__global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
+    const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
+    const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
+    float* __restrict__ db2p, float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4,
+    float* __restrict__ gb4, int B, F32Adam ad) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const int bid = blockIdx.x;
+  if (bid >= F1R_BLOCKS) {
+    f32_fc1_small512(bid - F1R_BLOCKS, dz, h, dlog, gb3, gW4, gb4, B, smf);
+    return;
+  }
+  constexpr int KS = 4 * G;  // K steps of the wgrad chain (samples padded to 16 G)
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int f0 = 16 * bid, nb = 128 * wave;
+  float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
+  // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch)
+  float a2r[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int b = 4 * s + lg;
+    a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
+  }
+  // dz staging: chunk c = dz[0 .. 16 G)[nb + 16 c .. + 16): lane -> row (lane >> 2) + 16 it, float4 (lane & 3)
+  float4 zst[G];
+  auto load_z = [&](int c) {
+    const int n = nb + 16 * c + 4 * (lane & 3);
+#pragma unroll
+    for (int it = 0; it < G; ++it) {
+      const int b = (lane >> 2) + 16 * it;
+      zst[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)min(b, B - 1) * 1024 + n), b < B);
+    }
+  };
+  auto store_z = [&](float* buf) {
+#pragma unroll
+    for (int it = 0; it < G; ++it)
+      *reinterpret_cast<float4*>(buf + ((lane >> 2) + 16 * it) * 16 + 4 * (lane & 3)) = zst[it];
+  };
+  // p (and m, v) of chunk c: W3[f0 + lr][nb + 16 c + 4 lg .. + 3]
+  const int64_t rowo = (int64_t)(f0 + lr) * 1024 + nb + 4 * lg;
+  float4 pv[3], mv[3], vv[3];
+  auto load_pmv = [&](int c, int slot) {
+    const int64_t o = rowo + 16 * c;
+    pv[slot] = *reinterpret_cast<const float4*>(w3 + o);
+    if constexpr (ADAM) {
+      mv[slot] = *reinterpret_cast<const float4*>(ad.m + o);
+      vv[slot] = *reinterpret_cast<const float4*>(ad.v + o);
+    }
+  };
+  AdamCoef coef{};
+  if constexpr (ADAM) coef = f32_adam_coef(ad);
+  f32x4 acc[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load_z(0);
+  load_pmv(0, 0);
+  load_pmv(1, 1);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float* buf = buf0 + (c & 1) * F1R_LDS_BUF;
+    store_z(buf);
+    if (c + 1 < 8) load_z(c + 1);
+    if (c + 2 < 8) load_pmv(c + 2, (c + 2) % 3);
+    lds_wave_fence();
+    const int s3 = c % 3;
+    const float4 p = pv[s3];
+    // dgrad: G tiles of 16 samples, the four k elements of the chunk outer (independent accumulators)
+    float4 zb[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) zb[u] = *reinterpret_cast<const float4*>(buf + (16 * u + lr) * 16 + 4 * lg);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(p.x, zb[u].x, acc[u]);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(p.y, zb[u].y, acc[u]);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(p.z, zb[u].z, acc[u]);
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc[u] = mfma4(p.w, zb[u].w, acc[u]);
+    // wgrad: dW3[f0 + lr][nn + 4 lg + i] over the batch, two alternating accumulators
+    f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
+#pragma unroll
+    for (int s = 0; s < KS; s += 2) {
+      const float z0 = buf[(4 * s + lg) * 16 + lr];
+      const float z1 = buf[(4 * s + 4 + lg) * 16 + lr];
+      w0 = mfma4(z0, a2r[s], w0);
+      w1 = mfma4(z1, a2r[s + 1], w1);
+    }
+    const f32x4 g = w0 + w1;
+    const int64_t o = rowo + 16 * c;
+    float4 gg = make_float4(g[0], g[1], g[2], g[3]);
+    if constexpr (STORE) *reinterpret_cast<float4*>(gW3 + o) = gg;
+    if constexpr (ADAM) {
+      float4 pp = p, mm = mv[s3], vq = vv[s3];
+      adam4_f32(pp, mm, vq, gg, coef);
+      *reinterpret_cast<float4*>(w3 + o) = pp;
+      *reinterpret_cast<float4*>(ad.m + o) = mm;
+      *reinterpret_cast<float4*>(ad.v + o) = vq;
+    }
+  }
+  // the eight K-part partials meet in LDS (the dz buffers are dead after the barrier)
+  __syncthreads();
+  float4* red = reinterpret_cast<float4*>(smf);  // [8 waves][8 tiles][64 lanes]
+#pragma unroll
+  for (int u = 0; u < G; ++u) red[(wave * 8 + u) * 64 + lane] = make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+  __syncthreads();
+  const int jt = bid >> 2, py = jt / 7, px = jt - 7 * py;
+  if (t < G * 64) {  // wave u handles tile u
+    const int u = t >> 6, ln = lane, r = ln & 15, q = ln >> 4;
+    float4 s = red[(0 * 8 + u) * 64 + ln];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) s = f4add(s, red[(w * 8 + u) * 64 + ln]);
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+    const int m = 16 * u + r, mc = min(m, B - 1), co = 16 * (bid & 3) + 4 * q, j = 64 * jt + co;
+    const bool valid = m < B;
+    const float4 av = *reinterpret_cast<const float4*>(a2 + (int64_t)mc * 3136 + j);
+    const uint32_t ix = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc * 3136 + j);
+    const float ae[4] = {av.x, av.y, av.z, av.w};
+    float gq[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gq[e] = (valid && ae[e] > 0.f) ? sv[e] : 0.f;
+    float sm[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sm[e] = row_sum16(gq[e]);  // over the 16 samples of tile u
+    if (r == 0)
+      *reinterpret_cast<float4*>(db2p + ((int64_t)u * 49 + jt) * 64 + co) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+    if (valid) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        float o4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[e] = (int)((ix >> (8 * e)) & 0xff) == d ? gq[e] : 0.f;
+        const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
+        *reinterpret_cast<float4*>(dY2 + (((int64_t)m * 14 + y) * 14 + x) * 64 + co) =
+            make_float4(o4[0], o4[1], o4[2], o4[3]);
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -780,10 +1027,6 @@ __device__ __forceinline__ void c1n_arrive(const F32Conv1Next& c1) {
   }
 }
 
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-
 // sum of rows r0, r0 + step, ... (< n) of a float4 column, 8 loads in flight per round
 __device__ __forceinline__ float4 strided_sum8(const float4* __restrict__ p, int64_t stride4, int r0, int step, int n) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -954,9 +1197,39 @@ int64_t f32_dgrad_blocks(int64_t B) {
   return (nt + tpb - 1) / tpb;
 }
 
+// F32Adam of the fc1 row kernel (f32_fwd.hip builds the others)
+static F32Adam f32_fc1_adam(at::Tensor& w3, const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
+                            const c10::optional<at::Tensor>& state, double lr, double b1, double b2, double eps,
+                            double gscale, int64_t rule) {
+  F32Adam a;
+  if (!(m3.has_value() && m3->defined())) return a;
+  TORCH_CHECK(v3.has_value() && v3->defined() && state.has_value() && state->defined(),
+              "f32_fc1_bwd: the fused dense/kernel Adam needs m3, v3 and the step state");
+  for (const at::Tensor* t : {&*m3, &*v3})
+    TORCH_CHECK(t->is_cuda() && t->dtype() == at::kFloat && t->is_contiguous() && t->numel() == 3136 * 1024 &&
+                    ((uintptr_t)t->data_ptr() & 15) == 0,
+                "f32_fc1_bwd: Adam slots must be 16-byte aligned contiguous fp32 [3136 x 1024]");
+  TORCH_CHECK(((uintptr_t)w3.data_ptr() & 15) == 0, "f32_fc1_bwd: w3 must be 16-byte aligned");
+  a.p = w3.data_ptr<float>();
+  a.m = m3->data_ptr<float>();
+  a.v = v3->data_ptr<float>();
+  a.n4 = 3136 * 1024 / 4;
+  a.state = state->data_ptr<int64_t>();
+  a.lr = (float)lr;
+  a.b1 = (float)b1;
+  a.b2 = (float)b2;
+  a.eps = (float)eps;
+  a.gscale = (float)gscale;
+  a.rule = (int)rule;
+  a.nblk = 1;
+  return a;
+}
+
 void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
-                 const at::Tensor& dlog, const at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
-                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4) {
+                 const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
+                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
+                 const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr, double beta1,
+                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_bwd: batch 1..128");
   chk_f32(dz, (int64_t)B * 1024, "f32_fc1_bwd: dz");
@@ -971,11 +1244,45 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   chk_f32(gb3, 1024, "f32_fc1_bwd: gb3");
   chk_f32(gW4, 10240, "f32_fc1_bwd: gW4");
   chk_f32(gb4, 10, "f32_fc1_bwd: gb4");
+  const F32Adam ad = f32_fc1_adam(w3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule);
+  const bool adam = ad.nblk > 0;
+  TORCH_CHECK(adam || store_w3, "f32_fc1_bwd: without the fused Adam the dense/kernel gradient must be stored");
+  const int G = (B + 15) / 16;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  // Row form (default): dgrad + dW3 (+ the fused dense/kernel Adam) from one read of W3.
+  // MIHVD_F32_F1B=0: the earlier three-role launch (window dgrad, separate dW3 tiles; no fused Adam).
+  if (env_knob("MIHVD_F32_F1B", 1) != 0 || adam) {
+    auto launch = [&](auto kern) {
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1R_LDS);
+      kern<<<F1R_BLOCKS + F1B_SMALL, 512, F1R_LDS, stream>>>(
+          dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
+          dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
+          gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad);
+    };
+#define F1R_CASE(GG)                                                       \
+  case GG:                                                                 \
+    if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>); \
+    else if (adam) launch(f32_fc1_bwd_rows_kernel<GG, true, false>);       \
+    else launch(f32_fc1_bwd_rows_kernel<GG, false, true>);                 \
+    break;
+    switch (G) {
+      F1R_CASE(1)
+      F1R_CASE(2)
+      F1R_CASE(3)
+      F1R_CASE(4)
+      F1R_CASE(5)
+      F1R_CASE(6)
+      F1R_CASE(7)
+      default:
+        F1R_CASE(8)
+    }
+#undef F1R_CASE
+    return;
+  }
   // MIHVD_F32_F1B_KS=1 selects the K-split dgrad form with the unrolled wgrad chain (study: same
   // dgrad time, fc1_bwd 27.0 vs 25.5 us at B = 100, so the window form stays the default)
   const int dg_ks = env_knob("MIHVD_F32_F1B_KS", 0) != 0;
-  const int G = (B + 15) / 16, n_dg = dg_ks ? F1B_DG2 : 56 * G;
-  auto stream = c10::hip::getCurrentHIPStream().stream();
+  const int n_dg = dg_ks ? F1B_DG2 : 56 * G;
   // study knob: MIHVD_F32_F1B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only
   const int role = env_knob("MIHVD_F32_F1B_ROLE", 0);
   const int grid = role == 1 ? n_dg : role == 2 ? F1B_WGRAD : n_dg + F1B_SMALL + F1B_WGRAD;

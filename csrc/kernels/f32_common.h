@@ -34,6 +34,10 @@ __device__ __forceinline__ f32x4 mfma4_q(const float4& a, const float4& b, f32x4
   return mfma4(a.w, b.w, c);
 }
 
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
 __device__ __forceinline__ float4 mask_f4(float4 v, bool keep) {
   const uint32_t m = keep ? 0xffffffffu : 0u;
   return make_float4(__uint_as_float(__float_as_uint(v.x) & m), __uint_as_float(__float_as_uint(v.y) & m),

@@ -26,10 +26,13 @@ namespace mihvd {
 
 // Phase stamps of f32_conv2_fwd blocks (study instrument; f32_stamps_enable(1, n) in f32_bwd.hip
 // sets the buffer): slots 0 start, 1 staging barrier, 2 + pair index: end of each tile pair.
+// (compiled in only by a study build, MIHVD_F32_STAMPS: see c2b_stamp in f32_bwd.hip)
 __device__ unsigned long long* g_c2f_stamps = nullptr;
 __device__ __forceinline__ void c2f_stamp(int k) {
+#ifdef MIHVD_F32_STAMPS
   unsigned long long* p = g_c2f_stamps;
   if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memtime();
+#endif
 }
 void f32_fwd_stamps_set(unsigned long long* p) {
   TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_c2f_stamps), &p, sizeof(p)) == hipSuccess, "c2f stamps");
@@ -671,9 +674,11 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   const F32Adam ad =
       f32_adam_args(p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule, nt_tail, "f32_conv2_fwd");
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  // MIHVD_F32_C2F_LDS (study knob): request more dynamic LDS than the image needs, which caps
-  // how many blocks share a CU
-  const int lds = std::max(C2F_LDS, std::min(env_knob("MIHVD_F32_C2F_LDS", 0), 163840));
+  // When the grid fits the CUs, request more LDS than the image needs (> half a CU's) so no two
+  // blocks share a CU: the dispatcher otherwise doubles blocks up on some CUs while others idle
+  // (measured 20.6 -> 19.7 us at B = 100). MIHVD_F32_C2F_LDS overrides (study knob).
+  const int spread = (nblk + (ad.nblk > 0 ? ad.nblk : 0)) <= device_cu_count() ? 81920 + 1024 : 0;
+  const int lds = std::max(C2F_LDS, std::min(env_knob("MIHVD_F32_C2F_LDS", spread), 163840));
   auto launch = [&](auto kern, int extra) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nblk + extra, 256, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),

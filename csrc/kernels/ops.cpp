@@ -99,8 +99,10 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
                       at::Tensor& dlog, at::Tensor& stats);
 void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
-                 const at::Tensor& dlog, const at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
-                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4);
+                 const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
+                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
+                 const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr, double beta1,
+                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3);
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    at::Tensor& cpart, at::Tensor& slab);
@@ -251,8 +253,11 @@ void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const 
   mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats);
 }
 void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, const Tensor& h, const Tensor& dlog,
-                    const Tensor& w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4) {
-  mihvd::f32_fc1_bwd(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4);
+                    Tensor w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, const OptT& m3,
+                    const OptT& v3, const OptT& state, double lr, double beta1, double beta2, double eps,
+                    double grad_scale, int64_t rule, bool store_w3) {
+  mihvd::f32_fc1_bwd(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4, m3, v3, state, lr, beta1, beta2, eps,
+                     grad_scale, rule, store_w3);
 }
 void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, const Tensor& idx1, const Tensor& x,
                       const OptT& rows, const OptT& state, Tensor cpart, Tensor slab) {
@@ -325,8 +330,10 @@ TORCH_LIBRARY(mihvd, m) {
         "float grad_scale=1., int rule=0) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
-  m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor w3, Tensor(a!) dY2, "
-        "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4) -> ()");
+  m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor(w!) w3, Tensor(a!) dY2, "
+        "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4, Tensor(m!)? m3=None, "
+        "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
+        "float grad_scale=1., int rule=0, bool store_w3=True) -> ()");
   m.def("f32_conv2_bwd(Tensor dY2, Tensor w2, Tensor a1, Tensor idx1, Tensor x, Tensor? rows, Tensor? state, "
         "Tensor(a!) cpart, Tensor(b!) slab) -> ()");
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "

@@ -109,6 +109,8 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int | None =
     ]
     if os.environ.get("MIHVD_SAVE_TEMPS"):
         common += ["-save-temps=obj"]
+    if os.environ.get("MIHVD_F32_STAMPS") == "1":  # study build: in-kernel phase stamps (scripts/stamps_f32.py)
+        common += ["-DMIHVD_F32_STAMPS=1"]
 
     def compile_one(src):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")

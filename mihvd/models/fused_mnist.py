@@ -302,12 +302,13 @@ class FusedMNISTTrainer:
         # (default: one per CU)
         self.f32_fused_opt = self.f32 and os.environ.get("MIHVD_FUSED_OPT", "1") != "0"
         self.f32_tail_blocks = int(os.environ.get("MIHVD_F32_TAIL_BLOCKS", "0"))
-        # where dense/kernel's fused Adam update runs: "fc1" = deferred into the next step's fc1_fwd,
-        # which reads W3 anyway (each lane updates the fragment it multiplies with: one read of p
-        # instead of two); "tail" = deferred into tail blocks of the next conv2_fwd; "side" = on the
+        # where dense/kernel's fused Adam update runs: "bwd" (default) = inside f32_fc1_bwd, whose row
+        # blocks read W3 once for the dgrad, form dW3 of the same elements in registers and update
+        # them (dW3 never goes through HBM); "fc1" = deferred into the next step's fc1_fwd, which
+        # reads W3 anyway; "tail" = deferred into tail blocks of the next conv2_fwd; "side" = on the
         # side stream beside the conv backward of the same step (world size 1 only; the cross-queue
         # join of a captured graph costs more than it hides here)
-        self.f32_w3 = os.environ.get("MIHVD_F32_W3", "fc1")
+        self.f32_w3 = os.environ.get("MIHVD_F32_W3", "bwd")
         if self.f32_w3 == "fc1" and B > 112:  # the fused update keeps the a2 slice + a W3 tile in LDS
             self.f32_w3 = "tail"
         self._w3_pending = False
@@ -653,8 +654,16 @@ class FusedMNISTTrainer:
             o.f32_fc1_fwd(self.a2, w3, self.zpart)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
-        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
-                      G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+        w3_bwd = self.f32_fused_opt and not self.collectives and self.f32_w3 == "bwd"
+        if w3_bwd:
+            # dgrad, dW3 and dense/kernel's Adam from one read of W3 (dW3 stays in registers unless
+            # keep_w3_grad)
+            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3], self.v[s3], st, self.lr,
+                          b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad)
+        else:
+            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
         overlap = self.collectives and self.overlap
         w3_side = self.f32_fused_opt and not self.collectives and self.f32_w3 == "side"
         if overlap:
@@ -693,9 +702,9 @@ class FusedMNISTTrainer:
                         self.eps, 1.0 / self.world, self.rule, 1)
         if w3_side:
             main.wait_stream(self._side)
-        elif self.f32_fused_opt:
-            # dense/kernel's update is deferred into the next step's conv2_fwd launch (or applied by
-            # _flush_w3 when no step follows: end of an eager step or of a captured graph)
+        elif self.f32_fused_opt and not w3_bwd:
+            # dense/kernel's update is deferred into the next step's fc1_fwd / conv2_fwd launch (or
+            # applied by _flush_w3 when no step follows: end of an eager step or of a captured graph)
             self._w3_pending = True
 
     def _launch_step_f32_shard(self, x, rows, labels):

@@ -84,6 +84,10 @@ def main():
                                            tr.rows, st, tr.seed, tr.dropout, tr.h, tr.dz, tr.dlog, tr.stats),
         "fc1_bwd": lambda: o.f32_fc1_bwd(tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"),
                                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias")),
+        "fc1_bwd+W3 adam": lambda: o.f32_fc1_bwd(tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p,
+                                                 G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"),
+                                                 G("dense_1/bias"), tr.m[s3], tr.v[s3], st, 0.0, b1, b2, tr.eps, 1.0,
+                                                 tr.rule, False),
         "conv2_bwd": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab),
         "conv_reduce": lambda: o.f32_conv_reduce(tr.slab, tr.cpart, tr.db2p, *gconv),
         "conv_reduce+adam": lambda: o.f32_conv_reduce(
@@ -116,12 +120,12 @@ def main():
         "conv2_fwd [LDS 96 KB: 1 block/CU]": ({"MIHVD_F32_C2F_LDS": "98304"}, ks["conv2_fwd"]),
         "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd"]),
-        "fc1_bwd [dgrad role only]": ({"MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
-        "fc1_bwd [wgrad role only]": ({"MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
+        "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
+        "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
+        "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
         "fc1_fwd [earlier form]": ({"MIHVD_F32_F1F": "0"}, ks["fc1_fwd"]),
         "fc1_fwd+W3 adam [earlier form]": ({"MIHVD_F32_F1F": "0"}, ks["fc1_fwd+W3 adam"]),
-        "fc1_bwd [K-split dgrad form]": ({"MIHVD_F32_F1B_KS": "1"}, ks["fc1_bwd"]),
-        "fc1_bwd [K-split dgrad form, dgrad only]": ({"MIHVD_F32_F1B_KS": "1", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
+
     }
     for name, (env, fn) in study.items():
         old_env = {k: os.environ.get(k) for k in env}
@@ -139,7 +143,7 @@ def main():
     res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
     tr._join()
     mode = tr.f32_w3
-    for alt in ("fc1", "tail", "side"):
+    for alt in ("bwd", "fc1", "tail", "side"):
         if alt != mode:
             tr.f32_w3 = alt
             res[f"whole step [dense/kernel Adam: {alt}]"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)

@@ -3,6 +3,8 @@
 
 Prints, per role, the median and max cycles of each phase and when blocks start relative to the
 first block (second-round blocks start late), plus the kernel's event-timed duration for scale.
+Needs the study build of the kernels (the stamps are compiled out of production builds):
+``MIHVD_F32_STAMPS=1 python -m mihvd._build kernels --force``.
 """
 import os
 import sys

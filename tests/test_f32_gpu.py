@@ -128,6 +128,76 @@ def test_f32_fc1_bwd(ops, B):
     assert rel_err(gb4, dlog.sum(0)) < 1e-6
 
 
+@pytest.mark.parametrize("B", [7, 100, 128])
+def test_f32_fc1_bwd_fused_adam(ops, B):
+    """The row form's fused dense/kernel Adam: dgrad from the OLD W3, dW3 from the accumulators, and
+    the TF1 Adam update of W3 / m / v equal the stored-gradient launch followed by adam_step (bit for
+    bit: the same dW3 arithmetic and the same adam1); and the earlier 3-role form agrees on dY2 / dW3
+    to fp32 rounding."""
+    import os
+
+    g = torch.Generator(device="cuda").manual_seed(14)
+    a2 = F.relu(torch.randn(B, 3136, device="cuda", generator=g))
+    idx2 = torch.randint(0, 4, (B, 3136), device="cuda", generator=g, dtype=torch.int64).to(torch.uint8)
+    w3 = torch.randn(3136, 1024, device="cuda", generator=g) * 0.02
+    m3 = torch.randn(3136, 1024, device="cuda", generator=g).abs() * 1e-3
+    v3 = torch.randn(3136, 1024, device="cuda", generator=g).abs() * 1e-5
+    dz = torch.randn(B, 1024, device="cuda", generator=g)
+    h = torch.rand(B, 1024, device="cuda", generator=g)
+    dlog = torch.randn(B, 10, device="cuda", generator=g)
+    st = torch.tensor([5, 7, 0, 0], device="cuda", dtype=torch.int64)
+
+    def run(fused, w, m, v, env=None):
+        dY2 = torch.full((B, 14, 14, 64), float("nan"), device="cuda")
+        db2p = torch.empty(int(ops.f32_db2_rows(B)), 64, device="cuda")
+        gW3 = torch.full((3136, 1024), float("nan"), device="cuda")
+        small = [torch.empty(1024, device="cuda"), torch.empty(1024, 10, device="cuda"), torch.empty(10, device="cuda")]
+        old = os.environ.get("MIHVD_F32_F1B")
+        if env is not None:
+            os.environ["MIHVD_F32_F1B"] = env
+        try:
+            if fused:
+                ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small, m, v, st, 1e-3, 0.9, 0.999, 1e-8,
+                                1.0, 0, True)
+            else:
+                ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small)
+        finally:
+            if env is not None:
+                if old is None:
+                    os.environ.pop("MIHVD_F32_F1B", None)
+                else:
+                    os.environ["MIHVD_F32_F1B"] = old
+        return dY2, db2p, gW3, small
+
+    wf, mf, vf = w3.clone(), m3.clone(), v3.clone()
+    dY2f, db2f, gW3f, smallf = run(True, wf, mf, vf)
+    ws = w3.clone()
+    dY2s, db2s, gW3s, smalls = run(False, ws, None, None)
+    assert torch.equal(dY2f, dY2s) and torch.equal(db2f, db2s) and torch.equal(gW3f, gW3s)
+    assert torch.equal(ws, w3)  # no update without the Adam operands
+    ms, vs = m3.clone(), v3.clone()
+    ops.adam_step(ws.view(-1), gW3s.view(-1), ms.view(-1), vs.view(-1), None, st, 0, 1e-3, 0.9, 0.999, 1e-8, 1.0, 0, 0)
+    assert torch.equal(wf, ws) and torch.equal(mf, ms) and torch.equal(vf, vs)
+    # dW3 and the routed dgrad against fp64
+    assert rel_err(gW3f, a2.double().t() @ dz.double()) < 1e-6
+    g2 = (dz.double() @ w3.double().t()) * (a2 > 0)
+    ref = torch.zeros(B, 14, 14, 64, dtype=torch.float64, device="cuda")
+    win = torch.arange(3136, device="cuda")
+    pos = win // 64
+    py, px, co = pos // 7, pos % 7, win % 64
+    d = idx2.long()
+    y = 2 * py.unsqueeze(0) + d // 2
+    x = 2 * px.unsqueeze(0) + d % 2
+    bi = torch.arange(B, device="cuda").unsqueeze(1).expand(B, 3136)
+    ref[bi, y, x, co.unsqueeze(0).expand(B, 3136)] = g2
+    assert rel_err(dY2f, ref) < 1e-6
+    # the earlier 3-role form computes the same quantities (other summation order)
+    dY2o, db2o, gW3o, smallo = run(False, w3.clone(), None, None, env="0")
+    assert rel_err(dY2o, dY2f) < 1e-5 and rel_err(gW3o, gW3f) < 1e-5 and rel_err(db2o, db2f) < 1e-5
+    for a, b in zip(smallo, smallf):
+        assert rel_err(a, b) < 1e-5
+
+
 @pytest.mark.parametrize("B", [7, 100])
 def test_f32_conv2_bwd_and_reduce(ops, B):
     """conv2 dgrad + fused conv1 wgrad, conv2 wgrad slabs, and the reduction, vs autograd of
@@ -183,6 +253,7 @@ def test_f32_step_matches_fp32_model(ops, B):
     from mihvd.models.mnist import TF_PARAM_ORDER, softmax_cross_entropy
 
     tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, dropout=0.0, seed=3, device="cuda", precision="fp32")
+    tr.keep_w3_grad = True  # dW3 is compared below (the fused update keeps it in registers otherwise)
     g = torch.Generator(device="cuda").manual_seed(8)
     x = torch.rand(B, 784, device="cuda", generator=g)
     y = torch.randint(0, 10, (B,), device="cuda", generator=g)
@@ -272,12 +343,13 @@ def test_f32_graph_replay_converges(ops):
     assert tr.last_accuracy() > 0.8
 
 
-@pytest.mark.parametrize("w3_mode", ["fc1", "side", "tail"])
+@pytest.mark.parametrize("w3_mode", ["bwd", "fc1", "side", "tail"])
 def test_f32_fused_optimizer_matches_separate_adam(ops, monkeypatch, w3_mode):
     """MIHVD_FUSED_OPT=1 (small-parameter Adam inside the reduction launch; dense/kernel's update
-    deferred into the next step's fc1_fwd or conv2_fwd tail blocks and flushed at the end of each
-    graph / eager step, or on the side stream beside the conv backward) is bitwise equal to a
-    separate adam_step after every step, graph-replayed and eager."""
+    inside f32_fc1_bwd from the dW3 accumulators ("bwd"), or deferred into the next step's fc1_fwd or
+    conv2_fwd tail blocks and flushed at the end of each graph / eager step, or on the side stream
+    beside the conv backward) is bitwise equal to a separate adam_step after every step,
+    graph-replayed and eager."""
     from mihvd.models.fused_mnist import FusedMNISTTrainer
     from mihvd.utils.data import synthetic_mnist
 
@@ -416,6 +488,7 @@ def test_f32_step_with_dropout_matches_fp32_model(ops, B):
     from mihvd.models.mnist import TF_PARAM_ORDER, MNISTConvNet
 
     tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, dropout=0.5, seed=3, device="cuda", precision="fp32")
+    tr.keep_w3_grad = True
     g = torch.Generator(device="cuda").manual_seed(8)
     x = torch.rand(B, 784, device="cuda", generator=g)
     y = torch.randint(0, 10, (B,), device="cuda", generator=g)
