@@ -664,7 +664,20 @@ static_assert(4 * 5 * 4 * 64 * 16 <= CBF_LDS_WG, "wgrad partial exchange fits th
 // 100 floats per lane) is loaded into registers once, so the tap loop has no global load and no
 // barrier. 8 waves: wave w = ci half (w & 1) x co
 // quarter (w >> 1) of K; the four co-quarter partials are summed through LDS before the epilogue.
-template <int TPB>
+// A block barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)), not for
+// its global loads in flight — __syncthreads() also drains vmcnt, which would make a register
+// prefetch issued before it (the W2 operand) complete before the barrier. The asm memory clobbers
+// keep the compiler from moving LDS accesses across it (s_barrier alone is not a memory fence).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// PREW: the W2 register operand is loaded BEFORE the staging barrier (after the staging loads, so the
+// staging writes wait only for their own loads), and the barrier orders LDS alone: the 25 W2 loads
+// per lane (200 KB per block from L2) land while the dY2 image is staged instead of after it.
+template <int TPB, bool PREW>
 __device__ __forceinline__ void f32_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
@@ -699,6 +712,17 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
       *reinterpret_cast<float4*>(dimg + (rr * 18 + (rem >> 4)) * CBF_PS + (rem & 15) * 4) = iv[it];
     }
   }
+  // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3].
+  // PREW: issued right behind the staging writes (which wait only for the staging loads), so they
+  // are in flight across the barrier
+  const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
+  float4 wb[25];
+  if constexpr (PREW) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   int abase[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) {
@@ -709,15 +733,18 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   f32x4 acc[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();  // the dY2 image is complete; no barrier in the tap loop
+  if constexpr (PREW) {
+    lds_barrier();  // the dY2 image is complete; the W2 loads stay in flight
+  } else {
+    __syncthreads();  // the dY2 image is complete; no barrier in the tap loop
+  }
   c2b_stamp(1);
-  // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3].
-  // Issued after the barrier (whose vmcnt(0) would otherwise wait for all 25 loads): the tap loop
-  // consumes them in issue order, so tap t waits only for its own.
-  const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
-  float4 wb[25];
+  if constexpr (!PREW) {
+    // Issued after the barrier (whose vmcnt(0) would otherwise wait for all 25 loads): the tap loop
+    // consumes them in issue order, so tap t waits only for its own.
 #pragma unroll
-  for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
+    for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
+  }
   // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched
   constexpr int NP = (2 * TPB + 7) / 8;  // (nt, tile) pairs per wave
   float ea[NP][4];
@@ -959,7 +986,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   c2b_stamp(6);
 }
 
-template <int TPB>
+template <int TPB, bool PREW>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
@@ -968,7 +995,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
   const int bid = blockIdx.x;
   c2b_stamp(0);
   if (bid < n_dg) {
-    f32_conv2_dgrad_block<TPB>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
+    f32_conv2_dgrad_block<TPB, PREW>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
     return;
   }
   f32_conv2_wgrad_block(bid - n_dg, dY2, a1, slab, B, smf);
@@ -1349,15 +1376,23 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
                                      cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg);
   };
+  // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form)
+  const bool prew = env_knob("MIHVD_F32_C2B_PREW", 1) != 0;
+#define C2B_CASE(T)                                                             \
+  case T:                                                                       \
+    prew ? launch(f32_conv2_bwd_kernel<T, true>) : launch(f32_conv2_bwd_kernel<T, false>); \
+    break;
   switch (tpb) {
-    case 1: launch(f32_conv2_bwd_kernel<1>); break;
-    case 2: launch(f32_conv2_bwd_kernel<2>); break;
-    case 3: launch(f32_conv2_bwd_kernel<3>); break;
-    case 4: launch(f32_conv2_bwd_kernel<4>); break;
-    case 5: launch(f32_conv2_bwd_kernel<5>); break;
-    case 6: launch(f32_conv2_bwd_kernel<6>); break;
-    default: launch(f32_conv2_bwd_kernel<7>); break;
+    C2B_CASE(1)
+    C2B_CASE(2)
+    C2B_CASE(3)
+    C2B_CASE(4)
+    C2B_CASE(5)
+    C2B_CASE(6)
+    default:
+      C2B_CASE(7)
   }
+#undef C2B_CASE
 }
 
 void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,

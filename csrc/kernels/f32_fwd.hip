@@ -128,10 +128,105 @@ __device__ __forceinline__ void c2f_tiles(const float* img, const int (&ab)[2], 
 // dense/kernel update, deferred into this MFMA-bound launch, which leaves HBM idle). They are first
 // in dispatch order, so they take the CUs before the conv blocks; a tail block and a conv block fit
 // one CU together when registers allow (2 x 76 KB of LDS).
-template <int TPB, bool TAIL>
+// A block barrier that orders LDS only (see lds_barrier in f32_bwd.hip): the W2 register prefetch
+// stays in flight across it.
+__device__ __forceinline__ void c2f_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// conv1 operands of the fused conv1 + conv2 forward (FUSE1): the block computes the a1 rows its
+// conv2 tiles read (their halo included) straight from x, instead of loading them from a1.
+struct C1Fuse {
+  const float* x = nullptr;
+  const int* rows = nullptr;
+  int n_pool = 0;
+  const int64_t* state = nullptr;
+  const float* w1 = nullptr;
+  const float* b1 = nullptr;
+  float* a1 = nullptr;     // written for the backward: the rows of the block's own window rows
+  uint8_t* idx1 = nullptr;
+};
+constexpr int C2F_XIM = 2 * 1024;  // two padded x images [32][32] after the tall image
+
+// FUSE1 staging: conv1 (25 taps on 16x16x4 MFMA, as f32_conv1_block) of the a1 rows in tall rows
+// [R0, R1) of images b0 .. b1i, pooled + bias + ReLU straight into the tall padded LDS image (whose
+// padding was zeroed), and into a1 / idx1 for the rows of this block's own conv2 window rows (rows
+// two blocks share are written by both, with identical values).
+__device__ __forceinline__ void c2f_conv1_stage(const C1Fuse& c1, float* img, float* xim, int B, int R0, int R1,
+                                                int b0, int b1i, int gw0, int gw1) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  float wb1[2][7];
+  int toff[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    const int k = 4 * s + lg, kc = min(k, 24);
+    toff[s] = (kc / 5) * 32 + (kc % 5);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) wb1[nt][s] = mask_f(c1.w1[kc * 32 + 16 * nt + lr], k < 25);
+  }
+  const float bias0 = c1.b1[lr], bias1 = c1.b1[16 + lr];
+  // window segments (a1 pixels) of the two images, in tiles of 4 windows
+  int slo[2], shi[2], ntile[2], own_lo[2], own_hi[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int bb = q == 0 ? b0 : b1i;
+    const int ylo = max(0, R0 - 18 * bb - 2), yhi = min(13, R1 - 1 - 18 * bb - 2);
+    const bool used = q == 0 || b1i != b0;
+    slo[q] = ylo * 14;
+    shi[q] = (used && yhi >= ylo) ? (yhi + 1) * 14 : slo[q];
+    ntile[q] = (shi[q] - slo[q] + 3) / 4;
+    const int wlo = max(gw0, 49 * bb) - 49 * bb, whi = min(gw1, 49 * bb + 48) - 49 * bb;  // conv2 windows
+    own_lo[q] = 2 * (wlo / 7) * 14;
+    own_hi[q] = (2 * (whi / 7) + 2) * 14;
+  }
+  const int nt_all = ntile[0] + ntile[1];
+  for (int tl = wave; tl < nt_all; tl += 4) {  // wave-uniform
+    const int q = tl < ntile[0] ? 0 : 1, tq = q == 0 ? tl : tl - ntile[0];
+    const int bb = q == 0 ? b0 : b1i;
+    const float* xs = xim + (bb - b0) * 1024;
+    const int wa = min(slo[q] + 4 * tq + (lr >> 2), shi[q] - 1), d = lr & 3;
+    const int pya = wa / 14, pxa = wa - pya * 14;
+    const int base = (2 * pya + (d >> 1)) * 32 + 2 * pxa + (d & 1);
+    float av[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) av[s] = xs[base + toff[s]];
+    f32x4 cc0 = {0.f, 0.f, 0.f, 0.f}, cc1 = cc0;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      cc0 = mfma4(av[s], wb1[0][s], cc0);
+      cc1 = mfma4(av[s], wb1[1][s], cc1);
+    }
+    const int win = slo[q] + 4 * tq + lg;
+    if (win < shi[q]) {
+      const int py = win / 14, px = win - py * 14;
+      const int R = 18 * bb + py + 2 - R0;
+      const bool own = win >= own_lo[q] && win < own_hi[q];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x4 c = nt ? cc1 : cc0;
+        int best;
+        const float m = pool4(c, best);
+        const float v = fmaxf(m + (nt ? bias1 : bias0), 0.f);
+        img[(R * C2F_RW + px + 2) * C2F_PS + 16 * nt + lr] = v;
+        if (own) {
+          const int64_t o = (((int64_t)bb * 14 + py) * 14 + px) * 32 + 16 * nt + lr;
+          c1.a1[o] = v;
+          c1.idx1[o] = (uint8_t)best;
+        }
+      }
+    }
+  }
+}
+
+// PREW: the W2 register operand is issued right behind the staging writes and the barrier orders
+// LDS alone, so the 200 KB per block of W2 loads overlap the barrier wait and the first taps.
+// FUSE1: the a1 rows are computed from x in the block (conv1 fused, C1Fuse) instead of loaded.
+template <int TPB, bool TAIL, bool PREW = false, bool FUSE1 = false>
 __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, float* __restrict__ a2,
-                                                            uint8_t* __restrict__ idx2, int B, F32Adam ad) {
+                                                            uint8_t* __restrict__ idx2, int B, F32Adam ad, C1Fuse c1) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   if constexpr (TAIL) {
     if ((int)blockIdx.x < ad.nblk) {
@@ -148,40 +243,72 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
   const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
   const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
-  // 1. the image rows
-  float4 iv[C2F_MAXCH];
+  if constexpr (FUSE1) {
+    // 1. x of the (at most two) images into LDS, the tall image zeroed (its padding stays zero)
+    float* xim = smf + C2F_MAXR * C2F_RS;
+    int64_t step = c1.state ? c1.state[ST_FWD] : 0;
 #pragma unroll
-  for (int it = 0; it < C2F_MAXCH; ++it) {
-    const int i = min(t + 256 * it, nch - 1);
-    const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, ch = rem & 7;
-    const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
-    const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
-    const float4 v = *reinterpret_cast<const float4*>(
-        a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
-    iv[it] = mask_f4(v, in);
-  }
+    for (int it = 0; it < 8; ++it) {
+      const int i = t + 256 * it, sl = i >> 10, pix = i & 1023, Y = (pix >> 5) - 2, X = (pix & 31) - 2;
+      const int bb = min(b0 + sl, B - 1);
+      int row = bb;
+      if (c1.rows != nullptr) row = c1.rows[(int)((step * (int64_t)B + bb) % c1.n_pool)];
+      const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
+      xim[i] = mask_f(c1.x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
+    }
+    const int nz = (R1 - R0) * C2F_RS / 4;
+    for (int i = t; i < nz; i += 256) reinterpret_cast<float4*>(img)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    c2f_conv1_stage(c1, img, xim, B, R0, R1, b0, b1i, gw0, gw1);
+  } else {
+    // 1. the image rows
+    float4 iv[C2F_MAXCH];
 #pragma unroll
-  for (int it = 0; it < C2F_MAXCH; ++it) {
-    const int i = t + 256 * it;
-    if (i < nch) {
-      const int rr = i / 144, rem = i - rr * 144;
-      *reinterpret_cast<float4*>(img + (rr * C2F_RW + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
+    for (int it = 0; it < C2F_MAXCH; ++it) {
+      const int i = min(t + 256 * it, nch - 1);
+      const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, ch = rem & 7;
+      const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
+      const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+      const float4 v = *reinterpret_cast<const float4*>(
+          a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
+      iv[it] = mask_f4(v, in);
+    }
+#pragma unroll
+    for (int it = 0; it < C2F_MAXCH; ++it) {
+      const int i = t + 256 * it;
+      if (i < nch) {
+        const int rr = i / 144, rem = i - rr * 144;
+        *reinterpret_cast<float4*>(img + (rr * C2F_RW + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
+      }
     }
   }
-  __syncthreads();  // the image is complete; no barrier below
-  c2f_stamp(1);
-  // the weights, issued after the barrier (whose vmcnt(0) would otherwise wait for all 200 loads):
-  // the MFMA steps consume them in issue order, each waiting only for its own
   float wb[200];  // wb[8 tap + 4 c2 + j] = W2[tap][16 c2 + 4 lg + j][16 w + lr]
   const float* wp = w2 + (4 * lg) * 64 + 16 * wave + lr;
+  auto load_w = [&]() {
 #pragma unroll
-  for (int tap = 0; tap < 25; ++tap)
+    for (int tap = 0; tap < 25; ++tap)
 #pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2)
+      for (int c2 = 0; c2 < 2; ++c2)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wb[8 * tap + 4 * c2 + j] = wp[tap * 2048 + (16 * c2 + j) * 64];
+        for (int j = 0; j < 4; ++j) wb[8 * tap + 4 * c2 + j] = wp[tap * 2048 + (16 * c2 + j) * 64];
+  };
+  if constexpr (PREW) {
+    __builtin_amdgcn_sched_barrier(0);
+    load_w();
+    __builtin_amdgcn_sched_barrier(0);
+    c2f_lds_barrier();  // the image is complete; the W2 loads stay in flight
+  } else {
+    __syncthreads();  // the image is complete; no barrier below
+    // the weights, issued after the barrier (whose vmcnt(0) would otherwise wait for all 200
+    // loads): the MFMA steps consume them in issue order, each waiting only for its own
+    load_w();
+  }
+  c2f_stamp(1);
   const int co = 16 * wave + lr;
   const float bias = b2[co];
+  // unrolled: the first tile pair's MFMAs then wait for each W2 tap as it lands (a runtime loop
+  // waits for every outstanding load at its entry)
+#pragma unroll
   for (int i = 0; i < TPB; i += 2) {  // block-uniform
     const int tile0 = T0 + i, tile1 = T0 + min(i + 1, TPB - 1);
     const int ab[2] = {c2f_abase(tile0, lr, lg, nwin, R0), c2f_abase(tile1, lr, lg, nwin, R0)};
@@ -399,7 +526,9 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
         *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
       }
     }
-    __syncthreads();
+    // LDS-only barrier: the W3 fragments (issued before the a2 writes, read from HBM) stay in
+    // flight; the MFMA chain consumes them in issue order
+    c2f_lds_barrier();
     if (sh == 0)
       f1f_mma<NT0, 0, 14>(wa, bp, acc);
     else
@@ -651,11 +780,54 @@ static F32Adam f32_adam_args(const c10::optional<at::Tensor>& p, const c10::opti
   return a;
 }
 
+static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2,
+                               at::Tensor& idx2, const c10::optional<at::Tensor>& p3,
+                               const c10::optional<at::Tensor>& g3, const c10::optional<at::Tensor>& m3,
+                               const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr,
+                               double beta1, double beta2, double eps, double grad_scale, int64_t rule,
+                               int64_t tail_blocks, const C1Fuse& c1);
+
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
                    const c10::optional<at::Tensor>& p3, const c10::optional<at::Tensor>& g3,
                    const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
                    const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
                    double grad_scale, int64_t rule, int64_t tail_blocks) {
+  f32_conv2_fwd_impl(a1, w2, b2, a2, idx2, p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule, tail_blocks,
+                     C1Fuse{});
+}
+
+// conv1 + conv2 forward in one launch: every conv2 block computes the a1 rows it reads from x (see
+// c2f_conv1_stage); a1 / idx1 are written for the backward.
+void f32_conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1, const at::Tensor& w2,
+                    const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2) {
+  const int B = a1.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv12_fwd: batch 1..128");
+  TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv12_fwd: x");
+  check_f32(a1, (int64_t)B * 6272, "f32_conv12_fwd: a1");
+  check_u8(idx1, (int64_t)B * 6272, "f32_conv12_fwd: idx1");
+  check_f32(w1, 800, "f32_conv12_fwd: w1");
+  check_f32(b1, 32, "f32_conv12_fwd: b1");
+  C1Fuse c1;
+  c1.n_pool = x.size(0);
+  c1.rows = rows_ptr(rows, c1.n_pool, B, "f32_conv12_fwd");
+  c1.x = x.data_ptr<float>();
+  c1.state = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  c1.w1 = w1.data_ptr<float>();
+  c1.b1 = b1.data_ptr<float>();
+  c1.a1 = a1.data_ptr<float>();
+  c1.idx1 = idx1.data_ptr<uint8_t>();
+  f32_conv2_fwd_impl(a1, w2, b2, a2, idx2, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, 0.0,
+                     0.0, 0.0, 0.0, 1.0, 0, 0, c1);
+}
+
+static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2,
+                               at::Tensor& idx2, const c10::optional<at::Tensor>& p3,
+                               const c10::optional<at::Tensor>& g3, const c10::optional<at::Tensor>& m3,
+                               const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr,
+                               double beta1, double beta2, double eps, double grad_scale, int64_t rule,
+                               int64_t tail_blocks, const C1Fuse& c1) {
+  const bool fuse1 = c1.x != nullptr;
   const int B = a2.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv2_fwd: batch 1..128");
   check_f32(a1, (int64_t)B * 6272, "f32_conv2_fwd: a1");
@@ -678,15 +850,21 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   // blocks share a CU: the dispatcher otherwise doubles blocks up on some CUs while others idle
   // (measured 20.6 -> 19.7 us at B = 100). MIHVD_F32_C2F_LDS overrides (study knob).
   const int spread = (nblk + (ad.nblk > 0 ? ad.nblk : 0)) <= device_cu_count() ? 81920 + 1024 : 0;
-  const int lds = std::max(C2F_LDS, std::min(env_knob("MIHVD_F32_C2F_LDS", spread), 163840));
+  const int need = C2F_LDS + (fuse1 ? C2F_XIM * 4 : 0);
+  const int lds = std::max(need, std::min(env_knob("MIHVD_F32_C2F_LDS", spread), 163840));
   auto launch = [&](auto kern, int extra) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nblk + extra, 256, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
-                                                 a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, ad);
+                                                 a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, ad, c1);
   };
+  // MIHVD_F32_C2F_PREW=0: the W2 operand loaded after a full barrier (the earlier form)
+  const bool prew = env_knob("MIHVD_F32_C2F_PREW", 1) != 0;
+  TORCH_CHECK(!(fuse1 && ad.nblk > 0), "f32_conv2_fwd: the fused conv1 has no optimizer tail");
 #define C2F_CASE(T)                                                                  \
   case T:                                                                            \
     if (ad.nblk > 0) launch(f32_conv2_fwd_kernel<T, true>, ad.nblk);                 \
+    else if (fuse1) launch(f32_conv2_fwd_kernel<T, false, true, true>, 0);           \
+    else if (prew) launch(f32_conv2_fwd_kernel<T, false, true>, 0);                  \
     else launch(f32_conv2_fwd_kernel<T, false>, 0);                                  \
     break;
   switch (tpb) {
@@ -698,6 +876,8 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
     C2F_CASE(6)
     default:
       if (ad.nblk > 0) launch(f32_conv2_fwd_kernel<7, true>, ad.nblk);
+      else if (fuse1) launch(f32_conv2_fwd_kernel<7, false, true, true>, 0);
+      else if (prew) launch(f32_conv2_fwd_kernel<7, false, true>, 0);
       else launch(f32_conv2_fwd_kernel<7, false>, 0);
   }
 #undef C2F_CASE

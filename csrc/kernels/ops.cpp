@@ -90,6 +90,9 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
                    const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
                    const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
                    double grad_scale, int64_t rule, int64_t tail_blocks);
+void f32_conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1, const at::Tensor& w2,
+                    const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
 void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const c10::optional<at::Tensor>& g3,
                  const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
                  const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
@@ -242,6 +245,10 @@ void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a
   mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule,
                        tail_blocks);
 }
+void f32_conv12_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
+                   Tensor idx1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2) {
+  mihvd::f32_conv12_fwd(x, rows, state, w1, b1, a1, idx1, w2, b2, a2, idx2);
+}
 void f32_fc1_fwd_op(const Tensor& a2, Tensor w3, Tensor zpart, const OptT& g3, const OptT& m3, const OptT& v3,
                     const OptT& state, double lr, double beta1, double beta2, double eps, double grad_scale,
                     int64_t rule) {
@@ -325,6 +332,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor(c!)? p3=None, "
         "Tensor? g3=None, Tensor(d!)? m3=None, Tensor(e!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., "
         "float beta2=0., float eps=0., float grad_scale=1., int rule=0, int tail_blocks=0) -> ()");
+  m.def("f32_conv12_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
+        "Tensor w2, Tensor b2, Tensor(c!) a2, Tensor(d!) idx2) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor(w!) w3, Tensor(a!) zpart, Tensor? g3=None, Tensor(m!)? m3=None, "
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0) -> ()");
@@ -381,6 +390,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("bump_step_", &bump_step_op);
   m.impl("f32_conv1_fwd", &f32_conv1_op);
   m.impl("f32_conv2_fwd", &f32_conv2_op);
+  m.impl("f32_conv12_fwd", &f32_conv12_op);
   m.impl("f32_fc1_fwd", &f32_fc1_fwd_op);
   m.impl("f32_head_fwd_bwd", &f32_head_op);
   m.impl("f32_fc1_bwd", &f32_fc1_bwd_op);

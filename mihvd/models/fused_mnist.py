@@ -4,15 +4,16 @@ This is the flagship path (bench.py ``--impl fused``). The default precision is 
 ``precision="fp32"`` (horovod/tensorflow_mnist.py:118-121,130 train fp32 variables with fp32
 placeholders and AdamOptimizer). Every operand stays fp32 and GEMM-shaped work runs on gfx950's
 fp32-input matrix cores (``v_mfma_f32_16x16x4_f32``: exact products, fp32 accumulation;
-csrc/kernels/f32_fwd.hip, f32_bwd.hip). At world size 1 a step is seven hand-written launches:
+csrc/kernels/f32_fwd.hip, f32_bwd.hip). At world size 1 a step is six hand-written launches:
 
-    f32_conv1_fwd   conv1 (K = 25 taps on MFMA) + bias + ReLU + 2x2 pool/argmax
-    f32_conv2_fwd   conv2 implicit GEMM (pool-window-major rows), bias/ReLU/pool/argmax in registers
-    f32_fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs; the previous step's dense/kernel Adam
-                    update is applied to each W3 fragment as it is read (one read of W3 for both)
+    f32_conv12_fwd  conv1 (K = 25 taps on MFMA, computed per conv2 block for the a1 rows it reads)
+                    + conv2 implicit GEMM (pool-window-major rows), bias/ReLU/pool/argmax in registers
+    f32_fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs
     f32_head        slab sum + bias + ReLU + dropout(0.5) + fc2 + softmax-xent + fc2 backward -> dz
-    f32_fc1_bwd     dgrad dz.W3^T routed through the pool argmax / ReLU mask -> dY2, and dW3, db3,
-                    dW4, db4 written straight into the flat gradient (= fusion) buffer
+    f32_fc1_bwd     one block per 16 rows of W3: W3 is read once for the dgrad dz.W3^T (routed
+                    through the pool argmax / ReLU mask -> dY2), dW3 of the same elements is formed in
+                    registers and dense/kernel's Adam is applied from them (dW3 never goes through
+                    HBM); db3, dW4, db4 into the flat gradient (= fusion) buffer
     f32_conv2_bwd   conv2 dgrad -> conv1 gradient on chip -> fused conv1 wgrad; conv2 wgrad slabs
     f32_conv_reduce slab/partial-row reduction + Adam of every parameter but dense/kernel + step bump
 
@@ -318,6 +319,10 @@ class FusedMNISTTrainer:
         # 6.9 + 7.0 us apart (150.7 vs 145.3 us/step): conv1 still waits for the whole reduction,
         # and the cross-XCD release/acquire costs more than the saved launch
         self.f32_conv1_fuse = self.f32 and os.environ.get("MIHVD_F32_CONV1_FUSE", "0") == "1"
+        # MIHVD_F32_CONV12=1 (default): conv1 runs inside the conv2 forward launch (f32_conv12_fwd:
+        # every conv2 block computes the a1 rows it reads from x and writes its own rows of a1/idx1
+        # for the backward) instead of a launch of its own
+        self.f32_conv12 = self.f32 and os.environ.get("MIHVD_F32_CONV12", "1") != "0"
         self._c1_ready = False
         self._c1_sync = torch.zeros(4, device=dev, dtype=torch.int32) if self.f32 else None
         if self.f32:
@@ -631,12 +636,18 @@ class FusedMNISTTrainer:
         s3 = slice(W3_START, FLAT_NUMEL)
         if self.shard_w3:
             return self._launch_step_f32_shard(x, rows, labels)
+        fused12 = self.f32_conv12 and not self._c1_ready and not (self._w3_pending and self.f32_w3 == "tail")
         if self._c1_ready:
             self._c1_ready = False  # the previous step's conv_reduce computed this step's conv1
+        elif fused12:
+            o.f32_conv12_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
+                             self.idx1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
         else:
             o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
                             self.idx1)
-        if self._w3_pending and self.f32_w3 == "tail":
+        if fused12:
+            pass  # conv2 ran in the launch above
+        elif self._w3_pending and self.f32_w3 == "tail":
             # the previous step's dense/kernel Adam update (98 % of the optimizer's bytes) streams in
             # tail blocks of this MFMA-bound launch; fc1_fwd below is its first reader
             o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, self.params[s3],
@@ -725,8 +736,13 @@ class FusedMNISTTrainer:
         w2 = P("conv_layer2/conv2d/kernel")
         w3 = P("dense/kernel")
         R, r = self._f32_R, self.rank
-        o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1, self.idx1)
-        o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
+        if self.f32_conv12:
+            o.f32_conv12_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
+                             self.idx1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
+        else:
+            o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
+                            self.idx1)
+            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
         if self._shadow_ev is not None:  # the previous step's W3 row gather
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None

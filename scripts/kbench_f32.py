@@ -74,6 +74,9 @@ def main():
         "conv1_fwd": lambda: o.f32_conv1_fwd(tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"),
                                              P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1),
         "conv2_fwd": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2),
+        "conv12_fwd (conv1 fused)": lambda: o.f32_conv12_fwd(tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"),
+                                                             P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1, w2,
+                                                             P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2),
         "conv2_fwd+W3 adam tail": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
                                                           tr.params[s3], tr.grads[s3], tr.m[s3], tr.v[s3], st, 0.0,
                                                           b1, b2, tr.eps, 1.0, tr.rule, tr.f32_tail_blocks),
@@ -117,8 +120,12 @@ def main():
         res[name] = timed(fn, args.reps)
     # study variants (host knobs read at capture time, csrc/kernels/f32_*.hip): placement and roles
     study = {
-        "conv2_fwd [LDS 96 KB: 1 block/CU]": ({"MIHVD_F32_C2F_LDS": "98304"}, ks["conv2_fwd"]),
+        "conv2_fwd [LDS 76 KB: blocks may share a CU]": ({"MIHVD_F32_C2F_LDS": "76032"}, ks["conv2_fwd"]),
+        "conv2_fwd [W2 after a full barrier]": ({"MIHVD_F32_C2F_PREW": "0"}, ks["conv2_fwd"]),
+        "conv2_bwd [W2 after a full barrier]": ({"MIHVD_F32_C2B_PREW": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
+        "conv2_bwd [dgrad role only, W2 after a full barrier]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_PREW": "0"},
+                                                                ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd"]),
         "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),

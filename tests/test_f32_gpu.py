@@ -65,6 +65,42 @@ def test_f32_conv2_fwd(ops, B):
     assert (idx.long()[pos] == rd.reshape(B, 3136)[pos]).float().mean() > 0.999
 
 
+@pytest.mark.parametrize("B", [1, 7, 100, 128])
+def test_f32_conv12_fwd_matches_separate_launches(ops, B):
+    """conv1 fused into the conv2 forward launch (each block computes the a1 rows it reads, halo
+    included, and writes its own rows): a1, idx1, a2 and idx2 bit for bit equal to the two separate
+    launches, with the resident dataset's row permutation and the device step counter."""
+    g = torch.Generator(device="cuda").manual_seed(21)
+    n_pool = 3 * B + 5
+    x = torch.rand(n_pool, 784, device="cuda", generator=g)
+    rows = torch.randperm(n_pool, generator=torch.Generator().manual_seed(3)).to(torch.int32).cuda()
+    st = torch.tensor([2, 0, 0, 0], device="cuda", dtype=torch.int64)
+    w1 = torch.randn(800, device="cuda", generator=g) * 0.2
+    b1 = torch.randn(32, device="cuda", generator=g) * 0.1
+    w2 = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
+    b2 = torch.randn(64, device="cuda", generator=g) * 0.1
+    outs = []
+    for fused in (True, False):
+        a1 = torch.full((B, 14, 14, 32), float("nan"), device="cuda")
+        idx1 = torch.full((B, 14, 14, 32), 77, device="cuda", dtype=torch.uint8)
+        a2 = torch.empty(B, 3136, device="cuda")
+        idx2 = torch.empty(B, 3136, device="cuda", dtype=torch.uint8)
+        if fused:
+            ops.f32_conv12_fwd(x, rows, st, w1, b1, a1, idx1, w2, b2, a2, idx2)
+        else:
+            ops.f32_conv1_fwd(x, rows, st, w1, b1, a1, idx1)
+            ops.f32_conv2_fwd(a1, w2, b2, a2, idx2)
+        outs.append((a1, idx1, a2, idx2))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # and the conv2 output against torch on the batch the permutation selects
+    sel = rows.long()[(2 * B + torch.arange(B, device="cuda")) % n_pool]
+    ref1, _ = ref_conv_pool(x[sel].view(B, 28, 28, 1), w1.view(5, 5, 1, 32), b1)
+    ref2, _ = ref_conv_pool(ref1, w2, b2)
+    assert rel_err(outs[0][2], ref2.reshape(B, 3136)) < 1e-5
+
+
 @pytest.mark.parametrize("B", [7, 100])
 def test_f32_fc1_fwd_and_head(ops, B):
     g = torch.Generator(device="cuda").manual_seed(3)
