@@ -16,22 +16,51 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+// The 16-bit operand format. The MFMA kernels (conv_fwd.hip, conv_bwd.hip, fc.hip, w3_tail.h and
+// the operand helpers below) are written once against bf16x8 / f2bf / bf2f / mfma16 and compiled
+// twice: the default build in namespace mihvd with bf16 operands (v_mfma_f32_16x16x32_bf16), and
+// a -DMIHVD_F16 build in namespace mihvd::f16 with IEEE fp16 operands (v_mfma_f32_16x16x32_f16;
+// the Keras 'mixed_float16' policy, loss-scaled). Everything else in this header is format-free and
+// lives in namespace mihvd for both.
+#ifdef MIHVD_F16
+#define MIHVD_OPNS_BEGIN namespace mihvd { namespace f16 {
+#define MIHVD_OPNS_END } }
+#define MIHVD_OP16 at::kHalf
+#else
+#define MIHVD_OPNS_BEGIN namespace mihvd {
+#define MIHVD_OPNS_END }
+#define MIHVD_OP16 at::kBFloat16
+#endif
+
 namespace mihvd {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 #define LDS_PTR(T) __attribute__((address_space(3))) T*
 
+}  // namespace mihvd
+
+MIHVD_OPNS_BEGIN
+
+#ifdef MIHVD_F16
+typedef _Float16 bf16x8 __attribute__((ext_vector_type(8)));  // (the name is the format-free operand vector)
+// v_cvt_f16_f32: round-to-nearest-even; past 65504 -> inf, which the loss scaler detects.
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (_Float16)f); }
+__device__ __forceinline__ float bf2f(u16 h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+#else
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Plain cast: hipcc emits v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN preserved).
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
 __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
-
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+#endif
 
 // Fragment from a K-contiguous LDS image: rows are M (or N) indices, k contiguous.
 // `p` points at this lane's 8 elements (row r, k0 + 8*(lane>>4)); must be 16-byte aligned.
@@ -49,6 +78,10 @@ __device__ __forceinline__ bf16x8 frag_tr(const u16* rowp0, const u16* rowp1) {
   short8_t s = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, s);
 }
+
+MIHVD_OPNS_END
+
+namespace mihvd {
 
 // Counter-based dropout RNG (stateless: mask(seed, step, index) is recomputable anywhere).
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
@@ -158,9 +191,17 @@ __device__ __forceinline__ float mask_f(float v, bool keep) {
   return __uint_as_float(__float_as_uint(v) & (keep ? 0xffffffffu : 0u));
 }
 
+}  // namespace mihvd
+
+MIHVD_OPNS_BEGIN
+
 __device__ __forceinline__ uint2 pack4bf(float a, float b, float c, float d) {
   return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
 }
+
+MIHVD_OPNS_END
+
+namespace mihvd {
 
 // Adam update of four consecutive elements (K12 of SURVEY.md §2.5), shared by the flat-buffer
 // optimizer (optim.hip) and the dW3 tiles of fc1_wgrad that update W3 straight from the MFMA
@@ -192,6 +233,10 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, const float 
   v = fmaf(c.b2, v, (1.f - c.b2) * gk * gk);
   p -= c.lr_t * m * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(v), c.inv_sqrt_bc2, c.eps_t));
 }
+}  // namespace mihvd
+
+MIHVD_OPNS_BEGIN
+
 __device__ __forceinline__ uint2 adam4(float4& pp, float4& mm, float4& vv, const float4 gg, const AdamCoef& c) {
   float* pa = &pp.x;
   float* ma = &mm.x;
@@ -205,6 +250,10 @@ __device__ __forceinline__ uint2 adam4(float4& pp, float4& mm, float4& vv, const
   }
   return make_uint2((uint32_t)sh[0] | ((uint32_t)sh[1] << 16), (uint32_t)sh[2] | ((uint32_t)sh[3] << 16));
 }
+
+MIHVD_OPNS_END
+
+namespace mihvd {
 
 // Arguments of an Adam update fused into another kernel (p, m, v, shadow are the slices of the flat
 // buffers that the update covers).
@@ -279,6 +328,10 @@ struct AdamTail {
   int64_t head;          // ... and alone take the chunks [0, head) (64 float4 each) before the shared range
 };
 
+}  // namespace mihvd
+
+MIHVD_OPNS_BEGIN
+
 // One float4 of every array per lane per iteration, grid-stride — the loop of the standalone
 // adam_kernel (optim.hip), which streams at full HBM rate even on one 4-wave block per CU; the
 // arrays are restrict-qualified locals so loads may be hoisted past the previous stores.
@@ -321,4 +374,4 @@ __device__ __forceinline__ void adam_tail_run(const AdamTail& at) {
   adam_tail_stream(at, c, head4 + ((int64_t)blockIdx.x * waves + wave) * 64 + lane, at.n4, (int64_t)gridDim.x * waves * 64);
 }
 
-}  // namespace mihvd
+MIHVD_OPNS_END

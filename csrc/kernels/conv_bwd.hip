@@ -22,7 +22,7 @@
 #include "w3_tail.h"
 #include "xgmi_role.h"
 
-namespace mihvd {
+MIHVD_OPNS_BEGIN
 
 constexpr int CB_IPB = 4;               // images per wgrad block (2 per wave group)
 constexpr int CB_KQ = 4;                // fc1 dgrad split-K slabs
@@ -831,17 +831,17 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
                              bool* fold_done = nullptr) {
   const int B = a1.size(0);
   const int G = (int)conv2_wgrad_groups(B);
-  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
-  TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && idx1.numel() == a1.numel() &&
+  TORCH_CHECK(g2.dtype() == MIHVD_OP16 && g2.numel() == (int64_t)B * 3136 && idx2.numel() == g2.numel(), "conv2_bwd: g2/idx2");
+  TORCH_CHECK(a1.dtype() == MIHVD_OP16 && a1.numel() == (int64_t)B * 6272 && idx1.numel() == a1.numel() &&
                   idx1.dtype() == at::kByte, "conv2_bwd: a1/idx1");
-  TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200, "conv2_bwd: w2");
+  TORCH_CHECK(w2bf.dtype() == MIHVD_OP16 && w2bf.numel() == 51200, "conv2_bwd: w2");
   TORCH_CHECK(x.dtype() == at::kFloat && x.size(-1) == 784 && x.is_contiguous(), "conv2_bwd: x");
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() >= (int64_t)G * 51200, "conv2_bwd: slab must hold ceil(B/4) x 51200");
   TORCH_CHECK(cpart.dtype() == at::kFloat && cpart.numel() >= (int64_t)B * CP_W && cpart.is_contiguous(),
               "conv2_bwd: cpart must hold B x 896 floats (per-image dW1 | db1 | db2)");
   u16* g1p = nullptr;
   if (g1.has_value() && g1->defined()) {
-    TORCH_CHECK(g1->dtype() == at::kBFloat16 && g1->numel() == a1.numel(), "conv2_bwd: g1");
+    TORCH_CHECK(g1->dtype() == MIHVD_OP16 && g1->numel() == a1.numel(), "conv2_bwd: g1");
     g1p = (u16*)g1->data_ptr();
   }
   const int* rp = nullptr;
@@ -953,7 +953,7 @@ void conv2_bwd_adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Tens
   check_flat(g3, at::kFloat, n, "conv2_bwd_adam: g3");
   check_flat(m3, at::kFloat, n, "conv2_bwd_adam: m3");
   check_flat(v3, at::kFloat, n, "conv2_bwd_adam: v3");
-  check_flat(shadow3, at::kBFloat16, n, "conv2_bwd_adam: shadow3");
+  check_flat(shadow3, MIHVD_OP16, n, "conv2_bwd_adam: shadow3");
   TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_WORDS, "conv2_bwd_adam: state");
   AdamTail at{p3.data_ptr<float>(), g3.data_ptr<float>(), m3.data_ptr<float>(), v3.data_ptr<float>(),
               (u16*)shadow3.data_ptr(), n / 4, state.data_ptr<int64_t>(), (float)lr, (float)b1, (float)b2,
@@ -974,12 +974,12 @@ void conv2_bwd_w3adam(const at::Tensor& g2, const at::Tensor& idx2, const at::Te
   const int B = a1.size(0);
   const int64_t n = (int64_t)W3T_K * W3T_N;
   TORCH_CHECK(B >= 1 && B <= W3T_KP, "conv2_bwd_w3adam: batch must be in [1, 128]");
-  check_flat(dzT, at::kBFloat16, (int64_t)W3T_N * W3T_KP, "conv2_bwd_w3adam: dzT [1024][128] bf16");
-  check_flat(a2T, at::kBFloat16, (int64_t)W3T_K * W3T_KP, "conv2_bwd_w3adam: a2T [3136][128] bf16");
+  check_flat(dzT, MIHVD_OP16, (int64_t)W3T_N * W3T_KP, "conv2_bwd_w3adam: dzT [1024][128] bf16");
+  check_flat(a2T, MIHVD_OP16, (int64_t)W3T_K * W3T_KP, "conv2_bwd_w3adam: a2T [3136][128] bf16");
   check_flat(p3, at::kFloat, n, "conv2_bwd_w3adam: p3");
   check_flat(m3, at::kFloat, n, "conv2_bwd_w3adam: m3");
   check_flat(v3, at::kFloat, n, "conv2_bwd_w3adam: v3");
-  check_flat(shadow3, at::kBFloat16, n, "conv2_bwd_w3adam: shadow3");
+  check_flat(shadow3, MIHVD_OP16, n, "conv2_bwd_w3adam: shadow3");
   float* gp = nullptr;
   if (gW3.has_value() && gW3->defined()) {
     check_flat(*gW3, at::kFloat, n, "conv2_bwd_w3adam: gW3");
@@ -1027,7 +1027,7 @@ static ReduceAdam make_reduce_adam(const at::Tensor& slab, const at::Tensor& cpa
   check_flat(p, at::kFloat, n, "conv2_wgrad_reduce_adam: p");
   check_flat(m, at::kFloat, n, "conv2_wgrad_reduce_adam: m");
   check_flat(v, at::kFloat, n, "conv2_wgrad_reduce_adam: v");
-  check_flat(shadow, at::kBFloat16, n, "conv2_wgrad_reduce_adam: shadow");
+  check_flat(shadow, MIHVD_OP16, n, "conv2_wgrad_reduce_adam: shadow");
   TORCH_CHECK(state.scalar_type() == at::kLong && state.numel() >= ST_WORDS, "conv2_wgrad_reduce_adam: state");
   TORCH_CHECK(fc_lo % 4 == 0 && w3_lo % 4 == 0 && 0 <= fc_lo && fc_lo <= w3_lo && w3_lo <= n,
               "conv2_wgrad_reduce_adam: fc_lo/w3_lo");
@@ -1098,8 +1098,9 @@ void conv2_bwd_adam_fold(const at::Tensor& g2, const at::Tensor& idx2, const at:
   if (!done) launch_reduce_adam(ra, slab, cpart, B_of(a1), gW2, gW1, gb1, gb2);
 }
 
-}  // namespace mihvd
+MIHVD_OPNS_END
 
+#ifndef MIHVD_F16
 namespace mihvd {
 // Read (and with reset, clear) the conv barrier error word; waits for the current stream.
 int64_t conv_barrier_error(bool reset) {
@@ -1116,3 +1117,4 @@ int64_t conv_barrier_error(bool reset) {
   return (int64_t)v;
 }
 }  // namespace mihvd
+#endif

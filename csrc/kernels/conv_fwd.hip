@@ -16,7 +16,7 @@
 #include "common.h"
 #include "xgmi_role.h"
 
-namespace mihvd {
+MIHVD_OPNS_BEGIN
 
 // ------------------------------------------------------------------------------------------ //
 // conv1: x[row][784] fp32 -> a1[b][14][14][32] bf16 + argmax idx1 (0..3, u8)
@@ -336,7 +336,7 @@ void conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const
                const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1) {
   const int B = a1.size(0);
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "conv1_fwd: x");
-  TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 14 * 14 * 32 && a1.is_contiguous(), "conv1_fwd: a1");
+  TORCH_CHECK(a1.dtype() == MIHVD_OP16 && a1.numel() == (int64_t)B * 14 * 14 * 32 && a1.is_contiguous(), "conv1_fwd: a1");
   TORCH_CHECK(idx1.dtype() == at::kByte && idx1.numel() == a1.numel(), "conv1_fwd: idx1");
   TORCH_CHECK(w1.numel() == 800 && b1.numel() == 32 && w1.dtype() == at::kFloat, "conv1_fwd: weights");
   const int* rp = nullptr;
@@ -355,10 +355,10 @@ void conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const
 
 void conv2_fwd(const at::Tensor& a1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2) {
   const int B = a1.size(0);
-  TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && a1.is_contiguous(), "conv2_fwd: a1");
-  TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200 && w2bf.is_contiguous(), "conv2_fwd: w2 (bf16)");
+  TORCH_CHECK(a1.dtype() == MIHVD_OP16 && a1.numel() == (int64_t)B * 6272 && a1.is_contiguous(), "conv2_fwd: a1");
+  TORCH_CHECK(w2bf.dtype() == MIHVD_OP16 && w2bf.numel() == 51200 && w2bf.is_contiguous(), "conv2_fwd: w2 (bf16)");
   TORCH_CHECK(b2.dtype() == at::kFloat && b2.numel() == 64, "conv2_fwd: b2");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * 3136 && idx2.numel() == a2.numel(), "conv2_fwd: out");
+  TORCH_CHECK(a2.dtype() == MIHVD_OP16 && a2.numel() == (int64_t)B * 3136 && idx2.numel() == a2.numel(), "conv2_fwd: out");
   static bool attr = [] {
     hipFuncSetAttribute((const void*)conv2_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, C2_LDS_BYTES);
     return true;
@@ -375,13 +375,13 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
                 at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2, int64_t coll) {
   const int B = a1.size(0);
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "conv12_fwd: x");
-  TORCH_CHECK(a1.dtype() == at::kBFloat16 && a1.numel() == (int64_t)B * 6272 && a1.is_contiguous(), "conv12_fwd: a1");
+  TORCH_CHECK(a1.dtype() == MIHVD_OP16 && a1.numel() == (int64_t)B * 6272 && a1.is_contiguous(), "conv12_fwd: a1");
   TORCH_CHECK(idx1.dtype() == at::kByte && idx1.numel() == a1.numel(), "conv12_fwd: idx1");
-  TORCH_CHECK(w1bf.dtype() == at::kBFloat16 && w1bf.numel() == 800 && w1bf.is_contiguous(), "conv12_fwd: w1 (bf16)");
+  TORCH_CHECK(w1bf.dtype() == MIHVD_OP16 && w1bf.numel() == 800 && w1bf.is_contiguous(), "conv12_fwd: w1 (bf16)");
   TORCH_CHECK(b1.dtype() == at::kFloat && b1.numel() == 32, "conv12_fwd: b1");
-  TORCH_CHECK(w2bf.dtype() == at::kBFloat16 && w2bf.numel() == 51200 && w2bf.is_contiguous(), "conv12_fwd: w2 (bf16)");
+  TORCH_CHECK(w2bf.dtype() == MIHVD_OP16 && w2bf.numel() == 51200 && w2bf.is_contiguous(), "conv12_fwd: w2 (bf16)");
   TORCH_CHECK(b2.dtype() == at::kFloat && b2.numel() == 64, "conv12_fwd: b2");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * 3136 && idx2.numel() == a2.numel() &&
+  TORCH_CHECK(a2.dtype() == MIHVD_OP16 && a2.numel() == (int64_t)B * 3136 && idx2.numel() == a2.numel() &&
                   idx2.dtype() == at::kByte, "conv12_fwd: a2/idx2");
   const int* rp = nullptr;
   int n_pool = x.size(0);
@@ -417,4 +417,4 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
   else launch(conv12_fwd_kernel<8>, 512);
 }
 
-}  // namespace mihvd
+MIHVD_OPNS_END

@@ -21,7 +21,7 @@
 #include "common.h"
 #include "xgmi_role.h"
 
-namespace mihvd {
+MIHVD_OPNS_BEGIN
 
 constexpr int FC1_K = 3136, FC1_N = 1024, FC1_KS = 7, FC1_KSL = FC1_K / FC1_KS;   // 448 = 14 K steps
 constexpr int FC1_NT = 32;                                                          // columns per block
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(NW * 64) fc1_fwd_kernel(const u16* __restrict_
 __global__ void __launch_bounds__(256) head_kernel(
     const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
-    int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, u16* __restrict__ h_out,
+    int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float dz_mul, u16* __restrict__ h_out,
     u16* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B, CollRole cr) {
   __shared__ float red[4][10];
   __shared__ float dl[10];
@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(256) head_kernel(
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < 10; ++c) s = fmaf(dl[c], w4r[i][c], s);
-    g[i] = h[i] > 0.f ? s * keep_scale : 0.f;
+    g[i] = h[i] > 0.f ? s * dz_mul : 0.f;  // dz_mul = keep_scale x the loss scale (fp16 build)
   }
   *reinterpret_cast<uint2*>(dz_out + (int64_t)b * FC1_N + n0) = pack4bf(g[0], g[1], g[2], g[3]);
 }
@@ -688,8 +688,8 @@ static void set_max_lds(K kernel, int bytes) {
 void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
   const int B = a2.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_fwd: batch must be in [1, 128] (got ", B, ")");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_fwd: a2");
-  TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_fwd: w3");
+  TORCH_CHECK(a2.dtype() == MIHVD_OP16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_fwd: a2");
+  TORCH_CHECK(w3bf.dtype() == MIHVD_OP16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_fwd: w3");
   TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "fc1_fwd: zpart [7][B][1024]");
   const int MT = (B + 15) >> 4;
   const int lds = (FC1_KSL * F1_WSTR + MT * 16 * F1_ASTR) * 2;
@@ -717,12 +717,12 @@ void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll) {
+                  int64_t coll, double dz_scale) {
   const int B = h.size(0);
   TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "head: zpart");
   TORCH_CHECK(b3.numel() == FC1_N && w4.numel() == FC1_N * 10 && b4.numel() == 10 && w4.dtype() == at::kFloat, "head: params");
   TORCH_CHECK(labels.dtype() == at::kLong, "head: labels must be int64");
-  TORCH_CHECK(h.dtype() == at::kBFloat16 && h.numel() == (int64_t)B * FC1_N && dz.numel() == h.numel(), "head: h/dz");
+  TORCH_CHECK(h.dtype() == MIHVD_OP16 && h.numel() == (int64_t)B * FC1_N && dz.numel() == h.numel(), "head: h/dz");
   TORCH_CHECK(dlog.numel() == B * 10 && stats.numel() == B * 2, "head: dlog/stats");
   TORCH_CHECK(rate >= 0.0 && rate < 1.0, "head: dropout rate");
   const int* rp = nullptr;
@@ -736,7 +736,8 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
   const CollRole cr = xgmi_role_lookup(coll);
   head_kernel<<<B + cr.nblk, 256, 0, stream>>>(zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(),
                                                b4.data_ptr<float>(), labels.data_ptr<int64_t>(), rp, n_pool, sp,
-                                               (uint32_t)seed, thresh, keep_scale, (u16*)h.data_ptr(),
+                                               (uint32_t)seed, thresh, keep_scale, (float)(keep_scale * dz_scale),
+                                               (u16*)h.data_ptr(),
                                                (u16*)dz.data_ptr(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B,
                                                cr);
 }
@@ -750,9 +751,9 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
                              const AdamArgs* ad, bool write_grad, int64_t jt_lo, int64_t jt_hi, int64_t coll) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_wgrad: batch");
-  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
-  TORCH_CHECK(a2.numel() == (int64_t)B * FC1_K && a2.dtype() == at::kBFloat16, "fc1_wgrad: a2");
-  TORCH_CHECK(h.numel() == (int64_t)B * FC1_N && h.dtype() == at::kBFloat16 && dlog.numel() == B * 10, "fc1_wgrad: h/dlog");
+  TORCH_CHECK(dz.dtype() == MIHVD_OP16 && dz.numel() == (int64_t)B * FC1_N, "fc1_wgrad: dz");
+  TORCH_CHECK(a2.numel() == (int64_t)B * FC1_K && a2.dtype() == MIHVD_OP16, "fc1_wgrad: a2");
+  TORCH_CHECK(h.numel() == (int64_t)B * FC1_N && h.dtype() == MIHVD_OP16 && dlog.numel() == B * 10, "fc1_wgrad: h/dlog");
   TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_wgrad: gW3");
   TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_wgrad: fc grads");
   TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_wgrad: roles must be 1, 2 or 3");
@@ -763,9 +764,9 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   if (dz_w3.has_value() && dz_w3->defined()) {
     TORCH_CHECK(a2_w3.has_value() && a2_w3->defined(), "fc1_wgrad: dz_w3 and a2_w3 go together");
     Kw = dz_w3->size(0);
-    TORCH_CHECK(dz_w3->dtype() == at::kBFloat16 && dz_w3->numel() == (int64_t)Kw * FC1_N && dz_w3->is_contiguous(),
+    TORCH_CHECK(dz_w3->dtype() == MIHVD_OP16 && dz_w3->numel() == (int64_t)Kw * FC1_N && dz_w3->is_contiguous(),
                 "fc1_wgrad: dz_w3 [K][1024] bf16");
-    TORCH_CHECK(a2_w3->dtype() == at::kBFloat16 && a2_w3->is_contiguous() && a2_w3->numel() % Kw == 0,
+    TORCH_CHECK(a2_w3->dtype() == MIHVD_OP16 && a2_w3->is_contiguous() && a2_w3->numel() % Kw == 0,
                 "fc1_wgrad: a2_w3 [K][3136] (or [K][C] columns of the row-tile range) bf16");
     a2s = (int)(a2_w3->numel() / Kw);
     if (a2s != FC1_K) {
@@ -886,7 +887,7 @@ void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor
   const int64_t n = (int64_t)FC1_K * FC1_N;
   for (const at::Tensor* t : {&p3, &m3, &v3})
     TORCH_CHECK(t->dtype() == at::kFloat && t->numel() == n && t->is_contiguous(), "fc1_wgrad_adam: p3/m3/v3 fp32 [3136*1024]");
-  TORCH_CHECK(shadow3.dtype() == at::kBFloat16 && shadow3.numel() == n && shadow3.is_contiguous(), "fc1_wgrad_adam: shadow3");
+  TORCH_CHECK(shadow3.dtype() == MIHVD_OP16 && shadow3.numel() == n && shadow3.is_contiguous(), "fc1_wgrad_adam: shadow3");
   TORCH_CHECK(state.dtype() == at::kLong && state.numel() >= ST_WORDS, "fc1_wgrad_adam: state");
   for (const at::Tensor* t : {&p3, &m3, &v3, &shadow3})
     TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "fc1_wgrad_adam: 16-byte aligned segments required");
@@ -899,10 +900,10 @@ void fc1_wgrad_adam(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor
 void fc1_dgrad(const at::Tensor& dz, const at::Tensor& w3bf, const at::Tensor& a2, at::Tensor& g2) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_dgrad: batch");
-  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N && dz.is_contiguous(), "fc1_dgrad: dz");
-  TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_dgrad: w3");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_dgrad: a2");
-  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * FC1_K && g2.is_contiguous(), "fc1_dgrad: g2");
+  TORCH_CHECK(dz.dtype() == MIHVD_OP16 && dz.numel() == (int64_t)B * FC1_N && dz.is_contiguous(), "fc1_dgrad: dz");
+  TORCH_CHECK(w3bf.dtype() == MIHVD_OP16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_dgrad: w3");
+  TORCH_CHECK(a2.dtype() == MIHVD_OP16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_dgrad: a2");
+  TORCH_CHECK(g2.dtype() == MIHVD_OP16 && g2.numel() == (int64_t)B * FC1_K && g2.is_contiguous(), "fc1_dgrad: g2");
   const int G = (B + DG_ROWS - 1) / DG_ROWS;
   const int grid = 8 * ((DG_JT + 7) / 8) * G;
   auto stream = c10::hip::getCurrentHIPStream().stream();
@@ -920,13 +921,13 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
   TORCH_CHECK(roles >= 1 && roles <= 3, "fc1_bwd: roles must be 1, 2 or 3");
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= MAXB, "fc1_bwd: batch");
-  TORCH_CHECK(dz.dtype() == at::kBFloat16 && dz.numel() == (int64_t)B * FC1_N && dz.is_contiguous(), "fc1_bwd: dz");
-  TORCH_CHECK(a2.dtype() == at::kBFloat16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_bwd: a2");
-  TORCH_CHECK(h.numel() == (int64_t)B * FC1_N && h.dtype() == at::kBFloat16 && dlog.numel() == B * 10, "fc1_bwd: h/dlog");
-  TORCH_CHECK(w3bf.dtype() == at::kBFloat16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_bwd: w3");
+  TORCH_CHECK(dz.dtype() == MIHVD_OP16 && dz.numel() == (int64_t)B * FC1_N && dz.is_contiguous(), "fc1_bwd: dz");
+  TORCH_CHECK(a2.dtype() == MIHVD_OP16 && a2.numel() == (int64_t)B * FC1_K && a2.is_contiguous(), "fc1_bwd: a2");
+  TORCH_CHECK(h.numel() == (int64_t)B * FC1_N && h.dtype() == MIHVD_OP16 && dlog.numel() == B * 10, "fc1_bwd: h/dlog");
+  TORCH_CHECK(w3bf.dtype() == MIHVD_OP16 && w3bf.numel() == (int64_t)FC1_K * FC1_N && w3bf.is_contiguous(), "fc1_bwd: w3");
   TORCH_CHECK(gW3.numel() == (int64_t)FC1_K * FC1_N && gW3.dtype() == at::kFloat && gW3.is_contiguous(), "fc1_bwd: gW3");
   TORCH_CHECK(gb3.numel() == FC1_N && gW4.numel() == FC1_N * 10 && gb4.numel() == 10, "fc1_bwd: fc grads");
-  TORCH_CHECK(g2.dtype() == at::kBFloat16 && g2.numel() == (int64_t)B * FC1_K && g2.is_contiguous(), "fc1_bwd: g2");
+  TORCH_CHECK(g2.dtype() == MIHVD_OP16 && g2.numel() == (int64_t)B * FC1_K && g2.is_contiguous(), "fc1_bwd: g2");
   const int G = (B + DG_ROWS - 1) / DG_ROWS;
   const int n_dg = 8 * ((DG_JT + 7) / 8) * G;
   const int n_small = (roles & 2) ? FB_TOTAL - FB_WGRAD : 0;
@@ -936,9 +937,9 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
   u16 *pa2T = nullptr, *pdzT = nullptr;
   if (a2T.has_value() && a2T->defined()) {
     TORCH_CHECK(dzT.has_value() && dzT->defined(), "fc1_bwd: a2T and dzT go together");
-    TORCH_CHECK(a2T->dtype() == at::kBFloat16 && a2T->numel() == (int64_t)FC1_K * FT_KP && a2T->is_contiguous(),
+    TORCH_CHECK(a2T->dtype() == MIHVD_OP16 && a2T->numel() == (int64_t)FC1_K * FT_KP && a2T->is_contiguous(),
                 "fc1_bwd: a2T must be bf16 [3136][128]");
-    TORCH_CHECK(dzT->dtype() == at::kBFloat16 && dzT->numel() == (int64_t)FC1_N * FT_KP && dzT->is_contiguous(),
+    TORCH_CHECK(dzT->dtype() == MIHVD_OP16 && dzT->numel() == (int64_t)FC1_N * FT_KP && dzT->is_contiguous(),
                 "fc1_bwd: dzT must be bf16 [1024][128]");
     pa2T = (u16*)a2T->data_ptr();
     pdzT = (u16*)dzT->data_ptr();
@@ -951,4 +952,4 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
       gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, n_dg, n_small, cr, pa2T, pdzT);
 }
 
-}  // namespace mihvd
+MIHVD_OPNS_END

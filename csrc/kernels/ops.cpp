@@ -19,7 +19,7 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll);
+                  int64_t coll, double dz_scale);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
                const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi, int64_t coll);
@@ -124,7 +124,33 @@ int64_t f32_dgrad_blocks(int64_t B);
 int64_t conv_barrier_error(bool reset);
 }  // namespace mihvd
 
+// The fp16-operand build of conv_fwd.hip / conv_bwd.hip / fc.hip (common.h, -DMIHVD_F16).
+namespace mihvd {
+namespace f16 {
+void conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+               const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1);
+void conv2_fwd(const at::Tensor& a1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
+void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                const at::Tensor& w1bf, const at::Tensor& b1, const at::Tensor& w2bf, const at::Tensor& b2, at::Tensor& a1,
+                at::Tensor& idx1, at::Tensor& a2, at::Tensor& idx2, int64_t coll);
+void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart);
+void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog,
+             const at::Tensor& w3bf, at::Tensor& gW3, at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, at::Tensor& g2,
+             int64_t roles, int64_t coll, const c10::optional<at::Tensor>& a2T,
+             const c10::optional<at::Tensor>& dzT);
+void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
+                  const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+                  int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
+                  int64_t coll, double dz_scale);
+void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
+               const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
+               const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1,
+               int64_t coll);
+}  // namespace f16
+}  // namespace mihvd
+
 namespace {
+
 using at::Tensor;
 using OptT = c10::optional<at::Tensor>;
 
@@ -148,8 +174,36 @@ void fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tenso
 void fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::fc1_fwd(a2, w3, zpart); }
 void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
              const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog, Tensor stats,
-             int64_t coll) {
-  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll);
+             int64_t coll, double dz_scale) {
+  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale);
+}
+// fp16-operand ops (the Keras mixed_float16 policy): the bf16 ops' schemas, half tensors.
+void conv1_fwd_f16_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1,
+                      Tensor a1, Tensor idx1) {
+  mihvd::f16::conv1_fwd(x, rows, state, w1, b1, a1, idx1);
+}
+void conv2_fwd_f16_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2) {
+  mihvd::f16::conv2_fwd(a1, w2, b2, a2, idx2);
+}
+void conv12_fwd_f16_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1,
+                       const Tensor& w2, const Tensor& b2, Tensor a1, Tensor idx1, Tensor a2, Tensor idx2, int64_t coll) {
+  mihvd::f16::conv12_fwd(x, rows, state, w1, b1, w2, b2, a1, idx1, a2, idx2, coll);
+}
+void fc1_fwd_f16_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f16::fc1_fwd(a2, w3, zpart); }
+void head_f16_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
+                 const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
+                 Tensor stats, int64_t coll, double dz_scale) {
+  mihvd::f16::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale);
+}
+void fc1_bwd_f16_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, const Tensor& w3,
+                    Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles, int64_t coll,
+                    const OptT& a2T, const OptT& dzT) {
+  mihvd::f16::fc1_bwd(dz, a2, h, dlog, w3, gW3, gb3, gW4, gb4, g2, roles, coll, a2T, dzT);
+}
+void conv2_bwd_f16_op(const Tensor& g2, const Tensor& idx2, const Tensor& a1, const Tensor& w2, const Tensor& x,
+                      const OptT& rows, const OptT& state, const Tensor& idx1, Tensor slab, Tensor cpart,
+                      const OptT& g1, int64_t coll) {
+  mihvd::f16::conv2_bwd(g2, idx2, a1, w2, x, rows, state, idx1, slab, cpart, g1, coll);
 }
 void fc1_wgrad_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, Tensor gW3, Tensor gb3,
                   Tensor gW4, Tensor gb4, int64_t roles, const OptT& dz_w3, const OptT& a2_w3, int64_t jt_lo,
@@ -291,7 +345,21 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(g!)? dzT=None) -> ()");
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
-        "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, int coll=-1) -> ()");
+        "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, int coll=-1, "
+        "float dz_scale=1.) -> ()");
+  m.def("conv1_fwd_f16(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
+  m.def("conv2_fwd_f16(Tensor a1, Tensor w2h, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
+  m.def("conv12_fwd_f16(Tensor x, Tensor? rows, Tensor? state, Tensor w1h, Tensor b1, Tensor w2h, Tensor b2, "
+        "Tensor(a!) a1, Tensor(b!) idx1, Tensor(c!) a2, Tensor(d!) idx2, int coll=-1) -> ()");
+  m.def("fc1_fwd_f16(Tensor a2, Tensor w3h, Tensor(a!) zpart) -> ()");
+  m.def("head_fwd_bwd_f16(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
+        "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
+        "int coll=-1, float dz_scale=1.) -> ()");
+  m.def("fc1_bwd_f16(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor w3h, Tensor(a!) gW3, Tensor(b!) gb3, "
+        "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3, int coll=-1, Tensor(f!)? a2T=None, "
+        "Tensor(g!)? dzT=None) -> ()");
+  m.def("conv2_bwd_f16(Tensor g2, Tensor idx2, Tensor a1, Tensor w2h, Tensor x, Tensor? rows, Tensor? state, "
+        "Tensor idx1, Tensor(a!) slab, Tensor(b!) cpart, Tensor(c!)? g1=None, int coll=-1) -> ()");
   m.def("fc1_wgrad(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor(a!) gW3, Tensor(b!) gb3, Tensor(c!) gW4, "
         "Tensor(d!) gb4, int roles=3, Tensor? dz_w3=None, Tensor? a2_w3=None, int jt_lo=0, int jt_hi=49, "
         "int coll=-1) -> ()");
@@ -374,6 +442,13 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("fc1_bwd", &fc1_bwd_op);
   m.impl("fc1_fwd", &fc1_fwd_op);
   m.impl("head_fwd_bwd", &head_op);
+  m.impl("conv1_fwd_f16", &conv1_fwd_f16_op);
+  m.impl("conv2_fwd_f16", &conv2_fwd_f16_op);
+  m.impl("conv12_fwd_f16", &conv12_fwd_f16_op);
+  m.impl("fc1_fwd_f16", &fc1_fwd_f16_op);
+  m.impl("head_fwd_bwd_f16", &head_f16_op);
+  m.impl("fc1_bwd_f16", &fc1_bwd_f16_op);
+  m.impl("conv2_bwd_f16", &conv2_bwd_f16_op);
   m.impl("fc1_wgrad", &fc1_wgrad_op);
   m.impl("fc1_wgrad_adam", &fc1_wgrad_adam_op);
   m.impl("fc1_dgrad", &fc1_dgrad_op);

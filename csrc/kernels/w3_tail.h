@@ -22,7 +22,7 @@
 
 #include "common.h"
 
-namespace mihvd {
+MIHVD_OPNS_BEGIN
 
 constexpr int W3T_N = 1024, W3T_K = 3136, W3T_KP = 128;  // factor rows are W3T_KP (= max batch) long
 constexpr int W3T_TILES = (W3T_K / 32) * (W3T_N / 32);    // 3136 wave tiles of 32 x 32
@@ -187,4 +187,4 @@ __device__ __forceinline__ void w3_tail_run(const W3TileTail& wt) {
   }
 }
 
-}  // namespace mihvd
+MIHVD_OPNS_END

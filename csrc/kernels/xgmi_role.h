@@ -81,6 +81,15 @@ struct CollRole {
   unsigned* herr = nullptr; // host-coherent mirror of err (the health monitor's watched word)
 };
 
+// Host: the prepared role of descriptor id (xgmi.hip); id < 0 -> no role (nblk = 0).
+CollRole xgmi_role_lookup(int64_t id);
+
+}  // namespace mihvd
+
+// The role code runs inside the MFMA kernels' launches and its fused Adam writes their operand
+// format's shadow (common.h), so it is compiled in the kernels' namespace.
+MIHVD_OPNS_BEGIN
+
 __device__ __forceinline__ unsigned* xg_u32(char* base, int64_t off) { return (unsigned*)(base + off); }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t xg_rsrc(const char* p, uint32_t bytes) {
@@ -236,7 +245,4 @@ __device__ __forceinline__ void coll_role_run(const CollRole& c, int bid) {
   xg_exit(c, e);
 }
 
-// Host: the prepared role of descriptor id (xgmi.hip); id < 0 -> no role (nblk = 0).
-CollRole xgmi_role_lookup(int64_t id);
-
-}  // namespace mihvd
+MIHVD_OPNS_END

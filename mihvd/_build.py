@@ -90,6 +90,10 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (set HIPCC)")
 
 
+# MFMA kernel sources compiled a second time with fp16 operands (-DMIHVD_F16).
+F16_SOURCES = ("conv_fwd.hip", "conv_bwd.hip", "fc.hip")
+
+
 def build_kernels(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "kernels", "*.cpp")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "kernels", "*.cuh")))
@@ -121,9 +125,17 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int | None =
             _run(cmd, cwd=BUILD)
         return obj
 
+    def compile_f16(src):
+        # the fp16-operand build of the MFMA kernels (common.h: namespace mihvd::f16, v_mfma_*_f16)
+        obj = os.path.join(BUILD, os.path.basename(src) + ".f16.o")
+        if force or _newer(obj, [src] + hdrs + [__file__]):
+            _run([hipcc, *common, "-DMIHVD_F16=1", "-c", src, "-o", obj], cwd=BUILD)
+        return obj
+
     jobs = jobs or min(8, os.cpu_count() or 4)
+    f16_srcs = [s for s in srcs if os.path.basename(s) in F16_SOURCES]
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(compile_one, srcs))
+        objs = list(ex.map(compile_one, srcs)) + list(ex.map(compile_f16, f16_srcs))
     tmp = KERNELS_SO + ".tmp%d" % os.getpid()
     link = [hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH, *objs, "-L" + tlib, "-ltorch", "-ltorch_cpu",
             "-lc10", "-lc10_hip", "-ltorch_hip", "-Wl,-rpath," + tlib, "-o", tmp]

@@ -273,17 +273,16 @@ class Model:
     """``policy`` is the Keras mixed-precision policy (tensorflow_mnist_gpu.py:26-28). A module with
     ``impl == "hip"`` (``MNISTConvNet(impl="hip")``) trains through the hand-written CDNA4 kernels
     (one fused forward+backward autograd node per batch): ``float32`` runs the exact-fp32 kernels,
-    ``mixed_bfloat16`` the bf16-operand kernels (fp32 accumulation and master weights);
-    ``mixed_float16`` has no fp16-operand kernel set and runs stock fp16 autocast ops with the HIP
-    dynamic loss scaler."""
+    ``mixed_bfloat16`` the bf16-operand kernels (fp32 accumulation and master weights),
+    ``mixed_float16`` the same kernels built with fp16 operands (v_mfma_f32_16x16x32_f16) under the
+    HIP dynamic loss scaler: the kernels scale dz by the current scale, the scaler unscales, checks
+    for overflow and skips the step on inf/NaN (Keras LossScaleOptimizer semantics)."""
 
     def __init__(self, module: torch.nn.Module, policy: str = "float32"):
         self.module = module
         self.policy = policy
         if getattr(module, "impl", None) == "hip":
-            if policy == "mixed_float16":
-                module.impl = "torch"  # no fp16-operand kernel set: stock fp16 autocast + HIP loss scaler
-            module.hip_precision = "fp32" if policy == "float32" else "bf16"
+            module.hip_precision = {"float32": "fp32", "mixed_float16": "fp16"}.get(policy, "bf16")
         self.optimizer = None
         self.loss_fn = None
         self.metrics = []
@@ -316,17 +315,21 @@ class Model:
     def train_on_batch(self, xb, yb):
         self.module.train()
         self.optimizer.zero_grad()
-        if getattr(self.module, "impl", None) == "hip" and self.policy != "mixed_float16":
-            # whole forward+backward in the CDNA4 kernels, one autograd node (bf16 MFMA inside)
+        if getattr(self.module, "impl", None) == "hip":
+            # whole forward+backward in the CDNA4 kernels, one autograd node (MFMA inside)
             from .ops.functional import fused_mnist_loss
 
-            loss, acc = fused_mnist_loss(self.module, xb, yb, training=True, return_accuracy=True)
-            loss.backward()
-            self.optimizer.step()
-            return loss.detach(), acc
-        with self._autocast():
-            logits = self.module(xb)
-        loss = self.loss_fn(logits.float(), yb)
+            S = float(self._scaler.scale) if self._scaler is not None else None
+            loss, acc = fused_mnist_loss(self.module, xb, yb, training=True, return_accuracy=True, loss_scale=S)
+            if self._scaler is None:
+                loss.backward()
+                self.optimizer.step()
+                return loss.detach(), acc
+            logits = None
+        else:
+            with self._autocast():
+                logits = self.module(xb)
+            loss = self.loss_fn(logits.float(), yb)
         if self._scaler is not None:
             self._scaler.scale_loss(loss).backward()
             self.optimizer.synchronize()
@@ -339,7 +342,8 @@ class Model:
         else:
             loss.backward()
             self.optimizer.step()
-        acc = (logits.argmax(1) == yb).float().mean()
+        if logits is not None:
+            acc = (logits.argmax(1) == yb).float().mean()
         return loss.detach(), acc.detach()
 
     @torch.no_grad()

@@ -58,10 +58,10 @@ def test_fused_example_throughput_matches_bench(tmp_path):
     assert example * 1.5 >= bench["value"], (example, bench["value"])
 
 
-@pytest.mark.parametrize("policy", ["mixed_bfloat16", "float32"])
+@pytest.mark.parametrize("policy", ["mixed_bfloat16", "float32", "mixed_float16"])
 def test_keras_example_trains_on_hip_kernels(tmp_path, policy):
     """tensorflow_mnist_gpu.py's Model.fit through MNISTConvNet(impl="hip"): one epoch of fused
-    forward+backward HIP kernels (bf16 or exact-fp32 operands by policy), DistributedOptimizer,
+    forward+backward HIP kernels (bf16, fp16 + loss scaling, or exact-fp32 operands by policy), DistributedOptimizer,
     evaluation, best checkpoint and the final save."""
     import torch
 

@@ -1,0 +1,123 @@
+"""fp16-operand build of the MFMA kernels (csrc/kernels/common.h -DMIHVD_F16: conv_fwd / conv_bwd /
+fc compiled a second time in namespace mihvd::f16 with v_mfma_f32_16x16x32_f16) — the Keras
+``mixed_float16`` policy of the reference (tensorflow_mnist_gpu.py:26-28) on the HIP path.
+
+Numerics are checked against a plain fp32 torch autograd reference of the same network (dropout
+off): the fp16 kernels must land within fp16-operand rounding of it, closer than the bf16 build
+(3 more mantissa bits), for any loss scale in the normal range; an oversized scale must surface as
+non-finite gradients (what the dynamic loss scaler skips on), never as silently wrong ones.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from mihvd import _native
+
+    _native.require_kernels()
+    assert hasattr(torch.ops.mihvd, "conv2_bwd_f16"), "kernel library built without the fp16 set"
+    return torch.ops.mihvd
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _batch(B=64, seed=9):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.rand(B, 784, device="cuda", generator=g)
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    return x, y
+
+
+def _ref_grads(x, y, seed=3):
+    from mihvd.models.mnist import MNISTConvNet
+
+    ref = MNISTConvNet(impl="torch", seed=seed).cuda().eval()
+    loss = torch.nn.functional.cross_entropy(ref(x), y)
+    loss.backward()
+    return loss.item(), {n: p.grad.clone() for n, p in ref.ordered_parameters()}
+
+
+def _hip_grads(x, y, precision, loss_scale=None, seed=3):
+    from mihvd.models.mnist import MNISTConvNet
+    from mihvd.ops.functional import fused_mnist_loss
+
+    model = MNISTConvNet(impl="hip", seed=seed).cuda()
+    loss = fused_mnist_loss(model, x, y, training=False, precision=precision, loss_scale=loss_scale)
+    loss.backward()
+    return loss.item(), {n: p.grad.clone() for n, p in model.ordered_parameters()}
+
+
+def test_f16_grads_match_fp32_reference(ops):
+    x, y = _batch()
+    l_ref, g_ref = _ref_grads(x, y)
+    l16, g16 = _hip_grads(x, y, "fp16")
+    lbf, gbf = _hip_grads(x, y, "bf16")
+    assert abs(l16 - l_ref) < 2e-3 * max(1.0, abs(l_ref)), (l16, l_ref)
+    e16 = {n: rel_err(g16[n], g_ref[n]) for n in g_ref}
+    ebf = {n: rel_err(gbf[n], g_ref[n]) for n in g_ref}
+    for n in g_ref:
+        assert torch.isfinite(g16[n]).all(), n
+        assert e16[n] < 1e-2, (n, e16[n])
+    # fp16 keeps 10 mantissa bits to bf16's 7: the large GEMM gradients come out closer
+    for n in ("dense/kernel", "conv_layer2/conv2d/kernel"):
+        assert e16[n] < ebf[n], (n, e16[n], ebf[n])
+
+
+@pytest.mark.parametrize("S", [2.0 ** 8, 2.0 ** 15])
+def test_f16_loss_scale_is_transparent(ops, S):
+    """The kernels scale dz by S and the node divides it back out: the gradients do not depend on
+    S (beyond fp16 rounding) and the loss not at all."""
+    x, y = _batch(seed=21)
+    l_ref, g_ref = _ref_grads(x, y)
+    l16, g16 = _hip_grads(x, y, "fp16", loss_scale=S)
+    assert abs(l16 - l_ref) < 2e-3 * max(1.0, abs(l_ref))
+    for n in g_ref:
+        assert rel_err(g16[n], g_ref[n]) < 1e-2, (n, S)
+
+
+def test_f16_overflow_surfaces_as_nonfinite(ops):
+    """dz x S past fp16's 65504 becomes inf in the kernels' 16-bit intermediates: every gradient
+    derived from dz turns non-finite (what the loss scaler checks), dW4/db4 (fp32 dlog) stay finite."""
+    x, y = _batch(seed=5)
+    _, g = _hip_grads(x, y, "fp16", loss_scale=2.0 ** 40)
+    bad = [n for n in g if not torch.isfinite(g[n]).all()]
+    assert any(n.startswith("dense/kernel") for n in bad), bad
+    assert torch.isfinite(g["dense_1/kernel"]).all() and torch.isfinite(g["dense_1/bias"]).all()
+
+
+def test_keras_mixed_float16_trains_on_f16_kernels(ops):
+    """hvd.Model(policy="mixed_float16") on an impl="hip" module: fp16 kernels + dynamic loss scaler;
+    an overflowing first scale is halved and the step skipped, then training converges."""
+    import mihvd.keras as K
+    from mihvd.models.mnist import MNISTConvNet
+
+    torch.manual_seed(0)
+    module = MNISTConvNet(impl="hip", seed=1).cuda()
+    m = K.Model(module, policy="mixed_float16")
+    assert module.hip_precision == "fp16"
+    opt = torch.optim.Adam(module.parameters(), lr=1e-3)
+    opt.synchronize = lambda: None
+    import contextlib
+
+    opt.skip_synchronize = contextlib.nullcontext
+    m.compile(opt, torch.nn.functional.cross_entropy)
+    m._scaler = K._LossScaler(init_scale=2.0 ** 40, growth_interval=10 ** 6)
+    x, y = _batch(B=100, seed=4)
+    before = [p.detach().clone() for p in module.parameters()]
+    m.train_on_batch(x, y)  # overflows: skipped, scale halved
+    assert all(torch.equal(a, p) for a, p in zip(before, module.parameters()))
+    assert float(m._scaler.scale) == 2.0 ** 39
+    m._scaler._ls[0] = 2.0 ** 15
+    first = None
+    for _ in range(60):
+        loss, acc = m.train_on_batch(x, y)
+        first = first if first is not None else float(loss)
+    assert float(loss) < 0.5 * first, (first, float(loss))
+    assert all(torch.isfinite(p).all() for p in module.parameters())
