@@ -645,7 +645,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
 constexpr int CBF_PS = 68, CBF_RS = 18 * CBF_PS, CBF_MAXR = 18;
 constexpr int CBF_IMG = CBF_MAXR * CBF_RS;            // floats: tall padded dY2 rows
 constexpr int CBF_XIM = 2 * 1024;                     // two padded x images [32][32]
-constexpr int CBF_PW = 8 * 26 * 16;                   // per-wave conv1 partials
+constexpr int CBF_PW = 8 * 2 * 64 * 4;                // per-wave conv1 partials (MEPI: 2 f32x4 per lane)
 constexpr int CBF_LDS_DG = (CBF_IMG + CBF_XIM + CBF_PW) * 4;               // 109,632 B
 constexpr int CBF_A1S = 14 * 18 * 32, CBF_DYS = 196 * 32, CBF_WBUF = CBF_A1S + CBF_DYS;
 constexpr int CBF_LDS_WG = 2 * CBF_WBUF * 4;                                // 114,688 B
@@ -654,6 +654,7 @@ constexpr int CBF_MAXCH = (CBF_MAXR * 18 * 16 + 511) / 512;                 // d
 constexpr int CBF_IG = 4;                                                   // images per wgrad block
 constexpr int CP_F32 = 832;                                                 // [dW1 (800) | db1 (32)]
 static_assert(CBF_LDS <= 163840, "f32_conv2_bwd LDS");
+static_assert(8 * 26 * 16 <= CBF_PW, "the VALU conv1-wgrad epilogue's partials fit");
 static_assert(4 * 2 * 7 * 64 * 16 <= CBF_IMG * 4, "dgrad partial exchange fits the dY2 image");
 static_assert(4 * 5 * 4 * 64 * 16 <= CBF_LDS_WG, "wgrad partial exchange fits the staging buffers");
 
@@ -677,7 +678,8 @@ __device__ __forceinline__ void lds_barrier() {
 // PREW: the W2 register operand is loaded BEFORE the staging barrier (after the staging loads, so the
 // staging writes wait only for their own loads), and the barrier orders LDS alone: the 25 W2 loads
 // per lane (200 KB per block from L2) land while the dY2 image is staged instead of after it.
-template <int TPB, bool PREW>
+// MEPI: the conv1 weight gradient of the epilogue on MFMA instead of VALU (see step 3 below).
+template <int TPB, bool PREW, bool MEPI>
 __device__ __forceinline__ void f32_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
@@ -745,16 +747,19 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
     for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
   }
-  // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched
-  constexpr int NP = (2 * TPB + 7) / 8;  // (nt, tile) pairs per wave
+  // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched.
+  // VALU form: (nt, tile) pairs p = wave + 8k, lane pixel 4 lg + r. MEPI form: the wave's pixel
+  // groups 4 cq + r of every tile, the same pixel on the four lane groups (channel 16 nt + lr).
+  constexpr int NP = MEPI ? TPB : (2 * TPB + 7) / 8;
   float ea[NP][4];
   int ex[NP][4];
 #pragma unroll
   for (int k = 0; k < NP; ++k)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int pp = wave + 8 * k, P = 16 * (T0 + (pp >> 1)) + 4 * lg + r;
-      const bool ok = pp < 2 * TPB && P < np;
+      const int pp = wave + 8 * k;
+      const int P = MEPI ? 16 * (T0 + k) + 4 * cq + r : 16 * (T0 + (pp >> 1)) + 4 * lg + r;
+      const bool ok = (MEPI || pp < 2 * TPB) && P < np;
       const int64_t o = (int64_t)min(P, np - 1) * 32 + 16 * nt + lr;
       ea[k][r] = mask_f(a1[o], ok);
       ex[k][r] = idx1[o];
@@ -820,6 +825,59 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
   for (int i = 0; i < TPB; ++i) red[((cq * 2 + nt) * TPB + i) * 64 + lane] = acc[i];
   __syncthreads();
+  if constexpr (MEPI) {
+    // 3'. the conv1 weight gradient as a small GEMM on MFMA: D[ci][tap] += sum_k A[ci][k] B[k][tap]
+    //     over the full-resolution pixels k of the pooled pixels this wave owns (pixel groups 4 cq + r
+    //     of every tile; k-step = one pooled pixel, its four 2x2 positions d = lg): A = the routed
+    //     gradient (g1 at the argmax position, 0 elsewhere), B = the x value under tap n of position d
+    //     (n = 25: 1, so that column is db1). Per pooled pixel 2 LDS reads + 2 MFMAs per lane, against
+    //     25 LDS reads + 26 FMAs per element (and the lane-group shuffles) of the VALU form.
+    int off0, off1;
+    {
+      const int n1 = 16 + lr;
+      off0 = (lr / 5) * 32 + lr % 5;
+      off1 = n1 < 25 ? (n1 / 5) * 32 + n1 % 5 : 0;
+    }
+    const float one1 = lr == 9 ? 1.f : 0.f;  // column 25 = db1
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+    for (int k = 0; k < TPB; ++k) {
+      // the four co-quarter partials of this pixel group (lane lr + 16 cq of the reduction layout)
+      const int li = lr + 16 * cq;
+      const f32x4 s = ((red[((0 * 2 + nt) * TPB + k) * 64 + li] + red[((1 * 2 + nt) * TPB + k) * 64 + li]) +
+                       red[((2 * 2 + nt) * TPB + k) * 64 + li]) +
+                      red[((3 * 2 + nt) * TPB + k) * 64 + li];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int P = 16 * (T0 + k) + 4 * cq + r;  // wave-uniform
+        if (P >= np) break;
+        const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
+        const float g = ea[k][r] > 0.f ? s[r] : 0.f;
+        const float a = ex[k][r] == lg ? g : 0.f;
+        const float* xs = xim + (bb - b0) * 1024 + (2 * py + (lg >> 1)) * 32 + 2 * px + (lg & 1);
+        const float x0 = xs[off0];
+        const float x1 = 16 + lr < 25 ? xs[off1] : one1;
+        c0 = mfma4(a, x0, c0);
+        c1 = mfma4(a, x1, c1);
+      }
+    }
+    // C[row = 4 lg + i][col = lr] = D[ci = 16 nt + 4 lg + i][tap = lr (c0) or 16 + lr (c1)]; the four
+    // waves of a channel half sum through LDS (the dY2 image area is still being read: use pw)
+    f32x4* pw4 = reinterpret_cast<f32x4*>(pw);
+    pw4[(wave * 2 + 0) * 64 + lane] = c0;
+    pw4[(wave * 2 + 1) * 64 + lane] = c1;
+    __syncthreads();
+    for (int q = t; q < CP_F32; q += 512) {
+      const int e = q >> 5, c = q & 31, h = c >> 4, l = c & 15;  // tap e (25 = db1), channel c
+      const int tile = e >> 4, col = (e & 15), ln = 16 * (l >> 2) + col, i = l & 3;
+      const float* pf = pw;
+      const float v = (pf[(((h + 0) * 2 + tile) * 64 + ln) * 4 + i] + pf[(((h + 2) * 2 + tile) * 64 + ln) * 4 + i]) +
+                      (pf[(((h + 4) * 2 + tile) * 64 + ln) * 4 + i] + pf[(((h + 6) * 2 + tile) * 64 + ln) * 4 + i]);
+      cpart[(int64_t)bid * CP_F32 + q] = v;  // q = tap * 32 + ci (dW1, HWIO) or 800 + ci (db1)
+    }
+    c2b_stamp(3);
+    return;
+  }
   // 3. epilogue: (nt, tile) pairs p = wave, wave + 8, ...: mask -> g1, the conv1 weight gradient of
   //    the routed g1 (one 5x5 patch of x per pooled element), db1
   float s25[26];
@@ -986,7 +1044,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   c2b_stamp(6);
 }
 
-template <int TPB, bool PREW>
+template <int TPB, bool PREW, bool MEPI>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
@@ -995,7 +1053,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
   const int bid = blockIdx.x;
   c2b_stamp(0);
   if (bid < n_dg) {
-    f32_conv2_dgrad_block<TPB, PREW>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
+    f32_conv2_dgrad_block<TPB, PREW, MEPI>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
     return;
   }
   f32_conv2_wgrad_block(bid - n_dg, dY2, a1, slab, B, smf);
@@ -1376,11 +1434,14 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
                                      cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg);
   };
-  // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form)
+  // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
+  // MIHVD_F32_C2B_MEPI=0: the conv1 weight gradient of the dgrad epilogue on VALU (the earlier form)
   const bool prew = env_knob("MIHVD_F32_C2B_PREW", 1) != 0;
-#define C2B_CASE(T)                                                             \
-  case T:                                                                       \
-    prew ? launch(f32_conv2_bwd_kernel<T, true>) : launch(f32_conv2_bwd_kernel<T, false>); \
+  const bool mepi = env_knob("MIHVD_F32_C2B_MEPI", 1) != 0;
+#define C2B_CASE(T)                                                                          \
+  case T:                                                                                    \
+    if (mepi) launch(f32_conv2_bwd_kernel<T, true, true>);                                   \
+    else prew ? launch(f32_conv2_bwd_kernel<T, true, false>) : launch(f32_conv2_bwd_kernel<T, false, false>); \
     break;
   switch (tpb) {
     C2B_CASE(1)
