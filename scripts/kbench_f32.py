@@ -156,6 +156,34 @@ def main():
             res[f"whole step [dense/kernel Adam: {alt}]"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
             tr._join()
     tr.f32_w3 = mode
+    # whole-step studies: trainer attributes and launch knobs (read at capture time)
+    steps = {
+        "whole step [conv1 separate]": ({"f32_conv12": False}, {}),
+        "whole step [conv1 separate, conv2_fwd blocks may share a CU]": ({"f32_conv12": False},
+                                                                         {"MIHVD_F32_C2F_LDS": "76032"}),
+        "whole step [conv1 separate, shared CU, W2 after a full barrier]": (
+            {"f32_conv12": False}, {"MIHVD_F32_C2F_LDS": "76032", "MIHVD_F32_C2F_PREW": "0"}),
+        "whole step [conv12, blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "76032"}),
+        "whole step [conv12, W2 after a full barrier]": ({}, {"MIHVD_F32_C2F_PREW": "0"}),
+        "whole step [conv1 wgrad epilogue on VALU]": ({}, {"MIHVD_F32_C2B_MEPI": "0"}),
+    }
+    for name, (attrs, env) in steps.items():
+        old_attr = {k: getattr(tr, k) for k in attrs}
+        old_env = {k: os.environ.get(k) for k in env}
+        for k, v in attrs.items():
+            setattr(tr, k, v)
+        os.environ.update(env)
+        try:
+            res[name] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
+            tr._join()
+        finally:
+            for k, v in old_attr.items():
+                setattr(tr, k, v)
+            for k, v in old_env.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     tr.lr = saved
     width = max(len(k) for k in res)
     for k, v in res.items():
