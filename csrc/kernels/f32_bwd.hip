@@ -982,18 +982,29 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     if (n + 1 < nimg) load_img(img0 + n + 1, v);
     const float* A1s = buf;
     const float* DYs = buf + CBF_A1S;
-    // K steps s = wave + 8u (pixels 2s: lanes 0-31, 2s + 1: lanes 32-63), unrolled so the LDS
-    // reads of later steps are in flight while earlier steps' MFMAs issue
+    // K steps s = wave + 8u (pixels 2s: lanes 0-31, 2s + 1: lanes 32-63). Software pipeline, fully
+    // unrolled: the six LDS operands of step u + 1 are read before step u's five MFMAs issue
+    // (sched_barrier pins it; left alone, the scheduler reads each operand pair right before its
+    // MFMAs and waits lgkmcnt(0) every two MFMAs, which idled the MFMA pipe about half the time).
+    float opa[2], opb[2][5];
+    auto load_step = [&](int u, float& a, float (&b)[5]) {
+      const int st = wave + 8 * u, q = 2 * st + hh, qy = q / 14, qx = q - 14 * qy;
+      a = DYs[q * 32 + l32];
+      const float* bp = A1s + (qy * 18 + qx) * 32 + l32;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) b[kw] = bp[kw * 32];
+    };
+    load_step(0, opa[0], opb[0]);
 #pragma unroll
     for (int u = 0; u < 13; ++u) {
-      const int s = wave + 8 * u;
-      if (u < 12 || s < 98) {  // wave-uniform (98 = 12 x 8 + 2)
-        const int q = 2 * s + hh, qy = q / 14, qx = q - 14 * qy;
-        const float a = DYs[q * 32 + l32];
-        const float* bp = A1s + (qy * 18 + qx) * 32 + l32;
+      const int cur = u & 1;
+      if (u + 1 < 12 || (u + 1 == 12 && wave + 96 < 98)) load_step(u + 1, opa[cur ^ 1], opb[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (u < 12 || wave + 96 < 98) {  // wave-uniform (98 = 12 x 8 + 2)
 #pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(a, bp[kw * 32], acc[kw]);
+        for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(opa[cur], opb[cur][kw], acc[kw]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (n + 1 < nimg) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();

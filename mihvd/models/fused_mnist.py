@@ -4,10 +4,10 @@ This is the flagship path (bench.py ``--impl fused``). The default precision is 
 ``precision="fp32"`` (horovod/tensorflow_mnist.py:118-121,130 train fp32 variables with fp32
 placeholders and AdamOptimizer). Every operand stays fp32 and GEMM-shaped work runs on gfx950's
 fp32-input matrix cores (``v_mfma_f32_16x16x4_f32``: exact products, fp32 accumulation;
-csrc/kernels/f32_fwd.hip, f32_bwd.hip). At world size 1 a step is six hand-written launches:
+csrc/kernels/f32_fwd.hip, f32_bwd.hip). At world size 1 a step is seven hand-written launches:
 
-    f32_conv12_fwd  conv1 (K = 25 taps on MFMA, computed per conv2 block for the a1 rows it reads)
-                    + conv2 implicit GEMM (pool-window-major rows), bias/ReLU/pool/argmax in registers
+    f32_conv1_fwd   conv1 (K = 25 taps on MFMA), bias/ReLU/pool/argmax in registers
+    f32_conv2_fwd   conv2 implicit GEMM (pool-window-major rows, W2 in registers), same epilogue
     f32_fc1_fwd     split-K GEMM over W3 -> fp32 partial slabs
     f32_head        slab sum + bias + ReLU + dropout(0.5) + fc2 + softmax-xent + fc2 backward -> dz
     f32_fc1_bwd     one block per 16 rows of W3: W3 is read once for the dgrad dz.W3^T (routed
@@ -319,10 +319,12 @@ class FusedMNISTTrainer:
         # 6.9 + 7.0 us apart (150.7 vs 145.3 us/step): conv1 still waits for the whole reduction,
         # and the cross-XCD release/acquire costs more than the saved launch
         self.f32_conv1_fuse = self.f32 and os.environ.get("MIHVD_F32_CONV1_FUSE", "0") == "1"
-        # MIHVD_F32_CONV12=1 (default): conv1 runs inside the conv2 forward launch (f32_conv12_fwd:
-        # every conv2 block computes the a1 rows it reads from x and writes its own rows of a1/idx1
-        # for the backward) instead of a launch of its own
-        self.f32_conv12 = self.f32 and os.environ.get("MIHVD_F32_CONV12", "1") != "0"
+        # MIHVD_F32_CONV12=1 (measured alternative, off): conv1 runs inside the conv2 forward launch
+        # (f32_conv12_fwd: every conv2 block computes the a1 rows it reads from x and writes its own
+        # rows of a1/idx1 for the backward) instead of a launch of its own. Bitwise equal, but each
+        # block recomputes its halo rows and the conv2 MFMA loop starts later: 135.1 vs 132.4 us per
+        # whole step (scripts/kbench_f32.py, profiles/r04/kbench_f32_r04c.txt)
+        self.f32_conv12 = self.f32 and os.environ.get("MIHVD_F32_CONV12", "0") == "1"
         self._c1_ready = False
         self._c1_sync = torch.zeros(4, device=dev, dtype=torch.int32) if self.f32 else None
         if self.f32:

@@ -127,6 +127,9 @@ def main():
         "conv2_bwd [dgrad role only, W2 after a full barrier]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_PREW": "0"},
                                                                 ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd"]),
+        "conv2_bwd [conv1 wgrad epilogue on VALU]": ({"MIHVD_F32_C2B_MEPI": "0"}, ks["conv2_bwd"]),
+        "conv2_bwd [dgrad role only, VALU epilogue]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_MEPI": "0"},
+                                                     ks["conv2_bwd"]),
         "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
@@ -158,13 +161,9 @@ def main():
     tr.f32_w3 = mode
     # whole-step studies: trainer attributes and launch knobs (read at capture time)
     steps = {
-        "whole step [conv1 separate]": ({"f32_conv12": False}, {}),
-        "whole step [conv1 separate, conv2_fwd blocks may share a CU]": ({"f32_conv12": False},
-                                                                         {"MIHVD_F32_C2F_LDS": "76032"}),
-        "whole step [conv1 separate, shared CU, W2 after a full barrier]": (
-            {"f32_conv12": False}, {"MIHVD_F32_C2F_LDS": "76032", "MIHVD_F32_C2F_PREW": "0"}),
-        "whole step [conv12, blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "76032"}),
-        "whole step [conv12, W2 after a full barrier]": ({}, {"MIHVD_F32_C2F_PREW": "0"}),
+        "whole step [conv1 fused into conv2_fwd (conv12)]": ({"f32_conv12": True}, {}),
+        "whole step [conv2_fwd blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "76032"}),
+        "whole step [conv2_fwd W2 after a full barrier]": ({}, {"MIHVD_F32_C2F_PREW": "0"}),
         "whole step [conv1 wgrad epilogue on VALU]": ({}, {"MIHVD_F32_C2B_MEPI": "0"}),
     }
     for name, (attrs, env) in steps.items():
