@@ -500,7 +500,10 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
   }
 }
 
-template <int G, bool ADAM, bool STORE>
+// PD: how many chunks ahead p/m/v are loaded (ring of PD + 1 register slots). The loop's HBM
+// traffic (p, m, v in; p, m, v out: 75 MB per step) is bound by the bytes each CU keeps in flight;
+// PD = 2 keeps ~48 KB per CU, PD = 4 ~96 KB.
+template <int G, bool ADAM, bool STORE, int PD = 2>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
@@ -540,7 +543,8 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   };
   // p (and m, v) of chunk c: W3[f0 + lr][nb + 16 c + 4 lg .. + 3]
   const int64_t rowo = (int64_t)(f0 + lr) * 1024 + nb + 4 * lg;
-  float4 pv[3], mv[3], vv[3];
+  constexpr int NS = PD + 1;
+  float4 pv[NS], mv[NS], vv[NS];
   auto load_pmv = [&](int c, int slot) {
     const int64_t o = rowo + 16 * c;
     pv[slot] = *reinterpret_cast<const float4*>(w3 + o);
@@ -555,16 +559,16 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
 #pragma unroll
   for (int u = 0; u < G; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   load_z(0);
-  load_pmv(0, 0);
-  load_pmv(1, 1);
+#pragma unroll
+  for (int c = 0; c < PD; ++c) load_pmv(c, c);
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     float* buf = buf0 + (c & 1) * F1R_LDS_BUF;
     store_z(buf);
     if (c + 1 < 8) load_z(c + 1);
-    if (c + 2 < 8) load_pmv(c + 2, (c + 2) % 3);
+    if (c + PD < 8) load_pmv(c + PD, (c + PD) % NS);
     lds_wave_fence();
-    const int s3 = c % 3;
+    const int s3 = c % NS;
     const float4 p = pv[s3];
     // dgrad: G tiles of 16 samples, the four k elements of the chunk outer (independent accumulators)
     float4 zb[G];
@@ -937,6 +941,24 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 // Per image: a1 padded rows kh..kh+13 [14][18][32] and the dY2 channel half [196][32], register-
 // staged double buffering (the next image's loads are in flight while this one is multiplied).
 // 8 waves split the K steps (w, w + 8, ...); their partial tiles are summed through LDS.
+// XCD-aware order of a role's blocks: the hardware deals a launch's blocks round-robin over the 8
+// XCDs (blockIdx & 7), each with its own L2. Returns the logical index of global block g within the
+// role's range [lo, hi) such that every XCD gets a contiguous run of logical indices, so blocks that
+// read the same data (the 10 wgrad blocks of an image group) share one XCD's L2 instead of fetching
+// it from HBM eight times.
+__device__ __forceinline__ int xcd_contiguous(int g, int lo, int hi) {
+  const int x = g & 7;
+  int before = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int first = lo + ((c - lo) & 7);
+    const int cnt = first < hi ? (hi - first + 7) >> 3 : 0;
+    if (c < x) before += cnt;
+  }
+  const int first_x = lo + ((x - lo) & 7);
+  return before + ((g - first_x) >> 3);
+}
+
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
                                                       float* smf) {
@@ -1059,7 +1081,8 @@ template <int TPB, bool PREW, bool MEPI>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
-    const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg) {
+    const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
+    int n_wg) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
@@ -1067,7 +1090,8 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     f32_conv2_dgrad_block<TPB, PREW, MEPI>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
     return;
   }
-  f32_conv2_wgrad_block(bid - n_dg, dY2, a1, slab, B, smf);
+  // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
+  f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, smf);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1355,11 +1379,14 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
           dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
           gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad);
     };
-#define F1R_CASE(GG)                                                       \
-  case GG:                                                                 \
-    if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>); \
-    else if (adam) launch(f32_fc1_bwd_rows_kernel<GG, true, false>);       \
-    else launch(f32_fc1_bwd_rows_kernel<GG, false, true>);                 \
+    // MIHVD_F32_F1R_PD: p/m/v prefetch depth of the fused-Adam form (4, or 2: the earlier depth)
+    const bool deep = env_knob("MIHVD_F32_F1R_PD", 4) >= 4;
+#define F1R_CASE(GG)                                                                              \
+  case GG:                                                                                        \
+    if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>);                        \
+    else if (adam && deep) launch(f32_fc1_bwd_rows_kernel<GG, true, false, 4>);                   \
+    else if (adam) launch(f32_fc1_bwd_rows_kernel<GG, true, false>);                              \
+    else launch(f32_fc1_bwd_rows_kernel<GG, false, true>);                                        \
     break;
     switch (G) {
       F1R_CASE(1)
@@ -1439,16 +1466,18 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const int lds = std::max(CBF_LDS, std::min(env_knob("MIHVD_F32_C2B_LDS", 0), 163840));
   const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
   const int ndg_arg = role == 2 ? 0 : n_dg;
+  const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
-                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg);
+                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg);
   };
   // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
-  // MIHVD_F32_C2B_MEPI=0: the conv1 weight gradient of the dgrad epilogue on VALU (the earlier form)
+  // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA
   const bool prew = env_knob("MIHVD_F32_C2B_PREW", 1) != 0;
-  const bool mepi = env_knob("MIHVD_F32_C2B_MEPI", 1) != 0;
+  // (MFMA form measured slower: 52.5 vs 51.1 us, dgrad role 28.9 vs 27.8 us, profiles/r04/kbench_f32_r04d.txt)
+  const bool mepi = env_knob("MIHVD_F32_C2B_MEPI", 0) != 0;
 #define C2B_CASE(T)                                                                          \
   case T:                                                                                    \
     if (mepi) launch(f32_conv2_bwd_kernel<T, true, true>);                                   \

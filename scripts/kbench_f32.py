@@ -127,9 +127,13 @@ def main():
         "conv2_bwd [dgrad role only, W2 after a full barrier]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_PREW": "0"},
                                                                 ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd"]),
-        "conv2_bwd [conv1 wgrad epilogue on VALU]": ({"MIHVD_F32_C2B_MEPI": "0"}, ks["conv2_bwd"]),
-        "conv2_bwd [dgrad role only, VALU epilogue]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_MEPI": "0"},
+        "conv2_bwd [conv1 wgrad epilogue on MFMA]": ({"MIHVD_F32_C2B_MEPI": "1"}, ks["conv2_bwd"]),
+        "conv2_bwd [dgrad role only, MFMA epilogue]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_MEPI": "1"},
                                                      ks["conv2_bwd"]),
+        "conv2_bwd [wgrad blocks in launch order]": ({"MIHVD_F32_C2B_XCD": "0"}, ks["conv2_bwd"]),
+        "conv2_bwd [wgrad role only, launch order]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_XCD": "0"},
+                                                     ks["conv2_bwd"]),
+        "fc1_bwd+W3 adam [p/m/v 2 chunks ahead]": ({"MIHVD_F32_F1R_PD": "2"}, ks["fc1_bwd+W3 adam"]),
         "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
@@ -164,7 +168,9 @@ def main():
         "whole step [conv1 fused into conv2_fwd (conv12)]": ({"f32_conv12": True}, {}),
         "whole step [conv2_fwd blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "76032"}),
         "whole step [conv2_fwd W2 after a full barrier]": ({}, {"MIHVD_F32_C2F_PREW": "0"}),
-        "whole step [conv1 wgrad epilogue on VALU]": ({}, {"MIHVD_F32_C2B_MEPI": "0"}),
+        "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
+        "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
+        "whole step [fc1_bwd p/m/v 2 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "2"}),
     }
     for name, (attrs, env) in steps.items():
         old_attr = {k: getattr(tr, k) for k in attrs}

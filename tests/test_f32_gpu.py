@@ -239,7 +239,7 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
 def test_f32_conv2_bwd_and_reduce(ops, B, mepi, monkeypatch):
     """conv2 dgrad + fused conv1 wgrad, conv2 wgrad slabs, and the reduction, vs autograd of
     conv1 -> pool -> conv2 with the routed conv2 gradient. mepi: the conv1 weight gradient of the
-    dgrad epilogue on MFMA (default) or on VALU (MIHVD_F32_C2B_MEPI=0)."""
+    dgrad epilogue on VALU (default) or on MFMA (MIHVD_F32_C2B_MEPI=1)."""
     monkeypatch.setenv("MIHVD_F32_C2B_MEPI", mepi)
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.rand(B, 784, device="cuda", generator=g)
