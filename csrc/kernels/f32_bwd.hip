@@ -35,6 +35,15 @@ __device__ __forceinline__ void c2b_stamp(int k) {
   if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memtime();
 #endif
 }
+// f32_fc1_bwd row form (f32_stamps_enable kernel 2): 0 start, 1 + c: wave 0's end of chunk c,
+// 9: after the partial-exchange barrier, 10: end of the routing epilogue (wave 0)
+__device__ unsigned long long* g_f1r_stamps = nullptr;
+__device__ __forceinline__ void f1r_stamp(int k) {
+#ifdef MIHVD_F32_STAMPS
+  unsigned long long* p = g_f1r_stamps;
+  if (p != nullptr && threadIdx.x == 0) p[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memtime();
+#endif
+}
 // per-wave stamp (lane 0 of every wave): slot 8 + wave
 __device__ __forceinline__ void c2b_stamp_wave() {
 #ifdef MIHVD_F32_STAMPS
@@ -518,6 +527,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   constexpr int KS = 4 * G;  // K steps of the wgrad chain (samples padded to 16 G)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * bid, nb = 128 * wave;
+  f1r_stamp(0);
   float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
   // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch)
   float a2r[KS];
@@ -602,9 +612,11 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
       *reinterpret_cast<float4*>(ad.m + o) = mm;
       *reinterpret_cast<float4*>(ad.v + o) = vq;
     }
+    f1r_stamp(1 + c);
   }
   // the eight K-part partials meet in LDS (the dz buffers are dead after the barrier)
   __syncthreads();
+  f1r_stamp(9);
   float4* red = reinterpret_cast<float4*>(smf);  // [8 waves][8 tiles][64 lanes]
 #pragma unroll
   for (int u = 0; u < G; ++u) red[(wave * 8 + u) * 64 + lane] = make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
@@ -641,6 +653,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
       }
     }
   }
+  f1r_stamp(10);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1289,8 +1302,8 @@ static void chk_f32(const at::Tensor& t, int64_t numel, const char* what) {
 void f32_fwd_stamps_set(unsigned long long* p);  // f32_fwd.hip
 
 at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel) {
-  static at::Tensor buf[2];
-  TORCH_CHECK(kernel == 0 || kernel == 1, "f32_stamps_enable: kernel 0 = conv2_bwd, 1 = conv2_fwd");
+  static at::Tensor buf[3];
+  TORCH_CHECK(kernel >= 0 && kernel <= 2, "f32_stamps_enable: kernel 0 = conv2_bwd, 1 = conv2_fwd, 2 = fc1_bwd");
   unsigned long long* p = nullptr;
   if (n_blocks > 0) {
     buf[kernel] = at::zeros({n_blocks * 16}, at::TensorOptions().dtype(at::kLong).device(at::kCUDA));
@@ -1300,6 +1313,8 @@ at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel) {
   }
   if (kernel == 0) {
     TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_c2b_stamps), &p, sizeof(p)) == hipSuccess, "f32_stamps_enable");
+  } else if (kernel == 2) {
+    TORCH_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_f1r_stamps), &p, sizeof(p)) == hipSuccess, "f32_stamps_enable");
   } else {
     f32_fwd_stamps_set(p);
   }
@@ -1379,8 +1394,9 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
           dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
           gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad);
     };
-    // MIHVD_F32_F1R_PD: p/m/v prefetch depth of the fused-Adam form (4, or 2: the earlier depth)
-    const bool deep = env_knob("MIHVD_F32_F1R_PD", 4) >= 4;
+    // MIHVD_F32_F1R_PD=4: p/m/v prefetched 4 chunks ahead instead of 2 (measured no faster:
+    // 28.2 vs 27.8 us, profiles/r04/kbench_f32_r04e.txt; the loop is not bound by HBM bytes in flight)
+    const bool deep = env_knob("MIHVD_F32_F1R_PD", 2) >= 4;
 #define F1R_CASE(GG)                                                                              \
   case GG:                                                                                        \
     if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>);                        \

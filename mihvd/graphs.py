@@ -31,9 +31,22 @@ import torch
 
 class CapturedStep:
     """``serialize=True``: each replay is launched only once the previous one has completed (a
-    host wait on an event; costs one launch latency per step)."""
+    host wait on an event; costs one launch latency per step).
 
-    def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False, sync_warmup: bool = True):
+    The parameters' ``AccumulateGrad`` nodes — the autograd nodes that add each backward's gradient
+    into ``p.grad`` — are kept alive from the warm-up through the capture (``self.accumulators``),
+    so the captured backward accumulates through the same nodes the warm-up created instead of
+    nodes created while capturing. Autograd holds a leaf's node only weakly: once the last warm-up
+    step's graph is freed the node dies and the capture's forward builds a new one. With the new
+    nodes, BERT-base under bf16 autocast replays correctly once and then writes non-finite values
+    into the Linear layers' bias gradients from the second replay on (scripts/bert_graph_bisect.py:
+    variant C0 fails, A0 — C0 holding only these nodes — tracks eager; fp32 (N) is unaffected;
+    profiles/r04/bert_graph_bisect_*.log). Holding the nodes costs no activation memory: a leaf's
+    node references the parameter, not the step's tensors. ``MIHVD_GRAPH_HOLD_ACCUMULATORS=0``
+    restores the failing form for study.
+    """
+
+    def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False, sync_warmup: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("CapturedStep needs a GPU")
         self.step_fn = step_fn
@@ -42,31 +55,23 @@ class CapturedStep:
         self._pending = False
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        # The last warm-up step's output, autograd graph included, stays alive for the life of the
-        # captured step, and each warm-up output is read back before the next step is issued. With
-        # the warm-up freed before capture instead, BERT-base's replays go non-finite at the second
-        # replay once the host synchronises between replays (scripts/bert_graph_bisect.py: variants
-        # H vs C, and this class with MIHVD_GRAPH_HOLD_WARMUP=0); held, they track eager. Costs one
-        # step's activations of memory. MIHVD_GRAPH_HOLD_WARMUP=0 restores the freeing form.
-        hold = os.environ.get("MIHVD_GRAPH_HOLD_WARMUP", "1") != "0"
-        self._held = None
+        hold = os.environ.get("MIHVD_GRAPH_HOLD_ACCUMULATORS", "1") != "0"
+        self.accumulators = []
         with torch.cuda.stream(side):  # warm-up on a side stream, as graph capture of autograd requires
-            for _ in range(warmup):
+            for i in range(warmup):
                 out = step_fn()
-                if hold:
-                    _readback(out)
-                    self._held = out
-                else:
-                    _detach(out)  # drop the autograd graph: no AccumulateGrad node outlives its step
+                if hold and i == warmup - 1:
+                    self.accumulators = accumulate_grad_nodes(out)
+                _detach(out)
                 del out
                 if sync_warmup:
-                    # each warm-up step completes before the next is issued (scripts/bert_graph_bisect.py:
-                    # variant H vs C)
-                    side.synchronize()
+                    side.synchronize()  # each warm-up step completes before the next is issued
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool):
+        # captured on the warm-up stream: the held nodes' stream is the capture stream, so autograd
+        # accumulates without a cross-stream hand-off (and without its stream-mismatch warning)
+        with torch.cuda.graph(self.graph, pool=pool, stream=side):
             self.output = _detach(step_fn())
         self.replays = 0
 
@@ -84,17 +89,35 @@ class CapturedStep:
         return self.graph.pool()
 
 
-def _readback(out):
-    """Copy one element of the first tensor in ``out`` to the host (synchronising its stream)."""
-    if torch.is_tensor(out):
-        if out.numel():
-            out.detach().reshape(-1)[:1].cpu()
-        return True
-    if isinstance(out, (list, tuple)):
-        return any(_readback(o) for o in out)
-    if isinstance(out, dict):
-        return any(_readback(o) for o in out.values())
-    return False
+def accumulate_grad_nodes(out):
+    """Every ``AccumulateGrad`` node reachable from the autograd graph of the tensors in ``out``
+    (a tensor, or a list / tuple / dict of them). The graph's saved tensors may already be freed
+    (after ``backward()``): only the node objects are walked."""
+    stack, seen, found, alive = [], set(), [], []
+
+    def roots(o):
+        if torch.is_tensor(o):
+            if o.grad_fn is not None:
+                stack.append(o.grad_fn)
+        elif isinstance(o, (list, tuple)):
+            for x in o:
+                roots(x)
+        elif isinstance(o, dict):
+            for x in o.values():
+                roots(x)
+
+    roots(out)
+    while stack:
+        fn = stack.pop()
+        if fn is None or id(fn) in seen:
+            continue
+        seen.add(id(fn))
+        alive.append(fn)  # keeps the wrapper alive: a freed wrapper's id() can be reused by the next one
+        if hasattr(fn, "variable"):  # torch::autograd::AccumulateGrad
+            found.append(fn)
+        for nxt, _ in fn.next_functions:
+            stack.append(nxt)
+    return found
 
 
 def _detach(out):

@@ -133,7 +133,7 @@ def main():
         "conv2_bwd [wgrad blocks in launch order]": ({"MIHVD_F32_C2B_XCD": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only, launch order]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_XCD": "0"},
                                                      ks["conv2_bwd"]),
-        "fc1_bwd+W3 adam [p/m/v 2 chunks ahead]": ({"MIHVD_F32_F1R_PD": "2"}, ks["fc1_bwd+W3 adam"]),
+        "fc1_bwd+W3 adam [p/m/v 4 chunks ahead]": ({"MIHVD_F32_F1R_PD": "4"}, ks["fc1_bwd+W3 adam"]),
         "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
@@ -170,7 +170,7 @@ def main():
         "whole step [conv2_fwd W2 after a full barrier]": ({}, {"MIHVD_F32_C2F_PREW": "0"}),
         "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
         "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
-        "whole step [fc1_bwd p/m/v 2 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "2"}),
+        "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
     }
     for name, (attrs, env) in steps.items():
         old_attr = {k: getattr(tr, k) for k in attrs}

@@ -12,6 +12,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
@@ -80,6 +81,33 @@ def main():
                         (0, 4, "block total")]:
         d = f[:, b] - f[:, a]
         print(f"    {label:14s} median {d.median():8.0f}  max {d.max():8.0f}")
+
+    # fc1_bwd row form with the fused dense/kernel Adam (as the trainer runs it at world size 1)
+    from mihvd.models.fused_mnist import FLAT_NUMEL, W3_START
+
+    G = tr.gview
+    s3 = slice(W3_START, FLAT_NUMEL)
+    m3, v3 = tr.m[s3], tr.v[s3]
+    w3 = P("dense/kernel")
+    run1 = lambda: o.f32_fc1_bwd(tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"),
+                                 G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), m3, v3, st, 0.0, 0.9,
+                                 0.999, tr.eps, 1.0, tr.rule, False)
+    run1()
+    torch.cuda.synchronize()
+    buf = o.f32_stamps_enable(196, 2)
+    run1()
+    torch.cuda.synchronize()
+    f = buf.view(-1, 16).cpu().double()
+    o.f32_stamps_enable(0, 2)
+    print("fc1_bwd rows (+W3 Adam): 196 blocks")
+    marks = [(0, 1, "chunk 0")] + [(c, c + 1, f"chunk {c}") for c in range(1, 8)] + [(8, 9, "exchange"),
+                                                                                    (9, 10, "epilogue"),
+                                                                                    (0, 10, "block total")]
+    for a, b, label in marks:
+        d = f[:, b] - f[:, a]
+        print(f"    {label:14s} median {d.median():8.0f}  max {d.max():8.0f}")
+    st0 = f[:, 0] - f[:, 0].min()
+    print(f"    start offset   median {st0.median():8.0f}  max {st0.max():8.0f}")
 
 
 if __name__ == "__main__":

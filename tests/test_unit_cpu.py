@@ -763,3 +763,23 @@ def test_native_engine_wrapper_routing():
     eng.flush()
     assert sorted(eng._o.waited) == [1, 2] and not eng._outstanding
     assert eng.collective("x", "broadcast", "sig", lambda: "launched") == "launched"
+
+
+def test_captured_step_holds_the_parameters_accumulate_grad_nodes():
+    """mihvd.graphs.accumulate_grad_nodes finds one AccumulateGrad node per parameter behind a
+    loss whose backward already ran, and holding them keeps autograd from building new ones for the
+    next forward (the capture): the node the next step uses is the held one (CapturedStep's fix of
+    the BERT-base capture NaN, scripts/bert_graph_bisect.py variant A0)."""
+    from mihvd.graphs import accumulate_grad_nodes
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.GELU(), torch.nn.Linear(16, 4))
+    loss = m(torch.randn(5, 8)).square().mean()
+    loss.backward()
+    nodes = accumulate_grad_nodes({"loss": loss, "aux": [loss * 2]})
+    assert len(nodes) == len(list(m.parameters()))
+    assert {id(n.variable) for n in nodes} == {id(p) for p in m.parameters()}
+    del loss
+    loss2 = m(torch.randn(5, 8)).sum()
+    used = {id(n) for n in accumulate_grad_nodes(loss2)}
+    assert used == {id(n) for n in nodes}  # the held nodes, not new ones
