@@ -69,9 +69,10 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        # captured on the warm-up stream: the held nodes' stream is the capture stream, so autograd
-        # accumulates without a cross-stream hand-off (and without its stream-mismatch warning)
-        with torch.cuda.graph(self.graph, pool=pool, stream=side):
+        # captured on torch's capture stream, not on `side`: the held nodes then accumulate on their
+        # own stream behind an event, which replays correctly; capturing on `side` itself (variant AR
+        # of scripts/bert_graph_bisect.py) fails like freshly created nodes do
+        with torch.cuda.graph(self.graph, pool=pool):
             self.output = _detach(step_fn())
         self.replays = 0
 
