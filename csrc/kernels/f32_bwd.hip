@@ -668,16 +668,23 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
 // ------------------------------------------------------------------------------------------ //
 constexpr int CBF_PS = 68, CBF_RS = 18 * CBF_PS, CBF_MAXR = 18;
 constexpr int CBF_IMG = CBF_MAXR * CBF_RS;            // floats: tall padded dY2 rows
+// one-round form (two tap-loop passes per dgrad block, twice the tiles): rows of up to 10 tiles
+constexpr int CBF_MAXR2 = 22, CBF_IMG2 = CBF_MAXR2 * CBF_RS;
+constexpr int cbf_maxr(int npass) { return npass == 2 ? CBF_MAXR2 : CBF_MAXR; }
+constexpr int cbf_img(int npass) { return cbf_maxr(npass) * CBF_RS; }
 constexpr int CBF_XIM = 2 * 1024;                     // two padded x images [32][32]
 constexpr int CBF_PW = 8 * 2 * 64 * 4;                // per-wave conv1 partials (MEPI: 2 f32x4 per lane)
 constexpr int CBF_LDS_DG = (CBF_IMG + CBF_XIM + CBF_PW) * 4;               // 109,632 B
 constexpr int CBF_A1S = 14 * 18 * 32, CBF_DYS = 196 * 32, CBF_WBUF = CBF_A1S + CBF_DYS;
 constexpr int CBF_LDS_WG = 2 * CBF_WBUF * 4;                                // 114,688 B
 constexpr int CBF_LDS = CBF_LDS_DG > CBF_LDS_WG ? CBF_LDS_DG : CBF_LDS_WG;
-constexpr int CBF_MAXCH = (CBF_MAXR * 18 * 16 + 511) / 512;                 // dY2 chunks per thread
+constexpr int CBF_LDS_DG2 = (CBF_IMG2 + CBF_XIM + CBF_PW) * 4;             // 123,008 B
+constexpr int CBF_LDS2 = CBF_LDS_DG2 > CBF_LDS_WG ? CBF_LDS_DG2 : CBF_LDS_WG;
 constexpr int CBF_IG = 4;                                                   // images per wgrad block
+constexpr int CBF_IG2 = 8;                                                  // ... in the one-round form
 constexpr int CP_F32 = 832;                                                 // [dW1 (800) | db1 (32)]
-static_assert(CBF_LDS <= 163840, "f32_conv2_bwd LDS");
+static_assert(CBF_LDS <= 163840 && CBF_LDS2 <= 163840, "f32_conv2_bwd LDS");
+static_assert(4 * 2 * 10 * 64 * 16 <= CBF_IMG2 * 4, "one-round dgrad partial exchange fits the dY2 image");
 static_assert(8 * 26 * 16 <= CBF_PW, "the VALU conv1-wgrad epilogue's partials fit");
 static_assert(4 * 2 * 7 * 64 * 16 <= CBF_IMG * 4, "dgrad partial exchange fits the dY2 image");
 static_assert(4 * 5 * 4 * 64 * 16 <= CBF_LDS_WG, "wgrad partial exchange fits the staging buffers");
@@ -703,13 +710,19 @@ __device__ __forceinline__ void lds_barrier() {
 // staging writes wait only for their own loads), and the barrier orders LDS alone: the 25 W2 loads
 // per lane (200 KB per block from L2) land while the dY2 image is staged instead of after it.
 // MEPI: the conv1 weight gradient of the epilogue on MFMA instead of VALU (see step 3 below).
-template <int TPB, bool PREW, bool MEPI>
+// NPASS = 2 (the one-round form): TPB tiles in two tap-loop passes of TPB / 2 over the same
+// register-resident W2 (the A register sets are reused, the accumulators of both passes live on),
+// so a block loads W2 once for twice the tiles and the halo rows are staged once for both.
+template <int TPB, bool PREW, bool MEPI, int NPASS = 1>
 __device__ __forceinline__ void f32_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf) {
+  static_assert(TPB % NPASS == 0, "tiles split evenly over the passes");
+  constexpr int TP = TPB / NPASS;                                        // tiles per pass
+  constexpr int MAXCH = (cbf_maxr(NPASS) * 18 * 16 + 511) / 512;         // dY2 chunks per thread
   float* dimg = smf;
-  float* xim = smf + CBF_IMG;
+  float* xim = smf + cbf_img(NPASS);
   float* pw = xim + CBF_XIM;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int np = 196 * B, T0 = bid * TPB;
@@ -719,9 +732,9 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   const int nch = (R1 - R0) * 288;  // 18 pixels x 16 float4
   const int nt = wave & 1, cq = wave >> 1;
   // 1. loads: the first two taps' weight fragments, the dY2 rows, the (at most two) x images
-  float4 iv[CBF_MAXCH];
+  float4 iv[MAXCH];
 #pragma unroll
-  for (int it = 0; it < CBF_MAXCH; ++it) {
+  for (int it = 0; it < MAXCH; ++it) {
     const int i = min(t + 512 * it, nch - 1);
     const int rr = i / 288, rem = i - rr * 288, c = rem >> 4, ch = rem & 15;
     const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
@@ -731,7 +744,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     iv[it] = mask_f4(v, in);
   }
 #pragma unroll
-  for (int it = 0; it < CBF_MAXCH; ++it) {
+  for (int it = 0; it < MAXCH; ++it) {
     const int i = t + 512 * it;
     if (i < nch) {
       const int rr = i / 288, rem = i - rr * 288;
@@ -806,38 +819,43 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   // Software pipeline, fully unrolled: the A chunks of tap t + 1 are read into the other register
   // set before tap t's MFMAs issue; sched_barrier pins that order (left alone, the scheduler
   // reuses one register set and waits on each read right before its MFMAs).
-  float4 ra[TPB], rb[TPB];
-  auto load_a = [&](float4 (&a)[TPB], int tap) {
-    const int kh = tap / 5, kw = tap - 5 * kh;
-    const int aoff = ((4 - kh) * 18 + (4 - kw)) * CBF_PS;
+  float4 ra[TP], rb[TP];
+  auto run_pass = [&](auto i0c) {
+    constexpr int I0 = decltype(i0c)::value;  // first tile of the pass
+    auto load_a = [&](float4 (&a)[TP], int tap) {
+      const int kh = tap / 5, kw = tap - 5 * kh;
+      const int aoff = ((4 - kh) * 18 + (4 - kw)) * CBF_PS;
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) a[i] = *reinterpret_cast<const float4*>(dimg + abase[i] + aoff);
-  };
-  auto mfma_tap = [&](const float4 (&a)[TPB], const float4& w) {
-    // k-element j outer, tiles inner: consecutive MFMAs use different accumulators
+      for (int i = 0; i < TP; ++i) a[i] = *reinterpret_cast<const float4*>(dimg + abase[I0 + i] + aoff);
+    };
+    auto mfma_tap = [&](const float4 (&a)[TP], const float4& w) {
+      // k-element j outer, tiles inner: consecutive MFMAs use different accumulators
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].x, w.x, acc[i]);
+      for (int i = 0; i < TP; ++i) acc[I0 + i] = mfma4(a[i].x, w.x, acc[I0 + i]);
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].y, w.y, acc[i]);
+      for (int i = 0; i < TP; ++i) acc[I0 + i] = mfma4(a[i].y, w.y, acc[I0 + i]);
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].z, w.z, acc[i]);
+      for (int i = 0; i < TP; ++i) acc[I0 + i] = mfma4(a[i].z, w.z, acc[I0 + i]);
 #pragma unroll
-    for (int i = 0; i < TPB; ++i) acc[i] = mfma4(a[i].w, w.w, acc[i]);
-  };
-  load_a(ra, 0);
+      for (int i = 0; i < TP; ++i) acc[I0 + i] = mfma4(a[i].w, w.w, acc[I0 + i]);
+    };
+    load_a(ra, 0);
 #pragma unroll
-  for (int tap = 0; tap < 25; tap += 2) {
-    if (tap + 1 < 25) load_a(rb, tap + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_tap(ra, wb[tap]);
-    __builtin_amdgcn_sched_barrier(0);
-    if (tap + 1 < 25) {
-      if (tap + 2 < 25) load_a(ra, tap + 2);
+    for (int tap = 0; tap < 25; tap += 2) {
+      if (tap + 1 < 25) load_a(rb, tap + 1);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_tap(rb, wb[tap + 1]);
+      mfma_tap(ra, wb[tap]);
       __builtin_amdgcn_sched_barrier(0);
+      if (tap + 1 < 25) {
+        if (tap + 2 < 25) load_a(ra, tap + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_tap(rb, wb[tap + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-  }
+  };
+  run_pass(std::integral_constant<int, 0>{});
+  if constexpr (NPASS == 2) run_pass(std::integral_constant<int, TP>{});
 #pragma unroll
   for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
   c2b_stamp(2);
@@ -981,10 +999,10 @@ __device__ __forceinline__ int xcd_contiguous(int g, int lo, int hi) {
 
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
-                                                      float* smf) {
+                                                      int ig, float* smf) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, l32 = lane & 31, hh = lane >> 5;
   const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
-  const int img0 = CBF_IG * grp, nimg = min(CBF_IG, B - img0);
+  const int img0 = ig * grp, nimg = min(ig, B - img0);
   auto load_img = [&](int b, float4 (&v)[7]) {
 #pragma unroll
     for (int it = 0; it < 7; ++it) {
@@ -1097,21 +1115,21 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   c2b_stamp(6);
 }
 
-template <int TPB, bool PREW, bool MEPI>
+template <int TPB, bool PREW, bool MEPI, int NPASS = 1>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg) {
+    int n_wg, int ig) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
   if (bid < n_dg) {
-    f32_conv2_dgrad_block<TPB, PREW, MEPI>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
+    f32_conv2_dgrad_block<TPB, PREW, MEPI, NPASS>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
     return;
   }
   // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
-  f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, smf);
+  f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, smf);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1329,13 +1347,25 @@ at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel) {
 }
 
 int64_t f32_db2_rows(int64_t B) { return 49 * ((B + 15) / 16); }
-int64_t f32_wgrad_groups(int64_t B) { return (B + CBF_IG - 1) / CBF_IG; }
 static int conv2b_tpb(int B) {
   const int nt = (196 * B + 15) / 16;
   return std::min(7, std::max(1, (nt + 255) / 256));
 }
+// One-round form (MIHVD_F32_C2B_R1, default on where it applies): dgrad blocks of twice the tiles
+// in two tap-loop passes and wgrad blocks of twice the images, so both roles fit the CUs in one
+// round (B = 100: 123 + 130 = 253 blocks) instead of two (245 + 250): W2 is loaded once per two
+// passes, the halo rows are staged once for twice the pixels, and no block starts behind another.
+static bool conv2b_one_round(int B) {
+  return env_knob("MIHVD_F32_C2B_R1", 1) != 0 && 2 * conv2b_tpb(B) <= 10;
+}
+static int conv2b_block_tiles(int B) { return conv2b_one_round(B) ? 2 * conv2b_tpb(B) : conv2b_tpb(B); }
+static int conv2b_images(int B) { return conv2b_one_round(B) ? CBF_IG2 : CBF_IG; }
+int64_t f32_wgrad_groups(int64_t B) {
+  const int ig = conv2b_images((int)B);
+  return (B + ig - 1) / ig;
+}
 int64_t f32_dgrad_blocks(int64_t B) {
-  const int tpb = conv2b_tpb((int)B), nt = (196 * (int)B + 15) / 16;
+  const int tpb = conv2b_block_tiles((int)B), nt = (196 * (int)B + 15) / 16;
   return (nt + tpb - 1) / tpb;
 }
 
@@ -1463,7 +1493,9 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   chk_f32(a1, (int64_t)B * 6272, "f32_conv2_bwd: a1");
   TORCH_CHECK(idx1.dtype() == at::kByte && idx1.numel() == (int64_t)B * 6272 && idx1.is_contiguous(), "f32_conv2_bwd: idx1");
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv2_bwd: x");
-  const int n_dg = (int)f32_dgrad_blocks(B), tpb = conv2b_tpb(B);
+  const bool r1 = conv2b_one_round(B);
+  const int n_dg = (int)f32_dgrad_blocks(B), tpb = conv2b_block_tiles(B), ig = conv2b_images(B);
+  const int maxr = r1 ? CBF_MAXR2 : CBF_MAXR;
   chk_f32(cpart, (int64_t)n_dg * CP_F32, "f32_conv2_bwd: cpart [dgrad blocks][832]");
   const int ngrp = (int)f32_wgrad_groups(B);
   chk_f32(slab, (int64_t)ngrp * 51200, "f32_conv2_bwd: slab [groups][51200]");
@@ -1480,13 +1512,13 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   for (int blk = 0; blk < n_dg; ++blk) {
     const int P0 = 16 * blk * tpb, P1 = std::min(16 * (blk + 1) * tpb, 196 * B) - 1;
     const int r0 = 18 * (P0 / 196) + (P0 % 196) / 14, r1 = 18 * (P1 / 196) + (P1 % 196) / 14 + 5;
-    TORCH_CHECK(r1 - r0 <= CBF_MAXR && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS image");
+    TORCH_CHECK(r1 - r0 <= maxr && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS image");
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
   // study knobs: MIHVD_F32_C2B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only (the other role's
   // outputs are then stale); MIHVD_F32_C2B_LDS requests more dynamic LDS than the roles need
   const int role = env_knob("MIHVD_F32_C2B_ROLE", 0);
-  const int lds = std::max(CBF_LDS, std::min(env_knob("MIHVD_F32_C2B_LDS", 0), 163840));
+  const int lds = std::max(r1 ? CBF_LDS2 : CBF_LDS, std::min(env_knob("MIHVD_F32_C2B_LDS", 0), 163840));
   const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
   const int ndg_arg = role == 2 ? 0 : n_dg;
   const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
@@ -1494,13 +1526,23 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
-                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg);
+                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig);
   };
   // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
   // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA
   const bool prew = env_knob("MIHVD_F32_C2B_PREW", 1) != 0;
   // (MFMA form measured slower: 52.5 vs 51.1 us, dgrad role 28.9 vs 27.8 us, profiles/r04/kbench_f32_r04d.txt)
   const bool mepi = env_knob("MIHVD_F32_C2B_MEPI", 0) != 0;
+  if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes (PREW, VALU epilogue)
+    switch (tpb) {
+      case 2: launch(f32_conv2_bwd_kernel<2, true, false, 2>); break;
+      case 4: launch(f32_conv2_bwd_kernel<4, true, false, 2>); break;
+      case 6: launch(f32_conv2_bwd_kernel<6, true, false, 2>); break;
+      case 8: launch(f32_conv2_bwd_kernel<8, true, false, 2>); break;
+      default: launch(f32_conv2_bwd_kernel<10, true, false, 2>); break;
+    }
+    return;
+  }
 #define C2B_CASE(T)                                                                          \
   case T:                                                                                    \
     if (mepi) launch(f32_conv2_bwd_kernel<T, true, true>);                                   \

@@ -115,6 +115,15 @@ def main():
             for k in study_env.get(variant, {}):
                 os.environ.pop(k, None)
         return
+    two = {}
+
+    def c2b_two_round():  # its own cpart / slab, sized for the two-round launch (read under the env)
+        key = (int(o.f32_dgrad_blocks(B)), int(o.f32_wgrad_groups(B)))
+        if key not in two:
+            two[key] = (torch.empty(key[0], 832, device="cuda"), torch.empty(key[1], 51200, device="cuda"))
+        cp, sl = two[key]
+        o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, cp, sl)
+
     res = {}
     for name, fn in ks.items():
         res[name] = timed(fn, args.reps)
@@ -131,6 +140,11 @@ def main():
         "conv2_bwd [dgrad role only, MFMA epilogue]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_MEPI": "1"},
                                                      ks["conv2_bwd"]),
         "conv2_bwd [wgrad blocks in launch order]": ({"MIHVD_F32_C2B_XCD": "0"}, ks["conv2_bwd"]),
+        "conv2_bwd [two-round form]": ({"MIHVD_F32_C2B_R1": "0"}, c2b_two_round),
+        "conv2_bwd [two-round form, dgrad role only]": ({"MIHVD_F32_C2B_R1": "0", "MIHVD_F32_C2B_ROLE": "1"},
+                                                      c2b_two_round),
+        "conv2_bwd [two-round form, wgrad role only]": ({"MIHVD_F32_C2B_R1": "0", "MIHVD_F32_C2B_ROLE": "2"},
+                                                      c2b_two_round),
         "conv2_bwd [wgrad role only, launch order]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_XCD": "0"},
                                                      ks["conv2_bwd"]),
         "fc1_bwd+W3 adam [p/m/v 4 chunks ahead]": ({"MIHVD_F32_F1R_PD": "4"}, ks["fc1_bwd+W3 adam"]),
