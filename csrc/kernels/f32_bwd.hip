@@ -580,18 +580,10 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     lds_wave_fence();
     const int s3 = c % NS;
     const float4 p = pv[s3];
-    // Every LDS operand of the chunk is read first (the dgrad B fragments, then the wgrad A
-    // operands, which land while the dgrad MFMAs issue); sched_barrier pins the order. Left to
-    // itself the scheduler interleaved each read with its MFMAs, waited lgkmcnt(0) every two tiles
-    // and chained the four k-steps of one tile back to back (dependent MFMAs, s_nop padding).
+    // dgrad: G tiles of 16 samples, the four k elements of the chunk outer (independent accumulators)
     float4 zb[G];
 #pragma unroll
     for (int u = 0; u < G; ++u) zb[u] = *reinterpret_cast<const float4*>(buf + (16 * u + lr) * 16 + 4 * lg);
-    float zw[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) zw[s] = buf[(4 * s + lg) * 16 + lr];
-    __builtin_amdgcn_sched_barrier(0);
-    // dgrad: G tiles of 16 samples, the four k elements of the chunk outer (independent accumulators)
 #pragma unroll
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.x, zb[u].x, acc[u]);
 #pragma unroll
@@ -600,15 +592,20 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.z, zb[u].z, acc[u]);
 #pragma unroll
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.w, zb[u].w, acc[u]);
-    __builtin_amdgcn_sched_barrier(0);
-    // wgrad: dW3[f0 + lr][nn + 4 lg + i] over the batch, four accumulator chains (dependent MFMAs
-    // four issues apart: 128 cycles against the ~40-cycle result latency)
-    f32x4 wc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
-                   f32x4{0.f, 0.f, 0.f, 0.f}};
+    // wgrad: dW3[f0 + lr][nn + 4 lg + i] over the batch, two alternating accumulators. (Reading every
+    // LDS operand of the chunk ahead of its MFMAs with the order pinned by sched_barrier, and four
+    // wgrad chains, was measured slower: 33.6 vs 27.7 us with the fused Adam, 27.5 vs 22.9 without,
+    // profiles/r04/kbench_f32_r04g.txt; the pinned order keeps the global loads and the Adam VALU
+    // work from interleaving with the MFMAs)
+    f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) wc[s & 3] = mfma4(zw[s], a2r[s], wc[s & 3]);
-    __builtin_amdgcn_sched_barrier(0);
-    const f32x4 g = (wc[0] + wc[1]) + (wc[2] + wc[3]);
+    for (int s = 0; s < KS; s += 2) {
+      const float z0 = buf[(4 * s + lg) * 16 + lr];
+      const float z1 = buf[(4 * s + 4 + lg) * 16 + lr];
+      w0 = mfma4(z0, a2r[s], w0);
+      w1 = mfma4(z1, a2r[s + 1], w1);
+    }
+    const f32x4 g = w0 + w1;
     const int64_t o = rowo + 16 * c;
     float4 gg = make_float4(g[0], g[1], g[2], g[3]);
     if constexpr (STORE) *reinterpret_cast<float4*>(gW3 + o) = gg;

@@ -44,6 +44,13 @@ class CapturedStep:
     profiles/r04/bert_graph_bisect_*.log). Holding the nodes costs no activation memory: a leaf's
     node references the parameter, not the step's tensors. ``MIHVD_GRAPH_HOLD_ACCUMULATORS=0``
     restores the failing form for study.
+
+    What the bisection pins down: the failing captures accumulate each bias gradient (a bf16 sum
+    over the batch, cast to fp32) on the stream that produced it; every passing form hands it to an
+    AccumulateGrad on another stream behind an event (A0) or has no cast node on the bias path (F0,
+    bias added in fp32). Nothing runs eagerly during the capture and no ``.grad`` tensor is swapped
+    for another (both checked per parameter), so the stale read is inside the graph's own replay of
+    autograd's same-stream accumulation path.
     """
 
     def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False, sync_warmup: bool = False):
@@ -69,11 +76,17 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        # captured on torch's capture stream, not on `side`: the held nodes then accumulate on their
+        # Captured on torch's capture stream, not on `side`: the held nodes then accumulate on their
         # own stream behind an event, which replays correctly; capturing on `side` itself (variant AR
-        # of scripts/bert_graph_bisect.py) fails like freshly created nodes do
-        with torch.cuda.graph(self.graph, pool=pool):
-            self.output = _detach(step_fn())
+        # of scripts/bert_graph_bisect.py) fails like freshly created nodes do. That stream mismatch
+        # is the point, so autograd's warning about it is switched off for the capture.
+        warn = _stream_mismatch_warning(False) if self.accumulators else None
+        try:
+            with torch.cuda.graph(self.graph, pool=pool):
+                self.output = _detach(step_fn())
+        finally:
+            if warn is not None:
+                _stream_mismatch_warning(warn)
         self.replays = 0
 
     def __call__(self):
@@ -88,6 +101,17 @@ class CapturedStep:
 
     def pool(self):
         return self.graph.pool()
+
+
+def _stream_mismatch_warning(on: bool):
+    """Set autograd's AccumulateGrad stream-mismatch warning; returns the previous setting."""
+    g = torch.autograd.graph
+    if not hasattr(g, "set_warn_on_accumulate_grad_stream_mismatch"):
+        return None
+    prev = bool(torch._C._warn_on_accumulate_grad_stream_mismatch()) if hasattr(
+        torch._C, "_warn_on_accumulate_grad_stream_mismatch") else True
+    g.set_warn_on_accumulate_grad_stream_mismatch(bool(on))
+    return prev
 
 
 def accumulate_grad_nodes(out):
