@@ -784,20 +784,26 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched.
   // VALU form: (nt, tile) pairs p = wave + 8k, lane pixel 4 lg + r. MEPI form: the wave's pixel
   // groups 4 cq + r of every tile, the same pixel on the four lane groups (channel 16 nt + lr).
+  // LATE (MEPI in the two-pass form): loaded after the tap loops instead (TPB x 4 x 2 registers
+  // would not fit beside the W2 operand); one exposed latency, then the short MFMA epilogue.
   constexpr int NP = MEPI ? TPB : (2 * TPB + 7) / 8;
+  constexpr bool LATE = MEPI && NPASS == 2;
   float ea[NP][4];
   int ex[NP][4];
+  auto load_epi = [&]() {
 #pragma unroll
-  for (int k = 0; k < NP; ++k)
+    for (int k = 0; k < NP; ++k)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int pp = wave + 8 * k;
-      const int P = MEPI ? 16 * (T0 + k) + 4 * cq + r : 16 * (T0 + (pp >> 1)) + 4 * lg + r;
-      const bool ok = (MEPI || pp < 2 * TPB) && P < np;
-      const int64_t o = (int64_t)min(P, np - 1) * 32 + 16 * nt + lr;
-      ea[k][r] = mask_f(a1[o], ok);
-      ex[k][r] = idx1[o];
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int pp = wave + 8 * k;
+        const int P = MEPI ? 16 * (T0 + k) + 4 * cq + r : 16 * (T0 + (pp >> 1)) + 4 * lg + r;
+        const bool ok = (MEPI || pp < 2 * TPB) && P < np;
+        const int64_t o = (int64_t)min(P, np - 1) * 32 + 16 * nt + lr;
+        ea[k][r] = mask_f(a1[o], ok);
+        ex[k][r] = idx1[o];
+      }
+  };
+  if constexpr (!LATE) load_epi();
   // the x patches are needed only by the epilogue: their gather (state -> rows -> x, three
   // dependent loads) is issued here and lands during the tap loop instead of before the barrier
   float xv[4];
@@ -861,6 +867,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   c2b_stamp(7);
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
+  if constexpr (LATE) load_epi();  // in flight while the partials are exchanged
 #pragma unroll
   for (int i = 0; i < TPB; ++i) red[((cq * 2 + nt) * TPB + i) * 64 + lane] = acc[i];
   __syncthreads();
@@ -1530,14 +1537,20 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const bool prew = env_knob("MIHVD_F32_C2B_PREW", 1) != 0;
   // (MFMA form measured slower: 52.5 vs 51.1 us, dgrad role 28.9 vs 27.8 us, profiles/r04/kbench_f32_r04d.txt)
   const bool mepi = env_knob("MIHVD_F32_C2B_MEPI", 0) != 0;
-  if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes (PREW, VALU epilogue)
+  if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes (PREW; epilogue per MIHVD_F32_C2B_MEPI)
+#define C2B_R1(T)                                                                                        \
+  case T:                                                                                                \
+    mepi ? launch(f32_conv2_bwd_kernel<T, true, true, 2>) : launch(f32_conv2_bwd_kernel<T, true, false, 2>); \
+    break;
     switch (tpb) {
-      case 2: launch(f32_conv2_bwd_kernel<2, true, false, 2>); break;
-      case 4: launch(f32_conv2_bwd_kernel<4, true, false, 2>); break;
-      case 6: launch(f32_conv2_bwd_kernel<6, true, false, 2>); break;
-      case 8: launch(f32_conv2_bwd_kernel<8, true, false, 2>); break;
-      default: launch(f32_conv2_bwd_kernel<10, true, false, 2>); break;
+      C2B_R1(2)
+      C2B_R1(4)
+      C2B_R1(6)
+      C2B_R1(8)
+      default:
+        C2B_R1(10)
     }
+#undef C2B_R1
     return;
   }
 #define C2B_CASE(T)                                                                          \
