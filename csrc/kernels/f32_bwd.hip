@@ -1003,7 +1003,7 @@ __device__ __forceinline__ int xcd_contiguous(int g, int lo, int hi) {
 
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
-                                                      int ig, float* smf) {
+                                                      int ig, int wmid, float* smf) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, l32 = lane & 31, hh = lane >> 5;
   const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
   const int img0 = ig * grp, nimg = min(ig, B - img0);
@@ -1058,6 +1058,10 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
 #pragma unroll
       for (int kw = 0; kw < 5; ++kw) b[kw] = bp[kw * 32];
     };
+    // wmid: the next image's LDS stores are issued halfway through this image's steps (the other
+    // buffer is free since the last barrier) instead of after them, so the store pass overlaps
+    // MFMAs and each image ends with the barrier alone
+    const bool nxt = n + 1 < nimg;
     load_step(0, opa[0], opb[0]);
 #pragma unroll
     for (int u = 0; u < 13; ++u) {
@@ -1069,8 +1073,9 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
         for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(opa[cur], opb[cur][kw], acc[kw]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (u == 6 && wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     }
-    if (n + 1 < nimg) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
+    if (!wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
   }
   c2b_stamp(5);
@@ -1124,7 +1129,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg, int ig) {
+    int n_wg, int ig, int wmid) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
@@ -1133,7 +1138,8 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     return;
   }
   // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
-  f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, smf);
+  f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, wmid,
+                        smf);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1526,11 +1532,13 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
   const int ndg_arg = role == 2 ? 0 : n_dg;
   const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
+  const int wmid = env_knob("MIHVD_F32_C2B_WMID", 1) != 0;  // 0: next image stored after the steps
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
-                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig);
+                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig,
+                                     wmid);
   };
   // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
   // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA

@@ -140,6 +140,9 @@ def main():
         "conv2_bwd [dgrad role only, MFMA epilogue]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_MEPI": "1"},
                                                      ks["conv2_bwd"]),
         "conv2_bwd [wgrad blocks in launch order]": ({"MIHVD_F32_C2B_XCD": "0"}, ks["conv2_bwd"]),
+        "conv2_bwd [wgrad next image stored after the steps]": ({"MIHVD_F32_C2B_WMID": "0"}, ks["conv2_bwd"]),
+        "conv2_bwd [wgrad role only, stored after the steps]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "0"},
+                                                               ks["conv2_bwd"]),
         "conv2_bwd [two-round form]": ({"MIHVD_F32_C2B_R1": "0"}, c2b_two_round),
         "conv2_bwd [two-round form, dgrad role only]": ({"MIHVD_F32_C2B_R1": "0", "MIHVD_F32_C2B_ROLE": "1"},
                                                       c2b_two_round),
