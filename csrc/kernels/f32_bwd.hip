@@ -886,26 +886,39 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     }
     const float one1 = lr == 9 ? 1.f : 0.f;  // column 25 = db1
     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-    for (int k = 0; k < TPB; ++k) {
+    // Software pipeline over the tiles: tile k + 1's eight x operands (four pixels x two taps) and
+    // its routed-gradient A values are read / formed before tile k's eight MFMAs issue (a serial
+    // read -> MFMA chain per pixel left the LDS latency exposed 4 TPB times per wave).
+    const int li = lr + 16 * cq;
+    float xa[2][4], xb[2][4], av[2][4];
+    auto prep = [&](int k, float (&x0)[4], float (&x1)[4], float (&a)[4]) {
       // the four co-quarter partials of this pixel group (lane lr + 16 cq of the reduction layout)
-      const int li = lr + 16 * cq;
-      const f32x4 s = ((red[((0 * 2 + nt) * TPB + k) * 64 + li] + red[((1 * 2 + nt) * TPB + k) * 64 + li]) +
-                       red[((2 * 2 + nt) * TPB + k) * 64 + li]) +
-                      red[((3 * 2 + nt) * TPB + k) * 64 + li];
+      const f32x4 sk = ((red[((0 * 2 + nt) * TPB + k) * 64 + li] + red[((1 * 2 + nt) * TPB + k) * 64 + li]) +
+                        red[((2 * 2 + nt) * TPB + k) * 64 + li]) +
+                       red[((3 * 2 + nt) * TPB + k) * 64 + li];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int P = 16 * (T0 + k) + 4 * cq + r;  // wave-uniform
-        if (P >= np) break;
+        const int P0r = 16 * (T0 + k) + 4 * cq + r, P = min(P0r, np - 1);  // wave-uniform
         const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
-        const float g = ea[k][r] > 0.f ? s[r] : 0.f;
-        const float a = ex[k][r] == lg ? g : 0.f;
+        const float g = ea[k][r] > 0.f ? sk[r] : 0.f;
+        a[r] = (P0r < np && ex[k][r] == lg) ? g : 0.f;
         const float* xs = xim + (bb - b0) * 1024 + (2 * py + (lg >> 1)) * 32 + 2 * px + (lg & 1);
-        const float x0 = xs[off0];
-        const float x1 = 16 + lr < 25 ? xs[off1] : one1;
-        c0 = mfma4(a, x0, c0);
-        c1 = mfma4(a, x1, c1);
+        x0[r] = xs[off0];
+        x1[r] = 16 + lr < 25 ? xs[off1] : one1;
       }
+    };
+    prep(0, xa[0], xb[0], av[0]);
+#pragma unroll
+    for (int k = 0; k < TPB; ++k) {
+      const int cur = k & 1;
+      if (k + 1 < TPB) prep(k + 1, xa[cur ^ 1], xb[cur ^ 1], av[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        c0 = mfma4(av[cur][r], xa[cur][r], c0);
+        c1 = mfma4(av[cur][r], xb[cur][r], c1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     // C[row = 4 lg + i][col = lr] = D[ci = 16 nt + 4 lg + i][tap = lr (c0) or 16 + lr (c1)]; the four
     // waves of a channel half sum through LDS (the dY2 image area is still being read: use pw)
