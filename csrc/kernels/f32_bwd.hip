@@ -512,7 +512,10 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
 // PD: how many chunks ahead p/m/v are loaded (ring of PD + 1 register slots). The loop's HBM
 // traffic (p, m, v in; p, m, v out: 75 MB per step) is bound by the bytes each CU keeps in flight;
 // PD = 2 keeps ~48 KB per CU, PD = 4 ~96 KB.
-template <int G, bool ADAM, bool STORE, int PD = 2>
+// PIN: the dgrad MFMAs of a chunk issue in the written order (k-element outer, tiles inner: dependent
+// MFMAs G issues apart), pinned by sched_barrier after their operand reads; left alone the scheduler
+// chains each tile's four k-steps back to back.
+template <int G, bool ADAM, bool STORE, int PD = 2, bool PIN = false>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
@@ -584,6 +587,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     float4 zb[G];
 #pragma unroll
     for (int u = 0; u < G; ++u) zb[u] = *reinterpret_cast<const float4*>(buf + (16 * u + lr) * 16 + 4 * lg);
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.x, zb[u].x, acc[u]);
 #pragma unroll
@@ -592,6 +596,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.z, zb[u].z, acc[u]);
 #pragma unroll
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.w, zb[u].w, acc[u]);
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
     // wgrad: dW3[f0 + lr][nn + 4 lg + i] over the batch, two alternating accumulators. (Reading every
     // LDS operand of the chunk ahead of its MFMAs with the order pinned by sched_barrier, and four
     // wgrad chains, was measured slower: 33.6 vs 27.7 us with the fused Adam, 27.5 vs 22.9 without,
@@ -663,27 +668,35 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
 // ------------------------------------------------------------------------------------------ //
 // f32_conv2_bwd (512-thread blocks)
 // ------------------------------------------------------------------------------------------ //
-constexpr int CBF_PS = 68, CBF_RS = 18 * CBF_PS, CBF_MAXR = 18;
+// Tall padded dY2 image: rows of CBF_RWD pixels (18 used: 2 + 14 + 2 padding columns) of CBF_PS
+// floats (64 channels + padding). 72 x 22 makes every ds_read_b128 of the tap loop conflict-free:
+// each 16-lane group (two 4-channel chunks x 8 consecutive output pixels) lands on 16 distinct
+// 16-byte slots for every tap and every row/image wrap of a tile (scripts/ldssim_conv2.py: 1.00
+// LDS cycles per group, against 2.70 for the 68 x 18 layout of round 3).
+constexpr int CBF_PS = 72, CBF_RWD = 22, CBF_RS = CBF_RWD * CBF_PS, CBF_MAXR = 16;
 constexpr int CBF_IMG = CBF_MAXR * CBF_RS;            // floats: tall padded dY2 rows
 // one-round form (two tap-loop passes per dgrad block, twice the tiles): rows of up to 10 tiles
-constexpr int CBF_MAXR2 = 22, CBF_IMG2 = CBF_MAXR2 * CBF_RS;
+constexpr int CBF_MAXR2 = 21, CBF_IMG2 = CBF_MAXR2 * CBF_RS;
 constexpr int cbf_maxr(int npass) { return npass == 2 ? CBF_MAXR2 : CBF_MAXR; }
 constexpr int cbf_img(int npass) { return cbf_maxr(npass) * CBF_RS; }
 constexpr int CBF_XIM = 2 * 1024;                     // two padded x images [32][32]
 constexpr int CBF_PW = 8 * 2 * 64 * 4;                // per-wave conv1 partials (MEPI: 2 f32x4 per lane)
-constexpr int CBF_LDS_DG = (CBF_IMG + CBF_XIM + CBF_PW) * 4;               // 109,632 B
+// The x images and the conv1 partials live in the dead image area behind the co-quarter partial
+// exchange (written after the tap loops' barrier): the image alone sets the dgrad LDS size.
+constexpr int cbf_red(int tpb) { return 4 * 2 * tpb * 64 * 4; }           // floats of the exchange
+constexpr int CBF_LDS_DG = CBF_IMG * 4;                                     // 101,376 B
 constexpr int CBF_A1S = 14 * 18 * 32, CBF_DYS = 196 * 32, CBF_WBUF = CBF_A1S + CBF_DYS;
 constexpr int CBF_LDS_WG = 2 * CBF_WBUF * 4;                                // 114,688 B
 constexpr int CBF_LDS = CBF_LDS_DG > CBF_LDS_WG ? CBF_LDS_DG : CBF_LDS_WG;
-constexpr int CBF_LDS_DG2 = (CBF_IMG2 + CBF_XIM + CBF_PW) * 4;             // 123,008 B
+constexpr int CBF_LDS_DG2 = CBF_IMG2 * 4;                                   // 133,056 B
 constexpr int CBF_LDS2 = CBF_LDS_DG2 > CBF_LDS_WG ? CBF_LDS_DG2 : CBF_LDS_WG;
 constexpr int CBF_IG = 4;                                                   // images per wgrad block
 constexpr int CBF_IG2 = 8;                                                  // ... in the one-round form
 constexpr int CP_F32 = 832;                                                 // [dW1 (800) | db1 (32)]
 static_assert(CBF_LDS <= 163840 && CBF_LDS2 <= 163840, "f32_conv2_bwd LDS");
-static_assert(4 * 2 * 10 * 64 * 16 <= CBF_IMG2 * 4, "one-round dgrad partial exchange fits the dY2 image");
+static_assert(cbf_red(10) + CBF_XIM + CBF_PW <= CBF_IMG2, "one-round dgrad exchange + x images + partials fit");
 static_assert(8 * 26 * 16 <= CBF_PW, "the VALU conv1-wgrad epilogue's partials fit");
-static_assert(4 * 2 * 7 * 64 * 16 <= CBF_IMG * 4, "dgrad partial exchange fits the dY2 image");
+static_assert(cbf_red(7) + CBF_XIM + CBF_PW <= CBF_IMG, "dgrad exchange + x images + partials fit the image");
 static_assert(4 * 5 * 4 * 64 * 16 <= CBF_LDS_WG, "wgrad partial exchange fits the staging buffers");
 
 // dgrad role. Pixels of the batch (flattened [B][196], raster order) in 16-pixel tiles; block owns
@@ -719,7 +732,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   constexpr int TP = TPB / NPASS;                                        // tiles per pass
   constexpr int MAXCH = (cbf_maxr(NPASS) * 18 * 16 + 511) / 512;         // dY2 chunks per thread
   float* dimg = smf;
-  float* xim = smf + cbf_img(NPASS);
+  float* xim = smf + cbf_red(TPB);  // behind the partial exchange, written after the tap loops
   float* pw = xim + CBF_XIM;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
   const int np = 196 * B, T0 = bid * TPB;
@@ -745,7 +758,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     const int i = t + 512 * it;
     if (i < nch) {
       const int rr = i / 288, rem = i - rr * 288;
-      *reinterpret_cast<float4*>(dimg + (rr * 18 + (rem >> 4)) * CBF_PS + (rem & 15) * 4) = iv[it];
+      *reinterpret_cast<float4*>(dimg + (rr * CBF_RWD + (rem >> 4)) * CBF_PS + (rem & 15) * 4) = iv[it];
     }
   }
   // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3].
@@ -764,7 +777,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   for (int i = 0; i < TPB; ++i) {
     const int P = min(16 * (T0 + i) + lr, np - 1);
     const int bb = P / 196, p = P - 196 * bb, py = p / 14, px = p - 14 * py;
-    abase[i] = ((18 * bb + py - R0) * 18 + px) * CBF_PS + 16 * cq + 4 * lg;
+    abase[i] = ((18 * bb + py - R0) * CBF_RWD + px) * CBF_PS + 16 * cq + 4 * lg;
   }
   f32x4 acc[TPB];
 #pragma unroll
@@ -827,7 +840,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     constexpr int I0 = decltype(i0c)::value;  // first tile of the pass
     auto load_a = [&](float4 (&a)[TP], int tap) {
       const int kh = tap / 5, kw = tap - 5 * kh;
-      const int aoff = ((4 - kh) * 18 + (4 - kw)) * CBF_PS;
+      const int aoff = ((4 - kh) * CBF_RWD + (4 - kw)) * CBF_PS;
 #pragma unroll
       for (int i = 0; i < TP; ++i) a[i] = *reinterpret_cast<const float4*>(dimg + abase[I0 + i] + aoff);
     };
@@ -859,12 +872,12 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   };
   run_pass(std::integral_constant<int, 0>{});
   if constexpr (NPASS == 2) run_pass(std::integral_constant<int, TP>{});
-#pragma unroll
-  for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];
   c2b_stamp(2);
   c2b_stamp_wave();
-  __syncthreads();  // every wave is done with the dY2 image; the x images are complete
+  __syncthreads();  // every wave is done with the dY2 image
   c2b_stamp(7);
+#pragma unroll
+  for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];  // (complete after the next barrier)
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
   if constexpr (LATE) load_epi();  // in flight while the partials are exchanged
@@ -1457,10 +1470,12 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
     // MIHVD_F32_F1R_PD=4: p/m/v prefetched 4 chunks ahead instead of 2 (measured no faster:
     // 28.2 vs 27.8 us, profiles/r04/kbench_f32_r04e.txt; the loop is not bound by HBM bytes in flight)
     const bool deep = env_knob("MIHVD_F32_F1R_PD", 2) >= 4;
+    const bool pin = env_knob("MIHVD_F32_F1R_PIN", 0) != 0;  // study: pinned dgrad MFMA order
 #define F1R_CASE(GG)                                                                              \
   case GG:                                                                                        \
     if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>);                        \
     else if (adam && deep) launch(f32_fc1_bwd_rows_kernel<GG, true, false, 4>);                   \
+    else if (adam && pin) launch(f32_fc1_bwd_rows_kernel<GG, true, false, 2, true>);              \
     else if (adam) launch(f32_fc1_bwd_rows_kernel<GG, true, false>);                              \
     else launch(f32_fc1_bwd_rows_kernel<GG, false, true>);                                        \
     break;

@@ -70,11 +70,14 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
 // dependent latency), the 25 taps fully unrolled (constant LDS offsets, static register indices).
 // Epilogue: 2x2 max-pool + argmax + bias + ReLU in registers.
 // ------------------------------------------------------------------------------------------ //
-// pixel stride 36 floats, 24 pixels per tall row (18 used): a tile's 16 rows (4 windows x 2x2
-// pixels: pixel offsets 2w + 24 dy + dx) then fall on 16 distinct 16-byte bank groups, so its
-// ds_read_b128 is conflict-free (with 18 pixels per row the 2x2 windows alias pairwise)
-constexpr int C2F_PS = 36, C2F_RW = 24, C2F_RS = C2F_RW * C2F_PS, C2F_MAXR = 22;
-constexpr int C2F_LDS = C2F_MAXR * C2F_RS * 4;                     // 76,032 B
+// Pixel stride 40 floats, 20 pixels per tall row (18 used). A ds_read_b128 is serviced in four
+// 16-lane groups, each pairing the lanes of two 4-channel chunks (lane groups lg 0/1 or 2/3) of 8
+// pixel rows each, over every tap offset and every window-row wrap of a tile; this stride and row
+// length give 1.4 LDS cycles per group on average (scripts/ldssim_conv2.py: exhaustive over the
+// B = 100 tiles and taps), against 2.3 for the 36 x 24 layout before (PMC: LDS_BANK_CONFLICT 3.5x
+// the active LDS cycles) and 1.0 only for tile shapes that leave MFMA rows idle.
+constexpr int C2F_PS = 40, C2F_RW = 20, C2F_RS = C2F_RW * C2F_PS, C2F_MAXR = 22;
+constexpr int C2F_LDS = C2F_MAXR * C2F_RS * 4;                     // 70,400 B
 constexpr int C2F_MAXCH = (C2F_MAXR * 18 * 8 + 255) / 256;         // image float4 chunks per thread
 
 // A row (tall-image offset) of lane row lr of tile `tile` (clamped past the batch)

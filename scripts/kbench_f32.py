@@ -129,7 +129,7 @@ def main():
         res[name] = timed(fn, args.reps)
     # study variants (host knobs read at capture time, csrc/kernels/f32_*.hip): placement and roles
     study = {
-        "conv2_fwd [LDS 76 KB: blocks may share a CU]": ({"MIHVD_F32_C2F_LDS": "76032"}, ks["conv2_fwd"]),
+        "conv2_fwd [LDS 70 KB: blocks may share a CU]": ({"MIHVD_F32_C2F_LDS": "70400"}, ks["conv2_fwd"]),
         "conv2_fwd [W2 after a full barrier]": ({"MIHVD_F32_C2F_PREW": "0"}, ks["conv2_fwd"]),
         "conv2_bwd [W2 after a full barrier]": ({"MIHVD_F32_C2B_PREW": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
@@ -151,6 +151,7 @@ def main():
         "conv2_bwd [wgrad role only, launch order]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_XCD": "0"},
                                                      ks["conv2_bwd"]),
         "fc1_bwd+W3 adam [p/m/v 4 chunks ahead]": ({"MIHVD_F32_F1R_PD": "4"}, ks["fc1_bwd+W3 adam"]),
+        "fc1_bwd+W3 adam [pinned dgrad MFMA order]": ({"MIHVD_F32_F1R_PIN": "1"}, ks["fc1_bwd+W3 adam"]),
         "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
@@ -183,11 +184,12 @@ def main():
     # whole-step studies: trainer attributes and launch knobs (read at capture time)
     steps = {
         "whole step [conv1 fused into conv2_fwd (conv12)]": ({"f32_conv12": True}, {}),
-        "whole step [conv2_fwd blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "76032"}),
+        "whole step [conv2_fwd blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "70400"}),
         "whole step [conv2_fwd W2 after a full barrier]": ({}, {"MIHVD_F32_C2F_PREW": "0"}),
         "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
         "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
         "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
+        "whole step [fc1_bwd pinned dgrad MFMA order]": ({}, {"MIHVD_F32_F1R_PIN": "1"}),
     }
     for name, (attrs, env) in steps.items():
         old_attr = {k: getattr(tr, k) for k in attrs}

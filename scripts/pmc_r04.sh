@@ -2,7 +2,7 @@
 # eagerly dispatched by kbench_f32 --only), summarised into $1/pmc_summary.txt
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 D=${1:-gpurun_out/pmc_r04}; mkdir -p $D
-ONLY="${ONLY:-conv12_fwd (conv1 fused),conv2_bwd,conv2_bwd:dg,conv2_bwd:wg,fc1_bwd+W3 adam,fc1_fwd,head,conv_reduce+adam}"
+ONLY="${ONLY:-conv1_fwd,conv2_fwd,conv2_bwd,conv2_bwd:dg,conv2_bwd:wg,fc1_bwd+W3 adam,fc1_fwd,head,conv_reduce+adam}"
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INST_LEVEL_VMEM SQ_BUSY_CYCLES --output-format csv -d $D/A -o run -- python scripts/kbench_f32.py --only "$ONLY" > $D/A.log 2>&1 || exit $?
 timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAVES --output-format csv -d $D/B -o run -- python scripts/kbench_f32.py --only "$ONLY" > $D/B.log 2>&1 || exit $?
 timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $D/C -o run -- python scripts/kbench_f32.py --only "$ONLY" > $D/C.log 2>&1 || exit $?
