@@ -817,6 +817,29 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
       }
   };
   if constexpr (!LATE) load_epi();
+  // LATE: one a1 and one idx1 load per tile and lane (lane group lg loads pixel 4 cq + lg of the
+  // tile, the one its row of the MFMA A operand is for), packed into a 4-bit code (ReLU bit | argmax)
+  // and exchanged across the four lane groups (two xor-shuffles), instead of 8 loads per tile.
+  int codes[LATE ? TPB : 1];
+  auto load_codes = [&]() {
+    float av[TPB];
+    int iv[TPB];
+#pragma unroll
+    for (int k = 0; k < TPB; ++k) {
+      const int P = min(16 * (T0 + k) + 4 * cq + lg, np - 1);
+      const int64_t o = (int64_t)P * 32 + 16 * nt + lr;
+      av[k] = a1[o];
+      iv[k] = idx1[o];
+    }
+#pragma unroll
+    for (int k = 0; k < TPB; ++k) {
+      const bool ok = 16 * (T0 + k) + 4 * cq + lg < np && av[k] > 0.f;
+      int c = ok ? (4 | iv[k]) << (4 * lg) : 0;
+      c |= __shfl_xor(c, 16, 64);
+      c |= __shfl_xor(c, 32, 64);
+      codes[k] = c;  // bits [4 r, 4 r + 3): pixel 4 cq + r's (relu << 2 | argmax)
+    }
+  };
   // the x patches are needed only by the epilogue: their gather (state -> rows -> x, three
   // dependent loads) is issued here and lands during the tap loop instead of before the barrier
   float xv[4];
@@ -880,7 +903,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];  // (complete after the next barrier)
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
-  if constexpr (LATE) load_epi();  // in flight while the partials are exchanged
+  if constexpr (LATE) load_codes();  // in flight while the partials are exchanged
 #pragma unroll
   for (int i = 0; i < TPB; ++i) red[((cq * 2 + nt) * TPB + i) * 64 + lane] = acc[i];
   __syncthreads();
@@ -913,8 +936,13 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
       for (int r = 0; r < 4; ++r) {
         const int P0r = 16 * (T0 + k) + 4 * cq + r, P = min(P0r, np - 1);  // wave-uniform
         const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
-        const float g = ea[k][r] > 0.f ? sk[r] : 0.f;
-        a[r] = (P0r < np && ex[k][r] == lg) ? g : 0.f;
+        if constexpr (LATE) {
+          const int c = (codes[k] >> (4 * r)) & 7;  // 0 past the batch or where ReLU cut the pixel
+          a[r] = (c == (4 | lg)) ? sk[r] : 0.f;
+        } else {
+          const float g = ea[k][r] > 0.f ? sk[r] : 0.f;
+          a[r] = (P0r < np && ex[k][r] == lg) ? g : 0.f;
+        }
         const float* xs = xim + (bb - b0) * 1024 + (2 * py + (lg >> 1)) * 32 + 2 * px + (lg & 1);
         x0[r] = xs[off0];
         x1[r] = 16 + lr < 25 ? xs[off1] : one1;
