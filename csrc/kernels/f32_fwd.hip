@@ -860,8 +860,11 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
     kern<<<nblk + extra, 256, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
                                                  a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, ad, c1);
   };
-  // MIHVD_F32_C2F_PREW=0: the W2 operand loaded after a full barrier (the earlier form)
-  const bool prew = env_knob("MIHVD_F32_C2F_PREW", 1) != 0;
+  // MIHVD_F32_C2F_PREW=1: the W2 operand issued before the staging barrier (LDS-only barrier)
+  // instead of after it. Measured slower standalone (21.0 vs 19.6 us: the 200 KB of W2 per block
+  // then competes with the a1 staging loads at kernel start) and neutral in the whole step
+  // (profiles/r04/kbench_f32_r04j.txt), so W2 follows a full barrier by default.
+  const bool prew = env_knob("MIHVD_F32_C2F_PREW", 0) != 0;
   TORCH_CHECK(!(fuse1 && ad.nblk > 0), "f32_conv2_fwd: the fused conv1 has no optimizer tail");
 #define C2F_CASE(T)                                                                  \
   case T:                                                                            \

@@ -130,7 +130,7 @@ def main():
     # study variants (host knobs read at capture time, csrc/kernels/f32_*.hip): placement and roles
     study = {
         "conv2_fwd [LDS 70 KB: blocks may share a CU]": ({"MIHVD_F32_C2F_LDS": "70400"}, ks["conv2_fwd"]),
-        "conv2_fwd [W2 after a full barrier]": ({"MIHVD_F32_C2F_PREW": "0"}, ks["conv2_fwd"]),
+        "conv2_fwd [W2 issued before the staging barrier]": ({"MIHVD_F32_C2F_PREW": "1"}, ks["conv2_fwd"]),
         "conv2_bwd [W2 after a full barrier]": ({"MIHVD_F32_C2B_PREW": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only, W2 after a full barrier]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_PREW": "0"},
@@ -185,7 +185,7 @@ def main():
     steps = {
         "whole step [conv1 fused into conv2_fwd (conv12)]": ({"f32_conv12": True}, {}),
         "whole step [conv2_fwd blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "70400"}),
-        "whole step [conv2_fwd W2 after a full barrier]": ({}, {"MIHVD_F32_C2F_PREW": "0"}),
+        "whole step [conv2_fwd W2 before the staging barrier]": ({}, {"MIHVD_F32_C2F_PREW": "1"}),
         "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
         "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
         "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
