@@ -1183,7 +1183,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg, int ig, int wmid) {
+    int n_wg, int ig, int wmid, int wdelay) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
@@ -1191,6 +1191,10 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     f32_conv2_dgrad_block<TPB, PREW, MEPI, NPASS>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
     return;
   }
+  // wdelay (one-round form): the wgrad blocks, which finish ahead of the dgrad blocks, hold their
+  // first loads back by ~wdelay x 1k cycles so the dgrad staging (the critical path) gets the memory
+  // system to itself at kernel start
+  for (int i = 0; i < wdelay; ++i) __builtin_amdgcn_s_sleep(16);
   // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
   f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, wmid,
                         smf);
@@ -1326,6 +1330,34 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
   }
   const int col = t & 63, part = t >> 6;  // dW2 blocks: 64 float4 x 4 slab quarters
   const int col16 = t & 15, part16 = t >> 4;  // cpart / db2 blocks: 16 float4 columns x 16 row parts
+  // the Adam operands (p, m, v) of the elements this thread will update, loaded before the partial
+  // sums so their latency overlaps the slab reads instead of following them
+  float4 pp{}, mm{}, vv{};
+  int64_t ao = -1;
+  if (opt) {
+    if (bid < CR_W2) {
+      if (t < 64) ao = sa.o_w2 + 4 * ((int64_t)bid * 64 + t);
+    } else if (t < 16) {
+      if (bid < CR_W2 + CR_CP) {
+        const int q0 = ((bid - CR_W2) * 16 + t) * 4;
+        ao = q0 < 800 ? sa.o_w1 + q0 : sa.o_b1 + (q0 - 800);
+      } else {
+        ao = sa.o_b2 + 4 * t;
+      }
+    }
+    if (ao >= 0 && bid < CR_W2) {  // the W2 segment is float4-aligned (checked on the host)
+      pp = *reinterpret_cast<const float4*>(sa.a.p + ao);
+      mm = *reinterpret_cast<const float4*>(sa.a.m + ao);
+      vv = *reinterpret_cast<const float4*>(sa.a.v + ao);
+    } else if (ao >= 0) {  // W1 / b1 / b2: no alignment guarantee, scalar loads
+      const float* P = sa.a.p + ao;
+      const float* M = sa.a.m + ao;
+      const float* V = sa.a.v + ao;
+      pp = make_float4(P[0], P[1], P[2], P[3]);
+      mm = make_float4(M[0], M[1], M[2], M[3]);
+      vv = make_float4(V[0], V[1], V[2], V[3]);
+    }
+  }
   float4 s;
   if (bid < CR_W2) {
     const int64_t i = (int64_t)bid * 64 + col;
@@ -1343,7 +1375,12 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       const float4 g = f4add(f4add(red[t], red[64 + t]), f4add(red[128 + t], red[192 + t]));
       const int64_t i = (int64_t)bid * 64 + t;
       reinterpret_cast<float4*>(gW2)[i] = g;
-      if (opt) adam_flat4(sa, sa.o_w2 + 4 * i, g, c);
+      if (opt) {
+        adam4_f32(pp, mm, vv, g, c);
+        *reinterpret_cast<float4*>(sa.a.p + ao) = pp;
+        *reinterpret_cast<float4*>(sa.a.m + ao) = mm;
+        *reinterpret_cast<float4*>(sa.a.v + ao) = vv;
+      }
     }
     return;
   }
@@ -1359,19 +1396,19 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       } else {
         *reinterpret_cast<float4*>(gb1 + (q0 - 800)) = g;
       }
-      if (opt) {
-        const int64_t o = q0 < 800 ? sa.o_w1 + q0 : sa.o_b1 + (q0 - 800);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) adam1(sa.a.p[o + e], sa.a.m[o + e], sa.a.v[o + e], ge[e], c);
-      }
     } else {
       *reinterpret_cast<float4*>(gb2 + 4 * t) = g;
-      if (opt) {
+    }
+    if (opt) {  // the prefetched operands (ao: this block's W1/b1 or b2 elements)
+      float* pe = &pp.x;
+      float* me = &mm.x;
+      float* ve = &vv.x;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t o = sa.o_b2 + 4 * t + e;
-          adam1(sa.a.p[o], sa.a.m[o], sa.a.v[o], ge[e], c);
-        }
+      for (int e = 0; e < 4; ++e) {
+        adam1(pe[e], me[e], ve[e], ge[e], c);
+        sa.a.p[ao + e] = pe[e];
+        sa.a.m[ao + e] = me[e];
+        sa.a.v[ao + e] = ve[e];
       }
     }
   }
@@ -1589,12 +1626,13 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const int ndg_arg = role == 2 ? 0 : n_dg;
   const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
   const int wmid = env_knob("MIHVD_F32_C2B_WMID", 1) != 0;  // 0: next image stored after the steps
+  const int wdelay = r1 ? std::max(0, std::min(env_knob("MIHVD_F32_C2B_WDELAY", 0), 64)) : 0;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
                                      cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig,
-                                     wmid);
+                                     wmid, wdelay);
   };
   // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
   // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA

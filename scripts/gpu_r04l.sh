@@ -1,0 +1,15 @@
+# Round 4, pass l: conv_reduce with the Adam operands prefetched, the wgrad start delay study, the
+# conv2_fwd W2-after-barrier default; tests, A/B, bench (driver form + 400 steps), profile.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r04l; mkdir -p $O
+T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
+timeout -k 10 500 $T tests/test_f32_gpu.py > $O/t_f32.log 2>&1
+rc=$?; grep -E "FAILED|ERROR|passed|failed" $O/t_f32.log | tail -5; [ $rc -ne 0 ] && { tail -40 $O/t_f32.log; exit $rc; }
+timeout -k 10 300 python scripts/kbench_f32.py --json $O/kbench_f32.json > $O/kbench_f32.log 2>&1 || { tail -30 $O/kbench_f32.log; exit 1; }
+grep -E "^conv_reduce|^conv2_bwd|^conv2_fwd|whole step" $O/kbench_f32.log
+for i in 1 2; do timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_drv$i.log 2>&1 || { tail -20 $O/bench_drv$i.log; exit 1; }; tail -1 $O/bench_drv$i.log | cut -c1-200; done
+timeout -k 10 200 python bench.py --steps 400 --warmup 40 > $O/bench_400.log 2>&1 || { tail -20 $O/bench_400.log; exit 1; }
+tail -1 $O/bench_400.log | cut -c1-200
+timeout -k 10 300 bash scripts/profile_bench.sh $O/prof > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+grep -v "^W2026\|^E2026" $O/prof.log | tail -10
+echo ALLDONE

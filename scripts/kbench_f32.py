@@ -143,6 +143,9 @@ def main():
         "conv2_bwd [wgrad next image stored after the steps]": ({"MIHVD_F32_C2B_WMID": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only, stored after the steps]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "0"},
                                                                ks["conv2_bwd"]),
+        "conv2_bwd [wgrad start held back ~4k cycles]": ({"MIHVD_F32_C2B_WDELAY": "4"}, ks["conv2_bwd"]),
+        "conv2_bwd [wgrad start held back ~8k cycles]": ({"MIHVD_F32_C2B_WDELAY": "8"}, ks["conv2_bwd"]),
+        "conv2_bwd [wgrad start held back ~12k cycles]": ({"MIHVD_F32_C2B_WDELAY": "12"}, ks["conv2_bwd"]),
         "conv2_bwd [two-round form]": ({"MIHVD_F32_C2B_R1": "0"}, c2b_two_round),
         "conv2_bwd [two-round form, dgrad role only]": ({"MIHVD_F32_C2B_R1": "0", "MIHVD_F32_C2B_ROLE": "1"},
                                                       c2b_two_round),
