@@ -92,10 +92,13 @@ __device__ __forceinline__ int c2f_abase(int tile, int lr, int lg, int nwin, int
 // NT (1 or 2) tiles against the register-resident weights: acc[u] += A(tile u) x W2. Software
 // pipeline over the 50 (tap, 16-channel) steps, fully unrolled: the A chunks of step s + 1 are read
 // into the other register set before step s's MFMAs issue (sched_barrier pins the order).
-template <int NT>
+// DEPTH: steps the A reads run ahead of the MFMAs (1, or 2 with a third register set; one wave per
+// SIMD has no other wave to cover an LDS latency the prefetch leaves exposed).
+template <int NT, int DEPTH = 2>
 __device__ __forceinline__ void c2f_tiles(const float* img, const int (&ab)[2], const float (&wb)[200],
                                           f32x4 (&acc)[2]) {
-  float4 ra[NT], rb[NT];
+  constexpr int R = DEPTH + 1;
+  float4 ra[R][NT];
   auto load_a = [&](float4 (&a)[NT], int st) {
     const int tap = st >> 1, c2 = st & 1, kh = tap / 5, kw = tap - 5 * kh;
     const int off = (kh * C2F_RW + kw) * C2F_PS + 16 * c2;
@@ -113,16 +116,13 @@ __device__ __forceinline__ void c2f_tiles(const float* img, const int (&ab)[2], 
 #pragma unroll
     for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].w, w[3], acc[u]);
   };
-  load_a(ra, 0);
 #pragma unroll
-  for (int st = 0; st < 50; st += 2) {
-    load_a(rb, st + 1);
+  for (int st = 0; st < DEPTH; ++st) load_a(ra[st], st);
+#pragma unroll
+  for (int st = 0; st < 50; ++st) {
+    if (st + DEPTH < 50) load_a(ra[(st + DEPTH) % R], st + DEPTH);
     __builtin_amdgcn_sched_barrier(0);
-    mfma_step(ra, st);
-    __builtin_amdgcn_sched_barrier(0);
-    if (st + 2 < 50) load_a(ra, st + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_step(rb, st + 1);
+    mfma_step(ra[st % R], st);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -226,7 +226,7 @@ __device__ __forceinline__ void c2f_conv1_stage(const C1Fuse& c1, float* img, fl
 // PREW: the W2 register operand is issued right behind the staging writes and the barrier orders
 // LDS alone, so the 200 KB per block of W2 loads overlap the barrier wait and the first taps.
 // FUSE1: the a1 rows are computed from x in the block (conv1 fused, C1Fuse) instead of loaded.
-template <int TPB, bool TAIL, bool PREW = false, bool FUSE1 = false>
+template <int TPB, bool TAIL, bool PREW = false, bool FUSE1 = false, int DEPTH = 2>
 __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, float* __restrict__ a2,
                                                             uint8_t* __restrict__ idx2, int B, F32Adam ad, C1Fuse c1) {
@@ -317,8 +317,8 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
     const int ab[2] = {c2f_abase(tile0, lr, lg, nwin, R0), c2f_abase(tile1, lr, lg, nwin, R0)};
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int nt = min(2, TPB - i);
-    if (nt == 2) c2f_tiles<2>(img, ab, wb, acc);
-    else c2f_tiles<1>(img, ab, wb, acc);
+    if (nt == 2) c2f_tiles<2, DEPTH>(img, ab, wb, acc);
+    else c2f_tiles<1, DEPTH>(img, ab, wb, acc);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int gw = 4 * (T0 + i + u) + lg;
@@ -865,12 +865,15 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
   // then competes with the a1 staging loads at kernel start) and neutral in the whole step
   // (profiles/r04/kbench_f32_r04j.txt), so W2 follows a full barrier by default.
   const bool prew = env_knob("MIHVD_F32_C2F_PREW", 0) != 0;
+  // MIHVD_F32_C2F_DEPTH=1: A reads one step ahead of the MFMAs instead of two (the earlier form)
+  const bool shallow = env_knob("MIHVD_F32_C2F_DEPTH", 2) < 2;
   TORCH_CHECK(!(fuse1 && ad.nblk > 0), "f32_conv2_fwd: the fused conv1 has no optimizer tail");
 #define C2F_CASE(T)                                                                  \
   case T:                                                                            \
     if (ad.nblk > 0) launch(f32_conv2_fwd_kernel<T, true>, ad.nblk);                 \
     else if (fuse1) launch(f32_conv2_fwd_kernel<T, false, true, true>, 0);           \
     else if (prew) launch(f32_conv2_fwd_kernel<T, false, true>, 0);                  \
+    else if (shallow) launch(f32_conv2_fwd_kernel<T, false, false, false, 1>, 0);    \
     else launch(f32_conv2_fwd_kernel<T, false>, 0);                                  \
     break;
   switch (tpb) {

@@ -131,6 +131,7 @@ def main():
     study = {
         "conv2_fwd [LDS 70 KB: blocks may share a CU]": ({"MIHVD_F32_C2F_LDS": "70400"}, ks["conv2_fwd"]),
         "conv2_fwd [W2 issued before the staging barrier]": ({"MIHVD_F32_C2F_PREW": "1"}, ks["conv2_fwd"]),
+        "conv2_fwd [A reads one step ahead]": ({"MIHVD_F32_C2F_DEPTH": "1"}, ks["conv2_fwd"]),
         "conv2_bwd [W2 after a full barrier]": ({"MIHVD_F32_C2B_PREW": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only, W2 after a full barrier]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_PREW": "0"},
