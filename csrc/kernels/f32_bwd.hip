@@ -69,7 +69,7 @@ __device__ __forceinline__ void f32_fc1_dgrad_block(int bid, const float* __rest
                                                     const uint8_t* __restrict__ idx2, const float* __restrict__ w3,
                                                     float* __restrict__ dY2, float* __restrict__ db2p, int B, int G,
                                                     float* smf) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int xcd = bid & 7, slot = bid >> 3, mg = slot % G, jt = (slot / G) * 8 + xcd;
   if (jt >= 49) return;
   const int m0 = 16 * mg;
@@ -161,7 +161,7 @@ __device__ __forceinline__ void f32_fc1_dgrad_ks_block(int bid, const float* __r
                                                        const uint8_t* __restrict__ idx2, const float* __restrict__ w3,
                                                        float* __restrict__ dY2, float* __restrict__ db2p, int B,
                                                        float* smf) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * bid, kb = 256 * wave;
   const float* wr = w3 + (int64_t)(f0 + lr) * 1024 + kb + 4 * lg;
   const float* zr[G];
@@ -326,7 +326,7 @@ __device__ __forceinline__ void f32_fc1_small_block(int bid, const float* __rest
 template <int G>
 __device__ __forceinline__ void f32_fc1_wgrad_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
                                                     float* __restrict__ gW3, int B, float* smf) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int jt = bid >> 4, ntile = bid & 15, j0 = 64 * jt, n0 = 64 * ntile;
   float* A2s = smf;                   // [128][64] rows b, cols j
   float* DZs = smf + F32_MAXB * 64;   // [128][64] rows b, cols n
@@ -528,7 +528,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     return;
   }
   constexpr int KS = 4 * G;  // K steps of the wgrad chain (samples padded to 16 G)
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * bid, nb = 128 * wave;
   f1r_stamp(0);
   float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
@@ -734,7 +734,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   float* dimg = smf;
   float* xim = smf + cbf_red(TPB);  // behind the partial exchange, written after the tap loops
   float* pw = xim + CBF_XIM;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int np = 196 * B, T0 = bid * TPB;
   const int P0 = 16 * T0, P1 = min(16 * (T0 + TPB), np) - 1;
   const int b0 = P0 / 196, b1i = P1 / 196;
@@ -945,7 +945,8 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
         }
         const float* xs = xim + (bb - b0) * 1024 + (2 * py + (lg >> 1)) * 32 + 2 * px + (lg & 1);
         x0[r] = xs[off0];
-        x1[r] = 16 + lr < 25 ? xs[off1] : one1;
+        const float xo = xs[off1];  // off1 = 0 past tap 24: an in-bounds read, replaced below
+        x1[r] = 16 + lr < 25 ? xo : one1;
       }
     };
     prep(0, xa[0], xb[0], av[0]);
@@ -1058,7 +1059,7 @@ __device__ __forceinline__ int xcd_contiguous(int g, int lo, int hi) {
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
                                                       int ig, int wmid, float* smf) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), l32 = lane & 31, hh = lane >> 5;
   const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
   const int img0 = ig * grp, nimg = min(ig, B - img0);
   auto load_img = [&](int b, float4 (&v)[7]) {

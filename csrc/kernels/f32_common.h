@@ -134,7 +134,7 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
                                                 int n_pool, const int64_t* state, const float* w1, const float* b1,
                                                 float* __restrict__ a1, uint8_t* __restrict__ idx1, int B, float* xim) {
   const int t = threadIdx.x;
-  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   int row = b;
   if (rows != nullptr) {
     int64_t step = 0;

@@ -159,7 +159,7 @@ constexpr int C2F_XIM = 2 * 1024;  // two padded x images [32][32] after the tal
 // two blocks share are written by both, with identical values).
 __device__ __forceinline__ void c2f_conv1_stage(const C1Fuse& c1, float* img, float* xim, int B, int R0, int R1,
                                                 int b0, int b1i, int gw0, int gw1) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   float wb1[2][7];
   int toff[7];
 #pragma unroll
@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
   }
   float* img = smf;
   c2f_stamp(0);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int nwin = 49 * B, T0 = ((int)blockIdx.x - (TAIL ? ad.nblk : 0)) * TPB;
   const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
   const int b0 = gw0 / 49, b1i = gw1 / 49;
@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd_kernel(const float* __restric
   extern __shared__ __attribute__((aligned(16))) float smf[];
   float* As = smf;  // [16 MT][228]: rows = samples, k contiguous
   const int nb = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
-  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int k0 = ks * F1F_KSL, nt = wave & 3, sh = wave >> 2;
   const int n = nb * 64 + nt * 16 + lr;
   constexpr int NCH = MT * 16 * 56, PER = (NCH + 511) / 512;
@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
   extern __shared__ __attribute__((aligned(16))) float smf[];
   float* As = smf;  // [16 MT][228]: rows = samples, k contiguous
   const int nb = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
-  const int lane = t & 63, wave = t >> 6, lr = lane & 15, lg = lane >> 4;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int k0 = ks * F1F_KSL, nt = wave & 3, sh = wave >> 2;
   const int n = nb * 64 + nt * 16 + lr;
   constexpr int NCH = MT * 16 * 56, PER = (NCH + 511) / 512;
@@ -622,7 +622,7 @@ __global__ void __launch_bounds__(256) f32_head_kernel(
     float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B) {
   __shared__ float red[4][10];
   __shared__ float dl[10];
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t step = state ? state[ST_FWD] : 0;
   const int n0 = t * 4;
   float4 parts[F1F_KS];
