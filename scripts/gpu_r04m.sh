@@ -2,14 +2,14 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r04m; mkdir -p $O
 T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
-timeout -k 10 500 $T tests/test_f32_gpu.py -k "conv2_fwd or conv12 or step_matches or trajectory" > $O/t_f32.log 2>&1
+timeout -k 10 500 $T tests/test_f32_gpu.py > $O/t_f32.log 2>&1
 rc=$?; grep -E "FAILED|ERROR|passed|failed" $O/t_f32.log | tail -5; [ $rc -ne 0 ] && { tail -40 $O/t_f32.log; exit $rc; }
 timeout -k 10 300 python scripts/kbench_f32.py --json $O/kbench_f32.json > $O/kbench_f32.log 2>&1 || { tail -30 $O/kbench_f32.log; exit 1; }
-grep -E "^conv2_fwd|^conv_reduce|whole step \(" $O/kbench_f32.log
+cat $O/kbench_f32.log
 for i in 1 2; do timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_drv$i.log 2>&1 || { tail -20 $O/bench_drv$i.log; exit 1; }; tail -1 $O/bench_drv$i.log | cut -c1-200; done
 timeout -k 10 200 python bench.py --steps 400 --warmup 40 > $O/bench_400.log 2>&1 || { tail -20 $O/bench_400.log; exit 1; }
 tail -1 $O/bench_400.log | cut -c1-200
 MIHVD_F32_STAMPS=1 timeout -k 10 400 python -m mihvd._build kernels --force > $O/stamps_build.log 2>&1 || { tail -20 $O/stamps_build.log; exit 1; }
 timeout -k 10 200 python scripts/stamps_f32.py > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
-grep -A6 "^conv2_fwd" $O/stamps.log
+cat $O/stamps.log
 echo ALLDONE
