@@ -231,6 +231,12 @@ def main():
         comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
     elif n == 1 and not tr.collectives:
         comm_desc = "none (1 GPU)"
+    elif tr.f32 and tr.shard_w3 and getattr(tr, "f32_factor", False):
+        comm_desc = ("fp32 factor gather over RCCL: all-gather of every rank's fp32 dz and all-to-all of the a2 "
+                     "columns of each rank's dense/kernel rows (beside fc1_bwd's dgrad and the conv backward) -> "
+                     "each rank's exact dW3 rows over all samples (one fp32 GEMM) and Adam on its 1/N of the rows "
+                     "-> RCCL all-gather of the updated fp32 rows (overlapping the next step's convolutions); RCCL "
+                     "allreduce of the other fp32 gradients; every step, in the HIP graph")
     elif tr.f32 and tr.shard_w3:
         comm_desc = ("RCCL reduce-scatter of dense/kernel's fp32 gradient by rows (overlapping the conv backward) -> "
                      "each rank's Adam on its 1/N of the rows -> RCCL all-gather of the updated fp32 rows "

@@ -515,7 +515,10 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
 // PIN: the dgrad MFMAs of a chunk issue in the written order (k-element outer, tiles inner: dependent
 // MFMAs G issues apart), pinned by sched_barrier after their operand reads; left alone the scheduler
 // chains each tile's four k-steps back to back.
-template <int G, bool ADAM, bool STORE, int PD = 2, bool PIN = false>
+// KW: K steps of the wgrad chain, 4 samples each: 4 G (the padded tiles) by default, ceil(B / 4) in
+// the exact-batch instantiation (B = 100: 25 instead of 28 MFMAs per chunk; the rows past the
+// batch are zero either way).
+template <int G, bool ADAM, bool STORE, int PD = 2, bool PIN = false, int KW = 4 * G>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
@@ -527,17 +530,23 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     f32_fc1_small512(bid - F1R_BLOCKS, dz, h, dlog, gb3, gW4, gb4, B, smf);
     return;
   }
-  constexpr int KS = 4 * G;  // K steps of the wgrad chain (samples padded to 16 G)
+  constexpr int KS = KW;  // K steps of the wgrad chain
+  // dgrad only (neither the fused Adam nor the stored gradient: the fp32 factor-gather plane forms
+  // dW3 from every rank's factors elsewhere): no a2 operand, no wgrad MFMAs, W3 read once
+  constexpr bool WG = ADAM || STORE;
+  static_assert(KS <= 4 * G && KS > 4 * G - 4, "wgrad K steps cover the batch tiles' last partial group");
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * bid, nb = 128 * wave;
   f1r_stamp(0);
   float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
   // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch)
   float a2r[KS];
+  if constexpr (WG) {
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int b = 4 * s + lg;
-    a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
+    for (int s = 0; s < KS; ++s) {
+      const int b = 4 * s + lg;
+      a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
+    }
   }
   // dz staging: chunk c = dz[0 .. 16 G)[nb + 16 c .. + 16): lane -> row (lane >> 2) + 16 it, float4 (lane & 3)
   float4 zst[G];
@@ -602,14 +611,19 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     // wgrad chains, was measured slower: 33.6 vs 27.7 us with the fused Adam, 27.5 vs 22.9 without,
     // profiles/r04/kbench_f32_r04g.txt; the pinned order keeps the global loads and the Adam VALU
     // work from interleaving with the MFMAs)
+    if constexpr (!WG) {
+      f1r_stamp(1 + c);
+      continue;
+    }
     f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
 #pragma unroll
-    for (int s = 0; s < KS; s += 2) {
+    for (int s = 0; s + 1 < KS; s += 2) {
       const float z0 = buf[(4 * s + lg) * 16 + lr];
       const float z1 = buf[(4 * s + 4 + lg) * 16 + lr];
       w0 = mfma4(z0, a2r[s], w0);
       w1 = mfma4(z1, a2r[s + 1], w1);
     }
+    if constexpr (KS & 1) w0 = mfma4(buf[(4 * (KS - 1) + lg) * 16 + lr], a2r[KS - 1], w0);
     const f32x4 g = w0 + w1;
     const int64_t o = rowo + 16 * c;
     float4 gg = make_float4(g[0], g[1], g[2], g[3]);
@@ -1520,12 +1534,13 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   chk_f32(gb4, 10, "f32_fc1_bwd: gb4");
   const F32Adam ad = f32_fc1_adam(w3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule);
   const bool adam = ad.nblk > 0;
-  TORCH_CHECK(adam || store_w3, "f32_fc1_bwd: without the fused Adam the dense/kernel gradient must be stored");
+  // neither adam nor store_w3: dgrad (+ db3, dW4, db4) only, gW3 untouched (fp32 factor-gather plane)
+  const bool dgrad_only = !adam && !store_w3;
   const int G = (B + 15) / 16;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   // Row form (default): dgrad + dW3 (+ the fused dense/kernel Adam) from one read of W3.
   // MIHVD_F32_F1B=0: the earlier three-role launch (window dgrad, separate dW3 tiles; no fused Adam).
-  if (env_knob("MIHVD_F32_F1B", 1) != 0 || adam) {
+  if (env_knob("MIHVD_F32_F1B", 1) != 0 || adam || dgrad_only) {
     auto launch = [&](auto kern) {
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1R_LDS);
       kern<<<F1R_BLOCKS + F1B_SMALL, 512, F1R_LDS, stream>>>(
@@ -1537,6 +1552,27 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
     // 28.2 vs 27.8 us, profiles/r04/kbench_f32_r04e.txt; the loop is not bound by HBM bytes in flight)
     const bool deep = env_knob("MIHVD_F32_F1R_PD", 2) >= 4;
     const bool pin = env_knob("MIHVD_F32_F1R_PIN", 0) != 0;  // study: pinned dgrad MFMA order
+    // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
+    // keeps the padded 28 for comparison)
+    if (dgrad_only) {
+      switch (G) {
+        case 1: launch(f32_fc1_bwd_rows_kernel<1, false, false>); break;
+        case 2: launch(f32_fc1_bwd_rows_kernel<2, false, false>); break;
+        case 3: launch(f32_fc1_bwd_rows_kernel<3, false, false>); break;
+        case 4: launch(f32_fc1_bwd_rows_kernel<4, false, false>); break;
+        case 5: launch(f32_fc1_bwd_rows_kernel<5, false, false>); break;
+        case 6: launch(f32_fc1_bwd_rows_kernel<6, false, false>); break;
+        case 7: launch(f32_fc1_bwd_rows_kernel<7, false, false>); break;
+        default: launch(f32_fc1_bwd_rows_kernel<8, false, false>);
+      }
+      return;
+    }
+    if (G == 7 && (B + 3) / 4 == 25 && !deep && !pin && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
+      if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 2, false, 25>);
+      else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 2, false, 25>);
+      else launch(f32_fc1_bwd_rows_kernel<7, false, true, 2, false, 25>);
+      return;
+    }
 #define F1R_CASE(GG)                                                                              \
   case GG:                                                                                        \
     if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>);                        \

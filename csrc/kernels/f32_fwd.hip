@@ -344,8 +344,11 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
 // K-contiguous LDS image (one float4 per 4 MFMAs). A lane's 4 accumulators are 4 consecutive
 // features of one sample: 16-byte slab stores.
 // ------------------------------------------------------------------------------------------ //
-constexpr int F1F_KS = 14, F1F_KSL = 224, F1F_AS = 228;
-constexpr int F1F_LDS = 128 * F1F_AS * 4;  // 116,736 B
+// a2 slice row stride 232 floats (58 16-byte slots, = 2 mod 4): the B-operand ds_read_b128 of lane
+// (lr, lg) at slot 58 lr + lg covers 16 distinct slots in each 16-lane group (scripts/ldssim_conv2.py
+// model: 1.0 LDS cycles per group; 228 gave 2.0, PMC LDS_BANK_CONFLICT 1.7x the active LDS cycles)
+constexpr int F1F_KS = 14, F1F_KSL = 224, F1F_AS = 232;
+constexpr int F1F_LDS = 128 * F1F_AS * 4;  // 118,784 B
 
 // ADAM: dense/kernel's deferred Adam update (the previous step's gradient) is applied here, where
 // W3 is read anyway (one read of p instead of two): the block first streams Adam over its
@@ -353,7 +356,8 @@ constexpr int F1F_LDS = 128 * F1F_AS * 4;  // 116,736 B
 // new tile in LDS and takes the MFMA fragments from there. Every W3 element belongs to exactly one
 // block. LDS: the a2 slice + the tile, so MT <= 7 (B <= 112).
 constexpr int F1F_WS = 64;                          // W3 tile row stride in LDS (floats)
-constexpr int F1F_LDS_ADAM = 7 * 16 * F1F_AS * 4 + F1F_KSL * F1F_WS * 4;   // 159,488 B
+constexpr int F1F_LDS_ADAM = 7 * 16 * F1F_AS * 4 + F1F_KSL * F1F_WS * 4;   // 161,280 B
+static_assert(F1F_LDS_ADAM <= 163840, "fc1 forward with the fused update: LDS");
 
 template <int MT, bool ADAM>
 __global__ void __launch_bounds__(512) f32_fc1_fwd_kernel(const float* __restrict__ a2, float* __restrict__ w3,

@@ -46,6 +46,8 @@ struct Rccl {
   decltype(&ncclBroadcast) broadcast = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
 };
 
 std::string loaded_rccl_path() {
@@ -87,6 +89,8 @@ Rccl& rccl() {
     MIHVD_SYM(broadcast, ncclBroadcast);
     MIHVD_SYM(group_start, ncclGroupStart);
     MIHVD_SYM(group_end, ncclGroupEnd);
+    MIHVD_SYM(send, ncclSend);
+    MIHVD_SYM(recv, ncclRecv);
 #undef MIHVD_SYM
   });
   TORCH_CHECK(r.lib != nullptr && r.init_rank != nullptr && r.all_reduce != nullptr && r.all_gather != nullptr &&
@@ -246,6 +250,36 @@ void rccl_all_reduce_many_(int64_t h, at::TensorList ts, int64_t op) {
   check(r.group_end(), "ncclGroupEnd");
 }
 
+// out[j] = peer j's in[rank]: `in` and `out` are world equal blocks (block j of `in` goes to rank j),
+// one RCCL group of point-to-point sends and receives (the own block is a device copy).
+void rccl_all_to_all(int64_t h, at::Tensor& out, const at::Tensor& in) {
+  Comm* c = get(h);
+  check_dev(c, out, "rccl_all_to_all: out");
+  check_dev(c, in, "rccl_all_to_all: in");
+  TORCH_CHECK(out.scalar_type() == in.scalar_type() && out.numel() == in.numel() && in.numel() % c->world == 0,
+              "rccl_all_to_all: in and out must hold world equal blocks of one dtype");
+  TORCH_CHECK(out.data_ptr() != in.data_ptr(), "rccl_all_to_all: out must not alias in");
+  if (in.numel() == 0) return;
+  Rccl& r = rccl();
+  TORCH_CHECK(r.send != nullptr && r.recv != nullptr && r.group_start != nullptr && r.group_end != nullptr,
+              "rccl_all_to_all: librccl lacks ncclSend / ncclRecv");
+  const size_t blk = (size_t)(in.numel() / c->world), bytes = blk * in.element_size();
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  const char* src = static_cast<const char*>(in.data_ptr());
+  char* dst = static_cast<char*>(out.data_ptr());
+  const ncclDataType_t dt = dtype_of(in);
+  C10_HIP_CHECK(hipMemcpyAsync(dst + c->rank * bytes, src + c->rank * bytes, bytes, hipMemcpyDeviceToDevice, stream));
+  if (c->world == 1) return;
+  check(r.group_start(), "ncclGroupStart");
+  for (int k = 1; k < c->world; ++k) {
+    // ring-ordered pairs (send to rank + k, receive from rank - k): every link carries one block
+    const int to = (c->rank + k) % c->world, from = (c->rank - k + c->world) % c->world;
+    check(r.send(src + to * bytes, blk, dt, to, c->comm, stream), "ncclSend");
+    check(r.recv(dst + from * bytes, blk, dt, from, c->comm, stream), "ncclRecv");
+  }
+  check(r.group_end(), "ncclGroupEnd");
+}
+
 // 0 healthy, else the ncclResult_t of an asynchronous failure of the communicator.
 int64_t rccl_async_error(int64_t h) {
   Comm* c = get(h);
@@ -309,6 +343,7 @@ TORCH_LIBRARY_FRAGMENT(mihvd, m) {
   m.def("rccl_all_gather(int comm, Tensor(a!) out, Tensor input) -> ()", &mihvd::rccl_all_gather);
   m.def("rccl_reduce_scatter(int comm, Tensor(a!) out, Tensor input, int op=0) -> ()", &mihvd::rccl_reduce_scatter);
   m.def("rccl_broadcast_(int comm, Tensor(a!) t, int root=0) -> ()", &mihvd::rccl_broadcast_);
+  m.def("rccl_all_to_all(int comm, Tensor(a!) out, Tensor input) -> ()", &mihvd::rccl_all_to_all);
   m.def("rccl_all_reduce_many_(int comm, Tensor(a!)[] ts, int op=0) -> ()", &mihvd::rccl_all_reduce_many_);
   m.def("rccl_async_error(int comm) -> int", &mihvd::rccl_async_error);
   m.def("rccl_comm_destroy(int comm, bool abort=False) -> ()", &mihvd::rccl_comm_destroy);

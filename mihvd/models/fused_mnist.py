@@ -198,6 +198,7 @@ class FusedMNISTTrainer:
         self.shadow = None if self.f32 else torch.zeros(FLAT_NUMEL, device=dev, dtype=torch.bfloat16)
         self.state = torch.zeros(4, device=dev, dtype=torch.int64)  # [fwd step, opt step t, -, -]
         self.shard_w3 = False
+        self.f32_factor = False
         ref = MNISTConvNet(impl="torch", seed=seed)
         self.load_model_weights(ref)
         B = self.B
@@ -342,6 +343,20 @@ class FusedMNISTTrainer:
             # sharded dense/kernel optimizer: this rank's rows of the reduce-scattered dW3
             self._f32_R = 3136 // self.world if self.world > 0 and 3136 % self.world == 0 else 0
             self.gshard = torch.empty(max(self._f32_R, 1), 1024, **f32) if self._f32_can_shard else None
+            # fp32 factor-gather plane (sharded optimizer; MIHVD_F32_PLANE=factor, or picked by
+            # select_data_plane): dW3 = a2^T dz has rank B per rank, so instead of reduce-scattering
+            # the 12.8 MB dW3 every rank all-gathers the fp32 dz of all ranks ([N][B][1024]) and
+            # receives from each rank the a2 columns of its own R rows ([N][B][R], all-to-all); its
+            # rows of dW3 are then the exact sum over all N B samples (one fp32 GEMM, R x NB x 1024,
+            # on the side stream beside the conv backward), and fc1_bwd runs its dgrad only. Per rank
+            # (N - 1) B (1024 + R) floats arrive instead of (N - 1) R 1024 (N = 8: 3.9 vs 11.2 MB).
+            if self._f32_can_shard:
+                N, R = self.world, self._f32_R
+                self.dz_all32 = torch.empty(N, B, 1024, **f32)
+                self.dz = self.dz_all32[self.rank]  # head writes this rank's block in place
+                self.a2_send = torch.empty(N, B, R, **f32)
+                self.a2_recv = torch.empty(N, B, R, **f32)
+                self.f32_factor = self.shard_w3 and os.environ.get("MIHVD_F32_PLANE", "rs") == "factor
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
@@ -752,11 +767,21 @@ class FusedMNISTTrainer:
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         gW3 = G("dense/kernel")
-        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3, G("dense/bias"),
-                      G("dense_1/kernel"), G("dense_1/bias"))
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self._reduce_scatter_rows(gW3, self.gshard, R)
+        if self.f32_factor:
+            # the factors of every rank (dz: all-gather; a2: this rank's R columns from each rank)
+            # and this rank's dW3 rows over all N B samples, beside fc1_bwd's dgrad and the conv
+            # backward
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._f32_factor_rows(R)
+            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
+        else:
+            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._reduce_scatter_rows(gW3, self.gshard, R)
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
                           G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
@@ -776,6 +801,14 @@ class FusedMNISTTrainer:
             self._shadow_ev = torch.cuda.Event()
             self._shadow_ev.record(side)
         self._full_state_valid = False
+
+    def _f32_factor_rows(self, R):
+        """gshard = this rank's R rows of dW3 summed over every rank's samples, from the gathered
+        factors (fp32 factor-gather plane, mihvd/parallel/factor.py; runs on the side stream)."""
+        from ..parallel.factor import factor_rows_
+
+        factor_rows_(self.gshard, self.a2, self.dz, self.dz_all32, self.a2_send, self.a2_recv, self.rank, self.world,
+                     self.ncomm)
 
     def _reduce_scatter_rows(self, full, out, R):
         """out = this rank's R rows of the sum over ranks of ``full`` (rows x 1024)."""
@@ -1277,10 +1310,10 @@ class FusedMNISTTrainer:
         self.grads[:W3_START].copy_(saved_grads)
         return ok
 
-    def _set_plane(self, xgmi: bool, shard: bool):
+    def _set_plane(self, xgmi: bool, shard: bool, factor: bool = False):
         """Switch data plane and sharding between steps (collective). Leaving the sharded xGMI
         plane, whose row gather of the last update would run in the next conv12_fwd launch,
-        gathers the rows now."""
+        gathers the rows now. ``factor``: the fp32 factor-gather plane (sharded only)."""
         self._join()
         if self.use_xgmi and self.shard_w3 and not (xgmi and shard):
             torch.cuda.synchronize(self.device)
@@ -1289,6 +1322,7 @@ class FusedMNISTTrainer:
             torch.cuda.synchronize(self.device)
         self.use_xgmi = bool(xgmi) and self.xplane is not None and not getattr(self, "_xplane_failed", False)
         self.set_sharding(shard)
+        self.f32_factor = bool(factor) and self.f32 and self.shard_w3
         self._graphs = {}
         self.graph = None
 
@@ -1306,6 +1340,7 @@ class FusedMNISTTrainer:
             self.gather_full_state()
             self._refresh_shadow()
         self.shard_w3 = shard
+        self.f32_factor = self.f32_factor and shard
         self._graphs = {}
         self.graph = None
 
@@ -1346,12 +1381,20 @@ class FusedMNISTTrainer:
 
                 warn_fallback("validation against the process group's collectives failed")
         cands = [(p, sh) for p in planes for sh in dict.fromkeys(shard_options)]
+        if self.f32 and self._f32_can_shard and True in shard_options:
+            # the fp32 factor-gather plane (sharded): MIHVD_F32_PLANE=auto (default) times it beside
+            # the reduce-scatter plane, "factor" uses it alone, "rs" leaves it out
+            fmode = os.environ.get("MIHVD_F32_PLANE", "auto").strip().lower()
+            if fmode == "factor":
+                cands = [("factor", True)]
+            elif fmode != "rs":
+                cands.append(("factor", True))
         host = self._host_collectives()
         # host (gloo) collectives cannot be captured or timed meaningfully: the candidates still run
         # (eagerly) for the consistency check below unless MIHVD_XGMI_CHECK=0, and the first
         # consistent candidate is kept
         if len(cands) == 1 or (host and os.environ.get("MIHVD_XGMI_CHECK", "1") == "0"):
-            self._set_plane(cands[0][0] == "xgmi", cands[0][1])
+            self._set_plane(cands[0][0] == "xgmi", cands[0][1], cands[0][0] == "factor")
             rep["plane"], rep["shard"] = cands[0]
             self._watch_plane()
             return rep
@@ -1364,7 +1407,7 @@ class FusedMNISTTrainer:
         # collective)
         snap = self._snapshot()
         for plane, sh in cands:
-            self._set_plane(plane == "xgmi", sh)
+            self._set_plane(plane == "xgmi", sh, plane == "factor")
             self._restore(snap)
             captured = self.build_graph(steps_per_replay=k, warmup=1)
             torch.cuda.synchronize(self.device)
@@ -1386,13 +1429,28 @@ class FusedMNISTTrainer:
         # (a gather that saw the previous step's rows) moves the result by the size of a whole
         # gradient term; on any mismatch, on any rank, every rank drops the plane.
         cons = {}
+        fcons = None
         for (plane, sh), fin in finals.items():
             ref = finals.get(("rccl", sh))
-            if plane != "xgmi" or ref is None:
+            if plane == "rccl" or ref is None:
                 continue
             upd = (ref - snap["params"]).norm().item()
             d = (fin - ref).norm().item() / max(upd, 1e-30)
-            cons[f"xgmi-{'shard' if sh else 'replicated'}"] = d if math.isfinite(d) else float("inf")
+            d = d if math.isfinite(d) else float("inf")
+            if plane == "factor":
+                fcons = d  # the fp32 factor plane: same exact sums in another order
+            else:
+                cons[f"xgmi-{'shard' if sh else 'replicated'}"] = d
+        if fcons is not None:
+            from ..parallel.xgmi import _group_ok
+
+            ok = _group_ok(fcons <= float(os.environ.get("MIHVD_XGMI_CHECK_TOL", "1e-3")), None, self.device)
+            rep["factor_consistency"] = round(fcons, 9)
+            if not ok:
+                import warnings
+
+                warnings.warn("fp32 factor-gather steps disagree with the reduce-scatter plane's; not used")
+                times = {key: t for key, t in times.items() if key[0] != "factor"}
         if cons:
             from ..parallel.xgmi import _group_ok, warn_fallback
 
@@ -1420,7 +1478,7 @@ class FusedMNISTTrainer:
             plane, sh = next(c for c in cands if c in times)
         else:
             plane, sh = min(times, key=lambda key: (times[key] != times[key], times[key]))
-        self._set_plane(plane == "xgmi", sh)
+        self._set_plane(plane == "xgmi", sh, plane == "factor")
         self._restore(snap)
         rep["us_per_step"] = {f"{p}{'-shard' if s else '-replicated'}": round(t, 2) for (p, s), t in times.items()}
         rep["plane"], rep["shard"] = plane, sh
@@ -1469,6 +1527,12 @@ class FusedMNISTTrainer:
         holds stale values."""
         if self.use_xgmi and self.gather:
             return torch.cat([self.gred, self.grads[W3_START:]])
+        if self.f32 and self.shard_w3:
+            # both fp32 sharded planes leave this rank's reduced dense/kernel rows in gshard
+            g = self.grads.clone()
+            R = self._f32_R
+            g[W3_START + self.rank * R * 1024:W3_START + (self.rank + 1) * R * 1024] = self.gshard.view(-1)
+            return g
         return self.grads
 
     def data_plane(self) -> str:
@@ -1476,6 +1540,8 @@ class FusedMNISTTrainer:
             return "none"
         if self.gather:
             return "xgmi" if self.use_xgmi else "rccl"
+        if self.f32 and self.f32_factor:
+            return "factor"
         return "xgmi" if self.xgmi and any(c is not None for c in self.xgmi.values()) else "rccl"
 
     def close(self):

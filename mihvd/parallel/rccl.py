@@ -86,6 +86,11 @@ class NativeComm:
         self._o.rccl_reduce_scatter(self.handle, out, inp, _OPS[op])
         return out
 
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """Block j of ``inp`` goes to rank j; block j of ``out`` comes from rank j (equal blocks)."""
+        self._o.rccl_all_to_all(self.handle, out, inp)
+        return out
+
     def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
         self._o.rccl_broadcast_(self.handle, t, root)
         return t

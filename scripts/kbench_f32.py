@@ -50,7 +50,12 @@ def main():
     ap.add_argument("--only", default=None, help="comma-separated entries: run each --eager times, eagerly "
                     "(for counter collection), and exit")
     ap.add_argument("--eager", type=int, default=20)
+    ap.add_argument("--match", default=None, help="'|'-separated substrings: time only the entries whose name "
+                    "contains one of them")
     args = ap.parse_args()
+
+    def want(name):
+        return not args.match or any(m in name for m in args.match.split("|"))
     from mihvd.models.fused_mnist import FC_START, FLAT_NUMEL, SEGMENTS, W3_START, FusedMNISTTrainer
     from mihvd.utils.data import synthetic_mnist
 
@@ -69,6 +74,10 @@ def main():
     gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
              G("conv_layer2/conv2d/bias"))
     w2, w3 = P("conv_layer2/conv2d/kernel"), P("dense/kernel")
+    fa8, fz8, fo8 = (torch.randn(8 * B, 392, device="cuda"), torch.randn(8 * B, 1024, device="cuda"),
+                     torch.empty(392, 1024, device="cuda"))
+    fa1, fz1, fo1 = (torch.randn(B, 3136, device="cuda"), torch.randn(B, 1024, device="cuda"),
+                     torch.empty(3136, 1024, device="cuda"))
     # lr 0 keeps the weights fixed while the optimizer kernels are timed
     ks = {
         "conv1_fwd": lambda: o.f32_conv1_fwd(tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"),
@@ -91,6 +100,12 @@ def main():
                                                  G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"),
                                                  G("dense_1/bias"), tr.m[s3], tr.v[s3], st, 0.0, b1, b2, tr.eps, 1.0,
                                                  tr.rule, False),
+        "fc1_bwd [dgrad only: fp32 factor plane]": lambda: o.f32_fc1_bwd(
+            tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"), G("dense/bias"),
+            G("dense_1/kernel"), G("dense_1/bias"), store_w3=False),
+        # the factor plane's dW3-row GEMM at N = 8 (392 rows x 800 samples x 1024) and N = 1
+        "factor GEMM N=8 (392x800x1024)": lambda: torch.mm(fa8.t(), fz8, out=fo8),
+        "factor GEMM N=1 (3136x100x1024)": lambda: torch.mm(fa1.t(), fz1, out=fo1),
         "conv2_bwd": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab),
         "conv_reduce": lambda: o.f32_conv_reduce(tr.slab, tr.cpart, tr.db2p, *gconv),
         "conv_reduce+adam": lambda: o.f32_conv_reduce(
@@ -126,7 +141,8 @@ def main():
 
     res = {}
     for name, fn in ks.items():
-        res[name] = timed(fn, args.reps)
+        if want(name):
+            res[name] = timed(fn, args.reps)
     # study variants (host knobs read at capture time, csrc/kernels/f32_*.hip): placement and roles
     study = {
         "conv2_fwd [LDS 70 KB: blocks may share a CU]": ({"MIHVD_F32_C2F_LDS": "70400"}, ks["conv2_fwd"]),
@@ -156,6 +172,7 @@ def main():
                                                      ks["conv2_bwd"]),
         "fc1_bwd+W3 adam [p/m/v 4 chunks ahead]": ({"MIHVD_F32_F1R_PD": "4"}, ks["fc1_bwd+W3 adam"]),
         "fc1_bwd+W3 adam [pinned dgrad MFMA order]": ({"MIHVD_F32_F1R_PIN": "1"}, ks["fc1_bwd+W3 adam"]),
+        "fc1_bwd+W3 adam [padded wgrad K (28 steps)]": ({"MIHVD_F32_F1R_KW": "0"}, ks["fc1_bwd+W3 adam"]),
         "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
@@ -164,6 +181,8 @@ def main():
 
     }
     for name, (env, fn) in study.items():
+        if not want(name):
+            continue
         old_env = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
@@ -176,11 +195,12 @@ def main():
                     os.environ[k] = v
     saved = tr.lr
     tr.lr = 0.0
-    res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
-    tr._join()
+    if want("whole step (graph, 20 steps/replay)"):
+        res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
+        tr._join()
     mode = tr.f32_w3
     for alt in ("bwd", "fc1", "tail", "side"):
-        if alt != mode:
+        if alt != mode and want(f"whole step [dense/kernel Adam: {alt}]"):
             tr.f32_w3 = alt
             res[f"whole step [dense/kernel Adam: {alt}]"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
             tr._join()
@@ -194,8 +214,11 @@ def main():
         "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
         "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
         "whole step [fc1_bwd pinned dgrad MFMA order]": ({}, {"MIHVD_F32_F1R_PIN": "1"}),
+        "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
     }
     for name, (attrs, env) in steps.items():
+        if not want(name):
+            continue
         old_attr = {k: getattr(tr, k) for k in attrs}
         old_env = {k: os.environ.get(k) for k in env}
         for k, v in attrs.items():

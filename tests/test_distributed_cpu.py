@@ -52,6 +52,16 @@ def test_collectives_two_ranks(tmp_path):
     assert a["join"] == 1
 
 
+@pytest.mark.parametrize("np_", [2, 4])
+def test_f32_factor_rows_gather(tmp_path, np_):
+    """The fp32 factor-gather plane's exchange + GEMM (mihvd/parallel/factor.py) on the host
+    collectives: rank r's dW3 rows from every rank's dz (all-gather) and a2 columns (all-to-all)."""
+    _, outs = run_scenario(tmp_path, "factor_rows", np_=np_)
+    for o in outs:
+        assert o["R"] == 3136 // np_ and o["dz_gathered"], o
+        assert o["rel"] < 1e-6, o
+
+
 def test_dp_equivalence(tmp_path):
     _, outs = run_scenario(tmp_path, "dp_equivalence")
     for o in outs:

@@ -183,16 +183,18 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
     dlog = torch.randn(B, 10, device="cuda", generator=g)
     st = torch.tensor([5, 7, 0, 0], device="cuda", dtype=torch.int64)
 
-    def run(fused, w, m, v, env=None):
+    def run(fused, w, m, v, env=None, key="MIHVD_F32_F1B"):
         dY2 = torch.full((B, 14, 14, 64), float("nan"), device="cuda")
         db2p = torch.empty(int(ops.f32_db2_rows(B)), 64, device="cuda")
         gW3 = torch.full((3136, 1024), float("nan"), device="cuda")
         small = [torch.empty(1024, device="cuda"), torch.empty(1024, 10, device="cuda"), torch.empty(10, device="cuda")]
-        old = os.environ.get("MIHVD_F32_F1B")
+        old = os.environ.get(key)
         if env is not None:
-            os.environ["MIHVD_F32_F1B"] = env
+            os.environ[key] = env
         try:
-            if fused:
+            if fused == "dgrad":  # the fp32 factor plane's launch: no dW3 at all
+                ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small, store_w3=False)
+            elif fused:
                 ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small, m, v, st, 1e-3, 0.9, 0.999, 1e-8,
                                 1.0, 0, True)
             else:
@@ -200,9 +202,9 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
         finally:
             if env is not None:
                 if old is None:
-                    os.environ.pop("MIHVD_F32_F1B", None)
+                    os.environ.pop(key, None)
                 else:
-                    os.environ["MIHVD_F32_F1B"] = old
+                    os.environ[key] = old
         return dY2, db2p, gW3, small
 
     wf, mf, vf = w3.clone(), m3.clone(), v3.clone()
@@ -214,6 +216,14 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
     ms, vs = m3.clone(), v3.clone()
     ops.adam_step(ws.view(-1), gW3s.view(-1), ms.view(-1), vs.view(-1), None, st, 0, 1e-3, 0.9, 0.999, 1e-8, 1.0, 0, 0)
     assert torch.equal(wf, ws) and torch.equal(mf, ms) and torch.equal(vf, vs)
+    # dgrad-only launch (fp32 factor plane): the same dY2 / db2 / small gradients, dW3 never written
+    dY2d, db2d, gW3d, smalld = run("dgrad", w3.clone(), None, None)
+    assert torch.equal(dY2d, dY2s) and torch.equal(db2d, db2s) and torch.isnan(gW3d).all()
+    assert all(torch.equal(a, b) for a, b in zip(smalld, smalls))
+    # the exact-batch wgrad chain (ceil(B / 4) K steps where B = 97..100) adds the same products as the
+    # padded one (the padded steps add exact zeros)
+    _, _, gW3p, _ = run(False, w3.clone(), None, None, env="0", key="MIHVD_F32_F1R_KW")
+    assert torch.equal(gW3p, gW3s)
     # dW3 and the routed dgrad against fp64
     assert rel_err(gW3f, a2.double().t() @ dz.double()) < 1e-6
     g2 = (dz.double() @ w3.double().t()) * (a2 > 0)

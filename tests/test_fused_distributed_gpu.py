@@ -61,6 +61,27 @@ def test_collectives_inside_hip_graph(tmp_path, prec, shard, xgmi, comm):
         assert set(r["select"]["us_per_step"]) == {"xgmi-shard", "rccl-shard"}, r
 
 
+def test_f32_factor_plane_inside_hip_graph(tmp_path):
+    """The fp32 factor-gather plane (MIHVD_F32_PLANE=factor) at world 1 with the collectives forced
+    on, on the native communicator: dz all-gather, a2-column all-to-all and the dW3-row GEMM on the
+    side stream, fc1_bwd's dgrad-only launch, sharded Adam and the row all-gather, captured in 2 x
+    5-step graphs and replayed. dW3 is summed by a GEMM in another order than the fused step's
+    MFMA chain, so the match with the trainer without collectives is to fp32 rounding, not bitwise."""
+    _gpu()
+    env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3="1",
+               MIHVD_XGMI="off", MIHVD_TEST_PRECISION="fp32", MIHVD_COMM="native", MIHVD_F32_PLANE="factor")
+    for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, WORKER, "rccl_graph", str(tmp_path)], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = json.loads((tmp_path / "rccl_graph.json").read_text())
+    assert r["captured"] and r["steps"] == r["pre_steps"] + 22, r
+    assert r["shard"] and r["plane"] == "factor" and r["native_comm"], r
+    assert r["rel_update_diff"] < 1e-5, r
+    assert abs(r["loss"] - r["loss_ref"]) < 1e-4 * max(1.0, abs(r["loss_ref"])), r
+
+
 @pytest.mark.parametrize("gather", ["1", "0"])
 def test_fused_data_parallel_equivalence_two_ranks(tmp_path, gather):
     """gather=1: dW3 from all-gathered factors (the default data plane); gather=0: bucket allreduce."""
@@ -168,19 +189,22 @@ def test_bench_flow_trains_at_8_ranks(tmp_path, n, prec):
         assert o["losses"][-1] < 1.0, o
 
 
-@pytest.mark.parametrize("n,prec,gather,shard,xgmi", [
-    (4, "fp32", "0", "0", "off"), (8, "fp32", "0", "0", "off"), (4, "fp32", "0", "1", "off"),
-    (8, "fp32", "0", "1", "off"),
-    (4, "bf16", "1", "1", "off"), (8, "bf16", "1", "1", "off"), (8, "bf16", "1", "0", "off"),
-    (8, "bf16", "0", "0", "off"), (8, "bf16", "1", "1", "on")])
-def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shard, xgmi):
+@pytest.mark.parametrize("n,prec,gather,shard,xgmi,f32plane", [
+    (4, "fp32", "0", "0", "off", "rs"), (8, "fp32", "0", "0", "off", "rs"), (4, "fp32", "0", "1", "off", "rs"),
+    (8, "fp32", "0", "1", "off", "rs"), (4, "fp32", "0", "1", "off", "factor"), (8, "fp32", "0", "1", "off", "factor"),
+    (4, "bf16", "1", "1", "off", "rs"), (8, "bf16", "1", "1", "off", "rs"), (8, "bf16", "1", "0", "off", "rs"),
+    (8, "bf16", "0", "0", "off", "rs"), (8, "bf16", "1", "1", "on", "rs")])
+def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shard, xgmi, f32plane):
     """N ranks x B=50 sharing this GPU over gloo: the reduced gradient of the first step equals the
     sum of the N single-process gradients (gradient rel < 1e-4), the update equals TF1 Adam on their
     average, every rank holds identical parameters, and training makes progress. At 8 ranks the
-    factor-gather dW3 runs over Kw = 400 rows (the 4-group K-split tiles of the sharded slice)."""
+    factor-gather dW3 runs over Kw = 400 rows (the 4-group K-split tiles of the sharded slice).
+    f32plane=factor: the fp32 factor-gather plane (each rank's dW3 rows from every rank's fp32 dz
+    and a2 columns) instead of the reduce-scatter of dW3."""
     _gpu()
     env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_SHARD_W3=shard,
-               MIHVD_XGMI=xgmi, MIHVD_TEST_PRECISION=prec, MIHVD_TEST_B="50", MIHVD_XGMI_TIMEOUT_MS="60000")
+               MIHVD_XGMI=xgmi, MIHVD_TEST_PRECISION=prec, MIHVD_TEST_B="50", MIHVD_XGMI_TIMEOUT_MS="60000",
+               MIHVD_F32_PLANE=f32plane)
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", str(n), sys.executable, WORKER, "dp_gloo_n", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -191,6 +215,8 @@ def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shar
         assert o["upd_rel"] < (1e-3 if prec == "fp32" else 1e-2), o
         assert o["losses"][-1] < o["losses"][0], o
         assert o["shard"] == (shard == "1"), o
+        if prec == "fp32" and shard == "1":
+            assert o["plane"] == ("factor" if f32plane == "factor" else "rccl"), o
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])

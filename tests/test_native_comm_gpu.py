@@ -30,7 +30,8 @@ def test_native_rccl_comm_one_gpu(tmp_path):
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     r = json.loads(out.read_text())
     assert r["world"] == 1
-    for k in ("allreduce_sum", "allreduce_avg", "allreduce_bf16", "all_gather", "reduce_scatter", "broadcast", "many"):
+    for k in ("allreduce_sum", "allreduce_avg", "allreduce_bf16", "all_gather", "reduce_scatter", "all_to_all",
+              "broadcast", "many"):
         assert r[k], (k, r)
     assert r["graph"] == 1024.0, r
     assert r["async_error"] == 0

@@ -414,6 +414,31 @@ def sc_keras_tf_api(outdir):
     out(outdir, "keras_tf_api", res)
 
 
+def sc_factor_rows(outdir):
+    """fp32 factor gather (mihvd/parallel/factor.py) over gloo: each rank's rows of dW3 formed from
+    the gathered factors equal those rows of the sum over ranks of a2_q^T dz_q."""
+    from mihvd.parallel.factor import factor_rows_
+
+    r, n = hvd.rank(), hvd.size()
+    B, R = 24, 3136 // n
+
+    def factors(q):
+        g = torch.Generator().manual_seed(100 + q)
+        return torch.randn(B, 3136, generator=g), torch.randn(B, 1024, generator=g)
+
+    a2, dz0 = factors(r)
+    dz_all = torch.empty(n, B, 1024)
+    dz = dz_all[r]
+    dz.copy_(dz0)
+    a2_send, a2_recv = torch.empty(n, B, R), torch.empty(n, B, R)
+    out_rows = torch.empty(R, 1024)
+    factor_rows_(out_rows, a2, dz, dz_all, a2_send, a2_recv, r, n)
+    ref = sum(f[0].double().t() @ f[1].double() for f in map(factors, range(n)))[r * R:(r + 1) * R]
+    rel = ((out_rows.double() - ref).norm() / ref.norm()).item()
+    out(outdir, "factor_rows", {"rel": rel, "R": R, "dz_gathered": bool(torch.equal(dz_all[(r + 1) % n],
+                                                                                     factors((r + 1) % n)[1]))})
+
+
 PS_INIT = []
 
 

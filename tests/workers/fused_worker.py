@@ -197,7 +197,7 @@ def sc_dp_gloo_n(outdir):
     red = tr.reduced_grads()
     if tr.gather or (tr.f32 and tr.shard_w3):
         # the factor-gather plane forms dW3 only for the rows whose optimizer this rank owns; the
-        # fp32 sharded optimizer reduce-scatters them
+        # fp32 sharded optimizer reduce-scatters them (or forms them from the gathered fp32 factors)
         if tr.f32:
             R = tr._f32_R
             rows = slice(FLAT_W3 + r * R * 1024, FLAT_W3 + (r + 1) * R * 1024)

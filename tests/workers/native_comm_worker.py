@@ -41,6 +41,10 @@ def main(out):
     out_rs = torch.zeros(8, device=dev)
     comm.reduce_scatter(out_rs, full[0])
     res["reduce_scatter"] = bool(torch.equal(out_rs, full[0]))
+    a2a_in = torch.arange(4096, device="cuda", dtype=torch.float32)
+    a2a_out = torch.full_like(a2a_in, float("nan"))
+    comm.all_to_all(a2a_out, a2a_in)
+    res["all_to_all"] = bool(torch.equal(a2a_out, a2a_in))
     comm.broadcast_(a, 0)
     res["broadcast"] = bool(torch.equal(a, ref))
     comm.all_reduce_many_([a, b])
