@@ -737,11 +737,13 @@ __device__ __forceinline__ void lds_barrier() {
 // NPASS = 2 (the one-round form): TPB tiles in two tap-loop passes of TPB / 2 over the same
 // register-resident W2 (the A register sets are reused, the accumulators of both passes live on),
 // so a block loads W2 once for twice the tiles and the halo rows are staged once for both.
-template <int TPB, bool PREW, bool MEPI, int NPASS = 1>
+// FRAG: W2 from the fragment copy (f32_w2_frag_block in f32_fwd.hip): one contiguous 1 KB per wave
+// and tap instead of 16 scattered 64-byte row pieces.
+template <int TPB, bool PREW, bool MEPI, int NPASS = 1, bool FRAG = false>
 __device__ __forceinline__ void f32_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
-    const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf) {
+    const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf, const float* __restrict__ w2f) {
   static_assert(TPB % NPASS == 0, "tiles split evenly over the passes");
   constexpr int TP = TPB / NPASS;                                        // tiles per pass
   constexpr int MAXCH = (cbf_maxr(NPASS) * 18 * 16 + 511) / 512;         // dY2 chunks per thread
@@ -779,11 +781,12 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   // PREW: issued right behind the staging writes (which wait only for the staging loads), so they
   // are in flight across the barrier
   const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
+  const float4* wfq = reinterpret_cast<const float4*>(w2f) + wave * 25 * 64 + lane;
   float4 wb[25];
   if constexpr (PREW) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
+    for (int tap = 0; tap < 25; ++tap) wb[tap] = FRAG ? wfq[tap * 64] : *reinterpret_cast<const float4*>(wq + tap * 2048);
     __builtin_amdgcn_sched_barrier(0);
   }
   int abase[TPB];
@@ -806,7 +809,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     // Issued after the barrier (whose vmcnt(0) would otherwise wait for all 25 loads): the tap loop
     // consumes them in issue order, so tap t waits only for its own.
 #pragma unroll
-    for (int tap = 0; tap < 25; ++tap) wb[tap] = *reinterpret_cast<const float4*>(wq + tap * 2048);
+    for (int tap = 0; tap < 25; ++tap) wb[tap] = FRAG ? wfq[tap * 64] : *reinterpret_cast<const float4*>(wq + tap * 2048);
   }
   // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched.
   // VALU form: (nt, tile) pairs p = wave + 8k, lane pixel 4 lg + r. MEPI form: the wave's pixel
@@ -1193,17 +1196,18 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   c2b_stamp(6);
 }
 
-template <int TPB, bool PREW, bool MEPI, int NPASS = 1>
+template <int TPB, bool PREW, bool MEPI, int NPASS = 1, bool FRAG = false>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg, int ig, int wmid, int wdelay) {
+    int n_wg, int ig, int wmid, int wdelay, const float* __restrict__ w2f) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
   if (bid < n_dg) {
-    f32_conv2_dgrad_block<TPB, PREW, MEPI, NPASS>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
+    f32_conv2_dgrad_block<TPB, PREW, MEPI, NPASS, FRAG>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf,
+                                                        w2f);
     return;
   }
   // wdelay (one-round form): the wgrad blocks, which finish ahead of the dgrad blocks, hold their
@@ -1625,9 +1629,15 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
 
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                   at::Tensor& cpart, at::Tensor& slab) {
+                   at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag) {
   const int B = a1.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv2_bwd: batch 1..128");
+  const float* w2f = nullptr;
+  if (w2frag.has_value() && w2frag->defined()) {
+    TORCH_CHECK(w2frag->is_cuda() && w2frag->dtype() == at::kFloat && w2frag->is_contiguous() &&
+                    w2frag->numel() >= 51200, "f32_conv2_bwd: w2frag (the dgrad fragment copy, 51200 floats)");
+    w2f = w2frag->data_ptr<float>();
+  }
   chk_f32(dY2, (int64_t)B * 196 * 64, "f32_conv2_bwd: dY2");
   chk_f32(w2, 51200, "f32_conv2_bwd: w2");
   chk_f32(a1, (int64_t)B * 6272, "f32_conv2_bwd: a1");
@@ -1669,7 +1679,7 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
                                      cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig,
-                                     wmid, wdelay);
+                                     wmid, wdelay, w2f);
   };
   // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
   // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA
@@ -1679,7 +1689,9 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes (PREW; epilogue per MIHVD_F32_C2B_MEPI)
 #define C2B_R1(T)                                                                                        \
   case T:                                                                                                \
-    mepi ? launch(f32_conv2_bwd_kernel<T, true, true, 2>) : launch(f32_conv2_bwd_kernel<T, true, false, 2>); \
+    if (mepi) launch(f32_conv2_bwd_kernel<T, true, true, 2>);                                             \
+    else if (w2f) launch(f32_conv2_bwd_kernel<T, true, false, 2, true>);                                  \
+    else launch(f32_conv2_bwd_kernel<T, true, false, 2>);                                                 \
     break;
     switch (tpb) {
       C2B_R1(2)

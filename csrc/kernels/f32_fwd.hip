@@ -45,11 +45,42 @@ void f32_fwd_stamps_set(unsigned long long* p) {
 // tiles 13q + w, +4, ... . A = im2col(x) gathered from the padded image in LDS (one ds_read_b32
 // per MFMA), B = W1 in registers (k = 4s + lane group, 25 taps zero-padded to 28).
 // ------------------------------------------------------------------------------------------ //
+// W2 fragment copies (MIHVD_F32_W2F): the register-resident W2 operands of conv2_fwd and of the
+// conv2_bwd dgrad blocks, each stored in the order the waves load them, so every load instruction
+// of a wave reads one contiguous 1 KB (a float4 per lane) instead of 16 (or 4) scattered 64-byte
+// pieces of the HWIO tensor: fewer load instructions (conv2_fwd: 50 instead of 200 per lane) and
+// whole 128-byte lines through the CU's L1. Written from W2 by extra blocks of the conv1 launch,
+// which precedes both readers in every step (W2 changes only in the step's final Adam).
+//   fwd [tap][c2][wave 4][lane][j] = W2[tap][16 c2 + 4 lg + j][16 wave + lr]
+//   bwd [wave 8][tap][lane][j]     = W2[tap][16 (wave & 1) + lr][16 (wave >> 1) + 4 lg + j]
+constexpr int W2F_F4 = 12800;                     // float4 per copy
+constexpr int W2F_BLOCKS_Y = 7;                   // extra grid rows of the conv1 launch (4 x 7 blocks)
+__device__ __forceinline__ void f32_w2_frag_block(int blk, const float* __restrict__ w2, float* __restrict__ w2f) {
+  float4* out = reinterpret_cast<float4*>(w2f);
+  for (int i = blk * 256 + (int)threadIdx.x; i < 2 * W2F_F4; i += 4 * W2F_BLOCKS_Y * 256) {
+    float4 v;
+    if (i < W2F_F4) {
+      const int lane = i & 63, wave = (i >> 6) & 3, c2 = (i >> 8) & 1, tap = i >> 9;
+      const float* q = w2 + tap * 2048 + (16 * c2 + 4 * (lane >> 4)) * 64 + 16 * wave + (lane & 15);
+      v = make_float4(q[0], q[64], q[128], q[192]);
+    } else {
+      const int k = i - W2F_F4, lane = k & 63, tap = (k >> 6) % 25, wave = (k >> 6) / 25;
+      v = *reinterpret_cast<const float4*>(w2 + tap * 2048 + (16 * (wave & 1) + (lane & 15)) * 64 +
+                                           16 * (wave >> 1) + 4 * (lane >> 4));
+    }
+    out[i] = v;
+  }
+}
+
 __global__ void __launch_bounds__(256) f32_conv1_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ a1, uint8_t* __restrict__ idx1,
-    int B) {
+    int B, const float* __restrict__ w2, float* __restrict__ w2f) {
   __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
+  if ((int)blockIdx.y >= B) {
+    f32_w2_frag_block(((int)blockIdx.y - B) * 4 + (int)blockIdx.x, w2, w2f);
+    return;
+  }
   f32_conv1_block<false>(blockIdx.x, blockIdx.y, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim);
 }
 
@@ -226,10 +257,12 @@ __device__ __forceinline__ void c2f_conv1_stage(const C1Fuse& c1, float* img, fl
 // PREW: the W2 register operand is issued right behind the staging writes and the barrier orders
 // LDS alone, so the 200 KB per block of W2 loads overlap the barrier wait and the first taps.
 // FUSE1: the a1 rows are computed from x in the block (conv1 fused, C1Fuse) instead of loaded.
-template <int TPB, bool TAIL, bool PREW = false, bool FUSE1 = false, int DEPTH = 2>
+// FRAG: the W2 operand from the fragment copy (f32_w2_frag_block): 50 float4 loads per lane.
+template <int TPB, bool TAIL, bool PREW = false, bool FUSE1 = false, int DEPTH = 2, bool FRAG = false>
 __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, float* __restrict__ a2,
-                                                            uint8_t* __restrict__ idx2, int B, F32Adam ad, C1Fuse c1) {
+                                                            uint8_t* __restrict__ idx2, int B, F32Adam ad, C1Fuse c1,
+                                                            const float* __restrict__ w2f) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   if constexpr (TAIL) {
     if ((int)blockIdx.x < ad.nblk) {
@@ -288,12 +321,24 @@ __global__ void __launch_bounds__(256) f32_conv2_fwd_kernel(const float* __restr
   float wb[200];  // wb[8 tap + 4 c2 + j] = W2[tap][16 c2 + 4 lg + j][16 w + lr]
   const float* wp = w2 + (4 * lg) * 64 + 16 * wave + lr;
   auto load_w = [&]() {
+    if constexpr (FRAG) {
+      const float4* fp = reinterpret_cast<const float4*>(w2f) + wave * 64 + lane;
 #pragma unroll
-    for (int tap = 0; tap < 25; ++tap)
+      for (int s2 = 0; s2 < 50; ++s2) {
+        const float4 v = fp[s2 * 256];
+        wb[4 * s2 + 0] = v.x;
+        wb[4 * s2 + 1] = v.y;
+        wb[4 * s2 + 2] = v.z;
+        wb[4 * s2 + 3] = v.w;
+      }
+    } else {
 #pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2)
+      for (int tap = 0; tap < 25; ++tap)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wb[8 * tap + 4 * c2 + j] = wp[tap * 2048 + (16 * c2 + j) * 64];
+        for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wb[8 * tap + 4 * c2 + j] = wp[tap * 2048 + (16 * c2 + j) * 64];
+    }
   };
   if constexpr (PREW) {
     __builtin_amdgcn_sched_barrier(0);
@@ -732,7 +777,8 @@ static const int* rows_ptr(const c10::optional<at::Tensor>& rows, int n_pool, in
 }
 
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                   const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1) {
+                   const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag) {
   const int B = a1.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv1_fwd: batch 1..128");
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv1_fwd: x");
@@ -744,9 +790,15 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
   const int* rp = rows_ptr(rows, n_pool, B, "f32_conv1_fwd");
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  f32_conv1_kernel<<<dim3(4, B), 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(),
-                                                   b1.data_ptr<float>(), a1.data_ptr<float>(),
-                                                   idx1.data_ptr<uint8_t>(), B);
+  // with w2 and w2frag: 4 x 7 more blocks write the W2 fragment copies for the conv2 launches
+  const bool frag = w2.has_value() && w2->defined() && w2frag.has_value() && w2frag->defined();
+  if (frag) {
+    check_f32(*w2, 51200, "f32_conv1_fwd: w2");
+    check_f32(*w2frag, 2 * 51200, "f32_conv1_fwd: w2frag [2][51200]");
+  }
+  f32_conv1_kernel<<<dim3(4, B + (frag ? W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
+      x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(), b1.data_ptr<float>(), a1.data_ptr<float>(),
+      idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr);
 }
 
 // tiles per block of f32_conv2_fwd for batch B (about one block per CU), and the block count
@@ -792,15 +844,21 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
                                const c10::optional<at::Tensor>& g3, const c10::optional<at::Tensor>& m3,
                                const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr,
                                double beta1, double beta2, double eps, double grad_scale, int64_t rule,
-                               int64_t tail_blocks, const C1Fuse& c1);
+                               int64_t tail_blocks, const C1Fuse& c1, const float* w2f);
 
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
                    const c10::optional<at::Tensor>& p3, const c10::optional<at::Tensor>& g3,
                    const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
                    const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
-                   double grad_scale, int64_t rule, int64_t tail_blocks) {
+                   double grad_scale, int64_t rule, int64_t tail_blocks, const c10::optional<at::Tensor>& w2frag) {
+  const float* w2f = nullptr;
+  if (w2frag.has_value() && w2frag->defined()) {
+    TORCH_CHECK(w2frag->is_cuda() && w2frag->dtype() == at::kFloat && w2frag->is_contiguous() &&
+                    w2frag->numel() >= 51200, "f32_conv2_fwd: w2frag (the forward fragment copy, 51200 floats)");
+    w2f = w2frag->data_ptr<float>();
+  }
   f32_conv2_fwd_impl(a1, w2, b2, a2, idx2, p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule, tail_blocks,
-                     C1Fuse{});
+                     C1Fuse{}, w2f);
 }
 
 // conv1 + conv2 forward in one launch: every conv2 block computes the a1 rows it reads from x (see
@@ -825,7 +883,7 @@ void f32_conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, 
   c1.a1 = a1.data_ptr<float>();
   c1.idx1 = idx1.data_ptr<uint8_t>();
   f32_conv2_fwd_impl(a1, w2, b2, a2, idx2, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, 0.0,
-                     0.0, 0.0, 0.0, 1.0, 0, 0, c1);
+                     0.0, 0.0, 0.0, 1.0, 0, 0, c1, nullptr);
 }
 
 static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2,
@@ -833,7 +891,7 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
                                const c10::optional<at::Tensor>& g3, const c10::optional<at::Tensor>& m3,
                                const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr,
                                double beta1, double beta2, double eps, double grad_scale, int64_t rule,
-                               int64_t tail_blocks, const C1Fuse& c1) {
+                               int64_t tail_blocks, const C1Fuse& c1, const float* w2f) {
   const bool fuse1 = c1.x != nullptr;
   const int B = a2.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv2_fwd: batch 1..128");
@@ -862,7 +920,7 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
   auto launch = [&](auto kern, int extra) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nblk + extra, 256, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
-                                                 a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, ad, c1);
+                                                 a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, ad, c1, w2f);
   };
   // MIHVD_F32_C2F_PREW=1: the W2 operand issued before the staging barrier (LDS-only barrier)
   // instead of after it. Measured slower standalone (21.0 vs 19.6 us: the 200 KB of W2 per block
@@ -878,6 +936,7 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
     else if (fuse1) launch(f32_conv2_fwd_kernel<T, false, true, true>, 0);           \
     else if (prew) launch(f32_conv2_fwd_kernel<T, false, true>, 0);                  \
     else if (shallow) launch(f32_conv2_fwd_kernel<T, false, false, false, 1>, 0);    \
+    else if (w2f) launch(f32_conv2_fwd_kernel<T, false, false, false, 2, true>, 0);  \
     else launch(f32_conv2_fwd_kernel<T, false>, 0);                                  \
     break;
   switch (tpb) {
@@ -891,6 +950,7 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
       if (ad.nblk > 0) launch(f32_conv2_fwd_kernel<7, true>, ad.nblk);
       else if (fuse1) launch(f32_conv2_fwd_kernel<7, false, true, true>, 0);
       else if (prew) launch(f32_conv2_fwd_kernel<7, false, true>, 0);
+      else if (w2f) launch(f32_conv2_fwd_kernel<7, false, false, false, 2, true>, 0);
       else launch(f32_conv2_fwd_kernel<7, false>, 0);
   }
 #undef C2F_CASE

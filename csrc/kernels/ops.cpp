@@ -84,12 +84,13 @@ void multi_tensor_sgd(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std:
                       double grad_scale);
 void bump_step_(at::Tensor& step);
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                   const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1);
+                   const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag);
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
                    const c10::optional<at::Tensor>& p3, const c10::optional<at::Tensor>& g3,
                    const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
                    const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
-                   double grad_scale, int64_t rule, int64_t tail_blocks);
+                   double grad_scale, int64_t rule, int64_t tail_blocks, const c10::optional<at::Tensor>& w2frag);
 void f32_conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                     const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1, const at::Tensor& w2,
                     const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
@@ -108,7 +109,7 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
                  double beta2, double eps, double grad_scale, int64_t rule, bool store_w3);
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                   at::Tensor& cpart, at::Tensor& slab);
+                   at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag);
 void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,
                      at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const c10::optional<at::Tensor>& params,
                      const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
@@ -290,14 +291,15 @@ void mt_sgd_op(at::TensorList p, at::TensorList g, at::TensorList bufs, double l
 }
 void bump_step_op(Tensor step) { mihvd::bump_step_(step); }
 void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
-                  Tensor idx1) {
-  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1);
+                  Tensor idx1, const OptT& w2, const OptT& w2frag) {
+  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag);
 }
 void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& p3,
                   const OptT& g3, const OptT& m3, const OptT& v3, const OptT& state, double lr, double beta1,
-                  double beta2, double eps, double grad_scale, int64_t rule, int64_t tail_blocks) {
+                  double beta2, double eps, double grad_scale, int64_t rule, int64_t tail_blocks,
+                  const OptT& w2frag) {
   mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule,
-                       tail_blocks);
+                       tail_blocks, w2frag);
 }
 void f32_conv12_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
                    Tensor idx1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2) {
@@ -321,8 +323,8 @@ void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, cons
                      grad_scale, rule, store_w3);
 }
 void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, const Tensor& idx1, const Tensor& x,
-                      const OptT& rows, const OptT& state, Tensor cpart, Tensor slab) {
-  mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab);
+                      const OptT& rows, const OptT& state, Tensor cpart, Tensor slab, const OptT& w2frag) {
+  mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab, w2frag);
 }
 void f32_conv_reduce_op(const Tensor& slab, const Tensor& cpart, const Tensor& db2p, Tensor gW2, Tensor gW1, Tensor gb1,
                         Tensor gb2, const OptT& params, const OptT& grads, const OptT& m, const OptT& v,
@@ -396,10 +398,11 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("multi_tensor_sgd(Tensor(a!)[] p, Tensor[] g, Tensor(b!)[] bufs, float lr, float momentum, float dampening, "
         "float weight_decay, bool nesterov, bool first, float grad_scale) -> ()");
   m.def("bump_step_(Tensor(a!) step) -> ()");
-  m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
+  m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
+        "Tensor? w2=None, Tensor(f!)? w2frag=None) -> ()");
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor(c!)? p3=None, "
         "Tensor? g3=None, Tensor(d!)? m3=None, Tensor(e!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., "
-        "float beta2=0., float eps=0., float grad_scale=1., int rule=0, int tail_blocks=0) -> ()");
+        "float beta2=0., float eps=0., float grad_scale=1., int rule=0, int tail_blocks=0, Tensor? w2frag=None) -> ()");
   m.def("f32_conv12_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
         "Tensor w2, Tensor b2, Tensor(c!) a2, Tensor(d!) idx2) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor(w!) w3, Tensor(a!) zpart, Tensor? g3=None, Tensor(m!)? m3=None, "
@@ -412,7 +415,7 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0, bool store_w3=True) -> ()");
   m.def("f32_conv2_bwd(Tensor dY2, Tensor w2, Tensor a1, Tensor idx1, Tensor x, Tensor? rows, Tensor? state, "
-        "Tensor(a!) cpart, Tensor(b!) slab) -> ()");
+        "Tensor(a!) cpart, Tensor(b!) slab, Tensor? w2frag=None) -> ()");
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
         "Tensor(d!) gb2, Tensor(e!)? params=None, Tensor? grads=None, Tensor(f!)? m=None, Tensor(g!)? v=None, "
         "Tensor(s!)? state=None, int o_w1=0, int o_b1=0, int o_w2=0, int o_b2=0, int fc_lo=0, int fc_hi=0, "

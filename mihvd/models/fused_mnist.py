@@ -326,6 +326,12 @@ class FusedMNISTTrainer:
         # block recomputes its halo rows and the conv2 MFMA loop starts later: 135.1 vs 132.4 us per
         # whole step (scripts/kbench_f32.py, profiles/r04/kbench_f32_r04c.txt)
         self.f32_conv12 = self.f32 and os.environ.get("MIHVD_F32_CONV12", "0") == "1"
+        # MIHVD_F32_W2F=1: the conv1 launch also writes two fragment copies of W2 (the register
+        # operands of conv2_fwd and of the conv2_bwd dgrad blocks, in the order their waves load them:
+        # one contiguous 1 KB per wave-load instead of scattered 64-byte row pieces), which both conv2
+        # launches of the step then read (csrc/kernels/f32_fwd.hip, f32_w2_frag_block)
+        self.w2frag = (torch.empty(2, 51200, device=dev, dtype=torch.float32)
+                       if self.f32 and os.environ.get("MIHVD_F32_W2F", "0") == "1" else None)
         self._c1_ready = False
         self._c1_sync = torch.zeros(4, device=dev, dtype=torch.int32) if self.f32 else None
         if self.f32:
@@ -356,7 +362,7 @@ class FusedMNISTTrainer:
                 self.dz = self.dz_all32[self.rank]  # head writes this rank's block in place
                 self.a2_send = torch.empty(N, B, R, **f32)
                 self.a2_recv = torch.empty(N, B, R, **f32)
-                self.f32_factor = self.shard_w3 and os.environ.get("MIHVD_F32_PLANE", "rs") == "factor
+                self.f32_factor = self.shard_w3 and os.environ.get("MIHVD_F32_PLANE", "rs") == "factor"
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
@@ -654,6 +660,7 @@ class FusedMNISTTrainer:
         if self.shard_w3:
             return self._launch_step_f32_shard(x, rows, labels)
         fused12 = self.f32_conv12 and not self._c1_ready and not (self._w3_pending and self.f32_w3 == "tail")
+        wf = None  # the W2 fragment copies, when this step's conv1 launch writes them
         if self._c1_ready:
             self._c1_ready = False  # the previous step's conv_reduce computed this step's conv1
         elif fused12:
@@ -661,7 +668,8 @@ class FusedMNISTTrainer:
                              self.idx1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
         else:
             o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                            self.idx1)
+                            self.idx1, *((w2, self.w2frag) if self.w2frag is not None else ()))
+            wf = self.w2frag
         if fused12:
             pass  # conv2 ran in the launch above
         elif self._w3_pending and self.f32_w3 == "tail":
@@ -672,7 +680,8 @@ class FusedMNISTTrainer:
                             self.rule, self.f32_tail_blocks)
             self._w3_pending = False
         else:
-            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
+            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2,
+                            w2frag=wf[0] if wf is not None else None)
         if self._w3_pending:
             # ... or inside fc1_fwd, W3's first reader: the update of each fragment in registers
             o.f32_fc1_fwd(self.a2, w3, self.zpart, self.grads[s3], self.m[s3], self.v[s3], st, self.lr, b1, b2,
@@ -705,7 +714,8 @@ class FusedMNISTTrainer:
             with torch.cuda.stream(self._side):
                 o.adam_step(self.params[s3], self.grads[s3], self.m[s3], self.v[s3], None, st, 0, self.lr, b1, b2,
                             self.eps, 1.0, self.rule, 0)
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab,
+                        w2frag=wf[1] if wf is not None else None)
         gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
                  G("conv_layer2/conv2d/bias"))
         if self.f32_fused_opt and not self.collectives:
@@ -753,13 +763,16 @@ class FusedMNISTTrainer:
         w2 = P("conv_layer2/conv2d/kernel")
         w3 = P("dense/kernel")
         R, r = self._f32_R, self.rank
+        wf = None
         if self.f32_conv12:
             o.f32_conv12_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
                              self.idx1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
         else:
             o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                            self.idx1)
-            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
+                            self.idx1, *((w2, self.w2frag) if self.w2frag is not None else ()))
+            wf = self.w2frag
+            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2,
+                            w2frag=wf[0] if wf is not None else None)
         if self._shadow_ev is not None:  # the previous step's W3 row gather
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None
@@ -782,7 +795,8 @@ class FusedMNISTTrainer:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 self._reduce_scatter_rows(gW3, self.gshard, R)
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab,
+                        w2frag=wf[1] if wf is not None else None)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
                           G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
         side.wait_stream(main)

@@ -74,6 +74,9 @@ def main():
     gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
              G("conv_layer2/conv2d/bias"))
     w2, w3 = P("conv_layer2/conv2d/kernel"), P("dense/kernel")
+    w2frag = torch.empty(2, 51200, device="cuda")
+    o.f32_conv1_fwd(tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1,
+                    w2, w2frag)
     fa8, fz8, fo8 = (torch.randn(8 * B, 392, device="cuda"), torch.randn(8 * B, 1024, device="cuda"),
                      torch.empty(392, 1024, device="cuda"))
     fa1, fz1, fo1 = (torch.randn(B, 3136, device="cuda"), torch.randn(B, 1024, device="cuda"),
@@ -100,6 +103,12 @@ def main():
                                                  G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"),
                                                  G("dense_1/bias"), tr.m[s3], tr.v[s3], st, 0.0, b1, b2, tr.eps, 1.0,
                                                  tr.rule, False),
+        "conv1_fwd [+ W2 fragment copies]": lambda: o.f32_conv1_fwd(
+            tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1, w2, w2frag),
+        "conv2_fwd [W2 fragment copy]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
+                                                                w2frag=w2frag[0]),
+        "conv2_bwd [W2 fragment copy]": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart,
+                                                                tr.slab, w2frag=w2frag[1]),
         "fc1_bwd [dgrad only: fp32 factor plane]": lambda: o.f32_fc1_bwd(
             tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"), G("dense/bias"),
             G("dense_1/kernel"), G("dense_1/bias"), store_w3=False),
@@ -215,6 +224,7 @@ def main():
         "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
         "whole step [fc1_bwd pinned dgrad MFMA order]": ({}, {"MIHVD_F32_F1R_PIN": "1"}),
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
+        "whole step [W2 fragment copies]": ({"w2frag": w2frag}, {}),
     }
     for name, (attrs, env) in steps.items():
         if not want(name):

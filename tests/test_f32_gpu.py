@@ -283,6 +283,68 @@ def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
     assert rel_err(gb2, db2p.sum(0)) < 1e-6
 
 
+@pytest.mark.parametrize("B", [7, 100])
+def test_f32_w2_fragment_copies(ops, B):
+    """MIHVD_F32_W2F: the conv1 launch's extra blocks write W2 in the load order of the conv2_fwd
+    waves ([tap][c2][wave][lane][j]) and of the conv2_bwd dgrad waves ([wave][tap][lane][j]); both
+    conv2 launches reading them produce bit-identical outputs to the HWIO reads."""
+    g = torch.Generator(device="cuda").manual_seed(15)
+    x = torch.rand(B, 784, device="cuda", generator=g)
+    w1 = torch.randn(800, device="cuda", generator=g) * 0.2
+    b1 = torch.randn(32, device="cuda", generator=g) * 0.1
+    w2 = torch.randn(25, 32, 64, device="cuda", generator=g) * 0.05
+    b2 = torch.randn(64, device="cuda", generator=g) * 0.1
+    a1, a1f = (torch.empty(B, 14, 14, 32, device="cuda") for _ in range(2))
+    idx1, idx1f = (torch.empty(B, 14, 14, 32, device="cuda", dtype=torch.uint8) for _ in range(2))
+    frag = torch.full((2, 51200), float("nan"), device="cuda")
+    ops.f32_conv1_fwd(x, None, None, w1, b1, a1, idx1)
+    ops.f32_conv1_fwd(x, None, None, w1, b1, a1f, idx1f, w2.view(-1), frag)
+    assert torch.equal(a1, a1f) and torch.equal(idx1, idx1f)
+    # [tap][c2][lg][j][wave][lr] -> [tap][c2][wave][lg][lr][j]; [tap][nt][lr][cq][lg][j] -> [cq][nt][tap][lg][lr][j]
+    ref_f = w2.view(25, 2, 4, 4, 4, 16).permute(0, 1, 4, 2, 5, 3).reshape(-1)
+    ref_b = w2.view(25, 2, 16, 4, 4, 4).permute(3, 1, 0, 4, 2, 5).reshape(-1)
+    assert torch.equal(frag[0], ref_f) and torch.equal(frag[1], ref_b)
+    a2, a2f = torch.empty(B, 3136, device="cuda"), torch.empty(B, 3136, device="cuda")
+    idx2, idx2f = (torch.empty(B, 3136, device="cuda", dtype=torch.uint8) for _ in range(2))
+    ops.f32_conv2_fwd(a1, w2.view(-1), b2, a2, idx2)
+    ops.f32_conv2_fwd(a1, w2.view(-1), b2, a2f, idx2f, w2frag=frag[0])
+    assert torch.equal(a2, a2f) and torch.equal(idx2, idx2f)
+    dY2 = torch.randn(B, 14, 14, 64, device="cuda", generator=g)
+    outs = []
+    for wf in (None, frag[1]):
+        cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, device="cuda")
+        slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, device="cuda")
+        ops.f32_conv2_bwd(dY2, w2.view(-1), a1, idx1, x, None, None, cpart, slab, w2frag=wf)
+        outs.append((cpart, slab))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_f32_trainer_w2_fragments_bitwise(ops, monkeypatch):
+    """Graph-replayed training steps with the W2 fragment copies (MIHVD_F32_W2F=1) equal the HWIO
+    reads bit for bit (W2 changes every step: the copies are rewritten by every conv1 launch)."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    (x, y), _ = synthetic_mnist(n_train=2000, n_test=10, seed=8)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    trs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("MIHVD_F32_W2F", flag)
+        tr = FusedMNISTTrainer(batch_size=100, lr=2e-3, seed=3, device="cuda", precision="fp32")
+        assert (tr.w2frag is not None) == (flag == "1")
+        tr.set_device_dataset(X, Y, seed=1)
+        tr.device_step()
+        tr.build_graph(steps_per_replay=5)
+        for _ in range(3):
+            tr.run_graph()
+        trs.append(tr)
+    torch.cuda.synchronize()
+    a, b = trs
+    for name in ("params", "m", "v", "state"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
 def _tf_adam_(p, grad, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
     """TF1 AdamOptimizer (tensorflow_mnist.py:130) in float64 on the host side of the test."""
     m.mul_(b1).add_(grad, alpha=1 - b1)

@@ -783,3 +783,23 @@ def test_captured_step_holds_the_parameters_accumulate_grad_nodes():
     loss2 = m(torch.randn(5, 8)).sum()
     used = {id(n) for n in accumulate_grad_nodes(loss2)}
     assert used == {id(n) for n in nodes}  # the held nodes, not new ones
+
+
+def test_every_python_source_compiles():
+    """Byte-compile every Python file of the package, the examples, the scripts and the tests: GPU-only
+    modules (the fused trainer, the kernel wrappers) are not imported by the CPU suite, so a syntax
+    error there would otherwise surface only on the GPU box."""
+    import glob
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = [f for d in ("mihvd", "examples", "scripts", "tests") for f in glob.glob(os.path.join(root, d, "**", "*.py"),
+                                                                                      recursive=True)]
+    files += [os.path.join(root, f) for f in ("bench.py", "__graft_entry__.py")]
+    bad = []
+    for f in files:
+        try:
+            with open(f, encoding="utf-8") as fh:
+                compile(fh.read(), f, "exec")
+        except SyntaxError as e:
+            bad.append(f"{f}: {e}")
+    assert len(files) > 50 and not bad, bad
