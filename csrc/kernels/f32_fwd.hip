@@ -542,7 +542,10 @@ __device__ __forceinline__ void f1f_mma(const float (&wa)[56], const float* __re
   }
 }
 
-template <int MT, bool ADAM>
+// SPLIT (no ADAM): the a2 slice is staged in two K halves of 112: the second half's loads (and its
+// W3 fragments) are in flight while the MFMAs of the first half issue, instead of every MFMA waiting
+// for the whole 100 KB slice.
+template <int MT, bool ADAM, bool SPLIT = false>
 __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restrict__ a2, float* __restrict__ w3,
                                                            float* __restrict__ zpart, int B, F32Adam ad) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
@@ -558,6 +561,66 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
   f32x4 acc[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (SPLIT) {
+    static_assert(!ADAM, "the split staging is the plain forward's");
+    constexpr int NCH2 = MT * 16 * 28, PER2 = (NCH2 + 511) / 512;  // one K half: 28 float4 per row
+    float4 v0[PER2], v1[PER2];
+    auto ld_half = [&](float4 (&v)[PER2], int h) {
+#pragma unroll
+      for (int it = 0; it < PER2; ++it) {
+        const int i = min(t + 512 * it, NCH2 - 1), r = i / 28, cc = 28 * h + i - 28 * r;
+        v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc), r < B);
+      }
+    };
+    auto st_half = [&](const float4 (&v)[PER2], int h) {
+#pragma unroll
+      for (int it = 0; it < PER2; ++it) {
+        const int i = t + 512 * it;
+        if (i < NCH2) {
+          const int r = i / 28, cc = 28 * h + i - 28 * r;
+          *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
+        }
+      }
+    };
+    const int64_t wo = (int64_t)(k0 + 4 * lg) * 1024 + n;
+    auto ld_w = [&](int q0, int q1) {
+#pragma unroll
+      for (int q = q0; q < q1; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wa[4 * q + j] = w3[wo + (16 * q + j) * 1024];
+    };
+    // issue order (pinned): a2 half 0, W3 q 0..6, a2 half 1, W3 q 7..13 — the in-order load counter
+    // then lets half 0's writes and MFMAs wait for their own operands only
+    ld_half(v0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    ld_w(0, 7);
+    __builtin_amdgcn_sched_barrier(0);
+    ld_half(v1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    ld_w(7, 14);
+    __builtin_amdgcn_sched_barrier(0);
+    st_half(v0, 0);
+    c2f_lds_barrier();
+    if (sh == 0)
+      f1f_mma<NT0, 0, 7>(wa, bp, acc);
+    else
+      f1f_mma<NT1, 0, 7>(wa, bp, acc);
+    st_half(v1, 1);  // K columns the first half's reads never touch
+    c2f_lds_barrier();
+    if (sh == 0)
+      f1f_mma<NT0, 7, 14>(wa, bp, acc);
+    else
+      f1f_mma<NT1, 7, 14>(wa, bp, acc);
+    const int ntl = sh == 0 ? NT0 : NT1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int tt = sh + 2 * u, m = tt * 16 + lr;
+      if (u < ntl && m < B)
+        *reinterpret_cast<float4*>(zpart + ((int64_t)ks * B + m) * 1024 + nb * 64 + nt * 16 + 4 * lg) =
+            make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+    }
+    return;
+  }
   float4 v[PER];
 #pragma unroll
   for (int it = 0; it < PER; ++it) {
@@ -978,9 +1041,12 @@ void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const 
   };
   // MIHVD_F32_F1F=0 selects the earlier form (whole-tile update, then the MFMAs) for comparison
   const bool v2 = env_knob("MIHVD_F32_F1F", 1) != 0;
+  // MIHVD_F32_F1F_SPLIT=1: the plain forward stages the a2 slice in two K halves (SPLIT above)
+  const bool split = v2 && ad.nblk == 0 && env_knob("MIHVD_F32_F1F_SPLIT", 0) != 0;
 #define F1F_CASE(T)                                                                                 \
   case T:                                                                                           \
     if (ad.nblk > 0) v2 ? launch(f32_fc1_fwd2_kernel<T, true>) : launch(f32_fc1_fwd_kernel<T, true>); \
+    else if (split) launch(f32_fc1_fwd2_kernel<T, false, true>);                                     \
     else v2 ? launch(f32_fc1_fwd2_kernel<T, false>) : launch(f32_fc1_fwd_kernel<T, false>);           \
     break;
   switch (mt) {
@@ -992,7 +1058,8 @@ void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const 
     F1F_CASE(6)
     F1F_CASE(7)
     default:
-      v2 ? launch(f32_fc1_fwd2_kernel<8, false>) : launch(f32_fc1_fwd_kernel<8, false>);
+      if (split) launch(f32_fc1_fwd2_kernel<8, false, true>);
+      else v2 ? launch(f32_fc1_fwd2_kernel<8, false>) : launch(f32_fc1_fwd_kernel<8, false>);
   }
 #undef F1F_CASE
 }

@@ -326,12 +326,14 @@ class FusedMNISTTrainer:
         # block recomputes its halo rows and the conv2 MFMA loop starts later: 135.1 vs 132.4 us per
         # whole step (scripts/kbench_f32.py, profiles/r04/kbench_f32_r04c.txt)
         self.f32_conv12 = self.f32 and os.environ.get("MIHVD_F32_CONV12", "0") == "1"
-        # MIHVD_F32_W2F=1: the conv1 launch also writes two fragment copies of W2 (the register
-        # operands of conv2_fwd and of the conv2_bwd dgrad blocks, in the order their waves load them:
-        # one contiguous 1 KB per wave-load instead of scattered 64-byte row pieces), which both conv2
-        # launches of the step then read (csrc/kernels/f32_fwd.hip, f32_w2_frag_block)
+        # MIHVD_F32_W2F=1 (default): the conv1 launch also writes two fragment copies of W2 (the
+        # register operands of conv2_fwd and of the conv2_bwd dgrad blocks, in the order their waves
+        # load them: one contiguous 1 KB per wave-load instead of scattered 64-byte row pieces), which
+        # both conv2 launches of the step then read (csrc/kernels/f32_fwd.hip, f32_w2_frag_block).
+        # Measured (B = 100): conv2_fwd 21.2 -> 19.8 us, conv2_bwd 43.8 -> 40.5 us, conv1 unchanged,
+        # whole step 124.7 -> 122.4 us (profiles/r04/kbench_f32_r04m.txt); bitwise equal
         self.w2frag = (torch.empty(2, 51200, device=dev, dtype=torch.float32)
-                       if self.f32 and os.environ.get("MIHVD_F32_W2F", "0") == "1" else None)
+                       if self.f32 and os.environ.get("MIHVD_F32_W2F", "1") != "0" else None)
         self._c1_ready = False
         self._c1_sync = torch.zeros(4, device=dev, dtype=torch.int32) if self.f32 else None
         if self.f32:

@@ -186,6 +186,7 @@ def main():
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
         "fc1_fwd [earlier form]": ({"MIHVD_F32_F1F": "0"}, ks["fc1_fwd"]),
+        "fc1_fwd [a2 staged in two K halves]": ({"MIHVD_F32_F1F_SPLIT": "1"}, ks["fc1_fwd"]),
         "fc1_fwd+W3 adam [earlier form]": ({"MIHVD_F32_F1F": "0"}, ks["fc1_fwd+W3 adam"]),
 
     }
@@ -224,7 +225,8 @@ def main():
         "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
         "whole step [fc1_bwd pinned dgrad MFMA order]": ({}, {"MIHVD_F32_F1R_PIN": "1"}),
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
-        "whole step [W2 fragment copies]": ({"w2frag": w2frag}, {}),
+        "whole step [W2 read as HWIO (no fragment copies)]": ({"w2frag": None}, {}),
+        "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
     }
     for name, (attrs, env) in steps.items():
         if not want(name):

@@ -101,8 +101,8 @@ def test_f32_conv12_fwd_matches_separate_launches(ops, B):
     assert rel_err(outs[0][2], ref2.reshape(B, 3136)) < 1e-5
 
 
-@pytest.mark.parametrize("B", [7, 100])
-def test_f32_fc1_fwd_and_head(ops, B):
+@pytest.mark.parametrize("B", [7, 100, 128])
+def test_f32_fc1_fwd_and_head(ops, B, monkeypatch):
     g = torch.Generator(device="cuda").manual_seed(3)
     a2 = torch.rand(B, 3136, device="cuda", generator=g)
     w3 = torch.randn(3136, 1024, device="cuda", generator=g) * 0.02
@@ -110,6 +110,14 @@ def test_f32_fc1_fwd_and_head(ops, B):
     ops.f32_fc1_fwd(a2, w3, zpart)
     z = a2.double() @ w3.double()
     assert rel_err(zpart.sum(0), z) < 1e-6
+    # the K-split staging (MIHVD_F32_F1F_SPLIT=1): the same products in the same order per slab
+    monkeypatch.setenv("MIHVD_F32_F1F_SPLIT", "1")
+    zs = torch.full_like(zpart, float("nan"))
+    ops.f32_fc1_fwd(a2, w3, zs)
+    monkeypatch.delenv("MIHVD_F32_F1F_SPLIT")
+    assert torch.equal(zs, zpart)
+    if B > 112:
+        return  # (the head's checks below at the two smaller batches)
     b3 = torch.randn(1024, device="cuda", generator=g) * 0.1
     w4 = torch.randn(1024, 10, device="cuda", generator=g) * 0.05
     b4 = torch.randn(10, device="cuda", generator=g) * 0.1
