@@ -110,6 +110,10 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag);
+void f32_factor_rows(const at::Tensor& a2c, const at::Tensor& dz, const c10::optional<at::Tensor>& out,
+                     const c10::optional<at::Tensor>& p, const c10::optional<at::Tensor>& m,
+                     const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, double lr,
+                     double beta1, double beta2, double eps, double grad_scale, int64_t rule);
 void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,
                      at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const c10::optional<at::Tensor>& params,
                      const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
@@ -326,6 +330,11 @@ void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, con
                       const OptT& rows, const OptT& state, Tensor cpart, Tensor slab, const OptT& w2frag) {
   mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab, w2frag);
 }
+void f32_factor_rows_op(const Tensor& a2c, const Tensor& dz, const OptT& out, const OptT& p, const OptT& m,
+                        const OptT& v, const OptT& state, double lr, double beta1, double beta2, double eps,
+                        double grad_scale, int64_t rule) {
+  mihvd::f32_factor_rows(a2c, dz, out, p, m, v, state, lr, beta1, beta2, eps, grad_scale, rule);
+}
 void f32_conv_reduce_op(const Tensor& slab, const Tensor& cpart, const Tensor& db2p, Tensor gW2, Tensor gW1, Tensor gb1,
                         Tensor gb2, const OptT& params, const OptT& grads, const OptT& m, const OptT& v,
                         const OptT& state, int64_t o_w1, int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo,
@@ -414,6 +423,9 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4, Tensor(m!)? m3=None, "
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0, bool store_w3=True) -> ()");
+  m.def("f32_factor_rows(Tensor a2c, Tensor dz, Tensor(a!)? out=None, Tensor(b!)? p=None, Tensor(c!)? m=None, "
+        "Tensor(d!)? v=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
+        "float grad_scale=1., int rule=0) -> ()");
   m.def("f32_conv2_bwd(Tensor dY2, Tensor w2, Tensor a1, Tensor idx1, Tensor x, Tensor? rows, Tensor? state, "
         "Tensor(a!) cpart, Tensor(b!) slab, Tensor? w2frag=None) -> ()");
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
@@ -467,6 +479,7 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("multi_tensor_sgd", &mt_sgd_op);
   m.impl("bump_step_", &bump_step_op);
   m.impl("f32_conv1_fwd", &f32_conv1_op);
+  m.impl("f32_factor_rows", &f32_factor_rows_op);
   m.impl("f32_conv2_fwd", &f32_conv2_op);
   m.impl("f32_conv12_fwd", &f32_conv12_op);
   m.impl("f32_fc1_fwd", &f32_fc1_fwd_op);

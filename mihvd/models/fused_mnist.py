@@ -782,15 +782,9 @@ class FusedMNISTTrainer:
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         gW3 = G("dense/kernel")
+        mine = slice(W3_START + r * R * 1024, W3_START + (r + 1) * R * 1024)
         if self.f32_factor:
-            # the factors of every rank (dz: all-gather; a2: this rank's R columns from each rank)
-            # and this rank's dW3 rows over all N B samples, beside fc1_bwd's dgrad and the conv
-            # backward
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                self._f32_factor_rows(R)
-            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
-                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
+            return self._launch_step_f32_factor(x, rows, st, w2, wf, gW3, R, mine)
         else:
             o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
                           G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
@@ -807,7 +801,6 @@ class FusedMNISTTrainer:
         main.wait_stream(side)
         o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START], None, st, 0,
                     self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-        mine = slice(W3_START + r * R * 1024, W3_START + (r + 1) * R * 1024)
         o.adam_step(self.params[mine], self.gshard.view(-1), self.m[mine], self.v[mine], None, st, 0, self.lr, b1, b2,
                     self.eps, 1.0 / self.world, self.rule, 0)
         side.wait_stream(main)
@@ -818,13 +811,49 @@ class FusedMNISTTrainer:
             self._shadow_ev.record(side)
         self._full_state_valid = False
 
-    def _f32_factor_rows(self, R):
-        """gshard = this rank's R rows of dW3 summed over every rank's samples, from the gathered
-        factors (fp32 factor-gather plane, mihvd/parallel/factor.py; runs on the side stream)."""
-        from ..parallel.factor import factor_rows_
+    def _launch_step_f32_factor(self, x, rows, st, w2, wf, gW3, R, mine):
+        """The rest of the fp32 step on the factor-gather plane (after the head):
 
-        factor_rows_(self.gshard, self.a2, self.dz, self.dz_all32, self.a2_send, self.a2_recv, self.rank, self.world,
-                     self.ncomm)
+            main: fc1_bwd (dgrad only) | conv2_bwd reduce |        Adam (small)
+            side:  exchange (a2 A2A, dz AG) | dW3 rows + Adam |  AR(small) | AG(W3 rows) -> next step
+
+        Everything about dense/kernel runs on the side stream: the factor exchange from the head on,
+        this rank's dW3 rows over all N B samples with their Adam update from the accumulators
+        (csrc/kernels/f32_factor.hip, once fc1_bwd, the step's last reader of W3, is done), and the
+        row all-gather, which the next step's fc1_fwd joins. The side stream's collectives keep one
+        order on every rank (one communicator, one stream)."""
+        from ..parallel.factor import factor_exchange_
+
+        o, P, G = self.ops, self.pview, self.gview
+        main, side = torch.cuda.current_stream(self.device), self._side
+        b1, b2 = self.betas
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            factor_exchange_(self.a2, self.dz, self.dz_all32, self.a2_send, self.a2_recv, self.rank, self.world,
+                             self.ncomm)
+        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, P("dense/kernel"), self.dY2, self.db2p, gW3,
+                      G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            o.f32_factor_rows(self.a2_recv, self.dz_all32, self.gshard if self.keep_w3_grad else None,
+                              self.params[mine], self.m[mine], self.v[mine], st, self.lr, b1, b2, self.eps,
+                              1.0 / self.world, self.rule)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab,
+                        w2frag=wf[1] if wf is not None else None)
+        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
+                          G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._allreduce(self.grads[:W3_START], 0, W3_START)
+        main.wait_stream(side)
+        o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START], None, st, 0,
+                    self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+        with torch.cuda.stream(side):
+            p3 = self.params[W3_START:].view(3136, 1024)
+            self._all_gather_rows(p3, p3[self.rank * R:(self.rank + 1) * R])
+            self._shadow_ev = torch.cuda.Event()
+            self._shadow_ev.record(side)
+        self._full_state_valid = False
 
     def _reduce_scatter_rows(self, full, out, R):
         """out = this rank's R rows of the sum over ranks of ``full`` (rows x 1024)."""

@@ -19,14 +19,12 @@ import torch
 import torch.distributed as dist
 
 
-def factor_rows_(out: torch.Tensor, a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor,
-                 a2_send: torch.Tensor, a2_recv: torch.Tensor, rank: int, world: int, comm=None) -> torch.Tensor:
-    """out[R][1024] = rows [rank R, (rank + 1) R) of sum over ranks of a2_q^T dz_q.
-
-    ``dz`` must be block ``rank`` of ``dz_all`` ([world][B][1024], gathered in place); ``a2_send`` /
-    ``a2_recv`` are [world][B][R] scratch. ``comm``: a :class:`mihvd.parallel.rccl.NativeComm` (the
-    collectives then run on the current HIP stream), else the default process group (nccl, or host
-    collectives such as gloo). Collective: every rank calls it."""
+def factor_exchange_(a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor, a2_send: torch.Tensor,
+                     a2_recv: torch.Tensor, rank: int, world: int, comm=None):
+    """The factor exchange alone: dz_all <- every rank's dz (all-gather; ``dz`` is block ``rank`` of
+    ``dz_all``), a2_recv[j] <- rank j's a2 columns of this rank's rows (all-to-all of [world][B][R]).
+    ``comm``: a :class:`mihvd.parallel.rccl.NativeComm` (the collectives then run on the current HIP
+    stream), else the default process group (nccl, or host collectives such as gloo). Collective."""
     N = world
     B = a2.shape[0]
     R = a2.shape[1] // N
@@ -45,7 +43,17 @@ def factor_rows_(out: torch.Tensor, a2: torch.Tensor, dz: torch.Tensor, dz_all: 
         for j in range(N):
             a2_recv[j].copy_(sends[j][rank])
         dist.all_gather(list(dz_all.unbind(0)), dz.clone())
+
+
+def factor_rows_(out: torch.Tensor, a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor,
+                 a2_send: torch.Tensor, a2_recv: torch.Tensor, rank: int, world: int, comm=None) -> torch.Tensor:
+    """out[R][1024] = rows [rank R, (rank + 1) R) of sum over ranks of a2_q^T dz_q: the exchange, then
+    one GEMM (the reference formulation; the trainer runs ``csrc/kernels/f32_factor.hip`` instead,
+    which applies Adam to the rows from the accumulators). Collective: every rank calls it."""
+    factor_exchange_(a2, dz, dz_all, a2_send, a2_recv, rank, world, comm)
+    N, B = world, a2.shape[0]
+    R = a2.shape[1] // N
     return torch.mm(a2_recv.view(N * B, R).t(), dz_all.view(N * B, dz_all.shape[-1]), out=out)
 
 
-__all__ = ["factor_rows_"]
+__all__ = ["factor_exchange_", "factor_rows_"]

@@ -81,6 +81,8 @@ def main():
                      torch.empty(392, 1024, device="cuda"))
     fa1, fz1, fo1 = (torch.randn(B, 3136, device="cuda"), torch.randn(B, 1024, device="cuda"),
                      torch.empty(3136, 1024, device="cuda"))
+    fp8, fm8, fv8 = (torch.zeros(392, 1024, device="cuda") for _ in range(3))
+    fp1, fm1, fv1 = (torch.zeros(3136, 1024, device="cuda") for _ in range(3))
     # lr 0 keeps the weights fixed while the optimizer kernels are timed
     ks = {
         "conv1_fwd": lambda: o.f32_conv1_fwd(tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"),
@@ -115,6 +117,10 @@ def main():
         # the factor plane's dW3-row GEMM at N = 8 (392 rows x 800 samples x 1024) and N = 1
         "factor GEMM N=8 (392x800x1024)": lambda: torch.mm(fa8.t(), fz8, out=fo8),
         "factor GEMM N=1 (3136x100x1024)": lambda: torch.mm(fa1.t(), fz1, out=fo1),
+        "factor rows + Adam N=8 (HIP)": lambda: o.f32_factor_rows(fa8, fz8, None, fp8, fm8, fv8, st, 0.0, b1, b2,
+                                                                  tr.eps, 0.125, tr.rule),
+        "factor rows + Adam N=1 (HIP)": lambda: o.f32_factor_rows(fa1, fz1, None, fp1, fm1, fv1, st, 0.0, b1, b2,
+                                                                  tr.eps, 1.0, tr.rule),
         "conv2_bwd": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab),
         "conv_reduce": lambda: o.f32_conv_reduce(tr.slab, tr.cpart, tr.db2p, *gconv),
         "conv_reduce+adam": lambda: o.f32_conv_reduce(

@@ -33,12 +33,13 @@ MB = 1e6
 
 # kernel-name regex -> (label, GFLOP, MB, what)
 WORK = [
-    (r"f32_conv2_fwd_kernel<[^>]*true>", "conv12_fwd", CONV1_GF + CONV2_GF,
+    (r"f32_conv2_fwd_kernel<\d+, false, true, true", "conv12_fwd", CONV1_GF + CONV2_GF,
      (B * 784 * F + B * 6272 * (F + 1) + B * 3136 * (F + 1) + 51200 * F + 800 * F) / MB,
      "conv1 + conv2 forward, bias/ReLU/pool/argmax fused (one launch)"),
     (r"f32_conv2_fwd_kernel", "conv2_fwd", CONV2_GF,
      (B * 6272 * F + B * 3136 * (F + 1) + 51200 * F) / MB, "conv2 forward, bias/ReLU/pool/argmax fused"),
-    (r"f32_conv1_kernel", "conv1_fwd", CONV1_GF, (B * 784 * F + B * 6272 * (F + 1)) / MB, "conv1 forward"),
+    (r"f32_conv1_kernel", "conv1_fwd", CONV1_GF, (B * 784 * F + B * 6272 * (F + 1) + 3 * 51200 * F) / MB,
+     "conv1 forward (+ the two W2 fragment copies)"),
     (r"f32_fc1_fwd2?_kernel<\d+, true>", "fc1_fwd+W3 adam", FC1_GF,
      (W3 * F * 7 + B * 3136 * F + 14 * B * 1024 * F) / MB, "fc1 split-K x14 + the deferred W3 Adam (p,g,m,v)"),
     (r"f32_fc1_fwd2?_kernel", "fc1_fwd", FC1_GF, (W3 * F + B * 3136 * F + 14 * B * 1024 * F) / MB, "fc1 split-K x14"),
@@ -114,6 +115,27 @@ def main():
         print(f"\nMeasured step (bench.py, graph-replayed, barrier + synchronize around the timed loop): "
               f"**{us:.1f} µs**; kernel sum {tot_us:.1f} µs, so {max(0.0, us - tot_us):.1f} µs of launch gaps. "
               f"Sum of per-kernel floors {floor_sum:.1f} µs ({100 * floor_sum / us:.0f}% of the step).")
+    # launch gaps of the graph-replayed steady state: start of each kernel minus the end of the
+    # kernel before it (same queue), by boundary
+    seq = [r for r in win if classify(r["Kernel_Name"]) is not None]
+    gaps = {}
+    for a, b in zip(seq, seq[1:]):
+        la, lb = classify(a["Kernel_Name"])[0], classify(b["Kernel_Name"])[0]
+        g = (int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3
+        if g < 50:  # (a replay boundary or a host gap is not a launch gap)
+            gaps.setdefault((la, lb), []).append(g)
+    if gaps:
+        print("\nLaunch gaps between consecutive kernels (median µs, start of the next minus end of the previous):\n")
+        print("| boundary | gap µs | count |")
+        print("|---|---|---|")
+        tot = 0.0
+        for (la, lb), v in sorted(gaps.items(), key=lambda kv: -len(kv[1])):
+            if len(v) < 0.5 * steps:
+                continue
+            m = statistics.median(v)
+            tot += m
+            print(f"| `{la}` -> `{lb}` | {m:.2f} | {len(v)} |")
+        print(f"| **per step** | {tot:.2f} | |")
     if skipped:
         print("\nFiltered out (start-up / warm-up / not once per step): " +
               ", ".join(f"`{n}` ×{k}" for n, k in skipped[:12]))

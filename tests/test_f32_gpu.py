@@ -353,6 +353,30 @@ def test_f32_trainer_w2_fragments_bitwise(ops, monkeypatch):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
 
 
+@pytest.mark.parametrize("NB,R", [(800, 392), (100, 3136), (200, 784), (7, 448), (350, 392)])
+def test_f32_factor_rows_kernel(ops, NB, R):
+    """The fp32 factor plane's dW3 rows (csrc/kernels/f32_factor.hip): a2c^T dz over all NB samples
+    against fp64, and the fused Adam equal (bit for bit) to adam_step on the stored rows."""
+    g = torch.Generator(device="cuda").manual_seed(NB + R)
+    a2c = torch.relu(torch.randn(NB, R, device="cuda", generator=g))
+    dz = torch.randn(NB, 1024, device="cuda", generator=g) * 0.01
+    out = torch.full((R, 1024), float("nan"), device="cuda")
+    p = torch.randn(R, 1024, device="cuda", generator=g) * 0.02
+    m = torch.randn(R, 1024, device="cuda", generator=g).abs() * 1e-3
+    v = torch.randn(R, 1024, device="cuda", generator=g).abs() * 1e-5
+    st = torch.tensor([5, 7, 0, 0], device="cuda", dtype=torch.int64)
+    pf, mf, vf = p.clone(), m.clone(), v.clone()
+    ops.f32_factor_rows(a2c, dz, out, pf, mf, vf, st, 1e-3, 0.9, 0.999, 1e-8, 0.125, 0)
+    assert rel_err(out, a2c.double().t() @ dz.double()) < 1e-6
+    ps, ms, vs = p.clone(), m.clone(), v.clone()
+    ops.adam_step(ps.view(-1), out.view(-1), ms.view(-1), vs.view(-1), None, st, 0, 1e-3, 0.9, 0.999, 1e-8, 0.125, 0, 0)
+    assert torch.equal(pf, ps) and torch.equal(mf, ms) and torch.equal(vf, vs)
+    # Adam only (the production launch): the same update without the stored rows
+    pa, ma, va = p.clone(), m.clone(), v.clone()
+    ops.f32_factor_rows(a2c, dz, None, pa, ma, va, st, 1e-3, 0.9, 0.999, 1e-8, 0.125, 0)
+    assert torch.equal(pa, pf) and torch.equal(ma, mf) and torch.equal(va, vf)
+
+
 def _tf_adam_(p, grad, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
     """TF1 AdamOptimizer (tensorflow_mnist.py:130) in float64 on the host side of the test."""
     m.mul_(b1).add_(grad, alpha=1 - b1)
