@@ -431,6 +431,10 @@ constexpr int F1R_LDS_BUF = F32_MAXB * 16;            // floats per wave buffer
 constexpr int F1R_LDS = 8 * 2 * F1R_LDS_BUF * 4;      // 131,072 B
 static_assert(8 * 8 * 64 * 16 <= F1R_LDS, "fc1 row form: dgrad partial exchange fits the dz buffers");
 
+// fc1 row form: the dz chunk swizzle (see store_z) and the column position of element `col` of `row`
+__device__ __forceinline__ int f1r_swz(int row) { return ((row >> 3) & 1) << 1; }
+__device__ __forceinline__ int f1r_col(int row, int col) { return 4 * ((col >> 2) ^ f1r_swz(row)) + (col & 3); }
+
 __device__ __forceinline__ void lds_wave_fence() {
   // the wave's own LDS writes before its later reads (LDS executes one wave's ops in order); a
   // compiler barrier keeps the program order
@@ -558,10 +562,15 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
       zst[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)min(b, B - 1) * 1024 + n), b < B);
     }
   };
+  // dz rows in LDS with the 16-byte chunks of rows 8..15 (mod 16) XOR-swizzled by 2: the dgrad's
+  // ds_read_b128 (lane (lr, lg) -> row lr, chunk lg) then hits 16 distinct slots per 16-lane group
+  // (2-way conflicts without), and the wgrad's ds_read_b32 of two adjacent rows stays conflict-free
   auto store_z = [&](float* buf) {
 #pragma unroll
-    for (int it = 0; it < G; ++it)
-      *reinterpret_cast<float4*>(buf + ((lane >> 2) + 16 * it) * 16 + 4 * (lane & 3)) = zst[it];
+    for (int it = 0; it < G; ++it) {
+      const int row = (lane >> 2) + 16 * it;
+      *reinterpret_cast<float4*>(buf + row * 16 + 4 * ((lane & 3) ^ f1r_swz(row))) = zst[it];
+    }
   };
   // p (and m, v) of chunk c: W3[f0 + lr][nb + 16 c + 4 lg .. + 3]
   const int64_t rowo = (int64_t)(f0 + lr) * 1024 + nb + 4 * lg;
@@ -595,7 +604,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     // dgrad: G tiles of 16 samples, the four k elements of the chunk outer (independent accumulators)
     float4 zb[G];
 #pragma unroll
-    for (int u = 0; u < G; ++u) zb[u] = *reinterpret_cast<const float4*>(buf + (16 * u + lr) * 16 + 4 * lg);
+    for (int u = 0; u < G; ++u) zb[u] = *reinterpret_cast<const float4*>(buf + (16 * u + lr) * 16 + 4 * (lg ^ f1r_swz(lr)));
     if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.x, zb[u].x, acc[u]);
@@ -618,12 +627,12 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
 #pragma unroll
     for (int s = 0; s + 1 < KS; s += 2) {
-      const float z0 = buf[(4 * s + lg) * 16 + lr];
-      const float z1 = buf[(4 * s + 4 + lg) * 16 + lr];
+      const float z0 = buf[(4 * s + lg) * 16 + f1r_col(4 * s + lg, lr)];
+      const float z1 = buf[(4 * s + 4 + lg) * 16 + f1r_col(4 * s + 4 + lg, lr)];
       w0 = mfma4(z0, a2r[s], w0);
       w1 = mfma4(z1, a2r[s + 1], w1);
     }
-    if constexpr (KS & 1) w0 = mfma4(buf[(4 * (KS - 1) + lg) * 16 + lr], a2r[KS - 1], w0);
+    if constexpr (KS & 1) w0 = mfma4(buf[(4 * (KS - 1) + lg) * 16 + f1r_col(4 * (KS - 1) + lg, lr)], a2r[KS - 1], w0);
     const f32x4 g = w0 + w1;
     const int64_t o = rowo + 16 * c;
     float4 gg = make_float4(g[0], g[1], g[2], g[3]);
@@ -1149,6 +1158,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     }
     if (!wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
+    if (n < 8) c2b_stamp(8 + n);  // (study build: wgrad blocks use the per-wave slots for per-image ends)
   }
   c2b_stamp(5);
   // partial exchange: [slot][kw][g][lane] float4, two rounds (waves 4-7 -> 0-3, then 0-3 -> all)

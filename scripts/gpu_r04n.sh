@@ -5,7 +5,9 @@ O=gpurun_out/r04n; mkdir -p $O
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 timeout -k 10 400 $T tests/test_f32_gpu.py > $O/t_f32.log 2>&1
 rc=$?; grep -E "FAILED|ERROR|passed|failed" $O/t_f32.log | tail -5; [ $rc -ne 0 ] && { tail -40 $O/t_f32.log; exit $rc; }
-timeout -k 10 300 python scripts/kbench_f32.py --match "conv2_fwd|conv2_bwd|fc1_fwd|whole step (graph|W2|K halves" > $O/kbench.log 2>&1 || { tail -30 $O/kbench.log; exit 1; }
+timeout -k 10 400 $T tests/test_fused_distributed_gpu.py -k "factor" > $O/t_dist.log 2>&1
+rc=$?; grep -E "PASSED|FAILED|ERROR|passed|failed" $O/t_dist.log | tail -6; [ $rc -ne 0 ] && { tail -60 $O/t_dist.log; exit $rc; }
+timeout -k 10 300 python scripts/kbench_f32.py --match "conv2_fwd|conv2_bwd|fc1_fwd|whole step (graph|W2|K halves|factor" > $O/kbench.log 2>&1 || { tail -30 $O/kbench.log; exit 1; }
 cat $O/kbench.log
 for i in 1 2; do timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_drv$i.log 2>&1 || { tail -20 $O/bench_drv$i.log; exit 1; }; tail -1 $O/bench_drv$i.log | cut -c1-200; done
 timeout -k 10 200 python bench.py --steps 400 --warmup 40 > $O/bench_400.log 2>&1 || { tail -20 $O/bench_400.log; exit 1; }

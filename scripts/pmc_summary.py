@@ -14,7 +14,8 @@ def load(d):
     out = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            key = (r["Kernel_Name"].split("(")[0][-44:], r["Grid_Size"])
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mihvd::", "mihvd:")
+            key = (name[-64:] if "mihvd" not in name else name[name.index("mihvd"):][:64], r["Grid_Size"])
             out[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return out
 
@@ -29,7 +30,7 @@ def main():
         if "mihvd" not in name and "f32" not in name:
             continue
         wc = cs.get("SQ_WAVE_CYCLES")
-        line = f"{name:44s} grid {grid:>7s}"
+        line = f"{name:64s} grid {grid:>7s}"
         if wc:
             line += (f" | wait {cs['SQ_WAIT_ANY'] / wc:.2f} waitInst {cs['SQ_WAIT_INST_ANY'] / wc:.2f}"
                      f" active {cs['SQ_ACTIVE_INST_ANY'] / wc:.2f} waitLDS {cs['SQ_WAIT_INST_LDS'] / wc:.2f}")

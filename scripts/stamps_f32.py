@@ -32,7 +32,9 @@ def main():
     n_dg = int(o.f32_dgrad_blocks(B))
     n_wg = 10 * int(o.f32_wgrad_groups(B))
     w2 = P("conv_layer2/conv2d/kernel")
-    run = lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab)
+    # the production launch: W2 from the fragment copy the step's conv1 launch wrote
+    wfb = tr.w2frag[1] if tr.w2frag is not None else None
+    run = lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab, w2frag=wfb)
     for _ in range(5):
         run()
     torch.cuda.synchronize()
@@ -66,6 +68,12 @@ def main():
     d = s[:n_dg, 8:16] - s[:n_dg, 1:2]
     print("    tap loop per wave (median over blocks): " + " ".join(f"{v:.0f}" for v in d.median(0).values))
     show("wgrad", s[n_dg:], [(0, 4, "first image"), (4, 5, "image loop"), (5, 6, "reduction"), (0, 6, "block total")])
+    # wgrad slots 8 + n: wave 0's end of image n (after the image's barrier), full 8-image groups
+    wg = s[n_dg:]
+    full = wg[(wg[:, 15] > 0)]
+    if full.shape[0]:
+        per = torch.cat([full[:, 8:9] - full[:, 4:5], full[:, 9:16] - full[:, 8:15]], 1)
+        print("    per image (median over full groups): " + " ".join(f"{v:.0f}" for v in per.median(0).values))
 
     # conv2_fwd: staging, then one stamp per tile pair
     a2, idx2 = tr.a2, tr.idx2
