@@ -5,12 +5,12 @@
 //   g[r][n] = sum_s A[s][r] D[s][n]    A = a2 columns of this rank's rows [NB][R] (all-to-all),
 //                                      D = every rank's dz [NB][1024] (all-gather), NB = N B
 //
-// grid (ceil(R / 16), 8): a block owns 16 rows x 128 columns; its 8 waves (two per SIMD) split the
+// 8 ceil(R / 16) blocks (column group = blockIdx & 7, the XCD): a block owns 16 rows x 128 columns; its 8 waves (two per SIMD) split the
 // NB samples into contiguous ranges of 4-sample k steps. v_mfma_f32_16x16x4_f32 with the rows of W3
 // on the MFMA row axis: lane (lr, lg) supplies A[s0 + lg][r0 + lr] and, for its 8 column tiles c,
 // D[s0 + lg][n0 + 8 lr + c] (two float4 loads per k step), so C of tile c is
 // g[r0 + 4 lg + i][n0 + 8 lr + c]. Operands come straight from L2 (A and D are 1.6 MB at N = 8),
-// batches of 2 k steps in a ring of three register stages (two batches in flight). The eight waves'
+// batches of 2 k steps in a ring of five register stages (four batches in flight). The eight waves'
 // partial tiles meet in LDS in a fixed order (deterministic) and form the block's [16][128] tile,
 // updated with coalesced float4 accesses by the same adam1() as every other optimizer kernel
 // (gscale = 1/N of the Average). Replaces a library GEMM (R x NB x 1024, 11.3 us at N = 8 on MI355X) plus an adam_step
@@ -24,6 +24,7 @@ namespace mihvd {
 
 constexpr int FAC_U = 2;   // k steps per load batch
 constexpr int FAC_W = 8;   // waves per block (the samples split 8 ways: two waves per SIMD)
+constexpr int FAC_S = 5;   // register stages of the load ring
 
 template <bool ADAM, bool STORE>
 __global__ void __launch_bounds__(512) f32_factor_rows_kernel(const float* __restrict__ A, const float* __restrict__ D,
@@ -32,7 +33,9 @@ __global__ void __launch_bounds__(512) f32_factor_rows_kernel(const float* __res
   f32x4* red = reinterpret_cast<f32x4*>(smf);  // [wave][tile][lane]: 64 KB
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15,
             lg = lane >> 4;
-  const int r0 = blockIdx.x * 16, n0 = blockIdx.y * 128;
+  // XCD-aware order: the 8 column groups are the 8 XCDs (the hardware deals blocks round-robin,
+  // blockIdx & 7), so every block reading a group's D columns shares one L2 (400 KB at N = 8)
+  const int r0 = (blockIdx.x >> 3) * 16, n0 = (blockIdx.x & 7) * 128;
   const int ra = min(r0 + lr, R - 1);
   const bool rin = r0 + lr < R;
   const int steps = (NB + 3) / 4, per = (steps + FAC_W - 1) / FAC_W;
@@ -69,24 +72,20 @@ __global__ void __launch_bounds__(512) f32_factor_rows_kernel(const float* __res
       acc[7] = mfma4(st.a[u], st.y[u].w, acc[7]);
     }
   };
-  // ring of three register stages, two batches in flight ahead of the MFMAs (wave-uniform trip
-  // count; steps past k_hi load zeros, and a batch wholly past k_hi is skipped)
-  Stage s0, s1, s2;
-  load(s0, k_lo);
-  load(s1, k_lo + FAC_U);
-  for (int kb = k_lo; kb < k_hi; kb += 3 * FAC_U) {
-    load(s2, kb + 2 * FAC_U);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(s0);
-    __builtin_amdgcn_sched_barrier(0);
-    load(s0, kb + 3 * FAC_U);
-    __builtin_amdgcn_sched_barrier(0);
-    if (kb + FAC_U < k_hi) mma(s1);
-    __builtin_amdgcn_sched_barrier(0);
-    load(s1, kb + 4 * FAC_U);
-    __builtin_amdgcn_sched_barrier(0);
-    if (kb + 2 * FAC_U < k_hi) mma(s2);
-    __builtin_amdgcn_sched_barrier(0);
+  // ring of FAC_S register stages, FAC_S - 1 batches in flight ahead of the MFMAs (the first pass
+  // over D misses the XCD's L2 on every block at once, so the lead has to cover MALL latency);
+  // wave-uniform trip count; steps past k_hi load zeros, and a batch wholly past k_hi is skipped
+  Stage st[FAC_S];
+#pragma unroll
+  for (int j = 0; j < FAC_S - 1; ++j) load(st[j], k_lo + j * FAC_U);
+  for (int kb = k_lo; kb < k_hi; kb += FAC_S * FAC_U) {
+#pragma unroll
+    for (int j = 0; j < FAC_S; ++j) {
+      load(st[(j + FAC_S - 1) % FAC_S], kb + (j + FAC_S - 1) * FAC_U);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kb + j * FAC_U < k_hi) mma(st[j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 #pragma unroll
   for (int c = 0; c < 8; ++c) red[(wave * 8 + c) * 64 + lane] = acc[c];
@@ -159,7 +158,7 @@ void f32_factor_rows(const at::Tensor& a2c, const at::Tensor& dz, const c10::opt
     ad.rule = (int)rule;
   }
   TORCH_CHECK(adam || store, "f32_factor_rows: nothing to write (neither out nor the Adam operands)");
-  const dim3 grid((unsigned)((R + 15) / 16), 8);
+  const dim3 grid((unsigned)(8 * ((R + 15) / 16)));
   auto stream = c10::hip::getCurrentHIPStream().stream();
   float* op = store ? out->data_ptr<float>() : nullptr;
   auto launch = [&](auto kern) {

@@ -803,3 +803,35 @@ def test_every_python_source_compiles():
         except SyntaxError as e:
             bad.append(f"{f}: {e}")
     assert len(files) > 50 and not bad, bad
+
+
+def test_roofline_f32_filters_startup_and_classifies(tmp_path):
+    """scripts/roofline_f32.py on a synthetic trace: start-up kernels (fills, copies, one-off torch
+    kernels) drop out, the fragment-copy conv2 instantiations are not mistaken for the fused conv12
+    launch, and the per-kernel times are medians over the steady-state window."""
+    import csv
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = ["mihvd::f32_conv1_kernel(float const*)", "void mihvd::f32_conv2_fwd_kernel<5, false, false, false, 2, true>(x)",
+             "void mihvd::f32_fc1_fwd2_kernel<7, false, false>(x)", "mihvd::f32_head_kernel(x)",
+             "void mihvd::f32_fc1_bwd_rows_kernel<7, true, false, 2, false, 25>(x)",
+             "void mihvd::f32_conv2_bwd_kernel<10, true, false, 2, true>(x)", "void mihvd::f32_conv_reduce_kernel<false>(x)"]
+    us = [7.0, 21.0, 12.0, 5.0, 28.0, 44.0, 5.0]
+    rows, t = [], 0
+    for _ in range(3):  # start-up noise
+        rows.append({"Kernel_Name": "__amd_rocclr_fillBufferAligned", "Start_Timestamp": t, "End_Timestamp": t + 500})
+        t += 1000
+    for _ in range(40):
+        for n, d in zip(names, us):
+            rows.append({"Kernel_Name": n, "Start_Timestamp": t, "End_Timestamp": t + int(d * 1000)})
+            t += int(d * 1000)
+    trace = tmp_path / "run_kernel_trace.csv"
+    with open(trace, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        w.writerows(rows)
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "roofline_f32.py"), str(trace)],
+                         capture_output=True, text=True, check=True).stdout
+    assert "`conv2_fwd`" in out and "conv12_fwd" not in out and "fillBuffer" not in out.split("Filtered")[0]
+    assert "| `conv2_bwd` |" in out and "44.00" in out and "| **kernel sum** | | 122.00" in out
