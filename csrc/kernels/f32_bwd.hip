@@ -1117,17 +1117,16 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   for (int k = 0; k < 5; ++k)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
-  // the next image's loads are issued one whole image ahead: image n + 1 arrives during image n - 1's
-  // second half and image n's first half, and is stored halfway through image n (the MALL latency of
-  // the first read of a1 / dY2 in the step, ~2 us, exceeds half an image of MFMAs)
+  // (loading the next image a whole image ahead instead — issued right after the previous store —
+  // was measured slower: 41.3 vs 39.8 us for the role, profiles/r04/kbench_f32_r04q.txt)
   float4 v[7];
   load_img(img0, v);
   c2b_stamp(4);
   store_img(smf, v);
-  if (nimg > 1) load_img(img0 + 1, v);
   __syncthreads();
   for (int n = 0; n < nimg; ++n) {
     const float* buf = smf + (n & 1) * CBF_WBUF;
+    if (n + 1 < nimg) load_img(img0 + n + 1, v);
     const float* A1s = buf;
     const float* DYs = buf + CBF_A1S;
     // K steps s = wave + 8u (pixels 2s: lanes 0-31, 2s + 1: lanes 32-63). Software pipeline, fully
@@ -1157,15 +1156,9 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
         for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(opa[cur], opb[cur][kw], acc[kw]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (u == 6 && wmid && nxt) {
-        store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
-        if (n + 2 < nimg) load_img(img0 + n + 2, v);
-      }
+      if (u == 6 && wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     }
-    if (!wmid && nxt) {
-      store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
-      if (n + 2 < nimg) load_img(img0 + n + 2, v);
-    }
+    if (!wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
     if (n < 8) c2b_stamp(8 + n);  // (study build: wgrad blocks use the per-wave slots for per-image ends)
   }

@@ -364,6 +364,10 @@ class FusedMNISTTrainer:
                 self.dz = self.dz_all32[self.rank]  # head writes this rank's block in place
                 self.a2_send = torch.empty(N, B, R, **f32)
                 self.a2_recv = torch.empty(N, B, R, **f32)
+            # the dW3 rows: a library fp32 GEMM + adam_step (default), or MIHVD_F32_FACTOR_KERNEL=1 the
+            # hand-written row kernel with Adam from the accumulators (csrc/kernels/f32_factor.hip;
+            # measured slower at N = 8: 17.3 us against 11.2 us + ~3 us, profiles/r04/kbench_f32_r04q.txt)
+            self.f32_factor_kernel = os.environ.get("MIHVD_F32_FACTOR_KERNEL", "0") == "1"
                 self.f32_factor = self.shard_w3 and os.environ.get("MIHVD_F32_PLANE", "rs") == "factor"
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
@@ -835,9 +839,15 @@ class FusedMNISTTrainer:
                       G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            o.f32_factor_rows(self.a2_recv, self.dz_all32, self.gshard if self.keep_w3_grad else None,
-                              self.params[mine], self.m[mine], self.v[mine], st, self.lr, b1, b2, self.eps,
-                              1.0 / self.world, self.rule)
+            if self.f32_factor_kernel:
+                o.f32_factor_rows(self.a2_recv, self.dz_all32, self.gshard if self.keep_w3_grad else None,
+                                  self.params[mine], self.m[mine], self.v[mine], st, self.lr, b1, b2, self.eps,
+                                  1.0 / self.world, self.rule)
+            else:
+                N, B = self.world, self.B
+                torch.mm(self.a2_recv.view(N * B, R).t(), self.dz_all32.view(N * B, 1024), out=self.gshard)
+                o.adam_step(self.params[mine], self.gshard.view(-1), self.m[mine], self.v[mine], None, st, 0, self.lr,
+                            b1, b2, self.eps, 1.0 / self.world, self.rule, 0)
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab,
                         w2frag=wf[1] if wf is not None else None)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),

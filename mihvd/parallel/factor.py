@@ -48,8 +48,8 @@ def factor_exchange_(a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor, a
 def factor_rows_(out: torch.Tensor, a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor,
                  a2_send: torch.Tensor, a2_recv: torch.Tensor, rank: int, world: int, comm=None) -> torch.Tensor:
     """out[R][1024] = rows [rank R, (rank + 1) R) of sum over ranks of a2_q^T dz_q: the exchange, then
-    one GEMM (the reference formulation; the trainer runs ``csrc/kernels/f32_factor.hip`` instead,
-    which applies Adam to the rows from the accumulators). Collective: every rank calls it."""
+    one GEMM (the trainer's default; ``MIHVD_F32_FACTOR_KERNEL=1`` runs ``csrc/kernels/f32_factor.hip``
+    instead, which applies Adam to the rows from the accumulators). Collective: every rank calls it."""
     factor_exchange_(a2, dz, dz_all, a2_send, a2_recv, rank, world, comm)
     N, B = world, a2.shape[0]
     R = a2.shape[1] // N
