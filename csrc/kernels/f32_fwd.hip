@@ -254,6 +254,141 @@ __device__ __forceinline__ void c2f_conv1_stage(const C1Fuse& c1, float* img, fl
   }
 }
 
+// ------------------------------------------------------------------------------------------ //
+// conv2 forward, 8-wave form (MIHVD_F32_C2F_W8=1): the same tiles, image and epilogue, but 512
+// threads: wave w = co group (w & 3) x ci half (w >> 2), so the two waves sharing a SIMD split K
+// (25 taps x 16 channels each, 100 W2 floats per lane) and hide each other's LDS and MFMA latency
+// instead of one wave per SIMD running the whole 800-deep chain; twice the threads stage the image.
+// The two ci halves' accumulators meet in LDS behind the image (a fixed order: half 0 + half 1);
+// the pool epilogue of the block's tiles is split between the halves.
+template <int NT, int DEPTH = 2>
+__device__ __forceinline__ void c2f_tiles_h(const float* img, const int (&ab)[2], const float (&wb)[100], int c2,
+                                            f32x4 (&acc)[2]) {
+  constexpr int R = DEPTH + 1;
+  float4 ra[R][NT];
+  auto load_a = [&](float4 (&a)[NT], int tap) {
+    const int kh = tap / 5, kw = tap - 5 * kh;
+    const int off = (kh * C2F_RW + kw) * C2F_PS + 16 * c2;
+#pragma unroll
+    for (int u = 0; u < NT; ++u) a[u] = *reinterpret_cast<const float4*>(img + ab[u] + off);
+  };
+  auto mfma_step = [&](const float4 (&a)[NT], int tap) {
+    const float* w = wb + 4 * tap;  // wb[4 tap + j]
+#pragma unroll
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].x, w[0], acc[u]);
+#pragma unroll
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].y, w[1], acc[u]);
+#pragma unroll
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].z, w[2], acc[u]);
+#pragma unroll
+    for (int u = 0; u < NT; ++u) acc[u] = mfma4(a[u].w, w[3], acc[u]);
+  };
+#pragma unroll
+  for (int st = 0; st < DEPTH; ++st) load_a(ra[st], st);
+#pragma unroll
+  for (int st = 0; st < 25; ++st) {
+    if (st + DEPTH < 25) load_a(ra[(st + DEPTH) % R], st + DEPTH);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_step(ra[st % R], st);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+constexpr int C2F8_MAXCH = (C2F_MAXR * 18 * 8 + 511) / 512;  // image float4 chunks per thread
+constexpr int C2F8_LDS = C2F_LDS + 4 * 7 * 64 * 16;          // image + [co group][tile][lane] f32x4 exchange
+
+template <int TPB, bool FRAG>
+__global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
+                                                             const float* __restrict__ b2, float* __restrict__ a2,
+                                                             uint8_t* __restrict__ idx2, int B,
+                                                             const float* __restrict__ w2f) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  float* img = smf;
+  f32x4* xr = reinterpret_cast<f32x4*>(smf + C2F_LDS / 4);
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
+  const int wco = wave & 3, c2 = wave >> 2;
+  const int nwin = 49 * B, T0 = (int)blockIdx.x * TPB;
+  const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
+  const int b0 = gw0 / 49, b1i = gw1 / 49;
+  const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
+  const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
+  const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
+  float4 iv[C2F8_MAXCH];
+#pragma unroll
+  for (int it = 0; it < C2F8_MAXCH; ++it) {
+    const int i = min(t + 512 * it, nch - 1);
+    const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, ch = rem & 7;
+    const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
+    const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+    const float4 v = *reinterpret_cast<const float4*>(
+        a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
+    iv[it] = mask_f4(v, in);
+  }
+#pragma unroll
+  for (int it = 0; it < C2F8_MAXCH; ++it) {
+    const int i = t + 512 * it;
+    if (i < nch) {
+      const int rr = i / 144, rem = i - rr * 144;
+      *reinterpret_cast<float4*>(img + (rr * C2F_RW + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
+    }
+  }
+  __syncthreads();  // the image is complete; no barrier below until the exchange
+  // this wave's W2 operand: wb[4 tap + j] = W2[tap][16 c2 + 4 lg + j][16 wco + lr], consumed in issue order
+  float wb[100];
+  if constexpr (FRAG) {
+    const float4* fp = reinterpret_cast<const float4*>(w2f) + (c2 * 4 + wco) * 64 + lane;
+#pragma unroll
+    for (int tap = 0; tap < 25; ++tap) {
+      const float4 v = fp[tap * 512];
+      wb[4 * tap + 0] = v.x;
+      wb[4 * tap + 1] = v.y;
+      wb[4 * tap + 2] = v.z;
+      wb[4 * tap + 3] = v.w;
+    }
+  } else {
+    const float* wp = w2 + (16 * c2 + 4 * lg) * 64 + 16 * wco + lr;
+#pragma unroll
+    for (int tap = 0; tap < 25; ++tap)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wb[4 * tap + j] = wp[tap * 2048 + j * 64];
+  }
+  f32x4 accs[TPB];
+#pragma unroll
+  for (int i = 0; i < TPB; i += 2) {  // block-uniform
+    const int tile0 = T0 + i, tile1 = T0 + min(i + 1, TPB - 1);
+    const int ab[2] = {c2f_abase(tile0, lr, 0, nwin, R0) + 4 * lg, c2f_abase(tile1, lr, 0, nwin, R0) + 4 * lg};
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int nt = min(2, TPB - i);
+    if (nt == 2) c2f_tiles_h<2>(img, ab, wb, c2, acc);
+    else c2f_tiles_h<1>(img, ab, wb, c2, acc);
+    accs[i] = acc[0];
+    if (i + 1 < TPB) accs[i + 1] = acc[1];
+  }
+  // exchange: tile u is finished by ci half (u >= H): the other half hands over its partial
+  constexpr int H = (TPB + 1) / 2;
+#pragma unroll
+  for (int u = 0; u < TPB; ++u)
+    if ((u >= H) != (c2 == 1)) xr[(wco * 7 + u) * 64 + lane] = accs[u];
+  __syncthreads();
+  const int co = 16 * wco + lr;
+  const float bias = b2[co];
+#pragma unroll
+  for (int u = 0; u < TPB; ++u) {
+    if ((u >= H) != (c2 == 1)) continue;
+    const f32x4 o = xr[(wco * 7 + u) * 64 + lane];
+    const f32x4 sum = c2 == 0 ? accs[u] + o : o + accs[u];  // half 0 + half 1 either way
+    const int gw = 4 * (T0 + u) + lg;
+    if (gw < nwin) {
+      const int bb = gw / 49, win = gw - 49 * bb;
+      int best;
+      const float m = pool4(sum, best);
+      const int64_t oo = (int64_t)bb * 3136 + win * 64 + co;
+      a2[oo] = fmaxf(m + bias, 0.f);
+      idx2[oo] = (uint8_t)best;
+    }
+  }
+}
+
 // PREW: the W2 register operand is issued right behind the staging writes and the barrier orders
 // LDS alone, so the 200 KB per block of W2 loads overlap the barrier wait and the first taps.
 // FUSE1: the a1 rows are computed from x in the block (conv1 fused, C1Fuse) instead of loaded.
@@ -992,6 +1127,32 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
   const bool prew = env_knob("MIHVD_F32_C2F_PREW", 0) != 0;
   // MIHVD_F32_C2F_DEPTH=1: A reads one step ahead of the MFMAs instead of two (the earlier form)
   const bool shallow = env_knob("MIHVD_F32_C2F_DEPTH", 2) < 2;
+  // MIHVD_F32_C2F_W8=1: the 8-wave form (two ci halves per co group, f32_conv2_fwd8_kernel)
+  const bool w8 = !fuse1 && ad.nblk == 0 && !prew && !shallow && env_knob("MIHVD_F32_C2F_W8", 0) != 0;
+  if (w8) {
+    TORCH_CHECK(tpb <= 7, "f32_conv2_fwd: 8-wave form needs <= 7 tiles per block");
+    auto launch8 = [&](auto kern) {
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C2F8_LDS);
+      kern<<<nblk, 512, C2F8_LDS, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+                                            a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, w2f);
+    };
+#define C2F8_CASE(T)                                                                           \
+  case T:                                                                                      \
+    w2f ? launch8(f32_conv2_fwd8_kernel<T, true>) : launch8(f32_conv2_fwd8_kernel<T, false>); \
+    break;
+    switch (tpb) {
+      C2F8_CASE(1)
+      C2F8_CASE(2)
+      C2F8_CASE(3)
+      C2F8_CASE(4)
+      C2F8_CASE(5)
+      C2F8_CASE(6)
+      default:
+        C2F8_CASE(7)
+    }
+#undef C2F8_CASE
+    return;
+  }
   TORCH_CHECK(!(fuse1 && ad.nblk > 0), "f32_conv2_fwd: the fused conv1 has no optimizer tail");
 #define C2F_CASE(T)                                                                  \
   case T:                                                                            \

@@ -50,8 +50,12 @@ def test_f32_conv1_fwd(ops, B):
     assert (idx.long()[pos] == rd[pos]).float().mean() > 0.999
 
 
+@pytest.mark.parametrize("w8", ["0", "1"])
 @pytest.mark.parametrize("B", [7, 100, 128])
-def test_f32_conv2_fwd(ops, B):
+def test_f32_conv2_fwd(ops, B, w8, monkeypatch):
+    """4-wave form (one wave per SIMD) and the 8-wave form (MIHVD_F32_C2F_W8=1: the two waves of a
+    SIMD split the input channels; their partials meet in LDS), HWIO and fragment-copy W2 reads."""
+    monkeypatch.setenv("MIHVD_F32_C2F_W8", w8)
     g = torch.Generator(device="cuda").manual_seed(2)
     a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
     w = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
@@ -59,6 +63,14 @@ def test_f32_conv2_fwd(ops, B):
     a2 = torch.empty(B, 3136, device="cuda")
     idx = torch.empty(B, 3136, device="cuda", dtype=torch.uint8)
     ops.f32_conv2_fwd(a1, w, b, a2, idx)
+    # the fragment-copy W2 reads give the same bits
+    frag = torch.empty(2, 51200, device="cuda")
+    ops.f32_conv1_fwd(torch.zeros(B, 784, device="cuda"), None, None, torch.zeros(800, device="cuda"),
+                      torch.zeros(32, device="cuda"), torch.empty(B, 14, 14, 32, device="cuda"),
+                      torch.empty(B, 14, 14, 32, device="cuda", dtype=torch.uint8), w.view(-1), frag)
+    a2f, idxf = torch.empty_like(a2), torch.empty_like(idx)
+    ops.f32_conv2_fwd(a1, w, b, a2f, idxf, w2frag=frag[0])
+    assert torch.equal(a2, a2f) and torch.equal(idx, idxf)
     ref, rd = ref_conv_pool(a1, w, b)
     assert rel_err(a2, ref.reshape(B, 3136)) < 1e-6
     pos = ref.reshape(B, 3136) > 1e-4
@@ -66,7 +78,7 @@ def test_f32_conv2_fwd(ops, B):
 
 
 @pytest.mark.parametrize("B", [1, 7, 100, 128])
-def test_f32_conv12_fwd_matches_separate_launches(ops, B):
+def test_f32_conv12_fwd_matches_separate_launches(ops, B, monkeypatch):
     """conv1 fused into the conv2 forward launch (each block computes the a1 rows it reads, halo
     included, and writes its own rows): a1, idx1, a2 and idx2 bit for bit equal to the two separate
     launches, with the resident dataset's row permutation and the device step counter."""
@@ -79,6 +91,7 @@ def test_f32_conv12_fwd_matches_separate_launches(ops, B):
     b1 = torch.randn(32, device="cuda", generator=g) * 0.1
     w2 = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
     b2 = torch.randn(64, device="cuda", generator=g) * 0.1
+    monkeypatch.setenv("MIHVD_F32_C2F_W8", "0")  # the fused launch is the 4-wave conv2 form
     outs = []
     for fused in (True, False):
         a1 = torch.full((B, 14, 14, 32), float("nan"), device="cuda")
