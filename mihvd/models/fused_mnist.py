@@ -364,11 +364,11 @@ class FusedMNISTTrainer:
                 self.dz = self.dz_all32[self.rank]  # head writes this rank's block in place
                 self.a2_send = torch.empty(N, B, R, **f32)
                 self.a2_recv = torch.empty(N, B, R, **f32)
+                self.f32_factor = self.shard_w3 and os.environ.get("MIHVD_F32_PLANE", "rs") == "factor"
             # the dW3 rows: a library fp32 GEMM + adam_step (default), or MIHVD_F32_FACTOR_KERNEL=1 the
             # hand-written row kernel with Adam from the accumulators (csrc/kernels/f32_factor.hip;
             # measured slower at N = 8: 17.3 us against 11.2 us + ~3 us, profiles/r04/kbench_f32_r04q.txt)
             self.f32_factor_kernel = os.environ.get("MIHVD_F32_FACTOR_KERNEL", "0") == "1"
-                self.f32_factor = self.shard_w3 and os.environ.get("MIHVD_F32_PLANE", "rs") == "factor"
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
