@@ -297,7 +297,7 @@ __device__ __forceinline__ void c2f_tiles_h(const float* img, const int (&ab)[2]
 constexpr int C2F8_MAXCH = (C2F_MAXR * 18 * 8 + 511) / 512;  // image float4 chunks per thread
 constexpr int C2F8_LDS = C2F_LDS + 4 * 7 * 64 * 16;          // image + [co group][tile][lane] f32x4 exchange
 
-template <int TPB, bool FRAG>
+template <int TPB, bool FRAG, int DEPTH = 2>
 __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                              const float* __restrict__ b2, float* __restrict__ a2,
                                                              uint8_t* __restrict__ idx2, int B,
@@ -359,8 +359,8 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
     const int ab[2] = {c2f_abase(tile0, lr, 0, nwin, R0) + 4 * lg, c2f_abase(tile1, lr, 0, nwin, R0) + 4 * lg};
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int nt = min(2, TPB - i);
-    if (nt == 2) c2f_tiles_h<2>(img, ab, wb, c2, acc);
-    else c2f_tiles_h<1>(img, ab, wb, c2, acc);
+    if (nt == 2) c2f_tiles_h<2, DEPTH>(img, ab, wb, c2, acc);
+    else c2f_tiles_h<1, DEPTH>(img, ab, wb, c2, acc);
     accs[i] = acc[0];
     if (i + 1 < TPB) accs[i + 1] = acc[1];
   }
@@ -1128,7 +1128,7 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
   // MIHVD_F32_C2F_DEPTH=1: A reads one step ahead of the MFMAs instead of two (the earlier form)
   const bool shallow = env_knob("MIHVD_F32_C2F_DEPTH", 2) < 2;
   // MIHVD_F32_C2F_W8=1: the 8-wave form (two ci halves per co group, f32_conv2_fwd8_kernel)
-  const bool w8 = !fuse1 && ad.nblk == 0 && !prew && !shallow && env_knob("MIHVD_F32_C2F_W8", 0) != 0;
+  const bool w8 = !fuse1 && ad.nblk == 0 && !prew && env_knob("MIHVD_F32_C2F_W8", 0) != 0;
   if (w8) {
     TORCH_CHECK(tpb <= 7, "f32_conv2_fwd: 8-wave form needs <= 7 tiles per block");
     auto launch8 = [&](auto kern) {
@@ -1138,7 +1138,8 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
     };
 #define C2F8_CASE(T)                                                                           \
   case T:                                                                                      \
-    w2f ? launch8(f32_conv2_fwd8_kernel<T, true>) : launch8(f32_conv2_fwd8_kernel<T, false>); \
+    if (shallow) w2f ? launch8(f32_conv2_fwd8_kernel<T, true, 1>) : launch8(f32_conv2_fwd8_kernel<T, false, 1>); \
+    else w2f ? launch8(f32_conv2_fwd8_kernel<T, true>) : launch8(f32_conv2_fwd8_kernel<T, false>);         \
     break;
     switch (tpb) {
       C2F8_CASE(1)
@@ -1159,6 +1160,7 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
     if (ad.nblk > 0) launch(f32_conv2_fwd_kernel<T, true>, ad.nblk);                 \
     else if (fuse1) launch(f32_conv2_fwd_kernel<T, false, true, true>, 0);           \
     else if (prew) launch(f32_conv2_fwd_kernel<T, false, true>, 0);                  \
+    else if (shallow && w2f) launch(f32_conv2_fwd_kernel<T, false, false, false, 1, true>, 0); \
     else if (shallow) launch(f32_conv2_fwd_kernel<T, false, false, false, 1>, 0);    \
     else if (w2f) launch(f32_conv2_fwd_kernel<T, false, false, false, 2, true>, 0);  \
     else launch(f32_conv2_fwd_kernel<T, false>, 0);                                  \

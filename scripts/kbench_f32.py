@@ -165,6 +165,10 @@ def main():
         "conv2_fwd [A reads one step ahead]": ({"MIHVD_F32_C2F_DEPTH": "1"}, ks["conv2_fwd"]),
         "conv2_fwd [8 waves: ci halves share a SIMD]": ({"MIHVD_F32_C2F_W8": "1"}, ks["conv2_fwd"]),
         "conv2_fwd [8 waves, W2 fragment copy]": ({"MIHVD_F32_C2F_W8": "1"}, ks["conv2_fwd [W2 fragment copy]"]),
+        "conv2_fwd [W2 fragment copy, A one step ahead]": ({"MIHVD_F32_C2F_DEPTH": "1"},
+                                                           ks["conv2_fwd [W2 fragment copy]"]),
+        "conv2_fwd [8 waves, W2 fragment copy, A one step ahead]": ({"MIHVD_F32_C2F_W8": "1", "MIHVD_F32_C2F_DEPTH": "1"},
+                                                                    ks["conv2_fwd [W2 fragment copy]"]),
         "conv2_bwd [W2 after a full barrier]": ({"MIHVD_F32_C2B_PREW": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
         "conv2_bwd [dgrad role only, W2 after a full barrier]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_PREW": "0"},
@@ -236,6 +240,8 @@ def main():
         "whole step [W2 read as HWIO (no fragment copies)]": ({"w2frag": None}, {}),
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
         "whole step [conv2_fwd 8 waves]": ({}, {"MIHVD_F32_C2F_W8": "1"}),
+        "whole step [conv2_fwd A one step ahead]": ({}, {"MIHVD_F32_C2F_DEPTH": "1"}),
+        "whole step [conv2_fwd 8 waves, A one step ahead]": ({}, {"MIHVD_F32_C2F_W8": "1", "MIHVD_F32_C2F_DEPTH": "1"}),
     }
     for name, (attrs, env) in steps.items():
         if not want(name):
