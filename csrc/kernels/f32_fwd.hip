@@ -1127,8 +1127,9 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
   const bool prew = env_knob("MIHVD_F32_C2F_PREW", 0) != 0;
   // MIHVD_F32_C2F_DEPTH=1: A reads one step ahead of the MFMAs instead of two (the earlier form)
   const bool shallow = env_knob("MIHVD_F32_C2F_DEPTH", 2) < 2;
-  // MIHVD_F32_C2F_W8=1: the 8-wave form (two ci halves per co group, f32_conv2_fwd8_kernel)
-  const bool w8 = !fuse1 && ad.nblk == 0 && !prew && env_knob("MIHVD_F32_C2F_W8", 0) != 0;
+  // MIHVD_F32_C2F_W8=1 (default): the 8-wave form (two ci halves per co group, f32_conv2_fwd8_kernel):
+  // 18.9 vs 19.2 us with the fragment W2, whole step 122.6 vs 122.9 us (profiles/r04/kbench_f32_r04s.txt)
+  const bool w8 = !fuse1 && ad.nblk == 0 && !prew && env_knob("MIHVD_F32_C2F_W8", 1) != 0;
   if (w8) {
     TORCH_CHECK(tpb <= 7, "f32_conv2_fwd: 8-wave form needs <= 7 tiles per block");
     auto launch8 = [&](auto kern) {

@@ -163,8 +163,8 @@ def main():
         "conv2_fwd [LDS 70 KB: blocks may share a CU]": ({"MIHVD_F32_C2F_LDS": "70400"}, ks["conv2_fwd"]),
         "conv2_fwd [W2 issued before the staging barrier]": ({"MIHVD_F32_C2F_PREW": "1"}, ks["conv2_fwd"]),
         "conv2_fwd [A reads one step ahead]": ({"MIHVD_F32_C2F_DEPTH": "1"}, ks["conv2_fwd"]),
-        "conv2_fwd [8 waves: ci halves share a SIMD]": ({"MIHVD_F32_C2F_W8": "1"}, ks["conv2_fwd"]),
-        "conv2_fwd [8 waves, W2 fragment copy]": ({"MIHVD_F32_C2F_W8": "1"}, ks["conv2_fwd [W2 fragment copy]"]),
+        "conv2_fwd [4 waves: one per SIMD, the whole K chain]": ({"MIHVD_F32_C2F_W8": "0"}, ks["conv2_fwd"]),
+        "conv2_fwd [4 waves, W2 fragment copy]": ({"MIHVD_F32_C2F_W8": "0"}, ks["conv2_fwd [W2 fragment copy]"]),
         "conv2_fwd [W2 fragment copy, A one step ahead]": ({"MIHVD_F32_C2F_DEPTH": "1"},
                                                            ks["conv2_fwd [W2 fragment copy]"]),
         "conv2_fwd [8 waves, W2 fragment copy, A one step ahead]": ({"MIHVD_F32_C2F_W8": "1", "MIHVD_F32_C2F_DEPTH": "1"},
@@ -239,7 +239,7 @@ def main():
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
         "whole step [W2 read as HWIO (no fragment copies)]": ({"w2frag": None}, {}),
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
-        "whole step [conv2_fwd 8 waves]": ({}, {"MIHVD_F32_C2F_W8": "1"}),
+        "whole step [conv2_fwd 4 waves]": ({}, {"MIHVD_F32_C2F_W8": "0"}),
         "whole step [conv2_fwd A one step ahead]": ({}, {"MIHVD_F32_C2F_DEPTH": "1"}),
         "whole step [conv2_fwd 8 waves, A one step ahead]": ({}, {"MIHVD_F32_C2F_W8": "1", "MIHVD_F32_C2F_DEPTH": "1"}),
     }

@@ -75,7 +75,8 @@ def main():
         per = torch.cat([full[:, 8:9] - full[:, 4:5], full[:, 9:16] - full[:, 8:15]], 1)
         print("    per image (median over full groups): " + " ".join(f"{v:.0f}" for v in per.median(0).values))
 
-    # conv2_fwd: staging, then one stamp per tile pair
+    # conv2_fwd: staging, then one stamp per tile pair (the 4-wave form carries the stamps)
+    os.environ["MIHVD_F32_C2F_W8"] = "0"
     a2, idx2 = tr.a2, tr.idx2
     runf = lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), a2, idx2)
     nblk = -(-((49 * B + 3) // 4) // 5)
