@@ -301,13 +301,17 @@ template <int TPB, bool FRAG, int DEPTH = 2>
 __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                              const float* __restrict__ b2, float* __restrict__ a2,
                                                              uint8_t* __restrict__ idx2, int B,
-                                                             const float* __restrict__ w2f) {
+                                                             const float* __restrict__ w2f, F32Adam ad) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
+  if ((int)blockIdx.x < ad.nblk) {  // optimizer tail blocks (MIHVD_F32_W3=tail), first in dispatch order
+    f32_adam_stream(ad, blockIdx.x);
+    return;
+  }
   float* img = smf;
   f32x4* xr = reinterpret_cast<f32x4*>(smf + C2F_LDS / 4);
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int wco = wave & 3, c2 = wave >> 2;
-  const int nwin = 49 * B, T0 = (int)blockIdx.x * TPB;
+  const int nwin = 49 * B, T0 = ((int)blockIdx.x - max(ad.nblk, 0)) * TPB;
   const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
   const int b0 = gw0 / 49, b1i = gw1 / 49;
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
@@ -1129,13 +1133,14 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
   const bool shallow = env_knob("MIHVD_F32_C2F_DEPTH", 2) < 2;
   // MIHVD_F32_C2F_W8=1 (default): the 8-wave form (two ci halves per co group, f32_conv2_fwd8_kernel):
   // 18.9 vs 19.2 us with the fragment W2, whole step 122.6 vs 122.9 us (profiles/r04/kbench_f32_r04s.txt)
-  const bool w8 = !fuse1 && ad.nblk == 0 && !prew && env_knob("MIHVD_F32_C2F_W8", 1) != 0;
+  const bool w8 = !fuse1 && !prew && env_knob("MIHVD_F32_C2F_W8", 1) != 0;
   if (w8) {
     TORCH_CHECK(tpb <= 7, "f32_conv2_fwd: 8-wave form needs <= 7 tiles per block");
     auto launch8 = [&](auto kern) {
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C2F8_LDS);
-      kern<<<nblk, 512, C2F8_LDS, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
-                                            a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, w2f);
+      kern<<<nblk + std::max(ad.nblk, 0), 512, C2F8_LDS, stream>>>(
+          a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(), a2.data_ptr<float>(),
+          idx2.data_ptr<uint8_t>(), B, w2f, ad);
     };
 #define C2F8_CASE(T)                                                                           \
   case T:                                                                                      \
