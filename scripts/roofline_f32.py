@@ -36,7 +36,7 @@ WORK = [
     (r"f32_conv2_fwd_kernel<\d+, false, true, true", "conv12_fwd", CONV1_GF + CONV2_GF,
      (B * 784 * F + B * 6272 * (F + 1) + B * 3136 * (F + 1) + 51200 * F + 800 * F) / MB,
      "conv1 + conv2 forward, bias/ReLU/pool/argmax fused (one launch)"),
-    (r"f32_conv2_fwd_kernel", "conv2_fwd", CONV2_GF,
+    (r"f32_conv2_fwd8?_kernel", "conv2_fwd", CONV2_GF,
      (B * 6272 * F + B * 3136 * (F + 1) + 51200 * F) / MB, "conv2 forward, bias/ReLU/pool/argmax fused"),
     (r"f32_conv1_kernel", "conv1_fwd", CONV1_GF, (B * 784 * F + B * 6272 * (F + 1) + 3 * 51200 * F) / MB,
      "conv1 forward (+ the two W2 fragment copies)"),
