@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--batch-size", type=int, default=PER_GPU_BATCH)
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--graph-steps", type=int, default=0, help="fused: steps captured per HIP graph (0=auto)")
+    ap.add_argument("--lead-steps", type=int, default=2, help="fused: steps of the short graph that starts every "
+                    "run (0: none)")
     ap.add_argument("--pool-batches", type=int, default=60, help="synthetic batches resident on device")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=os.environ.get("MIHVD_PRECISION", "fp32"),
@@ -144,6 +146,17 @@ def make_torch_graph_step(args, hvd, device):
     return run_step, "fp32", None
 
 
+def replay_schedule(n: int, k: int, lead: int) -> list:
+    """Graph replays (steps each) for n steps: a lead graph of ``lead`` steps, whole k-step graphs,
+    the remainder."""
+    if n <= 0:
+        return []
+    if lead <= 0 or n <= lead:
+        return [k] * (n // k) + ([n % k] if n % k else [])
+    m = n - lead
+    return [lead] + [k] * (m // k) + ([m % k] if m % k else [])
+
+
 def make_fused_step(args, hvd, device):
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
@@ -158,21 +171,27 @@ def make_fused_step(args, hvd, device):
     tr.plane_report = tr.select_data_plane() if tr.collectives else {"plane": "none"}
     k = args.graph_steps or 20  # steps per HIP-graph replay (20: measured 66.6 vs 67.5 us at 10)
     tr.build_graph(steps_per_replay=k)
-    # remainders of --steps / --warmup that are not multiples of k replay a shorter graph, so the
-    # timed region is exactly K steps
-    for r in {args.steps % k, args.warmup % k} - {0}:
+    # every run of n steps replays a short lead graph first, then whole k-step graphs, then the
+    # remainder, so the timed region is exactly K steps: the host call that launches a 20-step graph
+    # takes ~105 us (140 kernel nodes) before the GPU gets its first packet, so a 2-step lead graph
+    # starts the GPU at once and the long graph is launched while the lead runs (measured for the
+    # driver's 20 timed steps: 123.7 vs 126.1 us/step, scripts/launch_probe.py,
+    # profiles/r04/launch_probe_r04u.txt)
+    sizes = set(replay_schedule(args.steps, k, args.lead_steps)) | set(replay_schedule(args.warmup, k, args.lead_steps))
+    for r in sorted(sizes - {k, 0}):
         tr.build_graph(steps_per_replay=r, warmup=0, primary=False)
     # setup, like the eager steps build_graph runs: one untimed replay of every graph built, so the
     # first launch of a graph executable (one-time driver/queue setup, cold instruction caches) is
-    # not inside the warm-up-limited timed region (the driver times 20 steps = one replay)
+    # not inside the warm-up-limited timed region (the driver times 20 steps)
     tr.run_graph()
-    for r in {args.steps % k, args.warmup % k} - {0}:
+    for r in sorted(sizes - {k, 0}):
         tr.run_graph(r)
     torch.cuda.synchronize(device)
 
     def step(n=None):
-        tr.run_graph(n)
+        tr.run_graph(None if n == k else n)
 
+    step.schedule = lambda n: replay_schedule(n, k, args.lead_steps)
     return step, args.precision, tr
 
 
@@ -198,7 +217,12 @@ def main():
         per_call = 1
 
     def run(n):
-        """Exactly n steps: whole graphs of per_call steps, then one replay of the remainder."""
+        """Exactly n steps: whole graphs of per_call steps, then one replay of the remainder (the
+        fused trainer: its replay schedule, a short lead graph first)."""
+        if hasattr(step, "schedule"):
+            for s in step.schedule(n):
+                step(s)
+            return
         for _ in range(n // per_call):
             step()
         if n % per_call:
@@ -273,7 +297,9 @@ def main():
                        "image_shape": [28, 28, 1], "parallelism": f"dp{n}", "impl": args.impl,
                        "optimizer": "Adam (TF1 rule), lr=%g x size" % args.lr,
                        "allreduce": comm_desc,
-                       "steps_per_graph": per_call, "final_loss": loss_val},
+                       "steps_per_graph": per_call,
+                       "replays_timed": (step.schedule(steps_timed) if hasattr(step, "schedule") else None),
+                       "final_loss": loss_val},
         }
         if args.impl == "fused" and tr.collectives:
             rec["config"]["data_plane"] = tr.plane_report
