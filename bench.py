@@ -195,8 +195,27 @@ def make_fused_step(args, hvd, device):
     return step, args.precision, tr
 
 
+def _host_wait_mode():
+    """MIHVD_SYNC_WAIT=spin: the host waits for the GPU by spinning (hipDeviceScheduleSpin) instead of
+    HIP's default scheduling, so the synchronize that closes the timed region returns as soon as the
+    last kernel ends. Set on this rank's device before torch creates its HIP context."""
+    mode = os.environ.get("MIHVD_SYNC_WAIT", "auto").strip().lower()
+    if mode != "spin":
+        return
+    import ctypes
+
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+    except OSError:
+        return
+    dev = int(os.environ.get("LOCAL_RANK", "0"))
+    if hip.hipSetDevice(ctypes.c_int(dev)) == 0:
+        hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+
+
 def main():
     args = parse()
+    _host_wait_mode()
     if args.impl == "fused":
         # the fused trainer issues its own collectives (in its HIP graph): no engine thread cycling
         # beside the timed steps
