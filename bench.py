@@ -196,10 +196,12 @@ def make_fused_step(args, hvd, device):
 
 
 def _host_wait_mode():
-    """MIHVD_SYNC_WAIT=spin: the host waits for the GPU by spinning (hipDeviceScheduleSpin) instead of
-    HIP's default scheduling, so the synchronize that closes the timed region returns as soon as the
-    last kernel ends. Set on this rank's device before torch creates its HIP context."""
-    mode = os.environ.get("MIHVD_SYNC_WAIT", "auto").strip().lower()
+    """MIHVD_SYNC_WAIT=spin (default): the host waits for the GPU by spinning (hipDeviceScheduleSpin)
+    instead of HIP's default scheduling, so the synchronize that closes the timed region returns as
+    soon as the last kernel ends (driver form, fresh processes: 127.0 vs 128.8 µs/step median of 4,
+    profiles/r04/sync_wait_r04w.txt). Set on this rank's device before torch creates its HIP
+    context; MIHVD_SYNC_WAIT=auto keeps HIP's default."""
+    mode = os.environ.get("MIHVD_SYNC_WAIT", "spin").strip().lower()
     if mode != "spin":
         return
     import ctypes
