@@ -1064,24 +1064,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 // Per image: a1 padded rows kh..kh+13 [14][18][32] and the dY2 channel half [196][32], register-
 // staged double buffering (the next image's loads are in flight while this one is multiplied).
 // 8 waves split the K steps (w, w + 8, ...); their partial tiles are summed through LDS.
-// XCD-aware order of a role's blocks: the hardware deals a launch's blocks round-robin over the 8
-// XCDs (blockIdx & 7), each with its own L2. Returns the logical index of global block g within the
-// role's range [lo, hi) such that every XCD gets a contiguous run of logical indices, so blocks that
-// read the same data (the 10 wgrad blocks of an image group) share one XCD's L2 instead of fetching
-// it from HBM eight times.
-__device__ __forceinline__ int xcd_contiguous(int g, int lo, int hi) {
-  const int x = g & 7;
-  int before = 0;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int first = lo + ((c - lo) & 7);
-    const int cnt = first < hi ? (hi - first + 7) >> 3 : 0;
-    if (c < x) before += cnt;
-  }
-  const int first_x = lo + ((x - lo) & 7);
-  return before + ((g - first_x) >> 3);
-}
-
+// (xcd_contiguous: f32_common.h)
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
                                                       int ig, int wmid, float* smf) {

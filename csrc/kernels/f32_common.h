@@ -44,6 +44,24 @@ __device__ __forceinline__ float4 mask_f4(float4 v, bool keep) {
                      __uint_as_float(__float_as_uint(v.z) & m), __uint_as_float(__float_as_uint(v.w) & m));
 }
 
+// XCD-aware order of a role's blocks: the hardware deals a launch's blocks round-robin over the 8
+// XCDs (blockIdx & 7), each with its own L2. Returns the logical index of global block g within the
+// role's range [lo, hi) such that every XCD gets a contiguous run of logical indices, so blocks that
+// read the same data (the 10 wgrad blocks of an image group; conv1's blocks of an image and the conv2_fwd blocks that read its a1 rows) share one XCD's L2 instead of fetching
+// it from HBM eight times.
+__device__ __forceinline__ int xcd_contiguous(int g, int lo, int hi) {
+  const int x = g & 7;
+  int before = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int first = lo + ((c - lo) & 7);
+    const int cnt = first < hi ? (hi - first + 7) >> 3 : 0;
+    if (c < x) before += cnt;
+  }
+  const int first_x = lo + ((x - lo) & 7);
+  return before + ((g - first_x) >> 3);
+}
+
 // 2x2 max-pool of one window held in a lane's four accumulator rows (pixels d = 2 dy + dx in scan
 // order): the maximum and the index of its FIRST occurrence (the tie rule of TF's MaxPool gradient
 // and torch's max_pool2d backward).

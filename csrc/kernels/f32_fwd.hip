@@ -77,11 +77,16 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ a1, uint8_t* __restrict__ idx1,
     int B, const float* __restrict__ w2, float* __restrict__ w2f) {
   __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
-  if ((int)blockIdx.y >= B) {
-    f32_w2_frag_block(((int)blockIdx.y - B) * 4 + (int)blockIdx.x, w2, w2f);
+  const int id = blockIdx.x;
+  if (id >= 4 * B) {
+    f32_w2_frag_block(id - 4 * B, w2, w2f);
     return;
   }
-  f32_conv1_block<false>(blockIdx.x, blockIdx.y, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim);
+  // XCD-contiguous (image, quarter) order: XCD x writes the a1 rows of images [B x / 8, B (x + 1) / 8),
+  // the images whose conv2_fwd blocks run on XCD x (same mapping there), so conv2_fwd's staging
+  // reads hit that XCD's L2 instead of the MALL
+  const int L = xcd_contiguous(id, 0, 4 * B);
+  f32_conv1_block<false>(L & 3, L >> 2, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -311,7 +316,9 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
   f32x4* xr = reinterpret_cast<f32x4*>(smf + C2F_LDS / 4);
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int wco = wave & 3, c2 = wave >> 2;
-  const int nwin = 49 * B, T0 = ((int)blockIdx.x - max(ad.nblk, 0)) * TPB;
+  // XCD-contiguous tile ranges: XCD x takes the images whose a1 rows conv1's blocks on XCD x wrote
+  const int nblk = (((49 * B + 3) / 4) + TPB - 1) / TPB, lo = max(ad.nblk, 0);
+  const int nwin = 49 * B, T0 = xcd_contiguous((int)blockIdx.x, lo, lo + nblk) * TPB;
   const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
   const int b0 = gw0 / 49, b1i = gw1 / 49;
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
@@ -998,7 +1005,7 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
     check_f32(*w2, 51200, "f32_conv1_fwd: w2");
     check_f32(*w2frag, 2 * 51200, "f32_conv1_fwd: w2frag [2][51200]");
   }
-  f32_conv1_kernel<<<dim3(4, B + (frag ? W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
+  f32_conv1_kernel<<<dim3(4 * B + (frag ? 4 * W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
       x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(), b1.data_ptr<float>(), a1.data_ptr<float>(),
       idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr);
 }
