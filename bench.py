@@ -210,9 +210,15 @@ def _host_wait_mode():
         hip = ctypes.CDLL("libamdhip64.so")
     except OSError:
         return
-    dev = int(os.environ.get("LOCAL_RANK", "0"))
+    count = ctypes.c_int(0)
+    if hip.hipGetDeviceCount(ctypes.byref(count)) != 0 or count.value < 1:
+        hip.hipGetLastError()
+        return
+    # the device mihvd.init() picks for this rank (local rank modulo the visible devices)
+    dev = int(os.environ.get("LOCAL_RANK", "0")) % count.value
     if hip.hipSetDevice(ctypes.c_int(dev)) == 0:
         hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+    hip.hipGetLastError()  # leave no sticky error for torch's launch checks
 
 
 def main():
