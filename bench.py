@@ -180,10 +180,16 @@ def make_fused_step(args, hvd, device):
     sizes = set(replay_schedule(args.steps, k, args.lead_steps)) | set(replay_schedule(args.warmup, k, args.lead_steps))
     for r in sorted(sizes - {k, 0}):
         tr.build_graph(steps_per_replay=r, warmup=0, primary=False)
-    # setup, like the eager steps build_graph runs: one untimed replay of every graph built, so the
-    # first launch of a graph executable (one-time driver/queue setup, cold instruction caches) is
-    # not inside the warm-up-limited timed region (the driver times 20 steps)
-    for _ in range(max(1, int(os.environ.get("MIHVD_BENCH_SETUP_REPLAYS", "1")))):
+    # setup, like the eager steps build_graph runs: untimed replays of every graph built, so the
+    # first launch of a graph executable (one-time driver/queue setup, cold instruction caches) and
+    # the device's ramp to its steady clock/memory state are not inside the short timed region. A
+    # fresh process measured 125.8-127.6 us/step for the driver's 20 timed steps after one setup
+    # replay of the main graph and 123.2-123.5 after ten (interleaved runs,
+    # profiles/r04/setup_replays_r04aa.txt) -- the same as 400 timed steps (123.8-124.3): the first
+    # milliseconds of GPU work in a process run slower, so the setup replays the main graph ten times
+    # (200 untimed training steps, ~25 ms) before the --warmup steps. MIHVD_BENCH_SETUP_REPLAYS sets
+    # the count.
+    for _ in range(max(1, int(os.environ.get("MIHVD_BENCH_SETUP_REPLAYS", "10")))):
         tr.run_graph()
     for r in sorted(sizes - {k, 0}):
         tr.run_graph(r)
