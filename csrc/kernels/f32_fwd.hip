@@ -266,16 +266,34 @@ __device__ __forceinline__ void c2f_conv1_stage(const C1Fuse& c1, float* img, fl
 // instead of one wave per SIMD running the whole 800-deep chain; twice the threads stage the image.
 // The two ci halves' accumulators meet in LDS behind the image (a fixed order: half 0 + half 1);
 // the pool epilogue of the block's tiles is split between the halves.
+// The image of this form: unpadded 32-float pixels in 18-pixel tall rows, each pixel's eight 16-byte
+// chunks XOR-permuted by 2 ((row + column) & 3): the ds_read_b128 of every tap, tile and window-row
+// wrap then lands its 16-lane groups on 16 distinct slots (scripts/ldssim_conv2.py model: 1.00 LDS
+// cycles per group, against 1.42 for the padded 40 x 20 layout of the 4-wave form).
+constexpr int C2F8_PS = 32, C2F8_RW = 18, C2F8_RS = C2F8_RW * C2F8_PS;
+constexpr int C2F8_IMG = C2F_MAXR * C2F8_RS * 4;  // 50,688 B
+__device__ __forceinline__ int c2f8_swz(int row, int col) { return ((row + col) & 3) << 1; }
+
+// lane row lr of tile `tile`: pixel offset in the image (row * RW + col) * PS, and row + col
+__device__ __forceinline__ int c2f8_base(int tile, int lr, int nwin, int R0, int& rc) {
+  const int m = 16 * tile + lr;
+  const int gw = min(m >> 2, nwin - 1), d = m & 3;
+  const int bb = gw / 49, win = gw - 49 * bb, py = win / 7, px = win - 7 * py;
+  const int r = 18 * bb + 2 * py + (d >> 1) - R0, x = 2 * px + (d & 1);
+  rc = r + x;
+  return (r * C2F8_RW + x) * C2F8_PS;
+}
+
 template <int NT, int DEPTH = 2>
-__device__ __forceinline__ void c2f_tiles_h(const float* img, const int (&ab)[2], const float (&wb)[100], int c2,
-                                            f32x4 (&acc)[2]) {
+__device__ __forceinline__ void c2f_tiles_h(const float* img, const int (&ab)[2], const int (&cw)[2][4],
+                                            const float (&wb)[100], f32x4 (&acc)[2]) {
   constexpr int R = DEPTH + 1;
   float4 ra[R][NT];
   auto load_a = [&](float4 (&a)[NT], int tap) {
     const int kh = tap / 5, kw = tap - 5 * kh;
-    const int off = (kh * C2F_RW + kw) * C2F_PS + 16 * c2;
+    const int off = (kh * C2F8_RW + kw) * C2F8_PS;
 #pragma unroll
-    for (int u = 0; u < NT; ++u) a[u] = *reinterpret_cast<const float4*>(img + ab[u] + off);
+    for (int u = 0; u < NT; ++u) a[u] = *reinterpret_cast<const float4*>(img + ab[u] + off + cw[u][(kh + kw) & 3]);
   };
   auto mfma_step = [&](const float4 (&a)[NT], int tap) {
     const float* w = wb + 4 * tap;  // wb[4 tap + j]
@@ -300,7 +318,7 @@ __device__ __forceinline__ void c2f_tiles_h(const float* img, const int (&ab)[2]
 }
 
 constexpr int C2F8_MAXCH = (C2F_MAXR * 18 * 8 + 511) / 512;  // image float4 chunks per thread
-constexpr int C2F8_LDS = C2F_LDS + 4 * 7 * 64 * 16;          // image + [co group][tile][lane] f32x4 exchange
+constexpr int C2F8_LDS = C2F8_IMG + 4 * 7 * 64 * 16;         // image + [co group][tile][lane] f32x4 exchange
 
 template <int TPB, bool FRAG, int DEPTH = 2>
 __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
@@ -313,7 +331,7 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
     return;
   }
   float* img = smf;
-  f32x4* xr = reinterpret_cast<f32x4*>(smf + C2F_LDS / 4);
+  f32x4* xr = reinterpret_cast<f32x4*>(smf + C2F8_IMG / 4);
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int wco = wave & 3, c2 = wave >> 2;
   // XCD-contiguous tile ranges: XCD x takes the images whose a1 rows conv1's blocks on XCD x wrote
@@ -339,8 +357,8 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
   for (int it = 0; it < C2F8_MAXCH; ++it) {
     const int i = t + 512 * it;
     if (i < nch) {
-      const int rr = i / 144, rem = i - rr * 144;
-      *reinterpret_cast<float4*>(img + (rr * C2F_RW + (rem >> 3)) * C2F_PS + (rem & 7) * 4) = iv[it];
+      const int rr = i / 144, rem = i - rr * 144, c = rem >> 3;
+      *reinterpret_cast<float4*>(img + (rr * C2F8_RW + c) * C2F8_PS + 4 * ((rem & 7) ^ c2f8_swz(rr, c))) = iv[it];
     }
   }
   __syncthreads();  // the image is complete; no barrier below until the exchange
@@ -367,11 +385,19 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
 #pragma unroll
   for (int i = 0; i < TPB; i += 2) {  // block-uniform
     const int tile0 = T0 + i, tile1 = T0 + min(i + 1, TPB - 1);
-    const int ab[2] = {c2f_abase(tile0, lr, 0, nwin, R0) + 4 * lg, c2f_abase(tile1, lr, 0, nwin, R0) + 4 * lg};
+    int rc0, rc1;
+    const int ab[2] = {c2f8_base(tile0, lr, nwin, R0, rc0), c2f8_base(tile1, lr, nwin, R0, rc1)};
+    // the lane's chunk 4 c2 + lg, swizzled for each (row + column) residue the taps visit
+    int cw[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cw[0][j] = 4 * ((4 * c2 + lg) ^ c2f8_swz(rc0 + j, 0));
+      cw[1][j] = 4 * ((4 * c2 + lg) ^ c2f8_swz(rc1 + j, 0));
+    }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int nt = min(2, TPB - i);
-    if (nt == 2) c2f_tiles_h<2, DEPTH>(img, ab, wb, c2, acc);
-    else c2f_tiles_h<1, DEPTH>(img, ab, wb, c2, acc);
+    if (nt == 2) c2f_tiles_h<2, DEPTH>(img, ab, cw, wb, acc);
+    else c2f_tiles_h<1, DEPTH>(img, ab, cw, wb, acc);
     accs[i] = acc[0];
     if (i + 1 < TPB) accs[i + 1] = acc[1];
   }
@@ -1143,9 +1169,11 @@ static void f32_conv2_fwd_impl(const at::Tensor& a1, const at::Tensor& w2, const
   const bool w8 = !fuse1 && !prew && env_knob("MIHVD_F32_C2F_W8", 1) != 0;
   if (w8) {
     TORCH_CHECK(tpb <= 7, "f32_conv2_fwd: 8-wave form needs <= 7 tiles per block");
+    // (more LDS than a CU's half when the grid fits the CUs: one block per CU, as the 4-wave form)
+    const int lds8 = std::max(C2F8_LDS, std::min(env_knob("MIHVD_F32_C2F_LDS", spread), 163840));
     auto launch8 = [&](auto kern) {
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C2F8_LDS);
-      kern<<<nblk + std::max(ad.nblk, 0), 512, C2F8_LDS, stream>>>(
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds8);
+      kern<<<nblk + std::max(ad.nblk, 0), 512, lds8, stream>>>(
           a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(), a2.data_ptr<float>(),
           idx2.data_ptr<uint8_t>(), B, w2f, ad);
     };

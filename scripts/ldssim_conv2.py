@@ -60,6 +60,37 @@ def conv2_fwd(PS, RW, B=100, TPB=5, stride=7):
     return tot / ideal
 
 
+def conv2_fwd8(PS=32, RW=18, B=100, TPB=5, stride=7, swizzle=True):
+    """The 8-wave conv2_fwd layout (f32_fwd.hip, f32_conv2_fwd8_kernel): unpadded pixels, the 16-byte
+    chunk c of pixel (row r, column x) stored at c ^ 2 ((r + x) & 3)."""
+    nwin = 49 * B
+    tot = ideal = 0
+    for blk in range(0, (nwin // 4 + TPB - 1) // TPB, stride):
+        T0 = blk * TPB
+        gw0 = 4 * T0
+        b0 = gw0 // 49
+        R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) // 7)
+        for i in range(TPB):
+            for kh in range(5):
+                for kw in range(5):
+                    for c2 in range(2):
+                        addrs = []
+                        for lane in range(64):
+                            lr, lg = lane & 15, lane >> 4
+                            m = 16 * (T0 + i) + lr
+                            gw = min(m >> 2, nwin - 1)
+                            d = m & 3
+                            bb, win = gw // 49, gw % 49
+                            py, px = win // 7, win % 7
+                            r = 18 * bb + 2 * py + (d >> 1) + kh - R0
+                            x = 2 * px + (d & 1) + kw
+                            ch = (4 * c2 + lg) ^ ((2 * ((r + x) & 3)) if swizzle else 0)
+                            addrs.append((r * RW + x) * PS + 4 * ch)
+                        tot += cycles(addrs)
+                        ideal += 4
+    return tot / ideal
+
+
 def conv2_bwd_dgrad(PS, B=100, TPB=10, stride=5):
     np_ = 196 * B
     tot = ideal = 0
@@ -87,7 +118,9 @@ def main():
     ap.add_argument("--search", action="store_true", help="scan pixel strides / row lengths")
     a = ap.parse_args()
     print(f"conv2_fwd  PS 40 RW 20 (current): {conv2_fwd(40, 20):.2f}   PS 36 RW 24 (round 3): {conv2_fwd(36, 24):.2f}")
-    print(f"conv2_bwd dgrad PS 68 (current): {conv2_bwd_dgrad(68):.2f}")
+    print(f"conv2_fwd 8-wave form, PS 32 RW 18, chunks XOR 2((row + col) & 3): {conv2_fwd8():.2f} "
+          f"(unswizzled: {conv2_fwd8(swizzle=False):.2f})")
+    print(f"conv2_bwd dgrad PS 68, 18-pixel rows (round 3; now 72 x 22: conflict-free): {conv2_bwd_dgrad(68):.2f}")
     if a.search:
         for PS in (32, 36, 40, 44, 48):
             print("conv2_fwd PS", PS, " ".join(f"RW{RW}:{conv2_fwd(PS, RW, stride=28):.2f}" for RW in (18, 20, 22, 24, 26)))
