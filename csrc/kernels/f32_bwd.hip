@@ -702,7 +702,11 @@ constexpr int CBF_IMG = CBF_MAXR * CBF_RS;            // floats: tall padded dY2
 constexpr int CBF_MAXR2 = 21, CBF_IMG2 = CBF_MAXR2 * CBF_RS;
 constexpr int cbf_maxr(int npass) { return npass == 2 ? CBF_MAXR2 : CBF_MAXR; }
 constexpr int cbf_img(int npass) { return cbf_maxr(npass) * CBF_RS; }
-constexpr int CBF_XIM = 2 * 1024;                     // two padded x images [32][32]
+// padded x images [32][34]: the epilogue's 16 lanes of one pixel read its x patch at the pooled
+// argmax position (channel-dependent: offsets 0, 1, row, row + 1), so a 32-float row put the 0 and
+// row offsets on one bank (2-way ds_read_b32 conflicts, PMC ~5e5 cycles per launch); 34 separates them
+constexpr int CBF_XS = 34, CBF_XIMG = 32 * CBF_XS;
+constexpr int CBF_XIM = 2 * CBF_XIMG;                 // two padded x images
 constexpr int CBF_PW = 8 * 2 * 64 * 4;                // per-wave conv1 partials (MEPI: 2 f32x4 per lane)
 // The x images and the conv1 partials live in the dead image area behind the co-quarter partial
 // exchange (written after the tap loops' barrier): the image alone sets the dgrad LDS size.
@@ -926,7 +930,10 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   __syncthreads();  // every wave is done with the dY2 image
   c2b_stamp(7);
 #pragma unroll
-  for (int it = 0; it < 4; ++it) xim[t + 512 * it] = xv[it];  // (complete after the next barrier)
+  for (int it = 0; it < 4; ++it) {  // (complete after the next barrier)
+    const int i = t + 512 * it, sl = i >> 10, pix = i & 1023;
+    xim[sl * CBF_XIMG + (pix >> 5) * CBF_XS + (pix & 31)] = xv[it];
+  }
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
   if constexpr (LATE) load_codes();  // in flight while the partials are exchanged
@@ -943,8 +950,8 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     int off0, off1;
     {
       const int n1 = 16 + lr;
-      off0 = (lr / 5) * 32 + lr % 5;
-      off1 = n1 < 25 ? (n1 / 5) * 32 + n1 % 5 : 0;
+      off0 = (lr / 5) * CBF_XS + lr % 5;
+      off1 = n1 < 25 ? (n1 / 5) * CBF_XS + n1 % 5 : 0;
     }
     const float one1 = lr == 9 ? 1.f : 0.f;  // column 25 = db1
     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
@@ -969,7 +976,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
           const float g = ea[k][r] > 0.f ? sk[r] : 0.f;
           a[r] = (P0r < np && ex[k][r] == lg) ? g : 0.f;
         }
-        const float* xs = xim + (bb - b0) * 1024 + (2 * py + (lg >> 1)) * 32 + 2 * px + (lg & 1);
+        const float* xs = xim + (bb - b0) * CBF_XIMG + (2 * py + (lg >> 1)) * CBF_XS + 2 * px + (lg & 1);
         x0[r] = xs[off0];
         const float xo = xs[off1];  // off1 = 0 past tap 24: an in-bounds read, replaced below
         x1[r] = 16 + lr < 25 ? xo : one1;
@@ -1026,11 +1033,11 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
         const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
         const float g = ea[k][r] > 0.f ? sum[r] : 0.f;
         const int ix = ex[k][r];
-        const float* xs = xim + (bb - b0) * 1024 + (2 * py + (ix >> 1)) * 32 + 2 * px + (ix & 1);
+        const float* xs = xim + (bb - b0) * CBF_XIMG + (2 * py + (ix >> 1)) * CBF_XS + 2 * px + (ix & 1);
 #pragma unroll
         for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) s25[kh * 5 + kw] = fmaf(g, xs[kh * 32 + kw], s25[kh * 5 + kw]);
+          for (int kw = 0; kw < 5; ++kw) s25[kh * 5 + kw] = fmaf(g, xs[kh * CBF_XS + kw], s25[kh * 5 + kw]);
         s25[25] += g;
       }
     }
