@@ -1146,7 +1146,13 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
         for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(opa[cur], opb[cur][kw], acc[kw]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (u == 6 && wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
+      if (u == 6 && wmid == 1 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
+      // wmid 2: one chunk per step over u = 4..10, so each store waits only for its own load (the
+      // loads return in issue order; vmcnt counts down) instead of all seven at u = 6
+      if (u >= 4 && u < 11 && wmid == 2 && nxt) {
+        const int it = u - 4;
+        *reinterpret_cast<float4*>(smf + ((n + 1) & 1) * CBF_WBUF + 4 * (t + 512 * it)) = v[it];
+      }
     }
     if (!wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
@@ -1674,7 +1680,9 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
   const int ndg_arg = role == 2 ? 0 : n_dg;
   const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
-  const int wmid = env_knob("MIHVD_F32_C2B_WMID", 1) != 0;  // 0: next image stored after the steps
+  // 0: next image stored after the steps, 1: at step 6, 2 (default): one chunk per step over steps
+  // 4..10 (wgrad role alone 39.2 vs 40.1 us for 1, profiles/r04/kbench_f32_r04ag.txt; bitwise equal)
+  const int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 2);
   const int wdelay = r1 ? std::max(0, std::min(env_knob("MIHVD_F32_C2B_WDELAY", 0), 64)) : 0;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

@@ -69,6 +69,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("bench", nargs="?", help="bench.py stdout (its JSON line gives ms_per_step)")
     ap.add_argument("--tail", type=float, default=0.5, help="fraction of the trace taken as steady state")
+    ap.add_argument("--stats", help="also write the filtered per-kernel stats table to this file")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     t0, t1 = int(rows[0]["Start_Timestamp"]), int(rows[-1]["End_Timestamp"])
@@ -78,11 +79,27 @@ def main():
     for r in win:
         by.setdefault(r["Kernel_Name"], []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     steps = max(len(v) for v in by.values())
-    step_ms = None
+    step_ms, bench_line = None, None
     if a.bench:
         for line in open(a.bench):
             if line.startswith("{"):
-                step_ms = json.loads(line).get("ms_per_step")
+                step_ms, bench_line = json.loads(line).get("ms_per_step"), line.strip()
+    if a.stats:  # the filtered per-kernel table (profiles/rocprof_f32_kernel_stats_latest.txt)
+        keep = {n: v for n, v in by.items() if len(v) >= 0.8 * steps}
+        tot = sum(statistics.median(v) for v in keep.values())
+        with open(a.stats, "w") as f:
+            if bench_line:
+                f.write(bench_line + "\n")
+            f.write(f"# steady state: last {int(a.tail * 100)}% of {a.trace} (graph-replayed bench.py under "
+                    "rocprofv3 --kernel-trace --stats);\n")
+            f.write(f"# only kernels launched about once per step ({steps} launches) are listed: start-up "
+                    "fills/copies and warm-up kernels are dropped\n")
+            f.write(f"{'kernel':<62s} {'calls':>6s} {'median_us':>10s} {'mean_us':>10s} {'pct':>7s}\n")
+            for n, v in sorted(keep.items(), key=lambda kv: -statistics.median(kv[1])):
+                m = statistics.median(v)
+                f.write(f"{n[:62]:<62s} {len(v):>6d} {m:>10.2f} {statistics.mean(v):>10.2f} "
+                        f"{100 * m / tot:>6.1f}%\n")
+            f.write(f"{'sum of medians':<62s} {'':>6s} {tot:>10.2f}\n")
     print("# Roofline of the exact-fp32 headline step (B = 100, one MI355X)\n")
     print(f"Kernel times: median per kernel over the last {int(a.tail * 100)}% of `{a.trace}` "
           f"(graph-replayed steady state, {steps} launches of the most frequent kernel); start-up and warm-up "
