@@ -1078,21 +1078,37 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), l32 = lane & 31, hh = lane >> 5;
   const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
   const int img0 = ig * grp, nimg = min(ig, B - img0);
-  auto load_img = [&](int b, float4 (&v)[7]) {
+  // wmid bits 0-1: where the next image's LDS stores go (see the K-step loop); bit 2 ("late"): its
+  // global loads are issued after step 0's MFMAs instead of before the first operand reads
+  const int wm = wmid & 3;
+  const bool late = (wmid & 4) != 0;
+  // this thread's seven chunk offsets within an image, computed once (per image only the image
+  // term is added): chunk i < 2016 is an a1 chunk of the padded rows kh..kh+13, the rest dY2 chunks
+  int loff[7];
+  bool lin[7], la1[7];
 #pragma unroll
-    for (int it = 0; it < 7; ++it) {
-      const int i = t + 512 * it;  // < 3584 = 2016 a1 chunks + 1568 dY2 chunks
-      if (i < 2016) {
-        const int ly = i / 144, r2 = i - 144 * ly, c = r2 >> 3, q4 = r2 & 7;
-        const int y = ly + kh - 2, xx = c - 2;
-        const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
-        v[it] = mask_f4(*reinterpret_cast<const float4*>(
-                            a1 + (((int64_t)b * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + 4 * q4), in);
-      } else {
-        const int j = i - 2016, q = j >> 3, q4 = j & 7;
-        v[it] = *reinterpret_cast<const float4*>(dY2 + ((int64_t)b * 196 + q) * 64 + 32 * ch + 4 * q4);
-      }
+  for (int it = 0; it < 7; ++it) {
+    const int i = t + 512 * it;  // < 3584 = 2016 a1 chunks + 1568 dY2 chunks
+    if (i < 2016) {
+      const int ly = i / 144, r2 = i - 144 * ly, c = r2 >> 3, q4 = r2 & 7;
+      const int y = ly + kh - 2, xx = c - 2;
+      const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+      loff[it] = ((in ? y : 0) * 14 + (in ? xx : 0)) * 32 + 4 * q4;
+      lin[it] = in;
+      la1[it] = true;
+    } else {
+      const int j = i - 2016, q = j >> 3, q4 = j & 7;
+      loff[it] = q * 64 + 32 * ch + 4 * q4;
+      lin[it] = true;
+      la1[it] = false;
     }
+  }
+  auto load_img = [&](int b, float4 (&v)[7]) {
+    const float* pa = a1 + (int64_t)b * 6272;  // [14][14][32]
+    const float* pd = dY2 + (int64_t)b * 12544;  // [196][64]
+#pragma unroll
+    for (int it = 0; it < 7; ++it)
+      v[it] = mask_f4(*reinterpret_cast<const float4*>((la1[it] ? pa : pd) + loff[it]), lin[it]);
   };
   auto store_img = [&](float* buf, const float4 (&v)[7]) {
 #pragma unroll
@@ -1116,7 +1132,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   __syncthreads();
   for (int n = 0; n < nimg; ++n) {
     const float* buf = smf + (n & 1) * CBF_WBUF;
-    if (n + 1 < nimg) load_img(img0 + n + 1, v);
+    if (n + 1 < nimg && !late) load_img(img0 + n + 1, v);
     const float* A1s = buf;
     const float* DYs = buf + CBF_A1S;
     // K steps s = wave + 8u (pixels 2s: lanes 0-31, 2s + 1: lanes 32-63). Software pipeline, fully
@@ -1146,15 +1162,16 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
         for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(opa[cur], opb[cur][kw], acc[kw]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (u == 6 && wmid == 1 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
-      // wmid 2: one chunk per step over u = 4..10, so each store waits only for its own load (the
+      if (u == 0 && late && nxt) load_img(img0 + n + 1, v);
+      if (u == 6 && wm == 1 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
+      // wm 2: one chunk per step over u = 4..10, so each store waits only for its own load (the
       // loads return in issue order; vmcnt counts down) instead of all seven at u = 6
-      if (u >= 4 && u < 11 && wmid == 2 && nxt) {
+      if (u >= 4 && u < 11 && wm == 2 && nxt) {
         const int it = u - 4;
         *reinterpret_cast<float4*>(smf + ((n + 1) & 1) * CBF_WBUF + 4 * (t + 512 * it)) = v[it];
       }
     }
-    if (!wmid && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
+    if (wm == 0 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
     if (n < 8) c2b_stamp(8 + n);  // (study build: wgrad blocks use the per-wave slots for per-image ends)
   }
@@ -1681,7 +1698,8 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const int ndg_arg = role == 2 ? 0 : n_dg;
   const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
   // 0: next image stored after the steps, 1: at step 6, 2 (default): one chunk per step over steps
-  // 4..10 (wgrad role alone 39.2 vs 40.1 us for 1, profiles/r04/kbench_f32_r04ag.txt; bitwise equal)
+  // 4..10 (wgrad role alone 39.2 vs 40.1 us for 1, profiles/r04/kbench_f32_r04ag.txt; bitwise equal);
+  // + 4: the next image's global loads issued after step 0's MFMAs
   const int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 2);
   const int wdelay = r1 ? std::max(0, std::min(env_knob("MIHVD_F32_C2B_WDELAY", 0), 64)) : 0;
   auto launch = [&](auto kern) {

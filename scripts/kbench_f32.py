@@ -182,6 +182,10 @@ def main():
         "conv2_bwd [wgrad role only, stored after the steps]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "0"},
                                                                ks["conv2_bwd"]),
         "conv2_bwd [wgrad next image stored at step 6]": ({"MIHVD_F32_C2B_WMID": "1"}, ks["conv2_bwd"]),
+        "conv2_bwd [W2 fragment copy, wgrad loads after step 0]": ({"MIHVD_F32_C2B_WMID": "6"},
+                                                                   ks["conv2_bwd [W2 fragment copy]"]),
+        "conv2_bwd [wgrad role only, loads after step 0]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "6"},
+                                                           ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only, stored at step 6]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "1"},
                                                          ks["conv2_bwd"]),
         "conv2_bwd [wgrad start held back ~4k cycles]": ({"MIHVD_F32_C2B_WDELAY": "4"}, ks["conv2_bwd"]),
