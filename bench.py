@@ -228,6 +228,39 @@ def _host_wait_mode():
     hip.hipGetLastError()  # leave no sticky error for torch's launch checks
 
 
+def _rccl_witness(tr, device) -> dict:
+    """What RCCL itself reports (ncclCommCount / ncclCommUserRank) for the communicator the step's
+    collectives ran on: the trainer's framework-owned NativeComm, or at one GPU without collectives a
+    communicator created here, after the timed region, for the count alone. Every rank takes part (the
+    creation is collective); rank 0's values are printed, and ``rccl_nranks_agree`` says whether every
+    rank saw the same count."""
+    if device.type != "cuda" or not dist.is_initialized() or dist.get_backend() != "nccl":
+        return {"rccl_nranks": None}
+    from mihvd.parallel.rccl import NativeComm
+
+    comm = getattr(tr, "ncomm", None) if tr is not None else None
+    if comm is None and tr is None:  # --impl torch / torch-graph: DistributedOptimizer's bucket plane
+        from mihvd import basics
+
+        plane = getattr(basics._ctx, "plane", None)
+        comm = plane.comm if plane is not None else None
+    own = comm is None
+    try:
+        if own:
+            comm = NativeComm(device=device)
+        n, r = comm.nranks(), comm.user_rank()
+    except Exception as e:  # pragma: no cover - depends on the RCCL build
+        return {"rccl_nranks": None, "rccl_error": repr(e)[:200]}
+    finally:
+        if own and comm is not None:
+            comm.close()
+    t = torch.tensor([n, -n], dtype=torch.int64, device=device)
+    if dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"rccl_nranks": n, "rccl_user_rank": r, "rccl_nranks_agree": int(t[0]) == -int(t[1]) == n,
+            "rccl_comm": ("trainer" if tr is not None else "bucket plane") if not own else "witness"}
+
+
 def main():
     args = parse()
     _host_wait_mode()
@@ -321,6 +354,7 @@ def main():
     else:
         comm_desc = "RCCL allreduce of the fp32 gradient fusion buffer every step" + (
             " (bf16 wire)" if args.compression == "bf16" else "")
+    rccl = _rccl_witness(tr if args.impl == "fused" else None, device)
     if hvd.rank() == 0:
         rec = {
             "metric": METRIC, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": steps_timed,
@@ -335,6 +369,7 @@ def main():
                        "replays_timed": (step.schedule(steps_timed) if hasattr(step, "schedule") else None),
                        "final_loss": loss_val},
         }
+        rec["config"].update(rccl)
         if args.impl == "fused" and tr.collectives:
             rec["config"]["data_plane"] = tr.plane_report
         print(json.dumps(rec), flush=True)

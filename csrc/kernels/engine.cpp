@@ -265,6 +265,7 @@ class Engine {
     ann_dev_ = at::zeros({(int64_t)world_ * kAnnounce + kAnnounce}, i32.device(at::kCUDA, device_));
     ann_host_ = at::zeros({(int64_t)world_ * kAnnounce + kAnnounce}, i32.pinned_memory(true));
     hip_check(hipEventCreateWithFlags(&ctrl_ev_, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&data_ev_, hipEventDisableTiming), "hipEventCreate");
     thread_ = std::thread([this] { loop(); });
   }
 
@@ -272,6 +273,7 @@ class Engine {
     stop();
     for (hipEvent_t e : pool_) hipEventDestroy(e);
     if (ctrl_ev_) hipEventDestroy(ctrl_ev_);
+    if (data_ev_) hipEventDestroy(data_ev_);
   }
 
   int64_t enqueue(const at::Tensor& t, const std::string& name, int64_t op) {
@@ -448,8 +450,10 @@ class Engine {
     }
   }
 
-  // Polls `ev` (control stream) until it completes; meanwhile runs the negotiation stall check.
-  void wait_ctrl(hipEvent_t ev) {
+  // Polls `ev` (control stream) until it completes; meanwhile runs the negotiation stall check,
+  // unless `quiet`: a rank that is stopping with nothing pending waits for its peers to finish
+  // their work (they may be busy for long, e.g. rank 0 checkpointing) -- a clean wait, not a stall.
+  void wait_ctrl(hipEvent_t ev, bool quiet = false) {
     const auto t0 = Clock::now();
     bool warned = false;
     int spins = 0;
@@ -458,7 +462,7 @@ class Engine {
       if (q == hipSuccess) return;
       if (q != hipErrorNotReady) hip_check(q, "negotiation event");
       if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 10));
-      if ((spins & 255) != 0) continue;
+      if ((spins & 255) != 0 || quiet) continue;
       const double age = std::chrono::duration<double>(Clock::now() - t0).count();
       if (warn_s_ > 0 && age > warn_s_ && !warned) {
         warned = true;
@@ -523,13 +527,17 @@ class Engine {
         // a stopping rank first drains its own pending work (its peers will match it)
         hv[0] = (stopping && !any_pending) ? 1 : 0;
         hv[1] = announce_.empty() ? 0 : 1;
+        // the control communicator's kernels never run beside the data communicator's: the
+        // negotiation of this cycle follows the last cycle's collectives (two communicators whose
+        // kernels overlap in different orders on different ranks can deadlock)
+        hip_check(hipStreamWaitEvent(cst, data_ev_, 0), "hipStreamWaitEvent");
         hip_check(hipMemcpyAsync(ctrl_dev_.data_ptr(), hv, (2 + 2 * S) * 4, hipMemcpyHostToDevice, cst), "H2D");
         std::string err;
         if (rccl_all_reduce_raw(ctrl_dev_.data_ptr(), 2 + 2 * S, ncclInt32, ncclSum, ctrl_comm_, cst, &err) != 0)
           throw std::runtime_error("negotiation allreduce: " + err);
         hip_check(hipMemcpyAsync(hv, ctrl_dev_.data_ptr(), (2 + 2 * S) * 4, hipMemcpyDeviceToHost, cst), "D2H");
         hip_check(hipEventRecord(ctrl_ev_, cst), "hipEventRecord");
-        wait_ctrl(ctrl_ev_);
+        wait_ctrl(ctrl_ev_, stopping && !any_pending);
         {
           std::lock_guard<std::mutex> lk(mu_);
           ++cycles_;
@@ -685,6 +693,7 @@ class Engine {
         throw std::runtime_error("fused allreduce: " + err);
       launch_copies(out);  // MEMCPY_OUT_FUSION_BUFFER: one launch
     }
+    hip_check(hipEventRecord(data_ev_, st), "hipEventRecord");
     std::lock_guard<std::mutex> lk(mu_);
     ++collectives_;
     tensors_ += (int64_t)reqs.size();
@@ -742,6 +751,7 @@ class Engine {
   c10::hip::HIPStream stream_, ctrl_stream_;
   at::Tensor ctrl_dev_, ctrl_host_, ann_dev_, ann_host_, fusion_;
   hipEvent_t ctrl_ev_ = nullptr;
+  hipEvent_t data_ev_ = nullptr;  // the data stream's last collective (the control stream waits for it)
   // engine-thread state
   std::vector<Slot> slots_;
   std::unordered_map<uint32_t, int> slot_of_hash_;

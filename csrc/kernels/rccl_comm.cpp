@@ -48,6 +48,8 @@ struct Rccl {
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclCommCount) count = nullptr;
+  decltype(&ncclCommUserRank) user_rank = nullptr;
 };
 
 std::string loaded_rccl_path() {
@@ -91,6 +93,8 @@ Rccl& rccl() {
     MIHVD_SYM(group_end, ncclGroupEnd);
     MIHVD_SYM(send, ncclSend);
     MIHVD_SYM(recv, ncclRecv);
+    MIHVD_SYM(count, ncclCommCount);
+    MIHVD_SYM(user_rank, ncclCommUserRank);
 #undef MIHVD_SYM
   });
   TORCH_CHECK(r.lib != nullptr && r.init_rank != nullptr && r.all_reduce != nullptr && r.all_gather != nullptr &&
@@ -188,6 +192,24 @@ int64_t rccl_comm_init(const at::Tensor& uid, int64_t rank, int64_t world, int64
 int64_t rccl_comm_ptr(int64_t h) { return (int64_t)(uintptr_t)get(h)->comm; }
 
 std::string rccl_library_path() { return rccl().path; }
+
+// What RCCL itself reports for the communicator (ncclCommCount / ncclCommUserRank), not what the
+// caller passed to ncclCommInitRank: the witness bench.py prints as config.rccl_nranks.
+int64_t rccl_comm_count(int64_t h) {
+  Comm* c = get(h);
+  TORCH_CHECK(rccl().count != nullptr, "rccl_comm_count: librccl lacks ncclCommCount");
+  int n = 0;
+  check(rccl().count(c->comm, &n), "ncclCommCount");
+  return n;
+}
+
+int64_t rccl_comm_user_rank(int64_t h) {
+  Comm* c = get(h);
+  TORCH_CHECK(rccl().user_rank != nullptr, "rccl_comm_user_rank: librccl lacks ncclCommUserRank");
+  int r = -1;
+  check(rccl().user_rank(c->comm, &r), "ncclCommUserRank");
+  return r;
+}
 
 // ---- collectives: enqueued on the current HIP stream (capturable into a HIP graph) ----
 void rccl_all_reduce_(int64_t h, at::Tensor& t, int64_t op) {
@@ -339,6 +361,8 @@ TORCH_LIBRARY_FRAGMENT(mihvd, m) {
   m.def("rccl_comm_init(Tensor uid, int rank, int world, int device) -> int", &mihvd::rccl_comm_init);
   m.def("rccl_comm_ptr(int comm) -> int", &mihvd::rccl_comm_ptr);
   m.def("rccl_library_path() -> str", &mihvd::rccl_library_path);
+  m.def("rccl_comm_count(int comm) -> int", &mihvd::rccl_comm_count);
+  m.def("rccl_comm_user_rank(int comm) -> int", &mihvd::rccl_comm_user_rank);
   m.def("rccl_all_reduce_(int comm, Tensor(a!) t, int op=0) -> ()", &mihvd::rccl_all_reduce_);
   m.def("rccl_all_gather(int comm, Tensor(a!) out, Tensor input) -> ()", &mihvd::rccl_all_gather);
   m.def("rccl_reduce_scatter(int comm, Tensor(a!) out, Tensor input, int op=0) -> ()", &mihvd::rccl_reduce_scatter);

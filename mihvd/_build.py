@@ -99,6 +99,14 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int | None =
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "kernels", "*.cuh")))
     if not srcs:
         raise RuntimeError("no kernel sources under csrc/kernels")
+    # extra defines of a study build go into a flags stamp the rebuild check compares, so a stamped
+    # (instrumented) build is never silently kept by a later normal import, nor skipped by one
+    defines = ["-DMIHVD_F32_STAMPS=1"] if os.environ.get("MIHVD_F32_STAMPS") == "1" else []
+    os.makedirs(BUILD, exist_ok=True)
+    stamp = os.path.join(BUILD, "kernel_flags.txt")
+    old = open(stamp).read() if os.path.exists(stamp) else ""
+    if old != " ".join(defines):
+        force = True
     if not force and not _newer(KERNELS_SO, srcs + hdrs + [__file__]):
         return KERNELS_SO
     tdir, tinc, tlib, abi = _torch_paths()
@@ -113,8 +121,7 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int | None =
     ]
     if os.environ.get("MIHVD_SAVE_TEMPS"):
         common += ["-save-temps=obj"]
-    if os.environ.get("MIHVD_F32_STAMPS") == "1":  # study build: in-kernel phase stamps (scripts/stamps_f32.py)
-        common += ["-DMIHVD_F32_STAMPS=1"]
+    common += defines  # study build: in-kernel phase stamps (scripts/stamps_f32.py)
 
     def compile_one(src):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
@@ -141,6 +148,8 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int | None =
             "-lc10", "-lc10_hip", "-ltorch_hip", "-Wl,-rpath," + tlib, "-o", tmp]
     _run(link, cwd=BUILD)
     os.replace(tmp, KERNELS_SO)
+    with open(stamp, "w") as f:
+        f.write(" ".join(defines))
     return KERNELS_SO
 
 

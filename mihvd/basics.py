@@ -64,6 +64,7 @@ class _Context:
         self.store = None          # NativeStore (C++ TCP store) when launched by mihvdrun
         self.store_server = None   # StoreServer this process hosts (negotiation without mihvdrun)
         self.engine = None         # negotiated-collective Engine (MIHVD_NEGOTIATE=1)
+        self.plane = None          # DistributedOptimizer's bucket data plane (collectives.BucketPlane)
         self.elastic_gen = None    # elastic: membership generation of the current world (kept across re-inits)
         self.lock = threading.RLock()
 
@@ -382,6 +383,12 @@ def shutdown():
             _ctx.engine.flush(timeout=30)
             _ctx.engine.stop()
             _ctx.engine = None
+        if _ctx.plane is not None:
+            try:
+                _ctx.plane.close()
+            except Exception:  # pragma: no cover
+                pass
+            _ctx.plane = None
         if _ctx.stall is not None:
             _ctx.stall.stop()
             _ctx.stall = None

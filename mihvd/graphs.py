@@ -53,7 +53,8 @@ class CapturedStep:
     autograd's same-stream accumulation path.
     """
 
-    def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False, sync_warmup: bool = False):
+    def __init__(self, step_fn, warmup: int = 3, pool=None, serialize: bool = False, sync_warmup: bool = False,
+                 params=None):
         if not torch.cuda.is_available():
             raise RuntimeError("CapturedStep needs a GPU")
         self.step_fn = step_fn
@@ -68,7 +69,16 @@ class CapturedStep:
             for i in range(warmup):
                 out = step_fn()
                 if hold and i == warmup - 1:
-                    self.accumulators = accumulate_grad_nodes(out)
+                    # the nodes of the warm-up graph (step_fn returns a tensor with a grad_fn), or
+                    # those of ``params`` directly (a step that returns loss.detach(), a float, None)
+                    self.accumulators = (param_accumulate_grad_nodes(params) if params is not None
+                                         else accumulate_grad_nodes(out))
+                    if not self.accumulators:
+                        import warnings
+
+                        warnings.warn("CapturedStep: no AccumulateGrad node found to hold (step_fn returned "
+                                      "no tensor with a grad_fn; pass params=): the capture re-creates them, "
+                                      "the form that replays stale gradient reads (see the class docstring)")
                 _detach(out)
                 del out
                 if sync_warmup:
@@ -112,6 +122,18 @@ def _stream_mismatch_warning(on: bool):
         torch._C, "_warn_on_accumulate_grad_stream_mismatch") else True
     g.set_warn_on_accumulate_grad_stream_mismatch(bool(on))
     return prev
+
+
+def param_accumulate_grad_nodes(params):
+    """The ``AccumulateGrad`` node of every leaf tensor in ``params`` that requires grad (the node
+    autograd keeps for the leaf, reached through a view's backward)."""
+    found = []
+    for p in params:
+        if torch.is_tensor(p) and p.requires_grad and p.grad_fn is None:
+            node = p.view_as(p).grad_fn.next_functions[0][0]
+            if node is not None:
+                found.append(node)
+    return found
 
 
 def accumulate_grad_nodes(out):

@@ -72,6 +72,19 @@ FC_START = SEGMENTS["dense/bias"][0]    # bucket "fc" = [dense/bias .. dense/ker
 W3_START = SEGMENTS["dense/kernel"][0]  # [0, W3_START) = every gradient except dense/kernel
 
 
+def f32_plane_mode() -> str:
+    """``MIHVD_F32_PLANE``: the fp32 sharded data plane — ``auto`` (default: select_data_plane times
+    the reduce-scatter and the factor-gather planes and keeps the faster), ``rs`` or ``factor``."""
+    v = os.environ.get("MIHVD_F32_PLANE", "auto").strip().lower()
+    return v if v in ("rs", "factor") else "auto"
+
+
+def _check_tol() -> float:
+    """``MIHVD_XGMI_CHECK_TOL``: relative distance allowed between a candidate plane's timed steps and
+    the reference plane's from the same snapshot (select_data_plane)."""
+    return float(os.environ.get("MIHVD_XGMI_CHECK_TOL", "1e-3"))
+
+
 class _SyncOps:
     """torch.ops.mihvd with a synchronize + error check after every launch (MIHVD_DEBUG_SYNC)."""
 
@@ -160,6 +173,12 @@ class FusedMNISTTrainer:
         # communicator (mihvd/parallel/rccl.py) instead of the process group's; the process group
         # is the fallback (MIHVD_COMM=torch, or a communicator that cannot be created)
         self.ncomm = None
+        # a second framework-owned communicator for the fp32 step's small-gradient allreduce, which
+        # then runs on the main stream right behind the gradient reduction while the first carries
+        # dense/kernel's row collectives on the side stream: every rank issues each communicator's
+        # collectives in one program order on one stream, so the two never need a cross-stream
+        # edge to order them (docs/ARCHITECTURE.md, "N > 1 fp32 step")
+        self.ncomm_small = None
         if self.collectives:
             from ..parallel import rccl as _rccl
 
@@ -173,17 +192,21 @@ class FusedMNISTTrainer:
                 if dist.is_initialized() and dist.get_backend() == "nccl":
                     try:
                         self.ncomm = _rccl.NativeComm(device=self.device)
+                        if self.f32:
+                            self.ncomm_small = _rccl.NativeComm(device=self.device)
                     except Exception as e:  # pragma: no cover - depends on the RCCL build
                         import warnings
 
                         warnings.warn(f"native RCCL communicator unavailable ({e!r}); using the process group's")
-                        self.ncomm = None
-                    # every rank must use the same communicator: any failure moves all to the fallback
-                    flag = torch.tensor([0 if self.ncomm is not None else 1], device=self.device)
+                    ok = self.ncomm is not None and (self.ncomm_small is not None or not self.f32)
+                    # every rank must use the same communicators: any failure moves all to the fallback
+                    flag = torch.tensor([0 if ok else 1], device=self.device)
                     dist.all_reduce(flag)
-                    if int(flag.item()) != 0 and self.ncomm is not None:
-                        self.ncomm.close()
-                        self.ncomm = None
+                    if int(flag.item()) != 0:
+                        for c in (self.ncomm, self.ncomm_small):
+                            if c is not None:
+                                c.close()
+                        self.ncomm = self.ncomm_small = None
         self.rank = basics.rank() if basics.is_initialized() else 0
         self.op = op
         self.compression = compression
@@ -206,39 +229,34 @@ class FusedMNISTTrainer:
         u8 = dict(device=dev, dtype=torch.uint8)
         self.a1 = torch.empty(B, 14, 14, 32, **bf)
         self.idx1 = torch.empty(B, 14, 14, 32, **u8)
-        # Data-parallel "factor gather" (size > 1, op Average/Sum): dW3 = a2^T dz has rank B, so
-        # instead of allreducing the 12.8 MB dW3 every rank all-gathers the bf16 factors a2 and dz
-        # (832 KB per rank at B=100) and multiplies them over the batch of every rank — the exact
-        # sum the allreduce would produce (fp32 accumulation over all samples), 4-16x fewer bytes.
+        # Data-parallel "factor gather" (bf16 step, size > 1, op Average/Sum): dW3 = a2^T dz has rank
+        # B, so instead of allreducing the 12.8 MB dW3 every rank all-gathers the bf16 factors a2 and dz
+        # (832 KB per rank at B=100) and multiplies them over the batch of every rank — the exact sum
+        # the allreduce would produce (fp32 accumulation over all samples), 4-16x fewer bytes. With
+        # compression or Adasum the bf16 step reduces gradient buckets instead.
         from ..basics import ReduceOp
 
-        self.gather = (self.collectives and compression == "none" and not self.f32
-                       and os.environ.get("MIHVD_FC_GATHER", "1") != "0"
-                       and (op is None or ReduceOp(op) in (ReduceOp.Average, ReduceOp.Sum)))
-        # Sharded dense/kernel optimizer (factor-gather plane only; shard_optimizer=True or
-        # MIHVD_SHARD_W3=1): rank r owns W3 row tiles [r*T, (r+1)*T) of the 49 64-row tiles
-        # (T = ceil(49/size)). It computes dW3 for those rows only (over every rank's samples, so the
-        # result is the exact allreduced sum), applies Adam to them, and gathers the updated bf16
-        # rows of the other ranks into a padded shadow [size*T*64][1024] before the next fc1_fwd,
-        # instead of every rank computing all of dW3 and updating all of W3. fp32 master rows / Adam
-        # slots of other ranks' rows are not maintained here; call gather_full_state() on every
-        # rank before variables()/to_model(). Unsharded, every rank owns all 49 tiles. The flag can
-        # change between steps (set_sharding, collective): the row gather moves (size-1)/size of the
-        # 6.4 MB bf16 W3 per step over size-1 links, so it pays at 8 GPUs, not at 2.
+        avg_or_sum = op is None or ReduceOp(op) in (ReduceOp.Average, ReduceOp.Sum)
+        self.gather = self.collectives and compression == "none" and not self.f32 and avg_or_sum
+        # Sharded dense/kernel optimizer (shard_optimizer=True or MIHVD_SHARD_W3=1). bf16 (factor-gather
+        # plane): rank r owns W3 row tiles [r*T, (r+1)*T) of the 49 64-row tiles (T = ceil(49/size)); it
+        # computes dW3 for those rows only (over every rank's samples, so the result is the exact
+        # allreduced sum), applies Adam to them, and gathers the updated bf16 rows of the other ranks
+        # into a padded shadow [size*T*64][1024] before the next fc1_fwd. fp32: dense/kernel's gradient
+        # is reduce-scattered by rows (or formed from the exchanged factors, MIHVD_F32_PLANE), Adam
+        # runs on this rank's 3136/size rows, and the updated fp32 rows are all-gathered while the
+        # next step's convolutions run (at size 1 with MIHVD_FORCE_COLLECTIVES the same step runs with
+        # R = 3136 rows: the exact multi-rank launch/collective sequence, capture-testable on one GPU).
+        # fp32 master rows / Adam slots of other ranks' rows are not maintained here; call
+        # gather_full_state() on every rank before variables()/to_model(). The flag can change between
+        # steps (set_sharding, collective).
         if shard_optimizer is None:
             shard_optimizer = os.environ.get("MIHVD_SHARD_W3", "0") == "1"
-        self.shard_w3 = bool(shard_optimizer) and self.gather and not self.fuse_w3_requested()
-        # fp32 step over RCCL: the same option as a reduce-scatter of dW3 by rows, Adam on this rank's
-        # 3136/size rows, and an all-gather of the updated fp32 rows overlapping the next step's
-        # convolutions (instead of allreducing dW3 and every rank updating all of W3)
-        # (at size 1 with MIHVD_FORCE_COLLECTIVES the same step runs with R = 3136 rows: the exact
-        # multi-rank launch/collective sequence, capture-testable on one GPU)
-        self._f32_can_shard = (self.f32 and self.collectives and 3136 % self.world == 0
-                               and compression == "none" and (op is None or ReduceOp(op) in (ReduceOp.Average,
-                                                                                              ReduceOp.Sum)))
-        if self.f32:
-            self.shard_w3 = bool(shard_optimizer) and self._f32_can_shard
+        self._f32_can_shard = (self.f32 and self.collectives and 3136 % self.world == 0 and compression == "none"
+                               and avg_or_sum)
+        self.shard_w3 = bool(shard_optimizer) and (self._f32_can_shard if self.f32 else self.gather)
         self._shadow_ev = None
+        self._small_ev = None
         self._full_state_valid = True
         self._T = -(-49 // self.world)
         lo, hi = self.rank * self._T, min((self.rank + 1) * self._T, 49)
@@ -298,44 +316,15 @@ class FusedMNISTTrainer:
         self.g2 = torch.empty(B, 3136, **bf)        # pooled conv2 gradient, masked (fc1_dgrad output)
         self.slab = torch.empty(int(self.ops.conv2_wgrad_groups(B)), 51200, **f32)
         self.cpart = torch.empty(B, 896, **f32)     # per-image dW1 | db1 | db2 partial rows
-        # fp32 step: MIHVD_FUSED_OPT=1 (default) folds the optimizer into the step's kernels — the
-        # small parameters' Adam into the gradient-reduction launch (world size 1) and dense/kernel's
-        # into tail blocks of the next step's conv2_fwd launch; MIHVD_F32_TAIL_BLOCKS sets their count
-        # (default: one per CU)
-        self.f32_fused_opt = self.f32 and os.environ.get("MIHVD_FUSED_OPT", "1") != "0"
-        self.f32_tail_blocks = int(os.environ.get("MIHVD_F32_TAIL_BLOCKS", "0"))
-        # where dense/kernel's fused Adam update runs: "bwd" (default) = inside f32_fc1_bwd, whose row
-        # blocks read W3 once for the dgrad, form dW3 of the same elements in registers and update
-        # them (dW3 never goes through HBM); "fc1" = deferred into the next step's fc1_fwd, which
-        # reads W3 anyway; "tail" = deferred into tail blocks of the next conv2_fwd; "side" = on the
-        # side stream beside the conv backward of the same step (world size 1 only; the cross-queue
-        # join of a captured graph costs more than it hides here)
-        self.f32_w3 = os.environ.get("MIHVD_F32_W3", "bwd")
-        if self.f32_w3 == "fc1" and B > 112:  # the fused update keeps the a2 slice + a W3 tile in LDS
-            self.f32_w3 = "tail"
-        self._w3_pending = False
-        # MIHVD_F32_CONV1_FUSE=1 (measured alternative, off): in graph-replayed world-size-1 fp32
-        # steps the next step's conv1 runs inside this step's f32_conv_reduce launch (after W1/b1's
-        # Adam and the step bump; f32_bwd.hip). Bitwise equal, but 19.8 us for the merged launch vs
-        # 6.9 + 7.0 us apart (150.7 vs 145.3 us/step): conv1 still waits for the whole reduction,
-        # and the cross-XCD release/acquire costs more than the saved launch
-        self.f32_conv1_fuse = self.f32 and os.environ.get("MIHVD_F32_CONV1_FUSE", "0") == "1"
-        # MIHVD_F32_CONV12=1 (measured alternative, off): conv1 runs inside the conv2 forward launch
-        # (f32_conv12_fwd: every conv2 block computes the a1 rows it reads from x and writes its own
-        # rows of a1/idx1 for the backward) instead of a launch of its own. Bitwise equal, but each
-        # block recomputes its halo rows and the conv2 MFMA loop starts later: 135.1 vs 132.4 us per
-        # whole step (scripts/kbench_f32.py, profiles/r04/kbench_f32_r04c.txt)
-        self.f32_conv12 = self.f32 and os.environ.get("MIHVD_F32_CONV12", "0") == "1"
-        # MIHVD_F32_W2F=1 (default): the conv1 launch also writes two fragment copies of W2 (the
-        # register operands of conv2_fwd and of the conv2_bwd dgrad blocks, in the order their waves
-        # load them: one contiguous 1 KB per wave-load instead of scattered 64-byte row pieces), which
-        # both conv2 launches of the step then read (csrc/kernels/f32_fwd.hip, f32_w2_frag_block).
-        # Measured (B = 100): conv2_fwd 21.2 -> 19.8 us, conv2_bwd 43.8 -> 40.5 us, conv1 unchanged,
-        # whole step 124.7 -> 122.4 us (profiles/r04/kbench_f32_r04m.txt); bitwise equal
-        self.w2frag = (torch.empty(2, 51200, device=dev, dtype=torch.float32)
-                       if self.f32 and os.environ.get("MIHVD_F32_W2F", "1") != "0" else None)
-        self._c1_ready = False
-        self._c1_sync = torch.zeros(4, device=dev, dtype=torch.int32) if self.f32 else None
+        # fp32 step: the conv1 launch also writes two fragment copies of W2 (the register operands of
+        # conv2_fwd and of the conv2_bwd dgrad blocks, in the order their waves load them: one
+        # contiguous 1 KB per wave-load instead of scattered 64-byte row pieces), which both conv2
+        # launches of the step then read (csrc/kernels/f32_fwd.hip, f32_w2_frag_block). Measured
+        # (B = 100): conv2_fwd 21.2 -> 19.8 us, conv2_bwd 43.8 -> 40.5 us, whole step 124.7 -> 122.4 us
+        # (profiles/r04/kbench_f32_r04m.txt); bitwise equal
+        self.w2frag = torch.empty(2, 51200, device=dev, dtype=torch.float32) if self.f32 else None
+        self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when it is fused away
+        self.f32_factor = False
         if self.f32:
             ops = self.ops
             self.a1 = torch.empty(B, 14, 14, 32, **f32)
@@ -348,112 +337,46 @@ class FusedMNISTTrainer:
             self.slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, **f32)
             self.cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, **f32)
             self.g2 = None
-            # sharded dense/kernel optimizer: this rank's rows of the reduce-scattered dW3
+            # sharded dense/kernel optimizer: this rank's rows of the reduced dW3
             self._f32_R = 3136 // self.world if self.world > 0 and 3136 % self.world == 0 else 0
             self.gshard = torch.empty(max(self._f32_R, 1), 1024, **f32) if self._f32_can_shard else None
-            # fp32 factor-gather plane (sharded optimizer; MIHVD_F32_PLANE=factor, or picked by
-            # select_data_plane): dW3 = a2^T dz has rank B per rank, so instead of reduce-scattering
-            # the 12.8 MB dW3 every rank all-gathers the fp32 dz of all ranks ([N][B][1024]) and
-            # receives from each rank the a2 columns of its own R rows ([N][B][R], all-to-all); its
-            # rows of dW3 are then the exact sum over all N B samples (one fp32 GEMM, R x NB x 1024,
-            # on the side stream beside the conv backward), and fc1_bwd runs its dgrad only. Per rank
-            # (N - 1) B (1024 + R) floats arrive instead of (N - 1) R 1024 (N = 8: 3.9 vs 11.2 MB).
+            # fp32 factor-gather plane (sharded optimizer; MIHVD_F32_PLANE=factor, or timed by
+            # select_data_plane under "auto"): dW3 = a2^T dz has rank B per rank, so instead of
+            # reduce-scattering the 12.8 MB dW3 every rank all-gathers the fp32 dz of all ranks
+            # ([N][B][1024]) and receives from each rank the a2 columns of its own R rows ([N][B][R],
+            # all-to-all); its rows of dW3 are then the exact sum over all N B samples, formed by the
+            # hand-written row kernel with Adam applied from the accumulators (csrc/kernels/
+            # f32_factor.hip) on the side stream beside the conv backward, and fc1_bwd runs its dgrad
+            # only. Per rank (N - 1) B (1024 + R) floats arrive instead of (N - 1) R 1024 (N = 8: 3.9
+            # vs 11.2 MB).
             if self._f32_can_shard:
                 N, R = self.world, self._f32_R
                 self.dz_all32 = torch.empty(N, B, 1024, **f32)
-                self.dz = self.dz_all32[self.rank]  # head writes this rank's block in place
+                # (the head writes this rank's dz into self.dz, a buffer of its own: the all-gather
+                # copies it into dz_all32 while fc1_bwd reads self.dz, so the two never alias)
                 self.a2_send = torch.empty(N, B, R, **f32)
                 self.a2_recv = torch.empty(N, B, R, **f32)
-                self.f32_factor = self.shard_w3 and os.environ.get("MIHVD_F32_PLANE", "rs") == "factor"
-            # the dW3 rows: a library fp32 GEMM + adam_step (default), or MIHVD_F32_FACTOR_KERNEL=1 the
-            # hand-written row kernel with Adam from the accumulators (csrc/kernels/f32_factor.hip;
-            # measured slower at N = 8: 17.3 us against 11.2 us + ~3 us, profiles/r04/kbench_f32_r04q.txt)
-            self.f32_factor_kernel = os.environ.get("MIHVD_F32_FACTOR_KERNEL", "0") == "1"
+                self.f32_factor = self.shard_w3 and f32_plane_mode() == "factor"
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         self.X = self.Y = self.rows = None
         self.graph = None
         self._graphs = {}
         self.steps_per_replay = 1
-        # Overlap the "fc" bucket's allreduce with the conv backward on a side stream (N > 1). A
-        # stream fork/join costs a few us inside a HIP graph, so it is only used with collectives.
-        self.overlap = os.environ.get("MIHVD_OVERLAP", "1") != "0"
-        # MIHVD_ADAM_PIPELINE=1: the "fc" part of the Adam update runs on a side stream after the
-        # last reader of W3 (fc1_dgrad) and overlaps the conv backward and the next step's convs.
-        self.pipeline = os.environ.get("MIHVD_ADAM_PIPELINE", "0") == "1" and not self.gather
-        self.adam_blocks = int(os.environ.get("MIHVD_ADAM_BLOCKS", "0"))
-        # conv1 + conv2 forward in one launch (conv1 on MFMA with bf16 operands); 0 = separate
-        # launches with conv1 as an fp32 VALU convolution
-        self.conv12 = os.environ.get("MIHVD_CONV12", "1") != "0"
-        # fc1 dgrad tiles and the fc1 wgrad roles in one launch (0 = two launches)
-        self.fc1_merged = os.environ.get("MIHVD_FC1_BWD", "1") != "0"
-        # MIHVD_FUSE_W3_ADAM=1: the dW3 tiles of fc1_wgrad apply Adam to dense/kernel (98 %
-        # of the parameters) from their accumulators, so dW3 never goes through HBM and the flat
-        # optimizer only covers the other 65 K parameters. Needs dW3 to be complete on this rank:
-        # size 1, or the factor-gather data plane (dW3 over every rank's samples).
-        # Measured on MI355X (B=100): fused 21.4 us vs fc1_wgrad 7.1 + flat Adam 16.2 us; the fused
-        # epilogue streams p/m/v at ~5.9 TB/s in 256-B row pieces but does not hide the dW3 chain,
-        # so the step is 1-2 us slower and the option is off by default.
-        self.fuse_w3 = (os.environ.get("MIHVD_FUSE_W3_ADAM", "0") == "1" and not self.pipeline
-                        and (not self.collectives or self.gather))
-        self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when fused
-        # sharded factor-gather step over RCCL: dW3 of this rank's rows with Adam in the tile epilogue
-        # (the xGMI plane's form; the 8-rank slice 9.0 us vs 6.1 + 4.0 us for dW3 then adam_step,
-        # bit-identical: same tiles, same adam4). MIHVD_FUSE_W3_SLICE=0: the two launches
-        self.fuse_slice = os.environ.get("MIHVD_FUSE_W3_SLICE", "1") != "0"
-        # MIHVD_FUSED_OPT=1 (default at world size 1): no separate optimizer launch. The dense/kernel
-        # update (98 % of the optimizer's HBM traffic) streams in the tail of the conv2_bwd launch —
-        # tail-only blocks on the CUs the conv roles leave idle, conv blocks joining as they finish —
-        # and conv2_wgrad_reduce applies Adam to every other parameter as it produces the gradients.
+        # bf16 at world size 1: no separate optimizer launch. The dense/kernel update (98 % of the
+        # optimizer's HBM traffic) streams in the tail of the conv2_bwd launch — tail-only blocks on
+        # the CUs the conv roles leave idle, conv blocks joining as they finish — and
+        # conv2_wgrad_reduce applies Adam to every other parameter as it produces the gradients.
         # Measured (B=100): 78.4 us/step vs 80.0 us with the flat adam_step launch.
-        self.fused_opt = (os.environ.get("MIHVD_FUSED_OPT", "1") != "0" and not self.collectives and not self.f32
-                          and not self.pipeline and not self.fuse_w3)
-        # Fused optimizer split of dense/kernel: the first MIHVD_REDUCE_W3 of its rows (a fraction,
-        # rounded to 256 elements) are updated by the gradient-reduction launch next to the conv
-        # reductions, the rest streams inside conv2_bwd. Default 0: moving 10-30 % to the reduce
-        # launch measured 0.4-1.8 us slower per step (the reduce grows more than conv2_bwd shrinks).
-        frac = min(max(float(os.environ.get("MIHVD_REDUCE_W3", "0")), 0.0), 1.0)
-        self.tail_split = W3_START + int(frac * (FLAT_NUMEL - W3_START)) // 256 * 256
-        # MIHVD_FOLD_REDUCE=1 (opt-in): the gradient reduction + the rest of Adam run inside the conv2_bwd
-        # launch (conv2_bwd_adam_fold: arrival counter, write-through hand-off) instead of a launch of
-        # their own; the kernel falls back to two launches where every conv block cannot be resident.
-        # Bitwise equal, but measured slower on MI355X (35.6 vs 25.0 us for the pair): waiting for the
-        # slowest conv block serialises the reduction behind it (docs/ARCHITECTURE.md).
-        self.fold_reduce = self.fused_opt and os.environ.get("MIHVD_FOLD_REDUCE", "0") == "1"
-        self.fold_sync = torch.zeros(4, dtype=torch.int32, device=self.device)  # [arrive, depart, error, -]
-        # MIHVD_W3_TAIL=1 (opt-in, with the fused optimizer): conv2_bwd's tail computes dW3 = a2^T dz tile by
-        # tile on MFMA from the bf16 factors and applies Adam to dense/kernel from the accumulators
-        # (csrc/kernels/w3_tail.h), so fc1_bwd only runs the dgrad tiles and the small reductions and
-        # dW3 never goes through HBM (25.7 MB less per step); bitwise equal to the stored-dW3 tail.
-        self.w3_tail = self.fused_opt and os.environ.get("MIHVD_W3_TAIL", "0") == "1"
-        if self.w3_tail:
-            # the fc1 factors transposed (K-contiguous, zero past the batch), left by fc1_bwd's dgrad
-            # blocks for the tail's MFMA fragments
-            self.a2T = torch.zeros(3136, 128, **bf)
-            self.dzT = torch.zeros(1024, 128, **bf)
-        self._fc_update_pending = False
-        self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.pipeline or self.f32) else None
+        self.fused_opt = not self.collectives and not self.f32
+        self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.f32) else None
         if compression == "bf16" and self.collectives:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
         else:
             self.wire = None
-        # Bucket-allreduce plane (MIHVD_FC_GATHER=0) with MIHVD_XGMI_ALLREDUCE=1: the fp32 gradient
-        # buckets go through the direct xGMI one-shot allreduce (mihvd/parallel/xgmi.py) instead of
-        # RCCL. One context per bucket: the "fc" and "conv" buckets can be in flight on two streams
-        # at once. Contexts are created (collectively) on a bucket's first use, in the eager warm-up
-        # steps; ranks on several nodes fall back to RCCL (XGMIUnavailable on every rank alike).
-        self.xgmi = None
-        if (not self.gather and os.environ.get("MIHVD_XGMI_ALLREDUCE", "0") == "1" and self.collectives
-                and self.wire is None and self.world <= 8 and dev.type == "cuda"
-                and (op is None or ReduceOp(op) != ReduceOp.Adasum)):
-            self.xgmi = {}
         self._closed = False
 
     # ----------------------------------------------------------------------------- views
-    @staticmethod
-    def fuse_w3_requested() -> bool:
-        return os.environ.get("MIHVD_FUSE_W3_ADAM", "0") == "1"
-
     def w3_shadow(self) -> torch.Tensor:
         """The bf16 dense/kernel the MFMA kernels read ([3136][1024], contiguous): on the
         factor-gather plane the first 3136 rows of the (row-gathered) shadow3 buffer."""
@@ -547,320 +470,179 @@ class FusedMNISTTrainer:
         st = self.state
         main = torch.cuda.current_stream(self.device)
         self._conv_forward(x, rows, st)
-        if self._fc_update_pending:
-            # the previous step's "fc" Adam update (side stream) overlapped the two convolutions above
-            main.wait_stream(self._side)
-            self._fc_update_pending = False
         o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        b1, b2 = self.betas
         if self.fused_opt:
-            b1, b2 = self.betas
-            if self.w3_tail:  # dgrad tiles (+ the transposed factors) and the small reductions; dW3 runs in
-                # conv2_bwd's tail
-                o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.pview("dense/kernel", self.shadow),
-                          self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
-                          self.gview("dense_1/bias"), self.g2, 2, -1, self.a2T, self.dzT)
-            elif self.fc1_merged:  # dgrad tiles and every wgrad role in one launch
-                o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.pview("dense/kernel", self.shadow),
-                          self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
-                          self.gview("dense_1/bias"), self.g2)
-            else:
-                o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
-                            self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
-                o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)  # last reader of W3
-            w3 = slice(W3_START, FLAT_NUMEL)
+            # dgrad tiles and every wgrad role in one launch; dense/kernel's Adam streams in the tail
+            # of conv2_bwd, every other parameter's in the gradient-reduction launch
+            o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.pview("dense/kernel", self.shadow),
+                      self.gview("dense/kernel"), self.gview("dense/bias"), self.gview("dense_1/kernel"),
+                      self.gview("dense_1/bias"), self.g2)
+            t3 = slice(W3_START, FLAT_NUMEL)
             w2 = self.pview("conv_layer2/conv2d/kernel", self.shadow)
-            if self.w3_tail:
-                o.conv2_bwd_w3adam(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
-                                   self.dzT, self.a2T, self.params[w3], self.m[w3], self.v[w3], self.shadow[w3],
-                                   self.grads[w3] if self.keep_w3_grad else None, self.lr, b1, b2, self.eps, 1.0,
-                                   self.rule)
-                split = W3_START
-            elif self.fold_reduce and self.tail_split == W3_START:
-                o.conv2_bwd_adam_fold(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
-                                      self.gview("conv_layer2/conv2d/kernel"), self.gview("conv_layer1/conv2d/kernel"),
-                                      self.gview("conv_layer1/conv2d/bias"), self.gview("conv_layer2/conv2d/bias"),
-                                      self.grads, self.params, self.m, self.v, self.shadow, self.fold_sync, FC_START,
-                                      W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
-                return
-            else:
-                split = self.tail_split
-                t3 = slice(split, FLAT_NUMEL)
-                o.conv2_bwd_adam(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
-                                 self.params[t3], self.grads[t3], self.m[t3], self.v[t3], self.shadow[t3], self.lr, b1,
-                                 b2, self.eps, 1.0, self.rule)
+            o.conv2_bwd_adam(self.g2, self.idx2, self.a1, w2, x, rows, st, self.idx1, self.slab, self.cpart,
+                             self.params[t3], self.grads[t3], self.m[t3], self.v[t3], self.shadow[t3], self.lr, b1,
+                             b2, self.eps, 1.0, self.rule)
             o.conv2_wgrad_reduce_adam(self.slab, self.cpart, self.B, self.gview("conv_layer2/conv2d/kernel"),
                                       self.gview("conv_layer1/conv2d/kernel"), self.gview("conv_layer1/conv2d/bias"),
                                       self.gview("conv_layer2/conv2d/bias"), self.grads, self.params, self.m, self.v,
-                                      self.shadow, st, FC_START, split, self.lr, b1, b2, self.eps, 1.0, self.rule)
+                                      self.shadow, st, FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
             return
-        if self.fuse_w3:
-            # W3 is updated in place by the dW3 tiles: its last reader (fc1_dgrad) goes first
-            o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
-            self._fc1_wgrad_w3_adam(3, None, None)
-            self._conv_backward(x, rows, st)
-            b1, b2 = self.betas
-            o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START],
-                        self.shadow[:W3_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-            return
+        # bucket plane (bf16 step with compression or Adasum): bucket "fc" is complete after
+        # fc1_wgrad and is reduced on the side stream while the conv backward runs
         o.fc1_wgrad(self.dz, self.a2, self.h, self.dlog, self.gview("dense/kernel"), self.gview("dense/bias"),
                     self.gview("dense_1/kernel"), self.gview("dense_1/bias"))
-        fc_bucket = self.grads[FC_START:]
-        conv_bucket = self.grads[:FC_START]
-        overlap = self.collectives and self.overlap
-        ar_done = None
-        if overlap:
-            # bucket "fc" is complete: reduce it on the side stream while the conv backward runs
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                self._allreduce(fc_bucket, FC_START, FLAT_NUMEL)
-                if self.pipeline:
-                    ar_done = torch.cuda.Event()
-                    ar_done.record(self._side)
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            self._allreduce(self.grads[FC_START:], FC_START, FLAT_NUMEL)
         o.fc1_dgrad(self.dz, self.pview("dense/kernel", self.shadow), self.a2, self.g2)
-        b1, b2 = self.betas
-        if self.pipeline:
-            # fc1_dgrad was the last reader of W3: the "fc" update (98 % of the optimizer bytes) runs
-            # on the side stream, overlapping the conv backward and the next step's convolutions.
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                o.adam_step(self.params[FC_START:], fc_bucket, self.m[FC_START:], self.v[FC_START:],
-                            self.shadow[FC_START:], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 0,
-                            None, self.adam_blocks)
-            self._fc_update_pending = True
         self._conv_backward(x, rows, st)
-        if self.pipeline:
-            if self.collectives:
-                if ar_done is not None:
-                    main.wait_event(ar_done)  # one collective at a time on the communicator
-                self._allreduce(conv_bucket, 0, FC_START)
-            o.adam_step(self.params[:FC_START], conv_bucket, self.m[:FC_START], self.v[:FC_START],
-                        self.shadow[:FC_START], st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-            return
-        if overlap:
-            self._allreduce(conv_bucket, 0, FC_START)
-            main.wait_stream(self._side)
-        elif self.collectives:
-            self._allreduce(self.grads, 0, FLAT_NUMEL)  # one fused collective for the whole buffer
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):  # one communicator, one stream: the same order on every rank
+            self._allreduce(self.grads[:FC_START], 0, FC_START)
+        main.wait_stream(self._side)
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
 
     def _launch_step_f32(self, x, rows, labels):
-        """Exact-fp32 step (csrc/kernels/f32_fwd.hip, f32_bwd.hip), one stream at world size 1:
+        """Exact-fp32 step (csrc/kernels/f32_fwd.hip, f32_bwd.hip). At world size 1, seven launches on
+        one stream:
 
-            conv1 | conv2 | fc1_fwd | head | fc1_bwd (dgrad -> dY2, dW3, db3, dW4, db4) |
-            conv2_bwd (dgrad + fused conv1 wgrad, conv2 wgrad slabs) | conv reduce | adam
+            conv1 (+ W2 fragments) | conv2 | fc1_fwd | head | fc1_bwd (dgrad -> dY2; dW3 + W3 Adam in
+            registers; db3, dW4, db4) | conv2_bwd (dgrad + fused conv1 wgrad, conv2 wgrad slabs) |
+            conv_reduce (+ Adam of every other parameter, step bump)
 
-        With collectives the "fc" bucket (dense/*, dense_1/*: 98.4 % of the bytes) is complete
-        after fc1_bwd and is allreduced on the side stream while the conv backward runs; the conv
-        bucket follows the reduction; Adam applies the 1/size of Average."""
+        With collectives the step's second half moves to the side stream as soon as its inputs
+        exist (_launch_step_f32_shard / _f32_collective_tail); the next step's conv1 joins it."""
         o = self.ops
         st = self.state
         P, G = self.pview, self.gview
-        main = torch.cuda.current_stream(self.device)
         b1, b2 = self.betas
         w2 = P("conv_layer2/conv2d/kernel")
         w3 = P("dense/kernel")
         s3 = slice(W3_START, FLAT_NUMEL)
-        if self.shard_w3:
-            return self._launch_step_f32_shard(x, rows, labels)
-        fused12 = self.f32_conv12 and not self._c1_ready and not (self._w3_pending and self.f32_w3 == "tail")
-        wf = None  # the W2 fragment copies, when this step's conv1 launch writes them
-        if self._c1_ready:
-            self._c1_ready = False  # the previous step's conv_reduce computed this step's conv1
-        elif fused12:
-            o.f32_conv12_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                             self.idx1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
-        else:
-            o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                            self.idx1, *((w2, self.w2frag) if self.w2frag is not None else ()))
-            wf = self.w2frag
-        if fused12:
-            pass  # conv2 ran in the launch above
-        elif self._w3_pending and self.f32_w3 == "tail":
-            # the previous step's dense/kernel Adam update (98 % of the optimizer's bytes) streams in
-            # tail blocks of this MFMA-bound launch; fc1_fwd below is its first reader
-            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, self.params[s3],
-                            self.grads[s3], self.m[s3], self.v[s3], st, self.lr, b1, b2, self.eps, 1.0 / self.world,
-                            self.rule, self.f32_tail_blocks)
-            self._w3_pending = False
-        else:
-            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2,
-                            w2frag=wf[0] if wf is not None else None)
-        if self._w3_pending:
-            # ... or inside fc1_fwd, W3's first reader: the update of each fragment in registers
-            o.f32_fc1_fwd(self.a2, w3, self.zpart, self.grads[s3], self.m[s3], self.v[s3], st, self.lr, b1, b2,
-                          self.eps, 1.0 / self.world, self.rule)
-            self._w3_pending = False
-        else:
-            o.f32_fc1_fwd(self.a2, w3, self.zpart)
-        o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
-                           self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
-        w3_bwd = self.f32_fused_opt and not self.collectives and self.f32_w3 == "bwd"
-        if w3_bwd:
-            # dgrad, dW3 and dense/kernel's Adam from one read of W3 (dW3 stays in registers unless
-            # keep_w3_grad)
-            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
-                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3], self.v[s3], st, self.lr,
-                          b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad)
-        else:
-            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
-                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
-        overlap = self.collectives and self.overlap
-        w3_side = self.f32_fused_opt and not self.collectives and self.f32_w3 == "side"
-        if overlap:
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                self._allreduce(self.grads[FC_START:], FC_START, FLAT_NUMEL)
-        elif w3_side:
-            # dense/kernel's Adam (98 % of the optimizer's bytes, HBM-bound) runs beside the
-            # MFMA-bound conv backward; the step's end joins it
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                o.adam_step(self.params[s3], self.grads[s3], self.m[s3], self.v[s3], None, st, 0, self.lr, b1, b2,
-                            self.eps, 1.0, self.rule, 0)
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab,
-                        w2frag=wf[1] if wf is not None else None)
-        gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
-                 G("conv_layer2/conv2d/bias"))
-        if self.f32_fused_opt and not self.collectives:
-            # gradient reduction + Adam of every parameter but dense/kernel + the step bump, one launch
-            # (+ the next step's conv1 when the steps are being captured back to back)
-            c1 = self.f32_conv1_fuse and torch.cuda.is_current_stream_capturing()
-            o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv, self.params, self.grads, self.m, self.v, st,
-                              SEGMENTS["conv_layer1/conv2d/kernel"][0], SEGMENTS["conv_layer1/conv2d/bias"][0],
-                              SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0],
-                              FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule,
-                              *((x, rows, self.a1, self.idx1, self._c1_sync) if c1 else ()))
-            self._c1_ready = c1
-        else:
-            o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
-            if overlap:
-                self._allreduce(self.grads[:FC_START], 0, FC_START)
-                main.wait_stream(self._side)
-            elif self.collectives:
-                self._allreduce(self.grads, 0, FLAT_NUMEL)
-            hi = W3_START if self.f32_fused_opt else FLAT_NUMEL
-            o.adam_step(self.params[:hi], self.grads[:hi], self.m[:hi], self.v[:hi], None, st, 0, self.lr, b1, b2,
-                        self.eps, 1.0 / self.world, self.rule, 1)
-        if w3_side:
-            main.wait_stream(self._side)
-        elif self.f32_fused_opt and not w3_bwd:
-            # dense/kernel's update is deferred into the next step's fc1_fwd / conv2_fwd launch (or
-            # applied by _flush_w3 when no step follows: end of an eager step or of a captured graph)
-            self._w3_pending = True
-
-    def _launch_step_f32_shard(self, x, rows, labels):
-        """fp32 step with the dense/kernel optimizer sharded over RCCL (size > 1):
-
-            main: conv1 conv2 | fc1_fwd head fc1_bwd | conv2_bwd reduce | Adam (small + my rows) |
-            side:  AG(W3 rows) ->|   (prev. step)      RS(dW3 rows)      AR(small)              AG(W3 rows) -> next
-
-        The row all-gather of the updated fp32 W3 overlaps the next step's convolutions (an event
-        joins it before fc1_fwd, W3's first reader); the reduce-scatter overlaps the conv backward.
-        Adam slots of other ranks' rows are not maintained (gather_full_state() collects them)."""
-        o = self.ops
-        st = self.state
-        P, G = self.pview, self.gview
         main = torch.cuda.current_stream(self.device)
-        side = self._side
-        b1, b2 = self.betas
-        w2 = P("conv_layer2/conv2d/kernel")
-        w3 = P("dense/kernel")
-        R, r = self._f32_R, self.rank
-        wf = None
-        if self.f32_conv12:
-            o.f32_conv12_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                             self.idx1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2)
-        else:
-            o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                            self.idx1, *((w2, self.w2frag) if self.w2frag is not None else ()))
-            wf = self.w2frag
-            o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2,
-                            w2frag=wf[0] if wf is not None else None)
-        if self._shadow_ev is not None:  # the previous step's W3 row gather
+        if self._small_ev is not None:  # the previous step's small-parameter update (side stream)
+            main.wait_event(self._small_ev)
+            self._small_ev = None
+        wf = self.w2frag
+        o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
+                        self.idx1, w2, wf)
+        o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0])
+        if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None
         o.f32_fc1_fwd(self.a2, w3, self.zpart)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+        gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
+                 G("conv_layer2/conv2d/bias"))
+        if not self.collectives:
+            # dgrad, dW3 and dense/kernel's Adam from one read of W3 (dW3 stays in registers unless
+            # keep_w3_grad); then the gradient reduction + Adam of every other parameter + the step
+            # bump in one launch
+            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3], self.v[s3], st, self.lr,
+                          b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad)
+            o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+            o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv, self.params, self.grads, self.m, self.v, st,
+                              SEGMENTS["conv_layer1/conv2d/kernel"][0], SEGMENTS["conv_layer1/conv2d/bias"][0],
+                              SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0],
+                              FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
+            return
+        if self.shard_w3:
+            return self._launch_step_f32_shard(x, rows, st, w2, wf, gconv)
+        # replicated optimizer (sizes that do not divide 3136, Adasum, MIHVD_SHARD_W3=0): the "fc"
+        # bucket (98.4 % of the bytes) is complete after fc1_bwd; its allreduce and Adam run on the side
+        # stream beside the conv backward, then the conv bucket's
+        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
+                      G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+        side = self._side
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._allreduce(self.grads[FC_START:], FC_START, FLAT_NUMEL)
+            fc = slice(FC_START, FLAT_NUMEL)
+            o.adam_step(self.params[fc], self.grads[fc], self.m[fc], self.v[fc], None, st, 0, self.lr, b1, b2, self.eps,
+                        1.0 / self.world, self.rule, 0)
+            self._shadow_ev = torch.cuda.Event()  # the next step's fc1_fwd (W3's first reader) joins it
+            self._shadow_ev.record(side)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
+        self._f32_small_tail(main, FC_START)
+
+    def _f32_small_tail(self, main, hi):
+        """After the gradient reduction: allreduce of gradients [0, hi), their Adam update and the
+        step bump. With the second communicator (or host collectives, which run in host program
+        order) on the main stream, right behind the reduction: no stream edge, and the next step's
+        conv1 simply follows. On the process group's one RCCL communicator (MIHVD_COMM=torch) on the
+        side stream instead, behind the row collectives (one communicator, one stream: every rank
+        issues the step's collectives in one order); the next step's conv1 waits for its event."""
+        b1, b2 = self.betas
+        on_main = self.ncomm_small is not None or self._host_collectives()
+        stream = main if on_main else self._side
+        if not on_main:
+            stream.wait_stream(main)
+        with torch.cuda.stream(stream):
+            self._allreduce(self.grads[:hi], 0, hi, comm=self.ncomm_small)
+            self.ops.adam_step(self.params[:hi], self.grads[:hi], self.m[:hi], self.v[:hi], None, self.state, 0, self.lr,
+                               b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+            if not on_main:
+                self._small_ev = torch.cuda.Event()
+                self._small_ev.record(stream)
+
+    def _launch_step_f32_shard(self, x, rows, st, w2, wf, gconv):
+        """Rest of the fp32 step with dense/kernel's optimizer sharded by rows (after the head):
+
+            main: fc1_bwd (dgrad, dW3) | conv2_bwd | conv_reduce |
+            side:                      RS(dW3 rows) Adam(my rows) | AR(small) Adam(small) | AG(W3 rows)
+                                                                  ^ next conv1 waits    ^ next fc1_fwd waits
+
+        The reduce-scatter and this rank's row update overlap the conv backward; the small
+        gradients' allreduce + update follow the reduction launch; the row all-gather of the updated
+        fp32 W3 overlaps the next step's convolutions. On the factor plane fc1_bwd runs its dgrad only
+        and the side stream exchanges the fc1 factors instead (_launch_step_f32_factor). Adam slots of
+        other ranks' rows are not maintained (gather_full_state() collects them)."""
+        o, G = self.ops, self.gview
+        main, side = torch.cuda.current_stream(self.device), self._side
+        b1, b2 = self.betas
+        R, r = self._f32_R, self.rank
         gW3 = G("dense/kernel")
         mine = slice(W3_START + r * R * 1024, W3_START + (r + 1) * R * 1024)
+        w3 = self.pview("dense/kernel")
         if self.f32_factor:
-            return self._launch_step_f32_factor(x, rows, st, w2, wf, gW3, R, mine)
+            side.wait_stream(main)  # the head wrote dz; conv2_fwd wrote a2
+            with torch.cuda.stream(side):
+                from ..parallel.factor import factor_exchange_
+
+                factor_exchange_(self.a2, self.dz, self.dz_all32, self.a2_send, self.a2_recv, self.rank, self.world,
+                                 self.ncomm)
+            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
+            side.wait_stream(main)  # fc1_bwd, the step's last reader of W3, is done
+            with torch.cuda.stream(side):
+                # this rank's dW3 rows over all N B samples, Adam from the accumulators
+                o.f32_factor_rows(self.a2_recv, self.dz_all32, self.gshard if self.keep_w3_grad else None,
+                                  self.params[mine], self.m[mine], self.v[mine], st, self.lr, b1, b2, self.eps,
+                                  1.0 / self.world, self.rule)
         else:
             o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
                           G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                self._reduce_scatter_rows(gW3, self.gshard, R)
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab,
-                        w2frag=wf[1] if wf is not None else None)
-        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
-                          G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self._allreduce(self.grads[:W3_START], 0, W3_START)
-        main.wait_stream(side)
-        o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START], None, st, 0,
-                    self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-        o.adam_step(self.params[mine], self.gshard.view(-1), self.m[mine], self.v[mine], None, st, 0, self.lr, b1, b2,
-                    self.eps, 1.0 / self.world, self.rule, 0)
-        side.wait_stream(main)
+                # in place: this rank's rows of the sum land in its own rows of dW3 (at world size 1
+                # a no-op instead of a 12.8 MB copy)
+                mine_g = gW3.view(3136, 1024)[r * R:(r + 1) * R]
+                self._reduce_scatter_rows(gW3, mine_g, R)
+                o.adam_step(self.params[mine], mine_g.reshape(-1), self.m[mine], self.v[mine], None, st, 0, self.lr,
+                            b1, b2, self.eps, 1.0 / self.world, self.rule, 0)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
+        self._f32_small_tail(main, W3_START)
         with torch.cuda.stream(side):
             p3 = self.params[W3_START:].view(3136, 1024)
             self._all_gather_rows(p3, p3[r * R:(r + 1) * R])
-            self._shadow_ev = torch.cuda.Event()
-            self._shadow_ev.record(side)
-        self._full_state_valid = False
-
-    def _launch_step_f32_factor(self, x, rows, st, w2, wf, gW3, R, mine):
-        """The rest of the fp32 step on the factor-gather plane (after the head):
-
-            main: fc1_bwd (dgrad only) | conv2_bwd reduce |        Adam (small)
-            side:  exchange (a2 A2A, dz AG) | dW3 rows + Adam |  AR(small) | AG(W3 rows) -> next step
-
-        Everything about dense/kernel runs on the side stream: the factor exchange from the head on,
-        this rank's dW3 rows over all N B samples with their Adam update from the accumulators
-        (csrc/kernels/f32_factor.hip, once fc1_bwd, the step's last reader of W3, is done), and the
-        row all-gather, which the next step's fc1_fwd joins. The side stream's collectives keep one
-        order on every rank (one communicator, one stream)."""
-        from ..parallel.factor import factor_exchange_
-
-        o, P, G = self.ops, self.pview, self.gview
-        main, side = torch.cuda.current_stream(self.device), self._side
-        b1, b2 = self.betas
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            factor_exchange_(self.a2, self.dz, self.dz_all32, self.a2_send, self.a2_recv, self.rank, self.world,
-                             self.ncomm)
-        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, P("dense/kernel"), self.dY2, self.db2p, gW3,
-                      G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            if self.f32_factor_kernel:
-                o.f32_factor_rows(self.a2_recv, self.dz_all32, self.gshard if self.keep_w3_grad else None,
-                                  self.params[mine], self.m[mine], self.v[mine], st, self.lr, b1, b2, self.eps,
-                                  1.0 / self.world, self.rule)
-            else:
-                N, B = self.world, self.B
-                torch.mm(self.a2_recv.view(N * B, R).t(), self.dz_all32.view(N * B, 1024), out=self.gshard)
-                o.adam_step(self.params[mine], self.gshard.view(-1), self.m[mine], self.v[mine], None, st, 0, self.lr,
-                            b1, b2, self.eps, 1.0 / self.world, self.rule, 0)
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab,
-                        w2frag=wf[1] if wf is not None else None)
-        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, G("conv_layer2/conv2d/kernel"),
-                          G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self._allreduce(self.grads[:W3_START], 0, W3_START)
-        main.wait_stream(side)
-        o.adam_step(self.params[:W3_START], self.grads[:W3_START], self.m[:W3_START], self.v[:W3_START], None, st, 0,
-                    self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
-        with torch.cuda.stream(side):
-            p3 = self.params[W3_START:].view(3136, 1024)
-            self._all_gather_rows(p3, p3[self.rank * R:(self.rank + 1) * R])
             self._shadow_ev = torch.cuda.Event()
             self._shadow_ev.record(side)
         self._full_state_valid = False
@@ -875,17 +657,9 @@ class FusedMNISTTrainer:
             dist.reduce_scatter_tensor(out, full.view(self.world * R, -1))
         else:  # gloo has no reduce-scatter: allreduce in place, keep this rank's rows
             dist.all_reduce(full)
-            out.copy_(full.view(self.world * R, -1)[self.rank * R:(self.rank + 1) * R])
-
-    def _flush_w3(self):
-        """Apply a deferred dense/kernel Adam update now (fp32 step; see _launch_step_f32)."""
-        if not getattr(self, "_w3_pending", False):
-            return
-        b1, b2 = self.betas
-        s3 = slice(W3_START, FLAT_NUMEL)
-        self.ops.adam_step(self.params[s3], self.grads[s3], self.m[s3], self.v[s3], None, self.state, 0, self.lr, b1,
-                           b2, self.eps, 1.0 / self.world, self.rule, 0)
-        self._w3_pending = False
+            rows = full.view(self.world * R, -1)[self.rank * R:(self.rank + 1) * R]
+            if out.data_ptr() != rows.data_ptr():
+                out.copy_(rows)
 
     def _launch_step_gather(self, x, rows, labels):
         """Step with the factor-gather data plane over the process group (RCCL; see ``__init__``).
@@ -922,11 +696,8 @@ class FusedMNISTTrainer:
         gW3 = self.gview("dense/kernel")
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
                  self.gview("dense_1/bias"))
-        if self.fc1_merged:  # db3, dW4, db4 of the local batch + the dgrad tiles, one launch
-            o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2)
-        else:
-            o.fc1_wgrad(*small, 2)  # db3, dW4, db4 of the local batch
-            o.fc1_dgrad(self.dz, self.w3_shadow(), self.a2, self.g2)
+        # db3, dW4, db4 of the local batch + the dgrad tiles, one launch
+        o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2)
         self._conv_backward(x, rows, st)
         main.wait_stream(side)   # both gathers done: the communicator is free
         side.wait_stream(main)
@@ -936,7 +707,7 @@ class FusedMNISTTrainer:
         ar_done.record(side)
         b1, b2 = self.betas
         lo, hi = self._w3_tiles
-        if self.fuse_w3 or (self.shard_w3 and self.fuse_slice and hi > lo):
+        if self.shard_w3 and hi > lo:
             # dW3 summed over every rank's samples, Adam applied to W3 in the same tiles
             self._fc1_wgrad_w3_adam(1, self.dz_all, self.a2_all, lo, hi)
         elif hi > lo:
@@ -1040,17 +811,10 @@ class FusedMNISTTrainer:
                                 self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule, self.keep_w3_grad, lo, hi)
 
     def _conv_forward(self, x, rows, st):
-        o = self.ops
-        w2 = self.pview("conv_layer2/conv2d/kernel", self.shadow)
-        b2 = self.pview("conv_layer2/conv2d/bias")
-        if self.conv12:
-            # one launch: conv1 on MFMA into conv2's LDS input image (a1/idx1 still stored for the backward)
-            o.conv12_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel", self.shadow),
-                         self.pview("conv_layer1/conv2d/bias"), w2, b2, self.a1, self.idx1, self.a2, self.idx2)
-            return
-        o.conv1_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel"), self.pview("conv_layer1/conv2d/bias"),
-                    self.a1, self.idx1)
-        o.conv2_fwd(self.a1, w2, b2, self.a2, self.idx2)
+        # one launch: conv1 on MFMA into conv2's LDS input image (a1/idx1 still stored for the backward)
+        self.ops.conv12_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel", self.shadow),
+                            self.pview("conv_layer1/conv2d/bias"), self.pview("conv_layer2/conv2d/kernel", self.shadow),
+                            self.pview("conv_layer2/conv2d/bias"), self.a1, self.idx1, self.a2, self.idx2)
 
     def _conv_backward(self, x, rows, st, coll=-1):
         o = self.ops
@@ -1071,13 +835,11 @@ class FusedMNISTTrainer:
             dist.all_gather(list(full.chunk(self.world)), mine.clone())
 
     def _join(self):
-        """Make the current stream wait for any side-stream work of the last step, and apply a
-        deferred optimizer update (the step's results are then complete)."""
-        self._flush_w3()
-        self._c1_ready = False  # a step launched after this one recomputes its conv1 (idempotent)
-        if self._fc_update_pending:
-            torch.cuda.current_stream(self.device).wait_stream(self._side)
-            self._fc_update_pending = False
+        """Make the current stream wait for any side-stream work of the last step (the step's
+        results are then complete)."""
+        if self._small_ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._small_ev)
+            self._small_ev = None
         if self._shadow_ev is not None:
             torch.cuda.current_stream(self.device).wait_event(self._shadow_ev)
             self._shadow_ev = None
@@ -1109,7 +871,7 @@ class FusedMNISTTrainer:
         self._refresh_shadow()
         self._full_state_valid = True
 
-    def _allreduce(self, bucket, lo, hi):
+    def _allreduce(self, bucket, lo, hi, comm=None):
         import torch.distributed as dist
 
         from ..basics import ReduceOp
@@ -1121,22 +883,8 @@ class FusedMNISTTrainer:
             adasum_dispatch_(bucket, segs)
             bucket.mul_(self.world)  # adam divides by size; Adasum output is already the combined gradient
             return
-        if self.xgmi is not None:
-            ctx = self.xgmi.get((lo, hi), False)
-            if ctx is False:
-                from ..parallel import xgmi as _xg
-
-                idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-                try:
-                    ctx = _xg.XGMIAllreduce(hi - lo, device=torch.device("cuda", idx))
-                except _xg.XGMIUnavailable as e:
-                    _xg.warn_fallback(str(e))
-                    ctx = None
-                self.xgmi[(lo, hi)] = ctx
-            if ctx is not None:
-                ctx.allreduce_(bucket)  # sum; Adam applies the 1/size of Average
-                return
-        reduce_ = self.ncomm.all_reduce_ if self.ncomm is not None else dist.all_reduce
+        comm = comm if comm is not None else self.ncomm
+        reduce_ = comm.all_reduce_ if comm is not None else dist.all_reduce
         if self.wire is not None:
             w = self.wire[lo:hi]
             self.ops.scale_cast_bf16(bucket, w, 1.0)
@@ -1210,7 +958,7 @@ class FusedMNISTTrainer:
             warnings.warn(f"HIP graph capture failed ({e!r}); falling back to eager steps")
             if primary:
                 self.graph = None
-            self._fc_update_pending = False
+            self._small_ev = self._shadow_ev = None
             torch.cuda.synchronize(self.device)
             return False
         torch.cuda.current_stream(self.device).wait_stream(s)
@@ -1292,17 +1040,8 @@ class FusedMNISTTrainer:
         if not self.f32 and self.fused_opt and int(self.ops.conv_barrier_error(True)) != 0:
             raise RuntimeError("fused step: a conv2_bwd LDS barrier timed out (a broken wave count); the conv "
                                "gradients and optimizer state of that step are invalid")
-        if self._c1_sync is not None and int(self._c1_sync[2]) != 0:
-            raise RuntimeError("fused fp32 step: the next step's conv1 in f32_conv_reduce timed out waiting for the "
-                               "W1/b1 update; a1 of that step is invalid")
-        if getattr(self, "fold_reduce", False) and int(self.fold_sync[2]) != 0:
-            raise RuntimeError("fused step: the folded gradient reduction timed out waiting for the conv blocks "
-                               "(a conv block was not resident); parameters of that step are invalid")
         if self.xplane is not None and not getattr(self, "_xplane_failed", False):
             self.xplane.check()
-        for ctx in (self.xgmi or {}).values():
-            if ctx is not None:
-                ctx.check()
 
     def _validate_xgmi(self, rounds: int = 2) -> bool:
         """Run the plane's prepared xGMI collectives (the descriptors the step co-launches, here
@@ -1387,7 +1126,7 @@ class FusedMNISTTrainer:
         if self.f32:
             shard = bool(shard) and self._f32_can_shard
         else:
-            shard = bool(shard) and self.gather and not self.fuse_w3_requested()
+            shard = bool(shard) and self.gather
         if shard == self.shard_w3:
             return
         self._join()
@@ -1423,7 +1162,7 @@ class FusedMNISTTrainer:
             env = os.environ.get("MIHVD_SHARD_W3")
             # (one rank owns every tile either way: replicated, which has no row gather)
             shard_options = [env != "0"] if env is not None else ([True, False] if self.world > 1 else [False])
-        shard_options = [bool(x) and not self.fuse_w3_requested() for x in shard_options]
+        shard_options = [bool(x) for x in shard_options]
         planes = ["rccl"]
         if self.xplane is not None and self._xgmi_mode != "off":
             self.xplane.watch(False)  # a timeout while the plane is on trial means "use RCCL"
@@ -1439,16 +1178,15 @@ class FusedMNISTTrainer:
         if self.f32 and self._f32_can_shard and True in shard_options:
             # the fp32 factor-gather plane (sharded): MIHVD_F32_PLANE=auto (default) times it beside
             # the reduce-scatter plane, "factor" uses it alone, "rs" leaves it out
-            fmode = os.environ.get("MIHVD_F32_PLANE", "auto").strip().lower()
+            fmode = f32_plane_mode()
             if fmode == "factor":
                 cands = [("factor", True)]
             elif fmode != "rs":
                 cands.append(("factor", True))
         host = self._host_collectives()
         # host (gloo) collectives cannot be captured or timed meaningfully: the candidates still run
-        # (eagerly) for the consistency check below unless MIHVD_XGMI_CHECK=0, and the first
-        # consistent candidate is kept
-        if len(cands) == 1 or (host and os.environ.get("MIHVD_XGMI_CHECK", "1") == "0"):
+        # (eagerly) for the consistency check below, and the first consistent candidate is kept
+        if len(cands) == 1:
             self._set_plane(cands[0][0] == "xgmi", cands[0][1], cands[0][0] == "factor")
             rep["plane"], rep["shard"] = cands[0]
             self._watch_plane()
@@ -1499,7 +1237,7 @@ class FusedMNISTTrainer:
         if fcons is not None:
             from ..parallel.xgmi import _group_ok
 
-            ok = _group_ok(fcons <= float(os.environ.get("MIHVD_XGMI_CHECK_TOL", "1e-3")), None, self.device)
+            ok = _group_ok(fcons <= _check_tol(), None, self.device)
             rep["factor_consistency"] = round(fcons, 9)
             if not ok:
                 import warnings
@@ -1509,7 +1247,7 @@ class FusedMNISTTrainer:
         if cons:
             from ..parallel.xgmi import _group_ok, warn_fallback
 
-            tol = float(os.environ.get("MIHVD_XGMI_CHECK_TOL", "1e-3"))
+            tol = _check_tol()
             ok = _group_ok(all(v <= tol for v in cons.values()), None, self.device)
             rep["consistency"] = {key: round(v, 9) for key, v in cons.items()}
             rep["consistent"] = ok
@@ -1576,17 +1314,19 @@ class FusedMNISTTrainer:
     def reduced_grads(self) -> torch.Tensor:
         """The flat gradient buffer after the step's reduction (sums over ranks; the xGMI plane
         reduces the small gradients into a separate buffer instead of in place). On the
-        factor-gather plane (both the xGMI and the RCCL form: MIHVD_FUSE_W3_SLICE=1, the default,
-        computes dW3 + Adam in one tile epilogue) the dense/kernel segment is written only with
+        factor-gather plane (both the xGMI and the RCCL form compute dW3 + Adam in one tile
+        epilogue) the dense/kernel segment is written only with
         keep_w3_grad=True, and then only for the rows whose optimizer this rank owns; otherwise it
         holds stale values."""
         if self.use_xgmi and self.gather:
             return torch.cat([self.gred, self.grads[W3_START:]])
         if self.f32 and self.shard_w3:
-            # both fp32 sharded planes leave this rank's reduced dense/kernel rows in gshard
+            # the reduce-scatter plane leaves this rank's reduced dense/kernel rows in place in the
+            # gradient buffer, the factor plane in gshard (keep_w3_grad)
             g = self.grads.clone()
-            R = self._f32_R
-            g[W3_START + self.rank * R * 1024:W3_START + (self.rank + 1) * R * 1024] = self.gshard.view(-1)
+            if self.f32_factor:
+                R = self._f32_R
+                g[W3_START + self.rank * R * 1024:W3_START + (self.rank + 1) * R * 1024] = self.gshard.view(-1)
             return g
         return self.grads
 
@@ -1597,7 +1337,7 @@ class FusedMNISTTrainer:
             return "xgmi" if self.use_xgmi else "rccl"
         if self.f32 and self.f32_factor:
             return "factor"
-        return "xgmi" if self.xgmi and any(c is not None for c in self.xgmi.values()) else "rccl"
+        return "rccl"
 
     def close(self):
         """Release the direct-xGMI regions (collective when they exist: peers may still read this
@@ -1606,11 +1346,11 @@ class FusedMNISTTrainer:
         if self._closed:
             return
         self._closed = True
-        if self.ncomm is not None:
-            self.ncomm.close()
-            self.ncomm = None
-        ctxs = [c for c in (self.xgmi or {}).values() if c is not None]
-        if self.xplane is None and not ctxs:
+        for c in (self.ncomm, self.ncomm_small):
+            if c is not None:
+                c.close()
+        self.ncomm = self.ncomm_small = None
+        if self.xplane is None:
             return
         import torch.distributed as dist
 
@@ -1619,9 +1359,6 @@ class FusedMNISTTrainer:
         self._graphs = {}
         if dist.is_initialized():
             dist.barrier()
-        for c in ctxs:
-            c.close()
-        self.xgmi = {}
         if self.xplane is not None:
             for name in ("a2_all", "dz_all", "a2", "dz", "grads", "shadow3"):
                 if hasattr(self, name):

@@ -148,7 +148,9 @@ def _group_size(group) -> int:
 # allreduce
 # ------------------------------------------------------------------------------------------ #
 def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postscale_factor, group,
-                    segments=None, async_op=True, wire_buf=None):
+                    segments=None, async_op=True, wire_buf=None, plane=None):
+    """``plane``: a :class:`BucketPlane` to run the collective on (DistributedOptimizer's buckets),
+    instead of the engine / process group; it also runs at size 1 (forced collectives)."""
     ctx = basics._require()
     op = ReduceOp(op)
     n = _group_size(group)
@@ -173,7 +175,9 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
         # at size 1 the wire round trip still runs (Horovod compresses at any size)
         wire = hip_pack(compression, tensor, prescale_factor, out=wire_buf)
         scale = postscale_factor / n if op == ReduceOp.Average else postscale_factor
-        if n == 1 and not getattr(ctx.engine, "world_one", False):
+        if plane is not None:
+            work = plane.allreduce(wire, op)
+        elif n == 1 and not getattr(ctx.engine, "world_one", False):
             work = None
         else:
             work = _engine_allreduce(ctx, f"allreduce.{name}", wire, _torch_op(op), group, ("hip-pack",))
@@ -185,7 +189,9 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
         wire = out
     if prescale_factor != 1.0:
         wire.mul_(prescale_factor)
-    if n == 1 and not getattr(ctx.engine, "world_one", False):
+    if plane is not None:
+        work = plane.allreduce(wire, op)
+    elif n == 1 and not getattr(ctx.engine, "world_one", False):
         work = None
     else:
         work = _engine_allreduce(ctx, f"allreduce.{name}", wire, _torch_op(op), group, ())
@@ -200,6 +206,102 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
         return out
 
     return _register(work, out, post, f"allreduce.{name}")
+
+
+class _PlaneWork:
+    """Completion of a bucket collective on the plane's stream: ``wait()`` orders the caller's
+    current stream behind it (no host block, like a process-group work object on RCCL), so it is
+    also valid inside a HIP graph capture (the event becomes a graph dependency)."""
+
+    __slots__ = ("ev", "device")
+
+    def __init__(self, ev, device):
+        self.ev = ev
+        self.device = device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.ev)
+
+    def is_completed(self) -> bool:
+        return self.ev.query()
+
+
+class BucketPlane:
+    """DistributedOptimizer's gradient-bucket data plane on a framework-owned RCCL communicator
+    ("called directly ... not through torch.distributed's ProcessGroup"; the
+    reference's per-step allreduce is horovod/tensorflow_mnist.py:133). Each bucket's allreduce is
+    enqueued on one dedicated high-priority HIP stream, ordered after the producing backward kernels
+    by an event; the optimizer's ``synchronize()`` makes its stream wait for the bucket's completion
+    event. The optimizer releases buckets strictly in order, so every rank issues the same
+    collectives in the same order on the one stream -- no negotiation needed (the negotiated C++
+    engine, MIHVD_ENGINE=native, is the path for named collectives that ranks may issue in
+    different orders). Collective to construct: every rank of the world."""
+
+    _OPS = {ReduceOp.Sum: "sum", ReduceOp.Average: "sum", ReduceOp.Min: "min", ReduceOp.Max: "max",
+            ReduceOp.Product: "prod"}
+
+    def __init__(self, device: torch.device):
+        from .rccl import NativeComm
+
+        self.device = device
+        self.comm = NativeComm(device=device)
+        self.stream = torch.cuda.Stream(device=device, priority=-1)
+        self.launched = 0
+
+    def allreduce(self, wire: torch.Tensor, op: ReduceOp) -> _PlaneWork:
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)  # the bucket's gradients are complete on the producing stream
+        with torch.cuda.stream(self.stream):
+            self.comm.all_reduce_(wire, self._OPS[op])
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.launched += 1
+        return _PlaneWork(ev, self.device)
+
+    def close(self):
+        self.comm.close()
+
+
+def plane_wanted(world: int | None = None) -> bool:
+    """Whether DistributedOptimizer's buckets go through :class:`BucketPlane`: RCCL backend, a GPU,
+    ``MIHVD_COMM`` not ``torch``, and collectives (size > 1, or ``MIHVD_FORCE_COLLECTIVES=1``)."""
+    import os
+
+    from .rccl import env_mode
+
+    ctx = basics._require()
+    world = basics.size() if world is None else world
+    forced = os.environ.get("MIHVD_FORCE_COLLECTIVES") == "1"
+    return (ctx.backend == "nccl" and ctx.device is not None and ctx.device.type == "cuda" and env_mode() == "native"
+            and (world > 1 or forced))
+
+
+def bucket_plane():
+    """The world's :class:`BucketPlane`, created on first use (collective: call on every rank, e.g.
+    from every rank's DistributedOptimizer constructor), or None where :func:`plane_wanted` is
+    false or the communicator cannot be created (then every rank falls back to the process group)."""
+    ctx = basics._require()
+    if ctx.plane is not None:
+        return ctx.plane
+    if not plane_wanted():
+        return None
+    plane, err = None, None
+    try:
+        plane = BucketPlane(ctx.device)
+    except Exception as e:  # pragma: no cover - depends on the RCCL build
+        err = e
+    # every rank must use the same communicator: any failure moves all to the process group
+    flag = torch.tensor([0 if plane is not None else 1], device=ctx.device)
+    dist.all_reduce(flag)
+    if int(flag.item()) != 0:
+        if plane is not None:
+            plane.close()
+        import warnings
+
+        warnings.warn(f"mihvd: native RCCL bucket plane unavailable ({err!r}); using the process group")
+        return None
+    ctx.plane = plane
+    return plane
 
 
 def _capturing() -> bool:

@@ -21,8 +21,8 @@ import torch.distributed as dist
 
 def factor_exchange_(a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor, a2_send: torch.Tensor,
                      a2_recv: torch.Tensor, rank: int, world: int, comm=None):
-    """The factor exchange alone: dz_all <- every rank's dz (all-gather; ``dz`` is block ``rank`` of
-    ``dz_all``), a2_recv[j] <- rank j's a2 columns of this rank's rows (all-to-all of [world][B][R]).
+    """The factor exchange alone: dz_all <- every rank's dz (all-gather of ``dz``, which must not
+    alias ``dz_all``: a reader of ``dz`` may run beside the exchange), a2_recv[j] <- rank j's a2 columns of this rank's rows (all-to-all of [world][B][R]).
     ``comm``: a :class:`mihvd.parallel.rccl.NativeComm` (the collectives then run on the current HIP
     stream), else the default process group (nccl, or host collectives such as gloo). Collective."""
     N = world
@@ -34,6 +34,7 @@ def factor_exchange_(a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor, a
         comm.all_gather_into(dz_all, dz)
     elif N == 1:
         a2_recv.copy_(a2_send)
+        dz_all[0].copy_(dz)
     elif dist.get_backend() == "nccl":
         dist.all_to_all_single(a2_recv, a2_send)
         dist.all_gather_into_tensor(dz_all, dz)
@@ -48,8 +49,9 @@ def factor_exchange_(a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor, a
 def factor_rows_(out: torch.Tensor, a2: torch.Tensor, dz: torch.Tensor, dz_all: torch.Tensor,
                  a2_send: torch.Tensor, a2_recv: torch.Tensor, rank: int, world: int, comm=None) -> torch.Tensor:
     """out[R][1024] = rows [rank R, (rank + 1) R) of sum over ranks of a2_q^T dz_q: the exchange, then
-    one GEMM (the trainer's default; ``MIHVD_F32_FACTOR_KERNEL=1`` runs ``csrc/kernels/f32_factor.hip``
-    instead, which applies Adam to the rows from the accumulators). Collective: every rank calls it."""
+    one torch GEMM. The host-side reference of the exchange (tests); the trainer forms its rows with
+    the hand-written ``csrc/kernels/f32_factor.hip``, which also applies Adam to them from the
+    accumulators. Collective: every rank calls it."""
     factor_exchange_(a2, dz, dz_all, a2_send, a2_recv, rank, world, comm)
     N, B = world, a2.shape[0]
     R = a2.shape[1] // N

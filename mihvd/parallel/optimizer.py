@@ -10,9 +10,11 @@ Design (SURVEY.md §2.3 N1-N3, §5.8 "Overlap"):
   aligned fusion buffers, in reverse registration order (≈ the order backward produces them), and
   each ``param.grad`` becomes a *view* into its bucket — zero-copy fusion, no pack/unpack pass.
 * A post-accumulate-grad hook per parameter feeds the native ``Controller``; whenever a bucket is
-  complete *and* every earlier bucket has been launched, its allreduce is issued asynchronously
-  (RCCL runs it on its own stream, overlapping the rest of backward). Strict in-order release is
-  what gives all ranks the same collective order without Horovod's per-cycle negotiation.
+  complete *and* every earlier bucket has been launched, its allreduce is issued asynchronously on
+  the framework-owned RCCL communicator's high-priority stream (``collectives.BucketPlane``; the
+  process group only on gloo or with ``MIHVD_COMM=torch``), overlapping the rest of backward.
+  Strict in-order release is what gives all ranks the same collective order without Horovod's
+  per-cycle negotiation.
 * ``step()`` flushes buckets whose gradients never arrived (unused parameters), waits for all of
   them, then runs the wrapped optimizer.
 """
@@ -92,6 +94,9 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 raise ValueError("named_parameters was specified, but one or more model parameters "
                                  "were not named")
         self._params = params
+        # the framework-owned RCCL bucket plane (collective: every rank constructs its optimizer);
+        # None on gloo / at size 1 / with MIHVD_COMM=torch: the engine or the process group then
+        self._plane = C.bucket_plane() if any(p.is_cuda for p in params) else None
         self._names = [names.get(id(p), f"param.{i}") for i, p in enumerate(params)]
         self._index = {id(p): i for i, p in enumerate(params)}
         cfg = basics.config()
@@ -212,7 +217,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                                          post, None, segments=b.segments)
         else:
             b.handle = C._allreduce_impl(b.flat, b.flat, f"bucket{bid}", self._op, self._compression, pre, post, None,
-                                         wire_buf=b.wire)
+                                         wire_buf=b.wire, plane=self._plane if b.flat.is_cuda else None)
 
     def synchronize(self):
         """Launch any bucket not yet launched, then wait for every bucket's allreduce."""

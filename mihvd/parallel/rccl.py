@@ -95,6 +95,14 @@ class NativeComm:
         self._o.rccl_broadcast_(self.handle, t, root)
         return t
 
+    def nranks(self) -> int:
+        """The communicator's size as RCCL reports it (ncclCommCount)."""
+        return int(self._o.rccl_comm_count(self.handle))
+
+    def user_rank(self) -> int:
+        """This rank as RCCL reports it (ncclCommUserRank)."""
+        return int(self._o.rccl_comm_user_rank(self.handle))
+
     def async_error(self) -> int:
         return int(self._o.rccl_async_error(self.handle))
 

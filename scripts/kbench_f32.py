@@ -227,16 +227,8 @@ def main():
     if want("whole step (graph, 20 steps/replay)"):
         res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
         tr._join()
-    mode = tr.f32_w3
-    for alt in ("bwd", "fc1", "tail", "side"):
-        if alt != mode and want(f"whole step [dense/kernel Adam: {alt}]"):
-            tr.f32_w3 = alt
-            res[f"whole step [dense/kernel Adam: {alt}]"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
-            tr._join()
-    tr.f32_w3 = mode
     # whole-step studies: trainer attributes and launch knobs (read at capture time)
     steps = {
-        "whole step [conv1 fused into conv2_fwd (conv12)]": ({"f32_conv12": True}, {}),
         "whole step [conv2_fwd blocks may share a CU]": ({}, {"MIHVD_F32_C2F_LDS": "70400"}),
         "whole step [conv2_fwd W2 before the staging barrier]": ({}, {"MIHVD_F32_C2F_PREW": "1"}),
         "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
@@ -244,7 +236,6 @@ def main():
         "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
         "whole step [fc1_bwd pinned dgrad MFMA order]": ({}, {"MIHVD_F32_F1R_PIN": "1"}),
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
-        "whole step [W2 read as HWIO (no fragment copies)]": ({"w2frag": None}, {}),
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
         "whole step [conv2_fwd 4 waves]": ({}, {"MIHVD_F32_C2F_W8": "0"}),
         "whole step [conv2_fwd A one step ahead]": ({}, {"MIHVD_F32_C2F_DEPTH": "1"}),

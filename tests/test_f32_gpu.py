@@ -79,43 +79,6 @@ def test_f32_conv2_fwd(ops, B, form, monkeypatch):
     assert (idx.long()[pos] == rd.reshape(B, 3136)[pos]).float().mean() > 0.999
 
 
-@pytest.mark.parametrize("B", [1, 7, 100, 128])
-def test_f32_conv12_fwd_matches_separate_launches(ops, B, monkeypatch):
-    """conv1 fused into the conv2 forward launch (each block computes the a1 rows it reads, halo
-    included, and writes its own rows): a1, idx1, a2 and idx2 bit for bit equal to the two separate
-    launches, with the resident dataset's row permutation and the device step counter."""
-    g = torch.Generator(device="cuda").manual_seed(21)
-    n_pool = 3 * B + 5
-    x = torch.rand(n_pool, 784, device="cuda", generator=g)
-    rows = torch.randperm(n_pool, generator=torch.Generator().manual_seed(3)).to(torch.int32).cuda()
-    st = torch.tensor([2, 0, 0, 0], device="cuda", dtype=torch.int64)
-    w1 = torch.randn(800, device="cuda", generator=g) * 0.2
-    b1 = torch.randn(32, device="cuda", generator=g) * 0.1
-    w2 = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
-    b2 = torch.randn(64, device="cuda", generator=g) * 0.1
-    monkeypatch.setenv("MIHVD_F32_C2F_W8", "0")  # the fused launch is the 4-wave conv2 form
-    outs = []
-    for fused in (True, False):
-        a1 = torch.full((B, 14, 14, 32), float("nan"), device="cuda")
-        idx1 = torch.full((B, 14, 14, 32), 77, device="cuda", dtype=torch.uint8)
-        a2 = torch.empty(B, 3136, device="cuda")
-        idx2 = torch.empty(B, 3136, device="cuda", dtype=torch.uint8)
-        if fused:
-            ops.f32_conv12_fwd(x, rows, st, w1, b1, a1, idx1, w2, b2, a2, idx2)
-        else:
-            ops.f32_conv1_fwd(x, rows, st, w1, b1, a1, idx1)
-            ops.f32_conv2_fwd(a1, w2, b2, a2, idx2)
-        outs.append((a1, idx1, a2, idx2))
-    torch.cuda.synchronize()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-    # and the conv2 output against torch on the batch the permutation selects
-    sel = rows.long()[(2 * B + torch.arange(B, device="cuda")) % n_pool]
-    ref1, _ = ref_conv_pool(x[sel].view(B, 28, 28, 1), w1.view(5, 5, 1, 32), b1)
-    ref2, _ = ref_conv_pool(ref1, w2, b2)
-    assert rel_err(outs[0][2], ref2.reshape(B, 3136)) < 1e-5
-
-
 @pytest.mark.parametrize("B", [7, 100, 128])
 def test_f32_fc1_fwd_and_head(ops, B, monkeypatch):
     g = torch.Generator(device="cuda").manual_seed(3)
@@ -346,32 +309,6 @@ def test_f32_w2_fragment_copies(ops, B):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-def test_f32_trainer_w2_fragments_bitwise(ops, monkeypatch):
-    """Graph-replayed training steps with the W2 fragment copies (MIHVD_F32_W2F=1) equal the HWIO
-    reads bit for bit (W2 changes every step: the copies are rewritten by every conv1 launch)."""
-    from mihvd.models.fused_mnist import FusedMNISTTrainer
-    from mihvd.utils.data import synthetic_mnist
-
-    (x, y), _ = synthetic_mnist(n_train=2000, n_test=10, seed=8)
-    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
-    Y = torch.from_numpy(y.astype("int64")).cuda()
-    trs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("MIHVD_F32_W2F", flag)
-        tr = FusedMNISTTrainer(batch_size=100, lr=2e-3, seed=3, device="cuda", precision="fp32")
-        assert (tr.w2frag is not None) == (flag == "1")
-        tr.set_device_dataset(X, Y, seed=1)
-        tr.device_step()
-        tr.build_graph(steps_per_replay=5)
-        for _ in range(3):
-            tr.run_graph()
-        trs.append(tr)
-    torch.cuda.synchronize()
-    a, b = trs
-    for name in ("params", "m", "v", "state"):
-        assert torch.equal(getattr(a, name), getattr(b, name)), name
-
-
 @pytest.mark.parametrize("NB,R", [(800, 392), (100, 3136), (200, 784), (7, 448), (350, 392)])
 def test_f32_factor_rows_kernel(ops, NB, R):
     """The fp32 factor plane's dW3 rows (csrc/kernels/f32_factor.hip): a2c^T dz over all NB samples
@@ -506,74 +443,6 @@ def test_f32_graph_replay_converges(ops):
     assert int(tr.state[0].item()) == tr.global_step and int(tr.state[1].item()) == tr.global_step
     assert tr.last_loss() < first * 0.5, (first, tr.last_loss())
     assert tr.last_accuracy() > 0.8
-
-
-@pytest.mark.parametrize("w3_mode", ["bwd", "fc1", "side", "tail"])
-def test_f32_fused_optimizer_matches_separate_adam(ops, monkeypatch, w3_mode):
-    """MIHVD_FUSED_OPT=1 (small-parameter Adam inside the reduction launch; dense/kernel's update
-    inside f32_fc1_bwd from the dW3 accumulators ("bwd"), or deferred into the next step's fc1_fwd or
-    conv2_fwd tail blocks and flushed at the end of each graph / eager step, or on the side stream
-    beside the conv backward) is bitwise equal to a separate adam_step after every step,
-    graph-replayed and eager."""
-    from mihvd.models.fused_mnist import FusedMNISTTrainer
-    from mihvd.utils.data import synthetic_mnist
-
-    (x, y), _ = synthetic_mnist(n_train=2000, n_test=10, seed=6)
-    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
-    Y = torch.from_numpy(y.astype("int64")).cuda()
-    monkeypatch.setenv("MIHVD_F32_W3", w3_mode)
-    trs = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("MIHVD_FUSED_OPT", fused)
-        tr = FusedMNISTTrainer(batch_size=100, lr=2e-3, seed=4, device="cuda", precision="fp32")
-        assert tr.f32_fused_opt == (fused == "1")
-        tr.set_device_dataset(X, Y, seed=2)
-        tr.build_graph(steps_per_replay=5)
-        for _ in range(3):
-            tr.run_graph()
-        tr.device_step()
-        tr.run_graph()
-        trs.append(tr)
-    torch.cuda.synchronize()
-    a, b = trs
-    assert a.global_step == b.global_step == 2 + 21
-    for name in ("params", "m", "v", "state"):
-        assert torch.equal(getattr(a, name), getattr(b, name)), name
-
-
-def test_f32_next_conv1_in_reduce_launch_is_bitwise(ops, monkeypatch):
-    """Graph-replayed steps with the next step's conv1 inside f32_conv_reduce (MIHVD_F32_CONV1_FUSE=1:
-    conv1 blocks acquire the W1/b1 update and the step bump of the same launch) train bit for bit like
-    separate conv1 launches, across replays, an eager step in between and a shorter graph; the
-    launch's sync words are back to zero after every replay and never timed out."""
-    from mihvd.models.fused_mnist import FusedMNISTTrainer
-    from mihvd.utils.data import synthetic_mnist
-
-    (x, y), _ = synthetic_mnist(n_train=2000, n_test=10, seed=8)
-    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
-    Y = torch.from_numpy(y.astype("int64")).cuda()
-    trs = []
-    for fuse in ("1", "0"):
-        monkeypatch.setenv("MIHVD_F32_CONV1_FUSE", fuse)  # 1: the measured alternative
-        tr = FusedMNISTTrainer(batch_size=100, lr=2e-3, seed=3, device="cuda", precision="fp32")
-        assert tr.f32_conv1_fuse == (fuse == "1")
-        tr.set_device_dataset(X, Y, seed=1)
-        tr.build_graph(steps_per_replay=8)
-        tr.build_graph(steps_per_replay=3, warmup=0, primary=False)
-        for _ in range(3):
-            tr.run_graph()
-        tr.device_step()
-        tr.run_graph(3)
-        tr.run_graph()
-        tr.device_step()  # eager: both compute this step's conv1 on their own (a1 comparable)
-        trs.append(tr)
-    torch.cuda.synchronize()
-    a, b = trs
-    assert a.global_step == b.global_step
-    for name in ("params", "m", "v", "state", "a1"):
-        assert torch.equal(getattr(a, name), getattr(b, name)), name
-    assert a._c1_sync.tolist() == [0, 0, 0, 0], a._c1_sync.tolist()
-    a.check_xgmi()
 
 
 def _f32_head_mask(ops, B, step, seed, rate=0.5):

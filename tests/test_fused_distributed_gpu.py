@@ -63,10 +63,11 @@ def test_collectives_inside_hip_graph(tmp_path, prec, shard, xgmi, comm):
 
 def test_f32_factor_plane_inside_hip_graph(tmp_path):
     """The fp32 factor-gather plane (MIHVD_F32_PLANE=factor) at world 1 with the collectives forced
-    on, on the native communicator: dz all-gather, a2-column all-to-all and the dW3-row GEMM on the
-    side stream, fc1_bwd's dgrad-only launch, sharded Adam and the row all-gather, captured in 2 x
-    5-step graphs and replayed. dW3 is summed by a GEMM in another order than the fused step's
-    MFMA chain, so the match with the trainer without collectives is to fp32 rounding, not bitwise."""
+    on, on the native communicator: dz all-gather, a2-column all-to-all and the hand-written dW3-row
+    kernel with Adam from its accumulators (csrc/kernels/f32_factor.hip) on the side stream,
+    fc1_bwd's dgrad-only launch and the row all-gather, captured in 2 x 5-step graphs and replayed.
+    dW3 is summed in another order than the fused step's MFMA chain, so the match with the trainer
+    without collectives is to fp32 rounding, not bitwise."""
     _gpu()
     env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3="1",
                MIHVD_XGMI="off", MIHVD_TEST_PRECISION="fp32", MIHVD_COMM="native", MIHVD_F32_PLANE="factor")
@@ -82,11 +83,10 @@ def test_f32_factor_plane_inside_hip_graph(tmp_path):
     assert abs(r["loss"] - r["loss_ref"]) < 1e-4 * max(1.0, abs(r["loss_ref"])), r
 
 
-@pytest.mark.parametrize("gather", ["1", "0"])
-def test_fused_data_parallel_equivalence_two_ranks(tmp_path, gather):
-    """gather=1: dW3 from all-gathered factors (the default data plane); gather=0: bucket allreduce."""
+def test_fused_data_parallel_equivalence_two_ranks(tmp_path):
+    """bf16 step, dW3 from all-gathered factors (its data plane) over two ranks."""
     _gpu()
-    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather)
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -97,16 +97,14 @@ def test_fused_data_parallel_equivalence_two_ranks(tmp_path, gather):
         assert o["rel_update_diff"] < 0.05, o
 
 
-@pytest.mark.parametrize("gather", ["1", "0"])
-def test_fused_data_parallel_xgmi_two_ranks(tmp_path, gather):
-    """gather=1: the factor-gather plane over the direct xGMI collectives (a2/dz gathers and the
-    small-gradient reduction read the peer's region in place); gather=0: the gradient buckets over
-    the staged xGMI allreduce (MIHVD_XGMI_ALLREDUCE=1). gloo only carries the IPC handle exchange."""
+def test_fused_data_parallel_xgmi_two_ranks(tmp_path):
+    """The factor-gather plane over the direct xGMI collectives (a2/dz gathers and the
+    small-gradient reduction read the peer's region in place). gloo only carries the IPC handle
+    exchange."""
     _gpu()
     # both ranks share this one GPU: a rank's spinning phase barrier can wait for the other process's
     # kernels to be scheduled, so the device-side timeout is raised from 20 s (a timeout still fails)
-    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_XGMI_ALLREDUCE="1",
-               MIHVD_XGMI="on", MIHVD_XGMI_TIMEOUT_MS="60000")
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="on", MIHVD_XGMI_TIMEOUT_MS="60000")
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -189,12 +187,12 @@ def test_bench_flow_trains_at_8_ranks(tmp_path, n, prec):
         assert o["losses"][-1] < 1.0, o
 
 
-@pytest.mark.parametrize("n,prec,gather,shard,xgmi,f32plane", [
-    (4, "fp32", "0", "0", "off", "rs"), (8, "fp32", "0", "0", "off", "rs"), (4, "fp32", "0", "1", "off", "rs"),
-    (8, "fp32", "0", "1", "off", "rs"), (4, "fp32", "0", "1", "off", "factor"), (8, "fp32", "0", "1", "off", "factor"),
-    (4, "bf16", "1", "1", "off", "rs"), (8, "bf16", "1", "1", "off", "rs"), (8, "bf16", "1", "0", "off", "rs"),
-    (8, "bf16", "0", "0", "off", "rs"), (8, "bf16", "1", "1", "on", "rs")])
-def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shard, xgmi, f32plane):
+@pytest.mark.parametrize("n,prec,shard,xgmi,f32plane", [
+    (4, "fp32", "0", "off", "rs"), (8, "fp32", "0", "off", "rs"), (4, "fp32", "1", "off", "rs"),
+    (8, "fp32", "1", "off", "rs"), (4, "fp32", "1", "off", "factor"), (8, "fp32", "1", "off", "factor"),
+    (4, "bf16", "1", "off", "rs"), (8, "bf16", "1", "off", "rs"), (8, "bf16", "0", "off", "rs"),
+    (8, "bf16", "1", "on", "rs")])
+def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, shard, xgmi, f32plane):
     """N ranks x B=50 sharing this GPU over gloo: the reduced gradient of the first step equals the
     sum of the N single-process gradients (gradient rel < 1e-4), the update equals TF1 Adam on their
     average, every rank holds identical parameters, and training makes progress. At 8 ranks the
@@ -202,7 +200,7 @@ def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, gather, shar
     f32plane=factor: the fp32 factor-gather plane (each rank's dW3 rows from every rank's fp32 dz
     and a2 columns) instead of the reduce-scatter of dW3."""
     _gpu()
-    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_FC_GATHER=gather, MIHVD_SHARD_W3=shard,
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_SHARD_W3=shard,
                MIHVD_XGMI=xgmi, MIHVD_TEST_PRECISION=prec, MIHVD_TEST_B="50", MIHVD_XGMI_TIMEOUT_MS="60000",
                MIHVD_F32_PLANE=f32plane)
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", str(n), sys.executable, WORKER, "dp_gloo_n", str(tmp_path)]

@@ -64,3 +64,54 @@ def test_native_engine_one_gpu(tmp_path):
     assert r["optimizer_bitwise"] and r["optimizer_collectives"] >= 12, r
     assert r["cnn_rel_diff"] < 1e-5, r
     assert r["stats"]["cycles"] > 0 and r["stopped"], r
+
+
+def test_bucket_plane_carries_distributed_optimizer(tmp_path):
+    """DistributedOptimizer's buckets go through the framework-owned RCCL bucket plane
+    (collectives.BucketPlane: NativeComm on a high-priority side stream), eagerly and inside a
+    captured whole-step HIP graph, and bench.py --impl torch / torch-graph report it as the
+    communicator (config.rccl_comm, RCCL's own count in config.rccl_nranks). World size 1 with the
+    collectives forced on: the parameters must equal the plain optimizer's within its own run-to-run
+    noise (MIOpen's conv backward need not be bitwise reproducible)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    env = dict(os.environ, PYTHONPATH=ROOT, MIHVD_FORCE_COLLECTIVES="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    out = tmp_path / "plane.json"
+    run = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port"]
+    p = subprocess.run(run + ["29565", os.path.join(ROOT, "tests", "workers", "plane_worker.py"), str(out)], env=env,
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = json.loads(out.read_text())
+    for key in ("eager", "graph"):
+        assert r[key]["plane"] and r[key]["nranks"] == 1, r
+        assert r[key]["launched"] >= r[key]["buckets"] * 3, r  # every bucket of every step (eager warm-up too)
+        assert r[key]["rel"] <= max(10 * r[key]["noise"], 1e-6), r
+    for i, impl in enumerate(("torch", "torch-graph")):
+        p = subprocess.run(run + [str(29567 + i), os.path.join(ROOT, "bench.py"), "--impl", impl, "--steps", "10",
+                                  "--warmup", "3"], env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+        assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+        rec = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")][-1]
+        assert rec["config"]["rccl_comm"] == "bucket plane" and rec["config"]["rccl_nranks"] == 1, rec
+
+
+def test_bench_reports_rccl_rank_count(tmp_path):
+    """bench.py's default (fused) step at one GPU prints RCCL's own rank count (ncclCommCount of a
+    witness communicator; the trainer's own with forced collectives)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "10", "--warmup", "2"], env=env,
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    rec = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    assert rec["config"]["rccl_nranks"] == 1 and rec["config"]["rccl_user_rank"] == 0, rec
+    assert rec["config"]["rccl_nranks_agree"] is True, rec

@@ -428,8 +428,7 @@ def sc_factor_rows(outdir):
 
     a2, dz0 = factors(r)
     dz_all = torch.empty(n, B, 1024)
-    dz = dz_all[r]
-    dz.copy_(dz0)
+    dz = dz0.clone()  # a buffer of its own (the trainer's layout: dz never aliases dz_all)
     a2_send, a2_recv = torch.empty(n, B, R), torch.empty(n, B, R)
     out_rows = torch.empty(R, 1024)
     factor_rows_(out_rows, a2, dz, dz_all, a2_send, a2_recv, r, n)
