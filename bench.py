@@ -322,6 +322,11 @@ def main():
         comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
     elif n == 1 and not tr.collectives:
         comm_desc = "none (1 GPU)"
+    elif tr.f32 and tr.shard_w3 and tr.data_plane() == "xgmi":
+        comm_desc = ("fp32 direct xGMI (hipIpc peer memory, device-side phase barriers, one stream): after the "
+                     "gradient reduction one launch sums every rank's small gradients and this rank's 1/N of "
+                     "dense/kernel's rows over the peers' regions in place (one-shot, all links) with both Adam "
+                     "updates, a second gathers the peers' updated fp32 rows; every step, in the HIP graph")
     elif tr.f32 and tr.shard_w3 and getattr(tr, "f32_factor", False):
         comm_desc = ("fp32 factor gather over RCCL: all-gather of every rank's fp32 dz and all-to-all of the a2 "
                      "columns of each rank's dense/kernel rows (beside fc1_bwd's dgrad and the conv backward) -> "
@@ -329,10 +334,11 @@ def main():
                      "-> RCCL all-gather of the updated fp32 rows (overlapping the next step's convolutions); RCCL "
                      "allreduce of the other fp32 gradients; every step, in the HIP graph")
     elif tr.f32 and tr.shard_w3:
-        comm_desc = ("RCCL reduce-scatter of dense/kernel's fp32 gradient by rows (overlapping the conv backward) -> "
-                     "each rank's Adam on its 1/N of the rows -> RCCL all-gather of the updated fp32 rows "
-                     "(overlapping the next step's convolutions); RCCL allreduce of the other fp32 gradients; every "
-                     "step, in the HIP graph")
+        comm_desc = ("RCCL reduce-scatter of dense/kernel's fp32 gradient by rows and each rank's Adam on its 1/N "
+                     "of the rows on a side stream (overlapping the conv backward) -> RCCL all-gather of the "
+                     "updated fp32 rows (overlapping the next step's convolutions); RCCL allreduce of the other "
+                     "fp32 gradients + their Adam on the main stream over a second communicator; every step, in "
+                     "the HIP graph")
     elif tr.f32:
         comm_desc = ("RCCL allreduce of the fp32 gradient fusion buffer every step: the fc bucket (98.4 % of the "
                      "bytes) on a side stream overlapping the conv backward, then the conv bucket; in the HIP graph")

@@ -1255,7 +1255,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
 // With the optimizer fused (world size 1: the gradients are final here) every element is updated
 // by the thread that finishes its gradient and block 0 advances the forward step counter
 // (adam_step's bump): one launch for the gradient reduction and the whole optimizer except
-// dense/kernel (whose update is deferred into the next conv2_fwd launch, f32_fwd.hip).
+// dense/kernel (whose update runs in f32_fc1_bwd from the gradient in registers).
 // Fixed summation order (deterministic, no atomics).
 // ------------------------------------------------------------------------------------------ //
 struct F32SmallAdam {
@@ -1264,38 +1264,6 @@ struct F32SmallAdam {
   int fc_lo = 0, fc_hi = 0;                     // the small fc range (multiple-of-4 bounds)
 };
 constexpr int CR_W2 = 200, CR_CP = 13, CR_DB = 1, CR_FC0 = CR_W2 + CR_CP + CR_DB;
-
-// The NEXT step's conv1 in the same launch (graph-replayed world-size-1 steps): 4 B blocks after the
-// reduction/optimizer blocks. conv1 needs the updated W1/b1 (Adam of the 13 cpart blocks) and the
-// advanced forward step counter (block 0), so those 14 blocks count in on sync[0] after a release
-// fence, the last of them sets sync[1]; the conv1 blocks (dispatched after every producer, which
-// never waits) acquire sync[1] and read W1/b1/the counter with agent-scope loads. The last conv1
-// block to finish resets both words, so every launch starts from zero. A bounded spin sets sync[2]
-// (surfaced by the trainer's checks) instead of hanging.
-struct F32Conv1Next {
-  const float* x = nullptr;
-  const int* rows = nullptr;
-  int n_pool = 0, B = 0, nblk = 0;  // nblk = 4 B, or 0: no conv1 role
-  float* a1 = nullptr;
-  uint8_t* idx1 = nullptr;
-  int* sync = nullptr;              // [0] producer arrivals, [1] ready flag, [2] timeout, [3] consumer arrivals
-};
-constexpr int CR_PRODUCERS = CR_CP + 1;
-
-__device__ __forceinline__ void c1n_arrive(const F32Conv1Next& c1) {
-  // the barrier completes every wave's stores (to this XCD's L2); thread 0's release RMW writes
-  // them back (one L2 writeback per producer block). The last arriver acquires the others'
-  // releases once and publishes the ready word.
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(c1.sync, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == CR_PRODUCERS - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(c1.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(c1.sync + 1, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
 
 // sum of rows r0, r0 + step, ... (< n) of a float4 column, 8 loads in flight per round
 __device__ __forceinline__ float4 strided_sum8(const float4* __restrict__ p, int64_t stride4, int r0, int step, int n) {
@@ -1323,46 +1291,19 @@ __device__ __forceinline__ void adam_flat4(const F32SmallAdam& sa, int64_t o, fl
   *reinterpret_cast<float4*>(sa.a.v + o) = vv;
 }
 
-template <bool C1>  // C1: the next step's conv1 role (F32Conv1Next) is compiled in
 __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __restrict__ slab, int G,
                                                               const float* __restrict__ cpart, int ncp,
                                                               const float* __restrict__ db2p, int ndb,
                                                               float* __restrict__ gW2, float* __restrict__ gW1,
                                                               float* __restrict__ gb1, float* __restrict__ gb2,
-                                                              F32SmallAdam sa, int n_fc, F32Conv1Next c1) {
+                                                              F32SmallAdam sa, int n_fc) {
   __shared__ float4 red[256];
   const int bid = blockIdx.x, t = threadIdx.x;
   const bool opt = sa.a.nblk > 0;
-  if (C1 && bid >= CR_FC0 + n_fc) {  // the next step's conv1 (opt is on: state, W1 updates)
-    // relaxed agent-scope polling (an acquire per poll would invalidate the L2 under every other
-    // block of the launch); W1/b1/the counter are then read with agent-scope (coherent) loads
-    if (t == 0) {
-      int spins = 0;
-      while (__hip_atomic_load(c1.sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 22)) {
-          __hip_atomic_fetch_or(c1.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // no load below is hoisted above the poll
-    const int cb = bid - CR_FC0 - n_fc;
-    f32_conv1_block<true>(cb & 3, cb >> 2, c1.x, c1.rows, c1.n_pool, sa.a.state, sa.a.p + sa.o_w1, sa.a.p + sa.o_b1,
-                          c1.a1, c1.idx1, c1.B, reinterpret_cast<float*>(red));
-    __syncthreads();
-    if (t == 0 && __hip_atomic_fetch_add(c1.sync + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c1.nblk - 1) {
-      __hip_atomic_store(c1.sync + 3, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(c1.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
   AdamCoef c{};
   if (opt) {
     c = f32_adam_coef(sa.a);
     if (bid == 0 && t == 0) const_cast<int64_t*>(sa.a.state)[ST_FWD] += 1;
-    if (C1 && bid == 0) c1n_arrive(c1);
   }
   if (bid >= CR_FC0) {  // small fc parameters: gradients already final (fc1_bwd)
     const int64_t i = sa.fc_lo / 4 + (int64_t)(bid - CR_FC0) * 256 + t;
@@ -1456,7 +1397,6 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       }
     }
   }
-  if (C1 && bid < CR_W2 + CR_CP) c1n_arrive(c1);  // a cpart block: W1 / b1 are final
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1755,9 +1695,7 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
                      const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
                      const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, int64_t o_w1,
                      int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo, int64_t fc_hi, double lr, double b1,
-                     double b2, double eps, double grad_scale, int64_t rule, const c10::optional<at::Tensor>& c1_x,
-                     const c10::optional<at::Tensor>& c1_rows, const c10::optional<at::Tensor>& c1_a1,
-                     const c10::optional<at::Tensor>& c1_idx1, const c10::optional<at::Tensor>& c1_sync) {
+                     double b2, double eps, double grad_scale, int64_t rule) {
   TORCH_CHECK(slab.dtype() == at::kFloat && slab.numel() % 51200 == 0 && slab.numel() > 0, "f32_conv_reduce: slab");
   TORCH_CHECK(cpart.dtype() == at::kFloat && cpart.numel() % CP_F32 == 0 && cpart.numel() > 0, "f32_conv_reduce: cpart");
   TORCH_CHECK(db2p.dtype() == at::kFloat && db2p.numel() % 64 == 0 && db2p.numel() > 0, "f32_conv_reduce: db2p");
@@ -1807,37 +1745,11 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
     sa.fc_hi = (int)fc_hi;
     n_fc = (int)((fc_hi - fc_lo) / 4 + 255) / 256;
   }
-  F32Conv1Next c1;
-  if (c1_x.has_value() && c1_x->defined()) {
-    // the next step's conv1 in this launch: needs the fused optimizer (W1/b1 updates, step bump)
-    TORCH_CHECK(sa.a.nblk > 0, "f32_conv_reduce: the fused conv1 needs the fused optimizer");
-    TORCH_CHECK(c1_a1.has_value() && c1_idx1.has_value() && c1_sync.has_value(), "f32_conv_reduce: conv1 operands");
-    const at::Tensor &x = *c1_x, &a1 = *c1_a1, &idx1 = *c1_idx1, &sync = *c1_sync;
-    const int B = (int)(a1.numel() / 6272);
-    TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv_reduce: x");
-    chk_f32(a1, (int64_t)B * 6272, "f32_conv_reduce: a1");
-    TORCH_CHECK(B >= 1 && idx1.dtype() == at::kByte && idx1.numel() == a1.numel(), "f32_conv_reduce: idx1");
-    TORCH_CHECK(sync.is_cuda() && sync.dtype() == at::kInt && sync.numel() >= 4, "f32_conv_reduce: sync (int32[4])");
-    c1.x = x.data_ptr<float>();
-    c1.n_pool = (int)x.size(0);
-    if (c1_rows.has_value() && c1_rows->defined()) {
-      TORCH_CHECK(c1_rows->dtype() == at::kInt && c1_rows->numel() == c1.n_pool, "f32_conv_reduce: rows");
-      c1.rows = c1_rows->data_ptr<int>();
-    } else {
-      TORCH_CHECK(c1.n_pool >= B, "f32_conv_reduce: x has fewer rows than the batch");
-    }
-    c1.B = B;
-    c1.nblk = 4 * B;
-    c1.a1 = a1.data_ptr<float>();
-    c1.idx1 = idx1.data_ptr<uint8_t>();
-    c1.sync = sync.data_ptr<int>();
-  }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  auto kern = c1.nblk > 0 ? f32_conv_reduce_kernel<true> : f32_conv_reduce_kernel<false>;
-  kern<<<CR_FC0 + n_fc + c1.nblk, 256, 0, stream>>>(
+  f32_conv_reduce_kernel<<<CR_FC0 + n_fc, 256, 0, stream>>>(
       slab.data_ptr<float>(), (int)(slab.numel() / 51200), cpart.data_ptr<float>(), (int)(cpart.numel() / CP_F32),
       db2p.data_ptr<float>(), (int)(db2p.numel() / 64), gW2.data_ptr<float>(), gW1.data_ptr<float>(),
-      gb1.data_ptr<float>(), gb2.data_ptr<float>(), sa, n_fc, c1);
+      gb1.data_ptr<float>(), gb2.data_ptr<float>(), sa, n_fc);
 }
 
 }  // namespace mihvd

@@ -87,17 +87,8 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
                    const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag);
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
-                   const c10::optional<at::Tensor>& p3, const c10::optional<at::Tensor>& g3,
-                   const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
-                   const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
-                   double grad_scale, int64_t rule, int64_t tail_blocks, const c10::optional<at::Tensor>& w2frag);
-void f32_conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1, const at::Tensor& w2,
-                    const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2);
-void f32_fc1_fwd(const at::Tensor& a2, at::Tensor& w3, at::Tensor& zpart, const c10::optional<at::Tensor>& g3,
-                 const c10::optional<at::Tensor>& m3, const c10::optional<at::Tensor>& v3,
-                 const c10::optional<at::Tensor>& state, double lr, double beta1, double beta2, double eps,
-                 double grad_scale, int64_t rule);
+                   const c10::optional<at::Tensor>& w2frag);
+void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
@@ -119,9 +110,7 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
                      const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
                      const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, int64_t o_w1,
                      int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo, int64_t fc_hi, double lr, double b1,
-                     double b2, double eps, double grad_scale, int64_t rule, const c10::optional<at::Tensor>& c1_x,
-                     const c10::optional<at::Tensor>& c1_rows, const c10::optional<at::Tensor>& c1_a1,
-                     const c10::optional<at::Tensor>& c1_idx1, const c10::optional<at::Tensor>& c1_sync);
+                     double b2, double eps, double grad_scale, int64_t rule);
 int64_t f32_db2_rows(int64_t B);
 at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel);
 int64_t f32_wgrad_groups(int64_t B);
@@ -298,22 +287,10 @@ void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Te
                   Tensor idx1, const OptT& w2, const OptT& w2frag) {
   mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag);
 }
-void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& p3,
-                  const OptT& g3, const OptT& m3, const OptT& v3, const OptT& state, double lr, double beta1,
-                  double beta2, double eps, double grad_scale, int64_t rule, int64_t tail_blocks,
-                  const OptT& w2frag) {
-  mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, p3, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule,
-                       tail_blocks, w2frag);
+void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& w2frag) {
+  mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, w2frag);
 }
-void f32_conv12_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
-                   Tensor idx1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2) {
-  mihvd::f32_conv12_fwd(x, rows, state, w1, b1, a1, idx1, w2, b2, a2, idx2);
-}
-void f32_fc1_fwd_op(const Tensor& a2, Tensor w3, Tensor zpart, const OptT& g3, const OptT& m3, const OptT& v3,
-                    const OptT& state, double lr, double beta1, double beta2, double eps, double grad_scale,
-                    int64_t rule) {
-  mihvd::f32_fc1_fwd(a2, w3, zpart, g3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule);
-}
+void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
                  Tensor stats) {
@@ -338,11 +315,9 @@ void f32_factor_rows_op(const Tensor& a2c, const Tensor& dz, const OptT& out, co
 void f32_conv_reduce_op(const Tensor& slab, const Tensor& cpart, const Tensor& db2p, Tensor gW2, Tensor gW1, Tensor gb1,
                         Tensor gb2, const OptT& params, const OptT& grads, const OptT& m, const OptT& v,
                         const OptT& state, int64_t o_w1, int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo,
-                        int64_t fc_hi, double lr, double b1, double b2, double eps, double grad_scale, int64_t rule,
-                        const OptT& c1_x, const OptT& c1_rows, const OptT& c1_a1, const OptT& c1_idx1,
-                        const OptT& c1_sync) {
+                        int64_t fc_hi, double lr, double b1, double b2, double eps, double grad_scale, int64_t rule) {
   mihvd::f32_conv_reduce(slab, cpart, db2p, gW2, gW1, gb1, gb2, params, grads, m, v, state, o_w1, o_b1, o_w2, o_b2,
-                         fc_lo, fc_hi, lr, b1, b2, eps, grad_scale, rule, c1_x, c1_rows, c1_a1, c1_idx1, c1_sync);
+                         fc_lo, fc_hi, lr, b1, b2, eps, grad_scale, rule);
 }
 }  // namespace
 
@@ -409,14 +384,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("bump_step_(Tensor(a!) step) -> ()");
   m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
         "Tensor? w2=None, Tensor(f!)? w2frag=None) -> ()");
-  m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor(c!)? p3=None, "
-        "Tensor? g3=None, Tensor(d!)? m3=None, Tensor(e!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., "
-        "float beta2=0., float eps=0., float grad_scale=1., int rule=0, int tail_blocks=0, Tensor? w2frag=None) -> ()");
-  m.def("f32_conv12_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
-        "Tensor w2, Tensor b2, Tensor(c!) a2, Tensor(d!) idx2) -> ()");
-  m.def("f32_fc1_fwd(Tensor a2, Tensor(w!) w3, Tensor(a!) zpart, Tensor? g3=None, Tensor(m!)? m3=None, "
-        "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
-        "float grad_scale=1., int rule=0) -> ()");
+  m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None) -> ()");
+  m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
   m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor(w!) w3, Tensor(a!) dY2, "
@@ -431,8 +400,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
         "Tensor(d!) gb2, Tensor(e!)? params=None, Tensor? grads=None, Tensor(f!)? m=None, Tensor(g!)? v=None, "
         "Tensor(s!)? state=None, int o_w1=0, int o_b1=0, int o_w2=0, int o_b2=0, int fc_lo=0, int fc_hi=0, "
-        "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0, Tensor? c1_x=None, "
-        "Tensor? c1_rows=None, Tensor(h!)? c1_a1=None, Tensor(i!)? c1_idx1=None, Tensor(j!)? c1_sync=None) -> ()");
+        "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0) -> ()");
   m.def("f32_db2_rows(int B) -> int", &mihvd::f32_db2_rows);
   m.def("f32_stamps_enable(int n_blocks, int kernel=0) -> Tensor", &mihvd::f32_stamps_enable);
   m.def("f32_wgrad_groups(int B) -> int", &mihvd::f32_wgrad_groups);
@@ -481,7 +449,6 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("f32_conv1_fwd", &f32_conv1_op);
   m.impl("f32_factor_rows", &f32_factor_rows_op);
   m.impl("f32_conv2_fwd", &f32_conv2_op);
-  m.impl("f32_conv12_fwd", &f32_conv12_op);
   m.impl("f32_fc1_fwd", &f32_fc1_fwd_op);
   m.impl("f32_head_fwd_bwd", &f32_head_op);
   m.impl("f32_fc1_bwd", &f32_fc1_bwd_op);

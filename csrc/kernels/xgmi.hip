@@ -63,6 +63,20 @@ Ctx* get(int64_t id) {
 
 __global__ void __launch_bounds__(256) xgmi_role_kernel(CollRole c) { coll_role_run(c, (int)blockIdx.x); }
 
+// Split form (xgmi_role.h): the phase entry/exit of one or two collectives in one block, then a
+// launch whose blocks [0, a.nblk) move a's bytes and the rest b's (the fp32 plane's small-gradient
+// and dense/kernel-row reductions with their Adam updates, or its row gather alone).
+__global__ void __launch_bounds__(64) xgmi_enter_kernel(CollRole a, CollRole b, int two) {
+  coll_role_enter_exit(a);
+  if (two) coll_role_enter_exit(b);
+}
+
+__global__ void __launch_bounds__(256) xgmi_data_kernel(CollRole a, CollRole b, int two) {
+  const int bid = (int)blockIdx.x;
+  if (bid < a.nblk) coll_role_data(a, bid);
+  else if (two) coll_role_data(b, bid - a.nblk);
+}
+
 // Stage `in` into this rank's slot of parity (epoch+1)&1 at [slot_off + parity*slot_bytes).
 __global__ void __launch_bounds__(256) xgmi_stage_kernel(const float* __restrict__ in, char* base, int ph,
                                                          int64_t slot_off, int64_t slot_bytes, int64_t n) {
@@ -282,13 +296,66 @@ int64_t xgmi_role_reduce(int64_t id, int64_t ph, int64_t offset, at::Tensor& out
   return register_role(id, r);
 }
 
+// Reduce of n floats at region byte `offset` (sum over ranks, rank order, times scale) into `out`
+// (optional) with the Adam update of fp32 parameters p (m, v; no bf16 copy) from the sum; `bump`:
+// block 0 also advances the forward step counter. The fp32 plane's prepared reductions.
+int64_t xgmi_role_reduce_f32(int64_t id, int64_t ph, int64_t offset, int64_t n, const c10::optional<at::Tensor>& out,
+                             double scale, at::Tensor& p, at::Tensor& m, at::Tensor& v, const at::Tensor& state,
+                             double lr, double b1, double b2, double eps, double grad_scale, int64_t rule, bool bump,
+                             int64_t nblk) {
+  Ctx* c = get(id);
+  TORCH_CHECK(n > 0 && n % 4 == 0, "xgmi_role_reduce_f32: n must be a positive multiple of 4");
+  float* o = nullptr;
+  if (out.has_value() && out->defined()) {
+    check_out(c, *out, "xgmi_role_reduce_f32");
+    TORCH_CHECK(out->numel() == n, "xgmi_role_reduce_f32: out must hold n floats");
+    o = out->data_ptr<float>();
+  }
+  for (const at::Tensor* t : {&p, &m, &v})
+    TORCH_CHECK(t->is_cuda() && t->dtype() == at::kFloat && t->is_contiguous() && t->numel() == n &&
+                    t->get_device() == c->device && ((uintptr_t)t->data_ptr() & 15) == 0,
+                "xgmi_role_reduce_f32: p, m, v must be aligned contiguous fp32 tensors of n floats");
+  TORCH_CHECK(state.is_cuda() && state.dtype() == at::kLong && state.numel() >= ST_WORDS,
+              "xgmi_role_reduce_f32: state must be the int64 device step state");
+  CollRole r = reduce_role(c, ph, offset, 0, n, o, scale);
+  r.adam = 1;
+  r.bump = bump ? 1 : 0;
+  r.aa = AdamArgs{p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), nullptr, state.data_ptr<int64_t>(),
+                  (float)lr, (float)b1, (float)b2, (float)eps, (float)grad_scale, (int)rule};
+  if (nblk > 0) r.nblk = (int)nblk;
+  return register_role(id, r);
+}
+
+// One or two prepared collectives (different phases) in the split form on the current stream: a
+// one-block entry launch, then one data launch. role_b < 0: one collective. `in_step` keeps the
+// debug stale-read injection (a launch of the training step; see xgmi_run). `enter` = false: the
+// data launch alone (a world of one, which has no peer to wait for).
+void xgmi_run_split(int64_t role_a, int64_t role_b, bool in_step, bool enter) {
+  CollRole a = xgmi_role_lookup(role_a);
+  const bool two = role_b >= 0;
+  CollRole b = two ? xgmi_role_lookup(role_b) : a;
+  TORCH_CHECK(a.kind != COLL_NONE && b.kind != COLL_NONE && a.nblk > 0 && b.nblk > 0,
+              "xgmi_run_split: empty descriptor");
+  TORCH_CHECK(!two || a.ph != b.ph, "xgmi_run_split: the two collectives need different phases");
+  if (!in_step) a.dbg_stale = b.dbg_stale = 0;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  if (enter) {
+    xgmi_enter_kernel<<<1, 64, 0, stream>>>(a, b, two ? 1 : 0);
+    XGMI_HIP(hipGetLastError());
+  }
+  xgmi_data_kernel<<<a.nblk + (two ? b.nblk : 0), 256, 0, stream>>>(a, b, two ? 1 : 0);
+  XGMI_HIP(hipGetLastError());
+}
+
 // Launch a prepared collective on its own (current stream).
-void xgmi_run(int64_t role) {
+// `in_step`: a launch of the training step (the fp32 plane's row gather), which keeps the debug
+// stale-read injection; otherwise a standalone launch (start-up validation) that stays exact.
+void xgmi_run(int64_t role, bool in_step) {
   CollRole r = xgmi_role_lookup(role);
   TORCH_CHECK(r.kind != COLL_NONE && r.nblk > 0, "xgmi_run: empty descriptor");
   // the debug stale-read injection models in-step staleness only: standalone launches (the
   // start-up validation, _validate_xgmi) stay exact, so the end-to-end check must catch it
-  r.dbg_stale = 0;
+  if (!in_step) r.dbg_stale = 0;
   launch_role(r, c10::hip::getCurrentHIPStream().stream());
 }
 
@@ -376,7 +443,13 @@ TORCH_LIBRARY_FRAGMENT(mihvd, m) {
         "Tensor? v=None, Tensor? shadow=None, Tensor? state=None, float lr=0., float b1=0., float b2=0., float eps=0., "
         "float grad_scale=1., int rule=0, int nblk=0) -> int",
         &mihvd::xgmi_role_reduce);
-  m.def("xgmi_run(int role) -> ()", &mihvd::xgmi_run);
+  m.def("xgmi_role_reduce_f32(int ctx, int phase, int offset, int n, Tensor(a!)? out, float scale, Tensor(b!) p, "
+        "Tensor(c!) m, Tensor(d!) v, Tensor state, float lr, float b1, float b2, float eps, float grad_scale, int rule, "
+        "bool bump, int nblk=0) -> int",
+        &mihvd::xgmi_role_reduce_f32);
+  m.def("xgmi_run(int role, bool in_step=False) -> ()", &mihvd::xgmi_run);
+  m.def("xgmi_run_split(int role_a, int role_b=-1, bool in_step=False, bool enter=True) -> ()",
+        &mihvd::xgmi_run_split);
   m.def("xgmi_gather_(int ctx, int phase, int offset, int stride, int rows_per_rank, int total_rows, int col_off, "
         "int col_bytes) -> ()",
         &mihvd::xgmi_gather_);

@@ -76,7 +76,8 @@ struct CollRole {
   float* out = nullptr;
   float scale = 1.f;
   int adam = 0;
-  AdamArgs aa{};
+  int bump = 1;             // with adam: block 0 advances the forward step counter (adam_step's bump)
+  AdamArgs aa{};            // aa.shadow null: fp32 parameters only (the fp32 step has no bf16 copy)
   int dbg_stale = 0;        // debug (MIHVD_XGMI_DEBUG_STALE): gathers skip odd rows -> stale data
   unsigned* herr = nullptr; // host-coherent mirror of err (the health monitor's watched word)
 };
@@ -193,7 +194,7 @@ __device__ __forceinline__ void xg_reduce(const CollRole& c, int bid, bool ok, u
   AdamCoef ac{};
   if (c.adam) {
     ac = adam_coef((float)c.aa.state[ST_OPT], c.aa.lr, c.aa.b1, c.aa.b2, c.aa.eps, c.aa.gscale, c.aa.rule);
-    if (bid == 0 && threadIdx.x == 0) const_cast<int64_t*>(c.aa.state)[ST_FWD] += 1;
+    if (c.bump && bid == 0 && threadIdx.x == 0) const_cast<int64_t*>(c.aa.state)[ST_FWD] += 1;
   }
   const int64_t n4 = c.n >> 2;
   const int64_t nthreads = (int64_t)c.nblk * blockDim.x;
@@ -224,7 +225,7 @@ __device__ __forceinline__ void xg_reduce(const CollRole& c, int bid, bool ok, u
       ((float4*)c.aa.p)[i] = pp;
       ((float4*)c.aa.m)[i] = mm;
       ((float4*)c.aa.v)[i] = vv;
-      ((uint2*)c.aa.shadow)[i] = sh;
+      if (c.aa.shadow != nullptr) ((uint2*)c.aa.shadow)[i] = sh;
     }
   }
   for (int64_t i = (n4 << 2) + (int64_t)bid * blockDim.x + threadIdx.x; i < c.n; i += nthreads) {
@@ -234,6 +235,31 @@ __device__ __forceinline__ void xg_reduce(const CollRole& c, int bid, bool ok, u
           __builtin_amdgcn_raw_buffer_load_b32(xg_rsrc(c.pt.base[p] + off, span), (uint32_t)(i * 4), 0, kXgAuxSys));
     if (c.out) c.out[i] = ok ? a * c.scale : nan;
   }
+}
+
+// Split form (a dedicated launch pair instead of a co-launch): one block enters and leaves the phase
+// (signal + wait for every peer + publish the epoch), and the data blocks of the NEXT launch on the
+// same stream move the bytes without waiting. Only one block per rank polls, so several ranks
+// sharing one GPU (the multi-rank tests) cannot starve a peer's kernels of wave slots with hundreds
+// of spinning role blocks; stream order makes the data launch follow the completed entry.
+__device__ __forceinline__ void coll_role_enter_exit(CollRole c) {
+  c.nblk = 1;  // the ticket of this launch: one block
+  bool ok;
+  const unsigned e = xg_enter(c, 0, ok);
+  xg_exit(c, e);
+}
+
+__device__ __forceinline__ void coll_role_data(const CollRole& c, int bid) {
+  __shared__ unsigned s_e, s_err;
+  if (threadIdx.x == 0) {
+    char* mine = c.pt.base[c.rank];
+    s_e = __hip_atomic_load(xg_u32(mine, kXgEpochOff) + c.ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_err = __hip_atomic_load(xg_u32(mine, kXgErrOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  const bool ok = s_err == 0u;
+  if (c.kind == COLL_GATHER) xg_gather(c, bid, ok);
+  else if (c.kind == COLL_REDUCE) xg_reduce(c, bid, ok, s_e);
 }
 
 // Run the role as block `bid` of its nblk role blocks (any blockDim >= kXgMaxRanks threads).

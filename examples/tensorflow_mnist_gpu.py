@@ -11,10 +11,12 @@ fp16 with dynamic loss scaling); LR scaling as the reference; callbacks
 saves ``./final_model``.
 
 On an MI355X the model trains through the hand-written CDNA4 kernels (``--impl hip``, the default
-with a GPU): every ``fit`` batch is one fused forward+backward of ``csrc/kernels`` (bf16 MFMA
-operands under ``mixed_bfloat16``, the exact-fp32 kernels under ``--policy float32``), the gradients
-go through ``hvd.DistributedOptimizer``'s RCCL buckets and TF1/Keras Adam runs as the multi-tensor
-HIP kernel. ``--impl torch`` runs stock PyTorch-ROCm layers instead.
+with a GPU): under ``mixed_bfloat16`` / ``float32`` ``fit`` drives the fused training step
+(``FusedMNISTTrainer``: the dataset resident on the device, the whole step in seven launches, 20
+steps per HIP-graph replay between the callback points; bf16 MFMA operands, or the exact-fp32
+kernels under ``--policy float32``) and prints its images/sec; under ``mixed_float16`` every batch
+is one fused forward+backward autograd node with the gradients through ``hvd.DistributedOptimizer``
+and the HIP loss scaler. ``--impl torch`` runs stock PyTorch-ROCm layers instead.
 """
 import argparse
 import os
@@ -70,6 +72,9 @@ def main():
     model.fit(x_train, y_train, batch_size=args.batch_size, epochs=epochs, steps_per_epoch=steps_per_epoch,
               validation_data=(x_test, y_test), validation_steps=validation_steps, callbacks=callbacks,
               verbose=1 if hvd.rank() == 0 else 0, seed=hvd.rank())
+    if hvd.rank() == 0 and getattr(model, "fit_throughput", None) is not None:
+        print(f"fit throughput: {model.fit_throughput:.0f} images/sec (fused graph-replayed training steps, "
+              f"policy {policy})", flush=True)
     if hvd.rank() == 0:
         score = model.evaluate(x_test, y_test, verbose=0)
         print("Test loss:", score[0])

@@ -271,8 +271,11 @@ class _LossScaler:
 
 class Model:
     """``policy`` is the Keras mixed-precision policy (tensorflow_mnist_gpu.py:26-28). A module with
-    ``impl == "hip"`` (``MNISTConvNet(impl="hip")``) trains through the hand-written CDNA4 kernels
-    (one fused forward+backward autograd node per batch): ``float32`` runs the exact-fp32 kernels,
+    ``impl == "hip"`` (``MNISTConvNet(impl="hip")``) trains through the hand-written CDNA4 kernels:
+    under ``float32`` / ``mixed_bfloat16`` with a TF1/Keras-rule Adam, ``fit`` drives the fused,
+    graph-replayed training step (``FusedMNISTTrainer``: the whole step in seven launches, k steps per
+    HIP graph replay between callback points); otherwise one fused forward+backward autograd node
+    per batch: ``float32`` runs the exact-fp32 kernels,
     ``mixed_bfloat16`` the bf16-operand kernels (fp32 accumulation and master weights),
     ``mixed_float16`` the same kernels built with fp16 operands (v_mfma_f32_16x16x32_f16) under the
     HIP dynamic loss scaler: the kernels scale dz by the current scale, the scaler unscales, checks
@@ -362,12 +365,131 @@ class Model:
             tot_acc += (logits.argmax(1) == yb).float().mean()
         return [float(tot_loss) / steps, float(tot_acc) / steps]
 
+    # callbacks whose per-batch hooks the fused fit path reproduces (or that have none)
+    _FUSED_CALLBACKS = (BroadcastGlobalVariablesCallback, MetricAverageCallback, ModelCheckpoint, TensorBoard)
+
+    def _fused_fit_trainer(self, cbs, batch_size):
+        """The graph-replayed fit path (tensorflow_mnist_gpu.py:166-182 under ``float32`` /
+        ``mixed_bfloat16``): a :class:`~mihvd.models.fused_mnist.FusedMNISTTrainer` over the
+        module's weights and the optimizer's Adam hyper-parameters, or None where the per-batch path
+        must run (MIHVD_KERAS_FUSED=0, another policy or module, an optimizer or reduction the fused
+        step does not implement, existing optimizer state, or a callback with per-batch hooks)."""
+        if os.environ.get("MIHVD_KERAS_FUSED", "1") == "0":
+            return None
+        from .models.mnist import MNISTConvNet
+        from .optim import FusedAdam, TFAdam
+
+        m, opt = self.module, self.optimizer
+        if (not isinstance(m, MNISTConvNet) or getattr(m, "impl", None) != "hip" or self.policy not in
+                ("float32", "mixed_bfloat16") or opt is None or not 1 <= batch_size <= 128):
+            return None
+        if not isinstance(opt, (TFAdam, FusedAdam)) or len(opt.param_groups) != 1 or any(opt.state.values()):
+            return None
+        g = opt.param_groups[0]
+        if isinstance(opt, FusedAdam) and (g.get("rule") != "tf" or g.get("weight_decay", 0.0) != 0.0):
+            return None
+        op = getattr(opt, "_op", _b.Average)
+        if op not in (_b.Average, _b.Sum):
+            return None
+        for cb in cbs:
+            if not isinstance(cb, self._FUSED_CALLBACKS):
+                overridden = (type(cb).on_batch_begin is not Callback.on_batch_begin
+                              or type(cb).on_batch_end is not Callback.on_batch_end)
+                if overridden:
+                    return None
+        from .models.fused_mnist import FusedMNISTTrainer
+
+        tr = FusedMNISTTrainer(batch_size=batch_size, lr=g["lr"], betas=tuple(g["betas"]), eps=g["eps"],
+                               dropout=m.dropout_rate, device=self._device(), op=op,
+                               precision="fp32" if self.policy == "float32" else "bf16")
+        tr.load_model_weights(m)
+        tr.track_stats = True
+        return tr
+
+    def _fit_fused(self, tr, x, y, batch_size, epochs, steps_per_epoch, validation_data, validation_steps, cbs,
+                   verbose, shuffle, seed):
+        """fit() on the fused trainer: the dataset resident on the device, each epoch's steps replayed
+        from HIP graphs of ``MIHVD_KERAS_GRAPH_STEPS`` steps (default 20) between the callback points
+        (BroadcastGlobalVariablesCallback after the first batch, the epoch-end callbacks); the
+        module's weights are synchronised at every epoch end (validation, checkpoints) and the
+        optimizer's Adam slots at the end of fit."""
+        k = int(os.environ.get("MIHVD_KERAS_GRAPH_STEPS", "20"))
+        tr.set_device_dataset(torch.as_tensor(np.asarray(x, dtype=np.float32)),
+                              torch.as_tensor(np.asarray(y).astype(np.int64)), shuffle=shuffle,
+                              seed=0 if seed is None else int(seed))
+        bcast = [cb for cb in cbs if isinstance(cb, BroadcastGlobalVariablesCallback)]
+        self.fused_trainer = tr
+        t_epochs = []
+        for epoch in range(epochs):
+            for cb in cbs:
+                cb.on_epoch_begin(epoch)
+            t0 = time.time()
+            tr.reset_stats()
+            done = 0
+            if epoch == 0:
+                tr.device_step()  # batch 0 eagerly: the broadcast callback's point (optimizer state exists)
+                done = 1
+                for cb in bcast:
+                    if not cb.broadcast_done:
+                        tr.broadcast(cb.root_rank)
+                        cb.broadcast_done = True
+            tr.run_steps(steps_per_epoch - done, steps_per_replay=k)
+            loss, acc = tr.epoch_stats()  # (synchronises)
+            t_epochs.append(time.time() - t0)
+            tr.sync()
+            tr.gather_full_state()
+            tr.to_model(self.module)
+            logs = {"loss": loss, "accuracy": acc}
+            if validation_data is not None:
+                vl, va = self.evaluate(validation_data[0], validation_data[1], batch_size, validation_steps)
+                logs["val_loss"], logs["val_accuracy"] = vl, va
+            for cb in cbs:
+                cb.on_epoch_end(epoch, logs)
+            for k2, v in logs.items():
+                self.history.setdefault(k2, []).append(v)
+            if verbose:
+                dt = time.time() - t0
+                print(f"Epoch {epoch + 1}/{epochs} - {dt:.1f}s - " +
+                      " - ".join(f"{k2}: {v:.4f}" for k2, v in logs.items()), file=sys.stdout, flush=True)
+        # the Adam slots into the optimizer's state (a later per-batch fit or a checkpoint continues
+        # from them)
+        self._adam_state_from_trainer(tr)
+        # images/sec of the training steps (whole job), from the epochs after the first (whose time
+        # includes the HIP graph captures) when there are several
+        per_epoch = steps_per_epoch * batch_size * (_b.size() if _b.is_initialized() else 1)
+        timed = t_epochs[1:] if len(t_epochs) > 1 else t_epochs
+        self.fit_throughput = per_epoch * len(timed) / sum(timed) if sum(timed) > 0 else float("nan")
+        for cb in cbs:
+            cb.on_train_end()
+        return self
+
+    def _adam_state_from_trainer(self, tr):
+        opt = self.optimizer
+        names = dict(self.module.ordered_parameters())
+        t = int(tr.state[1].item())
+        for name, p in names.items():
+            st = opt.state[p]
+            st["step"] = torch.tensor(float(t))
+            st["exp_avg"] = tr.pview(name, tr.m).detach().clone().view_as(p)
+            st["exp_avg_sq"] = tr.pview(name, tr.v).detach().clone().view_as(p)
+
     def fit(self, x, y, batch_size=100, epochs=1, steps_per_epoch=None, validation_data=None, validation_steps=None,
             callbacks=(), verbose=1, shuffle=True, seed=None):
         cbs = list(callbacks)
         for cb in cbs:
             cb.set_model(self)
         n = len(x)
+        tr = self._fused_fit_trainer(cbs, batch_size)
+        if tr is not None:
+            steps_per_epoch = steps_per_epoch or max(1, n // batch_size)
+            self._steps_per_epoch = steps_per_epoch
+            for cb in cbs:
+                cb.on_train_begin()
+            try:
+                return self._fit_fused(tr, x, y, batch_size, epochs, steps_per_epoch, validation_data,
+                                       validation_steps, cbs, verbose, shuffle, seed)
+            finally:
+                tr.close()
         steps_per_epoch = steps_per_epoch or max(1, n // batch_size)
         self._steps_per_epoch = steps_per_epoch
         rng = np.random.default_rng(seed)

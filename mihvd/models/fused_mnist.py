@@ -291,6 +291,34 @@ class FusedMNISTTrainer:
             self.use_xgmi = self.xplane is not None and self._xgmi_mode == "on"
             if self.use_xgmi:
                 self.xplane.watch(True)
+        if self._f32_can_shard:
+            # fp32 direct-xGMI plane (sharded dense/kernel optimizer; MIHVD_XGMI, picked by
+            # select_data_plane under "auto"): the parameters and the gradient buffer live in the
+            # hipIpc-shared region; after the gradient reduction one launch sums every rank's small
+            # gradients and this rank's dense/kernel rows over the peers' regions in place (one-shot,
+            # all 7 links at once) with both Adam updates, and a second gathers the peers' updated
+            # rows: two launches on the one stream, no side stream, no RCCL ring
+            from ..parallel import xgmi as _xg
+
+            self._xgmi_mode = _xg.env_mode()
+            if self._xgmi_mode != "off" and self.world <= _xg.MAX_RANKS:
+                import torch.distributed as dist
+
+                if dist.is_initialized():
+                    try:
+                        self.xplane = _xg.XGMIRegion({"params": (FLAT_NUMEL, torch.float32),
+                                                      "grads": (FLAT_NUMEL, torch.float32)}, device=dev)
+                    except _xg.XGMIUnavailable as e:
+                        _xg.warn_fallback(str(e))
+            if self.xplane is not None:
+                pr = self.xplane.view("params")
+                pr.copy_(self.params)
+                self.params = pr
+                self.grads = self.xplane.view("grads")
+                self.grads.zero_()
+            self.use_xgmi = self.xplane is not None and self._xgmi_mode == "on" and self.shard_w3
+            if self.use_xgmi:
+                self.xplane.watch(True)
         if self.gather:
             if self.xplane is not None:
                 self.a2_all = self.xplane.view("a2").view(self.world * B, 3136)
@@ -359,6 +387,10 @@ class FusedMNISTTrainer:
                 self.f32_factor = self.shard_w3 and f32_plane_mode() == "factor"
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
+        # Keras fit (mihvd/keras.py): every step adds its (sum of losses, correct count) on the device
+        self.track_stats = False
+        self._stat_sum = torch.zeros(2, **f32)
+        self._stat_steps = 0
         self.X = self.Y = self.rows = None
         self.graph = None
         self._graphs = {}
@@ -462,6 +494,23 @@ class FusedMNISTTrainer:
 
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
+        self._launch_step_core(x, rows, labels)
+        if self.track_stats:  # Keras fit: the epoch's running (loss, accuracy) sums, on the device
+            self._stat_sum.add_(self.stats.sum(0))
+
+    def reset_stats(self):
+        """Start a new accumulation of per-step (loss, accuracy) sums (``track_stats``)."""
+        self._stat_sum.zero_()
+        self._stat_steps = 0
+
+    def epoch_stats(self):
+        """Mean loss and accuracy over the steps since ``reset_stats`` (``track_stats``; reading
+        synchronises)."""
+        n = max(1, self._stat_steps) * self.B
+        s = self._stat_sum.tolist()
+        return s[0] / n, s[1] / n
+
+    def _launch_step_core(self, x, rows, labels):
         if self.f32:
             return self._launch_step_f32(x, rows, labels)
         if self.gather:
@@ -552,6 +601,8 @@ class FusedMNISTTrainer:
                               SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0],
                               FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
             return
+        if self.shard_w3 and self.use_xgmi:
+            return self._launch_step_f32_xgmi(x, rows, st, w2, wf, gconv)
         if self.shard_w3:
             return self._launch_step_f32_shard(x, rows, st, w2, wf, gconv)
         # replicated optimizer (sizes that do not divide 3136, Adasum, MIHVD_SHARD_W3=0): the "fc"
@@ -647,6 +698,108 @@ class FusedMNISTTrainer:
             self._shadow_ev.record(side)
         self._full_state_valid = False
 
+    # phases of the fp32 xGMI plane (its own region), in step order
+    PH32_SMALL, PH32_ROWS, PH32_GATHER = 0, 1, 2
+
+    def _prepare_roles_f32(self):
+        """The fp32 plane's prepared collectives (they hold the buffers' pointers and the optimizer
+        hyper-parameters: a new learning rate, or keep_w3_grad, prepares them again)."""
+        xp, W, R, r = self.xplane, self.world, self._f32_R, self.rank
+        b1, b2 = self.betas
+        hyper = dict(state=self.state, lr=self.lr, b1=b1, b2=b2, eps=self.eps, grad_scale=1.0 / W, rule=self.rule)
+        h = slice(0, W3_START)
+        mine = slice(W3_START + r * R * 1024, W3_START + (r + 1) * R * 1024)
+        roles = {"lr": self.lr, "keep": self.keep_w3_grad}
+        # the small gradients summed over every rank + their Adam + the forward step bump
+        if self.keep_w3_grad and getattr(self, "gred32", None) is None:
+            self.gred32 = torch.empty(W3_START, device=self.device, dtype=torch.float32)
+        roles["small"] = xp.prepare_reduce_f32("grads", self.PH32_SMALL, W3_START,
+                                               dict(p=self.params[h], m=self.m[h], v=self.v[h], **hyper),
+                                               out=self.gred32 if self.keep_w3_grad else None, bump=True)
+        # this rank's dense/kernel rows summed over every rank + their Adam
+        roles["rows"] = xp.prepare_reduce_f32("grads", self.PH32_ROWS, R * 1024,
+                                              dict(p=self.params[mine], m=self.m[mine], v=self.v[mine], **hyper),
+                                              out=self.gshard if self.keep_w3_grad else None,
+                                              offset_elems=W3_START + r * R * 1024)
+        # every peer's updated rows into this rank's dense/kernel
+        roles["gather"] = xp.prepare_gather("params", self.PH32_GATHER, 4096, R, 3136, offset_bytes=W3_START * 4)
+        self._roles = roles
+
+    def _launch_step_f32_xgmi(self, x, rows, st, w2, wf, gconv):
+        """Rest of the fp32 step on the direct xGMI plane (after the head), one stream:
+
+            fc1_bwd (dgrad, dW3 -> region) | conv2_bwd | conv_reduce (small grads -> region) |
+            xGMI: small sum + Adam + bump, my dense/kernel rows' sum + Adam | xGMI: row gather
+
+        Buffer reuse follows the phase order (xgmi_role.h): a rank rewrites its gradients (next
+        fc1_bwd / conv_reduce) only after the row gather's phase, which every peer enters only
+        after its reductions (the readers of those gradients) completed; it rewrites its rows
+        (next reduction) only after every peer entered the next reduction phase, i.e. finished
+        this step's gather."""
+        o, G = self.ops, self.gview
+        R = self._roles
+        if R is None or R.get("kind") == "bf16" or R["lr"] != self.lr or R["keep"] != self.keep_w3_grad:
+            self._prepare_roles_f32()
+            R = self._roles
+        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, self.pview("dense/kernel"), self.dY2, self.db2p,
+                      G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
+        if self.world > 1:
+            self.xplane.run_split(R["small"], R["rows"])
+            self.xplane.run_split(R["gather"], in_step=True)
+        else:  # a world of one (forced collectives): no peer to wait for, no row to gather
+            self.xplane.run_split(R["small"], R["rows"], enter=False)
+        self._full_state_valid = False
+
+    def _validate_xgmi_f32(self) -> bool:
+        """Run the fp32 plane's collectives on random data (the reductions without their Adam
+        update) and compare them with the same collectives over the process group: the sums to
+        fp32 rounding, the row gather bitwise. Collective; the parameters and gradients are
+        restored."""
+        import torch.distributed as dist
+
+        if self._roles is None or self._roles.get("kind") == "bf16" or self._roles["lr"] != self.lr:
+            self._prepare_roles_f32()
+        W, r, R = self.world, self.rank, self._f32_R
+        g = torch.Generator(device="cpu").manual_seed(9173 + r)
+        saved_p, saved_g = self.params.clone(), self.grads.clone()
+        self.grads.copy_(torch.randn(FLAT_NUMEL, generator=g))
+        p3 = self.params[W3_START:].view(3136, 1024)
+        p3[r * R:(r + 1) * R].copy_(torch.randn(R, 1024, generator=g))
+        ref_g = self.grads.clone()
+        dist.all_reduce(ref_g)
+        ref_p = p3.clone()
+        self._all_gather_rows(ref_p, ref_p[r * R:(r + 1) * R])
+        torch.cuda.synchronize(self.device)
+        out_s = torch.empty(W3_START, device=self.device)
+        out_r = torch.empty(R * 1024, device=self.device)
+        if "v_small" not in self._roles:  # the reductions without their Adam update, into out_s / out_r
+            self._val_out = (out_s, out_r)
+            self._roles["v_small"] = self.xplane.prepare_reduce("grads", self.PH32_SMALL, out_s)
+            self._roles["v_rows"] = self.xplane.prepare_reduce("grads", self.PH32_ROWS, out_r,
+                                                               offset_elems=W3_START + r * R * 1024)
+        out_s, out_r = self._val_out
+        self.xplane.run_split(self._roles["v_small"], self._roles["v_rows"])
+        self.xplane.run_split(self._roles["gather"])
+        torch.cuda.synchronize(self.device)
+        mine = slice(W3_START + r * R * 1024, W3_START + (r + 1) * R * 1024)
+        ok = bool(torch.allclose(out_s, ref_g[:W3_START], rtol=1e-5, atol=1e-5))
+        ok &= bool(torch.allclose(out_r, ref_g[mine], rtol=1e-5, atol=1e-5))
+        ok &= bool(torch.equal(p3, ref_p))
+        try:
+            self.xplane.check()
+        except RuntimeError:
+            ok = False
+        from ..parallel.xgmi import _group_ok
+
+        ok = _group_ok(ok, None, self.device)
+        dist.barrier()  # every peer finished reading this rank's buffers before they are restored
+        self.params.copy_(saved_p)
+        self.grads.copy_(saved_g)
+        torch.cuda.synchronize(self.device)
+        return ok
+
     def _reduce_scatter_rows(self, full, out, R):
         """out = this rank's R rows of the sum over ranks of ``full`` (rows x 1024)."""
         import torch.distributed as dist
@@ -740,7 +893,7 @@ class FusedMNISTTrainer:
         lo, hi = self._w3_mine
         h = slice(0, W3_START)
         T64 = self._T * 64
-        r = {"lr": self.lr}
+        r = {"lr": self.lr, "kind": "bf16"}
         # dz rows, in fc1_bwd's launch (a multiple of 8 blocks: its dgrad tiles keep their XCD map)
         r["dz"] = xp.prepare_gather("dz", self.PH_DZ, 1024 * 2, B, nblk=64)
         # a2 columns of this rank's W3 row tiles (sharded) / whole rows (627 KB per peer), in the
@@ -902,6 +1055,7 @@ class FusedMNISTTrainer:
             self._launch_step(self.x_buf, None, self.y_buf)
             self._join()
         self.global_step += 1
+        self._stat_steps += 1
         return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
 
     def device_step(self):
@@ -913,6 +1067,7 @@ class FusedMNISTTrainer:
             self._launch_step(self.X, self.rows, self.Y)
             self._join()
         self.global_step += 1
+        self._stat_steps += 1
         return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
 
     def _maybe_reshuffle(self, k):
@@ -990,6 +1145,7 @@ class FusedMNISTTrainer:
         with trace_range(f"mihvd.graph_replay[{k} steps]"):
             g.replay()
         self.global_step += k
+        self._stat_steps += k
 
     def run_steps(self, k: int, steps_per_replay: int = 10) -> int:
         """Advance exactly ``k`` steps on the resident dataset, graph-replayed: the first call
@@ -1109,7 +1265,7 @@ class FusedMNISTTrainer:
         plane, whose row gather of the last update would run in the next conv12_fwd launch,
         gathers the rows now. ``factor``: the fp32 factor-gather plane (sharded only)."""
         self._join()
-        if self.use_xgmi and self.shard_w3 and not (xgmi and shard):
+        if self.use_xgmi and self.shard_w3 and not self.f32 and not (xgmi and shard):
             torch.cuda.synchronize(self.device)
             T64 = self._T * 64
             self._all_gather_rows(self.shadow3, self.shadow3[self.rank * T64:(self.rank + 1) * T64])
@@ -1166,7 +1322,7 @@ class FusedMNISTTrainer:
         planes = ["rccl"]
         if self.xplane is not None and self._xgmi_mode != "off":
             self.xplane.watch(False)  # a timeout while the plane is on trial means "use RCCL"
-            valid = self._validate_xgmi()
+            valid = self._validate_xgmi_f32() if self.f32 else self._validate_xgmi()
             rep["valid"] = valid
             if valid:
                 planes = ["xgmi"] if self._xgmi_mode == "on" else ["xgmi", "rccl"]
@@ -1175,6 +1331,8 @@ class FusedMNISTTrainer:
 
                 warn_fallback("validation against the process group's collectives failed")
         cands = [(p, sh) for p in planes for sh in dict.fromkeys(shard_options)]
+        if self.f32:  # the fp32 xGMI plane exists in the sharded form only
+            cands = [c for c in cands if not (c[0] == "xgmi" and not c[1])]
         if self.f32 and self._f32_can_shard and True in shard_options:
             # the fp32 factor-gather plane (sharded): MIHVD_F32_PLANE=auto (default) times it beside
             # the reduce-scatter plane, "factor" uses it alone, "rs" leaves it out
@@ -1322,9 +1480,12 @@ class FusedMNISTTrainer:
             return torch.cat([self.gred, self.grads[W3_START:]])
         if self.f32 and self.shard_w3:
             # the reduce-scatter plane leaves this rank's reduced dense/kernel rows in place in the
-            # gradient buffer, the factor plane in gshard (keep_w3_grad)
+            # gradient buffer, the factor and xGMI planes in gshard (keep_w3_grad); the xGMI plane's
+            # small-gradient sums are in gred32 (keep_w3_grad)
             g = self.grads.clone()
-            if self.f32_factor:
+            if self.use_xgmi and getattr(self, "gred32", None) is not None:
+                g[:W3_START] = self.gred32
+            if self.f32_factor or self.use_xgmi:
                 R = self._f32_R
                 g[W3_START + self.rank * R * 1024:W3_START + (self.rank + 1) * R * 1024] = self.gshard.view(-1)
             return g
@@ -1337,6 +1498,8 @@ class FusedMNISTTrainer:
             return "xgmi" if self.use_xgmi else "rccl"
         if self.f32 and self.f32_factor:
             return "factor"
+        if self.f32 and self.use_xgmi and self.shard_w3:
+            return "xgmi"
         return "rccl"
 
     def close(self):
@@ -1360,9 +1523,13 @@ class FusedMNISTTrainer:
         if dist.is_initialized():
             dist.barrier()
         if self.xplane is not None:
-            for name in ("a2_all", "dz_all", "a2", "dz", "grads", "shadow3"):
-                if hasattr(self, name):
-                    setattr(self, name, None)
+            if self.f32:  # the parameters and gradients lived in the region: keep readable copies
+                self.params = self.params.clone()
+                self.grads = self.grads.clone()
+            else:
+                for name in ("a2_all", "dz_all", "a2", "dz", "grads", "shadow3"):
+                    if hasattr(self, name):
+                        setattr(self, name, None)
             self.xplane.close()
             self.xplane = None
             self.use_xgmi = False

@@ -152,11 +152,11 @@ class XGMIRegion:
     # its first nblk blocks (co-launch: no extra launch, no stream fork in the step's HIP graph).
     # Descriptors hold raw pointers: the tensors they name must outlive them.
     def prepare_gather(self, name: str, phase: int, row_bytes: int, rows_per_rank: int, total_rows: int | None = None,
-                       col_lo: int = 0, col_hi: int | None = None, nblk: int = 0) -> int:
+                       col_lo: int = 0, col_hi: int | None = None, nblk: int = 0, offset_bytes: int = 0) -> int:
         total = self.world * rows_per_rank if total_rows is None else int(total_rows)
         col_hi = row_bytes if col_hi is None else int(col_hi)
-        return int(self._o.xgmi_role_gather(self.ctx, phase, self.offsets[name], row_bytes, rows_per_rank, total,
-                                            col_lo, col_hi - col_lo, nblk))
+        return int(self._o.xgmi_role_gather(self.ctx, phase, self.offsets[name] + int(offset_bytes), row_bytes,
+                                            rows_per_rank, total, col_lo, col_hi - col_lo, nblk))
 
     def prepare_reduce(self, name: str, phase: int, out: torch.Tensor, scale: float = 1.0, adam: dict | None = None,
                        nblk: int = 0, offset_elems: int = 0) -> int:
@@ -169,9 +169,29 @@ class XGMIRegion:
                                             a.get("lr", 0.0), a.get("b1", 0.0), a.get("b2", 0.0), a.get("eps", 0.0),
                                             a.get("grad_scale", 1.0), a.get("rule", 0), nblk))
 
-    def run(self, role: int):
-        """Launch a prepared collective on its own (current stream)."""
-        self._o.xgmi_run(role)
+    def prepare_reduce_f32(self, name: str, phase: int, n: int, adam: dict, out: torch.Tensor | None = None,
+                           scale: float = 1.0, offset_elems: int = 0, bump: bool = False, nblk: int = 0) -> int:
+        """The fp32 plane's reduction: the sum over ranks of ``n`` floats of buffer ``name`` from
+        ``offset_elems`` (rank order, times ``scale``), the Adam update of the fp32 parameters
+        ``adam["p"]`` (``m``, ``v``; no bf16 copy) from it, and with ``bump`` the forward step
+        counter's advance; ``out`` (optional) also receives the sum."""
+        a = adam
+        return int(self._o.xgmi_role_reduce_f32(self.ctx, phase, self.offsets[name] + 4 * int(offset_elems), int(n),
+                                                out, scale, a["p"], a["m"], a["v"], a["state"], a["lr"], a["b1"],
+                                                a["b2"], a["eps"], a["grad_scale"], a["rule"], bool(bump), nblk))
+
+    def run(self, role: int, in_step: bool = False):
+        """Launch a prepared collective on its own (current stream). ``in_step``: a launch of the
+        training step (keeps MIHVD_XGMI_DEBUG_STALE's injected stale reads)."""
+        self._o.xgmi_run(role, bool(in_step))
+
+    def run_split(self, role_a: int, role_b: int = -1, in_step: bool = False, enter: bool = True):
+        """One or two prepared collectives (different phases) as a dedicated launch pair on the
+        current stream: a one-block launch enters and leaves the phases (the only block that waits
+        for the peers), then the data launch moves the bytes (csrc/kernels/xgmi_role.h, split
+        form). ``in_step``: keep MIHVD_XGMI_DEBUG_STALE's injected stale reads. ``enter=False``: the
+        data launch alone (a world of one: no peer to wait for)."""
+        self._o.xgmi_run_split(role_a, role_b, bool(in_step), bool(enter))
 
     def check(self):
         """Wait for the current stream and raise if a device-side phase barrier timed out."""

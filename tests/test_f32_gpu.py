@@ -50,14 +50,10 @@ def test_f32_conv1_fwd(ops, B):
     assert (idx.long()[pos] == rd[pos]).float().mean() > 0.999
 
 
-@pytest.mark.parametrize("form", ["w4", "w4-d1", "w8", "w8-d1"])
 @pytest.mark.parametrize("B", [7, 100, 128])
-def test_f32_conv2_fwd(ops, B, form, monkeypatch):
-    """4-wave form (one wave per SIMD) and the 8-wave form (MIHVD_F32_C2F_W8=1: the two waves of a
-    SIMD split the input channels; their partials meet in LDS), A reads two or one (-d1) steps ahead,
-    HWIO and fragment-copy W2 reads."""
-    monkeypatch.setenv("MIHVD_F32_C2F_W8", "1" if form.startswith("w8") else "0")
-    monkeypatch.setenv("MIHVD_F32_C2F_DEPTH", "1" if form.endswith("d1") else "2")
+def test_f32_conv2_fwd(ops, B):
+    """The two waves of a SIMD split the input channels (their partials meet in LDS); HWIO and
+    fragment-copy W2 reads give the same bits."""
     g = torch.Generator(device="cuda").manual_seed(2)
     a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
     w = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05

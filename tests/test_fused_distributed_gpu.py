@@ -22,6 +22,7 @@ def _gpu():
 
 @pytest.mark.parametrize("prec,shard,xgmi,comm", [
     ("fp32", "1", "off", "native"), ("fp32", "0", "off", "native"), ("fp32", "1", "off", "torch"),
+    ("fp32", "1", "on", "native"), ("fp32", "1", "auto", "native"),
     ("bf16", "0", "off", "native"), ("bf16", "1", "off", "native"), ("bf16", "0", "on", "native"),
     ("bf16", "1", "on", "native"), ("bf16", "1", "auto", "native")])
 def test_collectives_inside_hip_graph(tmp_path, prec, shard, xgmi, comm):
@@ -32,8 +33,10 @@ def test_collectives_inside_hip_graph(tmp_path, prec, shard, xgmi, comm):
     boundary by an event), here with R = 3136 rows. bf16 shard=1: the sharded dense/kernel optimizer
     of the factor-gather plane, whose bf16 row gather runs on the side stream across step
     boundaries. xgmi=off: RCCL; on: the direct xGMI plane (all four collectives in the graph); auto:
-    plane selection (validation against RCCL + timed replays of both planes) first. comm=native:
-    the framework-owned communicator (the default); torch: the process group's (the fallback)."""
+    plane selection (validation against RCCL + timed replays of both planes) first. fp32 with
+    xgmi=on: the fp32 direct-xGMI plane (the reductions with both Adam updates, then the row
+    gather, as two launches of the one stream). comm=native: the framework-owned communicator (the
+    default); torch: the process group's (the fallback)."""
     _gpu()
     env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3=shard,
                MIHVD_XGMI=xgmi, MIHVD_TEST_PRECISION=prec, MIHVD_COMM=comm)
@@ -57,8 +60,9 @@ def test_collectives_inside_hip_graph(tmp_path, prec, shard, xgmi, comm):
     elif xgmi == "off":
         assert r["plane"] == "rccl", r
     else:
-        assert r["select"]["valid"] and r["plane"] in ("xgmi", "rccl"), r
-        assert set(r["select"]["us_per_step"]) == {"xgmi-shard", "rccl-shard"}, r
+        assert r["select"]["valid"] and r["plane"] in ("xgmi", "rccl", "factor"), r
+        planes = {"xgmi-shard", "rccl-shard"} | ({"factor-shard"} if prec == "fp32" else set())
+        assert set(r["select"]["us_per_step"]) == planes, r
 
 
 def test_f32_factor_plane_inside_hip_graph(tmp_path):
@@ -97,14 +101,17 @@ def test_fused_data_parallel_equivalence_two_ranks(tmp_path):
         assert o["rel_update_diff"] < 0.05, o
 
 
-def test_fused_data_parallel_xgmi_two_ranks(tmp_path):
-    """The factor-gather plane over the direct xGMI collectives (a2/dz gathers and the
-    small-gradient reduction read the peer's region in place). gloo only carries the IPC handle
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_fused_data_parallel_xgmi_two_ranks(tmp_path, prec):
+    """bf16: the factor-gather plane over the direct xGMI collectives (a2/dz gathers and the
+    small-gradient reduction read the peer's region in place). fp32: the fp32 plane (sharded rows:
+    one-shot reductions with Adam, then the row gather). gloo only carries the IPC handle
     exchange."""
     _gpu()
     # both ranks share this one GPU: a rank's spinning phase barrier can wait for the other process's
     # kernels to be scheduled, so the device-side timeout is raised from 20 s (a timeout still fails)
-    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="on", MIHVD_XGMI_TIMEOUT_MS="60000")
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="on", MIHVD_XGMI_TIMEOUT_MS="60000",
+               MIHVD_TEST_PRECISION=prec, MIHVD_SHARD_W3="1" if prec == "fp32" else "0")
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -191,7 +198,7 @@ def test_bench_flow_trains_at_8_ranks(tmp_path, n, prec):
     (4, "fp32", "0", "off", "rs"), (8, "fp32", "0", "off", "rs"), (4, "fp32", "1", "off", "rs"),
     (8, "fp32", "1", "off", "rs"), (4, "fp32", "1", "off", "factor"), (8, "fp32", "1", "off", "factor"),
     (4, "bf16", "1", "off", "rs"), (8, "bf16", "1", "off", "rs"), (8, "bf16", "0", "off", "rs"),
-    (8, "bf16", "1", "on", "rs")])
+    (8, "bf16", "1", "on", "rs"), (4, "fp32", "1", "on", "rs"), (8, "fp32", "1", "on", "rs")])
 def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, shard, xgmi, f32plane):
     """N ranks x B=50 sharing this GPU over gloo: the reduced gradient of the first step equals the
     sum of the N single-process gradients (gradient rel < 1e-4), the update equals TF1 Adam on their
@@ -214,7 +221,7 @@ def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, shard, xgmi,
         assert o["losses"][-1] < o["losses"][0], o
         assert o["shard"] == (shard == "1"), o
         if prec == "fp32" and shard == "1":
-            assert o["plane"] == ("factor" if f32plane == "factor" else "rccl"), o
+            assert o["plane"] == ("xgmi" if xgmi == "on" else "factor" if f32plane == "factor" else "rccl"), o
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])

@@ -813,7 +813,7 @@ def test_roofline_f32_filters_startup_and_classifies(tmp_path):
     import subprocess
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    names = ["mihvd::f32_conv1_kernel(float const*)", "void mihvd::f32_conv2_fwd_kernel<5, false, false, false, 2, true>(x)",
+    names = ["mihvd::f32_conv1_kernel(float const*)", "void mihvd::f32_conv2_fwd8_kernel<5, true, 2>(x)",
              "void mihvd::f32_fc1_fwd2_kernel<7, false, false>(x)", "mihvd::f32_head_kernel(x)",
              "void mihvd::f32_fc1_bwd_rows_kernel<7, true, false, 2, false, 25>(x)",
              "void mihvd::f32_conv2_bwd_kernel<10, true, false, 2, true>(x)", "void mihvd::f32_conv_reduce_kernel<false>(x)"]

@@ -70,11 +70,13 @@ def sc_rccl_graph(outdir):
 def sc_dp_gloo(outdir):
     r = hvd.rank()
     X, Y = data(600)
-    tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="bf16")
-    assert tr.gather
+    prec = os.environ.get("MIHVD_TEST_PRECISION", "bf16")
+    tr = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision=prec,
+                           shard_optimizer=os.environ.get("MIHVD_SHARD_W3") == "1" if prec == "fp32" else None)
+    assert tr.gather or prec == "fp32"
     tr.keep_w3_grad = True  # gradients are compared below
     tr.broadcast(0)
-    ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="bf16", world_size=1)
+    ref = FusedMNISTTrainer(batch_size=100, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision=prec, world_size=1)
     ref.keep_w3_grad = True
     p0 = ref.params.clone()
     grel = None
@@ -86,7 +88,13 @@ def sc_dp_gloo(outdir):
         torch.cuda.synchronize()
         if step == 0:
             # allreduced SUM of the two per-rank batch means == 2 x the 100-sample batch mean
-            grel = ((tr.reduced_grads() / 2 - ref.grads).norm() / ref.grads.norm()).item()
+            red, want = tr.reduced_grads() / 2, ref.grads
+            if tr.f32 and tr.shard_w3:  # the sharded fp32 planes reduce this rank's dense/kernel rows only
+                R = tr._f32_R
+                rows = slice(FLAT_W3 + r * R * 1024, FLAT_W3 + (r + 1) * R * 1024)
+                red, want = torch.cat([red[:FLAT_W3], red[rows]]), torch.cat([want[:FLAT_W3], want[rows]])
+            grel = ((red - want).norm() / want.norm()).item()
+    tr.gather_full_state()
     rel = ((tr.params - ref.params).norm() / (ref.params - p0).norm()).item()
     mx = (tr.params - ref.params).abs().max().item()
     spread = hvd.allgather(tr.params[:4096].cpu().view(1, -1))
