@@ -535,6 +535,79 @@ __global__ void __launch_bounds__(256) f32_head_kernel(
   *reinterpret_cast<float4*>(dz_out + (int64_t)b * 1024 + n0) = make_float4(g[0], g[1], g[2], g[3]);
 }
 
+// head, one thread per feature: 1024 threads (16 waves) per sample. Every slab load is a coalesced
+// 256-byte wave access, the feature-side work is 1/4 of a thread's in the form above, and the
+// logits are 16 wave sums that meet in LDS in a fixed order (deterministic).
+__global__ void __launch_bounds__(1024) f32_head1k_kernel(
+    const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
+    const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
+    int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
+    float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B) {
+  __shared__ float red[16][10];
+  __shared__ float dl[10];
+  const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = __builtin_amdgcn_readfirstlane(n >> 6);
+  const int64_t step = state ? state[ST_FWD] : 0;
+  float parts[F1F_KS];
+#pragma unroll
+  for (int s = 0; s < F1F_KS; ++s) parts[s] = zpart[((int64_t)s * B + b) * 1024 + n];
+  float w[10];  // W4[n][0..9]: 40 bytes, 8-byte aligned
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const float2 v = reinterpret_cast<const float2*>(w4 + n * 10)[k];
+    w[2 * k] = v.x;
+    w[2 * k + 1] = v.y;
+  }
+  const float bias = b3[n];
+  int y = 0;
+  if (wave == 0) {
+    int row = b;
+    if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
+    y = (int)labels[row];
+  }
+  float z = bias;
+#pragma unroll
+  for (int s = 0; s < F1F_KS; ++s) z += parts[s];
+  const bool keep = thresh24 == 0 || dropout_keep(seed, (uint32_t)step, (uint32_t)(b * 1024 + n), thresh24);
+  const float hv = keep ? fmaxf(z, 0.f) * keep_scale : 0.f;
+  h_out[(int64_t)b * 1024 + n] = hv;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    const float sc = wave_sum(hv * w[c]);
+    if (lane == 0) red[wave][c] = sc;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const int c = min(lane, 9);
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) acc += red[q][c] + red[q + 1][c];
+    const float lgt = acc + b4[c];
+    const float v = lane < 10 ? lgt : -INFINITY;
+    const float mx = wave_max(v);
+    const float e = lane < 10 ? expf(lgt - mx) : 0.f;
+    const float se = wave_sum(e);
+    const float lse = mx + logf(se);
+    const unsigned long long ismax = __ballot(lane < 10 && lgt == mx);
+    const int am = __ffsll((long long)ismax) - 1;
+    const float ly = __shfl(lgt, y, 64);
+    if (lane < 10) {
+      const float d = (expf(lgt - lse) - (lane == y ? 1.f : 0.f)) / (float)B;
+      dl[lane] = d;
+      dlog_out[b * 10 + lane] = d;
+    }
+    if (lane == 0) {
+      stats[b * 2 + 0] = lse - ly;
+      stats[b * 2 + 1] = (am == y) ? 1.f : 0.f;
+      if (b == 0 && state != nullptr) state[ST_OPT] += 1;
+    }
+  }
+  __syncthreads();
+  float g = 0.f;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) g = fmaf(dl[c], w[c], g);
+  dz_out[(int64_t)b * 1024 + n] = hv > 0.f ? g * keep_scale : 0.f;
+}
+
 // ------------------------------------------------------------------------------------------ //
 // host wrappers
 // ------------------------------------------------------------------------------------------ //
@@ -693,10 +766,12 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   const uint32_t thresh = (uint32_t)(rate * 16777216.0);
   const float keep_scale = rate > 0.0 ? (float)(1.0 / (1.0 - rate)) : 1.f;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  f32_head_kernel<<<B, 256, 0, stream>>>(zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(),
-                                         b4.data_ptr<float>(), labels.data_ptr<int64_t>(), rp, n_pool, sp,
-                                         (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(), dz.data_ptr<float>(),
-                                         dlog.data_ptr<float>(), stats.data_ptr<float>(), B);
+  // MIHVD_F32_HEAD1K=0: the 256-thread form (4 features per thread)
+  auto kern = env_knob("MIHVD_F32_HEAD1K", 1) != 0 ? f32_head1k_kernel : f32_head_kernel;
+  kern<<<B, env_knob("MIHVD_F32_HEAD1K", 1) != 0 ? 1024 : 256, 0, stream>>>(
+      zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(), b4.data_ptr<float>(),
+      labels.data_ptr<int64_t>(), rp, n_pool, sp, (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(),
+      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B);
 }
 
 }  // namespace mihvd

@@ -97,6 +97,15 @@ int blocks_for(int64_t units) {
   return (int)g;
 }
 
+// Block count of a split-form data launch: one 16-byte unit per thread per pass, at most 4 blocks
+// per CU (grid-stride beyond).
+int data_blocks(const CollRole& r) {
+  const int64_t units = r.kind == COLL_GATHER ? (int64_t)r.R * (r.col_bytes / 16) : (r.n + 3) / 4;
+  int64_t g = (units + 255) / 256;
+  const int64_t cap = 4 * (int64_t)device_cu_count();
+  return (int)std::max<int64_t>(1, std::min(g, cap));
+}
+
 void check_phase(int64_t ph) { TORCH_CHECK(ph >= 0 && ph < kXgPhases, "xgmi: phase must be in [0, ", kXgPhases, ")"); }
 
 CollRole base_role(Ctx* c, int64_t ph) {
@@ -343,6 +352,12 @@ void xgmi_run_split(int64_t role_a, int64_t role_b, bool in_step, bool enter) {
     xgmi_enter_kernel<<<1, 64, 0, stream>>>(a, b, two ? 1 : 0);
     XGMI_HIP(hipGetLastError());
   }
+  // The data blocks never wait (the entry launch did), so they need not all be resident: up to
+  // four per CU (16 waves) keep enough loads in flight for a memory-bound sum + Adam, where the
+  // co-launch cap of one block per CU left 4 waves per CU each walking its units one round trip
+  // at a time.
+  a.nblk = data_blocks(a);
+  if (two) b.nblk = data_blocks(b);
   xgmi_data_kernel<<<a.nblk + (two ? b.nblk : 0), 256, 0, stream>>>(a, b, two ? 1 : 0);
   XGMI_HIP(hipGetLastError());
 }

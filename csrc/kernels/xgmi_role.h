@@ -198,6 +198,10 @@ __device__ __forceinline__ void xg_reduce(const CollRole& c, int bid, bool ok, u
   }
   const int64_t n4 = c.n >> 2;
   const int64_t nthreads = (int64_t)c.nblk * blockDim.x;
+  // p, m, v are loaded with the peers' gradients (one memory round trip per unit, not two: behind
+  // the `adam && ok` branch they were issued only once the sum was formed); without Adam their
+  // resources have no records and the loads return 0 without a memory access
+  const uint32_t pspan = c.adam ? span : 0u;
   for (int64_t i = (int64_t)bid * blockDim.x + threadIdx.x; i < n4; i += nthreads) {
     xg_u32x4 v[kXgMaxRanks];
 #pragma unroll
@@ -206,6 +210,9 @@ __device__ __forceinline__ void xg_reduce(const CollRole& c, int bid, bool ok, u
       v[p] = __builtin_amdgcn_raw_buffer_load_b128(xg_rsrc(c.pt.base[live ? p : c.rank] + off, span),
                                                    live ? (uint32_t)(i * 16) : kXgOob, 0, kXgAuxSys);
     }
+    const xg_u32x4 pq = __builtin_amdgcn_raw_buffer_load_b128(xg_rsrc((const char*)c.aa.p, pspan), (uint32_t)(i * 16), 0, 0);
+    const xg_u32x4 mq = __builtin_amdgcn_raw_buffer_load_b128(xg_rsrc((const char*)c.aa.m, pspan), (uint32_t)(i * 16), 0, 0);
+    const xg_u32x4 vq = __builtin_amdgcn_raw_buffer_load_b128(xg_rsrc((const char*)c.aa.v, pspan), (uint32_t)(i * 16), 0, 0);
     float4 a = make_float4(__uint_as_float(v[0].x), __uint_as_float(v[0].y), __uint_as_float(v[0].z),
                            __uint_as_float(v[0].w));
 #pragma unroll
@@ -220,7 +227,9 @@ __device__ __forceinline__ void xg_reduce(const CollRole& c, int bid, bool ok, u
     if (!ok) a = make_float4(nan, nan, nan, nan);
     if (c.out) ((float4*)c.out)[i] = a;
     if (c.adam && ok) {  // poisoned: the parameters keep their last good values (no NaN update)
-      float4 pp = ((const float4*)c.aa.p)[i], mm = ((const float4*)c.aa.m)[i], vv = ((const float4*)c.aa.v)[i];
+      float4 pp = make_float4(__uint_as_float(pq.x), __uint_as_float(pq.y), __uint_as_float(pq.z), __uint_as_float(pq.w));
+      float4 mm = make_float4(__uint_as_float(mq.x), __uint_as_float(mq.y), __uint_as_float(mq.z), __uint_as_float(mq.w));
+      float4 vv = make_float4(__uint_as_float(vq.x), __uint_as_float(vq.y), __uint_as_float(vq.z), __uint_as_float(vq.w));
       const uint2 sh = adam4(pp, mm, vv, a, ac);
       ((float4*)c.aa.p)[i] = pp;
       ((float4*)c.aa.m)[i] = mm;

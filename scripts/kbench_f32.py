@@ -189,6 +189,7 @@ def main():
         "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
         "fc1_fwd [a2 staged in two K halves]": ({"MIHVD_F32_F1F_SPLIT": "1"}, ks["fc1_fwd"]),
+        "head [256 threads, 4 features each]": ({"MIHVD_F32_HEAD1K": "0"}, ks["head"]),
 
     }
     for name, (env, fn) in study.items():
@@ -217,6 +218,7 @@ def main():
         "whole step [fc1_bwd pinned dgrad MFMA order]": ({}, {"MIHVD_F32_F1R_PIN": "1"}),
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
+        "whole step [256-thread head]": ({}, {"MIHVD_F32_HEAD1K": "0"}),
     }
     for name, (attrs, env) in steps.items():
         if not want(name):

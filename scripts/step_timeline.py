@@ -14,7 +14,7 @@ import statistics
 
 
 def short(n):
-    n = n.split("(")[0].replace("void ", "").replace("mihvd::", "")
+    n = n.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("mihvd::", "")
     return n[:60]
 
 

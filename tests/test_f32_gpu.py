@@ -110,6 +110,13 @@ def test_f32_fc1_fwd_and_head(ops, B, monkeypatch):
     assert abs(stats[:, 0].mean().item() - loss.item()) < 1e-5
     assert rel_err(dz, zr.grad) < 1e-5
     assert rel_err(dlog, torch.softmax(logits, 1).sub(F.one_hot(y, 10).float()).div(B)) < 1e-5
+    # the 256-thread head (MIHVD_F32_HEAD1K=0): same features and mask, logits summed in another order
+    monkeypatch.setenv("MIHVD_F32_HEAD1K", "0")
+    h0, dz0, dlog0, stats0 = (torch.full_like(t, float("nan")) for t in (h, dz, dlog, stats))
+    ops.f32_head_fwd_bwd(zpart, b3, w4, b4, y, None, None, 0, 0.0, h0, dz0, dlog0, stats0)
+    monkeypatch.delenv("MIHVD_F32_HEAD1K")
+    assert torch.equal(h0, h)
+    assert rel_err(dz0, dz) < 1e-6 and rel_err(dlog0, dlog) < 1e-6 and rel_err(stats0, stats) < 1e-6
 
 
 @pytest.mark.parametrize("B", [7, 100])
