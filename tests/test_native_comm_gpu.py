@@ -66,6 +66,31 @@ def test_native_engine_one_gpu(tmp_path):
     assert r["stats"]["cycles"] > 0 and r["stopped"], r
 
 
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_native_engine_ranks_out_of_order(tmp_path, nranks):
+    """The C++ engine across GPUs (one rank per GPU; RCCL refuses two ranks on one device): the
+    same 80 names enqueued in a different order on every rank (more than one 64-signature announce
+    round), big tensors above the fusion threshold in rank-dependent order, then the same names
+    again from the signature cache; every result equals the closed-form sum, and every rank stops
+    cleanly. Needs ``nranks`` GPUs: skipped on a one-GPU box."""
+    import torch
+
+    if torch.cuda.device_count() < nranks:
+        pytest.skip(f"needs {nranks} GPUs (RCCL runs one rank per device)")
+    out = tmp_path / "eng"
+    env = dict(os.environ, PYTHONPATH=ROOT, MIHVD_ENGINE="native", MIHVD_FUSION_THRESHOLD=str(1 << 20))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
+           "--master-addr", "127.0.0.1", "--master-port", "29567",
+           os.path.join(ROOT, "tests", "workers", "native_engine_multi_worker.py"), str(out)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(nranks):
+        res = json.loads((tmp_path / f"eng.{r}").read_text())
+        assert res["world"] == nranks and res["ok"] == [True, True] and res["stopped"], res
+
+
 def test_bucket_plane_carries_distributed_optimizer(tmp_path):
     """DistributedOptimizer's buckets go through the framework-owned RCCL bucket plane
     (collectives.BucketPlane: NativeComm on a high-priority side stream), eagerly and inside a
