@@ -51,12 +51,9 @@ def test_f32_conv1_fwd(ops, B):
 
 
 @pytest.mark.parametrize("B", [7, 100, 128])
-@pytest.mark.parametrize("early", ["1", "0"])
-def test_f32_conv2_fwd(ops, B, early, monkeypatch):
+def test_f32_conv2_fwd(ops, B):
     """The two waves of a SIMD split the input channels (their partials meet in LDS); HWIO and
-    fragment-copy W2 reads give the same bits, with the fragment loads issued before the staging
-    barrier (default) or after it (MIHVD_F32_C2F_EARLY=0)."""
-    monkeypatch.setenv("MIHVD_F32_C2F_EARLY", early)
+    fragment-copy W2 reads give the same bits."""
     g = torch.Generator(device="cuda").manual_seed(2)
     a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
     w = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
