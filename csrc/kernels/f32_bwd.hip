@@ -527,7 +527,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
     float* __restrict__ db2p, float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4,
-    float* __restrict__ gb4, int B, F32Adam ad) {
+    float* __restrict__ gb4, int B, F32Adam ad, int pf) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   if (bid >= F1R_BLOCKS) {
@@ -542,6 +542,16 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * bid, nb = 128 * wave;
   f1r_stamp(0);
+  // pf: the routing epilogue's a2 / idx2 operands (they depend on the block alone) loaded at the
+  // start, so the epilogue after the exchange does not begin with a dependent global round trip
+  const int jt = bid >> 2, co_e = 16 * (bid & 3) + 4 * (lane >> 4), j_e = 64 * jt + co_e;
+  const int m_e = 16 * (t >> 6) + (lane & 15), mc_e = min(m_e, B - 1);
+  float4 av_e = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t ix_e = 0u;
+  if (pf && t < G * 64) {
+    av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
+    ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
+  }
   float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
   // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch)
   float a2r[KS];
@@ -653,17 +663,21 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
 #pragma unroll
   for (int u = 0; u < G; ++u) red[(wave * 8 + u) * 64 + lane] = make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
   __syncthreads();
-  const int jt = bid >> 2, py = jt / 7, px = jt - 7 * py;
+  const int py = jt / 7, px = jt - 7 * py;
   if (t < G * 64) {  // wave u handles tile u
-    const int u = t >> 6, ln = lane, r = ln & 15, q = ln >> 4;
+    const int u = t >> 6, ln = lane, r = ln & 15;
+    if (!pf) {
+      av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
+      ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
+    }
     float4 s = red[(0 * 8 + u) * 64 + ln];
 #pragma unroll
     for (int w = 1; w < 8; ++w) s = f4add(s, red[(w * 8 + u) * 64 + ln]);
     const float sv[4] = {s.x, s.y, s.z, s.w};
-    const int m = 16 * u + r, mc = min(m, B - 1), co = 16 * (bid & 3) + 4 * q, j = 64 * jt + co;
+    const int m = m_e, co = co_e;
     const bool valid = m < B;
-    const float4 av = *reinterpret_cast<const float4*>(a2 + (int64_t)mc * 3136 + j);
-    const uint32_t ix = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc * 3136 + j);
+    const float4 av = av_e;
+    const uint32_t ix = ix_e;
     const float ae[4] = {av.x, av.y, av.z, av.w};
     float gq[4];
 #pragma unroll
@@ -1515,7 +1529,8 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
       kern<<<F1R_BLOCKS + F1B_SMALL, 512, F1R_LDS, stream>>>(
           dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
           dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
-          gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad);
+          gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad,
+          env_knob("MIHVD_F32_F1R_PF", 0));
     };
     // MIHVD_F32_F1R_PD=4: p/m/v prefetched 4 chunks ahead instead of 2 (measured no faster:
     // 28.2 vs 27.8 us, profiles/r04/kbench_f32_r04e.txt; the loop is not bound by HBM bytes in flight)

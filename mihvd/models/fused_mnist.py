@@ -934,24 +934,25 @@ class FusedMNISTTrainer:
         if self._roles is None or self._roles["lr"] != self.lr:
             self._prepare_roles()
         R = self._roles
+        co = self.xplane.colaunch  # the role id for the op, or run split-form first (shared GPU)
         b1, b2 = self.betas
         w2 = self.pview("conv_layer2/conv2d/kernel", self.shadow)
         o.conv12_fwd(x, rows, st, self.pview("conv_layer1/conv2d/kernel", self.shadow),
                      self.pview("conv_layer1/conv2d/bias"), w2, self.pview("conv_layer2/conv2d/bias"), self.a1, self.idx1,
-                     self.a2, self.idx2, R["w3"] if self.shard_w3 else R["fence"])
+                     self.a2, self.idx2, co(R["w3"] if self.shard_w3 else R["fence"]))
         o.fc1_fwd(self.a2, self.w3_shadow(), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
                        labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
         gW3 = self.gview("dense/kernel")
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
                  self.gview("dense_1/bias"))
-        o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2, R["dz"])
-        self._conv_backward(x, rows, st, R["a2_shard"] if self.shard_w3 else R["a2_full"])
+        o.fc1_bwd(self.dz, self.a2, self.h, self.dlog, self.w3_shadow(), *small[4:], self.g2, 2, co(R["dz"]))
+        self._conv_backward(x, rows, st, co(R["a2_shard"] if self.shard_w3 else R["a2_full"]))
         lo, hi = self._w3_tiles
         w3 = slice(W3_START, FLAT_NUMEL)
         o.fc1_wgrad_adam(*small, 1, self.dz_all, self.a2_all, self.params[w3], self.m[w3], self.v[w3],
                          self.shadow3[:3136].view(-1), st, self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule,
-                         self.keep_w3_grad, lo, hi, R["small"])
+                         self.keep_w3_grad, lo, hi, co(R["small"]))
         if self.shard_w3:
             self._full_state_valid = False
 

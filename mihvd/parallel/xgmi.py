@@ -117,6 +117,14 @@ class XGMIRegion:
                 self.ctx = None
             raise XGMIUnavailable(f"IPC setup failed on at least one rank ({err!r})")
         dist.barrier(group=group)  # every peer opened every region before the first signal
+        # Ranks sharing one GPU (the one-GPU multi-rank tests): a collective whose blocks spin in the
+        # phase barrier can then hold the CUs a peer's kernel needs to reach that barrier, so every
+        # collective runs in the split form (one waiting block per rank, xgmi_role.h) instead of
+        # co-launched or standalone with all its blocks waiting.
+        props = torch.cuda.get_device_properties(self.device)
+        keys = [None] * self.world
+        dist.all_gather_object(keys, (props.pci_domain_id, props.pci_bus_id, props.pci_device_id), group=group)
+        self.shared_device = len(set(keys)) < self.world
         self._views = {}
         self._closed = False
 
@@ -182,8 +190,21 @@ class XGMIRegion:
 
     def run(self, role: int, in_step: bool = False):
         """Launch a prepared collective on its own (current stream). ``in_step``: a launch of the
-        training step (keeps MIHVD_XGMI_DEBUG_STALE's injected stale reads)."""
-        self._o.xgmi_run(role, bool(in_step))
+        training step (keeps MIHVD_XGMI_DEBUG_STALE's injected stale reads). On a shared device:
+        the split form."""
+        if self.shared_device:
+            self._o.xgmi_run_split(role, -1, bool(in_step), True)
+        else:
+            self._o.xgmi_run(role, bool(in_step))
+
+    def colaunch(self, role: int, in_step: bool = True) -> int:
+        """The id to hand a compute op for co-launching ``role``; on a shared device the role runs
+        here, split form, before that op (same stream, so it still follows every earlier launch and
+        precedes every later reader), and the op gets -1."""
+        if role < 0 or not self.shared_device:
+            return role
+        self._o.xgmi_run_split(role, -1, bool(in_step), True)
+        return -1
 
     def run_split(self, role_a: int, role_b: int = -1, in_step: bool = False, enter: bool = True):
         """One or two prepared collectives (different phases) as a dedicated launch pair on the

@@ -190,6 +190,7 @@ def main():
         "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
         "fc1_fwd [a2 staged in two K halves]": ({"MIHVD_F32_F1F_SPLIT": "1"}, ks["fc1_fwd"]),
         "head [256 threads, 4 features each]": ({"MIHVD_F32_HEAD1K": "0"}, ks["head"]),
+        "fc1_bwd+W3 adam [routing operands loaded at the start]": ({"MIHVD_F32_F1R_PF": "1"}, ks["fc1_bwd+W3 adam"]),
 
     }
     for name, (env, fn) in study.items():
@@ -219,6 +220,7 @@ def main():
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
         "whole step [256-thread head]": ({}, {"MIHVD_F32_HEAD1K": "0"}),
+        "whole step [fc1_bwd routing operands loaded at the start]": ({}, {"MIHVD_F32_F1R_PF": "1"}),
     }
     for name, (attrs, env) in steps.items():
         if not want(name):
