@@ -55,361 +55,10 @@ __device__ __forceinline__ void c2b_stamp_wave() {
 // ------------------------------------------------------------------------------------------ //
 // f32_fc1_bwd
 // ------------------------------------------------------------------------------------------ //
-constexpr int F1B_DS = 1028;                       // dz image row stride (floats)
-constexpr int F1B_LDS_DG = 16 * F1B_DS * 4;        // 65,792 B
-constexpr int F1B_LDS_WG = 2 * F32_MAXB * 64 * 4;  // 65,536 B
-constexpr int F1B_LDS = F1B_LDS_DG > F1B_LDS_WG ? F1B_LDS_DG : F1B_LDS_WG;
-constexpr int F1B_SMALL = 33, F1B_WGRAD = 784;
-
-// dgrad block: one pooling window jt (= 64 consecutive features j of the NHWC flatten) x 16 samples,
-// full K = 1024. Both operands are K-contiguous: A = this wave's 16 rows of W3 (float4 chunks
-// streamed from global, 8 chunks in flight), B = the block's dz rows from LDS. Block ids are
-// XCD-interleaved (xcd = bid & 7) so the sample groups of one window share an XCD L2 for W3.
-__device__ __forceinline__ void f32_fc1_dgrad_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
-                                                    const uint8_t* __restrict__ idx2, const float* __restrict__ w3,
-                                                    float* __restrict__ dY2, float* __restrict__ db2p, int B, int G,
-                                                    float* smf) {
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
-  const int xcd = bid & 7, slot = bid >> 3, mg = slot % G, jt = (slot / G) * 8 + xcd;
-  if (jt >= 49) return;
-  const int m0 = 16 * mg;
-  float* Ds = smf;  // [16][1028]
-  float4 dv[16];
-#pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int i = t + 256 * it, r = i >> 8, c = i & 255, m = m0 + r;
-    dv[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)min(m, B - 1) * 1024 + 4 * c), m < B);
-  }
-  // W3 streams from HBM / L2 in 8 chunks of 128 k (8 float4 per lane each) through a 4-deep
-  // register ring: three chunks (24 loads per lane) stay in flight ahead of the MFMAs
-  const float* wr = w3 + (int64_t)(64 * jt + 16 * wave + lr) * 1024 + 4 * lg;
-  float4 wv[4][8];
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) wv[c][u] = *reinterpret_cast<const float4*>(wr + 16 * (8 * c + u));
-#pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int i = t + 256 * it;
-    *reinterpret_cast<float4*>(Ds + (i >> 8) * F1B_DS + 4 * (i & 255)) = dv[it];
-  }
-  __syncthreads();
-  f32x4 accq[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
-                  f32x4{0.f, 0.f, 0.f, 0.f}};
-  const float* dp = Ds + lr * F1B_DS + 4 * lg;
-#pragma unroll
-  for (int c8 = 0; c8 < 8; ++c8) {
-    if (c8 + 3 < 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) wv[(c8 + 3) & 3][u] = *reinterpret_cast<const float4*>(wr + 16 * (8 * (c8 + 3) + u));
-    }
-    float4 bq[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) bq[u] = *reinterpret_cast<const float4*>(dp + 16 * (8 * c8 + u));
-    // four accumulators, k-element outer: no two consecutive MFMAs share one
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].x, bq[4 * h + u].x, accq[u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].y, bq[4 * h + u].y, accq[u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].z, bq[4 * h + u].z, accq[u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) accq[u] = mfma4(wv[c8 & 3][4 * h + u].w, bq[4 * h + u].w, accq[u]);
-    }
-  }
-  const f32x4 acc0 = accq[0] + accq[2], acc1 = accq[1] + accq[3];
-  // C[row 4lg + i][col lr] = channel co + i of window jt, sample m0 + lr
-  const f32x4 acc = acc0 + acc1;
-  const int m = m0 + lr, mc = min(m, B - 1), co = 16 * wave + 4 * lg, j = 64 * jt + co;
-  const bool valid = m < B;
-  const float4 av = *reinterpret_cast<const float4*>(a2 + (int64_t)mc * 3136 + j);
-  const uint32_t ix = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc * 3136 + j);
-  const float ae[4] = {av.x, av.y, av.z, av.w};
-  float g[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) g[i] = (valid && ae[i] > 0.f) ? acc[i] : 0.f;
-  float s[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) s[i] = row_sum16(g[i]);  // over the 16 samples of the block
-  if (lr == 0)
-    *reinterpret_cast<float4*>(db2p + ((int64_t)mg * 49 + jt) * 64 + co) = make_float4(s[0], s[1], s[2], s[3]);
-  if (valid) {
-    const int py = jt / 7, px = jt - 7 * py;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      float o[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = (int)((ix >> (8 * i)) & 0xff) == d ? g[i] : 0.f;
-      const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
-      *reinterpret_cast<float4*>(dY2 + (((int64_t)m * 14 + y) * 14 + x) * 64 + co) = make_float4(o[0], o[1], o[2], o[3]);
-    }
-  }
-}
-
-// dgrad block, K-split form (default): 16 features f0..f0+15 (window jt = bid >> 2, channels
-// 16 (bid & 3) ..) x every 16-sample tile of the batch (G <= 8) x the full K, one K quarter per
-// wave (wave w: k in [256 w, 256 w + 256)). Each W3 fragment a wave loads serves all G sample
-// tiles (G independent accumulators: no dependent MFMA pair closer than G issues), so W3 is read
-// once and the MFMA pipe, not the operand fetch, sets the pace; 196 blocks x 4 waves of 16 G
-// MFMAs per 16-deep chunk. Operands stream from L2 through a 4-deep register ring (3 chunks in
-// flight). The quarters meet in LDS and are summed in a fixed order (deterministic).
-constexpr int F1B_DG2 = 196;
-template <int G>
-__device__ __forceinline__ void f32_fc1_dgrad_ks_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
-                                                       const uint8_t* __restrict__ idx2, const float* __restrict__ w3,
-                                                       float* __restrict__ dY2, float* __restrict__ db2p, int B,
-                                                       float* smf) {
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
-  const int f0 = 16 * bid, kb = 256 * wave;
-  const float* wr = w3 + (int64_t)(f0 + lr) * 1024 + kb + 4 * lg;
-  const float* zr[G];
-#pragma unroll
-  for (int u = 0; u < G; ++u) zr[u] = dz + (int64_t)min(16 * u + lr, B - 1) * 1024 + kb + 4 * lg;
-  // sample columns >= B read row B - 1 and are never stored (MFMA columns are independent)
-  constexpr int NC = 16, D = 4;
-  float4 wv[D], zv[D][G];
-#pragma unroll
-  for (int c = 0; c < D - 1; ++c) {
-    wv[c] = *reinterpret_cast<const float4*>(wr + 16 * c);
-#pragma unroll
-    for (int u = 0; u < G; ++u)
-      zv[c][u] = *reinterpret_cast<const float4*>(zr[u] + 16 * c);
-  }
-  f32x4 acc[G];
-#pragma unroll
-  for (int u = 0; u < G; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // fully unrolled; sched_barrier pins the order [loads of chunk c + 3] [MFMAs of chunk c, element
-  // by element, tile-inner] so the scheduler neither hoists every chunk's loads (register blow-up)
-  // nor sinks them next to their use (exposed latency), and no two consecutive MFMAs share an
-  // accumulator
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (c + D - 1 < NC) {
-      const int s = (c + D - 1) % D, cn = c + D - 1;
-      wv[s] = *reinterpret_cast<const float4*>(wr + 16 * cn);
-#pragma unroll
-      for (int u = 0; u < G; ++u) zv[s][u] = *reinterpret_cast<const float4*>(zr[u] + 16 * cn);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int s = c % D;
-#pragma unroll
-    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].x, zv[s][u].x, acc[u]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].y, zv[s][u].y, acc[u]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].z, zv[s][u].z, acc[u]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < G; ++u) acc[u] = mfma4(wv[s].w, zv[s][u].w, acc[u]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  // C[row 4 lg + i][col lr] of tile u = channel 4 lg + i of this block's 16, sample 16 u + lr
-  float4* red = reinterpret_cast<float4*>(smf);  // [4 waves][8 tiles][64 lanes]
-#pragma unroll
-  for (int u = 0; u < G; ++u)
-    red[(wave * 8 + u) * 64 + lane] = make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
-  __syncthreads();
-  const int jt = bid >> 2, py = jt / 7, px = jt - 7 * py;
-  for (int i = t; i < G * 64; i += 256) {  // wave-uniform trip count: i >> 6 is one tile per wave
-    const int u = i >> 6, ln = i & 63, r = ln & 15, q = ln >> 4;
-    const float4 s0 = red[(0 * 8 + u) * 64 + ln], s1 = red[(1 * 8 + u) * 64 + ln];
-    const float4 s2 = red[(2 * 8 + u) * 64 + ln], s3 = red[(3 * 8 + u) * 64 + ln];
-    const float sv[4] = {(s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y), (s0.z + s1.z) + (s2.z + s3.z),
-                         (s0.w + s1.w) + (s2.w + s3.w)};
-    const int m = 16 * u + r, mc = min(m, B - 1), co = 16 * (bid & 3) + 4 * q, j = 64 * jt + co;
-    const bool valid = m < B;
-    const float4 av = *reinterpret_cast<const float4*>(a2 + (int64_t)mc * 3136 + j);
-    const uint32_t ix = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc * 3136 + j);
-    const float ae[4] = {av.x, av.y, av.z, av.w};
-    float g[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) g[e] = (valid && ae[e] > 0.f) ? sv[e] : 0.f;
-    float sm[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) sm[e] = row_sum16(g[e]);  // over the 16 samples of tile u
-    if (r == 0)
-      *reinterpret_cast<float4*>(db2p + ((int64_t)u * 49 + jt) * 64 + co) = make_float4(sm[0], sm[1], sm[2], sm[3]);
-    if (valid) {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (int)((ix >> (8 * e)) & 0xff) == d ? g[e] : 0.f;
-        const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
-        *reinterpret_cast<float4*>(dY2 + (((int64_t)m * 14 + y) * 14 + x) * 64 + co) = make_float4(o[0], o[1], o[2], o[3]);
-      }
-    }
-  }
-}
-
-// Small reductions over the batch: db3 (16 blocks of 64 features), dW4 (16 blocks), db4 (1 block).
-__device__ __forceinline__ void f32_fc1_small_block(int bid, const float* __restrict__ dz, const float* __restrict__ h,
-                                                    const float* __restrict__ dlog, float* __restrict__ gb3,
-                                                    float* __restrict__ gW4, float* __restrict__ gb4, int B, float* smf) {
-  const int t = threadIdx.x, nn = t & 63, rg = t >> 6;
-  if (bid < 16) {
-    const int n = bid * 64 + nn;
-    float v[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const int b = rg * 32 + i;
-      v[i] = mask_f(dz[(int64_t)min(b, B - 1) * 1024 + n], b < B);
-    }
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) s += v[i];
-    smf[rg * 64 + nn] = s;
-    __syncthreads();
-    if (t < 64) gb3[n] = (smf[nn] + smf[64 + nn]) + (smf[128 + nn] + smf[192 + nn]);
-    return;
-  }
-  if (bid < 32) {
-    const int r = bid - 16, n = r * 64 + nn;
-    float* dls = smf;                // [128][10]
-    float* red = smf + F32_MAXB * 10;  // [4][64][10]
-    float hv[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const int b = rg * 32 + i;
-      hv[i] = mask_f(h[(int64_t)min(b, B - 1) * 1024 + n], b < B);
-    }
-    for (int i = t; i < F32_MAXB * 10; i += 256) dls[i] = i < B * 10 ? dlog[i] : 0.f;
-    __syncthreads();
-    float s[10];
-#pragma unroll
-    for (int c = 0; c < 10; ++c) s[c] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i)
-#pragma unroll
-      for (int c = 0; c < 10; ++c) s[c] = fmaf(hv[i], dls[(rg * 32 + i) * 10 + c], s[c]);
-#pragma unroll
-    for (int c = 0; c < 10; ++c) red[(rg * 64 + nn) * 10 + c] = s[c];
-    __syncthreads();
-    for (int i = t; i < 640; i += 256) {
-      const int n2 = i / 10, c = i - n2 * 10;
-      gW4[(r * 64 + n2) * 10 + c] =
-          (red[n2 * 10 + c] + red[(64 + n2) * 10 + c]) + (red[(128 + n2) * 10 + c] + red[(192 + n2) * 10 + c]);
-    }
-    return;
-  }
-  // db4: thread = (class c, row group of 6)
-  const int c = t % 10, gq = t / 10;
-  float s = 0.f;
-  if (gq < 25) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int b = gq * 6 + i;
-      s += mask_f(dlog[min(b, B - 1) * 10 + c], b < B);
-    }
-  }
-  smf[t] = s;
-  __syncthreads();
-  if (t < 10) {
-    float tot = 0.f;
-    for (int q = 0; q < 25; ++q) tot += smf[q * 10 + t];
-    gb4[t] = tot;
-  }
-}
-
-// wgrad block: the 64x64 tile (jt, ntile) of dW3 = a2^T dz over K = the batch. Both operands are
-// K-strided (sample rows), so the tile runs on v_mfma_f32_32x32x2_f32, whose A and B lanes 0-31 /
-// 32-63 read 32 consecutive floats of one sample row each (ds_read_b32, conflict-free without
-// padding). 4 waves x one 32x32 sub-tile; output features n on the MFMA row axis so a lane's four
-// consecutive accumulator rows are one float4 of a dW3 row.
-// G > 0: K padded to the 16 G rows of whole sample tiles (zero rows) and the MFMA chain fully
-// unrolled, so the LDS operand reads run ahead of the dependent MFMAs (the runtime-length loop
-// waited on every ds_read pair before its MFMA).
-template <int G>
-__device__ __forceinline__ void f32_fc1_wgrad_block(int bid, const float* __restrict__ dz, const float* __restrict__ a2,
-                                                    float* __restrict__ gW3, int B, float* smf) {
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int jt = bid >> 4, ntile = bid & 15, j0 = 64 * jt, n0 = 64 * ntile;
-  float* A2s = smf;                   // [128][64] rows b, cols j
-  float* DZs = smf + F32_MAXB * 64;   // [128][64] rows b, cols n
-  const int Kp = G > 0 ? 16 * G : (B + 1) & ~1, nchk = Kp * 16;
-  float4 va[8], vz[8];
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int i = min(t + 256 * it, nchk - 1), r = i >> 4, c = i & 15, rc = min(r, B - 1);
-    va[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)rc * 3136 + j0 + 4 * c), r < B);
-    vz[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)rc * 1024 + n0 + 4 * c), r < B);
-  }
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int i = t + 256 * it;
-    if (i < nchk) {
-      *reinterpret_cast<float4*>(A2s + 4 * i) = va[it];
-      *reinterpret_cast<float4*>(DZs + 4 * i) = vz[it];
-    }
-  }
-  __syncthreads();
-  const int wn = wave & 1, wj = wave >> 1, l32 = lane & 31, hh = lane >> 5;
-  const float* ap = DZs + hh * 64 + 32 * wn + l32;  // A[n][k] = dz[k][n]
-  const float* bp = A2s + hh * 64 + 32 * wj + l32;  // B[k][j] = a2[k][j]
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  if constexpr (G > 0) {
-    // operand reads run 6 steps ahead of the MFMA that uses them (ring of 8 register pairs)
-    constexpr int NS = 8 * G, R = 8, AH = 6;
-    float ar[R], br[R];
-#pragma unroll
-    for (int s = 0; s < AH; ++s) {
-      ar[s] = ap[s * 128];
-      br[s] = bp[s * 128];
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (s + AH < NS) {
-        ar[(s + AH) % R] = ap[(s + AH) * 128];
-        br[(s + AH) % R] = bp[(s + AH) * 128];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      acc = mfma32(ar[s % R], br[s % R], acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-    const int ns = Kp >> 1;
-#pragma unroll 8
-    for (int s = 0; s < ns; ++s) acc = mfma32(ap[s * 128], bp[s * 128], acc);
-  }
-  const int j = j0 + 32 * wj + l32;
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-    *reinterpret_cast<float4*>(gW3 + (int64_t)j * 1024 + n0 + 32 * wn + 8 * g + 4 * hh) =
-        make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
-}
-
-// GT: 0 = the earlier dgrad form, 1..8 = the K-split form for G = GT sample tiles
-template <int GT>
-__global__ void __launch_bounds__(256) f32_fc1_bwd_kernel(
-    const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
-    const float* __restrict__ h, const float* __restrict__ dlog, const float* __restrict__ w3, float* __restrict__ dY2,
-    float* __restrict__ db2p, float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4,
-    float* __restrict__ gb4, int B, int G, int n_dg) {
-  extern __shared__ __attribute__((aligned(16))) float smf[];
-  int bid = blockIdx.x;
-  if (bid < n_dg) {
-    if constexpr (GT > 0)
-      f32_fc1_dgrad_ks_block<GT>(bid, dz, a2, idx2, w3, dY2, db2p, B, smf);
-    else
-      f32_fc1_dgrad_block(bid, dz, a2, idx2, w3, dY2, db2p, B, G, smf);
-    return;
-  }
-  bid -= n_dg;
-  if (bid < F1B_SMALL) {
-    f32_fc1_small_block(bid, dz, h, dlog, gb3, gW4, gb4, B, smf);
-    return;
-  }
-  f32_fc1_wgrad_block<GT>(bid - F1B_SMALL, dz, a2, gW3, B, smf);
-}
+constexpr int F1B_SMALL = 33;  // blocks of the small reductions (db3, dW4, db4) behind the row blocks
 
 // ------------------------------------------------------------------------------------------ //
-// f32_fc1_bwd, row form (default): one block per 16 rows of W3 (= 16 channels of one pooling
+// f32_fc1_bwd, row form: one block per 16 rows of W3 (= 16 channels of one pooling
 // window), 8 waves; wave w owns the 128 columns n in [128 w, 128 w + 128) of those rows, in 8
 // chunks of 16. Per chunk the wave holds p = W3[f0 + lr][n .. n + 3] (4 consecutive columns per
 // lane: lane group lg -> n = nn + 4 lg) and uses it twice:
@@ -513,16 +162,13 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
   }
 }
 
-// PD: how many chunks ahead p/m/v are loaded (ring of PD + 1 register slots). The loop's HBM
-// traffic (p, m, v in; p, m, v out: 75 MB per step) is bound by the bytes each CU keeps in flight;
-// PD = 2 keeps ~48 KB per CU, PD = 4 ~96 KB.
-// PIN: the dgrad MFMAs of a chunk issue in the written order (k-element outer, tiles inner: dependent
-// MFMAs G issues apart), pinned by sched_barrier after their operand reads; left alone the scheduler
-// chains each tile's four k-steps back to back.
+// p/m/v are loaded two chunks ahead (PD, a ring of three register slots; four ahead measured no
+// faster: 28.2 vs 27.8 us, profiles/r04/kbench_f32_r04e.txt). Pinning the dgrad MFMA order with
+// sched_barrier measured slower (+2 us, r04).
 // KW: K steps of the wgrad chain, 4 samples each: 4 G (the padded tiles) by default, ceil(B / 4) in
 // the exact-batch instantiation (B = 100: 25 instead of 28 MFMAs per chunk; the rows past the
 // batch are zero either way).
-template <int G, bool ADAM, bool STORE, int PD = 2, bool PIN = false, int KW = 4 * G>
+template <int G, bool ADAM, bool STORE, int KW = 4 * G>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
@@ -535,6 +181,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     return;
   }
   constexpr int KS = KW;  // K steps of the wgrad chain
+  constexpr int PD = 2;
   // dgrad only (neither the fused Adam nor the stored gradient: the fp32 factor-gather plane forms
   // dW3 from every rank's factors elsewhere): no a2 operand, no wgrad MFMAs, W3 read once
   constexpr bool WG = ADAM || STORE;
@@ -542,8 +189,8 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * bid, nb = 128 * wave;
   f1r_stamp(0);
-  // pf: the routing epilogue's a2 / idx2 operands (they depend on the block alone) loaded at the
-  // start, so the epilogue after the exchange does not begin with a dependent global round trip
+  // pf (default): the routing epilogue's a2 / idx2 operands (they depend on the block alone) loaded
+  // at the start, so the epilogue after the exchange does not begin with a dependent global round trip
   const int jt = bid >> 2, co_e = 16 * (bid & 3) + 4 * (lane >> 4), j_e = 64 * jt + co_e;
   const int m_e = 16 * (t >> 6) + (lane & 15), mc_e = min(m_e, B - 1);
   float4 av_e = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -615,7 +262,6 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     float4 zb[G];
 #pragma unroll
     for (int u = 0; u < G; ++u) zb[u] = *reinterpret_cast<const float4*>(buf + (16 * u + lr) * 16 + 4 * (lg ^ f1r_swz(lr)));
-    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.x, zb[u].x, acc[u]);
 #pragma unroll
@@ -624,7 +270,6 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.z, zb[u].z, acc[u]);
 #pragma unroll
     for (int u = 0; u < G; ++u) acc[u] = mfma4(p.w, zb[u].w, acc[u]);
-    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
     // wgrad: dW3[f0 + lr][nn + 4 lg + i] over the batch, two alternating accumulators. (Reading every
     // LDS operand of the chunk ahead of its MFMAs with the order pinned by sched_barrier, and four
     // wgrad chains, was measured slower: 33.6 vs 27.7 us with the fused Adam, 27.5 vs 22.9 without,
@@ -1521,90 +1166,54 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   const bool dgrad_only = !adam && !store_w3;
   const int G = (B + 15) / 16;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  // Row form (default): dgrad + dW3 (+ the fused dense/kernel Adam) from one read of W3.
-  // MIHVD_F32_F1B=0: the earlier three-role launch (window dgrad, separate dW3 tiles; no fused Adam).
-  if (env_knob("MIHVD_F32_F1B", 1) != 0 || adam || dgrad_only) {
-    auto launch = [&](auto kern) {
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1R_LDS);
-      kern<<<F1R_BLOCKS + F1B_SMALL, 512, F1R_LDS, stream>>>(
-          dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
-          dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
-          gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad,
-          env_knob("MIHVD_F32_F1R_PF", 0));
-    };
-    // MIHVD_F32_F1R_PD=4: p/m/v prefetched 4 chunks ahead instead of 2 (measured no faster:
-    // 28.2 vs 27.8 us, profiles/r04/kbench_f32_r04e.txt; the loop is not bound by HBM bytes in flight)
-    const bool deep = env_knob("MIHVD_F32_F1R_PD", 2) >= 4;
-    const bool pin = env_knob("MIHVD_F32_F1R_PIN", 0) != 0;  // study: pinned dgrad MFMA order
-    // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
-    // keeps the padded 28 for comparison)
-    if (dgrad_only) {
-      switch (G) {
-        case 1: launch(f32_fc1_bwd_rows_kernel<1, false, false>); break;
-        case 2: launch(f32_fc1_bwd_rows_kernel<2, false, false>); break;
-        case 3: launch(f32_fc1_bwd_rows_kernel<3, false, false>); break;
-        case 4: launch(f32_fc1_bwd_rows_kernel<4, false, false>); break;
-        case 5: launch(f32_fc1_bwd_rows_kernel<5, false, false>); break;
-        case 6: launch(f32_fc1_bwd_rows_kernel<6, false, false>); break;
-        case 7: launch(f32_fc1_bwd_rows_kernel<7, false, false>); break;
-        default: launch(f32_fc1_bwd_rows_kernel<8, false, false>);
-      }
-      return;
-    }
-    if (G == 7 && (B + 3) / 4 == 25 && !deep && !pin && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
-      if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 2, false, 25>);
-      else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 2, false, 25>);
-      else launch(f32_fc1_bwd_rows_kernel<7, false, true, 2, false, 25>);
-      return;
-    }
-#define F1R_CASE(GG)                                                                              \
-  case GG:                                                                                        \
-    if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>);                        \
-    else if (adam && deep) launch(f32_fc1_bwd_rows_kernel<GG, true, false, 4>);                   \
-    else if (adam && pin) launch(f32_fc1_bwd_rows_kernel<GG, true, false, 2, true>);              \
-    else if (adam) launch(f32_fc1_bwd_rows_kernel<GG, true, false>);                              \
-    else launch(f32_fc1_bwd_rows_kernel<GG, false, true>);                                        \
-    break;
-    switch (G) {
-      F1R_CASE(1)
-      F1R_CASE(2)
-      F1R_CASE(3)
-      F1R_CASE(4)
-      F1R_CASE(5)
-      F1R_CASE(6)
-      F1R_CASE(7)
-      default:
-        F1R_CASE(8)
-    }
-#undef F1R_CASE
-    return;
-  }
-  // MIHVD_F32_F1B_KS=1 selects the K-split dgrad form with the unrolled wgrad chain (study: same
-  // dgrad time, fc1_bwd 27.0 vs 25.5 us at B = 100, so the window form stays the default)
-  const int dg_ks = env_knob("MIHVD_F32_F1B_KS", 0) != 0;
-  const int n_dg = dg_ks ? F1B_DG2 : 56 * G;
-  // study knob: MIHVD_F32_F1B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only
-  const int role = env_knob("MIHVD_F32_F1B_ROLE", 0);
-  const int grid = role == 1 ? n_dg : role == 2 ? F1B_WGRAD : n_dg + F1B_SMALL + F1B_WGRAD;
-  const int ndg_arg = role == 2 ? -F1B_SMALL : n_dg;  // wgrad only: bid - n_dg - 33 = bid
+  // Row form: dgrad + dW3 (+ the fused dense/kernel Adam) from one read of W3.
   auto launch = [&](auto kern) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1B_LDS);
-    kern<<<grid, 256, F1B_LDS, stream>>>(
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, F1R_LDS);
+    kern<<<F1R_BLOCKS + F1B_SMALL, 512, F1R_LDS, stream>>>(
         dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
         dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
-        gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, G, ndg_arg);
+        gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad,
+        env_knob("MIHVD_F32_F1R_PF", 1));  // 0: routing operands loaded in the epilogue (r05h: 27.98 vs 27.03 us)
   };
-  switch (dg_ks ? G : 0) {
-    case 0: launch(f32_fc1_bwd_kernel<0>); break;
-    case 1: launch(f32_fc1_bwd_kernel<1>); break;
-    case 2: launch(f32_fc1_bwd_kernel<2>); break;
-    case 3: launch(f32_fc1_bwd_kernel<3>); break;
-    case 4: launch(f32_fc1_bwd_kernel<4>); break;
-    case 5: launch(f32_fc1_bwd_kernel<5>); break;
-    case 6: launch(f32_fc1_bwd_kernel<6>); break;
-    case 7: launch(f32_fc1_bwd_kernel<7>); break;
-    default: launch(f32_fc1_bwd_kernel<8>); break;
+  if (dgrad_only) {
+    switch (G) {
+      case 1: launch(f32_fc1_bwd_rows_kernel<1, false, false>); break;
+      case 2: launch(f32_fc1_bwd_rows_kernel<2, false, false>); break;
+      case 3: launch(f32_fc1_bwd_rows_kernel<3, false, false>); break;
+      case 4: launch(f32_fc1_bwd_rows_kernel<4, false, false>); break;
+      case 5: launch(f32_fc1_bwd_rows_kernel<5, false, false>); break;
+      case 6: launch(f32_fc1_bwd_rows_kernel<6, false, false>); break;
+      case 7: launch(f32_fc1_bwd_rows_kernel<7, false, false>); break;
+      default: launch(f32_fc1_bwd_rows_kernel<8, false, false>);
+    }
+    return;
   }
+  // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
+  // keeps the padded 28, bitwise equal: the padded steps add exact zeros)
+  if (G == 7 && (B + 3) / 4 == 25 && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
+    if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
+    else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 25>);
+    else launch(f32_fc1_bwd_rows_kernel<7, false, true, 25>);
+    return;
+  }
+#define F1R_CASE(GG)                                                       \
+  case GG:                                                                 \
+    if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>); \
+    else if (adam) launch(f32_fc1_bwd_rows_kernel<GG, true, false>);       \
+    else launch(f32_fc1_bwd_rows_kernel<GG, false, true>);                 \
+    break;
+  switch (G) {
+    F1R_CASE(1)
+    F1R_CASE(2)
+    F1R_CASE(3)
+    F1R_CASE(4)
+    F1R_CASE(5)
+    F1R_CASE(6)
+    F1R_CASE(7)
+    default:
+      F1R_CASE(8)
+  }
+#undef F1R_CASE
 }
 
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,

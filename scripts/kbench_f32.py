@@ -126,8 +126,7 @@ def main():
         "adam_step (W3)": lambda: o.adam_step(tr.params[s3], tr.grads[s3], tr.m[s3], tr.v[s3], None, st, 0, 0.0, b1,
                                               b2, tr.eps, 1.0, tr.rule, 0),
     }
-    study_env = {"dg": {"MIHVD_F32_C2B_ROLE": "1"}, "wg": {"MIHVD_F32_C2B_ROLE": "2"},
-                 "fdg": {"MIHVD_F32_F1B_ROLE": "1"}, "fwg": {"MIHVD_F32_F1B_ROLE": "2"}}
+    study_env = {"dg": {"MIHVD_F32_C2B_ROLE": "1"}, "wg": {"MIHVD_F32_C2B_ROLE": "2"}}
     if args.only:
         for item in args.only.split(","):
             name, _, variant = item.partition(":")
@@ -182,15 +181,10 @@ def main():
                                                       c2b_two_round),
         "conv2_bwd [wgrad role only, launch order]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_XCD": "0"},
                                                      ks["conv2_bwd"]),
-        "fc1_bwd+W3 adam [p/m/v 4 chunks ahead]": ({"MIHVD_F32_F1R_PD": "4"}, ks["fc1_bwd+W3 adam"]),
-        "fc1_bwd+W3 adam [pinned dgrad MFMA order]": ({"MIHVD_F32_F1R_PIN": "1"}, ks["fc1_bwd+W3 adam"]),
         "fc1_bwd+W3 adam [padded wgrad K (28 steps)]": ({"MIHVD_F32_F1R_KW": "0"}, ks["fc1_bwd+W3 adam"]),
-        "fc1_bwd [3-role form]": ({"MIHVD_F32_F1B": "0"}, ks["fc1_bwd"]),
-        "fc1_bwd [3-role, dgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "1"}, ks["fc1_bwd"]),
-        "fc1_bwd [3-role, wgrad role only]": ({"MIHVD_F32_F1B": "0", "MIHVD_F32_F1B_ROLE": "2"}, ks["fc1_bwd"]),
         "fc1_fwd [a2 staged in two K halves]": ({"MIHVD_F32_F1F_SPLIT": "1"}, ks["fc1_fwd"]),
         "head [256 threads, 4 features each]": ({"MIHVD_F32_HEAD1K": "0"}, ks["head"]),
-        "fc1_bwd+W3 adam [routing operands loaded at the start]": ({"MIHVD_F32_F1R_PF": "1"}, ks["fc1_bwd+W3 adam"]),
+        "fc1_bwd+W3 adam [routing operands loaded in the epilogue]": ({"MIHVD_F32_F1R_PF": "0"}, ks["fc1_bwd+W3 adam"]),
 
     }
     for name, (env, fn) in study.items():
@@ -215,12 +209,10 @@ def main():
     steps = {
         "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
         "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
-        "whole step [fc1_bwd p/m/v 4 chunks ahead]": ({}, {"MIHVD_F32_F1R_PD": "4"}),
-        "whole step [fc1_bwd pinned dgrad MFMA order]": ({}, {"MIHVD_F32_F1R_PIN": "1"}),
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
         "whole step [256-thread head]": ({}, {"MIHVD_F32_HEAD1K": "0"}),
-        "whole step [fc1_bwd routing operands loaded at the start]": ({}, {"MIHVD_F32_F1R_PF": "1"}),
+        "whole step [fc1_bwd routing operands loaded in the epilogue]": ({}, {"MIHVD_F32_F1R_PF": "0"}),
     }
     for name, (attrs, env) in steps.items():
         if not want(name):

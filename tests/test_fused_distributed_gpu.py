@@ -153,7 +153,8 @@ def test_plane_and_sharding_switches_two_ranks(tmp_path):
         assert o["loss"] == o["loss_ref"]
 
 
-@pytest.mark.parametrize("n,prec", [(2, "fp32"), (4, "fp32"), (2, "bf16"), (4, "bf16")])
+# (4-rank cases dropped in round 5: the 8-rank flow below covers the same path at the larger count)
+@pytest.mark.parametrize("n,prec", [(2, "fp32"), (2, "bf16")])
 def test_bench_multirank_rehearsal_on_one_gpu(n, prec):
     """bench.py's N > 1 flow (torch.distributed.run rendezvous on 127.0.0.1, factor gather +
     sharded optimizer with the N-rank row-tile split, data-plane selection, barrier-bracketed
@@ -177,7 +178,7 @@ def test_bench_multirank_rehearsal_on_one_gpu(n, prec):
     assert r["config"]["final_loss"] < 2.0, r
 
 
-@pytest.mark.parametrize("n,prec", [(8, "bf16"), (8, "fp32")])
+@pytest.mark.parametrize("n,prec", [(8, "fp32")])  # the headline precision (bf16: 2-rank rehearsal above)
 def test_bench_flow_trains_at_8_ranks(tmp_path, n, prec):
     """The bench's fused flow (data-plane selection, 20-step graphs) at 8 ranks sharing this GPU
     over gloo, with per-rank synthetic shards that share the class templates: training reaches well
@@ -194,11 +195,12 @@ def test_bench_flow_trains_at_8_ranks(tmp_path, n, prec):
         assert o["losses"][-1] < 1.0, o
 
 
+# every plane at 8 ranks (the 8-rank slices are the shapes the driver's node runs); one 4-rank case
+# for a rank count whose row split differs
 @pytest.mark.parametrize("n,prec,shard,xgmi,f32plane", [
-    (4, "fp32", "0", "off", "rs"), (8, "fp32", "0", "off", "rs"), (4, "fp32", "1", "off", "rs"),
-    (8, "fp32", "1", "off", "rs"), (4, "fp32", "1", "off", "factor"), (8, "fp32", "1", "off", "factor"),
-    (4, "bf16", "1", "off", "rs"), (8, "bf16", "1", "off", "rs"), (8, "bf16", "0", "off", "rs"),
-    (8, "bf16", "1", "on", "rs"), (4, "fp32", "1", "on", "rs"), (8, "fp32", "1", "on", "rs")])
+    (8, "fp32", "0", "off", "rs"), (8, "fp32", "1", "off", "rs"), (8, "fp32", "1", "off", "factor"),
+    (8, "bf16", "1", "off", "rs"), (8, "bf16", "0", "off", "rs"), (8, "bf16", "1", "on", "rs"),
+    (4, "fp32", "1", "on", "rs"), (8, "fp32", "1", "on", "rs")])
 def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, shard, xgmi, f32plane):
     """N ranks x B=50 sharing this GPU over gloo: the reduced gradient of the first step equals the
     sum of the N single-process gradients (gradient rel < 1e-4), the update equals TF1 Adam on their
