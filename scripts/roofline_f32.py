@@ -72,13 +72,17 @@ def main():
     ap.add_argument("--stats", help="also write the filtered per-kernel stats table to this file")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    t0, t1 = int(rows[0]["Start_Timestamp"]), int(rows[-1]["End_Timestamp"])
+    # the window: the tail of the span of the step's own kernels (start-up and teardown work -- fills,
+    # copies, communicator setup after the timed region -- lies outside it)
+    step_rows = [r for r in rows if classify(r["Kernel_Name"])] or rows
+    t0, t1 = int(step_rows[0]["Start_Timestamp"]), int(step_rows[-1]["End_Timestamp"])
     cut = t1 - a.tail * (t1 - t0)
-    win = [r for r in rows if int(r["Start_Timestamp"]) >= cut]
+    win = [r for r in rows if cut <= int(r["Start_Timestamp"]) <= t1]
     by = {}
     for r in win:
         by.setdefault(r["Kernel_Name"], []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    steps = max(len(v) for v in by.values())
+    steps = max(len(v) for n, v in by.items() if classify(n)) if any(classify(n) for n in by) else \
+        max(len(v) for v in by.values())
     step_ms, bench_line = None, None
     if a.bench:
         for line in open(a.bench):
