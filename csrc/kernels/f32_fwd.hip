@@ -448,7 +448,8 @@ __global__ void __launch_bounds__(256) f32_head_kernel(
     const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
-    float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B) {
+    float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B,
+    float* __restrict__ stats_acc) {
   __shared__ float red[4][10];
   __shared__ float dl[10];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -520,6 +521,10 @@ __global__ void __launch_bounds__(256) f32_head_kernel(
     if (lane == 0) {
       stats[b * 2 + 0] = lse - ly;
       stats[b * 2 + 1] = (am == y) ? 1.f : 0.f;
+      if (stats_acc != nullptr) {  // running per-sample sums (this block is the sample's only writer)
+        stats_acc[b * 2 + 0] += lse - ly;
+        stats_acc[b * 2 + 1] += (am == y) ? 1.f : 0.f;
+      }
       if (b == 0 && state != nullptr) state[ST_OPT] += 1;
     }
   }
@@ -542,7 +547,8 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
     const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
-    float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B) {
+    float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B,
+    float* __restrict__ stats_acc) {
   __shared__ float red[16][10];
   __shared__ float dl[10];
   const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = __builtin_amdgcn_readfirstlane(n >> 6);
@@ -598,6 +604,10 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
     if (lane == 0) {
       stats[b * 2 + 0] = lse - ly;
       stats[b * 2 + 1] = (am == y) ? 1.f : 0.f;
+      if (stats_acc != nullptr) {  // running per-sample sums (this block is the sample's only writer)
+        stats_acc[b * 2 + 0] += lse - ly;
+        stats_acc[b * 2 + 1] += (am == y) ? 1.f : 0.f;
+      }
       if (b == 0 && state != nullptr) state[ST_OPT] += 1;
     }
   }
@@ -747,7 +757,7 @@ void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) 
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
-                      at::Tensor& dlog, at::Tensor& stats) {
+                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc) {
   const int B = h.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_head: batch 1..128");
   check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_head: zpart");
@@ -758,6 +768,11 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   check_f32(dz, (int64_t)B * 1024, "f32_head: dz");
   check_f32(dlog, (int64_t)B * 10, "f32_head: dlog");
   check_f32(stats, (int64_t)B * 2, "f32_head: stats");
+  float* acc = nullptr;
+  if (stats_acc.has_value() && stats_acc->defined()) {
+    check_f32(*stats_acc, (int64_t)B * 2, "f32_head: stats_acc [B][2]");
+    acc = stats_acc->data_ptr<float>();
+  }
   TORCH_CHECK(labels.dtype() == at::kLong, "f32_head: labels int64");
   const int n_pool = labels.size(0);
   const int* rp = rows_ptr(rows, n_pool, B, "f32_head");
@@ -771,7 +786,7 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   kern<<<B, env_knob("MIHVD_F32_HEAD1K", 1) != 0 ? 1024 : 256, 0, stream>>>(
       zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(), b4.data_ptr<float>(),
       labels.data_ptr<int64_t>(), rp, n_pool, sp, (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(),
-      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B);
+      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc);
 }
 
 }  // namespace mihvd

@@ -89,7 +89,8 @@ __global__ void __launch_bounds__(256) head_kernel(
     const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float dz_mul, u16* __restrict__ h_out,
-    u16* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B, CollRole cr) {
+    u16* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B, CollRole cr,
+    float* __restrict__ stats_acc) {
   __shared__ float red[4][10];
   __shared__ float dl[10];
   // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk blocks
@@ -170,6 +171,10 @@ __global__ void __launch_bounds__(256) head_kernel(
     if (lane == 0) {
       stats[b * 2 + 0] = lse - ly;
       stats[b * 2 + 1] = (am == y) ? 1.f : 0.f;
+      if (stats_acc != nullptr) {  // running per-sample sums (this block is the sample's only writer)
+        stats_acc[b * 2 + 0] += lse - ly;
+        stats_acc[b * 2 + 1] += (am == y) ? 1.f : 0.f;
+      }
       if (b == 0 && state != nullptr) state[ST_OPT] += 1;
     }
   }
@@ -717,7 +722,7 @@ void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll, double dz_scale) {
+                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc) {
   const int B = h.size(0);
   TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "head: zpart");
   TORCH_CHECK(b3.numel() == FC1_N && w4.numel() == FC1_N * 10 && b4.numel() == 10 && w4.dtype() == at::kFloat, "head: params");
@@ -725,6 +730,12 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
   TORCH_CHECK(h.dtype() == MIHVD_OP16 && h.numel() == (int64_t)B * FC1_N && dz.numel() == h.numel(), "head: h/dz");
   TORCH_CHECK(dlog.numel() == B * 10 && stats.numel() == B * 2, "head: dlog/stats");
   TORCH_CHECK(rate >= 0.0 && rate < 1.0, "head: dropout rate");
+  float* acc = nullptr;
+  if (stats_acc.has_value() && stats_acc->defined()) {
+    TORCH_CHECK(stats_acc->is_cuda() && stats_acc->dtype() == at::kFloat && stats_acc->is_contiguous() &&
+                    stats_acc->numel() == B * 2, "head: stats_acc must be a contiguous fp32 [B][2] device tensor");
+    acc = stats_acc->data_ptr<float>();
+  }
   const int* rp = nullptr;
   int n_pool = labels.numel();
   if (rows.has_value() && rows->defined()) rp = rows->data_ptr<int>();
@@ -739,7 +750,7 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                                                (uint32_t)seed, thresh, keep_scale, (float)(keep_scale * dz_scale),
                                                (u16*)h.data_ptr(),
                                                (u16*)dz.data_ptr(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B,
-                                               cr);
+                                               cr, acc);
 }
 
 // roles: bit 0 = the dW3 tiles, bit 1 = the small reductions (db3, dW4, db4). dW3 multiplies dz_w3^T a2_w3 over their rows: the local dz/a2 by default, or the

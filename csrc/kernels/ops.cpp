@@ -19,7 +19,7 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll, double dz_scale);
+                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
                const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi, int64_t coll);
@@ -92,7 +92,7 @@ void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
-                      at::Tensor& dlog, at::Tensor& stats);
+                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc);
 void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
                  const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
                  at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
@@ -135,7 +135,7 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll, double dz_scale);
+                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc);
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1,
@@ -168,8 +168,8 @@ void fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tenso
 void fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::fc1_fwd(a2, w3, zpart); }
 void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
              const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog, Tensor stats,
-             int64_t coll, double dz_scale) {
-  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale);
+             int64_t coll, double dz_scale, const OptT& stats_acc) {
+  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale, stats_acc);
 }
 // fp16-operand ops (the Keras mixed_float16 policy): the bf16 ops' schemas, half tensors.
 void conv1_fwd_f16_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1,
@@ -186,8 +186,9 @@ void conv12_fwd_f16_op(const Tensor& x, const OptT& rows, const OptT& state, con
 void fc1_fwd_f16_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f16::fc1_fwd(a2, w3, zpart); }
 void head_f16_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
-                 Tensor stats, int64_t coll, double dz_scale) {
-  mihvd::f16::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale);
+                 Tensor stats, int64_t coll, double dz_scale, const OptT& stats_acc) {
+  mihvd::f16::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale,
+                           stats_acc);
 }
 void fc1_bwd_f16_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, const Tensor& w3,
                     Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles, int64_t coll,
@@ -293,8 +294,8 @@ void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a
 void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
-                 Tensor stats) {
-  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats);
+                 Tensor stats, const OptT& stats_acc) {
+  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, stats_acc);
 }
 void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, const Tensor& h, const Tensor& dlog,
                     Tensor w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, const OptT& m3,
@@ -332,7 +333,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, int coll=-1, "
-        "float dz_scale=1.) -> ()");
+        "float dz_scale=1., Tensor(e!)? stats_acc=None) -> ()");
   m.def("conv1_fwd_f16(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
   m.def("conv2_fwd_f16(Tensor a1, Tensor w2h, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
   m.def("conv12_fwd_f16(Tensor x, Tensor? rows, Tensor? state, Tensor w1h, Tensor b1, Tensor w2h, Tensor b2, "
@@ -340,7 +341,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("fc1_fwd_f16(Tensor a2, Tensor w3h, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd_f16(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
-        "int coll=-1, float dz_scale=1.) -> ()");
+        "int coll=-1, float dz_scale=1., Tensor(e!)? stats_acc=None) -> ()");
   m.def("fc1_bwd_f16(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor w3h, Tensor(a!) gW3, Tensor(b!) gb3, "
         "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3, int coll=-1, Tensor(f!)? a2T=None, "
         "Tensor(g!)? dzT=None) -> ()");
@@ -387,7 +388,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
-        "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats) -> ()");
+        "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
+        "Tensor(e!)? stats_acc=None) -> ()");
   m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor(w!) w3, Tensor(a!) dY2, "
         "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4, Tensor(m!)? m3=None, "
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "

@@ -389,7 +389,7 @@ class FusedMNISTTrainer:
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         # Keras fit (mihvd/keras.py): every step adds its (sum of losses, correct count) on the device
         self.track_stats = False
-        self._stat_sum = torch.zeros(2, **f32)
+        self._stat_acc = torch.zeros(B, 2, **f32)  # per-sample running (loss, correct) sums
         self._stat_steps = 0
         self.X = self.Y = self.rows = None
         self.graph = None
@@ -494,20 +494,20 @@ class FusedMNISTTrainer:
 
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
+        # track_stats (Keras fit): the head kernel adds each sample's (loss, correct) into _stat_acc
+        # [B][2] as it writes them -- the epoch's running sums without an extra launch per step
         self._launch_step_core(x, rows, labels)
-        if self.track_stats:  # Keras fit: the epoch's running (loss, accuracy) sums, on the device
-            self._stat_sum.add_(self.stats.sum(0))
 
     def reset_stats(self):
         """Start a new accumulation of per-step (loss, accuracy) sums (``track_stats``)."""
-        self._stat_sum.zero_()
+        self._stat_acc.zero_()
         self._stat_steps = 0
 
     def epoch_stats(self):
         """Mean loss and accuracy over the steps since ``reset_stats`` (``track_stats``; reading
         synchronises)."""
         n = max(1, self._stat_steps) * self.B
-        s = self._stat_sum.tolist()
+        s = self._stat_acc.sum(0).tolist()
         return s[0] / n, s[1] / n
 
     def _launch_step_core(self, x, rows, labels):
@@ -521,7 +521,8 @@ class FusedMNISTTrainer:
         self._conv_forward(x, rows, st)
         o.fc1_fwd(self.a2, self.pview("dense/kernel", self.shadow), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
-                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
+                       stats_acc=self._stat_acc if self.track_stats else None)
         b1, b2 = self.betas
         if self.fused_opt:
             # dgrad tiles and every wgrad role in one launch; dense/kernel's Adam streams in the tail
@@ -585,7 +586,8 @@ class FusedMNISTTrainer:
             self._shadow_ev = None
         o.f32_fc1_fwd(self.a2, w3, self.zpart)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
-                           self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+                           self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
+                           stats_acc=self._stat_acc if self.track_stats else None)
         gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
                  G("conv_layer2/conv2d/bias"))
         if not self.collectives:
@@ -842,7 +844,8 @@ class FusedMNISTTrainer:
             self._shadow_ev = None
         o.fc1_fwd(self.a2, self.w3_shadow(), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
-                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
+                       stats_acc=self._stat_acc if self.track_stats else None)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self._all_gather_rows(self.dz_all, self.dz)
@@ -942,7 +945,8 @@ class FusedMNISTTrainer:
                      self.a2, self.idx2, co(R["w3"] if self.shard_w3 else R["fence"]))
         o.fc1_fwd(self.a2, self.w3_shadow(), self.zpart)
         o.head_fwd_bwd(self.zpart, self.pview("dense/bias"), self.pview("dense_1/kernel"), self.pview("dense_1/bias"),
-                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats)
+                       labels, rows, st, self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
+                       stats_acc=self._stat_acc if self.track_stats else None)
         gW3 = self.gview("dense/kernel")
         small = (self.dz, self.a2, self.h, self.dlog, gW3, self.gview("dense/bias"), self.gview("dense_1/kernel"),
                  self.gview("dense_1/bias"))

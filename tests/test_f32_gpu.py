@@ -117,6 +117,11 @@ def test_f32_fc1_fwd_and_head(ops, B, monkeypatch):
     monkeypatch.delenv("MIHVD_F32_HEAD1K")
     assert torch.equal(h0, h)
     assert rel_err(dz0, dz) < 1e-6 and rel_err(dlog0, dlog) < 1e-6 and rel_err(stats0, stats) < 1e-6
+    # stats_acc (Keras fit's epoch metrics): every launch adds its per-sample (loss, correct) in place
+    acc = torch.zeros(B, 2, device="cuda")
+    for _ in range(3):
+        ops.f32_head_fwd_bwd(zpart, b3, w4, b4, y, None, None, 0, 0.0, h, dz, dlog, stats, stats_acc=acc)
+    assert torch.allclose(acc, 3 * stats, rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.parametrize("B", [7, 100])

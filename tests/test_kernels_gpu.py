@@ -142,6 +142,11 @@ def test_head_no_dropout(ops):
     assert abs(stats[:, 0].mean().item() - loss.item()) < 1e-3
     assert rel_err(dz, z.grad) < 1e-2
     assert stats[:, 1].mean().item() == pytest.approx((logits.argmax(1) == y).float().mean().item(), abs=0.02)
+    # stats_acc (Keras fit's epoch metrics): each launch adds its per-sample (loss, correct) in place
+    acc = torch.zeros(B, 2, device="cuda")
+    for _ in range(2):
+        ops.head_fwd_bwd(zp, b3, w4, b4, y, None, None, 0, 0.0, h, dz, dlog, stats, stats_acc=acc)
+    assert torch.allclose(acc, 2 * stats, rtol=1e-6, atol=1e-6)
 
 
 def test_head_dropout_rate(ops):
