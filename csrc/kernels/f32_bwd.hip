@@ -731,9 +731,12 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 // staged double buffering (the next image's loads are in flight while this one is multiplied).
 // 8 waves split the K steps (w, w + 8, ...); their partial tiles are summed through LDS.
 // (xcd_contiguous: f32_common.h)
+typedef __attribute__((address_space(3))) void lds_void_t;
+
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
-                                                      int ig, int wmid, float* smf) {
+                                                      int ig, int wmid, float* smf,
+                                                      const float* __restrict__ zeros) {
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), l32 = lane & 31, hh = lane >> 5;
   const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
   const int img0 = ig * grp, nimg = min(ig, B - img0);
@@ -741,6 +744,11 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   // global loads are issued after step 0's MFMAs instead of before the first operand reads
   const int wm = wmid & 3;
   const bool late = (wmid & 4) != 0;
+  // wm 3 (LDS-DMA): the next image goes global -> LDS by global_load_lds_dwordx4 issued at the image
+  // start (the staging image is lane-linear per wave: chunk t + 512 it at 16 (t + 512 it) bytes), so
+  // no register staging and no store sits between the MFMAs; padding chunks read a zero line.
+  // The image-end barrier (__syncthreads: vmcnt(0)) retires them before the buffer is read.
+  const bool dma = wm == 3 && zeros != nullptr;
   // this thread's seven chunk offsets within an image, computed once (per image only the image
   // term is added): chunk i < 2016 is an a1 chunk of the padded rows kh..kh+13, the rest dY2 chunks
   int loff[7];
@@ -769,6 +777,16 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     for (int it = 0; it < 7; ++it)
       v[it] = mask_f4(*reinterpret_cast<const float4*>((la1[it] ? pa : pd) + loff[it]), lin[it]);
   };
+  auto dma_img = [&](int b, float* buf) {
+    const float* pa = a1 + (int64_t)b * 6272;
+    const float* pd = dY2 + (int64_t)b * 12544;
+    const int w64 = (t >> 6) * 64;  // this wave's first chunk: the LDS base is wave-uniform
+#pragma unroll
+    for (int it = 0; it < 7; ++it) {
+      const float* src = lin[it] ? (la1[it] ? pa : pd) + loff[it] : zeros;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(buf + 4 * (w64 + 512 * it)), 16, 0, 0);
+    }
+  };
   auto store_img = [&](float* buf, const float4 (&v)[7]) {
 #pragma unroll
     for (int it = 0; it < 7; ++it) {
@@ -791,7 +809,11 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   __syncthreads();
   for (int n = 0; n < nimg; ++n) {
     const float* buf = smf + (n & 1) * CBF_WBUF;
-    if (n + 1 < nimg && !late) load_img(img0 + n + 1, v);
+    if (dma) {
+      if (n + 1 < nimg) dma_img(img0 + n + 1, smf + ((n + 1) & 1) * CBF_WBUF);
+    } else if (n + 1 < nimg && !late) {
+      load_img(img0 + n + 1, v);
+    }
     const float* A1s = buf;
     const float* DYs = buf + CBF_A1S;
     // K steps s = wave + 8u (pixels 2s: lanes 0-31, 2s + 1: lanes 32-63). Software pipeline, fully
@@ -821,7 +843,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
         for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(opa[cur], opb[cur][kw], acc[kw]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (u == 0 && late && nxt) load_img(img0 + n + 1, v);
+      if (u == 0 && late && nxt && !dma) load_img(img0 + n + 1, v);
       if (u == 6 && wm == 1 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
       // wm 2: one chunk per step over u = 4..10, so each store waits only for its own load (the
       // loads return in issue order; vmcnt counts down) instead of all seven at u = 6
@@ -885,7 +907,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg, int ig, int wmid, int wdelay, const float* __restrict__ w2f) {
+    int n_wg, int ig, int wmid, int wdelay, const float* __restrict__ w2f, const float* __restrict__ zeros) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
@@ -900,7 +922,7 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
   for (int i = 0; i < wdelay; ++i) __builtin_amdgcn_s_sleep(16);
   // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
   f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, wmid,
-                        smf);
+                        smf, zeros);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1264,14 +1286,32 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   // 0: next image stored after the steps, 1: at step 6, 2 (default): one chunk per step over steps
   // 4..10 (wgrad role alone 39.2 vs 40.1 us for 1, profiles/r04/kbench_f32_r04ag.txt; bitwise equal);
   // + 4: the next image's global loads issued after step 0's MFMAs
-  const int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 2);
+  int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 2);
+  // 3: the next image by LDS-DMA (global_load_lds) with padding chunks read from a zero line, which
+  // is allocated on the first eager call (never inside a stream capture: then the stores form runs)
+  static float* zero_line[64] = {nullptr};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const float* zl = nullptr;
+  if ((wmid & 3) == 3 && dev >= 0 && dev < 64) {
+    if (zero_line[dev] == nullptr) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(stream, &cs);
+      if (cs == hipStreamCaptureStatusNone && hipMalloc(&zero_line[dev], 256) == hipSuccess)
+        (void)hipMemset(zero_line[dev], 0, 256);
+      else
+        zero_line[dev] = nullptr;
+    }
+    zl = zero_line[dev];
+  }
+  if ((wmid & 3) == 3 && zl == nullptr) wmid = 2;
   const int wdelay = r1 ? std::max(0, std::min(env_knob("MIHVD_F32_C2B_WDELAY", 0), 64)) : 0;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
                                      cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig,
-                                     wmid, wdelay, w2f);
+                                     wmid, wdelay, w2f, zl);
   };
   // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
   // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA
