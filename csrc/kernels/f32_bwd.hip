@@ -1283,10 +1283,11 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
   const int ndg_arg = role == 2 ? 0 : n_dg;
   const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
-  // 0: next image stored after the steps, 1: at step 6, 2 (default): one chunk per step over steps
-  // 4..10 (wgrad role alone 39.2 vs 40.1 us for 1, profiles/r04/kbench_f32_r04ag.txt; bitwise equal);
+  // 0: next image stored after the steps, 1: at step 6, 2: one chunk per step over steps 4..10
+  // (wgrad role alone 39.2 vs 40.1 us for 1, profiles/r04/kbench_f32_r04ag.txt; bitwise equal);
   // + 4: the next image's global loads issued after step 0's MFMAs
-  int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 2);
+  // default 3 (r05j: whole step 117.73 -> 116.89 us, the wgrad role alone 38.96 -> 38.44 us)
+  int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 3);
   // 3: the next image by LDS-DMA (global_load_lds) with padding chunks read from a zero line, which
   // is allocated on the first eager call (never inside a stream capture: then the stores form runs)
   static float* zero_line[64] = {nullptr};

@@ -161,10 +161,10 @@ def main():
         "conv2_bwd [dgrad role only, MFMA epilogue]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_MEPI": "1"},
                                                      ks["conv2_bwd"]),
         "conv2_bwd [wgrad blocks in launch order]": ({"MIHVD_F32_C2B_XCD": "0"}, ks["conv2_bwd"]),
-        "conv2_bwd [W2 fragment copy, wgrad next image by LDS-DMA]": ({"MIHVD_F32_C2B_WMID": "3"},
-                                                                      ks["conv2_bwd [W2 fragment copy]"]),
-        "conv2_bwd [wgrad role only, next image by LDS-DMA]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "3"},
-                                                               ks["conv2_bwd [W2 fragment copy]"]),
+        "conv2_bwd [W2 fragment copy, wgrad next image register-staged]": ({"MIHVD_F32_C2B_WMID": "2"},
+                                                                           ks["conv2_bwd [W2 fragment copy]"]),
+        "conv2_bwd [wgrad role only, next image register-staged]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "2"},
+                                                                    ks["conv2_bwd [W2 fragment copy]"]),
         "conv2_bwd [wgrad role only, W2 fragment copy]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd [W2 fragment copy]"]),
         "conv2_bwd [wgrad next image stored after the steps]": ({"MIHVD_F32_C2B_WMID": "0"}, ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only, stored after the steps]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "0"},
@@ -217,7 +217,7 @@ def main():
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
         "whole step [256-thread head]": ({}, {"MIHVD_F32_HEAD1K": "0"}),
-        "whole step [conv2 wgrad next image by LDS-DMA]": ({}, {"MIHVD_F32_C2B_WMID": "3"}),
+        "whole step [conv2 wgrad next image register-staged]": ({}, {"MIHVD_F32_C2B_WMID": "2"}),
         "whole step [fc1_bwd routing operands loaded in the epilogue]": ({}, {"MIHVD_F32_F1R_PF": "0"}),
     }
     for name, (attrs, env) in steps.items():

@@ -235,8 +235,8 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
     assert torch.equal(dY2q, dY2s) and torch.equal(db2q, db2s) and torch.equal(gW3q, gW3s)
 
 
-@pytest.mark.parametrize("form", ["one-round", "one-round-mepi", "one-round-mid", "one-round-late", "one-round-dma",
-                                  "two-round", "two-round-mepi", "two-round-dma"])
+@pytest.mark.parametrize("form", ["one-round", "one-round-mepi", "one-round-mid", "one-round-late", "one-round-spread",
+                                  "two-round", "two-round-mepi", "two-round-spread"])
 @pytest.mark.parametrize("B", [7, 100, 128])
 def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
     """conv2 dgrad + fused conv1 wgrad, conv2 wgrad slabs, and the reduction, vs autograd of
@@ -244,12 +244,13 @@ def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
     dgrad blocks of two tap-loop passes, 8-image wgrad groups; B = 128 falls back to two rounds),
     the two-round launch (MIHVD_F32_C2B_R1=0) with the conv1 weight gradient of the dgrad epilogue
     on VALU or on MFMA (MIHVD_F32_C2B_MEPI=1); the wgrad blocks' next-image LDS stores one chunk per
-    step (MIHVD_F32_C2B_WMID=2, the default) or all at step 6 ("-mid": WMID=1), its global loads
-    issued after step 0's MFMAs ("-late": WMID=6), or the next image staged by LDS-DMA
-    (global_load_lds, "-dma": WMID=3)."""
+    the next image staged by LDS-DMA (global_load_lds, MIHVD_F32_C2B_WMID=3, the default), or
+    register-staged with its LDS stores one chunk per step ("-spread": WMID=2) or all at step 6
+    ("-mid": WMID=1), or with its global loads issued after step 0's MFMAs ("-late": WMID=6)."""
     monkeypatch.setenv("MIHVD_F32_C2B_R1", "1" if form.startswith("one-round") else "0")
     monkeypatch.setenv("MIHVD_F32_C2B_MEPI", "1" if form.endswith("mepi") else "0")
-    monkeypatch.setenv("MIHVD_F32_C2B_WMID", {"mid": "1", "late": "6", "dma": "3"}.get(form.rsplit("-", 1)[-1], "2"))
+    monkeypatch.setenv("MIHVD_F32_C2B_WMID", {"mid": "1", "late": "6", "dma": "3", "spread": "2"}.get(
+        form.rsplit("-", 1)[-1], "3"))
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.rand(B, 784, device="cuda", generator=g)
     w1 = torch.randn(5, 5, 1, 32, device="cuda", generator=g) * 0.2

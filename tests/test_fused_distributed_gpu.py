@@ -154,7 +154,7 @@ def test_plane_and_sharding_switches_two_ranks(tmp_path):
 
 
 # (4-rank cases dropped in round 5: the 8-rank flow below covers the same path at the larger count)
-@pytest.mark.parametrize("n,prec", [(2, "fp32"), (2, "bf16")])
+@pytest.mark.parametrize("n,prec", [(2, "fp32")])  # (bf16 at 2 ranks: the equivalence tests)
 def test_bench_multirank_rehearsal_on_one_gpu(n, prec):
     """bench.py's N > 1 flow (torch.distributed.run rendezvous on 127.0.0.1, factor gather +
     sharded optimizer with the N-rank row-tile split, data-plane selection, barrier-bracketed
