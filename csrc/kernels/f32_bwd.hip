@@ -1288,23 +1288,8 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   // + 4: the next image's global loads issued after step 0's MFMAs
   // default 3 (r05j: whole step 117.73 -> 116.89 us, the wgrad role alone 38.96 -> 38.44 us)
   int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 3);
-  // 3: the next image by LDS-DMA (global_load_lds) with padding chunks read from a zero line, which
-  // is allocated on the first eager call (never inside a stream capture: then the stores form runs)
-  static float* zero_line[64] = {nullptr};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  const float* zl = nullptr;
-  if ((wmid & 3) == 3 && dev >= 0 && dev < 64) {
-    if (zero_line[dev] == nullptr) {
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      (void)hipStreamIsCapturing(stream, &cs);
-      if (cs == hipStreamCaptureStatusNone && hipMalloc(&zero_line[dev], 256) == hipSuccess)
-        (void)hipMemset(zero_line[dev], 0, 256);
-      else
-        zero_line[dev] = nullptr;
-    }
-    zl = zero_line[dev];
-  }
+  // 3: the next image by LDS-DMA (global_load_lds) with padding chunks read from a zero line
+  const float* zl = (wmid & 3) == 3 ? f32_zero_line(stream) : nullptr;
   if ((wmid & 3) == 3 && zl == nullptr) wmid = 2;
   const int wdelay = r1 ? std::max(0, std::min(env_knob("MIHVD_F32_C2B_WDELAY", 0), 64)) : 0;
   auto launch = [&](auto kern) {

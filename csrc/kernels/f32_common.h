@@ -211,4 +211,25 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
   }
 }
 
+// A 256-byte zero line in device memory (one per device), the source of the padding chunks of
+// LDS-DMA staging (global_load_lds cannot mask a lane: a padding lane reads zeros instead). Created
+// on the first call outside a stream capture; nullptr while capturing before that (callers then
+// use their register-staged form).
+inline const float* f32_zero_line(hipStream_t stream) {
+  static float* line[64] = {nullptr};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (line[dev] == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(stream, &cs);
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
+    float* p = nullptr;
+    if (hipMalloc(&p, 256) != hipSuccess) return nullptr;
+    (void)hipMemset(p, 0, 256);
+    line[dev] = p;
+  }
+  return line[dev];
+}
+
 }  // namespace mihvd

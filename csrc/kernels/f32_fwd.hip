@@ -170,11 +170,18 @@ __device__ __forceinline__ void c2f_tiles_h(const float* img, const int (&ab)[2]
 constexpr int C2F8_MAXCH = (C2F_MAXR * 18 * 8 + 511) / 512;  // image float4 chunks per thread
 constexpr int C2F8_LDS = C2F8_IMG + 4 * 7 * 64 * 16;         // image + [co group][tile][lane] f32x4 exchange
 
-template <int TPB, bool FRAG, int DEPTH = 2>
+typedef __attribute__((address_space(3))) void c2f_lds_void;
+
+// DMA: the tall image staged by LDS-DMA (global_load_lds_dwordx4: LDS slot s of a wave-instruction is
+// its base + 16 B x lane, so the XOR swizzle is applied to the SOURCE chunk: slot s holds chunk
+// (s & 7) ^ swz; padding chunks read a zero line), the W2 operand loaded right behind it, one barrier
+// retiring both: no staging registers, no LDS write pass.
+template <int TPB, bool FRAG, int DEPTH = 2, bool DMA = false>
 __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                              const float* __restrict__ b2, float* __restrict__ a2,
                                                              uint8_t* __restrict__ idx2, int B,
-                                                             const float* __restrict__ w2f) {
+                                                             const float* __restrict__ w2f,
+                                                             const float* __restrict__ zeros) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   float* img = smf;
   f32x4* xr = reinterpret_cast<f32x4*>(smf + C2F8_IMG / 4);
@@ -188,6 +195,29 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
   const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
   const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
+  float wb[100];  // this wave's W2 operand (below)
+  if constexpr (DMA) {
+    const int w64 = 64 * wave;
+#pragma unroll
+    for (int it = 0; it < C2F8_MAXCH; ++it) {
+      const int sl = t + 512 * it;  // LDS slot (16-byte chunk) this lane fills
+      const int rr = sl / 144, rem = sl - rr * 144, c = rem >> 3, q = (rem & 7) ^ c2f8_swz(rr, c);
+      const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
+      const bool in = sl < nch && y >= 0 && y < 14 && xx >= 0 && xx < 14;
+      const float* src = in ? a1 + (((int64_t)bb * 14 + y) * 14 + xx) * 32 + q * 4 : zeros;
+      __builtin_amdgcn_global_load_lds((const void*)src, (c2f_lds_void*)(img + 4 * (w64 + 512 * it)), 16, 0, 0);
+    }
+    const float4* fp = reinterpret_cast<const float4*>(w2f) + (c2 * 4 + wco) * 64 + lane;
+#pragma unroll
+    for (int tap = 0; tap < 25; ++tap) {
+      const float4 v = fp[tap * 512];
+      wb[4 * tap + 0] = v.x;
+      wb[4 * tap + 1] = v.y;
+      wb[4 * tap + 2] = v.z;
+      wb[4 * tap + 3] = v.w;
+    }
+    __syncthreads();  // (vmcnt(0)): the image has landed in LDS
+  } else {
   float4 iv[C2F8_MAXCH];
 #pragma unroll
   for (int it = 0; it < C2F8_MAXCH; ++it) {
@@ -209,7 +239,6 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
   }
   __syncthreads();  // the image is complete; no barrier below until the exchange
   // this wave's W2 operand: wb[4 tap + j] = W2[tap][16 c2 + 4 lg + j][16 wco + lr], consumed in issue order
-  float wb[100];
   if constexpr (FRAG) {
     const float4* fp = reinterpret_cast<const float4*>(w2f) + (c2 * 4 + wco) * 64 + lane;
 #pragma unroll
@@ -227,6 +256,7 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
 #pragma unroll
       for (int j = 0; j < 4; ++j) wb[4 * tap + j] = wp[tap * 2048 + j * 64];
   }
+  }  // register-staged form
   f32x4 accs[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; i += 2) {  // block-uniform
@@ -698,14 +728,18 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   // blocks share a CU: the dispatcher otherwise doubles blocks up on some CUs while others idle
   // (measured 20.6 -> 19.7 us at B = 100).
   const int lds = nblk <= device_cu_count() ? std::max(C2F8_LDS, 81920 + 1024) : C2F8_LDS;
+  // MIHVD_F32_C2F_DMA=1: the image staged by LDS-DMA (study; needs the W2 fragment copy)
+  const float* zl = (w2f != nullptr && env_knob("MIHVD_F32_C2F_DMA", 0) != 0) ? f32_zero_line(stream) : nullptr;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nblk, 512, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
-                                     a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, w2f);
+                                     a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), B, w2f, zl);
   };
-#define C2F8_CASE(T)                                                                  \
-  case T:                                                                             \
-    w2f ? launch(f32_conv2_fwd8_kernel<T, true>) : launch(f32_conv2_fwd8_kernel<T, false>); \
+#define C2F8_CASE(T)                                                         \
+  case T:                                                                    \
+    if (zl) launch(f32_conv2_fwd8_kernel<T, true, 2, true>);                 \
+    else if (w2f) launch(f32_conv2_fwd8_kernel<T, true>);                    \
+    else launch(f32_conv2_fwd8_kernel<T, false>);                            \
     break;
   switch (tpb) {
     C2F8_CASE(1)
