@@ -728,8 +728,9 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   // blocks share a CU: the dispatcher otherwise doubles blocks up on some CUs while others idle
   // (measured 20.6 -> 19.7 us at B = 100).
   const int lds = nblk <= device_cu_count() ? std::max(C2F8_LDS, 81920 + 1024) : C2F8_LDS;
-  // MIHVD_F32_C2F_DMA=1: the image staged by LDS-DMA (study; needs the W2 fragment copy)
-  const float* zl = (w2f != nullptr && env_knob("MIHVD_F32_C2F_DMA", 0) != 0) ? f32_zero_line(stream) : nullptr;
+  // the image staged by LDS-DMA with the W2 fragment copy (default; r05k: 20.71 -> 19.31 us, whole step
+  // 117.42 -> 116.84 us); MIHVD_F32_C2F_DMA=0: register staging + LDS write pass
+  const float* zl = (w2f != nullptr && env_knob("MIHVD_F32_C2F_DMA", 1) != 0) ? f32_zero_line(stream) : nullptr;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nblk, 512, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),

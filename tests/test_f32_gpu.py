@@ -53,8 +53,8 @@ def test_f32_conv1_fwd(ops, B):
 @pytest.mark.parametrize("B", [7, 100, 128])
 def test_f32_conv2_fwd(ops, B, monkeypatch):
     """The two waves of a SIMD split the input channels (their partials meet in LDS); HWIO and
-    fragment-copy W2 reads give the same bits, and so does the image staged by LDS-DMA
-    (MIHVD_F32_C2F_DMA=1)."""
+    fragment-copy W2 reads give the same bits, with the image staged by LDS-DMA (the default with
+    the fragment copy) or through registers (MIHVD_F32_C2F_DMA=0)."""
     g = torch.Generator(device="cuda").manual_seed(2)
     a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
     w = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
@@ -70,7 +70,7 @@ def test_f32_conv2_fwd(ops, B, monkeypatch):
     a2f, idxf = torch.empty_like(a2), torch.empty_like(idx)
     ops.f32_conv2_fwd(a1, w, b, a2f, idxf, w2frag=frag[0])
     assert torch.equal(a2, a2f) and torch.equal(idx, idxf)
-    monkeypatch.setenv("MIHVD_F32_C2F_DMA", "1")
+    monkeypatch.setenv("MIHVD_F32_C2F_DMA", "0")
     a2d, idxd = torch.full_like(a2, float("nan")), torch.empty_like(idx)
     ops.f32_conv2_fwd(a1, w, b, a2d, idxd, w2frag=frag[0])
     monkeypatch.delenv("MIHVD_F32_C2F_DMA")
