@@ -417,8 +417,7 @@ template <int TPB, bool PREW, bool MEPI, int NPASS = 1, bool FRAG = false>
 __device__ __forceinline__ void f32_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
-    const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf, const float* __restrict__ w2f,
-    const float* __restrict__ dzeros) {
+    const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf, const float* __restrict__ w2f) {
   static_assert(TPB % NPASS == 0, "tiles split evenly over the passes");
   constexpr int TP = TPB / NPASS;                                        // tiles per pass
   constexpr int MAXCH = (cbf_maxr(NPASS) * 18 * 16 + 511) / 512;         // dY2 chunks per thread
@@ -433,27 +432,9 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   const int nch = (R1 - R0) * 288;  // 18 pixels x 16 float4
   const int nt = wave & 1, cq = wave >> 1;
   // 1. loads: the first two taps' weight fragments, the dY2 rows, the (at most two) x images
-  // dzeros (LDS-DMA staging): the padded image goes global -> LDS by global_load_lds_dwordx4 over
-  // every 16-byte slot of its rows (lane-linear per wave-instruction), pixel pads, unused pixels and
-  // halo chunks reading a zero line; the barrier below then waits for them (vmcnt)
-  const bool ddma = dzeros != nullptr;
-  if (ddma) {
-    constexpr int SROW = CBF_RWD * (CBF_PS / 4);                             // slots per tall row
-    constexpr int MAXS = (cbf_maxr(NPASS) * SROW + 511) / 512;
-    const int nsl = (R1 - R0) * SROW;
-#pragma unroll
-    for (int it = 0; it < MAXS; ++it) {
-      const int sl = t + 512 * it;
-      const int rr = sl / SROW, rem = sl - rr * SROW, c = rem / (CBF_PS / 4), k = rem - c * (CBF_PS / 4);
-      const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
-      const bool in = sl < nsl && k < 16 && y >= 0 && y < 14 && xx >= 0 && xx < 14;
-      const float* src = in ? dY2 + (((int64_t)bb * 14 + y) * 14 + xx) * 64 + k * 4 : dzeros;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(dimg + 4 * (64 * wave + 512 * it)), 16, 0, 0);
-    }
-  }
   float4 iv[MAXCH];
 #pragma unroll
-  for (int it = 0; it < MAXCH && !ddma; ++it) {
+  for (int it = 0; it < MAXCH; ++it) {
     const int i = min(t + 512 * it, nch - 1);
     const int rr = i / 288, rem = i - rr * 288, c = rem >> 4, ch = rem & 15;
     const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
@@ -463,7 +444,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
     iv[it] = mask_f4(v, in);
   }
 #pragma unroll
-  for (int it = 0; it < MAXCH && !ddma; ++it) {
+  for (int it = 0; it < MAXCH; ++it) {
     const int i = t + 512 * it;
     if (i < nch) {
       const int rr = i / 288, rem = i - rr * 288;
@@ -493,10 +474,7 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
   for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (PREW) {
-    // the dY2 image is complete; the W2 loads stay in flight (with LDS-DMA staging: the 25 W2 loads
-    // were issued after the DMA, so vmcnt(25) retires exactly the DMA)
-    if (ddma) asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
-    lds_barrier();
+    lds_barrier();  // the dY2 image is complete; the W2 loads stay in flight
   } else {
     __syncthreads();  // the dY2 image is complete; no barrier in the tap loop
   }
@@ -929,20 +907,15 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg, int ig, int wmid, int wdelay, const float* __restrict__ w2f, const float* __restrict__ zeros,
-    int ddma) {
+    int n_wg, int ig, int wmid, const float* __restrict__ w2f, const float* __restrict__ zeros) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
   if (bid < n_dg) {
     f32_conv2_dgrad_block<TPB, PREW, MEPI, NPASS, FRAG>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf,
-                                                        w2f, ddma ? zeros : nullptr);
+                                                        w2f);
     return;
   }
-  // wdelay (one-round form): the wgrad blocks, which finish ahead of the dgrad blocks, hold their
-  // first loads back by ~wdelay x 1k cycles so the dgrad staging (the critical path) gets the memory
-  // system to itself at kernel start
-  for (int i = 0; i < wdelay; ++i) __builtin_amdgcn_s_sleep(16);
   // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
   f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, wmid,
                         smf, zeros);
@@ -1299,15 +1272,10 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
     TORCH_CHECK(r1 - r0 <= maxr && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS image");
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  // study knobs: MIHVD_F32_C2B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only (the other role's
-  // outputs are then stale); MIHVD_F32_C2B_LDS requests more dynamic LDS than the roles need
+  // study knob: MIHVD_F32_C2B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only (the other role's
+  // outputs are then stale)
   const int role = env_knob("MIHVD_F32_C2B_ROLE", 0);
-  // MIHVD_F32_C2B_DDMA=1: the dgrad blocks' padded dY2 image by LDS-DMA (study); its last
-  // wave-instructions write whole 8 KB rounds of slots, up to 17 x 8 KB in the one-round form
-  const int ddma = env_knob("MIHVD_F32_C2B_DDMA", 0) != 0 ? 1 : 0;
-  const int lds = std::max(std::max(r1 ? CBF_LDS2 : CBF_LDS, ddma ? ((maxr * CBF_RWD * (CBF_PS / 4) + 511) / 512) * 8192 : 0),
-                           std::min(env_knob("MIHVD_F32_C2B_LDS", 0), 163840));
-  TORCH_CHECK(lds <= 163840, "f32_conv2_bwd: LDS");
+  const int lds = r1 ? CBF_LDS2 : CBF_LDS;
   const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
   const int ndg_arg = role == 2 ? 0 : n_dg;
   const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
@@ -1317,15 +1285,14 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   // default 3 (r05j: whole step 117.73 -> 116.89 us, the wgrad role alone 38.96 -> 38.44 us)
   int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 3);
   // 3: the next image by LDS-DMA (global_load_lds) with padding chunks read from a zero line
-  const float* zl = ((wmid & 3) == 3 || ddma) ? f32_zero_line(stream) : nullptr;
+  const float* zl = (wmid & 3) == 3 ? f32_zero_line(stream) : nullptr;
   if ((wmid & 3) == 3 && zl == nullptr) wmid = 2;
-  const int wdelay = r1 ? std::max(0, std::min(env_knob("MIHVD_F32_C2B_WDELAY", 0), 64)) : 0;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
                                      cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig,
-                                     wmid, wdelay, w2f, zl, zl != nullptr ? ddma : 0);
+                                     wmid, w2f, zl);
   };
   // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
   // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA

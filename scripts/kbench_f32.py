@@ -176,9 +176,6 @@ def main():
                                                            ks["conv2_bwd"]),
         "conv2_bwd [wgrad role only, stored at step 6]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "1"},
                                                          ks["conv2_bwd"]),
-        "conv2_bwd [wgrad start held back ~4k cycles]": ({"MIHVD_F32_C2B_WDELAY": "4"}, ks["conv2_bwd"]),
-        "conv2_bwd [wgrad start held back ~8k cycles]": ({"MIHVD_F32_C2B_WDELAY": "8"}, ks["conv2_bwd"]),
-        "conv2_bwd [wgrad start held back ~12k cycles]": ({"MIHVD_F32_C2B_WDELAY": "12"}, ks["conv2_bwd"]),
         "conv2_bwd [two-round form]": ({"MIHVD_F32_C2B_R1": "0"}, c2b_two_round),
         "conv2_bwd [two-round form, dgrad role only]": ({"MIHVD_F32_C2B_R1": "0", "MIHVD_F32_C2B_ROLE": "1"},
                                                       c2b_two_round),
@@ -189,10 +186,7 @@ def main():
         "fc1_bwd+W3 adam [padded wgrad K (28 steps)]": ({"MIHVD_F32_F1R_KW": "0"}, ks["fc1_bwd+W3 adam"]),
         "fc1_fwd [a2 staged in two K halves]": ({"MIHVD_F32_F1F_SPLIT": "1"}, ks["fc1_fwd"]),
         "head [256 threads, 4 features each]": ({"MIHVD_F32_HEAD1K": "0"}, ks["head"]),
-        "conv2_bwd [W2 fragment copy, dgrad image by LDS-DMA]": ({"MIHVD_F32_C2B_DDMA": "1"}, ks["conv2_bwd [W2 fragment copy]"]),
         "conv2_bwd [dgrad role only, W2 fragment copy]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd [W2 fragment copy]"]),
-        "conv2_bwd [dgrad role only, image by LDS-DMA]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_DDMA": "1"},
-                                                          ks["conv2_bwd [W2 fragment copy]"]),
         "conv2_fwd [W2 fragment copy, image register-staged]": ({"MIHVD_F32_C2F_DMA": "0"}, ks["conv2_fwd [W2 fragment copy]"]),
         "fc1_bwd+W3 adam [routing operands loaded in the epilogue]": ({"MIHVD_F32_F1R_PF": "0"}, ks["fc1_bwd+W3 adam"]),
 
@@ -223,7 +217,6 @@ def main():
         "whole step [fc1_fwd a2 in two K halves]": ({}, {"MIHVD_F32_F1F_SPLIT": "1"}),
         "whole step [256-thread head]": ({}, {"MIHVD_F32_HEAD1K": "0"}),
         "whole step [conv2_fwd image register-staged]": ({}, {"MIHVD_F32_C2F_DMA": "0"}),
-        "whole step [conv2 dgrad image by LDS-DMA]": ({}, {"MIHVD_F32_C2B_DDMA": "1"}),
         "whole step [conv2 wgrad next image register-staged]": ({}, {"MIHVD_F32_C2B_WMID": "2"}),
         "whole step [fc1_bwd routing operands loaded in the epilogue]": ({}, {"MIHVD_F32_F1R_PF": "0"}),
     }

@@ -242,7 +242,7 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
 
 
 @pytest.mark.parametrize("form", ["one-round", "one-round-mepi", "one-round-mid", "one-round-late", "one-round-spread",
-                                  "one-round-ddma", "two-round", "two-round-mepi", "two-round-spread", "two-round-ddma"])
+                                  "two-round", "two-round-mepi", "two-round-spread"])
 @pytest.mark.parametrize("B", [7, 100, 128])
 def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
     """conv2 dgrad + fused conv1 wgrad, conv2 wgrad slabs, and the reduction, vs autograd of
@@ -257,7 +257,6 @@ def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
     monkeypatch.setenv("MIHVD_F32_C2B_MEPI", "1" if form.endswith("mepi") else "0")
     monkeypatch.setenv("MIHVD_F32_C2B_WMID", {"mid": "1", "late": "6", "dma": "3", "spread": "2"}.get(
         form.rsplit("-", 1)[-1], "3"))
-    monkeypatch.setenv("MIHVD_F32_C2B_DDMA", "1" if form.endswith("ddma") else "0")
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.rand(B, 784, device="cuda", generator=g)
     w1 = torch.randn(5, 5, 1, 32, device="cuda", generator=g) * 0.2
