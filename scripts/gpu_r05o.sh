@@ -1,0 +1,13 @@
+# Round 5, pass o: fc1_fwd KH form (each W3 fragment loaded by one wave): fp32 tests, A/B timings,
+# driver-form bench.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export MIHVD_NO_AUTOBUILD=1
+O=gpurun_out/r05o; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
+  tests/test_f32_gpu.py > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -c PASSED $O/tests.log; grep -E "^FAILED|^ERROR" $O/tests.log | head; tail -1 $O/tests.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python scripts/kbench_f32.py --match "fc1_fwd|whole step (graph|whole step [fc1_fwd" > $O/kbench.log 2>&1 || { tail -20 $O/kbench.log; exit 1; }
+grep -v "^#" $O/kbench.log | tail -8
+for i in 1 2; do timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_drv$i.log 2>&1 || { tail -20 $O/bench_drv$i.log; exit 1; }; python3 -c "import json; [print('drv', json.loads(l)['ms_per_step']*1000) for l in open('$O/bench_drv$i.log') if l.startswith('{')]"; done
+echo ALLDONE

@@ -40,9 +40,9 @@ WORK = [
      (B * 6272 * F + B * 3136 * (F + 1) + 51200 * F) / MB, "conv2 forward, bias/ReLU/pool/argmax fused"),
     (r"f32_conv1_kernel", "conv1_fwd", CONV1_GF, (B * 784 * F + B * 6272 * (F + 1) + 3 * 51200 * F) / MB,
      "conv1 forward (+ the two W2 fragment copies)"),
-    (r"f32_fc1_fwd2?_kernel<\d+, true>", "fc1_fwd+W3 adam", FC1_GF,
+    (r"f32_fc1_fwd\d?_kernel<\d+, true>", "fc1_fwd+W3 adam", FC1_GF,
      (W3 * F * 7 + B * 3136 * F + 14 * B * 1024 * F) / MB, "fc1 split-K x14 + the deferred W3 Adam (p,g,m,v)"),
-    (r"f32_fc1_fwd2?_kernel", "fc1_fwd", FC1_GF, (W3 * F + B * 3136 * F + 14 * B * 1024 * F) / MB, "fc1 split-K x14"),
+    (r"f32_fc1_fwd\d?_kernel", "fc1_fwd", FC1_GF, (W3 * F + B * 3136 * F + 14 * B * 1024 * F) / MB, "fc1 split-K x14"),
     (r"f32_head1?k?_kernel", "head", 2 * 2 * B * 1024 * 10 / 1e9, (14 * B * 1024 * F + 3 * B * 1024 * F) / MB,
      "slab sum, bias, ReLU, dropout, fc2, softmax-xent, dz"),
     (r"f32_fc1_bwd_rows_kernel<\d+, true", "fc1_bwd+W3 adam", 2 * FC1_GF,
