@@ -407,94 +407,6 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
   }
 }
 
-// KH form (default): wave w = 16 columns (w & 3) x one K half (w >> 2, 112 deep) of the slice, all MT
-// sample tiles per wave. Every W3 fragment is loaded by ONE wave (57 KB of W3 per block; in the form
-// above the two waves of a column tile both load all 56 fragments: 114 KB through the CU's load
-// path beside the 100 KB a2 slice), each wave keeps MT independent accumulators, and the two K
-// halves' partial tiles meet in LDS behind the slice (half 0 + half 1, a fixed order).
-template <int MT>
-__device__ __forceinline__ void f1f_mma_kh(const float (&wa)[28], const float* __restrict__ bp, f32x4 (&acc)[MT]) {
-  constexpr int NQ = 7, DQ = 2, R = DQ + 1;
-  float4 bq[R][MT];
-#pragma unroll
-  for (int j = 0; j < DQ; ++j)
-#pragma unroll
-    for (int u = 0; u < MT; ++u) bq[j][u] = *reinterpret_cast<const float4*>(bp + u * 16 * F1F_AS + 16 * j);
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    if (q + DQ < NQ) {
-#pragma unroll
-      for (int u = 0; u < MT; ++u) bq[(q + DQ) % R][u] = *reinterpret_cast<const float4*>(bp + u * 16 * F1F_AS + 16 * (q + DQ));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int sl = q % R;
-#pragma unroll
-    for (int u = 0; u < MT; ++u) acc[u] = mfma4(wa[4 * q + 0], bq[sl][u].x, acc[u]);
-#pragma unroll
-    for (int u = 0; u < MT; ++u) acc[u] = mfma4(wa[4 * q + 1], bq[sl][u].y, acc[u]);
-#pragma unroll
-    for (int u = 0; u < MT; ++u) acc[u] = mfma4(wa[4 * q + 2], bq[sl][u].z, acc[u]);
-#pragma unroll
-    for (int u = 0; u < MT; ++u) acc[u] = mfma4(wa[4 * q + 3], bq[sl][u].w, acc[u]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-template <int MT>
-__global__ void __launch_bounds__(512) f32_fc1_fwd3_kernel(const float* __restrict__ a2, const float* __restrict__ w3,
-                                                           float* __restrict__ zpart, int B) {
-  extern __shared__ __attribute__((aligned(16))) float smf[];
-  float* As = smf;                                                    // [16 MT][232]
-  f32x4* xr = reinterpret_cast<f32x4*>(smf + MT * 16 * F1F_AS);       // [4 nt][MT][64 lanes]
-  const int nb = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
-  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
-  const int k0 = ks * F1F_KSL, nt = wave & 3, kh = wave >> 2;
-  const int n = nb * 64 + nt * 16 + lr;
-  constexpr int NCH = MT * 16 * 56, PER = (NCH + 511) / 512;
-  float4 v[PER];
-#pragma unroll
-  for (int it = 0; it < PER; ++it) {
-    const int i = min(t + 512 * it, NCH - 1), r = i / 56, cc = i - 56 * r;
-    v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc), r < B);
-  }
-  float wa[28];  // wa[4q + j] = W3[k0 + 112 kh + 16q + 4lg + j][n]
-  {
-    const int64_t wo = (int64_t)(k0 + 112 * kh + 4 * lg) * 1024 + n;
-#pragma unroll
-    for (int q = 0; q < 7; ++q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wa[4 * q + j] = w3[wo + (16 * q + j) * 1024];
-  }
-#pragma unroll
-  for (int it = 0; it < PER; ++it) {
-    const int i = t + 512 * it;
-    if (i < NCH) {
-      const int r = i / 56, cc = i - 56 * r;
-      *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
-    }
-  }
-  c2f_lds_barrier();  // LDS only: the W3 fragments stay in flight and are consumed in issue order
-  f32x4 acc[MT];
-#pragma unroll
-  for (int u = 0; u < MT; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f1f_mma_kh<MT>(wa, As + lr * F1F_AS + 112 * kh + 4 * lg, acc);
-  if (kh == 1) {
-#pragma unroll
-    for (int u = 0; u < MT; ++u) xr[(nt * MT + u) * 64 + lane] = acc[u];
-  }
-  __syncthreads();
-  if (kh == 0) {
-#pragma unroll
-    for (int u = 0; u < MT; ++u) {
-      const f32x4 o = acc[u] + xr[(nt * MT + u) * 64 + lane];
-      const int m = 16 * u + lr;
-      if (m < B)
-        *reinterpret_cast<float4*>(zpart + ((int64_t)ks * B + m) * 1024 + nb * 64 + nt * 16 + 4 * lg) =
-            make_float4(o[0], o[1], o[2], o[3]);
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------ //
 // head: one block per sample b, 256 threads x 4 features (K9-K11 of SURVEY.md §2.5):
 //   z = sum of the 14 slabs + b3; h = dropout(relu(z)); logits = h W4 + b4; softmax-xent;
@@ -789,17 +701,18 @@ void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) 
   check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_fc1_fwd: zpart [14][B][1024]");
   const int mt = (B + 15) / 16;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  // KH form (default); MIHVD_F32_F1F_KH=0: the form with every other sample tile per wave
-  const bool kh = env_knob("MIHVD_F32_F1F_KH", 1) != 0;
+  // (Measured alternatives, removed: the slice staged in two K halves, 10.7 vs 10.4 us; waves split by
+  // K half with every W3 fragment loaded by one wave instead of two, 11.20 vs 11.05 us, whole step
+  // 116.84 vs 116.91 us, profiles/r05/kbench_f32_r05o.txt -- the second wave's W3 loads hit the cache)
   auto launch = [&](auto kern) {
-    const int lds = mt * 16 * F1F_AS * 4 + (kh ? 4 * mt * 64 * 16 : 0);
+    const int lds = mt * 16 * F1F_AS * 4;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<dim3(16, F1F_KS), 512, lds, stream>>>(a2.data_ptr<float>(), w3.data_ptr<float>(), zpart.data_ptr<float>(),
                                                  B);
   };
-#define F1F_CASE(T)                                                                   \
-  case T:                                                                             \
-    kh ? launch(f32_fc1_fwd3_kernel<T>) : launch(f32_fc1_fwd2_kernel<T>);            \
+#define F1F_CASE(T)                          \
+  case T:                                    \
+    launch(f32_fc1_fwd2_kernel<T>);          \
     break;
   switch (mt) {
     F1F_CASE(1)

@@ -184,7 +184,6 @@ def main():
         "conv2_bwd [wgrad role only, launch order]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_XCD": "0"},
                                                      ks["conv2_bwd"]),
         "fc1_bwd+W3 adam [padded wgrad K (28 steps)]": ({"MIHVD_F32_F1R_KW": "0"}, ks["fc1_bwd+W3 adam"]),
-        "fc1_fwd [every other sample tile per wave, W3 loaded twice]": ({"MIHVD_F32_F1F_KH": "0"}, ks["fc1_fwd"]),
         "head [256 threads, 4 features each]": ({"MIHVD_F32_HEAD1K": "0"}, ks["head"]),
         "conv2_bwd [dgrad role only, W2 fragment copy]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd [W2 fragment copy]"]),
         "conv2_fwd [W2 fragment copy, image register-staged]": ({"MIHVD_F32_C2F_DMA": "0"}, ks["conv2_fwd [W2 fragment copy]"]),
@@ -214,7 +213,6 @@ def main():
         "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
         "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
         "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
-        "whole step [fc1_fwd W3 loaded twice per block]": ({}, {"MIHVD_F32_F1F_KH": "0"}),
         "whole step [256-thread head]": ({}, {"MIHVD_F32_HEAD1K": "0"}),
         "whole step [conv2_fwd image register-staged]": ({}, {"MIHVD_F32_C2F_DMA": "0"}),
         "whole step [conv2 wgrad next image register-staged]": ({}, {"MIHVD_F32_C2B_WMID": "2"}),
