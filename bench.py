@@ -304,7 +304,8 @@ def main():
     # communicator (one 4-byte allreduce on the current stream, then synchronize: ~10 us of RCCL
     # latency inside the timed region instead of the process group's barrier, which adds its own
     # stream hop and host wait), elsewhere hvd.barrier()
-    comm = getattr(tr, "ncomm", None) if args.impl == "fused" and n > 1 else None
+    forced = os.environ.get("MIHVD_FORCE_COLLECTIVES") == "1"  # (world 1 with collectives: the same path)
+    comm = getattr(tr, "ncomm", None) if args.impl == "fused" and (n > 1 or forced) else None
     if comm is not None:
         token = torch.zeros(1, dtype=torch.float32, device=device)
 
