@@ -147,45 +147,28 @@ __device__ __forceinline__ float f32_ld(const float* p) {
   if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else return *p;
 }
-// xn / xtag (optional, with rows and state): the batch's images gathered ahead into xn [B][784] by
-// the previous step's head launch (f32_gather_x_block), valid for the step number in *xtag. Their
-// loads are issued beside the step counter's and the tag's, so the image costs one memory round
-// trip instead of three dependent ones (counter -> rows -> x); on a tag mismatch (the first step,
-// a counter written by the host) the block falls back to the gather through rows.
 template <bool COH>
 __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __restrict__ x, const int* __restrict__ rows,
                                                 int n_pool, const int64_t* state, const float* w1, const float* b1,
-                                                float* __restrict__ a1, uint8_t* __restrict__ idx1, int B, float* xim,
-                                                const float* __restrict__ xn = nullptr,
-                                                const int64_t* __restrict__ xtag = nullptr) {
+                                                float* __restrict__ a1, uint8_t* __restrict__ idx1, int B, float* xim) {
   const int t = threadIdx.x;
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
-  auto load_img = [&](const float* xi, float (&xv)[4]) {
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int i = t + 256 * it, Y = (i >> 5) - 2, X = (i & 31) - 2;
-      const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
-      xv[it] = mask_f(xi[in ? Y * 28 + X : 0], in);
+  int row = b;
+  if (rows != nullptr) {
+    int64_t step = 0;
+    if (state) {
+      if constexpr (COH) step = __hip_atomic_load(state + ST_FWD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else step = state[ST_FWD];
     }
-  };
-  float xv[4];
-  int64_t step = 0;
-  bool have = false;
-  if (rows != nullptr && state != nullptr && xn != nullptr) {
-    load_img(xn + (int64_t)b * 784, xv);  // speculative: in flight beside the counter and the tag
-    step = state[ST_FWD];
-    have = *xtag == step;
+    row = rows[(int)((step * (int64_t)B + b) % n_pool)];
   }
-  if (!have) {  // block-uniform
-    int row = b;
-    if (rows != nullptr) {
-      if (state && xn == nullptr) {
-        if constexpr (COH) step = __hip_atomic_load(state + ST_FWD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else step = state[ST_FWD];
-      }
-      row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-    }
-    load_img(x + (int64_t)row * 784, xv);
+  const float* xi = x + (int64_t)row * 784;
+  float xv[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int i = t + 256 * it, Y = (i >> 5) - 2, X = (i & 31) - 2;
+    const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
+    xv[it] = mask_f(xi[in ? Y * 28 + X : 0], in);
   }
   float wb[2][7];
   int toff[7];

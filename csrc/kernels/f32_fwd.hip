@@ -75,8 +75,7 @@ __device__ __forceinline__ void f32_w2_frag_block(int blk, const float* __restri
 __global__ void __launch_bounds__(256) f32_conv1_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ a1, uint8_t* __restrict__ idx1,
-    int B, const float* __restrict__ w2, float* __restrict__ w2f, const float* __restrict__ xn,
-    const int64_t* __restrict__ xtag) {
+    int B, const float* __restrict__ w2, float* __restrict__ w2f) {
   __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
   const int id = blockIdx.x;
   if (id >= 4 * B) {
@@ -87,30 +86,7 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
   // the images whose conv2_fwd blocks run on XCD x (same mapping there), so conv2_fwd's staging
   // reads hit that XCD's L2 instead of the MALL
   const int L = xcd_contiguous(id, 0, 4 * B);
-  f32_conv1_block<false>(L & 3, L >> 2, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim, xn, xtag);
-}
-
-// The batch of step `step` gathered from the resident dataset into xn [B][784] (one float4 per
-// thread, blocks [0, nblk) of a launch); thread 0 of block 0 records the step in *xtag. Run by extra
-// blocks of the head launch for the next step (the head is B blocks on a chip of 256 CUs: the
-// gather takes otherwise idle CUs), and standalone after the host changed the epoch order.
-__device__ __forceinline__ void f32_gather_x_block(int blk, int nblk, const float* __restrict__ x,
-                                                   const int* __restrict__ rows, int n_pool, int64_t step, int B,
-                                                   float* __restrict__ xn, int64_t* __restrict__ xtag) {
-  const int n4 = B * 196;
-  for (int i = blk * (int)blockDim.x + (int)threadIdx.x; i < n4; i += nblk * (int)blockDim.x) {
-    const int b = i / 196, c = i - 196 * b;
-    const int row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-    reinterpret_cast<float4*>(xn)[i] = reinterpret_cast<const float4*>(x + (int64_t)row * 784)[c];
-  }
-  if (blk == 0 && threadIdx.x == 0) *xtag = step;
-}
-
-__global__ void __launch_bounds__(256) f32_gather_x_kernel(const float* __restrict__ x, const int* __restrict__ rows,
-                                                           int n_pool, const int64_t* __restrict__ state, int ahead,
-                                                           int B, float* __restrict__ xn, int64_t* __restrict__ xtag) {
-  const int64_t step = (state ? state[ST_FWD] : 0) + ahead;
-  f32_gather_x_block(blockIdx.x, gridDim.x, x, rows, n_pool, step, B, xn, xtag);
+  f32_conv1_block<false>(L & 3, L >> 2, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -441,15 +417,11 @@ __global__ void __launch_bounds__(256) f32_head_kernel(
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
     float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B,
-    float* __restrict__ stats_acc, const float* __restrict__ xsrc, float* __restrict__ xn, int64_t* __restrict__ xtag) {
+    float* __restrict__ stats_acc) {
   __shared__ float red[4][10];
   __shared__ float dl[10];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t step = state ? state[ST_FWD] : 0;
-  if (b >= B) {  // blocks past the batch: the next step's images (xn != nullptr only)
-    f32_gather_x_block(b - B, gridDim.x - B, xsrc, rows, n_pool, step + 1, B, xn, xtag);
-    return;
-  }
   const int n0 = t * 4;
   float4 parts[F1F_KS];
 #pragma unroll
@@ -544,15 +516,11 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
     float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B,
-    float* __restrict__ stats_acc, const float* __restrict__ xsrc, float* __restrict__ xn, int64_t* __restrict__ xtag) {
+    float* __restrict__ stats_acc) {
   __shared__ float red[16][10];
   __shared__ float dl[10];
   const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = __builtin_amdgcn_readfirstlane(n >> 6);
   const int64_t step = state ? state[ST_FWD] : 0;
-  if (b >= B) {  // blocks past the batch: the next step's images (xn != nullptr only)
-    f32_gather_x_block(b - B, gridDim.x - B, xsrc, rows, n_pool, step + 1, B, xn, xtag);
-    return;
-  }
   float parts[F1F_KS];
 #pragma unroll
   for (int s = 0; s < F1F_KS; ++s) parts[s] = zpart[((int64_t)s * B + b) * 1024 + n];
@@ -641,8 +609,7 @@ static const int* rows_ptr(const c10::optional<at::Tensor>& rows, int n_pool, in
 
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
-                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag,
-                   const c10::optional<at::Tensor>& x_next, const c10::optional<at::Tensor>& x_tag) {
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag) {
   const int B = a1.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv1_fwd: batch 1..128");
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv1_fwd: x");
@@ -660,46 +627,9 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
     check_f32(*w2, 51200, "f32_conv1_fwd: w2");
     check_f32(*w2frag, 2 * 51200, "f32_conv1_fwd: w2frag [2][51200]");
   }
-  // x_next + x_tag (with rows and state): the images the previous step's head gathered ahead
-  const float* xn = nullptr;
-  const int64_t* xt = nullptr;
-  if (x_next.has_value() && x_next->defined()) {
-    TORCH_CHECK(rp != nullptr && sp != nullptr, "f32_conv1_fwd: x_next needs rows and state");
-    check_f32(*x_next, (int64_t)B * 784, "f32_conv1_fwd: x_next [B][784]");
-    TORCH_CHECK(x_tag.has_value() && x_tag->defined() && x_tag->dtype() == at::kLong && x_tag->numel() >= 1 &&
-                    x_tag->is_cuda(), "f32_conv1_fwd: x_tag (int64 device word)");
-    xn = x_next->data_ptr<float>();
-    xt = x_tag->data_ptr<int64_t>();
-  }
   f32_conv1_kernel<<<dim3(4 * B + (frag ? 4 * W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
       x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(), b1.data_ptr<float>(), a1.data_ptr<float>(),
-      idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr,
-      xn, xt);
-}
-
-// checks of the resident dataset / gather-ahead buffer pair; returns the image count
-static int check_gather(const at::Tensor& x, const int* rp, const at::Tensor& xn, const at::Tensor& xtag, int B,
-                        const char* what) {
-  TORCH_CHECK(rp != nullptr, what, ": the gather ahead needs rows");
-  TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.dim() == 2 && x.size(1) == 784 &&
-                  ((uintptr_t)x.data_ptr() & 15) == 0, what, ": x must be a 16-byte aligned fp32 [n][784] tensor");
-  check_f32(xn, (int64_t)B * 784, what);
-  TORCH_CHECK(((uintptr_t)xn.data_ptr() & 15) == 0, what, ": x_next must be 16-byte aligned");
-  TORCH_CHECK(xtag.is_cuda() && xtag.dtype() == at::kLong && xtag.numel() >= 1, what, ": x_tag (int64 device word)");
-  return (int)x.size(0);
-}
-
-void f32_gather_x(const at::Tensor& x, const at::Tensor& rows, const c10::optional<at::Tensor>& state,
-                  at::Tensor& x_next, at::Tensor& x_tag, int64_t ahead) {
-  const int B = x_next.numel() / 784;
-  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_gather_x: batch 1..128");
-  const int n_pool = x.size(0);
-  const int* rp = rows_ptr(rows, n_pool, B, "f32_gather_x");
-  check_gather(x, rp, x_next, x_tag, B, "f32_gather_x");
-  const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
-  auto stream = c10::hip::getCurrentHIPStream().stream();
-  f32_gather_x_kernel<<<(B * 196 + 255) / 256, 256, 0, stream>>>(x.data_ptr<float>(), rp, n_pool, sp, (int)ahead, B,
-                                                                  x_next.data_ptr<float>(), x_tag.data_ptr<int64_t>());
+      idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr);
 }
 
 // tiles per block of f32_conv2_fwd for batch B (about one block per CU), and the block count
@@ -801,9 +731,7 @@ void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) 
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
-                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc,
-                      const c10::optional<at::Tensor>& x_src, const c10::optional<at::Tensor>& x_next,
-                      const c10::optional<at::Tensor>& x_tag) {
+                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc) {
   const int B = h.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_head: batch 1..128");
   check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_head: zpart");
@@ -828,29 +756,11 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   const float keep_scale = rate > 0.0 ? (float)(1.0 / (1.0 - rate)) : 1.f;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   // MIHVD_F32_HEAD1K=0: the 256-thread form (4 features per thread)
-  const bool k1 = env_knob("MIHVD_F32_HEAD1K", 1) != 0;
-  auto kern = k1 ? f32_head1k_kernel : f32_head_kernel;
-  const int nthr = k1 ? 1024 : 256;
-  // x_src + x_next + x_tag: blocks past the batch gather the next step's images (f32_conv1_fwd's x_next)
-  int ngath = 0;
-  const float* xs = nullptr;
-  float* xn = nullptr;
-  int64_t* xt = nullptr;
-  if (x_next.has_value() && x_next->defined()) {
-    TORCH_CHECK(x_src.has_value() && x_src->defined() && x_tag.has_value() && x_tag->defined(),
-                "f32_head: x_next needs x_src and x_tag");
-    TORCH_CHECK(sp != nullptr, "f32_head: the gather ahead needs the step state");
-    TORCH_CHECK(check_gather(*x_src, rp, *x_next, *x_tag, B, "f32_head") == n_pool,
-                "f32_head: x_src rows must match the labels");
-    ngath = (B * 196 + nthr - 1) / nthr;
-    xs = x_src->data_ptr<float>();
-    xn = x_next->data_ptr<float>();
-    xt = x_tag->data_ptr<int64_t>();
-  }
-  kern<<<B + ngath, nthr, 0, stream>>>(
+  auto kern = env_knob("MIHVD_F32_HEAD1K", 1) != 0 ? f32_head1k_kernel : f32_head_kernel;
+  kern<<<B, env_knob("MIHVD_F32_HEAD1K", 1) != 0 ? 1024 : 256, 0, stream>>>(
       zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(), b4.data_ptr<float>(),
       labels.data_ptr<int64_t>(), rp, n_pool, sp, (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(),
-      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc, xs, xn, xt);
+      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc);
 }
 
 }  // namespace mihvd

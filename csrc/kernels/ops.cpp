@@ -85,19 +85,14 @@ void multi_tensor_sgd(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std:
 void bump_step_(at::Tensor& step);
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
-                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag,
-                   const c10::optional<at::Tensor>& x_next, const c10::optional<at::Tensor>& x_tag);
-void f32_gather_x(const at::Tensor& x, const at::Tensor& rows, const c10::optional<at::Tensor>& state,
-                  at::Tensor& x_next, at::Tensor& x_tag, int64_t ahead);
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag);
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
                    const c10::optional<at::Tensor>& w2frag);
 void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
-                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc,
-                      const c10::optional<at::Tensor>& x_src, const c10::optional<at::Tensor>& x_next,
-                      const c10::optional<at::Tensor>& x_tag);
+                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc);
 void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
                  const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
                  at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
@@ -290,12 +285,8 @@ void mt_sgd_op(at::TensorList p, at::TensorList g, at::TensorList bufs, double l
 }
 void bump_step_op(Tensor step) { mihvd::bump_step_(step); }
 void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
-                  Tensor idx1, const OptT& w2, const OptT& w2frag, const OptT& x_next, const OptT& x_tag) {
-  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag, x_next, x_tag);
-}
-void f32_gather_x_op(const Tensor& x, const Tensor& rows, const OptT& state, Tensor x_next, Tensor x_tag,
-                     int64_t ahead) {
-  mihvd::f32_gather_x(x, rows, state, x_next, x_tag, ahead);
+                  Tensor idx1, const OptT& w2, const OptT& w2frag) {
+  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag);
 }
 void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& w2frag) {
   mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, w2frag);
@@ -303,9 +294,8 @@ void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a
 void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
-                 Tensor stats, const OptT& stats_acc, const OptT& x_src, const OptT& x_next, const OptT& x_tag) {
-  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, stats_acc, x_src,
-                          x_next, x_tag);
+                 Tensor stats, const OptT& stats_acc) {
+  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, stats_acc);
 }
 void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, const Tensor& h, const Tensor& dlog,
                     Tensor w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, const OptT& m3,
@@ -394,13 +384,12 @@ TORCH_LIBRARY(mihvd, m) {
         "float weight_decay, bool nesterov, bool first, float grad_scale) -> ()");
   m.def("bump_step_(Tensor(a!) step) -> ()");
   m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
-        "Tensor? w2=None, Tensor(f!)? w2frag=None, Tensor? x_next=None, Tensor? x_tag=None) -> ()");
-  m.def("f32_gather_x(Tensor x, Tensor rows, Tensor? state, Tensor(a!) x_next, Tensor(b!) x_tag, int ahead=0) -> ()");
+        "Tensor? w2=None, Tensor(f!)? w2frag=None) -> ()");
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
-        "Tensor(e!)? stats_acc=None, Tensor? x_src=None, Tensor(f!)? x_next=None, Tensor(g!)? x_tag=None) -> ()");
+        "Tensor(e!)? stats_acc=None) -> ()");
   m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor(w!) w3, Tensor(a!) dY2, "
         "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4, Tensor(m!)? m3=None, "
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
@@ -460,7 +449,6 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("multi_tensor_sgd", &mt_sgd_op);
   m.impl("bump_step_", &bump_step_op);
   m.impl("f32_conv1_fwd", &f32_conv1_op);
-  m.impl("f32_gather_x", &f32_gather_x_op);
   m.impl("f32_factor_rows", &f32_factor_rows_op);
   m.impl("f32_conv2_fwd", &f32_conv2_op);
   m.impl("f32_fc1_fwd", &f32_fc1_fwd_op);

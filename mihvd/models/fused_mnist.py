@@ -351,15 +351,6 @@ class FusedMNISTTrainer:
         # (B = 100): conv2_fwd 21.2 -> 19.8 us, conv2_bwd 43.8 -> 40.5 us, whole step 124.7 -> 122.4 us
         # (profiles/r04/kbench_f32_r04m.txt); bitwise equal
         self.w2frag = torch.empty(2, 51200, device=dev, dtype=torch.float32) if self.f32 else None
-        # fp32 step on the resident dataset: the head launch's spare blocks gather the NEXT step's
-        # images into x_next (tagged with that step number), so conv1 loads its image in one round
-        # trip instead of the dependent counter -> rows -> x chain; a stale tag (first step, counter
-        # written by the host) falls back to the chain, and a new epoch order re-gathers.
-        # MIHVD_F32_XNEXT=0: off
-        self.x_next = self.x_tag = None
-        if self.f32 and os.environ.get("MIHVD_F32_XNEXT", "1") != "0":
-            self.x_next = torch.empty(B, 784, device=dev, dtype=torch.float32)
-            self.x_tag = torch.full((1,), -1, device=dev, dtype=torch.int64)
         self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when it is fused away
         self.f32_factor = False
         if self.f32:
@@ -500,13 +491,6 @@ class FusedMNISTTrainer:
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._pin_ev[i] = ev
-        self._regather_x()
-
-    def _regather_x(self):
-        """The current step's images in the new epoch order into x_next (stream-ordered behind the
-        order's copy; the step number in x_tag already matches, so the tag alone cannot tell)."""
-        if self.x_next is not None and self.X is not None and self.rows is not None and self.rows.is_cuda:
-            self.ops.f32_gather_x(self.X, self.rows, self.state, self.x_next, self.x_tag, 0)
 
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
@@ -594,11 +578,8 @@ class FusedMNISTTrainer:
             main.wait_event(self._small_ev)
             self._small_ev = None
         wf = self.w2frag
-        # the resident dataset: conv1 reads the images the previous step's head gathered ahead
-        ahead = self.x_next is not None and rows is not None and x is self.X
-        xn = dict(x_next=self.x_next, x_tag=self.x_tag) if ahead else {}
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                        self.idx1, w2, wf, **xn)
+                        self.idx1, w2, wf)
         o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0])
         if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
@@ -606,9 +587,8 @@ class FusedMNISTTrainer:
         o.f32_fc1_fwd(self.a2, w3, self.zpart)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
-                           stats_acc=self._stat_acc if self.track_stats else None,
-                           **(dict(x_src=x, **xn) if ahead else {}))
-        gconv =(G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
+                           stats_acc=self._stat_acc if self.track_stats else None)
+        gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
                  G("conv_layer2/conv2d/bias"))
         if not self.collectives:
             # dgrad, dW3 and dense/kernel's Adam from one read of W3 (dW3 stays in registers unless
@@ -1489,7 +1469,6 @@ class FusedMNISTTrainer:
         if "rows" in snap and self.rows is not None:
             self.rows.copy_(snap["rows"])
             self._rng.bit_generator.state = snap["rng"]
-            self._regather_x()
         self.global_step = snap["global_step"]
         self._full_state_valid = True
         self._refresh_shadow()  # (and the full W3 row shadow of the factor-gather plane)
