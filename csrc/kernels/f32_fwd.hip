@@ -55,10 +55,9 @@ void f32_fwd_stamps_set(unsigned long long* p) {
 //   bwd [wave 8][tap][lane][j]     = W2[tap][16 (wave & 1) + lr][16 (wave >> 1) + 4 lg + j]
 constexpr int W2F_F4 = 12800;                     // float4 per copy
 constexpr int W2F_BLOCKS_Y = 7;                   // extra grid rows of the conv1 launch (4 x 7 blocks)
-__device__ __forceinline__ void f32_w2_frag_block(int blk, int nblk, const float* __restrict__ w2,
-                                                  float* __restrict__ w2f) {
+__device__ __forceinline__ void f32_w2_frag_block(int blk, const float* __restrict__ w2, float* __restrict__ w2f) {
   float4* out = reinterpret_cast<float4*>(w2f);
-  for (int i = blk * 256 + (int)threadIdx.x; i < 2 * W2F_F4; i += nblk * 256) {
+  for (int i = blk * 256 + (int)threadIdx.x; i < 2 * W2F_F4; i += 4 * W2F_BLOCKS_Y * 256) {
     float4 v;
     if (i < W2F_F4) {
       const int lane = i & 63, wave = (i >> 6) & 3, c2 = (i >> 8) & 1, tap = i >> 9;
@@ -80,7 +79,7 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
   __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
   const int id = blockIdx.x;
   if (id >= 4 * B) {
-    f32_w2_frag_block(id - 4 * B, gridDim.x - 4 * B, w2, w2f);
+    f32_w2_frag_block(id - 4 * B, w2, w2f);
     return;
   }
   // XCD-contiguous (image, quarter) order: XCD x writes the a1 rows of images [B x / 8, B (x + 1) / 8),
@@ -628,9 +627,9 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
     check_f32(*w2, 51200, "f32_conv1_fwd: w2");
     check_f32(*w2frag, 2 * 51200, "f32_conv1_fwd: w2frag [2][51200]");
   }
-  // study knob MIHVD_F32_W2F_BLOCKS: blocks of the fragment copies (100: one float4 per thread)
-  const int nfb = frag ? std::max(1, std::min(100, (int)env_knob("MIHVD_F32_W2F_BLOCKS", 4 * W2F_BLOCKS_Y))) : 0;
-  f32_conv1_kernel<<<dim3(4 * B + nfb), 256, 0, stream>>>(
+  // (100 fragment blocks, one float4 per thread, measured the same: conv1 7.16 us, whole step
+  // 117.6-119.1 us either way, profiles/r05/bench_w2f_blocks_ab_r05s.txt)
+  f32_conv1_kernel<<<dim3(4 * B + (frag ? 4 * W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
       x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(), b1.data_ptr<float>(), a1.data_ptr<float>(),
       idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr);
 }
