@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   if (bid >= F1R_BLOCKS) {
-    if constexpr (HD) f32_head_wait(hd.bar, B, hd.fence);
+    if constexpr (HD) f32_head_wait(hd.bar, B);
     f32_fc1_small512(bid - F1R_BLOCKS, dz, h, dlog, gb3, gW4, gb4, B, smf);
     return;
   }
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
 #pragma unroll
     for (int c = 0; c < PD; ++c) load_pmv(c, c);
     if (bid < B) f32_head_block512(hd, bid, B, smf);
-    f32_head_wait(hd.bar, B, hd.fence);
+    f32_head_wait(hd.bar, B);
     if constexpr (ADAM) coef = f32_adam_coef(ad);  // the step count the head advanced
     load_z(0);
   } else {
@@ -1312,7 +1312,6 @@ void f32_fc1_bwd_head(const at::Tensor& zpart, const at::Tensor& b3, const at::T
     hd.stats_acc = stats_acc->data_ptr<float>();
   }
   hd.bar = reinterpret_cast<unsigned long long*>(bar.data_ptr<int64_t>());
-  hd.fence = (int)env_knob("MIHVD_F32_HEAD_FENCE", 3);  // study knob (0 / 1 / 2: unsafe, timing only)
   // every block of the launch must be resident at once (one per CU: F1R_LDS), or the producers'
   // own waits would hold CUs that later producers need
   int dev = 0, ncu = 0;

@@ -237,7 +237,6 @@ struct F32HeadArgs {
   float* stats_acc = nullptr;
   // [0] samples finished (all launches), [1] waiter tickets (all launches), [2] barrier timeouts
   unsigned long long* bar = nullptr;
-  int fence = 3;  // study: bit 0 the producers' release fence, bit 1 the waiters' acquire fence
 };
 
 // One sample's head (f32_head1k_kernel's math) in a 512-thread block: thread t owns features t
@@ -325,7 +324,7 @@ __device__ __forceinline__ void f32_head_block512(const F32HeadArgs& a, int b, i
   // publish: every thread's stores are ordered before thread 0's device-scope release
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (a.fence & 1) __threadfence();
+    __threadfence();
     __hip_atomic_fetch_add(&a.bar[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -335,7 +334,7 @@ __device__ __forceinline__ void f32_head_block512(const F32HeadArgs& a, int b, i
 // reset (graph replays, host-written step state). The producers are blocks [0, B): dispatched
 // first, they never wait behind a waiting block. A wait past ~2 s (a bug, not a schedule) records a
 // timeout in bar[2] and lets the block go on, instead of hanging the device.
-__device__ __forceinline__ void f32_head_wait(unsigned long long* bar, int B, int fence = 3) {
+__device__ __forceinline__ void f32_head_wait(unsigned long long* bar, int B) {
   if (threadIdx.x == 0) {
     const unsigned long long tk = __hip_atomic_fetch_add(&bar[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long target = (tk / gridDim.x + 1ull) * (unsigned long long)B;
@@ -347,7 +346,7 @@ __device__ __forceinline__ void f32_head_wait(unsigned long long* bar, int B, in
         break;
       }
     }
-    if (fence & 2) __threadfence();  // acquire: the producers' dz / h / dlog / stats and the ST_OPT bump
+    __threadfence();  // acquire: the producers' dz / h / dlog / stats and the ST_OPT bump
   }
   __syncthreads();
 }
