@@ -168,19 +168,15 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
 // KW: K steps of the wgrad chain, 4 samples each: 4 G (the padded tiles) by default, ceil(B / 4) in
 // the exact-batch instantiation (B = 100: 25 instead of 28 MFMAs per chunk; the rows past the
 // batch are zero either way).
-// HD: the head runs inside this launch (F32HeadArgs, f32_common.h): blocks [0, B) compute one
-// sample's head each, every block waits for all of them before it reads dz / h / dlog (and the Adam
-// step count the head advances); the p / m / v and a2 register prefetches are issued before.
-template <int G, bool ADAM, bool STORE, int KW = 4 * G, bool HD = false>
+template <int G, bool ADAM, bool STORE, int KW = 4 * G>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
-    const float* dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
-    const float* h, const float* dlog, float* __restrict__ w3, float* __restrict__ dY2,
+    const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
+    const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
     float* __restrict__ db2p, float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4,
-    float* __restrict__ gb4, int B, F32Adam ad, int pf, F32HeadArgs hd) {
+    float* __restrict__ gb4, int B, F32Adam ad, int pf) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   if (bid >= F1R_BLOCKS) {
-    if constexpr (HD) f32_head_wait(hd.bar, B);
     f32_fc1_small512(bid - F1R_BLOCKS, dz, h, dlog, gb3, gW4, gb4, B, smf);
     return;
   }
@@ -246,23 +242,13 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     }
   };
   AdamCoef coef{};
+  if constexpr (ADAM) coef = f32_adam_coef(ad);
   f32x4 acc[G];
 #pragma unroll
   for (int u = 0; u < G; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (HD) {
-    // W3 (and m, v) of the first chunks in flight during the head and the wait
+  load_z(0);
 #pragma unroll
-    for (int c = 0; c < PD; ++c) load_pmv(c, c);
-    if (bid < B) f32_head_block512(hd, bid, B, smf);
-    f32_head_wait(hd.bar, B);
-    if constexpr (ADAM) coef = f32_adam_coef(ad);  // the step count the head advanced
-    load_z(0);
-  } else {
-    if constexpr (ADAM) coef = f32_adam_coef(ad);
-    load_z(0);
-#pragma unroll
-    for (int c = 0; c < PD; ++c) load_pmv(c, c);
-  }
+  for (int c = 0; c < PD; ++c) load_pmv(c, c);
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     float* buf = buf0 + (c & 1) * F1R_LDS_BUF;
@@ -1173,12 +1159,11 @@ static F32Adam f32_fc1_adam(at::Tensor& w3, const c10::optional<at::Tensor>& m3,
   return a;
 }
 
-static void fc1_bwd_launch(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
-                           const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
-                           at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
-                           const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr,
-                           double beta1, double beta2, double eps, double grad_scale, int64_t rule, bool store_w3,
-                           const F32HeadArgs& hd) {
+void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
+                 const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
+                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
+                 const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr, double beta1,
+                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_bwd: batch 1..128");
   chk_f32(dz, (int64_t)B * 1024, "f32_fc1_bwd: dz");
@@ -1206,10 +1191,8 @@ static void fc1_bwd_launch(const at::Tensor& dz, const at::Tensor& a2, const at:
         dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
         dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
         gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad,
-        env_knob("MIHVD_F32_F1R_PF", 1), hd);  // 0: routing operands loaded in the epilogue (r05h: 27.98 vs 27.03 us)
+        env_knob("MIHVD_F32_F1R_PF", 1));  // 0: routing operands loaded in the epilogue (r05h: 27.98 vs 27.03 us)
   };
-  const bool head = hd.zpart != nullptr;
-  TORCH_CHECK(!head || (adam && !store_w3), "f32_fc1_bwd_head: the head runs in the fused-Adam form only");
   if (dgrad_only) {
     switch (G) {
       case 1: launch(f32_fc1_bwd_rows_kernel<1, false, false>); break;
@@ -1226,16 +1209,14 @@ static void fc1_bwd_launch(const at::Tensor& dz, const at::Tensor& a2, const at:
   // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
   // keeps the padded 28, bitwise equal: the padded steps add exact zeros)
   if (G == 7 && (B + 3) / 4 == 25 && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
-    if (head) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25, true>);
-    else if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
+    if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
     else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 25>);
     else launch(f32_fc1_bwd_rows_kernel<7, false, true, 25>);
     return;
   }
 #define F1R_CASE(GG)                                                       \
   case GG:                                                                 \
-    if (head) launch(f32_fc1_bwd_rows_kernel<GG, true, false, 4 * GG, true>); \
-    else if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>); \
+    if (adam && store_w3) launch(f32_fc1_bwd_rows_kernel<GG, true, true>); \
     else if (adam) launch(f32_fc1_bwd_rows_kernel<GG, true, false>);       \
     else launch(f32_fc1_bwd_rows_kernel<GG, false, true>);                 \
     break;
@@ -1251,76 +1232,6 @@ static void fc1_bwd_launch(const at::Tensor& dz, const at::Tensor& a2, const at:
       F1R_CASE(8)
   }
 #undef F1R_CASE
-}
-
-void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
-                 const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
-                 at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
-                 const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr, double beta1,
-                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3) {
-  fc1_bwd_launch(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4, m3, v3, state, lr, beta1, beta2, eps,
-                 grad_scale, rule, store_w3, F32HeadArgs{});
-}
-
-// The head (f32_head_fwd_bwd's outputs h, dz, dlog, stats, stats_acc) and the fc1 backward with
-// the fused dense/kernel Adam in one launch (F32HeadArgs in f32_common.h). bar: int64 [3], zeroed
-// by the caller once, then owned by this launch shape (the same B and grid every call).
-void f32_fc1_bwd_head(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
-                      const at::Tensor& labels, const c10::optional<at::Tensor>& rows, int64_t seed, double rate,
-                      at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc, at::Tensor& bar,
-                      at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, at::Tensor& h, at::Tensor& dlog,
-                      at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3, at::Tensor& gb3,
-                      at::Tensor& gW4, at::Tensor& gb4, const at::Tensor& m3, const at::Tensor& v3,
-                      const at::Tensor& state, double lr, double beta1, double beta2, double eps, double grad_scale,
-                      int64_t rule) {
-  const int B = dz.size(0);
-  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_bwd_head: batch 1..128");
-  chk_f32(zpart, (int64_t)F32_ZSLABS * B * 1024, "f32_fc1_bwd_head: zpart [14][B][1024]");
-  chk_f32(b3, 1024, "f32_fc1_bwd_head: b3");
-  chk_f32(w4, 10240, "f32_fc1_bwd_head: w4");
-  TORCH_CHECK(((uintptr_t)w4.data_ptr() & 7) == 0, "f32_fc1_bwd_head: w4 must be 8-byte aligned");
-  chk_f32(b4, 10, "f32_fc1_bwd_head: b4");
-  chk_f32(stats, (int64_t)B * 2, "f32_fc1_bwd_head: stats");
-  TORCH_CHECK(labels.is_cuda() && labels.dtype() == at::kLong && labels.is_contiguous(), "f32_fc1_bwd_head: labels int64");
-  TORCH_CHECK(bar.is_cuda() && bar.dtype() == at::kLong && bar.numel() >= 3 && bar.is_contiguous(),
-              "f32_fc1_bwd_head: bar (int64 [3] device counters)");
-  TORCH_CHECK(state.is_cuda() && state.dtype() == at::kLong && state.numel() >= 4, "f32_fc1_bwd_head: state");
-  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "f32_fc1_bwd_head: dropout rate in [0, 1)");
-  F32HeadArgs hd;
-  hd.zpart = zpart.data_ptr<float>();
-  hd.b3 = b3.data_ptr<float>();
-  hd.w4 = w4.data_ptr<float>();
-  hd.b4 = b4.data_ptr<float>();
-  hd.labels = labels.data_ptr<int64_t>();
-  hd.n_pool = (int)labels.size(0);
-  if (rows.has_value() && rows->defined()) {
-    TORCH_CHECK(rows->dtype() == at::kInt && rows->numel() == hd.n_pool, "f32_fc1_bwd_head: rows must be int32 [n_pool]");
-    hd.rows = rows->data_ptr<int>();
-  } else {
-    TORCH_CHECK(hd.n_pool >= B, "f32_fc1_bwd_head: fewer labels than the batch");
-  }
-  hd.state = state.data_ptr<int64_t>();
-  hd.seed = (uint32_t)seed;
-  hd.thresh24 = (uint32_t)(rate * 16777216.0);
-  hd.keep_scale = rate > 0.0 ? (float)(1.0 / (1.0 - rate)) : 1.f;
-  hd.h = h.data_ptr<float>();
-  hd.dz = dz.data_ptr<float>();
-  hd.dlog = dlog.data_ptr<float>();
-  hd.stats = stats.data_ptr<float>();
-  if (stats_acc.has_value() && stats_acc->defined()) {
-    chk_f32(*stats_acc, (int64_t)B * 2, "f32_fc1_bwd_head: stats_acc [B][2]");
-    hd.stats_acc = stats_acc->data_ptr<float>();
-  }
-  hd.bar = reinterpret_cast<unsigned long long*>(bar.data_ptr<int64_t>());
-  // every block of the launch must be resident at once (one per CU: F1R_LDS), or the producers'
-  // own waits would hold CUs that later producers need
-  int dev = 0, ncu = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  TORCH_CHECK(ncu >= F1R_BLOCKS + F1B_SMALL, "f32_fc1_bwd_head: needs ", F1R_BLOCKS + F1B_SMALL,
-              " CUs for its grid wait, the device has ", ncu);
-  fc1_bwd_launch(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4, m3, v3, state, lr, beta1, beta2, eps,
-                 grad_scale, rule, false, hd);
 }
 
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,

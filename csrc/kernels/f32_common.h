@@ -211,146 +211,6 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
   }
 }
 
-// ------------------------------------------------------------------------------------------ //
-// The head inside the fc1 backward launch (f32_fc1_bwd_rows_kernel<..., HD = true>): its first B
-// row blocks each run one sample's head before their rows, every block of the launch then waits
-// for all B samples (a one-way, ticketed grid barrier) before it reads dz / h / dlog. The fc1
-// backward's own prologue (its p / m / v / a2 register prefetches, 9 MB from HBM) is in flight
-// during the head instead of after a separate head launch.
-constexpr int F32_ZSLABS = 14;  // fc1_fwd's split-K slabs (F1F_KS in f32_fwd.hip)
-
-struct F32HeadArgs {
-  const float* zpart = nullptr;  // nullptr: no head in this launch
-  const float* b3 = nullptr;
-  const float* w4 = nullptr;
-  const float* b4 = nullptr;
-  const int64_t* labels = nullptr;
-  const int* rows = nullptr;
-  int n_pool = 0;
-  int64_t* state = nullptr;
-  uint32_t seed = 0, thresh24 = 0;
-  float keep_scale = 1.f;
-  float* h = nullptr;
-  float* dz = nullptr;
-  float* dlog = nullptr;
-  float* stats = nullptr;
-  float* stats_acc = nullptr;
-  // [0] samples finished (all launches), [1] waiter tickets (all launches), [2] barrier timeouts
-  unsigned long long* bar = nullptr;
-};
-
-// One sample's head (f32_head1k_kernel's math) in a 512-thread block: thread t owns features t
-// and t + 512, so wave w's two 64-feature groups are the 1024-thread head's waves w and w + 8 —
-// the same wave sums in the same fixed order, bit for bit. lds: 170 floats.
-__device__ __forceinline__ void f32_head_block512(const F32HeadArgs& a, int b, int B, float* lds) {
-  float* red = lds;       // [16][10]
-  float* dl = lds + 160;  // [10]
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int64_t step = a.state ? a.state[ST_FWD] : 0;
-  float parts[2][F32_ZSLABS], w[2][10], bias[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int n = t + 512 * k;
-#pragma unroll
-    for (int s = 0; s < F32_ZSLABS; ++s) parts[k][s] = a.zpart[((int64_t)s * B + b) * 1024 + n];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      const float2 v = reinterpret_cast<const float2*>(a.w4 + n * 10)[q];
-      w[k][2 * q] = v.x;
-      w[k][2 * q + 1] = v.y;
-    }
-    bias[k] = a.b3[n];
-  }
-  int y = 0;
-  if (wave == 0) {
-    int row = b;
-    if (a.rows != nullptr) row = a.rows[(int)((step * (int64_t)B + b) % a.n_pool)];
-    y = (int)a.labels[row];
-  }
-  float hv[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int n = t + 512 * k;
-    float z = bias[k];
-#pragma unroll
-    for (int s = 0; s < F32_ZSLABS; ++s) z += parts[k][s];
-    const bool keep = a.thresh24 == 0 || dropout_keep(a.seed, (uint32_t)step, (uint32_t)(b * 1024 + n), a.thresh24);
-    hv[k] = keep ? fmaxf(z, 0.f) * a.keep_scale : 0.f;
-    a.h[(int64_t)b * 1024 + n] = hv[k];
-#pragma unroll
-    for (int c = 0; c < 10; ++c) {
-      const float sc = wave_sum(hv[k] * w[k][c]);
-      if (lane == 0) red[(wave + 8 * k) * 10 + c] = sc;
-    }
-  }
-  __syncthreads();
-  if (wave == 0) {
-    const int c = min(lane, 9);
-    float acc = 0.f;
-#pragma unroll
-    for (int q = 0; q < 16; q += 2) acc += red[q * 10 + c] + red[(q + 1) * 10 + c];
-    const float lgt = acc + a.b4[c];
-    const float v = lane < 10 ? lgt : -INFINITY;
-    const float mx = wave_max(v);
-    const float e = lane < 10 ? expf(lgt - mx) : 0.f;
-    const float se = wave_sum(e);
-    const float lse = mx + logf(se);
-    const unsigned long long ismax = __ballot(lane < 10 && lgt == mx);
-    const int am = __ffsll((long long)ismax) - 1;
-    const float ly = __shfl(lgt, y, 64);
-    if (lane < 10) {
-      const float d = (expf(lgt - lse) - (lane == y ? 1.f : 0.f)) / (float)B;
-      dl[lane] = d;
-      a.dlog[b * 10 + lane] = d;
-    }
-    if (lane == 0) {
-      a.stats[b * 2 + 0] = lse - ly;
-      a.stats[b * 2 + 1] = (am == y) ? 1.f : 0.f;
-      if (a.stats_acc != nullptr) {
-        a.stats_acc[b * 2 + 0] += lse - ly;
-        a.stats_acc[b * 2 + 1] += (am == y) ? 1.f : 0.f;
-      }
-      if (b == 0 && a.state != nullptr) a.state[ST_OPT] += 1;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    float g = 0.f;
-#pragma unroll
-    for (int c = 0; c < 10; ++c) g = fmaf(dl[c], w[k][c], g);
-    a.dz[(int64_t)b * 1024 + t + 512 * k] = hv[k] > 0.f ? g * a.keep_scale : 0.f;
-  }
-  // publish: every thread's stores are ordered before thread 0's device-scope release
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    __hip_atomic_fetch_add(&a.bar[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// Every block of the launch: wait until the launch's B samples are published. Launch e (counted by
-// the tickets, gridDim.x per launch) waits for (e + 1) B finished samples, so the counters never
-// reset (graph replays, host-written step state). The producers are blocks [0, B): dispatched
-// first, they never wait behind a waiting block. A wait past ~2 s (a bug, not a schedule) records a
-// timeout in bar[2] and lets the block go on, instead of hanging the device.
-__device__ __forceinline__ void f32_head_wait(unsigned long long* bar, int B) {
-  if (threadIdx.x == 0) {
-    const unsigned long long tk = __hip_atomic_fetch_add(&bar[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long target = (tk / gridDim.x + 1ull) * (unsigned long long)B;
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(&bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > 200000000ull) {  // 100 MHz constant clock: 2 s
-        __hip_atomic_store(&bar[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __threadfence();  // acquire: the producers' dz / h / dlog / stats and the ST_OPT bump
-  }
-  __syncthreads();
-}
-
 // A 256-byte zero line in device memory (one per device), the source of the padding chunks of
 // LDS-DMA staging (global_load_lds cannot mask a lane: a padding lane reads zeros instead). Created
 // on the first call outside a stream capture; nullptr while capturing before that (callers then

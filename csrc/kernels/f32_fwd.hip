@@ -315,7 +315,6 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
 // (lr, lg) at slot 58 lr + lg covers 16 distinct slots in each 16-lane group (scripts/ldssim_conv2.py
 // model: 1.0 LDS cycles per group; 228 gave 2.0, PMC LDS_BANK_CONFLICT 1.7x the active LDS cycles)
 constexpr int F1F_KS = 14, F1F_KSL = 224, F1F_AS = 232;
-static_assert(F1F_KS == F32_ZSLABS, "the head inside the fc1 backward launch sums the same slabs");
 constexpr int F1F_LDS = 128 * F1F_AS * 4;  // 118,784 B
 
 // MFMA core: a wave's NT tiles (sh, sh + 2, ...) are interleaved element-outer, tile-inner, so

@@ -98,14 +98,6 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
                  at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
                  const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr, double beta1,
                  double beta2, double eps, double grad_scale, int64_t rule, bool store_w3);
-void f32_fc1_bwd_head(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
-                      const at::Tensor& labels, const c10::optional<at::Tensor>& rows, int64_t seed, double rate,
-                      at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc, at::Tensor& bar,
-                      at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, at::Tensor& h, at::Tensor& dlog,
-                      at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3, at::Tensor& gb3,
-                      at::Tensor& gW4, at::Tensor& gb4, const at::Tensor& m3, const at::Tensor& v3,
-                      const at::Tensor& state, double lr, double beta1, double beta2, double eps, double grad_scale,
-                      int64_t rule);
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag);
@@ -312,15 +304,6 @@ void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, cons
   mihvd::f32_fc1_bwd(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4, m3, v3, state, lr, beta1, beta2, eps,
                      grad_scale, rule, store_w3);
 }
-void f32_fc1_bwd_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4,
-                         const Tensor& labels, const OptT& rows, int64_t seed, double rate, Tensor stats,
-                         const OptT& stats_acc, Tensor bar, Tensor dz, const Tensor& a2, const Tensor& idx2, Tensor h,
-                         Tensor dlog, Tensor w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4,
-                         Tensor gb4, Tensor m3, Tensor v3, Tensor state, double lr, double beta1, double beta2,
-                         double eps, double grad_scale, int64_t rule) {
-  mihvd::f32_fc1_bwd_head(zpart, b3, w4, b4, labels, rows, seed, rate, stats, stats_acc, bar, dz, a2, idx2, h, dlog,
-                          w3, dY2, db2p, gW3, gb3, gW4, gb4, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule);
-}
 void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, const Tensor& idx1, const Tensor& x,
                       const OptT& rows, const OptT& state, Tensor cpart, Tensor slab, const OptT& w2frag) {
   mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab, w2frag);
@@ -411,11 +394,6 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4, Tensor(m!)? m3=None, "
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0, bool store_w3=True) -> ()");
-  m.def("f32_fc1_bwd_head(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, int seed, "
-        "float rate, Tensor(s!) stats, Tensor(e!)? stats_acc, Tensor(k!) bar, Tensor(z!) dz, Tensor a2, Tensor idx2, "
-        "Tensor(h!) h, Tensor(l!) dlog, Tensor(w!) w3, Tensor(a!) dY2, Tensor(b!) db2p, Tensor(c!) gW3, "
-        "Tensor(d!) gb3, Tensor(f!) gW4, Tensor(g!) gb4, Tensor(m!) m3, Tensor(v!) v3, Tensor(t!) state, float lr, "
-        "float beta1, float beta2, float eps, float grad_scale=1., int rule=0) -> ()");
   m.def("f32_factor_rows(Tensor a2c, Tensor dz, Tensor(a!)? out=None, Tensor(b!)? p=None, Tensor(c!)? m=None, "
         "Tensor(d!)? v=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0) -> ()");
@@ -476,7 +454,6 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("f32_fc1_fwd", &f32_fc1_fwd_op);
   m.impl("f32_head_fwd_bwd", &f32_head_op);
   m.impl("f32_fc1_bwd", &f32_fc1_bwd_op);
-  m.impl("f32_fc1_bwd_head", &f32_fc1_bwd_head_op);
   m.impl("f32_conv2_bwd", &f32_conv2_bwd_op);
   m.impl("f32_conv_reduce", &f32_conv_reduce_op);
   m.impl("scale_cast_bf16", &scale_cast_op);

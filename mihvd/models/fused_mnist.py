@@ -351,12 +351,6 @@ class FusedMNISTTrainer:
         # (B = 100): conv2_fwd 21.2 -> 19.8 us, conv2_bwd 43.8 -> 40.5 us, whole step 124.7 -> 122.4 us
         # (profiles/r04/kbench_f32_r04m.txt); bitwise equal
         self.w2frag = torch.empty(2, 51200, device=dev, dtype=torch.float32) if self.f32 else None
-        # fp32, world size 1: the head inside the fc1 backward launch (f32_fc1_bwd_head); its grid-wait
-        # counters ([done, tickets, timeouts], never reset). MIHVD_F32_HEAD_IN_F1B=0: a head launch
-        self._head_bar = None
-        if (self.f32 and os.environ.get("MIHVD_F32_HEAD_IN_F1B", "1") != "0" and dev.type == "cuda"
-                and torch.cuda.get_device_properties(dev).multi_processor_count >= 229):  # (the grid, resident)
-            self._head_bar = torch.zeros(3, device=dev, dtype=torch.int64)
         self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when it is fused away
         self.f32_factor = False
         if self.f32:
@@ -591,29 +585,18 @@ class FusedMNISTTrainer:
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None
         o.f32_fc1_fwd(self.a2, w3, self.zpart)
-        acc = self._stat_acc if self.track_stats else None
-        # world size 1: the head runs inside the fc1 backward launch (its first B blocks, then a grid
-        # wait), beside that launch's W3 / m / v prefetch
-        head_in_f1b = self._head_bar is not None and not self.collectives and not self.keep_w3_grad
-        if not head_in_f1b:
-            o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
-                               self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats, stats_acc=acc)
+        o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
+                           self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
+                           stats_acc=self._stat_acc if self.track_stats else None)
         gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
                  G("conv_layer2/conv2d/bias"))
         if not self.collectives:
             # dgrad, dW3 and dense/kernel's Adam from one read of W3 (dW3 stays in registers unless
             # keep_w3_grad); then the gradient reduction + Adam of every other parameter + the step
             # bump in one launch
-            if head_in_f1b:
-                o.f32_fc1_bwd_head(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows,
-                                   self.seed, self.dropout, self.stats, acc, self._head_bar, self.dz, self.a2,
-                                   self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
-                                   G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3], self.v[s3], st,
-                                   self.lr, b1, b2, self.eps, 1.0, self.rule)
-            else:
-                o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p,
-                              G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3],
-                              self.v[s3], st, self.lr, b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad)
+            o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3], self.v[s3], st, self.lr,
+                          b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad)
             o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
             o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv, self.params, self.grads, self.m, self.v, st,
                               SEGMENTS["conv_layer1/conv2d/kernel"][0], SEGMENTS["conv_layer1/conv2d/bias"][0],

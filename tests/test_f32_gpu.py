@@ -235,61 +235,6 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
     assert torch.equal(dY2q, dY2s) and torch.equal(db2q, db2s) and torch.equal(gW3q, gW3s)
 
 
-@pytest.mark.parametrize("B", [7, 100, 128])
-def test_f32_head_inside_fc1_bwd(ops, B):
-    """f32_fc1_bwd_head (the head run by the fc1 backward launch's first B blocks, a grid wait, then
-    the fused-Adam fc1 backward) equals the head launch followed by f32_fc1_bwd, bit for bit: h, dz,
-    dlog, stats, the epoch sums, the step count, W3 / m / v, dY2 and every small gradient. The wait's
-    counters advance by B samples and one ticket per block each call, and never time out."""
-    g = torch.Generator(device="cuda").manual_seed(21)
-    n_pool = 3 * B
-    zpart = torch.randn(14, B, 1024, device="cuda", generator=g) * 0.1
-    b3 = torch.randn(1024, device="cuda", generator=g) * 0.1
-    w4 = torch.randn(1024, 10, device="cuda", generator=g) * 0.05
-    b4 = torch.randn(10, device="cuda", generator=g) * 0.1
-    labels = torch.randint(0, 10, (n_pool,), device="cuda", generator=g)
-    rows = torch.randperm(n_pool, device="cuda", generator=g).to(torch.int32)
-    a2 = F.relu(torch.randn(B, 3136, device="cuda", generator=g))
-    idx2 = torch.randint(0, 4, (B, 3136), device="cuda", generator=g, dtype=torch.int64).to(torch.uint8)
-    w3 = torch.randn(3136, 1024, device="cuda", generator=g) * 0.02
-    m3 = torch.randn(3136, 1024, device="cuda", generator=g).abs() * 1e-3
-    v3 = torch.randn(3136, 1024, device="cuda", generator=g).abs() * 1e-5
-    st0 = torch.tensor([2, 7, 0, 0], device="cuda", dtype=torch.int64)
-
-    def outputs():
-        return dict(h=torch.full((B, 1024), float("nan"), device="cuda"),
-                    dz=torch.full((B, 1024), float("nan"), device="cuda"),
-                    dlog=torch.full((B, 10), float("nan"), device="cuda"),
-                    stats=torch.full((B, 2), float("nan"), device="cuda"), acc=torch.ones(B, 2, device="cuda"),
-                    dY2=torch.full((B, 14, 14, 64), float("nan"), device="cuda"),
-                    db2p=torch.empty(int(ops.f32_db2_rows(B)), 64, device="cuda"),
-                    gW3=torch.empty(3136, 1024, device="cuda"), gb3=torch.empty(1024, device="cuda"),
-                    gW4=torch.empty(1024, 10, device="cuda"), gb4=torch.empty(10, device="cuda"),
-                    w3=w3.clone(), m3=m3.clone(), v3=v3.clone(), st=st0.clone())
-
-    def separate(o):
-        ops.f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, o["st"], 9, 0.5, o["h"], o["dz"], o["dlog"], o["stats"],
-                             stats_acc=o["acc"])
-        ops.f32_fc1_bwd(o["dz"], a2, idx2, o["h"], o["dlog"], o["w3"], o["dY2"], o["db2p"], o["gW3"], o["gb3"],
-                        o["gW4"], o["gb4"], o["m3"], o["v3"], o["st"], 1e-3, 0.9, 0.999, 1e-8, 1.0, 0, False)
-
-    def fused(o, bar):
-        ops.f32_fc1_bwd_head(zpart, b3, w4, b4, labels, rows, 9, 0.5, o["stats"], o["acc"], bar, o["dz"], a2, idx2,
-                             o["h"], o["dlog"], o["w3"], o["dY2"], o["db2p"], o["gW3"], o["gb3"], o["gW4"], o["gb4"],
-                             o["m3"], o["v3"], o["st"], 1e-3, 0.9, 0.999, 1e-8, 1.0, 0)
-
-    ref, got = outputs(), outputs()
-    bar = torch.zeros(3, device="cuda", dtype=torch.int64)
-    for _ in range(2):  # twice: the second call's wait targets the second epoch of the counters
-        separate(ref)
-        fused(got, bar)
-        torch.cuda.synchronize()
-        for k in ref:
-            if k != "gW3":  # (the fused-Adam launches do not store dW3)
-                assert torch.equal(ref[k], got[k]), k
-    assert bar.tolist() == [2 * B, 2 * (196 + 33), 0]
-
-
 @pytest.mark.parametrize("form", ["one-round", "one-round-mepi", "one-round-mid", "one-round-late", "one-round-spread",
                                   "two-round", "two-round-mepi", "two-round-spread"])
 @pytest.mark.parametrize("B", [7, 100, 128])
@@ -505,32 +450,6 @@ def test_f32_graph_replay_converges(ops):
     assert int(tr.state[0].item()) == tr.global_step and int(tr.state[1].item()) == tr.global_step
     assert tr.last_loss() < first * 0.5, (first, tr.last_loss())
     assert tr.last_accuracy() > 0.8
-
-
-def test_f32_trainer_head_inside_fc1_bwd_is_bitwise(ops, monkeypatch):
-    """The default world-1 step (the head inside the fc1 backward launch) trains bit for bit as the
-    form with a head launch (MIHVD_F32_HEAD_IN_F1B=0), eager and graph-replayed, with dropout."""
-    from mihvd.models.fused_mnist import FusedMNISTTrainer
-    from mihvd.utils.data import synthetic_mnist
-
-    (x, y), _ = synthetic_mnist(n_train=600, n_test=10, seed=8)
-    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
-    Y = torch.from_numpy(y.astype("int64")).cuda()
-    trs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("MIHVD_F32_HEAD_IN_F1B", flag)
-        tr = FusedMNISTTrainer(batch_size=100, lr=1e-3, seed=0, device="cuda", precision="fp32")
-        tr.set_device_dataset(X, Y)
-        trs.append(tr)
-    a, b = trs
-    assert a._head_bar is not None and b._head_bar is None
-    for tr in trs:
-        tr.device_step()
-        tr.run_steps(9, steps_per_replay=4)
-    torch.cuda.synchronize()
-    assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
-    assert torch.equal(a.state, b.state) and torch.equal(a.stats, b.stats)
-    assert int(a._head_bar[2].item()) == 0
 
 
 def _f32_head_mask(ops, B, step, seed, rate=0.5):
