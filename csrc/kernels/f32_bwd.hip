@@ -168,26 +168,7 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
 // KW: K steps of the wgrad chain, 4 samples each: 4 G (the padded tiles) by default, ceil(B / 4) in
 // the exact-batch instantiation (B = 100: 25 instead of 28 MFMAs per chunk; the rows past the
 // batch are zero either way).
-// NT (study): bit 0 the p / m / v loads, bit 1 the W3 / m / v stores as non-temporal (streaming)
-// accesses, so the 38.5 MB streamed through the launch do not fill the XCDs' L2s with lines the
-// kernel-end writeback then flushes and that evict the reused dz / a2 lines
-typedef float f32v4 __attribute__((ext_vector_type(4)));
-template <bool NTL>
-__device__ __forceinline__ float4 f1r_ld4(const float* p) {
-  if constexpr (NTL) {
-    const f32v4 v = __builtin_nontemporal_load(reinterpret_cast<const f32v4*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-  } else {
-    return *reinterpret_cast<const float4*>(p);
-  }
-}
-template <bool NTS>
-__device__ __forceinline__ void f1r_st4(float* p, const float4& v) {
-  if constexpr (NTS) __builtin_nontemporal_store(f32v4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32v4*>(p));
-  else *reinterpret_cast<float4*>(p) = v;
-}
-
-template <int G, bool ADAM, bool STORE, int KW = 4 * G, int NT = 0>
+template <int G, bool ADAM, bool STORE, int KW = 4 * G>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
@@ -254,10 +235,10 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   float4 pv[NS], mv[NS], vv[NS];
   auto load_pmv = [&](int c, int slot) {
     const int64_t o = rowo + 16 * c;
-    pv[slot] = f1r_ld4<(NT & 1) != 0>(w3 + o);
+    pv[slot] = *reinterpret_cast<const float4*>(w3 + o);
     if constexpr (ADAM) {
-      mv[slot] = f1r_ld4<(NT & 1) != 0>(ad.m + o);
-      vv[slot] = f1r_ld4<(NT & 1) != 0>(ad.v + o);
+      mv[slot] = *reinterpret_cast<const float4*>(ad.m + o);
+      vv[slot] = *reinterpret_cast<const float4*>(ad.v + o);
     }
   };
   AdamCoef coef{};
@@ -314,9 +295,9 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     if constexpr (ADAM) {
       float4 pp = p, mm = mv[s3], vq = vv[s3];
       adam4_f32(pp, mm, vq, gg, coef);
-      f1r_st4<(NT & 2) != 0>(w3 + o, pp);
-      f1r_st4<(NT & 2) != 0>(ad.m + o, mm);
-      f1r_st4<(NT & 2) != 0>(ad.v + o, vq);
+      *reinterpret_cast<float4*>(w3 + o) = pp;
+      *reinterpret_cast<float4*>(ad.m + o) = mm;
+      *reinterpret_cast<float4*>(ad.v + o) = vq;
     }
     f1r_stamp(1 + c);
   }
@@ -1228,11 +1209,7 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
   // keeps the padded 28, bitwise equal: the padded steps add exact zeros)
   if (G == 7 && (B + 3) / 4 == 25 && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
-    const int nt = (int)env_knob("MIHVD_F32_F1R_NT", 0);
-    if (adam && !store_w3 && nt == 1) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25, 1>);
-    else if (adam && !store_w3 && nt == 2) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25, 2>);
-    else if (adam && !store_w3 && nt == 3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25, 3>);
-    else if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
+    if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
     else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 25>);
     else launch(f32_fc1_bwd_rows_kernel<7, false, true, 25>);
     return;
