@@ -1302,7 +1302,8 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes (PREW; epilogue per MIHVD_F32_C2B_MEPI)
 #define C2B_R1(T)                                                                                        \
   case T:                                                                                                \
-    if (mepi) launch(f32_conv2_bwd_kernel<T, true, true, 2>);                                             \
+    if (mepi && w2f) launch(f32_conv2_bwd_kernel<T, true, true, 2, true>);                                \
+    else if (mepi) launch(f32_conv2_bwd_kernel<T, true, true, 2>);                                        \
     else if (w2f) launch(f32_conv2_bwd_kernel<T, true, false, 2, true>);                                  \
     else launch(f32_conv2_bwd_kernel<T, true, false, 2>);                                                 \
     break;

@@ -281,10 +281,11 @@ def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [7, 100])
-def test_f32_w2_fragment_copies(ops, B):
+def test_f32_w2_fragment_copies(ops, B, monkeypatch):
     """MIHVD_F32_W2F: the conv1 launch's extra blocks write W2 in the load order of the conv2_fwd
     waves ([tap][c2][wave][lane][j]) and of the conv2_bwd dgrad waves ([wave][tap][lane][j]); both
-    conv2 launches reading them produce bit-identical outputs to the HWIO reads."""
+    conv2 launches reading them produce bit-identical outputs to the HWIO reads (conv2_bwd with the
+    conv1 weight-gradient epilogue on VALU and on MFMA, MIHVD_F32_C2B_MEPI=1)."""
     g = torch.Generator(device="cuda").manual_seed(15)
     x = torch.rand(B, 784, device="cuda", generator=g)
     w1 = torch.randn(800, device="cuda", generator=g) * 0.2
@@ -307,13 +308,15 @@ def test_f32_w2_fragment_copies(ops, B):
     ops.f32_conv2_fwd(a1, w2.view(-1), b2, a2f, idx2f, w2frag=frag[0])
     assert torch.equal(a2, a2f) and torch.equal(idx2, idx2f)
     dY2 = torch.randn(B, 14, 14, 64, device="cuda", generator=g)
-    outs = []
-    for wf in (None, frag[1]):
-        cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, device="cuda")
-        slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, device="cuda")
-        ops.f32_conv2_bwd(dY2, w2.view(-1), a1, idx1, x, None, None, cpart, slab, w2frag=wf)
-        outs.append((cpart, slab))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for mepi in ("0", "1"):
+        monkeypatch.setenv("MIHVD_F32_C2B_MEPI", mepi)
+        outs = []
+        for wf in (None, frag[1]):
+            cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, device="cuda")
+            slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, device="cuda")
+            ops.f32_conv2_bwd(dY2, w2.view(-1), a1, idx1, x, None, None, cpart, slab, w2frag=wf)
+            outs.append((cpart, slab))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("NB,R", [(800, 392), (100, 3136), (200, 784), (7, 448), (350, 392)])
