@@ -733,19 +733,6 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 // staged double buffering (the next image's loads are in flight while this one is multiplied).
 // 8 waves split the K steps (w, w + 8, ...); their partial tiles are summed through LDS.
 // (xcd_contiguous: f32_common.h)
-// The next image's LDS-DMA issued through inline asm (ADMA): LLVM's wait-count pass, seeing a
-// global_load_lds in flight across the K-step loop, waits lgkmcnt(0) on every other step's operand
-// reads (the reads just issued for the following step included) instead of leaving them in
-// flight (lgkmcnt(4) without the DMA in the function). Hidden from it, the DMA costs the compiler
-// nothing to track; the image-end wait is explicit (vmcnt(0) before the barrier), and any
-// compiler-counted wait on other loads can only over-wait, never under-wait.
-__device__ __forceinline__ void lds_dma16_asm(const void* src, const float* lds_dst) {
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(lds_dst));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
-}
-
-template <bool ADMA = false>
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
                                                       int ig, int wmid, float* smf,
@@ -797,8 +784,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
 #pragma unroll
     for (int it = 0; it < 7; ++it) {
       const float* src = lin[it] ? (la1[it] ? pa : pd) + loff[it] : zeros;
-      if constexpr (ADMA) lds_dma16_asm(src, buf + 4 * (w64 + 512 * it));
-      else __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(buf + 4 * (w64 + 512 * it)), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(buf + 4 * (w64 + 512 * it)), 16, 0, 0);
     }
   };
   auto store_img = [&](float* buf, const float4 (&v)[7]) {
@@ -867,9 +853,6 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
       }
     }
     if (wm == 0 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
-    if constexpr (ADMA) {
-      if (dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA the compiler cannot see
-    }
     __syncthreads();
     if (n < 8) c2b_stamp(8 + n);  // (study build: wgrad blocks use the per-wave slots for per-image ends)
   }
@@ -919,7 +902,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   c2b_stamp(6);
 }
 
-template <int TPB, bool PREW, bool MEPI, int NPASS = 1, bool FRAG = false, bool ADMA = false>
+template <int TPB, bool PREW, bool MEPI, int NPASS = 1, bool FRAG = false>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
@@ -934,8 +917,8 @@ __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     return;
   }
   // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
-  f32_conv2_wgrad_block<ADMA>(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig,
-                              wmid, smf, zeros);
+  f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, wmid,
+                        smf, zeros);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1316,14 +1299,11 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   const bool prew = env_knob("MIHVD_F32_C2B_PREW", 1) != 0;
   // (MFMA form measured slower: 52.5 vs 51.1 us, dgrad role 28.9 vs 27.8 us, profiles/r04/kbench_f32_r04d.txt)
   const bool mepi = env_knob("MIHVD_F32_C2B_MEPI", 0) != 0;
-  // the wgrad role's next-image LDS-DMA issued by inline asm (f32_conv2_wgrad_block<ADMA>)
-  const bool adma = (wmid & 3) == 3 && env_knob("MIHVD_F32_C2B_ADMA", 1) != 0;
   if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes (PREW; epilogue per MIHVD_F32_C2B_MEPI)
 #define C2B_R1(T)                                                                                        \
   case T:                                                                                                \
     if (mepi && w2f) launch(f32_conv2_bwd_kernel<T, true, true, 2, true>);                                \
     else if (mepi) launch(f32_conv2_bwd_kernel<T, true, true, 2>);                                        \
-    else if (w2f && adma) launch(f32_conv2_bwd_kernel<T, true, false, 2, true, true>);                    \
     else if (w2f) launch(f32_conv2_bwd_kernel<T, true, false, 2, true>);                                  \
     else launch(f32_conv2_bwd_kernel<T, true, false, 2>);                                                 \
     break;
