@@ -186,10 +186,11 @@ def make_fused_step(args, hvd, device):
     # fresh process measured 125.8-127.6 us/step for the driver's 20 timed steps after one setup
     # replay of the main graph and 123.2-123.5 after ten (interleaved runs,
     # profiles/r04/setup_replays_r04aa.txt) -- the same as 400 timed steps (123.8-124.3): the first
-    # milliseconds of GPU work in a process run slower, so the setup replays the main graph ten times
-    # (200 untimed training steps, ~25 ms) before the --warmup steps. MIHVD_BENCH_SETUP_REPLAYS sets
-    # the count.
-    for _ in range(max(1, int(os.environ.get("MIHVD_BENCH_SETUP_REPLAYS", "10")))):
+    # milliseconds of GPU work in a process run slower, so the setup replays the main graph before the
+    # --warmup steps: 100 times (2000 untimed training steps, ~0.25 s; round 5, three fresh processes
+    # each: 119.5-121.8 us/step against 118.7-127.1 with 10 and 119.8-121.0 with 400,
+    # profiles/r05/bench_setup_replays_r05aa.txt). MIHVD_BENCH_SETUP_REPLAYS sets the count.
+    for _ in range(max(1, int(os.environ.get("MIHVD_BENCH_SETUP_REPLAYS", "100")))):
         tr.run_graph()
     for r in sorted(sizes - {k, 0}):
         tr.run_graph(r)
