@@ -168,9 +168,7 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
 // KW: K steps of the wgrad chain, 4 samples each: 4 G (the padded tiles) by default, ceil(B / 4) in
 // the exact-batch instantiation (B = 100: 25 instead of 28 MFMAs per chunk; the rows past the
 // batch are zero either way).
-// ORD (study): 1 issues the first dz chunk and the first p / m / v before the a2 operand and the
-// routing operands (in-order vmcnt: the first chunk's LDS stores then wait for those alone)
-template <int G, bool ADAM, bool STORE, int KW = 4 * G, int ORD = 0>
+template <int G, bool ADAM, bool STORE, int KW = 4 * G>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
@@ -197,27 +195,19 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   const int m_e = 16 * (t >> 6) + (lane & 15), mc_e = min(m_e, B - 1);
   float4 av_e = make_float4(0.f, 0.f, 0.f, 0.f);
   uint32_t ix_e = 0u;
-  auto load_route = [&]() {
-    if (pf && t < G * 64) {
-      av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
-      ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
-    }
-  };
+  if (pf && t < G * 64) {
+    av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
+    ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
+  }
   float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
   // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch)
   float a2r[KS];
-  auto load_a2r = [&]() {
-    if constexpr (WG) {
+  if constexpr (WG) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int b = 4 * s + lg;
-        a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
-      }
+    for (int s = 0; s < KS; ++s) {
+      const int b = 4 * s + lg;
+      a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
     }
-  };
-  if constexpr (ORD == 0) {
-    load_route();
-    load_a2r();
   }
   // dz staging: chunk c = dz[0 .. 16 G)[nb + 16 c .. + 16): lane -> row (lane >> 2) + 16 it, float4 (lane & 3)
   float4 zst[G];
@@ -257,17 +247,8 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
 #pragma unroll
   for (int u = 0; u < G; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   load_z(0);
-  if constexpr (ORD == 0) {
 #pragma unroll
-    for (int c = 0; c < PD; ++c) load_pmv(c, c);
-  } else {
-    load_pmv(0, 0);
-    __builtin_amdgcn_sched_barrier(0);  // (left alone, the scheduler hoists the a2 loads to the top)
-    load_a2r();
-    load_route();
-#pragma unroll
-    for (int c = 1; c < PD; ++c) load_pmv(c, c);
-  }
+  for (int c = 0; c < PD; ++c) load_pmv(c, c);
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     float* buf = buf0 + (c & 1) * F1R_LDS_BUF;
@@ -1228,8 +1209,7 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
   // keeps the padded 28, bitwise equal: the padded steps add exact zeros)
   if (G == 7 && (B + 3) / 4 == 25 && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
-    if (adam && !store_w3 && env_knob("MIHVD_F32_F1R_ORD", 0) != 0) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25, 1>);
-    else if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
+    if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
     else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 25>);
     else launch(f32_fc1_bwd_rows_kernel<7, false, true, 25>);
     return;
