@@ -315,7 +315,11 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
 // (lr, lg) at slot 58 lr + lg covers 16 distinct slots in each 16-lane group (scripts/ldssim_conv2.py
 // model: 1.0 LDS cycles per group; 228 gave 2.0, PMC LDS_BANK_CONFLICT 1.7x the active LDS cycles)
 constexpr int F1F_KS = 14, F1F_KSL = 224, F1F_AS = 232;
-constexpr int F1F_LDS = 128 * F1F_AS * 4;  // 118,784 B
+// LDS rows of the a2 slice for MT sample tiles: 16 MT, plus the rows the last chunk pass of the
+// staging spills into (512-chunk passes over 56-chunk rows; those rows are never read)
+constexpr int f1f_rows(int mt) { return ((mt * 16 * 56 + 511) / 512) * 512 / 56 + 1; }
+constexpr int F1F_LDS = f1f_rows(8) * F1F_AS * 4;  // 119,712 B
+static_assert(F1F_LDS <= 163840, "fc1_fwd LDS");
 
 // MFMA core: a wave's NT tiles (sh, sh + 2, ...) are interleaved element-outer, tile-inner, so
 // dependent MFMAs sit NT issues apart (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency),
@@ -369,25 +373,31 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
   f32x4 acc[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // The a2 slice's loads, then the 56 W3 loads, then the a2 LDS writes: the writes wait (in-order
+  // vmcnt) for the a2 loads alone and the MFMA chain consumes the W3 fragments as they arrive. The
+  // raw values are masked only at the store, and every thread stores all PER chunks (the tail's
+  // chunks past the slice land in spare LDS rows, see f32_fc1_fwd): a mask right after each load
+  // made the compiler wait for the a2 loads before issuing W3, and the tail chunk's load, used only
+  // under the store's condition, was sunk behind the W3 loads, whose vmcnt(0) then held the whole
+  // block until every W3 fragment had arrived (the MFMA loop never overlapped the W3 stream).
   float4 v[PER];
 #pragma unroll
   for (int it = 0; it < PER; ++it) {
     const int i = min(t + 512 * it, NCH - 1), r = i / 56, cc = i - 56 * r;
-    v[it] = mask_f4(*reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc), r < B);
+    v[it] = *reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc);
   }
+  __builtin_amdgcn_sched_barrier(0);
   {
     const int64_t wo = (int64_t)(k0 + 4 * lg) * 1024 + n;
 #pragma unroll
     for (int q = 0; q < 14; ++q)
 #pragma unroll
       for (int j = 0; j < 4; ++j) wa[4 * q + j] = w3[wo + (16 * q + j) * 1024];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
-      const int i = t + 512 * it;
-      if (i < NCH) {
-        const int r = i / 56, cc = i - 56 * r;
-        *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = v[it];
-      }
+      const int i = t + 512 * it, r = i / 56, cc = i - 56 * r;  // r < F1F_ROWS(MT) for every i
+      *reinterpret_cast<float4*>(As + r * F1F_AS + 4 * cc) = mask_f4(v[it], r < B);
     }
     // LDS-only barrier: the W3 fragments (issued before the a2 writes, read from HBM) stay in
     // flight; the MFMA chain consumes them in issue order
@@ -707,7 +717,7 @@ void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) 
   // K half with every W3 fragment loaded by one wave instead of two, 11.20 vs 11.05 us, whole step
   // 116.84 vs 116.91 us, profiles/r05/kbench_f32_r05o.txt -- the second wave's W3 loads hit the cache)
   auto launch = [&](auto kern) {
-    const int lds = mt * 16 * F1F_AS * 4;
+    const int lds = f1f_rows(mt) * F1F_AS * 4;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<dim3(16, F1F_KS), 512, lds, stream>>>(a2.data_ptr<float>(), w3.data_ptr<float>(), zpart.data_ptr<float>(),
                                                  B);
