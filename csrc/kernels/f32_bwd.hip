@@ -431,6 +431,14 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   const int R0 = 18 * b0 + (P0 - 196 * b0) / 14, R1 = 18 * b1i + (P1 - 196 * b1i) / 14 + 5;
   const int nch = (R1 - R0) * 288;  // 18 pixels x 16 float4
   const int nt = wave & 1, cq = wave >> 1;
+  // the dataset rows of the block's (at most two) images: block-uniform, so the step counter and
+  // the two row indices are scalar loads whose waits leave the vector loads below in flight
+  int xrow0 = b0, xrow1 = min(b0 + 1, B - 1);
+  if (rows != nullptr) {
+    const int64_t step = state ? state[ST_FWD] : 0;
+    xrow0 = rows[(int)((step * (int64_t)B + xrow0) % n_pool)];
+    xrow1 = rows[(int)((step * (int64_t)B + xrow1) % n_pool)];
+  }
   // 1. loads: the first two taps' weight fragments, the dY2 rows, the (at most two) x images
   float4 iv[MAXCH];
 #pragma unroll
@@ -531,18 +539,14 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
       codes[k] = c;  // bits [4 r, 4 r + 3): pixel 4 cq + r's (relu << 2 | argmax)
     }
   };
-  // the x patches are needed only by the epilogue: their gather (state -> rows -> x, three
-  // dependent loads) is issued here and lands during the tap loop instead of before the barrier
+  // the x patches are needed only by the epilogue: loaded here, they land during the tap loop. The
+  // rows of the block's (at most two) images were looked up at block start with block-uniform
+  // (scalar) loads, so no vector wait on that dependent chain drains the W2 / epilogue loads
   float xv[4];
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
-    const int i = t + 512 * it, s = i >> 10, pix = i & 1023, Y = (pix >> 5) - 2, X = (pix & 31) - 2;
-    const int bb = min(b0 + s, B - 1);
-    int row = bb;
-    if (rows != nullptr) {
-      const int64_t step = state ? state[ST_FWD] : 0;
-      row = rows[(int)((step * (int64_t)B + bb) % n_pool)];
-    }
+    const int i = t + 512 * it, pix = i & 1023, Y = (pix >> 5) - 2, X = (pix & 31) - 2;
+    const int row = it < 2 ? xrow0 : xrow1;  // i >> 10 == it >> 1 (512-thread blocks)
     const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
     xv[it] = mask_f(x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
   }

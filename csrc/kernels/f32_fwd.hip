@@ -362,7 +362,11 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
                                                            float* __restrict__ zpart, int B) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   float* As = smf;  // [16 MT][228]: rows = samples, k contiguous
-  const int nb = blockIdx.x, ks = blockIdx.y, t = threadIdx.x;
+  // XCD-contiguous (K slice, column group) order: the 16 column-group blocks that stage the same a2
+  // slice run on one XCD (two slices per XCD), so the slice comes from that XCD's L2 after its first
+  // reader instead of being fetched into all eight L2s
+  const int L = xcd_contiguous(blockIdx.y * 16 + blockIdx.x, 0, 16 * F1F_KS);
+  const int nb = L & 15, ks = L >> 4, t = threadIdx.x;
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int k0 = ks * F1F_KSL, nt = wave & 3, sh = wave >> 2;
   const int n = nb * 64 + nt * 16 + lr;
