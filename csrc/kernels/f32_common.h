@@ -153,6 +153,19 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
                                                 float* __restrict__ a1, uint8_t* __restrict__ idx1, int B, float* xim) {
   const int t = threadIdx.x;
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
+  // W1 and b1 first, pinned ahead of the image gather (left alone, the scheduler issued them after
+  // the image's LDS barrier: a fourth memory round trip behind counter -> rows -> x)
+  float wb[2][7];
+  int toff[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    const int k = 4 * s + lg, kc = min(k, 24);
+    toff[s] = (kc / 5) * 32 + (kc % 5);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) wb[nt][s] = f32_ld<COH>(w1 + kc * 32 + 16 * nt + lr);
+  }
+  const float bias0 = f32_ld<COH>(b1 + lr), bias1 = f32_ld<COH>(b1 + 16 + lr);
+  __builtin_amdgcn_sched_barrier(0);
   int row = b;
   if (rows != nullptr) {
     int64_t step = 0;
@@ -170,16 +183,10 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
     const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
     xv[it] = mask_f(xi[in ? Y * 28 + X : 0], in);
   }
-  float wb[2][7];
-  int toff[7];
 #pragma unroll
-  for (int s = 0; s < 7; ++s) {
-    const int k = 4 * s + lg, kc = min(k, 24);
-    toff[s] = (kc / 5) * 32 + (kc % 5);
+  for (int s = 0; s < 7; ++s)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) wb[nt][s] = mask_f(f32_ld<COH>(w1 + kc * 32 + 16 * nt + lr), k < 25);
-  }
-  const float bias0 = f32_ld<COH>(b1 + lr), bias1 = f32_ld<COH>(b1 + 16 + lr);
+    for (int nt = 0; nt < 2; ++nt) wb[nt][s] = mask_f(wb[nt][s], 4 * s + lg < 25);
 #pragma unroll
   for (int it = 0; it < 4; ++it) xim[t + 256 * it] = xv[it];
   __syncthreads();

@@ -547,10 +547,12 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
   }
   const float bias = b3[n];
   int y = 0;
+  float bias4 = 0.f;  // b4 of lane c (wave 0), loaded with the other operands instead of behind the barrier
   if (wave == 0) {
     int row = b;
     if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
     y = (int)labels[row];
+    bias4 = b4[min(lane, 9)];
   }
   float z = bias;
 #pragma unroll
@@ -569,7 +571,7 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
     float acc = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; q += 2) acc += red[q][c] + red[q + 1][c];
-    const float lgt = acc + b4[c];
+    const float lgt = acc + bias4;
     const float v = lane < 10 ? lgt : -INFINITY;
     const float mx = wave_max(v);
     const float e = lane < 10 ? expf(lgt - mx) : 0.f;
