@@ -195,20 +195,24 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   const int m_e = 16 * (t >> 6) + (lane & 15), mc_e = min(m_e, B - 1);
   float4 av_e = make_float4(0.f, 0.f, 0.f, 0.f);
   uint32_t ix_e = 0u;
-  if (pf && t < G * 64) {
-    av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
-    ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
-  }
+  auto load_route = [&]() {
+    if (pf && t < G * 64) {
+      av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
+      ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
+    }
+  };
   float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
   // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch)
   float a2r[KS];
-  if constexpr (WG) {
+  auto load_a2r = [&]() {
+    if constexpr (WG) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int b = 4 * s + lg;
-      a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
+      for (int s = 0; s < KS; ++s) {
+        const int b = 4 * s + lg;
+        a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
+      }
     }
-  }
+  };
   // dz staging: chunk c = dz[0 .. 16 G)[nb + 16 c .. + 16): lane -> row (lane >> 2) + 16 it, float4 (lane & 3)
   float4 zst[G];
   auto load_z = [&](int c) {
@@ -246,9 +250,17 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   f32x4 acc[G];
 #pragma unroll
   for (int u = 0; u < G; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the first chunk's dz and p / m / v first: its LDS stores and dgrad MFMAs (in-order vmcnt) then
+  // wait for those alone, not for the 25 a2 loads of the wgrad operand and the routing operands
+  // issued behind them (pinned: the scheduler hoisted the a2 loads to the top; fc1_bwd 28.7 -> 28.1 us
+  // under rocprofv3, profiles/r05/fc1_bwd_load_order_r05ab.txt)
   load_z(0);
+  load_pmv(0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_a2r();
+  load_route();
 #pragma unroll
-  for (int c = 0; c < PD; ++c) load_pmv(c, c);
+  for (int c = 1; c < PD; ++c) load_pmv(c, c);
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     float* buf = buf0 + (c & 1) * F1R_LDS_BUF;
@@ -996,6 +1008,33 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
   }
   const int col = t & 63, part = t >> 6;  // dW2 blocks: 64 float4 x 4 slab quarters
   const int col16 = t & 15, part16 = t >> 4;  // cpart / db2 blocks: 16 float4 columns x 16 row parts
+  // this thread's partial-sum rows: one round of 8 loads covers the dW2 slabs and the cpart rows
+  // (G <= 32, dgrad blocks <= 128); the db2 rows take the looping strided_sum8
+  const float4* sbase;
+  int64_t sstride;
+  int sr0, sstep, sn;
+  if (bid < CR_W2) {
+    sbase = reinterpret_cast<const float4*>(slab) + (int64_t)bid * 64 + col;
+    sstride = 51200 / 4, sr0 = part, sstep = 4, sn = G;
+  } else if (bid < CR_W2 + CR_CP) {
+    sbase = reinterpret_cast<const float4*>(cpart) + (bid - CR_W2) * 16 + col16;
+    sstride = CP_F32 / 4, sr0 = part16, sstep = 16, sn = ncp;
+  } else {
+    sbase = reinterpret_cast<const float4*>(db2p) + col16;
+    sstride = 16, sr0 = part16, sstep = 16, sn = ndb;
+  }
+  const bool one = sn <= 8 * sstep;  // block-uniform
+  float4 sl[8];
+  if (one) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int rr = sr0 + u * sstep;
+      sl[u] = rr < sn ? sbase[(int64_t)rr * sstride] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // (pinned: the partial-sum loads are issued first; the Adam operands behind them stay in flight
+  // while the sums are formed -- as a loop the sums' loads waited for the Adam operands first)
+  __builtin_amdgcn_sched_barrier(0);
   // the Adam operands (p, m, v) of the elements this thread will update, loaded before the partial
   // sums so their latency overlaps the slab reads instead of following them
   float4 pp{}, mm{}, vv{};
@@ -1024,15 +1063,14 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       vv = make_float4(V[0], V[1], V[2], V[3]);
     }
   }
+  __builtin_amdgcn_sched_barrier(0);
   float4 s;
-  if (bid < CR_W2) {
-    const int64_t i = (int64_t)bid * 64 + col;
-    s = strided_sum8(reinterpret_cast<const float4*>(slab) + i, 51200 / 4, part, 4, G);
-  } else if (bid < CR_W2 + CR_CP) {
-    const int c4 = (bid - CR_W2) * 16 + col16;  // float4 column of the 208
-    s = strided_sum8(reinterpret_cast<const float4*>(cpart) + c4, CP_F32 / 4, part16, 16, ncp);
+  if (one) {  // the same order of additions as strided_sum8's single round
+    s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = f4add(s, sl[u]);
   } else {
-    s = strided_sum8(reinterpret_cast<const float4*>(db2p) + col16, 16, part16, 16, ndb);
+    s = strided_sum8(sbase, sstride, sr0, sstep, sn);
   }
   red[t] = s;
   __syncthreads();
