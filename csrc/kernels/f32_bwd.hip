@@ -168,10 +168,7 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
 // KW: K steps of the wgrad chain, 4 samples each: 4 G (the padded tiles) by default, ceil(B / 4) in
 // the exact-batch instantiation (B = 100: 25 instead of 28 MFMAs per chunk; the rows past the
 // batch are zero either way).
-// WP: the wgrad chain's LDS operands read one pair of K steps ahead of their MFMAs (the order pinned
-// by sched_barrier); left alone the compiler read each pair right before its two MFMAs and waited
-// lgkmcnt(0) there, exposing the LDS latency every 64 cycles of MFMA. WP = 0: that form (study).
-template <int G, bool ADAM, bool STORE, int KW = 4 * G, int WP = 1>
+template <int G, bool ADAM, bool STORE, int KW = 4 * G>
 __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
@@ -295,31 +292,14 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
       continue;
     }
     f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
-    auto zop = [&](int s) { return buf[(4 * s + lg) * 16 + f1r_col(4 * s + lg, lr)]; };
-    if constexpr (WP == 0) {
 #pragma unroll
-      for (int s = 0; s + 1 < KS; s += 2) {
-        const float z0 = zop(s), z1 = zop(s + 1);
-        w0 = mfma4(z0, a2r[s], w0);
-        w1 = mfma4(z1, a2r[s + 1], w1);
-      }
-      if constexpr (KS & 1) w0 = mfma4(zop(KS - 1), a2r[KS - 1], w0);
-    } else {
-      float zc0 = zop(0), zc1 = KS > 1 ? zop(1) : 0.f;
-#pragma unroll
-      for (int s = 0; s + 1 < KS; s += 2) {
-        float zn0 = 0.f, zn1 = 0.f;
-        if (s + 2 < KS) zn0 = zop(s + 2);
-        if (s + 3 < KS) zn1 = zop(s + 3);
-        __builtin_amdgcn_sched_barrier(0);
-        w0 = mfma4(zc0, a2r[s], w0);
-        w1 = mfma4(zc1, a2r[s + 1], w1);
-        __builtin_amdgcn_sched_barrier(0);
-        zc0 = zn0;
-        zc1 = zn1;
-      }
-      if constexpr (KS & 1) w0 = mfma4(zc0, a2r[KS - 1], w0);
+    for (int s = 0; s + 1 < KS; s += 2) {
+      const float z0 = buf[(4 * s + lg) * 16 + f1r_col(4 * s + lg, lr)];
+      const float z1 = buf[(4 * s + 4 + lg) * 16 + f1r_col(4 * s + 4 + lg, lr)];
+      w0 = mfma4(z0, a2r[s], w0);
+      w1 = mfma4(z1, a2r[s + 1], w1);
     }
+    if constexpr (KS & 1) w0 = mfma4(buf[(4 * (KS - 1) + lg) * 16 + f1r_col(4 * (KS - 1) + lg, lr)], a2r[KS - 1], w0);
     const f32x4 g = w0 + w1;
     const int64_t o = rowo + 16 * c;
     float4 gg = make_float4(g[0], g[1], g[2], g[3]);
@@ -1271,8 +1251,7 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
   // keeps the padded 28, bitwise equal: the padded steps add exact zeros)
   if (G == 7 && (B + 3) / 4 == 25 && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
-    if (adam && !store_w3 && env_knob("MIHVD_F32_F1R_WP", 1) == 0) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25, 0>);
-    else if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
+    if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
     else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 25>);
     else launch(f32_fc1_bwd_rows_kernel<7, false, true, 25>);
     return;
