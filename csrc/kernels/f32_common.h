@@ -218,17 +218,6 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
   }
 }
 
-// One lane-linear 16-byte LDS-DMA chunk per lane (global_load_lds_dwordx4, LDS base in M0) issued
-// through inline asm: LLVM's wait-count pass does not see it, so it neither forces vmcnt(0) before
-// the next LDS read nor lgkmcnt(0) on later LDS operand reads (what it does for the builtin). The
-// caller retires it explicitly: s_waitcnt vmcnt(N) with N = the vector-memory ops it issued after
-// the DMA (vmcnt retires in order), then a barrier before any wave reads the chunk.
-__device__ __forceinline__ void lds_dma16_asm(const void* src, const float* lds_dst) {
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(lds_dst));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
-}
-
 // A 256-byte zero line in device memory (one per device), the source of the padding chunks of
 // LDS-DMA staging (global_load_lds cannot mask a lane: a padding lane reads zeros instead). Created
 // on the first call outside a stream capture; nullptr while capturing before that (callers then

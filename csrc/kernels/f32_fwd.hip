@@ -176,7 +176,7 @@ typedef __attribute__((address_space(3))) void c2f_lds_void;
 // its base + 16 B x lane, so the XOR swizzle is applied to the SOURCE chunk: slot s holds chunk
 // (s & 7) ^ swz; padding chunks read a zero line), the W2 operand loaded right behind it, one barrier
 // retiring both: no staging registers, no LDS write pass.
-template <int TPB, bool FRAG, int DEPTH = 2, bool DMA = false, bool ADMA = false>
+template <int TPB, bool FRAG, int DEPTH = 2, bool DMA = false>
 __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __restrict__ a1, const float* __restrict__ w2,
                                                              const float* __restrict__ b2, float* __restrict__ a2,
                                                              uint8_t* __restrict__ idx2, int B,
@@ -205,8 +205,7 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
       const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
       const bool in = sl < nch && y >= 0 && y < 14 && xx >= 0 && xx < 14;
       const float* src = in ? a1 + (((int64_t)bb * 14 + y) * 14 + xx) * 32 + q * 4 : zeros;
-      if constexpr (ADMA) lds_dma16_asm(src, img + 4 * (w64 + 512 * it));
-      else __builtin_amdgcn_global_load_lds((const void*)src, (c2f_lds_void*)(img + 4 * (w64 + 512 * it)), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (c2f_lds_void*)(img + 4 * (w64 + 512 * it)), 16, 0, 0);
     }
     const float4* fp = reinterpret_cast<const float4*>(w2f) + (c2 * 4 + wco) * 64 + lane;
 #pragma unroll
@@ -217,16 +216,7 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
       wb[4 * tap + 2] = v.z;
       wb[4 * tap + 3] = v.w;
     }
-    if constexpr (ADMA) {
-      // ADMA: the DMA is invisible to the compiler; its 7 chunks are the oldest vector-memory ops,
-      // so vmcnt(25) retires them and leaves the 25 W2 loads in flight across the barrier, consumed
-      // by the tap loop as they arrive (the builtin form drained them: vmcnt(0) before the first read)
-      asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      __syncthreads();  // (vmcnt(0)): the image has landed in LDS
-    }
+    __syncthreads();  // (vmcnt(0)): the image has landed in LDS
   } else {
   float4 iv[C2F8_MAXCH];
 #pragma unroll
@@ -697,8 +687,6 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   // the image staged by LDS-DMA with the W2 fragment copy (default; r05k: 20.71 -> 19.31 us, whole step
   // 117.42 -> 116.84 us); MIHVD_F32_C2F_DMA=0: register staging + LDS write pass
   const float* zl = (w2f != nullptr && env_knob("MIHVD_F32_C2F_DMA", 1) != 0) ? f32_zero_line(stream) : nullptr;
-  // the DMA issued by inline asm, the W2 loads left in flight across the staging barrier
-  const bool adma = env_knob("MIHVD_F32_C2F_ADMA", 1) != 0;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nblk, 512, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
@@ -706,8 +694,7 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   };
 #define C2F8_CASE(T)                                                         \
   case T:                                                                    \
-    if (zl && adma) launch(f32_conv2_fwd8_kernel<T, true, 2, true, true>);   \
-    else if (zl) launch(f32_conv2_fwd8_kernel<T, true, 2, true>);            \
+    if (zl) launch(f32_conv2_fwd8_kernel<T, true, 2, true>);                 \
     else if (w2f) launch(f32_conv2_fwd8_kernel<T, true>);                    \
     else launch(f32_conv2_fwd8_kernel<T, false>);                            \
     break;
