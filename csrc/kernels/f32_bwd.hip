@@ -1032,11 +1032,10 @@ __global__ void __launch_bounds__(256) f32_conv_reduce_kernel(const float* __res
       sl[u] = rr < sn ? sbase[(int64_t)rr * sstride] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  // (pinned: the partial-sum loads are issued first; the Adam operands behind them stay in flight
-  // while the sums are formed -- as a loop the sums' loads waited for the Adam operands first)
   __builtin_amdgcn_sched_barrier(0);
-  // the Adam operands (p, m, v) of the elements this thread will update, loaded before the partial
-  // sums so their latency overlaps the slab reads instead of following them
+  // the Adam operands (p, m, v) of the elements this thread will update, issued right behind the
+  // partial-sum loads (pinned) so the two latencies overlap; the sums then wait for their own loads
+  // alone (as a loop, the sums' loads had waited for the Adam operands to arrive first)
   float4 pp{}, mm{}, vv{};
   int64_t ao = -1;
   if (opt) {
