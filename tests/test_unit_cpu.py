@@ -882,3 +882,20 @@ def test_fused_trainer_knob_count():
 
     knobs = set(re.findall(r"MIHVD_[A-Z0-9_]+", open(fm.__file__).read()))
     assert len(knobs) <= 12, sorted(knobs)
+
+
+@given(n=st.integers(0, 500), k=st.integers(1, 40), lead=st.integers(0, 5))
+@settings(max_examples=200, deadline=None)
+def test_bench_replay_schedule_covers_exactly_n_steps(n, k, lead):
+    """bench.py's timed region replays graphs of these lengths: exactly n steps in total, a short
+    lead graph first when n exceeds it, whole k-step graphs, then one remainder (the bench contract:
+    time EXACTLY --steps steps)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    s = bench.replay_schedule(n, k, lead)
+    assert sum(s) == n and all(x > 0 for x in s)
+    if lead > 0 and n > lead:
+        assert s[0] == lead and all(x == k for x in s[1:-1]) and 0 < s[-1] <= k
+    else:
+        assert all(x == k for x in s[:-1]) and (not s or 0 < s[-1] <= k)
