@@ -899,3 +899,60 @@ def test_bench_replay_schedule_covers_exactly_n_steps(n, k, lead):
         assert s[0] == lead and all(x == k for x in s[1:-1]) and 0 < s[-1] <= k
     else:
         assert all(x == k for x in s[:-1]) and (not s or 0 < s[-1] <= k)
+
+
+def _bench_line(out: str) -> dict:
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert len(recs) == 1, out[-2000:]  # rank 0 prints ONE line
+    return recs[0]
+
+
+def _check_bench_contract(r: dict, n: int, steps: int, warmup: int):
+    for key, typ in (("metric", str), ("unit", str), ("dtype", str), ("data", str), ("scaling", str),
+                     ("config", dict)):
+        assert isinstance(r[key], typ), (key, r)
+    assert r["n_gpus"] == n and r["steps"] == steps and r["warmup"] == warmup
+    assert r["higher_is_better"] is True and r["scaling"] in ("weak", "strong")
+    assert r["value"] > 0 and r["ms_per_step"] > 0
+    assert r["vs_baseline"] is None or r["vs_baseline"] > 0
+    c = r["config"]
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(c), c
+    assert c["parallelism"] == f"dp{n}" and c["global_batch"] == 100 * n
+    # value is the whole-job aggregate: global batch / step time
+    assert abs(r["value"] - c["global_batch"] / (r["ms_per_step"] / 1000.0)) <= 0.01 * r["value"] + 1.0, r
+
+
+def test_bench_json_contract_one_process_cpu():
+    """bench.py prints the driver's one-line JSON contract (CPU: the stock-PyTorch DistributedOptimizer
+    step on gloo; the flagship fused step needs the GPU, where the GPU tests check its line)."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--impl", "torch", "--steps", "2",
+                        "--warmup", "1"], env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    _check_bench_contract(_bench_line(p.stdout), 1, 2, 1)
+
+
+def test_bench_json_contract_two_ranks_cpu():
+    """The driver's multi-rank launch form (torch.distributed.run, 127.0.0.1) at two CPU ranks over
+    gloo: one JSON line from rank 0 with n_gpus = 2, dp2 and the whole-job images/s."""
+    import socket
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--impl", "torch",
+           "--steps", "2", "--warmup", "1"]
+    p = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    _check_bench_contract(_bench_line(p.stdout), 2, 2, 1)
