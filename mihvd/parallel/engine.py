@@ -213,7 +213,10 @@ class Engine:
                 n = sum(g.tensor.numel() for g in group)
                 buf = self._fusion.get(e0.fuse_key)
                 if buf is None or buf.numel() < n:
-                    buf = torch.empty(n, dtype=e0.tensor.dtype, device=e0.tensor.device)
+                    # geometric growth with a 64 K-element floor: readiness timing decides the groups,
+                    # so a run of ever-larger ones costs O(log) allocations, not one per group
+                    cap = max(n, 2 * (buf.numel() if buf is not None else 0), 1 << 16)
+                    buf = torch.empty(cap, dtype=e0.tensor.dtype, device=e0.tensor.device)
                     self._fusion[e0.fuse_key] = buf
                     self.fusion_allocs += 1
                 flat = buf[:n]
