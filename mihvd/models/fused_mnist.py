@@ -352,7 +352,6 @@ class FusedMNISTTrainer:
         # (profiles/r04/kbench_f32_r04m.txt); bitwise equal
         self.w2frag = torch.empty(2, 51200, device=dev, dtype=torch.float32) if self.f32 else None
         self.keep_w3_grad = False  # tests: also store dW3 into the gradient buffer when it is fused away
-        self._study_sleep = int(os.environ.get("MIHVD_STUDY_SLEEP", "-1"))
         self.f32_factor = False
         if self.f32:
             ops = self.ops
@@ -579,8 +578,6 @@ class FusedMNISTTrainer:
             main.wait_event(self._small_ev)
             self._small_ev = None
         wf = self.w2frag
-        if self._study_sleep >= 0:  # (study: a one-thread spin kernel between conv_reduce and conv1)
-            torch.cuda._sleep(self._study_sleep)
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
                         self.idx1, w2, wf)
         o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0])
