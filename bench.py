@@ -4,7 +4,8 @@
     python bench.py --gpus N --steps K --warmup W [--impl fused|torch|ddp]
 
 For N>1 the driver launches one rank per GPU with ``torch.distributed.run``; ranks read
-RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment. Model: the reference's 2-conv CNN
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment (``--gpus`` must equal WORLD_SIZE). Run
+without an outer launcher, ``--gpus N`` starts the N ranks itself (mihvd.runner, 127.0.0.1). Model: the reference's 2-conv CNN
 (horovod/tensorflow_mnist.py:38-73, 3,274,634 params, random init), per-GPU batch 100
 (:160-161), TF1 Adam (:130) with LR × size (:123), gradients averaged across ranks every step
 (:133). Data: synthetic 28×28 images resident on the device (no network for MNIST).
@@ -203,6 +204,34 @@ def make_fused_step(args, hvd, device):
     return step, args.precision, tr
 
 
+def _launch_ranks(args) -> None:
+    """``--gpus N`` without an outer launcher: start N ranks here, one child process per GPU, through
+    the framework's own launcher (mihvd/runner/launch.py, the mpirun form of the reference's job,
+    horovod/tensorflow-mnist.yaml:17-38), and exit with the job's code; rank 0's JSON line is the
+    output. Runs before anything touches the GPU (the children own the devices; this process only
+    waits). Under an outer launcher (torch.distributed.run / mihvdrun: WORLD_SIZE set) the world
+    size must equal ``--gpus``: a mismatch exits non-zero instead of timing another GPU count."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
+        return
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    # a GPU job needs one device per rank (device_count() does not initialise the GPU on this image);
+    # on a machine without GPUs the ranks run on the CPU over gloo (the tests' form)
+    ndev = torch.cuda.device_count()
+    if 0 < ndev < args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) are visible")
+    if args.gpus == 1:
+        return
+    from mihvd.runner.launch import LaunchSpec, launch
+
+    spec = LaunchSpec(np=args.gpus, hosts=[("localhost", args.gpus)], master_addr="127.0.0.1",
+                      command=[sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+    raise SystemExit(launch(spec))
+
+
 def _host_wait_mode():
     """MIHVD_SYNC_WAIT=spin (default): the host waits for the GPU by spinning (hipDeviceScheduleSpin)
     instead of HIP's default scheduling, so the synchronize that closes the timed region returns as
@@ -264,6 +293,7 @@ def _rccl_witness(tr, device) -> dict:
 
 def main():
     args = parse()
+    _launch_ranks(args)  # before any GPU call
     _host_wait_mode()
     if args.impl == "fused":
         # the fused trainer issues its own collectives (in its HIP graph): no engine thread cycling

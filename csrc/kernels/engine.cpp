@@ -450,9 +450,11 @@ class Engine {
     }
   }
 
-  // Polls `ev` (control stream) until it completes; meanwhile runs the negotiation stall check,
-  // unless `quiet`: a rank that is stopping with nothing pending waits for its peers to finish
-  // their work (they may be busy for long, e.g. rank 0 checkpointing) -- a clean wait, not a stall.
+  // Polls `ev` (control stream) until it completes; meanwhile runs the negotiation stall check.
+  // `quiet`: a rank that is stopping with nothing pending waits for its peers to finish their work
+  // (they may be busy for long, e.g. rank 0 checkpointing) -- a clean wait, not a stall, so no
+  // warning; but a peer that died during shutdown must not hold it forever: the abort still
+  // fires, at twice the stall-abort time.
   void wait_ctrl(hipEvent_t ev, bool quiet = false) {
     const auto t0 = Clock::now();
     bool warned = false;
@@ -462,9 +464,10 @@ class Engine {
       if (q == hipSuccess) return;
       if (q != hipErrorNotReady) hip_check(q, "negotiation event");
       if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 10));
-      if ((spins & 255) != 0 || quiet) continue;
+      if ((spins & 255) != 0) continue;
       const double age = std::chrono::duration<double>(Clock::now() - t0).count();
-      if (warn_s_ > 0 && age > warn_s_ && !warned) {
+      const double abort_after = quiet ? 2.0 * abort_s_ : abort_s_;
+      if (!quiet && warn_s_ > 0 && age > warn_s_ && !warned) {
         warned = true;
         std::string names;
         for (const auto& s : slots_)
@@ -478,9 +481,9 @@ class Engine {
         std::lock_guard<std::mutex> lk(mu_);
         ++stalls_warned_;
       }
-      if (abort_s_ > 0 && age > abort_s_) {
-        std::fprintf(stderr, "[mihvd engine] negotiation stalled for more than %.1f s: aborting (exit 134)\n",
-                     abort_s_);
+      if (abort_s_ > 0 && age > abort_after) {
+        std::fprintf(stderr, "[mihvd engine] negotiation stalled for more than %.1f s%s: aborting (exit 134)\n",
+                     abort_after, quiet ? " while stopping" : "");
         std::fflush(stderr);
         std::_Exit(134);
       }

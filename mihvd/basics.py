@@ -368,8 +368,10 @@ def engine_running() -> bool:
     return _ctx.engine is not None
 
 
-def shutdown():
-    """Tear down the world (``hvd.shutdown``). Safe to call more than once."""
+def shutdown(abort: bool = False):
+    """Tear down the world (``hvd.shutdown``). Safe to call more than once. ``abort``: after a
+    failure (mihvd.elastic), the framework-owned communicators are aborted without draining the
+    device first (a dead peer's collective would never complete)."""
     with _ctx.lock:
         if not _ctx.initialized:
             return
@@ -385,7 +387,7 @@ def shutdown():
             _ctx.engine = None
         if _ctx.plane is not None:
             try:
-                _ctx.plane.close()
+                _ctx.plane.close(abort=abort)
             except Exception:  # pragma: no cover
                 pass
             _ctx.plane = None

@@ -234,8 +234,10 @@ def _membership_changed(grace_s: float) -> bool:
     return False
 
 
-def _reset():
-    basics.shutdown()
+def _reset(failed: bool = False):
+    """Re-form the world. ``failed``: after a collective failure, the old communicators are aborted
+    instead of drained (a dead peer's bucket allreduce would never complete)."""
+    basics.shutdown(abort=failed)
     basics.init()
 
 
@@ -247,11 +249,12 @@ def run(func):
         if not basics.is_initialized():
             basics.init()
         grace = float(basics.config().elastic_grace_s)
-        reset = False
+        reset = failed = False
         while True:
             if reset:
-                _reset()
+                _reset(failed)
                 state.on_reset()
+                failed = False
             try:
                 state.sync()
                 return func(state, *args, **kwargs)
@@ -266,7 +269,7 @@ def run(func):
                 log.warning("[rank %d] collective failed (%s): rolling back to the last commit", basics.rank(),
                             str(e).splitlines()[0][:200])
                 state.restore()
-                reset = True
+                reset = failed = True
 
     return wrapper
 

@@ -60,9 +60,26 @@ class Callback:
 
 
 class BroadcastGlobalVariablesCallback(Callback):
+    """``device``: Horovod's device for the broadcast ops (e.g. ``'/cpu:0'``). The variables are
+    broadcast where they live (RCCL for device tensors, gloo for host tensors); a ``device`` naming
+    the other kind is reported once, since moving ~39 MB of state through the host to honour it
+    would only slow the broadcast down."""
+
     def __init__(self, root_rank: int = 0, device: str = ""):
         self.root_rank = root_rank
+        self.device = device
         self.broadcast_done = False
+
+    def set_model(self, model):
+        super().set_model(model)
+        want_cpu = "cpu" in str(self.device).lower()
+        if self.device and model is not None and model.module is not None:
+            on_cpu = next(model.module.parameters()).device.type == "cpu"
+            if want_cpu != on_cpu:
+                import warnings
+
+                warnings.warn(f"BroadcastGlobalVariablesCallback(device={self.device!r}): the variables are "
+                              f"broadcast on the device they live on ({'cpu' if on_cpu else 'gpu'})")
 
     def on_batch_end(self, batch, logs=None):
         if self.broadcast_done:
@@ -96,8 +113,11 @@ class LearningRateWarmupCallback(Callback):
     def __init__(self, initial_lr, warmup_epochs=5, momentum_correction=True, steps_per_epoch=None, verbose=0):
         self.initial_lr = initial_lr
         self.warmup_epochs = warmup_epochs
+        self.momentum_correction = momentum_correction
         self.steps_per_epoch = steps_per_epoch
+        self.verbose = verbose
         self._epoch = 0
+        self._restore_momentum = None
 
     def on_epoch_begin(self, epoch, logs=None):
         self._epoch = epoch
@@ -109,8 +129,36 @@ class LearningRateWarmupCallback(Callback):
         progress = (self._epoch + batch / spe) / self.warmup_epochs
         size = _b.size() if _b.is_initialized() else 1
         lr = self.initial_lr / size * (1 + progress * (size - 1))
-        for g in self.model.optimizer.param_groups:
-            g["lr"] = lr
+        _set_lr(self.model.optimizer, lr, self.momentum_correction, self)
+
+    def on_batch_end(self, batch, logs=None):
+        _restore_momentum(self.model.optimizer, self)
+
+    def on_epoch_end(self, epoch, logs=None):
+        if self.verbose and epoch == self.warmup_epochs - 1 and (not _b.is_initialized() or _b.rank() == 0):
+            print(f"Epoch {epoch + 1}: finished gradual learning rate warmup to {self.initial_lr:g}.", flush=True)
+
+
+def _set_lr(optimizer, lr, momentum_correction, owner):
+    """Set every param group's LR. With ``momentum_correction`` (Horovod's rule, Goyal et al.
+    2017), an optimizer with a momentum buffer (SGD's ``momentum``) scales its momentum by
+    new_lr / old_lr for the batch the LR changes in, so the accumulated velocity is not applied at
+    the new LR; the callback restores the momentum at the batch end. Adam has no such term."""
+    saved = []
+    for g in optimizer.param_groups:
+        old = g["lr"]
+        if momentum_correction and g.get("momentum") and old > 0 and lr != old:
+            saved.append((g, g["momentum"]))
+            g["momentum"] = g["momentum"] * lr / old
+        g["lr"] = lr
+    owner._restore_momentum = saved or None
+
+
+def _restore_momentum(optimizer, owner):
+    if owner._restore_momentum:
+        for g, m in owner._restore_momentum:
+            g["momentum"] = m
+        owner._restore_momentum = None
 
 
 class LearningRateScheduleCallback(Callback):
@@ -120,6 +168,8 @@ class LearningRateScheduleCallback(Callback):
 
     def __init__(self, initial_lr, multiplier, start_epoch=0, end_epoch=None, staircase=True,
                  momentum_correction=True, steps_per_epoch=None, verbose=0):
+        self.momentum_correction = momentum_correction
+        self._restore_momentum = None
         self.initial_lr = initial_lr
         self.multiplier = multiplier if callable(multiplier) else (lambda epoch, m=multiplier: m)
         self.start_epoch = start_epoch
@@ -132,8 +182,10 @@ class LearningRateScheduleCallback(Callback):
         return epoch >= self.start_epoch and (self.end_epoch is None or epoch < self.end_epoch)
 
     def _set(self, lr):
-        for g in self.model.optimizer.param_groups:
-            g["lr"] = lr
+        _set_lr(self.model.optimizer, lr, self.momentum_correction, self)
+
+    def on_batch_end(self, batch, logs=None):
+        _restore_momentum(self.model.optimizer, self)
 
     def on_epoch_begin(self, epoch, logs=None):
         self._epoch = epoch
@@ -374,29 +426,21 @@ class Model:
         module's weights and the optimizer's Adam hyper-parameters, or None where the per-batch path
         must run (MIHVD_KERAS_FUSED=0, another policy or module, an optimizer or reduction the fused
         step does not implement, existing optimizer state, or a callback with per-batch hooks)."""
-        if os.environ.get("MIHVD_KERAS_FUSED", "1") == "0":
+        ok = self._fused_fit_eligible(cbs, batch_size)
+        # Every rank must take the same path: building the trainer is collective and the two paths
+        # issue different collectives. The reference idiom gives rank 0 extra callbacks
+        # (tensorflow_mnist_gpu.py:156-163), so one rank's list can rule the fused path out: agree
+        # on the minimum before choosing.
+        if _b.is_initialized() and _b.size() > 1:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                                device=_b.device() if _b.backend() == "nccl" else "cpu")
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            ok = bool(flag.item())
+        if not ok:
             return None
-        from .models.mnist import MNISTConvNet
-        from .optim import FusedAdam, TFAdam
-
         m, opt = self.module, self.optimizer
-        if (not isinstance(m, MNISTConvNet) or getattr(m, "impl", None) != "hip" or self.policy not in
-                ("float32", "mixed_bfloat16") or opt is None or not 1 <= batch_size <= 128):
-            return None
-        if not isinstance(opt, (TFAdam, FusedAdam)) or len(opt.param_groups) != 1 or any(opt.state.values()):
-            return None
         g = opt.param_groups[0]
-        if isinstance(opt, FusedAdam) and (g.get("rule") != "tf" or g.get("weight_decay", 0.0) != 0.0):
-            return None
         op = getattr(opt, "_op", _b.Average)
-        if op not in (_b.Average, _b.Sum):
-            return None
-        for cb in cbs:
-            if not isinstance(cb, self._FUSED_CALLBACKS):
-                overridden = (type(cb).on_batch_begin is not Callback.on_batch_begin
-                              or type(cb).on_batch_end is not Callback.on_batch_end)
-                if overridden:
-                    return None
         from .models.fused_mnist import FusedMNISTTrainer
 
         tr = FusedMNISTTrainer(batch_size=batch_size, lr=g["lr"], betas=tuple(g["betas"]), eps=g["eps"],
@@ -405,6 +449,32 @@ class Model:
         tr.load_model_weights(m)
         tr.track_stats = True
         return tr
+
+    def _fused_fit_eligible(self, cbs, batch_size) -> bool:
+        """This rank's view of whether the fused fit path applies (see _fused_fit_trainer)."""
+        if os.environ.get("MIHVD_KERAS_FUSED", "1") == "0":
+            return False
+        from .models.mnist import MNISTConvNet
+        from .optim import FusedAdam, TFAdam
+
+        m, opt = self.module, self.optimizer
+        if (not isinstance(m, MNISTConvNet) or getattr(m, "impl", None) != "hip" or self.policy not in
+                ("float32", "mixed_bfloat16") or opt is None or not 1 <= batch_size <= 128):
+            return False
+        if not isinstance(opt, (TFAdam, FusedAdam)) or len(opt.param_groups) != 1 or any(opt.state.values()):
+            return False
+        g = opt.param_groups[0]
+        if isinstance(opt, FusedAdam) and (g.get("rule") != "tf" or g.get("weight_decay", 0.0) != 0.0):
+            return False
+        if getattr(opt, "_op", _b.Average) not in (_b.Average, _b.Sum):
+            return False
+        for cb in cbs:
+            if not isinstance(cb, self._FUSED_CALLBACKS):
+                overridden = (type(cb).on_batch_begin is not Callback.on_batch_begin
+                              or type(cb).on_batch_end is not Callback.on_batch_end)
+                if overridden:
+                    return False
+        return True
 
     def _fit_fused(self, tr, x, y, batch_size, epochs, steps_per_epoch, validation_data, validation_steps, cbs,
                    verbose, shuffle, seed):
@@ -423,6 +493,9 @@ class Model:
         for epoch in range(epochs):
             for cb in cbs:
                 cb.on_epoch_begin(epoch)
+            # an epoch-level callback (on_epoch_begin only: it passed the filter) may have changed the
+            # LR; the trainer bakes it into its graphs, so a change re-captures them
+            tr.set_lr(self.optimizer.param_groups[0]["lr"])
             t0 = time.time()
             tr.reset_stats()
             done = 0

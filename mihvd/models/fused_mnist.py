@@ -637,6 +637,11 @@ class FusedMNISTTrainer:
         stream = main if on_main else self._side
         if not on_main:
             stream.wait_stream(main)
+        elif self.ncomm_small is not None:
+            # two RCCL communicators must not run collectives concurrently (kernels of two
+            # communicators interleaved differently on different ranks can deadlock): the side
+            # stream's row / bucket collectives on ncomm complete before ncomm_small's allreduce
+            main.wait_stream(self._side)
         with torch.cuda.stream(stream):
             self._allreduce(self.grads[:hi], 0, hi, comm=self.ncomm_small)
             self.ops.adam_step(self.params[:hi], self.grads[:hi], self.m[:hi], self.v[:hi], None, self.state, 0, self.lr,
@@ -693,6 +698,8 @@ class FusedMNISTTrainer:
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
         self._f32_small_tail(main, W3_START)
+        if self.ncomm_small is not None:
+            side.wait_stream(main)  # the row all-gather (ncomm) after ncomm_small's allreduce
         with torch.cuda.stream(side):
             p3 = self.params[W3_START:].view(3136, 1024)
             self._all_gather_rows(p3, p3[r * R:(r + 1) * R])
@@ -1082,6 +1089,19 @@ class FusedMNISTTrainer:
         e1 = (self.global_step + k - 1) // self._epoch_steps
         if e1 != e0 or (self.global_step % self._epoch_steps == 0 and self.global_step > 0):
             self._reshuffle()  # stream-ordered: no host synchronisation
+
+    def set_lr(self, lr: float):
+        """A new learning rate for the following steps. The kernels take it as a launch argument,
+        so the captured graphs (and the xGMI plane's prepared collectives) are rebuilt on their next
+        use; the same value is a no-op."""
+        lr = float(lr)
+        if lr == self.lr:
+            return
+        self._join()
+        self.lr = lr
+        self._graphs = {}
+        self.graph = None
+        self._graph_tried = False
 
     # ----------------------------------------------------------------------------- graphs
     def build_graph(self, steps_per_replay: int = 10, warmup: int = 2, primary: bool = True):

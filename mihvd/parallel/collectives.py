@@ -258,8 +258,8 @@ class BucketPlane:
         self.launched += 1
         return _PlaneWork(ev, self.device)
 
-    def close(self):
-        self.comm.close()
+    def close(self, abort: bool = False):
+        self.comm.close(abort=abort)
 
 
 def plane_wanted(world: int | None = None) -> bool:

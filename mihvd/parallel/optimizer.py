@@ -263,7 +263,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
 
     def _elastic_reset(self):
         """Forget in-flight bucket allreduces of a step interrupted by a failed or re-formed world
-        (mihvd.elastic): the next backward starts with every bucket un-launched."""
+        (mihvd.elastic): the next backward starts with every bucket un-launched, on the bucket plane
+        of the NEW world (shutdown closed the old one; collective: every rank's State.sync() calls
+        this)."""
+        self._plane = C.bucket_plane() if any(p.is_cuda for p in self._params) else None
         if self._controller is not None:
             for b in self._buckets:
                 b.handle = None

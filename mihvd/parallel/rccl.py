@@ -113,7 +113,10 @@ class NativeComm:
             mon = getattr(basics._ctx, "health", None)
             if mon is not None:
                 mon.detach_rccl(int(self._o.rccl_comm_ptr(self.handle)))
-            torch.cuda.synchronize(self.device)
+            if not abort:
+                # a peer that died with a collective in flight would hold this wait forever: after a
+                # failure the communicator is aborted (ncclCommAbort) without draining the device
+                torch.cuda.synchronize(self.device)
             self._o.rccl_comm_destroy(self.handle, abort)
             self._closed = True
 

@@ -956,3 +956,85 @@ def test_bench_json_contract_two_ranks_cpu():
     p = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     _check_bench_contract(_bench_line(p.stdout), 2, 2, 1)
+
+
+def test_bench_gpus_flag_launches_its_ranks_cpu():
+    """``python3 bench.py --gpus 2`` with no outer launcher starts the two ranks itself (the
+    framework's launcher, gloo on the CPU): one JSON line with n_gpus = 2 — the flag is never
+    silently ignored."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "MIHVD_LAUNCHED"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--impl", "torch", "--steps",
+                        "2", "--warmup", "1"], env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    _check_bench_contract(_bench_line(p.stdout), 2, 2, 1)
+
+
+def test_bench_gpus_flag_mismatch_exits_nonzero_cpu():
+    """Under a launcher whose world size differs from ``--gpus`` the bench refuses to run."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--impl", "torch", "--steps",
+                        "2", "--warmup", "1"], env=env, cwd=root, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+    assert "WORLD_SIZE=1" in p.stderr and not any(ln.startswith("{") for ln in p.stdout.splitlines())
+
+
+def test_lr_callbacks_momentum_correction(hvd_single):
+    """LearningRateWarmupCallback / LearningRateScheduleCallback with ``momentum_correction``
+    (Horovod's default): while the LR changes, an optimizer with momentum (SGD) has its momentum
+    scaled by new_lr / old_lr for that batch and restored at the batch end; without it the momentum
+    is untouched."""
+    from mihvd import keras as K
+    from mihvd.models.mnist import MNISTConvNet
+
+    model = K.Model(MNISTConvNet(impl="torch", seed=1))
+    opt = torch.optim.SGD(model.module.parameters(), lr=0.1, momentum=0.9)
+    model.compile(opt, loss=None)
+    model._steps_per_epoch = 10
+    cb = K.callbacks.LearningRateScheduleCallback(initial_lr=0.1, multiplier=0.5, staircase=False)
+    cb.set_model(model)
+    cb.on_epoch_begin(0)
+    cb.on_batch_begin(0)
+    g = opt.param_groups[0]
+    assert g["lr"] == pytest.approx(0.05) and g["momentum"] == pytest.approx(0.45)
+    cb.on_batch_end(0)
+    assert g["momentum"] == pytest.approx(0.9) and g["lr"] == pytest.approx(0.05)
+    cb2 = K.callbacks.LearningRateScheduleCallback(initial_lr=0.1, multiplier=0.25, staircase=False,
+                                                    momentum_correction=False)
+    cb2.set_model(model)
+    cb2.on_epoch_begin(0)
+    cb2.on_batch_begin(1)
+    assert g["lr"] == pytest.approx(0.025) and g["momentum"] == pytest.approx(0.9)
+    w = K.callbacks.LearningRateWarmupCallback(initial_lr=0.2, warmup_epochs=2)
+    w.set_model(model)
+    w.on_epoch_begin(0)
+    w.on_batch_begin(0)  # size 1: the warmup target from the first batch
+    assert g["lr"] == pytest.approx(0.2) and g["momentum"] == pytest.approx(0.9 * 0.2 / 0.025)
+    w.on_batch_end(0)
+    assert g["momentum"] == pytest.approx(0.9)
+
+
+def test_distributed_optimizer_elastic_reset_resolves_the_new_plane(hvd_single, monkeypatch):
+    """After an elastic reset (shutdown closed the old world's bucket plane) DistributedOptimizer
+    must not keep the destroyed communicator: _elastic_reset resolves the new world's plane."""
+    from mihvd.parallel import collectives as C
+    from mihvd.models.mnist import MNISTConvNet
+
+    model = MNISTConvNet(impl="torch", seed=1)
+    opt = hvd_single.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1),
+                                          named_parameters=model.named_parameters())
+    opt._plane = "old world's plane"
+    calls = []
+    monkeypatch.setattr(C, "bucket_plane", lambda: calls.append(1) or "new plane")
+    opt._elastic_reset()
+    # host parameters: no plane at all (gloo); the stale one is dropped either way
+    assert opt._plane is None and calls == []
