@@ -21,6 +21,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include "f32_common.h"
+#include "xgmi_role.h"
 
 namespace mihvd {
 
@@ -72,12 +73,21 @@ __device__ __forceinline__ void f32_w2_frag_block(int blk, const float* __restri
   }
 }
 
+// `coll` (xgmi_role.h): a co-launched xGMI collective on blocks [0, coll.nblk) -- the fp32 plane's
+// row gather of the previous step's updated dense/kernel rows, on the CUs beside this latency-bound
+// launch (its blocks are small: several share a CU with the role block); coll.nblk = 0: none. The
+// conv blocks follow (nblk is a multiple of 8, so their XCD mapping is unchanged).
 __global__ void __launch_bounds__(256) f32_conv1_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ a1, uint8_t* __restrict__ idx1,
-    int B, const float* __restrict__ w2, float* __restrict__ w2f) {
+    int B, const float* __restrict__ w2, float* __restrict__ w2f, CollRole coll) {
   __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
-  const int id = blockIdx.x;
+  const int cb = coll.nblk;
+  if ((int)blockIdx.x < cb) {
+    coll_gather_run(coll, (int)blockIdx.x);
+    return;
+  }
+  const int id = blockIdx.x - cb;
   if (id >= 4 * B) {
     f32_w2_frag_block(id - 4 * B, w2, w2f);
     return;
@@ -625,9 +635,12 @@ static const int* rows_ptr(const c10::optional<at::Tensor>& rows, int n_pool, in
 
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
-                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag) {
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll) {
   const int B = a1.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv1_fwd: batch 1..128");
+  const CollRole cr = xgmi_role_lookup(coll);
+  TORCH_CHECK(cr.nblk % 8 == 0 && (cr.kind == COLL_GATHER || cr.nblk == 0),
+              "f32_conv1_fwd: a co-launched collective must be a gather of a multiple of 8 blocks");
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv1_fwd: x");
   check_f32(a1, (int64_t)B * 6272, "f32_conv1_fwd: a1");
   check_u8(idx1, (int64_t)B * 6272, "f32_conv1_fwd: idx1");
@@ -645,9 +658,10 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
   }
   // (100 fragment blocks, one float4 per thread, measured the same: conv1 7.16 us, whole step
   // 117.6-119.1 us either way, profiles/r05/bench_w2f_blocks_ab_r05s.txt)
-  f32_conv1_kernel<<<dim3(4 * B + (frag ? 4 * W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
+  f32_conv1_kernel<<<dim3(cr.nblk + 4 * B + (frag ? 4 * W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
       x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(), b1.data_ptr<float>(), a1.data_ptr<float>(),
-      idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr);
+      idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr,
+      cr);
 }
 
 // tiles per block of f32_conv2_fwd for batch B (about one block per CU), and the block count

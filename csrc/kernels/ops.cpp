@@ -85,7 +85,7 @@ void multi_tensor_sgd(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std:
 void bump_step_(at::Tensor& step);
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
-                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag);
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll);
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
                    const c10::optional<at::Tensor>& w2frag);
 void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
@@ -285,8 +285,8 @@ void mt_sgd_op(at::TensorList p, at::TensorList g, at::TensorList bufs, double l
 }
 void bump_step_op(Tensor step) { mihvd::bump_step_(step); }
 void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
-                  Tensor idx1, const OptT& w2, const OptT& w2frag) {
-  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag);
+                  Tensor idx1, const OptT& w2, const OptT& w2frag, int64_t coll) {
+  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag, coll);
 }
 void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& w2frag) {
   mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, w2frag);
@@ -384,7 +384,7 @@ TORCH_LIBRARY(mihvd, m) {
         "float weight_decay, bool nesterov, bool first, float grad_scale) -> ()");
   m.def("bump_step_(Tensor(a!) step) -> ()");
   m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
-        "Tensor? w2=None, Tensor(f!)? w2frag=None) -> ()");
+        "Tensor? w2=None, Tensor(f!)? w2frag=None, int coll=-1) -> ()");
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "

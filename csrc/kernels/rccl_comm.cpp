@@ -302,6 +302,63 @@ void rccl_all_to_all(int64_t h, at::Tensor& out, const at::Tensor& in) {
   check(r.group_end(), "ncclGroupEnd");
 }
 
+// One pairwise exchange as one RCCL group: `send` to rank `peer` and `recv` from it (both on the
+// current stream, so the step that follows reads `recv` in stream order). The Adasum
+// vector-halving / distance-doubling exchange (mihvd/parallel/adasum.py); an empty side is skipped.
+void rccl_send_recv(int64_t h, const at::Tensor& send, at::Tensor& recv, int64_t peer) {
+  Comm* c = get(h);
+  check_dev(c, send, "rccl_send_recv: send");
+  check_dev(c, recv, "rccl_send_recv: recv");
+  TORCH_CHECK(peer >= 0 && peer < c->world && peer != c->rank, "rccl_send_recv: bad peer ", peer);
+  TORCH_CHECK(send.scalar_type() == recv.scalar_type(), "rccl_send_recv: one dtype");
+  Rccl& r = rccl();
+  TORCH_CHECK(r.send != nullptr && r.recv != nullptr, "rccl_send_recv: librccl lacks ncclSend / ncclRecv");
+  if (send.numel() == 0 && recv.numel() == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  const ncclDataType_t dt = dtype_of(send);
+  check(r.group_start(), "ncclGroupStart");
+  if (send.numel() > 0) check(r.send(send.data_ptr(), (size_t)send.numel(), dt, (int)peer, c->comm, stream), "ncclSend");
+  if (recv.numel() > 0) check(r.recv(recv.data_ptr(), (size_t)recv.numel(), dt, (int)peer, c->comm, stream), "ncclRecv");
+  check(r.group_end(), "ncclGroupEnd");
+}
+
+// Uneven all-to-all (hvd.alltoall with splits): rows [soff[j], soff[j] + scnt[j]) of `in` (in
+// elements) go to rank j, rows from rank j land at [roff[j], roff[j] + rcnt[j]) of `out`; one group
+// of point-to-point transfers in ring order, the own block a device copy.
+void rccl_all_to_all_v(int64_t h, at::Tensor& out, const at::Tensor& in, at::IntArrayRef scnt, at::IntArrayRef soff,
+                       at::IntArrayRef rcnt, at::IntArrayRef roff) {
+  Comm* c = get(h);
+  check_dev(c, out, "rccl_all_to_all_v: out");
+  check_dev(c, in, "rccl_all_to_all_v: in");
+  TORCH_CHECK(out.scalar_type() == in.scalar_type(), "rccl_all_to_all_v: one dtype");
+  const int W = c->world;
+  TORCH_CHECK((int)scnt.size() == W && (int)soff.size() == W && (int)rcnt.size() == W && (int)roff.size() == W,
+              "rccl_all_to_all_v: one count and offset per rank");
+  for (int j = 0; j < W; ++j)
+    TORCH_CHECK(scnt[j] >= 0 && soff[j] >= 0 && soff[j] + scnt[j] <= in.numel() && rcnt[j] >= 0 && roff[j] >= 0 &&
+                    roff[j] + rcnt[j] <= out.numel(),
+                "rccl_all_to_all_v: block ", j, " exceeds its tensor");
+  TORCH_CHECK(scnt[c->rank] == rcnt[c->rank], "rccl_all_to_all_v: the own block must keep its size");
+  Rccl& r = rccl();
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  const size_t es = in.element_size();
+  const char* src = static_cast<const char*>(in.data_ptr());
+  char* dst = static_cast<char*>(out.data_ptr());
+  if (scnt[c->rank] > 0)
+    C10_HIP_CHECK(hipMemcpyAsync(dst + roff[c->rank] * es, src + soff[c->rank] * es, scnt[c->rank] * es,
+                                 hipMemcpyDeviceToDevice, stream));
+  if (W == 1) return;
+  TORCH_CHECK(r.send != nullptr && r.recv != nullptr, "rccl_all_to_all_v: librccl lacks ncclSend / ncclRecv");
+  const ncclDataType_t dt = dtype_of(in);
+  check(r.group_start(), "ncclGroupStart");
+  for (int k = 1; k < W; ++k) {
+    const int to = (c->rank + k) % W, from = (c->rank - k + W) % W;
+    if (scnt[to] > 0) check(r.send(src + soff[to] * es, (size_t)scnt[to], dt, to, c->comm, stream), "ncclSend");
+    if (rcnt[from] > 0) check(r.recv(dst + roff[from] * es, (size_t)rcnt[from], dt, from, c->comm, stream), "ncclRecv");
+  }
+  check(r.group_end(), "ncclGroupEnd");
+}
+
 // 0 healthy, else the ncclResult_t of an asynchronous failure of the communicator.
 int64_t rccl_async_error(int64_t h) {
   Comm* c = get(h);
@@ -369,6 +426,9 @@ TORCH_LIBRARY_FRAGMENT(mihvd, m) {
   m.def("rccl_broadcast_(int comm, Tensor(a!) t, int root=0) -> ()", &mihvd::rccl_broadcast_);
   m.def("rccl_all_to_all(int comm, Tensor(a!) out, Tensor input) -> ()", &mihvd::rccl_all_to_all);
   m.def("rccl_all_reduce_many_(int comm, Tensor(a!)[] ts, int op=0) -> ()", &mihvd::rccl_all_reduce_many_);
+  m.def("rccl_send_recv(int comm, Tensor send, Tensor(a!) recv, int peer) -> ()", &mihvd::rccl_send_recv);
+  m.def("rccl_all_to_all_v(int comm, Tensor(a!) out, Tensor input, int[] scnt, int[] soff, int[] rcnt, int[] roff) -> ()",
+        &mihvd::rccl_all_to_all_v);
   m.def("rccl_async_error(int comm) -> int", &mihvd::rccl_async_error);
   m.def("rccl_comm_destroy(int comm, bool abort=False) -> ()", &mihvd::rccl_comm_destroy);
 }

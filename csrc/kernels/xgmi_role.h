@@ -157,6 +157,7 @@ __device__ __forceinline__ void xg_exit(const CollRole& c, unsigned e) {
 // absent ranks get an out-of-range offset (the load returns 0 without a memory access), so there
 // is no branch around any load (a branch makes hipcc wait for each load before the next).
 __device__ __forceinline__ void xg_gather(const CollRole& c, int bid, bool ok) {
+  if (c.world == 1) return;  // a world of one: no peer rows (the phase entry/exit alone)
   const int64_t cu = c.col_bytes >> 4;
   const int64_t U = (int64_t)c.R * cu;
   const uint32_t span = (uint32_t)((int64_t)c.total_rows * c.stride);
@@ -269,6 +270,15 @@ __device__ __forceinline__ void coll_role_data(const CollRole& c, int bid) {
   const bool ok = s_err == 0u;
   if (c.kind == COLL_GATHER) xg_gather(c, bid, ok);
   else if (c.kind == COLL_REDUCE) xg_reduce(c, bid, ok, s_e);
+}
+
+// A gather role only (the host checked the kind): keeps the reduce + Adam code, and its registers,
+// out of a host kernel that co-launches gathers alone (f32_conv1_fwd).
+__device__ __forceinline__ void coll_gather_run(const CollRole& c, int bid) {
+  bool ok;
+  const unsigned e = xg_enter(c, bid, ok);
+  xg_gather(c, bid, ok);
+  xg_exit(c, e);
 }
 
 // Run the role as block `bid` of its nblk role blocks (any blockDim >= kXgMaxRanks threads).

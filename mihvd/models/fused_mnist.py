@@ -272,6 +272,7 @@ class FusedMNISTTrainer:
         self.use_xgmi = False
         self._xgmi_mode = "off"
         self._roles = None
+        self._f32_gather_pending = False  # fp32 xGMI plane: the last update's row gather not yet run
         if self.gather:
             from ..parallel import xgmi as _xg
 
@@ -578,8 +579,11 @@ class FusedMNISTTrainer:
             main.wait_event(self._small_ev)
             self._small_ev = None
         wf = self.w2frag
+        # fp32 xGMI plane: the previous step's row gather (every peer's updated dense/kernel rows)
+        # runs on the first blocks of this launch, beside conv1 (the next reader of W3 is fc1_fwd)
+        coll = self._f32_gather_colaunch() if (self.collectives and self.shard_w3 and self.use_xgmi) else -1
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                        self.idx1, w2, wf)
+                        self.idx1, w2, wf, coll=coll)
         o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0])
         if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
@@ -730,21 +734,67 @@ class FusedMNISTTrainer:
                                               dict(p=self.params[mine], m=self.m[mine], v=self.v[mine], **hyper),
                                               out=self.gshard if self.keep_w3_grad else None,
                                               offset_elems=W3_START + r * R * 1024)
-        # every peer's updated rows into this rank's dense/kernel
+        # every peer's updated rows into this rank's dense/kernel: as a split-form launch pair (the
+        # flush before a state read, validation) and co-launched on the first blocks of the next
+        # step's conv1 (one 256-thread block per CU beside conv1's small blocks; at world 1 a fence
+        # of 8 blocks that enters and leaves the phase and moves nothing, so the forced step prices
+        # the entry)
         roles["gather"] = xp.prepare_gather("params", self.PH32_GATHER, 4096, R, 3136, offset_bytes=W3_START * 4)
+        roles["gather_co"] = xp.prepare_gather("params", self.PH32_GATHER, 4096, R, 3136, offset_bytes=W3_START * 4,
+                                               nblk=self._gather_nblk())
         self._roles = roles
+
+    def _gather_nblk(self) -> int:
+        """Role blocks of the row gather co-launched in conv1: one 256-thread block per CU at N > 1
+        (a multiple of 8 keeps conv1's XCD map), a fence of 8 blocks at world 1 (nothing to move).
+        MIHVD_XGMI_GATHER_NBLK overrides (a multiple of 8; the shared-device co-launch test bounds
+        it)."""
+        env = os.environ.get("MIHVD_XGMI_GATHER_NBLK")
+        if env:
+            return max(8, int(env) // 8 * 8)
+        if self.world == 1:
+            return 8
+        return max(8, min(256, torch.cuda.get_device_properties(self.device).multi_processor_count) // 8 * 8)
+
+    def _f32_gather_colaunch(self) -> int:
+        """The gather descriptor for this step's conv1 (on a shared GPU the gather runs split-form
+        right here and conv1 gets -1; xgmi.py colaunch)."""
+        R = self._roles
+        if R is None or R.get("kind") == "bf16" or R["lr"] != self.lr or R["keep"] != self.keep_w3_grad:
+            self._prepare_roles_f32()
+            R = self._roles
+        self._f32_gather_pending = False
+        return self.xplane.colaunch(R["gather_co"])
+
+    def flush_row_gather(self):
+        """fp32 xGMI plane: run the row gather of the last update now, split form, instead of in the
+        next step's conv1 launch (before the parameters are read as a whole, or the plane changes).
+        Collective: every rank calls it at the same point (gather_full_state, _set_plane, close)."""
+        if not getattr(self, "_f32_gather_pending", False) or self.xplane is None:
+            self._f32_gather_pending = False
+            return
+        R = self._roles
+        if R is None or R.get("kind") == "bf16":
+            self._prepare_roles_f32()
+            R = self._roles
+        self.xplane.run_split(R["gather"], in_step=True)
+        self._f32_gather_pending = False
 
     def _launch_step_f32_xgmi(self, x, rows, st, w2, wf, gconv):
         """Rest of the fp32 step on the direct xGMI plane (after the head), one stream:
 
             fc1_bwd (dgrad, dW3 -> region) | conv2_bwd | conv_reduce (small grads -> region) |
-            xGMI: small sum + Adam + bump, my dense/kernel rows' sum + Adam | xGMI: row gather
+            xGMI: small sum + Adam + bump, my dense/kernel rows' sum + Adam |
+            next step: conv1 [+ the row gather of every peer's updated rows, co-launched]
 
-        Buffer reuse follows the phase order (xgmi_role.h): a rank rewrites its gradients (next
-        fc1_bwd / conv_reduce) only after the row gather's phase, which every peer enters only
-        after its reductions (the readers of those gradients) completed; it rewrites its rows
-        (next reduction) only after every peer entered the next reduction phase, i.e. finished
-        this step's gather."""
+        The row gather overlaps the next step's conv1 (its blocks move the bytes on the CUs beside
+        conv1's small blocks); fc1_fwd, W3's first reader, follows that launch. Buffer reuse follows
+        the phase order (xgmi_role.h): a rank rewrites its gradients (next fc1_bwd / conv_reduce)
+        only after the row gather's phase (in its next conv1), which every peer enters only after its
+        reductions (the readers of those gradients) completed; it rewrites its rows (next
+        reduction) only after every peer entered the next reduction phase, i.e. finished its conv1
+        launch and with it this update's gather. A gather with nothing new to move (the first step,
+        after a flush) copies rows equal to the local ones."""
         o, G = self.ops, self.gview
         R = self._roles
         if R is None or R.get("kind") == "bf16" or R["lr"] != self.lr or R["keep"] != self.keep_w3_grad:
@@ -754,11 +804,10 @@ class FusedMNISTTrainer:
                       G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
-        if self.world > 1:
-            self.xplane.run_split(R["small"], R["rows"])
-            self.xplane.run_split(R["gather"], in_step=True)
-        else:  # a world of one (forced collectives): no peer to wait for, no row to gather
-            self.xplane.run_split(R["small"], R["rows"], enter=False)
+        # (at world 1, forced collectives, the entry runs too: a self-peer phase, priced like N > 1)
+        self.xplane.run_split(R["small"], R["rows"])
+        # the row gather of this update runs in the next step's conv1 launch (or flush_row_gather)
+        self._f32_gather_pending = True
         self._full_state_valid = False
 
     def _validate_xgmi_f32(self) -> bool:
@@ -1015,7 +1064,8 @@ class FusedMNISTTrainer:
         if not self.shard_w3 or self._full_state_valid:
             return
         self._join()
-        if self.f32:  # the fp32 rows are gathered every step; the Adam slots here
+        if self.f32:  # the fp32 rows are gathered every step (the last update's here); the Adam slots
+            self.flush_row_gather()
             R = self._f32_R
             for buf in (self.m, self.v):
                 w3 = buf[W3_START:].view(3136, 1024)
@@ -1045,7 +1095,7 @@ class FusedMNISTTrainer:
             from ..parallel.collectives import adasum_dispatch_
 
             segs = [(o - lo, o - lo + n) for o, n in SEGMENTS.values() if lo <= o < hi]
-            adasum_dispatch_(bucket, segs)
+            adasum_dispatch_(bucket, segs, comm=comm if comm is not None else self.ncomm)
             bucket.mul_(self.world)  # adam divides by size; Adasum output is already the combined gradient
             return
         comm = comm if comm is not None else self.ncomm
@@ -1118,8 +1168,9 @@ class FusedMNISTTrainer:
         torch.cuda.synchronize(self.device)
         if primary:
             self.steps_per_replay = steps_per_replay
-        if (self.op is not None and int(self.op) == 2) or self.debug_sync or self._host_collectives():
-            # Adasum / serialized mode / gloo collectives (host-side, not capturable): eager
+        if (self._adasum_host() or self.debug_sync or self._host_collectives()):
+            # Adasum over the process group / serialized mode / gloo collectives (host-side, not
+            # capturable): eager
             if primary:
                 self.graph = None
             return False
@@ -1150,6 +1201,17 @@ class FusedMNISTTrainer:
             self.graph = g
         return True
 
+    def _adasum_host(self) -> bool:
+        """Adasum whose exchanges run over the process group (no framework communicator, or ranks
+        on several nodes: the cross-node part): not capturable. On the framework-owned RCCL
+        communicator of a one-node world every exchange is an RCCL call on the stream."""
+        if self.op is None or int(self.op) != 2:
+            return False
+        from .. import basics
+
+        one_node = not basics.is_initialized() or basics._ctx.topology.cross_size == 1
+        return self.ncomm is None or not one_node
+
     def _host_collectives(self) -> bool:
         if not self.collectives:
             return False
@@ -1169,6 +1231,8 @@ class FusedMNISTTrainer:
         self._maybe_reshuffle(k)
         with trace_range(f"mihvd.graph_replay[{k} steps]"):
             g.replay()
+        if self.f32 and self.collectives and self.shard_w3 and self.use_xgmi:
+            self._f32_gather_pending = True  # the replay's last update: gathered by the next conv1
         self.global_step += k
         self._stat_steps += k
 
@@ -1290,6 +1354,8 @@ class FusedMNISTTrainer:
         plane, whose row gather of the last update would run in the next conv12_fwd launch,
         gathers the rows now. ``factor``: the fp32 factor-gather plane (sharded only)."""
         self._join()
+        if self.use_xgmi and self.shard_w3 and self.f32:
+            self.flush_row_gather()  # (collective: every rank switches planes together)
         if self.use_xgmi and self.shard_w3 and not self.f32 and not (xgmi and shard):
             torch.cuda.synchronize(self.device)
             T64 = self._T * 64
@@ -1491,6 +1557,7 @@ class FusedMNISTTrainer:
             self._rng.bit_generator.state = snap["rng"]
         self.global_step = snap["global_step"]
         self._full_state_valid = True
+        self._f32_gather_pending = False  # every rank's rows are the snapshot's
         self._refresh_shadow()  # (and the full W3 row shadow of the factor-gather plane)
         torch.cuda.synchronize(self.device)
 
@@ -1542,6 +1609,8 @@ class FusedMNISTTrainer:
             return
         import torch.distributed as dist
 
+        if self.f32 and self.use_xgmi and self.shard_w3 and not getattr(self, "_xplane_failed", False):
+            self.flush_row_gather()  # every rank's rows complete before the region goes away
         torch.cuda.synchronize(self.device)
         self.graph = None
         self._graphs = {}
@@ -1614,8 +1683,11 @@ class FusedMNISTTrainer:
 
         self._join()
         self.gather_full_state()  # collective; no-op unless the dense/kernel optimizer is sharded
-        for buf in (self.params, self.m, self.v, self.state):
-            dist.broadcast(buf, src=root_rank)
+        for buf in (self.params, self.m, self.v, self.state):  # (~39 MB: weights + Adam slots + counters)
+            if self.ncomm is not None:  # the framework-owned communicator, on the current stream
+                self.ncomm.broadcast_(buf, root_rank)
+            else:
+                dist.broadcast(buf, src=root_rank)
         from ..parallel.collectives import broadcast_object
 
         self.global_step = int(broadcast_object(self.global_step, root_rank))

@@ -1,9 +1,13 @@
 """Tensor collectives with Horovod semantics (``hvd.allreduce / allgather / broadcast / alltoall /
 reducescatter``, their grouped and ``_async`` forms, sparse allreduce, ``synchronize`` and ``poll``).
 
-Each call is one RCCL collective on the process group (``nccl`` backend = RCCL over xGMI on
-MI355X; ``gloo`` on CPU). Async calls return an integer handle; the native stall inspector tracks
-every outstanding handle and the native timeline records a span per collective.
+On GPUs over RCCL (world size > 1, or the collectives forced on) each world-level call is one
+RCCL collective on the framework-owned communicator of :class:`BucketPlane` (NativeComm on its own
+high-priority stream, the same one DistributedOptimizer's buckets use), ordered after the caller's
+stream by an event; the handle's wait orders the caller's stream after it (no host block). Process
+sets, host tensors, gloo, a running negotiation engine and the all-ranks fallback (the plane could
+not be created) use the process group. Async calls return an integer handle; the native stall
+inspector tracks every outstanding handle and the native timeline records a span per collective.
 """
 from __future__ import annotations
 
@@ -154,6 +158,8 @@ def _allreduce_impl(tensor, out, name, op, compression, prescale_factor, postsca
     ctx = basics._require()
     op = ReduceOp(op)
     n = _group_size(group)
+    if plane is None and op != ReduceOp.Adasum:
+        plane = _api_plane(group, tensor)
     if op == ReduceOp.Adasum:
         if out is not tensor:
             out.copy_(tensor)
@@ -247,16 +253,37 @@ class BucketPlane:
         self.comm = NativeComm(device=device)
         self.stream = torch.cuda.Stream(device=device, priority=-1)
         self.launched = 0
+        self.counts: dict[str, int] = {}  # collectives issued per kind (the public API's routing test)
 
-    def allreduce(self, wire: torch.Tensor, op: ReduceOp) -> _PlaneWork:
+    def _run(self, kind: str, fn) -> _PlaneWork:
+        """``fn()`` on the plane's stream, ordered after everything the caller's stream queued so far
+        (the inputs are complete there); the work's wait() orders the caller's stream after it."""
         cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)  # the bucket's gradients are complete on the producing stream
+        self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
-            self.comm.all_reduce_(wire, self._OPS[op])
+            fn()
             ev = torch.cuda.Event()
             ev.record(self.stream)
         self.launched += 1
+        self.counts[kind] = self.counts.get(kind, 0) + 1
         return _PlaneWork(ev, self.device)
+
+    def allreduce(self, wire: torch.Tensor, op: ReduceOp) -> _PlaneWork:
+        return self._run("allreduce", lambda: self.comm.all_reduce_(wire, self._OPS[op]))
+
+    # the public collective API (hvd.broadcast / allgather / reducescatter / alltoall) on the same
+    # communicator and stream: every rank issues them in program order, like the bucket allreduces
+    def broadcast(self, t: torch.Tensor, root: int) -> _PlaneWork:
+        return self._run("broadcast", lambda: self.comm.broadcast_(t, root))
+
+    def allgather(self, out: torch.Tensor, inp: torch.Tensor) -> _PlaneWork:
+        return self._run("allgather", lambda: self.comm.all_gather_into(out, inp))
+
+    def reducescatter(self, out: torch.Tensor, inp: torch.Tensor, op: ReduceOp) -> _PlaneWork:
+        return self._run("reducescatter", lambda: self.comm.reduce_scatter(out, inp, self._OPS[op]))
+
+    def alltoall(self, out: torch.Tensor, inp: torch.Tensor, scnt, soff, rcnt, roff) -> _PlaneWork:
+        return self._run("alltoall", lambda: self.comm.all_to_all_v(out, inp, scnt, soff, rcnt, roff))
 
     def close(self, abort: bool = False):
         self.comm.close(abort=abort)
@@ -304,6 +331,22 @@ def bucket_plane():
     return plane
 
 
+def _api_plane(group, *tensors):
+    """The framework-owned communicator for a public collective (``hvd.allreduce`` outside
+    DistributedOptimizer, ``broadcast*``, ``allgather*``, ``reducescatter``, ``alltoall``): the whole
+    world, device tensors, the RCCL backend with ``MIHVD_COMM=native``, no negotiation engine (which
+    orders named collectives itself). Otherwise None: the process group (sub-groups, gloo, the
+    fallback every rank takes together when the plane cannot be created)."""
+    if group is not None and group is not dist.group.WORLD:
+        return None
+    ctx = basics._ctx
+    if ctx.engine is not None or not tensors or not all(t.is_cuda for t in tensors):
+        return None
+    if not plane_wanted():
+        return None
+    return bucket_plane()
+
+
 def _capturing() -> bool:
     return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
@@ -319,18 +362,30 @@ def _engine_allreduce(ctx, name, wire, torch_op, group, fuse_extra):
     return dist.all_reduce(wire, op=torch_op, group=group, async_op=True)
 
 
-def adasum_dispatch_(flat: torch.Tensor, segments=None):
+def adasum_dispatch_(flat: torch.Tensor, segments=None, comm=None):
     """Adasum with Horovod-GPU semantics: hierarchical (average within node, Adasum across nodes)
-    on the RCCL data plane, flat Adasum on gloo or when MIHVD_ADASUM_FLAT=1."""
+    on the RCCL data plane, flat Adasum on gloo or when MIHVD_ADASUM_FLAT=1. On RCCL the world-level
+    parts run on a framework-owned communicator (``comm``, else the bucket plane's): the node-local
+    average when the node is the world, and flat Adasum as vector halving / distance doubling over
+    ncclSend/ncclRecv (adasum.adasum_vhdd_) -- no host wait, capturable in a HIP graph. The
+    cross-node Adasum of the hierarchical form runs over the cross-node process group."""
     from .adasum import adasum_allreduce_
 
     ctx = basics._require()
     topo = ctx.topology
+    if comm is None and flat.is_cuda and ctx.backend == "nccl":
+        plane = bucket_plane()
+        comm = plane.comm if plane is not None else None
+        if plane is not None:
+            plane.launched += 1
     hierarchical = (ctx.backend == "nccl" and not ctx.config.adasum_flat and topo.local_size > 1
                     and ctx.local_group is not None)
     if not hierarchical:
-        return adasum_allreduce_(flat, segments)
-    dist.all_reduce(flat, group=ctx.local_group)
+        return adasum_allreduce_(flat, segments, comm=comm if comm is not None and comm.world == topo.size else None)
+    if comm is not None and topo.cross_size == 1 and comm.world == topo.size:
+        comm.all_reduce_(flat)  # the node is the world: the local average on the framework's communicator
+    else:
+        dist.all_reduce(flat, group=ctx.local_group)
     flat.div_(topo.local_size)
     if topo.cross_size > 1:
         ranks = list(range(topo.local_rank, topo.size, topo.local_size))
@@ -460,7 +515,10 @@ def broadcast_async_(tensor, root_rank, name=None, process_set=None) -> int:
     ctx = basics._require()
     group = _group(process_set)
     name = f"broadcast.{name or 'tensor'}"
-    if _group_size(group) == 1:
+    plane = _api_plane(group, tensor) if tensor.is_contiguous() else None
+    if plane is not None:  # (also at world 1 with the collectives forced on)
+        work = plane.broadcast(tensor, root_rank)
+    elif _group_size(group) == 1:
         work = None
     elif ctx.engine is not None:
         work = ctx.engine.collective(name, "broadcast", f"{tensor.dtype}|{tuple(tensor.shape)}|{root_rank}",
@@ -489,11 +547,31 @@ def allgather_async(tensor, name=None, process_set=None) -> int:
     group = _group(process_set)
     n = _group_size(group)
     name = f"allgather.{name or 'tensor'}"
-    if n == 1:
-        return _register(None, tensor.clone(), None, name)
     t = tensor.contiguous()
     if t.dim() == 0:
         t = t.view(1)
+    plane = _api_plane(group, t)
+    if plane is not None:
+        # dim 0 may differ per rank: the sizes first (one 8-byte all-gather on the plane, read on
+        # the host), then every rank's rows padded to the largest
+        dim0 = torch.tensor([t.shape[0]], dtype=torch.long, device=t.device)
+        sizes_dev = torch.empty(n, dtype=torch.long, device=t.device)
+        plane.allgather(sizes_dev, dim0).wait()
+        sizes = [int(v) for v in sizes_dev.tolist()]
+        mx = max(sizes)
+        if mx != t.shape[0]:
+            t = torch.cat([t, torch.zeros((mx - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)])
+        full = torch.empty((n * mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        work = plane.allgather(full, t)
+
+        def post_plane(_o, full=full, sizes=sizes, mx=mx):
+            if all(sz == mx for sz in sizes):
+                return full
+            return torch.cat([full[i * mx:i * mx + sz] for i, sz in enumerate(sizes)])
+
+        return _register(work, None, post_plane, name)
+    if n == 1:
+        return _register(None, tensor.clone(), None, name)
     res: dict = {}
 
     def launch(t=t):
@@ -552,6 +630,24 @@ def alltoall(tensor, splits=None, name=None, process_set=None):
             raise ValueError("alltoall: first dimension must divide the world size when splits is None")
         splits = [tensor.shape[0] // n] * n
     splits = [int(s) for s in (splits.tolist() if torch.is_tensor(splits) else splits)]
+    plane = _api_plane(group, tensor)
+    if plane is not None:
+        t = tensor.contiguous()
+        row = 1
+        for d in t.shape[1:]:
+            row *= int(d)
+        send_counts = torch.tensor(splits, dtype=torch.long, device=t.device)
+        recv_counts = torch.empty_like(send_counts)
+        ones = [1] * n
+        offs = list(range(n))
+        plane.alltoall(recv_counts, send_counts, ones, offs, ones, offs).wait()
+        rsplits = [int(x) for x in recv_counts.tolist()]
+        out = torch.empty((sum(rsplits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        soff = [sum(splits[:j]) * row for j in range(n)]
+        roff = [sum(rsplits[:j]) * row for j in range(n)]
+        plane.alltoall(out.view(-1), t.view(-1), [c * row for c in splits], soff, [c * row for c in rsplits],
+                       roff).wait()
+        return out, torch.tensor(rsplits)
     if n == 1:
         return tensor.clone(), torch.tensor(splits)
     send_counts = torch.tensor(splits, dtype=torch.long, device=tensor.device)
@@ -609,14 +705,27 @@ def reducescatter(tensor, op=ReduceOp.Average, name=None, process_set=None):
     _flush_engine()
     group = _group(process_set)
     n = _group_size(group)
-    if n == 1:
-        return tensor.clone()
     op = ReduceOp(op)
     t = tensor.contiguous()
+    plane = _api_plane(group, t) if op in BucketPlane._OPS else None
+    if plane is None and n == 1:
+        return tensor.clone()
     dim0 = t.shape[0]
     base, rem = divmod(dim0, n)
     counts = [base + (1 if i < rem else 0) for i in range(n)]
     me = dist.get_rank(group) if group is not None else basics.rank()
+    if plane is not None:
+        if rem == 0:
+            out = torch.empty((counts[me],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            plane.reducescatter(out, t, op).wait()
+        else:  # uneven blocks: the whole reduction, then this rank's rows
+            full = t.clone()
+            plane.allreduce(full, op).wait()
+            start = sum(counts[:me])
+            out = full[start:start + counts[me]].clone()
+        if op == ReduceOp.Average:
+            out.div_(n)
+        return out
     if rem == 0 and basics.backend() == "nccl":
         out = torch.empty((counts[me],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.reduce_scatter_tensor(out, t, op=_torch_op(op), group=group)

@@ -91,6 +91,17 @@ class NativeComm:
         self._o.rccl_all_to_all(self.handle, out, inp)
         return out
 
+    def send_recv(self, send: torch.Tensor, recv: torch.Tensor, peer: int) -> torch.Tensor:
+        """One pairwise exchange with ``peer`` (an RCCL group of one send and one receive)."""
+        self._o.rccl_send_recv(self.handle, send, recv, int(peer))
+        return recv
+
+    def all_to_all_v(self, out: torch.Tensor, inp: torch.Tensor, scnt, soff, rcnt, roff) -> torch.Tensor:
+        """Uneven all-to-all over flat element ranges (counts and offsets in elements, one per rank)."""
+        self._o.rccl_all_to_all_v(self.handle, out, inp, [int(v) for v in scnt], [int(v) for v in soff],
+                                  [int(v) for v in rcnt], [int(v) for v in roff])
+        return out
+
     def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
         self._o.rccl_broadcast_(self.handle, t, root)
         return t

@@ -125,6 +125,13 @@ class XGMIRegion:
         keys = [None] * self.world
         dist.all_gather_object(keys, (props.pci_domain_id, props.pci_bus_id, props.pci_device_id), group=group)
         self.shared_device = len(set(keys)) < self.world
+        # MIHVD_XGMI_COLAUNCH_SHARED=1 (tests): keep the co-launch form on a shared device at two
+        # ranks -- the exact form every rank of a real node runs -- with the hosts' role blocks
+        # bounded (MIHVD_XGMI_GATHER_NBLK, the bf16 plane's fixed nblk), so the two ranks' spinning
+        # role blocks cannot hold every CU the other's launch needs to reach the phase
+        self.colaunch_shared = (self.shared_device and self.world <= 2
+                                and os.environ.get("MIHVD_XGMI_COLAUNCH_SHARED", "0") == "1")
+        self.colaunched = 0  # collectives co-launched in a compute launch (not run split-form)
         self._views = {}
         self._closed = False
 
@@ -201,7 +208,10 @@ class XGMIRegion:
         """The id to hand a compute op for co-launching ``role``; on a shared device the role runs
         here, split form, before that op (same stream, so it still follows every earlier launch and
         precedes every later reader), and the op gets -1."""
-        if role < 0 or not self.shared_device:
+        if role < 0:
+            return role
+        if not self.shared_device or self.colaunch_shared:
+            self.colaunched += 1
             return role
         self._o.xgmi_run_split(role, -1, bool(in_step), True)
         return -1

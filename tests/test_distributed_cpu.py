@@ -97,6 +97,22 @@ def test_adasum(tmp_path, np_):
         assert o["param_spread"] < 1e-6
 
 
+@pytest.mark.parametrize("np_", [2, 3, 4, 8])
+def test_adasum_vector_halving(tmp_path, np_):
+    """Adasum by vector halving / distance doubling (mihvd/parallel/adasum.py adasum_vhdd_; the
+    same code runs over the framework-owned RCCL communicator on GPUs) matches the single-process
+    oracle of the pairing tree at 2, 3 (one folded rank), 4 and 8 ranks, and a power-of-two rank
+    sends about 2 S (N - 1) / N bytes (whole-vector doubling: log2(N) S)."""
+    _, outs = run_scenario(tmp_path, "adasum_vhdd", np_=np_, timeout=240)
+    p2 = 1 << (np_.bit_length() - 1)
+    for pos, o in enumerate(outs):
+        assert o["rel"] < 1e-5, o
+        S = o["numel"] * o["elem"]
+        if pos < p2 and p2 == np_:
+            assert o["bytes"] <= 2 * S * (np_ - 1) / np_ + 64 * 4 * 2 * np_, (o, S)
+            assert o["bytes"] < S * max(1, (np_ - 1).bit_length()) or np_ == 2
+
+
 def test_broadcast_optimizer_state(tmp_path):
     _, (a, b) = run_scenario(tmp_path, "optimizer_state")
     assert a == b and a["nstate"] > 0 and a["lr"] == pytest.approx(1e-3)

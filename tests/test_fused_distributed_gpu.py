@@ -65,6 +65,24 @@ def test_collectives_inside_hip_graph(tmp_path, prec, shard, xgmi, comm):
         assert set(r["select"]["us_per_step"]) == planes, r
 
 
+def test_adasum_fused_step_inside_hip_graph(tmp_path):
+    """op=Adasum on the framework-owned communicator (vector halving / distance doubling over
+    ncclSend/ncclRecv, adasum.adasum_vhdd_, no host wait) is captured in the trainer's HIP graph
+    like the average; at world 1 (collectives forced on) it is the identity, so the replayed steps
+    equal the trainer without collectives bit for bit."""
+    _gpu()
+    env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3="0",
+               MIHVD_XGMI="off", MIHVD_TEST_PRECISION="fp32", MIHVD_COMM="native", MIHVD_TEST_OP="adasum")
+    for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, WORKER, "rccl_graph", str(tmp_path)], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = json.loads((tmp_path / "rccl_graph.json").read_text())
+    assert r["captured"] and r["native_comm"], r
+    assert r["steps"] == r["pre_steps"] + 22 and r["bitwise"], r
+
+
 def test_f32_factor_plane_inside_hip_graph(tmp_path):
     """The fp32 factor-gather plane (MIHVD_F32_PLANE=factor) at world 1 with the collectives forced
     on, on the native communicator: dz all-gather, a2-column all-to-all and the hand-written dW3-row
@@ -101,26 +119,37 @@ def test_fused_data_parallel_equivalence_two_ranks(tmp_path):
         assert o["rel_update_diff"] < 0.05, o
 
 
+@pytest.mark.parametrize("form", ["split", "colaunch"])
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])
-def test_fused_data_parallel_xgmi_two_ranks(tmp_path, prec):
+def test_fused_data_parallel_xgmi_two_ranks(tmp_path, prec, form):
     """bf16: the factor-gather plane over the direct xGMI collectives (a2/dz gathers and the
     small-gradient reduction read the peer's region in place). fp32: the fp32 plane (sharded rows:
-    one-shot reductions with Adam, then the row gather). gloo only carries the IPC handle
-    exchange."""
+    one-shot reductions with Adam, then the row gather co-launched in the next step's conv1).
+    gloo only carries the IPC handle exchange. form=split: what ranks sharing a GPU run (every
+    collective as a split-form launch pair); colaunch: the form each rank of a real node runs (the
+    collectives on the first blocks of the compute launches), kept on the shared GPU at two ranks
+    with bounded role blocks (MIHVD_XGMI_COLAUNCH_SHARED, MIHVD_XGMI_GATHER_NBLK)."""
     _gpu()
     # both ranks share this one GPU: a rank's spinning phase barrier can wait for the other process's
     # kernels to be scheduled, so the device-side timeout is raised from 20 s (a timeout still fails)
     env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="on", MIHVD_XGMI_TIMEOUT_MS="60000",
                MIHVD_TEST_PRECISION=prec, MIHVD_SHARD_W3="1" if prec == "fp32" else "0")
+    if form == "colaunch":
+        env.update(MIHVD_XGMI_COLAUNCH_SHARED="1", MIHVD_XGMI_GATHER_NBLK="64")
     cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo", str(tmp_path)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(2):
         o = json.loads((tmp_path / f"dp_gloo.{r}.json").read_text())
         assert o["xgmi"], o
-        assert o["rank_spread"] == 0.0
+        assert o["rank_spread"] == 0.0 and o["w3_rank_spread"] == 0.0, o
         assert o["grad_rel"] < 1e-4, o
         assert o["rel_update_diff"] < 0.05, o
+        assert o["shared_device"] and o["xgmi_error"] == 0, o
+        if form == "colaunch":
+            assert o["colaunched"] >= 3, o  # every step's co-launched collectives ran in that form
+        else:
+            assert o["colaunched"] == 0, o
 
 
 @pytest.mark.parametrize("xgmi", ["off", "on"])

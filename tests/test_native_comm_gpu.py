@@ -92,7 +92,9 @@ def test_native_engine_ranks_out_of_order(tmp_path, nranks):
 
 
 def test_bucket_plane_carries_distributed_optimizer(tmp_path):
-    """DistributedOptimizer's buckets go through the framework-owned RCCL bucket plane
+    """DistributedOptimizer's buckets -- and the public collective API (allreduce, broadcast,
+    allgather, reducescatter, alltoall, broadcast_parameters) -- go through the framework-owned RCCL
+    bucket plane
     (collectives.BucketPlane: NativeComm on a high-priority side stream), eagerly and inside a
     captured whole-step HIP graph, and bench.py --impl torch / torch-graph report it as the
     communicator (config.rccl_comm, RCCL's own count in config.rccl_nranks). World size 1 with the
@@ -116,6 +118,14 @@ def test_bucket_plane_carries_distributed_optimizer(tmp_path):
         assert r[key]["plane"] and r[key]["nranks"] == 1, r
         assert r[key]["launched"] >= r[key]["buckets"] * 3, r  # every bucket of every step (eager warm-up too)
         assert r[key]["rel"] <= max(10 * r[key]["noise"], 1e-6), r
+    # the public API outside DistributedOptimizer goes through the same plane (a launch per call)
+    assert all(r["api"].values()), r["api"]
+    c = r["api_counts"]
+    assert c.get("allreduce", 0) >= 3 and c.get("broadcast", 0) >= 2 and c.get("allgather", 0) >= 2, c
+    assert c.get("reducescatter", 0) >= 1 and c.get("alltoall", 0) >= 2, c
+    # after an elastic reset the optimizer's buckets run on the new world's plane
+    e = r["elastic"]
+    assert e["had_plane"] and e["new_plane"] and e["uses_new"] and e["launched_after"] >= 2, e
     for i, impl in enumerate(("torch", "torch-graph")):
         p = subprocess.run(run + [str(29567 + i), os.path.join(ROOT, "bench.py"), "--impl", impl, "--steps", "10",
                                   "--warmup", "3"], env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)

@@ -171,6 +171,29 @@ def sc_adasum(outdir):
     out(outdir, "adasum", {"diff": d, "param_spread": (allp - allp[0]).abs().max().item()})
 
 
+def sc_adasum_vhdd(outdir):
+    """Vector-halving / distance-doubling Adasum (adasum.adasum_vhdd_ over the process group) on a
+    vector of several tensors with gaps, against the single-process oracle of the same pairing tree,
+    and this rank's sent bytes."""
+    from mihvd.parallel import adasum as A
+
+    r, n = hvd.rank(), hvd.size()
+    g = torch.Generator().manual_seed(11)
+    N = 10_000
+    segs = [(0, 3200), (3264, 3296), (3328, 8128), (8192, 8256), (8320, 9990)]
+    vecs = []
+    for i in range(n):
+        v = torch.randn(N, generator=g) * (1.0 + 0.3 * i)
+        for (s0, e0), (s1, _) in zip(segs, segs[1:] + [(N, N)]):
+            v[e0:s1] = 0.0  # the gaps (alignment padding of a fusion buffer) are zero
+        vecs.append(v)
+    ref = A.adasum_reference(vecs, segs)
+    got = vecs[r].clone()
+    A.adasum_allreduce_(got, segs)
+    rel = ((got - ref).norm() / ref.norm()).item()
+    out(outdir, "adasum_vhdd", {"rel": rel, "bytes": A.last_bytes_sent, "numel": N, "elem": 4})
+
+
 def sc_optimizer_state(outdir):
     r = hvd.rank()
     m = _model(seed=r)

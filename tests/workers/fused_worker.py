@@ -30,7 +30,8 @@ def sc_rccl_graph(outdir):
     # schedules of different lengths see the same batches
     X, Y = data(5000)
     prec = os.environ.get("MIHVD_TEST_PRECISION", "bf16")
-    a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda", precision=prec,
+    op = hvd.Adasum if os.environ.get("MIHVD_TEST_OP") == "adasum" else None
+    a = FusedMNISTTrainer(batch_size=100, seed=1, device="cuda", precision=prec, op=op,
                           shard_optimizer=os.environ.get("MIHVD_SHARD_W3") == "1")
     assert a.collectives, "MIHVD_FORCE_COLLECTIVES should enable the allreduce path"
     a.set_device_dataset(X, Y, seed=4)
@@ -99,8 +100,14 @@ def sc_dp_gloo(outdir):
     mx = (tr.params - ref.params).abs().max().item()
     spread = hvd.allgather(tr.params[:4096].cpu().view(1, -1))
     tr.check_xgmi()
+    w3 = tr.params[FLAT_W3:].view(3136, 1024)
+    w3_spread = hvd.allgather(w3[::97].cpu().reshape(1, -1))  # every rank's copy of dense/kernel (sampled)
     rec = {"gather": tr.gather, "xgmi": tr.data_plane() == "xgmi", "grad_rel": grel, "rel_update_diff": rel, "max": mx,
-           "rank_spread": (spread - spread[0]).abs().max().item()}
+           "rank_spread": (spread - spread[0]).abs().max().item(),
+           "w3_rank_spread": (w3_spread - w3_spread[0]).abs().max().item(),
+           "colaunched": getattr(tr.xplane, "colaunched", 0) if tr.xplane is not None else 0,
+           "shared_device": bool(getattr(tr.xplane, "shared_device", False)),
+           "xgmi_error": int(tr.ops.xgmi_error(tr.xplane.ctx)) if tr.xplane is not None else None}
     tr.close()
     with open(os.path.join(outdir, f"dp_gloo.{r}.json"), "w") as f:
         json.dump(rec, f)

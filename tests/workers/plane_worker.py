@@ -76,6 +76,36 @@ def main(out):
                     "buckets": len(o._buckets), "bitwise": bool(torch.equal(a, b)),
                     "rel": float((a - b).norm() / b.norm()), "noise": float((c - b).norm() / b.norm()),
                     "nranks": plane.comm.nranks() if plane is not None else None}
+    # the public collective API on the same framework-owned communicator (world 1, collectives forced
+    # on: every result is the identity), counted per kind by the plane
+    plane = basics._ctx.plane
+    c0 = dict(plane.counts) if plane is not None else {}
+    t = torch.arange(12, dtype=torch.float32, device=dev)
+    api = {
+        "allreduce": torch.equal(hvd.allreduce(t, op=hvd.Sum), t) and torch.equal(hvd.allreduce(t), t),
+        "allreduce_async": torch.equal(hvd.synchronize(hvd.allreduce_async(t.clone(), op=hvd.Sum)), t),
+        "broadcast": torch.equal(hvd.broadcast(t, 0), t),
+        "allgather": torch.equal(hvd.allgather(t.view(3, 4)), t.view(3, 4)),
+        "reducescatter": torch.equal(hvd.reducescatter(t.view(3, 4), op=hvd.Sum), t.view(3, 4)),
+        "alltoall": torch.equal(hvd.alltoall(t.view(6, 2))[0], t.view(6, 2)),
+    }
+    m0, _ = make(False)
+    hvd.broadcast_parameters(m0.state_dict(), 0)
+    c1 = dict(plane.counts) if plane is not None else {}
+    res["api"] = api
+    res["api_counts"] = {k: c1.get(k, 0) - c0.get(k, 0) for k in set(c1) | set(c0)}
+    # an elastic reset (mihvd.elastic: shutdown + init, then State.sync -> _elastic_reset) must move a
+    # DistributedOptimizer onto the new world's bucket plane
+    m1, o1 = make(True)
+    old = o1._plane
+    hvd.shutdown()
+    hvd.init()
+    o1._elastic_reset()
+    new_plane = basics._ctx.plane
+    train(m1, o1, 2, False)
+    res["elastic"] = {"had_plane": old is not None, "new_plane": new_plane is not None and new_plane is not old,
+                      "uses_new": o1._plane is new_plane,
+                      "launched_after": new_plane.launched if new_plane is not None else 0}
     with open(out, "w") as f:
         json.dump(res, f)
     hvd.shutdown()
