@@ -76,6 +76,8 @@
 #include <unordered_set>
 #include <vector>
 
+#include "../runtime/slot_agreement.h"
+
 namespace mihvd {
 
 // rccl_comm.cpp: the communicator behind a handle and the library's entry points
@@ -125,11 +127,7 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
-uint32_t fnv32(const std::string& s) {
-  uint32_t h = 2166136261u;
-  for (unsigned char c : s) h = (h ^ c) * 16777619u;
-  return h == 0 ? 1u : h;  // 0 means "nothing pending" / "no signature"
-}
+uint32_t fnv32(const std::string& s) { return engine_fnv32(s); }  // 0 is reserved: "nothing pending"
 
 int nccl_dtype(at::ScalarType t) {
   switch (t) {
@@ -181,60 +179,8 @@ struct Slot {
 
 }  // namespace
 
-// Pure planning step, shared by the engine loop and the CPU unit test (engine_plan op): given the
-// summed control vector, the slots' hashes and sizes/fuse keys, return the ready slots grouped for
-// fusion (-1 separates groups), or an error on a signature mismatch.
-std::vector<int64_t> engine_plan_groups(const int32_t* sum, int nslot, int world, const std::vector<uint32_t>& hash,
-                                        const std::vector<int64_t>& bytes, const std::vector<int64_t>& key,
-                                        int64_t threshold, std::vector<int>* partial, std::string* error) {
-  std::vector<int64_t> out;
-  int64_t cur_bytes = 0, cur_key = -1;
-  bool open = false;
-  for (int s = 0; s < nslot; ++s) {
-    const int cnt = sum[2 + s];
-    if (cnt == 0) continue;
-    if (cnt < world) {
-      if (partial) partial->push_back(s);
-      continue;
-    }
-    const uint32_t hs = (uint32_t)sum[2 + nslot + s];
-    if (hs != (uint32_t)((uint32_t)world * hash[s])) {
-      if (error) *error = "slot " + std::to_string(s) + ": ranks enqueued different collectives (name/dtype/size/op)";
-      return {};
-    }
-    const bool big = bytes[s] > threshold;
-    if (open && (big || key[s] != cur_key || cur_bytes + bytes[s] > threshold)) {
-      out.push_back(-1);
-      open = false;
-    }
-    out.push_back(s);
-    if (big) {
-      out.push_back(-1);
-      continue;
-    }
-    if (!open) {
-      open = true;
-      cur_bytes = 0;
-      cur_key = key[s];
-    }
-    cur_bytes += bytes[s];
-  }
-  if (open) out.push_back(-1);
-  return out;
-}
-
-// Slot agreement (step 3): `gathered` holds world x K announced hashes (0 = empty entry). Returns
-// the hashes that get new slots, in the order every rank appends them: the sorted union of the
-// announced hashes that have no slot yet. A pure function of data every rank holds identically.
-std::vector<uint32_t> engine_new_slot_order(const int32_t* gathered, int world, int K,
-                                            const std::unordered_set<uint32_t>& assigned) {
-  std::set<uint32_t> fresh;
-  for (int i = 0; i < world * K; ++i) {
-    const uint32_t h = (uint32_t)gathered[i];
-    if (h != 0 && assigned.count(h) == 0) fresh.insert(h);
-  }
-  return std::vector<uint32_t>(fresh.begin(), fresh.end());
-}
+// engine_plan_groups / engine_new_slot_order and the slot table itself (SlotAgreement) live in
+// csrc/runtime/slot_agreement.h: the same code runs over the TCP store in the CPU tests.
 
 namespace {
 
@@ -254,7 +200,8 @@ class Engine {
         abort_s_(abort_s),
         cap_((int)max_slots),
         stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_)),
-        ctrl_stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_)) {
+        ctrl_stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_)),
+        agree_(world_, (int)max_slots, kAnnounce) {
     TORCH_CHECK(rccl_comm_world(ctrl_comm) == world_ && rccl_comm_device(ctrl_comm) == device_,
                 "engine: the control communicator must span the same ranks and device");
     c10::hip::HIPGuard g((c10::DeviceIndex)device_);
@@ -266,6 +213,7 @@ class Engine {
     ann_host_ = at::zeros({(int64_t)world_ * kAnnounce + kAnnounce}, i32.pinned_memory(true));
     hip_check(hipEventCreateWithFlags(&ctrl_ev_, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventCreateWithFlags(&data_ev_, hipEventDisableTiming), "hipEventCreate");
+    ctrl_.e = this;
     thread_ = std::thread([this] { loop(); });
   }
 
@@ -438,15 +386,13 @@ class Engine {
     while (!queue_.empty()) {
       Item it = std::move(queue_.front());
       queue_.pop_front();
-      auto f = slot_of_hash_.find(it.hash);
-      if (f != slot_of_hash_.end()) {
-        slot_for_local(f->second, it).pending.push_back(std::move(it.req));
+      const int s = agree_.slot(it.hash);
+      if (s >= 0) {
+        slot_for_local(s, it).pending.push_back(std::move(it.req));
         continue;
       }
-      auto& st = unassigned_[it.hash];
-      if (st.empty() && std::find(announce_.begin(), announce_.end(), it.hash) == announce_.end())
-        announce_.push_back(it.hash);
-      st.push_back(std::move(it));
+      agree_.want(it.hash);  // announced in the coming cycles
+      unassigned_[it.hash].push_back(std::move(it));
     }
   }
 
@@ -516,31 +462,20 @@ class Engine {
           drain_locked();
           stopping = stopping_;
         }
-        // 2. negotiation on the control communicator
-        int32_t* hv = ctrl_host_.data_ptr<int32_t>();
+        // 2. negotiation on the control communicator (slot_agreement.h)
         const int S = cap_;
-        std::fill(hv, hv + 2 + 2 * S, 0);
+        std::vector<int> pending;
         bool any_pending = !unassigned_.empty();
         for (size_t s = 0; s < slots_.size(); ++s)
           if (!slots_[s].pending.empty()) {
-            hv[2 + s] = 1;
-            hv[2 + S + s] = (int32_t)slots_[s].hash;
+            pending.push_back((int)s);
             any_pending = true;
           }
         // a stopping rank first drains its own pending work (its peers will match it)
-        hv[0] = (stopping && !any_pending) ? 1 : 0;
-        hv[1] = announce_.empty() ? 0 : 1;
-        // the control communicator's kernels never run beside the data communicator's: the
-        // negotiation of this cycle follows the last cycle's collectives (two communicators whose
-        // kernels overlap in different orders on different ranks can deadlock)
-        hip_check(hipStreamWaitEvent(cst, data_ev_, 0), "hipStreamWaitEvent");
-        hip_check(hipMemcpyAsync(ctrl_dev_.data_ptr(), hv, (2 + 2 * S) * 4, hipMemcpyHostToDevice, cst), "H2D");
-        std::string err;
-        if (rccl_all_reduce_raw(ctrl_dev_.data_ptr(), 2 + 2 * S, ncclInt32, ncclSum, ctrl_comm_, cst, &err) != 0)
-          throw std::runtime_error("negotiation allreduce: " + err);
-        hip_check(hipMemcpyAsync(hv, ctrl_dev_.data_ptr(), (2 + 2 * S) * 4, hipMemcpyDeviceToHost, cst), "D2H");
-        hip_check(hipEventRecord(ctrl_ev_, cst), "hipEventRecord");
-        wait_ctrl(ctrl_ev_, stopping && !any_pending);
+        ctrl_.quiet = stopping && !any_pending;
+        const std::vector<int32_t> summed = agree_.negotiate(ctrl_, pending, stopping && !any_pending);
+        const int32_t* hv = summed.data();
+        std::copy(summed.begin(), summed.end(), ctrl_host_.data_ptr<int32_t>());  // (the stall report's view)
         {
           std::lock_guard<std::mutex> lk(mu_);
           ++cycles_;
@@ -549,7 +484,7 @@ class Engine {
         progressed = false;
         // 3. new signatures: all-gather the announced hashes, append their sorted union
         if (hv[1] > 0) {
-          announce_round(cst);
+          announce_round();
           progressed = true;
         }
         // 4. plan + execute on the data stream
@@ -595,25 +530,47 @@ class Engine {
     fail_all("engine stopped");
   }
 
-  void announce_round(hipStream_t cst) {
-    int32_t* ah = ann_host_.data_ptr<int32_t>();
-    const int64_t mine = world_ * (int64_t)kAnnounce;  // this rank's send block lives past the gather area
-    std::fill(ah, ah + world_ * kAnnounce + kAnnounce, 0);
-    for (int i = 0; i < kAnnounce && i < (int)announce_.size(); ++i) ah[mine + i] = (int32_t)announce_[i];
-    int32_t* ad = ann_dev_.data_ptr<int32_t>();
-    hip_check(hipMemcpyAsync(ad + mine, ah + mine, kAnnounce * 4, hipMemcpyHostToDevice, cst), "H2D announce");
-    std::string err;
-    if (rccl_all_gather_raw(ad + mine, ad, kAnnounce, ncclInt32, ctrl_comm_, cst, &err) != 0)
-      throw std::runtime_error("announce all-gather: " + err);
-    hip_check(hipMemcpyAsync(ah, ad, world_ * kAnnounce * 4, hipMemcpyDeviceToHost, cst), "D2H announce");
-    hip_check(hipEventRecord(ctrl_ev_, cst), "hipEventRecord");
-    wait_ctrl(ctrl_ev_);
-    std::unordered_set<uint32_t> assigned;
-    for (const auto& kv : slot_of_hash_) assigned.insert(kv.first);
-    const auto fresh = engine_new_slot_order(ah, world_, kAnnounce, assigned);
-    if ((int)slots_.size() + (int)fresh.size() > cap_)
-      throw ConsistentError("more than " + std::to_string(cap_) +
-                            " distinct collectives across the ranks (MIHVD_ENGINE_SLOTS)");
+  // The control plane's collectives on the control communicator: staged through small device
+  // buffers on the control stream, which first waits for the data stream's last collective (the
+  // control communicator's kernels never run beside the data communicator's: two communicators
+  // whose kernels overlap in different orders on different ranks can deadlock).
+  struct RcclCtrl final : CtrlTransport {
+    Engine* e = nullptr;
+    bool quiet = false;  // a stopping rank with nothing pending: no stall warning while it waits
+    int world() const override { return e->world_; }
+    void allreduce_sum_i32(int32_t* v, int n) override {
+      hipStream_t cst = e->ctrl_stream_.stream();
+      TORCH_CHECK(n <= e->ctrl_dev_.numel(), "engine: control vector too long");
+      hip_check(hipStreamWaitEvent(cst, e->data_ev_, 0), "hipStreamWaitEvent");
+      hip_check(hipMemcpyAsync(e->ctrl_dev_.data_ptr(), v, (size_t)n * 4, hipMemcpyHostToDevice, cst), "H2D");
+      std::string err;
+      if (rccl_all_reduce_raw(e->ctrl_dev_.data_ptr(), (size_t)n, ncclInt32, ncclSum, e->ctrl_comm_, cst, &err) != 0)
+        throw std::runtime_error("negotiation allreduce: " + err);
+      hip_check(hipMemcpyAsync(v, e->ctrl_dev_.data_ptr(), (size_t)n * 4, hipMemcpyDeviceToHost, cst), "D2H");
+      hip_check(hipEventRecord(e->ctrl_ev_, cst), "hipEventRecord");
+      e->wait_ctrl(e->ctrl_ev_, quiet);
+    }
+    void allgather_i32(const int32_t* mine, int K, int32_t* out) override {
+      hipStream_t cst = e->ctrl_stream_.stream();
+      int32_t* ad = e->ann_dev_.data_ptr<int32_t>();
+      const int64_t at = (int64_t)e->world_ * K;  // this rank's send block lives past the gather area
+      hip_check(hipMemcpyAsync(ad + at, mine, (size_t)K * 4, hipMemcpyHostToDevice, cst), "H2D announce");
+      std::string err;
+      if (rccl_all_gather_raw(ad + at, ad, (size_t)K, ncclInt32, e->ctrl_comm_, cst, &err) != 0)
+        throw std::runtime_error("announce all-gather: " + err);
+      hip_check(hipMemcpyAsync(out, ad, (size_t)at * 4, hipMemcpyDeviceToHost, cst), "D2H announce");
+      hip_check(hipEventRecord(e->ctrl_ev_, cst), "hipEventRecord");
+      e->wait_ctrl(e->ctrl_ev_);
+    }
+  };
+
+  void announce_round() {
+    std::vector<uint32_t> fresh;
+    try {
+      fresh = agree_.announce_round(ctrl_);
+    } catch (const ConsistentControlError& e) {
+      throw ConsistentError(e.what());
+    }
     std::lock_guard<std::mutex> lk(mu_);
     ++announces_;
     for (uint32_t h : fresh) {
@@ -621,13 +578,11 @@ class Engine {
       Slot sl;
       sl.hash = h;
       slots_.push_back(std::move(sl));
-      slot_of_hash_[h] = s;
       auto it = unassigned_.find(h);
       if (it != unassigned_.end()) {
         for (auto& item : it->second) slot_for_local(s, item).pending.push_back(std::move(item.req));
         unassigned_.erase(it);
       }
-      announce_.erase(std::remove(announce_.begin(), announce_.end(), h), announce_.end());
     }
   }
 
@@ -755,11 +710,11 @@ class Engine {
   at::Tensor ctrl_dev_, ctrl_host_, ann_dev_, ann_host_, fusion_;
   hipEvent_t ctrl_ev_ = nullptr;
   hipEvent_t data_ev_ = nullptr;  // the data stream's last collective (the control stream waits for it)
-  // engine-thread state
+  // engine-thread state: the agreed slot table (hashes, announce queue) and each slot's payload
+  SlotAgreement agree_;
+  RcclCtrl ctrl_;
   std::vector<Slot> slots_;
-  std::unordered_map<uint32_t, int> slot_of_hash_;
   std::unordered_map<uint32_t, std::deque<Item>> unassigned_;
-  std::vector<uint32_t> announce_;
   // shared state (mu_)
   std::mutex mu_;
   std::condition_variable cv_done_, cv_work_;

@@ -141,6 +141,26 @@ PYBIND11_MODULE(_mihvd_runtime, m) {
       .def("num_keys", &StoreServer::num_keys)
       .def("stop", &StoreServer::stop, gil_release());
 
+  py::class_<EngineNegotiation>(m, "EngineNegotiation")
+      .def(py::init<const std::string&, int, int, int, const std::string&, int, int>(), py::arg("host"),
+           py::arg("port"), py::arg("rank"), py::arg("world"), py::arg("prefix"), py::arg("cap") = 256,
+           py::arg("announce_k") = 64, gil_release())
+      .def("want", &EngineNegotiation::want)
+      .def("slot", &EngineNegotiation::slot)
+      .def("num_slots", &EngineNegotiation::num_slots)
+      .def("negotiate", &EngineNegotiation::negotiate, py::arg("pending"), py::arg("stop") = false, gil_release())
+      .def("announce_round", &EngineNegotiation::announce_round, gil_release())
+      .def("plan", [](const EngineNegotiation& e, const std::vector<int32_t>& summed, const std::vector<int64_t>& bytes,
+                      const std::vector<int64_t>& key, int64_t threshold) {
+             std::vector<int> partial;
+             auto groups = e.plan(summed, bytes, key, threshold, &partial);
+             return py::make_tuple(groups, partial);
+           })
+      .def_property_readonly("announces", &EngineNegotiation::announces)
+      .def_property_readonly("max_fresh", &EngineNegotiation::max_fresh)
+      .def_property_readonly("rounds", &EngineNegotiation::rounds);
+  m.def("engine_signature_hash", [](const std::string& sig) { return (int64_t)engine_fnv32(sig); });
+
   py::class_<StoreClient>(m, "StoreClient")
       .def(py::init<const std::string&, int, double>(), py::arg("host"), py::arg("port"),
            py::arg("connect_timeout_s") = 60.0, gil_release())

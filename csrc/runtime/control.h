@@ -33,6 +33,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "slot_agreement.h"
+
 namespace mihvd {
 
 // ---------------------------------------------------------------------------------------------
@@ -191,6 +193,56 @@ class Negotiator {
   std::map<std::pair<std::string, int64_t>, Pending> pending_;                // (name, generation)
   std::vector<std::unordered_map<std::string, int64_t>> generation_of_rank_;  // per rank, per name
   std::thread poster_, engine_, coordinator_;
+};
+
+// ---------------------------------------------------------------------------------------------
+// The native engine's control plane over the TCP store (engine.cpp runs it over RCCL)
+// ---------------------------------------------------------------------------------------------
+// CtrlTransport of SlotAgreement over the key-value store: round r of a collective is every rank's
+// value under <prefix>/r<r>/<rank>; a rank reads all of them (parked blocking gets) and deletes its
+// own value of round r - 2 (every rank has read it by then: it finished round r - 1).
+class StoreCtrlTransport final : public CtrlTransport {
+ public:
+  StoreCtrlTransport(const std::string& host, int port, int rank, int world, const std::string& prefix,
+                     double timeout_s = 60.0);
+  int world() const override { return world_; }
+  void allreduce_sum_i32(int32_t* v, int n) override;
+  void allgather_i32(const int32_t* mine, int K, int32_t* out) override;
+  int64_t rounds() const { return round_; }
+  int64_t bytes_posted() const { return bytes_; }
+
+ private:
+  std::vector<std::string> exchange(const std::string& mine);
+  StoreClient client_;
+  int rank_, world_;
+  std::string prefix_;
+  double timeout_s_;
+  int64_t round_ = 0, bytes_ = 0;
+};
+
+// The engine's negotiation (SlotAgreement) driven over StoreCtrlTransport: the CPU-testable form of
+// engine.cpp's cycle (tests/test_distributed_cpu.py::test_engine_slot_agreement_over_store).
+class EngineNegotiation {
+ public:
+  EngineNegotiation(const std::string& host, int port, int rank, int world, const std::string& prefix, int cap,
+                    int announce_k);
+  void want(uint32_t h) { agree_.want(h); }
+  int slot(uint32_t h) const { return agree_.slot(h); }
+  int num_slots() const { return agree_.num_slots(); }
+  std::vector<int32_t> negotiate(const std::vector<int>& pending, bool stop) {
+    return agree_.negotiate(ctrl_, pending, stop);
+  }
+  std::vector<uint32_t> announce_round() { return agree_.announce_round(ctrl_); }
+  // the ready slots of a summed control vector, grouped for fusion (-1 ends a group)
+  std::vector<int64_t> plan(const std::vector<int32_t>& summed, const std::vector<int64_t>& bytes,
+                            const std::vector<int64_t>& key, int64_t threshold, std::vector<int>* partial) const;
+  int64_t announces() const { return agree_.announces(); }
+  int64_t max_fresh() const { return agree_.max_fresh(); }
+  int64_t rounds() const { return ctrl_.rounds(); }
+
+ private:
+  SlotAgreement agree_;
+  StoreCtrlTransport ctrl_;
 };
 
 }  // namespace mihvd

@@ -113,6 +113,23 @@ def test_adasum_vector_halving(tmp_path, np_):
             assert o["bytes"] < S * max(1, (np_ - 1).bit_length()) or np_ == 2
 
 
+@pytest.mark.parametrize("np_", [2, 8])
+def test_engine_slot_agreement_over_store(tmp_path, np_):
+    """The C++ engine's slot agreement (csrc/runtime/slot_agreement.h: the code csrc/kernels/engine.cpp
+    runs over its RCCL control communicator) over the TCP store transport, at 2 and 8 CPU ranks:
+    every rank enqueues the same 120 collectives in its own order -- 80 at once (more than one
+    64-hash announce block: over 64 new slots agreed in one cycle), 40 staggered by rank (slots
+    pending on some ranks only), the first 80 again from the slot cache -- and every rank must see
+    the same ready sequence, each collective exactly once per enqueue, then stop together."""
+    _, outs = run_scenario(tmp_path, "engine_slots", np_=np_, timeout=240)
+    ref = outs[0]
+    assert sorted(ref["ready"]) == sorted(list(range(120)) + list(range(80))), ref
+    for o in outs:
+        assert o["ready"] == ref["ready"], "ranks derived different collective orders"
+        assert o["slots"] == 120 and o["max_fresh"] > 64 and o["announces"] >= 2, o
+        assert o["partial_seen"] > 0, o  # some slots were pending on part of the ranks only
+
+
 def test_broadcast_optimizer_state(tmp_path):
     _, (a, b) = run_scenario(tmp_path, "optimizer_state")
     assert a == b and a["nstate"] > 0 and a["lr"] == pytest.approx(1e-3)

@@ -194,6 +194,74 @@ def sc_adasum_vhdd(outdir):
     out(outdir, "adasum_vhdd", {"rel": rel, "bytes": A.last_bytes_sent, "numel": N, "elem": 4})
 
 
+def sc_engine_slots(outdir):
+    """The native engine's negotiation (csrc/runtime/slot_agreement.h, the code engine.cpp runs over
+    its RCCL control communicator) over the TCP store: three phases of enqueues in rank-dependent
+    orders -- 80 new signatures at once (more than one 64-hash announce block per rank), 40 new ones
+    staggered by rank (slots pending on some ranks only), the first 80 again from the slot cache --
+    then the stop protocol. Records the order in which this rank saw collectives become ready."""
+    import numpy as np
+
+    from mihvd import _native
+
+    rt = _native.runtime()
+    r, n = hvd.rank(), hvd.size()
+    host, port = os.environ["MIHVD_STORE_ADDR"].rsplit(":", 1)
+    neg = rt.EngineNegotiation(host, int(port), r, n, "mihvd/test/engine_slots", 256, 64)
+    rng = np.random.default_rng(100 + r)
+    numel = {i: 1000 + 37 * i for i in range(120)}
+    hsh = {i: rt.engine_signature_hash(f"grad.{i}|6|{numel[i]}|0") for i in range(120)}
+    by_hash = {h: i for i, h in hsh.items()}
+    # the enqueue schedule: cycle -> names this rank enqueues at the start of that cycle
+    sched = {0: list(rng.permutation(80))}
+    late = list(rng.permutation(np.arange(80, 120)))
+    for k in range(4):  # phase B: 10 per cycle, starting later on higher ranks
+        sched.setdefault(2 + r + k, []).extend(late[10 * k:10 * (k + 1)])
+    phase_c = 8 + n  # after every rank's phase B
+    sched.setdefault(phase_c, []).extend(rng.permutation(80))
+    last = max(sched)
+    pending: dict = {}
+    ready_log, partial_seen, cycles = [], 0, 0
+    while True:
+        for i in sched.get(cycles, []):
+            h = hsh[int(i)]
+            pending[h] = pending.get(h, 0) + 1
+            neg.want(h)
+        mine = sorted(neg.slot(h) for h, c in pending.items() if c > 0 and neg.slot(h) >= 0)
+        stop = cycles > last and not any(c > 0 for c in pending.values())
+        summed = neg.negotiate(mine, stop)
+        cycles += 1
+        if summed[0] == n:
+            break
+        if summed[1] > 0:
+            neg.announce_round()
+        nb = neg.num_slots()
+        bytes_ = [4 * numel[by_hash[h]] for h in (neg_slot_hashes(neg, by_hash, hsh, nb))]
+        groups, partial = neg.plan(summed, bytes_, [0] * nb, 1 << 20)
+        partial_seen += len(partial)
+        for s in groups:
+            if s < 0:
+                continue
+            h = neg_slot_hashes(neg, by_hash, hsh, nb)[s]
+            pending[h] -= 1
+            ready_log.append(by_hash[h])
+        if cycles > 400:
+            raise RuntimeError("negotiation did not finish")
+    out(outdir, "engine_slots", {"ready": ready_log, "announces": neg.announces, "max_fresh": neg.max_fresh,
+                                 "partial_seen": partial_seen, "slots": neg.num_slots(), "cycles": cycles,
+                                 "rounds": neg.rounds})
+
+
+def neg_slot_hashes(neg, by_hash, hsh, nb):
+    """slot -> hash for the slots [0, nb) (via the known signatures)."""
+    inv = {}
+    for h in hsh.values():
+        s = neg.slot(h)
+        if 0 <= s < nb:
+            inv[s] = h
+    return [inv[s] for s in range(nb)]
+
+
 def sc_optimizer_state(outdir):
     r = hvd.rank()
     m = _model(seed=r)
