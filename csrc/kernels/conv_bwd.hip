@@ -693,7 +693,7 @@ struct FoldArgs {
 
 // Arrival: every storing wave drains its write-through stores, then one lane counts the block in.
 __device__ __forceinline__ void conv2_fold_arrive(const FoldArgs& fa, ConvBarrier<true>& bar) {
-  if ((fa.on >> 1) == 3) return;
+  (void)fa;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores have landed
   bar.sync();
   if (threadIdx.x == 0)
@@ -709,9 +709,7 @@ __device__ __forceinline__ void conv2_fold_reduce(const FoldArgs& fa, ConvBarrie
   gu32* depart = arrive + 1;
   gu32* err = arrive + 2;
   const int t = threadIdx.x, wave = t >> 6;
-  const int dbg = fa.on >> 1;  // profiling (MIHVD_FOLD_DEBUG): 1 no items, 2 no wait, 3 stores only
-  if (dbg == 3) return;
-  if (wave == 0 && dbg != 2) {
+  if (wave == 0) {
     // every conv block is resident (grid <= CUs, checked at launch); bounded: ~0.1 s, then an error
     int spin = 0;
     while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)n_conv) {
@@ -736,7 +734,6 @@ __device__ __forceinline__ void conv2_fold_reduce(const FoldArgs& fa, ConvBarrie
   const AdamCoef c = adam_coef((float)ra.ad.state[ST_OPT], ra.ad.lr, ra.ad.b1, ra.ad.b2, ra.ad.eps, ra.ad.gscale,
                                ra.ad.rule);
   if (bx == 0 && t == 0) const_cast<int64_t*>(ra.ad.state)[ST_FWD] += 1;  // every conv block has read it
-  if (dbg == 1) return;
   const int half = t >> 8, th = t & 255;
   float4* r4 = reinterpret_cast<float4*>(smem) + half * 256;
   const ReduceLoads<true> ld(slab, fa.nslab, cpart);
@@ -869,13 +866,10 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
   const CollRole cr = xgmi_role_lookup(coll);
   if (w3t != nullptr) {
     // one 512-thread block per CU (144 KB of LDS): the tail-only blocks take the CUs the conv roles
-    // leave free and start on the dW3 tiles at once (MIHVD_W3T_HEAD: their share, tuned on MI355X)
+    // leave free and start on the dW3 tiles at once (their share of the tiles tuned on MI355X)
     const int ncu = device_cu_count();
     const int grid = std::max(n_conv + 8, ncu);
-    static const double head_frac = [] {
-      const char* e = getenv("MIHVD_W3T_HEAD");
-      return e ? atof(e) : 0.25;
-    }();
+    constexpr double head_frac = 0.25;
     W3TileTail wtl = *w3t;
     wtl.first_free = n_conv;
     wtl.head = (int)(head_frac * W3T_TILES);
@@ -896,18 +890,12 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     // the first cycle on every CU (the conv roles are latency-bound and leave HBM idle)
     const int ncu = device_cu_count();
     const int grid = std::max(n_conv + 8, ncu);
-    // MIHVD_TAIL_STREAMERS: streamer waves per compute block (0 .. 4; 768 threads at most)
-    static const int sw = [] {
-      const char* e = getenv("MIHVD_TAIL_STREAMERS");
-      return e ? std::max(0, std::min(4, atoi(e))) : 4;
-    }();
+    // four streamer waves per compute block (768 threads)
+    constexpr int sw = 4;
     const int nthr = debug_phase_exit() ? 512 : 512 + 64 * sw;  // profiling cuts: conv waves alone
-    // The free waves' head range (MIHVD_TAIL_HEAD: its fraction of the update), tuned on MI355X:
-    // with streamers they carry most of the update while the conv roles run.
-    static const double head_frac = [] {
-      const char* e = getenv("MIHVD_TAIL_HEAD");
-      return e ? atof(e) : (sw > 0 ? 0.8 : 0.2);
-    }();
+    // The free waves' head range (their fraction of the update), tuned on MI355X: with streamers
+    // they carry most of the update while the conv roles run.
+    constexpr double head_frac = 0.8;
     AdamTail at = *tail;
     at.first_free = n_conv;
     at.head = (int64_t)(head_frac * (double)((at.n4 + 63) / 64));
@@ -917,11 +905,6 @@ static void conv2_bwd_launch(const at::Tensor& g2, const at::Tensor& idx2, const
     FoldArgs fa = fold ? *fold : FoldArgs{};
     fa.on = fold != nullptr && nthr > 512 && role == -1 && n_conv <= grid && grid <= ncu;
     if (fold) *fold_done = fa.on != 0;
-    static const int fold_dbg = [] {
-      const char* e = getenv("MIHVD_FOLD_DEBUG");
-      return e ? atoi(e) : 0;
-    }();
-    if (fa.on) fa.on |= fold_dbg << 1;
     conv2_bwd_kernel<TAIL_ADAM><<<grid, nthr, nthr > 512 ? CB_LDS_SW : CB_LDS, stream>>>(
         (const u16*)g2.data_ptr(), idx2.data_ptr<uint8_t>(), (const u16*)a1.data_ptr(), (const u16*)w2bf.data_ptr(),
         x.data_ptr<float>(), rp, n_pool, sp, idx1.data_ptr<uint8_t>(), g1p, slab.data_ptr<float>(),

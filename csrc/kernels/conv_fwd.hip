@@ -398,12 +398,8 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
     return true;
   }();
   (void)attr;
-  // waves per block (MIHVD_CONV12_WAVES, 4 or 8): one block per CU either way (LDS), more waves
-  // hide more of the gather/MFMA latency chains
-  static const int nw = [] {
-    const char* e = getenv("MIHVD_CONV12_WAVES");
-    return (e && atoi(e) == 4) ? 4 : 8;
-  }();
+  // 8 waves per block (one block per CU either way, LDS): more waves hide more of the gather/MFMA
+  // latency chains than 4
   auto stream = c10::hip::getCurrentHIPStream().stream();
   CollRole cr = xgmi_role_lookup(coll);
   TORCH_CHECK(cr.nblk % 2 == 0, "conv12_fwd: a co-launched collective needs an even number of blocks");
@@ -413,8 +409,7 @@ void conv12_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, cons
         (const u16*)w2bf.data_ptr(), b2.data_ptr<float>(), (u16*)a1.data_ptr(), idx1.data_ptr<uint8_t>(),
         (u16*)a2.data_ptr(), idx2.data_ptr<uint8_t>(), B, cr);
   };
-  if (nw == 4) launch(conv12_fwd_kernel<4>, 256);
-  else launch(conv12_fwd_kernel<8>, 512);
+  launch(conv12_fwd_kernel<8>, 512);
 }
 
 MIHVD_OPNS_END

@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
     float* __restrict__ db2p, float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4,
-    float* __restrict__ gb4, int B, F32Adam ad, int pf) {
+    float* __restrict__ gb4, int B, F32Adam ad) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   if (bid >= F1R_BLOCKS) {
@@ -189,14 +189,15 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * bid, nb = 128 * wave;
   f1r_stamp(0);
-  // pf (default): the routing epilogue's a2 / idx2 operands (they depend on the block alone) loaded
-  // at the start, so the epilogue after the exchange does not begin with a dependent global round trip
+  // the routing epilogue's a2 / idx2 operands (they depend on the block alone) are loaded at the
+  // start, so the epilogue after the exchange does not begin with a dependent global round trip
+  // (r05h: 27.98 -> 27.03 us)
   const int jt = bid >> 2, co_e = 16 * (bid & 3) + 4 * (lane >> 4), j_e = 64 * jt + co_e;
   const int m_e = 16 * (t >> 6) + (lane & 15), mc_e = min(m_e, B - 1);
   float4 av_e = make_float4(0.f, 0.f, 0.f, 0.f);
   uint32_t ix_e = 0u;
   auto load_route = [&]() {
-    if (pf && t < G * 64) {
+    if (t < G * 64) {
       av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
       ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
     }
@@ -323,10 +324,6 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
   const int py = jt / 7, px = jt - 7 * py;
   if (t < G * 64) {  // wave u handles tile u
     const int u = t >> 6, ln = lane, r = ln & 15;
-    if (!pf) {
-      av_e = *reinterpret_cast<const float4*>(a2 + (int64_t)mc_e * 3136 + j_e);
-      ix_e = *reinterpret_cast<const uint32_t*>(idx2 + (int64_t)mc_e * 3136 + j_e);
-    }
     float4 s = red[(0 * 8 + u) * 64 + ln];
 #pragma unroll
     for (int w = 1; w < 8; ++w) s = f4add(s, red[(w * 8 + u) * 64 + ln]);
@@ -378,7 +375,7 @@ constexpr int cbf_img(int npass) { return cbf_maxr(npass) * CBF_RS; }
 // row offsets on one bank (2-way ds_read_b32 conflicts, PMC ~5e5 cycles per launch); 34 separates them
 constexpr int CBF_XS = 34, CBF_XIMG = 32 * CBF_XS;
 constexpr int CBF_XIM = 2 * CBF_XIMG;                 // two padded x images
-constexpr int CBF_PW = 8 * 2 * 64 * 4;                // per-wave conv1 partials (MEPI: 2 f32x4 per lane)
+constexpr int CBF_PW = 8 * 2 * 64 * 4;                // per-wave conv1 partials (8 waves x 26 x 16 used)
 // The x images and the conv1 partials live in the dead image area behind the co-quarter partial
 // exchange (written after the tap loops' barrier): the image alone sets the dgrad LDS size.
 constexpr int cbf_red(int tpb) { return 4 * 2 * tpb * 64 * 4; }           // floats of the exchange
@@ -416,16 +413,17 @@ __device__ __forceinline__ void lds_barrier() {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// PREW: the W2 register operand is loaded BEFORE the staging barrier (after the staging loads, so the
+// The W2 register operand is loaded BEFORE the staging barrier (after the staging loads, so the
 // staging writes wait only for their own loads), and the barrier orders LDS alone: the 25 W2 loads
-// per lane (200 KB per block from L2) land while the dY2 image is staged instead of after it.
-// MEPI: the conv1 weight gradient of the epilogue on MFMA instead of VALU (see step 3 below).
+// per lane (200 KB per block from L2) land while the dY2 image is staged instead of after it. (The
+// conv1 weight gradient of the epilogue on MFMA instead of VALU measured slower every time it was
+// tried: dgrad role 42.3 -> 45.7 us, profiles/r05/conv2_bwd_mfma_epilogue_r05y.txt; removed.)
 // NPASS = 2 (the one-round form): TPB tiles in two tap-loop passes of TPB / 2 over the same
 // register-resident W2 (the A register sets are reused, the accumulators of both passes live on),
 // so a block loads W2 once for twice the tiles and the halo rows are staged once for both.
 // FRAG: W2 from the fragment copy (f32_w2_frag_block in f32_fwd.hip): one contiguous 1 KB per wave
 // and tap instead of 16 scattered 64-byte row pieces.
-template <int TPB, bool PREW, bool MEPI, int NPASS = 1, bool FRAG = false>
+template <int TPB, int NPASS = 1, bool FRAG = false>
 __device__ __forceinline__ void f32_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
@@ -471,18 +469,16 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
       *reinterpret_cast<float4*>(dimg + (rr * CBF_RWD + (rem >> 4)) * CBF_PS + (rem & 15) * 4) = iv[it];
     }
   }
-  // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3].
-  // PREW: issued right behind the staging writes (which wait only for the staging loads), so they
-  // are in flight across the barrier
+  // this wave's whole B operand in registers: wb[tap] = W2[tap][16 nt + lr][16 cq + 4 lg .. + 3],
+  // issued right behind the staging writes (which wait only for the staging loads), so they are in
+  // flight across the barrier
   const float* wq = w2 + (16 * nt + lr) * 64 + 16 * cq + 4 * lg;
   const float4* wfq = reinterpret_cast<const float4*>(w2f) + wave * 25 * 64 + lane;
   float4 wb[25];
-  if constexpr (PREW) {
-    __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int tap = 0; tap < 25; ++tap) wb[tap] = FRAG ? wfq[tap * 64] : *reinterpret_cast<const float4*>(wq + tap * 2048);
-    __builtin_amdgcn_sched_barrier(0);
-  }
+  for (int tap = 0; tap < 25; ++tap) wb[tap] = FRAG ? wfq[tap * 64] : *reinterpret_cast<const float4*>(wq + tap * 2048);
+  __builtin_amdgcn_sched_barrier(0);
   int abase[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) {
@@ -493,25 +489,11 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   f32x4 acc[TPB];
 #pragma unroll
   for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (PREW) {
-    lds_barrier();  // the dY2 image is complete; the W2 loads stay in flight
-  } else {
-    __syncthreads();  // the dY2 image is complete; no barrier in the tap loop
-  }
+  lds_barrier();  // the dY2 image is complete; the W2 loads stay in flight
   c2b_stamp(1);
-  if constexpr (!PREW) {
-    // Issued after the barrier (whose vmcnt(0) would otherwise wait for all 25 loads): the tap loop
-    // consumes them in issue order, so tap t waits only for its own.
-#pragma unroll
-    for (int tap = 0; tap < 25; ++tap) wb[tap] = FRAG ? wfq[tap * 64] : *reinterpret_cast<const float4*>(wq + tap * 2048);
-  }
-  // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched.
-  // VALU form: (nt, tile) pairs p = wave + 8k, lane pixel 4 lg + r. MEPI form: the wave's pixel
-  // groups 4 cq + r of every tile, the same pixel on the four lane groups (channel 16 nt + lr).
-  // LATE (MEPI in the two-pass form): loaded after the tap loops instead (TPB x 4 x 2 registers
-  // would not fit beside the W2 operand); one exposed latency, then the short MFMA epilogue.
-  constexpr int NP = MEPI ? TPB : (2 * TPB + 7) / 8;
-  constexpr bool LATE = MEPI && NPASS == 2;
+  // the epilogue's conv1 operands (ReLU sign and pool argmax of this lane's a1 elements), prefetched:
+  // (nt, tile) pairs p = wave + 8k, lane pixel 4 lg + r
+  constexpr int NP = (2 * TPB + 7) / 8;
   float ea[NP][4];
   int ex[NP][4];
   auto load_epi = [&]() {
@@ -520,37 +502,14 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int pp = wave + 8 * k;
-        const int P = MEPI ? 16 * (T0 + k) + 4 * cq + r : 16 * (T0 + (pp >> 1)) + 4 * lg + r;
-        const bool ok = (MEPI || pp < 2 * TPB) && P < np;
+        const int P = 16 * (T0 + (pp >> 1)) + 4 * lg + r;
+        const bool ok = pp < 2 * TPB && P < np;
         const int64_t o = (int64_t)min(P, np - 1) * 32 + 16 * nt + lr;
         ea[k][r] = mask_f(a1[o], ok);
         ex[k][r] = idx1[o];
       }
   };
-  if constexpr (!LATE) load_epi();
-  // LATE: one a1 and one idx1 load per tile and lane (lane group lg loads pixel 4 cq + lg of the
-  // tile, the one its row of the MFMA A operand is for), packed into a 4-bit code (ReLU bit | argmax)
-  // and exchanged across the four lane groups (two xor-shuffles), instead of 8 loads per tile.
-  int codes[LATE ? TPB : 1];
-  auto load_codes = [&]() {
-    float av[TPB];
-    int iv[TPB];
-#pragma unroll
-    for (int k = 0; k < TPB; ++k) {
-      const int P = min(16 * (T0 + k) + 4 * cq + lg, np - 1);
-      const int64_t o = (int64_t)P * 32 + 16 * nt + lr;
-      av[k] = a1[o];
-      iv[k] = idx1[o];
-    }
-#pragma unroll
-    for (int k = 0; k < TPB; ++k) {
-      const bool ok = 16 * (T0 + k) + 4 * cq + lg < np && av[k] > 0.f;
-      int c = ok ? (4 | iv[k]) << (4 * lg) : 0;
-      c |= __shfl_xor(c, 16, 64);
-      c |= __shfl_xor(c, 32, 64);
-      codes[k] = c;  // bits [4 r, 4 r + 3): pixel 4 cq + r's (relu << 2 | argmax)
-    }
-  };
+  load_epi();
   // the x patches are needed only by the epilogue: loaded here, they land during the tap loop. The
   // rows of the block's (at most two) images were looked up at block start with block-uniform
   // (scalar) loads, so no vector wait on that dependent chain drains the W2 / epilogue loads
@@ -613,82 +572,9 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
   }
   // 2. sum the four co-quarter partials (the dY2 image is dead now)
   f32x4* red = reinterpret_cast<f32x4*>(dimg);  // [cq][nt][TPB][64]
-  if constexpr (LATE) load_codes();  // in flight while the partials are exchanged
 #pragma unroll
   for (int i = 0; i < TPB; ++i) red[((cq * 2 + nt) * TPB + i) * 64 + lane] = acc[i];
   __syncthreads();
-  if constexpr (MEPI) {
-    // 3'. the conv1 weight gradient as a small GEMM on MFMA: D[ci][tap] += sum_k A[ci][k] B[k][tap]
-    //     over the full-resolution pixels k of the pooled pixels this wave owns (pixel groups 4 cq + r
-    //     of every tile; k-step = one pooled pixel, its four 2x2 positions d = lg): A = the routed
-    //     gradient (g1 at the argmax position, 0 elsewhere), B = the x value under tap n of position d
-    //     (n = 25: 1, so that column is db1). Per pooled pixel 2 LDS reads + 2 MFMAs per lane, against
-    //     25 LDS reads + 26 FMAs per element (and the lane-group shuffles) of the VALU form.
-    int off0, off1;
-    {
-      const int n1 = 16 + lr;
-      off0 = (lr / 5) * CBF_XS + lr % 5;
-      off1 = n1 < 25 ? (n1 / 5) * CBF_XS + n1 % 5 : 0;
-    }
-    const float one1 = lr == 9 ? 1.f : 0.f;  // column 25 = db1
-    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-    // Software pipeline over the tiles: tile k + 1's eight x operands (four pixels x two taps) and
-    // its routed-gradient A values are read / formed before tile k's eight MFMAs issue (a serial
-    // read -> MFMA chain per pixel left the LDS latency exposed 4 TPB times per wave).
-    const int li = lr + 16 * cq;
-    float xa[2][4], xb[2][4], av[2][4];
-    auto prep = [&](int k, float (&x0)[4], float (&x1)[4], float (&a)[4]) {
-      // the four co-quarter partials of this pixel group (lane lr + 16 cq of the reduction layout)
-      const f32x4 sk = ((red[((0 * 2 + nt) * TPB + k) * 64 + li] + red[((1 * 2 + nt) * TPB + k) * 64 + li]) +
-                        red[((2 * 2 + nt) * TPB + k) * 64 + li]) +
-                       red[((3 * 2 + nt) * TPB + k) * 64 + li];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int P0r = 16 * (T0 + k) + 4 * cq + r, P = min(P0r, np - 1);  // wave-uniform
-        const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
-        if constexpr (LATE) {
-          const int c = (codes[k] >> (4 * r)) & 7;  // 0 past the batch or where ReLU cut the pixel
-          a[r] = (c == (4 | lg)) ? sk[r] : 0.f;
-        } else {
-          const float g = ea[k][r] > 0.f ? sk[r] : 0.f;
-          a[r] = (P0r < np && ex[k][r] == lg) ? g : 0.f;
-        }
-        const float* xs = xim + (bb - b0) * CBF_XIMG + (2 * py + (lg >> 1)) * CBF_XS + 2 * px + (lg & 1);
-        x0[r] = xs[off0];
-        const float xo = xs[off1];  // off1 = 0 past tap 24: an in-bounds read, replaced below
-        x1[r] = 16 + lr < 25 ? xo : one1;
-      }
-    };
-    prep(0, xa[0], xb[0], av[0]);
-#pragma unroll
-    for (int k = 0; k < TPB; ++k) {
-      const int cur = k & 1;
-      if (k + 1 < TPB) prep(k + 1, xa[cur ^ 1], xb[cur ^ 1], av[cur ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        c0 = mfma4(av[cur][r], xa[cur][r], c0);
-        c1 = mfma4(av[cur][r], xb[cur][r], c1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // C[row = 4 lg + i][col = lr] = D[ci = 16 nt + 4 lg + i][tap = lr (c0) or 16 + lr (c1)]; the four
-    // waves of a channel half sum through LDS (the dY2 image area is still being read: use pw)
-    f32x4* pw4 = reinterpret_cast<f32x4*>(pw);
-    pw4[(wave * 2 + 0) * 64 + lane] = c0;
-    pw4[(wave * 2 + 1) * 64 + lane] = c1;
-    __syncthreads();
-    for (int q = t; q < CP_F32; q += 512) {
-      const int e = q >> 5, c = q & 31, h = c >> 4, l = c & 15;  // tap e (25 = db1), channel c
-      const int tile = e >> 4, col = (e & 15), ln = 16 * (l >> 2) + col, i = l & 3;
-      const float* pf = pw;
-      const float v = (pf[(((h + 0) * 2 + tile) * 64 + ln) * 4 + i] + pf[(((h + 2) * 2 + tile) * 64 + ln) * 4 + i]) +
-                      (pf[(((h + 4) * 2 + tile) * 64 + ln) * 4 + i] + pf[(((h + 6) * 2 + tile) * 64 + ln) * 4 + i]);
-      cpart[(int64_t)bid * CP_F32 + q] = v;  // q = tap * 32 + ci (dW1, HWIO) or 800 + ci (db1)
-    }
-    c2b_stamp(3);
-    return;
-  }
   // 3. epilogue: (nt, tile) pairs p = wave, wave + 8, ...: mask -> g1, the conv1 weight gradient of
   //    the routed g1 (one 5x5 patch of x per pooled element), db1
   float s25[26];
@@ -751,20 +637,19 @@ __device__ __forceinline__ void f32_conv2_dgrad_block(
 // (xcd_contiguous: f32_common.h)
 __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
-                                                      int ig, int wmid, float* smf,
+                                                      int ig, float* smf,
                                                       const float* __restrict__ zeros) {
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), l32 = lane & 31, hh = lane >> 5;
   const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
   const int img0 = ig * grp, nimg = min(ig, B - img0);
-  // wmid bits 0-1: where the next image's LDS stores go (see the K-step loop); bit 2 ("late"): its
-  // global loads are issued after step 0's MFMAs instead of before the first operand reads
-  const int wm = wmid & 3;
-  const bool late = (wmid & 4) != 0;
-  // wm 3 (LDS-DMA): the next image goes global -> LDS by global_load_lds_dwordx4 issued at the image
-  // start (the staging image is lane-linear per wave: chunk t + 512 it at 16 (t + 512 it) bytes), so
-  // no register staging and no store sits between the MFMAs; padding chunks read a zero line.
-  // The image-end barrier (__syncthreads: vmcnt(0)) retires them before the buffer is read.
-  const bool dma = wm == 3 && zeros != nullptr;
+  // The next image goes global -> LDS by global_load_lds_dwordx4 issued at the image start (the
+  // staging image is lane-linear per wave: chunk t + 512 it at 16 (t + 512 it) bytes), so no register
+  // staging and no store sits between the MFMAs; padding chunks read a zero line. The image-end
+  // barrier (__syncthreads: vmcnt(0)) retires them before the buffer is read. Without the zero line
+  // (`zeros` null) the register-staged form: its LDS stores one chunk per K step over steps 4..10.
+  // (r05j: the role 38.96 -> 38.44 us, the step 117.73 -> 116.89 us; the other store placements
+  // measured slower and were removed)
+  const bool dma = zeros != nullptr;
   // this thread's seven chunk offsets within an image, computed once (per image only the image
   // term is added): chunk i < 2016 is an a1 chunk of the padded rows kh..kh+13, the rest dY2 chunks
   int loff[7];
@@ -827,7 +712,7 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
     const float* buf = smf + (n & 1) * CBF_WBUF;
     if (dma) {
       if (n + 1 < nimg) dma_img(img0 + n + 1, smf + ((n + 1) & 1) * CBF_WBUF);
-    } else if (n + 1 < nimg && !late) {
+    } else if (n + 1 < nimg) {
       load_img(img0 + n + 1, v);
     }
     const float* A1s = buf;
@@ -844,10 +729,10 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
 #pragma unroll
       for (int kw = 0; kw < 5; ++kw) b[kw] = bp[kw * 32];
     };
-    // wmid: the next image's LDS stores are issued halfway through this image's steps (the other
-    // buffer is free since the last barrier) instead of after them, so the store pass overlaps
-    // MFMAs and each image ends with the barrier alone
-    const bool nxt = n + 1 < nimg;
+    // register-staged form: the next image's LDS stores are spread over this image's steps (the other
+    // buffer is free since the last barrier), so the store pass overlaps MFMAs and each image ends
+    // with the barrier alone
+    const bool nxt = n + 1 < nimg && !dma;
     load_step(0, opa[0], opb[0]);
 #pragma unroll
     for (int u = 0; u < 13; ++u) {
@@ -859,16 +744,13 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
         for (int kw = 0; kw < 5; ++kw) acc[kw] = mfma32(opa[cur], opb[cur][kw], acc[kw]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (u == 0 && late && nxt && !dma) load_img(img0 + n + 1, v);
-      if (u == 6 && wm == 1 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
-      // wm 2: one chunk per step over u = 4..10, so each store waits only for its own load (the
-      // loads return in issue order; vmcnt counts down) instead of all seven at u = 6
-      if (u >= 4 && u < 11 && wm == 2 && nxt) {
+      // one chunk per step over u = 4..10, so each store waits only for its own load (the loads
+      // return in issue order; vmcnt counts down) instead of all seven at once
+      if (u >= 4 && u < 11 && nxt) {
         const int it = u - 4;
         *reinterpret_cast<float4*>(smf + ((n + 1) & 1) * CBF_WBUF + 4 * (t + 512 * it)) = v[it];
       }
     }
-    if (wm == 0 && nxt) store_img(smf + ((n + 1) & 1) * CBF_WBUF, v);
     __syncthreads();
     if (n < 8) c2b_stamp(8 + n);  // (study build: wgrad blocks use the per-wave slots for per-image ends)
   }
@@ -918,23 +800,21 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   c2b_stamp(6);
 }
 
-template <int TPB, bool PREW, bool MEPI, int NPASS = 1, bool FRAG = false>
+template <int TPB, int NPASS = 1, bool FRAG = false>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg, int ig, int wmid, const float* __restrict__ w2f, const float* __restrict__ zeros) {
+    int n_wg, int ig, const float* __restrict__ w2f, const float* __restrict__ zeros) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   c2b_stamp(0);
   if (bid < n_dg) {
-    f32_conv2_dgrad_block<TPB, PREW, MEPI, NPASS, FRAG>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf,
-                                                        w2f);
+    f32_conv2_dgrad_block<TPB, NPASS, FRAG>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf, w2f);
     return;
   }
-  // n_wg > 0: XCD-contiguous order of the wgrad blocks (MIHVD_F32_C2B_XCD=0: launch order)
-  f32_conv2_wgrad_block(n_wg > 0 ? xcd_contiguous(bid, n_dg, n_dg + n_wg) : bid - n_dg, dY2, a1, slab, B, ig, wmid,
-                        smf, zeros);
+  // XCD-contiguous order of the wgrad blocks
+  f32_conv2_wgrad_block(xcd_contiguous(bid, n_dg, n_dg + n_wg), dY2, a1, slab, B, ig, smf, zeros);
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -1154,13 +1034,11 @@ static int conv2b_tpb(int B) {
   const int nt = (196 * B + 15) / 16;
   return std::min(7, std::max(1, (nt + 255) / 256));
 }
-// One-round form (MIHVD_F32_C2B_R1, default on where it applies): dgrad blocks of twice the tiles
+// One-round form (wherever it applies): dgrad blocks of twice the tiles
 // in two tap-loop passes and wgrad blocks of twice the images, so both roles fit the CUs in one
 // round (B = 100: 123 + 130 = 253 blocks) instead of two (245 + 250): W2 is loaded once per two
 // passes, the halo rows are staged once for twice the pixels, and no block starts behind another.
-static bool conv2b_one_round(int B) {
-  return env_knob("MIHVD_F32_C2B_R1", 1) != 0 && 2 * conv2b_tpb(B) <= 10;
-}
+static bool conv2b_one_round(int B) { return 2 * conv2b_tpb(B) <= 10; }
 static int conv2b_block_tiles(int B) { return conv2b_one_round(B) ? 2 * conv2b_tpb(B) : conv2b_tpb(B); }
 static int conv2b_images(int B) { return conv2b_one_round(B) ? CBF_IG2 : CBF_IG; }
 int64_t f32_wgrad_groups(int64_t B) {
@@ -1231,8 +1109,7 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
     kern<<<F1R_BLOCKS + F1B_SMALL, 512, F1R_LDS, stream>>>(
         dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
         dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
-        gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad,
-        env_knob("MIHVD_F32_F1R_PF", 1));  // 0: routing operands loaded in the epilogue (r05h: 27.98 vs 27.03 us)
+        gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad);
   };
   if (dgrad_only) {
     switch (G) {
@@ -1247,9 +1124,9 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
     }
     return;
   }
-  // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; MIHVD_F32_F1R_KW=0
-  // keeps the padded 28, bitwise equal: the padded steps add exact zeros)
-  if (G == 7 && (B + 3) / 4 == 25 && env_knob("MIHVD_F32_F1R_KW", 1) != 0) {
+  // exact wgrad K steps for the headline batch (B = 97..100: 25 instead of 28; bitwise equal to the
+  // padded 28, whose extra steps add exact zeros)
+  if (G == 7 && (B + 3) / 4 == 25) {
     if (adam && !store_w3) launch(f32_fc1_bwd_rows_kernel<7, true, false, 25>);
     else if (adam) launch(f32_fc1_bwd_rows_kernel<7, true, true, 25>);
     else launch(f32_fc1_bwd_rows_kernel<7, false, true, 25>);
@@ -1313,40 +1190,22 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
     TORCH_CHECK(r1 - r0 <= maxr && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS image");
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  // study knob: MIHVD_F32_C2B_ROLE = 1 dgrad blocks only, 2 wgrad blocks only (the other role's
-  // outputs are then stale)
-  const int role = env_knob("MIHVD_F32_C2B_ROLE", 0);
   const int lds = r1 ? CBF_LDS2 : CBF_LDS;
-  const int grid = role == 1 ? n_dg : role == 2 ? 10 * ngrp : n_dg + 10 * ngrp;
-  const int ndg_arg = role == 2 ? 0 : n_dg;
-  const int nwg_arg = env_knob("MIHVD_F32_C2B_XCD", 1) != 0 ? 10 * ngrp : 0;
-  // 0: next image stored after the steps, 1: at step 6, 2: one chunk per step over steps 4..10
-  // (wgrad role alone 39.2 vs 40.1 us for 1, profiles/r04/kbench_f32_r04ag.txt; bitwise equal);
-  // + 4: the next image's global loads issued after step 0's MFMAs
-  // default 3 (r05j: whole step 117.73 -> 116.89 us, the wgrad role alone 38.96 -> 38.44 us)
-  int wmid = (int)env_knob("MIHVD_F32_C2B_WMID", 3);
-  // 3: the next image by LDS-DMA (global_load_lds) with padding chunks read from a zero line
-  const float* zl = (wmid & 3) == 3 ? f32_zero_line(stream) : nullptr;
-  if ((wmid & 3) == 3 && zl == nullptr) wmid = 2;
+  const int grid = n_dg + 10 * ngrp;
+  // the wgrad role's next image by LDS-DMA (padding chunks from a zero line); without the zero line
+  // the register-staged form
+  const float* zl = f32_zero_line(stream);
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<grid, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
                                      idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
-                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg_arg, nwg_arg, ig,
-                                     wmid, w2f, zl);
+                                     cpart.data_ptr<float>(), slab.data_ptr<float>(), B, n_dg, 10 * ngrp, ig, w2f, zl);
   };
-  // MIHVD_F32_C2B_PREW=0: the W2 operand loaded after a full barrier (the earlier form);
-  // MIHVD_F32_C2B_MEPI=1: the conv1 weight gradient of the dgrad epilogue on MFMA
-  const bool prew = env_knob("MIHVD_F32_C2B_PREW", 1) != 0;
-  // (MFMA form measured slower: 52.5 vs 51.1 us, dgrad role 28.9 vs 27.8 us, profiles/r04/kbench_f32_r04d.txt)
-  const bool mepi = env_knob("MIHVD_F32_C2B_MEPI", 0) != 0;
-  if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes (PREW; epilogue per MIHVD_F32_C2B_MEPI)
-#define C2B_R1(T)                                                                                        \
-  case T:                                                                                                \
-    if (mepi && w2f) launch(f32_conv2_bwd_kernel<T, true, true, 2, true>);                                \
-    else if (mepi) launch(f32_conv2_bwd_kernel<T, true, true, 2>);                                        \
-    else if (w2f) launch(f32_conv2_bwd_kernel<T, true, false, 2, true>);                                  \
-    else launch(f32_conv2_bwd_kernel<T, true, false, 2>);                                                 \
+  if (r1) {  // one-round form: 2, 4, ..., 10 tiles in two passes
+#define C2B_R1(T)                                                       \
+  case T:                                                               \
+    if (w2f) launch(f32_conv2_bwd_kernel<T, 2, true>);                  \
+    else launch(f32_conv2_bwd_kernel<T, 2>);                            \
     break;
     switch (tpb) {
       C2B_R1(2)
@@ -1359,10 +1218,9 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
 #undef C2B_R1
     return;
   }
-#define C2B_CASE(T)                                                                          \
-  case T:                                                                                    \
-    if (mepi) launch(f32_conv2_bwd_kernel<T, true, true>);                                   \
-    else prew ? launch(f32_conv2_bwd_kernel<T, true, false>) : launch(f32_conv2_bwd_kernel<T, false, false>); \
+#define C2B_CASE(T)                               \
+  case T:                                         \
+    launch(f32_conv2_bwd_kernel<T>);              \
     break;
   switch (tpb) {
     C2B_CASE(1)

@@ -432,109 +432,14 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------------------------------------ //
-// head: one block per sample b, 256 threads x 4 features (K9-K11 of SURVEY.md §2.5):
+// head: one block per sample b (K9-K11 of SURVEY.md §2.5):
 //   z = sum of the 14 slabs + b3; h = dropout(relu(z)); logits = h W4 + b4; softmax-xent;
 //   dlogits = (softmax - onehot) / B; dz = (dlogits W4^T) * relu'(z) * dropout mask
 // ------------------------------------------------------------------------------------------ //
-__global__ void __launch_bounds__(256) f32_head_kernel(
-    const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
-    const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
-    int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
-    float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B,
-    float* __restrict__ stats_acc) {
-  __shared__ float red[4][10];
-  __shared__ float dl[10];
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int64_t step = state ? state[ST_FWD] : 0;
-  const int n0 = t * 4;
-  float4 parts[F1F_KS];
-#pragma unroll
-  for (int s = 0; s < F1F_KS; ++s)
-    parts[s] = *reinterpret_cast<const float4*>(zpart + ((int64_t)s * B + b) * 1024 + n0);
-  float w4r[4][10];  // this thread's 4 rows of W4 = 40 contiguous floats
-  {
-    float4 wv[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) wv[k] = reinterpret_cast<const float4*>(w4 + n0 * 10)[k];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const float e[4] = {wv[k].x, wv[k].y, wv[k].z, wv[k].w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) w4r[(4 * k + u) / 10][(4 * k + u) % 10] = e[u];
-    }
-  }
-  const float4 bb = *reinterpret_cast<const float4*>(b3 + n0);
-  int y = 0;
-  if (t < 64) {
-    int row = b;
-    if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-    y = (int)labels[row];
-  }
-  float z[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-  for (int s = 0; s < F1F_KS; ++s) {
-    z[0] += parts[s].x;
-    z[1] += parts[s].y;
-    z[2] += parts[s].z;
-    z[3] += parts[s].w;
-  }
-  float h[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bool keep = thresh24 == 0 || dropout_keep(seed, (uint32_t)step, (uint32_t)(b * 1024 + n0 + i), thresh24);
-    h[i] = keep ? fmaxf(z[i], 0.f) * keep_scale : 0.f;
-  }
-  *reinterpret_cast<float4*>(h_out + (int64_t)b * 1024 + n0) = make_float4(h[0], h[1], h[2], h[3]);
-  float part[10];
-#pragma unroll
-  for (int c = 0; c < 10; ++c) part[c] = h[0] * w4r[0][c] + h[1] * w4r[1][c] + h[2] * w4r[2][c] + h[3] * w4r[3][c];
-#pragma unroll
-  for (int c = 0; c < 10; ++c) {
-    const float s = wave_sum(part[c]);
-    if (lane == 0) red[wave][c] = s;
-  }
-  __syncthreads();
-  if (t < 64) {
-    const int c = min(lane, 9);
-    const float lgt = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]) + b4[c];
-    const float v = lane < 10 ? lgt : -INFINITY;
-    const float mx = wave_max(v);
-    const float e = lane < 10 ? expf(lgt - mx) : 0.f;
-    const float se = wave_sum(e);
-    const float lse = mx + logf(se);
-    const unsigned long long ismax = __ballot(lane < 10 && lgt == mx);
-    const int am = __ffsll((long long)ismax) - 1;
-    const float ly = __shfl(lgt, y, 64);
-    if (lane < 10) {
-      const float d = (expf(lgt - lse) - (lane == y ? 1.f : 0.f)) / (float)B;
-      dl[lane] = d;
-      dlog_out[b * 10 + lane] = d;
-    }
-    if (lane == 0) {
-      stats[b * 2 + 0] = lse - ly;
-      stats[b * 2 + 1] = (am == y) ? 1.f : 0.f;
-      if (stats_acc != nullptr) {  // running per-sample sums (this block is the sample's only writer)
-        stats_acc[b * 2 + 0] += lse - ly;
-        stats_acc[b * 2 + 1] += (am == y) ? 1.f : 0.f;
-      }
-      if (b == 0 && state != nullptr) state[ST_OPT] += 1;
-    }
-  }
-  __syncthreads();
-  float g[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < 10; ++c) s = fmaf(dl[c], w4r[i][c], s);
-    g[i] = h[i] > 0.f ? s * keep_scale : 0.f;
-  }
-  *reinterpret_cast<float4*>(dz_out + (int64_t)b * 1024 + n0) = make_float4(g[0], g[1], g[2], g[3]);
-}
-
-// head, one thread per feature: 1024 threads (16 waves) per sample. Every slab load is a coalesced
-// 256-byte wave access, the feature-side work is 1/4 of a thread's in the form above, and the
-// logits are 16 wave sums that meet in LDS in a fixed order (deterministic).
+// One thread per feature: 1024 threads (16 waves) per sample. Every slab load is a coalesced
+// 256-byte wave access and the logits are 16 wave sums that meet in LDS in a fixed order
+// (deterministic). (A 256-thread form with 4 features per thread measured 4.45 vs 4.38 us and the
+// whole step 120.0 vs 119.0 us; removed.)
 __global__ void __launch_bounds__(1024) f32_head1k_kernel(
     const float* __restrict__ zpart, const float* __restrict__ b3, const float* __restrict__ w4,
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
@@ -698,9 +603,9 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
   // blocks share a CU: the dispatcher otherwise doubles blocks up on some CUs while others idle
   // (measured 20.6 -> 19.7 us at B = 100).
   const int lds = nblk <= device_cu_count() ? std::max(C2F8_LDS, 81920 + 1024) : C2F8_LDS;
-  // the image staged by LDS-DMA with the W2 fragment copy (default; r05k: 20.71 -> 19.31 us, whole step
-  // 117.42 -> 116.84 us); MIHVD_F32_C2F_DMA=0: register staging + LDS write pass
-  const float* zl = (w2f != nullptr && env_knob("MIHVD_F32_C2F_DMA", 1) != 0) ? f32_zero_line(stream) : nullptr;
+  // the image staged by LDS-DMA with the W2 fragment copy (r05k: 20.71 -> 19.31 us, whole step
+  // 117.42 -> 116.84 us); without the fragment copy (or the zero line) register staging + LDS writes
+  const float* zl = w2f != nullptr ? f32_zero_line(stream) : nullptr;
   auto launch = [&](auto kern) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nblk, 512, lds, stream>>>(a1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
@@ -787,9 +692,7 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   const uint32_t thresh = (uint32_t)(rate * 16777216.0);
   const float keep_scale = rate > 0.0 ? (float)(1.0 / (1.0 - rate)) : 1.f;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  // MIHVD_F32_HEAD1K=0: the 256-thread form (4 features per thread)
-  auto kern = env_knob("MIHVD_F32_HEAD1K", 1) != 0 ? f32_head1k_kernel : f32_head_kernel;
-  kern<<<B, env_knob("MIHVD_F32_HEAD1K", 1) != 0 ? 1024 : 256, 0, stream>>>(
+  f32_head1k_kernel<<<B, 1024, 0, stream>>>(
       zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(), b4.data_ptr<float>(),
       labels.data_ptr<int64_t>(), rp, n_pool, sp, (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(),
       dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc);

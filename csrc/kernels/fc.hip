@@ -699,24 +699,12 @@ void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
   const int MT = (B + 15) >> 4;
   const int lds = (FC1_KSL * F1_WSTR + MT * 16 * F1_ASTR) * 2;
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  // waves per block (MIHVD_FC1_FWD_WAVES, 4 or 8); one block per CU either way (LDS)
-  static const int nw = [] {
-    const char* e = getenv("MIHVD_FC1_FWD_WAVES");
-    return (e && atoi(e) == 4) ? 4 : 8;
-  }();
-  if (nw == 4) {
-    MIHVD_MT_SWITCH(MT, {
-      set_max_lds(fc1_fwd_kernel<MT_, 4>, F1_LDS);
-      fc1_fwd_kernel<MT_, 4><<<dim3(FC1_N / FC1_NT, FC1_KS), 256, lds, stream>>>(
-          (const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(), zpart.data_ptr<float>(), B);
-    })
-  } else {
-    MIHVD_MT_SWITCH(MT, {
-      set_max_lds(fc1_fwd_kernel<MT_, 8>, F1_LDS);
-      fc1_fwd_kernel<MT_, 8><<<dim3(FC1_N / FC1_NT, FC1_KS), 512, lds, stream>>>(
-          (const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(), zpart.data_ptr<float>(), B);
-    })
-  }
+  // 8 waves per block (one block per CU: LDS)
+  MIHVD_MT_SWITCH(MT, {
+    set_max_lds(fc1_fwd_kernel<MT_, 8>, F1_LDS);
+    fc1_fwd_kernel<MT_, 8><<<dim3(FC1_N / FC1_NT, FC1_KS), 512, lds, stream>>>(
+        (const u16*)a2.data_ptr(), (const u16*)w3bf.data_ptr(), zpart.data_ptr<float>(), B);
+  })
 }
 
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
@@ -802,17 +790,9 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const u16 *pdz = (const u16*)dz.data_ptr(), *pa2 = (const u16*)a2.data_ptr(), *ph = (const u16*)h.data_ptr();
   // dW3 tiles alone over a K of two or more 128-row chunks (all-gathered factors): the K-split
-  // group tiles, 2 groups, or 4 from MIHVD_WGRAD_KG4_CHUNKS chunks on (default 4: the 4- and
-  // 8-rank factors; 0 = never); MIHVD_WGRAD_KG2=0 keeps the 4-wave tiles
-  static const bool kg2 = [] {
-    const char* e = getenv("MIHVD_WGRAD_KG2");
-    return !(e && atoi(e) == 0);
-  }();
-  static const int kg4_from = [] {
-    const char* e = getenv("MIHVD_WGRAD_KG4_CHUNKS");
-    return e ? atoi(e) : 4;
-  }();
-  if (kg2 && roles == 1 && Kw > MAXB) {
+  // group tiles, 2 groups, or 4 from 4 chunks on (the 4- and 8-rank factors)
+  constexpr int kg4_from = 4;
+  if (roles == 1 && Kw > MAXB) {
     const int nch = (Kw + MAXB - 1) / MAXB;
     auto run = [&](auto kt, auto ka, int groups) {
       const int lds = groups * FB_LDS_WG;
@@ -834,12 +814,8 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
     const int ncu = device_cu_count();
     // 32-feature tiles (twice the blocks, each with half the MFMA work and half the Adam epilogue)
     // when they still fit the CUs one block each: the 8-rank slice dW3 7.2 -> 6.3 us, dW3 + Adam
-    // 11.4 -> 9.0 us (MIHVD_WGRAD_NARROW=0 keeps the 64-feature tiles)
-    static const bool narrow = [] {
-      const char* e = getenv("MIHVD_WGRAD_NARROW");
-      return !(e && atoi(e) == 0);
-    }();
-    if (kg4_from > 0 && nch >= kg4_from && narrow && 2 * tiles + cr.nblk <= ncu) {
+    // 11.4 -> 9.0 us
+    if (nch >= kg4_from && 2 * tiles + cr.nblk <= ncu) {
       const int grid32 = 2 * tiles + cr.nblk;
       const int lds = 4 * FB_LDS_WG;
       const int tb32 = (int)jt_lo * (FC1_N / 32);
@@ -854,21 +830,12 @@ static void fc1_wgrad_launch(const at::Tensor& dz, const at::Tensor& a2, const a
       }
       return;
     }
-    if (kg4_from > 0 && nch >= kg4_from && tiles + cr.nblk <= ncu)
+    if (nch >= kg4_from && tiles + cr.nblk <= ncu)
       run(fc1_dw3_kg_kernel<false, 4>, fc1_dw3_kg_kernel<true, 4>, 4);
     else run(fc1_dw3_kg_kernel<false, 2>, fc1_dw3_kg_kernel<true, 2>, 2);
     return;
   }
-  // MIHVD_WGRAD_ADAM_OCC=4: registers capped for 4 blocks per CU (784 tiles resident at once)
-  static const int occ = [] {
-    const char* e = getenv("MIHVD_WGRAD_ADAM_OCC");
-    return e ? atoi(e) : 0;
-  }();
-  if (ad != nullptr && occ == 4) {
-    fc1_wgrad_kernel<true, 4><<<grid, 256, FB_LDS_WG, stream>>>(
-        pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
-        gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0, a2s, a2c0, cr);
-  } else if (ad != nullptr) {
+  if (ad != nullptr) {
     fc1_wgrad_kernel<true><<<grid, 256, FB_LDS_WG, stream>>>(
         pdz, pa2, ph, dlog.data_ptr<float>(), dzw, a2w, Kw, gW3.data_ptr<float>(), gb3.data_ptr<float>(),
         gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, tile_base, n_small, *ad, write_grad ? 1 : 0, a2s, a2c0, cr);

@@ -126,117 +126,21 @@ def main():
         "adam_step (W3)": lambda: o.adam_step(tr.params[s3], tr.grads[s3], tr.m[s3], tr.v[s3], None, st, 0, 0.0, b1,
                                               b2, tr.eps, 1.0, tr.rule, 0),
     }
-    study_env = {"dg": {"MIHVD_F32_C2B_ROLE": "1"}, "wg": {"MIHVD_F32_C2B_ROLE": "2"}}
     if args.only:
-        for item in args.only.split(","):
-            name, _, variant = item.partition(":")
-            os.environ.update(study_env.get(variant, {}))
+        for name in args.only.split(","):
             for _ in range(args.eager):
                 ks[name]()
             torch.cuda.synchronize()
-            for k in study_env.get(variant, {}):
-                os.environ.pop(k, None)
         return
-    two = {}
-
-    def c2b_two_round():  # its own cpart / slab, sized for the two-round launch (read under the env)
-        key = (int(o.f32_dgrad_blocks(B)), int(o.f32_wgrad_groups(B)))
-        if key not in two:
-            two[key] = (torch.empty(key[0], 832, device="cuda"), torch.empty(key[1], 51200, device="cuda"))
-        cp, sl = two[key]
-        o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, cp, sl)
-
     res = {}
     for name, fn in ks.items():
         if want(name):
             res[name] = timed(fn, args.reps)
-    # study variants (host knobs read at capture time, csrc/kernels/f32_*.hip): placement and roles
-    study = {
-        "conv2_bwd [W2 after a full barrier]": ({"MIHVD_F32_C2B_PREW": "0"}, ks["conv2_bwd"]),
-        "conv2_bwd [dgrad role only]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd"]),
-        "conv2_bwd [dgrad role only, W2 after a full barrier]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_PREW": "0"},
-                                                                ks["conv2_bwd"]),
-        "conv2_bwd [wgrad role only]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd"]),
-        "conv2_bwd [conv1 wgrad epilogue on MFMA]": ({"MIHVD_F32_C2B_MEPI": "1"}, ks["conv2_bwd"]),
-        "conv2_bwd [dgrad role only, MFMA epilogue]": ({"MIHVD_F32_C2B_ROLE": "1", "MIHVD_F32_C2B_MEPI": "1"},
-                                                     ks["conv2_bwd"]),
-        "conv2_bwd [wgrad blocks in launch order]": ({"MIHVD_F32_C2B_XCD": "0"}, ks["conv2_bwd"]),
-        "conv2_bwd [W2 fragment copy, wgrad next image register-staged]": ({"MIHVD_F32_C2B_WMID": "2"},
-                                                                           ks["conv2_bwd [W2 fragment copy]"]),
-        "conv2_bwd [wgrad role only, next image register-staged]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "2"},
-                                                                    ks["conv2_bwd [W2 fragment copy]"]),
-        "conv2_bwd [wgrad role only, W2 fragment copy]": ({"MIHVD_F32_C2B_ROLE": "2"}, ks["conv2_bwd [W2 fragment copy]"]),
-        "conv2_bwd [wgrad next image stored after the steps]": ({"MIHVD_F32_C2B_WMID": "0"}, ks["conv2_bwd"]),
-        "conv2_bwd [wgrad role only, stored after the steps]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "0"},
-                                                               ks["conv2_bwd"]),
-        "conv2_bwd [wgrad next image stored at step 6]": ({"MIHVD_F32_C2B_WMID": "1"}, ks["conv2_bwd"]),
-        "conv2_bwd [W2 fragment copy, wgrad loads after step 0]": ({"MIHVD_F32_C2B_WMID": "6"},
-                                                                   ks["conv2_bwd [W2 fragment copy]"]),
-        "conv2_bwd [wgrad role only, loads after step 0]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "6"},
-                                                           ks["conv2_bwd"]),
-        "conv2_bwd [wgrad role only, stored at step 6]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_WMID": "1"},
-                                                         ks["conv2_bwd"]),
-        "conv2_bwd [two-round form]": ({"MIHVD_F32_C2B_R1": "0"}, c2b_two_round),
-        "conv2_bwd [two-round form, dgrad role only]": ({"MIHVD_F32_C2B_R1": "0", "MIHVD_F32_C2B_ROLE": "1"},
-                                                      c2b_two_round),
-        "conv2_bwd [two-round form, wgrad role only]": ({"MIHVD_F32_C2B_R1": "0", "MIHVD_F32_C2B_ROLE": "2"},
-                                                      c2b_two_round),
-        "conv2_bwd [wgrad role only, launch order]": ({"MIHVD_F32_C2B_ROLE": "2", "MIHVD_F32_C2B_XCD": "0"},
-                                                     ks["conv2_bwd"]),
-        "fc1_bwd+W3 adam [padded wgrad K (28 steps)]": ({"MIHVD_F32_F1R_KW": "0"}, ks["fc1_bwd+W3 adam"]),
-        "head [256 threads, 4 features each]": ({"MIHVD_F32_HEAD1K": "0"}, ks["head"]),
-        "conv2_bwd [dgrad role only, W2 fragment copy]": ({"MIHVD_F32_C2B_ROLE": "1"}, ks["conv2_bwd [W2 fragment copy]"]),
-        "conv2_fwd [W2 fragment copy, image register-staged]": ({"MIHVD_F32_C2F_DMA": "0"}, ks["conv2_fwd [W2 fragment copy]"]),
-        "fc1_bwd+W3 adam [routing operands loaded in the epilogue]": ({"MIHVD_F32_F1R_PF": "0"}, ks["fc1_bwd+W3 adam"]),
-
-    }
-    for name, (env, fn) in study.items():
-        if not want(name):
-            continue
-        old_env = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
-        try:
-            res[name] = timed(fn, args.reps)
-        finally:
-            for k, v in old_env.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
     saved = tr.lr
     tr.lr = 0.0
     if want("whole step (graph, 20 steps/replay)"):
         res["whole step (graph, 20 steps/replay)"] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
         tr._join()
-    # whole-step studies: trainer attributes and launch knobs (read at capture time)
-    steps = {
-        "whole step [conv1 wgrad epilogue on MFMA]": ({}, {"MIHVD_F32_C2B_MEPI": "1"}),
-        "whole step [conv2 wgrad blocks in launch order]": ({}, {"MIHVD_F32_C2B_XCD": "0"}),
-        "whole step [fc1_bwd padded wgrad K]": ({}, {"MIHVD_F32_F1R_KW": "0"}),
-        "whole step [256-thread head]": ({}, {"MIHVD_F32_HEAD1K": "0"}),
-        "whole step [conv2_fwd image register-staged]": ({}, {"MIHVD_F32_C2F_DMA": "0"}),
-        "whole step [conv2 wgrad next image register-staged]": ({}, {"MIHVD_F32_C2B_WMID": "2"}),
-        "whole step [fc1_bwd routing operands loaded in the epilogue]": ({}, {"MIHVD_F32_F1R_PF": "0"}),
-    }
-    for name, (attrs, env) in steps.items():
-        if not want(name):
-            continue
-        old_attr = {k: getattr(tr, k) for k in attrs}
-        old_env = {k: os.environ.get(k) for k in env}
-        for k, v in attrs.items():
-            setattr(tr, k, v)
-        os.environ.update(env)
-        try:
-            res[name] = timed(lambda: tr._launch_step(tr.X, tr.rows, tr.Y), 20)
-            tr._join()
-        finally:
-            for k, v in old_attr.items():
-                setattr(tr, k, v)
-            for k, v in old_env.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
     tr.lr = saved
     width = max(len(k) for k in res)
     for k, v in res.items():

@@ -52,9 +52,9 @@ def test_f32_conv1_fwd(ops, B):
 
 @pytest.mark.parametrize("B", [7, 100, 128])
 def test_f32_conv2_fwd(ops, B, monkeypatch):
-    """The two waves of a SIMD split the input channels (their partials meet in LDS); HWIO and
-    fragment-copy W2 reads give the same bits, with the image staged by LDS-DMA (the default with
-    the fragment copy) or through registers (MIHVD_F32_C2F_DMA=0)."""
+    """The two waves of a SIMD split the input channels (their partials meet in LDS); HWIO reads
+    (image staged through registers) and fragment-copy W2 reads (image staged by LDS-DMA) give the
+    same bits."""
     g = torch.Generator(device="cuda").manual_seed(2)
     a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
     w = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
@@ -70,11 +70,6 @@ def test_f32_conv2_fwd(ops, B, monkeypatch):
     a2f, idxf = torch.empty_like(a2), torch.empty_like(idx)
     ops.f32_conv2_fwd(a1, w, b, a2f, idxf, w2frag=frag[0])
     assert torch.equal(a2, a2f) and torch.equal(idx, idxf)
-    monkeypatch.setenv("MIHVD_F32_C2F_DMA", "0")
-    a2d, idxd = torch.full_like(a2, float("nan")), torch.empty_like(idx)
-    ops.f32_conv2_fwd(a1, w, b, a2d, idxd, w2frag=frag[0])
-    monkeypatch.delenv("MIHVD_F32_C2F_DMA")
-    assert torch.equal(a2, a2d) and torch.equal(idx, idxd)
     ref, rd = ref_conv_pool(a1, w, b)
     assert rel_err(a2, ref.reshape(B, 3136)) < 1e-6
     pos = ref.reshape(B, 3136) > 1e-4
@@ -110,13 +105,6 @@ def test_f32_fc1_fwd_and_head(ops, B, monkeypatch):
     assert abs(stats[:, 0].mean().item() - loss.item()) < 1e-5
     assert rel_err(dz, zr.grad) < 1e-5
     assert rel_err(dlog, torch.softmax(logits, 1).sub(F.one_hot(y, 10).float()).div(B)) < 1e-5
-    # the 256-thread head (MIHVD_F32_HEAD1K=0): same features and mask, logits summed in another order
-    monkeypatch.setenv("MIHVD_F32_HEAD1K", "0")
-    h0, dz0, dlog0, stats0 = (torch.full_like(t, float("nan")) for t in (h, dz, dlog, stats))
-    ops.f32_head_fwd_bwd(zpart, b3, w4, b4, y, None, None, 0, 0.0, h0, dz0, dlog0, stats0)
-    monkeypatch.delenv("MIHVD_F32_HEAD1K")
-    assert torch.equal(h0, h)
-    assert rel_err(dz0, dz) < 1e-6 and rel_err(dlog0, dlog) < 1e-6 and rel_err(stats0, stats) < 1e-6
     # stats_acc (Keras fit's epoch metrics): every launch adds its per-sample (loss, correct) in place
     acc = torch.zeros(B, 2, device="cuda")
     for _ in range(3):
@@ -176,28 +164,18 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
     dlog = torch.randn(B, 10, device="cuda", generator=g)
     st = torch.tensor([5, 7, 0, 0], device="cuda", dtype=torch.int64)
 
-    def run(fused, w, m, v, env=None, key="MIHVD_F32_F1R_KW"):
+    def run(fused, w, m, v):
         dY2 = torch.full((B, 14, 14, 64), float("nan"), device="cuda")
         db2p = torch.empty(int(ops.f32_db2_rows(B)), 64, device="cuda")
         gW3 = torch.full((3136, 1024), float("nan"), device="cuda")
         small = [torch.empty(1024, device="cuda"), torch.empty(1024, 10, device="cuda"), torch.empty(10, device="cuda")]
-        old = os.environ.get(key)
-        if env is not None:
-            os.environ[key] = env
-        try:
-            if fused == "dgrad":  # the fp32 factor plane's launch: no dW3 at all
-                ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small, store_w3=False)
-            elif fused:
-                ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small, m, v, st, 1e-3, 0.9, 0.999, 1e-8,
-                                1.0, 0, True)
-            else:
-                ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small)
-        finally:
-            if env is not None:
-                if old is None:
-                    os.environ.pop(key, None)
-                else:
-                    os.environ[key] = old
+        if fused == "dgrad":  # the fp32 factor plane's launch: no dW3 at all
+            ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small, store_w3=False)
+        elif fused:
+            ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small, m, v, st, 1e-3, 0.9, 0.999, 1e-8,
+                            1.0, 0, True)
+        else:
+            ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, w, dY2, db2p, gW3, *small)
         return dY2, db2p, gW3, small
 
     wf, mf, vf = w3.clone(), m3.clone(), v3.clone()
@@ -213,10 +191,6 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
     dY2d, db2d, gW3d, smalld = run("dgrad", w3.clone(), None, None)
     assert torch.equal(dY2d, dY2s) and torch.equal(db2d, db2s) and torch.isnan(gW3d).all()
     assert all(torch.equal(a, b) for a, b in zip(smalld, smalls))
-    # the exact-batch wgrad chain (ceil(B / 4) K steps where B = 97..100) adds the same products as the
-    # padded one (the padded steps add exact zeros)
-    _, _, gW3p, _ = run(False, w3.clone(), None, None, env="0", key="MIHVD_F32_F1R_KW")
-    assert torch.equal(gW3p, gW3s)
     # dW3 and the routed dgrad against fp64
     assert rel_err(gW3f, a2.double().t() @ dz.double()) < 1e-6
     g2 = (dz.double() @ w3.double().t()) * (a2 > 0)
@@ -230,27 +204,14 @@ def test_f32_fc1_bwd_fused_adam(ops, B):
     bi = torch.arange(B, device="cuda").unsqueeze(1).expand(B, 3136)
     ref[bi, y, x, co.unsqueeze(0).expand(B, 3136)] = g2
     assert rel_err(dY2f, ref) < 1e-6
-    # the routing operands loaded in the epilogue instead of at the start (MIHVD_F32_F1R_PF=0): the same bits
-    dY2q, db2q, gW3q, smallq = run(False, w3.clone(), None, None, env="0", key="MIHVD_F32_F1R_PF")
-    assert torch.equal(dY2q, dY2s) and torch.equal(db2q, db2s) and torch.equal(gW3q, gW3s)
 
 
-@pytest.mark.parametrize("form", ["one-round", "one-round-mepi", "one-round-mid", "one-round-late", "one-round-spread",
-                                  "two-round", "two-round-mepi", "two-round-spread"])
 @pytest.mark.parametrize("B", [7, 100, 128])
-def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
+def test_f32_conv2_bwd_and_reduce(ops, B):
     """conv2 dgrad + fused conv1 wgrad, conv2 wgrad slabs, and the reduction, vs autograd of
-    conv1 -> pool -> conv2 with the routed conv2 gradient. Forms: the one-round launch (default:
-    dgrad blocks of two tap-loop passes, 8-image wgrad groups; B = 128 falls back to two rounds),
-    the two-round launch (MIHVD_F32_C2B_R1=0) with the conv1 weight gradient of the dgrad epilogue
-    on VALU or on MFMA (MIHVD_F32_C2B_MEPI=1); the wgrad blocks' next-image LDS stores one chunk per
-    the next image staged by LDS-DMA (global_load_lds, MIHVD_F32_C2B_WMID=3, the default), or
-    register-staged with its LDS stores one chunk per step ("-spread": WMID=2) or all at step 6
-    ("-mid": WMID=1), or with its global loads issued after step 0's MFMAs ("-late": WMID=6)."""
-    monkeypatch.setenv("MIHVD_F32_C2B_R1", "1" if form.startswith("one-round") else "0")
-    monkeypatch.setenv("MIHVD_F32_C2B_MEPI", "1" if form.endswith("mepi") else "0")
-    monkeypatch.setenv("MIHVD_F32_C2B_WMID", {"mid": "1", "late": "6", "dma": "3", "spread": "2"}.get(
-        form.rsplit("-", 1)[-1], "3"))
+    conv1 -> pool -> conv2 with the routed conv2 gradient: the one-round launch (B = 7, 100: dgrad
+    blocks of two tap-loop passes, 8-image wgrad groups) and the two-round launch (B = 128), the
+    wgrad blocks' next image staged by LDS-DMA (global_load_lds)."""
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.rand(B, 784, device="cuda", generator=g)
     w1 = torch.randn(5, 5, 1, 32, device="cuda", generator=g) * 0.2
@@ -284,8 +245,7 @@ def test_f32_conv2_bwd_and_reduce(ops, B, form, monkeypatch):
 def test_f32_w2_fragment_copies(ops, B, monkeypatch):
     """MIHVD_F32_W2F: the conv1 launch's extra blocks write W2 in the load order of the conv2_fwd
     waves ([tap][c2][wave][lane][j]) and of the conv2_bwd dgrad waves ([wave][tap][lane][j]); both
-    conv2 launches reading them produce bit-identical outputs to the HWIO reads (conv2_bwd with the
-    conv1 weight-gradient epilogue on VALU and on MFMA, MIHVD_F32_C2B_MEPI=1)."""
+    conv2 launches reading them produce bit-identical outputs to the HWIO reads."""
     g = torch.Generator(device="cuda").manual_seed(15)
     x = torch.rand(B, 784, device="cuda", generator=g)
     w1 = torch.randn(800, device="cuda", generator=g) * 0.2
@@ -308,15 +268,13 @@ def test_f32_w2_fragment_copies(ops, B, monkeypatch):
     ops.f32_conv2_fwd(a1, w2.view(-1), b2, a2f, idx2f, w2frag=frag[0])
     assert torch.equal(a2, a2f) and torch.equal(idx2, idx2f)
     dY2 = torch.randn(B, 14, 14, 64, device="cuda", generator=g)
-    for mepi in ("0", "1"):
-        monkeypatch.setenv("MIHVD_F32_C2B_MEPI", mepi)
-        outs = []
-        for wf in (None, frag[1]):
-            cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, device="cuda")
-            slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, device="cuda")
-            ops.f32_conv2_bwd(dY2, w2.view(-1), a1, idx1, x, None, None, cpart, slab, w2frag=wf)
-            outs.append((cpart, slab))
-        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    outs = []
+    for wf in (None, frag[1]):
+        cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, device="cuda")
+        slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, device="cuda")
+        ops.f32_conv2_bwd(dY2, w2.view(-1), a1, idx1, x, None, None, cpart, slab, w2frag=wf)
+        outs.append((cpart, slab))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("NB,R", [(800, 392), (100, 3136), (200, 784), (7, 448), (350, 392)])
