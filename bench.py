@@ -15,7 +15,9 @@ Implementations:
            buffer, RCCL collectives on it, TF1-Adam; the whole step (incl. the collectives) replayed
            as one HIP graph. --precision fp32 (default, the reference's precision): exact fp32
            operands on the fp32-input MFMAs (v_mfma_f32_16x16x4_f32 / 32x32x2_f32); --precision
-           bf16: bf16 MFMA operands with fp32 accumulation, master weights and optimizer state.
+           bf16: bf16 MFMA operands with fp32 accumulation, master weights and optimizer state;
+           --precision fp16: the Keras mixed_float16 step (tensorflow_mnist_gpu.py:26-28) — fp16
+           MFMA operands, fp32 master state, dynamic loss scaling held on the device.
   torch  — stock PyTorch-ROCm ops (fp32) + mihvd DistributedOptimizer (bucketed RCCL allreduce) +
            TF1 Adam on the multi-tensor HIP kernel.
   torch-graph — the same step (data gather, forward, backward, bucket allreduces, FusedAdam with a
@@ -58,10 +60,11 @@ def parse():
                     "run (0: none)")
     ap.add_argument("--pool-batches", type=int, default=60, help="synthetic batches resident on device")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
-    ap.add_argument("--precision", choices=["fp32", "bf16"], default=os.environ.get("MIHVD_PRECISION", "fp32"),
+    ap.add_argument("--precision", choices=["fp32", "bf16", "fp16"], default=os.environ.get("MIHVD_PRECISION", "fp32"),
                     help="fused: operand precision of the hand-written step. fp32 (default) = the reference's "
                          "launched config (fp32 placeholders + AdamOptimizer, tensorflow_mnist.py:118-130) on the "
-                         "fp32-input MFMAs; bf16 = bf16 MFMA operands, fp32 accumulation/master weights")
+                         "fp32-input MFMAs; bf16 = bf16 MFMA operands, fp32 accumulation/master weights; fp16 = the "
+                         "mixed_float16 step with the device loss scaler")
     return ap.parse_args()
 
 

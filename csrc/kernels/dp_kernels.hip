@@ -161,11 +161,14 @@ __global__ void __launch_bounds__(256) grad_check_kernel(TensorTable tt, float* 
   if (__any(bad) && (threadIdx.x & 63) == 0) ls[1] = 1.f;
 }
 
+// state (optional, the fused fp16 step): a skipped update does not count as an optimizer step,
+// like Keras' LossScaleOptimizer, so the step the head advanced is taken back
 __global__ void update_scale_kernel(float* __restrict__ ls, int32_t* __restrict__ tracker, float growth, float backoff,
-                                    int interval, float min_scale) {
+                                    int interval, float min_scale, int64_t* __restrict__ state) {
   if (ls[1] != 0.f) {
     ls[0] = fmaxf(ls[0] * backoff, min_scale);
     tracker[0] = 0;
+    if (state != nullptr) state[ST_OPT] -= 1;
   } else if (++tracker[0] >= interval) {
     const float s = ls[0] * growth;
     if (isfinite(s)) ls[0] = s;
@@ -244,12 +247,18 @@ void grad_check_(at::TensorList grads, at::Tensor& ls, bool unscale) {
 }
 
 void update_scale_(at::Tensor& ls, at::Tensor& tracker, double growth, double backoff, int64_t interval,
-                   double min_scale) {
+                   double min_scale, const c10::optional<at::Tensor>& state) {
   check_f32_cuda(ls, "update_scale_(ls)");
   TORCH_CHECK(tracker.is_cuda() && tracker.dtype() == at::kInt && tracker.numel() >= 1, "update_scale_: int32 tracker");
+  int64_t* sp = nullptr;
+  if (state.has_value() && state->defined()) {
+    TORCH_CHECK(state->is_cuda() && state->dtype() == at::kLong && state->numel() >= ST_WORDS,
+                "update_scale_: state must be the int64 device step state");
+    sp = state->data_ptr<int64_t>();
+  }
   auto stream = c10::hip::getCurrentHIPStream().stream();
   update_scale_kernel<<<1, 1, 0, stream>>>(ls.data_ptr<float>(), tracker.data_ptr<int32_t>(), (float)growth,
-                                           (float)backoff, (int)interval, (float)min_scale);
+                                           (float)backoff, (int)interval, (float)min_scale, sp);
 }
 
 // ------------------------------------------------------------------------------------------ //

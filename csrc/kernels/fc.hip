@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) head_kernel(
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float dz_mul, u16* __restrict__ h_out,
     u16* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B, CollRole cr,
-    float* __restrict__ stats_acc) {
+    float* __restrict__ stats_acc, const float* __restrict__ ls) {
   __shared__ float red[4][10];
   __shared__ float dl[10];
   // co-launched xGMI collective (xgmi_role.h) on the first cr.nblk blocks
@@ -166,7 +166,9 @@ __global__ void __launch_bounds__(256) head_kernel(
     if (lane < 10) {
       const float d = (__expf(lg - lse) - (lane == y ? 1.f : 0.f)) * (1.0f / (float)B);
       dl[lane] = d;
-      dlog_out[b * 10 + lane] = d;
+      // ls (the fused fp16 step's device loss scale [S, found]): dlog is stored S-scaled like dz,
+      // so every gradient of the step (dW4 / db4 included) carries S and one unscale fits all
+      dlog_out[b * 10 + lane] = ls != nullptr ? d * ls[0] : d;
     }
     if (lane == 0) {
       stats[b * 2 + 0] = lse - ly;
@@ -185,7 +187,8 @@ __global__ void __launch_bounds__(256) head_kernel(
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < 10; ++c) s = fmaf(dl[c], w4r[i][c], s);
-    g[i] = h[i] > 0.f ? s * dz_mul : 0.f;  // dz_mul = keep_scale x the loss scale (fp16 build)
+    // dz_mul = keep_scale x the loss scale (fp16 build; with ls the scale is read on the device)
+    g[i] = h[i] > 0.f ? s * (ls != nullptr ? dz_mul * ls[0] : dz_mul) : 0.f;
   }
   *reinterpret_cast<uint2*>(dz_out + (int64_t)b * FC1_N + n0) = pack4bf(g[0], g[1], g[2], g[3]);
 }
@@ -710,7 +713,8 @@ void fc1_fwd(const at::Tensor& a2, const at::Tensor& w3bf, at::Tensor& zpart) {
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc) {
+                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc,
+                  const c10::optional<at::Tensor>& loss_scale) {
   const int B = h.size(0);
   TORCH_CHECK(zpart.dtype() == at::kFloat && zpart.numel() == (int64_t)FC1_KS * B * FC1_N, "head: zpart");
   TORCH_CHECK(b3.numel() == FC1_N && w4.numel() == FC1_N * 10 && b4.numel() == 10 && w4.dtype() == at::kFloat, "head: params");
@@ -731,6 +735,13 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
   int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   const uint32_t thresh = (uint32_t)(rate * 16777216.0);
   const float keep_scale = (float)(1.0 / (1.0 - rate));
+  const float* lsp = nullptr;
+  if (loss_scale.has_value() && loss_scale->defined()) {
+    TORCH_CHECK(loss_scale->is_cuda() && loss_scale->dtype() == at::kFloat && loss_scale->numel() == 2,
+                "head: loss_scale must be the float32 device pair [scale, found_nonfinite]");
+    TORCH_CHECK(dz_scale == 1.0, "head: a device loss scale replaces dz_scale");
+    lsp = loss_scale->data_ptr<float>();
+  }
   auto stream = c10::hip::getCurrentHIPStream().stream();
   const CollRole cr = xgmi_role_lookup(coll);
   head_kernel<<<B + cr.nblk, 256, 0, stream>>>(zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(),
@@ -738,7 +749,7 @@ void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tenso
                                                (uint32_t)seed, thresh, keep_scale, (float)(keep_scale * dz_scale),
                                                (u16*)h.data_ptr(),
                                                (u16*)dz.data_ptr(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B,
-                                               cr, acc);
+                                               cr, acc, lsp);
 }
 
 // roles: bit 0 = the dW3 tiles, bit 1 = the small reductions (db3, dW4, db4). dW3 multiplies dz_w3^T a2_w3 over their rows: the local dz/a2 by default, or the

@@ -19,7 +19,8 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc);
+                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc,
+                  const c10::optional<at::Tensor>& loss_scale);
 void fc1_wgrad(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, const at::Tensor& dlog, at::Tensor& gW3,
                at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, int64_t roles, const c10::optional<at::Tensor>& dz_w3,
                const c10::optional<at::Tensor>& a2_w3, int64_t jt_lo, int64_t jt_hi, int64_t coll);
@@ -73,7 +74,7 @@ void adasum_combine(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
                     const at::Tensor& dots, at::Tensor& out);
 void grad_check_(at::TensorList grads, at::Tensor& ls, bool unscale);
 void update_scale_(at::Tensor& ls, at::Tensor& tracker, double growth, double backoff, int64_t interval,
-                   double min_scale);
+                   double min_scale, const c10::optional<at::Tensor>& state);
 void gather_cols_bf16(const at::Tensor& src, int64_t col0, at::Tensor& dst);
 void multi_tensor_adam(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std::vector<at::Tensor> m,
                        std::vector<at::Tensor> v, const c10::optional<at::Tensor>& step, int64_t host_step, double lr,
@@ -135,7 +136,8 @@ void fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& h, co
 void head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                   const at::Tensor& labels, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                   int64_t seed, double rate, at::Tensor& h, at::Tensor& dz, at::Tensor& dlog, at::Tensor& stats,
-                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc);
+                  int64_t coll, double dz_scale, const c10::optional<at::Tensor>& stats_acc,
+                  const c10::optional<at::Tensor>& loss_scale);
 void conv2_bwd(const at::Tensor& g2, const at::Tensor& idx2, const at::Tensor& a1, const at::Tensor& w2bf,
                const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                const at::Tensor& idx1, at::Tensor& slab, at::Tensor& cpart, const c10::optional<at::Tensor>& g1,
@@ -168,8 +170,9 @@ void fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tenso
 void fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::fc1_fwd(a2, w3, zpart); }
 void head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
              const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog, Tensor stats,
-             int64_t coll, double dz_scale, const OptT& stats_acc) {
-  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale, stats_acc);
+             int64_t coll, double dz_scale, const OptT& stats_acc, const OptT& loss_scale) {
+  mihvd::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale, stats_acc,
+                      loss_scale);
 }
 // fp16-operand ops (the Keras mixed_float16 policy): the bf16 ops' schemas, half tensors.
 void conv1_fwd_f16_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1,
@@ -186,9 +189,9 @@ void conv12_fwd_f16_op(const Tensor& x, const OptT& rows, const OptT& state, con
 void fc1_fwd_f16_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f16::fc1_fwd(a2, w3, zpart); }
 void head_f16_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
-                 Tensor stats, int64_t coll, double dz_scale, const OptT& stats_acc) {
+                 Tensor stats, int64_t coll, double dz_scale, const OptT& stats_acc, const OptT& loss_scale) {
   mihvd::f16::head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, coll, dz_scale,
-                           stats_acc);
+                           stats_acc, loss_scale);
 }
 void fc1_bwd_f16_op(const Tensor& dz, const Tensor& a2, const Tensor& h, const Tensor& dlog, const Tensor& w3,
                     Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, Tensor g2, int64_t roles, int64_t coll,
@@ -269,8 +272,9 @@ void adasum_combine_op(const Tensor& a, const Tensor& b, const Tensor& offs, int
   mihvd::adasum_combine(a, b, offs, max_len, dots, out);
 }
 void grad_check_op(at::TensorList grads, Tensor ls, bool unscale) { mihvd::grad_check_(grads, ls, unscale); }
-void update_scale_op(Tensor ls, Tensor tracker, double growth, double backoff, int64_t interval, double min_scale) {
-  mihvd::update_scale_(ls, tracker, growth, backoff, interval, min_scale);
+void update_scale_op(Tensor ls, Tensor tracker, double growth, double backoff, int64_t interval, double min_scale,
+                     const OptT& state) {
+  mihvd::update_scale_(ls, tracker, growth, backoff, interval, min_scale, state);
 }
 void gather_cols_op(const Tensor& src, int64_t col0, Tensor dst) { mihvd::gather_cols_bf16(src, col0, dst); }
 void mt_adam_op(at::TensorList p, at::TensorList g, at::TensorList m, at::TensorList v, const OptT& step,
@@ -333,7 +337,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("fc1_fwd(Tensor a2, Tensor w3bf, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, Tensor(s!)? state, "
         "int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, int coll=-1, "
-        "float dz_scale=1., Tensor(e!)? stats_acc=None) -> ()");
+        "float dz_scale=1., Tensor(e!)? stats_acc=None, Tensor? loss_scale=None) -> ()");
   m.def("conv1_fwd_f16(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1) -> ()");
   m.def("conv2_fwd_f16(Tensor a1, Tensor w2h, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2) -> ()");
   m.def("conv12_fwd_f16(Tensor x, Tensor? rows, Tensor? state, Tensor w1h, Tensor b1, Tensor w2h, Tensor b2, "
@@ -341,7 +345,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("fc1_fwd_f16(Tensor a2, Tensor w3h, Tensor(a!) zpart) -> ()");
   m.def("head_fwd_bwd_f16(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
-        "int coll=-1, float dz_scale=1., Tensor(e!)? stats_acc=None) -> ()");
+        "int coll=-1, float dz_scale=1., Tensor(e!)? stats_acc=None, Tensor? loss_scale=None) -> ()");
   m.def("fc1_bwd_f16(Tensor dz, Tensor a2, Tensor h, Tensor dlog, Tensor w3h, Tensor(a!) gW3, Tensor(b!) gb3, "
         "Tensor(c!) gW4, Tensor(d!) gb4, Tensor(e!) g2, int roles=3, int coll=-1, Tensor(f!)? a2T=None, "
         "Tensor(g!)? dzT=None) -> ()");
@@ -417,7 +421,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("adasum_combine(Tensor a, Tensor b, Tensor offs, int max_seg_len, Tensor dots, Tensor(a!) out) -> ()");
   m.def("grad_check_(Tensor(a!)[] grads, Tensor(b!) ls, bool unscale) -> ()");
   m.def("update_scale_(Tensor(a!) ls, Tensor(b!) tracker, float growth, float backoff, int interval, "
-        "float min_scale) -> ()");
+        "float min_scale, Tensor(c!)? state=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {

@@ -324,7 +324,7 @@ class _LossScaler:
 class Model:
     """``policy`` is the Keras mixed-precision policy (tensorflow_mnist_gpu.py:26-28). A module with
     ``impl == "hip"`` (``MNISTConvNet(impl="hip")``) trains through the hand-written CDNA4 kernels:
-    under ``float32`` / ``mixed_bfloat16`` with a TF1/Keras-rule Adam, ``fit`` drives the fused,
+    under ``float32`` / ``mixed_bfloat16`` / ``mixed_float16`` with a TF1/Keras-rule Adam, ``fit`` drives the fused,
     graph-replayed training step (``FusedMNISTTrainer``: the whole step in seven launches, k steps per
     HIP graph replay between callback points); otherwise one fused forward+backward autograd node
     per batch: ``float32`` runs the exact-fp32 kernels,
@@ -421,8 +421,8 @@ class Model:
     _FUSED_CALLBACKS = (BroadcastGlobalVariablesCallback, MetricAverageCallback, ModelCheckpoint, TensorBoard)
 
     def _fused_fit_trainer(self, cbs, batch_size):
-        """The graph-replayed fit path (tensorflow_mnist_gpu.py:166-182 under ``float32`` /
-        ``mixed_bfloat16``): a :class:`~mihvd.models.fused_mnist.FusedMNISTTrainer` over the
+        """The graph-replayed fit path (tensorflow_mnist_gpu.py:166-182 under ``float32``,
+        ``mixed_bfloat16`` or ``mixed_float16``, the last with the device loss scaler in the graph): a :class:`~mihvd.models.fused_mnist.FusedMNISTTrainer` over the
         module's weights and the optimizer's Adam hyper-parameters, or None where the per-batch path
         must run (MIHVD_KERAS_FUSED=0, another policy or module, an optimizer or reduction the fused
         step does not implement, existing optimizer state, or a callback with per-batch hooks)."""
@@ -443,9 +443,11 @@ class Model:
         op = getattr(opt, "_op", _b.Average)
         from .models.fused_mnist import FusedMNISTTrainer
 
+        precision = {"float32": "fp32", "mixed_float16": "fp16"}.get(self.policy, "bf16")
         tr = FusedMNISTTrainer(batch_size=batch_size, lr=g["lr"], betas=tuple(g["betas"]), eps=g["eps"],
-                               dropout=m.dropout_rate, device=self._device(), op=op,
-                               precision="fp32" if self.policy == "float32" else "bf16")
+                               dropout=m.dropout_rate, device=self._device(), op=op, precision=precision)
+        if precision == "fp16" and self._scaler is not None and self._scaler._ls is not None:
+            tr.loss_scale.copy_(self._scaler._ls)  # continue from the per-batch path's scale
         tr.load_model_weights(m)
         tr.track_stats = True
         return tr
@@ -459,7 +461,7 @@ class Model:
 
         m, opt = self.module, self.optimizer
         if (not isinstance(m, MNISTConvNet) or getattr(m, "impl", None) != "hip" or self.policy not in
-                ("float32", "mixed_bfloat16") or opt is None or not 1 <= batch_size <= 128):
+                ("float32", "mixed_bfloat16", "mixed_float16") or opt is None or not 1 <= batch_size <= 128):
             return False
         if not isinstance(opt, (TFAdam, FusedAdam)) or len(opt.param_groups) != 1 or any(opt.state.values()):
             return False
@@ -525,8 +527,11 @@ class Model:
                 print(f"Epoch {epoch + 1}/{epochs} - {dt:.1f}s - " +
                       " - ".join(f"{k2}: {v:.4f}" for k2, v in logs.items()), file=sys.stdout, flush=True)
         # the Adam slots into the optimizer's state (a later per-batch fit or a checkpoint continues
-        # from them)
+        # from them), and under mixed_float16 the device loss scale into the model's scaler
         self._adam_state_from_trainer(tr)
+        if getattr(tr, "f16", False) and self._scaler is not None:
+            self._scaler._device_state(tr.device)
+            self._scaler._ls.copy_(tr.loss_scale)
         # images/sec of the training steps (whole job), from the epochs after the first (whose time
         # includes the HIP graph captures) when there are several
         per_epoch = steps_per_epoch * batch_size * (_b.size() if _b.is_initialized() else 1)

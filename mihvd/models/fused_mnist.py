@@ -138,11 +138,15 @@ class FusedMNISTTrainer:
         # AdamOptimizer, horovod/tensorflow_mnist.py:118-121,130; csrc/kernels/f32_*.hip), "bf16" =
         # bf16 MFMA operands with fp32 accumulation and fp32 master weights (the MI355X analogue of
         # the mixed_float16 variant, tensorflow_mnist_gpu.py:26-28).
+        # "fp16" = the reference's mixed_float16 policy itself (tensorflow_mnist_gpu.py:26-28): fp16
+        # MFMA operands (the fp16 build of the bf16 kernels) with in-graph dynamic loss scaling
+        # (_launch_step_f16)
         precision = (precision or os.environ.get("MIHVD_PRECISION", "fp32")).lower()
-        if precision not in ("fp32", "bf16"):
-            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if precision not in ("fp32", "bf16", "fp16"):
+            raise ValueError("precision must be 'fp32', 'bf16' or 'fp16'")
         self.precision = precision
         self.f32 = precision == "fp32"
+        self.f16 = precision == "fp16"
 
         self.ops = torch.ops.mihvd
         # MIHVD_DEBUG_SYNC=1: serialized bisection mode (the HIP_LAUNCH_BLOCKING of this engine):
@@ -218,14 +222,24 @@ class FusedMNISTTrainer:
         self.m = torch.zeros(FLAT_NUMEL, **f32)
         self.v = torch.zeros(FLAT_NUMEL, **f32)
         # bf16 copy of the parameters that the bf16 kernels read (the fp32 kernels read params)
-        self.shadow = None if self.f32 else torch.zeros(FLAT_NUMEL, device=dev, dtype=torch.bfloat16)
+        self.op16 = torch.float16 if self.f16 else torch.bfloat16  # the 16-bit operand format
+        self.shadow = None if self.f32 else torch.zeros(FLAT_NUMEL, device=dev, dtype=self.op16)
+        if self.f16:
+            from ..ops.functional import _Ops16
+
+            self._o16 = _Ops16(fp16=True)
+            # Keras LossScaleOptimizer's dynamic loss scale, on the device: [scale, found_nonfinite]
+            # (start 2**15, halve on overflow and skip the step, double after 2000 clean steps)
+            self.loss_scale = torch.tensor([2.0 ** 15, 0.0], device=dev, dtype=torch.float32)
+            self._ls_tracker = torch.zeros(1, device=dev, dtype=torch.int32)
+            self.ls_growth_interval = 2000
         self.state = torch.zeros(4, device=dev, dtype=torch.int64)  # [fwd step, opt step t, -, -]
         self.shard_w3 = False
         self.f32_factor = False
         ref = MNISTConvNet(impl="torch", seed=seed)
         self.load_model_weights(ref)
         B = self.B
-        bf = dict(device=dev, dtype=torch.bfloat16)
+        bf = dict(device=dev, dtype=self.op16)
         u8 = dict(device=dev, dtype=torch.uint8)
         self.a1 = torch.empty(B, 14, 14, 32, **bf)
         self.idx1 = torch.empty(B, 14, 14, 32, **u8)
@@ -237,7 +251,7 @@ class FusedMNISTTrainer:
         from ..basics import ReduceOp
 
         avg_or_sum = op is None or ReduceOp(op) in (ReduceOp.Average, ReduceOp.Sum)
-        self.gather = self.collectives and compression == "none" and not self.f32 and avg_or_sum
+        self.gather = self.collectives and compression == "none" and not self.f32 and not self.f16 and avg_or_sum
         # Sharded dense/kernel optimizer (shard_optimizer=True or MIHVD_SHARD_W3=1). bf16 (factor-gather
         # plane): rank r owns W3 row tiles [r*T, (r+1)*T) of the 49 64-row tiles (T = ceil(49/size)); it
         # computes dW3 for those rows only (over every rank's samples, so the result is the exact
@@ -401,7 +415,7 @@ class FusedMNISTTrainer:
         # the CUs the conv roles leave idle, conv blocks joining as they finish — and
         # conv2_wgrad_reduce applies Adam to every other parameter as it produces the gradients.
         # Measured (B=100): 78.4 us/step vs 80.0 us with the flat adam_step launch.
-        self.fused_opt = not self.collectives and not self.f32
+        self.fused_opt = not self.collectives and not self.f32 and not self.f16
         self._side = torch.cuda.Stream(device=dev) if (self.collectives or self.f32) else None
         if compression == "bf16" and self.collectives:
             self.wire = torch.empty(FLAT_NUMEL, **bf)
@@ -438,7 +452,10 @@ class FusedMNISTTrainer:
     def _refresh_shadow(self):
         if self.shadow is None:  # fp32 step: the kernels read the fp32 parameters
             return
-        self.ops.scale_cast_bf16(self.params, self.shadow, 1.0)
+        if self.f16:
+            self.ops.scale_cast_f16(self.params, self.shadow, 1.0)
+        else:
+            self.ops.scale_cast_bf16(self.params, self.shadow, 1.0)
         if getattr(self, "shadow3", None) is not None:
             self.shadow3[:3136].copy_(self.pview("dense/kernel", self.shadow))
 
@@ -514,6 +531,8 @@ class FusedMNISTTrainer:
     def _launch_step_core(self, x, rows, labels):
         if self.f32:
             return self._launch_step_f32(x, rows, labels)
+        if self.f16:
+            return self._launch_step_f16(x, rows, labels)
         if self.gather:
             return self._launch_step_gather(x, rows, labels)
         o = self.ops
@@ -556,6 +575,45 @@ class FusedMNISTTrainer:
         main.wait_stream(self._side)
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
                     1.0 / self.world, self.rule, 1)
+
+    def _launch_step_f16(self, x, rows, labels):
+        """The Keras ``mixed_float16`` step (tensorflow_mnist_gpu.py:26-28,141-145): fp16 MFMA operands
+        (the fp16 build of the bf16 kernel set), fp32 master weights, Adam state and gradients, and
+        Keras LossScaleOptimizer's dynamic loss scaling entirely on the device, so the step replays
+        from a HIP graph like the others:
+
+            conv12 | fc1_fwd | head (dz and dlog times S = loss_scale[0]) | fc1_bwd | conv2_bwd |
+            wgrad reduce | [allreduce of the S-scaled gradients] | non-finite check -> loss_scale[1] |
+            Adam (skips itself on overflow, divides by S) | fp16 operand copy | scale update
+
+        Every gradient carries S (the head scales dlog too), so one check and one unscale cover
+        them all; a skipped update takes back the optimizer step the head advanced (update_scale_)."""
+        o, o16 = self.ops, self._o16
+        st = self.state
+        P, G, S = self.pview, self.gview, self.shadow
+        b1, b2 = self.betas
+        o16.conv12_fwd(x, rows, st, P("conv_layer1/conv2d/kernel", S), P("conv_layer1/conv2d/bias"),
+                       P("conv_layer2/conv2d/kernel", S), P("conv_layer2/conv2d/bias"), self.a1, self.idx1, self.a2,
+                       self.idx2)
+        o16.fc1_fwd(self.a2, P("dense/kernel", S), self.zpart)
+        o16.head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st, self.seed,
+                         self.dropout, self.h, self.dz, self.dlog, self.stats, -1, 1.0,
+                         self._stat_acc if self.track_stats else None, self.loss_scale)
+        o16.fc1_bwd(self.dz, self.a2, self.h, self.dlog, P("dense/kernel", S), G("dense/kernel"), G("dense/bias"),
+                    G("dense_1/kernel"), G("dense_1/bias"), self.g2)
+        o16.conv2_bwd(self.g2, self.idx2, self.a1, P("conv_layer2/conv2d/kernel", S), x, rows, st, self.idx1, self.slab,
+                      self.cpart)
+        o.conv2_wgrad_reduce(self.slab, self.cpart, self.B, G("conv_layer2/conv2d/kernel"),
+                             G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"), G("conv_layer2/conv2d/bias"))
+        if self.collectives:
+            # the S-scaled gradients: an overflow on any rank reaches every rank's sum, so every
+            # rank skips the same steps
+            self._allreduce(self.grads, 0, FLAT_NUMEL)
+        o.grad_check_([self.grads], self.loss_scale, False)
+        o.adam_step(self.params, self.grads, self.m, self.v, None, st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world,
+                    self.rule, 1, loss_scale=self.loss_scale)
+        o.scale_cast_f16(self.params, self.shadow, 1.0)
+        o.update_scale_(self.loss_scale, self._ls_tracker, 2.0, 0.5, self.ls_growth_interval, 1.0, state=st)
 
     def _launch_step_f32(self, x, rows, labels):
         """Exact-fp32 step (csrc/kernels/f32_fwd.hip, f32_bwd.hip). At world size 1, seven launches on

@@ -124,3 +124,84 @@ def test_keras_mixed_float16_trains_on_f16_kernels(ops):
         first = first if first is not None else float(loss)
     assert float(loss) < 0.5 * first, (first, float(loss))
     assert all(torch.isfinite(p).all() for p in module.parameters())
+
+
+def test_fused_trainer_fp16_matches_the_autograd_path_and_replays(ops):
+    """FusedMNISTTrainer(precision="fp16"): the mixed_float16 step with the loss scaler on the device.
+    One eager step lands where the per-batch fp16 autograd path + TF1 Adam lands (same kernels, same
+    scale; only where the 1/S is applied differs), then 5 x 10-step graph replays train on."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.models.mnist import MNISTConvNet
+    from mihvd.ops.functional import fused_mnist_loss
+    from mihvd.optim import TFAdam
+
+    x, y = _batch(B=100, seed=4)
+    tr = FusedMNISTTrainer(batch_size=100, lr=1e-3, seed=1, dropout=0.0, device="cuda", precision="fp16")
+    assert tr.f16 and tr.shadow.dtype == torch.float16 and float(tr.loss_scale[0]) == 2.0 ** 15
+    ref = MNISTConvNet(impl="hip", seed=1).cuda()
+    ref.dropout_rate = 0.0
+    p0 = torch.cat([p.detach().reshape(-1).clone() for _, p in ref.ordered_parameters()])
+    opt = TFAdam(ref.parameters(), lr=1e-3)
+    loss = fused_mnist_loss(ref, x, y, training=True, precision="fp16", loss_scale=2.0 ** 15)
+    loss.backward()
+    opt.step()
+    out = tr.train_step(x, y)
+    assert abs(float(out["loss"]) - float(loss)) < 1e-3 * max(1.0, abs(float(loss)))
+    got = torch.cat([tr.pview(n).reshape(-1) for n, _ in ref.ordered_parameters()])
+    want = torch.cat([p.detach().reshape(-1) for _, p in ref.ordered_parameters()])
+    # one TF1-Adam step is ~ -lr * sign(g): only near-zero gradients (rounding-order differences of
+    # the two wgrad reductions) can move differently
+    assert rel_err(got - p0, want - p0) < 1e-2, rel_err(got - p0, want - p0)
+    assert int(tr.state[1]) == 1 and float(tr.loss_scale[1]) == 0.0
+    X = torch.rand(2000, 784, device="cuda", generator=torch.Generator(device="cuda").manual_seed(7))
+    Y = (X[:, :392].sum(1) > X[:, 392:].sum(1)).long() * 3  # a learnable two-class labelling
+    tr.set_device_dataset(X, Y)
+    assert tr.build_graph(steps_per_replay=10, warmup=1)
+    first = tr.last_loss()
+    for _ in range(5):
+        tr.run_graph()
+    last = tr.last_loss()
+    assert last == last and last < first, (first, last)
+    assert torch.isfinite(tr.params).all() and 2.0 ** 10 <= float(tr.loss_scale[0]) <= 2.0 ** 15
+
+
+def test_fused_trainer_fp16_skips_overflowing_steps_on_the_device(ops):
+    """An oversized loss scale overflows the fp16 backward: the step is skipped (parameters and Adam
+    slots untouched, the optimizer step taken back), the scale halves -- all inside the step's
+    launches, so a graph replay does the same -- and training then proceeds."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+
+    x, y = _batch(B=100, seed=5)
+    tr = FusedMNISTTrainer(batch_size=100, lr=1e-3, seed=2, device="cuda", precision="fp16")
+    tr.loss_scale[0] = 2.0 ** 60
+    p0, m0 = tr.params.clone(), tr.m.clone()
+    tr.train_step(x, y)
+    torch.cuda.synchronize()
+    assert torch.equal(tr.params, p0) and torch.equal(tr.m, m0)
+    assert float(tr.loss_scale[0]) == 2.0 ** 59 and float(tr.loss_scale[1]) == 0.0
+    assert int(tr.state[1]) == 0 and int(tr.state[0]) == 1  # no optimizer step; the forward step advanced
+    tr.loss_scale[0] = 2.0 ** 15
+    tr.train_step(x, y)
+    torch.cuda.synchronize()
+    assert not torch.equal(tr.params, p0) and int(tr.state[1]) == 1
+
+
+def test_keras_mixed_float16_fit_is_graph_replayed(ops):
+    """hvd.Model.fit under mixed_float16 drives the fused fp16 trainer (no per-batch autograd node):
+    the loss falls over the epochs and the device loss scale comes back into the model's scaler."""
+    import mihvd.keras as K
+    from mihvd.models.mnist import MNISTConvNet
+    from mihvd.optim import TFAdam
+
+    module = MNISTConvNet(impl="hip", seed=1).cuda()
+    m = K.Model(module, policy="mixed_float16")
+    m.compile(TFAdam(module.parameters(), lr=1e-3), torch.nn.functional.cross_entropy)
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(3000, 784, generator=g)
+    y = (x[:, :392].sum(1) > x[:, 392:].sum(1)).long() * 7
+    m.fit(x.numpy(), y.numpy(), batch_size=100, epochs=3, verbose=0)
+    assert getattr(m, "fused_trainer", None) is not None and m.fused_trainer.f16
+    assert m.history["loss"][-1] < m.history["loss"][0], m.history
+    import math
+
+    assert math.isfinite(float(m._scaler.scale)) and float(m._scaler.scale) >= 1.0

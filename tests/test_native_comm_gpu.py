@@ -121,7 +121,8 @@ def test_bucket_plane_carries_distributed_optimizer(tmp_path):
     # the public API outside DistributedOptimizer goes through the same plane (a launch per call)
     assert all(r["api"].values()), r["api"]
     c = r["api_counts"]
-    assert c.get("allreduce", 0) >= 3 and c.get("broadcast", 0) >= 2 and c.get("allgather", 0) >= 2, c
+    # (broadcast_parameters is a no-op at world size 1: only hvd.broadcast counts here)
+    assert c.get("allreduce", 0) >= 3 and c.get("broadcast", 0) >= 1 and c.get("allgather", 0) >= 2, c
     assert c.get("reducescatter", 0) >= 1 and c.get("alltoall", 0) >= 2, c
     # after an elastic reset the optimizer's buckets run on the new world's plane
     e = r["elastic"]
