@@ -203,30 +203,25 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     }
   };
   float* buf0 = smf + wave * 2 * F1R_LDS_BUF;
-  // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch). Only the
-  // last K step can reach past the batch (KS = ceil(B / 4) or the padded 4 G, and B > 16 (G - 1)):
-  // the others load unmasked, without the clamp and select
+  // the wgrad B operand for the whole kernel: a2[4 s + lg][f0 + lr] (zero past the batch)
   float a2r[KS];
   auto load_a2r = [&]() {
     if constexpr (WG) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int b = 4 * s + lg;
-        if (4 * s + 3 < 16 * (G - 1)) a2r[s] = a2[(int64_t)b * 3136 + f0 + lr];
-        else a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
+        a2r[s] = mask_f(a2[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
       }
     }
   };
   // dz staging: chunk c = dz[0 .. 16 G)[nb + 16 c .. + 16): lane -> row (lane >> 2) + 16 it, float4 (lane & 3)
-  // (rows of the first G - 1 tiles are inside the batch: G = ceil(B / 16); only the last is masked)
   float4 zst[G];
   auto load_z = [&](int c) {
     const int n = nb + 16 * c + 4 * (lane & 3);
 #pragma unroll
     for (int it = 0; it < G; ++it) {
       const int b = (lane >> 2) + 16 * it;
-      if (it + 1 < G) zst[it] = *reinterpret_cast<const float4*>(dz + (int64_t)b * 1024 + n);
-      else zst[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)min(b, B - 1) * 1024 + n), b < B);
+      zst[it] = mask_f4(*reinterpret_cast<const float4*>(dz + (int64_t)min(b, B - 1) * 1024 + n), b < B);
     }
   };
   // dz rows in LDS with the 16-byte chunks of rows 8..15 (mod 16) XOR-swizzled by 2: the dgrad's

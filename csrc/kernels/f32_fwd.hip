@@ -313,6 +313,135 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
 }
 
 // ------------------------------------------------------------------------------------------ //
+// conv2 forward, split-bf16 products (f32_common.h "x9"): the same tiles, block shape and epilogue
+// as f32_conv2_fwd8_kernel, but every 32-channel tap is one 32-deep k chunk of nine
+// v_mfma_f32_16x16x32_bf16 (144 cycles) instead of eight 16x16x4 f32 MFMAs per 16 channels (256).
+// The two waves of a SIMD split the taps (0..12 | 13..24) instead of the channels; the image is
+// split into its three bf16 planes while it is staged ([plane][tall row][col][32 channels], 64 B per
+// pixel and plane, the 16-byte chunk g of a pixel at chunk g ^ x9_swz: a ds_read_b128 group of 16
+// lanes then covers 16 distinct bank slots in most tiles, 1.34 LDS cycles per group at B = 100 by
+// the bank model); the W2 operand of a tap (8 channels per lane) is read from the forward fragment
+// copy and split in registers one tap ahead, and the loop is tap-outer, tile-inner, so a wave holds
+// one tap's fragment and every tile's accumulator.
+constexpr int X9F_PS = 16;                              // dwords per pixel and plane
+constexpr int X9F_PLANE = C2F_MAXR * 18 * X9F_PS;       // dwords per plane
+constexpr int X9F_IMG = 3 * X9F_PLANE * 4;              // 76,032 B
+constexpr int X9F_LDS = X9F_IMG + 4 * 7 * 64 * 16;      // + the ci-half exchange of the fp32 form
+__device__ __forceinline__ int x9f_swz(int r, int x) { return (((x >> 1) + (r >> 1)) & 1) << 1; }
+
+template <int TPB>
+__global__ void __launch_bounds__(512) f32x9_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2f,
+                                                              const float* __restrict__ b2, float* __restrict__ a2,
+                                                              uint8_t* __restrict__ idx2, int B) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  uint32_t* img = reinterpret_cast<uint32_t*>(smf);
+  f32x4* xr = reinterpret_cast<f32x4*>(smf + X9F_IMG / 4);
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, g = lane >> 4;
+  const int wco = wave & 3, kh2 = wave >> 2;  // co group, tap half
+  const int tap0 = kh2 ? 13 : 0, ntap = kh2 ? 12 : 13;
+  const int nblk = (((49 * B + 3) / 4) + TPB - 1) / TPB;
+  const int nwin = 49 * B, T0 = xcd_contiguous((int)blockIdx.x, 0, nblk) * TPB;
+  const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
+  const int b0 = gw0 / 49, b1i = gw1 / 49;
+  const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
+  const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
+  const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
+  // W2 operand of a tap: W2[tap][8 g + j][16 wco + lr], j < 8 = two float4 of the fragment copy
+  // fwd [tap][c2][wave][lane][j] = W2[tap][16 c2 + 4 lg + j][16 wave + lr]  (c2 = g >> 1, lg = 2 (g & 1) + h)
+  const float4* wf = reinterpret_cast<const float4*>(w2f) + ((g >> 1) * 4 + wco) * 64 + lr + 32 * (g & 1);
+  float4 wraw[2] = {wf[tap0 * 512], wf[tap0 * 512 + 16]};
+  // stage: a1 chunk (pixel, 4 channels) -> its 4 bf16 in each plane
+  {
+    float4 iv[C2F8_MAXCH];
+#pragma unroll
+    for (int it = 0; it < C2F8_MAXCH; ++it) {
+      const int i = min(t + 512 * it, nch - 1);
+      const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, ch = rem & 7;
+      const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
+      const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+      const float4 v = *reinterpret_cast<const float4*>(
+          a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
+      iv[it] = mask_f4(v, in);
+    }
+#pragma unroll
+    for (int it = 0; it < C2F8_MAXCH; ++it) {
+      const int i = t + 512 * it;
+      if (i < nch) {
+        const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, q = rem & 7;
+        const int o = (rr * 18 + c) * X9F_PS + 4 * ((q >> 1) ^ x9f_swz(rr, c)) + 2 * (q & 1);
+        uint2 h, m, l;
+        x9_split4(iv[it], h, m, l);
+        *reinterpret_cast<uint2*>(img + o) = h;
+        *reinterpret_cast<uint2*>(img + X9F_PLANE + o) = m;
+        *reinterpret_cast<uint2*>(img + 2 * X9F_PLANE + o) = l;
+      }
+    }
+  }
+  // this lane's pixel (tall row, column) of every tile, before the tap offset
+  int pr[TPB], px[TPB];
+#pragma unroll
+  for (int u = 0; u < TPB; ++u) {
+    const int m = 16 * (T0 + u) + lr;
+    const int gw = min(m >> 2, nwin - 1), d = m & 3;
+    const int bb = gw / 49, win = gw - 49 * bb, py = win / 7, pxw = win - 7 * py;
+    pr[u] = 18 * bb + 2 * py + (d >> 1) - R0;
+    px[u] = 2 * pxw + (d & 1);
+  }
+  f32x4 acc[TPB];
+#pragma unroll
+  for (int u = 0; u < TPB; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // the image is complete; no barrier below until the exchange
+  auto load_a = [&](int u, int kh, int kw) {
+    const int r = pr[u] + kh, x = px[u] + kw;
+    const uint32_t* p = img + (r * 18 + x) * X9F_PS + 4 * (g ^ x9f_swz(r, x));
+    X9Frag f;
+    f.p[0] = *reinterpret_cast<const bf16x8*>(p);
+    f.p[1] = *reinterpret_cast<const bf16x8*>(p + X9F_PLANE);
+    f.p[2] = *reinterpret_cast<const bf16x8*>(p + 2 * X9F_PLANE);
+    return f;
+  };
+  for (int s = 0; s < ntap; ++s) {  // wave-uniform
+    const int tap = tap0 + s, kh = tap / 5, kw = tap - 5 * kh;
+    const X9Frag wb = x9_split8(wraw[0], wraw[1]);
+    if (s + 1 < ntap) {
+      wraw[0] = wf[(tap + 1) * 512];
+      wraw[1] = wf[(tap + 1) * 512 + 16];
+    }
+    X9Frag fa = load_a(0, kh, kw);
+#pragma unroll
+    for (int u = 0; u < TPB; ++u) {
+      X9Frag fn;
+      if (u + 1 < TPB) fn = load_a(u + 1, kh, kw);
+      acc[u] = x9_mma(fa, wb, acc[u]);
+      if (u + 1 < TPB) fa = fn;
+    }
+  }
+  // exchange: tile u is finished by tap half (u >= H): the other half hands over its partial
+  constexpr int H = (TPB + 1) / 2;
+#pragma unroll
+  for (int u = 0; u < TPB; ++u)
+    if ((u >= H) != (kh2 == 1)) xr[(wco * 7 + u) * 64 + lane] = acc[u];
+  __syncthreads();
+  const int co = 16 * wco + lr;
+  const float bias = b2[co];
+#pragma unroll
+  for (int u = 0; u < TPB; ++u) {
+    if ((u >= H) != (kh2 == 1)) continue;
+    const f32x4 o = xr[(wco * 7 + u) * 64 + lane];
+    const f32x4 sum = kh2 == 0 ? acc[u] + o : o + acc[u];  // half 0 + half 1 either way
+    const int gw = 4 * (T0 + u) + g;
+    if (gw < nwin) {
+      const int bb = gw / 49, win = gw - 49 * bb;
+      int best;
+      const float m = pool4(sum, best);
+      const int64_t oo = (int64_t)bb * 3136 + win * 64 + co;
+      a2[oo] = fmaxf(m + bias, 0.f);
+      idx2[oo] = (uint8_t)best;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ //
 // fc1 forward: zpart[ks][b][n] = sum_{k in slice ks} a2[b][k] W3[k][n]   (14 slices of 224)
 // grid (16, 14): 64 columns x one K slice per block, 8 waves: wave w = 16 columns (w & 3) x every
 // other 16-sample tile (w >> 2). The transposed product puts features on the MFMA row axis: A =
@@ -520,6 +649,25 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
 // ------------------------------------------------------------------------------------------ //
 // host wrappers
 // ------------------------------------------------------------------------------------------ //
+// Product form of the fp32 step's GEMM-shaped kernels: 0 = fp32-input MFMAs, 1 = split-bf16 (x9).
+// Initial value from MIHVD_F32_PRODUCTS ("native" | "split"); f32_products(mode) sets it (mode < 0:
+// query). The kernels read it at launch, so a captured graph keeps the form it was captured with.
+static int g_f32_products = -1;
+bool f32_split_products() {
+  if (g_f32_products < 0) {
+    const char* e = std::getenv("MIHVD_F32_PRODUCTS");
+    g_f32_products = (e != nullptr && std::string(e) == "split") ? 1 : 0;
+  }
+  return g_f32_products == 1;
+}
+int64_t f32_products(int64_t mode) {
+  if (mode >= 0) {
+    TORCH_CHECK(mode <= 1, "f32_products: 0 (fp32-input MFMA) or 1 (split-bf16)");
+    g_f32_products = (int)mode;
+  }
+  return f32_split_products() ? 1 : 0;
+}
+
 static void check_f32(const at::Tensor& t, int64_t numel, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.dtype() == at::kFloat && t.is_contiguous() && t.numel() == numel, what,
               ": expected a contiguous fp32 device tensor of ", numel, " elements");
@@ -599,6 +747,23 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
     TORCH_CHECK(r1 - r0 <= C2F_MAXR, "f32_conv2_fwd: row span exceeds the LDS image");
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
+  if (w2f != nullptr && f32_split_products()) {
+    auto launch = [&](auto kern) {
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, X9F_LDS);
+      kern<<<nblk, 512, X9F_LDS, stream>>>(a1.data_ptr<float>(), w2f, b2.data_ptr<float>(), a2.data_ptr<float>(),
+                                           idx2.data_ptr<uint8_t>(), B);
+    };
+    switch (tpb) {
+      case 1: launch(f32x9_conv2_fwd_kernel<1>); break;
+      case 2: launch(f32x9_conv2_fwd_kernel<2>); break;
+      case 3: launch(f32x9_conv2_fwd_kernel<3>); break;
+      case 4: launch(f32x9_conv2_fwd_kernel<4>); break;
+      case 5: launch(f32x9_conv2_fwd_kernel<5>); break;
+      case 6: launch(f32x9_conv2_fwd_kernel<6>); break;
+      default: launch(f32x9_conv2_fwd_kernel<7>); break;
+    }
+    return;
+  }
   // When the grid fits the CUs, request more LDS than the block needs (> half a CU's) so no two
   // blocks share a CU: the dispatcher otherwise doubles blocks up on some CUs while others idle
   // (measured 20.6 -> 19.7 us at B = 100).

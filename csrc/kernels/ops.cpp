@@ -113,6 +113,7 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
                      int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo, int64_t fc_hi, double lr, double b1,
                      double b2, double eps, double grad_scale, int64_t rule);
 int64_t f32_db2_rows(int64_t B);
+int64_t f32_products(int64_t mode);
 at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel);
 int64_t f32_wgrad_groups(int64_t B);
 int64_t f32_dgrad_blocks(int64_t B);
@@ -408,6 +409,7 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(s!)? state=None, int o_w1=0, int o_b1=0, int o_w2=0, int o_b2=0, int fc_lo=0, int fc_hi=0, "
         "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0) -> ()");
   m.def("f32_db2_rows(int B) -> int", &mihvd::f32_db2_rows);
+  m.def("f32_products(int mode=-1) -> int", &mihvd::f32_products);
   m.def("f32_stamps_enable(int n_blocks, int kernel=0) -> Tensor", &mihvd::f32_stamps_enable);
   m.def("f32_wgrad_groups(int B) -> int", &mihvd::f32_wgrad_groups);
   m.def("f32_dgrad_blocks(int B) -> int", &mihvd::f32_dgrad_blocks);
