@@ -423,6 +423,12 @@ def main():
                        "final_loss": loss_val},
         }
         rec["config"].update(rccl)
+        if args.impl == "fused" and getattr(tr, "f32", False):
+            k = tr.f32_products
+            rec["config"]["fp32_products"] = (
+                "fp32-input MFMA (v_mfma_f32_16x16x4_f32)" if k == 0 else
+                f"fp32 operands split exactly into 3 bf16 parts, {k} part products on bf16 MFMA, fp32 accumulation "
+                f"({'exact products' if k == 9 else 'dropped terms < 2^-24 relative'}) in conv2_fwd; fp32-input MFMA elsewhere")
         if args.impl == "fused" and tr.collectives:
             rec["config"]["data_plane"] = tr.plane_report
         print(json.dumps(rec), flush=True)

@@ -219,43 +219,45 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
 }
 
 // ------------------------------------------------------------------------------------------ //
-// Split-bf16 fp32 products ("x9"). An fp32 value is the EXACT sum of three bf16 parts by truncation:
-//   hi = x with the low 16 bits cleared; r = x - hi (exact: same binade, |r| < ulp_bf16(x));
-//   mid = r truncated the same way; lo = r - mid, which has at most 8 significant bits (x carries
-//   24), so it IS a bf16 value.
-// bf16 x bf16 products are exact in fp32, so the nine part products of a * b sum to a * b exactly
-// and a 16x16x32 bf16 MFMA chain over the nine (a_i, b_j) plane pairs computes the fp32 dot
-// product with exact products and fp32 accumulation -- the contract of v_mfma_f32_16x16x4_f32 --
-// in 9 x 16 = 144 MFMA cycles per 32-deep k chunk instead of 8 x 32 = 256 (only the summation
-// order differs). Parts are accumulated smallest first.
+// Split-bf16 fp32 products. An fp32 value is the EXACT sum of three bf16 parts by round-to-nearest
+// (v_cvt_pk_bf16_f32): hi = bf16(x); r = x - hi (exact: |r| <= half a bf16 ulp of x, on x's ulp
+// grid: <= 16 significant bits); mid = bf16(r); lo = r - mid, which has at most 8 significant bits,
+// so it IS a bf16 value (|mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|). bf16 x bf16 products are exact in
+// fp32, and a 16x16x32 bf16 MFMA chain over the part pairs accumulates in fp32:
+//   NPROD = 9: all nine pairs -- every product a * b exact, only the fp32 summation order differs
+//              from v_mfma_f32_16x16x4_f32 (144 MFMA cycles per 32-deep k chunk instead of 256);
+//   NPROD = 6: the pairs down to 2^-16 relative -- the dropped mid*lo, lo*mid, lo*lo are below
+//              2^-24 |a b| together (fp32's own rounding unit) and zero-mean under round-to-nearest
+//              (96 cycles per chunk: 2.7x the fp32-input MFMA rate).
+// Pairs are accumulated smallest first.
 // ------------------------------------------------------------------------------------------ //
-// Host: which product form the fp32 kernels launch (f32_products in f32_fwd.hip; 1 = split-bf16).
-bool f32_split_products();
-
 struct X9Frag {
   bf16x8 p[3];  // hi, mid, lo: 8 consecutive k per lane each
 };
 
-__device__ __forceinline__ void x9_split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
-  h = __float_as_uint(x) & 0xffff0000u;
-  const float r1 = x - __uint_as_float(h);
-  m = __float_as_uint(r1) & 0xffff0000u;
-  l = __float_as_uint(r1 - __uint_as_float(m)) & 0xffff0000u;
+__device__ __forceinline__ void x9_split1(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
 }
 
-// the high halves of a (low 16 bits of the result) and b (high 16 bits)
-__device__ __forceinline__ uint32_t x9_pk(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
-
-// 4 consecutive-k values -> two dwords of each plane
+// 4 consecutive-k values -> two dwords (4 bf16) of each plane
 __device__ __forceinline__ void x9_split4(const float4& v, uint2& h, uint2& m, uint2& l) {
-  uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
-  x9_split1(v.x, h0, m0, l0);
-  x9_split1(v.y, h1, m1, l1);
-  x9_split1(v.z, h2, m2, l2);
-  x9_split1(v.w, h3, m3, l3);
-  h = make_uint2(x9_pk(h0, h1), x9_pk(h2, h3));
-  m = make_uint2(x9_pk(m0, m1), x9_pk(m2, m3));
-  l = make_uint2(x9_pk(l0, l1), x9_pk(l2, l3));
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  bf16x4_t hv, mv, lv;
+  const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    __bf16 a, b, c;
+    x9_split1(e[j], a, b, c);
+    hv[j] = a;
+    mv[j] = b;
+    lv[j] = c;
+  }
+  h = __builtin_bit_cast(uint2, hv);
+  m = __builtin_bit_cast(uint2, mv);
+  l = __builtin_bit_cast(uint2, lv);
 }
 
 // 8 consecutive-k values (two float4) -> a fragment of each plane
@@ -270,14 +272,18 @@ __device__ __forceinline__ X9Frag x9_split8(const float4& a, const float4& b) {
   return f;
 }
 
-// c += A . B over one 32-deep k chunk with exact products: the nine plane pairs, smallest first
+// c += A . B over one 32-deep k chunk: the part pairs, smallest first
+template <int NPROD>
 __device__ __forceinline__ f32x4 x9_mma(const X9Frag& a, const X9Frag& b, f32x4 c) {
-  c = mfma16(a.p[2], b.p[2], c);
-  c = mfma16(a.p[2], b.p[1], c);
-  c = mfma16(a.p[1], b.p[2], c);
+  static_assert(NPROD == 6 || NPROD == 9, "6 or 9 part products");
+  if constexpr (NPROD == 9) {
+    c = mfma16(a.p[2], b.p[2], c);
+    c = mfma16(a.p[2], b.p[1], c);
+    c = mfma16(a.p[1], b.p[2], c);
+  }
   c = mfma16(a.p[2], b.p[0], c);
-  c = mfma16(a.p[1], b.p[1], c);
   c = mfma16(a.p[0], b.p[2], c);
+  c = mfma16(a.p[1], b.p[1], c);
   c = mfma16(a.p[1], b.p[0], c);
   c = mfma16(a.p[0], b.p[1], c);
   return mfma16(a.p[0], b.p[0], c);

@@ -313,32 +313,34 @@ __global__ void __launch_bounds__(512) f32_conv2_fwd8_kernel(const float* __rest
 }
 
 // ------------------------------------------------------------------------------------------ //
-// conv2 forward, split-bf16 products (f32_common.h "x9"): the same tiles, block shape and epilogue
-// as f32_conv2_fwd8_kernel, but every 32-channel tap is one 32-deep k chunk of nine
-// v_mfma_f32_16x16x32_bf16 (144 cycles) instead of eight 16x16x4 f32 MFMAs per 16 channels (256).
-// The two waves of a SIMD split the taps (0..12 | 13..24) instead of the channels; the image is
-// split into its three bf16 planes while it is staged ([plane][tall row][col][32 channels], 64 B per
-// pixel and plane, the 16-byte chunk g of a pixel at chunk g ^ x9_swz: a ds_read_b128 group of 16
-// lanes then covers 16 distinct bank slots in most tiles, 1.34 LDS cycles per group at B = 100 by
-// the bank model); the W2 operand of a tap (8 channels per lane) is read from the forward fragment
-// copy and split in registers one tap ahead, and the loop is tap-outer, tile-inner, so a wave holds
-// one tap's fragment and every tile's accumulator.
+// conv2 forward, split-bf16 products (f32_common.h: NPROD part products per 32-deep k chunk on
+// v_mfma_f32_16x16x32_bf16). Same tiles, blocks and epilogue as f32_conv2_fwd8_kernel; the k chunk is
+// one tap's 32 channels. 8 waves = co half (w & 1: co groups 2 ch, 2 ch + 1, 16 channels each) x tap
+// quarter (w >> 1: taps 0-6 | 7-12 | 13-18 | 19-24; the two waves of a SIMD, w and w + 4, hold
+// quarters q and q + 2: 13 or 12 taps per SIMD). Every A fragment read from LDS feeds both co groups
+// (2 NPROD MFMAs per 3 ds_read_b128). The image is split into its three bf16 planes while it is
+// staged ([plane][tall row][col][32 channels]: 64 B per pixel and plane, 16-byte chunk g of a pixel
+// at chunk g ^ x9f_swz); the W2 operand of a tap is read from the forward fragment copy and split in
+// registers one tap ahead; the tap loop is tap-outer, tile-inner (one tap's fragments, every tile's
+// accumulators). The four quarter partials of a tile meet in LDS (over the dead image) and quarter
+// u % 4 finishes tile u, summing q0 + q1 + q2 + q3 in that order.
 constexpr int X9F_PS = 16;                              // dwords per pixel and plane
 constexpr int X9F_PLANE = C2F_MAXR * 18 * X9F_PS;       // dwords per plane
 constexpr int X9F_IMG = 3 * X9F_PLANE * 4;              // 76,032 B
-constexpr int X9F_LDS = X9F_IMG + 4 * 7 * 64 * 16;      // + the ci-half exchange of the fp32 form
+constexpr int x9f_lds(int tpb) {                       // the image, or the exchange if larger
+  return X9F_IMG > 4 * 2 * 2 * tpb * 64 * 16 ? X9F_IMG : 4 * 2 * 2 * tpb * 64 * 16;
+}
 __device__ __forceinline__ int x9f_swz(int r, int x) { return (((x >> 1) + (r >> 1)) & 1) << 1; }
 
-template <int TPB>
+template <int TPB, int NPROD>
 __global__ void __launch_bounds__(512) f32x9_conv2_fwd_kernel(const float* __restrict__ a1, const float* __restrict__ w2f,
                                                               const float* __restrict__ b2, float* __restrict__ a2,
                                                               uint8_t* __restrict__ idx2, int B) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   uint32_t* img = reinterpret_cast<uint32_t*>(smf);
-  f32x4* xr = reinterpret_cast<f32x4*>(smf + X9F_IMG / 4);
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, g = lane >> 4;
-  const int wco = wave & 3, kh2 = wave >> 2;  // co group, tap half
-  const int tap0 = kh2 ? 13 : 0, ntap = kh2 ? 12 : 13;
+  const int ch = wave & 1, q = wave >> 1;  // co half, tap quarter
+  const int tap0 = q == 0 ? 0 : 6 * q + 1, ntap = q == 0 ? 7 : 6;
   const int nblk = (((49 * B + 3) / 4) + TPB - 1) / TPB;
   const int nwin = 49 * B, T0 = xcd_contiguous((int)blockIdx.x, 0, nblk) * TPB;
   const int gw0 = 4 * T0, gw1 = min(4 * (T0 + TPB), nwin) - 1;
@@ -346,29 +348,38 @@ __global__ void __launch_bounds__(512) f32x9_conv2_fwd_kernel(const float* __res
   const int R0 = 18 * b0 + 2 * ((gw0 - 49 * b0) / 7);
   const int R1 = 18 * b1i + 2 * ((gw1 - 49 * b1i) / 7) + 6;
   const int nch = (R1 - R0) * 144;  // 18 pixels x 8 float4 per tall row
-  // W2 operand of a tap: W2[tap][8 g + j][16 wco + lr], j < 8 = two float4 of the fragment copy
-  // fwd [tap][c2][wave][lane][j] = W2[tap][16 c2 + 4 lg + j][16 wave + lr]  (c2 = g >> 1, lg = 2 (g & 1) + h)
-  const float4* wf = reinterpret_cast<const float4*>(w2f) + ((g >> 1) * 4 + wco) * 64 + lr + 32 * (g & 1);
-  float4 wraw[2] = {wf[tap0 * 512], wf[tap0 * 512 + 16]};
+  // W2 operand of a tap and co group cg: W2[tap][8 g + j][16 cg + lr], j < 8 = two float4 of the
+  // fragment copy fwd [tap][c2][cg][lane][j] = W2[tap][16 c2 + 4 lg + j][16 cg + lr]
+  // (c2 = g >> 1, lg = 2 (g & 1) + h)
+  const float4* wf = reinterpret_cast<const float4*>(w2f) + ((g >> 1) * 4 + 2 * ch) * 64 + lr + 32 * (g & 1);
+  float4 wraw[2][2];
+  auto load_w = [&](int tap) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      wraw[c][0] = wf[tap * 512 + 64 * c];
+      wraw[c][1] = wf[tap * 512 + 64 * c + 16];
+    }
+  };
+  load_w(tap0);
   // stage: a1 chunk (pixel, 4 channels) -> its 4 bf16 in each plane
   {
     float4 iv[C2F8_MAXCH];
 #pragma unroll
     for (int it = 0; it < C2F8_MAXCH; ++it) {
       const int i = min(t + 512 * it, nch - 1);
-      const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, ch = rem & 7;
+      const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, chn = rem & 7;
       const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
       const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
       const float4 v = *reinterpret_cast<const float4*>(
-          a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + ch * 4);
+          a1 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 32 + chn * 4);
       iv[it] = mask_f4(v, in);
     }
 #pragma unroll
     for (int it = 0; it < C2F8_MAXCH; ++it) {
       const int i = t + 512 * it;
       if (i < nch) {
-        const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, q = rem & 7;
-        const int o = (rr * 18 + c) * X9F_PS + 4 * ((q >> 1) ^ x9f_swz(rr, c)) + 2 * (q & 1);
+        const int rr = i / 144, rem = i - rr * 144, c = rem >> 3, qc = rem & 7;
+        const int o = (rr * 18 + c) * X9F_PS + 4 * ((qc >> 1) ^ x9f_swz(rr, c)) + 2 * (qc & 1);
         uint2 h, m, l;
         x9_split4(iv[it], h, m, l);
         *reinterpret_cast<uint2*>(img + o) = h;
@@ -387,10 +398,12 @@ __global__ void __launch_bounds__(512) f32x9_conv2_fwd_kernel(const float* __res
     pr[u] = 18 * bb + 2 * py + (d >> 1) - R0;
     px[u] = 2 * pxw + (d & 1);
   }
-  f32x4 acc[TPB];
+  f32x4 acc[2][TPB];
 #pragma unroll
-  for (int u = 0; u < TPB; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();  // the image is complete; no barrier below until the exchange
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int u = 0; u < TPB; ++u) acc[c][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // the image is complete
   auto load_a = [&](int u, int kh, int kw) {
     const int r = pr[u] + kh, x = px[u] + kw;
     const uint32_t* p = img + (r * 18 + x) * X9F_PS + 4 * (g ^ x9f_swz(r, x));
@@ -402,41 +415,46 @@ __global__ void __launch_bounds__(512) f32x9_conv2_fwd_kernel(const float* __res
   };
   for (int s = 0; s < ntap; ++s) {  // wave-uniform
     const int tap = tap0 + s, kh = tap / 5, kw = tap - 5 * kh;
-    const X9Frag wb = x9_split8(wraw[0], wraw[1]);
-    if (s + 1 < ntap) {
-      wraw[0] = wf[(tap + 1) * 512];
-      wraw[1] = wf[(tap + 1) * 512 + 16];
-    }
+    const X9Frag wb0 = x9_split8(wraw[0][0], wraw[0][1]);
+    const X9Frag wb1 = x9_split8(wraw[1][0], wraw[1][1]);
+    if (s + 1 < ntap) load_w(tap + 1);
     X9Frag fa = load_a(0, kh, kw);
 #pragma unroll
     for (int u = 0; u < TPB; ++u) {
       X9Frag fn;
       if (u + 1 < TPB) fn = load_a(u + 1, kh, kw);
-      acc[u] = x9_mma(fa, wb, acc[u]);
+      acc[0][u] = x9_mma<NPROD>(fa, wb0, acc[0][u]);
+      acc[1][u] = x9_mma<NPROD>(fa, wb1, acc[1][u]);
       if (u + 1 < TPB) fa = fn;
     }
   }
-  // exchange: tile u is finished by tap half (u >= H): the other half hands over its partial
-  constexpr int H = (TPB + 1) / 2;
+  // exchange over the dead image: xr[co half][tile][quarter][co group][lane]
+  __syncthreads();
+  f32x4* xr = reinterpret_cast<f32x4*>(smf);
 #pragma unroll
   for (int u = 0; u < TPB; ++u)
-    if ((u >= H) != (kh2 == 1)) xr[(wco * 7 + u) * 64 + lane] = acc[u];
+    if ((u & 3) != q)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) xr[(((ch * TPB + u) * 4 + q) * 2 + c) * 64 + lane] = acc[c][u];
   __syncthreads();
-  const int co = 16 * wco + lr;
-  const float bias = b2[co];
 #pragma unroll
   for (int u = 0; u < TPB; ++u) {
-    if ((u >= H) != (kh2 == 1)) continue;
-    const f32x4 o = xr[(wco * 7 + u) * 64 + lane];
-    const f32x4 sum = kh2 == 0 ? acc[u] + o : o + acc[u];  // half 0 + half 1 either way
+    if ((u & 3) != q) continue;
     const int gw = 4 * (T0 + u) + g;
-    if (gw < nwin) {
-      const int bb = gw / 49, win = gw - 49 * bb;
-      int best;
-      const float m = pool4(sum, best);
-      const int64_t oo = (int64_t)bb * 3136 + win * 64 + co;
-      a2[oo] = fmaxf(m + bias, 0.f);
-      idx2[oo] = (uint8_t)best;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 sum = q == 0 ? acc[c][u] : xr[(((ch * TPB + u) * 4 + 0) * 2 + c) * 64 + lane];
+#pragma unroll
+      for (int qq = 1; qq < 4; ++qq) sum += qq == q ? acc[c][u] : xr[(((ch * TPB + u) * 4 + qq) * 2 + c) * 64 + lane];
+      const int co = 16 * (2 * ch + c) + lr;
+      if (gw < nwin) {
+        const int bb = gw / 49, win = gw - 49 * bb;
+        int best;
+        const float m = pool4(sum, best);
+        const int64_t oo = (int64_t)bb * 3136 + win * 64 + co;
+        a2[oo] = fmaxf(m + b2[co], 0.f);
+        idx2[oo] = (uint8_t)best;
+      }
     }
   }
 }
@@ -649,25 +667,6 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
 // ------------------------------------------------------------------------------------------ //
 // host wrappers
 // ------------------------------------------------------------------------------------------ //
-// Product form of the fp32 step's GEMM-shaped kernels: 0 = fp32-input MFMAs, 1 = split-bf16 (x9).
-// Initial value from MIHVD_F32_PRODUCTS ("native" | "split"); f32_products(mode) sets it (mode < 0:
-// query). The kernels read it at launch, so a captured graph keeps the form it was captured with.
-static int g_f32_products = -1;
-bool f32_split_products() {
-  if (g_f32_products < 0) {
-    const char* e = std::getenv("MIHVD_F32_PRODUCTS");
-    g_f32_products = (e != nullptr && std::string(e) == "split") ? 1 : 0;
-  }
-  return g_f32_products == 1;
-}
-int64_t f32_products(int64_t mode) {
-  if (mode >= 0) {
-    TORCH_CHECK(mode <= 1, "f32_products: 0 (fp32-input MFMA) or 1 (split-bf16)");
-    g_f32_products = (int)mode;
-  }
-  return f32_split_products() ? 1 : 0;
-}
-
 static void check_f32(const at::Tensor& t, int64_t numel, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.dtype() == at::kFloat && t.is_contiguous() && t.numel() == numel, what,
               ": expected a contiguous fp32 device tensor of ", numel, " elements");
@@ -723,8 +722,10 @@ static int conv2f_tpb(int B) {
   return std::min(7, std::max(1, (nt + 255) / 256));
 }
 
+// products: 0 = fp32-input MFMAs; 6 / 9 = split-bf16 part products (f32_common.h; needs w2frag)
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
-                   const c10::optional<at::Tensor>& w2frag) {
+                   const c10::optional<at::Tensor>& w2frag, int64_t products) {
+  TORCH_CHECK(products == 0 || products == 6 || products == 9, "f32_conv2_fwd: products 0, 6 or 9");
   const float* w2f = nullptr;
   if (w2frag.has_value() && w2frag->defined()) {
     TORCH_CHECK(w2frag->is_cuda() && w2frag->dtype() == at::kFloat && w2frag->is_contiguous() &&
@@ -747,21 +748,30 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
     TORCH_CHECK(r1 - r0 <= C2F_MAXR, "f32_conv2_fwd: row span exceeds the LDS image");
   }
   auto stream = c10::hip::getCurrentHIPStream().stream();
-  if (w2f != nullptr && f32_split_products()) {
-    auto launch = [&](auto kern) {
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, X9F_LDS);
-      kern<<<nblk, 512, X9F_LDS, stream>>>(a1.data_ptr<float>(), w2f, b2.data_ptr<float>(), a2.data_ptr<float>(),
-                                           idx2.data_ptr<uint8_t>(), B);
+  if (products != 0) {
+    TORCH_CHECK(w2f != nullptr, "f32_conv2_fwd: split-bf16 products read the W2 fragment copy (w2frag)");
+    auto launch = [&](auto kern, int lds) {
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      kern<<<nblk, 512, lds, stream>>>(a1.data_ptr<float>(), w2f, b2.data_ptr<float>(), a2.data_ptr<float>(),
+                                       idx2.data_ptr<uint8_t>(), B);
     };
+    const bool p9 = products == 9;
+#define X9F_CASE(T)                                                                          \
+  case T:                                                                                    \
+    if (p9) launch(f32x9_conv2_fwd_kernel<T, 9>, x9f_lds(T));                                \
+    else launch(f32x9_conv2_fwd_kernel<T, 6>, x9f_lds(T));                                   \
+    break;
     switch (tpb) {
-      case 1: launch(f32x9_conv2_fwd_kernel<1>); break;
-      case 2: launch(f32x9_conv2_fwd_kernel<2>); break;
-      case 3: launch(f32x9_conv2_fwd_kernel<3>); break;
-      case 4: launch(f32x9_conv2_fwd_kernel<4>); break;
-      case 5: launch(f32x9_conv2_fwd_kernel<5>); break;
-      case 6: launch(f32x9_conv2_fwd_kernel<6>); break;
-      default: launch(f32x9_conv2_fwd_kernel<7>); break;
+      X9F_CASE(1)
+      X9F_CASE(2)
+      X9F_CASE(3)
+      X9F_CASE(4)
+      X9F_CASE(5)
+      X9F_CASE(6)
+      default:
+        X9F_CASE(7)
     }
+#undef X9F_CASE
     return;
   }
   // When the grid fits the CUs, request more LDS than the block needs (> half a CU's) so no two

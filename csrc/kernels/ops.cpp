@@ -88,7 +88,7 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
                    const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll);
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
-                   const c10::optional<at::Tensor>& w2frag);
+                   const c10::optional<at::Tensor>& w2frag, int64_t products);
 void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
@@ -113,7 +113,6 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
                      int64_t o_b1, int64_t o_w2, int64_t o_b2, int64_t fc_lo, int64_t fc_hi, double lr, double b1,
                      double b2, double eps, double grad_scale, int64_t rule);
 int64_t f32_db2_rows(int64_t B);
-int64_t f32_products(int64_t mode);
 at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel);
 int64_t f32_wgrad_groups(int64_t B);
 int64_t f32_dgrad_blocks(int64_t B);
@@ -293,8 +292,9 @@ void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Te
                   Tensor idx1, const OptT& w2, const OptT& w2frag, int64_t coll) {
   mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag, coll);
 }
-void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& w2frag) {
-  mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, w2frag);
+void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& w2frag,
+                  int64_t products) {
+  mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, w2frag, products);
 }
 void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
@@ -390,7 +390,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("bump_step_(Tensor(a!) step) -> ()");
   m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
         "Tensor? w2=None, Tensor(f!)? w2frag=None, int coll=-1) -> ()");
-  m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None) -> ()");
+  m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None, int products=0) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
@@ -409,7 +409,6 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(s!)? state=None, int o_w1=0, int o_b1=0, int o_w2=0, int o_b2=0, int fc_lo=0, int fc_hi=0, "
         "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0) -> ()");
   m.def("f32_db2_rows(int B) -> int", &mihvd::f32_db2_rows);
-  m.def("f32_products(int mode=-1) -> int", &mihvd::f32_products);
   m.def("f32_stamps_enable(int n_blocks, int kernel=0) -> Tensor", &mihvd::f32_stamps_enable);
   m.def("f32_wgrad_groups(int B) -> int", &mihvd::f32_wgrad_groups);
   m.def("f32_dgrad_blocks(int B) -> int", &mihvd::f32_dgrad_blocks);

@@ -129,7 +129,8 @@ class FusedMNISTTrainer:
     def __init__(self, batch_size: int = 100, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  dropout: float = 0.5, seed: int = 0, device=None, compression: str = "none", op=None,
                  adam_rule: str = "tf", dropout_seed: int | None = None, world_size: int | None = None,
-                 shard_optimizer: bool | None = None, precision: str | None = None):
+                 shard_optimizer: bool | None = None, precision: str | None = None,
+                 f32_products: int | None = None):
         _native.require_kernels()
         from .. import basics
 
@@ -146,6 +147,16 @@ class FusedMNISTTrainer:
             raise ValueError("precision must be 'fp32', 'bf16' or 'fp16'")
         self.precision = precision
         self.f32 = precision == "fp32"
+        # How the fp32 step's GEMM-shaped kernels form their products (MIHVD_F32_PRODUCTS): 6 (default)
+        # or 9 = fp32 operands split exactly into three bf16 parts, the 6 / 9 part products on the bf16
+        # MFMAs with fp32 accumulation (csrc/kernels/f32_common.h: products exact (9) or within fp32's
+        # rounding unit (6); measured closer to a float64 reference than the fp32-input MFMA path,
+        # tests/test_f32_split_gpu.py); 0 = the fp32-input MFMAs (v_mfma_f32_16x16x4_f32).
+        if f32_products is None:
+            f32_products = int(os.environ.get("MIHVD_F32_PRODUCTS", "6"))
+        if int(f32_products) not in (0, 6, 9):
+            raise ValueError("f32_products must be 0 (fp32-input MFMA), 6 or 9 (split-bf16 part products)")
+        self.f32_products = int(f32_products) if self.f32 else 0
         self.f16 = precision == "fp16"
 
         self.ops = torch.ops.mihvd
@@ -642,7 +653,8 @@ class FusedMNISTTrainer:
         coll = self._f32_gather_colaunch() if (self.collectives and self.shard_w3 and self.use_xgmi) else -1
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
                         self.idx1, w2, wf, coll=coll)
-        o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0])
+        o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0],
+                        products=self.f32_products)
         if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None

@@ -101,8 +101,10 @@ def main():
             tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1, w2, w2frag),
         "conv2_fwd [W2 fragment copy]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
                                                                 w2frag=w2frag[0]),
-        "conv2_fwd [split-bf16 x9]": lambda: (o.f32_products(1), o.f32_conv2_fwd(
-            tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2, w2frag=w2frag[0]), o.f32_products(0)),
+        "conv2_fwd [split-bf16 x9]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
+                                                             w2frag=w2frag[0], products=9),
+        "conv2_fwd [split-bf16 x6]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
+                                                             w2frag=w2frag[0], products=6),
         "conv2_bwd [W2 fragment copy]": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart,
                                                                 tr.slab, w2frag=w2frag[1]),
         "fc1_bwd [dgrad only: fp32 factor plane]": lambda: o.f32_fc1_bwd(

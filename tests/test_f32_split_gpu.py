@@ -12,17 +12,14 @@ from test_f32_gpu import ref_conv_pool, rel_err
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture()
+@pytest.fixture(scope="module")
 def ops():
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     from mihvd import _native
 
     _native.require_kernels()
-    o = torch.ops.mihvd
-    before = o.f32_products(-1)
-    yield o
-    o.f32_products(before)
+    return torch.ops.mihvd
 
 
 def _frag(ops, B, w):
@@ -33,25 +30,25 @@ def _frag(ops, B, w):
     return frag
 
 
+@pytest.mark.parametrize("nprod", [9, 6])
 @pytest.mark.parametrize("B", [7, 100, 128])
-def test_split_conv2_fwd_is_fp32_accurate(ops, B):
+def test_split_conv2_fwd_is_fp32_accurate(ops, B, nprod):
     g = torch.Generator(device="cuda").manual_seed(12)
     a1 = torch.rand(B, 14, 14, 32, device="cuda", generator=g)
     w = torch.randn(5, 5, 32, 64, device="cuda", generator=g) * 0.05
     b = torch.randn(64, device="cuda", generator=g) * 0.1
     frag = _frag(ops, B, w)
     out = {}
-    for mode in (0, 1):
-        ops.f32_products(mode)
+    for mode in (0, nprod):
         a2 = torch.full((B, 3136), float("nan"), device="cuda")
         idx = torch.empty(B, 3136, device="cuda", dtype=torch.uint8)
-        ops.f32_conv2_fwd(a1, w, b, a2, idx, w2frag=frag[0])
+        ops.f32_conv2_fwd(a1, w, b, a2, idx, w2frag=frag[0], products=mode)
         out[mode] = (a2, idx)
     ref, rd = ref_conv_pool(a1.double(), w.double(), b.double())
     ref, rd = ref.reshape(B, 3136), rd.reshape(B, 3136)
-    e_native, e_split = rel_err(out[0][0], ref), rel_err(out[1][0], ref)
-    print(f"B={B} rel err vs fp64: fp32 MFMA {e_native:.3e}, split-bf16 {e_split:.3e}")
-    assert torch.isfinite(out[1][0]).all()
+    e_native, e_split = rel_err(out[0][0], ref), rel_err(out[nprod][0], ref)
+    print(f"B={B} rel err vs fp64: fp32 MFMA {e_native:.3e}, split-bf16 x{nprod} {e_split:.3e}")
+    assert torch.isfinite(out[nprod][0]).all()
     assert e_split < 1e-6 and e_split <= 2.0 * e_native + 1e-8, (e_native, e_split)
     pos = ref > 1e-4
-    assert (out[1][1].long()[pos] == rd[pos]).float().mean() > 0.999
+    assert (out[nprod][1].long()[pos] == rd[pos]).float().mean() > 0.999
