@@ -800,6 +800,244 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
   c2b_stamp(6);
 }
 
+// ------------------------------------------------------------------------------------------ //
+// dgrad role on split-bf16 products (f32_common.h: NPROD part products per 32-deep k chunk on
+// v_mfma_f32_16x16x32_bf16). The k chunk is (tap, 32 output channels): A = the routed gradient's
+// three bf16 planes in LDS ([plane][tall row][18 cols][64 co]: 128 B per pixel and plane; the
+// 16-byte chunk k of a pixel at k ^ x6d_swz, conflict-free for every tap and row / image wrap of a
+// tile by the bank model of scripts/ldssim_conv2.py), B = W2[tap][ci][co 8 g .. + 7] (32 contiguous
+// bytes of the HWIO tensor per lane), split in registers one tap ahead. 8 waves = co half (w & 1) x
+// tap quarter (w >> 1: taps 0-6 | 7-12 | 13-18 | 19-24; a SIMD's two waves w, w + 4 hold quarters
+// q, q + 2); each wave computes both 16-channel ci groups, so every A read feeds 2 NPROD MFMAs. The
+// co halves meet first (h0 + h1), then the four quarters in the native form's order and layout, and
+// the epilogue (ReLU / pool routing, the conv1 weight gradient, db1) is the native form's.
+constexpr int X6D_PS = 32;                               // dwords per pixel and plane
+constexpr int X6D_MAXR = 23;                             // tall rows of a 12-tile block across an image edge
+constexpr int X6D_PLANE = X6D_MAXR * 18 * X6D_PS;        // dwords per plane
+constexpr int X6D_LDS = 3 * X6D_PLANE * 4;               // 158,976 B
+static_assert(X6D_LDS <= 163840, "split dgrad LDS");
+static_assert(cbf_red(12) + CBF_XIM + CBF_PW <= 3 * X6D_PLANE, "split dgrad exchange + x images + partials fit");
+__device__ __forceinline__ int x6d_swz(int pix, int r) { return (((pix >> 1) + 2 * r) & 3) << 1; }
+
+template <int TPB, int NPROD, int STUDY = 0>
+__device__ __forceinline__ void f32x_conv2_dgrad_block(
+    int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
+    const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
+    const int64_t* __restrict__ state, float* __restrict__ cpart, int B, float* smf) {
+  constexpr int MAXCH = (X6D_MAXR * 288 + 511) / 512;  // dY2 float4 chunks per thread
+  uint32_t* img = reinterpret_cast<uint32_t*>(smf);
+  float* xim = smf + cbf_red(TPB);  // behind the partial exchange, written after the tap loop
+  float* pw = xim + CBF_XIM;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
+  // wave = ci group (w & 1) x co half (w >> 1 & 1) x tap half (w >> 2: taps 0-12 | 13-24; the two
+  // waves of a SIMD, w and w + 4, hold the two halves)
+  const int cg = wave & 1, h = (wave >> 1) & 1, th = wave >> 2, kp = wave >> 1;  // K part = (th, h)
+  const int tap0 = th ? 13 : 0, ntap = th ? 12 : 13;
+  const int np = 196 * B, T0 = bid * TPB;
+  const int P0 = 16 * T0, P1 = min(16 * (T0 + TPB), np) - 1;
+  const int b0 = P0 / 196, b1i = P1 / 196;
+  const int R0 = 18 * b0 + (P0 - 196 * b0) / 14, R1 = 18 * b1i + (P1 - 196 * b1i) / 14 + 5;
+  const int nch = (R1 - R0) * 288;  // 18 pixels x 16 float4
+  int xrow0 = b0, xrow1 = min(b0 + 1, B - 1);
+  if (rows != nullptr) {
+    const int64_t step = state ? state[ST_FWD] : 0;
+    xrow0 = rows[(int)((step * (int64_t)B + xrow0) % n_pool)];
+    xrow1 = rows[(int)((step * (int64_t)B + xrow1) % n_pool)];
+  }
+  // B operand of a tap: W2[tap][16 cg + lr][32 h + 8 lg + j], j < 8
+  const float* wq = w2 + (16 * cg + lr) * 64 + 32 * h + 8 * lg;
+  float4 wraw[2];
+  auto load_w = [&](int tap) {
+    wraw[0] = *reinterpret_cast<const float4*>(wq + tap * 2048);
+    wraw[1] = *reinterpret_cast<const float4*>(wq + tap * 2048 + 4);
+  };
+  load_w(tap0);
+  // 1. the routed gradient rows -> the three planes
+  {
+    float4 iv[MAXCH];
+#pragma unroll
+    for (int it = 0; it < MAXCH; ++it) {
+      const int i = min(t + 512 * it, nch - 1);
+      const int rr = i / 288, rem = i - rr * 288, c = rem >> 4, ch = rem & 15;
+      const int R = R0 + rr, bb = R / 18, y = R - 18 * bb - 2, xx = c - 2;
+      const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+      const float4 v = *reinterpret_cast<const float4*>(
+          dY2 + (((int64_t)bb * 14 + (in ? y : 0)) * 14 + (in ? xx : 0)) * 64 + ch * 4);
+      iv[it] = mask_f4(v, in);
+    }
+#pragma unroll
+    for (int it = 0; it < MAXCH; ++it) {
+      const int i = t + 512 * it;
+      if (i < nch) {
+        const int rr = i / 288, rem = i - rr * 288, c = rem >> 4, ch = rem & 15;
+        const int pix = rr * 18 + c;
+        const int o = pix * X6D_PS + 4 * ((ch >> 1) ^ x6d_swz(pix, rr)) + 2 * (ch & 1);
+        uint2 hh, mm, ll;
+        x9_split4(iv[it], hh, mm, ll);
+        *reinterpret_cast<uint2*>(img + o) = hh;
+        *reinterpret_cast<uint2*>(img + X6D_PLANE + o) = mm;
+        *reinterpret_cast<uint2*>(img + 2 * X6D_PLANE + o) = ll;
+      }
+    }
+  }
+  float xv[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int i = t + 512 * it, pix = i & 1023, Y = (pix >> 5) - 2, X = (pix & 31) - 2;
+    const int row = it < 2 ? xrow0 : xrow1;
+    const bool in = Y >= 0 && Y < 28 && X >= 0 && X < 28;
+    xv[it] = mask_f(x[(int64_t)row * 784 + (in ? Y * 28 + X : 0)], in);
+  }
+  f32x4 acc[TPB];
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // the planes are complete
+  // the lane's output pixel of every tile: (tall row << 16) | pixel index (row * 18 + column)
+  int pb[TPB];
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) {
+    const int P = min(16 * (T0 + i) + lr, np - 1);
+    const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
+    const int r = 18 * bb + py - R0;
+    pb[i] = (r << 16) | (r * 18 + px);
+  }
+  auto load_a = [&](int i, int kh, int kw) {
+    const int r = (pb[i] >> 16) + 4 - kh, pix = (pb[i] & 0xffff) + (4 - kh) * 18 + 4 - kw;
+    const uint32_t* p = img + pix * X6D_PS + 4 * ((4 * h + lg) ^ x6d_swz(pix, r));
+    X9Frag f;
+    f.p[0] = *reinterpret_cast<const bf16x8*>(p);
+    f.p[1] = *reinterpret_cast<const bf16x8*>(p + X6D_PLANE);
+    f.p[2] = *reinterpret_cast<const bf16x8*>(p + 2 * X6D_PLANE);
+    return f;
+  };
+  // the running sums alternate sign tap by tap (x9_neg: the bf16 MFMA's rounding bias cancels over
+  // consecutive taps); after tap s they hold (-1)^s times the partial sum
+  for (int s = 0; s < ntap; ++s) {  // wave-uniform
+    const int tap = tap0 + s, kh = tap / 5, kw = tap - 5 * kh;
+    X9Frag wb = x9_split8(wraw[0], wraw[1]);
+    if (s & 1) wb = x9_neg(wb);
+    if (s + 1 < ntap) load_w(tap + 1);
+    X9Frag fa = STUDY == 2 ? wb : load_a(0, kh, kw);
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) {
+      X9Frag fn;
+      if (i + 1 < TPB && STUDY != 2) fn = load_a(i + 1, kh, kw);
+      // pinned: the next tile's reads issue ahead of this tile's MFMAs (left alone, the scheduler
+      // waits on each read right before its MFMAs: the LDS latency was exposed every tile)
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (STUDY == 1) {  // no MFMA
+        acc[i][0] += (float)fa.p[0][0] + (float)fa.p[1][1] + (float)fa.p[2][2] + (float)wb.p[0][0];
+      } else {
+        acc[i] = x9_mma<NPROD>(fa, wb, acc[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < TPB) fa = fn;
+      if (s + 1 < ntap) acc[i] = f4neg(acc[i]);
+    }
+  }
+  if ((ntap - 1) & 1) {  // wave-uniform: back to the partial sum's own sign
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) acc[i] = f4neg(acc[i]);
+  }
+  if constexpr (STUDY == 3) {  // no epilogue: keep the accumulators live
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < TPB; ++i) z += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+    if (z == 12345.f) cpart[t] = z;
+    return;
+  }
+  // the epilogue's conv1 operands (as the native form; loaded after the tap loop, whose registers
+  // the accumulators need): (nt, tile) pairs p = wave + 8k
+  const int nt = wave & 1;
+  constexpr int NP = (2 * TPB + 7) / 8;
+  float ea[NP][4];
+  int ex[NP][4];
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pp = wave + 8 * k;
+      const int P = 16 * (T0 + (pp >> 1)) + 4 * lg + r;
+      const bool ok = pp < 2 * TPB && P < np;
+      const int64_t o = (int64_t)min(P, np - 1) * 32 + 16 * nt + lr;
+      ea[k][r] = mask_f(a1[o], ok);
+      ex[k][r] = idx1[o];
+    }
+  __syncthreads();  // every wave is done with the planes
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {  // (complete after the next barrier)
+    const int i = t + 512 * it, sl = i >> 10, pix = i & 1023;
+    xim[sl * CBF_XIMG + (pix >> 5) * CBF_XS + (pix & 31)] = xv[it];
+  }
+  // 2. the four K-part partials of each (ci group, tile) in the native form's layout
+  f32x4* red = reinterpret_cast<f32x4*>(smf);  // [K part][ci group][TPB][64]
+#pragma unroll
+  for (int i = 0; i < TPB; ++i) red[((kp * 2 + cg) * TPB + i) * 64 + lane] = acc[i];
+  __syncthreads();
+  // 3. epilogue (the native form's): mask -> g1, conv1 weight gradient of the routed g1, db1
+  float s25[26];
+#pragma unroll
+  for (int e = 0; e < 26; ++e) s25[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int p = wave + 8 * k;  // wave-uniform; p & 1 == nt
+    if (p >= 2 * TPB) break;
+    const int i = p >> 1;
+    const f32x4 sum = ((red[((0 * 2 + nt) * TPB + i) * 64 + lane] + red[((1 * 2 + nt) * TPB + i) * 64 + lane]) +
+                       red[((2 * 2 + nt) * TPB + i) * 64 + lane]) +
+                      red[((3 * 2 + nt) * TPB + i) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int P = 16 * (T0 + i) + 4 * lg + r;
+      if (P < np) {
+        const int bb = P / 196, pp = P - 196 * bb, py = pp / 14, px = pp - 14 * py;
+        const float gv = ea[k][r] > 0.f ? sum[r] : 0.f;
+        const int ix = ex[k][r];
+        const float* xs = xim + (bb - b0) * CBF_XIMG + (2 * py + (ix >> 1)) * CBF_XS + 2 * px + (ix & 1);
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) s25[kh * 5 + kw] = fmaf(gv, xs[kh * CBF_XS + kw], s25[kh * 5 + kw]);
+        s25[25] += gv;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 26; ++e) {
+    float v = s25[e];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    s25[e] = v;
+  }
+  if (lg == 0) {
+#pragma unroll
+    for (int e = 0; e < 26; ++e) pw[(wave * 26 + e) * 16 + lr] = s25[e];
+  }
+  __syncthreads();
+  for (int qq = t; qq < CP_F32; qq += 512) {
+    const int e = qq >> 5, c = qq & 31, hh = c >> 4, l = c & 15;
+    const float v = (pw[((hh + 0) * 26 + e) * 16 + l] + pw[((hh + 2) * 26 + e) * 16 + l]) +
+                    (pw[((hh + 4) * 26 + e) * 16 + l] + pw[((hh + 6) * 26 + e) * 16 + l]);
+    cpart[(int64_t)bid * CP_F32 + qq] = v;
+  }
+}
+
+// conv2_bwd with the split-bf16 dgrad role (the wgrad role is the native form's)
+template <int TPB, int NPROD, int STUDY = 0>
+__global__ void __launch_bounds__(512) f32x_conv2_bwd_kernel(
+    const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
+    const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
+    const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
+    int n_wg, int ig, const float* __restrict__ zeros) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  const int bid = blockIdx.x;
+  if (bid < n_dg) {
+    f32x_conv2_dgrad_block<TPB, NPROD, STUDY>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
+    return;
+  }
+  f32_conv2_wgrad_block(xcd_contiguous(bid, n_dg, n_dg + n_wg), dY2, a1, slab, B, ig, smf, zeros);
+}
+
 template <int TPB, int NPASS = 1, bool FRAG = false>
 __global__ void __launch_bounds__(512) f32_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
@@ -1041,12 +1279,24 @@ static int conv2b_tpb(int B) {
 static bool conv2b_one_round(int B) { return 2 * conv2b_tpb(B) <= 10; }
 static int conv2b_block_tiles(int B) { return conv2b_one_round(B) ? 2 * conv2b_tpb(B) : conv2b_tpb(B); }
 static int conv2b_images(int B) { return conv2b_one_round(B) ? CBF_IG2 : CBF_IG; }
-int64_t f32_wgrad_groups(int64_t B) {
-  const int ig = conv2b_images((int)B);
+// The split-bf16 dgrad role (f32x_conv2_bwd_kernel) does a tile in ~2/5 of the native MFMA time, so
+// it takes blocks of up to 12 tiles (the LDS holds their three planes: X6D_MAXR rows) and the wgrad
+// role the CUs it leaves (images per group chosen so both roles fit one round of blocks).
+static int conv2bx_tiles(int B) {
+  const int nt = (196 * B + 15) / 16;
+  return std::min(12, std::max(1, (nt + 99) / 100));
+}
+static int conv2bx_images(int B) {
+  const int nt = (196 * B + 15) / 16, tpb = conv2bx_tiles(B), n_dg = (nt + tpb - 1) / tpb;
+  const int free = std::max(10, device_cu_count() - n_dg);
+  return std::min(B, std::max(1, (10 * B + free - 1) / free));
+}
+int64_t f32_wgrad_groups(int64_t B, int64_t products) {
+  const int ig = products ? conv2bx_images((int)B) : conv2b_images((int)B);
   return (B + ig - 1) / ig;
 }
-int64_t f32_dgrad_blocks(int64_t B) {
-  const int tpb = conv2b_block_tiles((int)B), nt = (196 * (int)B + 15) / 16;
+int64_t f32_dgrad_blocks(int64_t B, int64_t products) {
+  const int tpb = products ? conv2bx_tiles((int)B) : conv2b_block_tiles((int)B), nt = (196 * (int)B + 15) / 16;
   return (nt + tpb - 1) / tpb;
 }
 
@@ -1154,9 +1404,10 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
 
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                   at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag) {
+                   at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag, int64_t products) {
   const int B = a1.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv2_bwd: batch 1..128");
+  TORCH_CHECK(products == 0 || products == 6 || products == 9, "f32_conv2_bwd: products 0, 6 or 9");
   const float* w2f = nullptr;
   if (w2frag.has_value() && w2frag->defined()) {
     TORCH_CHECK(w2frag->is_cuda() && w2frag->dtype() == at::kFloat && w2frag->is_contiguous() &&
@@ -1169,11 +1420,13 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
   TORCH_CHECK(idx1.dtype() == at::kByte && idx1.numel() == (int64_t)B * 6272 && idx1.is_contiguous(), "f32_conv2_bwd: idx1");
   TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_conv2_bwd: x");
   const bool r1 = conv2b_one_round(B);
-  const int n_dg = (int)f32_dgrad_blocks(B), tpb = conv2b_block_tiles(B), ig = conv2b_images(B);
+  const int n_dg = (int)f32_dgrad_blocks(B, 0), tpb = conv2b_block_tiles(B), ig = conv2b_images(B);
   const int maxr = r1 ? CBF_MAXR2 : CBF_MAXR;
-  chk_f32(cpart, (int64_t)n_dg * CP_F32, "f32_conv2_bwd: cpart [dgrad blocks][832]");
-  const int ngrp = (int)f32_wgrad_groups(B);
-  chk_f32(slab, (int64_t)ngrp * 51200, "f32_conv2_bwd: slab [groups][51200]");
+  const int ngrp = (int)f32_wgrad_groups(B, 0);
+  if (products == 0) {
+    chk_f32(cpart, (int64_t)n_dg * CP_F32, "f32_conv2_bwd: cpart [dgrad blocks][832]");
+    chk_f32(slab, (int64_t)ngrp * 51200, "f32_conv2_bwd: slab [groups][51200]");
+  }
   const int n_pool = x.size(0);
   const int* rp = nullptr;
   if (rows.has_value() && rows->defined()) {
@@ -1183,6 +1436,53 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
     TORCH_CHECK(n_pool >= B, "f32_conv2_bwd: x has fewer rows than the batch");
   }
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  if (products != 0) {  // split-bf16 dgrad role
+    const int n_dg = (int)f32_dgrad_blocks(B, products), tpb = conv2bx_tiles(B), ig = conv2bx_images(B);
+    const int ngrp = (int)f32_wgrad_groups(B, products);
+    chk_f32(cpart, (int64_t)n_dg * CP_F32, "f32_conv2_bwd: cpart [dgrad blocks][832]");
+    chk_f32(slab, (int64_t)ngrp * 51200, "f32_conv2_bwd: slab [groups][51200]");
+    for (int blk = 0; blk < n_dg; ++blk) {
+      const int P0 = 16 * blk * tpb, P1 = std::min(16 * (blk + 1) * tpb, 196 * B) - 1;
+      const int r0 = 18 * (P0 / 196) + (P0 % 196) / 14, r1 = 18 * (P1 / 196) + (P1 % 196) / 14 + 5;
+      TORCH_CHECK(r1 - r0 <= X6D_MAXR && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS planes");
+    }
+    auto stream = c10::hip::getCurrentHIPStream().stream();
+    const int lds = std::max(X6D_LDS, CBF_LDS_WG);
+    const float* zl = f32_zero_line(stream);
+    auto launch = [&](auto kern) {
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      const int role = env_knob("MIHVD_C2BX_ROLE", 0);  // STUDY: 1 dgrad blocks only, 2 wgrad only
+      const int ndg = role == 2 ? 0 : n_dg, nwg = role == 1 ? 0 : 10 * ngrp;
+      kern<<<ndg + nwg, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
+                                            idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
+                                            cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg, nwg, ig, zl);
+    };
+#define C2BX_CASE(T)                                                      \
+  case T:                                                                 \
+    if (products == 9) launch(f32x_conv2_bwd_kernel<T, 9>);               \
+    else if (env_knob("MIHVD_C2BX_STUDY", 0) == 1) launch(f32x_conv2_bwd_kernel<T, 6, 1>); \
+    else if (env_knob("MIHVD_C2BX_STUDY", 0) == 2) launch(f32x_conv2_bwd_kernel<T, 6, 2>); \
+    else if (env_knob("MIHVD_C2BX_STUDY", 0) == 3) launch(f32x_conv2_bwd_kernel<T, 6, 3>); \
+    else launch(f32x_conv2_bwd_kernel<T, 6>);                             \
+    break;
+    switch (tpb) {
+      C2BX_CASE(1)
+      C2BX_CASE(2)
+      C2BX_CASE(3)
+      C2BX_CASE(4)
+      C2BX_CASE(5)
+      C2BX_CASE(6)
+      C2BX_CASE(7)
+      C2BX_CASE(8)
+      C2BX_CASE(9)
+      C2BX_CASE(10)
+      C2BX_CASE(11)
+      default:
+        C2BX_CASE(12)
+    }
+#undef C2BX_CASE
+    return;
+  }
   // host check of the dgrad blocks' row spans (the LDS image) and image count (<= 2)
   for (int blk = 0; blk < n_dg; ++blk) {
     const int P0 = 16 * blk * tpb, P1 = std::min(16 * (blk + 1) * tpb, 196 * B) - 1;

@@ -272,6 +272,29 @@ __device__ __forceinline__ X9Frag x9_split8(const float4& a, const float4& b) {
   return f;
 }
 
+// The bf16 MFMA's internal accumulation is not round-to-nearest: its results are biased toward
+// -inf (bench_native/mfma_split_numerics.hip: mean signed error about -0.05 of the rms error per
+// output, where v_mfma_f32_16x16x4_f32 is unbiased). Per element that is harmless, but a gradient
+// summed over thousands of such outputs with cancellation (db1 / dW1 from conv2_bwd's dA1) picks the
+// bias up coherently: 10x the fp32-input MFMA's error. The k loops therefore alternate the sign of
+// the running sum chunk by chunk (negate the accumulator and the chunk's B fragment, x9_neg): a
+// rounding toward -inf of -(S + X) is a rounding toward +inf of S + X, so consecutive chunks' biases
+// cancel.
+__device__ __forceinline__ X9Frag x9_neg(const X9Frag& f) {
+  X9Frag n;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    uint4 u = __builtin_bit_cast(uint4, f.p[p]);
+    u.x ^= 0x80008000u;
+    u.y ^= 0x80008000u;
+    u.z ^= 0x80008000u;
+    u.w ^= 0x80008000u;
+    n.p[p] = __builtin_bit_cast(bf16x8, u);
+  }
+  return n;
+}
+__device__ __forceinline__ f32x4 f4neg(const f32x4& c) { return -c; }
+
 // c += A . B over one 32-deep k chunk: the part pairs, smallest first
 template <int NPROD>
 __device__ __forceinline__ f32x4 x9_mma(const X9Frag& a, const X9Frag& b, f32x4 c) {

@@ -413,20 +413,38 @@ __global__ void __launch_bounds__(512) f32x9_conv2_fwd_kernel(const float* __res
     f.p[2] = *reinterpret_cast<const bf16x8*>(p + 2 * X9F_PLANE);
     return f;
   };
+  // the running sums alternate sign tap by tap (f32_common.h x9_neg: the bf16 MFMA's rounding bias
+  // cancels over consecutive taps); after tap s they hold (-1)^s times the partial sum
   for (int s = 0; s < ntap; ++s) {  // wave-uniform
     const int tap = tap0 + s, kh = tap / 5, kw = tap - 5 * kh;
-    const X9Frag wb0 = x9_split8(wraw[0][0], wraw[0][1]);
-    const X9Frag wb1 = x9_split8(wraw[1][0], wraw[1][1]);
+    X9Frag wb0 = x9_split8(wraw[0][0], wraw[0][1]);
+    X9Frag wb1 = x9_split8(wraw[1][0], wraw[1][1]);
+    if (s & 1) {
+      wb0 = x9_neg(wb0);
+      wb1 = x9_neg(wb1);
+    }
     if (s + 1 < ntap) load_w(tap + 1);
     X9Frag fa = load_a(0, kh, kw);
 #pragma unroll
     for (int u = 0; u < TPB; ++u) {
       X9Frag fn;
       if (u + 1 < TPB) fn = load_a(u + 1, kh, kw);
+      __builtin_amdgcn_sched_barrier(0);  // the next tile's reads ahead of this tile's MFMAs (pinned)
       acc[0][u] = x9_mma<NPROD>(fa, wb0, acc[0][u]);
       acc[1][u] = x9_mma<NPROD>(fa, wb1, acc[1][u]);
+      __builtin_amdgcn_sched_barrier(0);
       if (u + 1 < TPB) fa = fn;
+      if (s + 1 < ntap) {
+        acc[0][u] = f4neg(acc[0][u]);
+        acc[1][u] = f4neg(acc[1][u]);
+      }
     }
+  }
+  if ((ntap - 1) & 1) {  // wave-uniform: back to the partial sum's own sign
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int u = 0; u < TPB; ++u) acc[c][u] = f4neg(acc[c][u]);
   }
   // exchange over the dead image: xr[co half][tile][quarter][co group][lane]
   __syncthreads();

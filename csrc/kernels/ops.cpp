@@ -101,7 +101,7 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
                  double beta2, double eps, double grad_scale, int64_t rule, bool store_w3);
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
-                   at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag);
+                   at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag, int64_t products);
 void f32_factor_rows(const at::Tensor& a2c, const at::Tensor& dz, const c10::optional<at::Tensor>& out,
                      const c10::optional<at::Tensor>& p, const c10::optional<at::Tensor>& m,
                      const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, double lr,
@@ -114,8 +114,8 @@ void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::
                      double b2, double eps, double grad_scale, int64_t rule);
 int64_t f32_db2_rows(int64_t B);
 at::Tensor f32_stamps_enable(int64_t n_blocks, int64_t kernel);
-int64_t f32_wgrad_groups(int64_t B);
-int64_t f32_dgrad_blocks(int64_t B);
+int64_t f32_wgrad_groups(int64_t B, int64_t products);
+int64_t f32_dgrad_blocks(int64_t B, int64_t products);
 int64_t conv_barrier_error(bool reset);
 }  // namespace mihvd
 
@@ -310,8 +310,9 @@ void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, cons
                      grad_scale, rule, store_w3);
 }
 void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, const Tensor& idx1, const Tensor& x,
-                      const OptT& rows, const OptT& state, Tensor cpart, Tensor slab, const OptT& w2frag) {
-  mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab, w2frag);
+                      const OptT& rows, const OptT& state, Tensor cpart, Tensor slab, const OptT& w2frag,
+                      int64_t products) {
+  mihvd::f32_conv2_bwd(dY2, w2, a1, idx1, x, rows, state, cpart, slab, w2frag, products);
 }
 void f32_factor_rows_op(const Tensor& a2c, const Tensor& dz, const OptT& out, const OptT& p, const OptT& m,
                         const OptT& v, const OptT& state, double lr, double beta1, double beta2, double eps,
@@ -403,15 +404,15 @@ TORCH_LIBRARY(mihvd, m) {
         "Tensor(d!)? v=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0) -> ()");
   m.def("f32_conv2_bwd(Tensor dY2, Tensor w2, Tensor a1, Tensor idx1, Tensor x, Tensor? rows, Tensor? state, "
-        "Tensor(a!) cpart, Tensor(b!) slab, Tensor? w2frag=None) -> ()");
+        "Tensor(a!) cpart, Tensor(b!) slab, Tensor? w2frag=None, int products=0) -> ()");
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
         "Tensor(d!) gb2, Tensor(e!)? params=None, Tensor? grads=None, Tensor(f!)? m=None, Tensor(g!)? v=None, "
         "Tensor(s!)? state=None, int o_w1=0, int o_b1=0, int o_w2=0, int o_b2=0, int fc_lo=0, int fc_hi=0, "
         "float lr=0., float b1=0., float b2=0., float eps=0., float grad_scale=1., int rule=0) -> ()");
   m.def("f32_db2_rows(int B) -> int", &mihvd::f32_db2_rows);
   m.def("f32_stamps_enable(int n_blocks, int kernel=0) -> Tensor", &mihvd::f32_stamps_enable);
-  m.def("f32_wgrad_groups(int B) -> int", &mihvd::f32_wgrad_groups);
-  m.def("f32_dgrad_blocks(int B) -> int", &mihvd::f32_dgrad_blocks);
+  m.def("f32_wgrad_groups(int B, int products=0) -> int", &mihvd::f32_wgrad_groups);
+  m.def("f32_dgrad_blocks(int B, int products=0) -> int", &mihvd::f32_dgrad_blocks);
   m.def("conv_barrier_error(bool reset=True) -> int", &mihvd::conv_barrier_error);
   m.def("gather_cols_bf16(Tensor src, int col0, Tensor(a!) dst) -> ()");
   m.def("scale_cast_bf16(Tensor src, Tensor(a!) dst, float scale) -> ()");

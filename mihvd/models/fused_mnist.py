@@ -388,8 +388,8 @@ class FusedMNISTTrainer:
             self.dz = torch.empty(B, 1024, **f32)
             self.dY2 = torch.empty(B, 14, 14, 64, **f32)   # routed conv2 output gradient
             self.db2p = torch.empty(int(ops.f32_db2_rows(B)), 64, **f32)
-            self.slab = torch.empty(int(ops.f32_wgrad_groups(B)), 51200, **f32)
-            self.cpart = torch.empty(int(ops.f32_dgrad_blocks(B)), 832, **f32)
+            self.slab = torch.empty(int(ops.f32_wgrad_groups(B, self.f32_products)), 51200, **f32)
+            self.cpart = torch.empty(int(ops.f32_dgrad_blocks(B, self.f32_products)), 832, **f32)
             self.g2 = None
             # sharded dense/kernel optimizer: this rank's rows of the reduced dW3
             self._f32_R = 3136 // self.world if self.world > 0 and 3136 % self.world == 0 else 0
@@ -671,7 +671,8 @@ class FusedMNISTTrainer:
             o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
                           G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3], self.v[s3], st, self.lr,
                           b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad)
-            o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+            o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
+                            products=self.f32_products)
             o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv, self.params, self.grads, self.m, self.v, st,
                               SEGMENTS["conv_layer1/conv2d/kernel"][0], SEGMENTS["conv_layer1/conv2d/bias"][0],
                               SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0],
@@ -695,7 +696,8 @@ class FusedMNISTTrainer:
                         1.0 / self.world, self.rule, 0)
             self._shadow_ev = torch.cuda.Event()  # the next step's fc1_fwd (W3's first reader) joins it
             self._shadow_ev.record(side)
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
+                            products=self.f32_products)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
         self._f32_small_tail(main, FC_START)
 
@@ -769,7 +771,8 @@ class FusedMNISTTrainer:
                 self._reduce_scatter_rows(gW3, mine_g, R)
                 o.adam_step(self.params[mine], mine_g.reshape(-1), self.m[mine], self.v[mine], None, st, 0, self.lr,
                             b1, b2, self.eps, 1.0 / self.world, self.rule, 0)
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
+                            products=self.f32_products)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
         self._f32_small_tail(main, W3_START)
         if self.ncomm_small is not None:
@@ -872,7 +875,8 @@ class FusedMNISTTrainer:
             R = self._roles
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, self.pview("dense/kernel"), self.dY2, self.db2p,
                       G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
-        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1])
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
+                            products=self.f32_products)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
         # (at world 1, forced collectives, the entry runs too: a self-peer phase, priced like N > 1)
         self.xplane.run_split(R["small"], R["rows"])

@@ -1,0 +1,16 @@
+# Round 6, pass n: split-bf16 conv2_fwd + conv2_bwd dgrad (one ci group per wave, pinned prefetch):
+# numerics, kernel times, fp32 suite, bench (split vs fp32-input MFMA), driver form.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export MIHVD_NO_AUTOBUILD=1
+O=gpurun_out/r06n; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -v -s --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_f32_split_gpu.py > $O/tests_split.log 2>&1
+rc=$?; tail -2 $O/tests_split.log; grep -E "x6 dW1|x6 db1|^FAILED|Error" $O/tests_split.log | head -20; [ $rc -ne 0 ] && exit $rc
+for st in 0 1 3; do MIHVD_C2BX_ROLE=1 MIHVD_C2BX_STUDY=$st timeout -k 10 120 python scripts/kbench_f32.py --match "x6 dgrad" > $O/s$st.txt 2>&1 || { tail -20 $O/s$st.txt; exit 1; }; echo "study $st: $(grep x6 $O/s$st.txt)"; done
+timeout -k 10 200 python scripts/kbench_f32.py > $O/kbench.txt 2>&1 || { tail -20 $O/kbench.txt; exit 1; }
+cat $O/kbench.txt
+timeout -k 10 400 python -u -m pytest -v --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_f32_gpu.py > $O/tests_f32.log 2>&1
+rc=$?; tail -2 $O/tests_f32.log; grep -E "^FAILED|^ERROR" $O/tests_f32.log | head -20; [ $rc -ne 0 ] && exit $rc
+for m in 6 0 6; do MIHVD_F32_PRODUCTS=$m timeout -k 10 200 python bench.py --gpus 1 --steps 200 --warmup 20 > $O/bench_p$m.log 2>&1 || { tail -20 $O/bench_p$m.log; exit 1; }; python3 -c "import json; [print('products $m', json.loads(l)['ms_per_step']*1000, json.loads(l)['value']) for l in open('$O/bench_p$m.log') if l.startswith('{')]"; done
+timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_drv.log 2>&1 || { tail -20 $O/bench_drv.log; exit 1; }
+python3 -c "import json; [print('driver form', json.loads(l)['ms_per_step']*1000) for l in open('$O/bench_drv.log') if l.startswith('{')]"
+echo ALLDONE

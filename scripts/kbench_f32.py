@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--only", default=None, help="comma-separated entries: run each --eager times, eagerly "
                     "(for counter collection), and exit")
     ap.add_argument("--eager", type=int, default=20)
+    ap.add_argument("--products", type=int, default=6, help="the trainer's fp32 product form (whole-step entry)")
     ap.add_argument("--match", default=None, help="'|'-separated substrings: time only the entries whose name "
                     "contains one of them")
     args = ap.parse_args()
@@ -63,7 +64,8 @@ def main():
     (x, y), _ = synthetic_mnist(n_train=B * 20, n_test=10, seed=1)
     X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
     Y = torch.from_numpy(y.astype("int64")).cuda()
-    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, seed=0, device="cuda", precision="fp32")
+    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, seed=0, device="cuda", precision="fp32",
+                           f32_products=args.products)
     tr.set_device_dataset(X, Y)
     for _ in range(3):
         tr.device_step()
@@ -83,6 +85,10 @@ def main():
                      torch.empty(3136, 1024, device="cuda"))
     fp8, fm8, fv8 = (torch.zeros(392, 1024, device="cuda") for _ in range(3))
     fp1, fm1, fv1 = (torch.zeros(3136, 1024, device="cuda") for _ in range(3))
+    slab0 = torch.empty(int(o.f32_wgrad_groups(B, 0)), 51200, device="cuda")
+    cpart0 = torch.empty(int(o.f32_dgrad_blocks(B, 0)), 832, device="cuda")
+    slab6 = torch.empty(int(o.f32_wgrad_groups(B, 6)), 51200, device="cuda")
+    cpart6 = torch.empty(int(o.f32_dgrad_blocks(B, 6)), 832, device="cuda")
     # lr 0 keeps the weights fixed while the optimizer kernels are timed
     ks = {
         "conv1_fwd": lambda: o.f32_conv1_fwd(tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"),
@@ -105,8 +111,10 @@ def main():
                                                              w2frag=w2frag[0], products=9),
         "conv2_fwd [split-bf16 x6]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
                                                              w2frag=w2frag[0], products=6),
-        "conv2_bwd [W2 fragment copy]": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart,
-                                                                tr.slab, w2frag=w2frag[1]),
+        "conv2_bwd [split-bf16 x6 dgrad]": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, cpart6,
+                                                                   slab6, products=6),
+        "conv2_bwd [W2 fragment copy]": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, cpart0,
+                                                                slab0, w2frag=w2frag[1]),
         "fc1_bwd [dgrad only: fp32 factor plane]": lambda: o.f32_fc1_bwd(
             tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"), G("dense/bias"),
             G("dense_1/kernel"), G("dense_1/bias"), store_w3=False),
@@ -118,7 +126,7 @@ def main():
                                                                   tr.eps, 0.125, tr.rule),
         "factor rows + Adam N=1 (HIP)": lambda: o.f32_factor_rows(fa1, fz1, None, fp1, fm1, fv1, st, 0.0, b1, b2,
                                                                   tr.eps, 1.0, tr.rule),
-        "conv2_bwd": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, tr.cpart, tr.slab),
+        "conv2_bwd": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, cpart0, slab0),
         "conv_reduce": lambda: o.f32_conv_reduce(tr.slab, tr.cpart, tr.db2p, *gconv),
         "conv_reduce+adam": lambda: o.f32_conv_reduce(
             tr.slab, tr.cpart, tr.db2p, *gconv, tr.params, tr.grads, tr.m, tr.v, st,
