@@ -597,6 +597,105 @@ __global__ void __launch_bounds__(512) f32_fc1_fwd2_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------------------------------------ //
+// fc1 forward on split-bf16 products (f32_common.h): the same grid, slices, waves and slab stores as
+// f32_fc1_fwd2_kernel; the 224-deep slice is 7 k chunks of 32. A = W3^T: a lane's 8 consecutive k of
+// its column n (the same 56 HBM loads per lane), split in registers chunk by chunk; B = a2^T: the
+// slice's three bf16 planes staged once per block ([plane][row][240]: the 16-byte reads of a 16-lane
+// group hit 16 distinct slots for every chunk), so an A fragment feeds every tile's NPROD MFMAs and
+// a B read 3 ds_read_b128. Sign-alternating accumulation as in conv2_fwd. Batches of up to 112 (the
+// planes of 7 sample tiles fill the LDS); larger ones take the fp32-input form.
+constexpr int X6F1_S = 240;                        // bf16 per plane row
+constexpr int x6f1_plane(int mt) { return mt * 16 * X6F1_S / 2; }  // dwords per plane
+static_assert(3 * x6f1_plane(7) * 4 <= 163840, "split fc1_fwd planes");
+
+template <int MT, int NPROD>
+__global__ void __launch_bounds__(512) f32x_fc1_fwd_kernel(const float* __restrict__ a2, const float* __restrict__ w3,
+                                                           float* __restrict__ zpart, int B) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  uint32_t* pl = reinterpret_cast<uint32_t*>(smf);
+  constexpr int PL = x6f1_plane(MT);
+  const int L = xcd_contiguous(blockIdx.y * 16 + blockIdx.x, 0, 16 * F1F_KS);
+  const int nb = L & 15, ks = L >> 4, t = threadIdx.x;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, g = lane >> 4;
+  const int k0 = ks * F1F_KSL, nt = wave & 3, sh = wave >> 2;
+  const int n = nb * 64 + nt * 16 + lr;
+  constexpr int NCH = MT * 16 * 56, PER = (NCH + 511) / 512;
+  constexpr int NT0 = (MT + 1) / 2, NT1 = MT / 2;
+  // the slice's a2 loads, then the 56 W3 loads (A: wa[8 c + j] = W3[k0 + 32 c + 8 g + j][n])
+  float4 v[PER];
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = min(t + 512 * it, NCH - 1), r = i / 56, cc = i - 56 * r;
+    v[it] = *reinterpret_cast<const float4*>(a2 + (int64_t)min(r, B - 1) * 3136 + k0 + 4 * cc);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  float wa[56];
+  {
+    const int64_t wo = (int64_t)(k0 + 8 * g) * 1024 + n;
+#pragma unroll
+    for (int c = 0; c < 7; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wa[8 * c + j] = w3[wo + (32 * c + j) * 1024];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int it = 0; it < PER; ++it) {
+    const int i = t + 512 * it;
+    if (i < NCH) {
+      const int r = i / 56, cc = i - 56 * r;
+      uint2 h, m, l;
+      x9_split4(mask_f4(v[it], r < B), h, m, l);
+      const int o = r * (X6F1_S / 2) + 2 * cc;
+      *reinterpret_cast<uint2*>(pl + o) = h;
+      *reinterpret_cast<uint2*>(pl + PL + o) = m;
+      *reinterpret_cast<uint2*>(pl + 2 * PL + o) = l;
+    }
+  }
+  c2f_lds_barrier();  // LDS only: the W3 loads stay in flight
+  const int ntl = sh == 0 ? NT0 : NT1;
+  f32x4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto load_b = [&](int u, int c) {
+    const uint32_t* p = pl + ((sh + 2 * u) * 16 + lr) * (X6F1_S / 2) + 16 * c + 4 * g;
+    X9Frag f;
+    f.p[0] = *reinterpret_cast<const bf16x8*>(p);
+    f.p[1] = *reinterpret_cast<const bf16x8*>(p + PL);
+    f.p[2] = *reinterpret_cast<const bf16x8*>(p + 2 * PL);
+    return f;
+  };
+  auto run = [&](auto ntc) {
+    constexpr int NT = decltype(ntc)::value;
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+      X9Frag fa = x9_split8(make_float4(wa[8 * c], wa[8 * c + 1], wa[8 * c + 2], wa[8 * c + 3]),
+                            make_float4(wa[8 * c + 4], wa[8 * c + 5], wa[8 * c + 6], wa[8 * c + 7]));
+      if (c & 1) fa = x9_neg(fa);
+      X9Frag fb = load_b(0, c);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        X9Frag fn;
+        if (u + 1 < NT) fn = load_b(u + 1, c);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[u] = x9_mma<NPROD>(fa, fb, acc[u]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 1 < NT) fb = fn;
+        if (c < 6) acc[u] = f4neg(acc[u]);
+      }
+    }
+  };
+  if (sh == 0) run(std::integral_constant<int, NT0>{});
+  else run(std::integral_constant<int, NT1>{});
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int tt = sh + 2 * u, m = tt * 16 + lr;
+    if (u < ntl && m < B)
+      *reinterpret_cast<float4*>(zpart + ((int64_t)ks * B + m) * 1024 + nb * 64 + nt * 16 + 4 * g) =
+          make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ //
 // head: one block per sample b (K9-K11 of SURVEY.md §2.5):
 //   z = sum of the 14 slabs + b3; h = dropout(relu(z)); logits = h W4 + b4; softmax-xent;
 //   dlogits = (softmax - onehot) / B; dz = (dlogits W4^T) * relu'(z) * dropout mask
@@ -823,14 +922,40 @@ void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor&
 #undef C2F8_CASE
 }
 
-void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart) {
+void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart, int64_t products) {
   const int B = a2.size(0);
+  TORCH_CHECK(products == 0 || products == 6 || products == 9, "f32_fc1_fwd: products 0, 6 or 9");
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_fwd: batch 1..128");
   check_f32(a2, (int64_t)B * 3136, "f32_fc1_fwd: a2");
   check_f32(w3, 3136 * 1024, "f32_fc1_fwd: w3");
   check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_fc1_fwd: zpart [14][B][1024]");
   const int mt = (B + 15) / 16;
   auto stream = c10::hip::getCurrentHIPStream().stream();
+  if (products != 0 && mt <= 7) {
+    auto launchx = [&](auto kern) {
+      const int lds = 3 * x6f1_plane(mt) * 4;
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      kern<<<dim3(16, F1F_KS), 512, lds, stream>>>(a2.data_ptr<float>(), w3.data_ptr<float>(),
+                                                   zpart.data_ptr<float>(), B);
+    };
+#define X6F1_CASE(T)                                                       \
+  case T:                                                                  \
+    if (products == 9) launchx(f32x_fc1_fwd_kernel<T, 9>);                 \
+    else launchx(f32x_fc1_fwd_kernel<T, 6>);                               \
+    break;
+    switch (mt) {
+      X6F1_CASE(1)
+      X6F1_CASE(2)
+      X6F1_CASE(3)
+      X6F1_CASE(4)
+      X6F1_CASE(5)
+      X6F1_CASE(6)
+      default:
+        X6F1_CASE(7)
+    }
+#undef X6F1_CASE
+    return;
+  }
   // (Measured alternatives, removed: the slice staged in two K halves, 10.7 vs 10.4 us; waves split by
   // K half with every W3 fragment loaded by one wave instead of two, 11.20 vs 11.05 us, whole step
   // 116.84 vs 116.91 us, profiles/r05/kbench_f32_r05o.txt -- the second wave's W3 loads hit the cache)

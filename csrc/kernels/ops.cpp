@@ -89,7 +89,7 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
                    const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll);
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
                    const c10::optional<at::Tensor>& w2frag, int64_t products);
-void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart);
+void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart, int64_t products);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
@@ -296,7 +296,9 @@ void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a
                   int64_t products) {
   mihvd::f32_conv2_fwd(a1, w2, b2, a2, idx2, w2frag, products);
 }
-void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart) { mihvd::f32_fc1_fwd(a2, w3, zpart); }
+void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart, int64_t products) {
+  mihvd::f32_fc1_fwd(a2, w3, zpart, products);
+}
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
                  Tensor stats, const OptT& stats_acc) {
@@ -392,7 +394,7 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
         "Tensor? w2=None, Tensor(f!)? w2frag=None, int coll=-1) -> ()");
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None, int products=0) -> ()");
-  m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart) -> ()");
+  m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart, int products=0) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
         "Tensor(e!)? stats_acc=None) -> ()");

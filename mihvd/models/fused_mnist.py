@@ -658,7 +658,7 @@ class FusedMNISTTrainer:
         if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None
-        o.f32_fc1_fwd(self.a2, w3, self.zpart)
+        o.f32_fc1_fwd(self.a2, w3, self.zpart, products=self.f32_products)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
                            stats_acc=self._stat_acc if self.track_stats else None)

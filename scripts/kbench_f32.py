@@ -95,6 +95,7 @@ def main():
                                              P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1),
         "conv2_fwd": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2),
         "fc1_fwd": lambda: o.f32_fc1_fwd(tr.a2, w3, tr.zpart),
+        "fc1_fwd [split-bf16 x6]": lambda: o.f32_fc1_fwd(tr.a2, w3, tr.zpart, products=6),
         "head": lambda: o.f32_head_fwd_bwd(tr.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), tr.Y,
                                            tr.rows, st, tr.seed, tr.dropout, tr.h, tr.dz, tr.dlog, tr.stats),
         "fc1_bwd": lambda: o.f32_fc1_bwd(tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"),

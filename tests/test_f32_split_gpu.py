@@ -92,3 +92,23 @@ def test_split_conv2_bwd_dgrad_is_fp32_accurate(ops, B, nprod):
         print(f"B={B} x{nprod} {name}: fp32 MFMA {e0:.3e}, split {e1:.3e}")
         assert torch.isfinite(got[nprod][k]).all(), name
         assert e1 <= 2.0 * e0 + 1e-7, (name, e0, e1)
+
+
+@pytest.mark.parametrize("nprod", [6, 9])
+@pytest.mark.parametrize("B", [7, 100, 112, 128])
+def test_split_fc1_fwd_is_fp32_accurate(ops, B, nprod):
+    """fc1 forward partial slabs on split-bf16 products (B <= 112; B = 128 runs the fp32-input form):
+    the slab sum against float64 a2 @ W3."""
+    g = torch.Generator(device="cuda").manual_seed(8)
+    a2 = torch.relu(torch.randn(B, 3136, device="cuda", generator=g))
+    w3 = torch.randn(3136, 1024, device="cuda", generator=g) * 0.02
+    ref = a2.double() @ w3.double()
+    got = {}
+    for mode in (0, nprod):
+        zp = torch.full((14, B, 1024), float("nan"), device="cuda")
+        ops.f32_fc1_fwd(a2, w3, zp, products=mode)
+        got[mode] = zp.sum(0)
+    e0, e1 = rel_err(got[0], ref), rel_err(got[nprod], ref)
+    print(f"B={B} x{nprod} fc1_fwd: fp32 MFMA {e0:.3e}, split {e1:.3e}")
+    assert torch.isfinite(got[nprod]).all()
+    assert e1 <= 2.0 * e0 + 1e-8, (e0, e1)
