@@ -812,14 +812,14 @@ __device__ __forceinline__ void f32_conv2_wgrad_block(int bid, const float* __re
 // co halves meet first (h0 + h1), then the four quarters in the native form's order and layout, and
 // the epilogue (ReLU / pool routing, the conv1 weight gradient, db1) is the native form's.
 constexpr int X6D_PS = 32;                               // dwords per pixel and plane
-constexpr int X6D_MAXR = 23;                             // tall rows of a 12-tile block across an image edge
+constexpr int X6D_MAXR = 21;                             // tall rows of a 10-tile block across an image edge
 constexpr int X6D_PLANE = X6D_MAXR * 18 * X6D_PS;        // dwords per plane
-constexpr int X6D_LDS = 3 * X6D_PLANE * 4;               // 158,976 B
+constexpr int X6D_LDS = 3 * X6D_PLANE * 4;               // 145,152 B
 static_assert(X6D_LDS <= 163840, "split dgrad LDS");
-static_assert(cbf_red(12) + CBF_XIM + CBF_PW <= 3 * X6D_PLANE, "split dgrad exchange + x images + partials fit");
+static_assert(cbf_red(10) + CBF_XIM + CBF_PW <= 3 * X6D_PLANE, "split dgrad exchange + x images + partials fit");
 __device__ __forceinline__ int x6d_swz(int pix, int r) { return (((pix >> 1) + 2 * r) & 3) << 1; }
 
-template <int TPB, int NPROD, int STUDY = 0>
+template <int TPB, int NPROD>
 __device__ __forceinline__ void f32x_conv2_dgrad_block(
     int bid, const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
@@ -917,19 +917,15 @@ __device__ __forceinline__ void f32x_conv2_dgrad_block(
     X9Frag wb = x9_split8(wraw[0], wraw[1]);
     if (s & 1) wb = x9_neg(wb);
     if (s + 1 < ntap) load_w(tap + 1);
-    X9Frag fa = STUDY == 2 ? wb : load_a(0, kh, kw);
+    X9Frag fa = load_a(0, kh, kw);
 #pragma unroll
     for (int i = 0; i < TPB; ++i) {
       X9Frag fn;
-      if (i + 1 < TPB && STUDY != 2) fn = load_a(i + 1, kh, kw);
+      if (i + 1 < TPB) fn = load_a(i + 1, kh, kw);
       // pinned: the next tile's reads issue ahead of this tile's MFMAs (left alone, the scheduler
       // waits on each read right before its MFMAs: the LDS latency was exposed every tile)
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (STUDY == 1) {  // no MFMA
-        acc[i][0] += (float)fa.p[0][0] + (float)fa.p[1][1] + (float)fa.p[2][2] + (float)wb.p[0][0];
-      } else {
-        acc[i] = x9_mma<NPROD>(fa, wb, acc[i]);
-      }
+      acc[i] = x9_mma<NPROD>(fa, wb, acc[i]);
       __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < TPB) fa = fn;
       if (s + 1 < ntap) acc[i] = f4neg(acc[i]);
@@ -938,13 +934,6 @@ __device__ __forceinline__ void f32x_conv2_dgrad_block(
   if ((ntap - 1) & 1) {  // wave-uniform: back to the partial sum's own sign
 #pragma unroll
     for (int i = 0; i < TPB; ++i) acc[i] = f4neg(acc[i]);
-  }
-  if constexpr (STUDY == 3) {  // no epilogue: keep the accumulators live
-    float z = 0.f;
-#pragma unroll
-    for (int i = 0; i < TPB; ++i) z += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
-    if (z == 12345.f) cpart[t] = z;
-    return;
   }
   // the epilogue's conv1 operands (as the native form; loaded after the tap loop, whose registers
   // the accumulators need): (nt, tile) pairs p = wave + 8k
@@ -1022,20 +1011,214 @@ __device__ __forceinline__ void f32x_conv2_dgrad_block(
   }
 }
 
-// conv2_bwd with the split-bf16 dgrad role (the wgrad role is the native form's)
-template <int TPB, int NPROD, int STUDY = 0>
+// ------------------------------------------------------------------------------------------ //
+// wgrad role on split-bf16 products: dW2[kh][kw][ci][co half] over an image group, as the native role
+// (M = 32 co, N = 32 ci per kw: five 32x32 tiles, K = pixels), on v_mfma_f32_32x32x16_bf16 with the
+// NPROD part products. Both operands are K-strided in their natural [pixel][channel] layouts, so they
+// are staged as bf16 planes of those layouts and read TRANSPOSED: ds_read_b64_tr_b16 delivers, per
+// 16-lane group, column i of four rows to lane i (bench_native/tr16_probe.hip), the rows' addresses
+// coming from the lanes -- so the kw shift of the a1 operand and the 14-pixel row wrap are just row
+// addresses, no copies. Per image: a1 padded rows kh .. kh + 13 ([252 pixels][32 ci] per plane) and
+// the dY2 channel half ([196 pixels + 16 zero rows][32 co]); 13 k chunks of 16 pixels, the 91 of a
+// 7-image group dealt round-robin over the 8 waves (chunk n * 13 + kc to wave (n * 13 + kc) % 8),
+// the next image's loads in registers during the current one. Sign-alternating accumulation as in
+// the dgrad role. The partial exchange and the slab writes are the native role's.
+constexpr int X6W_A1PL = 252 * 16;                      // dwords per a1 plane
+constexpr int X6W_DYPL = 212 * 16;                      // dwords per dY2 plane (16 zero rows)
+constexpr int X6W_LDS = (3 * X6W_A1PL + 3 * X6W_DYPL) * 4;   // 89,088 B
+static_assert(4 * 5 * 4 * 64 * 16 <= X6W_LDS, "split wgrad exchange fits the planes");
+typedef short x6w_v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 x6w_tr8(const uint32_t* row0, const uint32_t* row1) {
+  // two transposed reads: elements 0..3 from the first four rows, 4..7 from the next four
+  const x6w_v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) x6w_v4s*)row0);
+  const x6w_v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) x6w_v4s*)row1);
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+template <int NPROD>
+__device__ __forceinline__ f32x16 x6w_mma(const X9Frag& a, const X9Frag& b, f32x16 c) {
+  auto m = [](const bf16x8& x, const bf16x8& y, f32x16 acc) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
+  };
+  if constexpr (NPROD == 9) {
+    c = m(a.p[2], b.p[2], c);
+    c = m(a.p[2], b.p[1], c);
+    c = m(a.p[1], b.p[2], c);
+  }
+  c = m(a.p[2], b.p[0], c);
+  c = m(a.p[0], b.p[2], c);
+  c = m(a.p[1], b.p[1], c);
+  c = m(a.p[1], b.p[0], c);
+  c = m(a.p[0], b.p[1], c);
+  return m(a.p[0], b.p[0], c);
+}
+
+template <int NPROD>
+__device__ __forceinline__ void f32x_conv2_wgrad_block(int bid, const float* __restrict__ dY2,
+                                                       const float* __restrict__ a1, float* __restrict__ slab, int B,
+                                                       int ig, float* smf) {
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int grp = bid / 10, rem = bid - 10 * grp, kh = rem >> 1, ch = rem & 1;
+  const int img0 = ig * grp, nimg = min(ig, B - img0);
+  uint32_t* a1p = reinterpret_cast<uint32_t*>(smf);
+  uint32_t* dyp = a1p + 3 * X6W_A1PL;
+  // staging chunks (as the native role): i < 2016 an a1 chunk of the padded rows kh..kh+13, the rest
+  // dY2 chunks; the LDS dword offset of each chunk's 4 channels within a plane
+  int loff[7], soff[7];
+  bool lin[7], la1[7];
+#pragma unroll
+  for (int it = 0; it < 7; ++it) {
+    const int i = t + 512 * it;
+    if (i < 2016) {
+      const int ly = i / 144, r2 = i - 144 * ly, c = r2 >> 3, q4 = r2 & 7;
+      const int y = ly + kh - 2, xx = c - 2;
+      const bool in = y >= 0 && y < 14 && xx >= 0 && xx < 14;
+      loff[it] = ((in ? y : 0) * 14 + (in ? xx : 0)) * 32 + 4 * q4;
+      lin[it] = in;
+      la1[it] = true;
+      soff[it] = (ly * 18 + c) * 16 + 2 * q4;
+    } else {
+      const int j = i - 2016, q = j >> 3, q4 = j & 7;
+      loff[it] = q * 64 + 32 * ch + 4 * q4;
+      lin[it] = i < 3584;
+      la1[it] = false;
+      soff[it] = 3 * X6W_A1PL + q * 16 + 2 * q4;
+    }
+  }
+  auto load_img = [&](int b, float4 (&v)[7]) {
+    const float* pa = a1 + (int64_t)b * 6272;
+    const float* pd = dY2 + (int64_t)b * 12544;
+#pragma unroll
+    for (int it = 0; it < 7; ++it)
+      v[it] = mask_f4(*reinterpret_cast<const float4*>((la1[it] ? pa : pd) + (lin[it] ? loff[it] : 0)), lin[it]);
+  };
+  auto store_img = [&](const float4 (&v)[7]) {
+#pragma unroll
+    for (int it = 0; it < 7; ++it) {
+      if (t + 512 * it < 3584) {
+        uint2 h, m, l;
+        x9_split4(v[it], h, m, l);
+        const int pl = la1[it] ? X6W_A1PL : X6W_DYPL;
+        *reinterpret_cast<uint2*>(a1p + soff[it]) = h;
+        *reinterpret_cast<uint2*>(a1p + soff[it] + pl) = m;
+        *reinterpret_cast<uint2*>(a1p + soff[it] + 2 * pl) = l;
+      }
+    }
+  };
+  // the dY2 planes' 16 padding rows (pixels 196..211) are zero for the whole block
+  for (int i = t; i < 3 * 16 * 16; i += 512) dyp[(i / 256) * X6W_DYPL + 196 * 16 + (i & 255)] = 0u;
+  f32x16 acc[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
+  float4 v[7];
+  load_img(img0, v);
+  store_img(v);
+  __syncthreads();
+  // per-lane transposed-read geometry: group G (l >> 4) reads rows 8 (G >> 1) + 4 r + qq of the chunk,
+  // columns 16 (G & 1) + 4 p .. + 3 (lane 4 qq + p of the group)
+  const int G = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+  const int colw = 8 * (G & 1) + 2 * pp;  // dword offset of the lane's 4 columns within a 64-byte row
+  int nch = 0;                             // this wave's chunks so far (sign alternation)
+  for (int n = 0; n < nimg; ++n) {
+    if (n + 1 < nimg) load_img(img0 + n + 1, v);
+    const int k0 = (((wave - 13 * n) % 8) + 8) % 8;
+    for (int kc = k0; kc < 13; kc += 8) {  // wave-uniform
+      const bool neg = nch & 1;
+      // rows (pixels) of this lane's two transposed reads
+      const int qa = 16 * kc + 8 * (G >> 1) + qq, qb = qa + 4;
+      X9Frag fa;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        fa.p[pl] = x6w_tr8(dyp + pl * X6W_DYPL + qa * 16 + colw, dyp + pl * X6W_DYPL + qb * 16 + colw);
+      if (neg) fa = x9_neg(fa);
+      const int ca = min(qa, 195), cb = min(qb, 195);  // (padding pixels: dY2 is zero there)
+      const int pa = (ca / 14) * 18 + ca % 14, pb = (cb / 14) * 18 + cb % 14;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        X9Frag fb;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          fb.p[pl] = x6w_tr8(a1p + pl * X6W_A1PL + (pa + kw) * 16 + colw, a1p + pl * X6W_A1PL + (pb + kw) * 16 + colw);
+        acc[kw] = x6w_mma<NPROD>(fa, fb, acc[kw]);
+      }
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) acc[kw] = -acc[kw];
+      ++nch;
+    }
+    if (n + 1 < nimg) {
+      __syncthreads();  // every wave is done with this image's planes
+      store_img(v);
+      __syncthreads();
+    }
+  }
+  if (nch & 1) {  // one flip per chunk: after an odd number the sums carry a minus sign
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) acc[kw] = -acc[kw];
+  }
+  __syncthreads();  // the planes are dead: the exchange reuses them
+  // partial exchange and slab writes: the native role's
+  float4* xr = reinterpret_cast<float4*>(smf);
+  if (wave >= 4) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        xr[(((wave - 4) * 5 + kw) * 4 + g) * 64 + lane] =
+            make_float4(acc[kw][4 * g], acc[kw][4 * g + 1], acc[kw][4 * g + 2], acc[kw][4 * g + 3]);
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 o = xr[((wave * 5 + kw) * 4 + g) * 64 + lane];
+        acc[kw][4 * g] += o.x;
+        acc[kw][4 * g + 1] += o.y;
+        acc[kw][4 * g + 2] += o.z;
+        acc[kw][4 * g + 3] += o.w;
+      }
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        xr[((wave * 5 + kw) * 4 + g) * 64 + lane] =
+            make_float4(acc[kw][4 * g], acc[kw][4 * g + 1], acc[kw][4 * g + 2], acc[kw][4 * g + 3]);
+  }
+  __syncthreads();
+  for (int it = t; it < 1280; it += 512) {
+    const int kw = it >> 8, g = (it >> 6) & 3, ln = it & 63;
+    const float4 a = xr[((0 * 5 + kw) * 4 + g) * 64 + ln], b = xr[((1 * 5 + kw) * 4 + g) * 64 + ln];
+    const float4 c = xr[((2 * 5 + kw) * 4 + g) * 64 + ln], d = xr[((3 * 5 + kw) * 4 + g) * 64 + ln];
+    const float4 s = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                                 (a.w + b.w) + (c.w + d.w));
+    const int tap = kh * 5 + kw, ci = ln & 31, co = 32 * ch + 8 * g + 4 * (ln >> 5);
+    *reinterpret_cast<float4*>(slab + (int64_t)grp * 51200 + (tap * 32 + ci) * 64 + co) = s;
+  }
+}
+
+// conv2_bwd with both roles on split-bf16 products
+template <int TPB, int NPROD>
 __global__ void __launch_bounds__(512) f32x_conv2_bwd_kernel(
     const float* __restrict__ dY2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ x, const int* __restrict__ rows, int n_pool,
     const int64_t* __restrict__ state, float* __restrict__ cpart, float* __restrict__ slab, int B, int n_dg,
-    int n_wg, int ig, const float* __restrict__ zeros) {
+    int n_wg, int ig) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   if (bid < n_dg) {
-    f32x_conv2_dgrad_block<TPB, NPROD, STUDY>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
+    f32x_conv2_dgrad_block<TPB, NPROD>(bid, dY2, w2, a1, idx1, x, rows, n_pool, state, cpart, B, smf);
     return;
   }
-  f32_conv2_wgrad_block(xcd_contiguous(bid, n_dg, n_dg + n_wg), dY2, a1, slab, B, ig, smf, zeros);
+  f32x_conv2_wgrad_block<NPROD>(xcd_contiguous(bid, n_dg, n_dg + n_wg), dY2, a1, slab, B, ig, smf);
 }
 
 template <int TPB, int NPASS = 1, bool FRAG = false>
@@ -1279,12 +1462,14 @@ static int conv2b_tpb(int B) {
 static bool conv2b_one_round(int B) { return 2 * conv2b_tpb(B) <= 10; }
 static int conv2b_block_tiles(int B) { return conv2b_one_round(B) ? 2 * conv2b_tpb(B) : conv2b_tpb(B); }
 static int conv2b_images(int B) { return conv2b_one_round(B) ? CBF_IG2 : CBF_IG; }
-// The split-bf16 dgrad role (f32x_conv2_bwd_kernel) does a tile in ~2/5 of the native MFMA time, so
-// it takes blocks of up to 12 tiles (the LDS holds their three planes: X6D_MAXR rows) and the wgrad
-// role the CUs it leaves (images per group chosen so both roles fit one round of blocks).
+// The split-bf16 roles (f32x_conv2_bwd_kernel): dgrad blocks of up to 10 tiles, the wgrad role the
+// CUs they leave (images per group chosen so both roles fit one round of blocks). Measured at B = 100
+// (profiles/r06/conv2_bwd_split_balance_r06q2.txt): 10 tiles + 8-image groups (123 + 130 blocks)
+// 34.1 us; 12 + 7 (103 + 150) 35.3 us; 11 tiles needs 7-image groups to stay in one round of blocks
+// (262 blocks: 54.9 us) or 8 (36.8 us).
 static int conv2bx_tiles(int B) {
   const int nt = (196 * B + 15) / 16;
-  return std::min(12, std::max(1, (nt + 99) / 100));
+  return std::min(10, std::max(1, (nt + 99) / 100));
 }
 static int conv2bx_images(int B) {
   const int nt = (196 * B + 15) / 16, tpb = conv2bx_tiles(B), n_dg = (nt + tpb - 1) / tpb;
@@ -1447,22 +1632,17 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
       TORCH_CHECK(r1 - r0 <= X6D_MAXR && P1 / 196 - P0 / 196 <= 1, "f32_conv2_bwd: dgrad tile span exceeds the LDS planes");
     }
     auto stream = c10::hip::getCurrentHIPStream().stream();
-    const int lds = std::max(X6D_LDS, CBF_LDS_WG);
-    const float* zl = f32_zero_line(stream);
+    const int lds = std::max(X6D_LDS, X6W_LDS);
     auto launch = [&](auto kern) {
       hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      const int role = env_knob("MIHVD_C2BX_ROLE", 0);  // STUDY: 1 dgrad blocks only, 2 wgrad only
-      const int ndg = role == 2 ? 0 : n_dg, nwg = role == 1 ? 0 : 10 * ngrp;
-      kern<<<ndg + nwg, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
-                                            idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
-                                            cpart.data_ptr<float>(), slab.data_ptr<float>(), B, ndg, nwg, ig, zl);
+      kern<<<n_dg + 10 * ngrp, 512, lds, stream>>>(dY2.data_ptr<float>(), w2.data_ptr<float>(), a1.data_ptr<float>(),
+                                                   idx1.data_ptr<uint8_t>(), x.data_ptr<float>(), rp, n_pool, sp,
+                                                   cpart.data_ptr<float>(), slab.data_ptr<float>(), B, n_dg, 10 * ngrp,
+                                                   ig);
     };
 #define C2BX_CASE(T)                                                      \
   case T:                                                                 \
     if (products == 9) launch(f32x_conv2_bwd_kernel<T, 9>);               \
-    else if (env_knob("MIHVD_C2BX_STUDY", 0) == 1) launch(f32x_conv2_bwd_kernel<T, 6, 1>); \
-    else if (env_knob("MIHVD_C2BX_STUDY", 0) == 2) launch(f32x_conv2_bwd_kernel<T, 6, 2>); \
-    else if (env_knob("MIHVD_C2BX_STUDY", 0) == 3) launch(f32x_conv2_bwd_kernel<T, 6, 3>); \
     else launch(f32x_conv2_bwd_kernel<T, 6>);                             \
     break;
     switch (tpb) {
@@ -1475,10 +1655,8 @@ void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor
       C2BX_CASE(7)
       C2BX_CASE(8)
       C2BX_CASE(9)
-      C2BX_CASE(10)
-      C2BX_CASE(11)
       default:
-        C2BX_CASE(12)
+        C2BX_CASE(10)
     }
 #undef C2BX_CASE
     return;
