@@ -380,6 +380,11 @@ def main():
                      "each rank's exact dW3 rows over all samples (one fp32 GEMM) and Adam on its 1/N of the rows "
                      "-> RCCL all-gather of the updated fp32 rows (overlapping the next step's convolutions); RCCL "
                      "allreduce of the other fp32 gradients; every step, in the HIP graph")
+    elif tr.f32 and tr.data_plane() == "factor_rep":
+        comm_desc = ("fp32 replicated factor gather over RCCL: all-gather of every rank's fp32 a2 (behind conv2_fwd) "
+                     "and dz (behind the head) on a side stream beside fc1_fwd / head / fc1_bwd's dgrad -> every "
+                     "rank forms all of dW3 over the N B samples with Adam on every row (no gradient reduce-scatter, "
+                     "no row gather); RCCL allreduce of the other fp32 gradients; every step, in the HIP graph")
     elif tr.f32 and tr.shard_w3:
         comm_desc = ("RCCL reduce-scatter of dense/kernel's fp32 gradient by rows and each rank's Adam on its 1/N "
                      "of the rows on a side stream (overlapping the conv backward) -> RCCL all-gather of the "

@@ -150,7 +150,8 @@ __device__ __forceinline__ float f32_ld(const float* p) {
 template <bool COH>
 __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __restrict__ x, const int* __restrict__ rows,
                                                 int n_pool, const int64_t* state, const float* w1, const float* b1,
-                                                float* __restrict__ a1, uint8_t* __restrict__ idx1, int B, float* xim) {
+                                                float* __restrict__ a1, uint8_t* __restrict__ idx1, int B, float* xim,
+                                                const float* __restrict__ xpre = nullptr) {
   const int t = threadIdx.x;
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   // W1 and b1 first, pinned ahead of the image gather (left alone, the scheduler issued them after
@@ -166,8 +167,12 @@ __device__ __forceinline__ void f32_conv1_block(int q, int b, const float* __res
   }
   const float bias0 = f32_ld<COH>(b1 + lr), bias1 = f32_ld<COH>(b1 + 16 + lr);
   __builtin_amdgcn_sched_barrier(0);
+  // xpre: this step's batch, gathered ahead by the previous step's head (f32_head1k_kernel) or by
+  // f32_prime_kernel -- one load instead of the dependent counter -> rows -> image chain
   int row = b;
-  if (rows != nullptr) {
+  if (xpre != nullptr) {
+    x = xpre;
+  } else if (rows != nullptr) {
     int64_t step = 0;
     if (state) {
       if constexpr (COH) step = __hip_atomic_load(state + ST_FWD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -117,6 +117,104 @@ __global__ void __launch_bounds__(512) f32_factor_rows_kernel(const float* __res
 }
 constexpr int FAC_LDS = FAC_W * 8 * 64 * 16 + 16 * 128 * 4;  // 73,728 B: partial tiles + the row tile
 
+// ------------------------------------------------------------------------------------------ //
+// Replicated factor plane (small N: mihvd/parallel/factor.py factor_gather_all_): EVERY row of the
+// summed gradient from the all-gathered factors A = a2 [N][B][3136] and D = dz [N][B][1024],
+//   g[f][n] = sum_q sum_b A[q][b][f] D[q][b][n]   (segments q in rank order: the same sum on every rank)
+// with Adam applied from the accumulators to every row (the optimizer stays replicated: no row
+// gather afterwards). The wgrad role of f32_fc1_bwd's row form without its dgrad: one block per 16
+// rows of W3 (196 blocks), 8 waves of 128 columns in 8 chunks of 16; per segment the wave holds
+// that segment's a2 column in registers (the MFMA B operand) and stages each dz chunk through a
+// per-wave double buffer in LDS (A = dz^T, ds_read_b32 of 64 consecutive floats per MFMA:
+// conflict-free); v_mfma_f32_16x16x4_f32 with two alternating accumulators per chunk as in
+// f32_fc1_bwd (at N = 1 the result is bitwise that kernel's). In the last segment the chunk's Adam
+// follows its MFMAs, with p / m / v loaded two chunks ahead, so W3's update streams under the MFMAs.
+// ------------------------------------------------------------------------------------------ //
+template <int G, int KS, bool STORE>
+__global__ void __launch_bounds__(512) f32_factor_full_kernel(const float* __restrict__ A, const float* __restrict__ D,
+                                                              int N, int B, float* __restrict__ out, F32Adam ad) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  static_assert(KS <= 4 * G && KS > 4 * G - 4, "K steps cover the segment's last partial group");
+  constexpr int BUF = 16 * G * 16;  // floats per wave buffer: [16 G rows][16 columns]
+  constexpr int NS = 3;             // p / m / v register slots (two chunks ahead)
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
+  const int f0 = 16 * blockIdx.x, nb = 128 * wave;
+  float* buf0 = smf + wave * 2 * BUF;
+  const int64_t rowo = (int64_t)(f0 + lr) * 1024 + nb + 4 * lg;
+  const AdamCoef coef = f32_adam_coef(ad);
+  f32x4 tot[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) tot[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float a2r[KS];
+  float4 zst[G];
+  float4 pv[NS], mv[NS], vv[NS];
+  for (int seg = 0; seg < N; ++seg) {  // wave-uniform
+    const float* As = A + (int64_t)seg * B * 3136;
+    const float* Ds = D + (int64_t)seg * B * 1024;
+    const bool last = seg == N - 1;
+    auto load_z = [&](int c) {
+      const int n = nb + 16 * c + 4 * (lane & 3);
+#pragma unroll
+      for (int it = 0; it < G; ++it) {
+        const int b = (lane >> 2) + 16 * it;
+        zst[it] = mask_f4(*reinterpret_cast<const float4*>(Ds + (int64_t)min(b, B - 1) * 1024 + n), b < B);
+      }
+    };
+    auto load_pmv = [&](int c, int slot) {
+      const int64_t o = rowo + 16 * c;
+      pv[slot] = *reinterpret_cast<const float4*>(ad.p + o);
+      mv[slot] = *reinterpret_cast<const float4*>(ad.m + o);
+      vv[slot] = *reinterpret_cast<const float4*>(ad.v + o);
+    };
+    load_z(0);
+    if (last) {
+      load_pmv(0, 0);
+      load_pmv(1, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int b = 4 * s + lg;
+      a2r[s] = mask_f(As[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float* buf = buf0 + (c & 1) * BUF;
+#pragma unroll
+      for (int it = 0; it < G; ++it) {
+        const int row = (lane >> 2) + 16 * it;
+        *reinterpret_cast<float4*>(buf + row * 16 + 4 * (lane & 3)) = zst[it];
+      }
+      if (c + 1 < 8) load_z(c + 1);
+      if (last && c + 2 < 8) load_pmv(c + 2, (c + 2) % NS);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS writes before its reads
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
+#pragma unroll
+      for (int s = 0; s + 1 < KS; s += 2) {
+        w0 = mfma4(buf[(4 * s + lg) * 16 + lr], a2r[s], w0);
+        w1 = mfma4(buf[(4 * s + 4 + lg) * 16 + lr], a2r[s + 1], w1);
+      }
+      if constexpr (KS & 1) w0 = mfma4(buf[(4 * (KS - 1) + lg) * 16 + lr], a2r[KS - 1], w0);
+      tot[c] += w0 + w1;
+      if (last) {
+        const f32x4 g = tot[c];
+        float4 gg = make_float4(g[0], g[1], g[2], g[3]);
+        const int64_t o = rowo + 16 * c;
+        if constexpr (STORE) *reinterpret_cast<float4*>(out + o) = gg;
+        const int s3 = c % NS;
+        float4 pp = pv[s3], mm = mv[s3], vq = vv[s3];
+        adam4_f32(pp, mm, vq, gg, coef);
+        *reinterpret_cast<float4*>(ad.p + o) = pp;
+        *reinterpret_cast<float4*>(ad.m + o) = mm;
+        *reinterpret_cast<float4*>(ad.v + o) = vq;
+      }
+    }
+  }
+}
+constexpr int ffu_lds(int G) { return 8 * 2 * 16 * G * 16 * 4; }  // G = 7: 114,688 B
+
 static void fac_chk(const at::Tensor& t, int64_t numel, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.dtype() == at::kFloat && t.is_contiguous() && t.numel() == numel &&
                   ((uintptr_t)t.data_ptr() & 15) == 0,
@@ -168,6 +266,67 @@ void f32_factor_rows(const at::Tensor& a2c, const at::Tensor& dz, const c10::opt
   if (adam && store) launch(f32_factor_rows_kernel<true, true>);
   else if (adam) launch(f32_factor_rows_kernel<true, false>);
   else launch(f32_factor_rows_kernel<false, true>);
+}
+
+// Every row of dW3 over the N B all-gathered samples (segments of B, rank order) with Adam on
+// every row: a2 [N B][3136], dz [N B][1024], p / m / v the full dense/kernel [3136][1024]; out
+// (optional): the gradient.
+void f32_factor_full(const at::Tensor& a2, const at::Tensor& dz, int64_t B, const c10::optional<at::Tensor>& out,
+                     at::Tensor& p, at::Tensor& m, at::Tensor& v, const at::Tensor& state, double lr, double beta1,
+                     double beta2, double eps, double grad_scale, int64_t rule) {
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_factor_full: batch 1..128");
+  TORCH_CHECK(dz.dim() >= 2 && dz.size(-1) == 1024 && dz.numel() % (B * 1024) == 0, "f32_factor_full: dz [N B][1024]");
+  const int64_t N = dz.numel() / (B * 1024);
+  TORCH_CHECK(N >= 1 && N <= 64, "f32_factor_full: 1..64 segments");
+  fac_chk(dz, N * B * 1024, "f32_factor_full: dz");
+  fac_chk(a2, N * B * 3136, "f32_factor_full: a2");
+  fac_chk(p, 3136 * 1024, "f32_factor_full: p");
+  fac_chk(m, 3136 * 1024, "f32_factor_full: m");
+  fac_chk(v, 3136 * 1024, "f32_factor_full: v");
+  TORCH_CHECK(state.is_cuda() && state.dtype() == at::kLong && state.numel() >= ST_WORDS, "f32_factor_full: state");
+  const bool store = out.has_value() && out->defined();
+  if (store) fac_chk(*out, 3136 * 1024, "f32_factor_full: out");
+  F32Adam ad;
+  ad.p = p.data_ptr<float>();
+  ad.m = m.data_ptr<float>();
+  ad.v = v.data_ptr<float>();
+  ad.state = state.data_ptr<int64_t>();
+  ad.lr = (float)lr;
+  ad.b1 = (float)beta1;
+  ad.b2 = (float)beta2;
+  ad.eps = (float)eps;
+  ad.gscale = (float)grad_scale;
+  ad.rule = (int)rule;
+  float* op = store ? out->data_ptr<float>() : nullptr;
+  const int G = (int)((B + 15) / 16);
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  auto launch = [&](auto kern) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ffu_lds(G));
+    kern<<<196, 512, ffu_lds(G), stream>>>(a2.data_ptr<float>(), dz.data_ptr<float>(), (int)N, (int)B, op, ad);
+  };
+  // the exact K steps of the headline batch (B = 97..100: 25), as f32_fc1_bwd
+  if (G == 7 && (B + 3) / 4 == 25) {
+    if (store) launch(f32_factor_full_kernel<7, 25, true>);
+    else launch(f32_factor_full_kernel<7, 25, false>);
+    return;
+  }
+#define FFU_CASE(GG)                                                  \
+  case GG:                                                            \
+    if (store) launch(f32_factor_full_kernel<GG, 4 * GG, true>);      \
+    else launch(f32_factor_full_kernel<GG, 4 * GG, false>);           \
+    break;
+  switch (G) {
+    FFU_CASE(1)
+    FFU_CASE(2)
+    FFU_CASE(3)
+    FFU_CASE(4)
+    FFU_CASE(5)
+    FFU_CASE(6)
+    FFU_CASE(7)
+    default:
+      FFU_CASE(8)
+  }
+#undef FFU_CASE
 }
 
 }  // namespace mihvd

@@ -80,7 +80,7 @@ __device__ __forceinline__ void f32_w2_frag_block(int blk, const float* __restri
 __global__ void __launch_bounds__(256) f32_conv1_kernel(
     const float* __restrict__ x, const int* __restrict__ rows, int n_pool, const int64_t* __restrict__ state,
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ a1, uint8_t* __restrict__ idx1,
-    int B, const float* __restrict__ w2, float* __restrict__ w2f, CollRole coll) {
+    int B, const float* __restrict__ w2, float* __restrict__ w2f, CollRole coll, const float* __restrict__ xpre) {
   __shared__ float xim[32 * 32];  // 28 x 28 image with a 2-pixel zero halo
   const int cb = coll.nblk;
   if ((int)blockIdx.x < cb) {
@@ -96,7 +96,22 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
   // the images whose conv2_fwd blocks run on XCD x (same mapping there), so conv2_fwd's staging
   // reads hit that XCD's L2 instead of the MALL
   const int L = xcd_contiguous(id, 0, 4 * B);
-  f32_conv1_block<false>(L & 3, L >> 2, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim);
+  f32_conv1_block<false>(L & 3, L >> 2, x, rows, n_pool, state, w1, b1, a1, idx1, B, xim, xpre);
+}
+
+// The batch of step state[ST_FWD] gathered from the resident set into xpre [B][784] (and its labels
+// into ypre [B]): the start of a chain that every f32_head1k_kernel continues for the next step, so
+// conv1 reads its images with one load. Run whenever the counter, the epoch order or the set change
+// outside a step (FusedMNISTTrainer._prime_batch).
+__global__ void __launch_bounds__(256) f32_prime_kernel(const float* __restrict__ x, const int64_t* __restrict__ labels,
+                                                        const int* __restrict__ rows, int n_pool,
+                                                        const int64_t* __restrict__ state, int B,
+                                                        float* __restrict__ xpre, int* __restrict__ ypre) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int64_t step = state[ST_FWD];
+  const int row = rows[(int)((step * (int64_t)B + b) % n_pool)];
+  if (t < 196) reinterpret_cast<float4*>(xpre + (int64_t)b * 784)[t] = reinterpret_cast<const float4*>(x + (int64_t)row * 784)[t];
+  if (t == 196) ypre[b] = (int)labels[row];
 }
 
 // ------------------------------------------------------------------------------------------ //
@@ -709,11 +724,21 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
     float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B,
-    float* __restrict__ stats_acc) {
+    float* __restrict__ stats_acc, const float* __restrict__ xsrc, float* __restrict__ xpre, int* __restrict__ ypre) {
   __shared__ float red[16][10];
   __shared__ float dl[10];
   const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = __builtin_amdgcn_readfirstlane(n >> 6);
   const int64_t step = state ? state[ST_FWD] : 0;
+  // resident set (ypre != nullptr): this step's label was gathered ahead (ypre[b]); waves 1..4 gather
+  // the NEXT step's image into xpre[b] (its conv1 has read this step's) and wave 0 its label, behind
+  // this step's use of ypre[b]
+  const bool pre = ypre != nullptr;
+  int row_next = 0;
+  if (pre && (wave == 0 || (n >= 64 && n < 64 + 196)))
+    row_next = rows[(int)(((step + 1) * (int64_t)B + b) % n_pool)];
+  if (pre && n >= 64 && n < 64 + 196)
+    reinterpret_cast<float4*>(xpre + (int64_t)b * 784)[n - 64] =
+        reinterpret_cast<const float4*>(xsrc + (int64_t)row_next * 784)[n - 64];
   float parts[F1F_KS];
 #pragma unroll
   for (int s = 0; s < F1F_KS; ++s) parts[s] = zpart[((int64_t)s * B + b) * 1024 + n];
@@ -727,10 +752,16 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
   const float bias = b3[n];
   int y = 0;
   float bias4 = 0.f;  // b4 of lane c (wave 0), loaded with the other operands instead of behind the barrier
+  int y_next = 0;
   if (wave == 0) {
-    int row = b;
-    if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
-    y = (int)labels[row];
+    if (pre) {
+      y = ypre[b];
+      y_next = (int)labels[row_next];
+    } else {
+      int row = b;
+      if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
+      y = (int)labels[row];
+    }
     bias4 = b4[min(lane, 9)];
   }
   float z = bias;
@@ -772,6 +803,7 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
         stats_acc[b * 2 + 1] += (am == y) ? 1.f : 0.f;
       }
       if (b == 0 && state != nullptr) state[ST_OPT] += 1;
+      if (pre) ypre[b] = y_next;  // (this step's ypre[b] was consumed above: y feeds the loss)
     }
   }
   __syncthreads();
@@ -804,7 +836,8 @@ static const int* rows_ptr(const c10::optional<at::Tensor>& rows, int n_pool, in
 
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
-                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll) {
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll,
+                   const c10::optional<at::Tensor>& xpre) {
   const int B = a1.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_conv1_fwd: batch 1..128");
   const CollRole cr = xgmi_role_lookup(coll);
@@ -820,6 +853,11 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
   const int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
   auto stream = c10::hip::getCurrentHIPStream().stream();
   // with w2 and w2frag: 4 x 7 more blocks write the W2 fragment copies for the conv2 launches
+  const float* xp = nullptr;
+  if (xpre.has_value() && xpre->defined()) {
+    check_f32(*xpre, (int64_t)B * 784, "f32_conv1_fwd: xpre [B][784]");
+    xp = xpre->data_ptr<float>();
+  }
   const bool frag = w2.has_value() && w2->defined() && w2frag.has_value() && w2frag->defined();
   if (frag) {
     check_f32(*w2, 51200, "f32_conv1_fwd: w2");
@@ -830,7 +868,23 @@ void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, c
   f32_conv1_kernel<<<dim3(cr.nblk + 4 * B + (frag ? 4 * W2F_BLOCKS_Y : 0)), 256, 0, stream>>>(
       x.data_ptr<float>(), rp, n_pool, sp, w1.data_ptr<float>(), b1.data_ptr<float>(), a1.data_ptr<float>(),
       idx1.data_ptr<uint8_t>(), B, frag ? w2->data_ptr<float>() : nullptr, frag ? w2frag->data_ptr<float>() : nullptr,
-      cr);
+      cr, xp);
+}
+
+void f32_prime_batch(const at::Tensor& x, const at::Tensor& labels, const at::Tensor& rows, const at::Tensor& state,
+                     at::Tensor& xpre, at::Tensor& ypre) {
+  const int B = xpre.size(0);
+  TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_prime_batch: batch 1..128");
+  TORCH_CHECK(x.is_cuda() && x.dtype() == at::kFloat && x.is_contiguous() && x.size(-1) == 784, "f32_prime_batch: x");
+  const int n_pool = x.size(0);
+  TORCH_CHECK(labels.dtype() == at::kLong && labels.is_contiguous() && labels.size(0) == n_pool, "f32_prime_batch: labels");
+  TORCH_CHECK(rows.dtype() == at::kInt && rows.numel() == n_pool, "f32_prime_batch: rows int32 [n_pool]");
+  TORCH_CHECK(state.dtype() == at::kLong && state.numel() >= ST_WORDS, "f32_prime_batch: state");
+  check_f32(xpre, (int64_t)B * 784, "f32_prime_batch: xpre [B][784]");
+  TORCH_CHECK(ypre.dtype() == at::kInt && ypre.numel() == B && ypre.is_contiguous(), "f32_prime_batch: ypre int32 [B]");
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  f32_prime_kernel<<<B, 256, 0, stream>>>(x.data_ptr<float>(), labels.data_ptr<int64_t>(), rows.data_ptr<int>(), n_pool,
+                                          state.data_ptr<int64_t>(), B, xpre.data_ptr<float>(), ypre.data_ptr<int>());
 }
 
 // tiles per block of f32_conv2_fwd for batch B (about one block per CU), and the block count
@@ -986,7 +1040,9 @@ void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart, 
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
-                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc) {
+                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc,
+                      const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& xpre,
+                      const c10::optional<at::Tensor>& ypre) {
   const int B = h.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_head: batch 1..128");
   check_f32(zpart, (int64_t)F1F_KS * B * 1024, "f32_head: zpart");
@@ -1006,6 +1062,21 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   const int n_pool = labels.size(0);
   const int* rp = rows_ptr(rows, n_pool, B, "f32_head");
   int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
+  // the next step's batch gathered ahead (resident set): the set, its xpre and ypre buffers
+  const float* xs = nullptr;
+  float* xp = nullptr;
+  int* yp = nullptr;
+  if (ypre.has_value() && ypre->defined()) {
+    TORCH_CHECK(rp != nullptr && sp != nullptr, "f32_head: the batch gathered ahead needs rows and state");
+    TORCH_CHECK(x.has_value() && x->defined() && xpre.has_value() && xpre->defined(), "f32_head: ypre needs x and xpre");
+    TORCH_CHECK(x->is_cuda() && x->dtype() == at::kFloat && x->is_contiguous() && x->size(-1) == 784 &&
+                    x->size(0) == n_pool, "f32_head: x [n_pool][784]");
+    check_f32(*xpre, (int64_t)B * 784, "f32_head: xpre [B][784]");
+    TORCH_CHECK(ypre->dtype() == at::kInt && ypre->numel() == B && ypre->is_contiguous(), "f32_head: ypre int32 [B]");
+    xs = x->data_ptr<float>();
+    xp = xpre->data_ptr<float>();
+    yp = ypre->data_ptr<int>();
+  }
   TORCH_CHECK(rate >= 0.0 && rate < 1.0, "f32_head: dropout rate in [0, 1)");
   const uint32_t thresh = (uint32_t)(rate * 16777216.0);
   const float keep_scale = rate > 0.0 ? (float)(1.0 / (1.0 - rate)) : 1.f;
@@ -1013,7 +1084,7 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   f32_head1k_kernel<<<B, 1024, 0, stream>>>(
       zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(), b4.data_ptr<float>(),
       labels.data_ptr<int64_t>(), rp, n_pool, sp, (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(),
-      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc);
+      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc, xs, xp, yp);
 }
 
 }  // namespace mihvd

@@ -86,14 +86,19 @@ void multi_tensor_sgd(std::vector<at::Tensor> p, std::vector<at::Tensor> g, std:
 void bump_step_(at::Tensor& step);
 void f32_conv1_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    const at::Tensor& w1, const at::Tensor& b1, at::Tensor& a1, at::Tensor& idx1,
-                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll);
+                   const c10::optional<at::Tensor>& w2, const c10::optional<at::Tensor>& w2frag, int64_t coll,
+                   const c10::optional<at::Tensor>& xpre);
+void f32_prime_batch(const at::Tensor& x, const at::Tensor& labels, const at::Tensor& rows, const at::Tensor& state,
+                     at::Tensor& xpre, at::Tensor& ypre);
 void f32_conv2_fwd(const at::Tensor& a1, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& a2, at::Tensor& idx2,
                    const c10::optional<at::Tensor>& w2frag, int64_t products);
 void f32_fc1_fwd(const at::Tensor& a2, const at::Tensor& w3, at::Tensor& zpart, int64_t products);
 void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::Tensor& w4, const at::Tensor& b4,
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
-                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc);
+                      at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc,
+                      const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& xpre,
+                      const c10::optional<at::Tensor>& ypre);
 void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
                  const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
                  at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
@@ -106,6 +111,9 @@ void f32_factor_rows(const at::Tensor& a2c, const at::Tensor& dz, const c10::opt
                      const c10::optional<at::Tensor>& p, const c10::optional<at::Tensor>& m,
                      const c10::optional<at::Tensor>& v, const c10::optional<at::Tensor>& state, double lr,
                      double beta1, double beta2, double eps, double grad_scale, int64_t rule);
+void f32_factor_full(const at::Tensor& a2, const at::Tensor& dz, int64_t B, const c10::optional<at::Tensor>& out,
+                     at::Tensor& p, at::Tensor& m, at::Tensor& v, const at::Tensor& state, double lr, double beta1,
+                     double beta2, double eps, double grad_scale, int64_t rule);
 void f32_conv_reduce(const at::Tensor& slab, const at::Tensor& cpart, const at::Tensor& db2p, at::Tensor& gW2,
                      at::Tensor& gW1, at::Tensor& gb1, at::Tensor& gb2, const c10::optional<at::Tensor>& params,
                      const c10::optional<at::Tensor>& grads, const c10::optional<at::Tensor>& m,
@@ -289,8 +297,12 @@ void mt_sgd_op(at::TensorList p, at::TensorList g, at::TensorList bufs, double l
 }
 void bump_step_op(Tensor step) { mihvd::bump_step_(step); }
 void f32_conv1_op(const Tensor& x, const OptT& rows, const OptT& state, const Tensor& w1, const Tensor& b1, Tensor a1,
-                  Tensor idx1, const OptT& w2, const OptT& w2frag, int64_t coll) {
-  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag, coll);
+                  Tensor idx1, const OptT& w2, const OptT& w2frag, int64_t coll, const OptT& xpre) {
+  mihvd::f32_conv1_fwd(x, rows, state, w1, b1, a1, idx1, w2, w2frag, coll, xpre);
+}
+void f32_prime_op(const Tensor& x, const Tensor& labels, const Tensor& rows, const Tensor& state, Tensor xpre,
+                  Tensor ypre) {
+  mihvd::f32_prime_batch(x, labels, rows, state, xpre, ypre);
 }
 void f32_conv2_op(const Tensor& a1, const Tensor& w2, const Tensor& b2, Tensor a2, Tensor idx2, const OptT& w2frag,
                   int64_t products) {
@@ -301,8 +313,9 @@ void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart, int64_t pr
 }
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
-                 Tensor stats, const OptT& stats_acc) {
-  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, stats_acc);
+                 Tensor stats, const OptT& stats_acc, const OptT& x, const OptT& xpre, const OptT& ypre) {
+  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, stats_acc, x, xpre,
+                          ypre);
 }
 void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, const Tensor& h, const Tensor& dlog,
                     Tensor w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, const OptT& m3,
@@ -320,6 +333,11 @@ void f32_factor_rows_op(const Tensor& a2c, const Tensor& dz, const OptT& out, co
                         const OptT& v, const OptT& state, double lr, double beta1, double beta2, double eps,
                         double grad_scale, int64_t rule) {
   mihvd::f32_factor_rows(a2c, dz, out, p, m, v, state, lr, beta1, beta2, eps, grad_scale, rule);
+}
+void f32_factor_full_op(const Tensor& a2, const Tensor& dz, int64_t B, const OptT& out, Tensor p, Tensor m, Tensor v,
+                        const Tensor& state, double lr, double beta1, double beta2, double eps, double grad_scale,
+                        int64_t rule) {
+  mihvd::f32_factor_full(a2, dz, B, out, p, m, v, state, lr, beta1, beta2, eps, grad_scale, rule);
 }
 void f32_conv_reduce_op(const Tensor& slab, const Tensor& cpart, const Tensor& db2p, Tensor gW2, Tensor gW1, Tensor gb1,
                         Tensor gb2, const OptT& params, const OptT& grads, const OptT& m, const OptT& v,
@@ -392,12 +410,13 @@ TORCH_LIBRARY(mihvd, m) {
         "float weight_decay, bool nesterov, bool first, float grad_scale) -> ()");
   m.def("bump_step_(Tensor(a!) step) -> ()");
   m.def("f32_conv1_fwd(Tensor x, Tensor? rows, Tensor? state, Tensor w1, Tensor b1, Tensor(a!) a1, Tensor(b!) idx1, "
-        "Tensor? w2=None, Tensor(f!)? w2frag=None, int coll=-1) -> ()");
+        "Tensor? w2=None, Tensor(f!)? w2frag=None, int coll=-1, Tensor? xpre=None) -> ()");
+  m.def("f32_prime_batch(Tensor x, Tensor labels, Tensor rows, Tensor state, Tensor(a!) xpre, Tensor(b!) ypre) -> ()");
   m.def("f32_conv2_fwd(Tensor a1, Tensor w2, Tensor b2, Tensor(a!) a2, Tensor(b!) idx2, Tensor? w2frag=None, int products=0) -> ()");
   m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart, int products=0) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
-        "Tensor(e!)? stats_acc=None) -> ()");
+        "Tensor(e!)? stats_acc=None, Tensor? x=None, Tensor(f!)? xpre=None, Tensor(g!)? ypre=None) -> ()");
   m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor(w!) w3, Tensor(a!) dY2, "
         "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4, Tensor(m!)? m3=None, "
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
@@ -405,6 +424,8 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_factor_rows(Tensor a2c, Tensor dz, Tensor(a!)? out=None, Tensor(b!)? p=None, Tensor(c!)? m=None, "
         "Tensor(d!)? v=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0) -> ()");
+  m.def("f32_factor_full(Tensor a2, Tensor dz, int B, Tensor(a!)? out, Tensor(b!) p, Tensor(c!) m, Tensor(d!) v, "
+        "Tensor state, float lr, float beta1, float beta2, float eps, float grad_scale, int rule) -> ()");
   m.def("f32_conv2_bwd(Tensor dY2, Tensor w2, Tensor a1, Tensor idx1, Tensor x, Tensor? rows, Tensor? state, "
         "Tensor(a!) cpart, Tensor(b!) slab, Tensor? w2frag=None, int products=0) -> ()");
   m.def("f32_conv_reduce(Tensor slab, Tensor cpart, Tensor db2p, Tensor(a!) gW2, Tensor(b!) gW1, Tensor(c!) gb1, "
@@ -457,7 +478,9 @@ TORCH_LIBRARY_IMPL(mihvd, CUDA, m) {
   m.impl("multi_tensor_sgd", &mt_sgd_op);
   m.impl("bump_step_", &bump_step_op);
   m.impl("f32_conv1_fwd", &f32_conv1_op);
+  m.impl("f32_prime_batch", &f32_prime_op);
   m.impl("f32_factor_rows", &f32_factor_rows_op);
+  m.impl("f32_factor_full", &f32_factor_full_op);
   m.impl("f32_conv2_fwd", &f32_conv2_op);
   m.impl("f32_fc1_fwd", &f32_fc1_fwd_op);
   m.impl("f32_head_fwd_bwd", &f32_head_op);

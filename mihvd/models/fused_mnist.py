@@ -73,10 +73,11 @@ W3_START = SEGMENTS["dense/kernel"][0]  # [0, W3_START) = every gradient except 
 
 
 def f32_plane_mode() -> str:
-    """``MIHVD_F32_PLANE``: the fp32 sharded data plane — ``auto`` (default: select_data_plane times
-    the reduce-scatter and the factor-gather planes and keeps the faster), ``rs`` or ``factor``."""
+    """``MIHVD_F32_PLANE``: the fp32 data plane — ``auto`` (default: select_data_plane times the
+    reduce-scatter, the sharded and the replicated factor-gather planes and keeps the fastest), ``rs``,
+    ``factor`` (sharded) or ``factor_rep`` (replicated)."""
     v = os.environ.get("MIHVD_F32_PLANE", "auto").strip().lower()
-    return v if v in ("rs", "factor") else "auto"
+    return v if v in ("rs", "factor", "factor_rep") else "auto"
 
 
 def _check_tol() -> float:
@@ -411,6 +412,29 @@ class FusedMNISTTrainer:
                 self.a2_send = torch.empty(N, B, R, **f32)
                 self.a2_recv = torch.empty(N, B, R, **f32)
                 self.f32_factor = self.shard_w3 and f32_plane_mode() == "factor"
+            # replicated fp32 factor-gather plane (small N; MIHVD_F32_PLANE=factor_rep, or timed by
+            # select_data_plane): every rank all-gathers every rank's fp32 a2 and dz ([N][B][3136],
+            # [N][B][1024]: (N - 1) B 4160 floats arrive, 1.66 MB per peer at B = 100, on every link at
+            # once) and forms ALL of dW3 over the N B samples with Adam on every row
+            # (f32_factor_full): no reduce-scatter of the 12.8 MB gradient and no row gather, at
+            # N B / B times fc1's wgrad MFMA work. N = 2 moves 1.66 MB per link per step instead of the
+            # sharded planes' 12.85 MB.
+            self._f32_can_factor = self.collectives and compression == "none" and avg_or_sum
+            self.f32_factor_rep = False
+            if self._f32_can_factor:
+                N = self.world
+                self.a2_all32 = torch.empty(N, B, 3136, **f32)
+                if getattr(self, "dz_all32", None) is None:
+                    self.dz_all32 = torch.empty(N, B, 1024, **f32)
+                self.f32_factor_rep = not self.shard_w3 and f32_plane_mode() == "factor_rep"
+        # fp32 step on the resident set: the batch gathered one step ahead (xpre images, ypre labels)
+        # by the head kernel, so the next conv1 reads its images with one load instead of the dependent
+        # counter -> rows -> image chain; _xpre_valid: they hold the batch of the device counter's step
+        # (anything else that moves the counter, the epoch order or the set re-primes them)
+        self.xpre = torch.empty(B, 784, **f32) if self.f32 else None
+        self.ypre = torch.empty(B, device=dev, dtype=torch.int32) if self.f32 else None
+        self._xpre_valid = False
+        self.gather_ahead = self.f32  # (tests: False gathers in conv1 / head as the host-fed step does)
         self.x_buf = torch.zeros(B, 784, **f32)
         self.y_buf = torch.zeros(B, device=dev, dtype=torch.int64)
         # Keras fit (mihvd/keras.py): every step adds its (sum of losses, correct count) on the device
@@ -495,6 +519,7 @@ class FusedMNISTTrainer:
         self._shuffle = shuffle
         self._rng = np.random.default_rng(seed + 1000 * self.rank)
         self.rows = torch.empty(n, device=self.device, dtype=torch.int32)
+        self._xpre_valid = False
         self._reshuffle()
         self._epoch_steps = n // self.B
 
@@ -503,6 +528,7 @@ class FusedMNISTTrainer:
         compute stream (stream order keeps it behind every step still reading the old order), from
         one of two pinned host buffers, so an epoch boundary costs no host synchronisation."""
         n = self.X.shape[0]
+        self._xpre_valid = False  # the batch gathered ahead came from the old order
         perm = self._rng.permutation(n) if self._shuffle else np.arange(n)
         if not self.rows.is_cuda:
             self.rows.copy_(torch.from_numpy(perm.astype(np.int32)))
@@ -648,20 +674,31 @@ class FusedMNISTTrainer:
             main.wait_event(self._small_ev)
             self._small_ev = None
         wf = self.w2frag
+        pre = rows is not None and self.gather_ahead
+        if pre:
+            self._prime_batch()
+        else:
+            self._xpre_valid = False  # a host-fed step advances the counter
         # fp32 xGMI plane: the previous step's row gather (every peer's updated dense/kernel rows)
         # runs on the first blocks of this launch, beside conv1 (the next reader of W3 is fc1_fwd)
         coll = self._f32_gather_colaunch() if (self.collectives and self.shard_w3 and self.use_xgmi) else -1
         o.f32_conv1_fwd(x, rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), self.a1,
-                        self.idx1, w2, wf, coll=coll)
+                        self.idx1, w2, wf, coll=coll, xpre=self.xpre if pre else None)
         o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0],
                         products=self.f32_products)
+        rep_factor = self.collectives and self.f32_factor_rep
+        if rep_factor:  # replicated factor plane: every rank's a2, beside fc1_fwd / head / fc1_bwd
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                self._gather_factor(self.a2_all32, self.a2)
         if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None
         o.f32_fc1_fwd(self.a2, w3, self.zpart, products=self.f32_products)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
-                           stats_acc=self._stat_acc if self.track_stats else None)
+                           stats_acc=self._stat_acc if self.track_stats else None,
+                           x=x if pre else None, xpre=self.xpre if pre else None, ypre=self.ypre if pre else None)
         gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
                  G("conv_layer2/conv2d/bias"))
         if not self.collectives:
@@ -678,6 +715,8 @@ class FusedMNISTTrainer:
                               SEGMENTS["conv_layer2/conv2d/kernel"][0], SEGMENTS["conv_layer2/conv2d/bias"][0],
                               FC_START, W3_START, self.lr, b1, b2, self.eps, 1.0, self.rule)
             return
+        if rep_factor:
+            return self._launch_step_f32_factor_rep(x, rows, st, w2, wf, gconv)
         if self.shard_w3 and self.use_xgmi:
             return self._launch_step_f32_xgmi(x, rows, st, w2, wf, gconv)
         if self.shard_w3:
@@ -700,6 +739,57 @@ class FusedMNISTTrainer:
                             products=self.f32_products)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
         self._f32_small_tail(main, FC_START)
+
+    def _gather_factor(self, out, mine):
+        """out[q] <- rank q's ``mine`` (all-gather on the current stream: the framework communicator,
+        else the process group; at world 1 a copy)."""
+        import torch.distributed as dist
+
+        if self.ncomm is not None:
+            self.ncomm.all_gather_into(out, mine)
+        elif self.world == 1:
+            out[0].copy_(mine)
+        elif dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(out, mine)
+        else:  # host collectives (gloo)
+            dist.all_gather(list(out.unbind(0)), mine.clone())
+
+    def _launch_step_f32_factor_rep(self, x, rows, st, w2, wf, gconv):
+        """Rest of the fp32 step on the replicated factor-gather plane (after the head; the a2
+        all-gather was issued behind conv2_fwd):
+
+            main: fc1_bwd (dgrad only) |      | dW3 of all N B samples + Adam, every row | conv2_bwd |
+                                         wait   conv_reduce | AR(small) + Adam
+            side: AG(a2) ......... AG(dz) ^
+
+        Both all-gathers run beside fc1_fwd, the head and fc1_bwd's dgrad, and complete before
+        conv2_bwd (the one launch that holds every CU) starts; dense/kernel's update is replicated,
+        so nothing of it crosses the links after the step."""
+        o, G = self.ops, self.gview
+        main, side = torch.cuda.current_stream(self.device), self._side
+        b1, b2 = self.betas
+        side.wait_stream(main)  # the head wrote dz
+        with torch.cuda.stream(side):
+            self._gather_factor(self.dz_all32, self.dz)
+        o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, self.pview("dense/kernel"), self.dY2, self.db2p,
+                      G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
+        main.wait_stream(side)
+        s3 = slice(W3_START, FLAT_NUMEL)
+        o.f32_factor_full(self.a2_all32.view(-1, 3136), self.dz_all32.view(-1, 1024), self.B,
+                          G("dense/kernel") if self.keep_w3_grad else None, self.params[s3], self.m[s3], self.v[s3], st,
+                          self.lr, b1, b2, self.eps, 1.0 / self.world, self.rule)
+        o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
+                        products=self.f32_products)
+        o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
+        self._f32_small_tail(main, W3_START)
+
+    def _prime_batch(self):
+        """fp32, resident set: gather the batch of the device counter's step into xpre/ypre unless the
+        previous step's head already did (stream-ordered, no host synchronisation)."""
+        if self._xpre_valid or not self.gather_ahead:
+            return
+        self.ops.f32_prime_batch(self.X, self.Y, self.rows, self.state, self.xpre, self.ypre)
+        self._xpre_valid = True
 
     def _f32_small_tail(self, main, hi):
         """After the gradient reduction: allreduce of gradients [0, hi), their Adam update and the
@@ -1248,6 +1338,8 @@ class FusedMNISTTrainer:
             if primary:
                 self.graph = None
             return False
+        if self.f32:
+            self._prime_batch()  # eagerly: the captured steps start from a gathered batch
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -1303,6 +1395,8 @@ class FusedMNISTTrainer:
                 self.device_step()
             return
         self._maybe_reshuffle(k)
+        if self.f32:
+            self._prime_batch()  # (a reshuffle or a host-side change broke the chain: re-gather)
         with trace_range(f"mihvd.graph_replay[{k} steps]"):
             g.replay()
         if self.f32 and self.collectives and self.shard_w3 and self.use_xgmi:
@@ -1438,6 +1532,7 @@ class FusedMNISTTrainer:
         self.use_xgmi = bool(xgmi) and self.xplane is not None and not getattr(self, "_xplane_failed", False)
         self.set_sharding(shard)
         self.f32_factor = bool(factor) and self.f32 and self.shard_w3
+        self.f32_factor_rep = bool(factor) and self.f32 and not self.shard_w3 and getattr(self, "_f32_can_factor", False)
         self._graphs = {}
         self.graph = None
 
@@ -1456,6 +1551,7 @@ class FusedMNISTTrainer:
             self._refresh_shadow()
         self.shard_w3 = shard
         self.f32_factor = self.f32_factor and shard
+        self.f32_factor_rep = getattr(self, "f32_factor_rep", False) and not shard
         self._graphs = {}
         self.graph = None
 
@@ -1504,8 +1600,15 @@ class FusedMNISTTrainer:
             fmode = f32_plane_mode()
             if fmode == "factor":
                 cands = [("factor", True)]
-            elif fmode != "rs":
+            elif fmode != "rs" and fmode != "factor_rep":
                 cands.append(("factor", True))
+        if self.f32 and getattr(self, "_f32_can_factor", False) and False in shard_options:
+            # the replicated fp32 factor-gather plane (every row's dW3 from the gathered factors)
+            fmode = f32_plane_mode()
+            if fmode == "factor_rep":
+                cands = [("factor", False)]
+            elif fmode == "auto":
+                cands.append(("factor", False))
         host = self._host_collectives()
         # host (gloo) collectives cannot be captured or timed meaningfully: the candidates still run
         # (eagerly) for the consistency check below, and the first consistent candidate is kept
@@ -1554,7 +1657,7 @@ class FusedMNISTTrainer:
             d = (fin - ref).norm().item() / max(upd, 1e-30)
             d = d if math.isfinite(d) else float("inf")
             if plane == "factor":
-                fcons = d  # the fp32 factor plane: same exact sums in another order
+                fcons = max(d, fcons or 0.0)  # the fp32 factor planes: same exact sums in another order
             else:
                 cons[f"xgmi-{'shard' if sh else 'replicated'}"] = d
         if fcons is not None:
@@ -1630,6 +1733,7 @@ class FusedMNISTTrainer:
             self.rows.copy_(snap["rows"])
             self._rng.bit_generator.state = snap["rng"]
         self.global_step = snap["global_step"]
+        self._xpre_valid = False
         self._full_state_valid = True
         self._f32_gather_pending = False  # every rank's rows are the snapshot's
         self._refresh_shadow()  # (and the full W3 row shadow of the factor-gather plane)
@@ -1664,6 +1768,8 @@ class FusedMNISTTrainer:
             return "xgmi" if self.use_xgmi else "rccl"
         if self.f32 and self.f32_factor:
             return "factor"
+        if self.f32 and getattr(self, "f32_factor_rep", False):
+            return "factor_rep"
         if self.f32 and self.use_xgmi and self.shard_w3:
             return "xgmi"
         return "rccl"
@@ -1744,6 +1850,7 @@ class FusedMNISTTrainer:
             if 0 < bp < 1:
                 t = round(math.log(bp) / math.log(self.betas[0])) - 1
         self.state.copy_(torch.tensor([self.global_step, t, 0, 0], dtype=torch.int64))
+        self._xpre_valid = False
         self._refresh_shadow()
         self._full_state_valid = True
 
@@ -1765,4 +1872,5 @@ class FusedMNISTTrainer:
         from ..parallel.collectives import broadcast_object
 
         self.global_step = int(broadcast_object(self.global_step, root_rank))
+        self._xpre_valid = False
         self._refresh_shadow()

@@ -83,6 +83,8 @@ def main():
                      torch.empty(392, 1024, device="cuda"))
     fa1, fz1, fo1 = (torch.randn(B, 3136, device="cuda"), torch.randn(B, 1024, device="cuda"),
                      torch.empty(3136, 1024, device="cuda"))
+    fa2, fz2 = torch.randn(2 * B, 3136, device="cuda"), torch.randn(2 * B, 1024, device="cuda")
+    fa4, fz4 = torch.randn(4 * B, 3136, device="cuda"), torch.randn(4 * B, 1024, device="cuda")
     fp8, fm8, fv8 = (torch.zeros(392, 1024, device="cuda") for _ in range(3))
     fp1, fm1, fv1 = (torch.zeros(3136, 1024, device="cuda") for _ in range(3))
     slab0 = torch.empty(int(o.f32_wgrad_groups(B, 0)), 51200, device="cuda")
@@ -106,6 +108,12 @@ def main():
                                                  tr.rule, False),
         "conv1_fwd [+ W2 fragment copies]": lambda: o.f32_conv1_fwd(
             tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1, w2, w2frag),
+        "conv1_fwd [+ W2 fragments, batch gathered ahead]": lambda: o.f32_conv1_fwd(
+            tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1, w2, w2frag,
+            xpre=tr.xpre),
+        "head [+ next batch gathered]": lambda: o.f32_head_fwd_bwd(
+            tr.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), tr.Y, tr.rows, st, tr.seed, tr.dropout,
+            tr.h, tr.dz, tr.dlog, tr.stats, x=tr.X, xpre=tr.xpre, ypre=tr.ypre),
         "conv2_fwd [W2 fragment copy]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
                                                                 w2frag=w2frag[0]),
         "conv2_fwd [split-bf16 x9]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
@@ -127,6 +135,13 @@ def main():
                                                                   tr.eps, 0.125, tr.rule),
         "factor rows + Adam N=1 (HIP)": lambda: o.f32_factor_rows(fa1, fz1, None, fp1, fm1, fv1, st, 0.0, b1, b2,
                                                                   tr.eps, 1.0, tr.rule),
+        # the replicated factor plane's dW3 (every row, N segments of B samples) + Adam
+        "factor full + Adam N=1 (HIP)": lambda: o.f32_factor_full(fa1, fz1, B, None, fp1, fm1, fv1, st, 0.0, b1, b2,
+                                                                  tr.eps, 1.0, tr.rule),
+        "factor full + Adam N=2 (HIP)": lambda: o.f32_factor_full(fa2, fz2, B, None, fp1, fm1, fv1, st, 0.0, b1, b2,
+                                                                  tr.eps, 0.5, tr.rule),
+        "factor full + Adam N=4 (HIP)": lambda: o.f32_factor_full(fa4, fz4, B, None, fp1, fm1, fv1, st, 0.0, b1, b2,
+                                                                  tr.eps, 0.25, tr.rule),
         "conv2_bwd": lambda: o.f32_conv2_bwd(tr.dY2, w2, tr.a1, tr.idx1, tr.X, tr.rows, st, cpart0, slab0),
         "conv_reduce": lambda: o.f32_conv_reduce(tr.slab, tr.cpart, tr.db2p, *gconv),
         "conv_reduce+adam": lambda: o.f32_conv_reduce(

@@ -301,6 +301,43 @@ def test_f32_factor_rows_kernel(ops, NB, R):
     assert torch.equal(pa, pf) and torch.equal(ma, mf) and torch.equal(va, vf)
 
 
+@pytest.mark.parametrize("N,B", [(1, 100), (2, 100), (3, 100), (4, 50), (2, 7)])
+def test_f32_factor_full_kernel(ops, N, B):
+    """The replicated fp32 factor plane's dW3 (csrc/kernels/f32_factor.hip, f32_factor_full): every
+    row of sum_q a2_q^T dz_q over N segments of B samples against fp64, the fused Adam equal (bit for
+    bit) to adam_step on the stored gradient, and at N = 1 bitwise f32_fc1_bwd's fused wgrad + Adam."""
+    g = torch.Generator(device="cuda").manual_seed(17 * N + B)
+    a2 = torch.relu(torch.randn(N * B, 3136, device="cuda", generator=g))
+    dz = torch.randn(N * B, 1024, device="cuda", generator=g) * 0.01
+    out = torch.full((3136, 1024), float("nan"), device="cuda")
+    p = torch.randn(3136, 1024, device="cuda", generator=g) * 0.02
+    m = torch.randn(3136, 1024, device="cuda", generator=g).abs() * 1e-3
+    v = torch.randn(3136, 1024, device="cuda", generator=g).abs() * 1e-5
+    st = torch.tensor([5, 7, 0, 0], device="cuda", dtype=torch.int64)
+    pf, mf, vf = p.clone(), m.clone(), v.clone()
+    ops.f32_factor_full(a2, dz, B, out, pf, mf, vf, st, 1e-3, 0.9, 0.999, 1e-8, 1.0 / N, 0)
+    assert rel_err(out, a2.double().t() @ dz.double()) < 1e-6
+    ps, ms, vs = p.clone(), m.clone(), v.clone()
+    ops.adam_step(ps.view(-1), out.view(-1), ms.view(-1), vs.view(-1), None, st, 0, 1e-3, 0.9, 0.999, 1e-8, 1.0 / N, 0,
+                  0)
+    assert torch.equal(pf, ps) and torch.equal(mf, ms) and torch.equal(vf, vs)
+    pa, ma, va = p.clone(), m.clone(), v.clone()  # Adam only (the production launch)
+    ops.f32_factor_full(a2, dz, B, None, pa, ma, va, st, 1e-3, 0.9, 0.999, 1e-8, 1.0 / N, 0)
+    assert torch.equal(pa, pf) and torch.equal(ma, mf) and torch.equal(va, vf)
+    if N == 1:  # the wgrad role of the fused fc1_bwd, without its dgrad: the same chain, the same bits
+        idx2 = torch.zeros(B, 3136, device="cuda", dtype=torch.uint8)
+        h, dlog = torch.rand(B, 1024, device="cuda", generator=g), torch.randn(B, 10, device="cuda", generator=g)
+        dY2 = torch.empty(B, 196 * 64, device="cuda")
+        db2p = torch.empty(int(ops.f32_db2_rows(B)), 64, device="cuda")
+        gW3 = torch.empty(3136 * 1024, device="cuda")
+        pb, mb, vb = p.clone(), m.clone(), v.clone()
+        ops.f32_fc1_bwd(dz, a2, idx2, h, dlog, pb, dY2, db2p, gW3, torch.empty(1024, device="cuda"),
+                        torch.empty(10240, device="cuda"), torch.empty(10, device="cuda"), mb.view(-1), vb.view(-1), st,
+                        1e-3, 0.9, 0.999, 1e-8, 1.0, 0, True)
+        assert torch.equal(gW3.view(3136, 1024), out)
+        assert torch.equal(pb, pf) and torch.equal(mb, mf) and torch.equal(vb, vf)
+
+
 def _tf_adam_(p, grad, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
     """TF1 AdamOptimizer (tensorflow_mnist.py:130) in float64 on the host side of the test."""
     m.mul_(b1).add_(grad, alpha=1 - b1)
@@ -411,6 +448,47 @@ def test_f32_graph_replay_converges(ops):
     assert int(tr.state[0].item()) == tr.global_step and int(tr.state[1].item()) == tr.global_step
     assert tr.last_loss() < first * 0.5, (first, tr.last_loss())
     assert tr.last_accuracy() > 0.8
+
+
+def test_f32_batch_gathered_ahead_matches_direct_gather(ops):
+    """The resident-set step reads its batch gathered one step ahead (the previous head's xpre/ypre,
+    or f32_prime_batch after anything that breaks the chain): bitwise the same training as conv1 /
+    head gathering through counter -> rows themselves, across graph replays, epoch reshuffles inside
+    and between replays, a host-fed step, a snapshot restore and a checkpoint load."""
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    B = 100
+    (x, y), _ = synthetic_mnist(n_train=5 * B, n_test=10, seed=12)  # 5 steps per epoch
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    runs = []
+    for ahead in (True, False):
+        tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, seed=4, device="cuda", precision="fp32")
+        tr.gather_ahead = ahead
+        tr.set_device_dataset(X, Y, seed=9)
+        losses = [tr.device_step()["loss"].item() for _ in range(2)]
+        assert tr.build_graph(steps_per_replay=3, warmup=1)
+        for _ in range(4):
+            tr.run_graph()
+            losses.append(tr.last_loss())
+        tr.train_step(X[:B], Y[:B])
+        losses.append(tr.device_step()["loss"].item())
+        snap = tr._snapshot()
+        tr.run_graph()
+        tr._restore(snap)
+        tr.run_graph()
+        losses.append(tr.last_loss())
+        v = tr.variables()
+        tr.run_graph()
+        tr.load_variables(v)
+        tr.run_graph()
+        losses.append(tr.last_loss())
+        torch.cuda.synchronize()
+        runs.append((losses, tr.params.clone(), tr.m.clone(), tr.stats.clone()))
+    (la, pa, ma, sa), (lb, pb, mb, sb) = runs
+    assert la == lb
+    assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(sa, sb)
 
 
 def _f32_head_mask(ops, B, step, seed, rate=0.5):

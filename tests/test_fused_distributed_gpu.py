@@ -105,6 +105,27 @@ def test_f32_factor_plane_inside_hip_graph(tmp_path):
     assert abs(r["loss"] - r["loss_ref"]) < 1e-4 * max(1.0, abs(r["loss_ref"])), r
 
 
+def test_f32_factor_rep_plane_inside_hip_graph(tmp_path):
+    """The replicated fp32 factor-gather plane (MIHVD_F32_PLANE=factor_rep, unsharded optimizer) at
+    world 1 with the collectives forced on, on the native communicator: the a2 all-gather behind
+    conv2_fwd and the dz all-gather behind the head on the side stream, fc1_bwd's dgrad-only launch,
+    then every row's dW3 + Adam from the gathered factors (f32_factor_full), captured in 2 x 5-step
+    graphs and replayed. At one segment that kernel is fc1_bwd's own wgrad chain, so the replayed
+    steps equal the trainer without collectives bit for bit."""
+    _gpu()
+    env = dict(os.environ, MIHVD_FORCE_COLLECTIVES="1", PYTHONPATH=ROOT, MIHVD_BACKEND="nccl", MIHVD_SHARD_W3="0",
+               MIHVD_XGMI="off", MIHVD_TEST_PRECISION="fp32", MIHVD_COMM="native", MIHVD_F32_PLANE="factor_rep")
+    for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, WORKER, "rccl_graph", str(tmp_path)], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = json.loads((tmp_path / "rccl_graph.json").read_text())
+    assert r["captured"] and r["steps"] == r["pre_steps"] + 22, r
+    assert not r["shard"] and r["plane"] == "factor_rep" and r["native_comm"], r
+    assert r["bitwise"], r
+
+
 def test_fused_data_parallel_equivalence_two_ranks(tmp_path):
     """bf16 step, dW3 from all-gathered factors (its data plane) over two ranks."""
     _gpu()
@@ -230,7 +251,8 @@ def test_bench_flow_trains_at_8_ranks(tmp_path, n, prec):
 @pytest.mark.parametrize("n,prec,shard,xgmi,f32plane", [
     (8, "fp32", "1", "off", "rs"), (8, "fp32", "1", "off", "factor"),
     (8, "bf16", "1", "off", "rs"), (8, "bf16", "1", "on", "rs"),
-    (4, "fp32", "1", "on", "rs"), (8, "fp32", "1", "on", "rs")])
+    (4, "fp32", "1", "on", "rs"), (8, "fp32", "1", "on", "rs"),
+    (2, "fp32", "0", "off", "factor_rep"), (4, "fp32", "0", "off", "factor_rep")])
 def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, shard, xgmi, f32plane):
     """N ranks x B=50 sharing this GPU over gloo: the reduced gradient of the first step equals the
     sum of the N single-process gradients (gradient rel < 1e-4), the update equals TF1 Adam on their
@@ -254,6 +276,8 @@ def test_fused_data_parallel_equivalence_n_ranks(tmp_path, n, prec, shard, xgmi,
         assert o["shard"] == (shard == "1"), o
         if prec == "fp32" and shard == "1":
             assert o["plane"] == ("xgmi" if xgmi == "on" else "factor" if f32plane == "factor" else "rccl"), o
+        if f32plane == "factor_rep":
+            assert o["plane"] == "factor_rep", o
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])
