@@ -58,7 +58,10 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=0, help="fused: steps captured per HIP graph (0=auto)")
     ap.add_argument("--lead-steps", type=int, default=2, help="fused: steps of the short graph that starts every "
                     "run (0: none)")
-    ap.add_argument("--pool-batches", type=int, default=60, help="synthetic batches resident on device")
+    ap.add_argument("--pool-batches", type=int, default=600,
+                    help="synthetic batches resident on device per rank (600 x 100 = the 60,000 images of MNIST's "
+                         "training set the reference's ranks each iterate over: an epoch of 600 steps, reshuffled "
+                         "at its boundary)")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
     ap.add_argument("--precision", choices=["fp32", "bf16", "fp16"], default=os.environ.get("MIHVD_PRECISION", "fp32"),
                     help="fused: operand precision of the hand-written step. fp32 (default) = the reference's "

@@ -135,85 +135,109 @@ __global__ void __launch_bounds__(512) f32_factor_full_kernel(const float* __res
                                                               int N, int B, float* __restrict__ out, F32Adam ad) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   static_assert(KS <= 4 * G && KS > 4 * G - 4, "K steps cover the segment's last partial group");
-  constexpr int BUF = 16 * G * 16;  // floats per wave buffer: [16 G rows][16 columns]
-  constexpr int NS = 3;             // p / m / v register slots (two chunks ahead)
+  constexpr int BUF = 16 * G * 16;  // floats per buffer: [16 G samples][16 columns or rows]
+  constexpr int PA = 2;             // p / m / v chunks loaded ahead of their Adam
+  constexpr int NS = PA + 1;        // ... in a ring of register slots
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * blockIdx.x, nb = 128 * wave;
-  float* buf0 = smf + wave * 2 * BUF;
+  float* buf0 = smf + wave * 2 * BUF;  // this wave's dz chunk double buffer
+  float* abuf = smf + 16 * BUF;        // the block's a2 column of a segment, [sample][16 rows], double-buffered
   const int64_t rowo = (int64_t)(f0 + lr) * 1024 + nb + 4 * lg;
   const AdamCoef coef = f32_adam_coef(ad);
   f32x4 tot[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) tot[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float a2r[KS];
-  float4 zst[G];
+  // Operands run ahead of the MFMAs across segment boundaries: the dz chunks two ahead (two register
+  // stages), the next segment's a2 column (one LDS copy per block, read by all eight waves as the
+  // MFMA B operand) from chunk 4 on, p / m / v of the last segment two chunks ahead (its first two
+  // during the segment before it; three ahead spilled registers). Per chunk a wave's 25 MFMAs (~800 cycles) cannot cover an
+  // L2 round trip issued one chunk ahead.
+  float4 zs[2][G];
   float4 pv[NS], mv[NS], vv[NS];
-  for (int seg = 0; seg < N; ++seg) {  // wave-uniform
-    const float* As = A + (int64_t)seg * B * 3136;
+  auto load_z = [&](float4 (&z)[G], const float* Ds, int c) {
+    const int n = nb + 16 * c + 4 * (lane & 3);
+#pragma unroll
+    for (int it = 0; it < G; ++it) {
+      const int b = (lane >> 2) + 16 * it;
+      z[it] = mask_f4(*reinterpret_cast<const float4*>(Ds + (int64_t)min(b, B - 1) * 1024 + n), b < B);
+    }
+  };
+  // the a2 column of a segment: 16 G samples x 16 rows, 4 floats per thread (threads past it idle)
+  constexpr int ANT = (16 * G * 16) / 4;
+  float4 an = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load_a = [&](const float* As) {
+    if (t < ANT) {
+      const int b = t >> 2, r4 = 4 * (t & 3);
+      an = mask_f4(*reinterpret_cast<const float4*>(As + (int64_t)min(b, B - 1) * 3136 + f0 + r4), b < B);
+    }
+  };
+  auto store_a = [&](int slot) {
+    if (t < ANT) *reinterpret_cast<float4*>(abuf + slot * BUF + 4 * t) = an;
+  };
+  auto load_pmv = [&](int c) {
+    const int64_t o = rowo + 16 * c;
+    const int slot = c % NS;
+    pv[slot] = *reinterpret_cast<const float4*>(ad.p + o);
+    mv[slot] = *reinterpret_cast<const float4*>(ad.m + o);
+    vv[slot] = *reinterpret_cast<const float4*>(ad.v + o);
+  };
+  load_a(A);
+  load_z(zs[0], D, 0);
+  load_z(zs[1], D, 1);
+  if (N == 1) {
+#pragma unroll
+    for (int c = 0; c < PA; ++c) load_pmv(c);
+  }
+  store_a(0);
+  __syncthreads();
+  for (int seg = 0; seg < N; ++seg) {  // block-uniform
     const float* Ds = D + (int64_t)seg * B * 1024;
-    const bool last = seg == N - 1;
-    auto load_z = [&](int c) {
-      const int n = nb + 16 * c + 4 * (lane & 3);
-#pragma unroll
-      for (int it = 0; it < G; ++it) {
-        const int b = (lane >> 2) + 16 * it;
-        zst[it] = mask_f4(*reinterpret_cast<const float4*>(Ds + (int64_t)min(b, B - 1) * 1024 + n), b < B);
-      }
-    };
-    auto load_pmv = [&](int c, int slot) {
-      const int64_t o = rowo + 16 * c;
-      pv[slot] = *reinterpret_cast<const float4*>(ad.p + o);
-      mv[slot] = *reinterpret_cast<const float4*>(ad.m + o);
-      vv[slot] = *reinterpret_cast<const float4*>(ad.v + o);
-    };
-    load_z(0);
-    if (last) {
-      load_pmv(0, 0);
-      load_pmv(1, 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int b = 4 * s + lg;
-      a2r[s] = mask_f(As[(int64_t)min(b, B - 1) * 3136 + f0 + lr], b < B);
-    }
+    const float* Dn = Ds + (int64_t)B * 1024;
+    const float* as = abuf + (seg & 1) * BUF;
+    const bool last = seg == N - 1, more = seg + 1 < N, next_last = seg + 2 == N;
+    if (more) load_a(A + (int64_t)(seg + 1) * B * 3136);
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       float* buf = buf0 + (c & 1) * BUF;
 #pragma unroll
       for (int it = 0; it < G; ++it) {
         const int row = (lane >> 2) + 16 * it;
-        *reinterpret_cast<float4*>(buf + row * 16 + 4 * (lane & 3)) = zst[it];
+        *reinterpret_cast<float4*>(buf + row * 16 + 4 * (lane & 3)) = zs[c & 1][it];
       }
-      if (c + 1 < 8) load_z(c + 1);
-      if (last && c + 2 < 8) load_pmv(c + 2, (c + 2) % NS);
+      if (c + 2 < 8) load_z(zs[c & 1], Ds, c + 2);
+      else if (more) load_z(zs[c & 1], Dn, c + 2 - 8);
+      if (last && c + PA < 8) load_pmv(c + PA);
+      if (next_last && c >= 8 - PA) load_pmv(c - (8 - PA));
+      if (c == 4 && more) store_a((seg + 1) & 1);  // (the other buffer: nobody reads it this segment)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS writes before its reads
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
 #pragma unroll
       for (int s = 0; s + 1 < KS; s += 2) {
-        w0 = mfma4(buf[(4 * s + lg) * 16 + lr], a2r[s], w0);
-        w1 = mfma4(buf[(4 * s + 4 + lg) * 16 + lr], a2r[s + 1], w1);
+        w0 = mfma4(buf[(4 * s + lg) * 16 + lr], as[(4 * s + lg) * 16 + lr], w0);
+        w1 = mfma4(buf[(4 * s + 4 + lg) * 16 + lr], as[(4 * s + 4 + lg) * 16 + lr], w1);
       }
-      if constexpr (KS & 1) w0 = mfma4(buf[(4 * (KS - 1) + lg) * 16 + lr], a2r[KS - 1], w0);
+      if constexpr (KS & 1)
+        w0 = mfma4(buf[(4 * (KS - 1) + lg) * 16 + lr], as[(4 * (KS - 1) + lg) * 16 + lr], w0);
       tot[c] += w0 + w1;
       if (last) {
         const f32x4 g = tot[c];
         float4 gg = make_float4(g[0], g[1], g[2], g[3]);
         const int64_t o = rowo + 16 * c;
         if constexpr (STORE) *reinterpret_cast<float4*>(out + o) = gg;
-        const int s3 = c % NS;
-        float4 pp = pv[s3], mm = mv[s3], vq = vv[s3];
+        const int slot = c % NS;
+        float4 pp = pv[slot], mm = mv[slot], vq = vv[slot];
         adam4_f32(pp, mm, vq, gg, coef);
         *reinterpret_cast<float4*>(ad.p + o) = pp;
         *reinterpret_cast<float4*>(ad.m + o) = mm;
         *reinterpret_cast<float4*>(ad.v + o) = vq;
       }
     }
+    if (more) __syncthreads();  // the next a2 column is in LDS; every wave is done with this one
   }
 }
-constexpr int ffu_lds(int G) { return 8 * 2 * 16 * G * 16 * 4; }  // G = 7: 114,688 B
+constexpr int ffu_lds(int G) { return (8 * 2 + 2) * 16 * G * 16 * 4; }  // G = 7: 129,024 B
 
 static void fac_chk(const at::Tensor& t, int64_t numel, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.dtype() == at::kFloat && t.is_contiguous() && t.numel() == numel &&

@@ -518,34 +518,63 @@ class FusedMNISTTrainer:
         self.Y = Y[:n].to(self.device, torch.int64).contiguous()
         self._shuffle = shuffle
         self._rng = np.random.default_rng(seed + 1000 * self.rank)
+        self._next_perm = None
         self.rows = torch.empty(n, device=self.device, dtype=torch.int32)
         self._xpre_valid = False
         self._reshuffle()
         self._epoch_steps = n // self.B
+        self._prepare_next_perm()
+
+    def _draw_perm(self):
+        """The next epoch order from the set's RNG (``_rng_pre``: the RNG state before the draw)."""
+        import copy
+
+        n = self.X.shape[0]
+        self._rng_pre = copy.deepcopy(self._rng.bit_generator.state)
+        return self._rng.permutation(n) if self._shuffle else np.arange(n)
+
+    def _prepare_next_perm(self):
+        """Draw the next epoch's order now, on the host, while the GPU runs the steps just launched,
+        and upload it to ``_rows_next`` on a copy stream: the epoch boundary itself then costs one
+        device-to-device copy on the compute stream. Drawing and uploading at the boundary (a host
+        permutation and a pinned host-to-device copy whose DMA the compute queue waited for) left
+        the GPU idle for ~30 us in bench.py's 20-step timed region, where the boundary falls between
+        the lead graph and the long graph (profiles/r06/driver_form_reshuffle_gap_r06z.txt). The
+        same draws in the same order as drawing at the boundary."""
+        if self.X is None or getattr(self, "_next_perm", None) is not None:
+            return
+        self._next_perm = self._draw_perm()
+        if not self.rows.is_cuda:
+            return
+        n = self.rows.numel()
+        if getattr(self, "_pin", None) is None or self._pin.numel() != n:
+            self._pin = torch.empty(n, dtype=torch.int32).pin_memory()
+            self._rows_next = torch.empty_like(self.rows)
+            self._copy_stream = torch.cuda.Stream(device=self.device)
+        if getattr(self, "_next_ev", None) is not None:
+            self._next_ev.synchronize()  # the pinned buffer's last upload (done unless an order was dropped)
+        self._pin.numpy()[:] = self._next_perm
+        cs = self._copy_stream
+        cs.wait_stream(torch.cuda.current_stream(self.device))  # the last boundary's read of _rows_next
+        with torch.cuda.stream(cs):
+            self._rows_next.copy_(self._pin, non_blocking=True)
+            self._next_ev = torch.cuda.Event()
+            self._next_ev.record(cs)
 
     def _reshuffle(self):
-        """New epoch permutation of the resident dataset. The copy into ``rows`` is queued on the
-        compute stream (stream order keeps it behind every step still reading the old order), from
-        one of two pinned host buffers, so an epoch boundary costs no host synchronisation."""
-        n = self.X.shape[0]
+        """New epoch permutation of the resident dataset, copied into ``rows`` on the compute stream
+        (stream order keeps it behind every step still reading the old order) from the order
+        prepared and uploaded an epoch earlier (_prepare_next_perm)."""
         self._xpre_valid = False  # the batch gathered ahead came from the old order
-        perm = self._rng.permutation(n) if self._shuffle else np.arange(n)
+        if getattr(self, "_next_perm", None) is None:
+            self._prepare_next_perm()
+        perm = self._next_perm
+        self._next_perm = None
         if not self.rows.is_cuda:
             self.rows.copy_(torch.from_numpy(perm.astype(np.int32)))
             return
-        if getattr(self, "_pin", None) is None or self._pin[0].numel() != n:
-            self._pin = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(2)]
-            self._pin_ev = [None, None]
-            self._pin_i = 0
-        i = self._pin_i
-        self._pin_i ^= 1
-        if self._pin_ev[i] is not None:
-            self._pin_ev[i].synchronize()  # that buffer's copy (an epoch ago) has long finished
-        self._pin[i].numpy()[:] = perm
-        self.rows.copy_(self._pin[i], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self._pin_ev[i] = ev
+        self._next_ev.synchronize()  # the upload (issued an epoch ago) has long finished
+        self.rows.copy_(self._rows_next)
 
     # ----------------------------------------------------------------------------- step
     def _launch_step(self, x, rows, labels):
@@ -687,10 +716,8 @@ class FusedMNISTTrainer:
         o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0],
                         products=self.f32_products)
         rep_factor = self.collectives and self.f32_factor_rep
-        if rep_factor:  # replicated factor plane: every rank's a2, beside fc1_fwd / head / fc1_bwd
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                self._gather_factor(self.a2_all32, self.a2)
+        if rep_factor:  # replicated factor plane: every rank's a2 (on this stream: see below)
+            self._gather_factor(self.a2_all32, self.a2)
         if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None
@@ -756,24 +783,24 @@ class FusedMNISTTrainer:
 
     def _launch_step_f32_factor_rep(self, x, rows, st, w2, wf, gconv):
         """Rest of the fp32 step on the replicated factor-gather plane (after the head; the a2
-        all-gather was issued behind conv2_fwd):
+        all-gather ran behind conv2_fwd), one stream:
 
-            main: fc1_bwd (dgrad only) |      | dW3 of all N B samples + Adam, every row | conv2_bwd |
-                                         wait   conv_reduce | AR(small) + Adam
-            side: AG(a2) ......... AG(dz) ^
+            AG(a2) | fc1_fwd | head | AG(dz) | fc1_bwd (dgrad only) | dW3 of all N B samples + Adam,
+            every row | conv2_bwd | conv_reduce | AR(small) + Adam
 
-        Both all-gathers run beside fc1_fwd, the head and fc1_bwd's dgrad, and complete before
-        conv2_bwd (the one launch that holds every CU) starts; dense/kernel's update is replicated,
-        so nothing of it crosses the links after the step."""
+        dense/kernel's update is replicated, so nothing of it crosses the links after the step. The
+        all-gathers stay on the compute stream: forked onto a side stream inside the HIP graph (a2
+        beside fc1_fwd / head, dz beside fc1_bwd's dgrad) the step measured 149.9 us at forced world
+        1, its three cross-queue edges ~10 us each (fc1_fwd started 11.8 us after conv2_fwd,
+        fc1_bwd 11.0 us after the head, the join 9.5 us after fc1_bwd:
+        profiles/r06/timeline_f32_factor_rep_forked_world1_r06y.txt) -- more than the 22-33 us of
+        link time per step the fork could hide at N = 2."""
         o, G = self.ops, self.gview
-        main, side = torch.cuda.current_stream(self.device), self._side
+        main = torch.cuda.current_stream(self.device)
         b1, b2 = self.betas
-        side.wait_stream(main)  # the head wrote dz
-        with torch.cuda.stream(side):
-            self._gather_factor(self.dz_all32, self.dz)
+        self._gather_factor(self.dz_all32, self.dz)
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, self.pview("dense/kernel"), self.dY2, self.db2p,
                       G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
-        main.wait_stream(side)
         s3 = slice(W3_START, FLAT_NUMEL)
         o.f32_factor_full(self.a2_all32.view(-1, 3136), self.dz_all32.view(-1, 1024), self.B,
                           G("dense/kernel") if self.keep_w3_grad else None, self.params[s3], self.m[s3], self.v[s3], st,
@@ -1292,6 +1319,7 @@ class FusedMNISTTrainer:
         with trace_range("mihvd.fused_step"):
             self._launch_step(self.X, self.rows, self.Y)
             self._join()
+        self._prepare_next_perm()
         self.global_step += 1
         self._stat_steps += 1
         return {"loss": self.stats[:, 0].mean(), "accuracy": self.stats[:, 1].mean()}
@@ -1399,6 +1427,7 @@ class FusedMNISTTrainer:
             self._prime_batch()  # (a reshuffle or a host-side change broke the chain: re-gather)
         with trace_range(f"mihvd.graph_replay[{k} steps]"):
             g.replay()
+        self._prepare_next_perm()  # (host work while the replay runs)
         if self.f32 and self.collectives and self.shard_w3 and self.use_xgmi:
             self._f32_gather_pending = True  # the replay's last update: gathered by the next conv1
         self.global_step += k
@@ -1720,7 +1749,9 @@ class FusedMNISTTrainer:
         if self.rows is not None:  # the resident dataset's current epoch order and its RNG
             torch.cuda.synchronize(self.device)
             snap["rows"] = self.rows.clone()
-            snap["rng"] = copy.deepcopy(self._rng.bit_generator.state)
+            # (the state before a prepared next order was drawn: the restored run draws it again)
+            pre = self._rng_pre if getattr(self, "_next_perm", None) is not None else self._rng.bit_generator.state
+            snap["rng"] = copy.deepcopy(pre)
         return snap
 
     def _restore(self, snap: dict):
@@ -1732,6 +1763,7 @@ class FusedMNISTTrainer:
         if "rows" in snap and self.rows is not None:
             self.rows.copy_(snap["rows"])
             self._rng.bit_generator.state = snap["rng"]
+            self._next_perm = None
         self.global_step = snap["global_step"]
         self._xpre_valid = False
         self._full_state_valid = True
