@@ -491,6 +491,41 @@ def test_f32_batch_gathered_ahead_matches_direct_gather(ops):
     assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(sa, sb)
 
 
+def test_epoch_orders_drawn_ahead_follow_the_seeded_rng(ops):
+    """The epoch orders are drawn (and uploaded) one epoch ahead of their boundary: the sequence is
+    still the seeded RNG's permutations in order, and a snapshot taken with the next order already
+    drawn restores to the state before that draw (the restored run draws the same orders)."""
+    import numpy as np
+
+    from mihvd.models.fused_mnist import FusedMNISTTrainer
+    from mihvd.utils.data import synthetic_mnist
+
+    B, E = 100, 5
+    (x, y), _ = synthetic_mnist(n_train=E * B, n_test=10, seed=13)
+    X = torch.from_numpy(x.reshape(-1, 784)).float().cuda() / 255.0
+    Y = torch.from_numpy(y.astype("int64")).cuda()
+    tr = FusedMNISTTrainer(batch_size=B, lr=1e-3, seed=2, device="cuda", precision="fp32")
+    tr.set_device_dataset(X, Y, seed=9)
+    rng = np.random.default_rng(9)  # rank 0's epoch orders
+    want = [rng.permutation(E * B) for _ in range(4)]
+    rows = lambda: tr.rows.cpu().numpy()  # noqa: E731
+    assert np.array_equal(rows(), want[0])
+    snap = tr._snapshot()
+    for _ in range(E + 1):  # steps 0..5: the first step of the next epoch reshuffles first
+        tr.device_step()
+    assert np.array_equal(rows(), want[1])
+    for _ in range(E):  # steps 6..10
+        tr.device_step()
+    assert np.array_equal(rows(), want[2])
+    tr._restore(snap)
+    assert np.array_equal(rows(), want[0])
+    assert tr.build_graph(steps_per_replay=E, warmup=0)
+    tr.run_graph()
+    tr.run_graph()  # crosses the boundary: reshuffled before the replay
+    torch.cuda.synchronize()
+    assert np.array_equal(rows(), want[1])
+
+
 def _f32_head_mask(ops, B, step, seed, rate=0.5):
     """The fp32 head's dropout keep-mask for (seed, step): run it on all-positive pre-activations
     (zpart slabs of 1/14, so z = 1 + b3 = 1 everywhere) and read which h survived."""
