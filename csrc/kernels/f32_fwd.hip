@@ -733,18 +733,15 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
   // the NEXT step's image into xpre[b] (its conv1 has read this step's) and wave 0 its label, behind
   // this step's use of ypre[b]
   const bool pre = ypre != nullptr;
-  const bool xcopy = pre && n >= 64 && n < 64 + 196;
   int row_next = 0;
-  if (pre && (wave == 0 || xcopy)) row_next = rows[(int)(((step + 1) * (int64_t)B + b) % n_pool)];
+  if (pre && (wave == 0 || (n >= 64 && n < 64 + 196)))
+    row_next = rows[(int)(((step + 1) * (int64_t)B + b) % n_pool)];
+  if (pre && n >= 64 && n < 64 + 196)
+    reinterpret_cast<float4*>(xpre + (int64_t)b * 784)[n - 64] =
+        reinterpret_cast<const float4*>(xsrc + (int64_t)row_next * 784)[n - 64];
   float parts[F1F_KS];
 #pragma unroll
   for (int s = 0; s < F1F_KS; ++s) parts[s] = zpart[((int64_t)s * B + b) * 1024 + n];
-  // the next image's load behind this step's slab loads (its store waits for them anyway), so the
-  // slab sums of waves 1..4 do not wait for the counter -> rows -> image chain first (in front of
-  // them: head 4.96 -> 5.16 us in the step, profiles/r06/roofline_f32_gather_ahead_r06x.md)
-  __builtin_amdgcn_sched_barrier(0);
-  float4 xnext = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (xcopy) xnext = reinterpret_cast<const float4*>(xsrc + (int64_t)row_next * 784)[n - 64];
   float w[10];  // W4[n][0..9]: 40 bytes, 8-byte aligned
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -773,7 +770,6 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
   const bool keep = thresh24 == 0 || dropout_keep(seed, (uint32_t)step, (uint32_t)(b * 1024 + n), thresh24);
   const float hv = keep ? fmaxf(z, 0.f) * keep_scale : 0.f;
   h_out[(int64_t)b * 1024 + n] = hv;
-  if (xcopy) reinterpret_cast<float4*>(xpre + (int64_t)b * 784)[n - 64] = xnext;
 #pragma unroll
   for (int c = 0; c < 10; ++c) {
     const float sc = wave_sum(hv * w[c]);
