@@ -136,8 +136,8 @@ __global__ void __launch_bounds__(512) f32_factor_full_kernel(const float* __res
   extern __shared__ __attribute__((aligned(16))) float smf[];
   static_assert(KS <= 4 * G && KS > 4 * G - 4, "K steps cover the segment's last partial group");
   constexpr int BUF = 16 * G * 16;  // floats per buffer: [16 G samples][16 columns or rows]
-  constexpr int PA = 8;             // p / m / v chunks loaded ahead of their Adam
-  constexpr int NS = PA < 8 ? PA + 1 : 8;  // ... in a ring of register slots
+  constexpr int PA = 2;             // p / m / v chunks loaded ahead of their Adam
+  constexpr int NS = PA + 1;        // ... in a ring of register slots
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), lr = lane & 15, lg = lane >> 4;
   const int f0 = 16 * blockIdx.x, nb = 128 * wave;
   float* buf0 = smf + wave * 2 * BUF;  // this wave's dz chunk double buffer
