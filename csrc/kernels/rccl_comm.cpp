@@ -234,6 +234,28 @@ void rccl_all_gather(int64_t h, at::Tensor& out, const at::Tensor& in) {
         "ncclAllGather");
 }
 
+// Several all-gathers as one RCCL group (one launch): outs[i] = concatenation over ranks of ins[i]
+// (ins[i] may be this rank's block of outs[i]: in place).
+void rccl_all_gather_many(int64_t h, at::TensorList outs, at::TensorList ins) {
+  Comm* c = get(h);
+  TORCH_CHECK(outs.size() == ins.size(), "rccl_all_gather_many: as many outputs as inputs");
+  for (size_t i = 0; i < outs.size(); ++i) {
+    check_dev(c, outs[i], "rccl_all_gather_many: out");
+    check_dev(c, ins[i], "rccl_all_gather_many: in");
+    TORCH_CHECK(outs[i].scalar_type() == ins[i].scalar_type() && outs[i].numel() == ins[i].numel() * c->world,
+                "rccl_all_gather_many: out must hold world x in elements of in's dtype");
+  }
+  auto stream = c10::hip::getCurrentHIPStream().stream();
+  Rccl& r = rccl();
+  check(r.group_start(), "ncclGroupStart");
+  for (size_t i = 0; i < outs.size(); ++i)
+    if (ins[i].numel() > 0)
+      check(r.all_gather(ins[i].data_ptr(), outs[i].data_ptr(), (size_t)ins[i].numel(), dtype_of(ins[i]), c->comm,
+                         stream),
+            "ncclAllGather");
+  check(r.group_end(), "ncclGroupEnd");
+}
+
 // out = this rank's block of the reduction over ranks of `in` (world x out elements).
 void rccl_reduce_scatter(int64_t h, at::Tensor& out, const at::Tensor& in, int64_t op) {
   Comm* c = get(h);
@@ -422,6 +444,7 @@ TORCH_LIBRARY_FRAGMENT(mihvd, m) {
   m.def("rccl_comm_user_rank(int comm) -> int", &mihvd::rccl_comm_user_rank);
   m.def("rccl_all_reduce_(int comm, Tensor(a!) t, int op=0) -> ()", &mihvd::rccl_all_reduce_);
   m.def("rccl_all_gather(int comm, Tensor(a!) out, Tensor input) -> ()", &mihvd::rccl_all_gather);
+  m.def("rccl_all_gather_many(int comm, Tensor(a!)[] outs, Tensor[] ins) -> ()", &mihvd::rccl_all_gather_many);
   m.def("rccl_reduce_scatter(int comm, Tensor(a!) out, Tensor input, int op=0) -> ()", &mihvd::rccl_reduce_scatter);
   m.def("rccl_broadcast_(int comm, Tensor(a!) t, int root=0) -> ()", &mihvd::rccl_broadcast_);
   m.def("rccl_all_to_all(int comm, Tensor(a!) out, Tensor input) -> ()", &mihvd::rccl_all_to_all);

@@ -421,12 +421,14 @@ class FusedMNISTTrainer:
             # sharded planes' 12.85 MB.
             self._f32_can_factor = self.collectives and compression == "none" and avg_or_sum
             self.f32_factor_rep = False
+            self._a2_own, self._dz_own = self.a2, self.dz
             if self._f32_can_factor:
                 N = self.world
                 self.a2_all32 = torch.empty(N, B, 3136, **f32)
                 if getattr(self, "dz_all32", None) is None:
                     self.dz_all32 = torch.empty(N, B, 1024, **f32)
                 self.f32_factor_rep = not self.shard_w3 and f32_plane_mode() == "factor_rep"
+            self._bind_factor_views()
         # fp32 step on the resident set: the batch gathered one step ahead (xpre images, ypre labels)
         # by the head kernel, so the next conv1 reads its images with one load instead of the dependent
         # counter -> rows -> image chain; _xpre_valid: they hold the batch of the device counter's step
@@ -716,8 +718,6 @@ class FusedMNISTTrainer:
         o.f32_conv2_fwd(self.a1, w2, P("conv_layer2/conv2d/bias"), self.a2, self.idx2, w2frag=wf[0],
                         products=self.f32_products)
         rep_factor = self.collectives and self.f32_factor_rep
-        if rep_factor:  # replicated factor plane: every rank's a2 (on this stream: see below)
-            self._gather_factor(self.a2_all32, self.a2)
         if self._shadow_ev is not None:  # the previous step's W3 row gather (side stream)
             main.wait_event(self._shadow_ev)
             self._shadow_ev = None
@@ -767,26 +767,43 @@ class FusedMNISTTrainer:
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)
         self._f32_small_tail(main, FC_START)
 
-    def _gather_factor(self, out, mine):
-        """out[q] <- rank q's ``mine`` (all-gather on the current stream: the framework communicator,
-        else the process group; at world 1 a copy)."""
+    def _bind_factor_views(self):
+        """fp32: on the replicated factor plane conv2_fwd and the head write this rank's a2 and dz
+        straight into its slices of the all-gather buffers (the gathers run in place); elsewhere
+        into buffers of their own."""
+        if not self.f32 or getattr(self, "_a2_own", None) is None:
+            return
+        if getattr(self, "f32_factor_rep", False):
+            self.a2, self.dz = self.a2_all32[self.rank], self.dz_all32[self.rank]
+        else:
+            self.a2, self.dz = self._a2_own, self._dz_own
+
+    def _gather_factors(self):
+        """Every rank's a2 and dz into a2_all32 / dz_all32, in place (this rank's slices already hold
+        its own): one RCCL group on the framework communicator (nothing to move at world 1), else
+        the process group."""
         import torch.distributed as dist
 
+        r = self.rank
+        outs = (self.a2_all32, self.dz_all32)
+        mine = (self.a2_all32[r], self.dz_all32[r])
         if self.ncomm is not None:
-            self.ncomm.all_gather_into(out, mine)
+            self.ncomm.all_gather_many_into(outs, mine)
         elif self.world == 1:
-            out[0].copy_(mine)
+            return
         elif dist.get_backend() == "nccl":
-            dist.all_gather_into_tensor(out, mine)
+            for o, m in zip(outs, mine):
+                dist.all_gather_into_tensor(o, m)
         else:  # host collectives (gloo)
-            dist.all_gather(list(out.unbind(0)), mine.clone())
+            for o, m in zip(outs, mine):
+                dist.all_gather(list(o.unbind(0)), m.clone())
 
     def _launch_step_f32_factor_rep(self, x, rows, st, w2, wf, gconv):
-        """Rest of the fp32 step on the replicated factor-gather plane (after the head; the a2
-        all-gather ran behind conv2_fwd), one stream:
+        """Rest of the fp32 step on the replicated factor-gather plane (after the head; conv2_fwd and
+        the head wrote this rank's a2 and dz into its slices of a2_all32 / dz_all32), one stream:
 
-            AG(a2) | fc1_fwd | head | AG(dz) | fc1_bwd (dgrad only) | dW3 of all N B samples + Adam,
-            every row | conv2_bwd | conv_reduce | AR(small) + Adam
+            AG(a2, dz: one RCCL group, in place) | fc1_bwd (dgrad only) | dW3 of all N B samples +
+            Adam, every row | conv2_bwd | conv_reduce | AR(small) + Adam
 
         dense/kernel's update is replicated, so nothing of it crosses the links after the step. The
         all-gathers stay on the compute stream: forked onto a side stream inside the HIP graph (a2
@@ -794,11 +811,12 @@ class FusedMNISTTrainer:
         1, its three cross-queue edges ~10 us each (fc1_fwd started 11.8 us after conv2_fwd,
         fc1_bwd 11.0 us after the head, the join 9.5 us after fc1_bwd:
         profiles/r06/timeline_f32_factor_rep_forked_world1_r06y.txt) -- more than the 22-33 us of
-        link time per step the fork could hide at N = 2."""
+        link time per step the fork could hide at N = 2. Serial with two copying all-gathers:
+        122.8 us (profiles/r06/timeline_f32_factor_rep_world1_r06aa.txt)."""
         o, G = self.ops, self.gview
         main = torch.cuda.current_stream(self.device)
         b1, b2 = self.betas
-        self._gather_factor(self.dz_all32, self.dz)
+        self._gather_factors()
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, self.pview("dense/kernel"), self.dY2, self.db2p,
                       G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
         s3 = slice(W3_START, FLAT_NUMEL)
@@ -1562,6 +1580,7 @@ class FusedMNISTTrainer:
         self.set_sharding(shard)
         self.f32_factor = bool(factor) and self.f32 and self.shard_w3
         self.f32_factor_rep = bool(factor) and self.f32 and not self.shard_w3 and getattr(self, "_f32_can_factor", False)
+        self._bind_factor_views()
         self._graphs = {}
         self.graph = None
 
@@ -1581,6 +1600,7 @@ class FusedMNISTTrainer:
         self.shard_w3 = shard
         self.f32_factor = self.f32_factor and shard
         self.f32_factor_rep = getattr(self, "f32_factor_rep", False) and not shard
+        self._bind_factor_views()
         self._graphs = {}
         self.graph = None
 

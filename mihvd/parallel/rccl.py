@@ -82,6 +82,11 @@ class NativeComm:
         self._o.rccl_all_gather(self.handle, out, inp)
         return out
 
+    def all_gather_many_into(self, outs, inps):
+        """Several all-gathers as one RCCL group call (``inps[i]`` may be this rank's slice of
+        ``outs[i]``: in place)."""
+        self._o.rccl_all_gather_many(self.handle, list(outs), list(inps))
+
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum") -> torch.Tensor:
         self._o.rccl_reduce_scatter(self.handle, out, inp, _OPS[op])
         return out
