@@ -781,22 +781,10 @@ class FusedMNISTTrainer:
     def _gather_factors(self):
         """Every rank's a2 and dz into a2_all32 / dz_all32, in place (this rank's slices already hold
         its own): one RCCL group on the framework communicator (nothing to move at world 1), else
-        the process group."""
-        import torch.distributed as dist
+        the process group (mihvd/parallel/factor.py)."""
+        from ..parallel.factor import factor_gather_all_
 
-        r = self.rank
-        outs = (self.a2_all32, self.dz_all32)
-        mine = (self.a2_all32[r], self.dz_all32[r])
-        if self.ncomm is not None:
-            self.ncomm.all_gather_many_into(outs, mine)
-        elif self.world == 1:
-            return
-        elif dist.get_backend() == "nccl":
-            for o, m in zip(outs, mine):
-                dist.all_gather_into_tensor(o, m)
-        else:  # host collectives (gloo)
-            for o, m in zip(outs, mine):
-                dist.all_gather(list(o.unbind(0)), m.clone())
+        factor_gather_all_(self.a2_all32, self.dz_all32, self.rank, self.world, self.ncomm)
 
     def _launch_step_f32_factor_rep(self, x, rows, st, w2, wf, gconv):
         """Rest of the fp32 step on the replicated factor-gather plane (after the head; conv2_fwd and

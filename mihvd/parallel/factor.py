@@ -12,6 +12,10 @@ W3 is sharded by rows (rank r owns rows [r R, (r + 1) R), R = 3136 / N), by movi
 after which rank r forms its rows of the summed gradient exactly, over all N B samples, as one fp32
 GEMM (R x N B x 1024). Per rank (N - 1) B (1024 + R) floats arrive instead of the reduce-scatter's
 (N - 1) R 1024 (N = 8, B = 100: 3.9 MB instead of 11.2 MB).
+
+For small N the replicated form needs no sharding at all: every rank all-gathers every rank's a2
+and dz ((N - 1) B (3136 + 1024) floats, 1.66 MB per peer at B = 100, on every link at once) and forms
+ALL of dW3 (factor_full_), so neither the 12.8 MB gradient nor the updated rows cross the links.
 """
 from __future__ import annotations
 
@@ -58,4 +62,33 @@ def factor_rows_(out: torch.Tensor, a2: torch.Tensor, dz: torch.Tensor, dz_all: 
     return torch.mm(a2_recv.view(N * B, R).t(), dz_all.view(N * B, dz_all.shape[-1]), out=out)
 
 
-__all__ = ["factor_exchange_", "factor_rows_"]
+def factor_gather_all_(a2_all: torch.Tensor, dz_all: torch.Tensor, rank: int, world: int, comm=None):
+    """The replicated factor plane's exchange, in place: a2_all[q] / dz_all[q] ([N][B][3136] /
+    [N][B][1024]) <- rank q's a2 / dz, this rank's slices already holding its own. ``comm``: a
+    :class:`mihvd.parallel.rccl.NativeComm` (one RCCL group on the current HIP stream), else the
+    default process group. Collective."""
+    outs, mine = (a2_all, dz_all), (a2_all[rank], dz_all[rank])
+    if comm is not None:
+        comm.all_gather_many_into(outs, mine)
+    elif world == 1:
+        return
+    elif dist.get_backend() == "nccl":
+        for o, m in zip(outs, mine):
+            dist.all_gather_into_tensor(o, m)
+    else:  # host collectives (gloo)
+        for o, m in zip(outs, mine):
+            dist.all_gather(list(o.unbind(0)), m.clone())
+
+
+def factor_full_(out: torch.Tensor, a2_all: torch.Tensor, dz_all: torch.Tensor, rank: int, world: int,
+                 comm=None) -> torch.Tensor:
+    """out[3136][1024] = sum over ranks of a2_q^T dz_q, every row on every rank (the replicated
+    plane): the in-place exchange, then one torch GEMM over the N B gathered samples. The host-side
+    reference; the trainer forms the rows with ``csrc/kernels/f32_factor.hip::f32_factor_full``,
+    which also applies Adam to them. Collective."""
+    factor_gather_all_(a2_all, dz_all, rank, world, comm)
+    N, B = a2_all.shape[0], a2_all.shape[1]
+    return torch.mm(a2_all.view(N * B, -1).t(), dz_all.view(N * B, -1), out=out)
+
+
+__all__ = ["factor_exchange_", "factor_rows_", "factor_gather_all_", "factor_full_"]

@@ -62,6 +62,17 @@ def test_f32_factor_rows_gather(tmp_path, np_):
         assert o["rel"] < 1e-6, o
 
 
+@pytest.mark.parametrize("np_", [2, 3])
+def test_f32_factor_full_gather(tmp_path, np_):
+    """The replicated fp32 factor plane's in-place exchange + GEMM (mihvd/parallel/factor.py) on the
+    host collectives: every rank forms all of dW3 from every rank's a2 and dz (3 ranks: 3136 rows do
+    not split evenly, which this plane does not need)."""
+    _, outs = run_scenario(tmp_path, "factor_full", np_=np_)
+    for o in outs:
+        assert o["gathered"], o
+        assert o["rel"] < 1e-6, o
+
+
 def test_dp_equivalence(tmp_path):
     _, outs = run_scenario(tmp_path, "dp_equivalence")
     for o in outs:

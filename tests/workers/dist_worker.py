@@ -529,6 +529,29 @@ def sc_factor_rows(outdir):
                                                                                      factors((r + 1) % n)[1]))})
 
 
+def sc_factor_full(outdir):
+    """The replicated fp32 factor plane's exchange + GEMM (mihvd/parallel/factor.py) over gloo: every
+    rank's dW3 from the in-place all-gathered a2 / dz equals the sum over ranks of a2_q^T dz_q, on
+    every rank, also where 3136 rows do not split evenly over the ranks."""
+    from mihvd.parallel.factor import factor_full_
+
+    r, n = hvd.rank(), hvd.size()
+    B = 24
+
+    def factors(q):
+        g = torch.Generator().manual_seed(200 + q)
+        return torch.randn(B, 3136, generator=g), torch.randn(B, 1024, generator=g)
+
+    a2_all, dz_all = torch.full((n, B, 3136), float("nan")), torch.full((n, B, 1024), float("nan"))
+    a2_all[r], dz_all[r] = factors(r)  # this rank's slices: written by conv2_fwd / the head in the trainer
+    out_full = torch.empty(3136, 1024)
+    factor_full_(out_full, a2_all, dz_all, r, n)
+    ref = sum(f[0].double().t() @ f[1].double() for f in map(factors, range(n)))
+    rel = ((out_full.double() - ref).norm() / ref.norm()).item()
+    out(outdir, "factor_full", {"rel": rel, "gathered": all(torch.equal(a2_all[q], factors(q)[0]) and
+                                                            torch.equal(dz_all[q], factors(q)[1]) for q in range(n))})
+
+
 PS_INIT = []
 
 
