@@ -31,6 +31,7 @@ sides; the max elapsed over ranks is used. Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -350,6 +351,11 @@ def main():
             comm.all_reduce_(token)
     else:
         barrier = hvd.barrier
+    # no Python garbage collection inside the timed region (a collection pause on the host while the
+    # lead graph runs could delay the long graph's launch past the lead's end). No gc.collect() in
+    # front of it either: the GPU slows down while the host idles (a collection there measured
+    # 118-129 us/step, profiles/r06/driver_form_gc_collect_r06ah.txt; scripts/idle_probe.py)
+    gc.disable()
     sync()
     barrier()
     sync()
@@ -359,6 +365,7 @@ def main():
     barrier()
     sync()
     el = time.perf_counter() - t0
+    gc.enable()
     t = torch.tensor([el], dtype=torch.float64, device=device)
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
