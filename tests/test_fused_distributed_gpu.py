@@ -203,6 +203,24 @@ def test_plane_and_sharding_switches_two_ranks(tmp_path):
         assert o["loss"] == o["loss_ref"]
 
 
+def test_f32_plane_switches_into_and_out_of_the_replicated_factor_plane_two_ranks(tmp_path):
+    """fp32 plane switches between steps through the replicated factor plane (its a2 / dz views
+    rebound at every switch) track a trainer that stays on the replicated allreduce, to fp32
+    rounding of the update, with every rank equal."""
+    _gpu()
+    env = dict(os.environ, MIHVD_BACKEND="gloo", PYTHONPATH=ROOT, MIHVD_XGMI="off")
+    cmd = [sys.executable, "-m", "mihvd.runner", "-np", "2", sys.executable, WORKER, "dp_gloo_switch_f32", str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(2):
+        o = json.loads((tmp_path / f"dp_gloo_switch_f32.{r}.json").read_text())
+        assert o["planes"] == ["rccl-shard", "factor_rep-replicated", "rccl-replicated", "factor-shard",
+                               "factor_rep-replicated"], o
+        assert o["rank_spread"] == 0.0, o
+        assert o["rel"] < 1e-3, o
+        assert abs(o["loss"] - o["loss_ref"]) < 1e-3 * max(1.0, abs(o["loss_ref"])), o
+
+
 # (4-rank cases dropped in round 5: the 8-rank flow below covers the same path at the larger count)
 @pytest.mark.parametrize("n,prec", [(2, "fp32")])  # (bf16 at 2 ranks: the equivalence tests)
 def test_bench_multirank_rehearsal_on_one_gpu(n, prec):

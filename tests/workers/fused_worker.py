@@ -172,6 +172,45 @@ def sc_dp_gloo_switch(outdir):
         json.dump(rec, f)
 
 
+def sc_dp_gloo_switch_f32(outdir):
+    """fp32 plane switches between steps, into and out of the replicated factor plane (whose
+    conv2_fwd / head write a2 / dz into the gather buffers: the views are rebound at every switch):
+    reduce-scatter sharded -> factor replicated -> RCCL replicated -> factor sharded -> factor
+    replicated, against a trainer that stays on the replicated allreduce. The planes sum dW3 in
+    different orders, so the match is to fp32 rounding of the update, and every rank stays equal."""
+    r = hvd.rank()
+    X, Y = data(1200)
+    a = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="fp32",
+                          shard_optimizer=True)
+    ref = FusedMNISTTrainer(batch_size=50, lr=1e-3, dropout=0.0, seed=1, device="cuda", precision="fp32",
+                            shard_optimizer=False)
+    for tr in (a, ref):
+        tr.broadcast(0)
+    p0 = ref.params.clone()
+    ref._set_plane(False, False)
+    plan = [(True, False), (False, True), (False, False), (True, True), (False, True)]  # (shard, factor)
+    step, planes = 0, []
+    for sh, fac in plan:
+        a._set_plane(False, sh, fac)
+        planes.append(a.data_plane() + ("-shard" if a.shard_w3 else "-replicated"))
+        for _ in range(2):
+            xb = X[step * 100:(step + 1) * 100]
+            yb = Y[step * 100:(step + 1) * 100]
+            for tr in (a, ref):
+                tr.train_step(xb[r * 50:(r + 1) * 50], yb[r * 50:(r + 1) * 50])
+            step += 1
+    torch.cuda.synchronize()
+    a.gather_full_state()
+    rel = ((a.params - ref.params).norm() / (ref.params - p0).norm()).item()
+    spread = hvd.allgather(a.params.cpu().view(1, -1))
+    rec = {"rel": rel, "planes": planes, "loss": a.last_loss(), "loss_ref": ref.last_loss(),
+           "rank_spread": (spread - spread[0]).abs().max().item()}
+    for tr in (a, ref):
+        tr.close()
+    with open(os.path.join(outdir, f"dp_gloo_switch_f32.{r}.json"), "w") as f:
+        json.dump(rec, f)
+
+
 def _tf_adam_host(p, g, t, lr, b1=0.9, b2=0.999, eps=1e-8):
     """One TF1 Adam step from zero slots, float64 (tensorflow_mnist.py:130)."""
     m = (1 - b1) * g
