@@ -64,6 +64,9 @@ def parse():
                          "training set the reference's ranks each iterate over: an epoch of 600 steps, reshuffled "
                          "at its boundary)")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
+    ap.add_argument("--use-adasum", action="store_true", default=False,
+                    help="fused: Adasum instead of the average (the reference's --use-adasum, "
+                         "horovod/tensorflow_mnist.py:31-32,126-133: lr x local_size over NCCL/RCCL, else x 1)")
     ap.add_argument("--precision", choices=["fp32", "bf16", "fp16"], default=os.environ.get("MIHVD_PRECISION", "fp32"),
                     help="fused: operand precision of the hand-written step. fp32 (default) = the reference's "
                          "launched config (fp32 placeholders + AdamOptimizer, tensorflow_mnist.py:118-130) on the "
@@ -168,8 +171,15 @@ def replay_schedule(n: int, k: int, lead: int) -> list:
 def make_fused_step(args, hvd, device):
     from mihvd.models.fused_mnist import FusedMNISTTrainer
 
-    tr = FusedMNISTTrainer(batch_size=args.batch_size, lr=args.lr * hvd.size(), seed=42, device=device,
+    # the reference's learning-rate rule (tensorflow_mnist.py:123-130): x size for the average; x
+    # local_size over NCCL (here RCCL) for Adasum, else x 1
+    if args.use_adasum:
+        lr_scaler = hvd.local_size() if hvd.nccl_built() else 1
+    else:
+        lr_scaler = hvd.size()
+    tr = FusedMNISTTrainer(batch_size=args.batch_size, lr=args.lr * lr_scaler, seed=42, device=device,
                            compression=args.compression, precision=args.precision,
+                           op=hvd.Adasum if args.use_adasum else None,
                            shard_optimizer=os.environ.get("MIHVD_SHARD_W3", "1") != "0")
     tr.broadcast(0)
     X, Y = synthetic_pool(args.pool_batches, args.batch_size, device, seed=hvd.rank())
@@ -379,6 +389,10 @@ def main():
         comm_desc = "RCCL allreduce of fp32 gradient buckets (DistributedOptimizer / DDP)"
     elif n == 1 and not tr.collectives:
         comm_desc = "none (1 GPU)"
+    elif args.use_adasum:
+        comm_desc = ("Adasum of the fp32 gradient buckets on the framework communicator: vector halving / distance "
+                     "doubling over grouped ncclSend/ncclRecv, each level's dot products in one allreduce, HIP "
+                     "combine kernels (mihvd/parallel/adasum.py adasum_vhdd_); every step, in the HIP graph")
     elif tr.f32 and tr.shard_w3 and tr.data_plane() == "xgmi":
         comm_desc = ("fp32 direct xGMI (hipIpc peer memory, device-side phase barriers, one stream): after the "
                      "gradient reduction one launch sums every rank's small gradients and this rank's 1/N of "
@@ -431,7 +445,10 @@ def main():
             "config": {"model": "tensorflow_mnist 2-conv CNN (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.5-fc10, 3,274,634 params)",
                        "global_batch": args.batch_size * n, "per_gpu_batch": args.batch_size, "seq_len": None,
                        "image_shape": [28, 28, 1], "parallelism": f"dp{n}", "impl": args.impl,
-                       "optimizer": "Adam (TF1 rule), lr=%g x size" % args.lr,
+                       "optimizer": ("Adam (TF1 rule), lr=%g x %s, %s" % (
+                           args.lr, "local_size" if args.use_adasum else "size",
+                           "Adasum (vector halving / distance doubling)" if args.use_adasum else "average"))
+                       if args.impl == "fused" else "Adam (TF1 rule), lr=%g x size" % args.lr,
                        "allreduce": comm_desc,
                        "steps_per_graph": per_call,
                        "replays_timed": (step.schedule(steps_timed) if hasattr(step, "schedule") else None),

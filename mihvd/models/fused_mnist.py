@@ -642,7 +642,7 @@ class FusedMNISTTrainer:
             self._allreduce(self.grads[:FC_START], 0, FC_START)
         main.wait_stream(self._side)
         o.adam_step(self.params, self.grads, self.m, self.v, self.shadow, st, 0, self.lr, b1, b2, self.eps,
-                    1.0 / self.world, self.rule, 1)
+                    self._gscale(), self.rule, 1)
 
     def _launch_step_f16(self, x, rows, labels):
         """The Keras ``mixed_float16`` step (tensorflow_mnist_gpu.py:26-28,141-145): fp16 MFMA operands
@@ -678,7 +678,7 @@ class FusedMNISTTrainer:
             # rank skips the same steps
             self._allreduce(self.grads, 0, FLAT_NUMEL)
         o.grad_check_([self.grads], self.loss_scale, False)
-        o.adam_step(self.params, self.grads, self.m, self.v, None, st, 0, self.lr, b1, b2, self.eps, 1.0 / self.world,
+        o.adam_step(self.params, self.grads, self.m, self.v, None, st, 0, self.lr, b1, b2, self.eps, self._gscale(),
                     self.rule, 1, loss_scale=self.loss_scale)
         o.scale_cast_f16(self.params, self.shadow, 1.0)
         o.update_scale_(self.loss_scale, self._ls_tracker, 2.0, 0.5, self.ls_growth_interval, 1.0, state=st)
@@ -759,7 +759,7 @@ class FusedMNISTTrainer:
             self._allreduce(self.grads[FC_START:], FC_START, FLAT_NUMEL)
             fc = slice(FC_START, FLAT_NUMEL)
             o.adam_step(self.params[fc], self.grads[fc], self.m[fc], self.v[fc], None, st, 0, self.lr, b1, b2, self.eps,
-                        1.0 / self.world, self.rule, 0)
+                        self._gscale(), self.rule, 0)
             self._shadow_ev = torch.cuda.Event()  # the next step's fc1_fwd (W3's first reader) joins it
             self._shadow_ev.record(side)
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
@@ -844,7 +844,7 @@ class FusedMNISTTrainer:
         with torch.cuda.stream(stream):
             self._allreduce(self.grads[:hi], 0, hi, comm=self.ncomm_small)
             self.ops.adam_step(self.params[:hi], self.grads[:hi], self.m[:hi], self.v[:hi], None, self.state, 0, self.lr,
-                               b1, b2, self.eps, 1.0 / self.world, self.rule, 1)
+                               b1, b2, self.eps, self._gscale(), self.rule, 1)
             if not on_main:
                 self._small_ev = torch.cuda.Event()
                 self._small_ev.record(stream)
@@ -1283,6 +1283,15 @@ class FusedMNISTTrainer:
         self._refresh_shadow()
         self._full_state_valid = True
 
+    def _gscale(self) -> float:
+        """Adam's gradient scale on the replicated paths: 1/N of the allreduced sum (the average), 1
+        for Adasum, whose exchange already yields the combined gradient."""
+        from ..basics import ReduceOp
+
+        if self.op is not None and ReduceOp(self.op) == ReduceOp.Adasum:
+            return 1.0
+        return 1.0 / self.world
+
     def _allreduce(self, bucket, lo, hi, comm=None):
         import torch.distributed as dist
 
@@ -1293,8 +1302,7 @@ class FusedMNISTTrainer:
 
             segs = [(o - lo, o - lo + n) for o, n in SEGMENTS.values() if lo <= o < hi]
             adasum_dispatch_(bucket, segs, comm=comm if comm is not None else self.ncomm)
-            bucket.mul_(self.world)  # adam divides by size; Adasum output is already the combined gradient
-            return
+            return  # (the combined gradient: its Adam takes grad_scale 1, _gscale)
         comm = comm if comm is not None else self.ncomm
         reduce_ = comm.all_reduce_ if comm is not None else dist.all_reduce
         if self.wire is not None:
