@@ -162,6 +162,33 @@ __device__ __forceinline__ void f32_fc1_small512(int bid, const float* __restric
   }
 }
 
+// The next step's batch gathered ahead (resident set): the images into xpre [B][784] and the labels
+// into ypre [B], by the small-reduction blocks, which run on CUs the 196 row blocks leave free and
+// finish long before them; conv1 and the head of the next step read these with one load instead of
+// the counter -> rows -> image / label chain. (In the head, a step earlier in the chain, the same
+// gather cost 0.2 us of head time: profiles/r06/roofline_f32_gather_ahead_r06x.md.)
+struct F32Prefetch {
+  const float* x = nullptr;        // the resident set [n_pool][784]
+  const int64_t* labels = nullptr; // [n_pool]
+  const int* rows = nullptr;       // the epoch order [n_pool]
+  const int64_t* state = nullptr;  // state[ST_FWD]: this step (the next is + 1)
+  int n_pool = 0;
+  float* xpre = nullptr;
+  int* ypre = nullptr;
+};
+
+__device__ __forceinline__ void f32_prefetch_next(const F32Prefetch& pf, int s, int nsb, int B) {
+  const int t = threadIdx.x;
+  const int64_t step = pf.state[ST_FWD] + 1;
+  for (int b = s; b < B; b += nsb) {  // block-uniform
+    const int row = pf.rows[(int)((step * (int64_t)B + b) % pf.n_pool)];
+    if (t < 196)
+      reinterpret_cast<float4*>(pf.xpre + (int64_t)b * 784)[t] = reinterpret_cast<const float4*>(pf.x + (int64_t)row * 784)[t];
+    else if (t == 196)
+      pf.ypre[b] = (int)pf.labels[row];
+  }
+}
+
 // p/m/v are loaded two chunks ahead (PD, a ring of three register slots; four ahead measured no
 // faster: 28.2 vs 27.8 us, profiles/r04/kbench_f32_r04e.txt). Pinning the dgrad MFMA order with
 // sched_barrier measured slower (+2 us, r04).
@@ -173,10 +200,11 @@ __global__ void __launch_bounds__(512) f32_fc1_bwd_rows_kernel(
     const float* __restrict__ dz, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ h, const float* __restrict__ dlog, float* __restrict__ w3, float* __restrict__ dY2,
     float* __restrict__ db2p, float* __restrict__ gW3, float* __restrict__ gb3, float* __restrict__ gW4,
-    float* __restrict__ gb4, int B, F32Adam ad) {
+    float* __restrict__ gb4, int B, F32Adam ad, F32Prefetch pf) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   const int bid = blockIdx.x;
   if (bid >= F1R_BLOCKS) {
+    if (pf.ypre != nullptr) f32_prefetch_next(pf, bid - F1R_BLOCKS, F1B_SMALL, B);
     f32_fc1_small512(bid - F1R_BLOCKS, dz, h, dlog, gb3, gW4, gb4, B, smf);
     return;
   }
@@ -1517,7 +1545,10 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
                  const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
                  at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
                  const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr, double beta1,
-                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3) {
+                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3,
+                 const c10::optional<at::Tensor>& px, const c10::optional<at::Tensor>& plabels,
+                 const c10::optional<at::Tensor>& prows, const c10::optional<at::Tensor>& pstate,
+                 const c10::optional<at::Tensor>& xpre, const c10::optional<at::Tensor>& ypre) {
   const int B = dz.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_fc1_bwd: batch 1..128");
   chk_f32(dz, (int64_t)B * 1024, "f32_fc1_bwd: dz");
@@ -1534,6 +1565,29 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
   chk_f32(gb4, 10, "f32_fc1_bwd: gb4");
   const F32Adam ad = f32_fc1_adam(w3, m3, v3, state, lr, beta1, beta2, eps, grad_scale, rule);
   const bool adam = ad.nblk > 0;
+  F32Prefetch pf;
+  if (ypre.has_value() && ypre->defined()) {
+    TORCH_CHECK(px.has_value() && px->defined() && plabels.has_value() && plabels->defined() && prows.has_value() &&
+                    prows->defined() && pstate.has_value() && pstate->defined() && xpre.has_value() && xpre->defined(),
+                "f32_fc1_bwd: the next batch's gather needs px, plabels, prows, pstate, xpre and ypre");
+    const int n_pool = px->size(0);
+    TORCH_CHECK(px->is_cuda() && px->dtype() == at::kFloat && px->is_contiguous() && px->dim() == 2 &&
+                    px->size(1) == 784, "f32_fc1_bwd: px [n_pool][784]");
+    TORCH_CHECK(plabels->dtype() == at::kLong && plabels->is_contiguous() && plabels->numel() == n_pool,
+                "f32_fc1_bwd: plabels int64 [n_pool]");
+    TORCH_CHECK(prows->dtype() == at::kInt && prows->is_contiguous() && prows->numel() == n_pool,
+                "f32_fc1_bwd: prows int32 [n_pool]");
+    TORCH_CHECK(pstate->dtype() == at::kLong && pstate->numel() >= ST_WORDS, "f32_fc1_bwd: pstate");
+    chk_f32(*xpre, (int64_t)B * 784, "f32_fc1_bwd: xpre [B][784]");
+    TORCH_CHECK(ypre->dtype() == at::kInt && ypre->is_contiguous() && ypre->numel() == B, "f32_fc1_bwd: ypre int32 [B]");
+    pf.x = px->data_ptr<float>();
+    pf.labels = plabels->data_ptr<int64_t>();
+    pf.rows = prows->data_ptr<int>();
+    pf.state = pstate->data_ptr<int64_t>();
+    pf.n_pool = n_pool;
+    pf.xpre = xpre->data_ptr<float>();
+    pf.ypre = ypre->data_ptr<int>();
+  }
   // neither adam nor store_w3: dgrad (+ db3, dW4, db4) only, gW3 untouched (fp32 factor-gather plane)
   const bool dgrad_only = !adam && !store_w3;
   const int G = (B + 15) / 16;
@@ -1544,7 +1598,7 @@ void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& i
     kern<<<F1R_BLOCKS + F1B_SMALL, 512, F1R_LDS, stream>>>(
         dz.data_ptr<float>(), a2.data_ptr<float>(), idx2.data_ptr<uint8_t>(), h.data_ptr<float>(),
         dlog.data_ptr<float>(), w3.data_ptr<float>(), dY2.data_ptr<float>(), db2p.data_ptr<float>(),
-        gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad);
+        gW3.data_ptr<float>(), gb3.data_ptr<float>(), gW4.data_ptr<float>(), gb4.data_ptr<float>(), B, ad, pf);
   };
   if (dgrad_only) {
     switch (G) {

@@ -100,8 +100,9 @@ __global__ void __launch_bounds__(256) f32_conv1_kernel(
 }
 
 // The batch of step state[ST_FWD] gathered from the resident set into xpre [B][784] (and its labels
-// into ypre [B]): the start of a chain that every f32_head1k_kernel continues for the next step, so
-// conv1 reads its images with one load. Run whenever the counter, the epoch order or the set change
+// into ypre [B]): the start of a chain that every f32_fc1_bwd continues for the next step (its
+// small-reduction blocks, f32_bwd.hip f32_prefetch_next), so conv1 reads its images and the head its
+// labels with one load. Run whenever the counter, the epoch order or the set change
 // outside a step (FusedMNISTTrainer._prime_batch).
 __global__ void __launch_bounds__(256) f32_prime_kernel(const float* __restrict__ x, const int64_t* __restrict__ labels,
                                                         const int* __restrict__ rows, int n_pool,
@@ -724,21 +725,13 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
     const float* __restrict__ b4, const int64_t* __restrict__ labels, const int* __restrict__ rows, int n_pool,
     int64_t* __restrict__ state, uint32_t seed, uint32_t thresh24, float keep_scale, float* __restrict__ h_out,
     float* __restrict__ dz_out, float* __restrict__ dlog_out, float* __restrict__ stats, int B,
-    float* __restrict__ stats_acc, const float* __restrict__ xsrc, float* __restrict__ xpre, int* __restrict__ ypre) {
+    float* __restrict__ stats_acc, const int* __restrict__ ypre) {
   __shared__ float red[16][10];
   __shared__ float dl[10];
   const int b = blockIdx.x, n = threadIdx.x, lane = n & 63, wave = __builtin_amdgcn_readfirstlane(n >> 6);
   const int64_t step = state ? state[ST_FWD] : 0;
-  // resident set (ypre != nullptr): this step's label was gathered ahead (ypre[b]); waves 1..4 gather
-  // the NEXT step's image into xpre[b] (its conv1 has read this step's) and wave 0 its label, behind
-  // this step's use of ypre[b]
-  const bool pre = ypre != nullptr;
-  int row_next = 0;
-  if (pre && (wave == 0 || (n >= 64 && n < 64 + 196)))
-    row_next = rows[(int)(((step + 1) * (int64_t)B + b) % n_pool)];
-  if (pre && n >= 64 && n < 64 + 196)
-    reinterpret_cast<float4*>(xpre + (int64_t)b * 784)[n - 64] =
-        reinterpret_cast<const float4*>(xsrc + (int64_t)row_next * 784)[n - 64];
+  // resident set (ypre != nullptr): this step's label was gathered ahead by the previous step's
+  // fc1_bwd (or f32_prime_kernel): one load instead of counter -> rows -> label
   float parts[F1F_KS];
 #pragma unroll
   for (int s = 0; s < F1F_KS; ++s) parts[s] = zpart[((int64_t)s * B + b) * 1024 + n];
@@ -752,11 +745,9 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
   const float bias = b3[n];
   int y = 0;
   float bias4 = 0.f;  // b4 of lane c (wave 0), loaded with the other operands instead of behind the barrier
-  int y_next = 0;
   if (wave == 0) {
-    if (pre) {
+    if (ypre != nullptr) {
       y = ypre[b];
-      y_next = (int)labels[row_next];
     } else {
       int row = b;
       if (rows != nullptr) row = rows[(int)((step * (int64_t)B + b) % n_pool)];
@@ -803,7 +794,6 @@ __global__ void __launch_bounds__(1024) f32_head1k_kernel(
         stats_acc[b * 2 + 1] += (am == y) ? 1.f : 0.f;
       }
       if (b == 0 && state != nullptr) state[ST_OPT] += 1;
-      if (pre) ypre[b] = y_next;  // (this step's ypre[b] was consumed above: y feeds the loss)
     }
   }
   __syncthreads();
@@ -1041,7 +1031,6 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
                       at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc,
-                      const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& xpre,
                       const c10::optional<at::Tensor>& ypre) {
   const int B = h.size(0);
   TORCH_CHECK(B >= 1 && B <= F32_MAXB, "f32_head: batch 1..128");
@@ -1062,19 +1051,10 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   const int n_pool = labels.size(0);
   const int* rp = rows_ptr(rows, n_pool, B, "f32_head");
   int64_t* sp = (state.has_value() && state->defined()) ? state->data_ptr<int64_t>() : nullptr;
-  // the next step's batch gathered ahead (resident set): the set, its xpre and ypre buffers
-  const float* xs = nullptr;
-  float* xp = nullptr;
-  int* yp = nullptr;
+  // this step's labels gathered ahead (resident set)
+  const int* yp = nullptr;
   if (ypre.has_value() && ypre->defined()) {
-    TORCH_CHECK(rp != nullptr && sp != nullptr, "f32_head: the batch gathered ahead needs rows and state");
-    TORCH_CHECK(x.has_value() && x->defined() && xpre.has_value() && xpre->defined(), "f32_head: ypre needs x and xpre");
-    TORCH_CHECK(x->is_cuda() && x->dtype() == at::kFloat && x->is_contiguous() && x->size(-1) == 784 &&
-                    x->size(0) == n_pool, "f32_head: x [n_pool][784]");
-    check_f32(*xpre, (int64_t)B * 784, "f32_head: xpre [B][784]");
     TORCH_CHECK(ypre->dtype() == at::kInt && ypre->numel() == B && ypre->is_contiguous(), "f32_head: ypre int32 [B]");
-    xs = x->data_ptr<float>();
-    xp = xpre->data_ptr<float>();
     yp = ypre->data_ptr<int>();
   }
   TORCH_CHECK(rate >= 0.0 && rate < 1.0, "f32_head: dropout rate in [0, 1)");
@@ -1084,7 +1064,7 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
   f32_head1k_kernel<<<B, 1024, 0, stream>>>(
       zpart.data_ptr<float>(), b3.data_ptr<float>(), w4.data_ptr<float>(), b4.data_ptr<float>(),
       labels.data_ptr<int64_t>(), rp, n_pool, sp, (uint32_t)seed, thresh, keep_scale, h.data_ptr<float>(),
-      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc, xs, xp, yp);
+      dz.data_ptr<float>(), dlog.data_ptr<float>(), stats.data_ptr<float>(), B, acc, yp);
 }
 
 }  // namespace mihvd

@@ -97,13 +97,15 @@ void f32_head_fwd_bwd(const at::Tensor& zpart, const at::Tensor& b3, const at::T
                       const at::Tensor& labels, const c10::optional<at::Tensor>& rows,
                       const c10::optional<at::Tensor>& state, int64_t seed, double rate, at::Tensor& h, at::Tensor& dz,
                       at::Tensor& dlog, at::Tensor& stats, const c10::optional<at::Tensor>& stats_acc,
-                      const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& xpre,
                       const c10::optional<at::Tensor>& ypre);
 void f32_fc1_bwd(const at::Tensor& dz, const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& h,
                  const at::Tensor& dlog, at::Tensor& w3, at::Tensor& dY2, at::Tensor& db2p, at::Tensor& gW3,
                  at::Tensor& gb3, at::Tensor& gW4, at::Tensor& gb4, const c10::optional<at::Tensor>& m3,
                  const c10::optional<at::Tensor>& v3, const c10::optional<at::Tensor>& state, double lr, double beta1,
-                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3);
+                 double beta2, double eps, double grad_scale, int64_t rule, bool store_w3,
+                 const c10::optional<at::Tensor>& px, const c10::optional<at::Tensor>& plabels,
+                 const c10::optional<at::Tensor>& prows, const c10::optional<at::Tensor>& pstate,
+                 const c10::optional<at::Tensor>& xpre, const c10::optional<at::Tensor>& ypre);
 void f32_conv2_bwd(const at::Tensor& dY2, const at::Tensor& w2, const at::Tensor& a1, const at::Tensor& idx1,
                    const at::Tensor& x, const c10::optional<at::Tensor>& rows, const c10::optional<at::Tensor>& state,
                    at::Tensor& cpart, at::Tensor& slab, const c10::optional<at::Tensor>& w2frag, int64_t products);
@@ -313,16 +315,16 @@ void f32_fc1_fwd_op(const Tensor& a2, const Tensor& w3, Tensor zpart, int64_t pr
 }
 void f32_head_op(const Tensor& zpart, const Tensor& b3, const Tensor& w4, const Tensor& b4, const Tensor& labels,
                  const OptT& rows, const OptT& state, int64_t seed, double rate, Tensor h, Tensor dz, Tensor dlog,
-                 Tensor stats, const OptT& stats_acc, const OptT& x, const OptT& xpre, const OptT& ypre) {
-  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, stats_acc, x, xpre,
-                          ypre);
+                 Tensor stats, const OptT& stats_acc, const OptT& ypre) {
+  mihvd::f32_head_fwd_bwd(zpart, b3, w4, b4, labels, rows, state, seed, rate, h, dz, dlog, stats, stats_acc, ypre);
 }
 void f32_fc1_bwd_op(const Tensor& dz, const Tensor& a2, const Tensor& idx2, const Tensor& h, const Tensor& dlog,
                     Tensor w3, Tensor dY2, Tensor db2p, Tensor gW3, Tensor gb3, Tensor gW4, Tensor gb4, const OptT& m3,
                     const OptT& v3, const OptT& state, double lr, double beta1, double beta2, double eps,
-                    double grad_scale, int64_t rule, bool store_w3) {
+                    double grad_scale, int64_t rule, bool store_w3, const OptT& px, const OptT& plabels,
+                    const OptT& prows, const OptT& pstate, const OptT& xpre, const OptT& ypre) {
   mihvd::f32_fc1_bwd(dz, a2, idx2, h, dlog, w3, dY2, db2p, gW3, gb3, gW4, gb4, m3, v3, state, lr, beta1, beta2, eps,
-                     grad_scale, rule, store_w3);
+                     grad_scale, rule, store_w3, px, plabels, prows, pstate, xpre, ypre);
 }
 void f32_conv2_bwd_op(const Tensor& dY2, const Tensor& w2, const Tensor& a1, const Tensor& idx1, const Tensor& x,
                       const OptT& rows, const OptT& state, Tensor cpart, Tensor slab, const OptT& w2frag,
@@ -416,11 +418,12 @@ TORCH_LIBRARY(mihvd, m) {
   m.def("f32_fc1_fwd(Tensor a2, Tensor w3, Tensor(a!) zpart, int products=0) -> ()");
   m.def("f32_head_fwd_bwd(Tensor zpart, Tensor b3, Tensor w4, Tensor b4, Tensor labels, Tensor? rows, "
         "Tensor(s!)? state, int seed, float rate, Tensor(a!) h, Tensor(b!) dz, Tensor(c!) dlog, Tensor(d!) stats, "
-        "Tensor(e!)? stats_acc=None, Tensor? x=None, Tensor(f!)? xpre=None, Tensor(g!)? ypre=None) -> ()");
+        "Tensor(e!)? stats_acc=None, Tensor? ypre=None) -> ()");
   m.def("f32_fc1_bwd(Tensor dz, Tensor a2, Tensor idx2, Tensor h, Tensor dlog, Tensor(w!) w3, Tensor(a!) dY2, "
         "Tensor(b!) db2p, Tensor(c!) gW3, Tensor(d!) gb3, Tensor(e!) gW4, Tensor(f!) gb4, Tensor(m!)? m3=None, "
         "Tensor(v!)? v3=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
-        "float grad_scale=1., int rule=0, bool store_w3=True) -> ()");
+        "float grad_scale=1., int rule=0, bool store_w3=True, Tensor? px=None, Tensor? plabels=None, "
+        "Tensor? prows=None, Tensor? pstate=None, Tensor(p!)? xpre=None, Tensor(q!)? ypre=None) -> ()");
   m.def("f32_factor_rows(Tensor a2c, Tensor dz, Tensor(a!)? out=None, Tensor(b!)? p=None, Tensor(c!)? m=None, "
         "Tensor(d!)? v=None, Tensor? state=None, float lr=0., float beta1=0., float beta2=0., float eps=0., "
         "float grad_scale=1., int rule=0) -> ()");

@@ -724,8 +724,9 @@ class FusedMNISTTrainer:
         o.f32_fc1_fwd(self.a2, w3, self.zpart, products=self.f32_products)
         o.f32_head_fwd_bwd(self.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), labels, rows, st,
                            self.seed, self.dropout, self.h, self.dz, self.dlog, self.stats,
-                           stats_acc=self._stat_acc if self.track_stats else None,
-                           x=x if pre else None, xpre=self.xpre if pre else None, ypre=self.ypre if pre else None)
+                           stats_acc=self._stat_acc if self.track_stats else None, ypre=self.ypre if pre else None)
+        # fc1_bwd's small-reduction blocks gather the next step's batch (every fp32 plane's fc1_bwd)
+        self._pf = dict(px=x, plabels=labels, prows=rows, pstate=st, xpre=self.xpre, ypre=self.ypre) if pre else {}
         gconv = (G("conv_layer2/conv2d/kernel"), G("conv_layer1/conv2d/kernel"), G("conv_layer1/conv2d/bias"),
                  G("conv_layer2/conv2d/bias"))
         if not self.collectives:
@@ -734,7 +735,7 @@ class FusedMNISTTrainer:
             # bump in one launch
             o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
                           G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), self.m[s3], self.v[s3], st, self.lr,
-                          b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad)
+                          b1, b2, self.eps, 1.0, self.rule, self.keep_w3_grad, **self._pf)
             o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
                             products=self.f32_products)
             o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv, self.params, self.grads, self.m, self.v, st,
@@ -752,7 +753,7 @@ class FusedMNISTTrainer:
         # bucket (98.4 % of the bytes) is complete after fc1_bwd; its allreduce and Adam run on the side
         # stream beside the conv backward, then the conv bucket's
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, G("dense/kernel"),
-                      G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+                      G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), **self._pf)
         side = self._side
         side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -806,7 +807,7 @@ class FusedMNISTTrainer:
         b1, b2 = self.betas
         self._gather_factors()
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, self.pview("dense/kernel"), self.dY2, self.db2p,
-                      G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
+                      G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False, **self._pf)
         s3 = slice(W3_START, FLAT_NUMEL)
         o.f32_factor_full(self.a2_all32.view(-1, 3136), self.dz_all32.view(-1, 1024), self.B,
                           G("dense/kernel") if self.keep_w3_grad else None, self.params[s3], self.m[s3], self.v[s3], st,
@@ -876,7 +877,7 @@ class FusedMNISTTrainer:
                 factor_exchange_(self.a2, self.dz, self.dz_all32, self.a2_send, self.a2_recv, self.rank, self.world,
                                  self.ncomm)
             o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
-                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False)
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), store_w3=False, **self._pf)
             side.wait_stream(main)  # fc1_bwd, the step's last reader of W3, is done
             with torch.cuda.stream(side):
                 # this rank's dW3 rows over all N B samples, Adam from the accumulators
@@ -885,7 +886,7 @@ class FusedMNISTTrainer:
                                   1.0 / self.world, self.rule)
         else:
             o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, w3, self.dY2, self.db2p, gW3,
-                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+                          G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), **self._pf)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 # in place: this rank's rows of the sum land in its own rows of dW3 (at world size 1
@@ -997,7 +998,7 @@ class FusedMNISTTrainer:
             self._prepare_roles_f32()
             R = self._roles
         o.f32_fc1_bwd(self.dz, self.a2, self.idx2, self.h, self.dlog, self.pview("dense/kernel"), self.dY2, self.db2p,
-                      G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"))
+                      G("dense/kernel"), G("dense/bias"), G("dense_1/kernel"), G("dense_1/bias"), **self._pf)
         o.f32_conv2_bwd(self.dY2, w2, self.a1, self.idx1, x, rows, st, self.cpart, self.slab, w2frag=wf[1],
                             products=self.f32_products)
         o.f32_conv_reduce(self.slab, self.cpart, self.db2p, *gconv)

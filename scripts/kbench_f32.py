@@ -111,9 +111,13 @@ def main():
         "conv1_fwd [+ W2 fragments, batch gathered ahead]": lambda: o.f32_conv1_fwd(
             tr.X, tr.rows, st, P("conv_layer1/conv2d/kernel"), P("conv_layer1/conv2d/bias"), tr.a1, tr.idx1, w2, w2frag,
             xpre=tr.xpre),
-        "head [+ next batch gathered]": lambda: o.f32_head_fwd_bwd(
+        "head [labels gathered ahead]": lambda: o.f32_head_fwd_bwd(
             tr.zpart, P("dense/bias"), P("dense_1/kernel"), P("dense_1/bias"), tr.Y, tr.rows, st, tr.seed, tr.dropout,
-            tr.h, tr.dz, tr.dlog, tr.stats, x=tr.X, xpre=tr.xpre, ypre=tr.ypre),
+            tr.h, tr.dz, tr.dlog, tr.stats, ypre=tr.ypre),
+        "fc1_bwd+W3 adam [+ next batch gathered]": lambda: o.f32_fc1_bwd(
+            tr.dz, tr.a2, tr.idx2, tr.h, tr.dlog, w3, tr.dY2, tr.db2p, G("dense/kernel"), G("dense/bias"),
+            G("dense_1/kernel"), G("dense_1/bias"), tr.m[s3], tr.v[s3], st, 0.0, b1, b2, tr.eps, 1.0, tr.rule, False,
+            px=tr.X, plabels=tr.Y, prows=tr.rows, pstate=st, xpre=tr.xpre, ypre=tr.ypre),
         "conv2_fwd [W2 fragment copy]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
                                                                 w2frag=w2frag[0]),
         "conv2_fwd [split-bf16 x9]": lambda: o.f32_conv2_fwd(tr.a1, w2, P("conv_layer2/conv2d/bias"), tr.a2, tr.idx2,
