@@ -369,8 +369,13 @@ def main():
     sync()
     barrier()
     sync()
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if device.type == "cuda" else None
     t0 = time.perf_counter()
+    if ev:
+        ev[0].record()
     run(steps_timed)
+    if ev:
+        ev[1].record()
     sync()
     barrier()
     sync()
@@ -452,7 +457,10 @@ def main():
                        "allreduce": comm_desc,
                        "steps_per_graph": per_call,
                        "replays_timed": (step.schedule(steps_timed) if hasattr(step, "schedule") else None),
-                       "final_loss": loss_val},
+                       "final_loss": loss_val,
+                       # this rank's device time between events around the timed steps (the host
+                       # bracket above adds the launch of the first replay and the final wait)
+                       "device_ms_per_step": (round(ev[0].elapsed_time(ev[1]) / steps_timed, 5) if ev else None)},
         }
         rec["config"].update(rccl)
         if args.impl == "fused" and getattr(tr, "f32", False):
