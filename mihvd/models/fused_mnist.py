@@ -430,9 +430,10 @@ class FusedMNISTTrainer:
                 self.f32_factor_rep = not self.shard_w3 and f32_plane_mode() == "factor_rep"
             self._bind_factor_views()
         # fp32 step on the resident set: the batch gathered one step ahead (xpre images, ypre labels)
-        # by the head kernel, so the next conv1 reads its images with one load instead of the dependent
-        # counter -> rows -> image chain; _xpre_valid: they hold the batch of the device counter's step
-        # (anything else that moves the counter, the epoch order or the set re-primes them)
+        # by fc1_bwd's small-reduction blocks, so the next conv1 reads its images and the next head its
+        # labels with one load instead of the dependent counter -> rows -> image / label chain;
+        # _xpre_valid: they hold the batch of the device counter's step (anything else that moves the
+        # counter, the epoch order or the set re-primes them: _prime_batch)
         self.xpre = torch.empty(B, 784, **f32) if self.f32 else None
         self.ypre = torch.empty(B, device=dev, dtype=torch.int32) if self.f32 else None
         self._xpre_valid = False
