@@ -64,6 +64,9 @@ def parse():
                          "training set the reference's ranks each iterate over: an epoch of 600 steps, reshuffled "
                          "at its boundary)")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
+    ap.add_argument("--device-span", action="store_true", default=False,
+                    help="also report device_ms_per_step: the device time between events recorded around the "
+                         "timed steps (host bracket minus launch / wait latency)")
     ap.add_argument("--use-adasum", action="store_true", default=False,
                     help="fused: Adasum instead of the average (the reference's --use-adasum, "
                          "horovod/tensorflow_mnist.py:31-32,126-133: lr x local_size over NCCL/RCCL, else x 1)")
@@ -369,7 +372,10 @@ def main():
     sync()
     barrier()
     sync()
-    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if device.type == "cuda" else None
+    # --device-span: events around the timed steps (their record calls add a few us of host time to
+    # the bracket, so the headline runs without them)
+    ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          if device.type == "cuda" and args.device_span else None)
     t0 = time.perf_counter()
     if ev:
         ev[0].record()
